@@ -1,0 +1,156 @@
+/* rgbd360_hip.h — C-ABI of librgbd360_hip.so, the MI355X-native (gfx950) implementation of
+ * rgbd360's frame-to-frame registration hot path.
+ *
+ * This is the drop-in boundary.  The reference (Dorothy-2016/rgbd360) has no plugin/FFI layer:
+ * its applications instantiate header-only classes directly.  Each entry point
+ * below replaces one method of those classes; the C++ façade headers in include/rgbd360/ keep
+ * the reference class names and signatures on top of this ABI.
+ *
+ * Conventions
+ *   - 4x4 poses are float[16] COLUMN-major (Eigen default, as Eigen::Matrix4f::data()).
+ *     6x6 matrices are float[36] column-major (symmetric ones are identical either way).
+ *   - Sensor images: 8 sensors stored contiguously, each rows x cols, BGR u8 interleaved
+ *     (as cv::Mat CV_8UC3 in the .bin files) and depth u16 millimetres (CV_16UC1).
+ *   - Return codes: 0 = OK, 1 = soft failure (the reference returned false / ill-posed),
+ *     < 0 = error (message in r360_last_error(), thread-local).  No exceptions cross the ABI.
+ *   - One r360_ctx per (GPU, host thread); a ctx is not thread-safe.  All calls are ordered on
+ *     the ctx's HIP stream and synchronous at return unless named *_async.
+ */
+#ifndef RGBD360_HIP_H
+#define RGBD360_HIP_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define R360_NUM_SENSORS 8
+#define R360_MAX_PYR 6
+
+typedef struct r360_ctx r360_ctx;
+typedef struct r360_calib r360_calib;
+typedef struct r360_frame r360_frame;
+
+/* ---------------------------------------------------------------- context */
+int         r360_ctx_create(int device, r360_ctx** out);
+void        r360_ctx_destroy(r360_ctx* ctx);
+int         r360_ctx_sync(r360_ctx* ctx);
+void*       r360_ctx_stream(r360_ctx* ctx);        /* hipStream_t of the ctx */
+const char* r360_last_error(void);
+const char* r360_version(void);
+
+/* ---------------------------------------------------------------- Calib360
+ * Replaces include/Calib360.h:44-132.  rows/cols = per-sensor image size; the pinhole
+ * cameraMatrix is f = 525*cols/640, c = (cols/2-0.5, rows/2-0.5), which reproduces the
+ * reference's QVGA constant (Calib360.h:73-77) and its commented VGA one (:83-85). */
+int  r360_calib_create(r360_ctx* ctx, int rows, int cols, r360_calib** out);
+void r360_calib_destroy(r360_calib* c);
+/* Rt_[8] (Calib360.h:53), column-major 8 x float[16]; Rt_inv is derived (Calib360.h:129). */
+int  r360_calib_set_extrinsics(r360_calib* c, const float* rt8);
+int  r360_calib_get_extrinsics(const r360_calib* c, float* rt8, float* rt_inv8, float K[9]);
+/* loadExtrinsicCalibration(dir): reads dir/Rt_0{1..8}.txt (Calib360.h:122-131). */
+int  r360_calib_load_extrinsics(r360_calib* c, const char* dir);
+/* loadIntrinsicCalibration(dir): CLAMS dir/distortion_model{1..8} + downsampleParams(2)
+ * (Calib360.h:104-119).  Without intrinsics undistort() is the identity. */
+int  r360_calib_load_intrinsics(r360_calib* c, const char* dir);
+
+/* ---------------------------------------------------------------- Frame360
+ * Replaces include/Frame360.h:93-1150. */
+enum {
+    R360_BUILD_UNDISTORT = 1u << 0,  /* Frame360::undistort()            Frame360.h:293   */
+    R360_BUILD_SPHERE    = 1u << 1,  /* Frame360::stitchSphericalImage() Frame360.h:386   */
+    R360_BUILD_PYRAMID   = 1u << 2,  /* RegisterPhotoICP::set{Source,Target}Frame :480-516 */
+    R360_BUILD_CLOUD     = 1u << 3,  /* Frame360::buildSphereCloud()     Frame360.h:467   */
+    R360_BUILD_PLANES    = 1u << 4,  /* Frame360::getPlanes()            Frame360.h:615   */
+};
+int  r360_frame_create(r360_ctx* ctx, const r360_calib* calib, r360_frame** out);
+void r360_frame_destroy(r360_frame* f);
+/* Host images -> HBM (8 sensors contiguous).  Replaces loadFrame's decode step. */
+int  r360_frame_upload(r360_frame* f, const uint8_t* bgr8, const uint16_t* depth8);
+/* Device-resident images (already in HBM on the ctx's device); copied device-to-device. */
+int  r360_frame_upload_device(r360_frame* f, const void* d_bgr8, const void* d_depth8);
+/* Frame360::loadFrame(path) (Frame360.h:231-266): Boost binary archive of 8 x {RGB, depth}. */
+int  r360_frame_load_bin(r360_frame* f, const char* path);
+int  r360_frame_build(r360_frame* f, unsigned flags);
+int  r360_frame_build_async(r360_frame* f, unsigned flags);
+int  r360_frame_dims(const r360_frame* f, int* rows, int* cols, int* sph_rows, int* sph_cols);
+/* sphereRGB (BGR u8) / sphereDepth (u16 range mm) (Frame360.h:104-107). */
+int  r360_frame_get_sphere(r360_frame* f, uint8_t* bgr, uint16_t* depth);
+/* Undistorted per-sensor depth in metres (CloudRGBD_Ext::m_depthEigUndistort). */
+int  r360_frame_get_depth_m(r360_frame* f, float* depth8);
+/* Pyramid level of the frame as RegisterPhotoICP sees it (gray /255, depth m, target
+ * gradients with the alignFrames360 seam mask applied).  Any pointer may be NULL. */
+int  r360_frame_get_level(r360_frame* f, int level, int* rows, int* cols, float* gray, float* depth,
+                          float* gx, float* gy, float* dgx, float* dgy);
+
+/* ---------------------------------------------------------------- RegisterPhotoICP
+ * Replaces include/RegisterPhotoICP.h:85-4784 (spherical path). */
+enum { R360_PHOTO_CONSISTENCY = 0, R360_DEPTH_CONSISTENCY = 1, R360_PHOTO_DEPTH = 2 };
+
+typedef struct {
+    int    n_pyr;               /* setNumPyr (default 4; odometry apps use 5)  :224      */
+    int    max_iters;           /* maxIters per level = 10                     :4593     */
+    float  min_depth;           /* setMinDepth 0.3                             :202,230  */
+    float  max_depth;           /* setMaxDepth 6.0                             :203,236  */
+    float  std_dev_photo;       /* setGrayVariance: stdDevPhoto (6/255)        :208,242  */
+    float  std_dev_depth;       /* setDepthVariance: stdDevDepth (0.2)         :211,248  */
+    float  thres_sal_int;       /* thresSaliencyIntensity 0.01                 :218      */
+    float  thres_sal_depth;     /* thresSaliencyDepth 0.01                     :219      */
+    double tol_residual;        /* 1e-3                                        :4594     */
+    double tol_update;          /* 1e-4                                        :4595     */
+    double lambda;              /* 1.0, rank test only                         :4589     */
+    int    fixed_iters_level0;  /* 0: reference schedule.  K>0: benchmark timing mode, exactly
+                                   K candidate evaluations at level 0 (no convergence exit). */
+} r360_icp_params;
+
+typedef struct {
+    int    iters[8];            /* num_iterations per level (:4772)          */
+    int    evals[8];            /* candidate evaluations per level           */
+    int    illposed;            /* 1: rank(H + lambda diag H) != 6 (:4682)   */
+    float  sso;                 /* SSO (:3226)                               */
+    double error;               /* accepted error at level 0                 */
+    int    passes;              /* fused residual/Jacobian/JtJ passes run     */
+    int    pad;
+} r360_icp_stats;
+
+void r360_icp_default_params(r360_icp_params* p);
+
+/* alignFrames360(pose_guess, method, occlusion) after setTargetFrame(trg)/setSourceFrame(src)
+ * (:4519-4784).  pose_out = getOptimalPose(), H_out = getHessian(), g_out = getGradient().
+ * Returns 1 (R360_ILLPOSED) when the reference would print "ILL-POSED" and return early. */
+int r360_align360(r360_ctx* ctx, r360_frame* trg, r360_frame* src, const float init[16],
+                  int method, int occlusion, const r360_icp_params* p,
+                  float pose_out[16], float H_out[36], float g_out[6], r360_icp_stats* st);
+int r360_align360_async(r360_ctx* ctx, r360_frame* trg, r360_frame* src, const float init[16],
+                        int method, int occlusion, const r360_icp_params* p);
+int r360_align360_result(r360_ctx* ctx, float pose_out[16], float H_out[36], float g_out[6],
+                         r360_icp_stats* st);
+
+/* One fused pass at a fixed pose: errorPhotoICP_sphere (:2545-2739) + calcHessGrad_sphere
+ * (:2745-3228) at pyramid level `level`.  H/g in double (sum of the float per-pixel terms). */
+int r360_icp_eval(r360_ctx* ctx, r360_frame* trg, r360_frame* src, int level, const float pose[16],
+                  int method, const r360_icp_params* p, double H[36], double g[6],
+                  double* err2, int* n_valid, int* n_visible);
+
+/* CPose3D::exp(mu, pseudo) (MRPT; used at RegisterPhotoICP.h:4697). */
+void r360_exp_se3(const double mu[6], int pseudo, float T[16]);
+
+/* ---------------------------------------------------------------- synthetic scenes
+ * Procedural indoor room rendered by the 8 rig cameras.  Deterministic in
+ * (seed, frame).  Rig pose of frame `frame` along the generator's planar path; pose_out
+ * (column-major) is that rig pose in the room frame. */
+int r360_synth_frame(const r360_calib* calib, uint32_t seed, const float rig_pose[16],
+                     uint8_t* bgr8, uint16_t* depth8);
+int r360_synth_path_pose(uint32_t seed, int frame, float pose_out[16]);
+
+/* ---------------------------------------------------------------- timing hooks (bench) */
+int r360_ctx_timing(r360_ctx* ctx, int enable);
+/* Per-kernel accumulated device time (ms) and launch counts since the last reset. */
+int r360_ctx_timing_read(r360_ctx* ctx, const char* kernel, double* ms, long* launches);
+int r360_ctx_timing_reset(r360_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

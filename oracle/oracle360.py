@@ -1,0 +1,280 @@
+"""ctypes wrapper of oracle/liboracle360.so — the CPU ORACLE.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg, as the checker / CPU baseline.  The product (rgbd360_amd) never imports this module.
+
+Parity status: the reference cannot be compiled or imported here.  The parts
+restating vendored reference code (.bin reader, CLAMS, stitching, RegisterPhotoICP arithmetic) follow
+the cited file:line expression by expression; OpenCV's cvtColor/pyrDown rounding and all PCL/MRPT
+pieces are restated from their published algorithms — **parity unpinned** at those boundaries.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle360.so")
+
+PHOTO, DEPTH, PHOTO_DEPTH = 0, 1, 2
+
+
+class IcpParams(C.Structure):
+    _fields_ = [
+        ("n_pyr", C.c_int), ("max_iters", C.c_int), ("min_depth", C.c_float), ("max_depth", C.c_float),
+        ("std_dev_photo", C.c_float), ("std_dev_depth", C.c_float), ("thres_sal_int", C.c_float),
+        ("thres_sal_depth", C.c_float), ("tol_residual", C.c_double), ("tol_update", C.c_double),
+        ("lambda_", C.c_double), ("fixed_iters_level0", C.c_int),
+    ]
+
+    @classmethod
+    def default(cls, n_pyr=4, std_dev_photo=6.0 / 255, fixed_iters_level0=0):
+        return cls(n_pyr, 10, 0.3, 6.0, np.float32(std_dev_photo), 0.2, 0.01, 0.01, 1e-3, 1e-4, 1.0,
+                   fixed_iters_level0)
+
+
+class IcpStats(C.Structure):
+    _fields_ = [("iters", C.c_int * 8), ("evals", C.c_int * 8), ("illposed", C.c_int), ("sso", C.c_float),
+                ("error", C.c_double)]
+
+
+class Level(C.Structure):
+    _fields_ = [("rows", C.c_int), ("cols", C.c_int)] + [
+        (n, C.POINTER(C.c_float)) for n in ("gray_src", "depth_src", "gray_trg", "depth_trg", "gx", "gy", "dgx", "dgy")]
+
+
+_lib = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = C.CDLL(LIB)
+        fp, dp, ip, vp = C.POINTER(C.c_float), C.POINTER(C.c_double), C.POINTER(C.c_int), C.c_void_p
+        sig = {
+            "orc_bin_dims": (C.c_int, [C.c_char_p, ip, ip]),
+            "orc_bin_load": (C.c_int, [C.c_char_p, vp, vp]),
+            "orc_bin_write": (C.c_int, [C.c_char_p, vp, vp, C.c_int, C.c_int]),
+            "orc_clams_load": (vp, [C.c_char_p]),
+            "orc_clams_free": (None, [vp]),
+            "orc_clams_undistort": (None, [vp, vp, C.c_int, C.c_int]),
+            "orc_clams_export": (C.c_int, [vp, ip, fp, fp]),
+            "orc_stitch": (None, [vp, vp, C.c_int, C.c_int, fp, fp, vp, vp]),
+            "orc_rgb2gray": (None, [vp, C.c_int, fp]),
+            "orc_depth_to_m": (None, [vp, C.c_int, fp]),
+            "orc_pyrdown": (None, [fp, C.c_int, C.c_int, fp]),
+            "orc_pyr_range": (None, [fp, C.c_int, C.c_int, C.c_float, C.c_float, fp]),
+            "orc_gradient": (None, [fp, C.c_int, C.c_int, fp, fp]),
+            "orc_error_sphere": (C.c_double, [C.POINTER(Level), fp, C.c_int, C.POINTER(IcpParams), ip, dp]),
+            "orc_hessgrad_sphere": (None, [C.POINTER(Level), fp, C.c_int, C.POINTER(IcpParams), dp, dp, ip]),
+            "orc_align360": (C.c_int, [vp, vp, vp, vp, C.c_int, C.c_int, fp, C.c_int, C.POINTER(IcpParams), fp,
+                                       fp, fp, C.POINTER(IcpStats)]),
+            "orc_exp_se3": (None, [dp, C.c_int, fp]),
+            "orc_huber": (C.c_float, [C.c_float, C.c_float]),
+        }
+        for k, (r, a) in sig.items():
+            f = getattr(L, k)
+            f.restype, f.argtypes = r, a
+        _lib = L
+    return _lib
+
+
+def _f(a):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def _v(a):
+    return C.c_void_p(a.ctypes.data)
+
+
+def mat16(m) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(m, np.float32).T).reshape(16).copy()
+
+
+def from16(a) -> np.ndarray:
+    return np.asarray(a, np.float32).reshape(4, 4).T.copy()
+
+
+# ---------------------------------------------------------------- A1 / A2 / A10
+def load_bin(path: str):
+    r, c = C.c_int(), C.c_int()
+    if lib().orc_bin_dims(path.encode(), C.byref(r), C.byref(c)):
+        raise IOError(path)
+    bgr = np.zeros((8, r.value, c.value, 3), np.uint8)
+    dep = np.zeros((8, r.value, c.value), np.uint16)
+    rc = lib().orc_bin_load(path.encode(), _v(bgr), _v(dep))
+    if rc:
+        raise IOError(f"{path}: {rc}")
+    return bgr, dep
+
+
+def write_bin(path: str, bgr, dep):
+    bgr = np.ascontiguousarray(bgr, np.uint8)
+    dep = np.ascontiguousarray(dep, np.uint16)
+    assert lib().orc_bin_write(path.encode(), _v(bgr), _v(dep), dep.shape[1], dep.shape[2]) == 0
+
+
+def read_extrinsics(dirpath: str) -> np.ndarray:
+    """Rt_0{1..8}.txt (Calib360.h:122-131) as (8,4,4) float32; Rt_inv via float64 inverse."""
+    return np.stack([np.loadtxt(os.path.join(dirpath, f"Rt_0{k + 1}.txt")).reshape(4, 4) for k in range(8)]
+                    ).astype(np.float32)
+
+
+def camera_matrix(rows: int, cols: int) -> np.ndarray:
+    f = np.float32(525 * np.float32(cols / 640.0))
+    return np.array([[f, 0, cols // 2 - 0.5], [0, f, rows // 2 - 0.5], [0, 0, 1]], np.float32)
+
+
+class Clams:
+    def __init__(self, path: str):
+        self.h = lib().orc_clams_load(path.encode())
+        if not self.h:
+            raise IOError(path)
+
+    def undistort(self, depth_m: np.ndarray) -> np.ndarray:
+        d = np.ascontiguousarray(depth_m, np.float32).copy()
+        lib().orc_clams_undistort(self.h, _v(d), d.shape[0], d.shape[1])
+        return d
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_clams_free(self.h)
+
+
+def depth_to_m(d: np.ndarray) -> np.ndarray:
+    d = np.ascontiguousarray(d, np.uint16)
+    out = np.zeros(d.shape, np.float32)
+    lib().orc_depth_to_m(_v(d), d.size, _f(out))
+    return out
+
+
+def stitch(bgr8, dep8, rt_inv8: np.ndarray, K: np.ndarray):
+    """rt_inv8: column-major (8*16,) float32 as the product stores it; K: 3x3."""
+    bgr8 = np.ascontiguousarray(bgr8, np.uint8)
+    dep8 = np.ascontiguousarray(dep8, np.uint16)
+    rows, cols = dep8.shape[1], dep8.shape[2]
+    W = rows * 8
+    H = int(W * 0.5 * 60.0 / 180)
+    sb = np.zeros((H, W, 3), np.uint8)
+    sd = np.zeros((H, W), np.uint16)
+    Kc = np.ascontiguousarray(np.asarray(K, np.float32).T).reshape(9).copy()
+    rti = np.ascontiguousarray(rt_inv8, np.float32)
+    lib().orc_stitch(_v(bgr8), _v(dep8), rows, cols, _f(rti), _f(Kc), _v(sb), _v(sd))
+    return sb, sd
+
+
+# ---------------------------------------------------------------- A14
+def rgb2gray(bgr: np.ndarray) -> np.ndarray:
+    bgr = np.ascontiguousarray(bgr, np.uint8)
+    out = np.zeros(bgr.shape[:-1], np.float32)
+    lib().orc_rgb2gray(_v(bgr), out.size, _f(out))
+    return out
+
+
+def pyrdown(img: np.ndarray) -> np.ndarray:
+    img = np.ascontiguousarray(img, np.float32)
+    out = np.zeros((img.shape[0] // 2, img.shape[1] // 2), np.float32)
+    lib().orc_pyrdown(_f(img), img.shape[0], img.shape[1], _f(out))
+    return out
+
+
+def pyr_range(img: np.ndarray, min_d=0.3, max_d=6.0) -> np.ndarray:
+    img = np.ascontiguousarray(img, np.float32)
+    out = np.zeros((img.shape[0] // 2, img.shape[1] // 2), np.float32)
+    lib().orc_pyr_range(_f(img), img.shape[0], img.shape[1], min_d, max_d, _f(out))
+    return out
+
+
+def gradient(img: np.ndarray):
+    img = np.ascontiguousarray(img, np.float32)
+    gx, gy = np.zeros_like(img), np.zeros_like(img)
+    lib().orc_gradient(_f(img), img.shape[0], img.shape[1], _f(gx), _f(gy))
+    return gx, gy
+
+
+def seam_mask(g: np.ndarray) -> np.ndarray:
+    """alignFrames360 seam masking (RegisterPhotoICP.h:4538-4549)."""
+    g = g.copy()
+    ws = g.shape[1] // 8
+    for s in range(1, 8):
+        g[:, s * ws - 1:s * ws + 1] = 0
+    return g
+
+
+def sphere_pyramid(sph_bgr, sph_depth, n_levels: int, mask: bool = True):
+    """setSourceFrame/setTargetFrame pyramids (:480-516) + seam masks, per level dicts."""
+    gray = rgb2gray(sph_bgr)
+    dep = depth_to_m(sph_depth)
+    levels = []
+    for l in range(n_levels):
+        if l:
+            gray, dep = pyrdown(gray), pyr_range(dep)
+        gx, gy = gradient(gray)
+        dgx, dgy = gradient(dep)
+        if mask:
+            gx, gy, dgx, dgy = map(seam_mask, (gx, gy, dgx, dgy))
+        levels.append(dict(gray=gray, depth=dep, gx=gx, gy=gy, dgx=dgx, dgy=dgy))
+    return levels
+
+
+def _level_struct(src: dict, trg: dict):
+    arrs = [np.ascontiguousarray(a, np.float32) for a in
+            (src["gray"], src["depth"], trg["gray"], trg["depth"], trg["gx"], trg["gy"], trg["dgx"], trg["dgy"])]
+    L = Level(arrs[0].shape[0], arrs[0].shape[1], *[_f(a) for a in arrs])
+    return L, arrs
+
+
+def error_sphere(src: dict, trg: dict, pose, method=PHOTO_DEPTH, params: IcpParams | None = None):
+    L, keep = _level_struct(src, trg)
+    p = params or IcpParams.default()
+    nv, e2 = C.c_int(), C.c_double()
+    e = lib().orc_error_sphere(C.byref(L), _f(mat16(pose)), method, C.byref(p), C.byref(nv), C.byref(e2))
+    return e, e2.value, nv.value
+
+
+def hessgrad_sphere(src: dict, trg: dict, pose, method=PHOTO_DEPTH, params: IcpParams | None = None):
+    L, keep = _level_struct(src, trg)
+    p = params or IcpParams.default()
+    H, g, nvis = np.zeros(36), np.zeros(6), C.c_int()
+    lib().orc_hessgrad_sphere(C.byref(L), _f(mat16(pose)), method, C.byref(p),
+                              H.ctypes.data_as(C.POINTER(C.c_double)), g.ctypes.data_as(C.POINTER(C.c_double)),
+                              C.byref(nvis))
+    return H.reshape(6, 6), g, nvis.value
+
+
+def align360(trg_bgr, trg_dep, src_bgr, src_dep, init=None, method=PHOTO_DEPTH, params: IcpParams | None = None):
+    trg_bgr, trg_dep, src_bgr, src_dep = [np.ascontiguousarray(a) for a in (trg_bgr, trg_dep, src_bgr, src_dep)]
+    p = params or IcpParams.default()
+    init16 = mat16(np.eye(4) if init is None else init)
+    po, Ho, go = np.zeros(16, np.float32), np.zeros(36, np.float32), np.zeros(6, np.float32)
+    st = IcpStats()
+    rc = lib().orc_align360(_v(trg_bgr), _v(trg_dep), _v(src_bgr), _v(src_dep), src_dep.shape[0], src_dep.shape[1],
+                            _f(init16), method, C.byref(p), _f(po), _f(Ho), _f(go), C.byref(st))
+    return rc, from16(po), Ho.reshape(6, 6).T.copy(), go, st
+
+
+def exp_se3(mu, pseudo=True) -> np.ndarray:
+    m = np.asarray(mu, np.float64)
+    T = np.zeros(16, np.float32)
+    lib().orc_exp_se3(m.ctypes.data_as(C.POINTER(C.c_double)), int(pseudo), _f(T))
+    return from16(T)
+
+
+def huber(e: float, reg: float) -> float:
+    return lib().orc_huber(e, reg)
+
+
+def rot_angle(Ra, Rb) -> float:
+    """Angle (rad) of Ra Rb^T — the angularDistance of diffRotation (Miscellaneous.h:127-139)."""
+    R = np.asarray(Ra, np.float64)[:3, :3] @ np.asarray(Rb, np.float64)[:3, :3].T
+    c = np.clip((np.trace(R) - 1) / 2, -1.0, 1.0)
+    return float(np.arccos(c))

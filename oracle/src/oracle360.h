@@ -1,0 +1,107 @@
+/* oracle360.h — C ABI of the CPU ORACLE for the rgbd360 registration hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This library is a plain C++17 restatement of the
+ * reference (Dorothy-2016/rgbd360, header-only C++) written for this repository.
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
+ * it, and only as the checker / the timed CPU baseline.  The product library
+ * (rgbd360_amd/lib/librgbd360_hip.so) never links, loads or calls it.
+ *
+ * Every function cites the reference file:line it restates.  The reference
+ * itself cannot be compiled here (Eigen/OpenCV/Boost/PCL/MRPT absent, see
+ * DESIGN.md §Oracle), so for the unvendored pieces (OpenCV pyrDown/cvtColor
+ * rounding, PCL normals/segmentation/bilateral, MRPT-pbmap) parity is
+ * "unpinned": the restatement follows SURVEY.md Appendix C.
+ *
+ * Conventions: 4x4 poses are float[16] column-major (Eigen default), images are
+ * row-major, BGR u8 interleaved, depth u16 millimetres.
+ */
+#ifndef ORACLE360_H
+#define ORACLE360_H
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { ORC_PHOTO = 0, ORC_DEPTH = 1, ORC_PHOTO_DEPTH = 2 };
+
+/* Mirrors RegisterPhotoICP members (include/RegisterPhotoICP.h:119-151,201-221)
+ * and the constants of alignFrames360 (:4589-4596). */
+typedef struct {
+    int    n_pyr;               /* nPyrLevels                          */
+    int    max_iters;           /* maxIters per level (10)             */
+    float  min_depth;           /* minDepth 0.3                        */
+    float  max_depth;           /* maxDepth 6.0                        */
+    float  std_dev_photo;       /* stdDevPhoto 6/255 (setGrayVariance) */
+    float  std_dev_depth;       /* stdDevDepth 0.2                     */
+    float  thres_sal_int;       /* thresSaliencyIntensity 0.01         */
+    float  thres_sal_depth;     /* thresSaliencyDepth 0.01             */
+    double tol_residual;        /* 1e-3                                */
+    double tol_update;          /* 1e-4                                */
+    double lambda;              /* 1.0 (only used by the rank test)    */
+    int    fixed_iters_level0;  /* 0 = reference schedule; K>0: timing mode, exactly K
+                                   candidate evaluations at level 0, no convergence exit */
+} orc_icp_params;
+
+typedef struct {
+    int    iters[8];            /* num_iterations per level             */
+    int    evals[8];            /* error evaluations per level          */
+    int    illposed;            /* 1 if the rank test stopped the solve */
+    float  sso;                 /* SSO from the last calcHessGrad       */
+    double error;               /* last accepted error (level 0)        */
+} orc_icp_stats;
+
+/* One pyramid level of the spherical frames (RegisterPhotoICP.h:197-198). */
+typedef struct {
+    int rows, cols;
+    const float *gray_src, *depth_src;
+    const float *gray_trg, *depth_trg, *gx, *gy, *dgx, *dgy;
+} orc_level;
+
+/* ---- A1: .bin Frame360 archive (Frame360.h:231-266, cvmat_serialization.h:39-55) */
+int  orc_bin_dims(const char* path, int* rows, int* cols);
+int  orc_bin_load(const char* path, uint8_t* bgr8, uint16_t* depth8);
+int  orc_bin_write(const char* path, const uint8_t* bgr8, const uint16_t* depth8, int rows, int cols);
+
+/* ---- A2: CLAMS DiscreteDepthDistortionModel (discrete_depth_distortion_model.cpp) */
+void* orc_clams_load(const char* path);          /* load + downsampleParams(2) */
+void  orc_clams_free(void* model);
+void  orc_clams_undistort(const void* model, float* depth_m, int rows, int cols);
+int   orc_clams_export(const void* model, int* hdr /*8*/, float* mult, float* counts);
+
+/* ---- A10: spherical stitching (Frame360.h:386-405, 1099-1148) */
+void orc_stitch(const uint8_t* bgr8, const uint16_t* depth8, int rows, int cols,
+                const float* rt_inv8 /* 8 x 16 col-major */, const float* K /* 9 col-major */,
+                uint8_t* sph_bgr, uint16_t* sph_depth);
+
+/* ---- A14: RegisterPhotoICP pre-processing */
+void orc_rgb2gray(const uint8_t* bgr, int n, float* gray);                 /* :485-486 */
+void orc_depth_to_m(const uint16_t* d, int n, float* out);                /* :316-317 */
+void orc_pyrdown(const float* src, int rows, int cols, float* dst);       /* :292-308 */
+void orc_pyr_range(const float* src, int rows, int cols, float min_d, float max_d, float* dst); /* :312-354 */
+void orc_gradient(const float* src, int rows, int cols, float* gx, float* gy); /* :365-398 */
+
+/* ---- A16 / A17 */
+double orc_error_sphere(const orc_level* L, const float pose[16], int method,
+                        const orc_icp_params* p, int* n_valid, double* err2);
+void   orc_hessgrad_sphere(const orc_level* L, const float pose[16], int method,
+                           const orc_icp_params* p, double H[36], double g[6], int* n_visible);
+
+/* ---- A15: full alignFrames360 from sphere images */
+int orc_align360(const uint8_t* trg_bgr, const uint16_t* trg_depth,
+                 const uint8_t* src_bgr, const uint16_t* src_depth,
+                 int rows, int cols, const float init[16], int method,
+                 const orc_icp_params* p, float pose_out[16], float H_out[36],
+                 float g_out[6], orc_icp_stats* st);
+
+/* ---- A18: CPose3D::exp(mu, pseudo) */
+void orc_exp_se3(const double mu[6], int pseudo, float T[16]);
+
+/* Huber weight (RegisterPhotoICP.h:545-554), float instantiation */
+float orc_huber(float err, float reg);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

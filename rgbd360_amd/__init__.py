@@ -1,0 +1,358 @@
+"""rgbd360_amd — MI355X-native (gfx950) registration hot path of rgbd360.
+
+Python mirror of the reference's C++ class surface for the hot path, written over the C-ABI of
+``rgbd360_amd/lib/librgbd360_hip.so`` (declared in ``include/rgbd360_hip.h``):
+
+    Calib360          include/Calib360.h:44-132
+    Frame360          include/Frame360.h:93-1150   (loadFrame / undistort / stitchSphericalImage)
+    RegisterPhotoICP  include/RegisterPhotoICP.h:85-4784 (setSourceFrame / setTargetFrame /
+                      alignFrames360 / getOptimalPose / getHessian / getGradient)
+
+The HIP library is the only compute path: there is no CPU fallback.  Importing works without a
+GPU (so the CPU test-suite can check that the library loads and exports its ABI); creating a
+``Context`` on a machine without a GPU raises ``RuntimeError``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import numpy as np
+
+__all__ = [
+    "lib", "Context", "Calib360", "Frame360", "RegisterPhotoICP", "IcpParams", "IcpStats",
+    "PHOTO_CONSISTENCY", "DEPTH_CONSISTENCY", "PHOTO_DEPTH", "synth_path_pose", "exp_se3",
+    "LIB_PATH", "ABI_SYMBOLS",
+]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "librgbd360_hip.so")
+REPO_ROOT = os.path.dirname(_HERE)
+
+PHOTO_CONSISTENCY, DEPTH_CONSISTENCY, PHOTO_DEPTH = 0, 1, 2
+BUILD_UNDISTORT, BUILD_SPHERE, BUILD_PYRAMID, BUILD_CLOUD, BUILD_PLANES = 1, 2, 4, 8, 16
+
+
+class IcpParams(C.Structure):
+    """r360_icp_params — RegisterPhotoICP settings (see include/rgbd360_hip.h)."""
+    _fields_ = [
+        ("n_pyr", C.c_int), ("max_iters", C.c_int), ("min_depth", C.c_float), ("max_depth", C.c_float),
+        ("std_dev_photo", C.c_float), ("std_dev_depth", C.c_float), ("thres_sal_int", C.c_float),
+        ("thres_sal_depth", C.c_float), ("tol_residual", C.c_double), ("tol_update", C.c_double),
+        ("lambda_", C.c_double), ("fixed_iters_level0", C.c_int),
+    ]
+
+    @classmethod
+    def default(cls) -> "IcpParams":
+        p = cls()
+        lib().r360_icp_default_params(C.byref(p))
+        return p
+
+
+class IcpStats(C.Structure):
+    _fields_ = [
+        ("iters", C.c_int * 8), ("evals", C.c_int * 8), ("illposed", C.c_int), ("sso", C.c_float),
+        ("error", C.c_double), ("passes", C.c_int), ("pad", C.c_int),
+    ]
+
+
+# (name, restype, argtypes) of every exported entry point of include/rgbd360_hip.h
+_P = C.c_void_p
+_FP = C.POINTER(C.c_float)
+_DP = C.POINTER(C.c_double)
+_IP = C.POINTER(C.c_int)
+_SIGS = [
+    ("r360_ctx_create", C.c_int, [C.c_int, C.POINTER(_P)]),
+    ("r360_ctx_destroy", None, [_P]),
+    ("r360_ctx_sync", C.c_int, [_P]),
+    ("r360_ctx_stream", _P, [_P]),
+    ("r360_last_error", C.c_char_p, []),
+    ("r360_version", C.c_char_p, []),
+    ("r360_calib_create", C.c_int, [_P, C.c_int, C.c_int, C.POINTER(_P)]),
+    ("r360_calib_destroy", None, [_P]),
+    ("r360_calib_set_extrinsics", C.c_int, [_P, _FP]),
+    ("r360_calib_get_extrinsics", C.c_int, [_P, _FP, _FP, _FP]),
+    ("r360_calib_load_extrinsics", C.c_int, [_P, C.c_char_p]),
+    ("r360_calib_load_intrinsics", C.c_int, [_P, C.c_char_p]),
+    ("r360_frame_create", C.c_int, [_P, _P, C.POINTER(_P)]),
+    ("r360_frame_destroy", None, [_P]),
+    ("r360_frame_upload", C.c_int, [_P, _P, _P]),
+    ("r360_frame_upload_device", C.c_int, [_P, _P, _P]),
+    ("r360_frame_load_bin", C.c_int, [_P, C.c_char_p]),
+    ("r360_frame_build", C.c_int, [_P, C.c_uint]),
+    ("r360_frame_build_async", C.c_int, [_P, C.c_uint]),
+    ("r360_frame_dims", C.c_int, [_P, _IP, _IP, _IP, _IP]),
+    ("r360_frame_get_sphere", C.c_int, [_P, _P, _P]),
+    ("r360_frame_get_depth_m", C.c_int, [_P, _P]),
+    ("r360_frame_get_level", C.c_int, [_P, C.c_int, _IP, _IP, _P, _P, _P, _P, _P, _P]),
+    ("r360_icp_default_params", None, [C.POINTER(IcpParams)]),
+    ("r360_align360", C.c_int, [_P, _P, _P, _FP, C.c_int, C.c_int, C.POINTER(IcpParams), _FP, _FP, _FP,
+                                C.POINTER(IcpStats)]),
+    ("r360_align360_async", C.c_int, [_P, _P, _P, _FP, C.c_int, C.c_int, C.POINTER(IcpParams)]),
+    ("r360_align360_result", C.c_int, [_P, _FP, _FP, _FP, C.POINTER(IcpStats)]),
+    ("r360_icp_eval", C.c_int, [_P, _P, _P, C.c_int, _FP, C.c_int, C.POINTER(IcpParams), _DP, _DP, _DP, _IP,
+                                _IP]),
+    ("r360_exp_se3", None, [_DP, C.c_int, _FP]),
+    ("r360_synth_frame", C.c_int, [_P, C.c_uint32, _FP, _P, _P]),
+    ("r360_synth_path_pose", C.c_int, [C.c_uint32, C.c_int, _FP]),
+    ("r360_ctx_timing", C.c_int, [_P, C.c_int]),
+    ("r360_ctx_timing_read", C.c_int, [_P, C.c_char_p, _DP, C.POINTER(C.c_long)]),
+    ("r360_ctx_timing_reset", C.c_int, [_P]),
+]
+ABI_SYMBOLS = [s[0] for s in _SIGS]
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load librgbd360_hip.so (fails loudly if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = C.CDLL(LIB_PATH)
+        for name, res, args in _SIGS:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(rc: int, what: str) -> int:
+    if rc < 0:
+        raise RuntimeError(f"{what} failed ({rc}): {lib().r360_last_error().decode()}")
+    return rc
+
+
+def _fptr(a: np.ndarray):
+    return a.ctypes.data_as(_FP)
+
+
+def _vptr(a: np.ndarray):
+    return C.c_void_p(a.ctypes.data)
+
+
+def _mat16(m) -> np.ndarray:
+    """4x4 numpy (row-major semantic) -> column-major float[16] (Eigen::Matrix4f::data())."""
+    return np.ascontiguousarray(np.asarray(m, dtype=np.float32).T).reshape(16).copy()
+
+
+def _from16(a: np.ndarray) -> np.ndarray:
+    return a.reshape(4, 4).T.copy()
+
+
+class Context:
+    """One HIP device + stream (r360_ctx).  Not thread-safe; use one per host thread."""
+
+    def __init__(self, device: int = 0):
+        h = C.c_void_p()
+        _check(lib().r360_ctx_create(device, C.byref(h)), "r360_ctx_create")
+        self.h = h
+        self.device = device
+
+    def sync(self):
+        _check(lib().r360_ctx_sync(self.h), "r360_ctx_sync")
+
+    def timing(self, enable: bool):
+        _check(lib().r360_ctx_timing(self.h, int(enable)), "timing")
+
+    def timing_read(self, kernel: str):
+        ms, n = C.c_double(), C.c_long()
+        _check(lib().r360_ctx_timing_read(self.h, kernel.encode(), C.byref(ms), C.byref(n)), "timing_read")
+        return ms.value, n.value
+
+    def timing_reset(self):
+        _check(lib().r360_ctx_timing_reset(self.h), "timing_reset")
+
+    def close(self):
+        if self.h:
+            lib().r360_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Calib360:
+    """Calib360 (include/Calib360.h:44-132): Rt_[8], Rt_inv[8], cameraMatrix, CLAMS models."""
+
+    def __init__(self, ctx: Context, rows: int = 240, cols: int = 320):
+        h = C.c_void_p()
+        _check(lib().r360_calib_create(ctx.h, rows, cols, C.byref(h)), "r360_calib_create")
+        self.h, self.ctx, self.rows, self.cols = h, ctx, rows, cols
+
+    def loadExtrinsicCalibration(self, path: str):
+        _check(lib().r360_calib_load_extrinsics(self.h, path.encode()), "loadExtrinsicCalibration")
+
+    def loadIntrinsicCalibration(self, path: str):
+        _check(lib().r360_calib_load_intrinsics(self.h, path.encode()), "loadIntrinsicCalibration")
+
+    def setRt(self, rt8: np.ndarray):
+        """rt8: (8,4,4) rig extrinsics (row-major numpy)."""
+        a = np.concatenate([_mat16(m) for m in rt8]).astype(np.float32)
+        _check(lib().r360_calib_set_extrinsics(self.h, _fptr(a)), "setRt")
+
+    def extrinsics(self):
+        rt = np.zeros(128, np.float32)
+        rti = np.zeros(128, np.float32)
+        K = np.zeros(9, np.float32)
+        _check(lib().r360_calib_get_extrinsics(self.h, _fptr(rt), _fptr(rti), _fptr(K)), "get_extrinsics")
+        return rt, rti, K  # column-major blocks, as the C-ABI stores them
+
+    def synth_frame(self, seed: int, rig_pose: np.ndarray):
+        """Render a synthetic 8-camera frame of the procedural room (seed) at rig_pose (4x4)."""
+        bgr = np.zeros((8, self.rows, self.cols, 3), np.uint8)
+        dep = np.zeros((8, self.rows, self.cols), np.uint16)
+        p = _mat16(rig_pose)
+        _check(lib().r360_synth_frame(self.h, seed, _fptr(p), _vptr(bgr), _vptr(dep)), "synth_frame")
+        return bgr, dep
+
+    def close(self):
+        if self.h:
+            lib().r360_calib_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Frame360:
+    """Frame360 (include/Frame360.h:93-1150) with device-resident images and sphere pyramid."""
+
+    def __init__(self, calib: Calib360):
+        h = C.c_void_p()
+        _check(lib().r360_frame_create(calib.ctx.h, calib.h, C.byref(h)), "r360_frame_create")
+        self.h, self.calib = h, calib
+        r, c, sr, sc = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+        lib().r360_frame_dims(h, C.byref(r), C.byref(c), C.byref(sr), C.byref(sc))
+        self.rows, self.cols, self.sph_rows, self.sph_cols = r.value, c.value, sr.value, sc.value
+
+    def loadFrame(self, path: str):
+        _check(lib().r360_frame_load_bin(self.h, path.encode()), "loadFrame")
+
+    def upload(self, bgr8: np.ndarray, depth8: np.ndarray):
+        bgr8 = np.ascontiguousarray(bgr8, np.uint8)
+        depth8 = np.ascontiguousarray(depth8, np.uint16)
+        assert bgr8.shape == (8, self.rows, self.cols, 3) and depth8.shape == (8, self.rows, self.cols)
+        _check(lib().r360_frame_upload(self.h, _vptr(bgr8), _vptr(depth8)), "upload")
+
+    def upload_device(self, d_bgr: int, d_depth: int):
+        _check(lib().r360_frame_upload_device(self.h, C.c_void_p(d_bgr), C.c_void_p(d_depth)), "upload_device")
+
+    def build(self, flags: int = BUILD_UNDISTORT | BUILD_SPHERE | BUILD_PYRAMID, sync: bool = True):
+        fn = lib().r360_frame_build if sync else lib().r360_frame_build_async
+        _check(fn(self.h, flags), "r360_frame_build")
+
+    def undistort(self):
+        self.build(BUILD_UNDISTORT)
+
+    def stitchSphericalImage(self):
+        self.build(BUILD_SPHERE | BUILD_PYRAMID)
+
+    def sphere(self):
+        bgr = np.zeros((self.sph_rows, self.sph_cols, 3), np.uint8)
+        dep = np.zeros((self.sph_rows, self.sph_cols), np.uint16)
+        _check(lib().r360_frame_get_sphere(self.h, _vptr(bgr), _vptr(dep)), "get_sphere")
+        return bgr, dep
+
+    def depth_m(self):
+        d = np.zeros((8, self.rows, self.cols), np.float32)
+        _check(lib().r360_frame_get_depth_m(self.h, _vptr(d)), "get_depth_m")
+        return d
+
+    def level(self, level: int):
+        r, c = C.c_int(), C.c_int()
+        _check(lib().r360_frame_get_level(self.h, level, C.byref(r), C.byref(c), None, None, None, None, None,
+                                          None), "get_level")
+        arrs = [np.zeros((r.value, c.value), np.float32) for _ in range(6)]
+        _check(lib().r360_frame_get_level(self.h, level, C.byref(r), C.byref(c), *[_vptr(a) for a in arrs]),
+               "get_level")
+        return dict(zip(["gray", "depth", "gx", "gy", "dgx", "dgy"], arrs))
+
+    def close(self):
+        if self.h:
+            lib().r360_frame_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class RegisterPhotoICP:
+    """RegisterPhotoICP spherical path (include/RegisterPhotoICP.h), frames stay in HBM."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+        self.params = IcpParams.default()
+        self.src = self.trg = None
+        self.relPose = np.eye(4, dtype=np.float32)
+        self.hessian = np.zeros((6, 6), np.float32)
+        self.gradient = np.zeros(6, np.float32)
+        self.stats = IcpStats()
+
+    # setters (:224-269)
+    def setNumPyr(self, n: int): self.params.n_pyr = n
+    def setMinDepth(self, d: float): self.params.min_depth = d
+    def setMaxDepth(self, d: float): self.params.max_depth = d
+    def setGrayVariance(self, s: float): self.params.std_dev_photo = s
+    def setDepthVariance(self, s: float): self.params.std_dev_depth = s
+
+    def useSaliency(self, b: bool):
+        if b:
+            raise NotImplementedError("saliency subsampling is commented out in the reference's sphere path")
+
+    def setSourceFrame(self, f: Frame360): self.src = f
+    def setTargetFrame(self, f: Frame360): self.trg = f
+
+    def alignFrames360(self, pose_guess=None, method: int = PHOTO_CONSISTENCY, occlusion: int = 0) -> int:
+        init = _mat16(np.eye(4) if pose_guess is None else pose_guess)
+        po, Ho, go = np.zeros(16, np.float32), np.zeros(36, np.float32), np.zeros(6, np.float32)
+        rc = _check(lib().r360_align360(self.ctx.h, self.trg.h, self.src.h, _fptr(init), method, occlusion,
+                                        C.byref(self.params), _fptr(po), _fptr(Ho), _fptr(go),
+                                        C.byref(self.stats)), "alignFrames360")
+        self.relPose = _from16(po)
+        self.hessian = Ho.reshape(6, 6).T.copy()
+        self.gradient = go.copy()
+        return rc
+
+    def getOptimalPose(self): return self.relPose
+    def getHessian(self): return self.hessian
+    def getGradient(self): return self.gradient
+
+    def eval(self, level: int, pose, method: int = PHOTO_DEPTH):
+        """One fused errorPhotoICP_sphere + calcHessGrad_sphere pass at a fixed pose."""
+        p = _mat16(pose)
+        H, g = np.zeros(36), np.zeros(6)
+        e2, nv, nvis = C.c_double(), C.c_int(), C.c_int()
+        _check(lib().r360_icp_eval(self.ctx.h, self.trg.h, self.src.h, level, _fptr(p), method,
+                                   C.byref(self.params), H.ctypes.data_as(_DP), g.ctypes.data_as(_DP),
+                                   C.byref(e2), C.byref(nv), C.byref(nvis)), "icp_eval")
+        return H.reshape(6, 6), g, e2.value, nv.value, nvis.value
+
+
+def synth_path_pose(seed: int, frame: int) -> np.ndarray:
+    a = np.zeros(16, np.float32)
+    lib().r360_synth_path_pose(seed, frame, _fptr(a))
+    return _from16(a)
+
+
+def exp_se3(mu, pseudo: bool = True) -> np.ndarray:
+    m = np.asarray(mu, np.float64)
+    T = np.zeros(16, np.float32)
+    lib().r360_exp_se3(m.ctypes.data_as(_DP), int(pseudo), _fptr(T))
+    return _from16(T)
+
+
+DATA_DIR = os.path.join(REPO_ROOT, "data")
+EXTRINSICS_DIR = os.path.join(DATA_DIR, "calib", "Extrinsics")   # Rt_0{1..8}.txt (reference rig)
+INTRINSICS_DIR = os.path.join(DATA_DIR, "calib", "Intrinsics")   # CLAMS tables (compact form)
+SAMPLES_DIR = os.path.join(DATA_DIR, "samples")                  # sphere_images_{1,10}.bin

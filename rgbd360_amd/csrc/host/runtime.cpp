@@ -1,0 +1,616 @@
+// runtime.cpp — host side of librgbd360_hip.so: contexts, Calib360, Frame360 and the
+// RegisterPhotoICP::alignFrames360 driver.  Everything here is plumbing around the HIP kernels
+// (frame_kernels.hip, icp_kernels.hip); the per-pixel work never runs on the CPU.
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../r360_internal.h"
+
+static thread_local std::string g_err;
+void r360_set_error(const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+}
+extern "C" const char* r360_last_error(void) { return g_err.c_str(); }
+extern "C" const char* r360_version(void) { return "rgbd360_amd 0.1 (gfx950)"; }
+
+#define CHECK_ARG(cond, msg)                 \
+    do {                                     \
+        if (!(cond)) {                       \
+            r360_set_error("%s", msg);       \
+            return -2;                       \
+        }                                    \
+    } while (0)
+
+// ------------------------------------------------------------------ timing (HIP events on the ctx stream)
+int timing_begin(r360_ctx* ctx, const char* name) {
+    if (!ctx || !ctx->timing) return -1;
+    if (ctx->ev_used + 2 > (int)ctx->ev_pool.size()) {
+        for (int i = 0; i < 64; ++i) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return -1;
+            ctx->ev_pool.push_back(e);
+        }
+    }
+    const int a = ctx->ev_used++, b = ctx->ev_used++;
+    hipEventRecord(ctx->ev_pool[a], ctx->stream);
+    ctx->pending.push_back({name, a, b});
+    return (int)ctx->pending.size() - 1;
+}
+void timing_end(r360_ctx* ctx, int slot) {
+    if (slot < 0 || !ctx) return;
+    hipEventRecord(ctx->ev_pool[ctx->pending[slot].b], ctx->stream);
+}
+static void timing_flush(r360_ctx* ctx) {
+    if (!ctx->timing || ctx->pending.empty()) return;
+    hipStreamSynchronize(ctx->stream);
+    for (auto& p : ctx->pending) {
+        float ms = 0.f;
+        hipEventElapsedTime(&ms, ctx->ev_pool[p.a], ctx->ev_pool[p.b]);
+        bool found = false;
+        for (auto& kv : ctx->acc)
+            if (kv.first == p.name) { kv.second.ms += ms; kv.second.n += 1; found = true; break; }
+        if (!found) { r360_ctx::Acc a; a.ms = ms; a.n = 1; ctx->acc.push_back({p.name, a}); }
+    }
+    ctx->pending.clear();
+    ctx->ev_used = 0;
+}
+
+extern "C" int r360_ctx_timing(r360_ctx* ctx, int enable) {
+    CHECK_ARG(ctx, "null ctx");
+    timing_flush(ctx);
+    ctx->timing = enable;
+    return 0;
+}
+extern "C" int r360_ctx_timing_read(r360_ctx* ctx, const char* kernel, double* ms, long* launches) {
+    CHECK_ARG(ctx && kernel, "null arg");
+    timing_flush(ctx);
+    *ms = 0; *launches = 0;
+    for (auto& kv : ctx->acc)
+        if (kv.first == kernel) { *ms = kv.second.ms; *launches = kv.second.n; }
+    return 0;
+}
+extern "C" int r360_ctx_timing_reset(r360_ctx* ctx) {
+    CHECK_ARG(ctx, "null ctx");
+    timing_flush(ctx);
+    ctx->acc.clear();
+    return 0;
+}
+
+// ------------------------------------------------------------------ context
+extern "C" int r360_ctx_create(int device, r360_ctx** out) {
+    CHECK_ARG(out, "null out");
+    int n = 0;
+    R360_HIP(hipGetDeviceCount(&n));
+    CHECK_ARG(device >= 0 && device < n, "invalid device ordinal");
+    R360_HIP(hipSetDevice(device));
+    r360_ctx* c = new r360_ctx;
+    c->device = device;
+    R360_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    R360_HIP(hipMalloc(&c->d_state, sizeof(IcpState)));
+    R360_HIP(hipMemset(c->d_state, 0, sizeof(IcpState)));
+    c->partials_cap = 1024;
+    R360_HIP(hipMalloc(&c->d_partials, sizeof(double) * 32 * c->partials_cap));
+    R360_HIP(hipHostMalloc(&c->h_state, sizeof(IcpState), hipHostMallocDefault));
+    *out = c;
+    return 0;
+}
+
+extern "C" void r360_ctx_destroy(r360_ctx* c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    for (auto e : c->ev_pool) hipEventDestroy(e);
+    hipFree(c->d_state);
+    hipFree(c->d_partials);
+    hipHostFree(c->h_state);
+    hipStreamDestroy(c->stream);
+    delete c;
+}
+
+extern "C" int r360_ctx_sync(r360_ctx* c) {
+    CHECK_ARG(c, "null ctx");
+    R360_HIP(hipStreamSynchronize(c->stream));
+    return 0;
+}
+extern "C" void* r360_ctx_stream(r360_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+// ------------------------------------------------------------------ Calib360
+static void inverse4(const float* T, float* Ti) {  // rigid-or-general 4x4 inverse in double
+    double m[16], inv[16];
+    for (int i = 0; i < 16; ++i) m[i] = T[i];
+    inv[0] = m[5] * m[10] * m[15] - m[5] * m[11] * m[14] - m[9] * m[6] * m[15] + m[9] * m[7] * m[14] + m[13] * m[6] * m[11] - m[13] * m[7] * m[10];
+    inv[4] = -m[4] * m[10] * m[15] + m[4] * m[11] * m[14] + m[8] * m[6] * m[15] - m[8] * m[7] * m[14] - m[12] * m[6] * m[11] + m[12] * m[7] * m[10];
+    inv[8] = m[4] * m[9] * m[15] - m[4] * m[11] * m[13] - m[8] * m[5] * m[15] + m[8] * m[7] * m[13] + m[12] * m[5] * m[11] - m[12] * m[7] * m[9];
+    inv[12] = -m[4] * m[9] * m[14] + m[4] * m[10] * m[13] + m[8] * m[5] * m[14] - m[8] * m[6] * m[13] - m[12] * m[5] * m[10] + m[12] * m[6] * m[9];
+    inv[1] = -m[1] * m[10] * m[15] + m[1] * m[11] * m[14] + m[9] * m[2] * m[15] - m[9] * m[3] * m[14] - m[13] * m[2] * m[11] + m[13] * m[3] * m[10];
+    inv[5] = m[0] * m[10] * m[15] - m[0] * m[11] * m[14] - m[8] * m[2] * m[15] + m[8] * m[3] * m[14] + m[12] * m[2] * m[11] - m[12] * m[3] * m[10];
+    inv[9] = -m[0] * m[9] * m[15] + m[0] * m[11] * m[13] + m[8] * m[1] * m[15] - m[8] * m[3] * m[13] - m[12] * m[1] * m[11] + m[12] * m[3] * m[9];
+    inv[13] = m[0] * m[9] * m[14] - m[0] * m[10] * m[13] - m[8] * m[1] * m[14] + m[8] * m[2] * m[13] + m[12] * m[1] * m[10] - m[12] * m[2] * m[9];
+    inv[2] = m[1] * m[6] * m[15] - m[1] * m[7] * m[14] - m[5] * m[2] * m[15] + m[5] * m[3] * m[14] + m[13] * m[2] * m[7] - m[13] * m[3] * m[6];
+    inv[6] = -m[0] * m[6] * m[15] + m[0] * m[7] * m[14] + m[4] * m[2] * m[15] - m[4] * m[3] * m[14] - m[12] * m[2] * m[7] + m[12] * m[3] * m[6];
+    inv[10] = m[0] * m[5] * m[15] - m[0] * m[7] * m[13] - m[4] * m[1] * m[15] + m[4] * m[3] * m[13] + m[12] * m[1] * m[7] - m[12] * m[3] * m[5];
+    inv[14] = -m[0] * m[5] * m[14] + m[0] * m[6] * m[13] + m[4] * m[1] * m[14] - m[4] * m[2] * m[13] - m[12] * m[1] * m[6] + m[12] * m[2] * m[5];
+    inv[3] = -m[1] * m[6] * m[11] + m[1] * m[7] * m[10] + m[5] * m[2] * m[11] - m[5] * m[3] * m[10] - m[9] * m[2] * m[7] + m[9] * m[3] * m[6];
+    inv[7] = m[0] * m[6] * m[11] - m[0] * m[7] * m[10] - m[4] * m[2] * m[11] + m[4] * m[3] * m[10] + m[8] * m[2] * m[7] - m[8] * m[3] * m[6];
+    inv[11] = -m[0] * m[5] * m[11] + m[0] * m[7] * m[9] + m[4] * m[1] * m[11] - m[4] * m[3] * m[9] - m[8] * m[1] * m[7] + m[8] * m[3] * m[5];
+    inv[15] = m[0] * m[5] * m[10] - m[0] * m[6] * m[9] - m[4] * m[1] * m[10] + m[4] * m[2] * m[9] + m[8] * m[1] * m[6] - m[8] * m[2] * m[5];
+    double det = m[0] * inv[0] + m[1] * inv[4] + m[2] * inv[8] + m[3] * inv[12];
+    for (int i = 0; i < 16; ++i) Ti[i] = (float)(inv[i] / det);
+}
+
+static int upload_floats(float** dptr, const std::vector<float>& h) {
+    if (*dptr) hipFree(*dptr);
+    R360_HIP(hipMalloc(dptr, sizeof(float) * (h.size() ? h.size() : 1)));
+    R360_HIP(hipMemcpy(*dptr, h.data(), sizeof(float) * h.size(), hipMemcpyHostToDevice));
+    return 0;
+}
+
+// Trigonometric tables with the reference's exact float expressions:
+//   stitchImage (Frame360.h:1104-1129) and the alignFrames360 LUT (RegisterPhotoICP.h:4555-4569).
+static int calib_build_tables(r360_calib* c) {
+    const int W = c->rows * 8;
+    const int H = (int)(W * 0.5 * 60.0 / 180);
+    c->sph_rows = H; c->sph_cols = W;
+    const float offsetPhi = H / 2 - 0.5;
+    const float offsetTheta = -c->rows * 15 / 2 + 0.5;
+    const float angle_pixel = 2 * R360_PI / W;
+    std::vector<float> sp(H), cp(H), st(W), ct(W);
+    for (int r = 0; r < H; ++r) { float phi_i = (offsetPhi - r) * angle_pixel; sp[r] = std::sin(phi_i); cp[r] = std::cos(phi_i); }
+    for (int col = 0; col < W; ++col) { float th = (col + offsetTheta) * angle_pixel; st[col] = std::sin(th); ct[col] = std::cos(th); }
+    if (upload_floats(&c->d_st_sinphi, sp) || upload_floats(&c->d_st_cosphi, cp) ||
+        upload_floats(&c->d_st_sinth, st) || upload_floats(&c->d_st_costh, ct))
+        return -1;
+    // pyramid levels of the sphere
+    int R = H, C = W, nl = 0;
+    for (; nl < R360_MAX_PYR; ++nl) {
+        if (R < 2 || C < 8 || (C % 4) != 0) break;
+        const float angle_res = 2 * R360_PI / C;
+        const float half_nRows = 0.5 * R - 0.5;
+        std::vector<float> a(R), b(R), s(C), t(C);
+        for (int cc = 0; cc < C; ++cc) { float theta = cc * angle_res; s[cc] = std::sin(theta); t[cc] = std::cos(theta); }
+        for (int r = 0; r < R; ++r) { float phi = (half_nRows - r) * angle_res; a[r] = std::sin(phi); b[r] = std::cos(phi); }
+        LevelTrig& L = c->trig[nl];
+        if (upload_floats(&L.sinphi, a) || upload_floats(&L.cosphi, b) || upload_floats(&L.sinth, s) ||
+            upload_floats(&L.costh, t))
+            return -1;
+        if ((R % 2) || (C % 2)) { ++nl; break; }
+        R /= 2; C /= 2;
+    }
+    c->n_levels = nl;
+    return 0;
+}
+
+extern "C" int r360_calib_create(r360_ctx* ctx, int rows, int cols, r360_calib** out) {
+    CHECK_ARG(ctx && out, "null arg");
+    CHECK_ARG(rows > 0 && cols > 0 && rows % 2 == 0 && cols % 2 == 0, "sensor size must be even");
+    R360_HIP(hipSetDevice(ctx->device));
+    r360_calib* c = new r360_calib;
+    c->ctx = ctx; c->rows = rows; c->cols = cols;
+    // cameraMatrix: f = 525*cols/640, c = (cols/2-0.5, rows/2-0.5) (CloudRGBD_Ext.h:97-102;
+    // equals the QVGA constant of Calib360.h:73-77 and its commented VGA line :83-85)
+    const float f = 525 * (float)(cols / 640.0);
+    const float cx = cols / 2 - 0.5, cy = rows / 2 - 0.5;
+    const float K[9] = {f, 0, 0, 0, f, 0, cx, cy, 1};
+    memcpy(c->K, K, sizeof(K));
+    for (int k = 0; k < 8; ++k)
+        for (int i = 0; i < 16; ++i) c->rt[k][i] = c->rt_inv[k][i] = (i % 5 == 0) ? 1.f : 0.f;
+    R360_HIP(hipMalloc(&c->d_rt_inv, sizeof(float) * 128));
+    R360_HIP(hipMemcpy(c->d_rt_inv, c->rt_inv, sizeof(float) * 128, hipMemcpyHostToDevice));
+    if (calib_build_tables(c)) { delete c; return -1; }
+    *out = c;
+    return 0;
+}
+
+extern "C" void r360_calib_destroy(r360_calib* c) {
+    if (!c) return;
+    hipFree(c->d_rt_inv);
+    hipFree(c->d_st_sinphi); hipFree(c->d_st_cosphi); hipFree(c->d_st_sinth); hipFree(c->d_st_costh);
+    for (int l = 0; l < R360_MAX_PYR; ++l) {
+        hipFree(c->trig[l].sinphi); hipFree(c->trig[l].cosphi); hipFree(c->trig[l].sinth); hipFree(c->trig[l].costh);
+    }
+    hipFree(c->clams.d_mult); hipFree(c->clams.d_counts);
+    delete c;
+}
+
+extern "C" int r360_calib_set_extrinsics(r360_calib* c, const float* rt8) {
+    CHECK_ARG(c && rt8, "null arg");
+    for (int k = 0; k < 8; ++k) {
+        memcpy(c->rt[k], rt8 + 16 * k, sizeof(float) * 16);
+        inverse4(c->rt[k], c->rt_inv[k]);                       // Rt_inv = Rt_.inverse() (Calib360.h:129)
+    }
+    R360_HIP(hipMemcpy(c->d_rt_inv, c->rt_inv, sizeof(float) * 128, hipMemcpyHostToDevice));
+    return 0;
+}
+
+extern "C" int r360_calib_get_extrinsics(const r360_calib* c, float* rt8, float* rt_inv8, float K[9]) {
+    CHECK_ARG(c, "null calib");
+    if (rt8) memcpy(rt8, c->rt, sizeof(c->rt));
+    if (rt_inv8) memcpy(rt_inv8, c->rt_inv, sizeof(c->rt_inv));
+    if (K) memcpy(K, c->K, sizeof(c->K));
+    return 0;
+}
+
+extern "C" int r360_calib_load_extrinsics(r360_calib* c, const char* dir) {
+    CHECK_ARG(c && dir, "null arg");
+    float rt[8 * 16];
+    for (int k = 0; k < 8; ++k) {
+        char path[4096];
+        snprintf(path, sizeof(path), "%s/Rt_0%d.txt", dir, k + 1);  // Calib360.h:128
+        std::ifstream f(path);
+        if (!f) { r360_set_error("cannot open %s", path); return -1; }
+        double v[16];
+        for (int i = 0; i < 16; ++i)
+            if (!(f >> v[i])) { r360_set_error("bad matrix in %s", path); return -1; }
+        for (int r = 0; r < 4; ++r)
+            for (int cc = 0; cc < 4; ++cc) rt[16 * k + cc * 4 + r] = (float)v[r * 4 + cc];  // text is row-major
+    }
+    return r360_calib_set_extrinsics(c, rt);
+}
+
+// CLAMS model (discrete_depth_distortion_model.cpp:259-280, 82-91) -> per-bin multipliers/counts.
+// Accepts the reference's own files (dir/distortion_model{k}) or the compact R360CLAMS1 tables
+// (dir/distortion_model{k}.r360, written by tools/compact_clams.py).
+static int read_clams(const char* dir, int k, ClamsDev& M, std::vector<float>& mult, std::vector<float>& counts) {
+    char path[4096];
+    snprintf(path, sizeof(path), "%s/distortion_model%d", dir, k + 1);
+    std::ifstream in(path, std::ios::binary);
+    bool compact = false;
+    if (!in) {
+        snprintf(path, sizeof(path), "%s/distortion_model%d.r360", dir, k + 1);
+        in.open(path, std::ios::binary);
+        compact = true;
+    }
+    if (!in) { r360_set_error("cannot open %s/distortion_model%d[.r360]", dir, k + 1); return -1; }
+    std::string line;
+    std::getline(in, line);
+    int w, h, bw, bh, nx, ny, nb = 0; double bd;
+    if (compact) {
+        if (line != "R360CLAMS1") { r360_set_error("bad compact CLAMS header in %s", path); return -1; }
+        in.read((char*)&w, 4); in.read((char*)&h, 4); in.read((char*)&bw, 4); in.read((char*)&bh, 4);
+        in.read((char*)&nx, 4); in.read((char*)&ny, 4); in.read((char*)&nb, 4); in.read((char*)&bd, 8);
+        std::vector<float> c((size_t)nx * ny * nb), m((size_t)nx * ny * nb);
+        in.read((char*)c.data(), 4 * c.size());
+        in.read((char*)m.data(), 4 * m.size());
+        if (!in) { r360_set_error("truncated %s", path); return -1; }
+        counts.insert(counts.end(), c.begin(), c.end());
+        mult.insert(mult.end(), m.begin(), m.end());
+    } else {
+        if (line != "DiscreteDepthDistortionModel v01") { r360_set_error("bad CLAMS header in %s", path); return -1; }
+        in.read((char*)&w, 4); in.read((char*)&h, 4); in.read((char*)&bw, 4); in.read((char*)&bh, 4);
+        in.read((char*)&bd, 8); in.read((char*)&nx, 4); in.read((char*)&ny, 4);
+        if (!in) { r360_set_error("truncated %s", path); return -1; }
+        for (int i = 0; i < nx * ny; ++i) {
+            double maxd, bdep;
+            in.read((char*)&maxd, 8); in.read((char*)&nb, 4); in.read((char*)&bdep, 8);
+            std::vector<float> vec[4];
+            for (int q = 0; q < 4; ++q) {
+                int bytes, rr, cc;
+                in.read((char*)&bytes, 4); in.read((char*)&rr, 4); in.read((char*)&cc, 4);
+                vec[q].resize((size_t)rr * cc);
+                in.read((char*)vec[q].data(), 4 * vec[q].size());
+            }
+            if (!in || vec[0].size() != (size_t)nb || vec[3].size() != (size_t)nb) {
+                r360_set_error("bad frustum in %s", path); return -1;
+            }
+            for (int b = 0; b < nb; ++b) { counts.push_back(vec[0][b]); mult.push_back(vec[3][b]); }
+        }
+    }
+    // downsampleParams(2) (Calib360.h:115, discrete_depth_distortion_model.cpp:313-320)
+    M.width = w / 2; M.height = h / 2; M.bin_w = bw / 2; M.bin_h = bh / 2; M.nx = nx; M.ny = ny;
+    M.num_bins = nb; M.bin_depth = bd;
+    return 0;
+}
+
+extern "C" int r360_calib_load_intrinsics(r360_calib* c, const char* dir) {
+    CHECK_ARG(c && dir, "null arg");
+    std::vector<float> mult, counts;
+    for (int k = 0; k < 8; ++k)
+        if (read_clams(dir, k, c->clams, mult, counts)) return -1;
+    if (upload_floats(&c->clams.d_mult, mult) || upload_floats(&c->clams.d_counts, counts)) return -1;
+    c->has_intrinsics = true;
+    return 0;
+}
+
+// ------------------------------------------------------------------ Frame360
+extern "C" int r360_frame_create(r360_ctx* ctx, const r360_calib* calib, r360_frame** out) {
+    CHECK_ARG(ctx && calib && out, "null arg");
+    R360_HIP(hipSetDevice(ctx->device));
+    r360_frame* f = new r360_frame;
+    f->ctx = ctx; f->calib = calib;
+    f->rows = calib->rows; f->cols = calib->cols;
+    f->sph_rows = calib->sph_rows; f->sph_cols = calib->sph_cols;
+    f->n_levels = calib->n_levels;
+    const size_t ns = (size_t)8 * f->rows * f->cols, nsph = (size_t)f->sph_rows * f->sph_cols;
+    R360_HIP(hipMalloc(&f->d_bgr, ns * 3));
+    R360_HIP(hipMalloc(&f->d_depth, ns * 2));
+    R360_HIP(hipMalloc(&f->d_depth_m, ns * 4));
+    R360_HIP(hipMalloc(&f->d_sph_bgr, nsph * 3));
+    R360_HIP(hipMalloc(&f->d_sph_depth, nsph * 2));
+    int R = f->sph_rows, C = f->sph_cols;
+    for (int l = 0; l < f->n_levels; ++l) {
+        f->lv[l].rows = R; f->lv[l].cols = C;
+        R360_HIP(hipMalloc(&f->lv[l].p0, sizeof(float2) * (size_t)R * C));
+        R360_HIP(hipMalloc(&f->lv[l].tg, sizeof(float4) * (size_t)R * C));
+        R /= 2; C /= 2;
+    }
+    *out = f;
+    return 0;
+}
+
+extern "C" void r360_frame_destroy(r360_frame* f) {
+    if (!f) return;
+    hipStreamSynchronize(f->ctx->stream);
+    hipFree(f->d_bgr); hipFree(f->d_depth); hipFree(f->d_depth_m); hipFree(f->d_sph_bgr); hipFree(f->d_sph_depth);
+    for (int l = 0; l < f->n_levels; ++l) { hipFree(f->lv[l].p0); hipFree(f->lv[l].tg); }
+    delete f;
+}
+
+extern "C" int r360_frame_upload(r360_frame* f, const uint8_t* bgr8, const uint16_t* depth8) {
+    CHECK_ARG(f && bgr8 && depth8, "null arg");
+    const size_t ns = (size_t)8 * f->rows * f->cols;
+    R360_HIP(hipMemcpyAsync(f->d_bgr, bgr8, ns * 3, hipMemcpyHostToDevice, f->ctx->stream));
+    R360_HIP(hipMemcpyAsync(f->d_depth, depth8, ns * 2, hipMemcpyHostToDevice, f->ctx->stream));
+    R360_HIP(hipStreamSynchronize(f->ctx->stream));
+    f->built = 0;
+    return 0;
+}
+
+extern "C" int r360_frame_upload_device(r360_frame* f, const void* d_bgr8, const void* d_depth8) {
+    CHECK_ARG(f && d_bgr8 && d_depth8, "null arg");
+    const size_t ns = (size_t)8 * f->rows * f->cols;
+    R360_HIP(hipMemcpyAsync(f->d_bgr, d_bgr8, ns * 3, hipMemcpyDeviceToDevice, f->ctx->stream));
+    R360_HIP(hipMemcpyAsync(f->d_depth, d_depth8, ns * 2, hipMemcpyDeviceToDevice, f->ctx->stream));
+    f->built = 0;
+    return 0;
+}
+
+int parse_bin_file(const char* path, int rows, int cols, std::vector<uint8_t>& bgr, std::vector<uint16_t>& depth);
+
+extern "C" int r360_frame_load_bin(r360_frame* f, const char* path) {
+    CHECK_ARG(f && path, "null arg");
+    std::vector<uint8_t> bgr;
+    std::vector<uint16_t> depth;
+    if (parse_bin_file(path, f->rows, f->cols, bgr, depth)) return -1;
+    return r360_frame_upload(f, bgr.data(), depth.data());
+}
+
+extern "C" int r360_frame_build_async(r360_frame* f, unsigned flags) {
+    CHECK_ARG(f, "null frame");
+    if (flags & (R360_BUILD_UNDISTORT | R360_BUILD_CLOUD | R360_BUILD_PLANES)) {
+        if (launch_undistort(f)) return -1;
+        f->built |= R360_BUILD_UNDISTORT;
+    }
+    if (flags & (R360_BUILD_SPHERE | R360_BUILD_PYRAMID)) {
+        if (launch_stitch(f)) return -1;
+        f->built |= R360_BUILD_SPHERE;
+    }
+    if (flags & R360_BUILD_PYRAMID) {
+        if (launch_pyramid(f)) return -1;
+        f->built |= R360_BUILD_PYRAMID;
+    }
+    if (flags & (R360_BUILD_CLOUD | R360_BUILD_PLANES)) {
+        r360_set_error("R360_BUILD_CLOUD/PLANES: plane extraction is not built in this version");
+        return -3;
+    }
+    return 0;
+}
+
+extern "C" int r360_frame_build(r360_frame* f, unsigned flags) {
+    int rc = r360_frame_build_async(f, flags);
+    if (rc) return rc;
+    R360_HIP(hipStreamSynchronize(f->ctx->stream));
+    return 0;
+}
+
+extern "C" int r360_frame_dims(const r360_frame* f, int* rows, int* cols, int* sph_rows, int* sph_cols) {
+    CHECK_ARG(f, "null frame");
+    if (rows) *rows = f->rows;
+    if (cols) *cols = f->cols;
+    if (sph_rows) *sph_rows = f->sph_rows;
+    if (sph_cols) *sph_cols = f->sph_cols;
+    return 0;
+}
+
+extern "C" int r360_frame_get_sphere(r360_frame* f, uint8_t* bgr, uint16_t* depth) {
+    CHECK_ARG(f, "null frame");
+    CHECK_ARG(f->built & R360_BUILD_SPHERE, "sphere not built");
+    const size_t n = (size_t)f->sph_rows * f->sph_cols;
+    R360_HIP(hipStreamSynchronize(f->ctx->stream));
+    if (bgr) R360_HIP(hipMemcpy(bgr, f->d_sph_bgr, n * 3, hipMemcpyDeviceToHost));
+    if (depth) R360_HIP(hipMemcpy(depth, f->d_sph_depth, n * 2, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+extern "C" int r360_frame_get_depth_m(r360_frame* f, float* depth8) {
+    CHECK_ARG(f && depth8, "null arg");
+    CHECK_ARG(f->built & R360_BUILD_UNDISTORT, "undistorted depth not built");
+    R360_HIP(hipStreamSynchronize(f->ctx->stream));
+    R360_HIP(hipMemcpy(depth8, f->d_depth_m, sizeof(float) * 8 * f->rows * f->cols, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+extern "C" int r360_frame_get_level(r360_frame* f, int level, int* rows, int* cols, float* gray, float* depth,
+                                    float* gx, float* gy, float* dgx, float* dgy) {
+    CHECK_ARG(f, "null frame");
+    CHECK_ARG(level >= 0 && level < f->n_levels, "level out of range");
+    CHECK_ARG(f->built & R360_BUILD_PYRAMID, "pyramid not built");
+    const LevelBufs& L = f->lv[level];
+    if (rows) *rows = L.rows;
+    if (cols) *cols = L.cols;
+    const size_t n = (size_t)L.rows * L.cols;
+    R360_HIP(hipStreamSynchronize(f->ctx->stream));
+    std::vector<float2> p0(n);
+    std::vector<float4> tg(n);
+    R360_HIP(hipMemcpy(p0.data(), L.p0, n * sizeof(float2), hipMemcpyDeviceToHost));
+    R360_HIP(hipMemcpy(tg.data(), L.tg, n * sizeof(float4), hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < n; ++i) {
+        if (gray) gray[i] = p0[i].x;
+        if (depth) depth[i] = p0[i].y;
+        if (gx) gx[i] = tg[i].x;
+        if (gy) gy[i] = tg[i].y;
+        if (dgx) dgx[i] = tg[i].z;
+        if (dgy) dgy[i] = tg[i].w;
+    }
+    return 0;
+}
+
+// ------------------------------------------------------------------ RegisterPhotoICP
+extern "C" void r360_icp_default_params(r360_icp_params* p) {
+    p->n_pyr = 4;                  // RegisterPhotoICP() (:204)
+    p->max_iters = 10;             // :4593
+    p->min_depth = 0.3f;
+    p->max_depth = 6.0f;
+    p->std_dev_photo = (float)(6. / 255);
+    p->std_dev_depth = 0.2f;
+    p->thres_sal_int = 0.01f;
+    p->thres_sal_depth = 0.01f;
+    p->tol_residual = 1e-3;
+    p->tol_update = 1e-4;
+    p->lambda = 1.0;
+    p->fixed_iters_level0 = 0;
+}
+
+static IcpConst make_const(const r360_icp_params* p, int level, int n_pixels) {
+    IcpConst C;
+    memset(&C, 0, sizeof(C));
+    C.min_d = p->min_depth; C.max_d = p->max_depth;
+    C.sd_photo = p->std_dev_photo; C.sd_depth = p->std_dev_depth;
+    C.thr_int = p->thres_sal_int; C.thr_depth = p->thres_sal_depth;
+    C.sd_photo_inv_f = (float)(1. / p->std_dev_photo);
+    C.sd_photo_inv_d = 1. / p->std_dev_photo;
+    C.tol_res = p->tol_residual; C.tol_upd = p->tol_update; C.lambda = p->lambda;
+    C.max_iters = p->max_iters; C.fixed_iters0 = p->fixed_iters_level0;
+    C.n_pixels = n_pixels; C.level = level;
+    return C;
+}
+
+static int check_pair(r360_ctx* ctx, r360_frame* trg, r360_frame* src, const r360_icp_params* p) {
+    CHECK_ARG(ctx && trg && src && p, "null arg");
+    CHECK_ARG(trg->sph_rows == src->sph_rows && trg->sph_cols == src->sph_cols, "frame size mismatch");
+    CHECK_ARG((trg->built & R360_BUILD_PYRAMID) && (src->built & R360_BUILD_PYRAMID),
+              "frames need R360_BUILD_PYRAMID (setSourceFrame/setTargetFrame)");
+    CHECK_ARG(p->n_pyr >= 1 && p->n_pyr <= src->n_levels, "n_pyr exceeds the frame's pyramid depth");
+    CHECK_ARG(p->min_depth == 0.3f && p->max_depth == 6.0f,
+              "non-default min/max depth changes the depth pyramid: not supported in this version");
+    CHECK_ARG(ctx->partials_cap >= icp_blocks_for(src->lv[0].rows * src->lv[0].cols), "partials buffer too small");
+    return 0;
+}
+
+extern "C" int r360_align360_async(r360_ctx* ctx, r360_frame* trg, r360_frame* src, const float init[16], int method,
+                                   int occlusion, const r360_icp_params* p) {
+    if (int rc = check_pair(ctx, trg, src, p)) return rc;
+    CHECK_ARG(init, "null init pose");
+    CHECK_ARG(method >= 0 && method <= 2, "invalid method");
+    CHECK_ARG(occlusion == 0, "occlusion variants (Occ1/Occ2) are not built in this version");
+    IcpState* h = ctx->h_state;
+    memset(h, 0, sizeof(IcpState));
+    memcpy(h->pose, init, sizeof(float) * 16);
+    memcpy(h->cand, init, sizeof(float) * 16);
+    R360_HIP(hipMemcpyAsync(ctx->d_state, h, sizeof(IcpState), hipMemcpyHostToDevice, ctx->stream));
+    for (int l = p->n_pyr - 1; l >= 0; --l) {
+        const int np = src->lv[l].rows * src->lv[l].cols;
+        const IcpConst C = make_const(p, l, np);
+        const int passes = 1 + ((l == 0 && p->fixed_iters_level0 > 0) ? p->fixed_iters_level0 : p->max_iters);
+        for (int k = 0; k < passes; ++k)
+            if (launch_icp_level(ctx, trg, src, l, method, C, k == 0, 0)) return -1;
+    }
+    ctx->async_nL = p->n_pyr;
+    ctx->async_pending = 1;
+    return 0;
+}
+
+extern "C" int r360_align360_result(r360_ctx* ctx, float pose_out[16], float H_out[36], float g_out[6],
+                                    r360_icp_stats* st) {
+    CHECK_ARG(ctx && ctx->async_pending, "no alignment pending");
+    IcpState* h = ctx->h_state;
+    R360_HIP(hipMemcpyAsync(h, ctx->d_state, sizeof(IcpState), hipMemcpyDeviceToHost, ctx->stream));
+    R360_HIP(hipStreamSynchronize(ctx->stream));
+    ctx->async_pending = 0;
+    if (pose_out) memcpy(pose_out, h->pose, sizeof(float) * 16);
+    if (H_out) memcpy(H_out, h->Hout, sizeof(float) * 36);
+    if (g_out) memcpy(g_out, h->gout, sizeof(float) * 6);
+    if (st) {
+        memset(st, 0, sizeof(*st));
+        for (int l = 0; l < 8; ++l) { st->iters[l] = h->iters[l]; st->evals[l] = h->evals_l[l]; }
+        st->illposed = h->illposed;
+        st->sso = h->sso;
+        st->error = h->error;
+        st->passes = h->passes;
+    }
+    return h->illposed ? 1 : 0;
+}
+
+extern "C" int r360_align360(r360_ctx* ctx, r360_frame* trg, r360_frame* src, const float init[16], int method,
+                             int occlusion, const r360_icp_params* p, float pose_out[16], float H_out[36],
+                             float g_out[6], r360_icp_stats* st) {
+    if (int rc = r360_align360_async(ctx, trg, src, init, method, occlusion, p)) return rc;
+    return r360_align360_result(ctx, pose_out, H_out, g_out, st);
+}
+
+extern "C" int r360_icp_eval(r360_ctx* ctx, r360_frame* trg, r360_frame* src, int level, const float pose[16],
+                             int method, const r360_icp_params* p, double H[36], double g[6], double* err2,
+                             int* n_valid, int* n_visible) {
+    if (int rc = check_pair(ctx, trg, src, p)) return rc;
+    CHECK_ARG(level >= 0 && level < src->n_levels, "level out of range");
+    CHECK_ARG(method >= 0 && method <= 2, "invalid method");
+    IcpState* h = ctx->h_state;
+    memset(h, 0, sizeof(IcpState));
+    memcpy(h->cand, pose, sizeof(float) * 16);
+    memcpy(h->pose, pose, sizeof(float) * 16);
+    R360_HIP(hipMemcpyAsync(ctx->d_state, h, sizeof(IcpState), hipMemcpyHostToDevice, ctx->stream));
+    const IcpConst C = make_const(p, level, src->lv[level].rows * src->lv[level].cols);
+    if (launch_icp_level(ctx, trg, src, level, method, C, 0, 1)) return -1;
+    R360_HIP(hipMemcpyAsync(h, ctx->d_state, sizeof(IcpState), hipMemcpyDeviceToHost, ctx->stream));
+    R360_HIP(hipStreamSynchronize(ctx->stream));
+    const double* s = h->sums;
+    int k = 0;
+    for (int u = 0; u < 6; ++u)
+        for (int v = u; v < 6; ++v) { H[u * 6 + v] = H[v * 6 + u] = s[k++]; }
+    for (int u = 0; u < 6; ++u) g[u] = s[21 + u];
+    if (err2) *err2 = s[R360_SUM_ERR2];
+    if (n_valid) *n_valid = (int)s[R360_SUM_NVALID];
+    if (n_visible) *n_visible = (int)s[R360_SUM_NVIS];
+    return 0;
+}
+
+// CPose3D::exp (host copy for callers of the façade, e.g. the Register() alias)
+extern "C" void r360_exp_se3(const double mu[6], int pseudo, float T[16]) {
+    const double wx = mu[3], wy = mu[4], wz = mu[5];
+    const double th2 = wx * wx + wy * wy + wz * wz, th = std::sqrt(th2);
+    double A, B, Cc;
+    if (th < 1e-6) { A = 1 - th2 / 6; B = 0.5 - th2 / 24; Cc = 1.0 / 6 - th2 / 120; }
+    else { A = std::sin(th) / th; B = (1 - std::cos(th)) / th2; Cc = (th - std::sin(th)) / (th2 * th); }
+    const double W[9] = {0, -wz, wy, wz, 0, -wx, -wy, wx, 0};
+    double W2[9];
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) {
+            double s = 0;
+            for (int k = 0; k < 3; ++k) s += W[r * 3 + k] * W[k * 3 + c];
+            W2[r * 3 + c] = s;
+        }
+    for (int c = 0; c < 4; ++c)
+        for (int r = 0; r < 4; ++r) {
+            double v;
+            const double I = (r == c) ? 1.0 : 0.0;
+            if (r < 3 && c < 3) v = I + A * W[r * 3 + c] + B * W2[r * 3 + c];
+            else if (r < 3) {
+                if (pseudo) v = mu[r];
+                else {
+                    v = 0;
+                    for (int k = 0; k < 3; ++k) v += ((r == k ? 1.0 : 0.0) + B * W[r * 3 + k] + Cc * W2[r * 3 + k]) * mu[k];
+                }
+            } else v = (c == 3) ? 1.0 : 0.0;
+            T[c * 4 + r] = (float)v;
+        }
+}

@@ -1,0 +1,199 @@
+// frame_kernels.hip — Frame360 construction on gfx950:
+//   k_undistort : loadDepthEigen + CLAMS undistort           (Frame360.h:254-258, 293-310)
+//   k_stitch    : stitchSphericalImage + cvtColor + depth m   (Frame360.h:1099-1148,
+//                 RegisterPhotoICP.h:485-486, 316-317)
+//   k_pyramid   : pyrDown (gray) + buildPyramidRange (depth)  (RegisterPhotoICP.h:292-354)
+//   k_gradient  : calcGradientXY for gray and depth + the alignFrames360 seam mask
+//                 (RegisterPhotoICP.h:365-398, 4538-4549)
+// All are HBM-streaming, one thread per output pixel.  Compiled with -ffp-contract=off so each
+// float expression rounds exactly as the reference's scalar C++ does.
+#include "../r360_internal.h"
+
+namespace {
+
+constexpr int TPB = 256;
+
+// ------------------------------------------------------------------ undistort
+__global__ void k_undistort(const uint16_t* __restrict__ depth, float* __restrict__ depth_m, int rows, int cols,
+                            const float* __restrict__ mult, const float* __restrict__ counts, int nx, int bin_w,
+                            int bin_h, int nb, double bin_depth, int apply) {
+    const long n = (long)R360_NUM_SENSORS * rows * cols;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+        float z = (float)depth[i] * 0.001f;                       // convertTo(CV_32FC1, 0.001)
+        if (apply && z != 0) {                                    // discrete_depth_distortion_model.cpp:175-186
+            const int s = (int)(i / ((long)rows * cols));
+            const int pix = (int)(i - (long)s * rows * cols);
+            const int v = pix / cols, u = pix - v * cols;
+            const long fr = ((long)s * (rows / bin_h) * nx + (long)(v / bin_h) * nx + (u / bin_w)) * nb;
+            int idx = (int)floor(z / bin_depth);
+            idx = idx < nb - 1 ? idx : nb - 1;
+            float start = (float)(bin_depth * idx);
+            int idx1 = (z - start < bin_depth / 2) ? idx : idx + 1;  // interpolatedUndistort :48-68
+            int idx0 = idx1 - 1;
+            if (idx0 < 0 || idx1 >= nb || counts[fr + idx0] < 50 || counts[fr + idx1] < 50) {
+                z *= mult[fr + idx];
+            } else {
+                double z0 = (idx0 + 1) * bin_depth - bin_depth * 0.5;
+                double c1 = (z - z0) / bin_depth;
+                double c0 = 1.0 - c1;
+                double m = c0 * mult[fr + idx0] + c1 * mult[fr + idx1];
+                z = (float)(z * m);
+            }
+        }
+        depth_m[i] = z;
+    }
+}
+
+// ------------------------------------------------------------------ stitch
+// One thread per sphere pixel.  Sensor k owns columns [(7-k)*rows, (8-k)*rows)  (:1119-1120).
+__global__ void k_stitch(const uint8_t* __restrict__ bgr8, const uint16_t* __restrict__ depth8, int rows, int cols,
+                         int H, int W, const float* __restrict__ sinphi, const float* __restrict__ cosphi,
+                         const float* __restrict__ sinth, const float* __restrict__ costh,
+                         const float* __restrict__ rt_inv, float fx, float fy, float cx, float cy,
+                         uint8_t* __restrict__ sph_bgr, uint16_t* __restrict__ sph_depth, float2* __restrict__ p0) {
+    const long n = (long)H * W;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+        const int row = (int)(i / W), col = (int)(i - (long)row * W);
+        const int k = 7 - col / rows;
+        const float* T = rt_inv + 16 * k;
+        const float v0 = sinphi[row], cos_phi = cosphi[row];
+        const float v1 = cos_phi * sinth[col];
+        const float v2 = cos_phi * costh[col];
+        float p0x = T[0] * v0 + T[4] * v1 + T[8] * v2;
+        float p1 = T[1] * v0 + T[5] * v1 + T[9] * v2;
+        float p2 = T[2] * v0 + T[6] * v1 + T[10] * v2;
+        p0x = p0x + T[12]; p1 = p1 + T[13]; p2 = p2 + T[14];
+        const float u = fx * p0x / p2 + cx;                          // :1133
+        const float v = fy * p1 / p2 + cy;                           // :1134
+        uint8_t b = 0, g = 0, r = 0;
+        uint16_t dd = 0;
+        if (u >= 0 && u < cols && v >= 0 && v < rows) {
+            const int iu = (int)u, iv = (int)v;
+            const long si = (long)k * rows * cols + (long)iv * cols + iu;
+            b = bgr8[si * 3 + 0]; g = bgr8[si * 3 + 1]; r = bgr8[si * 3 + 2];
+            const double du = (double)((u - cx) / fx), dv = (double)((v - cy) / fy);
+            dd = (uint16_t)(depth8[si] * sqrt(1 + du * du + dv * dv));  // :1142 (range in mm)
+        }
+        sph_bgr[i * 3 + 0] = b; sph_bgr[i * 3 + 1] = g; sph_bgr[i * 3 + 2] = r;
+        sph_depth[i] = dd;
+        // setSourceFrame / setTargetFrame level 0: CV_RGB2GRAY on BGR data, /255; depth *0.001
+        const int y = (b * 4899 + g * 9617 + r * 1868 + (1 << 13)) >> 14;
+        p0[i] = make_float2((float)y * (float)(1. / 255), (float)dd * 0.001f);
+    }
+}
+
+__device__ __forceinline__ int refl101(int p, int n) {
+    p = p < 0 ? -p : p;
+    return p >= n ? 2 * n - p - 2 : p;
+}
+
+// ------------------------------------------------------------------ pyramid (level l -> l+1)
+__global__ void k_pyramid(const float2* __restrict__ in, int R, int C, float2* __restrict__ out, float min_d,
+                          float max_d) {
+    const int dr = R / 2, dc = C / 2;
+    const long n = (long)dr * dc;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+        const int y = (int)(i / dc), x = (int)(i - (long)y * dc);
+        // cv::pyrDown: horizontal [1 4 6 4 1] per source row, then the vertical SSE order.
+        const int sx = 2 * x;
+        const int xa = refl101(sx - 2, C), xb = refl101(sx - 1, C), xd = refl101(sx + 1, C), xe = refl101(sx + 2, C);
+        float h[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const int yy = refl101(2 * y - 2 + k, R);
+            const float2* s = in + (long)yy * C;
+            const float a = s[xa].x, b = s[xb].x, c = s[sx].x, d = s[xd].x, e = s[xe].x;
+            h[k] = c * 6 + (b + d) * 4 + a + e;
+        }
+        float t0 = h[0] + h[4];
+        const float t1 = (h[1] + h[3]) + h[2];
+        t0 = t0 + (h[2] + h[2]);
+        t0 = t0 + t1 * 4.f;
+        const float gray = t0 * (1.f / 256);
+        // buildPyramidRange: mean of the 2x2 depths in (minDepth, maxDepth) (:330-348)
+        float av = 0.f; unsigned nv = 0;
+        const float2* s0 = in + (long)(2 * y) * C + sx;
+        const float2* s1 = s0 + C;
+        const float z0 = s0[0].y, z1 = s0[1].y, z2 = s1[0].y, z3 = s1[1].y;
+        if (z0 > min_d && z0 < max_d) { av += z0; ++nv; }
+        if (z1 > min_d && z1 < max_d) { av += z1; ++nv; }
+        if (z2 > min_d && z2 < max_d) { av += z2; ++nv; }
+        if (z3 > min_d && z3 < max_d) { av += z3; ++nv; }
+        out[i] = make_float2(gray, nv > 0 ? av / nv : 0.f);
+    }
+}
+
+// ------------------------------------------------------------------ gradients + seam mask
+__device__ __forceinline__ float harm(float fl, float f, float fr) {
+    if ((f > fr && f < fl) || (f < fr && f > fl)) return 2.f / (1 / (fr - f) + 1 / (f - fl));
+    return 0.f;
+}
+
+__global__ void k_gradient(const float2* __restrict__ p0, int R, int C, float4* __restrict__ tg) {
+    const long n = (long)R * C;
+    const int ws = C / 8;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+        const int r = (int)(i / C), c = (int)(i - (long)r * C);
+        float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+        // seam columns s*ws-1 and s*ws, s = 1..7, are zeroed by alignFrames360 (:4538-4549)
+        const int m = c % ws;
+        const bool seam = (c >= ws - 1) && (c < 7 * ws + 1) && (m == 0 || m == ws - 1);
+        if (!seam && r >= 1 && r < R - 1 && c >= 1 && c < C - 1) {
+            const float2 f = p0[i], fl = p0[i - 1], fr = p0[i + 1], fu = p0[i - C], fd = p0[i + C];
+            o.x = harm(fl.x, f.x, fr.x);
+            o.y = harm(fu.x, f.x, fd.x);
+            o.z = harm(fl.y, f.y, fr.y);
+            o.w = harm(fu.y, f.y, fd.y);
+        }
+        tg[i] = o;
+    }
+}
+
+inline int grid_for(long n) {
+    long b = (n + TPB - 1) / TPB;
+    return (int)(b < 8192 ? (b > 0 ? b : 1) : 8192);
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ launchers
+int launch_undistort(r360_frame* f) {
+    const r360_calib* c = f->calib;
+    const long n = (long)R360_NUM_SENSORS * f->rows * f->cols;
+    const bool apply = c->has_intrinsics && c->clams.width == f->cols && c->clams.height == f->rows;
+    hipLaunchKernelGGL(k_undistort, dim3(grid_for(n)), dim3(TPB), 0, f->ctx->stream, f->d_depth, f->d_depth_m, f->rows,
+                       f->cols, c->clams.d_mult, c->clams.d_counts, c->clams.nx, c->clams.bin_w, c->clams.bin_h,
+                       c->clams.num_bins, c->clams.bin_depth, apply ? 1 : 0);
+    R360_HIP(hipGetLastError());
+    return 0;
+}
+
+int launch_stitch(r360_frame* f) {
+    const r360_calib* c = f->calib;
+    const long n = (long)f->sph_rows * f->sph_cols;
+    const int slot = timing_begin(f->ctx, "k_stitch");
+    hipLaunchKernelGGL(k_stitch, dim3(grid_for(n)), dim3(TPB), 0, f->ctx->stream, f->d_bgr, f->d_depth, f->rows,
+                       f->cols, f->sph_rows, f->sph_cols, c->d_st_sinphi, c->d_st_cosphi, c->d_st_sinth,
+                       c->d_st_costh, c->d_rt_inv, c->K[0], c->K[4], c->K[6], c->K[7], f->d_sph_bgr,
+                       f->d_sph_depth, f->lv[0].p0);
+    timing_end(f->ctx, slot);
+    R360_HIP(hipGetLastError());
+    return 0;
+}
+
+int launch_pyramid(r360_frame* f) {
+    // RegisterPhotoICP constructor defaults minDepth 0.3 / maxDepth 6.0 (:202-203)
+    const float min_d = 0.3f, max_d = 6.0f;
+    for (int l = 1; l < f->n_levels; ++l) {
+        const long n = (long)f->lv[l].rows * f->lv[l].cols;
+        hipLaunchKernelGGL(k_pyramid, dim3(grid_for(n)), dim3(TPB), 0, f->ctx->stream, f->lv[l - 1].p0,
+                           f->lv[l - 1].rows, f->lv[l - 1].cols, f->lv[l].p0, min_d, max_d);
+    }
+    for (int l = 0; l < f->n_levels; ++l) {
+        const long n = (long)f->lv[l].rows * f->lv[l].cols;
+        hipLaunchKernelGGL(k_gradient, dim3(grid_for(n)), dim3(TPB), 0, f->ctx->stream, f->lv[l].p0, f->lv[l].rows,
+                           f->lv[l].cols, f->lv[l].tg);
+    }
+    R360_HIP(hipGetLastError());
+    return 0;
+}

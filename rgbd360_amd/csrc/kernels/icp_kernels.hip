@@ -1,0 +1,483 @@
+// icp_kernels.hip — the fused spherical photometric+geometric ICP pass for gfx950.
+//
+// One launch = one "pass" of RegisterPhotoICP::alignFrames360 at one pyramid level:
+//   errorPhotoICP_sphere (RegisterPhotoICP.h:2545-2739) and calcHessGrad_sphere (:2745-3228)
+//   evaluated together at the same pose (they share the transform/projection/gathers), the
+//   6x6 JtJ / 6x1 Jtr / error / count sums reduced in two stages (wave butterfly in registers
+//   -> LDS across waves -> one fp64 record per workgroup -> the last-arriving workgroup sums the
+//   records in a fixed order), and the Gauss-Newton step (:4611-4722) executed by that last
+//   workgroup on the device.  No host round trip per iteration: the host enqueues
+//   1 + maxIters passes per level and passes after convergence exit at entry.
+//
+// Memory: per source pixel 8 B ({gray, depth} float2, streamed); per visible pixel 16 B target
+// gradients {gx, gy, dgx, dgy} + 8 B target {gray, depth} gathered — the 8N + 24V algorithmic
+// bytes of SURVEY.md §8(d).  No Jacobian rows are materialised (the reference writes and
+// re-reads imgSize x 6 buffers, :2761-2767).
+#include "../r360_internal.h"
+
+namespace {
+
+constexpr int TPB = 256;
+constexpr int NW = TPB / 64;
+
+struct Pose12 { float R[9]; float t[3]; };
+
+__device__ __forceinline__ float huberf(float e, float reg) {  // weightHuber<float> (:545-554)
+    const float a = fabsf(e);
+    if (a < reg) return 1.f;
+    return sqrtf(2 * reg * a - reg * reg) / a;
+}
+
+// Accumulator slots: 0..20 upper-triangle H (row-major), 21..26 g, 27 n_valid, 28 n_visible.
+struct Acc {
+    float h[32];
+    double err2;
+};
+
+__device__ __forceinline__ void acc_row(Acc& A, const float J[6], float r) {
+    A.h[0] += J[0] * J[0];
+    A.h[1] += J[0] * J[1];
+    A.h[2] += J[0] * J[2];
+    A.h[3] += J[0] * J[3];
+    A.h[4] += J[0] * J[4];
+    A.h[5] += J[0] * J[5];
+    A.h[6] += J[1] * J[1];
+    A.h[7] += J[1] * J[2];
+    A.h[8] += J[1] * J[3];
+    A.h[9] += J[1] * J[4];
+    A.h[10] += J[1] * J[5];
+    A.h[11] += J[2] * J[2];
+    A.h[12] += J[2] * J[3];
+    A.h[13] += J[2] * J[4];
+    A.h[14] += J[2] * J[5];
+    A.h[15] += J[3] * J[3];
+    A.h[16] += J[3] * J[4];
+    A.h[17] += J[3] * J[5];
+    A.h[18] += J[4] * J[4];
+    A.h[19] += J[4] * J[5];
+    A.h[20] += J[5] * J[5];
+    A.h[21] += J[0] * r;
+    A.h[22] += J[1] * r;
+    A.h[23] += J[2] * r;
+    A.h[24] += J[3] * r;
+    A.h[25] += J[4] * r;
+    A.h[26] += J[5] * r;
+}
+
+template <int METHOD>
+__device__ __forceinline__ void pixel(Acc& A, const Pose12& P, float d, float gray_s, float sp, float cp, float st,
+                                      float ct, const float2* __restrict__ trg, const float4* __restrict__ tg,
+                                      int nRows, int nCols, float half_nRows, float angle_res_inv,
+                                      const IcpConst& C) {
+    if (!(C.min_d < d && d < C.max_d)) return;                     // LUT validity (:4578)
+    const float lx = d * sp;                                       // LUT_xyz_sphere (:4580-4582)
+    const float ly = -d * cp * st;
+    const float lz = -d * cp * ct;
+    float X = P.R[0] * lx + P.R[1] * ly + P.R[2] * lz; X = X + P.t[0];
+    float Y = P.R[3] * lx + P.R[4] * ly + P.R[5] * lz; Y = Y + P.t[1];
+    float Z = P.R[6] * lx + P.R[7] * ly + P.R[8] * lz; Z = Z + P.t[2];
+    const float dist = sqrtf(X * X + Y * Y + Z * Z);
+    const float dist_inv = 1.f / dist;
+    const float phi_trg = asinf(X * dist_inv);
+    const float theta_trg = (float)((double)atan2f(Y, Z) + R360_PI);
+    const int r = (int)roundf(half_nRows - phi_trg * angle_res_inv);
+    const int c = (int)roundf(theta_trg * angle_res_inv);
+    if (!((r >= 0 && r < nRows) && c < nCols)) return;            // (:2989)
+    A.h[28] += 1.f;                                                 // numVisiblePixels
+    const long t = (long)r * nCols + c;
+    const float4 G = tg[t];                                         // {gx, gy, dgx, dgy}
+    const bool photo = (METHOD == R360_PHOTO_CONSISTENCY || METHOD == R360_PHOTO_DEPTH);
+    const bool depth = (METHOD == R360_DEPTH_CONSISTENCY || METHOD == R360_PHOTO_DEPTH);
+    if (photo && fabsf(G.x) < C.thr_int && fabsf(G.y) < C.thr_int) return;  // 'continue' (:3038)
+    const float2 T = trg[t];                                        // {gray, depth} of target
+    // jacobianProj23 * jacobianT36 (:2995-3026), jacobianT36 = [I | -skew(p')]
+    const float z_inv = 1.f / Z;
+    const float z_inv2 = z_inv * z_inv;
+    const float D_atan_theta = 1.f / (1 + Y * Y * z_inv2) * angle_res_inv;
+    const float P01 = D_atan_theta * z_inv;
+    const float P02 = -Y * z_inv2 * D_atan_theta;
+    const float dist_inv2 = dist_inv * dist_inv;
+    const float x_dist_inv2 = X * dist_inv2;
+    const float D_asin = 1.f / sqrtf(1 - X * x_dist_inv2) * angle_res_inv;
+    const float P10 = -D_asin * dist_inv * (1 - X * x_dist_inv2);
+    const float P11 = D_asin * (x_dist_inv2 * Y * dist_inv);
+    const float P12 = D_asin * (x_dist_inv2 * Z * dist_inv);
+    // T36 rows: (1,0,0,0,Z,-Y) (0,1,0,-Z,0,X) (0,0,1,Y,-X,0)
+    const float T0[6] = {1, 0, 0, 0, Z, -Y};
+    const float T1[6] = {0, 1, 0, -Z, 0, X};
+    const float T2[6] = {0, 0, 1, Y, -X, 0};
+    float Jw0[6], Jw1[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        Jw0[k] = 0.f * T0[k] + P01 * T1[k] + P02 * T2[k];
+        Jw1[k] = P10 * T0[k] + P11 * T1[k] + P12 * T2[k];
+    }
+    if (photo) {
+        const float photoDiff = T.x - gray_s;
+        const float wh = huberf(photoDiff, C.sd_photo);
+        // errorPhotoICP_sphere: double weight, float residual (:2699-2709)
+        const float wEd = (float)((double)wh * C.sd_photo_inv_d * photoDiff);
+        A.err2 += (double)(wEd * wEd);
+        A.h[27] += 1.f;
+        // calcHessGrad_sphere: float weight (:3047-3052)
+        const float w = wh * C.sd_photo_inv_f;
+        const float res = w * photoDiff;
+        const float wgx = w * G.x, wgy = w * G.y;
+        float J[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) J[k] = wgx * Jw0[k] + wgy * Jw1[k];
+        acc_row(A, J, res);
+    }
+    if (depth) {
+        const float depth2 = T.y;
+        if (isfinite(depth2)) {
+            if (fabsf(G.z) < C.thr_depth && fabsf(G.w) < C.thr_depth) return;  // (:3072-3073)
+            const float depthDiff = depth2 - dist;
+            const float sd = C.sd_depth * depth2;
+            const float w = huberf(depthDiff, sd) / sd;
+            const float wE = (float)((double)w * depthDiff);
+            A.err2 += (double)(wE * wE);
+            A.h[27] += 1.f;
+            const float res = w * depthDiff;
+            const float js0 = X * dist_inv, js1 = Y * dist_inv, js2 = Z * dist_inv;
+            float J[6];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                const float ga = G.z * Jw0[k] + G.w * Jw1[k];
+                const float gb = js0 * T0[k] + js1 * T1[k] + js2 * T2[k];
+                J[k] = w * (ga - gb);
+            }
+            acc_row(A, J, res);
+        }
+    }
+}
+
+// Butterfly reduce-scatter of 32 floats across a 64-lane wave: 32 shuffles instead of 32*6.
+// On return lane L holds the wave total of slot idx(L) = (bit5 bit4 bit3 bit2 bit1 of L) in a
+// fixed bit order, identical for lanes L and L^1.
+template <int M, int HALF>
+__device__ __forceinline__ void bfly_step(float (&v)[32], int lane) {
+    const bool hi = (lane & M) != 0;
+#pragma unroll
+    for (int j = 0; j < HALF; ++j) {
+        const float keep = hi ? v[j + HALF] : v[j];
+        const float send = hi ? v[j] : v[j + HALF];
+        v[j] = keep + __shfl_xor(send, M, 64);
+    }
+}
+
+__device__ __forceinline__ float wave_reduce_scatter32(float (&v)[32], int lane) {
+    bfly_step<32, 16>(v, lane);
+    bfly_step<16, 8>(v, lane);
+    bfly_step<8, 4>(v, lane);
+    bfly_step<4, 2>(v, lane);
+    bfly_step<2, 1>(v, lane);
+    return v[0] + __shfl_xor(v[0], 1, 64);
+}
+
+__device__ __forceinline__ int scatter_slot(int lane) {
+    // step with mask 32 selects the upper half (+16), mask 16 -> +8, ... mask 2 -> +1
+    return ((lane >> 5) & 1) * 16 + ((lane >> 4) & 1) * 8 + ((lane >> 3) & 1) * 4 + ((lane >> 2) & 1) * 2 +
+           ((lane >> 1) & 1);
+}
+
+__device__ __forceinline__ double wave_sum_d(double x) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) x += __shfl_xor(x, m, 64);
+    return x;
+}
+
+// ---------------------------------------------------------------- GN step (thread 0 of last block)
+// The GN helpers work in an LDS workspace (only thread 0 of the last workgroup runs them), so the
+// pass kernel needs no scratch memory and its register budget is set by the pixel loop alone.
+struct GnWork { double M[36]; double A[42]; double Hd[36]; double HL[36]; double gd[6]; double x[6]; float Hc[36]; float gc[6]; float E[16]; };
+
+__device__ int rank6(const double* Min, double* M) {     // Eigen FullPivLU::rank(), default threshold
+    for (int i = 0; i < 36; ++i) M[i] = Min[i];
+    double piv[6];
+    for (int k = 0; k < 6; ++k) {
+        int br = k, bc = k; double bv = -1;
+        for (int r = k; r < 6; ++r)
+            for (int c = k; c < 6; ++c)
+                if (fabs(M[r * 6 + c]) > bv) { bv = fabs(M[r * 6 + c]); br = r; bc = c; }
+        for (int c = 0; c < 6; ++c) { double t = M[k * 6 + c]; M[k * 6 + c] = M[br * 6 + c]; M[br * 6 + c] = t; }
+        for (int r = 0; r < 6; ++r) { double t = M[r * 6 + k]; M[r * 6 + k] = M[r * 6 + bc]; M[r * 6 + bc] = t; }
+        piv[k] = M[k * 6 + k];
+        if (piv[k] != 0)
+            for (int r = k + 1; r < 6; ++r) {
+                double f = M[r * 6 + k] / piv[k];
+                for (int c = k; c < 6; ++c) M[r * 6 + c] -= f * M[k * 6 + c];
+            }
+    }
+    const double thr = 1.1920928955078125e-07 * 6 * fabs(piv[0]);
+    int rk = 0;
+    for (int k = 0; k < 6; ++k) rk += fabs(piv[k]) > thr;
+    return rk;
+}
+
+__device__ void solve6(const double* H, const double* g, double* x, double* A) {  // x = -H^-1 g (:4693)
+#define A_(r, c) A[(r) * 7 + (c)]
+    for (int r = 0; r < 6; ++r) { for (int c = 0; c < 6; ++c) A_(r, c) = H[r * 6 + c]; A_(r, 6) = -g[r]; }
+    for (int k = 0; k < 6; ++k) {
+        int p = k;
+        for (int r = k + 1; r < 6; ++r) if (fabs(A_(r, k)) > fabs(A_(p, k))) p = r;
+        for (int c = 0; c < 7; ++c) { double t = A_(k, c); A_(k, c) = A_(p, c); A_(p, c) = t; }
+        for (int r = k + 1; r < 6; ++r) {
+            double f = A_(r, k) / A_(k, k);
+            for (int c = k; c < 7; ++c) A_(r, c) -= f * A_(k, c);
+        }
+    }
+    for (int r = 5; r >= 0; --r) {
+        double s = A_(r, 6);
+        for (int c = r + 1; c < 6; ++c) s -= A_(r, c) * x[c];
+        x[r] = s / A_(r, r);
+    }
+#undef A_
+}
+
+__device__ void exp_se3(const double mu[6], int pseudo, float T[16]) {  // CPose3D::exp
+    const double wx = mu[3], wy = mu[4], wz = mu[5];
+    const double th2 = wx * wx + wy * wy + wz * wz, th = sqrt(th2);
+    double A, B, Cc;
+    if (th < 1e-6) { A = 1 - th2 / 6; B = 0.5 - th2 / 24; Cc = 1.0 / 6 - th2 / 120; }
+    else { A = sin(th) / th; B = (1 - cos(th)) / th2; Cc = (th - sin(th)) / (th2 * th); }
+    const double W[9] = {0, -wz, wy, wz, 0, -wx, -wy, wx, 0};
+    double W2[9];
+    _Pragma("unroll") for (int r = 0; r < 3; ++r)
+        _Pragma("unroll") for (int c = 0; c < 3; ++c) {
+            double s = 0;
+            _Pragma("unroll") for (int k = 0; k < 3; ++k) s += W[r * 3 + k] * W[k * 3 + c];
+            W2[r * 3 + c] = s;
+        }
+    double R[9], V[9];
+    _Pragma("unroll") for (int i = 0; i < 9; ++i) {
+        const double I = (i % 4 == 0) ? 1.0 : 0.0;
+        R[i] = I + A * W[i] + B * W2[i];
+        V[i] = I + B * W[i] + Cc * W2[i];
+    }
+    double t[3];
+    _Pragma("unroll") for (int r = 0; r < 3; ++r) t[r] = pseudo ? mu[r] : V[r * 3] * mu[0] + V[r * 3 + 1] * mu[1] + V[r * 3 + 2] * mu[2];
+    _Pragma("unroll") for (int c = 0; c < 4; ++c)
+        _Pragma("unroll") for (int r = 0; r < 4; ++r) {
+            double v;
+            if (r < 3 && c < 3) v = R[r * 3 + c];
+            else if (r < 3) v = t[r];
+            else v = (c == 3) ? 1.0 : 0.0;
+            T[c * 4 + r] = (float)v;
+        }
+}
+
+__device__ void matmul4f(const float* A, const float* B, float* Cm) {  // Eigen Matrix4f product order
+    float out[16];
+    _Pragma("unroll") for (int c = 0; c < 4; ++c)
+        _Pragma("unroll") for (int r = 0; r < 4; ++r) {
+            float s = A[r] * B[c * 4];
+            _Pragma("unroll") for (int k = 1; k < 4; ++k) s += A[k * 4 + r] * B[c * 4 + k];
+            out[c * 4 + r] = s;
+        }
+    _Pragma("unroll") for (int i = 0; i < 16; ++i) Cm[i] = out[i];
+}
+
+__device__ void gn_step(IcpState* S, const double* sums, const IcpConst& C, int first, GnWork* W) {
+    const double err2 = sums[R360_SUM_ERR2];
+    const double nvalid = sums[R360_SUM_NVALID];
+    const double new_err = sqrt(err2 / nvalid);
+    float* Hc = W->Hc; float* gc = W->gc;
+    {
+        int k = 0;
+        for (int u = 0; u < 6; ++u)
+            for (int v = u; v < 6; ++v) { Hc[u * 6 + v] = Hc[v * 6 + u] = (float)sums[k++]; }
+        for (int u = 0; u < 6; ++u) gc[u] = (float)sums[21 + u];
+    }
+    const float sso_c = (float)(sums[R360_SUM_NVIS] / C.n_pixels);
+    S->passes++;
+    if (first) {                                   // level start: error(pose_estim)  (:4599-4605)
+        S->error = new_err; S->diff_error = new_err;
+        for (int k = 0; k < 6; ++k) S->upd[k] = 1.f;
+        S->it = 0; S->loops = 0; S->evals = 0;
+        for (int k = 0; k < 36; ++k) S->Hcur[k] = Hc[k];
+        for (int k = 0; k < 6; ++k) S->gcur[k] = gc[k];
+        S->sso_cur = sso_c;
+    } else {                                       // candidate evaluated (:4705-4722)
+        S->evals++;
+        const double diff = S->error - new_err;
+        S->diff_error = diff;
+        if (diff > C.tol_res) {
+            for (int k = 0; k < 16; ++k) S->pose[k] = S->cand[k];
+            S->error = new_err;
+            S->it = S->it + 1;
+            for (int k = 0; k < 36; ++k) S->Hcur[k] = Hc[k];
+            for (int k = 0; k < 6; ++k) S->gcur[k] = gc[k];
+            S->sso_cur = sso_c;
+        }
+    }
+    const bool fixed = (C.level == 0 && C.fixed_iters0 > 0);
+    float nu = 0.f;
+    for (int k = 0; k < 6; ++k) nu += S->upd[k] * S->upd[k];
+    nu = sqrtf(nu);
+    const bool cont = fixed ? (S->loops < C.fixed_iters0)
+                            : (S->it < C.max_iters && nu > C.tol_upd && S->diff_error > C.tol_res);  // (:4611)
+    if (!cont) {
+        S->active = 0;
+        S->iters[C.level] = S->it;
+        S->evals_l[C.level] = S->evals;
+        return;
+    }
+    S->loops++;
+    double* Hd = W->Hd; double* HL = W->HL; double* gd = W->gd;
+    for (int k = 0; k < 36; ++k) { Hd[k] = S->Hcur[k]; HL[k] = Hd[k]; }
+    for (int k = 0; k < 6; ++k) { gd[k] = S->gcur[k]; HL[k * 7] += C.lambda * Hd[k * 7]; }
+    for (int k = 0; k < 36; ++k) S->Hout[k] = S->Hcur[k];
+    for (int k = 0; k < 6; ++k) S->gout[k] = S->gcur[k];
+    S->sso = S->sso_cur;
+    if (rank6(HL, W->M) != 6) {                          // ILL-POSED: stop the whole alignment (:4682-4690)
+        S->illposed = 1; S->stop = 1; S->active = 0;
+        S->iters[C.level] = S->it;
+        S->evals_l[C.level] = S->evals;
+        return;
+    }
+    double* x = W->x;
+    solve6(Hd, gd, x, W->A);
+    double ud[6];
+    for (int k = 0; k < 6; ++k) { S->upd[k] = (float)x[k]; ud[k] = S->upd[k]; }
+    float* E = W->E;
+    exp_se3(ud, 1, E);                             // pseudo-exponential (:4697)
+    matmul4f(E, S->pose, S->cand);
+    S->active = 1;
+}
+
+// ---------------------------------------------------------------- the fused pass
+template <int METHOD>
+__global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src, const float2* __restrict__ trg,
+                                                 const float4* __restrict__ tg, const float* __restrict__ sinphi,
+                                                 const float* __restrict__ cosphi, const float* __restrict__ sinth,
+                                                 const float* __restrict__ costh, int nRows, int nCols,
+                                                 IcpConst C, IcpState* S, double* __restrict__ partials, int first,
+                                                 int eval_only) {
+    __shared__ float s_red[NW][32];
+    __shared__ double s_err[NW];
+    __shared__ double s_fin[8][32];
+    __shared__ int s_last;
+    __shared__ GnWork s_gn;
+
+    if (S->stop) return;
+    if (!first && !S->active && !eval_only) return;
+
+    const float* pm = (first && !eval_only) ? S->pose : S->cand;
+    Pose12 P;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) P.R[r * 3 + c] = pm[c * 4 + r];
+        P.t[r] = pm[12 + r];
+    }
+    const float angle_res = (float)(2 * R360_PI / nCols);
+    const float angle_res_inv = 1 / angle_res;
+    const float half_nRows = (float)(0.5 * nRows - 0.5);
+
+    Acc A;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) A.h[k] = 0.f;
+    A.err2 = 0.0;
+
+    const int units = (nRows * nCols) >> 2;  // 4 pixels of one row per unit (nCols % 4 == 0)
+    const float4* src4 = reinterpret_cast<const float4*>(src);
+    const float4* st4 = reinterpret_cast<const float4*>(sinth);
+    const float4* ct4 = reinterpret_cast<const float4*>(costh);
+    const int cq = nCols >> 2;
+    for (int u = blockIdx.x * TPB + threadIdx.x; u < units; u += gridDim.x * TPB) {
+        const int r = u / cq;
+        const int c4 = u - r * cq;
+        const float4 a = src4[2 * u], b = src4[2 * u + 1];  // {g0,d0,g1,d1} {g2,d2,g3,d3}
+        const float4 s = st4[c4], c = ct4[c4];
+        const float sp = sinphi[r], cp = cosphi[r];
+        pixel<METHOD>(A, P, a.y, a.x, sp, cp, s.x, c.x, trg, tg, nRows, nCols, half_nRows, angle_res_inv, C);
+        pixel<METHOD>(A, P, a.w, a.z, sp, cp, s.y, c.y, trg, tg, nRows, nCols, half_nRows, angle_res_inv, C);
+        pixel<METHOD>(A, P, b.y, b.x, sp, cp, s.z, c.z, trg, tg, nRows, nCols, half_nRows, angle_res_inv, C);
+        pixel<METHOD>(A, P, b.w, b.z, sp, cp, s.w, c.w, trg, tg, nRows, nCols, half_nRows, angle_res_inv, C);
+    }
+
+    // ---- stage 1: wave butterfly (f32) -> LDS -> per-workgroup fp64 record
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const float mine = wave_reduce_scatter32(A.h, lane);
+    const double e2 = wave_sum_d(A.err2);
+    if ((lane & 1) == 0) s_red[wid][scatter_slot(lane)] = mine;
+    if (lane == 0) s_err[wid] = e2;
+    __syncthreads();
+    if (threadIdx.x < 32) {
+        double v;
+        if (threadIdx.x == R360_SUM_ERR2) {
+            v = 0; for (int w = 0; w < NW; ++w) v += s_err[w];
+        } else {
+            v = 0; for (int w = 0; w < NW; ++w) v += (double)s_red[w][threadIdx.x];
+        }
+        partials[(long)blockIdx.x * 32 + threadIdx.x] = v;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    // ---- stage 2: arrival ticket; the last workgroup reduces all records and runs the GN step
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned prev = __hip_atomic_fetch_add(&S->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = (prev == gridDim.x - 1);
+    }
+    __syncthreads();
+    if (!s_last) return;
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    {
+        const int v = threadIdx.x & 31, grp = threadIdx.x >> 5;  // 8 groups of 32
+        double acc = 0.0;
+        for (int bk = grp; bk < (int)gridDim.x; bk += 8) acc += partials[(long)bk * 32 + v];
+        s_fin[grp][v] = acc;
+    }
+    __syncthreads();
+    if (threadIdx.x < 32) {
+        double t = 0.0;
+        for (int g = 0; g < 8; ++g) t += s_fin[g][threadIdx.x];
+        s_fin[0][threadIdx.x] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (eval_only) {
+            for (int k = 0; k < 32; ++k) S->sums[k] = s_fin[0][k];
+        } else {
+            gn_step(S, s_fin[0], C, first, &s_gn);
+        }
+        S->ticket = 0;
+    }
+}
+
+}  // namespace
+
+int icp_blocks_for(int n_pixels) {
+    const int units = n_pixels / 4;
+    int b = (units + TPB * 2 - 1) / (TPB * 2);
+    if (b > 1024) b = 1024;
+    return b < 1 ? 1 : b;
+}
+
+int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src, int level, int method,
+                     const IcpConst& C, int first, int eval_only) {
+    const LevelBufs& Ls = src->lv[level];
+    const LevelBufs& Lt = trg->lv[level];
+    const LevelTrig& T = src->calib->trig[level];
+    const int nb = icp_blocks_for(Ls.rows * Ls.cols);
+    const char* name = level == 0 ? "k_icp_pass_L0" : "k_icp_pass";
+    const int slot = timing_begin(ctx, name);
+#define R360_LAUNCH(M)                                                                                       \
+    hipLaunchKernelGGL(k_icp_pass<M>, dim3(nb), dim3(TPB), 0, ctx->stream, Ls.p0, Lt.p0, Lt.tg, T.sinphi,   \
+                       T.cosphi, T.sinth, T.costh, Ls.rows, Ls.cols, C, ctx->d_state, ctx->d_partials, first, \
+                       eval_only)
+    if (method == R360_PHOTO_CONSISTENCY) R360_LAUNCH(R360_PHOTO_CONSISTENCY);
+    else if (method == R360_DEPTH_CONSISTENCY) R360_LAUNCH(R360_DEPTH_CONSISTENCY);
+    else R360_LAUNCH(R360_PHOTO_DEPTH);
+#undef R360_LAUNCH
+    timing_end(ctx, slot);
+    R360_HIP(hipGetLastError());
+    return 0;
+}

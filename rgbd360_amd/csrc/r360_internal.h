@@ -1,0 +1,140 @@
+// r360_internal.h — internal types shared by the HIP kernels and the host runtime of
+// librgbd360_hip.so.  Not part of the ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+#include <vector>
+#include "../../include/rgbd360_hip.h"
+
+#define R360_PI 3.14159265359  // include/Miscellaneous.h:44 (double literal)
+
+// ------------------------------------------------------------------ error plumbing
+void r360_set_error(const char* fmt, ...);
+#define R360_HIP(call)                                                                  \
+    do {                                                                                \
+        hipError_t _e = (call);                                                         \
+        if (_e != hipSuccess) {                                                         \
+            r360_set_error("%s:%d %s -> %s", __FILE__, __LINE__, #call, hipGetErrorString(_e)); \
+            return -1;                                                                  \
+        }                                                                               \
+    } while (0)
+
+// ------------------------------------------------------------------ device layouts
+// One pyramid level of a frame's sphere, as the fused ICP pass reads it:
+//   p0[i] = {gray, depth}          (source stream AND target gather)   8 B/px
+//   tg[i] = {gx, gy, dgx, dgy}     (target gradients, seam-masked)    16 B/px
+struct LevelBufs {
+    int rows = 0, cols = 0;
+    float2* p0 = nullptr;
+    float4* tg = nullptr;
+};
+
+// Per-geometry trigonometric tables, computed on the host with the same float expressions
+// as the reference (RegisterPhotoICP.h:4555-4569), so the device LUT is bit-identical.
+struct LevelTrig {
+    float* sinphi = nullptr;  // [rows]
+    float* cosphi = nullptr;  // [rows]
+    float* sinth = nullptr;   // [cols]
+    float* costh = nullptr;   // [cols]
+};
+
+struct IcpConst {
+    float min_d, max_d, sd_photo, sd_depth, thr_int, thr_depth;
+    float sd_photo_inv_f;     // float stdDevPhoto_inv = 1./stdDevPhoto   (:2774)
+    float pad0;
+    double sd_photo_inv_d;    // double stdDevPhoto_inv = 1./stdDevPhoto  (:2561)
+    double tol_res, tol_upd, lambda;
+    int max_iters, fixed_iters0, n_pixels, level;
+};
+
+// Device-resident Gauss-Newton state of one alignFrames360 call.
+struct IcpState {
+    float pose[16];     // pose_estim
+    float cand[16];     // pose evaluated by the next pass
+    float Hcur[36];     // H at pose_estim
+    float gcur[6];
+    float Hout[36];     // 'hessian' member: H of the last solve
+    float gout[6];
+    float upd[6];
+    float sso_cur, sso;
+    double error, diff_error;
+    int it, loops, evals, active, stop, illposed, passes, level;
+    int iters[8], evals_l[8];
+    unsigned ticket;
+    int pad1;
+    double sums[32];    // last pass sums (eval mode)
+};
+
+enum { R360_SUM_NVALID = 27, R360_SUM_NVIS = 28, R360_SUM_ERR2 = 31, R360_NSUMS = 32 };
+
+// ------------------------------------------------------------------ host objects
+struct r360_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    IcpState* d_state = nullptr;
+    double* d_partials = nullptr;
+    int partials_cap = 0;
+    IcpState* h_state = nullptr;  // pinned
+    int timing = 0;
+    std::vector<hipEvent_t> ev_pool;
+    int ev_used = 0;
+    struct TimedLaunch { std::string name; int a, b; };
+    std::vector<TimedLaunch> pending;
+    struct Acc { double ms = 0; long n = 0; };
+    std::vector<std::pair<std::string, Acc>> acc;
+    // async-align bookkeeping
+    int async_nL = 0, async_pending = 0;
+};
+
+struct ClamsDev {
+    int width = 0, height = 0, bin_w = 0, bin_h = 0, nx = 0, ny = 0, num_bins = 0;
+    double bin_depth = 2.0;
+    float* d_mult = nullptr;    // [8][ny*nx][num_bins]
+    float* d_counts = nullptr;  // [8][ny*nx][num_bins]
+};
+
+struct r360_calib {
+    r360_ctx* ctx = nullptr;
+    int rows = 0, cols = 0;
+    float rt[8][16];       // Rt_  (col-major)
+    float rt_inv[8][16];   // Rt_inv
+    float K[9];            // cameraMatrix (col-major)
+    bool has_intrinsics = false;
+    ClamsDev clams;
+    // stitch tables (Frame360.h:1104-1129): per sphere row sin/cos(phi_i); per col sin/cos(theta_i)
+    int sph_rows = 0, sph_cols = 0;
+    float* d_st_sinphi = nullptr;
+    float* d_st_cosphi = nullptr;
+    float* d_st_sinth = nullptr;
+    float* d_st_costh = nullptr;
+    float* d_rt_inv = nullptr;  // [8][16]
+    // ICP trig tables per pyramid level of the sphere
+    int n_levels = 0;
+    LevelTrig trig[R360_MAX_PYR];
+};
+
+struct r360_frame {
+    r360_ctx* ctx = nullptr;
+    const r360_calib* calib = nullptr;
+    int rows = 0, cols = 0, sph_rows = 0, sph_cols = 0, n_levels = 0;
+    uint8_t* d_bgr = nullptr;      // [8][rows][cols][3]
+    uint16_t* d_depth = nullptr;   // [8][rows][cols] mm
+    float* d_depth_m = nullptr;    // [8][rows][cols] undistorted metres
+    uint8_t* d_sph_bgr = nullptr;  // [H][W][3]
+    uint16_t* d_sph_depth = nullptr;
+    LevelBufs lv[R360_MAX_PYR];
+    unsigned built = 0;
+};
+
+// ------------------------------------------------------------------ kernel launchers
+int launch_undistort(r360_frame* f);
+int launch_stitch(r360_frame* f);
+int launch_pyramid(r360_frame* f);
+int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src, int level,
+                     int method, const IcpConst& C, int first, int eval_only);
+int icp_blocks_for(int n_pixels);
+
+// timing helpers (host_runtime.cpp)
+int  timing_begin(r360_ctx* ctx, const char* name);
+void timing_end(r360_ctx* ctx, int slot);

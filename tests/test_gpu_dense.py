@@ -1,0 +1,162 @@
+"""GPU parity tests of the dense half of the hot path (run on an MI355X through gpurun):
+undistort, stitch, pyramids/gradients, the fused ICP pass and alignFrames360, all through the C-ABI,
+compared with the CPU oracle on the same inputs.
+
+Bars: integer/byte outputs and the deterministic float pipelines (stitch, gray, pyramids,
+gradients, CLAMS) are bit-exact; the ICP sums differ only by fp64 summation order and rare 1-ulp
+asinf/atan2f rounding flips (glibc vs ocml), so H/g/err2 are checked to 1e-5 relative and the counts
+to 1e-4 of the pixels; poses to the north-star tolerance 1e-4 rad / 1e-3 m."""
+import os
+
+import numpy as np
+import pytest
+
+import rgbd360_amd as R
+from oracle import oracle360 as O
+
+pytestmark = pytest.mark.gpu
+
+ROT_TOL, TRANS_TOL = 1e-4, 1e-3
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = R.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def qvga(ctx):
+    cal = R.Calib360(ctx, 240, 320)
+    cal.loadExtrinsicCalibration(R.EXTRINSICS_DIR)
+    cal.loadIntrinsicCalibration(R.INTRINSICS_DIR)
+    f1, f2 = R.Frame360(cal), R.Frame360(cal)
+    f1.loadFrame(os.path.join(R.SAMPLES_DIR, "sphere_images_1.bin"))
+    f2.loadFrame(os.path.join(R.SAMPLES_DIR, "sphere_images_10.bin"))
+    f1.build(); f2.build()
+    b1, d1 = O.load_bin(os.path.join(R.SAMPLES_DIR, "sphere_images_1.bin"))
+    b2, d2 = O.load_bin(os.path.join(R.SAMPLES_DIR, "sphere_images_10.bin"))
+    rt, rti, K = cal.extrinsics()
+    Km = K.reshape(3, 3).T
+    return dict(cal=cal, f1=f1, f2=f2, raw=(b1, d1, b2, d2), rti=rti, K=Km)
+
+
+def _pose_err(A, B):
+    return O.rot_angle(A, B), float(np.linalg.norm(np.asarray(A)[:3, 3] - np.asarray(B)[:3, 3]))
+
+
+def test_undistort_bitexact(qvga):
+    b1, d1, _, _ = qvga["raw"]
+    gpu = qvga["f1"].depth_m()
+    for k in range(8):
+        cl = O.Clams(os.path.join(R.INTRINSICS_DIR, f"distortion_model{k + 1}.r360"))
+        ref = cl.undistort(O.depth_to_m(d1[k]))
+        assert np.array_equal(gpu[k], ref), k
+
+
+def test_stitch_bitexact(qvga):
+    b1, d1, b2, d2 = qvga["raw"]
+    for f, b, d in ((qvga["f1"], b1, d1), (qvga["f2"], b2, d2)):
+        gb, gd = f.sphere()
+        ob, od = O.stitch(b, d, qvga["rti"], qvga["K"])
+        assert np.array_equal(gb, ob)
+        assert np.array_equal(gd, od)
+
+
+def test_pyramid_bitexact(qvga):
+    for f in (qvga["f1"], qvga["f2"]):
+        sb, sd = f.sphere()
+        ref = O.sphere_pyramid(sb, sd, 6)
+        for l in range(6):
+            got = f.level(l)
+            for k in ("gray", "depth", "gx", "gy", "dgx", "dgy"):
+                assert np.array_equal(got[k], ref[l][k]), (l, k)
+
+
+def _icp_check(H, g, e2, nv, nvis, Hr, gr, e2r, nvr, nvisr, npx):
+    sH = np.abs(Hr).max()
+    assert np.abs(H - Hr).max() <= 1e-5 * sH
+    assert np.abs(g - gr).max() <= 1e-5 * max(np.abs(gr).max(), 1e-3 * sH ** 0.5)
+    assert abs(e2 - e2r) <= 1e-5 * e2r
+    assert abs(nv - nvr) <= max(2, 1e-4 * npx)
+    assert abs(nvis - nvisr) <= max(2, 1e-4 * npx)
+
+
+@pytest.mark.parametrize("method", [0, 1, 2])
+def test_icp_pass_parity_samples(ctx, qvga, method):
+    reg = R.RegisterPhotoICP(ctx)
+    reg.setTargetFrame(qvga["f1"]); reg.setSourceFrame(qvga["f2"])
+    poses = [np.eye(4, dtype=np.float32), O.exp_se3([0.02, -0.03, 0.05, 0.01, -0.015, 0.02])]
+    for l in range(5):
+        lt, ls = qvga["f1"].level(l), qvga["f2"].level(l)
+        for P in poses:
+            H, g, e2, nv, nvis = reg.eval(l, P, method)
+            e, e2r, nvr = O.error_sphere(ls, lt, P, method)
+            Hr, gr, nvisr = O.hessgrad_sphere(ls, lt, P, method)
+            _icp_check(H, g, e2, nv, nvis, Hr, gr, e2r, nvr, nvisr, lt["gray"].size)
+
+
+def test_align360_parity_samples(ctx, qvga):
+    reg = R.RegisterPhotoICP(ctx)
+    reg.setNumPyr(5); reg.setGrayVariance(3.0 / 255)           # Registration/OdometryRGBD360.cpp:92-95
+    reg.setTargetFrame(qvga["f1"]); reg.setSourceFrame(qvga["f2"])
+    rc = reg.alignFrames360(np.eye(4), R.PHOTO_DEPTH)
+    b1, d1, b2, d2 = qvga["raw"]
+    s1b, s1d = O.stitch(b1, d1, qvga["rti"], qvga["K"])
+    s2b, s2d = O.stitch(b2, d2, qvga["rti"], qvga["K"])
+    p = O.IcpParams.default(n_pyr=5, std_dev_photo=np.float32(3.0 / 255))
+    rco, pose, H, g, st = O.align360(s1b, s1d, s2b, s2d, None, O.PHOTO_DEPTH, p)
+    assert rc == rco
+    dr, dt = _pose_err(reg.getOptimalPose(), pose)
+    assert dr <= ROT_TOL and dt <= TRANS_TOL, (dr, dt)
+    assert list(reg.stats.iters)[:5] == list(st.iters)[:5]
+    assert np.allclose(reg.getHessian(), H, rtol=1e-4, atol=1e-4 * np.abs(H).max())
+
+
+@pytest.fixture(scope="module")
+def vga(ctx):
+    cal = R.Calib360(ctx, 480, 640)
+    cal.loadExtrinsicCalibration(R.EXTRINSICS_DIR)
+    seed = 360 << 16
+    A = R.synth_path_pose(seed, 0)
+    rel = np.eye(4, dtype=np.float32)
+    a = np.deg2rad(4.0)
+    rel[1:3, 1:3] = [[np.cos(a), -np.sin(a)], [np.sin(a), np.cos(a)]]
+    rel[:3, 3] = [0, 0.25, 0.15]
+    B = A @ rel
+    b1, d1 = cal.synth_frame(seed, A)
+    b2, d2 = cal.synth_frame(seed, B)
+    f1, f2 = R.Frame360(cal), R.Frame360(cal)
+    f1.upload(b1, d1); f2.upload(b2, d2)
+    f1.build(); f2.build()
+    rt, rti, K = cal.extrinsics()
+    return dict(cal=cal, f1=f1, f2=f2, raw=(b1, d1, b2, d2), rti=rti, K=K.reshape(3, 3).T, rel=rel)
+
+
+def test_synth_frame_statistics(vga):
+    b1, d1, b2, d2 = vga["raw"]
+    hole = (d1 == 0).reshape(8, -1).mean(1)
+    assert (hole > 0.05).all() and (hole < 0.45).all(), hole
+    assert d1[d1 > 0].min() >= 400 and d1.max() <= 8000
+
+
+@pytest.mark.parametrize("fixed", [0, 20])
+def test_align360_parity_synth_vga(ctx, vga, fixed):
+    reg = R.RegisterPhotoICP(ctx)
+    reg.setNumPyr(5); reg.setGrayVariance(3.0 / 255)
+    reg.params.fixed_iters_level0 = fixed
+    reg.setTargetFrame(vga["f1"]); reg.setSourceFrame(vga["f2"])
+    rc = reg.alignFrames360(np.eye(4), R.PHOTO_DEPTH)
+    b1, d1, b2, d2 = vga["raw"]
+    s1b, s1d = vga["f1"].sphere()
+    s2b, s2d = vga["f2"].sphere()
+    ob, od = O.stitch(b1, d1, vga["rti"], vga["K"])
+    assert np.array_equal(ob, s1b) and np.array_equal(od, s1d)
+    p = O.IcpParams.default(n_pyr=5, std_dev_photo=np.float32(3.0 / 255), fixed_iters_level0=fixed)
+    rco, pose, H, g, st = O.align360(s1b, s1d, s2b, s2d, None, O.PHOTO_DEPTH, p)
+    assert rc == rco
+    dr, dt = _pose_err(reg.getOptimalPose(), pose)
+    assert dr <= ROT_TOL and dt <= TRANS_TOL, (dr, dt)
+    if fixed:
+        assert reg.stats.passes == sum(1 + st.evals[l] for l in range(1, 5)) + 1 + fixed
