@@ -80,9 +80,12 @@ __device__ __forceinline__ void pixel(Acc& A, const Pose12& P, float d, float gr
     const float dist_inv = 1.f / dist;
     const float phi_trg = asinf(X * dist_inv);
     const float theta_trg = (float)((double)atan2f(Y, Z) + R360_PI);
-    const int r = (int)roundf(half_nRows - phi_trg * angle_res_inv);
-    const int c = (int)roundf(theta_trg * angle_res_inv);
-    if (!((r >= 0 && r < nRows) && c < nCols)) return;            // (:2989)
+    // round() + int conversion + the (:2989) bounds test, done on the float values so NaN and
+    // out-of-range projections are rejected exactly as the x86 reference's (int) conversion does.
+    const float rf = roundf(half_nRows - phi_trg * angle_res_inv);
+    const float cf = roundf(theta_trg * angle_res_inv);
+    if (!((rf >= 0.f && rf < (float)nRows) && cf < (float)nCols)) return;
+    const int r = (int)rf, c = (int)cf;
     A.h[28] += 1.f;                                                 // numVisiblePixels
     const long t = (long)r * nCols + c;
     const float4 G = tg[t];                                         // {gx, gy, dgx, dgy}
