@@ -144,6 +144,12 @@ int r360_synth_frame(const r360_calib* calib, uint32_t seed, const float rig_pos
                      uint8_t* bgr8, uint16_t* depth8);
 int r360_synth_path_pose(uint32_t seed, int frame, float pose_out[16]);
 
+/* ---------------------------------------------------------------- test hooks
+ * The float asinf/atan2f program used by the projection (libm_f32.h, bit-identical to x86-64 glibc)
+ * evaluated on the host (on_device = 0) or on the GPU (on_device = 1). */
+int r360_libm_eval(const float* x, const float* y, const float* z, int n, float* asin_out, float* atan2_out,
+                   int on_device);
+
 /* ---------------------------------------------------------------- timing hooks (bench) */
 int r360_ctx_timing(r360_ctx* ctx, int enable);
 /* Per-kernel accumulated device time (ms) and launch counts since the last reset. */

@@ -80,6 +80,7 @@ def lib() -> C.CDLL:
                                        fp, fp, C.POINTER(IcpStats)]),
             "orc_exp_se3": (None, [dp, C.c_int, fp]),
             "orc_huber": (C.c_float, [C.c_float, C.c_float]),
+            "orc_libm": (None, [fp, fp, fp, C.c_int, fp, fp]),
         }
         for k, (r, a) in sig.items():
             f = getattr(L, k)
@@ -267,6 +268,13 @@ def exp_se3(mu, pseudo=True) -> np.ndarray:
     T = np.zeros(16, np.float32)
     lib().orc_exp_se3(m.ctypes.data_as(C.POINTER(C.c_double)), int(pseudo), _f(T))
     return from16(T)
+
+
+def libm(x, y, z):
+    x, y, z = (np.ascontiguousarray(a, np.float32) for a in (x, y, z))
+    a, t = np.zeros_like(x), np.zeros_like(x)
+    lib().orc_libm(_f(x), _f(y), _f(z), x.size, _f(a), _f(t))
+    return a, t
 
 
 def huber(e: float, reg: float) -> float:

@@ -98,6 +98,9 @@ int orc_align360(const uint8_t* trg_bgr, const uint16_t* trg_depth,
 /* ---- A18: CPose3D::exp(mu, pseudo) */
 void orc_exp_se3(const double mu[6], int pseudo, float T[16]);
 
+/* glibc std::asin(float) / std::atan2(float,float) — what the reference's projection calls */
+void orc_libm(const float* x, const float* y, const float* z, int n, float* asin_out, float* atan2_out);
+
 /* Huber weight (RegisterPhotoICP.h:545-554), float instantiation */
 float orc_huber(float err, float reg);
 

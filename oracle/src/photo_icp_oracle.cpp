@@ -514,3 +514,8 @@ done:
     if (g_out) memcpy(g_out, gf, sizeof(gf));
     return ret;
 }
+
+// glibc float asinf / atan2f as the reference calls them (std::asin(float), std::atan2(float, float))
+extern "C" void orc_libm(const float* x, const float* y, const float* z, int n, float* as, float* at) {
+    for (int i = 0; i < n; ++i) { as[i] = std::asin(x[i]); at[i] = std::atan2(y[i], z[i]); }
+}

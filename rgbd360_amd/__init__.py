@@ -94,6 +94,7 @@ _SIGS = [
     ("r360_exp_se3", None, [_DP, C.c_int, _FP]),
     ("r360_synth_frame", C.c_int, [_P, C.c_uint32, _FP, _P, _P]),
     ("r360_synth_path_pose", C.c_int, [C.c_uint32, C.c_int, _FP]),
+    ("r360_libm_eval", C.c_int, [_FP, _FP, _FP, C.c_int, _FP, _FP, C.c_int]),
     ("r360_ctx_timing", C.c_int, [_P, C.c_int]),
     ("r360_ctx_timing_read", C.c_int, [_P, C.c_char_p, _DP, C.POINTER(C.c_long)]),
     ("r360_ctx_timing_reset", C.c_int, [_P]),
@@ -337,6 +338,15 @@ class RegisterPhotoICP:
                                    C.byref(self.params), H.ctypes.data_as(_DP), g.ctypes.data_as(_DP),
                                    C.byref(e2), C.byref(nv), C.byref(nvis)), "icp_eval")
         return H.reshape(6, 6), g, e2.value, nv.value, nvis.value
+
+
+def libm_eval(x, y, z, on_device: bool = False):
+    """Evaluate the projection's asinf / atan2f port (libm_f32.h) on the host or the GPU."""
+    x, y, z = (np.ascontiguousarray(a, np.float32) for a in (x, y, z))
+    a, t = np.zeros_like(x), np.zeros_like(x)
+    _check(lib().r360_libm_eval(_fptr(x), _fptr(y), _fptr(z), x.size, _fptr(a), _fptr(t), int(on_device)),
+           "libm_eval")
+    return a, t
 
 
 def synth_path_pose(seed: int, frame: int) -> np.ndarray:

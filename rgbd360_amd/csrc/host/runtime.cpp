@@ -350,7 +350,8 @@ extern "C" int r360_frame_create(r360_ctx* ctx, const r360_calib* calib, r360_fr
 
 extern "C" void r360_frame_destroy(r360_frame* f) {
     if (!f) return;
-    hipStreamSynchronize(f->ctx->stream);
+    // hipFree synchronises the device; the frame never dereferences its ctx here so frames may
+    // outlive their context at interpreter shutdown.
     hipFree(f->d_bgr); hipFree(f->d_depth); hipFree(f->d_depth_m); hipFree(f->d_sph_bgr); hipFree(f->d_sph_depth);
     for (int l = 0; l < f->n_levels; ++l) { hipFree(f->lv[l].p0); hipFree(f->lv[l].tg); }
     delete f;

@@ -14,6 +14,7 @@
 // bytes of SURVEY.md §8(d).  No Jacobian rows are materialised (the reference writes and
 // re-reads imgSize x 6 buffers, :2761-2767).
 #include "../r360_internal.h"
+#include "../libm_f32.h"
 
 namespace {
 
@@ -78,8 +79,8 @@ __device__ __forceinline__ void pixel(Acc& A, const Pose12& P, float d, float gr
     float Z = P.R[6] * lx + P.R[7] * ly + P.R[8] * lz; Z = Z + P.t[2];
     const float dist = sqrtf(X * X + Y * Y + Z * Z);
     const float dist_inv = 1.f / dist;
-    const float phi_trg = asinf(X * dist_inv);
-    const float theta_trg = (float)((double)atan2f(Y, Z) + R360_PI);
+    const float phi_trg = r360m::asinf(X * dist_inv);        // glibc-exact (libm_f32.h)
+    const float theta_trg = (float)((double)r360m::atan2f(Y, Z) + R360_PI);
     // round() + int conversion + the (:2989) bounds test, done on the float values so NaN and
     // out-of-range projections are rejected exactly as the x86 reference's (int) conversion does.
     const float rf = roundf(half_nRows - phi_trg * angle_res_inv);
@@ -456,6 +457,35 @@ __global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src
 }
 
 }  // namespace
+
+namespace {
+__global__ void k_libm(const float* x, const float* y, const float* z, int n, float* as, float* at) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) { as[i] = r360m::asinf(x[i]); at[i] = r360m::atan2f(y[i], z[i]); }
+}
+}  // namespace
+
+// Test hook: evaluates the asinf/atan2f port on the host or on the device.
+extern "C" int r360_libm_eval(const float* x, const float* y, const float* z, int n, float* asin_out,
+                              float* atan2_out, int on_device) {
+    if (!on_device) {
+        for (int i = 0; i < n; ++i) { asin_out[i] = r360m::asinf(x[i]); atan2_out[i] = r360m::atan2f(y[i], z[i]); }
+        return 0;
+    }
+    float* d = nullptr;
+    const size_t b = sizeof(float) * (size_t)n;
+    R360_HIP(hipMalloc(&d, 5 * b));
+    R360_HIP(hipMemcpy(d, x, b, hipMemcpyHostToDevice));
+    R360_HIP(hipMemcpy(d + n, y, b, hipMemcpyHostToDevice));
+    R360_HIP(hipMemcpy(d + 2 * (size_t)n, z, b, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_libm, dim3((n + 255) / 256), dim3(256), 0, 0, d, d + n, d + 2 * (size_t)n, n,
+                       d + 3 * (size_t)n, d + 4 * (size_t)n);
+    R360_HIP(hipGetLastError());
+    R360_HIP(hipMemcpy(asin_out, d + 3 * (size_t)n, b, hipMemcpyDeviceToHost));
+    R360_HIP(hipMemcpy(atan2_out, d + 4 * (size_t)n, b, hipMemcpyDeviceToHost));
+    R360_HIP(hipFree(d));
+    return 0;
+}
 
 int icp_blocks_for(int n_pixels) {
     const int units = n_pixels / 4;

@@ -52,6 +52,28 @@ def test_exp_se3_host_matches_rodrigues():
     assert np.allclose(T[:3, 3], mu[:3], atol=1e-7)
 
 
+def test_libm_port_matches_glibc():
+    """libm_f32.h (host instantiation) == glibc std::asin(float)/std::atan2(float,float), as called by
+    the reference's projection (RegisterPhotoICP.h:2677-2678), over 4M random + special arguments."""
+    import numpy as np
+    from oracle import oracle360 as O
+    rng = np.random.default_rng(11)
+    n = 1 << 22
+    x = rng.uniform(-1, 1, n).astype(np.float32)
+    x[:64] = [0.0, -0.0, 1.0, -1.0, 0.5, -0.5, 0.975, -0.975, 1e-20, -1e-20, 1.5, np.nan] + [0.25] * 52
+    y = rng.uniform(-6, 6, n).astype(np.float32)
+    z = rng.uniform(-6, 6, n).astype(np.float32)
+    z[::9] = 1.0
+    y[::13] = 0.0
+    z[::17] = 0.0
+    a, t = R.libm_eval(x, y, z, on_device=False)
+    ra, rt = O.libm(x, y, z)
+    # bit-equal, except that any NaN matches any NaN (payload/sign are not part of the contract)
+    for u, v in ((a, ra), (t, rt)):
+        same = (u.view(np.uint32) == v.view(np.uint32)) | (np.isnan(u) & np.isnan(v))
+        assert same.all(), np.flatnonzero(~same)[:10]
+
+
 def test_context_without_gpu_fails_loudly():
     try:
         ctx = R.Context(0)

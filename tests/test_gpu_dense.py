@@ -21,9 +21,8 @@ ROT_TOL, TRANS_TOL = 1e-4, 1e-3
 
 @pytest.fixture(scope="module")
 def ctx():
-    c = R.Context(0)
-    yield c
-    c.close()
+    # no explicit close: frames/calibs hold the ctx alive and are destroyed first
+    return R.Context(0)
 
 
 @pytest.fixture(scope="module")
@@ -44,6 +43,21 @@ def qvga(ctx):
 
 def _pose_err(A, B):
     return O.rot_angle(A, B), float(np.linalg.norm(np.asarray(A)[:3, 3] - np.asarray(B)[:3, 3]))
+
+
+def test_libm_port_bitexact_on_device():
+    """The device asinf/atan2f (libm_f32.h) equals glibc's std::asin/std::atan2 bit for bit."""
+    rng = np.random.default_rng(7)
+    n = 1 << 22
+    x = rng.uniform(-1, 1, n).astype(np.float32)
+    y = rng.uniform(-6, 6, n).astype(np.float32)
+    z = rng.uniform(-6, 6, n).astype(np.float32)
+    a, t = R.libm_eval(x, y, z, on_device=True)
+    ra, rt = O.libm(x, y, z)
+    # bit-equal, except that any NaN matches any NaN (payload/sign are not part of the contract)
+    for u, v in ((a, ra), (t, rt)):
+        same = (u.view(np.uint32) == v.view(np.uint32)) | (np.isnan(u) & np.isnan(v))
+        assert same.all(), np.flatnonzero(~same)[:10]
 
 
 def test_undistort_bitexact(qvga):
@@ -75,12 +89,15 @@ def test_pyramid_bitexact(qvga):
 
 
 def _icp_check(H, g, e2, nv, nvis, Hr, gr, e2r, nvr, nvisr, npx):
+    """The projection is bit-identical (glibc-exact asinf/atan2f port), so pixel sets and counts
+    match exactly; the sums differ only by summation order (GPU: per-thread f32 partials over a few
+    pixels, then fp64), bounded per component by 1e-5 of the Cauchy-Schwarz scale sqrt(H_kk e2)."""
+    assert (nv, nvis) == (nvr, nvisr)
     sH = np.abs(Hr).max()
     assert np.abs(H - Hr).max() <= 1e-5 * sH
-    assert np.abs(g - gr).max() <= 1e-5 * max(np.abs(gr).max(), 1e-3 * sH ** 0.5)
-    assert abs(e2 - e2r) <= 1e-5 * e2r
-    assert abs(nv - nvr) <= max(2, 1e-4 * npx)
-    assert abs(nvis - nvisr) <= max(2, 1e-4 * npx)
+    scale = np.sqrt(np.abs(np.diag(Hr)) * max(e2r, 1e-30))
+    assert (np.abs(g - gr) <= 1e-5 * scale + 1e-12).all(), (g - gr, scale)
+    assert abs(e2 - e2r) <= 1e-6 * e2r
 
 
 @pytest.mark.parametrize("method", [0, 1, 2])
