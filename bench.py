@@ -145,7 +145,9 @@ def main():
 
     total_pairs = args.steps * world
     value = total_pairs / elapsed
-    N0 = (args.rows * 8 // 3) * (args.rows * 8)  # sphere level 0 (640 x 3840 at VGA)
+    W0 = args.rows * 8
+    H0 = int(W0 * 0.5 * 60.0 / 180)               # Frame360.h:391-392 (640 x 3840 at VGA)
+    N0 = H0 * W0
     sso = float(reg.stats.sso)
     V = sso * N0
     alg_bytes = 8.0 * N0 + 24.0 * V            # B = 8 N + 24 V per pass
@@ -159,7 +161,7 @@ def main():
             "workload": "config3: synthetic 8x640x480 Frame360 pair -> stitch + 5-level pyramid x2 -> "
                         "alignFrames360(PHOTO_DEPTH) levels 4..1 reference schedule + "
                         f"{args.iters0} GN iterations at level 0",
-            "sensors": f"8x{args.cols}x{args.rows}", "sphere": f"{args.rows * 8 // 3}x{args.rows * 8}",
+            "sensors": f"8x{args.cols}x{args.rows}", "sphere": f"{H0}x{W0}",
             "n_pyr": 5, "parallelism": f"pair-per-GPU dp{world}",
         },
         "roofline": {

@@ -284,5 +284,6 @@ def huber(e: float, reg: float) -> float:
 def rot_angle(Ra, Rb) -> float:
     """Angle (rad) of Ra Rb^T — the angularDistance of diffRotation (Miscellaneous.h:127-139)."""
     R = np.asarray(Ra, np.float64)[:3, :3] @ np.asarray(Rb, np.float64)[:3, :3].T
-    c = np.clip((np.trace(R) - 1) / 2, -1.0, 1.0)
-    return float(np.arccos(c))
+    c = (np.trace(R) - 1) / 2
+    s = 0.5 * np.linalg.norm([R[2, 1] - R[1, 2], R[0, 2] - R[2, 0], R[1, 0] - R[0, 1]])
+    return float(np.arctan2(s, c))  # well conditioned near 0, unlike arccos
