@@ -192,165 +192,8 @@ __device__ __forceinline__ double wave_sum_d(double x) {
 }
 
 // ---------------------------------------------------------------- GN step (thread 0 of last block)
-// The GN helpers work in an LDS workspace (only thread 0 of the last workgroup runs them), so the
-// pass kernel needs no scratch memory and its register budget is set by the pixel loop alone.
-struct GnWork { double M[36]; double A[42]; double Hd[36]; double HL[36]; double gd[6]; double x[6]; float Hc[36]; float gc[6]; float E[16]; };
+#include "icp_gn.inc"
 
-__device__ int rank6(const double* Min, double* M) {     // Eigen FullPivLU::rank(), default threshold
-    for (int i = 0; i < 36; ++i) M[i] = Min[i];
-    double piv[6];
-    for (int k = 0; k < 6; ++k) {
-        int br = k, bc = k; double bv = -1;
-        for (int r = k; r < 6; ++r)
-            for (int c = k; c < 6; ++c)
-                if (fabs(M[r * 6 + c]) > bv) { bv = fabs(M[r * 6 + c]); br = r; bc = c; }
-        for (int c = 0; c < 6; ++c) { double t = M[k * 6 + c]; M[k * 6 + c] = M[br * 6 + c]; M[br * 6 + c] = t; }
-        for (int r = 0; r < 6; ++r) { double t = M[r * 6 + k]; M[r * 6 + k] = M[r * 6 + bc]; M[r * 6 + bc] = t; }
-        piv[k] = M[k * 6 + k];
-        if (piv[k] != 0)
-            for (int r = k + 1; r < 6; ++r) {
-                double f = M[r * 6 + k] / piv[k];
-                for (int c = k; c < 6; ++c) M[r * 6 + c] -= f * M[k * 6 + c];
-            }
-    }
-    const double thr = 1.1920928955078125e-07 * 6 * fabs(piv[0]);
-    int rk = 0;
-    for (int k = 0; k < 6; ++k) rk += fabs(piv[k]) > thr;
-    return rk;
-}
-
-__device__ void solve6(const double* H, const double* g, double* x, double* A) {  // x = -H^-1 g (:4693)
-#define A_(r, c) A[(r) * 7 + (c)]
-    for (int r = 0; r < 6; ++r) { for (int c = 0; c < 6; ++c) A_(r, c) = H[r * 6 + c]; A_(r, 6) = -g[r]; }
-    for (int k = 0; k < 6; ++k) {
-        int p = k;
-        for (int r = k + 1; r < 6; ++r) if (fabs(A_(r, k)) > fabs(A_(p, k))) p = r;
-        for (int c = 0; c < 7; ++c) { double t = A_(k, c); A_(k, c) = A_(p, c); A_(p, c) = t; }
-        for (int r = k + 1; r < 6; ++r) {
-            double f = A_(r, k) / A_(k, k);
-            for (int c = k; c < 7; ++c) A_(r, c) -= f * A_(k, c);
-        }
-    }
-    for (int r = 5; r >= 0; --r) {
-        double s = A_(r, 6);
-        for (int c = r + 1; c < 6; ++c) s -= A_(r, c) * x[c];
-        x[r] = s / A_(r, r);
-    }
-#undef A_
-}
-
-__device__ void exp_se3(const double mu[6], int pseudo, float T[16]) {  // CPose3D::exp
-    const double wx = mu[3], wy = mu[4], wz = mu[5];
-    const double th2 = wx * wx + wy * wy + wz * wz, th = sqrt(th2);
-    double A, B, Cc;
-    if (th < 1e-6) { A = 1 - th2 / 6; B = 0.5 - th2 / 24; Cc = 1.0 / 6 - th2 / 120; }
-    else { A = sin(th) / th; B = (1 - cos(th)) / th2; Cc = (th - sin(th)) / (th2 * th); }
-    const double W[9] = {0, -wz, wy, wz, 0, -wx, -wy, wx, 0};
-    double W2[9];
-    _Pragma("unroll") for (int r = 0; r < 3; ++r)
-        _Pragma("unroll") for (int c = 0; c < 3; ++c) {
-            double s = 0;
-            _Pragma("unroll") for (int k = 0; k < 3; ++k) s += W[r * 3 + k] * W[k * 3 + c];
-            W2[r * 3 + c] = s;
-        }
-    double R[9], V[9];
-    _Pragma("unroll") for (int i = 0; i < 9; ++i) {
-        const double I = (i % 4 == 0) ? 1.0 : 0.0;
-        R[i] = I + A * W[i] + B * W2[i];
-        V[i] = I + B * W[i] + Cc * W2[i];
-    }
-    double t[3];
-    _Pragma("unroll") for (int r = 0; r < 3; ++r) t[r] = pseudo ? mu[r] : V[r * 3] * mu[0] + V[r * 3 + 1] * mu[1] + V[r * 3 + 2] * mu[2];
-    _Pragma("unroll") for (int c = 0; c < 4; ++c)
-        _Pragma("unroll") for (int r = 0; r < 4; ++r) {
-            double v;
-            if (r < 3 && c < 3) v = R[r * 3 + c];
-            else if (r < 3) v = t[r];
-            else v = (c == 3) ? 1.0 : 0.0;
-            T[c * 4 + r] = (float)v;
-        }
-}
-
-__device__ void matmul4f(const float* A, const float* B, float* Cm) {  // Eigen Matrix4f product order
-    float out[16];
-    _Pragma("unroll") for (int c = 0; c < 4; ++c)
-        _Pragma("unroll") for (int r = 0; r < 4; ++r) {
-            float s = A[r] * B[c * 4];
-            _Pragma("unroll") for (int k = 1; k < 4; ++k) s += A[k * 4 + r] * B[c * 4 + k];
-            out[c * 4 + r] = s;
-        }
-    _Pragma("unroll") for (int i = 0; i < 16; ++i) Cm[i] = out[i];
-}
-
-__device__ void gn_step(IcpState* S, const double* sums, const IcpConst& C, int first, GnWork* W) {
-    const double err2 = sums[R360_SUM_ERR2];
-    const double nvalid = sums[R360_SUM_NVALID];
-    const double new_err = sqrt(err2 / nvalid);
-    float* Hc = W->Hc; float* gc = W->gc;
-    {
-        int k = 0;
-        for (int u = 0; u < 6; ++u)
-            for (int v = u; v < 6; ++v) { Hc[u * 6 + v] = Hc[v * 6 + u] = (float)sums[k++]; }
-        for (int u = 0; u < 6; ++u) gc[u] = (float)sums[21 + u];
-    }
-    const float sso_c = (float)(sums[R360_SUM_NVIS] / C.n_pixels);
-    S->passes++;
-    if (first) {                                   // level start: error(pose_estim)  (:4599-4605)
-        S->error = new_err; S->diff_error = new_err;
-        for (int k = 0; k < 6; ++k) S->upd[k] = 1.f;
-        S->it = 0; S->loops = 0; S->evals = 0;
-        for (int k = 0; k < 36; ++k) S->Hcur[k] = Hc[k];
-        for (int k = 0; k < 6; ++k) S->gcur[k] = gc[k];
-        S->sso_cur = sso_c;
-    } else {                                       // candidate evaluated (:4705-4722)
-        S->evals++;
-        const double diff = S->error - new_err;
-        S->diff_error = diff;
-        if (diff > C.tol_res) {
-            for (int k = 0; k < 16; ++k) S->pose[k] = S->cand[k];
-            S->error = new_err;
-            S->it = S->it + 1;
-            for (int k = 0; k < 36; ++k) S->Hcur[k] = Hc[k];
-            for (int k = 0; k < 6; ++k) S->gcur[k] = gc[k];
-            S->sso_cur = sso_c;
-        }
-    }
-    const bool fixed = (C.level == 0 && C.fixed_iters0 > 0);
-    float nu = 0.f;
-    for (int k = 0; k < 6; ++k) nu += S->upd[k] * S->upd[k];
-    nu = sqrtf(nu);
-    const bool cont = fixed ? (S->loops < C.fixed_iters0)
-                            : (S->it < C.max_iters && nu > C.tol_upd && S->diff_error > C.tol_res);  // (:4611)
-    if (!cont) {
-        S->active = 0;
-        S->iters[C.level] = S->it;
-        S->evals_l[C.level] = S->evals;
-        return;
-    }
-    S->loops++;
-    double* Hd = W->Hd; double* HL = W->HL; double* gd = W->gd;
-    for (int k = 0; k < 36; ++k) { Hd[k] = S->Hcur[k]; HL[k] = Hd[k]; }
-    for (int k = 0; k < 6; ++k) { gd[k] = S->gcur[k]; HL[k * 7] += C.lambda * Hd[k * 7]; }
-    for (int k = 0; k < 36; ++k) S->Hout[k] = S->Hcur[k];
-    for (int k = 0; k < 6; ++k) S->gout[k] = S->gcur[k];
-    S->sso = S->sso_cur;
-    if (rank6(HL, W->M) != 6) {                          // ILL-POSED: stop the whole alignment (:4682-4690)
-        S->illposed = 1; S->stop = 1; S->active = 0;
-        S->iters[C.level] = S->it;
-        S->evals_l[C.level] = S->evals;
-        return;
-    }
-    double* x = W->x;
-    solve6(Hd, gd, x, W->A);
-    double ud[6];
-    for (int k = 0; k < 6; ++k) { S->upd[k] = (float)x[k]; ud[k] = S->upd[k]; }
-    float* E = W->E;
-    exp_se3(ud, 1, E);                             // pseudo-exponential (:4697)
-    matmul4f(E, S->pose, S->cand);
-    S->active = 1;
-}
-
-// ---------------------------------------------------------------- the fused pass
 template <int METHOD>
 __global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src, const float2* __restrict__ trg,
                                                  const float4* __restrict__ tg, const float* __restrict__ sinphi,
@@ -362,7 +205,7 @@ __global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src
     __shared__ double s_err[NW];
     __shared__ double s_fin[8][32];
     __shared__ int s_last;
-    __shared__ GnWork s_gn;
+    __shared__ GnShared s_gn;
 
     if (S->stop) return;
     if (!first && !S->active && !eval_only) return;
@@ -434,9 +277,20 @@ __global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src
     }
     __syncthreads();
     {
+        // fixed-order reduction of the per-workgroup records; 8 independent accumulators per thread
+        // keep 8 loads in flight (the serial chain of dependent loads was the finalize's cost)
         const int v = threadIdx.x & 31, grp = threadIdx.x >> 5;  // 8 groups of 32
+        double a8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        const int nb = (int)gridDim.x;
+        int bk = grp;
+        for (; bk + 56 < nb; bk += 64) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) a8[j] += partials[(long)(bk + 8 * j) * 32 + v];
+        }
+        for (int j = 0; bk < nb; bk += 8, ++j) a8[j & 7] += partials[(long)bk * 32 + v];
         double acc = 0.0;
-        for (int bk = grp; bk < (int)gridDim.x; bk += 8) acc += partials[(long)bk * 32 + v];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc += a8[j];
         s_fin[grp][v] = acc;
     }
     __syncthreads();
@@ -446,13 +300,13 @@ __global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src
         s_fin[0][threadIdx.x] = t;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (threadIdx.x < 64) {
         if (eval_only) {
-            for (int k = 0; k < 32; ++k) S->sums[k] = s_fin[0][k];
+            if (threadIdx.x < 32) S->sums[threadIdx.x] = s_fin[0][threadIdx.x];
         } else {
-            gn_step(S, s_fin[0], C, first, &s_gn);
+            gn_step_wave(S, s_fin[0], C, first, &s_gn, threadIdx.x);
         }
-        S->ticket = 0;
+        if (threadIdx.x == 0) S->ticket = 0;
     }
 }
 
