@@ -206,6 +206,7 @@ __global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src
     __shared__ double s_fin[8][32];
     __shared__ int s_last;
     __shared__ GnShared s_gn;
+    __shared__ IcpState s_state;
 
     if (S->stop) return;
     if (!first && !S->active && !eval_only) return;
@@ -304,9 +305,23 @@ __global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src
         if (eval_only) {
             if (threadIdx.x < 32) S->sums[threadIdx.x] = s_fin[0][threadIdx.x];
         } else {
-            gn_step_wave(S, s_fin[0], C, first, &s_gn, threadIdx.x);
+            // Stage the whole state in LDS with one coalesced 16-B access per lane, run the step on
+            // the LDS copy (a single lane walking global memory serialises ~150 dependent accesses,
+            // ~35 us), then write it back the same way.
+            constexpr int NQ = (int)(sizeof(IcpState) / 16);
+            uint4* sq = reinterpret_cast<uint4*>(&s_state);
+            const uint4* gq = reinterpret_cast<const uint4*>(S);
+            for (int q = threadIdx.x; q < NQ; q += 64) sq[q] = gq[q];
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            gn_step_wave(&s_state, s_fin[0], C, first, &s_gn, threadIdx.x);
+            if (threadIdx.x == 0) s_state.ticket = 0;
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            uint4* wq = reinterpret_cast<uint4*>(S);
+            for (int q = threadIdx.x; q < NQ; q += 64) wq[q] = sq[q];
         }
-        if (threadIdx.x == 0) S->ticket = 0;
+        if (eval_only && threadIdx.x == 0) S->ticket = 0;
     }
 }
 

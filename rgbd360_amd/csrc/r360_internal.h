@@ -49,7 +49,7 @@ struct IcpConst {
 };
 
 // Device-resident Gauss-Newton state of one alignFrames360 call.
-struct IcpState {
+struct alignas(16) IcpState {
     float pose[16];     // pose_estim
     float cand[16];     // pose evaluated by the next pass
     float Hcur[36];     // H at pose_estim
