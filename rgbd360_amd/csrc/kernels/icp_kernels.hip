@@ -194,6 +194,11 @@ __device__ __forceinline__ double wave_sum_d(double x) {
 // ---------------------------------------------------------------- GN step (thread 0 of last block)
 #include "icp_gn.inc"
 
+__device__ __forceinline__ double ld_sc1(const double* p) {  // agent-scope (L1-bypassing) load
+    return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
 template <int METHOD>
 __global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src, const float2* __restrict__ trg,
                                                  const float4* __restrict__ tg, const float* __restrict__ sinphi,
@@ -259,24 +264,23 @@ __global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src
         } else {
             v = 0; for (int w = 0; w < NW; ++w) v += (double)s_red[w][threadIdx.x];
         }
-        partials[(long)blockIdx.x * 32 + threadIdx.x] = v;
+        // write-through (sc1) store: visible at agent scope without an L2 write-back fence
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(partials) + (long)blockIdx.x * 32 + threadIdx.x,
+                           (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
     // ---- stage 2: arrival ticket; the last workgroup reduces all records and runs the GN step
+    // Hand-off (MI355X_MICROARCH.md 'Valid forms', row 1): every record store is sc1 and drained by
+    // its wave (vmcnt(0) above) before the barrier; one relaxed agent-scope add per workgroup; the
+    // last adder reads every record with sc1 loads.  No buffer_wbl2 / buffer_inv fences: a release
+    // fence per workgroup wrote back each XCD's dirty L2 (tens of us per pass).
     if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned prev = __hip_atomic_fetch_add(&S->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_last = (prev == gridDim.x - 1);
     }
     __syncthreads();
     if (!s_last) return;
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
     {
         // fixed-order reduction of the per-workgroup records; 8 independent accumulators per thread
         // keep 8 loads in flight (the serial chain of dependent loads was the finalize's cost)
@@ -286,9 +290,9 @@ __global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src
         int bk = grp;
         for (; bk + 56 < nb; bk += 64) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) a8[j] += partials[(long)(bk + 8 * j) * 32 + v];
+            for (int j = 0; j < 8; ++j) a8[j] += ld_sc1(partials + (long)(bk + 8 * j) * 32 + v);
         }
-        for (int j = 0; bk < nb; bk += 8, ++j) a8[j & 7] += partials[(long)bk * 32 + v];
+        for (int j = 0; bk < nb; bk += 8, ++j) a8[j & 7] += ld_sc1(partials + (long)bk * 32 + v);
         double acc = 0.0;
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc += a8[j];
