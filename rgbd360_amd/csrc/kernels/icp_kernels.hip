@@ -65,12 +65,20 @@ __device__ __forceinline__ void acc_row(Acc& A, const float J[6], float r) {
     A.h[26] += J[5] * r;
 }
 
-template <int METHOD>
-__device__ __forceinline__ void pixel(Acc& A, const Pose12& P, float d, float gray_s, float sp, float cp, float st,
-                                      float ct, const float2* __restrict__ trg, const float4* __restrict__ tg,
-                                      int nRows, int nCols, float half_nRows, float angle_res_inv,
-                                      const IcpConst& C) {
-    if (!(C.min_d < d && d < C.max_d)) return;                     // LUT validity (:4578)
+// ---------------------------------------------------------------- per-pixel pipeline
+// Exact part: LUT point, transform and spherical projection, bit-identical to the reference
+// (same float expressions, glibc-exact asinf/atan2f, IEEE sqrt/div).  Everything that decides WHICH
+// target pixel is read, and the error terms, stays exact; only the Jacobian uses fast rcp/rsq.
+struct Proj {
+    float X, Y, Z, dist, dist_inv, gray_s;
+    int t;          // target pixel index (0 when not visible)
+    bool vis;       // valid source depth and projected inside the target image
+};
+
+__device__ __forceinline__ Proj project(const Pose12& P, float d, float gray_s, float sp, float cp, float st, float ct,
+                                        int nRows, int nCols, float half_nRows, float angle_res_inv, const IcpConst& C) {
+    Proj o;
+    const bool valid = (C.min_d < d && d < C.max_d);                // LUT validity (:4578)
     const float lx = d * sp;                                       // LUT_xyz_sphere (:4580-4582)
     const float ly = -d * cp * st;
     const float lz = -d * cp * ct;
@@ -79,80 +87,97 @@ __device__ __forceinline__ void pixel(Acc& A, const Pose12& P, float d, float gr
     float Z = P.R[6] * lx + P.R[7] * ly + P.R[8] * lz; Z = Z + P.t[2];
     const float dist = sqrtf(X * X + Y * Y + Z * Z);
     const float dist_inv = 1.f / dist;
-    const float phi_trg = r360m::asinf(X * dist_inv);        // glibc-exact (libm_f32.h)
-    const float theta_trg = (float)((double)r360m::atan2f(Y, Z) + R360_PI);
-    // round() + int conversion + the (:2989) bounds test, done on the float values so NaN and
-    // out-of-range projections are rejected exactly as the x86 reference's (int) conversion does.
+    const float phi_trg = r360m::asinf(X * dist_inv);             // glibc-exact (libm_f32.h)
+    const float theta_trg = (float)((double)r360m::atan2f_sel(Y, Z) + R360_PI);
+    // round() + int conversion + the (:2989) bounds test, on the float values so NaN and out-of-range
+    // projections are rejected exactly as the x86 reference's (int) conversion does.
     const float rf = roundf(half_nRows - phi_trg * angle_res_inv);
     const float cf = roundf(theta_trg * angle_res_inv);
-    if (!((rf >= 0.f && rf < (float)nRows) && cf < (float)nCols)) return;
-    const int r = (int)rf, c = (int)cf;
-    A.h[28] += 1.f;                                                 // numVisiblePixels
-    const long t = (long)r * nCols + c;
-    const float4 G = tg[t];                                         // {gx, gy, dgx, dgy}
-    const bool photo = (METHOD == R360_PHOTO_CONSISTENCY || METHOD == R360_PHOTO_DEPTH);
-    const bool depth = (METHOD == R360_DEPTH_CONSISTENCY || METHOD == R360_PHOTO_DEPTH);
-    if (photo && fabsf(G.x) < C.thr_int && fabsf(G.y) < C.thr_int) return;  // 'continue' (:3038)
-    const float2 T = trg[t];                                        // {gray, depth} of target
-    // jacobianProj23 * jacobianT36 (:2995-3026), jacobianT36 = [I | -skew(p')]
-    const float z_inv = 1.f / Z;
-    const float z_inv2 = z_inv * z_inv;
-    const float D_atan_theta = 1.f / (1 + Y * Y * z_inv2) * angle_res_inv;
-    const float P01 = D_atan_theta * z_inv;
-    const float P02 = -Y * z_inv2 * D_atan_theta;
-    const float dist_inv2 = dist_inv * dist_inv;
-    const float x_dist_inv2 = X * dist_inv2;
-    const float D_asin = 1.f / sqrtf(1 - X * x_dist_inv2) * angle_res_inv;
-    const float P10 = -D_asin * dist_inv * (1 - X * x_dist_inv2);
-    const float P11 = D_asin * (x_dist_inv2 * Y * dist_inv);
-    const float P12 = D_asin * (x_dist_inv2 * Z * dist_inv);
-    // T36 rows: (1,0,0,0,Z,-Y) (0,1,0,-Z,0,X) (0,0,1,Y,-X,0)
-    const float T0[6] = {1, 0, 0, 0, Z, -Y};
-    const float T1[6] = {0, 1, 0, -Z, 0, X};
-    const float T2[6] = {0, 0, 1, Y, -X, 0};
+    o.vis = valid && (rf >= 0.f && rf < (float)nRows) && cf < (float)nCols;
+    o.t = o.vis ? (int)rf * nCols + (int)cf : 0;
+    o.X = X; o.Y = Y; o.Z = Z; o.dist = dist; o.dist_inv = dist_inv; o.gray_s = gray_s;
+    return o;
+}
+
+__device__ __forceinline__ void acc_fma(Acc& A, const float J[6], float r) {
+#pragma clang fp contract(fast)
+    A.h[0] += J[0] * J[0]; A.h[1] += J[0] * J[1]; A.h[2] += J[0] * J[2];
+    A.h[3] += J[0] * J[3]; A.h[4] += J[0] * J[4]; A.h[5] += J[0] * J[5];
+    A.h[6] += J[1] * J[1]; A.h[7] += J[1] * J[2]; A.h[8] += J[1] * J[3];
+    A.h[9] += J[1] * J[4]; A.h[10] += J[1] * J[5]; A.h[11] += J[2] * J[2];
+    A.h[12] += J[2] * J[3]; A.h[13] += J[2] * J[4]; A.h[14] += J[2] * J[5];
+    A.h[15] += J[3] * J[3]; A.h[16] += J[3] * J[4]; A.h[17] += J[3] * J[5];
+    A.h[18] += J[4] * J[4]; A.h[19] += J[4] * J[5]; A.h[20] += J[5] * J[5];
+    A.h[21] += J[0] * r; A.h[22] += J[1] * r; A.h[23] += J[2] * r;
+    A.h[24] += J[3] * r; A.h[25] += J[4] * r; A.h[26] += J[5] * r;
+}
+
+// Residuals, weights and Jacobian rows of one projected pixel, accumulated branch-free: a pixel that
+// the reference skips contributes through selects that zero its row (never a multiply by 0, which
+// would let a NaN of an invalid pixel through).
+template <int METHOD>
+__device__ __forceinline__ void contribute(Acc& A, const Proj& o, const float4 G, const float2 T, float angle_res_inv,
+                                           const IcpConst& C) {
+    constexpr bool photo = (METHOD == R360_PHOTO_CONSISTENCY || METHOD == R360_PHOTO_DEPTH);
+    constexpr bool depth = (METHOD == R360_DEPTH_CONSISTENCY || METHOD == R360_PHOTO_DEPTH);
+    const float X = o.X, Y = o.Y, Z = o.Z, dist = o.dist, dist_inv = o.dist_inv;
+    A.h[28] += o.vis ? 1.f : 0.f;                                               // numVisiblePixels
+    // photo saliency fails -> 'continue' skips the depth term too (:3038-3039)
+    const bool sal_p = !(fabsf(G.x) < C.thr_int && fabsf(G.y) < C.thr_int);
+    const bool p_ok = photo && o.vis && sal_p;
+    const bool d_ok = depth && o.vis && (!photo || sal_p) && isfinite(T.y) &&
+                      !(fabsf(G.z) < C.thr_depth && fabsf(G.w) < C.thr_depth);  // (:3064-3073)
+    // exact error terms (they steer the accept/reject test :4715)
+    const float photoDiff = T.x - o.gray_s;
+    const float whp = huberf(photoDiff, C.sd_photo);
+    const float wEd = (float)((double)whp * C.sd_photo_inv_d * photoDiff);            // (:2699-2700)
+    const float depthDiff = T.y - dist;
+    const float sd = C.sd_depth * T.y;
+    const float wd = huberf(depthDiff, sd) / sd;                                        // (:3077-3078)
+    const float wEdep = (float)((double)wd * depthDiff);
+    if (photo) { A.err2 += p_ok ? (double)(wEd * wEd) : 0.0; A.h[27] += p_ok ? 1.f : 0.f; }
+    if (depth) { A.err2 += d_ok ? (double)(wEdep * wEdep) : 0.0; A.h[27] += d_ok ? 1.f : 0.f; }
+    // Jacobian of the spherical warp (:2995-3026), expanded with T36 = [I | -skew(p')]
     float Jw0[6], Jw1[6];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-        Jw0[k] = 0.f * T0[k] + P01 * T1[k] + P02 * T2[k];
-        Jw1[k] = P10 * T0[k] + P11 * T1[k] + P12 * T2[k];
+    {
+#pragma clang fp contract(fast)
+        const float z_inv = __builtin_amdgcn_rcpf(Z);
+        const float z_inv2 = z_inv * z_inv;
+        const float D_atan = __builtin_amdgcn_rcpf(1 + Y * Y * z_inv2) * angle_res_inv;
+        const float P01 = D_atan * z_inv;
+        const float P02 = -Y * z_inv2 * D_atan;
+        const float x_dist_inv2 = X * (dist_inv * dist_inv);
+        const float D_asin = __builtin_amdgcn_rsqf(1 - X * x_dist_inv2) * angle_res_inv;
+        const float P10 = -D_asin * dist_inv * (1 - X * x_dist_inv2);
+        const float P11 = D_asin * (x_dist_inv2 * Y * dist_inv);
+        const float P12 = D_asin * (x_dist_inv2 * Z * dist_inv);
+        Jw0[0] = 0.f; Jw0[1] = P01; Jw0[2] = P02; Jw0[3] = P02 * Y - P01 * Z; Jw0[4] = -P02 * X; Jw0[5] = P01 * X;
+        Jw1[0] = P10; Jw1[1] = P11; Jw1[2] = P12; Jw1[3] = P12 * Y - P11 * Z; Jw1[4] = P10 * Z - P12 * X;
+        Jw1[5] = P11 * X - P10 * Y;
     }
     if (photo) {
-        const float photoDiff = T.x - gray_s;
-        const float wh = huberf(photoDiff, C.sd_photo);
-        // errorPhotoICP_sphere: double weight, float residual (:2699-2709)
-        const float wEd = (float)((double)wh * C.sd_photo_inv_d * photoDiff);
-        A.err2 += (double)(wEd * wEd);
-        A.h[27] += 1.f;
-        // calcHessGrad_sphere: float weight (:3047-3052)
-        const float w = wh * C.sd_photo_inv_f;
-        const float res = w * photoDiff;
+#pragma clang fp contract(fast)
+        const float w = whp * C.sd_photo_inv_f;                                        // (:3047)
         const float wgx = w * G.x, wgy = w * G.y;
         float J[6];
 #pragma unroll
-        for (int k = 0; k < 6; ++k) J[k] = wgx * Jw0[k] + wgy * Jw1[k];
-        acc_row(A, J, res);
+        for (int k = 0; k < 6; ++k) J[k] = p_ok ? wgx * Jw0[k] + wgy * Jw1[k] : 0.f;
+        acc_fma(A, J, p_ok ? w * photoDiff : 0.f);
     }
     if (depth) {
-        const float depth2 = T.y;
-        if (isfinite(depth2)) {
-            if (fabsf(G.z) < C.thr_depth && fabsf(G.w) < C.thr_depth) return;  // (:3072-3073)
-            const float depthDiff = depth2 - dist;
-            const float sd = C.sd_depth * depth2;
-            const float w = huberf(depthDiff, sd) / sd;
-            const float wE = (float)((double)w * depthDiff);
-            A.err2 += (double)(wE * wE);
-            A.h[27] += 1.f;
-            const float res = w * depthDiff;
-            const float js0 = X * dist_inv, js1 = Y * dist_inv, js2 = Z * dist_inv;
-            float J[6];
+#pragma clang fp contract(fast)
+        // (dgrad * Jw - (p'/|p'|)^T T36): the rotational part of (p'/|p'|)^T T36 is p' x p' / |p'| = 0
+        const float js0 = X * dist_inv, js1 = Y * dist_inv, js2 = Z * dist_inv;
+        float J[6];
+        J[0] = G.z * Jw0[0] + G.w * Jw1[0] - js0;
+        J[1] = G.z * Jw0[1] + G.w * Jw1[1] - js1;
+        J[2] = G.z * Jw0[2] + G.w * Jw1[2] - js2;
+        J[3] = G.z * Jw0[3] + G.w * Jw1[3];
+        J[4] = G.z * Jw0[4] + G.w * Jw1[4];
+        J[5] = G.z * Jw0[5] + G.w * Jw1[5];
 #pragma unroll
-            for (int k = 0; k < 6; ++k) {
-                const float ga = G.z * Jw0[k] + G.w * Jw1[k];
-                const float gb = js0 * T0[k] + js1 * T1[k] + js2 * T2[k];
-                J[k] = w * (ga - gb);
-            }
-            acc_row(A, J, res);
-        }
+        for (int k = 0; k < 6; ++k) J[k] = d_ok ? wd * J[k] : 0.f;
+        acc_fma(A, J, d_ok ? wd * depthDiff : 0.f);
     }
 }
 
@@ -244,10 +269,23 @@ __global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src
         const float4 a = src4[2 * u], b = src4[2 * u + 1];  // {g0,d0,g1,d1} {g2,d2,g3,d3}
         const float4 s = st4[c4], c = ct4[c4];
         const float sp = sinphi[r], cp = cosphi[r];
-        pixel<METHOD>(A, P, a.y, a.x, sp, cp, s.x, c.x, trg, tg, nRows, nCols, half_nRows, angle_res_inv, C);
-        pixel<METHOD>(A, P, a.w, a.z, sp, cp, s.y, c.y, trg, tg, nRows, nCols, half_nRows, angle_res_inv, C);
-        pixel<METHOD>(A, P, b.y, b.x, sp, cp, s.z, c.z, trg, tg, nRows, nCols, half_nRows, angle_res_inv, C);
-        pixel<METHOD>(A, P, b.w, b.z, sp, cp, s.w, c.w, trg, tg, nRows, nCols, half_nRows, angle_res_inv, C);
+        // two pixels at a time: project both, issue both gathers, then the math (ILP + loads in flight)
+        {
+            const Proj o0 = project(P, a.y, a.x, sp, cp, s.x, c.x, nRows, nCols, half_nRows, angle_res_inv, C);
+            const Proj o1 = project(P, a.w, a.z, sp, cp, s.y, c.y, nRows, nCols, half_nRows, angle_res_inv, C);
+            const float4 G0 = tg[o0.t], G1 = tg[o1.t];
+            const float2 T0 = trg[o0.t], T1 = trg[o1.t];
+            contribute<METHOD>(A, o0, G0, T0, angle_res_inv, C);
+            contribute<METHOD>(A, o1, G1, T1, angle_res_inv, C);
+        }
+        {
+            const Proj o2 = project(P, b.y, b.x, sp, cp, s.z, c.z, nRows, nCols, half_nRows, angle_res_inv, C);
+            const Proj o3 = project(P, b.w, b.z, sp, cp, s.w, c.w, nRows, nCols, half_nRows, angle_res_inv, C);
+            const float4 G2 = tg[o2.t], G3 = tg[o3.t];
+            const float2 T2 = trg[o2.t], T3 = trg[o3.t];
+            contribute<METHOD>(A, o2, G2, T2, angle_res_inv, C);
+            contribute<METHOD>(A, o3, G3, T3, angle_res_inv, C);
+        }
     }
 
     // ---- stage 1: wave butterfly (f32) -> LDS -> per-workgroup fp64 record
@@ -334,7 +372,7 @@ __global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src
 namespace {
 __global__ void k_libm(const float* x, const float* y, const float* z, int n, float* as, float* at) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) { as[i] = r360m::asinf(x[i]); at[i] = r360m::atan2f(y[i], z[i]); }
+    if (i < n) { as[i] = r360m::asinf(x[i]); at[i] = r360m::atan2f_sel(y[i], z[i]); }
 }
 }  // namespace
 
@@ -342,7 +380,7 @@ __global__ void k_libm(const float* x, const float* y, const float* z, int n, fl
 extern "C" int r360_libm_eval(const float* x, const float* y, const float* z, int n, float* asin_out,
                               float* atan2_out, int on_device) {
     if (!on_device) {
-        for (int i = 0; i < n; ++i) { asin_out[i] = r360m::asinf(x[i]); atan2_out[i] = r360m::atan2f(y[i], z[i]); }
+        for (int i = 0; i < n; ++i) { asin_out[i] = r360m::asinf(x[i]); atan2_out[i] = r360m::atan2f_sel(y[i], z[i]); }
         return 0;
     }
     float* d = nullptr;
@@ -362,7 +400,7 @@ extern "C" int r360_libm_eval(const float* x, const float* y, const float* z, in
 
 int icp_blocks_for(int n_pixels) {
     const int units = n_pixels / 4;
-    int b = (units + TPB * 2 - 1) / (TPB * 2);
+    int b = (units + TPB - 1) / TPB;  // one 4-pixel unit per thread up to 1024 workgroups
     if (b > 1024) b = 1024;
     return b < 1 ? 1 : b;
 }

@@ -149,4 +149,49 @@ R360_HD float atan2f(float y, float x) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Branch-light forms for the GPU pixel loop: the same arithmetic as atanf/atan2f above (so the same
+// bits), with the argument-reduction case chosen by selects and ONE division, so a wave does not
+// serialise the five reduction branches.  Special arguments (zeros, infinities, NaN, x == 1,
+// |y/x| beyond 2^+-60) take the exact reference path above.
+R360_HD float atanf_sel(float x) {
+    const float atanhi0 = 4.6364760399e-01f, atanhi1 = 7.8539812565e-01f, atanhi2 = 9.8279368877e-01f,
+                atanhi3 = 1.5707962513e+00f;
+    const float atanlo0 = 5.0121582440e-09f, atanlo1 = 3.7748947079e-08f, atanlo2 = 3.4473217170e-08f,
+                atanlo3 = 7.5497894159e-08f;
+    const int32_t hx = (int32_t)fbits(x);
+    const int32_t ix = hx & 0x7fffffff;
+    const int id = ix < 0x3ee00000 ? -1 : (ix < 0x3f300000 ? 0 : (ix < 0x3f980000 ? 1 : (ix < 0x401c0000 ? 2 : 3)));
+    const float ax = fabs_(x);
+    const float num = id < 0 ? x : (id == 0 ? 2.0f * ax - 1.0f : (id == 1 ? ax - 1.0f : (id == 2 ? ax - 1.5f : -1.0f)));
+    const float den = id < 0 ? 1.0f : (id == 0 ? 2.0f + ax : (id == 1 ? ax + 1.0f : (id == 2 ? 1.0f + 1.5f * ax : ax)));
+    const float xr = num / den;  // exact: num/1 == num for id < 0
+    const float z = xr * xr;
+    const float w = z * z;
+    const float s1 = z * (3.3333334327e-01f + w * (1.4285714924e-01f + w * (9.0908870101e-02f +
+                     w * (6.6610731184e-02f + w * (4.9768779427e-02f + w * 1.6285819933e-02f)))));
+    const float s2 = w * (-2.0000000298e-01f + w * (-1.1111110449e-01f + w * (-7.6918758452e-02f +
+                     w * (-5.8335702866e-02f + w * -3.6531571299e-02f))));
+    const float hi = id == 0 ? atanhi0 : (id == 1 ? atanhi1 : (id == 2 ? atanhi2 : atanhi3));
+    const float lo = id == 0 ? atanlo0 : (id == 1 ? atanlo1 : (id == 2 ? atanlo2 : atanlo3));
+    const float zz = hi - ((xr * (s1 + s2) - lo) - xr);
+    float res = id < 0 ? xr - xr * (s1 + s2) : (hx < 0 ? -zz : zz);
+    if (ix < 0x31000000) res = x;                                    // |x| < 2^-29
+    if (ix >= 0x4c000000) res = ix > 0x7f800000 ? x + x : (hx > 0 ? atanhi3 + atanlo3 : -atanhi3 - atanlo3);
+    return res;
+}
+
+R360_HD float atan2f_sel(float y, float x) {
+    const float pi = 3.1415927410e+00f, pi_lo = -8.7422776573e-08f;
+    const int32_t hx = (int32_t)fbits(x), ix = hx & 0x7fffffff;
+    const int32_t hy = (int32_t)fbits(y), iy = hy & 0x7fffffff;
+    const int k = (iy - ix) >> 23;
+    const bool special = (ix == 0) | (iy == 0) | (ix >= 0x7f800000) | (iy >= 0x7f800000) | (hx == 0x3f800000) |
+                         (k > 60) | (hx < 0 && k < -60);
+    if (special) return atan2f(y, x);
+    const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
+    const float z = atanf_sel(fabs_(y / x));
+    return m == 0 ? z : (m == 1 ? -z : (m == 2 ? pi - (z - pi_lo) : (z - pi_lo) - pi));
+}
+
 }  // namespace r360m
