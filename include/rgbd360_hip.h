@@ -150,6 +150,9 @@ int r360_synth_path_pose(uint32_t seed, int frame, float pose_out[16]);
 int r360_libm_eval(const float* x, const float* y, const float* z, int n, float* asin_out, float* atan2_out,
                    int on_device);
 
+/* s_memrealtime stamps (100 MHz) of the last ICP pass; written only by a -DR360_STAMPS build. */
+int r360_ctx_debug_stamps(r360_ctx* ctx, unsigned long long* out12);
+
 /* ---------------------------------------------------------------- timing hooks (bench) */
 int r360_ctx_timing(r360_ctx* ctx, int enable);
 /* Per-kernel accumulated device time (ms) and launch counts since the last reset. */

@@ -25,7 +25,7 @@ __all__ = [
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "librgbd360_hip.so")
+LIB_PATH = os.environ.get("R360_LIB") or os.path.join(_HERE, "lib", "librgbd360_hip.so")
 REPO_ROOT = os.path.dirname(_HERE)
 
 PHOTO_CONSISTENCY, DEPTH_CONSISTENCY, PHOTO_DEPTH = 0, 1, 2
@@ -95,6 +95,7 @@ _SIGS = [
     ("r360_synth_frame", C.c_int, [_P, C.c_uint32, _FP, _P, _P]),
     ("r360_synth_path_pose", C.c_int, [C.c_uint32, C.c_int, _FP]),
     ("r360_libm_eval", C.c_int, [_FP, _FP, _FP, C.c_int, _FP, _FP, C.c_int]),
+    ("r360_ctx_debug_stamps", C.c_int, [_P, C.POINTER(C.c_ulonglong)]),
     ("r360_ctx_timing", C.c_int, [_P, C.c_int]),
     ("r360_ctx_timing_read", C.c_int, [_P, C.c_char_p, _DP, C.POINTER(C.c_long)]),
     ("r360_ctx_timing_reset", C.c_int, [_P]),

@@ -518,6 +518,7 @@ extern "C" int r360_align360_async(r360_ctx* ctx, r360_frame* trg, r360_frame* s
     memset(h, 0, sizeof(IcpState));
     memcpy(h->pose, init, sizeof(float) * 16);
     memcpy(h->cand, init, sizeof(float) * 16);
+    h->dbg[8] = ~0ull;
     R360_HIP(hipMemcpyAsync(ctx->d_state, h, sizeof(IcpState), hipMemcpyHostToDevice, ctx->stream));
     for (int l = p->n_pyr - 1; l >= 0; --l) {
         const int np = src->lv[l].rows * src->lv[l].cols;
@@ -569,6 +570,7 @@ extern "C" int r360_icp_eval(r360_ctx* ctx, r360_frame* trg, r360_frame* src, in
     memset(h, 0, sizeof(IcpState));
     memcpy(h->cand, pose, sizeof(float) * 16);
     memcpy(h->pose, pose, sizeof(float) * 16);
+    h->dbg[8] = ~0ull;
     R360_HIP(hipMemcpyAsync(ctx->d_state, h, sizeof(IcpState), hipMemcpyHostToDevice, ctx->stream));
     const IcpConst C = make_const(p, level, src->lv[level].rows * src->lv[level].cols);
     if (launch_icp_level(ctx, trg, src, level, method, C, 0, 1)) return -1;
@@ -614,4 +616,13 @@ extern "C" void r360_exp_se3(const double mu[6], int pseudo, float T[16]) {
             } else v = (c == 3) ? 1.0 : 0.0;
             T[c * 4 + r] = (float)v;
         }
+}
+
+// Diagnostic: the s_memrealtime stamps of the last pass (only written by a -DR360_STAMPS build).
+extern "C" int r360_ctx_debug_stamps(r360_ctx* ctx, unsigned long long* out12) {
+    CHECK_ARG(ctx && out12, "null arg");
+    R360_HIP(hipStreamSynchronize(ctx->stream));
+    R360_HIP(hipMemcpy(out12, (const char*)ctx->d_state + offsetof(IcpState, dbg), sizeof(unsigned long long) * 12,
+                       hipMemcpyDeviceToHost));
+    return 0;
 }

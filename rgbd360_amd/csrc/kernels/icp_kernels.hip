@@ -239,6 +239,9 @@ __global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src
     __shared__ IcpState s_state;
 
     if (S->stop) return;
+#ifdef R360_STAMPS
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+#endif
     if (!first && !S->active && !eval_only) return;
 
     const float* pm = (first && !eval_only) ? S->pose : S->cand;
@@ -288,6 +291,13 @@ __global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src
         }
     }
 
+#ifdef R360_STAMPS
+    const unsigned long long t_loop = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_min(&S->dbg[8], t_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_max(&S->dbg[9], t_loop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#endif
     // ---- stage 1: wave butterfly (f32) -> LDS -> per-workgroup fp64 record
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const float mine = wave_reduce_scatter32(A.h, lane);
@@ -319,6 +329,9 @@ __global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src
     }
     __syncthreads();
     if (!s_last) return;
+#ifdef R360_STAMPS
+    const unsigned long long t_ticket = __builtin_amdgcn_s_memrealtime();
+#endif
     {
         // fixed-order reduction of the per-workgroup records; 8 independent accumulators per thread
         // keep 8 loads in flight (the serial chain of dependent loads was the finalize's cost)
@@ -343,9 +356,21 @@ __global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src
         s_fin[0][threadIdx.x] = t;
     }
     __syncthreads();
+#ifdef R360_STAMPS
+    const unsigned long long t_recs = __builtin_amdgcn_s_memrealtime();
+#endif
     if (threadIdx.x < 64) {
         if (eval_only) {
             if (threadIdx.x < 32) S->sums[threadIdx.x] = s_fin[0][threadIdx.x];
+#ifdef R360_STAMPS
+            if (threadIdx.x == 0) {
+                const unsigned long long mn = __hip_atomic_load(&S->dbg[8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long mx = __hip_atomic_load(&S->dbg[9], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                S->dbg[5] = mn; S->dbg[6] = mx; S->dbg[8] = ~0ull; S->dbg[9] = 0;
+                S->dbg[0] = t_start; S->dbg[1] = t_loop; S->dbg[2] = t_ticket; S->dbg[3] = t_recs;
+                S->dbg[4] = __builtin_amdgcn_s_memrealtime();
+            }
+#endif
         } else {
             // Stage the whole state in LDS with one coalesced 16-B access per lane, run the step on
             // the LDS copy (a single lane walking global memory serialises ~150 dependent accesses,
@@ -358,10 +383,23 @@ __global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
             gn_step_wave(&s_state, s_fin[0], C, first, &s_gn, threadIdx.x);
             if (threadIdx.x == 0) s_state.ticket = 0;
+#ifdef R360_STAMPS
+            if (threadIdx.x == 0) {
+                s_state.dbg[5] = s_state.dbg[8]; s_state.dbg[6] = s_state.dbg[9];
+                s_state.dbg[8] = ~0ull; s_state.dbg[9] = 0;
+            }
+#endif
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
             uint4* wq = reinterpret_cast<uint4*>(S);
             for (int q = threadIdx.x; q < NQ; q += 64) wq[q] = sq[q];
+#ifdef R360_STAMPS
+            if (threadIdx.x == 0) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+                S->dbg[0] = t_start; S->dbg[1] = t_loop; S->dbg[2] = t_ticket; S->dbg[3] = t_recs; S->dbg[4] = t_end;
+            }
+#endif
         }
         if (eval_only && threadIdx.x == 0) S->ticket = 0;
     }

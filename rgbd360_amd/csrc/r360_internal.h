@@ -64,6 +64,7 @@ struct alignas(16) IcpState {
     unsigned ticket;
     int pad1;
     double sums[32];    // last pass sums (eval mode)
+    unsigned long long dbg[12];  // s_memrealtime stamps of the diagnostic build (-DR360_STAMPS)
 };
 
 enum { R360_SUM_NVALID = 27, R360_SUM_NVIS = 28, R360_SUM_ERR2 = 31, R360_NSUMS = 32 };

@@ -1,0 +1,33 @@
+"""Diagnostic: in-kernel stamps of the last ICP pass per level (needs the -DR360_STAMPS library:
+`make -C rgbd360_amd/csrc stamps`, run with R360_LIB=rgbd360_amd/lib/librgbd360_hip_stamps.so)."""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import rgbd360_amd as R  # noqa: E402
+
+ctx = R.Context(0)
+cal = R.Calib360(ctx, 480, 640)
+cal.loadExtrinsicCalibration(R.EXTRINSICS_DIR)
+seed = 360 << 16
+fr = []
+for i in range(2):
+    b, d = cal.synth_frame(seed, R.synth_path_pose(seed, i))
+    f = R.Frame360(cal); f.upload(b, d); f.build(); fr.append(f)
+reg = R.RegisterPhotoICP(ctx)
+reg.setNumPyr(5); reg.setGrayVariance(3.0 / 255)
+reg.setTargetFrame(fr[0]); reg.setSourceFrame(fr[1])
+P = np.eye(4, dtype=np.float32)
+for lv in (4, 3, 2, 1, 0):
+    for rep in range(4):
+        reg.eval(lv, P, R.PHOTO_DEPTH)
+    st = (C.c_ulonglong * 12)()
+    R.lib().r360_ctx_debug_stamps(ctx.h, st)
+    t = np.array(list(st), dtype=np.int64)
+    base = t[5]
+    us = lambda x: (x - base) / 100.0
+    print(f"level {lv}: all-blocks loop end {us(t[6]):7.2f} | last block: start {us(t[0]):7.2f} loop-end {us(t[1]):7.2f}"
+          f" ticket {us(t[2]):7.2f} records {us(t[3]):7.2f} end {us(t[4]):7.2f}  (us from first block start)")
