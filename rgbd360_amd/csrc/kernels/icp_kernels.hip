@@ -35,36 +35,6 @@ struct Acc {
     double err2;
 };
 
-__device__ __forceinline__ void acc_row(Acc& A, const float J[6], float r) {
-    A.h[0] += J[0] * J[0];
-    A.h[1] += J[0] * J[1];
-    A.h[2] += J[0] * J[2];
-    A.h[3] += J[0] * J[3];
-    A.h[4] += J[0] * J[4];
-    A.h[5] += J[0] * J[5];
-    A.h[6] += J[1] * J[1];
-    A.h[7] += J[1] * J[2];
-    A.h[8] += J[1] * J[3];
-    A.h[9] += J[1] * J[4];
-    A.h[10] += J[1] * J[5];
-    A.h[11] += J[2] * J[2];
-    A.h[12] += J[2] * J[3];
-    A.h[13] += J[2] * J[4];
-    A.h[14] += J[2] * J[5];
-    A.h[15] += J[3] * J[3];
-    A.h[16] += J[3] * J[4];
-    A.h[17] += J[3] * J[5];
-    A.h[18] += J[4] * J[4];
-    A.h[19] += J[4] * J[5];
-    A.h[20] += J[5] * J[5];
-    A.h[21] += J[0] * r;
-    A.h[22] += J[1] * r;
-    A.h[23] += J[2] * r;
-    A.h[24] += J[3] * r;
-    A.h[25] += J[4] * r;
-    A.h[26] += J[5] * r;
-}
-
 // ---------------------------------------------------------------- per-pixel pipeline
 // Exact part: LUT point, transform and spherical projection, bit-identical to the reference
 // (same float expressions, glibc-exact asinf/atan2f, IEEE sqrt/div).  Everything that decides WHICH
@@ -224,7 +194,9 @@ __device__ __forceinline__ double ld_sc1(const double* p) {  // agent-scope (L1-
                                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
-template <int METHOD>
+struct UnitIn { float4 a, b, s, c; float sp, cp; };
+
+template <int METHOD, int PF>
 __global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src, const float2* __restrict__ trg,
                                                  const float4* __restrict__ tg, const float* __restrict__ sinphi,
                                                  const float* __restrict__ cosphi, const float* __restrict__ sinth,
@@ -266,12 +238,18 @@ __global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src
     const float4* st4 = reinterpret_cast<const float4*>(sinth);
     const float4* ct4 = reinterpret_cast<const float4*>(costh);
     const int cq = nCols >> 2;
-    for (int u = blockIdx.x * TPB + threadIdx.x; u < units; u += gridDim.x * TPB) {
+    auto load_unit = [&](int u) {
+        UnitIn in;
         const int r = u / cq;
         const int c4 = u - r * cq;
-        const float4 a = src4[2 * u], b = src4[2 * u + 1];  // {g0,d0,g1,d1} {g2,d2,g3,d3}
-        const float4 s = st4[c4], c = ct4[c4];
-        const float sp = sinphi[r], cp = cosphi[r];
+        in.a = src4[2 * u]; in.b = src4[2 * u + 1];  // {g0,d0,g1,d1} {g2,d2,g3,d3}
+        in.s = st4[c4]; in.c = ct4[c4];
+        in.sp = sinphi[r]; in.cp = cosphi[r];
+        return in;
+    };
+    auto process_unit = [&](const UnitIn& in) {
+        const float4 a = in.a, b = in.b, s = in.s, c = in.c;
+        const float sp = in.sp, cp = in.cp;
         // two pixels at a time: project both, issue both gathers, then the math (ILP + loads in flight)
         {
             const Proj o0 = project(P, a.y, a.x, sp, cp, s.x, c.x, nRows, nCols, half_nRows, angle_res_inv, C);
@@ -289,15 +267,28 @@ __global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src
             contribute<METHOD>(A, o2, G2, T2, angle_res_inv, C);
             contribute<METHOD>(A, o3, G3, T3, angle_res_inv, C);
         }
+    };
+    const int stride = gridDim.x * TPB;
+    if (PF) {
+        // software pipeline: the next unit's source loads are in flight while this unit computes
+        int u = blockIdx.x * TPB + threadIdx.x;
+        if (u < units) {
+            UnitIn cur = load_unit(u);
+            for (;;) {
+                const int un = u + stride;
+                const bool more = un < units;
+                UnitIn nxt;
+                if (more) nxt = load_unit(un);
+                process_unit(cur);
+                if (!more) break;
+                cur = nxt;
+                u = un;
+            }
+        }
+    } else {
+        for (int u = blockIdx.x * TPB + threadIdx.x; u < units; u += stride) process_unit(load_unit(u));
     }
 
-#ifdef R360_STAMPS
-    const unsigned long long t_loop = __builtin_amdgcn_s_memrealtime();
-    if (threadIdx.x == 0) {
-        __hip_atomic_fetch_min(&S->dbg[8], t_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_max(&S->dbg[9], t_loop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-#endif
     // ---- stage 1: wave butterfly (f32) -> LDS -> per-workgroup fp64 record
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const float mine = wave_reduce_scatter32(A.h, lane);
@@ -438,9 +429,22 @@ extern "C" int r360_libm_eval(const float* x, const float* y, const float* z, in
 
 int icp_blocks_for(int n_pixels) {
     const int units = n_pixels / 4;
-    int b = (units + TPB - 1) / TPB;  // one 4-pixel unit per thread up to 1024 workgroups
+    int b = (units + TPB - 1) / TPB;  // one 4-pixel unit per thread up to the cap
     if (b > 1024) b = 1024;
     return b < 1 ? 1 : b;
+}
+
+static int env_int(const char* name, int dflt) {
+    const char* v = getenv(name);
+    return v ? atoi(v) : dflt;
+}
+
+template <int M, int PF>
+static void launch_pass(r360_ctx* ctx, int nb, const LevelBufs& Ls, const LevelBufs& Lt, const LevelTrig& T,
+                        const IcpConst& C, int first, int eval_only) {
+    hipLaunchKernelGGL((k_icp_pass<M, PF>), dim3(nb), dim3(TPB), 0, ctx->stream, Ls.p0, Lt.p0, Lt.tg, T.sinphi,
+                       T.cosphi, T.sinth, T.costh, Ls.rows, Ls.cols, C, ctx->d_state, ctx->d_partials, first,
+                       eval_only);
 }
 
 int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src, int level, int method,
@@ -448,17 +452,32 @@ int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src
     const LevelBufs& Ls = src->lv[level];
     const LevelBufs& Lt = trg->lv[level];
     const LevelTrig& T = src->calib->trig[level];
-    const int nb = icp_blocks_for(Ls.rows * Ls.cols);
+    static const int pf = env_int("R360_ICP_PF", 1);
+    static int cap = -1;
+    if (cap < 0) {
+        // one resident round: CUs x workgroups per CU of this kernel (grid-stride beyond it)
+        int dev = 0, cus = 0, per = 0;
+        hipGetDevice(&dev);
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)k_icp_pass<R360_PHOTO_DEPTH, 1>, TPB, 0);
+        cap = env_int("R360_ICP_CAP", cus * (per > 0 ? per : 4));
+        if (cap > ctx->partials_cap) cap = ctx->partials_cap;
+        if (cap < 1) cap = 1;
+    }
+    int nb = icp_blocks_for(Ls.rows * Ls.cols);
+    if (nb > cap) nb = cap;
     const char* name = level == 0 ? "k_icp_pass_L0" : "k_icp_pass";
     const int slot = timing_begin(ctx, name);
-#define R360_LAUNCH(M)                                                                                       \
-    hipLaunchKernelGGL(k_icp_pass<M>, dim3(nb), dim3(TPB), 0, ctx->stream, Ls.p0, Lt.p0, Lt.tg, T.sinphi,   \
-                       T.cosphi, T.sinth, T.costh, Ls.rows, Ls.cols, C, ctx->d_state, ctx->d_partials, first, \
-                       eval_only)
-    if (method == R360_PHOTO_CONSISTENCY) R360_LAUNCH(R360_PHOTO_CONSISTENCY);
-    else if (method == R360_DEPTH_CONSISTENCY) R360_LAUNCH(R360_DEPTH_CONSISTENCY);
-    else R360_LAUNCH(R360_PHOTO_DEPTH);
-#undef R360_LAUNCH
+    if (method == R360_PHOTO_CONSISTENCY) {
+        if (pf) launch_pass<R360_PHOTO_CONSISTENCY, 1>(ctx, nb, Ls, Lt, T, C, first, eval_only);
+        else launch_pass<R360_PHOTO_CONSISTENCY, 0>(ctx, nb, Ls, Lt, T, C, first, eval_only);
+    } else if (method == R360_DEPTH_CONSISTENCY) {
+        if (pf) launch_pass<R360_DEPTH_CONSISTENCY, 1>(ctx, nb, Ls, Lt, T, C, first, eval_only);
+        else launch_pass<R360_DEPTH_CONSISTENCY, 0>(ctx, nb, Ls, Lt, T, C, first, eval_only);
+    } else {
+        if (pf) launch_pass<R360_PHOTO_DEPTH, 1>(ctx, nb, Ls, Lt, T, C, first, eval_only);
+        else launch_pass<R360_PHOTO_DEPTH, 0>(ctx, nb, Ls, Lt, T, C, first, eval_only);
+    }
     timing_end(ctx, slot);
     R360_HIP(hipGetLastError());
     return 0;

@@ -26,7 +26,7 @@ for lv in (4, 3, 2, 1, 0):
         reg.eval(lv, P, R.PHOTO_DEPTH)
     st = (C.c_ulonglong * 12)()
     R.lib().r360_ctx_debug_stamps(ctx.h, st)
-    t = np.array(list(st), dtype=np.int64)
+    t = np.array(list(st), dtype=np.uint64).astype(np.float64)
     base = t[5]
     us = lambda x: (x - base) / 100.0
     print(f"level {lv}: all-blocks loop end {us(t[6]):7.2f} | last block: start {us(t[0]):7.2f} loop-end {us(t[1]):7.2f}"
