@@ -22,7 +22,7 @@ reg.setNumPyr(5); reg.setGrayVariance(3.0 / 255)
 reg.setTargetFrame(fr[0]); reg.setSourceFrame(fr[1])
 P = np.eye(4, dtype=np.float32)
 tag = f"PF={os.environ.get('R360_ICP_PF', 'dflt')} CAP={os.environ.get('R360_ICP_CAP', 'dflt')}"
-for lv in (0, 1, 2):
+for lv in [int(x) for x in os.environ.get("LEVELS", "0,1,2").split(",")]:
     for _ in range(3):
         reg.eval(lv, P, R.PHOTO_DEPTH)
     ctx.timing(True); ctx.timing_reset()
