@@ -194,8 +194,6 @@ __device__ __forceinline__ double ld_sc1(const double* p) {  // agent-scope (L1-
                                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
-struct UnitIn { float4 a, b, s, c; float sp, cp; };
-
 template <int METHOD, int PF>
 __global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src, const float2* __restrict__ trg,
                                                  const float4* __restrict__ tg, const float* __restrict__ sinphi,
@@ -238,55 +236,43 @@ __global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src
     const float4* st4 = reinterpret_cast<const float4*>(sinth);
     const float4* ct4 = reinterpret_cast<const float4*>(costh);
     const int cq = nCols >> 2;
-    auto load_unit = [&](int u) {
-        UnitIn in;
-        const int r = u / cq;
-        const int c4 = u - r * cq;
-        in.a = src4[2 * u]; in.b = src4[2 * u + 1];  // {g0,d0,g1,d1} {g2,d2,g3,d3}
-        in.s = st4[c4]; in.c = ct4[c4];
-        in.sp = sinphi[r]; in.cp = cosphi[r];
-        return in;
+    auto one = [&](float d, float g, float sp, float cp, float st, float ct) {
+        const Proj o = project(P, d, g, sp, cp, st, ct, nRows, nCols, half_nRows, angle_res_inv, C);
+        const float4 G = tg[o.t];
+        const float2 T = trg[o.t];
+        contribute<METHOD>(A, o, G, T, angle_res_inv, C);
     };
-    auto process_unit = [&](const UnitIn& in) {
-        const float4 a = in.a, b = in.b, s = in.s, c = in.c;
-        const float sp = in.sp, cp = in.cp;
-        // two pixels at a time: project both, issue both gathers, then the math (ILP + loads in flight)
-        {
-            const Proj o0 = project(P, a.y, a.x, sp, cp, s.x, c.x, nRows, nCols, half_nRows, angle_res_inv, C);
-            const Proj o1 = project(P, a.w, a.z, sp, cp, s.y, c.y, nRows, nCols, half_nRows, angle_res_inv, C);
-            const float4 G0 = tg[o0.t], G1 = tg[o1.t];
-            const float2 T0 = trg[o0.t], T1 = trg[o1.t];
-            contribute<METHOD>(A, o0, G0, T0, angle_res_inv, C);
-            contribute<METHOD>(A, o1, G1, T1, angle_res_inv, C);
-        }
-        {
-            const Proj o2 = project(P, b.y, b.x, sp, cp, s.z, c.z, nRows, nCols, half_nRows, angle_res_inv, C);
-            const Proj o3 = project(P, b.w, b.z, sp, cp, s.w, c.w, nRows, nCols, half_nRows, angle_res_inv, C);
-            const float4 G2 = tg[o2.t], G3 = tg[o3.t];
-            const float2 T2 = trg[o2.t], T3 = trg[o3.t];
-            contribute<METHOD>(A, o2, G2, T2, angle_res_inv, C);
-            contribute<METHOD>(A, o3, G3, T3, angle_res_inv, C);
-        }
+    auto two = [&](float d0, float g0, float d1, float g1, float sp, float cp, float st0, float ct0, float st1,
+                   float ct1) {
+        // project both, issue both gathers, then the math (ILP + loads in flight)
+        const Proj o0 = project(P, d0, g0, sp, cp, st0, ct0, nRows, nCols, half_nRows, angle_res_inv, C);
+        const Proj o1 = project(P, d1, g1, sp, cp, st1, ct1, nRows, nCols, half_nRows, angle_res_inv, C);
+        const float4 G0 = tg[o0.t], G1 = tg[o1.t];
+        const float2 T0 = trg[o0.t], T1 = trg[o1.t];
+        contribute<METHOD>(A, o0, G0, T0, angle_res_inv, C);
+        contribute<METHOD>(A, o1, G1, T1, angle_res_inv, C);
     };
     const int stride = gridDim.x * TPB;
     if (PF) {
-        // software pipeline: the next unit's source loads are in flight while this unit computes
-        int u = blockIdx.x * TPB + threadIdx.x;
-        if (u < units) {
-            UnitIn cur = load_unit(u);
-            for (;;) {
-                const int un = u + stride;
-                const bool more = un < units;
-                UnitIn nxt;
-                if (more) nxt = load_unit(un);
-                process_unit(cur);
-                if (!more) break;
-                cur = nxt;
-                u = un;
-            }
+        // large levels: 4-pixel units (vector loads), processed as two pixel pairs (ILP)
+        for (int u = blockIdx.x * TPB + threadIdx.x; u < units; u += stride) {
+            const int r = u / cq;
+            const int c4 = u - r * cq;
+            const float4 a = src4[2 * u], b = src4[2 * u + 1];  // {g0,d0,g1,d1} {g2,d2,g3,d3}
+            const float4 s = st4[c4], c = ct4[c4];
+            const float sp = sinphi[r], cp = cosphi[r];
+            two(a.y, a.x, a.w, a.z, sp, cp, s.x, c.x, s.y, c.y);
+            two(b.y, b.x, b.w, b.z, sp, cp, s.z, c.z, s.w, c.w);
         }
     } else {
-        for (int u = blockIdx.x * TPB + threadIdx.x; u < units; u += stride) process_unit(load_unit(u));
+        // small levels: one pixel per thread, so the latency chain per thread is a quarter as long
+        const int npx = nRows * nCols;
+        for (int i = blockIdx.x * TPB + threadIdx.x; i < npx; i += stride) {
+            const int r = i / nCols;
+            const int c = i - r * nCols;
+            const float2 a = src[i];
+            one(a.y, a.x, sinphi[r], cosphi[r], sinth[c], costh[c]);
+        }
     }
 
     // ---- stage 1: wave butterfly (f32) -> LDS -> per-workgroup fp64 record
@@ -452,7 +438,9 @@ int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src
     const LevelBufs& Ls = src->lv[level];
     const LevelBufs& Lt = trg->lv[level];
     const LevelTrig& T = src->calib->trig[level];
-    static const int pf = env_int("R360_ICP_PF", 1);
+    // 4-pixel units on the large levels, one pixel per thread where that still fits one resident
+    // round (latency-bound small levels); R360_ICP_PF=0/1 forces one form (experiments)
+    static const int pf_env = env_int("R360_ICP_PF", -1);
     static int cap = -1;
     if (cap < 0) {
         // one resident round: CUs x workgroups per CU of this kernel (grid-stride beyond it)
@@ -464,7 +452,9 @@ int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src
         if (cap > ctx->partials_cap) cap = ctx->partials_cap;
         if (cap < 1) cap = 1;
     }
-    int nb = icp_blocks_for(Ls.rows * Ls.cols);
+    const int npx = Ls.rows * Ls.cols;
+    const int pf = pf_env >= 0 ? pf_env : (npx > cap * TPB ? 1 : 0);
+    int nb = pf ? icp_blocks_for(npx) : (npx + TPB - 1) / TPB;
     if (nb > cap) nb = cap;
     const char* name = level == 0 ? "k_icp_pass_L0" : "k_icp_pass";
     const int slot = timing_begin(ctx, name);
