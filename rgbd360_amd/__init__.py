@@ -18,6 +18,8 @@ import ctypes as C
 import os
 import numpy as np
 
+C = C  # re-exported for callers that drive the C-ABI directly (bench.py)
+
 __all__ = [
     "lib", "Context", "Calib360", "Frame360", "RegisterPhotoICP", "IcpParams", "IcpStats",
     "PHOTO_CONSISTENCY", "DEPTH_CONSISTENCY", "PHOTO_DEPTH", "synth_path_pose", "exp_se3",
