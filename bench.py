@@ -36,15 +36,15 @@ def make_pair_frames(R, cal, seed, i):
     return cal.synth_frame(seed, A), cal.synth_frame(seed, B)
 
 
-def cpu_baseline(R, cal, pairs, fixed_iters, budget_s=20.0):
+def cpu_baseline(R, cal, pairs, fixed_iters, budget_s=12.0):
     """The CPU oracle (C++ restatement, OpenMP) on a bounded sample of the same workload."""
     from oracle import oracle360 as O
     _, rti, K = cal.extrinsics()
     Km = K.reshape(3, 3).T
     prm = O.IcpParams.default(n_pyr=5, std_dev_photo=np.float32(3.0 / 255), fixed_iters_level0=fixed_iters)
     n, t0 = 0, time.perf_counter()
-    while n < len(pairs):
-        (b1, d1), (b2, d2) = pairs[n]
+    while True:
+        (b1, d1), (b2, d2) = pairs[n % len(pairs)]
         s1b, s1d = O.stitch(b1, d1, rti, Km)
         s2b, s2d = O.stitch(b2, d2, rti, Km)
         O.align360(s1b, s1d, s2b, s2d, None, O.PHOTO_DEPTH, prm)
@@ -54,7 +54,7 @@ def cpu_baseline(R, cal, pairs, fixed_iters, budget_s=20.0):
     dt = time.perf_counter() - t0
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     return {"value": n / dt, "unit": "pairs/s", "cores": cores, "kind": "port",
-            "sample": f"{n} synthetic 8x480x640 pairs (stitch x2 + alignFrames360 nPyr=5, "
+            "sample": f"{n} synthetic 8x480x640 pairs (cycling {len(pairs)}) (stitch x2 + alignFrames360 nPyr=5, "
                       f"{fixed_iters} level-0 iterations), oracle/liboracle360.so, {dt:.1f} s"}
 
 
@@ -182,6 +182,12 @@ def main():
     alg_bytes = 8.0 * N0 + 24.0 * V            # B = 8 N + 24 V per pass
     avg_ms = l0_ms / max(l0_n, 1)
     achieved = alg_bytes / (avg_ms * 1e-3) / 1e9 if l0_n else None
+    # HBM bytes per level-0 launch from the rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes of this same
+    # command (tools/profile.sh + tools/profile_summary.py, committed under profiles/)
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", "latest", "l0_pass.json")
+    if os.path.exists(tf):
+        traffic = json.load(open(tf)).get("hbm_bytes_per_launch")
     out = {
         "metric": METRIC, "value": value, "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,  # one step = P pairs per GPU "higher_is_better": True,
@@ -195,7 +201,7 @@ def main():
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+            "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
             "kernel": "k_icp_pass<PHOTO_DEPTH> (level 0)", "avg_launch_ms": avg_ms, "launches": l0_n,
             "bytes_per_launch": alg_bytes, "visible_frac": sso,
         },
