@@ -142,6 +142,9 @@ void r360_exp_se3(const double mu[6], int pseudo, float T[16]);
  * (column-major) is that rig pose in the room frame. */
 int r360_synth_frame(const r360_calib* calib, uint32_t seed, const float rig_pose[16],
                      uint8_t* bgr8, uint16_t* depth8);
+/* Host-only variant (no GPU needed): rt8 = the 8 extrinsics Rt_k, column-major, back to back. */
+int r360_synth_frame_rt(int rows, int cols, const float* rt8, uint32_t seed, const float rig_pose[16],
+                        uint8_t* bgr8, uint16_t* depth8);
 int r360_synth_path_pose(uint32_t seed, int frame, float pose_out[16]);
 
 /* ---------------------------------------------------------------- test hooks

@@ -46,6 +46,19 @@ class Level(C.Structure):
         (n, C.POINTER(C.c_float)) for n in ("gray_src", "depth_src", "gray_trg", "depth_trg", "gx", "gy", "dgx", "dgy")]
 
 
+class Region(C.Structure):
+    _fields_ = [("label", C.c_int), ("count", C.c_int), ("start_idx", C.c_int), ("n_contour", C.c_int),
+                ("contour_off", C.c_int), ("centroid", C.c_float * 3), ("cov", C.c_float * 9),
+                ("model", C.c_float * 4), ("curvature", C.c_float)]
+
+
+class Plane(C.Structure):
+    _fields_ = [("normal", C.c_float * 3), ("center", C.c_float * 3), ("d", C.c_float), ("area", C.c_float),
+                ("elongation", C.c_float), ("curvature", C.c_float), ("ppal", C.c_float * 3), ("nrgb", C.c_float * 3),
+                ("intensity", C.c_float), ("id", C.c_int), ("sensor", C.c_int), ("n_inliers", C.c_int),
+                ("n_hull", C.c_int)]
+
+
 _lib = None
 
 
@@ -81,6 +94,16 @@ def lib() -> C.CDLL:
             "orc_exp_se3": (None, [dp, C.c_int, fp]),
             "orc_huber": (C.c_float, [C.c_float, C.c_float]),
             "orc_libm": (None, [fp, fp, fp, C.c_int, fp, fp]),
+            "orc_cloud_downsample": (None, [fp, vp, C.c_int, C.c_int, fp, vp]),
+            "orc_bilateral": (None, [fp, C.c_int, C.c_int]),
+            "orc_normals": (None, [fp, C.c_int, C.c_int, fp, fp]),
+            "orc_segment": (C.c_int, [fp, fp, C.c_int, C.c_int, ip, ip, C.POINTER(Region), C.c_int, ip, C.c_int]),
+            "orc_pbmap_build": (vp, [fp, vp, C.c_int, C.c_int, fp]),
+            "orc_pbmap_free": (None, [vp]),
+            "orc_pbmap_count": (C.c_int, [vp]),
+            "orc_pbmap_get": (C.c_int, [vp, C.c_int, C.POINTER(Plane), fp, C.c_int]),
+            "orc_match_tables": (C.c_int, [vp, vp, C.c_size_t, C.c_int, ip, ip, ip, ip, vp, vp, C.c_int]),
+            "orc_register_pbmap": (C.c_int, [vp, vp, C.c_size_t, C.c_int, fp, fp, ip, C.c_int, ip, fp, fp, fp]),
         }
         for k, (r, a) in sig.items():
             f = getattr(L, k)
@@ -287,3 +310,124 @@ def rot_angle(Ra, Rb) -> float:
     c = (np.trace(R) - 1) / 2
     s = 0.5 * np.linalg.norm([R[2, 1] - R[1, 2], R[0, 2] - R[2, 0], R[1, 0] - R[0, 1]])
     return float(np.arctan2(s, c))  # well conditioned near 0, unlike arccos
+
+
+# ---------------------------------------------------------------- plane half: per-pixel stages
+def cloud_downsample(depth_m: np.ndarray, bgr: np.ndarray):
+    """A3 for one sensor: (rows, cols) metres + (rows, cols, 3) BGR -> xyz4 (h, w, 4) f32, rgb4 u8."""
+    rows, cols = depth_m.shape
+    d = np.ascontiguousarray(depth_m, np.float32)
+    b = np.ascontiguousarray(bgr, np.uint8)
+    xyz = np.zeros((rows // 2, cols // 2, 4), np.float32)
+    rgb = np.zeros((rows // 2, cols // 2, 4), np.uint8)
+    lib().orc_cloud_downsample(_f(d), _v(b), rows, cols, _f(xyz), _v(rgb))
+    return xyz, rgb
+
+
+def bilateral(xyz4: np.ndarray) -> np.ndarray:
+    """A4: returns a filtered copy (only z changes)."""
+    out = np.ascontiguousarray(xyz4, np.float32).copy()
+    h, w = out.shape[:2]
+    lib().orc_bilateral(_f(out), w, h)
+    return out
+
+
+def normals(xyz4: np.ndarray):
+    """A6: -> (nrm4 (h, w, 4), distance map (h, w))."""
+    x = np.ascontiguousarray(xyz4, np.float32)
+    h, w = x.shape[:2]
+    n = np.zeros((h, w, 4), np.float32)
+    dm = np.zeros((h, w), np.float32)
+    lib().orc_normals(_f(x), w, h, _f(n), _f(dm))
+    return n, dm
+
+
+def segment(xyz4: np.ndarray, nrm4: np.ndarray, max_regions: int = 512):
+    """A7: -> (labels_ccl, labels_final, [region dicts with 'contour' index arrays])."""
+    x = np.ascontiguousarray(xyz4, np.float32)
+    n = np.ascontiguousarray(nrm4, np.float32)
+    h, w = x.shape[:2]
+    lc = np.zeros((h, w), np.int32)
+    lf = np.zeros((h, w), np.int32)
+    regs = (Region * max_regions)()
+    cap = 64 * w * h
+    cont = np.zeros(cap, np.int32)
+    ip = C.POINTER(C.c_int)
+    nr = lib().orc_segment(_f(x), _f(n), w, h, lc.ctypes.data_as(ip), lf.ctypes.data_as(ip), regs, max_regions,
+                           cont.ctypes.data_as(ip), cap)
+    if nr < 0:
+        raise RuntimeError("orc_segment: capacity exceeded")
+    out = []
+    for r in regs[:nr]:
+        out.append(dict(label=r.label, count=r.count, start_idx=r.start_idx, centroid=np.array(r.centroid[:]),
+                        cov=np.array(r.cov[:]).reshape(3, 3), model=np.array(r.model[:]), curvature=r.curvature,
+                        contour=cont[r.contour_off:r.contour_off + r.n_contour].copy()))
+    return lc, lf, out
+
+
+# ---------------------------------------------------------------- plane half: PbMap + registration
+DEFAULT_6DoF, PLANAR_3DoF, ODOMETRY_6DoF, PLANAR_ODOMETRY_3DoF = 0, 1, 2, 3
+
+
+def plane_dict(p: Plane, hull: np.ndarray) -> dict:
+    return dict(normal=np.array(p.normal[:]), center=np.array(p.center[:]), d=p.d, area=p.area,
+                elongation=p.elongation, curvature=p.curvature, ppal=np.array(p.ppal[:]), nrgb=np.array(p.nrgb[:]),
+                intensity=p.intensity, id=p.id, sensor=p.sensor, n_inliers=p.n_inliers, hull=hull)
+
+
+class PbMap:
+    """Plane half of one frame (A3-A9): depth_m8 (8, rows, cols) undistorted metres, bgr8 (8, rows, cols, 3),
+    rt8 (8, 4, 4) extrinsics."""
+
+    def __init__(self, depth_m8, bgr8, rt8):
+        d = np.ascontiguousarray(depth_m8, np.float32)
+        b = np.ascontiguousarray(bgr8, np.uint8)
+        rt = np.ascontiguousarray(np.stack([mat16(m) for m in rt8]), np.float32)
+        self.h = lib().orc_pbmap_build(_f(d), _v(b), d.shape[1], d.shape[2], _f(rt))
+        if not self.h:
+            raise RuntimeError("orc_pbmap_build failed")
+
+    def __len__(self):
+        return lib().orc_pbmap_count(self.h)
+
+    def planes(self) -> list[dict]:
+        out = []
+        for i in range(len(self)):
+            p = Plane()
+            hull = np.zeros((4096, 3), np.float32)
+            lib().orc_pbmap_get(self.h, i, C.byref(p), _f(hull), 4096)
+            out.append(plane_dict(p, hull[:p.n_hull].copy()))
+        return out
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_pbmap_free(self.h)
+            self.h = None
+
+
+def match_tables(ref: PbMap, trg: PbMap, max_match_planes=25, mode=PLANAR_3DoF, cap=128):
+    ns, nt = C.c_int(), C.c_int()
+    sid = np.zeros(cap, np.int32)
+    tid = np.zeros(cap, np.int32)
+    un = np.zeros(cap * cap, np.uint8)
+    words = (cap * cap + 63) // 64
+    bi = np.zeros(cap * cap * words, np.uint64)
+    ip = C.POINTER(C.c_int)
+    w = lib().orc_match_tables(ref.h, trg.h, max_match_planes, mode, C.byref(ns), C.byref(nt), sid.ctypes.data_as(ip),
+                               tid.ctypes.data_as(ip), _v(un), _v(bi), cap)
+    n, m = ns.value, nt.value
+    return dict(sid=sid[:n].copy(), tid=tid[:m].copy(), unary=un[:n * m].reshape(n, m).copy(),
+                binary=bi[:n * m * w].reshape(n * m, w).copy(), words=w)
+
+
+def register_pbmap(ref: PbMap, trg: PbMap, max_match_planes=25, mode=PLANAR_3DoF):
+    pose = np.zeros(16, np.float32)
+    info = np.zeros(36, np.float32)
+    pairs = np.zeros(2 * 256, np.int32)
+    n, am, as_, at = C.c_int(), C.c_float(), C.c_float(), C.c_float()
+    ip = C.POINTER(C.c_int)
+    rc = lib().orc_register_pbmap(ref.h, trg.h, max_match_planes, mode, _f(pose), _f(info), pairs.ctypes.data_as(ip),
+                                  256, C.byref(n), C.byref(am), C.byref(as_), C.byref(at))
+    return dict(good=rc, pose=from16(pose), info=info.reshape(6, 6).T.copy(),
+                matches={int(pairs[2 * k]): int(pairs[2 * k + 1]) for k in range(min(n.value, 256))},
+                area_matched=am.value, area_src=as_.value, area_trg=at.value)

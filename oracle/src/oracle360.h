@@ -104,6 +104,63 @@ void orc_libm(const float* x, const float* y, const float* z, int n, float* asin
 /* Huber weight (RegisterPhotoICP.h:545-554), float instantiation */
 float orc_huber(float err, float reg);
 
+/* =============================== plane half (A3-A9, A11-A13) ===============================
+ * Organized clouds are w x h = (cols/2) x (rows/2) per sensor, row-major:
+ *   xyz4[i] = {x, y, z, 0} float, rgb4[i] = {r, g, b, 0} u8, nrm4[i] = {nx, ny, nz, 0}. */
+
+/* A3: CloudRGBD_Ext::getPointCloudUndist (CloudRGBD_Ext.h:78-139) + DownsampleRGBD(2)::
+ * downsamplePointCloud (DownsampleRGBD.h:209-311) of one sensor. */
+void orc_cloud_downsample(const float* depth_m, const uint8_t* bgr, int rows, int cols,
+                          float* xyz4, uint8_t* rgb4);
+/* A4: pcl::FastBilateralFilter, sigma_s 10, sigma_r 0.05 (Frame360.h:493-499) */
+void orc_bilateral(float* xyz4, int w, int h);
+/* A6: pcl::IntegralImageNormalEstimation AVERAGE_3D_GRADIENT, maxDepthChangeFactor 0.02,
+ * smoothing 8, depth dependent (Frame360.h:945-955).  dist = distance map. */
+void orc_normals(const float* xyz4, int w, int h, float* nrm4, float* dist);
+
+/* A7: one PlanarRegion of OrganizedMultiPlaneSegmentation::segmentAndRefine (App. C.2). */
+typedef struct {
+    int   label;          /* CCL label (= index into label_indices)                  */
+    int   count;          /* inliers after refinement                                */
+    int   start_idx;      /* inlier_indices[i].indices[0]                            */
+    int   n_contour;      /* boundary length; indices at contour[contour_off ...]    */
+    int   contour_off;
+    float centroid[3];    /* pre-refinement statistics (PlanarRegion)                */
+    float cov[9];
+    float model[4];       /* ModelCoefficients (n, d)                                */
+    float curvature;
+} orc_region;
+
+/* Returns the number of regions, or -1 if max_regions / contour_cap is too small.
+ * labels_ccl: CCL labels (-1 = none); labels_final: labels after refinement. */
+int orc_segment(const float* xyz4, const float* nrm4, int w, int h,
+                int* labels_ccl, int* labels_final,
+                orc_region* regions, int max_regions, int* contour, int contour_cap);
+
+/* A8/A9: one PbMap plane (mrpt::pbmap::Plane fields used on the path). */
+typedef struct {
+    float normal[3], center[3], d, area, elongation, curvature, ppal[3], nrgb[3], intensity;
+    int   id, sensor, n_inliers, n_hull;
+} orc_plane;
+
+/* PbMap of a frame from per-sensor segmentations (regions packed sensor after sensor,
+ * contour_base[s] = offset of sensor s in contour_all). rt8 = Rt_k col-major. */
+void* orc_pbmap_from_segments(int n_sensors, int w, int h, const float* xyz4_all, const uint8_t* rgb4_all,
+                              const int* labels_final_all, const orc_region* regions, const int* n_regions,
+                              const int* contour_all, const int* contour_base, const float* rt8);
+/* Whole plane half of one frame: depth_m8 = 8 undistorted depth images (metres), bgr8 = 8 BGR. */
+void* orc_pbmap_build(const float* depth_m8, const uint8_t* bgr8, int rows, int cols, const float* rt8);
+void  orc_pbmap_free(void* h);
+int   orc_pbmap_count(const void* h);
+int   orc_pbmap_get(const void* h, int i, orc_plane* out, float* hull_xyz, int hull_cap);
+/* A11+A12 tables: subgraph ids, unary [ns][nt] and binary [(i*nt+j)][words] bitsets; returns words. */
+int   orc_match_tables(const void* href, const void* htrg, size_t max_match_planes, int mode, int* ns, int* nt,
+                       int* sid, int* tid, uint8_t* unary, uint64_t* binary, int cap);
+/* A11-A13: RegisterRGBD360::RegisterPbMap.  Returns 1 good, 0 insufficient / ill-conditioned. */
+int   orc_register_pbmap(const void* href, const void* htrg, size_t max_match_planes, int mode, float pose[16],
+                         float info[36], int* pairs, int pair_cap, int* n_match, float* area_matched,
+                         float* area_src, float* area_trg);
+
 #ifdef __cplusplus
 }
 #endif

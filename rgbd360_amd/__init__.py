@@ -95,6 +95,7 @@ _SIGS = [
                                 _IP]),
     ("r360_exp_se3", None, [_DP, C.c_int, _FP]),
     ("r360_synth_frame", C.c_int, [_P, C.c_uint32, _FP, _P, _P]),
+    ("r360_synth_frame_rt", C.c_int, [C.c_int, C.c_int, _FP, C.c_uint32, _FP, _P, _P]),
     ("r360_synth_path_pose", C.c_int, [C.c_uint32, C.c_int, _FP]),
     ("r360_libm_eval", C.c_int, [_FP, _FP, _FP, C.c_int, _FP, _FP, C.c_int]),
     ("r360_ctx_debug_stamps", C.c_int, [_P, C.POINTER(C.c_ulonglong)]),
@@ -350,6 +351,16 @@ def libm_eval(x, y, z, on_device: bool = False):
     _check(lib().r360_libm_eval(_fptr(x), _fptr(y), _fptr(z), x.size, _fptr(a), _fptr(t), int(on_device)),
            "libm_eval")
     return a, t
+
+
+def synth_frame_rt(rows: int, cols: int, rt8: np.ndarray, seed: int, rig_pose: np.ndarray):
+    """Host-only synthetic frame (no GPU): rt8 = (8, 4, 4) extrinsics."""
+    bgr = np.zeros((8, rows, cols, 3), np.uint8)
+    dep = np.zeros((8, rows, cols), np.uint16)
+    rt = np.ascontiguousarray(np.stack([_mat16(m) for m in rt8]), np.float32)
+    p = _mat16(rig_pose)
+    _check(lib().r360_synth_frame_rt(rows, cols, _fptr(rt), seed, _fptr(p), _vptr(bgr), _vptr(dep)), "synth_frame_rt")
+    return bgr, dep
 
 
 def synth_path_pose(seed: int, frame: int) -> np.ndarray:

@@ -105,19 +105,19 @@ extern "C" int r360_synth_path_pose(uint32_t seed, int frame, float pose_out[16]
 
 // rig_pose: column-major 4x4 rig -> room.  noise seed = scene seed ^ hash(rig pose bits) unless
 // the caller varies the scene seed; depth noise uses (seed, sensor, pixel).
-extern "C" int r360_synth_frame(const r360_calib* calib, uint32_t seed, const float rig_pose[16], uint8_t* bgr8,
-                                uint16_t* depth8) {
-    if (!calib || !rig_pose || !bgr8 || !depth8) { r360_set_error("null arg"); return -2; }
+static int synth_impl(int rows, int cols, const float (*rt)[16], uint32_t seed, const float rig_pose[16],
+                      uint8_t* bgr8, uint16_t* depth8) {
     const Scene sc = make_scene(seed >> 16);
-    const int rows = calib->rows, cols = calib->cols;
-    const float f = calib->K[0], cx = calib->K[6], cy = calib->K[7];
+    // cameraMatrix convention of r360_calib_create (CloudRGBD_Ext.h:97-102)
+    const float f = 525 * (float)(cols / 640.0);
+    const float cx = cols / 2 - 0.5, cy = rows / 2 - 0.5;
     uint32_t pose_h = seed;
     for (int i = 0; i < 16; ++i) { uint32_t b; memcpy(&b, &rig_pose[i], 4); pose_h = mix32(pose_h ^ b); }
     const float* P = rig_pose;
 #pragma omp parallel for schedule(dynamic, 4)
     for (int job = 0; job < 8 * rows; ++job) {
         const int k = job / rows, v = job % rows;
-        const float* Rt = calib->rt[k];
+        const float* Rt = rt[k];
         for (int u = 0; u < cols; ++u) {
             const float dc[3] = {(u - cx) / f, (v - cy) / f, 1.f};
             float dr[3], orr[3], dw[3], ow[3];
@@ -168,4 +168,18 @@ extern "C" int r360_synth_frame(const r360_calib* calib, uint32_t seed, const fl
         }
     }
     return 0;
+}
+
+extern "C" int r360_synth_frame(const r360_calib* calib, uint32_t seed, const float rig_pose[16], uint8_t* bgr8,
+                                uint16_t* depth8) {
+    if (!calib || !rig_pose || !bgr8 || !depth8) { r360_set_error("null arg"); return -2; }
+    return synth_impl(calib->rows, calib->cols, calib->rt, seed, rig_pose, bgr8, depth8);
+}
+
+extern "C" int r360_synth_frame_rt(int rows, int cols, const float* rt8, uint32_t seed, const float rig_pose[16],
+                                   uint8_t* bgr8, uint16_t* depth8) {
+    if (!rt8 || !rig_pose || !bgr8 || !depth8 || rows <= 0 || cols <= 0) { r360_set_error("null arg"); return -2; }
+    float rt[8][16];
+    memcpy(rt, rt8, sizeof(rt));
+    return synth_impl(rows, cols, rt, seed, rig_pose, bgr8, depth8);
 }
