@@ -136,6 +136,54 @@ int r360_icp_eval(r360_ctx* ctx, r360_frame* trg, r360_frame* src, int level, co
 /* CPose3D::exp(mu, pseudo) (MRPT; used at RegisterPhotoICP.h:4697). */
 void r360_exp_se3(const double mu[6], int pseudo, float T[16]);
 
+/* ---------------------------------------------------------------- PbMap (Frame360 planes)
+ * Frame360::getPlanes (Frame360.h:615-640) runs when a frame is built with R360_BUILD_PLANES:
+ * cloud + bilateral filter + normals + segmentation on the GPU, per-plane descriptors and the
+ * sensor grouping/merging on the host.  One plane = the mrpt::pbmap::Plane fields used on the
+ * path, in the rig frame. */
+typedef struct {
+    float normal[3], center[3], d, area, elongation, curvature, ppal[3], nrgb[3], intensity;
+    int   id, sensor, n_inliers, n_hull;
+} r360_plane;
+
+int r360_frame_get_planes(r360_frame* f, r360_plane* out, int cap, int* n);
+/* Closed convex hull polygon (polygonContourPtr) of plane i, xyz triples. */
+int r360_frame_get_plane_hull(r360_frame* f, int i, float* xyz, int cap, int* n);
+
+/* ---------------------------------------------------------------- RegisterRGBD360
+ * Replaces include/RegisterRGBD360.h:97-337.  registrationType (:260-266). */
+enum { R360_DEFAULT_6DoF = 0, R360_PLANAR_3DoF = 1, R360_ODOMETRY_6DoF = 2, R360_PLANAR_ODOMETRY_3DoF = 3 };
+
+/* RegisterPbMap(ref, trg, max_match_planes, mode) (:276-337): returns 1 (good alignment) or 0
+ * (insufficient matching / ill-conditioned; pose and info are then left untouched, :306-310).
+ * pose = getPose() (target as seen from the reference), info = getInfoMat(), match_pairs =
+ * getMatchedPlanes() as (ref id, trg id) pairs, area_matched = getAreaMatched(),
+ * area_src/area_trg = the public areaSource/areaTarget members. */
+int r360_register_pbmap(r360_ctx* ctx, r360_frame* ref, r360_frame* trg, size_t max_match_planes, int mode,
+                        float pose[16], float info[36], int* match_pairs, int pair_cap, int* n_match,
+                        float* area_matched, float* area_src, float* area_trg);
+/* Register(): RegisterPbMap, then alignFrames360 initialised with rotOffset * P * rotOffset^-1
+ * (OdometryKeyFrame360.cpp:167-171, 205, 244-254; guess replaces P when the PbMap registration
+ * fails); pose = rotOffset^-1 * getOptimalPose() * rotOffset.  Returns 0, or 1 when the PbMap stage
+ * failed and the dense stage started from guess. */
+int r360_register(r360_ctx* ctx, r360_frame* ref, r360_frame* trg, const float guess[16],
+                  const r360_icp_params* p, size_t max_match_planes, int mode, float pose[16],
+                  float info[36], r360_icp_stats* st);
+/* SubgraphMatcher constraint tables (k_match_tables): unary [ns][nt], binary [(i*nt+j)][words]
+ * bitsets over (k*nt+l).  Returns words.  Inspection/parity hook. */
+int r360_pbmap_match_tables(r360_ctx* ctx, r360_frame* ref, r360_frame* trg, size_t max_match_planes,
+                            int mode, int* ns, int* nt, int* sid, int* tid, uint8_t* unary,
+                            uint64_t* binary, int cap);
+
+/* Inspection hooks of the per-pixel plane half (parity tests).  Sizes: 8 x (rows/2) x (cols/2). */
+typedef struct {
+    int   label, count, start_idx, n_contour, n_fit;
+    float centroid[3], cov[9], model[4], curvature;
+} r360_region;
+int r360_frame_get_cloud(r360_frame* f, float* xyz4, uint8_t* rgb4, float* nrm4, float* dist);
+int r360_frame_get_labels(r360_frame* f, int* lab, int* labf);
+int r360_frame_get_regions(r360_frame* f, int sensor, r360_region* out, int cap, int* n);
+
 /* ---------------------------------------------------------------- synthetic scenes
  * Procedural indoor room rendered by the 8 rig cameras.  Deterministic in
  * (seed, frame).  Rig pose of frame `frame` along the generator's planar path; pose_out

@@ -4,7 +4,10 @@ Python mirror of the reference's C++ class surface for the hot path, written ove
 ``rgbd360_amd/lib/librgbd360_hip.so`` (declared in ``include/rgbd360_hip.h``):
 
     Calib360          include/Calib360.h:44-132
-    Frame360          include/Frame360.h:93-1150   (loadFrame / undistort / stitchSphericalImage)
+    Frame360          include/Frame360.h:93-1150   (loadFrame / undistort / stitchSphericalImage /
+                      buildSphereCloud / getPlanes)
+    RegisterRGBD360   include/RegisterRGBD360.h:47-340 (RegisterPbMap / getPose / getInfoMat /
+                      getMatchedPlanes / getAreaMatched / areaSource / areaTarget, Register alias)
     RegisterPhotoICP  include/RegisterPhotoICP.h:85-4784 (setSourceFrame / setTargetFrame /
                       alignFrames360 / getOptimalPose / getHessian / getGradient)
 
@@ -21,7 +24,7 @@ import numpy as np
 C = C  # re-exported for callers that drive the C-ABI directly (bench.py)
 
 __all__ = [
-    "lib", "Context", "Calib360", "Frame360", "RegisterPhotoICP", "IcpParams", "IcpStats",
+    "lib", "Context", "Calib360", "Frame360", "RegisterPhotoICP", "RegisterRGBD360", "IcpParams", "IcpStats",
     "PHOTO_CONSISTENCY", "DEPTH_CONSISTENCY", "PHOTO_DEPTH", "synth_path_pose", "exp_se3",
     "LIB_PATH", "ABI_SYMBOLS",
 ]
@@ -55,6 +58,23 @@ class IcpStats(C.Structure):
         ("iters", C.c_int * 8), ("evals", C.c_int * 8), ("illposed", C.c_int), ("sso", C.c_float),
         ("error", C.c_double), ("passes", C.c_int), ("pad", C.c_int),
     ]
+
+
+class Plane(C.Structure):
+    """r360_plane — the mrpt::pbmap::Plane fields used on the path (rig frame)."""
+    _fields_ = [("normal", C.c_float * 3), ("center", C.c_float * 3), ("d", C.c_float), ("area", C.c_float),
+                ("elongation", C.c_float), ("curvature", C.c_float), ("ppal", C.c_float * 3), ("nrgb", C.c_float * 3),
+                ("intensity", C.c_float), ("id", C.c_int), ("sensor", C.c_int), ("n_inliers", C.c_int),
+                ("n_hull", C.c_int)]
+
+
+class Region(C.Structure):
+    _fields_ = [("label", C.c_int), ("count", C.c_int), ("start_idx", C.c_int), ("n_contour", C.c_int),
+                ("n_fit", C.c_int), ("centroid", C.c_float * 3), ("cov", C.c_float * 9), ("model", C.c_float * 4),
+                ("curvature", C.c_float)]
+
+
+DEFAULT_6DoF, PLANAR_3DoF, ODOMETRY_6DoF, PLANAR_ODOMETRY_3DoF = 0, 1, 2, 3
 
 
 # (name, restype, argtypes) of every exported entry point of include/rgbd360_hip.h
@@ -94,6 +114,15 @@ _SIGS = [
     ("r360_icp_eval", C.c_int, [_P, _P, _P, C.c_int, _FP, C.c_int, C.POINTER(IcpParams), _DP, _DP, _DP, _IP,
                                 _IP]),
     ("r360_exp_se3", None, [_DP, C.c_int, _FP]),
+    ("r360_frame_get_planes", C.c_int, [_P, C.POINTER(Plane), C.c_int, _IP]),
+    ("r360_frame_get_plane_hull", C.c_int, [_P, C.c_int, _FP, C.c_int, _IP]),
+    ("r360_register_pbmap", C.c_int, [_P, _P, _P, C.c_size_t, C.c_int, _FP, _FP, _IP, C.c_int, _IP, _FP, _FP, _FP]),
+    ("r360_register", C.c_int, [_P, _P, _P, _FP, C.POINTER(IcpParams), C.c_size_t, C.c_int, _FP, _FP,
+                                C.POINTER(IcpStats)]),
+    ("r360_pbmap_match_tables", C.c_int, [_P, _P, _P, C.c_size_t, C.c_int, _IP, _IP, _IP, _IP, _P, _P, C.c_int]),
+    ("r360_frame_get_cloud", C.c_int, [_P, _FP, _P, _FP, _FP]),
+    ("r360_frame_get_labels", C.c_int, [_P, _IP, _IP]),
+    ("r360_frame_get_regions", C.c_int, [_P, C.c_int, C.POINTER(Region), C.c_int, _IP]),
     ("r360_synth_frame", C.c_int, [_P, C.c_uint32, _FP, _P, _P]),
     ("r360_synth_frame_rt", C.c_int, [C.c_int, C.c_int, _FP, C.c_uint32, _FP, _P, _P]),
     ("r360_synth_path_pose", C.c_int, [C.c_uint32, C.c_int, _FP]),
@@ -260,6 +289,55 @@ class Frame360:
     def stitchSphericalImage(self):
         self.build(BUILD_SPHERE | BUILD_PYRAMID)
 
+    def buildSphereCloud(self):
+        self.build(BUILD_UNDISTORT | BUILD_CLOUD)
+
+    def getPlanes(self):
+        """Frame360::getPlanes (Frame360.h:615-640): builds the PbMap; returns the plane list."""
+        self.build(BUILD_UNDISTORT | BUILD_PLANES)
+        return self.planes()
+
+    def planes(self) -> list[dict]:
+        n = C.c_int()
+        _check(lib().r360_frame_get_planes(self.h, None, 0, C.byref(n)), "get_planes")
+        arr = (Plane * max(n.value, 1))()
+        _check(lib().r360_frame_get_planes(self.h, arr, n.value, C.byref(n)), "get_planes")
+        out = []
+        for i, p in enumerate(arr[:n.value]):
+            hull = np.zeros((max(p.n_hull, 1), 3), np.float32)
+            m = C.c_int()
+            _check(lib().r360_frame_get_plane_hull(self.h, i, _fptr(hull), p.n_hull, C.byref(m)), "get_plane_hull")
+            out.append(dict(normal=np.array(p.normal[:]), center=np.array(p.center[:]), d=p.d, area=p.area,
+                            elongation=p.elongation, curvature=p.curvature, ppal=np.array(p.ppal[:]),
+                            nrgb=np.array(p.nrgb[:]), intensity=p.intensity, id=p.id, sensor=p.sensor,
+                            n_inliers=p.n_inliers, hull=hull[:p.n_hull].copy()))
+        return out
+
+    def cloud(self):
+        """Per-sensor organized clouds after downsample + bilateral filter, normals and distance map."""
+        h, w = self.rows // 2, self.cols // 2
+        xyz = np.zeros((8, h, w, 4), np.float32)
+        rgb = np.zeros((8, h, w, 4), np.uint8)
+        nrm = np.zeros((8, h, w, 4), np.float32)
+        dist = np.zeros((8, h, w), np.float32)
+        _check(lib().r360_frame_get_cloud(self.h, _fptr(xyz), _vptr(rgb), _fptr(nrm), _fptr(dist)), "get_cloud")
+        return xyz, rgb, nrm, dist
+
+    def labels(self):
+        h, w = self.rows // 2, self.cols // 2
+        lab = np.zeros((8, h, w), np.int32)
+        labf = np.zeros((8, h, w), np.int32)
+        _check(lib().r360_frame_get_labels(self.h, lab.ctypes.data_as(_IP), labf.ctypes.data_as(_IP)), "get_labels")
+        return lab, labf
+
+    def regions(self, sensor: int) -> list[dict]:
+        n = C.c_int()
+        arr = (Region * 64)()
+        _check(lib().r360_frame_get_regions(self.h, sensor, arr, 64, C.byref(n)), "get_regions")
+        return [dict(label=r.label, count=r.count, start_idx=r.start_idx, n_contour=r.n_contour, n_fit=r.n_fit,
+                     centroid=np.array(r.centroid[:]), cov=np.array(r.cov[:]).reshape(3, 3),
+                     model=np.array(r.model[:]), curvature=r.curvature) for r in arr[:n.value]]
+
     def sphere(self):
         bgr = np.zeros((self.sph_rows, self.sph_cols, 3), np.uint8)
         dep = np.zeros((self.sph_rows, self.sph_cols), np.uint16)
@@ -290,6 +368,81 @@ class Frame360:
             self.close()
         except Exception:
             pass
+
+
+class RegisterRGBD360:
+    """RegisterRGBD360 (include/RegisterRGBD360.h:47-340): PbMap registration of two Frame360."""
+
+    def __init__(self, ctx: "Context", config_file: str | None = None):
+        # the matcher thresholds are those of config_files/configLocaliser_sphericalOdometry.ini
+        self.ctx = ctx
+        self.config_file = config_file
+        self.rigidTransf = np.eye(4, dtype=np.float32)
+        self.informationM = np.zeros((6, 6), np.float32)
+        self.bestMatch: dict[int, int] = {}
+        self.areaMatched = self.areaSource = self.areaTarget = 0.0
+        self.ref = self.trg = None
+        self.max_match_planes = 0
+
+    def setReference(self, ref: "Frame360", max_match_planes: int = 0):
+        self.ref, self.max_match_planes = ref, max_match_planes
+
+    def setTarget(self, trg: "Frame360", max_match_planes: int = 0):
+        self.trg, self.max_match_planes = trg, max_match_planes
+
+    def RegisterPbMap(self, frame1=None, frame2=None, max_match_planes: int = 0, registMode: int = DEFAULT_6DoF) -> bool:
+        if frame1 is not None:
+            self.setReference(frame1, max_match_planes)
+        if frame2 is not None:
+            self.setTarget(frame2, max_match_planes)
+        pose = _mat16(self.rigidTransf)
+        info = np.ascontiguousarray(self.informationM.T).reshape(36).copy()
+        pairs = np.zeros(512, np.int32)
+        n = C.c_int()
+        am, as_, at = C.c_float(), C.c_float(self.areaSource), C.c_float(self.areaTarget)
+        rc = _check(lib().r360_register_pbmap(self.ctx.h, self.ref.h, self.trg.h, self.max_match_planes, registMode,
+                                              _fptr(pose), _fptr(info), pairs.ctypes.data_as(_IP), 256, C.byref(n),
+                                              C.byref(am), C.byref(as_), C.byref(at)), "RegisterPbMap")
+        self.bestMatch = {int(pairs[2 * k]): int(pairs[2 * k + 1]) for k in range(min(n.value, 256))}
+        self.areaMatched = am.value
+        if rc == 1:
+            self.rigidTransf = _from16(pose)
+            self.informationM = info.reshape(6, 6).T.copy()
+            self.areaSource, self.areaTarget = as_.value, at.value
+        return rc == 1
+
+    def getPose(self): return self.rigidTransf
+    def getInfoMat(self): return self.informationM
+    def getCovMat(self): return np.linalg.inv(self.informationM.astype(np.float64)).astype(np.float32)
+    def getMatchedPlanes(self): return dict(self.bestMatch)
+    def getAreaMatched(self): return self.areaMatched
+
+    def match_tables(self, mode: int = PLANAR_3DoF, cap: int = 128):
+        """k_match_tables output for the current reference/target subgraphs (inspection)."""
+        ns, nt = C.c_int(), C.c_int()
+        sid, tid = np.zeros(cap, np.int32), np.zeros(cap, np.int32)
+        un = np.zeros(cap * cap, np.uint8)
+        words = (cap * cap + 63) // 64
+        bi = np.zeros(cap * cap * words, np.uint64)
+        w = _check(lib().r360_pbmap_match_tables(self.ctx.h, self.ref.h, self.trg.h, self.max_match_planes, mode,
+                                                 C.byref(ns), C.byref(nt), sid.ctypes.data_as(_IP),
+                                                 tid.ctypes.data_as(_IP), _vptr(un), _vptr(bi), cap), "match_tables")
+        n, m = ns.value, nt.value
+        return dict(sid=sid[:n].copy(), tid=tid[:m].copy(), unary=un[:n * m].reshape(n, m).copy(),
+                    binary=bi[:n * m * w].reshape(n * m, w).copy(), words=w)
+
+
+def register(ctx: "Context", ref: "Frame360", trg: "Frame360", guess=None, params: "IcpParams | None" = None,
+             max_match_planes: int = 25, mode: int = PLANAR_3DoF):
+    """Register() alias: PbMap -> rotOffset conjugation -> alignFrames360 (OdometryKeyFrame360.cpp:248-254).
+    Returns (pose, info, stats, pbmap_ok)."""
+    g = _mat16(np.eye(4) if guess is None else guess)
+    pose, info = np.zeros(16, np.float32), np.zeros(36, np.float32)
+    st = IcpStats()
+    p = params if params is not None else IcpParams.default()
+    rc = _check(lib().r360_register(ctx.h, ref.h, trg.h, _fptr(g), C.byref(p), max_match_planes, mode, _fptr(pose),
+                                    _fptr(info), C.byref(st)), "register")
+    return _from16(pose), info.reshape(6, 6).T.copy(), st, rc == 0
 
 
 class RegisterPhotoICP:

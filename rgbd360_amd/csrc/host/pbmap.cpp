@@ -1,0 +1,873 @@
+// pbmap.cpp — host side of the plane half of librgbd360_hip.so:
+//   * plane-buffer allocation and the device->host hand-over of the segmentation (plane_seg.hip)
+//   * Frame360::getPlanesSensor descriptors (include/Frame360.h:940-1075), groupPlanes / mergePlanes
+//     (:657-832) — sequential, per-plane work on a few dozen planes, so it stays on the host
+//   * RegisterRGBD360::setReference/setTarget (RegisterRGBD360.h:111-196), RegisterPbMap (:276-337)
+//     with the interpretation tree on unary/binary tables computed by k_match_tables (plane_match.hip)
+//     and the ConsistencyTest pose/information estimate
+//   * the Register() alias of OdometryKeyFrame360.cpp:248-254 (PbMap -> rotOffset conjugation ->
+//     alignFrames360)
+// The MRPT-pbmap definitions (hull, descriptors, same-plane tests, matcher, consistency) are the ones
+// documented in DESIGN.md §PbMap; the oracle (oracle/src/pbmap_oracle.cpp) restates them independently.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <set>
+#include <vector>
+
+#include "../r360_internal.h"
+
+#define CHECK_ARG(cond, msg)                  \
+    do {                                      \
+        if (!(cond)) {                        \
+            r360_set_error("%s", msg);        \
+            return -2;                        \
+        }                                     \
+    } while (0)
+
+int launch_match_tables(r360_ctx* ctx, const float* d_desc, int ns, int nt, int mode, uint8_t* d_unary,
+                        unsigned long long* d_bin, int words);
+
+namespace {
+
+struct P3 {
+    float x = 0, y = 0, z = 0;
+    float at(int k) const { return k == 0 ? x : (k == 1 ? y : z); }
+};
+inline float dot(const P3& a, const P3& b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+inline P3 minus(const P3& a, const P3& b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline float norm2(const P3& a) { return dot(a, a); }
+inline P3 affine(const float* T, const P3& p) {
+    return {T[0] * p.x + T[4] * p.y + T[8] * p.z + T[12], T[1] * p.x + T[5] * p.y + T[9] * p.z + T[13],
+            T[2] * p.x + T[6] * p.y + T[10] * p.z + T[14]};
+}
+inline P3 linear(const float* T, const P3& p) {
+    return {T[0] * p.x + T[4] * p.y + T[8] * p.z, T[1] * p.x + T[5] * p.y + T[9] * p.z, T[2] * p.x + T[6] * p.y + T[10] * p.z};
+}
+
+struct HPlane {
+    P3 normal, center, ppal;
+    float d = 0, area = 0, elongation = 1, curvature = 0;
+    float nrgb[3] = {0, 0, 0};
+    float intensity = 0;
+    int id = 0, sensor = 0;
+    std::vector<P3> hull;   // closed polygon
+    r360p::Moments st;
+};
+
+int axis_of(const P3& n) {
+    int k0 = (std::fabs(n.at(0)) > std::fabs(n.at(1))) ? 0 : 1;
+    return (std::fabs(n.at(k0)) > std::fabs(n.at(2))) ? k0 : 2;
+}
+
+// calcConvexHull: monotone chain on the two coordinates orthogonal to the dominant normal axis
+void convex_hull(HPlane& pl, const std::vector<P3>& pts) {
+    const int k0 = axis_of(pl.normal), a = (k0 + 1) % 3, b = (k0 + 2) % 3;
+    const int n = int(pts.size());
+    pl.hull.clear();
+    if (!n) return;
+    std::vector<int> idx(n);
+    for (int i = 0; i < n; ++i) idx[i] = i;
+    std::sort(idx.begin(), idx.end(), [&](int u, int v) {
+        const float ux = pts[u].at(a), vx = pts[v].at(a), uy = pts[u].at(b), vy = pts[v].at(b);
+        if (ux != vx) return ux < vx;
+        if (uy != vy) return uy < vy;
+        return u < v;
+    });
+    auto turn = [&](int o, int p, int q) {
+        const double ox = pts[o].at(a), oy = pts[o].at(b);
+        return ((double)pts[p].at(a) - ox) * ((double)pts[q].at(b) - oy) -
+               ((double)pts[p].at(b) - oy) * ((double)pts[q].at(a) - ox);
+    };
+    std::vector<int> chain;
+    chain.reserve(2 * n + 1);
+    for (int i = 0; i < n; ++i) {           // lower hull
+        while (chain.size() >= 2 && turn(chain[chain.size() - 2], chain.back(), idx[i]) <= 0) chain.pop_back();
+        chain.push_back(idx[i]);
+    }
+    const size_t lower = chain.size() + 1;
+    for (int i = n - 2; i >= 0; --i) {      // upper hull
+        while (chain.size() >= lower && turn(chain[chain.size() - 2], chain.back(), idx[i]) <= 0) chain.pop_back();
+        chain.push_back(idx[i]);
+    }
+    for (int i : chain) pl.hull.push_back(pts[i]);
+}
+
+// computeMassCenterAndArea
+void area_and_center(HPlane& pl) {
+    const int k0 = axis_of(pl.normal), k1 = (k0 + 1) % 3, k2 = (k0 + 2) % 3;
+    const float ct = std::fabs(pl.normal.at(k0));
+    float twice = 0.0f;
+    float mc[3] = {0, 0, 0};
+    const size_t n = pl.hull.size();
+    for (size_t i = 0; i < n; i++) {
+        const P3& p = pl.hull[i];
+        const P3& q = pl.hull[(i + 1) % n];
+        const double cs = p.at(k1) * q.at(k2) - p.at(k2) * q.at(k1);
+        twice += cs;
+        mc[k1] += (p.at(k1) + q.at(k1)) * cs;
+        mc[k2] += (p.at(k2) + q.at(k2)) * cs;
+    }
+    pl.area = std::fabs(twice) / (2 * ct);
+    mc[k1] /= (3 * twice);
+    mc[k2] /= (3 * twice);
+    const float nc = dot(pl.normal, pl.center);
+    mc[k0] = (nc - pl.normal.at(k1) * mc[k1] - pl.normal.at(k2) * mc[k2]) / pl.normal.at(k0);
+    pl.center = {mc[0], mc[1], mc[2]};
+    pl.d = -dot(pl.normal, pl.center);
+}
+
+// symmetric 3x3 eigen-decomposition (cyclic Jacobi), eigenvalues descending, V columns
+void sym_eigen3(const double Ain[9], double ev[3], double V[9]) {
+    double A[9];
+    memcpy(A, Ain, sizeof A);
+    for (int i = 0; i < 9; ++i) V[i] = (i % 4 == 0) ? 1.0 : 0.0;
+    static const int PQ[3][2] = {{0, 1}, {0, 2}, {1, 2}};
+    for (int sweep = 0; sweep < 32; ++sweep) {
+        if (A[1] * A[1] + A[2] * A[2] + A[5] * A[5] < 1e-300) break;
+        for (const auto& pq : PQ) {
+            const int p = pq[0], q = pq[1];
+            const double apq = A[p * 3 + q];
+            if (apq == 0.0) continue;
+            const double th = (A[q * 3 + q] - A[p * 3 + p]) / (2.0 * apq);
+            const double t = (th >= 0 ? 1.0 : -1.0) / (std::fabs(th) + std::sqrt(th * th + 1.0));
+            const double c = 1.0 / std::sqrt(t * t + 1.0), s = t * c;
+            for (int k = 0; k < 3; ++k) {
+                const double x = A[k * 3 + p], y = A[k * 3 + q];
+                A[k * 3 + p] = c * x - s * y;
+                A[k * 3 + q] = s * x + c * y;
+            }
+            for (int k = 0; k < 3; ++k) {
+                const double x = A[p * 3 + k], y = A[q * 3 + k];
+                A[p * 3 + k] = c * x - s * y;
+                A[q * 3 + k] = s * x + c * y;
+            }
+            for (int k = 0; k < 3; ++k) {
+                const double x = V[k * 3 + p], y = V[k * 3 + q];
+                V[k * 3 + p] = c * x - s * y;
+                V[k * 3 + q] = s * x + c * y;
+            }
+        }
+    }
+    int o[3] = {0, 1, 2};
+    const double dg[3] = {A[0], A[4], A[8]};
+    std::sort(o, o + 3, [&](int u, int v) { return dg[u] > dg[v] || (dg[u] == dg[v] && u < v); });
+    double W[9];
+    for (int j = 0; j < 3; ++j) {
+        ev[j] = dg[o[j]];
+        for (int k = 0; k < 3; ++k) W[k * 3 + j] = V[k * 3 + o[j]];
+    }
+    memcpy(V, W, sizeof W);
+}
+
+// calcElongationAndPpalDir + calcMainColor2 from the exact inlier statistics
+void descriptors(HPlane& pl) {
+    double mean[3], cov[9];
+    r360p::moments_mean_cov(pl.st, mean, cov);
+    double ev[3], V[9];
+    sym_eigen3(cov, ev, V);
+    pl.elongation = float(std::sqrt(ev[0] / ev[1]));
+    pl.ppal = {float(V[0]), float(V[3]), float(V[6])};
+    const double dn = (double)pl.st.n;
+    for (int k = 0; k < 3; ++k) pl.nrgb[k] = float(((double)pl.st.c[k] * 1.1641532182693481e-10) / dn);
+    pl.intensity = float((double)pl.st.c[3] / (3.0 * dn));
+}
+
+// MRPT dist3D_Segment_to_Segment2
+float seg_dist2(const P3& a0, const P3& a1, const P3& b0, const P3& b1) {
+    const float SMALL = 0.00000001f;
+    const P3 u = minus(a1, a0), v = minus(b1, b0), w = minus(a0, b0);
+    const float a = dot(u, u), b = dot(u, v), c = dot(v, v), d = dot(u, w), e = dot(v, w);
+    const float D = a * c - b * b;
+    float sN, sD = D, tN, tD = D;
+    if (D < SMALL) {
+        sN = 0.0f; sD = 1.0f; tN = e; tD = c;
+    } else {
+        sN = (b * e - c * d);
+        tN = (a * e - b * d);
+        if (sN < 0.0f) { sN = 0.0f; tN = e; tD = c; }
+        else if (sN > sD) { sN = sD; tN = e + b; tD = c; }
+    }
+    if (tN < 0.0f) {
+        tN = 0.0f;
+        if (-d < 0.0f) sN = 0.0f;
+        else if (-d > a) sN = sD;
+        else { sN = -d; sD = a; }
+    } else if (tN > tD) {
+        tN = tD;
+        if ((-d + b) < 0.0f) sN = 0;
+        else if ((-d + b) > a) sN = sD;
+        else { sN = (-d + b); sD = a; }
+    }
+    const float sc = (std::fabs(sN) < SMALL ? 0.0f : sN / sD);
+    const float tc = (std::fabs(tN) < SMALL ? 0.0f : tN / tD);
+    const P3 dp = {w.x + (sc * u.x) - (tc * v.x), w.y + (sc * u.y) - (tc * v.y), w.z + (sc * u.z) - (tc * v.z)};
+    return dot(dp, dp);
+}
+
+bool nearby(const HPlane& A, const HPlane& B, float thr) {
+    const float t2 = thr * thr;
+    if (norm2(minus(A.center, B.center)) < t2) return true;
+    for (size_t i = 1; i < A.hull.size(); i++)
+        if (norm2(minus(A.hull[i], B.center)) < t2) return true;
+    for (size_t j = 1; j < B.hull.size(); j++)
+        if (norm2(minus(A.center, B.hull[j])) < t2) return true;
+    for (size_t i = 1; i < A.hull.size(); i++)
+        for (size_t j = 1; j < B.hull.size(); j++)
+            if (norm2(minus(A.hull[i], B.hull[j])) < t2) return true;
+    for (size_t i = 1; i < A.hull.size(); i++)
+        for (size_t j = 1; j < B.hull.size(); j++)
+            if (seg_dist2(A.hull[i], A.hull[i - 1], B.hull[j], B.hull[j - 1]) < t2) return true;
+    return false;
+}
+
+bool same_plane(const HPlane& A, const HPlane& B, float cos_angle, float dist, float prox) {
+    if (dot(A.normal, B.normal) < cos_angle) return false;
+    if (std::fabs(dot(A.normal, minus(B.center, A.center))) > dist) return false;
+    return nearby(A, B, prox);
+}
+
+// mergePlane2
+void merge_into(HPlane& A, const HPlane& B) {
+    const P3 n = {A.area * A.normal.x + B.area * B.normal.x, A.area * A.normal.y + B.area * B.normal.y,
+                  A.area * A.normal.z + B.area * B.normal.z};
+    const float len = std::sqrt(dot(n, n));
+    A.normal = {n.x / len, n.y / len, n.z / len};
+    std::vector<P3> pts(A.hull);
+    pts.insert(pts.end(), B.hull.begin(), B.hull.end());
+    convex_hull(A, pts);
+    r360p::moments_merge(A.st, B.st);
+    area_and_center(A);
+    A.d = -dot(A.normal, A.center);
+    descriptors(A);
+}
+
+// pcl::VoxelGrid (leaf 0.05): centroids of the occupied voxels in increasing voxel index.  Voxel
+// sums are exact in double (see plane_math.h), so the arrival order of the points is irrelevant.
+std::vector<P3> voxel_centroids(const std::vector<P3>& pts) {
+    std::vector<P3> out;
+    if (pts.empty()) return out;
+    const float inv = 1.0f / 0.05f;
+    P3 lo = pts[0], hi = pts[0];
+    for (const P3& p : pts) {
+        lo = {std::min(lo.x, p.x), std::min(lo.y, p.y), std::min(lo.z, p.z)};
+        hi = {std::max(hi.x, p.x), std::max(hi.y, p.y), std::max(hi.z, p.z)};
+    }
+    const long long b0 = (long long)std::floor(lo.x * inv), b1 = (long long)std::floor(lo.y * inv),
+                    b2 = (long long)std::floor(lo.z * inv);
+    const long long d0 = (long long)std::floor(hi.x * inv) - b0 + 1, d1 = (long long)std::floor(hi.y * inv) - b1 + 1;
+    std::vector<std::pair<long long, int>> key(pts.size());
+    for (size_t i = 0; i < pts.size(); ++i) {
+        const P3& p = pts[i];
+        key[i] = {((long long)std::floor(p.x * inv) - b0) + ((long long)std::floor(p.y * inv) - b1) * d0 +
+                      ((long long)std::floor(p.z * inv) - b2) * d0 * d1,
+                  int(i)};
+    }
+    std::sort(key.begin(), key.end());
+    for (size_t i = 0; i < key.size();) {
+        size_t j = i;
+        double s0 = 0, s1 = 0, s2 = 0;
+        for (; j < key.size() && key[j].first == key[i].first; ++j) {
+            const P3& p = pts[key[j].second];
+            s0 += p.x; s1 += p.y; s2 += p.z;
+        }
+        const double c = double(j - i);
+        out.push_back({float(s0 / c), float(s1 / c), float(s2 / c)});
+        i = j;
+    }
+    return out;
+}
+
+const float kMaxCurvature = 0.0013f;   // include/Miscellaneous.h:54
+const float kMinArea = 0.12f;          // :57
+const float kMaxElongation = 6.0f;     // :60
+
+bool hulls_touch(const HPlane& A, const HPlane& B, float max_dist, float max_normal_off) {
+    // the vertex/vertex then segment/segment tests of groupPlanes (:774-808) and mergePlanes (:671-703)
+    for (size_t i = 1; i < A.hull.size(); i++)
+        for (size_t ii = 1; ii < B.hull.size(); ii++) {
+            const P3 diff = minus(A.hull[i], B.hull[ii]);
+            if (std::sqrt(norm2(diff)) < max_dist && std::fabs(dot(A.normal, diff)) < max_normal_off) return true;
+        }
+    for (size_t i = 1; i < A.hull.size(); i++)
+        for (size_t ii = 1; ii < B.hull.size(); ii++) {
+            const float dist = std::sqrt(seg_dist2(A.hull[i], A.hull[i - 1], B.hull[ii], B.hull[ii - 1]));
+            if (dist < max_dist) {
+                const P3 diff = minus(A.hull[i], B.hull[ii]);
+                if (std::fabs(dot(A.normal, diff)) < max_normal_off) return true;
+            }
+        }
+    return false;
+}
+
+}  // namespace
+
+struct PbMapHost {
+    std::vector<HPlane> planes;
+};
+
+// ------------------------------------------------------------------ buffers
+int plane_bufs_alloc(r360_frame* f) {
+    PlaneBufs& P = f->pl;
+    if (P.cloud) return 0;
+    P.w = f->cols / 2;
+    P.h = f->rows / 2;
+    const long N = (long)P.w * P.h, T = 8 * N;
+    const long sw = (P.w - 1) / 10 + 5, sh = (P.h - 1) / 10 + 5;
+    P.sd_max = 208;
+    P.grid_cells = sw * sh * P.sd_max;
+    R360_HIP(hipMalloc(&P.cloud, sizeof(float4) * T));
+    R360_HIP(hipMalloc(&P.rgb, sizeof(uchar4) * T));
+    R360_HIP(hipMalloc(&P.nrm, sizeof(float4) * T));
+    R360_HIP(hipMalloc(&P.dist0, sizeof(float) * T));
+    R360_HIP(hipMalloc(&P.dist, sizeof(float) * T));
+    R360_HIP(hipMalloc(&P.grids, sizeof(float2) * 16 * P.grid_cells));
+    R360_HIP(hipMalloc(&P.parent, sizeof(int) * T));
+    R360_HIP(hipMalloc(&P.root, sizeof(int) * T));
+    R360_HIP(hipMalloc(&P.lab, sizeof(int) * T));
+    R360_HIP(hipMalloc(&P.labf, sizeof(int) * T));
+    R360_HIP(hipMalloc(&P.cnt, sizeof(int) * T));
+    R360_HIP(hipMalloc(&P.nlab, sizeof(int) * 8));
+    R360_HIP(hipMalloc(&P.big, sizeof(int) * 8 * R360_MAX_BIG));
+    R360_HIP(hipMalloc(&P.nbig, sizeof(int) * 8));
+    R360_HIP(hipMalloc(&P.mom, sizeof(r360p::Moments) * 8 * R360_MAX_BIG));
+    R360_HIP(hipMalloc(&P.models, sizeof(PlaneModel) * 8 * R360_MAX_MODELS));
+    R360_HIP(hipMalloc(&P.nmodels, sizeof(int) * 8));
+    R360_HIP(hipMalloc(&P.state, T));
+    R360_HIP(hipMalloc(&P.mask, sizeof(unsigned long long) * T));
+    R360_HIP(hipMalloc(&P.out, sizeof(PlaneOut) * 8 * R360_MAX_MODELS));
+    P.contour_cap = 2 * T;
+    P.vox_cap = T;
+    R360_HIP(hipMalloc(&P.contour, sizeof(float4) * P.contour_cap));
+    R360_HIP(hipMalloc(&P.vox, sizeof(float4) * P.vox_cap));
+    R360_HIP(hipMalloc(&P.totals, sizeof(long) * 2));
+    R360_HIP(hipMalloc(&P.err, sizeof(int)));
+    R360_HIP(hipHostMalloc(&P.h_out, sizeof(PlaneOut) * 8 * R360_MAX_MODELS));
+    R360_HIP(hipHostMalloc(&P.h_nmodels, sizeof(int) * 16));
+    return 0;
+}
+
+void plane_bufs_free(r360_frame* f) {
+    PlaneBufs& P = f->pl;
+    void* dev[] = {P.cloud, P.rgb, P.nrm, P.dist0, P.dist, P.grids, P.parent, P.root, P.lab, P.labf, P.cnt, P.nlab,
+                   P.big, P.nbig, P.mom, P.models, P.nmodels, P.state, P.mask, P.out, P.contour, P.vox, P.totals, P.err};
+    for (void* p : dev) hipFree(p);
+    hipHostFree(P.h_out);
+    hipHostFree(P.h_nmodels);
+    P = PlaneBufs();
+    delete f->pbmap;
+    f->pbmap = nullptr;
+}
+
+// GPU part of getPlanes (enqueued on the ctx stream): cloud, filter, normals, segmentation
+int planes_enqueue(r360_frame* f) {
+    if (plane_bufs_alloc(f)) return -1;
+    PlaneBufs& P = f->pl;
+    R360_HIP(hipMemsetAsync(P.err, 0, sizeof(int), f->ctx->stream));
+    if (launch_cloud_normals(f)) return -1;
+    if (launch_segmentation(f)) return -1;
+    R360_HIP(hipMemcpyAsync(P.h_out, P.out, sizeof(PlaneOut) * 8 * R360_MAX_MODELS, hipMemcpyDeviceToHost,
+                            f->ctx->stream));
+    R360_HIP(hipMemcpyAsync(P.h_nmodels, P.nmodels, sizeof(int) * 8, hipMemcpyDeviceToHost, f->ctx->stream));
+    R360_HIP(hipMemcpyAsync(P.h_nmodels + 8, P.err, sizeof(int), hipMemcpyDeviceToHost, f->ctx->stream));
+    R360_HIP(hipMemcpyAsync(P.h_nmodels + 10, P.totals, sizeof(long) * 2, hipMemcpyDeviceToHost, f->ctx->stream));
+    delete f->pbmap;
+    f->pbmap = nullptr;
+    return 0;
+}
+
+// Host part of getPlanes: waits for the stream, then builds the PbMap (A8 + A9)
+int planes_finish(r360_frame* f) {
+    if (f->pbmap) return 0;
+    PlaneBufs& P = f->pl;
+    if (!P.cloud) { r360_set_error("planes were not built (R360_BUILD_PLANES)"); return -2; }
+    hipStream_t st = f->ctx->stream;
+    R360_HIP(hipStreamSynchronize(st));
+    const int err = P.h_nmodels[8];
+    if (err) {
+        r360_set_error("plane segmentation capacity exceeded (code %d: 1 bilateral depth range, 2 labels, 4 models, "
+                       "8 contour length, 16 pools)", err);
+        return -1;
+    }
+    const long* totals = reinterpret_cast<const long*>(P.h_nmodels + 10);
+    std::vector<float4> contour(totals[0]), vox(totals[1]);
+    if (totals[0]) R360_HIP(hipMemcpyAsync(contour.data(), P.contour, sizeof(float4) * totals[0], hipMemcpyDeviceToHost, st));
+    if (totals[1]) R360_HIP(hipMemcpyAsync(vox.data(), P.vox, sizeof(float4) * totals[1], hipMemcpyDeviceToHost, st));
+    R360_HIP(hipStreamSynchronize(st));
+    const r360_calib* cal = f->calib;
+    std::vector<std::vector<HPlane>> local(8);
+    for (int s = 0; s < 8; ++s) {
+        const float* Rt = cal->rt[s];
+        for (int m = 0; m < P.h_nmodels[s]; ++m) {
+            const PlaneOut& O = P.h_out[s * R360_MAX_MODELS + m];
+            HPlane pl;
+            pl.sensor = s;
+            pl.center = {O.model.centroid[0], O.model.centroid[1], O.model.centroid[2]};
+            pl.normal = {O.model.v[0], O.model.v[1], O.model.v[2]};
+            if (dot(pl.normal, pl.center) > 0) pl.normal = {-pl.normal.x, -pl.normal.y, -pl.normal.z};  // :988-992
+            pl.curvature = O.model.curvature;
+            pl.st = O.stats;
+            std::vector<P3> pts;
+            if (O.n_contour > 0) {
+                for (int k = 0; k < O.n_contour; ++k) {
+                    const float4 q = contour[O.contour_off + k];
+                    pts.push_back({q.x, q.y, q.z});
+                }
+            } else {                                                    // "HULL 000" (:1017-1026)
+                std::vector<P3> inl;
+                for (int k = 0; k < O.n_vox; ++k) {
+                    const float4 q = vox[O.vox_off + k];
+                    inl.push_back({q.x, q.y, q.z});
+                }
+                pts = voxel_centroids(inl);
+            }
+            convex_hull(pl, pts);
+            area_and_center(pl);
+            if (pl.area < kMinArea) continue;                           // :1034
+            pl.d = -dot(pl.normal, pl.center);                          // :1037
+            descriptors(pl);
+            if (pl.elongation > kMaxElongation) continue;               // :1041
+            pl.normal = linear(Rt, pl.normal);                          // transform(Rt) :1051
+            pl.center = affine(Rt, pl.center);
+            pl.d = -dot(pl.normal, pl.center);
+            for (P3& v : pl.hull) v = affine(Rt, v);
+            bool merged = false;
+            if (pl.curvature < kMaxCurvature)
+                for (HPlane& q : local[s])
+                    if (q.curvature < kMaxCurvature && same_plane(q, pl, 0.99f, 0.05f, 0.2f)) {
+                        merge_into(q, pl);
+                        merged = true;
+                        break;
+                    }
+            if (!merged) {
+                pl.id = int(local[s].size());
+                local[s].push_back(pl);
+            }
+        }
+    }
+    // groupPlanes (:742-832)
+    auto* pm = new PbMapHost;
+    std::vector<HPlane>& G = pm->planes;
+    G = local[0];
+    std::set<unsigned> first, prev;
+    for (const HPlane& p : G) first.insert(unsigned(p.id));
+    prev = first;
+    for (int s = 1; s < 8; ++s) {
+        std::set<unsigned> next;
+        for (HPlane& L : local[s]) {
+            bool same = false;
+            size_t j = 0;
+            if (L.area > 0.5f || L.curvature < kMaxCurvature)
+                for (auto it = prev.begin(); it != prev.end() && !same; ++it) {
+                    j = *it;
+                    if (G[j].area < 0.5f || G[j].curvature > kMaxCurvature) continue;
+                    if (std::fabs(G[j].d - L.d) < 0.45f && dot(G[j].normal, L.normal) > 0.99f)
+                        same = hulls_touch(G[j], L, 0.5f, 0.09f);
+                }
+            if (same) {
+                next.insert(unsigned(G[j].id));
+                merge_into(G[j], L);
+            } else {
+                next.insert(unsigned(G.size()));
+                L.id = int(G.size());
+                G.push_back(L);
+            }
+        }
+        prev = next;
+        if (s == 6) prev.insert(first.begin(), first.end());
+    }
+    // mergePlanes (:657-739)
+    for (size_t j = 0; j < G.size(); j++) {
+        if (!(G[j].curvature < kMaxCurvature)) continue;
+        for (size_t k = j + 1; k < G.size(); k++) {
+            if (!(G[k].curvature < kMaxCurvature)) continue;
+            bool same = false;
+            if (dot(G[j].normal, G[k].normal) > 0.99f && std::fabs(G[j].d - G[k].d) < 0.45f)
+                same = hulls_touch(G[j], G[k], 0.3f, 0.06f);
+            if (same) {
+                merge_into(G[j], G[k]);
+                for (size_t hh = k + 1; hh < G.size(); hh++) --G[hh].id;
+                G.erase(G.begin() + long(k));
+                j--;
+                break;
+            }
+        }
+    }
+    f->pbmap = pm;
+    return 0;
+}
+
+// ------------------------------------------------------------------ RegisterRGBD360
+namespace {
+
+// setReference / setTarget (RegisterRGBD360.h:111-196); labels are never set on this path
+std::vector<int> subgraph(const std::vector<HPlane>& P, size_t max_match_planes) {
+    std::vector<int> ids;
+    if (max_match_planes > 0 && P.size() > max_match_planes) {
+        std::vector<float> areas(P.size(), 0.f);
+        for (size_t i = 0; i < P.size(); i++)
+            if (P[i].curvature < kMaxCurvature) areas[i] = P[i].area;
+        std::vector<float> sorted(areas);
+        std::sort(sorted.begin(), sorted.end());
+        const float thr = sorted[P.size() - max_match_planes - 1];
+        for (size_t i = 0; i < P.size(); i++)
+            if (areas[i] > thr) ids.push_back(P[i].id);
+    } else {
+        for (size_t i = 0; i < P.size(); i++)
+            if (P[i].curvature < kMaxCurvature) ids.push_back(P[i].id);
+    }
+    std::sort(ids.begin(), ids.end());
+    return ids;
+}
+
+void pack_desc(const HPlane& p, float* d) {
+    const float v[16] = {p.normal.x, p.normal.y, p.normal.z, p.center.x, p.center.y, p.center.z, p.d, p.area,
+                         p.elongation, p.nrgb[0], p.nrgb[1], p.nrgb[2], p.intensity, 0, 0, 0};
+    memcpy(d, v, sizeof v);
+}
+
+struct Tables {
+    int ns = 0, nt = 0, words = 0;
+    const uint8_t* unary = nullptr;
+    const unsigned long long* bin = nullptr;
+    bool pair_ok(int i, int j, int k, int l) const {
+        const int bit = k * nt + l;
+        return (bin[(size_t)(i * nt + j) * words + bit / 64] >> (bit % 64)) & 1;
+    }
+};
+
+int gpu_tables(r360_ctx* ctx, const std::vector<HPlane>& S, const std::vector<int>& si, const std::vector<HPlane>& T,
+               const std::vector<int>& ti, int mode, Tables& tb) {
+    const int ns = int(si.size()), nt = int(ti.size());
+    const int cap = std::max(ns, nt);
+    if (cap > ctx->match_cap) {
+        hipFree(ctx->d_match_desc); hipFree(ctx->d_unary); hipFree(ctx->d_bin);
+        hipHostFree(ctx->h_unary); hipHostFree(ctx->h_bin);
+        ctx->match_cap = std::max(cap, 32);
+        const size_t c = ctx->match_cap, np = c * c, words = (np + 63) / 64;
+        R360_HIP(hipMalloc(&ctx->d_match_desc, sizeof(float) * 16 * 2 * c));
+        R360_HIP(hipMalloc(&ctx->d_unary, np));
+        R360_HIP(hipMalloc(&ctx->d_bin, sizeof(unsigned long long) * np * words));
+        R360_HIP(hipHostMalloc(&ctx->h_unary, np));
+        R360_HIP(hipHostMalloc(&ctx->h_bin, sizeof(unsigned long long) * np * words));
+    }
+    tb.ns = ns; tb.nt = nt;
+    tb.words = (ns * nt + 63) / 64;
+    tb.unary = ctx->h_unary;
+    tb.bin = ctx->h_bin;
+    if (ns == 0 || nt == 0) return 0;
+    std::vector<float> desc(16 * (size_t)(ns + nt));
+    for (int i = 0; i < ns; ++i) pack_desc(S[si[i]], &desc[16 * i]);
+    for (int j = 0; j < nt; ++j) pack_desc(T[ti[j]], &desc[16 * (ns + j)]);
+    hipStream_t st = ctx->stream;
+    R360_HIP(hipMemcpyAsync(ctx->d_match_desc, desc.data(), sizeof(float) * desc.size(), hipMemcpyHostToDevice, st));
+    if (launch_match_tables(ctx, ctx->d_match_desc, ns, nt, mode, ctx->d_unary, ctx->d_bin, tb.words)) return -1;
+    R360_HIP(hipMemcpyAsync(ctx->h_unary, ctx->d_unary, (size_t)ns * nt, hipMemcpyDeviceToHost, st));
+    R360_HIP(hipMemcpyAsync(ctx->h_bin, ctx->d_bin, sizeof(unsigned long long) * (size_t)ns * nt * tb.words,
+                            hipMemcpyDeviceToHost, st));
+    R360_HIP(hipStreamSynchronize(st));
+    return 0;
+}
+
+// interpretation tree: depth-first over reference planes; largest consistent set, ties by matched
+// reference area; deterministic node budget
+struct Tree {
+    const Tables* tb = nullptr;
+    std::vector<double> area, rest;
+    std::vector<int> cur, best;
+    int n_cur = 0, n_best = 0;
+    double a_cur = 0, a_best = 0;
+    long nodes = 0, budget = 4000000;
+    void go(int i) {
+        if (++nodes > budget) return;
+        if (i == tb->ns) {
+            if (n_cur > n_best || (n_cur == n_best && a_cur > a_best)) { best = cur; n_best = n_cur; a_best = a_cur; }
+            return;
+        }
+        const int left = tb->ns - i;
+        if (n_cur + left < n_best) return;
+        if (n_cur + left == n_best && a_cur + rest[i] <= a_best) return;
+        for (int t = 0; t < tb->nt; ++t) {
+            if (!tb->unary[(size_t)i * tb->nt + t]) continue;
+            bool ok = true;
+            for (int k = 0; k < i && ok; ++k)
+                if (cur[k] >= 0) ok = cur[k] != t && tb->pair_ok(i, t, k, cur[k]);
+            if (!ok) continue;
+            cur[i] = t; ++n_cur; a_cur += area[i];
+            go(i + 1);
+            cur[i] = -1; --n_cur; a_cur -= area[i];
+        }
+        go(i + 1);
+    }
+};
+
+double det33(const double A[9]) {
+    return A[0] * (A[4] * A[8] - A[5] * A[7]) - A[1] * (A[3] * A[8] - A[5] * A[6]) + A[2] * (A[3] * A[7] - A[4] * A[6]);
+}
+
+// ConsistencyTest::estimatePoseWithCovariance: Kabsch on area-weighted normals, plane-offset least
+// squares for t, information blockdiag(sum w n n^T, sum w (I - n n^T)); false when ill-conditioned
+bool estimate_pose(const std::vector<HPlane>& R, const std::vector<HPlane>& T, const std::map<unsigned, unsigned>& m,
+                   float pose[16], float info[36]) {
+    if (m.size() < 3) return false;
+    double M[9] = {0}, Ht[9] = {0}, Hr[9] = {0}, g[3] = {0};
+    for (const auto& kv : m) {
+        const HPlane& r = R[kv.first];
+        const HPlane& t = T[kv.second];
+        const double w = t.area;
+        const double nr[3] = {r.normal.x, r.normal.y, r.normal.z}, nt[3] = {t.normal.x, t.normal.y, t.normal.z};
+        for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 3; ++b) {
+                M[a * 3 + b] += w * nt[a] * nr[b];
+                Ht[a * 3 + b] += w * nr[a] * nr[b];
+                Hr[a * 3 + b] += w * ((a == b ? 1.0 : 0.0) - nr[a] * nr[b]);
+            }
+        const double e = double(t.d) - double(r.d);
+        for (int a = 0; a < 3; ++a) g[a] += w * nr[a] * e;
+    }
+    double MtM[9];
+    for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b) {
+            double s = 0;
+            for (int k = 0; k < 3; ++k) s += M[k * 3 + a] * M[k * 3 + b];
+            MtM[a * 3 + b] = s;
+        }
+    double lam[3], V[9], U[9], sig[3];
+    sym_eigen3(MtM, lam, V);
+    for (int k = 0; k < 3; ++k) sig[k] = std::sqrt(std::max(0.0, lam[k]));
+    if (!(sig[1] > 1e-6 * sig[0])) return false;
+    for (int k = 0; k < 2; ++k)
+        for (int a = 0; a < 3; ++a) {
+            double s = 0;
+            for (int b = 0; b < 3; ++b) s += M[a * 3 + b] * V[b * 3 + k];
+            U[a * 3 + k] = s / sig[k];
+        }
+    U[2] = U[3] * U[7] - U[6] * U[4];
+    U[5] = U[6] * U[1] - U[0] * U[7];
+    U[8] = U[0] * U[4] - U[3] * U[1];
+    double Rm[9];
+    for (int pass = 0; pass < 2; ++pass) {
+        for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 3; ++b) {
+                double s = 0;
+                for (int k = 0; k < 3; ++k) s += V[a * 3 + k] * U[b * 3 + k];
+                Rm[a * 3 + b] = s;
+            }
+        if (det33(Rm) > 0) break;
+        for (int a = 0; a < 3; ++a) V[a * 3 + 2] = -V[a * 3 + 2];
+    }
+    double lt[3], Vt[9];
+    sym_eigen3(Ht, lt, Vt);
+    if (!(lt[2] > 0) || lt[0] / lt[2] > 8000.0) return false;   // threshold_conditioning (Miscellaneous.h:76)
+    double t[3] = {0, 0, 0};
+    for (int k = 0; k < 3; ++k) {
+        double proj = 0;
+        for (int a = 0; a < 3; ++a) proj += Vt[a * 3 + k] * g[a];
+        for (int a = 0; a < 3; ++a) t[a] += Vt[a * 3 + k] * proj / lt[k];
+    }
+    for (int i = 0; i < 16; ++i) pose[i] = (i % 5 == 0) ? 1.f : 0.f;
+    for (int a = 0; a < 3; ++a) {
+        for (int b = 0; b < 3; ++b) pose[b * 4 + a] = float(Rm[a * 3 + b]);
+        pose[12 + a] = float(t[a]);
+    }
+    for (int i = 0; i < 36; ++i) info[i] = 0.f;
+    for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b) {
+            info[b * 6 + a] = float(Ht[a * 3 + b]);
+            info[(b + 3) * 6 + (a + 3)] = float(Hr[a * 3 + b]);
+        }
+    return true;
+}
+
+int ready(r360_frame* f) {
+    if (!f) { r360_set_error("null frame"); return -2; }
+    if (!(f->built & R360_BUILD_PLANES)) { r360_set_error("frame planes not built (R360_BUILD_PLANES)"); return -2; }
+    return planes_finish(f);
+}
+
+}  // namespace
+
+extern "C" int r360_frame_get_planes(r360_frame* f, r360_plane* out, int cap, int* n) {
+    if (int rc = ready(f)) return rc;
+    const auto& P = f->pbmap->planes;
+    if (n) *n = int(P.size());
+    for (int i = 0; i < int(P.size()) && i < cap && out; ++i) {
+        const HPlane& p = P[i];
+        r360_plane& o = out[i];
+        const P3* src[3] = {&p.normal, &p.center, &p.ppal};
+        float* dst[3] = {o.normal, o.center, o.ppal};
+        for (int k = 0; k < 3; ++k) { dst[k][0] = src[k]->x; dst[k][1] = src[k]->y; dst[k][2] = src[k]->z; }
+        o.d = p.d; o.area = p.area; o.elongation = p.elongation; o.curvature = p.curvature;
+        for (int k = 0; k < 3; ++k) o.nrgb[k] = p.nrgb[k];
+        o.intensity = p.intensity;
+        o.id = p.id; o.sensor = p.sensor; o.n_inliers = int(p.st.n); o.n_hull = int(p.hull.size());
+    }
+    return 0;
+}
+
+extern "C" int r360_frame_get_plane_hull(r360_frame* f, int i, float* xyz, int cap, int* n) {
+    if (int rc = ready(f)) return rc;
+    const auto& P = f->pbmap->planes;
+    CHECK_ARG(i >= 0 && i < int(P.size()), "plane index out of range");
+    const auto& H = P[i].hull;
+    if (n) *n = int(H.size());
+    for (int k = 0; k < int(H.size()) && k < cap && xyz; ++k) {
+        xyz[3 * k] = H[k].x; xyz[3 * k + 1] = H[k].y; xyz[3 * k + 2] = H[k].z;
+    }
+    return 0;
+}
+
+extern "C" int r360_pbmap_match_tables(r360_ctx* ctx, r360_frame* ref, r360_frame* trg, size_t max_match_planes,
+                                       int mode, int* ns, int* nt, int* sid, int* tid, uint8_t* unary,
+                                       uint64_t* binary, int cap) {
+    CHECK_ARG(ctx && ns && nt, "null arg");
+    if (int rc = ready(ref)) return rc;
+    if (int rc = ready(trg)) return rc;
+    const auto& S = ref->pbmap->planes;
+    const auto& T = trg->pbmap->planes;
+    const std::vector<int> si = subgraph(S, max_match_planes), ti = subgraph(T, max_match_planes);
+    *ns = int(si.size());
+    *nt = int(ti.size());
+    CHECK_ARG(*ns <= cap && *nt <= cap, "subgraph larger than cap");
+    Tables tb;
+    if (gpu_tables(ctx, S, si, T, ti, mode, tb)) return -1;
+    for (int i = 0; i < *ns; ++i) if (sid) sid[i] = si[i];
+    for (int j = 0; j < *nt; ++j) if (tid) tid[j] = ti[j];
+    if (unary) memcpy(unary, tb.unary, (size_t)*ns * *nt);
+    if (binary) memcpy(binary, tb.bin, sizeof(uint64_t) * (size_t)*ns * *nt * tb.words);
+    return tb.words;
+}
+
+extern "C" int r360_register_pbmap(r360_ctx* ctx, r360_frame* ref, r360_frame* trg, size_t max_match_planes, int mode,
+                                   float pose[16], float info[36], int* match_pairs, int pair_cap, int* n_match,
+                                   float* area_matched, float* area_src, float* area_trg) {
+    CHECK_ARG(ctx && pose && info, "null arg");
+    CHECK_ARG(mode >= 0 && mode <= 3, "registrationType must be 0..3");
+    if (int rc = ready(ref)) return rc;
+    if (int rc = ready(trg)) return rc;
+    const auto& S = ref->pbmap->planes;
+    const auto& T = trg->pbmap->planes;
+    const std::vector<int> si = subgraph(S, max_match_planes), ti = subgraph(T, max_match_planes);
+    Tables tb;
+    if (gpu_tables(ctx, S, si, T, ti, mode, tb)) return -1;
+    Tree tr;
+    tr.tb = &tb;
+    tr.area.resize(si.size());
+    tr.rest.assign(si.size() + 1, 0.0);
+    for (size_t i = 0; i < si.size(); ++i) tr.area[i] = S[si[i]].area;
+    for (int i = int(si.size()) - 1; i >= 0; --i) tr.rest[i] = tr.rest[i + 1] + tr.area[i];
+    tr.cur.assign(si.size(), -1);
+    tr.best.assign(si.size(), -1);
+    tr.go(0);
+    std::map<unsigned, unsigned> best;
+    for (size_t i = 0; i < si.size(); ++i)
+        if (tr.best[i] >= 0) best[unsigned(si[i])] = unsigned(ti[tr.best[i]]);
+    int k = 0;
+    float am = 0.f;
+    for (const auto& kv : best) {
+        if (match_pairs && k < pair_cap) { match_pairs[2 * k] = int(kv.first); match_pairs[2 * k + 1] = int(kv.second); }
+        ++k;
+        am += S[kv.first].area;                     // calcAreaMatched
+    }
+    if (n_match) *n_match = int(best.size());
+    if (area_matched) *area_matched = am;
+    if (best.size() < 3) return 0;                  // "Insuficient matching" (:306-310); pose untouched
+    float p[16], inf[36];
+    if (!estimate_pose(S, T, best, p, inf)) return 0;
+    memcpy(pose, p, sizeof p);
+    memcpy(info, inf, sizeof inf);
+    float as = 0.f, at = 0.f;                       // :323-334
+    for (int id : si) as += S[id].area;
+    for (int id : ti) at += T[id].area;
+    if (area_src) *area_src = as;
+    if (area_trg) *area_trg = at;
+    return 1;
+}
+
+// Register(): PbMap registration, then the dense refinement initialised with the rotOffset-conjugated
+// PbMap pose (OdometryKeyFrame360.cpp:167-171, 205, 244-254).  guess = fallback initial pose in the rig
+// frame when the PbMap registration fails (the caller's previous relative pose).
+extern "C" int r360_register(r360_ctx* ctx, r360_frame* ref, r360_frame* trg, const float guess[16],
+                             const r360_icp_params* p, size_t max_match_planes, int mode, float pose[16],
+                             float info[36], r360_icp_stats* st) {
+    CHECK_ARG(ctx && ref && trg && pose, "null arg");
+    float pb[16], inf[36];
+    for (int i = 0; i < 16; ++i) pb[i] = guess ? guess[i] : ((i % 5 == 0) ? 1.f : 0.f);
+    for (int i = 0; i < 36; ++i) inf[i] = 0.f;
+    const int good = r360_register_pbmap(ctx, ref, trg, max_match_planes, mode, pb, inf, nullptr, 0, nullptr, nullptr,
+                                         nullptr, nullptr);
+    if (good < 0) return good;
+    // rotOffset: rotation of angleOffset = 157.5 deg about x (OdometryRGBD360.cpp:138-139)
+    const float a = 157.5f;
+    const float c = (float)cos(a * R360_PI / 180), s = (float)sin(a * R360_PI / 180);
+    const float Ro[16] = {1, 0, 0, 0, 0, c, -s, 0, 0, s, c, 0, 0, 0, 0, 1};       // col-major: (1,2)=s, (2,1)=-s
+    const float Ri[16] = {1, 0, 0, 0, 0, c, s, 0, 0, -s, c, 0, 0, 0, 0, 1};       // its inverse (transpose)
+    auto mul = [](const float* A, const float* B, float* C) {
+        for (int col = 0; col < 4; ++col)
+            for (int r = 0; r < 4; ++r) {
+                float acc = A[r] * B[col * 4];
+                for (int k = 1; k < 4; ++k) acc += A[k * 4 + r] * B[col * 4 + k];
+                C[col * 4 + r] = acc;
+            }
+    };
+    float t1[16], init[16], dense[16], t2[16];
+    mul(Ro, pb, t1);
+    mul(t1, Ri, init);                              // rotOffset * pose * rotOffset^-1
+    float H[36], g[6];
+    const int rc = r360_align360(ctx, ref, trg, init, R360_PHOTO_DEPTH, 0, p, dense, H, g, st);
+    if (rc < 0) return rc;
+    mul(Ri, dense, t2);
+    mul(t2, Ro, pose);                              // rotOffset^-1 * dense * rotOffset
+    if (info) memcpy(info, inf, sizeof inf);
+    return good ? 0 : 1;
+}
+
+// ------------------------------------------------------------------ inspection (parity tests)
+extern "C" int r360_frame_get_cloud(r360_frame* f, float* xyz4, uint8_t* rgb4, float* nrm4, float* dist) {
+    CHECK_ARG(f && (f->built & R360_BUILD_CLOUD), "frame cloud not built (R360_BUILD_CLOUD)");
+    PlaneBufs& P = f->pl;
+    const size_t T = 8 * (size_t)P.w * P.h;
+    hipStream_t st = f->ctx->stream;
+    if (xyz4) R360_HIP(hipMemcpyAsync(xyz4, P.cloud, sizeof(float4) * T, hipMemcpyDeviceToHost, st));
+    if (rgb4) R360_HIP(hipMemcpyAsync(rgb4, P.rgb, sizeof(uchar4) * T, hipMemcpyDeviceToHost, st));
+    if (nrm4) R360_HIP(hipMemcpyAsync(nrm4, P.nrm, sizeof(float4) * T, hipMemcpyDeviceToHost, st));
+    if (dist) R360_HIP(hipMemcpyAsync(dist, P.dist, sizeof(float) * T, hipMemcpyDeviceToHost, st));
+    R360_HIP(hipStreamSynchronize(st));
+    return 0;
+}
+
+extern "C" int r360_frame_get_labels(r360_frame* f, int* lab, int* labf) {
+    CHECK_ARG(f && (f->built & R360_BUILD_PLANES), "frame planes not built (R360_BUILD_PLANES)");
+    PlaneBufs& P = f->pl;
+    const size_t T = 8 * (size_t)P.w * P.h;
+    hipStream_t st = f->ctx->stream;
+    if (lab) R360_HIP(hipMemcpyAsync(lab, P.lab, sizeof(int) * T, hipMemcpyDeviceToHost, st));
+    if (labf) R360_HIP(hipMemcpyAsync(labf, P.labf, sizeof(int) * T, hipMemcpyDeviceToHost, st));
+    R360_HIP(hipStreamSynchronize(st));
+    return 0;
+}
+
+extern "C" int r360_frame_get_regions(r360_frame* f, int sensor, r360_region* out, int cap, int* n) {
+    if (int rc = ready(f)) return rc;
+    CHECK_ARG(sensor >= 0 && sensor < 8, "sensor out of range");
+    PlaneBufs& P = f->pl;
+    const int nm = P.h_nmodels[sensor];
+    if (n) *n = nm;
+    for (int m = 0; m < nm && m < cap && out; ++m) {
+        const PlaneOut& O = P.h_out[sensor * R360_MAX_MODELS + m];
+        r360_region& r = out[m];
+        r.label = O.model.label;
+        r.count = (int)O.stats.n;
+        r.start_idx = O.start;
+        r.n_contour = O.n_contour;
+        r.n_fit = O.model.n_fit;
+        for (int k = 0; k < 3; ++k) r.centroid[k] = O.model.centroid[k];
+        for (int k = 0; k < 9; ++k) r.cov[k] = O.model.cov[k];
+        for (int k = 0; k < 4; ++k) r.model[k] = O.model.v[k];
+        r.curvature = O.model.curvature;
+    }
+    return 0;
+}

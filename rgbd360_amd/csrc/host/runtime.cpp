@@ -114,6 +114,8 @@ extern "C" void r360_ctx_destroy(r360_ctx* c) {
     hipFree(c->d_state);
     hipFree(c->d_partials);
     hipHostFree(c->h_state);
+    hipFree(c->d_match_desc); hipFree(c->d_unary); hipFree(c->d_bin);
+    hipHostFree(c->h_unary); hipHostFree(c->h_bin);
     hipStreamDestroy(c->stream);
     delete c;
 }
@@ -207,6 +209,8 @@ extern "C" int r360_calib_create(r360_ctx* ctx, int rows, int cols, r360_calib**
         for (int i = 0; i < 16; ++i) c->rt[k][i] = c->rt_inv[k][i] = (i % 5 == 0) ? 1.f : 0.f;
     R360_HIP(hipMalloc(&c->d_rt_inv, sizeof(float) * 128));
     R360_HIP(hipMemcpy(c->d_rt_inv, c->rt_inv, sizeof(float) * 128, hipMemcpyHostToDevice));
+    R360_HIP(hipMalloc(&c->d_rt, sizeof(float) * 128));
+    R360_HIP(hipMemcpy(c->d_rt, c->rt, sizeof(float) * 128, hipMemcpyHostToDevice));
     if (calib_build_tables(c)) { delete c; return -1; }
     *out = c;
     return 0;
@@ -215,6 +219,7 @@ extern "C" int r360_calib_create(r360_ctx* ctx, int rows, int cols, r360_calib**
 extern "C" void r360_calib_destroy(r360_calib* c) {
     if (!c) return;
     hipFree(c->d_rt_inv);
+    hipFree(c->d_rt);
     hipFree(c->d_st_sinphi); hipFree(c->d_st_cosphi); hipFree(c->d_st_sinth); hipFree(c->d_st_costh);
     for (int l = 0; l < R360_MAX_PYR; ++l) {
         hipFree(c->trig[l].sinphi); hipFree(c->trig[l].cosphi); hipFree(c->trig[l].sinth); hipFree(c->trig[l].costh);
@@ -230,6 +235,7 @@ extern "C" int r360_calib_set_extrinsics(r360_calib* c, const float* rt8) {
         inverse4(c->rt[k], c->rt_inv[k]);                       // Rt_inv = Rt_.inverse() (Calib360.h:129)
     }
     R360_HIP(hipMemcpy(c->d_rt_inv, c->rt_inv, sizeof(float) * 128, hipMemcpyHostToDevice));
+    R360_HIP(hipMemcpy(c->d_rt, c->rt, sizeof(float) * 128, hipMemcpyHostToDevice));
     return 0;
 }
 
@@ -354,6 +360,7 @@ extern "C" void r360_frame_destroy(r360_frame* f) {
     // outlive their context at interpreter shutdown.
     hipFree(f->d_bgr); hipFree(f->d_depth); hipFree(f->d_depth_m); hipFree(f->d_sph_bgr); hipFree(f->d_sph_depth);
     for (int l = 0; l < f->n_levels; ++l) { hipFree(f->lv[l].p0); hipFree(f->lv[l].tg); }
+    plane_bufs_free(f);
     delete f;
 }
 
@@ -401,8 +408,10 @@ extern "C" int r360_frame_build_async(r360_frame* f, unsigned flags) {
         f->built |= R360_BUILD_PYRAMID;
     }
     if (flags & (R360_BUILD_CLOUD | R360_BUILD_PLANES)) {
-        r360_set_error("R360_BUILD_CLOUD/PLANES: plane extraction is not built in this version");
-        return -3;
+        // buildSphereCloud + getPlanes (Frame360.h:467-510, 615-640): the per-pixel part is enqueued
+        // here; the per-plane PbMap assembly runs on the host when the planes are first needed
+        if (planes_enqueue(f)) return -1;
+        f->built |= R360_BUILD_CLOUD | R360_BUILD_PLANES;
     }
     return 0;
 }
@@ -410,6 +419,7 @@ extern "C" int r360_frame_build_async(r360_frame* f, unsigned flags) {
 extern "C" int r360_frame_build(r360_frame* f, unsigned flags) {
     int rc = r360_frame_build_async(f, flags);
     if (rc) return rc;
+    if (flags & R360_BUILD_PLANES) return planes_finish(f);
     R360_HIP(hipStreamSynchronize(f->ctx->stream));
     return 0;
 }

@@ -1,0 +1,646 @@
+// plane_seg.hip — OrganizedMultiPlaneSegmentation::segmentAndRefine on gfx950 and the
+// per-plane statistics the PbMap descriptors need (A8):
+//   k_ccl_*        4-connected components under PlaneCoefficientComparator (lock-free union-find,
+//                  roots = smallest raster index, labels numbered in raster order of their roots — the
+//                  reference's run-id compaction order)
+//   k_label_count  label sizes (wave-aggregated atomics);  k_big_list: labels with > 80 points, in order
+//   k_label_moments  exact moments per large label (one workgroup per label, int64/int128 sums)
+//   k_plane_fit    eigen33 plane fit, curvature test and the accumulating viewpoint of segment()
+//   k_refine       the two raster sweeps of refine(): one wave per sensor walks the rows; within a row
+//                  the left-to-right (right-to-left) label chains are resolved with wave scans over
+//                  per-lane chunk summaries; closeness to every model is precomputed per pixel as a
+//                  bit mask (k_refine_init)
+//   k_model_stats  final inlier moments (rig frame) + colour sums + the region's first pixel
+//   k_trace        findLabeledRegionBoundary (Moore-neighbour trace), one thread per region
+//   k_gather_vox   inlier points of regions without a contour (VoxelGrid fallback, Frame360.h:1017-1026)
+// Arithmetic follows oracle/src/planes_oracle.cpp and pbmap_oracle.cpp; see rgbd360_amd/csrc/plane_math.h.
+#include "../r360_internal.h"
+#include "../plane_math.h"
+
+namespace {
+
+__device__ __forceinline__ bool isfin(float v) { return __builtin_isfinite(v); }
+
+// ------------------------------------------------------------------ CCL
+__global__ void k_ccl_init(const float4* __restrict__ cloud, long total, int* __restrict__ parent) {
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x)
+        parent[i] = isfin(cloud[i].x) ? (int)i : -1;
+}
+
+__device__ __forceinline__ int ld(const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+__device__ int find_root(const int* parent, int x) {
+    int p = ld(parent + x);
+    while (p != x) {
+        x = p;
+        p = ld(parent + x);
+    }
+    return x;
+}
+
+__device__ void unite(int* parent, int a, int b) {
+    while (true) {
+        a = find_root(parent, a);
+        b = find_root(parent, b);
+        if (a == b) return;
+        if (a < b) { const int t = a; a = b; b = t; }
+        const int old = atomicCAS(parent + a, a, b);
+        if (old == a) return;
+        a = old;
+    }
+}
+
+// PlaneCoefficientComparator::compare(a, b), depth dependent (threshold 0.02 * z_a^2)
+__device__ __forceinline__ bool plane_cmp(const float4& pa, const float4& na, const float4& nb, float ang_thr) {
+    float thr = 0.02f;
+    const float z = pa.x * 0.f + pa.y * 0.f + pa.z * 1.f;
+    thr *= z * z;
+    const float nd = na.x * nb.x + na.y * nb.y + na.z * nb.z;
+    return fabsf(na.w - nb.w) < thr && nd > ang_thr;
+}
+
+__global__ void k_ccl_merge(const float4* __restrict__ cloud, const float4* __restrict__ nrm, int w, int h,
+                            float ang_thr, int* __restrict__ parent) {
+    const long N = (long)w * h, total = 8 * N;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        if (ld(parent + i) < 0) continue;
+        const int j = (int)(i % N);
+        const int r = j / w, c = j - (j / w) * w;
+        const float4 p = cloud[i], n = nrm[i];
+        if (c >= 1 && plane_cmp(p, n, nrm[i - 1], ang_thr)) unite(parent, (int)i, (int)i - 1);
+        if (r >= 1 && plane_cmp(p, n, nrm[i - w], ang_thr)) unite(parent, (int)i, (int)(i - w));
+    }
+}
+
+__global__ void k_ccl_flatten(const int* __restrict__ parent, long total, int* __restrict__ root) {
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x)
+        root[i] = parent[i] < 0 ? -1 : find_root(parent, (int)i);
+}
+
+// block-wide exclusive scan of one int per thread (blockDim.x = 1024)
+__device__ int block_exscan(int v, int* sh, int& total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    __syncthreads();
+    if (lane == 63) sh[wid] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int acc = 0;
+        for (int k = 0; k < nw; ++k) { const int t = sh[k]; sh[k] = acc; acc += t; }
+        sh[nw] = acc;
+    }
+    __syncthreads();
+    total = sh[nw];
+    return sh[wid] + x - v;
+}
+
+// roots -> label ids in raster order (one workgroup per sensor); rank stored at the root's slot
+__global__ void __launch_bounds__(1024) k_ccl_number(const int* __restrict__ root, int N, int* __restrict__ rank,
+                                                     int* __restrict__ nlab) {
+    __shared__ int sh[17];
+    const int s = blockIdx.x;
+    const long base = (long)s * N;
+    int acc = 0;
+    for (int j0 = 0; j0 < N; j0 += blockDim.x) {
+        const int j = j0 + threadIdx.x;
+        const int is_root = (j < N && root[base + j] == (int)(base + j)) ? 1 : 0;
+        int tot;
+        const int ex = block_exscan(is_root, sh, tot);
+        if (is_root) rank[base + j] = acc + ex;
+        acc += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) nlab[s] = acc;
+}
+
+__global__ void k_ccl_label(const int* __restrict__ root, const int* __restrict__ rank, int N, int* __restrict__ lab,
+                            int* __restrict__ cnt) {
+    const long total = 8L * N;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int rt = root[i];
+        const int L = rt < 0 ? -1 : rank[rt];
+        lab[i] = L;
+        // wave-aggregated label counts
+        const int s = (int)(i / N);
+        long key = L < 0 ? -1 : (long)s * N + L;
+        bool pending = key >= 0;
+        while (__any(pending)) {
+            const unsigned long long act = __ballot(pending);
+            const int leader = __ffsll((long long)act) - 1;
+            const long lk = __shfl(key, leader, 64);
+            const bool mine = pending && key == lk;
+            const unsigned long long same = __ballot(mine);
+            if (mine && (int)(threadIdx.x & 63) == leader) atomicAdd(cnt + lk, __popcll(same));
+            if (mine) pending = false;
+        }
+    }
+}
+
+// labels with more than min_inliers points, in increasing label order (one workgroup per sensor)
+__global__ void __launch_bounds__(1024) k_big_list(const int* __restrict__ cnt, const int* __restrict__ nlab, int N,
+                                                   int min_inliers, int* __restrict__ big, int* __restrict__ nbig,
+                                                   int maxbig, int* __restrict__ err) {
+    __shared__ int sh[17];
+    const int s = blockIdx.x;
+    const int n = nlab[s];
+    int acc = 0;
+    for (int j0 = 0; j0 < n; j0 += blockDim.x) {
+        const int j = j0 + threadIdx.x;
+        const int f = (j < n && cnt[(long)s * N + j] > min_inliers) ? 1 : 0;
+        int tot;
+        const int ex = block_exscan(f, sh, tot);
+        if (f && acc + ex < maxbig) big[s * maxbig + acc + ex] = j;
+        acc += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        nbig[s] = acc < maxbig ? acc : maxbig;
+        if (acc > maxbig) atomicOr(err, 2);
+    }
+}
+
+// ------------------------------------------------------------------ moments
+constexpr int MOM_TPB = 256;
+
+struct alignas(16) MomShared {
+    r360p::i128 s2[MOM_TPB];
+    long long v[MOM_TPB];
+};
+
+// block reduction of a Moments struct, field by field (exact integer sums: order-free)
+__device__ void block_reduce_moments(r360p::Moments& m, MomShared* sh) {
+    auto red64 = [&](long long& x) {
+        sh->v[threadIdx.x] = x;
+        __syncthreads();
+        for (int o = MOM_TPB / 2; o > 0; o >>= 1) {
+            if ((int)threadIdx.x < o) sh->v[threadIdx.x] += sh->v[threadIdx.x + o];
+            __syncthreads();
+        }
+        x = sh->v[0];
+        __syncthreads();
+    };
+    auto red128 = [&](r360p::i128& x) {
+        sh->s2[threadIdx.x] = x;
+        __syncthreads();
+        for (int o = MOM_TPB / 2; o > 0; o >>= 1) {
+            if ((int)threadIdx.x < o) sh->s2[threadIdx.x] += sh->s2[threadIdx.x + o];
+            __syncthreads();
+        }
+        x = sh->s2[0];
+        __syncthreads();
+    };
+    red64(m.n);
+    for (int k = 0; k < 3; ++k) red64(m.s1[k]);
+    for (int k = 0; k < 6; ++k) red128(m.s2[k]);
+    for (int k = 0; k < 4; ++k) red64(m.c[k]);
+}
+
+__global__ void __launch_bounds__(MOM_TPB) k_label_moments(const float4* __restrict__ cloud, const int* __restrict__ lab,
+                                                          int N, const int* __restrict__ big,
+                                                          const int* __restrict__ nbig, int maxbig,
+                                                          r360p::Moments* __restrict__ mom) {
+    __shared__ MomShared sh;
+    const int s = blockIdx.y, b = blockIdx.x;
+    if (b >= nbig[s]) return;
+    const int L = big[s * maxbig + b];
+    const long base = (long)s * N;
+    r360p::Moments m;
+    r360p::moments_zero(m);
+    for (int j = threadIdx.x; j < N; j += MOM_TPB)
+        if (lab[base + j] == L) {
+            const float4 p = cloud[base + j];
+            if (isfin(p.x) && isfin(p.y) && isfin(p.z)) r360p::moments_add_xyz(m, p.x, p.y, p.z);
+        }
+    block_reduce_moments(m, &sh);
+    if (threadIdx.x == 0) mom[s * maxbig + b] = m;
+}
+
+// OrganizedMultiPlaneSegmentation::segment plane fit, one thread per sensor over its large labels in
+// label order (the viewpoint vp accumulates across labels, as in PCL 1.7)
+__global__ void k_plane_fit(const r360p::Moments* __restrict__ mom, const int* __restrict__ big,
+                            const int* __restrict__ nbig, int maxbig, float max_curvature, PlaneModel* __restrict__ models,
+                            int* __restrict__ nmodels, int* __restrict__ err) {
+    const int s = threadIdx.x;
+    if (s >= 8) return;
+    float vp[4] = {0, 0, 0, 0};
+    int nm = 0;
+    for (int b = 0; b < nbig[s]; ++b) {
+        const r360p::Moments m = mom[s * maxbig + b];
+        double mean[3], cv[9];
+        r360p::moments_mean_cov(m, mean, cv);
+        float centroid[4] = {(float)mean[0], (float)mean[1], (float)mean[2], 1.f};
+        float cov[9];
+        for (int k = 0; k < 9; ++k) cov[k] = (float)cv[k];
+        float eval, evec[3];
+        r360p::eigen33_min(cov, eval, evec);
+        float pp[4] = {evec[0], evec[1], evec[2], 0};
+        pp[3] = -1 * r360p::dot4(pp, centroid);
+        for (int k = 0; k < 4; ++k) vp[k] -= centroid[k];
+        const float cos_theta = r360p::dot4(vp, pp);
+        if (cos_theta < 0) {
+            for (int k = 0; k < 4; ++k) pp[k] *= -1;
+            pp[3] = -1 * r360p::dot4(pp, centroid);
+        }
+        const float eig_sum = cov[0] + cov[4] + cov[8];
+        const float curv = eig_sum != 0 ? fabsf(eval / eig_sum) : 0.f;
+        if (curv < max_curvature) {
+            if (nm >= R360_MAX_MODELS) { atomicOr(err, 4); break; }
+            PlaneModel& M = models[s * R360_MAX_MODELS + nm];
+            M.label = big[s * maxbig + b];
+            M.n_fit = (int)m.n;
+            for (int k = 0; k < 4; ++k) M.v[k] = pp[k];
+            for (int k = 0; k < 3; ++k) M.centroid[k] = centroid[k];
+            for (int k = 0; k < 9; ++k) M.cov[k] = cov[k];
+            M.curvature = curv;
+            ++nm;
+        }
+    }
+    nmodels[s] = nm;
+}
+
+// ------------------------------------------------------------------ refine
+// state: -1 no label, -2 non-planar label, m >= 0 planar model m.  mask bit m: |model_m . p| < 0.02
+__global__ void k_refine_init(const float4* __restrict__ cloud, const int* __restrict__ lab, int N,
+                              const PlaneModel* __restrict__ models, const int* __restrict__ nmodels,
+                              int8_t* __restrict__ state, unsigned long long* __restrict__ mask) {
+    const long total = 8L * N;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int s = (int)(i / N);
+        const int L = lab[i];
+        const int nm = nmodels[s];
+        const PlaneModel* M = models + s * R360_MAX_MODELS;
+        int st = L < 0 ? -1 : -2;
+        unsigned long long bits = 0;
+        const float4 p = cloud[i];
+        for (int m = 0; m < nm; ++m) {
+            if (L >= 0 && M[m].label == L) st = m;
+            const double ptp = fabs((double)(M[m].v[0] * p.x + M[m].v[1] * p.y + M[m].v[2] * p.z + M[m].v[3]));
+            if (ptp < (double)0.02f) bits |= 1ull << m;
+        }
+        state[i] = (int8_t)st;
+        mask[i] = bits;
+    }
+}
+
+// forward (dir = +1) or backward (dir = -1) wave scans over lanes in walking order
+__device__ __forceinline__ int lane_from(int lane, int off, int dir) { return dir > 0 ? lane - off : lane + off; }
+
+// Chain resolution of one row.  L[k]: states of this lane's K columns (in walking order k = 0..K-1),
+// M[k]: masks.  Returns F in place of L (original kept by the caller).  dir: +1 left-to-right.
+template <int K>
+__device__ void resolve_chain(const int (&L)[K], const unsigned long long (&M)[K], int (&F)[K], int dir) {
+    const int lane = threadIdx.x & 63;
+    // lane summary
+    bool anch = false;
+    unsigned long long am = ~0ull;
+    int out = -2;
+    {
+        int v = -2;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            if (L[k] != -2) { anch = true; v = L[k]; }
+            else if (anch) v = (v >= 0 && ((M[k] >> v) & 1)) ? v : -2;
+            else am &= M[k];
+        }
+        out = v;
+    }
+    // exclusive max-scan of anchor positions (in walking order) and segmented AND-scan of masks
+    const int wl = dir > 0 ? lane : 63 - lane;        // walking position of this lane
+    int apos = anch ? wl : -1;
+    unsigned long long segm = anch ? ~0ull : am;       // AND since the last anchor, inclusive
+    bool segf = anch;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int src = lane_from(lane, o, dir);
+        const int pa = __shfl(apos, src & 63, 64);
+        const unsigned long long pm = __shfl(segm, src & 63, 64);
+        const int pf = __shfl((int)segf, src & 63, 64);
+        if (wl >= o) {
+            apos = pa > apos ? pa : apos;
+            if (!segf) { segm &= pm; segf = pf; }
+        }
+    }
+    // values of the previous lane (walking order)
+    const int prev = lane_from(lane, 1, dir) & 63;
+    const int a_prev = __shfl(apos, prev, 64);               // last anchor at or before the previous lane
+    const unsigned long long m_prev = __shfl(segm, prev, 64);  // AND of masks after that anchor
+    const int a_lane = a_prev < 0 ? 0 : (dir > 0 ? a_prev : 63 - a_prev);
+    const int o_anchor = __shfl(out, a_lane, 64);
+    int in = -2;
+    if (wl > 0 && a_prev >= 0 && o_anchor >= 0 && ((m_prev >> o_anchor) & 1)) in = o_anchor;
+    int v = in;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        F[k] = (L[k] == -2 && v >= 0 && ((M[k] >> v) & 1)) ? v : L[k];
+        v = F[k];
+    }
+}
+
+template <int K>
+__global__ void __launch_bounds__(64) k_refine(int8_t* __restrict__ state_all,
+                                              const unsigned long long* __restrict__ mask_all, int w, int h) {
+    const int s = blockIdx.x;
+    const int lane = threadIdx.x;
+    const long N = (long)w * h;
+    int8_t* S = state_all + s * N;
+    const unsigned long long* MK = mask_all + s * N;
+    auto load = [&](int r, int (&L)[K], unsigned long long (&M)[K], int dir) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            // walking order: dir>0 -> column lane*K + k; dir<0 -> column (63-lane)*K + (K-1-k)
+            const int c = dir > 0 ? lane * K + k : (63 - lane) * K + (K - 1 - k);
+            L[k] = c < w ? (int)S[(long)r * w + c] : -1;
+            M[k] = c < w ? MK[(long)r * w + c] : 0ull;
+        }
+    };
+    auto store = [&](int r, const int (&L)[K], int dir) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int c = dir > 0 ? lane * K + k : (63 - lane) * K + (K - 1 - k);
+            if (c < w) S[(long)r * w + c] = (int8_t)L[k];
+        }
+    };
+    // ---------------- first sweep: top->bottom, left->right; right and down checks
+    {
+        int cur[K], nxt[K], F[K];
+        unsigned long long cm[K], nm[K];
+        load(0, cur, cm, +1);
+        for (int r = 0; r < h - 1; ++r) {
+            load(r + 1, nxt, nm, +1);
+            resolve_chain<K>(cur, cm, F, +1);
+            // original state of the column to the right of each of this lane's columns
+            const int right_of_last = __shfl(cur[0], (lane + 1) & 63, 64);
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int c = lane * K + k;
+                if (c >= w - 1) continue;
+                const int rl = k + 1 < K ? cur[k + 1] : (lane < 63 ? right_of_last : -1);
+                if (F[k] == -1 || rl == -1) continue;
+                if (nxt[k] == -1) continue;
+                if (F[k] >= 0 && nxt[k] == -2 && ((nm[k] >> F[k]) & 1)) nxt[k] = F[k];
+            }
+            store(r, F, +1);
+#pragma unroll
+            for (int k = 0; k < K; ++k) { cur[k] = nxt[k]; cm[k] = nm[k]; }
+        }
+        store(h - 1, cur, +1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    // ---------------- second sweep: bottom->top, right->left; left and up checks
+    {
+        int cur[K], up[K], F[K];
+        unsigned long long cm[K], um[K];
+        load(h - 1, cur, cm, -1);
+        const int cl = w - 1;                                    // owner of column w-1 (walking order)
+        const int own_lane = 63 - cl / K, own_k = K - 1 - cl % K;
+        for (int r = h - 1; r >= 1; --r) {
+            load(r - 1, up, um, -1);
+            resolve_chain<K>(cur, cm, F, -1);
+            // original state of the column to the left (walking order: the next element)
+            const int left_of_last = __shfl(cur[0], (lane + 1) & 63, 64);
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int c = (63 - lane) * K + (K - 1 - k);
+                if (c >= w || c == 0) continue;
+                const int ll = k + 1 < K ? cur[k + 1] : (lane < 63 ? left_of_last : -1);
+                if (F[k] == -1 || ll == -1) continue;
+                if (up[k] == -1) continue;
+                if (F[k] >= 0 && up[k] == -2 && ((um[k] >> F[k]) & 1)) up[k] = F[k];
+            }
+            // column 0: its "left" neighbour is the last pixel of the row above (flat-index wrap)
+            int upw = -1;
+            unsigned long long upw_m = 0;
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                if (k == own_k) { upw = up[k]; upw_m = um[k]; }
+            upw = __shfl(upw, own_lane, 64);
+            upw_m = __shfl(upw_m, own_lane, 64);
+            const int f0 = __shfl(F[K - 1], 63, 64);             // column 0 = lane 63, k = K-1
+            const int up0 = __shfl(up[K - 1], 63, 64);
+            const unsigned long long um0 = __shfl(um[K - 1], 63, 64);
+            int new_upw = upw, new_up0 = up0;
+            if (f0 != -1 && upw != -1) {
+                if (f0 >= 0 && upw == -2 && ((upw_m >> f0) & 1)) new_upw = f0;
+                if (up0 != -1 && f0 >= 0 && up0 == -2 && ((um0 >> f0) & 1)) new_up0 = f0;
+            }
+            if (w - 1 == 0) new_upw = new_up0;                   // degenerate single-column image
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                if (lane == own_lane && k == own_k) up[k] = new_upw;
+                if (lane == 63 && k == K - 1) up[k] = new_up0;
+            }
+            store(r, F, -1);
+#pragma unroll
+            for (int k = 0; k < K; ++k) { cur[k] = up[k]; cm[k] = um[k]; }
+        }
+        store(0, cur, -1);
+    }
+}
+
+__global__ void k_refine_final(const int8_t* __restrict__ state, const int* __restrict__ lab, int N,
+                               const PlaneModel* __restrict__ models, int* __restrict__ labf) {
+    const long total = 8L * N;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int s = (int)(i / N);
+        const int st = state[i];
+        labf[i] = st >= 0 ? models[s * R360_MAX_MODELS + st].label : (st == -2 ? lab[i] : -1);
+    }
+}
+
+// ------------------------------------------------------------------ per-model statistics
+__global__ void __launch_bounds__(MOM_TPB) k_model_stats(const float4* __restrict__ cloud, const uchar4* __restrict__ rgb,
+                                                        const int* __restrict__ lab, const int* __restrict__ labf,
+                                                        int N, const PlaneModel* __restrict__ models,
+                                                        const int* __restrict__ nmodels, const float* __restrict__ rt8,
+                                                        PlaneOut* __restrict__ out) {
+    __shared__ MomShared sh;
+    __shared__ int smin[MOM_TPB];
+    const int s = blockIdx.y, m = blockIdx.x;
+    if (m >= nmodels[s]) return;
+    const PlaneModel& M = models[s * R360_MAX_MODELS + m];
+    const int L = M.label;
+    const float* T = rt8 + 16 * s;
+    const long base = (long)s * N;
+    r360p::Moments mo;
+    r360p::moments_zero(mo);
+    int first = N;
+    for (int j = threadIdx.x; j < N; j += MOM_TPB) {
+        if (lab[base + j] == L && j < first) first = j;
+        if (labf[base + j] == L) {
+            const float4 p = cloud[base + j];
+            // Eigen Affine3f * Vector3f (pcl::transformPointCloud), column-major T
+            const float x = T[0] * p.x + T[4] * p.y + T[8] * p.z + T[12];
+            const float y = T[1] * p.x + T[5] * p.y + T[9] * p.z + T[13];
+            const float z = T[2] * p.x + T[6] * p.y + T[10] * p.z + T[14];
+            r360p::moments_add_xyz(mo, x, y, z);
+            const uchar4 c = rgb[base + j];
+            r360p::moments_add_rgb(mo, c.x, c.y, c.z);
+        }
+    }
+    smin[threadIdx.x] = first;
+    __syncthreads();
+    for (int o = MOM_TPB / 2; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) smin[threadIdx.x] = min(smin[threadIdx.x], smin[threadIdx.x + o]);
+        __syncthreads();
+    }
+    block_reduce_moments(mo, &sh);
+    if (threadIdx.x == 0) {
+        PlaneOut& O = out[s * R360_MAX_MODELS + m];
+        O.model = M;
+        O.stats = mo;
+        O.start = smin[0];
+        O.n_contour = 0;
+        O.contour_off = 0;
+        O.n_vox = 0;
+        O.vox_off = 0;
+    }
+}
+
+// findLabeledRegionBoundary; mode 0 counts, mode 1 writes the contour points (local frame)
+__global__ void k_trace(const int* __restrict__ labf, const float4* __restrict__ cloud, int w, int h,
+                        const int* __restrict__ nmodels, PlaneOut* __restrict__ out, float4* __restrict__ pool,
+                        long pool_cap, int mode, int* __restrict__ err) {
+    const int s = blockIdx.x;
+    const int m = threadIdx.x;
+    if (m >= nmodels[s]) return;
+    PlaneOut& O = out[s * R360_MAX_MODELS + m];
+    const long N = (long)w * h;
+    const int* Lb = labf + s * N;
+    const float4* P = cloud + s * N;
+    const int dxs[8] = {-1, -1, 0, 1, 1, 1, 0, -1}, dys[8] = {0, -1, -1, -1, 0, 1, 1, 1};
+    const int start = O.start;
+    const int label = Lb[start];
+    int cx = start % w, cy = start / w, cidx = start, dir = -1;
+    for (int d = 0; d < 8; ++d) {
+        const int x = cx + dxs[d], y = cy + dys[d];
+        if (x >= 0 && x < w && y >= 0 && y < h && Lb[cidx + dys[d] * w + dxs[d]] != label) { dir = d; break; }
+    }
+    if (dir < 0) {
+        if (mode == 0) O.n_contour = 0;
+        return;
+    }
+    long n = 0;
+    const long off = mode ? O.contour_off : 0;
+    const long max_len = 8 * N;
+    if (mode && off + n < pool_cap) pool[off + n] = P[start];
+    ++n;
+    do {
+        int nd = 0;
+        for (int d = 1; d <= 8; ++d) {
+            nd = (dir + d) & 7;
+            const int x = cx + dxs[nd], y = cy + dys[nd];
+            if (x >= 0 && x < w && y >= 0 && y < h && Lb[cidx + dys[nd] * w + dxs[nd]] == label) break;
+        }
+        dir = (nd + 4) & 7;
+        cidx += dys[nd] * w + dxs[nd];
+        cx += dxs[nd];
+        cy += dys[nd];
+        if (mode) {
+            if (off + n < pool_cap) pool[off + n] = P[cidx];
+        }
+        ++n;
+        if (n > max_len) { atomicOr(err, 8); break; }
+    } while (cidx != start);
+    if (mode == 0) O.n_contour = (int)n;
+}
+
+// prefix offsets of the contour and voxel-fallback pools (single thread)
+__global__ void k_alloc(const int* __restrict__ nmodels, PlaneOut* __restrict__ out, long* __restrict__ totals,
+                        long contour_cap, long vox_cap, int* __restrict__ err) {
+    if (threadIdx.x != 0) return;
+    long co = 0, vo = 0;
+    for (int s = 0; s < 8; ++s)
+        for (int m = 0; m < nmodels[s]; ++m) {
+            PlaneOut& O = out[s * R360_MAX_MODELS + m];
+            O.contour_off = co;
+            co += O.n_contour;
+            O.vox_off = vo;
+            O.n_vox = 0;
+            if (O.n_contour == 0) vo += O.stats.n;
+        }
+    totals[0] = co;
+    totals[1] = vo;
+    if (co > contour_cap || vo > vox_cap) atomicOr(err, 16);
+}
+
+__global__ void k_gather_vox(const int* __restrict__ labf, const float4* __restrict__ cloud, int N,
+                             const int* __restrict__ nmodels, PlaneOut* __restrict__ out, float4* __restrict__ pool,
+                             long pool_cap) {
+    const int s = blockIdx.y, m = blockIdx.x;
+    if (m >= nmodels[s]) return;
+    PlaneOut& O = out[s * R360_MAX_MODELS + m];
+    if (O.n_contour != 0) return;
+    const int L = O.model.label;
+    const long base = (long)s * N;
+    for (int j = threadIdx.x; j < N; j += blockDim.x)
+        if (labf[base + j] == L) {
+            const int k = atomicAdd(&O.n_vox, 1);
+            if (O.vox_off + k < pool_cap) pool[O.vox_off + k] = cloud[base + j];
+        }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ launcher
+int launch_segmentation(r360_frame* f) {
+    PlaneBufs& P = f->pl;
+    r360_ctx* ctx = f->ctx;
+    hipStream_t st = ctx->stream;
+    const int w = P.w, h = P.h, N = w * h;
+    const long total = 8L * N;
+    const int blocks = (int)((total + 255) / 256);
+    // PlaneCoefficientComparator::setAngularThreshold stores cosf(angle) (angle 0.039812, Frame360.h:959)
+    const float ang_thr = cosf((float)0.039812);
+    int slot = timing_begin(ctx, "k_ccl");
+    hipLaunchKernelGGL(k_ccl_init, dim3(blocks), dim3(256), 0, st, P.cloud, total, P.parent);
+    hipLaunchKernelGGL(k_ccl_merge, dim3(blocks), dim3(256), 0, st, P.cloud, P.nrm, w, h, ang_thr, P.parent);
+    hipLaunchKernelGGL(k_ccl_flatten, dim3(blocks), dim3(256), 0, st, P.parent, total, P.root);
+    hipLaunchKernelGGL(k_ccl_number, dim3(8), dim3(1024), 0, st, P.root, N, P.parent, P.nlab);
+    R360_HIP(hipMemsetAsync(P.cnt, 0, sizeof(int) * total, st));
+    hipLaunchKernelGGL(k_ccl_label, dim3(blocks), dim3(256), 0, st, P.root, P.parent, N, P.lab, P.cnt);
+    timing_end(ctx, slot);
+    R360_HIP(hipGetLastError());
+    slot = timing_begin(ctx, "k_plane_fit");
+    hipLaunchKernelGGL(k_big_list, dim3(8), dim3(1024), 0, st, P.cnt, P.nlab, N, 80, P.big, P.nbig, R360_MAX_BIG, P.err);
+    hipLaunchKernelGGL(k_label_moments, dim3(R360_MAX_BIG, 8), dim3(MOM_TPB), 0, st, P.cloud, P.lab, N, P.big, P.nbig,
+                       R360_MAX_BIG, P.mom);
+    hipLaunchKernelGGL(k_plane_fit, dim3(1), dim3(64), 0, st, P.mom, P.big, P.nbig, R360_MAX_BIG, 0.001f, P.models,
+                       P.nmodels, P.err);
+    timing_end(ctx, slot);
+    R360_HIP(hipGetLastError());
+    slot = timing_begin(ctx, "k_refine");
+    hipLaunchKernelGGL(k_refine_init, dim3(blocks), dim3(256), 0, st, P.cloud, P.lab, N, P.models, P.nmodels, P.state,
+                       P.mask);
+    const int K = (w + 63) / 64;
+    switch (K) {
+#define R360_REFINE_CASE(k) \
+    case k: hipLaunchKernelGGL(k_refine<k>, dim3(8), dim3(64), 0, st, P.state, P.mask, w, h); break;
+        R360_REFINE_CASE(1) R360_REFINE_CASE(2) R360_REFINE_CASE(3) R360_REFINE_CASE(4) R360_REFINE_CASE(5)
+        R360_REFINE_CASE(6) R360_REFINE_CASE(7) R360_REFINE_CASE(8) R360_REFINE_CASE(9) R360_REFINE_CASE(10)
+#undef R360_REFINE_CASE
+        default: r360_set_error("refine: cloud width %d > 640 unsupported", w); return -1;
+    }
+    hipLaunchKernelGGL(k_refine_final, dim3(blocks), dim3(256), 0, st, P.state, P.lab, N, P.models, P.labf);
+    timing_end(ctx, slot);
+    R360_HIP(hipGetLastError());
+    slot = timing_begin(ctx, "k_model_stats");
+    hipLaunchKernelGGL(k_model_stats, dim3(R360_MAX_MODELS, 8), dim3(MOM_TPB), 0, st, P.cloud, P.rgb, P.lab, P.labf, N,
+                       P.models, P.nmodels, f->calib->d_rt, P.out);
+    hipLaunchKernelGGL(k_trace, dim3(8), dim3(R360_MAX_MODELS), 0, st, P.labf, P.cloud, w, h, P.nmodels, P.out,
+                       P.contour, P.contour_cap, 0, P.err);
+    hipLaunchKernelGGL(k_alloc, dim3(1), dim3(64), 0, st, P.nmodels, P.out, P.totals, P.contour_cap, P.vox_cap, P.err);
+    hipLaunchKernelGGL(k_trace, dim3(8), dim3(R360_MAX_MODELS), 0, st, P.labf, P.cloud, w, h, P.nmodels, P.out,
+                       P.contour, P.contour_cap, 1, P.err);
+    hipLaunchKernelGGL(k_gather_vox, dim3(R360_MAX_MODELS, 8), dim3(256), 0, st, P.labf, P.cloud, N, P.nmodels, P.out,
+                       P.vox, P.vox_cap);
+    timing_end(ctx, slot);
+    R360_HIP(hipGetLastError());
+    return 0;
+}

@@ -69,6 +69,66 @@ struct alignas(16) IcpState {
 
 enum { R360_SUM_NVALID = 27, R360_SUM_NVIS = 28, R360_SUM_ERR2 = 31, R360_NSUMS = 32 };
 
+// ------------------------------------------------------------------ plane half
+#include "plane_math.h"
+#define R360_MAX_MODELS 64     // planar models per sensor (refinement closeness bit masks are 64-bit)
+#define R360_MAX_BIG 512       // labels with > 80 points per sensor
+
+// One planar model of segment() (PlanarRegion statistics + ModelCoefficients)
+struct PlaneModel {
+    int label, n_fit;
+    float v[4];
+    float centroid[3];
+    float cov[9];
+    float curvature;
+};
+
+// Per-model device output copied to the host for the PbMap descriptors
+struct alignas(16) PlaneOut {
+    r360p::Moments stats;   // final inliers: rig-frame moments + colour sums
+    PlaneModel model;
+    int start;              // inlier_indices[i][0]
+    int n_contour, n_vox;
+    long contour_off, vox_off;
+};
+
+// Device buffers of a frame's plane half (allocated on the first CLOUD/PLANES build)
+struct PlaneBufs {
+    int w = 0, h = 0;
+    float4* cloud = nullptr;    // [8][h][w] {x, y, z, 0}
+    uchar4* rgb = nullptr;      // [8][h][w] {r, g, b, 0}
+    float4* nrm = nullptr;      // [8][h][w] {nx, ny, nz, d = p.n}
+    float* dist0 = nullptr;     // distance-map init (depth-change map)
+    float* dist = nullptr;      // distance map
+    float2* grids = nullptr;    // bilateral grids, 8 x 2 x grid_cells
+    long grid_cells = 0;
+    int sd_max = 0;
+    int* parent = nullptr;      // union-find parents, then root ranks
+    int* root = nullptr;
+    int* lab = nullptr;         // CCL labels (per-sensor ids, -1 none)
+    int* labf = nullptr;        // labels after refinement
+    int* cnt = nullptr;         // label sizes [8][N]
+    int* nlab = nullptr;        // [8]
+    int* big = nullptr;         // [8][R360_MAX_BIG]
+    int* nbig = nullptr;        // [8]
+    r360p::Moments* mom = nullptr;   // [8][R360_MAX_BIG]
+    PlaneModel* models = nullptr;    // [8][R360_MAX_MODELS]
+    int* nmodels = nullptr;          // [8]
+    int8_t* state = nullptr;         // refinement state [8][N]
+    unsigned long long* mask = nullptr;  // closeness masks [8][N]
+    PlaneOut* out = nullptr;         // [8][R360_MAX_MODELS]
+    float4* contour = nullptr;       // contour pool
+    long contour_cap = 0;
+    float4* vox = nullptr;           // voxel-fallback point pool
+    long vox_cap = 0;
+    long* totals = nullptr;          // [2] pool usage
+    int* err = nullptr;              // error bits
+    // pinned host mirrors
+    PlaneOut* h_out = nullptr;
+    int* h_nmodels = nullptr;        // [8], then err at [8], totals at (long*)(h_nmodels + 10)
+};
+struct PbMapHost;                    // host PbMap (host/pbmap.cpp)
+
 // ------------------------------------------------------------------ host objects
 struct r360_ctx {
     int device = 0;
@@ -86,6 +146,13 @@ struct r360_ctx {
     std::vector<std::pair<std::string, Acc>> acc;
     // async-align bookkeeping
     int async_nL = 0, async_pending = 0;
+    // PbMap matcher scratch (k_match_tables)
+    int match_cap = 0;                       // planes per subgraph
+    float* d_match_desc = nullptr;
+    uint8_t* d_unary = nullptr;
+    unsigned long long* d_bin = nullptr;
+    uint8_t* h_unary = nullptr;              // pinned
+    unsigned long long* h_bin = nullptr;     // pinned
 };
 
 struct ClamsDev {
@@ -110,6 +177,7 @@ struct r360_calib {
     float* d_st_sinth = nullptr;
     float* d_st_costh = nullptr;
     float* d_rt_inv = nullptr;  // [8][16]
+    float* d_rt = nullptr;      // [8][16]
     // ICP trig tables per pyramid level of the sphere
     int n_levels = 0;
     LevelTrig trig[R360_MAX_PYR];
@@ -126,6 +194,8 @@ struct r360_frame {
     uint16_t* d_sph_depth = nullptr;
     LevelBufs lv[R360_MAX_PYR];
     unsigned built = 0;
+    PlaneBufs pl;
+    PbMapHost* pbmap = nullptr;
 };
 
 // ------------------------------------------------------------------ kernel launchers
@@ -135,6 +205,12 @@ int launch_pyramid(r360_frame* f);
 int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src, int level,
                      int method, const IcpConst& C, int first, int eval_only);
 int icp_blocks_for(int n_pixels);
+int launch_cloud_normals(r360_frame* f);
+int launch_segmentation(r360_frame* f);
+int plane_bufs_alloc(r360_frame* f);
+void plane_bufs_free(r360_frame* f);
+int planes_enqueue(r360_frame* f);
+int planes_finish(r360_frame* f);
 
 // timing helpers (host_runtime.cpp)
 int  timing_begin(r360_ctx* ctx, const char* name);

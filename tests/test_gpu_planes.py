@@ -1,0 +1,161 @@
+"""GPU parity tests of the plane half (A3-A9, A11-A13) through the C-ABI, against the CPU oracle on
+the same inputs (the two QVGA sample captures with their CLAMS models, and a synthetic VGA pair).
+
+Bars: the per-pixel stages are bit-exact (cloud + median downsample, bilateral filter, normals, CCL
+labels, refined labels), the distance map is exact below the 9.5 cap it is consumed at, the per-label
+statistics are exact integer moments so plane models, contours, PbMap descriptors, matcher tables,
+matches and the PbMap pose are identical to the oracle's.  PCL/MRPT pieces are 'parity unpinned'
+against the reference itself."""
+import os
+
+import numpy as np
+import pytest
+
+import rgbd360_amd as R
+from oracle import oracle360 as O
+
+pytestmark = pytest.mark.gpu
+
+RT = None
+
+
+def _same(a, b):
+    """bitwise equality with NaN == NaN"""
+    a, b = np.asarray(a), np.asarray(b)
+    return a.shape == b.shape and bool(np.all((a == b) | (np.isnan(a) & np.isnan(b))))
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    return R.Context(0)
+
+
+def _oracle_inputs_qvga(path):
+    b, d = O.load_bin(path)
+    dm = np.stack([O.Clams(os.path.join(R.INTRINSICS_DIR, f"distortion_model{k + 1}.r360")).undistort(O.depth_to_m(d[k]))
+                   for k in range(8)])
+    return b, dm
+
+
+@pytest.fixture(scope="module")
+def qvga(ctx):
+    cal = R.Calib360(ctx, 240, 320)
+    cal.loadExtrinsicCalibration(R.EXTRINSICS_DIR)
+    cal.loadIntrinsicCalibration(R.INTRINSICS_DIR)
+    rt = O.read_extrinsics(R.EXTRINSICS_DIR)
+    frames, inputs = [], []
+    for name in ("sphere_images_1.bin", "sphere_images_10.bin"):
+        p = os.path.join(R.SAMPLES_DIR, name)
+        f = R.Frame360(cal)
+        f.loadFrame(p)
+        f.getPlanes()
+        frames.append(f)
+        inputs.append(_oracle_inputs_qvga(p))
+    return dict(cal=cal, frames=frames, inputs=inputs, rt=rt)
+
+
+@pytest.fixture(scope="module")
+def vga(ctx):
+    cal = R.Calib360(ctx, 480, 640)
+    cal.loadExtrinsicCalibration(R.EXTRINSICS_DIR)
+    rt = O.read_extrinsics(R.EXTRINSICS_DIR)
+    seed = 360 << 16
+    A = R.synth_path_pose(seed, 0)
+    rel = np.eye(4, dtype=np.float32)
+    a = np.deg2rad(4.0)
+    rel[1:3, 1:3] = [[np.cos(a), -np.sin(a)], [np.sin(a), np.cos(a)]]
+    rel[:3, 3] = [0, 0.25, 0.15]
+    frames, inputs = [], []
+    for P in (A, A @ rel):
+        b, d = cal.synth_frame(seed, P)
+        f = R.Frame360(cal)
+        f.upload(b, d)
+        f.getPlanes()
+        frames.append(f)
+        inputs.append((b, d.astype(np.float32) * np.float32(0.001)))
+    return dict(cal=cal, frames=frames, inputs=inputs, rt=rt, rel=rel)
+
+
+def _per_sensor_oracle(b, dm):
+    out = []
+    for k in range(8):
+        xyz, rgb = O.cloud_downsample(dm[k], b[k])
+        xf = O.bilateral(xyz)
+        nrm, dist = O.normals(xf)
+        lc, lf, regs = O.segment(xf, nrm)
+        out.append(dict(xyz=xf, rgb=rgb, nrm=nrm, dist=dist, lc=lc, lf=lf, regs=regs))
+    return out
+
+
+@pytest.mark.parametrize("which", ["qvga", "vga"])
+def test_per_pixel_stages_bitexact(request, which):
+    D = request.getfixturevalue(which)
+    for f, (b, dm) in zip(D["frames"], D["inputs"]):
+        xyz, rgb, nrm, dist = f.cloud()
+        lab, labf = f.labels()
+        ref = _per_sensor_oracle(b, dm)
+        for k in range(8):
+            r = ref[k]
+            assert _same(xyz[k], r["xyz"]), ("cloud", k)
+            assert np.array_equal(rgb[k], r["rgb"]), ("rgb", k)
+            assert _same(np.minimum(dist[k], 9.5), np.minimum(r["dist"], 9.5)), ("dist", k)
+            assert _same(nrm[k][..., :3], r["nrm"][..., :3]), ("normals", k)
+            assert np.array_equal(lab[k], r["lc"]), ("ccl", k)
+            assert np.array_equal(labf[k], r["lf"]), ("refined labels", k)
+            regs = f.regions(k)
+            assert len(regs) == len(r["regs"]), ("regions", k)
+            for g, o in zip(regs, r["regs"]):
+                assert (g["label"], g["count"], g["start_idx"], g["n_contour"]) == \
+                    (o["label"], o["count"], o["start_idx"], len(o["contour"])), ("region", k)
+                for key in ("centroid", "cov", "model"):
+                    assert np.array_equal(g[key], o[key]), (key, k)
+                assert g["curvature"] == o["curvature"]
+
+
+def _cmp_planes(gp, op):
+    assert len(gp) == len(op)
+    for g, o in zip(gp, op):
+        for key in ("normal", "center", "ppal", "nrgb", "hull"):
+            assert np.array_equal(g[key], o[key]), key
+        for key in ("d", "area", "elongation", "curvature", "intensity", "id", "sensor", "n_inliers"):
+            assert g[key] == o[key], key
+
+
+@pytest.mark.parametrize("which", ["qvga", "vga"])
+def test_pbmap_planes_identical(request, which):
+    D = request.getfixturevalue(which)
+    maps = []
+    for f, (b, dm) in zip(D["frames"], D["inputs"]):
+        om = O.PbMap(dm, b, D["rt"])
+        _cmp_planes(f.planes(), om.planes())
+        maps.append(om)
+    D["oracle_maps"] = maps
+
+
+@pytest.mark.parametrize("which", ["qvga", "vga"])
+def test_match_tables_and_register_pbmap(ctx, request, which):
+    D = request.getfixturevalue(which)
+    maps = D.get("oracle_maps") or [O.PbMap(dm, b, D["rt"]) for (b, dm) in D["inputs"]]
+    reg = R.RegisterRGBD360(ctx)
+    reg.setReference(D["frames"][0], 25)
+    reg.setTarget(D["frames"][1], 25)
+    gt = reg.match_tables(R.PLANAR_3DoF)
+    ot = O.match_tables(maps[0], maps[1], 25, O.PLANAR_3DoF)
+    for key in ("sid", "tid", "unary", "binary"):
+        assert np.array_equal(gt[key], ot[key]), key
+    ok = reg.RegisterPbMap(D["frames"][0], D["frames"][1], 25, R.PLANAR_3DoF)
+    r = O.register_pbmap(maps[0], maps[1], 25, O.PLANAR_3DoF)
+    assert ok == bool(r["good"])
+    assert reg.getMatchedPlanes() == r["matches"]
+    assert reg.getAreaMatched() == r["area_matched"]
+    if ok:
+        assert np.array_equal(reg.getPose(), r["pose"])
+        assert np.array_equal(reg.getInfoMat(), r["info"])
+
+
+def test_register_pbmap_synthetic_accuracy(ctx, vga):
+    reg = R.RegisterRGBD360(ctx)
+    assert reg.RegisterPbMap(vga["frames"][0], vga["frames"][1], 25, R.PLANAR_3DoF)
+    P, rel = reg.getPose(), vga["rel"]
+    assert np.rad2deg(O.rot_angle(P[:3, :3], rel[:3, :3])) < 0.3
+    assert np.linalg.norm(P[:3, 3] - rel[:3, 3]) < 0.02
