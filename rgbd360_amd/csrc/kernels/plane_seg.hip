@@ -287,15 +287,13 @@ __global__ void k_refine_init(const float4* __restrict__ cloud, const int* __res
     }
 }
 
-// forward (dir = +1) or backward (dir = -1) wave scans over lanes in walking order
-__device__ __forceinline__ int lane_from(int lane, int off, int dir) { return dir > 0 ? lane - off : lane + off; }
-
-// Chain resolution of one row.  L[k]: states of this lane's K columns (in walking order k = 0..K-1),
-// M[k]: masks.  Returns F in place of L (original kept by the caller).  dir: +1 left-to-right.
+// Chain resolution of one row.  The row is laid out in walking order across the wave: lane l holds
+// the K consecutive walking positions l*K .. l*K+K-1 (left-to-right in the first sweep, right-to-left
+// in the second).  L[k]: states, M[k]: closeness masks; F receives the states after the chain.
 template <int K>
-__device__ void resolve_chain(const int (&L)[K], const unsigned long long (&M)[K], int (&F)[K], int dir) {
+__device__ void resolve_chain(const int (&L)[K], const unsigned long long (&M)[K], int (&F)[K]) {
     const int lane = threadIdx.x & 63;
-    // lane summary
+    // lane summary: anchored (some non-chain state) -> outgoing value fixed; else AND of masks
     bool anch = false;
     unsigned long long am = ~0ull;
     int out = -2;
@@ -309,30 +307,25 @@ __device__ void resolve_chain(const int (&L)[K], const unsigned long long (&M)[K
         }
         out = v;
     }
-    // exclusive max-scan of anchor positions (in walking order) and segmented AND-scan of masks
-    const int wl = dir > 0 ? lane : 63 - lane;        // walking position of this lane
-    int apos = anch ? wl : -1;
-    unsigned long long segm = anch ? ~0ull : am;       // AND since the last anchor, inclusive
-    bool segf = anch;
+    // inclusive max-scan of anchor lanes and segmented AND-scan of masks since the last anchor
+    int apos = anch ? lane : -1;
+    unsigned long long segm = anch ? ~0ull : am;
+    int segf = anch;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-        const int src = lane_from(lane, o, dir);
-        const int pa = __shfl(apos, src & 63, 64);
-        const unsigned long long pm = __shfl(segm, src & 63, 64);
-        const int pf = __shfl((int)segf, src & 63, 64);
-        if (wl >= o) {
+        const int pa = __shfl_up(apos, o, 64);
+        const unsigned long long pm = __shfl_up(segm, o, 64);
+        const int pf = __shfl_up(segf, o, 64);
+        if (lane >= o) {
             apos = pa > apos ? pa : apos;
             if (!segf) { segm &= pm; segf = pf; }
         }
     }
-    // values of the previous lane (walking order)
-    const int prev = lane_from(lane, 1, dir) & 63;
-    const int a_prev = __shfl(apos, prev, 64);               // last anchor at or before the previous lane
-    const unsigned long long m_prev = __shfl(segm, prev, 64);  // AND of masks after that anchor
-    const int a_lane = a_prev < 0 ? 0 : (dir > 0 ? a_prev : 63 - a_prev);
-    const int o_anchor = __shfl(out, a_lane, 64);
+    const int a_prev = __shfl_up(apos, 1, 64);                 // last anchor lane before this lane
+    const unsigned long long m_prev = __shfl_up(segm, 1, 64);  // AND of masks after that anchor
+    const int o_anchor = __shfl(out, a_prev < 0 ? 0 : a_prev, 64);
     int in = -2;
-    if (wl > 0 && a_prev >= 0 && o_anchor >= 0 && ((m_prev >> o_anchor) & 1)) in = o_anchor;
+    if (lane > 0 && a_prev >= 0 && o_anchor >= 0 && ((m_prev >> o_anchor) & 1)) in = o_anchor;
     int v = in;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -372,7 +365,7 @@ __global__ void __launch_bounds__(64) k_refine(int8_t* __restrict__ state_all,
         load(0, cur, cm, +1);
         for (int r = 0; r < h - 1; ++r) {
             load(r + 1, nxt, nm, +1);
-            resolve_chain<K>(cur, cm, F, +1);
+            resolve_chain<K>(cur, cm, F);
             // original state of the column to the right of each of this lane's columns
             const int right_of_last = __shfl(cur[0], (lane + 1) & 63, 64);
 #pragma unroll
@@ -402,7 +395,7 @@ __global__ void __launch_bounds__(64) k_refine(int8_t* __restrict__ state_all,
         const int own_lane = 63 - cl / K, own_k = K - 1 - cl % K;
         for (int r = h - 1; r >= 1; --r) {
             load(r - 1, up, um, -1);
-            resolve_chain<K>(cur, cm, F, -1);
+            resolve_chain<K>(cur, cm, F);
             // original state of the column to the left (walking order: the next element)
             const int left_of_last = __shfl(cur[0], (lane + 1) & 63, 64);
 #pragma unroll
