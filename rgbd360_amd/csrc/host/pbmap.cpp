@@ -12,7 +12,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <set>
@@ -385,7 +388,14 @@ int planes_finish(r360_frame* f) {
     PlaneBufs& P = f->pl;
     if (!P.cloud) { r360_set_error("planes were not built (R360_BUILD_PLANES)"); return -2; }
     hipStream_t st = f->ctx->stream;
+    static const bool prof = getenv("R360_PBMAP_PROFILE") != nullptr;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto us = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+        return std::chrono::duration<double, std::micro>(b - a).count();
+    };
+    const auto t0 = now();
     R360_HIP(hipStreamSynchronize(st));
+    const auto t1 = now();
     const int err = P.h_nmodels[8];
     if (err) {
         r360_set_error("plane segmentation capacity exceeded (code %d: 1 bilateral depth range, 2 labels, 4 models, "
@@ -397,6 +407,7 @@ int planes_finish(r360_frame* f) {
     if (totals[0]) R360_HIP(hipMemcpyAsync(contour.data(), P.contour, sizeof(float4) * totals[0], hipMemcpyDeviceToHost, st));
     if (totals[1]) R360_HIP(hipMemcpyAsync(vox.data(), P.vox, sizeof(float4) * totals[1], hipMemcpyDeviceToHost, st));
     R360_HIP(hipStreamSynchronize(st));
+    const auto t2 = now();
     const r360_calib* cal = f->calib;
     std::vector<std::vector<HPlane>> local(8);
     for (int s = 0; s < 8; ++s) {
@@ -448,6 +459,7 @@ int planes_finish(r360_frame* f) {
             }
         }
     }
+    const auto t3 = now();
     // groupPlanes (:742-832)
     auto* pm = new PbMapHost;
     std::vector<HPlane>& G = pm->planes;
@@ -497,6 +509,9 @@ int planes_finish(r360_frame* f) {
         }
     }
     f->pbmap = pm;
+    if (prof)
+        fprintf(stderr, "[pbmap] gpu wait %.0f us, pools %ld+%ld pts D2H %.0f us, descriptors %.0f us, group/merge %.0f us\n",
+                us(t0, t1), totals[0], totals[1], us(t1, t2), us(t2, t3), us(t3, now()));
     return 0;
 }
 

@@ -16,9 +16,6 @@ from oracle import oracle360 as O
 
 pytestmark = pytest.mark.gpu
 
-RT = None
-
-
 def _same(a, b):
     """bitwise equality with NaN == NaN"""
     a, b = np.asarray(a), np.asarray(b)
@@ -159,3 +156,53 @@ def test_register_pbmap_synthetic_accuracy(ctx, vga):
     P, rel = reg.getPose(), vga["rel"]
     assert np.rad2deg(O.rot_angle(P[:3, :3], rel[:3, :3])) < 0.3
     assert np.linalg.norm(P[:3, 3] - rel[:3, 3]) < 0.02
+
+
+def _rot_offset(a_deg=157.5):
+    """rotOffset of OdometryRGBD360.cpp:138-139 (float angleOffset, double PI) and its transpose."""
+    a = np.float64(np.float32(a_deg)) * 3.14159265359 / 180
+    Ro = np.eye(4, dtype=np.float32)
+    c, s = np.float32(np.cos(a)), np.float32(np.sin(a))
+    Ro[1, 1] = Ro[2, 2] = c
+    Ro[1, 2], Ro[2, 1] = s, -s
+    return Ro, Ro.T.copy()
+
+
+def _mul4(A, B):
+    """Eigen Matrix4f product order in float32: ((a0 b0 + a1 b1) + a2 b2) + a3 b3"""
+    C = np.zeros((4, 4), np.float32)
+    for r in range(4):
+        for c in range(4):
+            acc = np.float32(A[r, 0] * B[0, c])
+            for k in range(1, 4):
+                acc = np.float32(acc + np.float32(A[r, k] * B[k, c]))
+            C[r, c] = acc
+    return C
+
+
+def test_register_alias_parity_synth_vga(ctx, vga):
+    """Register(): PbMap pose -> rotOffset conjugation -> alignFrames360 (OdometryKeyFrame360.cpp:248-254),
+    compared with the oracle chain on the same pair (north-star tolerance 1e-4 rad / 1e-3 m)."""
+    f1, f2 = vga["frames"]
+    for f in (f1, f2):
+        f.build(R.BUILD_UNDISTORT | R.BUILD_SPHERE | R.BUILD_PYRAMID)
+    p = R.IcpParams.default()
+    p.n_pyr = 5
+    p.std_dev_photo = np.float32(3.0 / 255)
+    pose, info, st, ok = R.register(ctx, f1, f2, None, p, 25, R.PLANAR_3DoF)
+    assert ok
+    maps = vga.get("oracle_maps") or [O.PbMap(dm, b, vga["rt"]) for (b, dm) in vga["inputs"]]
+    r = O.register_pbmap(maps[0], maps[1], 25, O.PLANAR_3DoF)
+    Ro, Ri = _rot_offset()
+    init = _mul4(_mul4(Ro, r["pose"]), Ri)
+    s1b, s1d = f1.sphere()
+    s2b, s2d = f2.sphere()
+    op = O.IcpParams.default(n_pyr=5, std_dev_photo=np.float32(3.0 / 255))
+    rco, dense, H, g, ost = O.align360(s1b, s1d, s2b, s2d, init, O.PHOTO_DEPTH, op)
+    ref = _mul4(_mul4(Ri, dense), Ro)
+    assert O.rot_angle(pose[:3, :3], ref[:3, :3]) <= 1e-4
+    assert np.linalg.norm(pose[:3, 3] - ref[:3, 3]) <= 1e-3
+    # and the registration is right: the synthetic pair's relative pose
+    rel = vga["rel"]
+    assert np.rad2deg(O.rot_angle(pose[:3, :3], rel[:3, :3])) < 0.2
+    assert np.linalg.norm(pose[:3, 3] - rel[:3, 3]) < 0.02
