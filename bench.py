@@ -1,17 +1,22 @@
 """bench.py — registered Frame360 pairs/sec on MI355X (BASELINE.json metric) + ICP-reduce roofline.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload full|dense]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-Workload (BASELINE.json configs[2], "single synthetic 8x640x480 pair, full RegisterPhotoICP (20 iters)
-with JtJ reduction"): one step = one Frame360 pair of the synthetic 256-frame sequence (procedural
-room, seed 360) registered end to end on the GPU — both frames stitched (8 x 480x640 -> 640x3840
-sphere) and pyramided (5 levels, gray + depth + target gradients), then
-RegisterPhotoICP::alignFrames360(PHOTO_DEPTH) with the reference schedule on levels 4..1 and exactly
-20 Gauss-Newton iterations at level 0 (timing mode).  Raw sensor images are resident
-in HBM before the timed region.  Multi-GPU: pair-per-GPU sharding of the sequence (weak scaling,
-no data-path collective) + one RCCL all_gather of the resulting 4x4 poses.
+Workload "full" (default; BASELINE.json configs[1]+[2] as one registration, run the way configs[3]
+runs them): the synthetic 256-frame OdometryRGBD360 sequence (procedural room, seed 360, 8 x 480x640
+sensors).  One step registers, on each of P pipelines of each GPU, the next consecutive pair of the
+rank's shard: the new Frame360 is built end to end on the GPU (undistort, cloud + 2x2 median
+downsample, bilateral filter, normals, plane segmentation + refinement, PbMap descriptors and
+grouping, spherical stitch, 5-level pyramid with gradients), then RegisterRGBD360::RegisterPbMap
+(25 planes, PLANAR_3DoF) and RegisterPhotoICP::alignFrames360(PHOTO_DEPTH) initialised with the
+rotOffset-conjugated PbMap pose (OdometryKeyFrame360.cpp:205-254), with the reference schedule on
+levels 4..1 and exactly 20 Gauss-Newton iterations at level 0 (timing mode).
+Workload "dense" (configs[2] alone): stitch + pyramid of both frames + alignFrames360.
+Raw sensor images are resident in HBM before the timed region.  Multi-GPU: each rank registers its
+own contiguous shard of the sequence (weak scaling, no data-path collective) and the 4x4 poses are
+gathered with one RCCL all_gather over xGMI.
 
 Prints ONE JSON line on rank 0.
 """
@@ -28,34 +33,56 @@ sys.path.insert(0, ROOT)
 
 METRIC = "registered Frame360 pairs/sec @ 8×640×480; ICP-reduce HBM GB/s vs roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+SEQ_LEN = 256
 
 
-def make_pair_frames(R, cal, seed, i):
-    A = R.synth_path_pose(seed, i)
-    B = R.synth_path_pose(seed, i + 1)
-    return cal.synth_frame(seed, A), cal.synth_frame(seed, B)
-
-
-def cpu_baseline(R, cal, pairs, fixed_iters, budget_s=12.0):
-    """The CPU oracle (C++ restatement, OpenMP) on a bounded sample of the same workload."""
+def cpu_baseline(R, cal, seed, first, workload, iters0, budget_s=15.0):
+    """The CPU oracle (C++ restatement, OpenMP over the 8 sensors / rows) on a bounded sample of the
+    same workload: consecutive pairs of the same synthetic sequence."""
     from oracle import oracle360 as O
-    _, rti, K = cal.extrinsics()
+    rt, rti, K = cal.extrinsics()
     Km = K.reshape(3, 3).T
-    prm = O.IcpParams.default(n_pyr=5, std_dev_photo=np.float32(3.0 / 255), fixed_iters_level0=fixed_iters)
+    rt8 = np.stack([rt[16 * k:16 * k + 16].reshape(4, 4).T for k in range(8)])
+    prm = O.IcpParams.default(n_pyr=5, std_dev_photo=np.float32(3.0 / 255), fixed_iters_level0=iters0)
+    a = np.float64(np.float32(157.5)) * 3.14159265359 / 180
+    Ro = np.eye(4, dtype=np.float32)
+    Ro[1, 1] = Ro[2, 2] = np.float32(np.cos(a))
+    Ro[1, 2], Ro[2, 1] = np.float32(np.sin(a)), -np.float32(np.sin(a))
+    Ri = Ro.T.copy()
+
+    def frame(i):
+        b, d = cal.synth_frame(seed, R.synth_path_pose(seed, i))
+        return b, d
+
+    def build(b, d):
+        sb, sd = O.stitch(b, d, rti, Km)
+        pm = O.PbMap(d.astype(np.float32) * np.float32(0.001), b, rt8) if workload == "full" else None
+        return sb, sd, pm
+
+    raw = [frame(first + j) for j in range(6)]
+    prev = build(*raw[0])
     n, t0 = 0, time.perf_counter()
     while True:
-        (b1, d1), (b2, d2) = pairs[n % len(pairs)]
-        s1b, s1d = O.stitch(b1, d1, rti, Km)
-        s2b, s2d = O.stitch(b2, d2, rti, Km)
-        O.align360(s1b, s1d, s2b, s2d, None, O.PHOTO_DEPTH, prm)
+        b, d = raw[(n + 1) % len(raw)]
+        cur = build(b, d)
+        if workload == "full":
+            r = O.register_pbmap(prev[2], cur[2], 25, O.PLANAR_3DoF)
+            init = Ro @ (r["pose"] if r["good"] else np.eye(4, dtype=np.float32)) @ Ri
+        else:
+            prev = build(*raw[n % len(raw)])     # dense: both frames per pair
+            init = None
+        O.align360(prev[0], prev[1], cur[0], cur[1], init, O.PHOTO_DEPTH, prm)
+        prev = cur
         n += 1
         if time.perf_counter() - t0 > budget_s:
             break
     dt = time.perf_counter() - t0
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    what = ("PbMap build of the new frame + RegisterPbMap + stitch + alignFrames360" if workload == "full"
+            else "stitch x2 + alignFrames360")
     return {"value": n / dt, "unit": "pairs/s", "cores": cores, "kind": "port",
-            "sample": f"{n} synthetic 8x480x640 pairs (cycling {len(pairs)}) (stitch x2 + alignFrames360 nPyr=5, "
-                      f"{fixed_iters} level-0 iterations), oracle/liboracle360.so, {dt:.1f} s"}
+            "sample": f"{n} consecutive synthetic 8x480x640 pairs ({what}, nPyr=5, {iters0} level-0 iterations), "
+                      f"oracle/liboracle360.so, {dt:.1f} s"}
 
 
 def main():
@@ -66,7 +93,9 @@ def main():
     ap.add_argument("--rows", type=int, default=480)
     ap.add_argument("--cols", type=int, default=640)
     ap.add_argument("--iters0", type=int, default=20)
+    ap.add_argument("--workload", choices=["full", "dense"], default="full")
     ap.add_argument("--streams", type=int, default=8, help="pairs in flight per GPU (one HIP stream each)")
+    ap.add_argument("--window", type=int, default=16, help="sequence frames resident per pipeline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -83,8 +112,10 @@ def main():
     import rgbd360_amd as R
 
     # P independent pipelines (one r360_ctx = one HIP stream + device GN state each) keep several pairs
-    # in flight, so the latency-bound coarse pyramid levels of one pair overlap other pairs' work
+    # in flight: one pipeline's host-side PbMap work and latency-bound coarse ICP levels overlap the
+    # other pipelines' kernels
     P = max(1, args.streams)
+    F = max(3, args.window)
     ctxs = [R.Context(local) for _ in range(P)]
     cals = []
     for c in ctxs:
@@ -93,41 +124,52 @@ def main():
         cals.append(cal)
     cal = cals[0]
     seed = 360 << 16
-
-    # this rank's shard of the 256-frame sequence: consecutive pairs, one pair per pipeline per step
-    n_frames_local = 4
-    first = (rank * 32) % 252
-    raw = [cal.synth_frame(seed, R.synth_path_pose(seed, first + j)) for j in range(n_frames_local)]
+    # this rank's shard of the 256-frame sequence; pipeline p walks its own contiguous window of it
+    shard = SEQ_LEN // world
+    first = rank * shard
+    flags = R.BUILD_UNDISTORT | R.BUILD_SPHERE | R.BUILD_PYRAMID
+    if args.workload == "full":
+        flags |= R.BUILD_PLANES
     frames = []
-    for c in cals:
+    for p, c in enumerate(cals):
         fl = []
-        for (b, d) in raw:
+        base = first + (p * F) % max(1, shard - F)
+        for j in range(F):
+            b, d = cal.synth_frame(seed, R.synth_path_pose(seed, base + j))
             f = R.Frame360(c)
-            f.upload(b, d)  # raw 8-sensor images resident in HBM before timing
+            f.upload(b, d)          # raw 8-sensor images resident in HBM before timing
+            f.build(flags)          # allocates every device buffer outside the timed region
             fl.append(f)
         frames.append(fl)
-    regs = []
-    for c in ctxs:
-        reg = R.RegisterPhotoICP(c)
-        reg.setNumPyr(5)
-        reg.setGrayVariance(3.0 / 255)
-        reg.params.fixed_iters_level0 = args.iters0
-        regs.append(reg)
+    params = R.IcpParams.default()
+    params.n_pyr = 5
+    params.std_dev_photo = np.float32(3.0 / 255)       # OdometryRGBD360.cpp:92-95
+    params.fixed_iters_level0 = args.iters0
     L = R.lib()
-    init16 = np.eye(4, dtype=np.float32).reshape(16)
+    eye16 = np.eye(4, dtype=np.float32).reshape(16)
     pout = np.zeros((P, 16), np.float32)
+    stats = [R.IcpStats() for _ in range(P)]
 
     def step(k):
-        i = k % (n_frames_local - 1)
-        for p in range(P):   # enqueue every pipeline's pair, then collect
-            trg, src = frames[p][i], frames[p][i + 1]
-            trg.build(R.BUILD_SPHERE | R.BUILD_PYRAMID, sync=False)
-            src.build(R.BUILD_SPHERE | R.BUILD_PYRAMID, sync=False)
-            rc = L.r360_align360_async(ctxs[p].h, trg.h, src.h, R._fptr(init16), R.PHOTO_DEPTH, 0,
-                                       R.C.byref(regs[p].params))
+        j = k % (F - 1)
+        for p in range(P):                       # enqueue every pipeline's GPU frame builds
+            if args.workload == "dense" or j == 0:
+                frames[p][j].build(flags, sync=False)
+            frames[p][j + 1].build(flags, sync=False)
+        for p in range(P):                       # PbMap stage (host) + enqueue the dense stage
+            ref, trg = frames[p][j], frames[p][j + 1]
+            if args.workload == "full":
+                rc = L.r360_register_async(ctxs[p].h, ref.h, trg.h, R._fptr(eye16), R.C.byref(params), 25,
+                                           R.PLANAR_3DoF)
+            else:
+                rc = L.r360_align360_async(ctxs[p].h, ref.h, trg.h, R._fptr(eye16), R.PHOTO_DEPTH, 0,
+                                           R.C.byref(params))
             assert rc == 0, L.r360_last_error()
         for p in range(P):
-            rc = L.r360_align360_result(ctxs[p].h, R._fptr(pout[p]), None, None, R.C.byref(regs[p].stats))
+            if args.workload == "full":
+                rc = L.r360_register_result(ctxs[p].h, R._fptr(pout[p]), None, R.C.byref(stats[p]))
+            else:
+                rc = L.r360_align360_result(ctxs[p].h, R._fptr(pout[p]), None, None, R.C.byref(stats[p]))
             assert rc >= 0, L.r360_last_error()
         return pout
 
@@ -149,7 +191,7 @@ def main():
         c.timing_reset()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        poses[k] = step(k)
+        poses[k] = step(args.warmup + k)
     for c in ctxs:
         c.sync()
     if dist is not None:  # RCCL pose gather over xGMI
@@ -161,11 +203,16 @@ def main():
     elapsed = time.perf_counter() - t0
     barrier()
     l0_ms, l0_n = 0.0, 0
+    stage = {}
     for c in ctxs:
         c.timing(False)
         ms, n = c.timing_read("k_icp_pass_L0")
-        l0_ms += ms; l0_n += n
-    reg = regs[0]
+        l0_ms += ms
+        l0_n += n
+        for name in ("k_cloud", "k_bilateral", "k_distmap", "k_normals", "k_ccl", "k_plane_fit", "k_refine",
+                     "k_model_stats", "k_icp_pass", "k_icp_pass_L0"):
+            ms, n = c.timing_read(name)
+            stage[name] = stage.get(name, 0.0) + ms
     if dist is not None:
         import torch
         e = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
@@ -177,7 +224,7 @@ def main():
     W0 = args.rows * 8
     H0 = int(W0 * 0.5 * 60.0 / 180)               # Frame360.h:391-392 (640 x 3840 at VGA)
     N0 = H0 * W0
-    sso = float(reg.stats.sso)
+    sso = float(stats[0].sso)
     V = sso * N0
     alg_bytes = 8.0 * N0 + 24.0 * V            # B = 8 N + 24 V per pass
     avg_ms = l0_ms / max(l0_n, 1)
@@ -188,16 +235,26 @@ def main():
     tf = os.path.join(ROOT, "profiles", "latest", "l0_pass.json")
     if os.path.exists(tf):
         traffic = json.load(open(tf)).get("hbm_bytes_per_launch")
+    pairs_timed = args.steps * P
+    if args.workload == "full":
+        workload = ("config2+3 (run as config4's sequence): per pair, the new synthetic 8x640x480 Frame360 is "
+                    "built on the GPU (undistort, cloud + median downsample, bilateral, normals, plane "
+                    "segmentation + refinement, PbMap descriptors/grouping, stitch, 5-level pyramid), then "
+                    "RegisterPbMap(25 planes, PLANAR_3DoF) + alignFrames360(PHOTO_DEPTH) initialised with the "
+                    f"rotOffset-conjugated PbMap pose: levels 4..1 reference schedule + {args.iters0} GN "
+                    "iterations at level 0")
+    else:
+        workload = ("config3: synthetic 8x640x480 Frame360 pair -> stitch + 5-level pyramid x2 -> "
+                    f"alignFrames360(PHOTO_DEPTH) levels 4..1 reference schedule + {args.iters0} GN iterations "
+                    "at level 0")
     out = {
         "metric": METRIC, "value": value, "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,  # one step = P pairs per GPU "higher_is_better": True,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {
-            "workload": "config3: synthetic 8x640x480 Frame360 pair -> stitch + 5-level pyramid x2 -> "
-                        "alignFrames360(PHOTO_DEPTH) levels 4..1 reference schedule + "
-                        f"{args.iters0} GN iterations at level 0",
-            "sensors": f"8x{args.cols}x{args.rows}", "sphere": f"{H0}x{W0}",
+            "workload": workload, "sensors": f"8x{args.cols}x{args.rows}", "sphere": f"{H0}x{W0}",
             "n_pyr": 5, "parallelism": f"pair-per-GPU dp{world}", "pairs_in_flight_per_gpu": P,
+            "pairs_per_step_per_gpu": P,
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -205,10 +262,10 @@ def main():
             "kernel": "k_icp_pass<PHOTO_DEPTH> (level 0)", "avg_launch_ms": avg_ms, "launches": l0_n,
             "bytes_per_launch": alg_bytes, "visible_frac": sso,
         },
+        "stage_ms_per_pair": {k: v / max(pairs_timed, 1) for k, v in stage.items()},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        pairs = [make_pair_frames(R, cal, seed, first + j) for j in range(2)]
-        out["cpu_baseline"] = cpu_baseline(R, cal, pairs, args.iters0)
+        out["cpu_baseline"] = cpu_baseline(R, cal, seed, first, args.workload, args.iters0)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -169,6 +169,11 @@ int r360_register_pbmap(r360_ctx* ctx, r360_frame* ref, r360_frame* trg, size_t 
 int r360_register(r360_ctx* ctx, r360_frame* ref, r360_frame* trg, const float guess[16],
                   const r360_icp_params* p, size_t max_match_planes, int mode, float pose[16],
                   float info[36], r360_icp_stats* st);
+/* Split form for pipelining several pairs: the PbMap stage runs at the call (it waits for the two
+ * frames' plane builds), the dense stage is enqueued on ctx's stream; _result waits for it. */
+int r360_register_async(r360_ctx* ctx, r360_frame* ref, r360_frame* trg, const float guess[16],
+                        const r360_icp_params* p, size_t max_match_planes, int mode);
+int r360_register_result(r360_ctx* ctx, float pose[16], float info[36], r360_icp_stats* st);
 /* SubgraphMatcher constraint tables (k_match_tables): unary [ns][nt], binary [(i*nt+j)][words]
  * bitsets over (k*nt+l).  Returns words.  Inspection/parity hook. */
 int r360_pbmap_match_tables(r360_ctx* ctx, r360_frame* ref, r360_frame* trg, size_t max_match_planes,

@@ -119,6 +119,8 @@ _SIGS = [
     ("r360_register_pbmap", C.c_int, [_P, _P, _P, C.c_size_t, C.c_int, _FP, _FP, _IP, C.c_int, _IP, _FP, _FP, _FP]),
     ("r360_register", C.c_int, [_P, _P, _P, _FP, C.POINTER(IcpParams), C.c_size_t, C.c_int, _FP, _FP,
                                 C.POINTER(IcpStats)]),
+    ("r360_register_async", C.c_int, [_P, _P, _P, _FP, C.POINTER(IcpParams), C.c_size_t, C.c_int]),
+    ("r360_register_result", C.c_int, [_P, _FP, _FP, C.POINTER(IcpStats)]),
     ("r360_pbmap_match_tables", C.c_int, [_P, _P, _P, C.c_size_t, C.c_int, _IP, _IP, _IP, _IP, _P, _P, C.c_int]),
     ("r360_frame_get_cloud", C.c_int, [_P, _FP, _P, _FP, _FP]),
     ("r360_frame_get_labels", C.c_int, [_P, _IP, _IP]),

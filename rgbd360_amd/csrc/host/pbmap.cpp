@@ -805,39 +805,67 @@ extern "C" int r360_register_pbmap(r360_ctx* ctx, r360_frame* ref, r360_frame* t
 // Register(): PbMap registration, then the dense refinement initialised with the rotOffset-conjugated
 // PbMap pose (OdometryKeyFrame360.cpp:167-171, 205, 244-254).  guess = fallback initial pose in the rig
 // frame when the PbMap registration fails (the caller's previous relative pose).
-extern "C" int r360_register(r360_ctx* ctx, r360_frame* ref, r360_frame* trg, const float guess[16],
-                             const r360_icp_params* p, size_t max_match_planes, int mode, float pose[16],
-                             float info[36], r360_icp_stats* st) {
-    CHECK_ARG(ctx && ref && trg && pose, "null arg");
+namespace {
+// rotOffset: rotation of angleOffset = 157.5 deg about x (OdometryRGBD360.cpp:138-139), column-major
+void rot_offset(float Ro[16], float Ri[16]) {
+    const float a = 157.5f;
+    const float c = (float)cos(a * R360_PI / 180), s = (float)sin(a * R360_PI / 180);
+    const float o[16] = {1, 0, 0, 0, 0, c, -s, 0, 0, s, c, 0, 0, 0, 0, 1};   // (1,2) = s, (2,1) = -s
+    const float t[16] = {1, 0, 0, 0, 0, c, s, 0, 0, -s, c, 0, 0, 0, 0, 1};   // inverse = transpose
+    memcpy(Ro, o, sizeof o);
+    memcpy(Ri, t, sizeof t);
+}
+void mul4(const float* A, const float* B, float* C) {   // Eigen Matrix4f product order
+    float out[16];
+    for (int col = 0; col < 4; ++col)
+        for (int r = 0; r < 4; ++r) {
+            float acc = A[r] * B[col * 4];
+            for (int k = 1; k < 4; ++k) acc += A[k * 4 + r] * B[col * 4 + k];
+            out[col * 4 + r] = acc;
+        }
+    memcpy(C, out, sizeof out);
+}
+}  // namespace
+
+extern "C" int r360_register_async(r360_ctx* ctx, r360_frame* ref, r360_frame* trg, const float guess[16],
+                                   const r360_icp_params* p, size_t max_match_planes, int mode) {
+    CHECK_ARG(ctx && ref && trg && p, "null arg");
     float pb[16], inf[36];
     for (int i = 0; i < 16; ++i) pb[i] = guess ? guess[i] : ((i % 5 == 0) ? 1.f : 0.f);
     for (int i = 0; i < 36; ++i) inf[i] = 0.f;
     const int good = r360_register_pbmap(ctx, ref, trg, max_match_planes, mode, pb, inf, nullptr, 0, nullptr, nullptr,
                                          nullptr, nullptr);
     if (good < 0) return good;
-    // rotOffset: rotation of angleOffset = 157.5 deg about x (OdometryRGBD360.cpp:138-139)
-    const float a = 157.5f;
-    const float c = (float)cos(a * R360_PI / 180), s = (float)sin(a * R360_PI / 180);
-    const float Ro[16] = {1, 0, 0, 0, 0, c, -s, 0, 0, s, c, 0, 0, 0, 0, 1};       // col-major: (1,2)=s, (2,1)=-s
-    const float Ri[16] = {1, 0, 0, 0, 0, c, s, 0, 0, -s, c, 0, 0, 0, 0, 1};       // its inverse (transpose)
-    auto mul = [](const float* A, const float* B, float* C) {
-        for (int col = 0; col < 4; ++col)
-            for (int r = 0; r < 4; ++r) {
-                float acc = A[r] * B[col * 4];
-                for (int k = 1; k < 4; ++k) acc += A[k * 4 + r] * B[col * 4 + k];
-                C[col * 4 + r] = acc;
-            }
-    };
-    float t1[16], init[16], dense[16], t2[16];
-    mul(Ro, pb, t1);
-    mul(t1, Ri, init);                              // rotOffset * pose * rotOffset^-1
-    float H[36], g[6];
-    const int rc = r360_align360(ctx, ref, trg, init, R360_PHOTO_DEPTH, 0, p, dense, H, g, st);
+    float Ro[16], Ri[16], t1[16], init[16];
+    rot_offset(Ro, Ri);
+    mul4(Ro, pb, t1);
+    mul4(t1, Ri, init);                             // rotOffset * pose * rotOffset^-1
+    if (int rc = r360_align360_async(ctx, ref, trg, init, R360_PHOTO_DEPTH, 0, p)) return rc;
+    ctx->reg_pending = 1;
+    ctx->reg_good = good;
+    memcpy(ctx->reg_info, inf, sizeof inf);
+    return 0;
+}
+
+extern "C" int r360_register_result(r360_ctx* ctx, float pose[16], float info[36], r360_icp_stats* st) {
+    CHECK_ARG(ctx && ctx->reg_pending && pose, "no registration pending");
+    ctx->reg_pending = 0;
+    float dense[16];
+    const int rc = r360_align360_result(ctx, dense, nullptr, nullptr, st);
     if (rc < 0) return rc;
-    mul(Ri, dense, t2);
-    mul(t2, Ro, pose);                              // rotOffset^-1 * dense * rotOffset
-    if (info) memcpy(info, inf, sizeof inf);
-    return good ? 0 : 1;
+    float Ro[16], Ri[16], t2[16];
+    rot_offset(Ro, Ri);
+    mul4(Ri, dense, t2);
+    mul4(t2, Ro, pose);                             // rotOffset^-1 * dense * rotOffset
+    if (info) memcpy(info, ctx->reg_info, sizeof ctx->reg_info);
+    return ctx->reg_good ? 0 : 1;
+}
+
+extern "C" int r360_register(r360_ctx* ctx, r360_frame* ref, r360_frame* trg, const float guess[16],
+                             const r360_icp_params* p, size_t max_match_planes, int mode, float pose[16],
+                             float info[36], r360_icp_stats* st) {
+    if (int rc = r360_register_async(ctx, ref, trg, guess, p, max_match_planes, mode)) return rc;
+    return r360_register_result(ctx, pose, info, st);
 }
 
 // ------------------------------------------------------------------ inspection (parity tests)

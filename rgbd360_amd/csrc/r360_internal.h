@@ -153,6 +153,9 @@ struct r360_ctx {
     unsigned long long* d_bin = nullptr;
     uint8_t* h_unary = nullptr;              // pinned
     unsigned long long* h_bin = nullptr;     // pinned
+    // Register() in flight (r360_register_async)
+    int reg_pending = 0, reg_good = 0;
+    float reg_info[36];
 };
 
 struct ClamsDev {
