@@ -13,6 +13,8 @@
 
 #include <algorithm>
 #include <chrono>
+#include <string>
+#include <thread>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -72,31 +74,28 @@ void convex_hull(HPlane& pl, const std::vector<P3>& pts) {
     const int n = int(pts.size());
     pl.hull.clear();
     if (!n) return;
-    std::vector<int> idx(n);
-    for (int i = 0; i < n; ++i) idx[i] = i;
-    std::sort(idx.begin(), idx.end(), [&](int u, int v) {
-        const float ux = pts[u].at(a), vx = pts[v].at(a), uy = pts[u].at(b), vy = pts[v].at(b);
-        if (ux != vx) return ux < vx;
-        if (uy != vy) return uy < vy;
-        return u < v;
+    struct Q { float x, y; int i; };
+    std::vector<Q> q(n);
+    for (int i = 0; i < n; ++i) q[i] = {pts[i].at(a), pts[i].at(b), i};
+    std::sort(q.begin(), q.end(), [](const Q& u, const Q& v) {
+        return u.x < v.x || (u.x == v.x && (u.y < v.y || (u.y == v.y && u.i < v.i)));
     });
-    auto turn = [&](int o, int p, int q) {
-        const double ox = pts[o].at(a), oy = pts[o].at(b);
-        return ((double)pts[p].at(a) - ox) * ((double)pts[q].at(b) - oy) -
-               ((double)pts[p].at(b) - oy) * ((double)pts[q].at(a) - ox);
+    auto turn = [&](int o, int p, int r) {
+        const double ox = q[o].x, oy = q[o].y;
+        return ((double)q[p].x - ox) * ((double)q[r].y - oy) - ((double)q[p].y - oy) * ((double)q[r].x - ox);
     };
-    std::vector<int> chain;
+    std::vector<int> chain;                 // positions in q
     chain.reserve(2 * n + 1);
     for (int i = 0; i < n; ++i) {           // lower hull
-        while (chain.size() >= 2 && turn(chain[chain.size() - 2], chain.back(), idx[i]) <= 0) chain.pop_back();
-        chain.push_back(idx[i]);
+        while (chain.size() >= 2 && turn(chain[chain.size() - 2], chain.back(), i) <= 0) chain.pop_back();
+        chain.push_back(i);
     }
     const size_t lower = chain.size() + 1;
     for (int i = n - 2; i >= 0; --i) {      // upper hull
-        while (chain.size() >= lower && turn(chain[chain.size() - 2], chain.back(), idx[i]) <= 0) chain.pop_back();
-        chain.push_back(idx[i]);
+        while (chain.size() >= lower && turn(chain[chain.size() - 2], chain.back(), i) <= 0) chain.pop_back();
+        chain.push_back(i);
     }
-    for (int i : chain) pl.hull.push_back(pts[i]);
+    for (int c : chain) pl.hull.push_back(pts[q[c].i]);
 }
 
 // computeMassCenterAndArea
@@ -248,42 +247,6 @@ void merge_into(HPlane& A, const HPlane& B) {
     descriptors(A);
 }
 
-// pcl::VoxelGrid (leaf 0.05): centroids of the occupied voxels in increasing voxel index.  Voxel
-// sums are exact in double (see plane_math.h), so the arrival order of the points is irrelevant.
-std::vector<P3> voxel_centroids(const std::vector<P3>& pts) {
-    std::vector<P3> out;
-    if (pts.empty()) return out;
-    const float inv = 1.0f / 0.05f;
-    P3 lo = pts[0], hi = pts[0];
-    for (const P3& p : pts) {
-        lo = {std::min(lo.x, p.x), std::min(lo.y, p.y), std::min(lo.z, p.z)};
-        hi = {std::max(hi.x, p.x), std::max(hi.y, p.y), std::max(hi.z, p.z)};
-    }
-    const long long b0 = (long long)std::floor(lo.x * inv), b1 = (long long)std::floor(lo.y * inv),
-                    b2 = (long long)std::floor(lo.z * inv);
-    const long long d0 = (long long)std::floor(hi.x * inv) - b0 + 1, d1 = (long long)std::floor(hi.y * inv) - b1 + 1;
-    std::vector<std::pair<long long, int>> key(pts.size());
-    for (size_t i = 0; i < pts.size(); ++i) {
-        const P3& p = pts[i];
-        key[i] = {((long long)std::floor(p.x * inv) - b0) + ((long long)std::floor(p.y * inv) - b1) * d0 +
-                      ((long long)std::floor(p.z * inv) - b2) * d0 * d1,
-                  int(i)};
-    }
-    std::sort(key.begin(), key.end());
-    for (size_t i = 0; i < key.size();) {
-        size_t j = i;
-        double s0 = 0, s1 = 0, s2 = 0;
-        for (; j < key.size() && key[j].first == key[i].first; ++j) {
-            const P3& p = pts[key[j].second];
-            s0 += p.x; s1 += p.y; s2 += p.z;
-        }
-        const double c = double(j - i);
-        out.push_back({float(s0 / c), float(s1 / c), float(s2 / c)});
-        i = j;
-    }
-    return out;
-}
-
 const float kMaxCurvature = 0.0013f;   // include/Miscellaneous.h:54
 const float kMinArea = 0.12f;          // :57
 const float kMaxElongation = 6.0f;     // :60
@@ -344,8 +307,11 @@ int plane_bufs_alloc(r360_frame* f) {
     R360_HIP(hipMalloc(&P.out, sizeof(PlaneOut) * 8 * R360_MAX_MODELS));
     P.contour_cap = 2 * T;
     P.vox_cap = T;
-    R360_HIP(hipMalloc(&P.contour, sizeof(float4) * P.contour_cap));
-    R360_HIP(hipMalloc(&P.vox, sizeof(float4) * P.vox_cap));
+    // the contour and voxel outputs are written by the kernels straight into pinned host memory (a
+    // few hundred KB per frame), so the host assembly needs no second device->host copy
+    R360_HIP(hipHostMalloc(&P.contour, sizeof(float4) * P.contour_cap));
+    R360_HIP(hipHostMalloc(&P.vox, sizeof(VoxOut) * P.vox_cap));
+    R360_HIP(hipEventCreateWithFlags(&P.done, hipEventDisableTiming | hipEventBlockingSync));
     R360_HIP(hipMalloc(&P.totals, sizeof(long) * 2));
     R360_HIP(hipMalloc(&P.err, sizeof(int)));
     R360_HIP(hipHostMalloc(&P.h_out, sizeof(PlaneOut) * 8 * R360_MAX_MODELS));
@@ -355,19 +321,35 @@ int plane_bufs_alloc(r360_frame* f) {
 
 void plane_bufs_free(r360_frame* f) {
     PlaneBufs& P = f->pl;
+    planes_join(f);
     void* dev[] = {P.cloud, P.rgb, P.nrm, P.dist0, P.dist, P.grids, P.parent, P.root, P.lab, P.labf, P.cnt, P.nlab,
-                   P.big, P.nbig, P.mom, P.models, P.nmodels, P.state, P.mask, P.out, P.contour, P.vox, P.totals, P.err};
+                   P.big, P.nbig, P.mom, P.models, P.nmodels, P.state, P.mask, P.out, P.totals, P.err};
     for (void* p : dev) hipFree(p);
+    hipHostFree(P.contour);
+    hipHostFree(P.vox);
     hipHostFree(P.h_out);
     hipHostFree(P.h_nmodels);
+    if (P.done) hipEventDestroy(P.done);
     P = PlaneBufs();
     delete f->pbmap;
     f->pbmap = nullptr;
 }
 
+int ctx_vhash_reserve(r360_ctx* ctx, long min_cells) {
+    long cap = 1;
+    while (cap < min_cells) cap <<= 1;
+    if (ctx->vhash_cap >= cap) return 0;
+    hipFree(ctx->d_vhash);
+    ctx->d_vhash = nullptr;
+    R360_HIP(hipMalloc(&ctx->d_vhash, sizeof(VoxCell) * cap));
+    ctx->vhash_cap = cap;
+    return 0;
+}
+
 // GPU part of getPlanes (enqueued on the ctx stream): cloud, filter, normals, segmentation
 int planes_enqueue(r360_frame* f) {
     if (plane_bufs_alloc(f)) return -1;
+    planes_join(f);
     PlaneBufs& P = f->pl;
     R360_HIP(hipMemsetAsync(P.err, 0, sizeof(int), f->ctx->stream));
     if (launch_cloud_normals(f)) return -1;
@@ -377,24 +359,55 @@ int planes_enqueue(r360_frame* f) {
     R360_HIP(hipMemcpyAsync(P.h_nmodels, P.nmodels, sizeof(int) * 8, hipMemcpyDeviceToHost, f->ctx->stream));
     R360_HIP(hipMemcpyAsync(P.h_nmodels + 8, P.err, sizeof(int), hipMemcpyDeviceToHost, f->ctx->stream));
     R360_HIP(hipMemcpyAsync(P.h_nmodels + 10, P.totals, sizeof(long) * 2, hipMemcpyDeviceToHost, f->ctx->stream));
+    R360_HIP(hipEventRecord(P.done, f->ctx->stream));
     delete f->pbmap;
     f->pbmap = nullptr;
+    // the per-plane host work of this frame runs on its own thread as soon as the GPU part is done,
+    // overlapping other frames' kernels and the caller
+    P.worker_rc = 0;
+    P.worker_err.clear();
+    P.worker = new std::thread([f] {
+        PlaneBufs& Q = f->pl;
+        if (hipEventSynchronize(Q.done) != hipSuccess) {
+            Q.worker_rc = -1;
+            Q.worker_err = "plane build: GPU work failed";
+            return;
+        }
+        Q.worker_rc = planes_assemble(f);
+        if (Q.worker_rc) Q.worker_err = r360_last_error();
+    });
     return 0;
 }
 
-// Host part of getPlanes: waits for the stream, then builds the PbMap (A8 + A9)
+void planes_join(r360_frame* f) {
+    PlaneBufs& P = f->pl;
+    if (P.worker) {
+        P.worker->join();
+        delete P.worker;
+        P.worker = nullptr;
+    }
+}
+
+// Host part of getPlanes: waits for the assembly thread
 int planes_finish(r360_frame* f) {
-    if (f->pbmap) return 0;
     PlaneBufs& P = f->pl;
     if (!P.cloud) { r360_set_error("planes were not built (R360_BUILD_PLANES)"); return -2; }
-    hipStream_t st = f->ctx->stream;
+    planes_join(f);
+    if (P.worker_rc) { r360_set_error("%s", P.worker_err.c_str()); return P.worker_rc; }
+    if (!f->pbmap) { r360_set_error("planes were not built (R360_BUILD_PLANES)"); return -2; }
+    return 0;
+}
+
+// Per-plane host part of getPlanes (A8 + A9), run by the frame's assembly thread once the GPU part
+// (including the pinned contour/voxel outputs) is complete
+int planes_assemble(r360_frame* f) {
+    PlaneBufs& P = f->pl;
     static const bool prof = getenv("R360_PBMAP_PROFILE") != nullptr;
     auto now = [] { return std::chrono::steady_clock::now(); };
     auto us = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
         return std::chrono::duration<double, std::micro>(b - a).count();
     };
     const auto t0 = now();
-    R360_HIP(hipStreamSynchronize(st));
     const auto t1 = now();
     const int err = P.h_nmodels[8];
     if (err) {
@@ -403,10 +416,8 @@ int planes_finish(r360_frame* f) {
         return -1;
     }
     const long* totals = reinterpret_cast<const long*>(P.h_nmodels + 10);
-    std::vector<float4> contour(totals[0]), vox(totals[1]);
-    if (totals[0]) R360_HIP(hipMemcpyAsync(contour.data(), P.contour, sizeof(float4) * totals[0], hipMemcpyDeviceToHost, st));
-    if (totals[1]) R360_HIP(hipMemcpyAsync(vox.data(), P.vox, sizeof(float4) * totals[1], hipMemcpyDeviceToHost, st));
-    R360_HIP(hipStreamSynchronize(st));
+    const float4* contour = P.contour;
+    const VoxOut* vox = P.vox;
     const auto t2 = now();
     const r360_calib* cal = f->calib;
     std::vector<std::vector<HPlane>> local(8);
@@ -428,12 +439,10 @@ int planes_finish(r360_frame* f) {
                     pts.push_back({q.x, q.y, q.z});
                 }
             } else {                                                    // "HULL 000" (:1017-1026)
-                std::vector<P3> inl;
-                for (int k = 0; k < O.n_vox; ++k) {
-                    const float4 q = vox[O.vox_off + k];
-                    inl.push_back({q.x, q.y, q.z});
-                }
-                pts = voxel_centroids(inl);
+                // VoxelGrid centroids from k_vox_*, in increasing voxel index (PCL's output order)
+                std::vector<VoxOut> v(vox + O.vox_off, vox + O.vox_off + O.n_vox);
+                std::sort(v.begin(), v.end(), [](const VoxOut& a, const VoxOut& b) { return a.key < b.key; });
+                for (const VoxOut& q : v) pts.push_back({q.x, q.y, q.z});
             }
             convex_hull(pl, pts);
             area_and_center(pl);

@@ -114,7 +114,7 @@ extern "C" void r360_ctx_destroy(r360_ctx* c) {
     hipFree(c->d_state);
     hipFree(c->d_partials);
     hipHostFree(c->h_state);
-    hipFree(c->d_match_desc); hipFree(c->d_unary); hipFree(c->d_bin);
+    hipFree(c->d_match_desc); hipFree(c->d_unary); hipFree(c->d_bin); hipFree(c->d_vhash);
     hipHostFree(c->h_unary); hipHostFree(c->h_bin);
     hipStreamDestroy(c->stream);
     delete c;

@@ -11,8 +11,9 @@
 //                  per-lane chunk summaries; closeness to every model is precomputed per pixel as a
 //                  bit mask (k_refine_init)
 //   k_model_stats  final inlier moments (rig frame) + colour sums + the region's first pixel
-//   k_trace        findLabeledRegionBoundary (Moore-neighbour trace), one thread per region
-//   k_gather_vox   inlier points of regions without a contour (VoxelGrid fallback, Frame360.h:1017-1026)
+//   k_trace        findLabeledRegionBoundary (Moore-neighbour trace) on an LDS membership bitmap
+//   k_vox_*        VoxelGrid of regions without a contour (Frame360.h:1017-1026): (region, voxel) hash
+//                  table with exact double sums, compacted into per-region voxel lists
 // Arithmetic follows oracle/src/planes_oracle.cpp and pbmap_oracle.cpp; see rgbd360_amd/csrc/plane_math.h.
 #include "../r360_internal.h"
 #include "../plane_math.h"
@@ -360,11 +361,12 @@ __global__ void __launch_bounds__(64) k_refine(int8_t* __restrict__ state_all,
     };
     // ---------------- first sweep: top->bottom, left->right; right and down checks
     {
-        int cur[K], nxt[K], F[K];
-        unsigned long long cm[K], nm[K];
+        int cur[K], nxt[K], nn[K], F[K];
+        unsigned long long cm[K], nm[K], nnm[K];
         load(0, cur, cm, +1);
+        if (h > 1) load(1, nxt, nm, +1);
         for (int r = 0; r < h - 1; ++r) {
-            load(r + 1, nxt, nm, +1);
+            if (r + 2 < h) load(r + 2, nn, nnm, +1);     // prefetch: consumed one row later
             resolve_chain<K>(cur, cm, F);
             // original state of the column to the right of each of this lane's columns
             const int right_of_last = __shfl(cur[0], (lane + 1) & 63, 64);
@@ -379,7 +381,7 @@ __global__ void __launch_bounds__(64) k_refine(int8_t* __restrict__ state_all,
             }
             store(r, F, +1);
 #pragma unroll
-            for (int k = 0; k < K; ++k) { cur[k] = nxt[k]; cm[k] = nm[k]; }
+            for (int k = 0; k < K; ++k) { cur[k] = nxt[k]; cm[k] = nm[k]; nxt[k] = nn[k]; nm[k] = nnm[k]; }
         }
         store(h - 1, cur, +1);
     }
@@ -388,13 +390,14 @@ __global__ void __launch_bounds__(64) k_refine(int8_t* __restrict__ state_all,
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     // ---------------- second sweep: bottom->top, right->left; left and up checks
     {
-        int cur[K], up[K], F[K];
-        unsigned long long cm[K], um[K];
+        int cur[K], up[K], uu[K], F[K];
+        unsigned long long cm[K], um[K], uum[K];
         load(h - 1, cur, cm, -1);
+        if (h > 1) load(h - 2, up, um, -1);
         const int cl = w - 1;                                    // owner of column w-1 (walking order)
         const int own_lane = 63 - cl / K, own_k = K - 1 - cl % K;
         for (int r = h - 1; r >= 1; --r) {
-            load(r - 1, up, um, -1);
+            if (r - 2 >= 0) load(r - 2, uu, uum, -1);    // prefetch: consumed one row later
             resolve_chain<K>(cur, cm, F);
             // original state of the column to the left (walking order: the next element)
             const int left_of_last = __shfl(cur[0], (lane + 1) & 63, 64);
@@ -431,7 +434,7 @@ __global__ void __launch_bounds__(64) k_refine(int8_t* __restrict__ state_all,
             }
             store(r, F, -1);
 #pragma unroll
-            for (int k = 0; k < K; ++k) { cur[k] = up[k]; cm[k] = um[k]; }
+            for (int k = 0; k < K; ++k) { cur[k] = up[k]; cm[k] = um[k]; up[k] = uu[k]; um[k] = uum[k]; }
         }
         store(0, cur, -1);
     }
@@ -454,6 +457,7 @@ __global__ void __launch_bounds__(MOM_TPB) k_model_stats(const float4* __restric
                                                         const int* __restrict__ nmodels, const float* __restrict__ rt8,
                                                         PlaneOut* __restrict__ out) {
     __shared__ MomShared sh;
+    __shared__ float sbox[6][MOM_TPB];
     __shared__ int smin[MOM_TPB];
     const int s = blockIdx.y, m = blockIdx.x;
     if (m >= nmodels[s]) return;
@@ -464,10 +468,13 @@ __global__ void __launch_bounds__(MOM_TPB) k_model_stats(const float4* __restric
     r360p::Moments mo;
     r360p::moments_zero(mo);
     int first = N;
+    float bx[6] = {3.4e38f, 3.4e38f, 3.4e38f, -3.4e38f, -3.4e38f, -3.4e38f};   // local-frame bounds
     for (int j = threadIdx.x; j < N; j += MOM_TPB) {
         if (lab[base + j] == L && j < first) first = j;
         if (labf[base + j] == L) {
             const float4 p = cloud[base + j];
+            bx[0] = fminf(bx[0], p.x); bx[1] = fminf(bx[1], p.y); bx[2] = fminf(bx[2], p.z);
+            bx[3] = fmaxf(bx[3], p.x); bx[4] = fmaxf(bx[4], p.y); bx[5] = fmaxf(bx[5], p.z);
             // Eigen Affine3f * Vector3f (pcl::transformPointCloud), column-major T
             const float x = T[0] * p.x + T[4] * p.y + T[8] * p.z + T[12];
             const float y = T[1] * p.x + T[5] * p.y + T[9] * p.z + T[13];
@@ -478,9 +485,14 @@ __global__ void __launch_bounds__(MOM_TPB) k_model_stats(const float4* __restric
         }
     }
     smin[threadIdx.x] = first;
+    for (int k = 0; k < 6; ++k) sbox[k][threadIdx.x] = bx[k];
     __syncthreads();
     for (int o = MOM_TPB / 2; o > 0; o >>= 1) {
-        if ((int)threadIdx.x < o) smin[threadIdx.x] = min(smin[threadIdx.x], smin[threadIdx.x + o]);
+        if ((int)threadIdx.x < o) {
+            smin[threadIdx.x] = min(smin[threadIdx.x], smin[threadIdx.x + o]);
+            for (int k = 0; k < 3; ++k) sbox[k][threadIdx.x] = fminf(sbox[k][threadIdx.x], sbox[k][threadIdx.x + o]);
+            for (int k = 3; k < 6; ++k) sbox[k][threadIdx.x] = fmaxf(sbox[k][threadIdx.x], sbox[k][threadIdx.x + o]);
+        }
         __syncthreads();
     }
     block_reduce_moments(mo, &sh);
@@ -489,31 +501,66 @@ __global__ void __launch_bounds__(MOM_TPB) k_model_stats(const float4* __restric
         O.model = M;
         O.stats = mo;
         O.start = smin[0];
+        for (int k = 0; k < 3; ++k) { O.bmin[k] = sbox[k][0]; O.bmax[k] = sbox[k + 3][0]; }
         O.n_contour = 0;
         O.contour_off = 0;
         O.n_vox = 0;
+        O.vox_fill = 0;
         O.vox_off = 0;
     }
 }
 
-// findLabeledRegionBoundary; mode 0 counts, mode 1 writes the contour points (local frame)
-__global__ void k_trace(const int* __restrict__ labf, const float4* __restrict__ cloud, int w, int h,
-                        const int* __restrict__ nmodels, PlaneOut* __restrict__ out, float4* __restrict__ pool,
-                        long pool_cap, int mode, int* __restrict__ err) {
-    const int s = blockIdx.x;
-    const int m = threadIdx.x;
+// findLabeledRegionBoundary on a per-region membership bitmap in LDS (one workgroup per region);
+// mode 0 counts, mode 1 writes the contour points (local frame).  The bitmap has a one-pixel zero
+// border, so a step reads its 3x3 neighbourhood with six independent LDS loads and no bounds tests.
+__global__ void __launch_bounds__(256) k_trace(const int* __restrict__ labf, const float4* __restrict__ cloud, int w,
+                                              int h, const int* __restrict__ nmodels, PlaneOut* __restrict__ out,
+                                              float4* __restrict__ pool, long pool_cap, int mode,
+                                              int* __restrict__ err) {
+    extern __shared__ unsigned bits[];
+    const int s = blockIdx.y, m = blockIdx.x;
     if (m >= nmodels[s]) return;
     PlaneOut& O = out[s * R360_MAX_MODELS + m];
-    const long N = (long)w * h;
-    const int* Lb = labf + s * N;
-    const float4* P = cloud + s * N;
+    const int N = w * h;
+    const int RW = (w + 2 + 31) / 32 + 1;                  // words per padded row (+1 for the pair reads)
+    const int NW = (h + 2) * RW;
+    const int* Lb = labf + (long)s * N;
+    const int label = O.model.label;
+    for (int q = threadIdx.x; q < NW; q += blockDim.x) {
+        const int yy = q / RW, cw = q - (q / RW) * RW;
+        const int y = yy - 1;
+        unsigned word = 0;
+        if (y >= 0 && y < h)
+            for (int b = 0; b < 32; ++b) {
+                const int x = cw * 32 + b - 1;
+                if (x >= 0 && x < w && Lb[y * w + x] == label) word |= 1u << b;
+            }
+        bits[q] = word;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    // bits of padded columns px..px+2 in padded row yy
+    auto row3 = [&](int px, int yy) -> unsigned {
+        const int q = yy * RW + (px >> 5);
+        const unsigned long long v = (unsigned long long)bits[q] | ((unsigned long long)bits[q + 1] << 32);
+        return (unsigned)(v >> (px & 31)) & 7u;
+    };
+    const float4* P = cloud + (long)s * N;
     const int dxs[8] = {-1, -1, 0, 1, 1, 1, 0, -1}, dys[8] = {0, -1, -1, -1, 0, 1, 1, 1};
+    // neighbour d of the 3x3 block (rows r0 (y-1), r1 (y), r2 (y+1); bit i = column x-1+i)
+    auto nbit = [&](unsigned r0, unsigned r1, unsigned r2, int d) -> int {
+        const int dx = dxs[d] + 1, dy = dys[d];
+        const unsigned r = dy < 0 ? r0 : (dy > 0 ? r2 : r1);
+        return (r >> dx) & 1;
+    };
     const int start = O.start;
-    const int label = Lb[start];
     int cx = start % w, cy = start / w, cidx = start, dir = -1;
-    for (int d = 0; d < 8; ++d) {
-        const int x = cx + dxs[d], y = cy + dys[d];
-        if (x >= 0 && x < w && y >= 0 && y < h && Lb[cidx + dys[d] * w + dxs[d]] != label) { dir = d; break; }
+    {
+        const unsigned r0 = row3(cx, cy), r1 = row3(cx, cy + 1), r2 = row3(cx, cy + 2);
+        for (int d = 0; d < 8; ++d) {
+            const int x = cx + dxs[d], y = cy + dys[d];
+            if (x >= 0 && x < w && y >= 0 && y < h && !nbit(r0, r1, r2, d)) { dir = d; break; }
+        }
     }
     if (dir < 0) {
         if (mode == 0) O.n_contour = 0;
@@ -521,62 +568,133 @@ __global__ void k_trace(const int* __restrict__ labf, const float4* __restrict__
     }
     long n = 0;
     const long off = mode ? O.contour_off : 0;
-    const long max_len = 8 * N;
+    const long max_len = 8L * N;
     if (mode && off + n < pool_cap) pool[off + n] = P[start];
     ++n;
     do {
+        const unsigned r0 = row3(cx, cy), r1 = row3(cx, cy + 1), r2 = row3(cx, cy + 2);
+        unsigned mask8 = 0;
+#pragma unroll
+        for (int d = 0; d < 8; ++d) mask8 |= (unsigned)nbit(r0, r1, r2, d) << d;
         int nd = 0;
         for (int d = 1; d <= 8; ++d) {
             nd = (dir + d) & 7;
-            const int x = cx + dxs[nd], y = cy + dys[nd];
-            if (x >= 0 && x < w && y >= 0 && y < h && Lb[cidx + dys[nd] * w + dxs[nd]] == label) break;
+            if ((mask8 >> nd) & 1) break;
         }
         dir = (nd + 4) & 7;
         cidx += dys[nd] * w + dxs[nd];
         cx += dxs[nd];
         cy += dys[nd];
-        if (mode) {
-            if (off + n < pool_cap) pool[off + n] = P[cidx];
-        }
+        if (mode && off + n < pool_cap) pool[off + n] = P[cidx];
         ++n;
         if (n > max_len) { atomicOr(err, 8); break; }
     } while (cidx != start);
     if (mode == 0) O.n_contour = (int)n;
 }
 
-// prefix offsets of the contour and voxel-fallback pools (single thread)
+// contour pool offsets (single thread)
 __global__ void k_alloc(const int* __restrict__ nmodels, PlaneOut* __restrict__ out, long* __restrict__ totals,
-                        long contour_cap, long vox_cap, int* __restrict__ err) {
+                        long contour_cap, int* __restrict__ err) {
     if (threadIdx.x != 0) return;
-    long co = 0, vo = 0;
+    long co = 0;
     for (int s = 0; s < 8; ++s)
         for (int m = 0; m < nmodels[s]; ++m) {
             PlaneOut& O = out[s * R360_MAX_MODELS + m];
             O.contour_off = co;
             co += O.n_contour;
-            O.vox_off = vo;
-            O.n_vox = 0;
-            if (O.n_contour == 0) vo += O.stats.n;
         }
     totals[0] = co;
-    totals[1] = vo;
-    if (co > contour_cap || vo > vox_cap) atomicOr(err, 16);
+    if (co > contour_cap) atomicOr(err, 16);
 }
 
-__global__ void k_gather_vox(const int* __restrict__ labf, const float4* __restrict__ cloud, int N,
-                             const int* __restrict__ nmodels, PlaneOut* __restrict__ out, float4* __restrict__ pool,
-                             long pool_cap) {
-    const int s = blockIdx.y, m = blockIdx.x;
-    if (m >= nmodels[s]) return;
-    PlaneOut& O = out[s * R360_MAX_MODELS + m];
-    if (O.n_contour != 0) return;
-    const int L = O.model.label;
-    const long base = (long)s * N;
-    for (int j = threadIdx.x; j < N; j += blockDim.x)
-        if (labf[base + j] == L) {
-            const int k = atomicAdd(&O.n_vox, 1);
-            if (O.vox_off + k < pool_cap) pool[O.vox_off + k] = cloud[base + j];
+// pcl::VoxelGrid (leaf 0.05) of the inliers of regions without a contour (Frame360.h:1017-1026):
+// points are hashed by (region, voxel index); voxel sums of <= a few hundred coordinates with ulps
+// >= 2^-36 are exact in double, so atomic accumulation is order-free and equals the sequential sum.
+__device__ __forceinline__ unsigned long long vhash(unsigned long long tag, unsigned long long mask) {
+    return (tag * 0x9E3779B97F4A7C15ull >> 20) & mask;
+}
+
+__global__ void k_vox_hash(const float4* __restrict__ cloud, const int8_t* __restrict__ state, int N,
+                           PlaneOut* __restrict__ out, VoxCell* __restrict__ tab, unsigned long long mask,
+                           int* __restrict__ err) {
+    const long total = 8L * N;
+    const float inv = 1.0f / 0.05f;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int m = state[i];
+        if (m < 0) continue;
+        const int s = (int)(i / N);
+        PlaneOut& O = out[s * R360_MAX_MODELS + m];
+        if (O.n_contour != 0) continue;
+        const float4 p = cloud[i];
+        const long long b0 = (long long)floorf(O.bmin[0] * inv), b1 = (long long)floorf(O.bmin[1] * inv),
+                        b2 = (long long)floorf(O.bmin[2] * inv);
+        const long long d0 = (long long)floorf(O.bmax[0] * inv) - b0 + 1, d1 = (long long)floorf(O.bmax[1] * inv) - b1 + 1;
+        const long long key = ((long long)floorf(p.x * inv) - b0) + ((long long)floorf(p.y * inv) - b1) * d0 +
+                              ((long long)floorf(p.z * inv) - b2) * d0 * d1;
+        const unsigned long long tag = ((unsigned long long)(s * R360_MAX_MODELS + m + 1) << 48) | (unsigned long long)key;
+        unsigned long long hsh = vhash(tag, mask);
+        for (unsigned long long probe = 0;; ++probe) {
+            const unsigned long long prev = atomicCAS(&tab[hsh].tag, 0ull, tag);
+            if (prev == 0ull) { atomicAdd(&O.n_vox, 1); break; }
+            if (prev == tag) break;
+            hsh = (hsh + 1) & mask;
+            if (probe > mask) { atomicOr(err, 16); hsh = ~0ull; break; }
         }
+        if (hsh == ~0ull) continue;
+        atomicAdd(&tab[hsh].s[0], (double)p.x);
+        atomicAdd(&tab[hsh].s[1], (double)p.y);
+        atomicAdd(&tab[hsh].s[2], (double)p.z);
+        atomicAdd(&tab[hsh].cnt, 1u);
+    }
+}
+
+__global__ void k_vox_alloc(const int* __restrict__ nmodels, PlaneOut* __restrict__ out, long* __restrict__ totals,
+                            long vox_cap, int* __restrict__ err) {
+    if (threadIdx.x != 0) return;
+    long vo = 0;
+    for (int s = 0; s < 8; ++s)
+        for (int m = 0; m < nmodels[s]; ++m) {
+            PlaneOut& O = out[s * R360_MAX_MODELS + m];
+            O.vox_off = vo;
+            vo += O.n_vox;
+        }
+    totals[1] = vo;
+    if (vo > vox_cap) atomicOr(err, 16);
+}
+
+__global__ void k_vox_compact(const VoxCell* __restrict__ tab, unsigned long long cells, PlaneOut* __restrict__ out,
+                              VoxOut* __restrict__ pool, long pool_cap) {
+    for (unsigned long long c = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; c < cells;
+         c += (unsigned long long)gridDim.x * blockDim.x) {
+        const unsigned long long tag = tab[c].tag;
+        const int sm = tag ? (int)(tag >> 48) - 1 : -1;
+        // one atomic per (wave, region): lanes of the same region take consecutive slots
+        int pos = 0;
+        bool pending = sm >= 0;
+        while (__any(pending)) {
+            const int leader = __ffsll((long long)__ballot(pending)) - 1;
+            const int lsm = __shfl(sm, leader, 64);
+            const bool mine = pending && sm == lsm;
+            const unsigned long long same = __ballot(mine);
+            int basepos = 0;
+            if ((int)(threadIdx.x & 63) == leader) basepos = atomicAdd(&out[lsm].vox_fill, __popcll(same));
+            basepos = __shfl(basepos, leader, 64);
+            if (mine) {
+                pos = basepos + __popcll(same & ((1ull << (threadIdx.x & 63)) - 1));
+                pending = false;
+            }
+        }
+        if (sm < 0) continue;
+        PlaneOut& O = out[sm];
+        const double cnt = (double)tab[c].cnt;
+        VoxOut v;
+        v.key = (long long)(tag & ((1ull << 48) - 1));
+        v.x = (float)(tab[c].s[0] / cnt);
+        v.y = (float)(tab[c].s[1] / cnt);
+        v.z = (float)(tab[c].s[2] / cnt);
+        v.pad = 0.f;
+        if (O.vox_off + pos < pool_cap) pool[O.vox_off + pos] = v;
+    }
 }
 
 }  // namespace
@@ -626,13 +744,22 @@ int launch_segmentation(r360_frame* f) {
     slot = timing_begin(ctx, "k_model_stats");
     hipLaunchKernelGGL(k_model_stats, dim3(R360_MAX_MODELS, 8), dim3(MOM_TPB), 0, st, P.cloud, P.rgb, P.lab, P.labf, N,
                        P.models, P.nmodels, f->calib->d_rt, P.out);
-    hipLaunchKernelGGL(k_trace, dim3(8), dim3(R360_MAX_MODELS), 0, st, P.labf, P.cloud, w, h, P.nmodels, P.out,
+    const size_t lds = sizeof(unsigned) * (size_t)(h + 2) * ((w + 2 + 31) / 32 + 1);
+    hipLaunchKernelGGL(k_trace, dim3(R360_MAX_MODELS, 8), dim3(256), lds, st, P.labf, P.cloud, w, h, P.nmodels, P.out,
                        P.contour, P.contour_cap, 0, P.err);
-    hipLaunchKernelGGL(k_alloc, dim3(1), dim3(64), 0, st, P.nmodels, P.out, P.totals, P.contour_cap, P.vox_cap, P.err);
-    hipLaunchKernelGGL(k_trace, dim3(8), dim3(R360_MAX_MODELS), 0, st, P.labf, P.cloud, w, h, P.nmodels, P.out,
+    hipLaunchKernelGGL(k_alloc, dim3(1), dim3(64), 0, st, P.nmodels, P.out, P.totals, P.contour_cap, P.err);
+    hipLaunchKernelGGL(k_trace, dim3(R360_MAX_MODELS, 8), dim3(256), lds, st, P.labf, P.cloud, w, h, P.nmodels, P.out,
                        P.contour, P.contour_cap, 1, P.err);
-    hipLaunchKernelGGL(k_gather_vox, dim3(R360_MAX_MODELS, 8), dim3(256), 0, st, P.labf, P.cloud, N, P.nmodels, P.out,
-                       P.vox, P.vox_cap);
+    timing_end(ctx, slot);
+    R360_HIP(hipGetLastError());
+    slot = timing_begin(ctx, "k_voxel");
+    if (ctx_vhash_reserve(ctx, 12L * N)) return -1;
+    R360_HIP(hipMemsetAsync(ctx->d_vhash, 0, sizeof(VoxCell) * ctx->vhash_cap, st));
+    hipLaunchKernelGGL(k_vox_hash, dim3(blocks), dim3(256), 0, st, P.cloud, P.state, N, P.out, ctx->d_vhash,
+                       (unsigned long long)(ctx->vhash_cap - 1), P.err);
+    hipLaunchKernelGGL(k_vox_alloc, dim3(1), dim3(64), 0, st, P.nmodels, P.out, P.totals, P.vox_cap, P.err);
+    hipLaunchKernelGGL(k_vox_compact, dim3(2048), dim3(256), 0, st, ctx->d_vhash, (unsigned long long)ctx->vhash_cap,
+                       P.out, P.vox, P.vox_cap);
     timing_end(ctx, slot);
     R360_HIP(hipGetLastError());
     return 0;

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string>
+#include <thread>
 #include <vector>
 #include "../../include/rgbd360_hip.h"
 
@@ -88,8 +89,20 @@ struct alignas(16) PlaneOut {
     r360p::Moments stats;   // final inliers: rig-frame moments + colour sums
     PlaneModel model;
     int start;              // inlier_indices[i][0]
-    int n_contour, n_vox;
+    int n_contour, n_vox, vox_fill;
+    float bmin[3], bmax[3]; // local-frame bounds of the inliers (VoxelGrid)
     long contour_off, vox_off;
+};
+
+// (region, voxel) hash cell of the VoxelGrid fallback and its compacted output
+struct VoxCell {
+    unsigned long long tag;  // 0 = empty; ((sensor*64 + model + 1) << 48) | voxel index
+    double s[3];
+    unsigned cnt, pad;
+};
+struct VoxOut {
+    long long key;
+    float x, y, z, pad;
 };
 
 // Device buffers of a frame's plane half (allocated on the first CLOUD/PLANES build)
@@ -119,13 +132,18 @@ struct PlaneBufs {
     PlaneOut* out = nullptr;         // [8][R360_MAX_MODELS]
     float4* contour = nullptr;       // contour pool
     long contour_cap = 0;
-    float4* vox = nullptr;           // voxel-fallback point pool
+    VoxOut* vox = nullptr;           // voxel-fallback centroids
     long vox_cap = 0;
     long* totals = nullptr;          // [2] pool usage
     int* err = nullptr;              // error bits
     // pinned host mirrors
     PlaneOut* h_out = nullptr;
     int* h_nmodels = nullptr;        // [8], then err at [8], totals at (long*)(h_nmodels + 10)
+    // host assembly thread (planes_enqueue -> planes_finish)
+    hipEvent_t done = nullptr;
+    std::thread* worker = nullptr;
+    int worker_rc = 0;
+    std::string worker_err;
 };
 struct PbMapHost;                    // host PbMap (host/pbmap.cpp)
 
@@ -153,6 +171,9 @@ struct r360_ctx {
     unsigned long long* d_bin = nullptr;
     uint8_t* h_unary = nullptr;              // pinned
     unsigned long long* h_bin = nullptr;     // pinned
+    // VoxelGrid hash table (plane builds of the frames on this ctx)
+    VoxCell* d_vhash = nullptr;
+    long vhash_cap = 0;
     // Register() in flight (r360_register_async)
     int reg_pending = 0, reg_good = 0;
     float reg_info[36];
@@ -213,7 +234,10 @@ int launch_segmentation(r360_frame* f);
 int plane_bufs_alloc(r360_frame* f);
 void plane_bufs_free(r360_frame* f);
 int planes_enqueue(r360_frame* f);
+int ctx_vhash_reserve(r360_ctx* ctx, long min_cells);
 int planes_finish(r360_frame* f);
+int planes_assemble(r360_frame* f);
+void planes_join(r360_frame* f);
 
 // timing helpers (host_runtime.cpp)
 int  timing_begin(r360_ctx* ctx, const char* name);
