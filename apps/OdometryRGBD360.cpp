@@ -1,0 +1,91 @@
+// OdometryRGBD360 — the reference's Registration/OdometryRGBD360.cpp / OdometryKeyFrame360.cpp loop over
+// the MI355X library: for each new Frame360, PbMap registration against the previous keyframe, dense
+// RegisterPhotoICP refinement initialised with the rotOffset-conjugated PbMap pose (Register()), the
+// |t| < 0.4 m frame skip (:230-238) and the trajectory prefix product currentPose *= rigidTransf (:257).
+//   usage: OdometryRGBD360 <dir with sphere_images_<n>.bin> [first] [step] [calib_dir]
+//          OdometryRGBD360 --synthetic <n_frames>        (procedural room, 8 x 480x640, no I/O)
+#include <rgbd360/rgbd360.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <memory>
+#include <string>
+#include <sys/stat.h>
+#include <vector>
+
+static bool fexists(const std::string& p) { struct stat st; return stat(p.c_str(), &st) == 0; }
+
+int main(int argc, char** argv) {
+    if (argc < 2) {
+        std::fprintf(stderr, "usage: %s <dir> [first] [step] [calib_dir] | --synthetic <n_frames>\n", argv[0]);
+        return 1;
+    }
+    const bool synthetic = std::string(argv[1]) == "--synthetic";
+    const int n_synth = synthetic && argc > 2 ? std::atoi(argv[2]) : 32;
+    const std::string dir = argv[1];
+    int frame = !synthetic && argc > 2 ? std::atoi(argv[2]) : 1;
+    const int step = !synthetic && argc > 3 ? std::atoi(argv[3]) : 1;
+    const std::string calib_dir = !synthetic && argc > 4 ? argv[4] : std::string(RGBD360_DATA_DIR) + "/calib";
+    try {
+        r360::Context ctx(0);
+        r360::Calib360 calib(ctx, synthetic ? 480 : 240, synthetic ? 640 : 320);
+        calib.loadExtrinsicCalibration(calib_dir + "/Extrinsics");
+        if (!synthetic) calib.loadIntrinsicCalibration(calib_dir + "/Intrinsics");
+        r360_icp_params icp;
+        r360_icp_default_params(&icp);
+        icp.n_pyr = 5;                                       // OdometryRGBD360.cpp:92-95
+        icp.std_dev_photo = 3.0f / 255;
+        const uint32_t seed = 360u << 16;
+        std::vector<uint8_t> bgr;
+        std::vector<uint16_t> depth;
+        auto load = [&](r360::Frame360& f, int idx) -> bool {
+            if (synthetic) {
+                if (idx >= n_synth) return false;
+                float P[16];
+                r360_synth_path_pose(seed, idx, P);
+                bgr.resize(size_t(8) * 480 * 640 * 3);
+                depth.resize(size_t(8) * 480 * 640);
+                r360::check(r360_synth_frame(calib.get(), seed, P, bgr.data(), depth.data()), "synth_frame");
+                f.upload(bgr.data(), depth.data());
+                return true;
+            }
+            const std::string path = dir + "/sphere_images_" + std::to_string(idx) + ".bin";
+            if (!fexists(path)) return false;
+            f.loadFrame(path);
+            return true;
+        };
+        auto build = [&](r360::Frame360& f) {
+            f.getPlanes();
+            f.stitchSphericalImage();
+        };
+        std::unique_ptr<r360::Frame360> f1(new r360::Frame360(&calib));
+        if (!load(*f1, frame)) { std::fprintf(stderr, "no first frame\n"); return 3; }
+        build(*f1);
+        r360::RegisterRGBD360 registerer(ctx, "config_files/configLocaliser_sphericalOdometry.ini");
+        r360::Matrix4f currentPose, prevRel;
+        int n_kf = 1;
+        for (int idx = frame + step;; idx += step) {
+            std::unique_ptr<r360::Frame360> f2(new r360::Frame360(&calib));
+            if (!load(*f2, idx)) break;
+            build(*f2);
+            r360::Matrix4f rigidTransf;
+            const bool pbmap_ok = registerer.Register(f1.get(), f2.get(), icp, rigidTransf, prevRel, 25,
+                                                      r360::RegisterRGBD360::PLANAR_3DoF);
+            const float dist = std::sqrt(rigidTransf(0, 3) * rigidTransf(0, 3) + rigidTransf(1, 3) * rigidTransf(1, 3) +
+                                         rigidTransf(2, 3) * rigidTransf(2, 3));
+            std::printf("frame %d: PbMap %s, dist %.3f\n", idx, pbmap_ok ? "ok" : "failed (dense from prior)", dist);
+            if (dist < 0.4f && !synthetic) continue;         // skip frames too close to the keyframe (:230-238)
+            currentPose = currentPose * rigidTransf;          // :257
+            prevRel = rigidTransf;
+            f1 = std::move(f2);
+            ++n_kf;
+            std::printf("  pose t = (%.3f %.3f %.3f)\n", currentPose(0, 3), currentPose(1, 3), currentPose(2, 3));
+        }
+        std::printf("%d keyframes\n", n_kf);
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "error: %s\n", e.what());
+        return 2;
+    }
+    return 0;
+}

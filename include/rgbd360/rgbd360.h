@@ -1,0 +1,283 @@
+// rgbd360/rgbd360.h — C++ façade of librgbd360_hip.so with the reference's class names and method
+// signatures for the registration hot path:
+//
+//   Calib360          include/Calib360.h:44-132
+//   Frame360          include/Frame360.h:93-1150   loadFrame / undistort / stitchSphericalImage /
+//                                                  buildSphereCloud / getPlanes / planes
+//   RegisterPhotoICP  include/RegisterPhotoICP.h   setters :224-269, setSourceFrame/setTargetFrame
+//                                                  :480-516, alignFrames360 :4519, getOptimalPose :273,
+//                                                  getHessian/getGradient :279-288
+//   RegisterRGBD360   include/RegisterRGBD360.h    ctor(ini) :97, setReference/setTarget :111/:161,
+//                                                  RegisterPbMap :276, getPose :199, getCovMat :208,
+//                                                  getInfoMat :219, getMatchedPlanes :242,
+//                                                  getAreaMatched :251, areaSource/areaTarget :91-94,
+//                                                  Register() = OdometryKeyFrame360.cpp:205-254
+//
+// Header-only; every body is a call into the C-ABI (include/rgbd360_hip.h).  Matrices are the
+// column-major Eigen layout; r360::Matrix4f / Matrix6f are minimal stand-ins with Eigen's (row, col)
+// accessors and data() — define RGBD360_WITH_EIGEN to use Eigen::Matrix4f / Matrix<float,6,6>.
+// Differences from the reference surface, all forced by the GPU-resident design:
+//   * RegisterPhotoICP::setSourceFrame/setTargetFrame take the Frame360 (its sphere and pyramid live
+//     in HBM) instead of the cv::Mat sphereRGB/sphereDepth pair;
+//   * objects are bound to an r360::Context (one GPU + HIP stream); errors throw r360::Error.
+#pragma once
+#include <rgbd360_hip.h>
+
+#include <cstring>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#ifdef RGBD360_WITH_EIGEN
+#include <Eigen/Dense>
+#endif
+
+namespace r360 {
+
+struct Error : std::runtime_error {
+    explicit Error(const std::string& what) : std::runtime_error(what + ": " + r360_last_error()) {}
+};
+inline int check(int rc, const char* what) {
+    if (rc < 0) throw Error(what);
+    return rc;
+}
+
+#ifdef RGBD360_WITH_EIGEN
+typedef Eigen::Matrix4f Matrix4f;
+typedef Eigen::Matrix<float, 6, 6> Matrix6f;
+#else
+template <int N>
+struct MatrixNf {                       // column-major, Eigen's (row, col) and data()
+    float v[N * N];
+    MatrixNf() { for (int i = 0; i < N * N; ++i) v[i] = (i % (N + 1) == 0) ? 1.f : 0.f; }
+    static MatrixNf Identity() { return MatrixNf(); }
+    float& operator()(int r, int c) { return v[c * N + r]; }
+    float operator()(int r, int c) const { return v[c * N + r]; }
+    float* data() { return v; }
+    const float* data() const { return v; }
+    MatrixNf operator*(const MatrixNf& b) const {
+        MatrixNf o;
+        for (int c = 0; c < N; ++c)
+            for (int r = 0; r < N; ++r) {
+                float acc = (*this)(r, 0) * b(0, c);
+                for (int k = 1; k < N; ++k) acc += (*this)(r, k) * b(k, c);
+                o(r, c) = acc;
+            }
+        return o;
+    }
+};
+typedef MatrixNf<4> Matrix4f;
+typedef MatrixNf<6> Matrix6f;
+#endif
+
+class Context {
+  public:
+    explicit Context(int device = 0) { check(r360_ctx_create(device, &h_), "r360_ctx_create"); }
+    ~Context() { r360_ctx_destroy(h_); }
+    Context(const Context&) = delete;
+    Context& operator=(const Context&) = delete;
+    r360_ctx* get() const { return h_; }
+    void sync() { check(r360_ctx_sync(h_), "r360_ctx_sync"); }
+  private:
+    r360_ctx* h_ = nullptr;
+};
+
+// ------------------------------------------------------------------ Calib360
+class Calib360 {
+  public:
+    // rows x cols per sensor (the reference's QVGA default, Calib360.h:73-77)
+    explicit Calib360(Context& ctx, int rows = 240, int cols = 320) : ctx_(ctx) {
+        check(r360_calib_create(ctx.get(), rows, cols, &h_), "r360_calib_create");
+    }
+    ~Calib360() { r360_calib_destroy(h_); }
+    Calib360(const Calib360&) = delete;
+    Calib360& operator=(const Calib360&) = delete;
+    void loadExtrinsicCalibration(const std::string& dir) {
+        check(r360_calib_load_extrinsics(h_, dir.c_str()), "loadExtrinsicCalibration");
+    }
+    void loadIntrinsicCalibration(const std::string& dir) {
+        check(r360_calib_load_intrinsics(h_, dir.c_str()), "loadIntrinsicCalibration");
+    }
+    Matrix4f getRt_id(int sensor_id) const {
+        float rt[128];
+        check(r360_calib_get_extrinsics(h_, rt, nullptr, nullptr), "getRt_id");
+        Matrix4f m;
+        std::memcpy(m.data(), rt + 16 * sensor_id, sizeof(float) * 16);
+        return m;
+    }
+    r360_calib* get() const { return h_; }
+    Context& ctx() const { return ctx_; }
+  private:
+    Context& ctx_;
+    r360_calib* h_ = nullptr;
+};
+
+// ------------------------------------------------------------------ Frame360
+struct Plane {                          // mrpt::pbmap::Plane fields used on the path
+    float v3normal[3], v3center[3], d, areaHull, elongation, curvature, v3PpalDir[3], v3colorNrgb[3],
+        dominantIntensity;
+    unsigned id;
+    int sensor;
+    size_t n_inliers;
+    std::vector<float> polygonContour;  // closed hull polygon, xyz triples
+};
+
+class Frame360 {
+  public:
+    explicit Frame360(Calib360* calib) : calib_(calib) {
+        check(r360_frame_create(calib->ctx().get(), calib->get(), &h_), "r360_frame_create");
+    }
+    ~Frame360() { r360_frame_destroy(h_); }
+    Frame360(const Frame360&) = delete;
+    Frame360& operator=(const Frame360&) = delete;
+
+    void loadFrame(const std::string& path) { check(r360_frame_load_bin(h_, path.c_str()), "loadFrame"); }
+    void upload(const uint8_t* bgr8, const uint16_t* depth8) { check(r360_frame_upload(h_, bgr8, depth8), "upload"); }
+    void undistort() { check(r360_frame_build(h_, R360_BUILD_UNDISTORT), "undistort"); }
+    void stitchSphericalImage() { check(r360_frame_build(h_, R360_BUILD_SPHERE | R360_BUILD_PYRAMID), "stitch"); }
+    void buildSphereCloud() { check(r360_frame_build(h_, R360_BUILD_UNDISTORT | R360_BUILD_CLOUD), "buildSphereCloud"); }
+    void getPlanes() {
+        check(r360_frame_build(h_, R360_BUILD_UNDISTORT | R360_BUILD_PLANES), "getPlanes");
+        fetch_planes();
+    }
+    // Frame360::getPlanarArea (Frame360.h:157)
+    float getPlanarArea() const {
+        float a = 0.f;
+        for (const Plane& p : planes) a += p.areaHull;
+        return a;
+    }
+    std::vector<Plane> planes;          // the frame's PbMap ("planes.vPlanes")
+    Matrix4f pose;
+    unsigned id = 0;
+    r360_frame* get() const { return h_; }
+
+  private:
+    void fetch_planes() {
+        int n = 0;
+        check(r360_frame_get_planes(h_, nullptr, 0, &n), "getPlanes");
+        std::vector<r360_plane> raw(n > 0 ? n : 1);
+        check(r360_frame_get_planes(h_, raw.data(), n, &n), "getPlanes");
+        planes.clear();
+        for (int i = 0; i < n; ++i) {
+            const r360_plane& r = raw[i];
+            Plane p;
+            std::memcpy(p.v3normal, r.normal, sizeof p.v3normal);
+            std::memcpy(p.v3center, r.center, sizeof p.v3center);
+            std::memcpy(p.v3PpalDir, r.ppal, sizeof p.v3PpalDir);
+            std::memcpy(p.v3colorNrgb, r.nrgb, sizeof p.v3colorNrgb);
+            p.d = r.d; p.areaHull = r.area; p.elongation = r.elongation; p.curvature = r.curvature;
+            p.dominantIntensity = r.intensity; p.id = unsigned(r.id); p.sensor = r.sensor;
+            p.n_inliers = size_t(r.n_inliers);
+            p.polygonContour.resize(3 * size_t(r.n_hull));
+            int m = 0;
+            check(r360_frame_get_plane_hull(h_, i, p.polygonContour.data(), r.n_hull, &m), "getPlanes");
+            planes.push_back(p);
+        }
+    }
+    Calib360* calib_;
+    r360_frame* h_ = nullptr;
+};
+
+// ------------------------------------------------------------------ RegisterPhotoICP
+class RegisterPhotoICP {
+  public:
+    enum costFuncType { PHOTO_CONSISTENCY = 0, DEPTH_CONSISTENCY = 1, PHOTO_DEPTH = 2 };
+    explicit RegisterPhotoICP(Context& ctx) : ctx_(ctx) { r360_icp_default_params(&p_); }
+    void setNumPyr(int n) { p_.n_pyr = n; }
+    void setMinDepth(float d) { p_.min_depth = d; }
+    void setMaxDepth(float d) { p_.max_depth = d; }
+    void setGrayVariance(float s) { p_.std_dev_photo = s; }   // sets stdDevPhoto (RegisterPhotoICP.h:242-245)
+    void setDepthVariance(float s) { p_.std_dev_depth = s; }
+    void setSourceFrame(Frame360& f) { ensure_pyramid(f); src_ = &f; }
+    void setTargetFrame(Frame360& f) { ensure_pyramid(f); trg_ = &f; }
+    // benchmark timing mode: exactly K level-0 iterations (0 = reference schedule)
+    void setFixedIterationsLevel0(int k) { p_.fixed_iters_level0 = k; }
+    // returns false where the reference prints "ILL-POSED" and returns early (:4682-4690)
+    bool alignFrames360(const Matrix4f& pose_guess = Matrix4f::Identity(), costFuncType method = PHOTO_CONSISTENCY,
+                        int occlusion = 0) {
+        float g[6];
+        const int rc = check(r360_align360(ctx_.get(), trg_->get(), src_->get(), pose_guess.data(), method, occlusion,
+                                           &p_, relPose_.data(), hessian_.data(), g, &st_),
+                             "alignFrames360");
+        std::memcpy(gradient_, g, sizeof g);
+        SSO = st_.sso;
+        return rc == 0;
+    }
+    Matrix4f getOptimalPose() const { return relPose_; }
+    Matrix6f getHessian() const { return hessian_; }
+    const float* getGradient() const { return gradient_; }
+    float SSO = 0.f;
+    const r360_icp_stats& stats() const { return st_; }
+    r360_icp_params& params() { return p_; }
+  private:
+    static void ensure_pyramid(Frame360& f) {
+        check(r360_frame_build(f.get(), R360_BUILD_UNDISTORT | R360_BUILD_SPHERE | R360_BUILD_PYRAMID), "pyramid");
+    }
+    Context& ctx_;
+    r360_icp_params p_;
+    r360_icp_stats st_{};
+    Frame360* src_ = nullptr;
+    Frame360* trg_ = nullptr;
+    Matrix4f relPose_;
+    Matrix6f hessian_;
+    float gradient_[6] = {0, 0, 0, 0, 0, 0};
+};
+
+// ------------------------------------------------------------------ RegisterRGBD360
+class RegisterRGBD360 {
+  public:
+    enum registrationType { DEFAULT_6DoF = 0, PLANAR_3DoF = 1, ODOMETRY_6DoF = 2, PLANAR_ODOMETRY_3DoF = 3 };
+    // the matcher thresholds are those of config_files/configLocaliser_sphericalOdometry.ini
+    RegisterRGBD360(Context& ctx, const std::string& configFile = "") : ctx_(ctx), config_(configFile) {
+        std::memset(informationM_.data(), 0, sizeof(float) * 36);
+    }
+    void setReference(Frame360* ref, size_t max_match_planes = 0) { ref_ = ref; max_ = max_match_planes; done_ = false; }
+    void setTarget(Frame360* trg, size_t max_match_planes = 0) { trg_ = trg; max_ = max_match_planes; done_ = false; }
+    bool RegisterPbMap(Frame360* frame1 = nullptr, Frame360* frame2 = nullptr, size_t max_match_planes = 0,
+                       registrationType registMode = DEFAULT_6DoF) {
+        if (frame1) setReference(frame1, max_match_planes);
+        if (frame2) setTarget(frame2, max_match_planes);
+        mode_ = registMode;
+        done_ = true;
+        std::vector<int> pairs(512);
+        int n = 0;
+        const int rc = check(r360_register_pbmap(ctx_.get(), ref_->get(), trg_->get(), max_, registMode,
+                                                 rigidTransf_.data(), informationM_.data(), pairs.data(), 256, &n,
+                                                 &areaMatched_, &areaSource, &areaTarget),
+                             "RegisterPbMap");
+        bestMatch_.clear();
+        for (int k = 0; k < n && k < 256; ++k) bestMatch_[unsigned(pairs[2 * k])] = unsigned(pairs[2 * k + 1]);
+        return rc == 1;                 // false leaves rigidTransf untouched (RegisterRGBD360.h:306-310)
+    }
+    Matrix4f getPose() { if (!done_) RegisterPbMap(); return rigidTransf_; }
+    Matrix6f& getInfoMat() { if (!done_) RegisterPbMap(); return informationM_; }
+    std::map<unsigned, unsigned> getMatchedPlanes() { if (!done_) RegisterPbMap(); return bestMatch_; }
+    float getAreaMatched() { if (!done_) RegisterPbMap(); return areaMatched_; }
+    // Register(): PbMap -> rotOffset conjugation -> alignFrames360 -> back (OdometryKeyFrame360.cpp:205-254);
+    // guess is used when the PbMap stage fails.  Returns true when the PbMap stage succeeded.
+    bool Register(Frame360* frame1, Frame360* frame2, const r360_icp_params& icp, Matrix4f& pose,
+                  const Matrix4f& guess = Matrix4f::Identity(), size_t max_match_planes = 25,
+                  registrationType registMode = PLANAR_3DoF) {
+        r360_icp_stats st;
+        const int rc = check(r360_register(ctx_.get(), frame1->get(), frame2->get(), guess.data(), &icp,
+                                           max_match_planes, registMode, pose.data(), informationM_.data(), &st),
+                             "Register");
+        return rc == 0;
+    }
+    float areaSource = 0.f, areaTarget = 0.f;
+  private:
+    Context& ctx_;
+    std::string config_;
+    Frame360* ref_ = nullptr;
+    Frame360* trg_ = nullptr;
+    size_t max_ = 0;
+    int mode_ = DEFAULT_6DoF;
+    bool done_ = false;
+    Matrix4f rigidTransf_;
+    Matrix6f informationM_;
+    std::map<unsigned, unsigned> bestMatch_;
+    float areaMatched_ = 0.f;
+};
+
+}  // namespace r360
