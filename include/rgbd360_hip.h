@@ -203,6 +203,10 @@ int r360_synth_path_pose(uint32_t seed, int frame, float pose_out[16]);
 /* ---------------------------------------------------------------- test hooks
  * The float asinf/atan2f program used by the projection (libm_f32.h, bit-identical to x86-64 glibc)
  * evaluated on the host (on_device = 0) or on the GPU (on_device = 1). */
+/* Fast-guarded vs exact spherical projection of points (X, Y, Z) for an nRows x nCols sphere:
+ * pixel-decision mismatches (must be 0) and exact fallbacks taken. */
+int r360_proj_check(const float* X, const float* Y, const float* Z, int n, int nRows, int nCols,
+                    unsigned long long* mismatches, unsigned long long* fallbacks);
 int r360_libm_eval(const float* x, const float* y, const float* z, int n, float* asin_out, float* atan2_out,
                    int on_device);
 

@@ -129,6 +129,8 @@ _SIGS = [
     ("r360_synth_frame_rt", C.c_int, [C.c_int, C.c_int, _FP, C.c_uint32, _FP, _P, _P]),
     ("r360_synth_path_pose", C.c_int, [C.c_uint32, C.c_int, _FP]),
     ("r360_libm_eval", C.c_int, [_FP, _FP, _FP, C.c_int, _FP, _FP, C.c_int]),
+    ("r360_proj_check", C.c_int, [_FP, _FP, _FP, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_ulonglong),
+                                  C.POINTER(C.c_ulonglong)]),
     ("r360_ctx_debug_stamps", C.c_int, [_P, C.POINTER(C.c_ulonglong)]),
     ("r360_ctx_timing", C.c_int, [_P, C.c_int]),
     ("r360_ctx_timing_read", C.c_int, [_P, C.c_char_p, _DP, C.POINTER(C.c_long)]),

@@ -13,6 +13,7 @@
 // gradients {gx, gy, dgx, dgy} + 8 B target {gray, depth} gathered — the 8N + 24V algorithmic
 // bytes of SURVEY.md §8(d).  No Jacobian rows are materialised (the reference writes and
 // re-reads imgSize x 6 buffers, :2761-2767).
+#include <cstdio>
 #include "../r360_internal.h"
 #include "../libm_f32.h"
 
@@ -45,6 +46,12 @@ struct Proj {
     bool vis;       // valid source depth and projected inside the target image
 };
 
+// Guard bands (pixels) around the .5 rounding boundaries inside which the fast projection defers to the
+// exact one.  Worst-case fast-vs-exact differences at level 0 of a 3840-column sphere: row 2e-4 px
+// (asin of a ~2-ulp argument, |phi| <= pi/2 rows in view), column 7.5e-4 px (two reciprocal-based
+// divisions in atan2 plus the float rounding of theta + pi); coarser levels scale them down.
+constexpr float kGuardRow = 6e-4f, kGuardCol = 1.5e-3f;
+
 __device__ __forceinline__ Proj project(const Pose12& P, float d, float gray_s, float sp, float cp, float st, float ct,
                                         int nRows, int nCols, float half_nRows, float angle_res_inv, const IcpConst& C) {
     Proj o;
@@ -55,14 +62,28 @@ __device__ __forceinline__ Proj project(const Pose12& P, float d, float gray_s, 
     float X = P.R[0] * lx + P.R[1] * ly + P.R[2] * lz; X = X + P.t[0];
     float Y = P.R[3] * lx + P.R[4] * ly + P.R[5] * lz; Y = Y + P.t[1];
     float Z = P.R[6] * lx + P.R[7] * ly + P.R[8] * lz; Z = Z + P.t[2];
-    const float dist = sqrtf(X * X + Y * Y + Z * Z);
-    const float dist_inv = 1.f / dist;
-    const float phi_trg = r360m::asinf(X * dist_inv);             // glibc-exact (libm_f32.h)
-    const float theta_trg = (float)((double)r360m::atan2f_sel(Y, Z) + R360_PI);
+    const float d2 = X * X + Y * Y + Z * Z;
+    // |p'| is exact (it enters the depth residual); the projection itself uses hardware rsq/rcp
+    const float dist = sqrtf(d2);
+    float dist_inv = __builtin_amdgcn_rsqf(d2);
+    float phi_trg = r360m::asinf_fast(X * dist_inv);
+    float theta_trg = (float)((double)r360m::atan2f_fast(Y, Z) + R360_PI);
+    float rr = half_nRows - phi_trg * angle_res_inv;
+    float cc = theta_trg * angle_res_inv;
+    const float gr = fabsf(rr - floorf(rr) - 0.5f), gc = fabsf(cc - floorf(cc) - 0.5f);
+    if (valid && !(gr >= kGuardRow && gc >= kGuardCol)) {   // also catches a NaN of the fast path (poles)
+        // near a rounding boundary: the exact program (same float expressions as the reference,
+        // glibc-exact asinf/atan2f, IEEE sqrt/div) decides the pixel
+        dist_inv = 1.f / dist;
+        phi_trg = r360m::asinf(X * dist_inv);
+        theta_trg = (float)((double)r360m::atan2f_sel(Y, Z) + R360_PI);
+        rr = half_nRows - phi_trg * angle_res_inv;
+        cc = theta_trg * angle_res_inv;
+    }
     // round() + int conversion + the (:2989) bounds test, on the float values so NaN and out-of-range
     // projections are rejected exactly as the x86 reference's (int) conversion does.
-    const float rf = roundf(half_nRows - phi_trg * angle_res_inv);
-    const float cf = roundf(theta_trg * angle_res_inv);
+    const float rf = roundf(rr);
+    const float cf = roundf(cc);
     o.vis = valid && (rf >= 0.f && rf < (float)nRows) && cf < (float)nCols;
     o.t = o.vis ? (int)rf * nCols + (int)cf : 0;
     o.X = X; o.Y = Y; o.Z = Z; o.dist = dist; o.dist_inv = dist_inv; o.gray_s = gray_s;
@@ -253,7 +274,7 @@ __global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src
         contribute<METHOD>(A, o1, G1, T1, angle_res_inv, C);
     };
     const int stride = gridDim.x * TPB;
-    if (PF) {
+    if (PF == 1) {
         // large levels: 4-pixel units (vector loads), processed as two pixel pairs (ILP)
         for (int u = blockIdx.x * TPB + threadIdx.x; u < units; u += stride) {
             const int r = u / cq;
@@ -263,6 +284,44 @@ __global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src
             const float sp = sinphi[r], cp = cosphi[r];
             two(a.y, a.x, a.w, a.z, sp, cp, s.x, c.x, s.y, c.y);
             two(b.y, b.x, b.w, b.z, sp, cp, s.z, c.z, s.w, c.w);
+        }
+    } else if (PF == 2) {
+        // software-pipelined pixel stream, one wave = 64 consecutive pixels of one row (nCols % 64 == 0,
+        // so row/column come from wave-uniform scalar arithmetic and the row LUT is wave-uniform): while
+        // pixel k is accumulated, pixel k+1's target gathers and pixel k+2's source loads are in flight
+        const int npx = nRows * nCols;
+        const int lane = threadIdx.x & 63;
+        struct Src { float d, g, sp, cp, st, ct; };
+        auto ld = [&](int base) {                          // base: wave-uniform first pixel
+            const int r = __builtin_amdgcn_readfirstlane(base / nCols);
+            const int c = base - r * nCols + lane;
+            const float2 a = src[base + lane];
+            return Src{a.y, a.x, sinphi[r], cosphi[r], sinth[c], costh[c]};
+        };
+        int b = __builtin_amdgcn_readfirstlane((blockIdx.x * TPB + (threadIdx.x & ~63)));
+        if (b < npx) {
+            const Src s0 = ld(b);
+            Src s1 = b + stride < npx ? ld(b + stride) : s0;
+            Proj o0 = project(P, s0.d, s0.g, s0.sp, s0.cp, s0.st, s0.ct, nRows, nCols, half_nRows, angle_res_inv, C);
+            float4 G0 = tg[o0.t];
+            float2 T0 = trg[o0.t];
+            for (;;) {
+                const int b1 = b + stride, b2 = b + 2 * stride;
+                const bool more = b1 < npx;
+                Src s2 = s1;
+                if (b2 < npx) s2 = ld(b2);
+                Proj o1 = o0;
+                float4 G1 = G0;
+                float2 T1 = T0;
+                if (more) {
+                    o1 = project(P, s1.d, s1.g, s1.sp, s1.cp, s1.st, s1.ct, nRows, nCols, half_nRows, angle_res_inv, C);
+                    G1 = tg[o1.t];
+                    T1 = trg[o1.t];
+                }
+                contribute<METHOD>(A, o0, G0, T0, angle_res_inv, C);
+                if (!more) break;
+                b = b1; s1 = s2; o0 = o1; G0 = G1; T0 = T1;
+            }
         }
     } else {
         // small levels: one pixel per thread, so the latency chain per thread is a quarter as long
@@ -274,6 +333,13 @@ __global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src
             one(a.y, a.x, sinphi[r], cosphi[r], sinth[c], costh[c]);
         }
     }
+#ifdef R360_STAMPS
+    const unsigned long long t_loop = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) {   // earliest block start / latest loop end over the grid
+        __hip_atomic_fetch_min(&S->dbg[8], t_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_max(&S->dbg[9], t_loop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#endif
 
     // ---- stage 1: wave butterfly (f32) -> LDS -> per-workgroup fp64 record
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -420,6 +486,79 @@ int icp_blocks_for(int n_pixels) {
     return b < 1 ? 1 : b;
 }
 
+namespace {
+// Test hook: fast-guarded vs exact projection of arbitrary transformed points (pose = identity,
+// LUT bypassed): counts pixel-decision mismatches (must be 0) and exact fallbacks.
+__global__ void k_proj_check(const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
+                             int n, int nRows, int nCols, unsigned long long* __restrict__ out) {
+    const float angle_res = (float)(2 * R360_PI / nCols);
+    const float angle_res_inv = 1 / angle_res;
+    const float half_nRows = (float)(0.5 * nRows - 0.5);
+    unsigned long long mism = 0, fb = 0;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const float x = X[i], y = Y[i], z = Z[i];
+        const float d2 = x * x + y * y + z * z;
+        // exact
+        const float dist = sqrtf(d2);
+        const float dinv = 1.f / dist;
+        const float rr_e = half_nRows - r360m::asinf(x * dinv) * angle_res_inv;
+        const float cc_e = (float)((double)r360m::atan2f_sel(y, z) + R360_PI) * angle_res_inv;
+        // fast + guard (as project())
+        const float fi = __builtin_amdgcn_rsqf(d2);
+        float rr = half_nRows - r360m::asinf_fast(x * fi) * angle_res_inv;
+        float cc = (float)((double)r360m::atan2f_fast(y, z) + R360_PI) * angle_res_inv;
+        const float gr = fabsf(rr - floorf(rr) - 0.5f), gc = fabsf(cc - floorf(cc) - 0.5f);
+        const float rr_f = rr, cc_f = cc;
+        if (!(gr >= kGuardRow && gc >= kGuardCol)) { rr = rr_e; cc = cc_e; ++fb; }
+        // the decision the pass takes: visible or not, and which target pixel
+        auto decide = [&](float a, float b, long long& t) {
+            const float rf = roundf(a), cf = roundf(b);
+            const bool vis = (rf >= 0.f && rf < (float)nRows) && cf < (float)nCols;
+            t = vis ? (long long)rf * nCols + (long long)cf : -1;
+            return vis;
+        };
+        long long tf, te;
+        const bool vf = decide(rr, cc, tf), ve = decide(rr_e, cc_e, te);
+        const bool same = vf == ve && tf == te;
+        mism += same ? 0 : 1;
+        if (!same) {
+            out[2] = (unsigned long long)i;
+            out[3] = __float_as_uint(rr_f); out[4] = __float_as_uint(rr_e);
+            out[5] = __float_as_uint(cc_f); out[6] = __float_as_uint(cc_e);
+        }
+    }
+    atomicAdd(out, mism);
+    atomicAdd(out + 1, fb);
+}
+
+}  // namespace
+
+extern "C" int r360_proj_check(const float* X, const float* Y, const float* Z, int n, int nRows, int nCols,
+                               unsigned long long* mismatches, unsigned long long* fallbacks) {
+    float *dx, *dy, *dz;
+    unsigned long long* dout;
+    R360_HIP(hipMalloc(&dx, sizeof(float) * n));
+    R360_HIP(hipMalloc(&dy, sizeof(float) * n));
+    R360_HIP(hipMalloc(&dz, sizeof(float) * n));
+    R360_HIP(hipMalloc(&dout, 64));
+    R360_HIP(hipMemcpy(dx, X, sizeof(float) * n, hipMemcpyHostToDevice));
+    R360_HIP(hipMemcpy(dy, Y, sizeof(float) * n, hipMemcpyHostToDevice));
+    R360_HIP(hipMemcpy(dz, Z, sizeof(float) * n, hipMemcpyHostToDevice));
+    R360_HIP(hipMemset(dout, 0, 64));
+    hipLaunchKernelGGL(k_proj_check, dim3(1024), dim3(256), 0, 0, dx, dy, dz, n, nRows, nCols, dout);
+    R360_HIP(hipGetLastError());
+    unsigned long long h[8];
+    R360_HIP(hipMemcpy(h, dout, 64, hipMemcpyDeviceToHost));
+    if (h[0] && getenv("R360_PROJ_DEBUG"))
+        fprintf(stderr, "proj mismatch at %llu: rr fast %.9g exact %.9g, cc fast %.9g exact %.9g\n", h[2],
+                (double)__builtin_bit_cast(float, (unsigned)h[3]), (double)__builtin_bit_cast(float, (unsigned)h[4]),
+                (double)__builtin_bit_cast(float, (unsigned)h[5]), (double)__builtin_bit_cast(float, (unsigned)h[6]));
+    hipFree(dx); hipFree(dy); hipFree(dz); hipFree(dout);
+    *mismatches = h[0];
+    *fallbacks = h[1];
+    return 0;
+}
+
 static int env_int(const char* name, int dflt) {
     const char* v = getenv(name);
     return v ? atoi(v) : dflt;
@@ -453,21 +592,21 @@ int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src
         if (cap < 1) cap = 1;
     }
     const int npx = Ls.rows * Ls.cols;
-    const int pf = pf_env >= 0 ? pf_env : (npx > cap * TPB ? 1 : 0);
-    int nb = pf ? icp_blocks_for(npx) : (npx + TPB - 1) / TPB;
+    const int pf = pf_env >= 0 ? pf_env : ((Ls.cols % 64 == 0) ? 2 : 0);
+    int nb = pf == 1 ? icp_blocks_for(npx) : (npx + TPB - 1) / TPB;
     if (nb > cap) nb = cap;
     const char* name = level == 0 ? "k_icp_pass_L0" : "k_icp_pass";
     const int slot = timing_begin(ctx, name);
-    if (method == R360_PHOTO_CONSISTENCY) {
-        if (pf) launch_pass<R360_PHOTO_CONSISTENCY, 1>(ctx, nb, Ls, Lt, T, C, first, eval_only);
-        else launch_pass<R360_PHOTO_CONSISTENCY, 0>(ctx, nb, Ls, Lt, T, C, first, eval_only);
-    } else if (method == R360_DEPTH_CONSISTENCY) {
-        if (pf) launch_pass<R360_DEPTH_CONSISTENCY, 1>(ctx, nb, Ls, Lt, T, C, first, eval_only);
-        else launch_pass<R360_DEPTH_CONSISTENCY, 0>(ctx, nb, Ls, Lt, T, C, first, eval_only);
-    } else {
-        if (pf) launch_pass<R360_PHOTO_DEPTH, 1>(ctx, nb, Ls, Lt, T, C, first, eval_only);
-        else launch_pass<R360_PHOTO_DEPTH, 0>(ctx, nb, Ls, Lt, T, C, first, eval_only);
-    }
+#define R360_LAUNCH(M)                                                              \
+    do {                                                                            \
+        if (pf == 1) launch_pass<M, 1>(ctx, nb, Ls, Lt, T, C, first, eval_only);   \
+        else if (pf == 2) launch_pass<M, 2>(ctx, nb, Ls, Lt, T, C, first, eval_only); \
+        else launch_pass<M, 0>(ctx, nb, Ls, Lt, T, C, first, eval_only);          \
+    } while (0)
+    if (method == R360_PHOTO_CONSISTENCY) R360_LAUNCH(R360_PHOTO_CONSISTENCY);
+    else if (method == R360_DEPTH_CONSISTENCY) R360_LAUNCH(R360_DEPTH_CONSISTENCY);
+    else R360_LAUNCH(R360_PHOTO_DEPTH);
+#undef R360_LAUNCH
     timing_end(ctx, slot);
     R360_HIP(hipGetLastError());
     return 0;

@@ -194,4 +194,49 @@ R360_HD float atan2f_sel(float y, float x) {
     return m == 0 ? z : (m == 1 ? -z : (m == 2 ? pi - (z - pi_lo) : (z - pi_lo) - pi));
 }
 
+// ---------------------------------------------------------------------------------------------
+// Fast forms for the GPU projection (NOT bit-exact): the same polynomials with the IEEE division and
+// square root replaced by the hardware reciprocal / square root (~1 ulp).  The ICP pass uses them only
+// to decide on which side of a pixel-rounding boundary a projection falls; when it lands within the
+// guard band of a boundary the exact functions above recompute it (icp_kernels.hip, project()).
+#if defined(__HIPCC__)
+__device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float fast_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+
+__device__ __forceinline__ float asinf_fast(float x) {
+    const float p0 = 1.666675248e-1f, p1 = 7.495297643e-2f, p2 = 4.547037598e-2f, p3 = 2.417951451e-2f,
+                p4 = 4.216630880e-2f;
+    const float ax = fabs_(x);
+    if (ax < 0.5f) {                                       // the exact polynomial branch
+        const float t = x * x;
+        return x + x * (t * (p0 + t * (p1 + t * (p2 + t * (p3 + t * p4)))));
+    }
+    const float t = (1.0f - ax) * 0.5f;
+    const float p = t * (p0 + t * (p1 + t * (p2 + t * (p3 + t * p4))));
+    const float s = fast_sqrt(t);
+    const float r = 1.57079637050628662109375f - 2.0f * (s + s * p);
+    return x > 0 ? r : -r;
+}
+
+// atan2 with a two-way argument reduction (|t| <= tan(pi/8) < 7/16, fdlibm's polynomial domain):
+// atan(a) = a poly for a <= tan(pi/8), pi/4 + atan((a-1)/(a+1)) above; octants by selects.
+__device__ __forceinline__ float atan2f_fast(float y, float x) {
+    const float ay = fabs_(y), ax = fabs_(x);
+    const float mx = ay > ax ? ay : ax, mn = ay > ax ? ax : ay;
+    const float a = mn * fast_rcp(mx);                     // in [0, 1]
+    const bool big = a > 0.41421356f;
+    const float t = big ? (a - 1.0f) * fast_rcp(a + 1.0f) : a;
+    const float z = t * t, w = z * z;
+    const float s1 = z * (3.3333334327e-01f + w * (1.4285714924e-01f + w * (9.0908870101e-02f +
+                     w * (6.6610731184e-02f + w * (4.9768779427e-02f + w * 1.6285819933e-02f)))));
+    const float s2 = w * (-2.0000000298e-01f + w * (-1.1111110449e-01f + w * (-7.6918758452e-02f +
+                     w * (-5.8335702866e-02f + w * -3.6531571299e-02f))));
+    float r = t - t * (s1 + s2);
+    r = big ? r + 0.78539816f : r;
+    r = ay > ax ? 1.57079633f - r : r;
+    r = (fbits(x) >> 31) ? 3.14159265f - r : r;
+    return (fbits(y) >> 31) ? -r : r;
+}
+#endif
+
 }  // namespace r360m

@@ -179,3 +179,35 @@ def test_align360_parity_synth_vga(ctx, vga, fixed):
     assert dr <= ROT_TOL and dt <= TRANS_TOL, (dr, dt)
     if fixed:
         assert reg.stats.passes == sum(1 + st.evals[l] for l in range(1, 5)) + 1 + fixed
+
+
+@pytest.mark.parametrize("rows,cols", [(640, 3840), (320, 1920), (160, 960), (40, 240)])
+def test_fast_projection_guard_never_changes_a_pixel(rows, cols):
+    """The pass projects with hardware rsq/rcp and falls back to the exact (reference) program inside a
+    guard band around every .5 rounding boundary; over random and boundary-adversarial points the pass's
+    decisions (visible or not, and which target pixel) must be identical to the exact program's.  (Near the
+    poles, far outside the 60-degree band, the fast row can differ by more than the guard; such points are
+    invisible either way.)"""
+    rng = np.random.default_rng(rows * 7 + cols)
+    n = 1 << 22
+    # directions over the whole sphere, ranges 0.2-12 m
+    v = rng.normal(size=(n, 3)).astype(np.float32)
+    v /= np.linalg.norm(v, axis=1, keepdims=True)
+    v *= rng.uniform(0.2, 12.0, size=(n, 1)).astype(np.float32)
+    # adversarial: directions placed on pixel-rounding boundaries of this geometry (+- a few ulps)
+    m = n // 4
+    ares = 2 * 3.14159265359 / cols
+    r = rng.integers(-2, rows + 2, m) + 0.5 + rng.normal(scale=1e-4, size=m)
+    c = rng.integers(-2, cols + 2, m) + 0.5 + rng.normal(scale=1e-4, size=m)
+    phi = (rows / 2 - 0.5 - r) * ares
+    th = c * ares - 3.14159265359
+    d = rng.uniform(0.3, 8.0, m)
+    v[:m, 0] = d * np.sin(phi)
+    v[:m, 1] = d * np.cos(phi) * np.sin(th)
+    v[:m, 2] = d * np.cos(phi) * np.cos(th)
+    x, y, z = (np.ascontiguousarray(v[:, k]) for k in range(3))
+    mism, fb = R.C.c_ulonglong(), R.C.c_ulonglong()
+    R._check(R.lib().r360_proj_check(R._fptr(x), R._fptr(y), R._fptr(z), n, rows, cols, R.C.byref(mism),
+                                     R.C.byref(fb)), "proj_check")
+    assert mism.value == 0, mism.value
+    assert fb.value < n // 3          # the fast path decides most points
