@@ -99,7 +99,7 @@ extern "C" int r360_ctx_create(int device, r360_ctx** out) {
     R360_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     R360_HIP(hipMalloc(&c->d_state, sizeof(IcpState)));
     R360_HIP(hipMemset(c->d_state, 0, sizeof(IcpState)));
-    c->partials_cap = 1024;
+    c->partials_cap = 2048;
     R360_HIP(hipMalloc(&c->d_partials, sizeof(double) * 32 * c->partials_cap));
     R360_HIP(hipHostMalloc(&c->h_state, sizeof(IcpState), hipHostMallocDefault));
     *out = c;

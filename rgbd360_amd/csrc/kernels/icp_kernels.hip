@@ -24,6 +24,26 @@ constexpr int NW = TPB / 64;
 
 struct Pose12 { float R[9]; float t[3]; };
 
+// Target gathers go through buffer loads (32-bit byte offsets, descriptor in SGPRs).  Besides the
+// smaller address arithmetic, an intrinsic load is not merged by InstCombine with the loop-carried
+// copy of the previous iteration's gather (phi(load a, load b) -> load(phi(a, b)) for plain loads),
+// which had moved every gather next to its use and exposed its full latency once per pixel.
+struct Gather {
+    __amdgpu_buffer_rsrc_t tg, trg;
+    __device__ __forceinline__ float4 g(int t) const {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(tg, t * 16, 0, 0);
+        return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+    }
+    __device__ __forceinline__ float2 T(int t) const {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(trg, t * 8, 0, 0);
+        return make_float2(__uint_as_float(v[0]), __uint_as_float(v[1]));
+    }
+};
+
+#ifdef R360_STAMPS
+__device__ unsigned long long g_blk_stamps[2][8192];  // per-workgroup start / loop end (diagnostic build)
+#endif
+
 __device__ __forceinline__ float huberf(float e, float reg) {  // weightHuber<float> (:545-554)
     const float a = fabsf(e);
     if (a < reg) return 1.f;
@@ -288,7 +308,7 @@ __global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src
     } else if (PF == 2) {
         // software-pipelined pixel stream, one wave = 64 consecutive pixels of one row (nCols % 64 == 0,
         // so row/column come from wave-uniform scalar arithmetic and the row LUT is wave-uniform): while
-        // pixel k is accumulated, pixel k+1's target gathers and pixel k+2's source loads are in flight
+        // chunk k is accumulated, chunk k+1's target gathers and chunk k+2's source loads are in flight
         const int npx = nRows * nCols;
         const int lane = threadIdx.x & 63;
         struct Src { float d, g, sp, cp, st, ct; };
@@ -298,29 +318,39 @@ __global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src
             const float2 a = src[base + lane];
             return Src{a.y, a.x, sinphi[r], cosphi[r], sinth[c], costh[c]};
         };
-        int b = __builtin_amdgcn_readfirstlane((blockIdx.x * TPB + (threadIdx.x & ~63)));
-        if (b < npx) {
-            const Src s0 = ld(b);
-            Src s1 = b + stride < npx ? ld(b + stride) : s0;
-            Proj o0 = project(P, s0.d, s0.g, s0.sp, s0.cp, s0.st, s0.ct, nRows, nCols, half_nRows, angle_res_inv, C);
-            float4 G0 = tg[o0.t];
-            float2 T0 = trg[o0.t];
-            for (;;) {
-                const int b1 = b + stride, b2 = b + 2 * stride;
-                const bool more = b1 < npx;
-                Src s2 = s1;
-                if (b2 < npx) s2 = ld(b2);
-                Proj o1 = o0;
-                float4 G1 = G0;
-                float2 T1 = T0;
-                if (more) {
-                    o1 = project(P, s1.d, s1.g, s1.sp, s1.cp, s1.st, s1.ct, nRows, nCols, half_nRows, angle_res_inv, C);
-                    G1 = tg[o1.t];
-                    T1 = trg[o1.t];
-                }
-                contribute<METHOD>(A, o0, G0, T0, angle_res_inv, C);
-                if (!more) break;
-                b = b1; s1 = s2; o0 = o1; G0 = G1; T0 = T1;
+        const Gather gt{__builtin_amdgcn_make_buffer_rsrc(const_cast<float4*>(tg), 0, npx * 16, 0x00020000),
+                        __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(trg), 0, npx * 8, 0x00020000)};
+        const int b0 = __builtin_amdgcn_readfirstlane((blockIdx.x * TPB + (threadIdx.x & ~63)));
+        if (b0 < npx) {
+            // Unrolled by two with fixed register roles (A, B) and unconditional loads (the chunk index is
+            // clamped to the wave's last chunk): no loop-carried copies of in-flight loads and the same
+            // number of loads on every path, so each wait names exactly the loads it needs.
+            const int n_it = (npx - 1 - b0) / stride + 1;  // chunks of this wave (>= 1)
+            auto base = [&](int k) { return b0 + (k < n_it ? k : n_it - 1) * stride; };
+            auto prj = [&](const Src& x) {
+                return project(P, x.d, x.g, x.sp, x.cp, x.st, x.ct, nRows, nCols, half_nRows, angle_res_inv, C);
+            };
+            // Per half-iteration h: load the source of chunk h+2, project chunk h+1 and issue its gathers,
+            // accumulate chunk h.  Loads are issued in the order they are consumed, so the in-order
+            // vmcnt lets each wait skip the five younger loads still in flight.
+            Src sA = ld(base(0));
+            Src sB = ld(base(1));
+            Proj oA = prj(sA);
+            float4 GA = gt.g(oA.t);
+            float2 TA = gt.T(oA.t);
+            for (int k = 0;; k += 2) {
+                sA = ld(base(k + 2));
+                const Proj oB = prj(sB);
+                const float4 GB = gt.g(oB.t);
+                const float2 TB = gt.T(oB.t);
+                contribute<METHOD>(A, oA, GA, TA, angle_res_inv, C);
+                if (k + 1 >= n_it) break;
+                sB = ld(base(k + 3));
+                oA = prj(sA);
+                GA = gt.g(oA.t);
+                TA = gt.T(oA.t);
+                contribute<METHOD>(A, oB, GB, TB, angle_res_inv, C);
+                if (k + 2 >= n_it) break;
             }
         }
     } else {
@@ -336,6 +366,7 @@ __global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src
 #ifdef R360_STAMPS
     const unsigned long long t_loop = __builtin_amdgcn_s_memrealtime();
     if (threadIdx.x == 0) {   // earliest block start / latest loop end over the grid
+        if (blockIdx.x < 8192) { g_blk_stamps[0][blockIdx.x] = t_start; g_blk_stamps[1][blockIdx.x] = t_loop; }
         __hip_atomic_fetch_min(&S->dbg[8], t_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_fetch_max(&S->dbg[9], t_loop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -553,11 +584,21 @@ extern "C" int r360_proj_check(const float* X, const float* Y, const float* Z, i
         fprintf(stderr, "proj mismatch at %llu: rr fast %.9g exact %.9g, cc fast %.9g exact %.9g\n", h[2],
                 (double)__builtin_bit_cast(float, (unsigned)h[3]), (double)__builtin_bit_cast(float, (unsigned)h[4]),
                 (double)__builtin_bit_cast(float, (unsigned)h[5]), (double)__builtin_bit_cast(float, (unsigned)h[6]));
-    hipFree(dx); hipFree(dy); hipFree(dz); hipFree(dout);
+    (void)hipFree(dx); (void)hipFree(dy); (void)hipFree(dz); (void)hipFree(dout);
     *mismatches = h[0];
     *fallbacks = h[1];
     return 0;
 }
+
+#ifdef R360_STAMPS
+// Diagnostic build only: per-workgroup start / loop-end stamps of the last pass.
+extern "C" int r360_debug_block_stamps(unsigned long long* out, int n) {
+    if (n > 8192) n = 8192;
+    R360_HIP(hipDeviceSynchronize());
+    R360_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_blk_stamps), sizeof(unsigned long long) * 8192 * 2));
+    return n;
+}
+#endif
 
 static int env_int(const char* name, int dflt) {
     const char* v = getenv(name);
@@ -580,19 +621,21 @@ int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src
     // 4-pixel units on the large levels, one pixel per thread where that still fits one resident
     // round (latency-bound small levels); R360_ICP_PF=0/1 forces one form (experiments)
     static const int pf_env = env_int("R360_ICP_PF", -1);
-    static int cap = -1;
-    if (cap < 0) {
-        // one resident round: CUs x workgroups per CU of this kernel (grid-stride beyond it)
-        int dev = 0, cus = 0, per = 0;
-        hipGetDevice(&dev);
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)k_icp_pass<R360_PHOTO_DEPTH, 1>, TPB, 0);
-        cap = env_int("R360_ICP_CAP", cus * (per > 0 ? per : 4));
-        if (cap > ctx->partials_cap) cap = ctx->partials_cap;
-        if (cap < 1) cap = 1;
+    // one resident round: CUs x workgroups per CU of the launched form (grid-stride beyond it)
+    static int cus = -1, per[3] = {0, 0, 0};
+    static const int cap_env = env_int("R360_ICP_CAP", -1);
+    if (cus < 0) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per[0], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 0>, TPB, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per[1], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 1>, TPB, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per[2], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 2>, TPB, 0);
     }
     const int npx = Ls.rows * Ls.cols;
     const int pf = pf_env >= 0 ? pf_env : ((Ls.cols % 64 == 0) ? 2 : 0);
+    int cap = cap_env > 0 ? cap_env : cus * (per[pf] > 0 ? per[pf] : 4);
+    if (cap > ctx->partials_cap) cap = ctx->partials_cap;
     int nb = pf == 1 ? icp_blocks_for(npx) : (npx + TPB - 1) / TPB;
     if (nb > cap) nb = cap;
     const char* name = level == 0 ? "k_icp_pass_L0" : "k_icp_pass";

@@ -97,7 +97,10 @@ R360_HD float atanf(float x) {
     const float s1 = z * (aT[0] + w * (aT[2] + w * (aT[4] + w * (aT[6] + w * (aT[8] + w * aT[10])))));
     const float s2 = w * (aT[1] + w * (aT[3] + w * (aT[5] + w * (aT[7] + w * aT[9]))));
     if (id < 0) return x - x * (s1 + s2);
-    const float zz = atanhi[id] - ((x * (s1 + s2) - atanlo[id]) - x);
+    // table entries by selects (an indexed load would be the only memory access of the device path)
+    const float hi = id == 0 ? atanhi[0] : (id == 1 ? atanhi[1] : (id == 2 ? atanhi[2] : atanhi[3]));
+    const float lo = id == 0 ? atanlo[0] : (id == 1 ? atanlo[1] : (id == 2 ? atanlo[2] : atanlo[3]));
+    const float zz = hi - ((x * (s1 + s2) - lo) - x);
     return hx < 0 ? -zz : zz;
 }
 

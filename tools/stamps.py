@@ -31,3 +31,27 @@ for lv in (4, 3, 2, 1, 0):
     us = lambda x: (x - base) / 100.0
     print(f"level {lv}: all-blocks loop end {us(t[6]):7.2f} | last block: start {us(t[0]):7.2f} loop-end {us(t[1]):7.2f}"
           f" ticket {us(t[2]):7.2f} records {us(t[3]):7.2f} end {us(t[4]):7.2f}  (us from first block start)")
+
+# per-workgroup start / loop-end distribution of the last level-0 pass
+nb = int(os.environ.get("NB", "768"))
+buf = (C.c_ulonglong * (2 * 8192))()
+R.lib().r360_debug_block_stamps(buf, 8192)
+a = np.array(list(buf), dtype=np.float64).reshape(2, 8192)[:, :nb]
+t0 = a[0].min()
+st, en = (a[0] - t0) / 100.0, (a[1] - t0) / 100.0
+q = lambda x: " ".join(f"{v:6.2f}" for v in np.percentile(x, [0, 10, 50, 90, 100]))
+print("block start   pct 0/10/50/90/100:", q(st))
+print("block loopend pct 0/10/50/90/100:", q(en))
+print("block busy    pct 0/10/50/90/100:", q(en - st))
+m = a[0] > 0
+b = np.nonzero(m)[0]
+busy = (a[1] - a[0])[m] / 100.0
+print("blocks used", len(b))
+for x in range(8):
+    sel = (b % 8) == x
+    print(f"xcd {x}: busy pct 0/50/100 {np.percentile(busy[sel], [0, 50, 100]).round(2)}")
+order = np.argsort(a[0][m])
+k = len(order)
+for part in range(4):
+    sl = order[part * k // 4:(part + 1) * k // 4]
+    print(f"start-quartile {part}: busy mean {busy[sl].mean():6.2f}")
