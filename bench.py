@@ -7,7 +7,8 @@
 Workload "full" (default; BASELINE.json configs[1]+[2] as one registration, run the way configs[3]
 runs them): the synthetic 256-frame OdometryRGBD360 sequence (procedural room, seed 360, 8 x 480x640
 sensors).  One step registers, on each of P pipelines of each GPU, the next consecutive pair of the
-rank's shard: the new Frame360 is built end to end on the GPU (undistort, cloud + 2x2 median
+rank's shard (pipelines run free on their own host threads and HIP streams; the timed region covers
+`steps` pairs per pipeline): the new Frame360 is built end to end on the GPU (undistort, cloud + 2x2 median
 downsample, bilateral filter, normals, plane segmentation + refinement, PbMap descriptors and
 grouping, spherical stitch, 5-level pyramid with gradients), then RegisterRGBD360::RegisterPbMap
 (25 planes, PLANAR_3DoF) and RegisterPhotoICP::alignFrames360(PHOTO_DEPTH) initialised with the
@@ -25,11 +26,16 @@ import json
 import os
 import sys
 import time
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# Hardware queues per process (HIP's default is 4): the per-frame plane kernels are latency-bound
+# (one workgroup or wave per sensor), so throughput comes from many pipelines' kernels running at
+# once; 16 queues let 16+ streams reach the hardware side by side.  Must precede HIP initialisation.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 
 METRIC = "registered Frame360 pairs/sec @ 8×640×480; ICP-reduce HBM GB/s vs roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
@@ -119,7 +125,7 @@ def main():
     ap.add_argument("--cols", type=int, default=640)
     ap.add_argument("--iters0", type=int, default=20)
     ap.add_argument("--workload", choices=["full", "dense"], default="full")
-    ap.add_argument("--streams", type=int, default=8, help="pairs in flight per GPU (one HIP stream each)")
+    ap.add_argument("--streams", type=int, default=16, help="pairs in flight per GPU (one pipeline = host thread + HIP stream each)")
     ap.add_argument("--window", type=int, default=16, help="sequence frames resident per pipeline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -177,31 +183,46 @@ def main():
     pout = np.zeros((P, 16), np.float32)
     stats = [R.IcpStats() for _ in range(P)]
 
-    def step(k):
-        j = k % (F - 1)
-        for p in range(P):                       # enqueue every pipeline's GPU frame builds
-            if args.workload == "dense" or j == 0:
-                frames[p][j].build(flags, sync=False)
-            frames[p][j + 1].build(flags, sync=False)
-        for p in range(P):                       # PbMap stage (host) + enqueue the dense stage
-            ref, trg = frames[p][j], frames[p][j + 1]
-            if args.workload == "full":
-                rc = L.r360_register_async(ctxs[p].h, ref.h, trg.h, R._fptr(eye16), R.C.byref(params), 25,
-                                           R.PLANAR_3DoF)
-            else:
-                rc = L.r360_align360_async(ctxs[p].h, ref.h, trg.h, R._fptr(eye16), R.PHOTO_DEPTH, 0,
-                                           R.C.byref(params))
-            assert rc == 0, L.r360_last_error()
-        for p in range(P):
-            if args.workload == "full":
-                rc = L.r360_register_result(ctxs[p].h, R._fptr(pout[p]), None, R.C.byref(stats[p]))
-            else:
-                rc = L.r360_align360_result(ctxs[p].h, R._fptr(pout[p]), None, None, R.C.byref(stats[p]))
-            assert rc >= 0, L.r360_last_error()
-        return pout
+    prof = os.environ.get("BENCH_PROFILE") is not None
+    tacc = np.zeros((P, 4))
 
-    for k in range(args.warmup):
-        step(k)
+    def pair(p, k, out):
+        """Pipeline p registers its k-th pair (frames j, j+1 of its window) and writes the pose to out."""
+        ta = time.perf_counter()
+        j = k % (F - 1)
+        if args.workload == "dense" or j == 0:
+            frames[p][j].build(flags, sync=False)
+        frames[p][j + 1].build(flags, sync=False)
+        ref, trg = frames[p][j], frames[p][j + 1]
+        tb = time.perf_counter()
+        if args.workload == "full":   # PbMap stage on this host thread, then the dense stage is enqueued
+            rc = L.r360_register_async(ctxs[p].h, ref.h, trg.h, R._fptr(eye16), R.C.byref(params), 25,
+                                       R.PLANAR_3DoF)
+        else:
+            rc = L.r360_align360_async(ctxs[p].h, ref.h, trg.h, R._fptr(eye16), R.PHOTO_DEPTH, 0,
+                                       R.C.byref(params))
+        assert rc == 0, L.r360_last_error()
+        tc = time.perf_counter()
+        if args.workload == "full":
+            rc = L.r360_register_result(ctxs[p].h, R._fptr(out), None, R.C.byref(stats[p]))
+        else:
+            rc = L.r360_align360_result(ctxs[p].h, R._fptr(out), None, None, R.C.byref(stats[p]))
+        assert rc >= 0, L.r360_last_error()
+        if prof:
+            tacc[p] += (tb - ta, tc - tb, time.perf_counter() - tc, 1)
+
+    # Each pipeline runs free on its own host thread (ctypes drops the GIL inside the library), so one
+    # pipeline's host PbMap stage and its wait for results never stall the others' GPU work.
+    pool = ThreadPoolExecutor(max_workers=P)
+
+    def run(k0, n, poses):
+        def worker(p):
+            for i in range(n):
+                pair(p, k0 + i, poses[i, p])
+        for f in [pool.submit(worker, p) for p in range(P)]:
+            f.result()
+
+    run(0, args.warmup, np.zeros((max(args.warmup, 1), P, 16), np.float32))
     for c in ctxs:
         c.sync()
 
@@ -217,8 +238,7 @@ def main():
         c.timing(True)
         c.timing_reset()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        poses[k] = step(args.warmup + k)
+    run(args.warmup, args.steps, poses)
     for c in ctxs:
         c.sync()
     if dist is not None:  # RCCL pose gather over xGMI
@@ -226,6 +246,10 @@ def main():
         gather_poses(dist, poses, "cuda")
         torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if prof:
+        n = max(tacc[:, 3].sum(), 1)
+        print(f"per pair (ms): build-enqueue {1e3 * tacc[:, 0].sum() / n:.2f}  pbmap-stage {1e3 * tacc[:, 1].sum() / n:.2f}"
+              f"  dense-wait {1e3 * tacc[:, 2].sum() / n:.2f}", file=sys.stderr)
     barrier()
     l0_ms, l0_n = 0.0, 0
     stage = {}

@@ -98,6 +98,52 @@ void convex_hull(HPlane& pl, const std::vector<P3>& pts) {
     for (int c : chain) pl.hull.push_back(pts[q[c].i]);
 }
 
+// Akl-Toussaint prefilter for convex_hull: keep[i] = 0 for points strictly inside the octagon spanned
+// by the extreme points in 8 directions (a convex polygon inside the hull), by a relative margin far
+// above the rounding of the double turn test.  In exact arithmetic the monotone chain's output does
+// not depend on interior points, so the hull is unchanged while a 40k-point plane shrinks to its rim.
+template <class Get>
+static int hull_prefilter(int n, int a, int b, Get get, std::vector<char>& keep) {
+    keep.assign(n, 1);
+    if (n < 64) return n;
+    // extreme indices for directions at 180, 225, 270, 315, 0, 45, 90, 135 degrees (CCW order)
+    int ex[8];
+    double best[8];
+    for (int k = 0; k < 8; ++k) { ex[k] = 0; best[k] = -INFINITY; }
+    for (int i = 0; i < n; ++i) {
+        const P3 q = get(i);
+        const double x = q.at(a), y = q.at(b);
+        const double v[8] = {-x, -x - y, -y, x - y, x, x + y, y, y - x};
+        for (int k = 0; k < 8; ++k)
+            if (v[k] > best[k]) { best[k] = v[k]; ex[k] = i; }
+    }
+    double vx[8], vy[8];
+    int m = 0;
+    for (int k = 0; k < 8; ++k) {
+        const P3 q = get(ex[k]);
+        const double x = q.at(a), y = q.at(b);
+        if (m && x == vx[m - 1] && y == vy[m - 1]) continue;
+        vx[m] = x; vy[m] = y; ++m;
+    }
+    if (m > 1 && vx[m - 1] == vx[0] && vy[m - 1] == vy[0]) --m;
+    if (m < 3) return n;
+    int kept = 0;
+    for (int i = 0; i < n; ++i) {
+        const P3 q = get(i);
+        const double x = q.at(a), y = q.at(b);
+        bool inside = true;
+        for (int k = 0; k < m && inside; ++k) {
+            const int k1 = (k + 1) % m;
+            const double ex_ = vx[k1] - vx[k], ey_ = vy[k1] - vy[k], px = x - vx[k], py = y - vy[k];
+            const double cr = ex_ * py - ey_ * px;
+            inside = cr > 1e-7 * (std::fabs(ex_) + std::fabs(ey_)) * (std::fabs(px) + std::fabs(py));
+        }
+        keep[i] = !inside;
+        kept += keep[i];
+    }
+    return kept;
+}
+
 // computeMassCenterAndArea
 void area_and_center(HPlane& pl) {
     const int k0 = axis_of(pl.normal), k1 = (k0 + 1) % 3, k2 = (k0 + 2) % 3;
@@ -421,6 +467,7 @@ int planes_assemble(r360_frame* f) {
     const auto t2 = now();
     const r360_calib* cal = f->calib;
     std::vector<std::vector<HPlane>> local(8);
+    std::vector<char> keep;
     for (int s = 0; s < 8; ++s) {
         const float* Rt = cal->rt[s];
         for (int m = 0; m < P.h_nmodels[s]; ++m) {
@@ -433,14 +480,21 @@ int planes_assemble(r360_frame* f) {
             pl.curvature = O.model.curvature;
             pl.st = O.stats;
             std::vector<P3> pts;
+            const int ax = axis_of(pl.normal), ha = (ax + 1) % 3, hb = (ax + 2) % 3;
             if (O.n_contour > 0) {
-                for (int k = 0; k < O.n_contour; ++k) {
-                    const float4 q = contour[O.contour_off + k];
-                    pts.push_back({q.x, q.y, q.z});
-                }
+                const float4* c = contour + O.contour_off;
+                auto get = [c](int k) { return P3{c[k].x, c[k].y, c[k].z}; };
+                hull_prefilter(O.n_contour, ha, hb, get, keep);
+                for (int k = 0; k < O.n_contour; ++k)
+                    if (keep[k]) pts.push_back(get(k));
             } else {                                                    // "HULL 000" (:1017-1026)
                 // VoxelGrid centroids from k_vox_*, in increasing voxel index (PCL's output order)
-                std::vector<VoxOut> v(vox + O.vox_off, vox + O.vox_off + O.n_vox);
+                const VoxOut* v0 = vox + O.vox_off;
+                auto get = [v0](int k) { return P3{v0[k].x, v0[k].y, v0[k].z}; };
+                hull_prefilter(O.n_vox, ha, hb, get, keep);
+                std::vector<VoxOut> v;
+                for (int k = 0; k < O.n_vox; ++k)
+                    if (keep[k]) v.push_back(v0[k]);
                 std::sort(v.begin(), v.end(), [](const VoxOut& a, const VoxOut& b) { return a.key < b.key; });
                 for (const VoxOut& q : v) pts.push_back({q.x, q.y, q.z});
             }
@@ -592,7 +646,7 @@ int gpu_tables(r360_ctx* ctx, const std::vector<HPlane>& S, const std::vector<in
     R360_HIP(hipMemcpyAsync(ctx->h_unary, ctx->d_unary, (size_t)ns * nt, hipMemcpyDeviceToHost, st));
     R360_HIP(hipMemcpyAsync(ctx->h_bin, ctx->d_bin, sizeof(unsigned long long) * (size_t)ns * nt * tb.words,
                             hipMemcpyDeviceToHost, st));
-    R360_HIP(hipStreamSynchronize(st));
+    if (ctx_wait(ctx)) return -1;
     return 0;
 }
 

@@ -33,6 +33,12 @@ extern "C" const char* r360_version(void) { return "rgbd360_amd 0.1 (gfx950)"; }
     } while (0)
 
 // ------------------------------------------------------------------ timing (HIP events on the ctx stream)
+int ctx_wait(r360_ctx* ctx) {
+    R360_HIP(hipEventRecord(ctx->wait_ev, ctx->stream));
+    R360_HIP(hipEventSynchronize(ctx->wait_ev));
+    return 0;
+}
+
 int timing_begin(r360_ctx* ctx, const char* name) {
     if (!ctx || !ctx->timing) return -1;
     if (ctx->ev_used + 2 > (int)ctx->ev_pool.size()) {
@@ -97,6 +103,7 @@ extern "C" int r360_ctx_create(int device, r360_ctx** out) {
     r360_ctx* c = new r360_ctx;
     c->device = device;
     R360_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    R360_HIP(hipEventCreateWithFlags(&c->wait_ev, hipEventDisableTiming | hipEventBlockingSync));
     R360_HIP(hipMalloc(&c->d_state, sizeof(IcpState)));
     R360_HIP(hipMemset(c->d_state, 0, sizeof(IcpState)));
     c->partials_cap = 2048;
@@ -111,6 +118,7 @@ extern "C" void r360_ctx_destroy(r360_ctx* c) {
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
     for (auto e : c->ev_pool) hipEventDestroy(e);
+    hipEventDestroy(c->wait_ev);
     hipFree(c->d_state);
     hipFree(c->d_partials);
     hipHostFree(c->h_state);
@@ -122,8 +130,7 @@ extern "C" void r360_ctx_destroy(r360_ctx* c) {
 
 extern "C" int r360_ctx_sync(r360_ctx* c) {
     CHECK_ARG(c, "null ctx");
-    R360_HIP(hipStreamSynchronize(c->stream));
-    return 0;
+    return ctx_wait(c);
 }
 extern "C" void* r360_ctx_stream(r360_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
@@ -547,7 +554,7 @@ extern "C" int r360_align360_result(r360_ctx* ctx, float pose_out[16], float H_o
     CHECK_ARG(ctx && ctx->async_pending, "no alignment pending");
     IcpState* h = ctx->h_state;
     R360_HIP(hipMemcpyAsync(h, ctx->d_state, sizeof(IcpState), hipMemcpyDeviceToHost, ctx->stream));
-    R360_HIP(hipStreamSynchronize(ctx->stream));
+    if (ctx_wait(ctx)) return -1;
     ctx->async_pending = 0;
     if (pose_out) memcpy(pose_out, h->pose, sizeof(float) * 16);
     if (H_out) memcpy(H_out, h->Hout, sizeof(float) * 36);

@@ -621,20 +621,22 @@ int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src
     // 4-pixel units on the large levels, one pixel per thread where that still fits one resident
     // round (latency-bound small levels); R360_ICP_PF=0/1 forces one form (experiments)
     static const int pf_env = env_int("R360_ICP_PF", -1);
-    // one resident round: CUs x workgroups per CU of the launched form (grid-stride beyond it)
-    static int cus = -1, per[3] = {0, 0, 0};
     static const int cap_env = env_int("R360_ICP_CAP", -1);
-    if (cus < 0) {
+    // one resident round: CUs x workgroups per CU of the launched form (grid-stride beyond it)
+    struct Occ { int cus = 0, per[3] = {0, 0, 0}; };
+    static const Occ occ = [] {   // thread-safe one-time query (contexts may be driven from several threads)
+        Occ o;
         int dev = 0;
         (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per[0], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 0>, TPB, 0);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per[1], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 1>, TPB, 0);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per[2], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 2>, TPB, 0);
-    }
+        (void)hipDeviceGetAttribute(&o.cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[0], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 0>, TPB, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[1], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 1>, TPB, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[2], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 2>, TPB, 0);
+        return o;
+    }();
     const int npx = Ls.rows * Ls.cols;
     const int pf = pf_env >= 0 ? pf_env : ((Ls.cols % 64 == 0) ? 2 : 0);
-    int cap = cap_env > 0 ? cap_env : cus * (per[pf] > 0 ? per[pf] : 4);
+    int cap = cap_env > 0 ? cap_env : occ.cus * (occ.per[pf] > 0 ? occ.per[pf] : 4);
     if (cap > ctx->partials_cap) cap = ctx->partials_cap;
     int nb = pf == 1 ? icp_blocks_for(npx) : (npx + TPB - 1) / TPB;
     if (nb > cap) nb = cap;

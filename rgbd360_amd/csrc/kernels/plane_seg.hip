@@ -510,101 +510,176 @@ __global__ void __launch_bounds__(MOM_TPB) k_model_stats(const float4* __restric
     }
 }
 
-// findLabeledRegionBoundary on a per-region membership bitmap in LDS (one workgroup per region);
-// mode 0 counts, mode 1 writes the contour points (local frame).  The bitmap has a one-pixel zero
-// border, so a step reads its 3x3 neighbourhood with six independent LDS loads and no bounds tests.
-__global__ void __launch_bounds__(256) k_trace(const int* __restrict__ labf, const float4* __restrict__ cloud, int w,
-                                              int h, const int* __restrict__ nmodels, PlaneOut* __restrict__ out,
-                                              float4* __restrict__ pool, long pool_cap, int mode,
-                                              int* __restrict__ err) {
-    extern __shared__ unsigned bits[];
-    const int s = blockIdx.y, m = blockIdx.x;
-    if (m >= nmodels[s]) return;
-    PlaneOut& O = out[s * R360_MAX_MODELS + m];
+// findLabeledRegionBoundary (Moore-neighbour trace), all regions of a sensor in one workgroup.
+// k_nbmask first stores, per pixel, the 8-bit mask of the neighbours carrying the same refined label
+// (bit d = direction d of {W, NW, N, NE, E, SE, S, SW}; out-of-image neighbours are 0).  A trace only
+// ever stands on member pixels of its region, so that mask is exactly the region-membership
+// neighbourhood of the reference's trace, and one step is one LDS byte read plus a rotate /
+// find-first-set.  k_trace loads the masks of its sensor into LDS, lane m of wave 0 walks region m
+// (all regions of the sensor in parallel), appending the visited pixel indices to 32-entry chunks of
+// an LDS list; then the whole workgroup writes the contour points to the pool in trace order.
+__global__ void k_nbmask(const int* __restrict__ labf, int w, int h, uint8_t* __restrict__ nb) {
     const int N = w * h;
-    const int RW = (w + 2 + 31) / 32 + 1;                  // words per padded row (+1 for the pair reads)
-    const int NW = (h + 2) * RW;
-    const int* Lb = labf + (long)s * N;
-    const int label = O.model.label;
-    for (int q = threadIdx.x; q < NW; q += blockDim.x) {
-        const int yy = q / RW, cw = q - (q / RW) * RW;
-        const int y = yy - 1;
-        unsigned word = 0;
-        if (y >= 0 && y < h)
-            for (int b = 0; b < 32; ++b) {
-                const int x = cw * 32 + b - 1;
-                if (x >= 0 && x < w && Lb[y * w + x] == label) word |= 1u << b;
-            }
-        bits[q] = word;
-    }
-    __syncthreads();
-    if (threadIdx.x != 0) return;
-    // bits of padded columns px..px+2 in padded row yy
-    auto row3 = [&](int px, int yy) -> unsigned {
-        const int q = yy * RW + (px >> 5);
-        const unsigned long long v = (unsigned long long)bits[q] | ((unsigned long long)bits[q + 1] << 32);
-        return (unsigned)(v >> (px & 31)) & 7u;
-    };
-    const float4* P = cloud + (long)s * N;
-    const int dxs[8] = {-1, -1, 0, 1, 1, 1, 0, -1}, dys[8] = {0, -1, -1, -1, 0, 1, 1, 1};
-    // neighbour d of the 3x3 block (rows r0 (y-1), r1 (y), r2 (y+1); bit i = column x-1+i)
-    auto nbit = [&](unsigned r0, unsigned r1, unsigned r2, int d) -> int {
-        const int dx = dxs[d] + 1, dy = dys[d];
-        const unsigned r = dy < 0 ? r0 : (dy > 0 ? r2 : r1);
-        return (r >> dx) & 1;
-    };
-    const int start = O.start;
-    int cx = start % w, cy = start / w, cidx = start, dir = -1;
-    {
-        const unsigned r0 = row3(cx, cy), r1 = row3(cx, cy + 1), r2 = row3(cx, cy + 2);
-        for (int d = 0; d < 8; ++d) {
-            const int x = cx + dxs[d], y = cy + dys[d];
-            if (x >= 0 && x < w && y >= 0 && y < h && !nbit(r0, r1, r2, d)) { dir = d; break; }
+    const long total = 8L * N;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int s = (int)(i / N), p = (int)(i - (long)s * N);
+        const int* Lb = labf + (long)s * N;
+        const int y = p / w, x = p - y * w;
+        const int L = Lb[p];
+        unsigned m = 0;
+        if (L >= 0) {
+            const bool l = x > 0, r = x < w - 1, u = y > 0, d = y < h - 1;
+            if (l && Lb[p - 1] == L) m |= 1u;
+            if (l && u && Lb[p - w - 1] == L) m |= 2u;
+            if (u && Lb[p - w] == L) m |= 4u;
+            if (r && u && Lb[p - w + 1] == L) m |= 8u;
+            if (r && Lb[p + 1] == L) m |= 16u;
+            if (r && d && Lb[p + w + 1] == L) m |= 32u;
+            if (d && Lb[p + w] == L) m |= 64u;
+            if (l && d && Lb[p + w - 1] == L) m |= 128u;
         }
+        nb[i] = (uint8_t)m;
     }
-    if (dir < 0) {
-        if (mode == 0) O.n_contour = 0;
-        return;
-    }
-    long n = 0;
-    const long off = mode ? O.contour_off : 0;
-    const long max_len = 8L * N;
-    if (mode && off + n < pool_cap) pool[off + n] = P[start];
-    ++n;
-    do {
-        const unsigned r0 = row3(cx, cy), r1 = row3(cx, cy + 1), r2 = row3(cx, cy + 2);
-        unsigned mask8 = 0;
-#pragma unroll
-        for (int d = 0; d < 8; ++d) mask8 |= (unsigned)nbit(r0, r1, r2, d) << d;
-        int nd = 0;
-        for (int d = 1; d <= 8; ++d) {
-            nd = (dir + d) & 7;
-            if ((mask8 >> nd) & 1) break;
-        }
-        dir = (nd + 4) & 7;
-        cidx += dys[nd] * w + dxs[nd];
-        cx += dxs[nd];
-        cy += dys[nd];
-        if (mode && off + n < pool_cap) pool[off + n] = P[cidx];
-        ++n;
-        if (n > max_len) { atomicOr(err, 8); break; }
-    } while (cidx != start);
-    if (mode == 0) O.n_contour = (int)n;
 }
 
-// contour pool offsets (single thread)
-__global__ void k_alloc(const int* __restrict__ nmodels, PlaneOut* __restrict__ out, long* __restrict__ totals,
-                        long contour_cap, int* __restrict__ err) {
+constexpr int TR_TPB = 1024;
+constexpr int TR_CHUNK = 32;
+constexpr int TR_LIST = 12288;                 // contour pixel indices per sensor held in LDS
+constexpr int TR_NCH = TR_LIST / TR_CHUNK;
+
+constexpr int TR_NB_MAX = 96 * 1024;          // largest sensor (w*h) whose masks are staged in LDS
+
+// Moore step: next direction = first neighbour in the mask clockwise after dir (the d = 1..8 scan of
+// the reference loop); an empty mask keeps nd = dir (the scan's last candidate), as the reference does.
+__device__ __forceinline__ int trace_next(unsigned m8, int dir) {
+    const unsigned r = ((m8 | (m8 << 8)) >> ((dir + 1) & 7)) & 0xffu;
+    return r ? (dir + 1 + __builtin_ctz(r)) & 7 : dir;
+}
+
+template <bool LDS>
+__global__ void __launch_bounds__(TR_TPB) k_trace(const uint8_t* __restrict__ nbg, const float4* __restrict__ cloud,
+                                                 int w, int h, const int* __restrict__ nmodels,
+                                                 PlaneOut* __restrict__ out, float4* __restrict__ pool, long pool_cap,
+                                                 int* __restrict__ err) {
+    // static LDS (a workgroup may hold all 160 KiB): masks, index list, chunk tables
+    __shared__ __attribute__((aligned(16))) unsigned char sm[LDS ? TR_NB_MAX : 16];
+    __shared__ int list[TR_LIST], link[TR_NCH], cout_[TR_NCH], cown[TR_NCH];
+    __shared__ int s_nch, s_len[R360_MAX_MODELS], s_head[R360_MAX_MODELS], s_over;
+    __shared__ long s_off[R360_MAX_MODELS];
+    const int s = blockIdx.x, N = w * h;
+    const uint8_t* nbs = nbg + (long)s * N;
+    const int nm = nmodels[s];
+    if (LDS) {
+        const uint4* src4 = reinterpret_cast<const uint4*>(nbs);
+        uint4* dst4 = reinterpret_cast<uint4*>(sm);
+        if ((N & 15) == 0 && ((reinterpret_cast<uintptr_t>(nbs) & 15) == 0)) {
+            for (int q = threadIdx.x; q < N / 16; q += TR_TPB) dst4[q] = src4[q];
+        } else {
+            for (int q = threadIdx.x; q < N; q += TR_TPB) sm[q] = nbs[q];
+        }
+    }
+    if (threadIdx.x == 0) { s_nch = 0; s_over = 0; }
+    __syncthreads();
+    const uint8_t* nb = LDS ? sm : nbs;
+    const int dxs[8] = {-1, -1, 0, 1, 1, 1, 0, -1}, dys[8] = {0, -1, -1, -1, 0, 1, 1, 1};
+    const long max_len = 8L * N;
+    const int m = threadIdx.x;
+    int dir0 = -1, start = 0;
+    if (m < nm) {
+        PlaneOut& O = out[s * R360_MAX_MODELS + m];
+        start = O.start;
+        const int cx = start % w, cy = start / w;
+        const unsigned m8 = nb[start];
+        for (int d = 0; d < 8; ++d) {
+            const int x = cx + dxs[d], y = cy + dys[d];
+            if (x >= 0 && x < w && y >= 0 && y < h && !((m8 >> d) & 1)) { dir0 = d; break; }
+        }
+        long n = 0;
+        if (dir0 >= 0) {
+            int chunk = atomicAdd(&s_nch, 1), pos = 0;
+            s_head[m] = chunk;
+            auto append = [&](int idx) {
+                if (chunk < TR_NCH) list[chunk * TR_CHUNK + pos] = idx;
+                if (++pos == TR_CHUNK) {
+                    const int nc = atomicAdd(&s_nch, 1);
+                    if (chunk < TR_NCH) link[chunk] = nc;
+                    chunk = nc;
+                    pos = 0;
+                }
+            };
+            append(start);
+            n = 1;
+            int cidx = start, dir = dir0;
+            do {
+                const int nd = trace_next(nb[cidx], dir);
+                dir = (nd + 4) & 7;
+                cidx += dys[nd] * w + dxs[nd];
+                append(cidx);
+                if (++n > max_len) { atomicOr(err, 8); break; }
+            } while (cidx != start);
+        }
+        s_len[m] = (int)n;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        // contour pool partitioned per sensor: sensor s owns [s, s+1) * pool_cap / 8
+        const long base = s * (pool_cap / 8), cap = pool_cap / 8;
+        long o = 0;
+        for (int k = 0; k < nm; ++k) { s_off[k] = base + o; o += s_len[k]; }
+        if (o > cap) atomicOr(err, 16);
+        if (s_nch > TR_NCH) s_over = 1;
+        for (int k = 0; k < nm; ++k) {
+            PlaneOut& O = out[s * R360_MAX_MODELS + k];
+            O.n_contour = s_len[k];
+            O.contour_off = s_off[k];
+        }
+    }
+    __syncthreads();
+    if (!s_over) {
+        // chunk -> (region, output position), one lane per region walking its chain
+        if (m < nm && s_len[m] > 0) {
+            int c = s_head[m];
+            for (int j = 0; j * TR_CHUNK < s_len[m]; ++j) {
+                cout_[c] = j * TR_CHUNK;
+                cown[c] = m;
+                if ((j + 1) * TR_CHUNK < s_len[m]) c = link[c];
+            }
+        }
+        __syncthreads();
+        const float4* P = cloud + (long)s * N;
+        const long cap_end = (s + 1) * (pool_cap / 8);
+        for (int e = threadIdx.x; e < s_nch * TR_CHUNK; e += TR_TPB) {
+            const int c = e / TR_CHUNK, k = cout_[c] + (e - c * TR_CHUNK);
+            const int r = cown[c];
+            if (k < s_len[r]) {
+                const long dst = s_off[r] + k;
+                if (dst < cap_end) pool[dst] = P[list[e]];
+            }
+        }
+    } else if (m < nm && dir0 >= 0) {
+        // more contour pixels than the LDS list holds: walk again, writing the points directly
+        const float4* P = cloud + (long)s * N;
+        const long cap_end = (s + 1) * (pool_cap / 8);
+        long n = 0, dst = s_off[m];
+        int cidx = start, dir = dir0;
+        if (dst < cap_end) pool[dst] = P[start];
+        ++n;
+        do {
+            const int nd = trace_next(nb[cidx], dir);
+            dir = (nd + 4) & 7;
+            cidx += dys[nd] * w + dxs[nd];
+            if (dst + n < cap_end) pool[dst + n] = P[cidx];
+        } while (++n <= max_len && cidx != start);
+    }
+}
+
+// contour total of the frame (profiling / pool accounting)
+__global__ void k_alloc(const int* __restrict__ nmodels, const PlaneOut* __restrict__ out, long* __restrict__ totals) {
     if (threadIdx.x != 0) return;
     long co = 0;
     for (int s = 0; s < 8; ++s)
-        for (int m = 0; m < nmodels[s]; ++m) {
-            PlaneOut& O = out[s * R360_MAX_MODELS + m];
-            O.contour_off = co;
-            co += O.n_contour;
-        }
+        for (int m = 0; m < nmodels[s]; ++m) co += out[s * R360_MAX_MODELS + m].n_contour;
     totals[0] = co;
-    if (co > contour_cap) atomicOr(err, 16);
 }
 
 // pcl::VoxelGrid (leaf 0.05) of the inliers of regions without a contour (Frame360.h:1017-1026):
@@ -744,12 +819,16 @@ int launch_segmentation(r360_frame* f) {
     slot = timing_begin(ctx, "k_model_stats");
     hipLaunchKernelGGL(k_model_stats, dim3(R360_MAX_MODELS, 8), dim3(MOM_TPB), 0, st, P.cloud, P.rgb, P.lab, P.labf, N,
                        P.models, P.nmodels, f->calib->d_rt, P.out);
-    const size_t lds = sizeof(unsigned) * (size_t)(h + 2) * ((w + 2 + 31) / 32 + 1);
-    hipLaunchKernelGGL(k_trace, dim3(R360_MAX_MODELS, 8), dim3(256), lds, st, P.labf, P.cloud, w, h, P.nmodels, P.out,
-                       P.contour, P.contour_cap, 0, P.err);
-    hipLaunchKernelGGL(k_alloc, dim3(1), dim3(64), 0, st, P.nmodels, P.out, P.totals, P.contour_cap, P.err);
-    hipLaunchKernelGGL(k_trace, dim3(R360_MAX_MODELS, 8), dim3(256), lds, st, P.labf, P.cloud, w, h, P.nmodels, P.out,
-                       P.contour, P.contour_cap, 1, P.err);
+    // the refinement's closeness masks are dead here: their storage holds the neighbour masks
+    uint8_t* nbm = reinterpret_cast<uint8_t*>(P.mask);
+    hipLaunchKernelGGL(k_nbmask, dim3(blocks), dim3(256), 0, st, P.labf, w, h, nbm);
+    if (N <= TR_NB_MAX)
+        hipLaunchKernelGGL(k_trace<true>, dim3(8), dim3(TR_TPB), 0, st, nbm, P.cloud, w, h, P.nmodels, P.out,
+                           P.contour, P.contour_cap, P.err);
+    else
+        hipLaunchKernelGGL(k_trace<false>, dim3(8), dim3(TR_TPB), 0, st, nbm, P.cloud, w, h, P.nmodels, P.out,
+                           P.contour, P.contour_cap, P.err);
+    hipLaunchKernelGGL(k_alloc, dim3(1), dim3(64), 0, st, P.nmodels, P.out, P.totals);
     timing_end(ctx, slot);
     R360_HIP(hipGetLastError());
     slot = timing_begin(ctx, "k_voxel");

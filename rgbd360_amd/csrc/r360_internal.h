@@ -151,6 +151,7 @@ struct PbMapHost;                    // host PbMap (host/pbmap.cpp)
 struct r360_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipEvent_t wait_ev = nullptr;   // blocking-sync event: host waits sleep instead of spinning
     IcpState* d_state = nullptr;
     double* d_partials = nullptr;
     int partials_cap = 0;
@@ -241,4 +242,7 @@ void planes_join(r360_frame* f);
 
 // timing helpers (host_runtime.cpp)
 int  timing_begin(r360_ctx* ctx, const char* name);
+// Wait for everything enqueued on the context's stream, sleeping (blocking-sync event) rather than
+// spinning, so many pipelines' host threads can wait while plane assembly threads keep the cores.
+int  ctx_wait(r360_ctx* ctx);
 void timing_end(r360_ctx* ctx, int slot);
