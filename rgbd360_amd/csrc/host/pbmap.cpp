@@ -337,11 +337,15 @@ int plane_bufs_alloc(r360_frame* f) {
     R360_HIP(hipMalloc(&P.dist0, sizeof(float) * T));
     R360_HIP(hipMalloc(&P.dist, sizeof(float) * T));
     R360_HIP(hipMalloc(&P.grids, sizeof(float2) * 16 * P.grid_cells));
+    R360_HIP(hipMalloc(&P.zmm, sizeof(int) * 16));
     R360_HIP(hipMalloc(&P.parent, sizeof(int) * T));
     R360_HIP(hipMalloc(&P.root, sizeof(int) * T));
     R360_HIP(hipMalloc(&P.lab, sizeof(int) * T));
     R360_HIP(hipMalloc(&P.labf, sizeof(int) * T));
     R360_HIP(hipMalloc(&P.cnt, sizeof(int) * T));
+    R360_HIP(hipMalloc(&P.blist, sizeof(int) * T));
+    R360_HIP(hipMalloc(&P.mlist, sizeof(int) * T));
+    R360_HIP(hipMalloc(&P.aux, sizeof(int) * 8 * (3 * R360_MAX_BIG + 3 * R360_MAX_MODELS)));
     R360_HIP(hipMalloc(&P.nlab, sizeof(int) * 8));
     R360_HIP(hipMalloc(&P.big, sizeof(int) * 8 * R360_MAX_BIG));
     R360_HIP(hipMalloc(&P.nbig, sizeof(int) * 8));
@@ -368,7 +372,7 @@ int plane_bufs_alloc(r360_frame* f) {
 void plane_bufs_free(r360_frame* f) {
     PlaneBufs& P = f->pl;
     planes_join(f);
-    void* dev[] = {P.cloud, P.rgb, P.nrm, P.dist0, P.dist, P.grids, P.parent, P.root, P.lab, P.labf, P.cnt, P.nlab,
+    void* dev[] = {P.cloud, P.rgb, P.nrm, P.dist0, P.dist, P.grids, P.zmm, P.parent, P.root, P.lab, P.labf, P.cnt, P.blist, P.mlist, P.aux, P.nlab,
                    P.big, P.nbig, P.mom, P.models, P.nmodels, P.state, P.mask, P.out, P.totals, P.err};
     for (void* p : dev) hipFree(p);
     hipHostFree(P.contour);

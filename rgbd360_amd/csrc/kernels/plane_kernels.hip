@@ -1,7 +1,7 @@
 // plane_kernels.hip — the per-pixel plane half of Frame360 on gfx950:
 //   k_cloud       back-projection + 2x2 upper-median downsample   (CloudRGBD_Ext.h:78-139,
 //                 DownsampleRGBD.h:209-311)
-//   k_bilateral   pcl::FastBilateralFilter (sigma_s 10, sigma_r 0.05), one workgroup per sensor
+//   k_bil_*       pcl::FastBilateralFilter (sigma_s 10, sigma_r 0.05): splat / fused blur / slice
 //   k_dcm         depth-change map + distance-map init            (IntegralImageNormalEstimation)
 //   k_distmap     two-pass chamfer distance map, row bands with halos (exact below the 9.5 cap)
 //   k_normals     AVERAGE_3D_GRADIENT normals from exact window sums + plane offset d = p.n
@@ -17,12 +17,20 @@ namespace {
 __device__ __forceinline__ bool isfin(float v) { return __builtin_isfinite(v); }
 
 // ------------------------------------------------------------------ A3
-__global__ void k_cloud(const float* __restrict__ depth_m, const uint8_t* __restrict__ bgr, int rows, int cols,
-                        float inv_f, float ox, float oy, float4* __restrict__ cloud, uchar4* __restrict__ rgb) {
-    const int w = cols / 2, h = rows / 2;
-    const long N = (long)w * h, total = 8 * N;
-    const float nan = __builtin_nanf("");
-    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+// order-preserving float <-> int map for integer atomic min / max
+__device__ __forceinline__ int f2ord(float f) {
+    const int b = __float_as_int(f);
+    return b >= 0 ? b : b ^ 0x7fffffff;
+}
+__device__ __forceinline__ float ord2f(int e) { return __int_as_float(e >= 0 ? e : e ^ 0x7fffffff); }
+constexpr int kOrdMinInit = 0x7f7f7f7f;            // memset byte 0x7f: above every finite float
+constexpr int kOrdMaxInit = (int)0x80808080;       // memset byte 0x80: below every finite float
+
+// one output point of k_cloud; returns its z
+__device__ __forceinline__ float cloud_point_impl(const float* __restrict__ depth_m, const uint8_t* __restrict__ bgr, int rows,
+                                  int cols, float inv_f, float ox, float oy, float4* __restrict__ cloud,
+                                  uchar4* __restrict__ rgb, long i, int w, long N, float nan) {
+    {
         const int s = (int)(i / N);
         const int j = (int)(i - (long)s * N);
         const int r2 = j / w, c2 = j - (j / w) * w;
@@ -62,115 +70,187 @@ __global__ void k_cloud(const float* __restrict__ depth_m, const uint8_t* __rest
         cloud[i] = o;
         const uint8_t* b = bgr + ((long)s * rows * cols + (long)(r + 1) * cols + c + 1) * 3;
         rgb[i] = make_uchar4(b[2], b[1], b[0], 0);
+        return o.z;
+    }
+}
+
+__global__ void k_cloud(const float* __restrict__ depth_m, const uint8_t* __restrict__ bgr, int rows, int cols,
+                        float inv_f, float ox, float oy, float4* __restrict__ cloud, uchar4* __restrict__ rgb,
+                        int* __restrict__ zmm, int* __restrict__ wmm) {
+    const int w = cols / 2, h = rows / 2;
+    const long N = (long)w * h, total = 8 * N;
+    const float nan = __builtin_nanf("");
+    const long stride = (long)gridDim.x * blockDim.x;
+    for (long i0 = blockIdx.x * (long)blockDim.x + (threadIdx.x & ~63); i0 < total; i0 += stride) {
+        const long i = i0 + (threadIdx.x & 63);
+        // per-sensor min / max of the finite depths (the bilateral filter's range), wave-reduced
+        int emin = kOrdMinInit, emax = kOrdMaxInit;
+        const int s0 = (int)(i0 / N);
+        if (i < total) {
+            const float z = cloud_point_impl(depth_m, bgr, rows, cols, inv_f, ox, oy, cloud, rgb, i, w, N, nan);
+            if (isfin(z)) { emin = f2ord(z); emax = emin; }
+        }
+        const bool one_sensor = (i0 + 63 < total) && ((i0 + 63) / N == s0);
+        if (one_sensor) {   // per-wave partial, reduced per sensor by k_zrange (no contended atomics)
+            for (int o = 32; o > 0; o >>= 1) {
+                emin = min(emin, __shfl_xor(emin, o, 64));
+                emax = max(emax, __shfl_xor(emax, o, 64));
+            }
+            if ((threadIdx.x & 63) == 0) {
+                wmm[2 * (i0 >> 6)] = emin;
+                wmm[2 * (i0 >> 6) + 1] = emax;
+            }
+        } else if (i < total && emin != kOrdMinInit) {
+            const int s = (int)(i / N);
+            atomicMin(zmm + s, emin);
+            atomicMax(zmm + 8 + s, emax);
+        }
+    }
+}
+
+
+// per-sensor depth range from k_cloud's per-wave partials (waves inside one sensor)
+__global__ void __launch_bounds__(1024) k_zrange(const int* __restrict__ wmm, long N, int* __restrict__ zmm) {
+    __shared__ int smin[16], smax[16];
+    const int s = blockIdx.x;
+    const long w0 = (s * N + 63) / 64, w1 = ((s + 1) * N) / 64;   // waves starting inside the sensor
+    int emin = kOrdMinInit, emax = kOrdMaxInit;
+    for (long w = w0 + threadIdx.x; w < w1; w += blockDim.x) {
+        if ((w * 64 + 63) / N != s) continue;                      // straddling wave: atomics in k_cloud
+        emin = min(emin, wmm[2 * w]);
+        emax = max(emax, wmm[2 * w + 1]);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        emin = min(emin, __shfl_xor(emin, o, 64));
+        emax = max(emax, __shfl_xor(emax, o, 64));
+    }
+    if ((threadIdx.x & 63) == 0) { smin[threadIdx.x >> 6] = emin; smax[threadIdx.x >> 6] = emax; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int q = 1; q < (int)(blockDim.x >> 6); ++q) { emin = min(emin, smin[q]); emax = max(emax, smax[q]); }
+        if (emin != kOrdMinInit) {
+            atomicMin(zmm + s, emin);
+            atomicMax(zmm + 8 + s, emax);
+        }
     }
 }
 
 // ------------------------------------------------------------------ A4
-// One workgroup per sensor.  grid0/grid1: 2 x (sw*sh*sd) float2 cells each, zeroed here.
-constexpr int BIL_TPB = 1024;
+// pcl::FastBilateralFilter as four fully parallel kernels over the 8 sensors:
+//   splat  one thread per (sx, sy) grid column, the column's sd cells accumulated in LDS in the
+//          reference's x-major / y-minor pixel order (so every cell sum has the reference's order);
+//   blur   per axis the two [1 2 1]/4 iterations fused (each output cell recomputes the three
+//          first-iteration cells it needs, with the same float expressions), boundaries zero;
+//   slice  trilinear interpolation, z <- D0 / D1.
+// Grids are stored z-major ([sz][sy][sx]); the depth range comes from k_cloud's atomics.
+constexpr int BIL_SD_MAX = 208;
+constexpr int BIL_COLS = 64;
 
-__device__ float block_reduce_minmax(float v, bool is_max, float* red) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-        const float o = __shfl_xor(v, m, 64);
-        v = is_max ? (o > v ? o : v) : (o < v ? o : v);
-    }
-    __syncthreads();
-    if (lane == 0) red[wid] = v;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        float r = red[0];
-        for (int k = 1; k < (int)(blockDim.x >> 6); ++k) r = is_max ? (red[k] > r ? red[k] : r) : (red[k] < r ? red[k] : r);
-        red[16] = r;
-    }
-    __syncthreads();
-    return red[16];
+// depth range and grid depth of sensor s; false when the filter does not run (no finite depth, or
+// a range beyond the grid capacity, which is flagged)
+__device__ __forceinline__ bool bil_params(const int* __restrict__ zmm, int s, int sd_max, float& bmin, float& bmax,
+                                           long& sd, bool& over) {
+    over = false;
+    const int emax = zmm[8 + s];
+    if (emax == kOrdMaxInit) return false;
+    bmin = ord2f(zmm[s]);
+    bmax = ord2f(emax);
+    const float base_delta = bmax - bmin;
+    sd = (long)(unsigned long)(base_delta / 0.05f) + 5;
+    over = sd > sd_max;
+    return !over;
 }
 
-__global__ void __launch_bounds__(BIL_TPB) k_bilateral(float4* __restrict__ cloud_all, int w, int h,
-                                                      float2* __restrict__ grids, long grid_cells, int sd_max,
-                                                      int* __restrict__ err) {
-    __shared__ float red[17];
-    const int s = blockIdx.x;
-    float4* cloud = cloud_all + (long)s * w * h;
-    float2* A = grids + (long)s * 2 * grid_cells;
-    float2* B = A + grid_cells;
-    const int n = w * h;
-    const float sigma_s = 10.0f, sigma_r = 0.05f;
-    float lmax = -3.40282347e38f, lmin = 3.40282347e38f;
-    int lfound = 0;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        const float z = cloud[i].z;
-        if (isfin(z)) {
-            lmax = lmax < z ? z : lmax;
-            lmin = lmin > z ? z : lmin;
-            lfound = 1;
-        }
-    }
-    const float base_max = block_reduce_minmax(lmax, true, red);
-    const float base_min = block_reduce_minmax(lmin, false, red);
-    const int found = __syncthreads_or(lfound);
-    if (!found) return;
-    for (int i = threadIdx.x; i < n; i += blockDim.x)
-        if (!isfin(cloud[i].z)) cloud[i].z = base_max;
-    const float base_delta = base_max - base_min;
-    const long sw = (long)(unsigned long)((float)(w - 1) / sigma_s) + 5;
-    const long sh = (long)(unsigned long)((float)(h - 1) / sigma_s) + 5;
-    const long sd = (long)(unsigned long)(base_delta / sigma_r) + 5;
-    if (sd > sd_max) {
-        if (threadIdx.x == 0) atomicOr(err, 1);
+__global__ void __launch_bounds__(BIL_COLS) k_bil_splat(const float4* __restrict__ cloud_all, int w, int h, long sw,
+                                                       long sh, const int* __restrict__ zmm, int sd_max,
+                                                       float2* __restrict__ grids, long grid_cells,
+                                                       int* __restrict__ err) {
+    __shared__ float cx[BIL_SD_MAX][BIL_COLS], cy[BIL_SD_MAX][BIL_COLS];
+    const int s = blockIdx.y, t = threadIdx.x;
+    float bmin, bmax;
+    long sd;
+    bool over;
+    if (!bil_params(zmm, s, sd_max, bmin, bmax, sd, over)) {
+        if (over && blockIdx.x == 0 && t == 0) atomicOr(err, 1);
         return;
     }
-    const long cells = sw * sh * sd;
-    for (long i = threadIdx.x; i < cells; i += blockDim.x) {
-        A[i] = make_float2(0.f, 0.f);
-        B[i] = make_float2(0.f, 0.f);
-    }
-    __syncthreads();
-    // splat: one thread per (sx, sy) column, points in the oracle's x-major, y-minor order
-    for (long col = threadIdx.x; col < sw * sh; col += blockDim.x) {
-        const int sx = (int)(col % sw), sy = (int)(col / sw);
-        const int x0 = max(0, 10 * (sx - 2) - 6), x1 = min(w - 1, 10 * (sx - 2) + 6);
-        const int y0 = max(0, 10 * (sy - 2) - 6), y1 = min(h - 1, 10 * (sy - 2) + 6);
-        for (int x = x0; x <= x1; ++x) {
-            if ((long)(unsigned long)((float)x / sigma_s + 0.5f) + 2 != sx) continue;
-            for (int y = y0; y <= y1; ++y) {
-                if ((long)(unsigned long)((float)y / sigma_s + 0.5f) + 2 != sy) continue;
-                const float Z = cloud[(long)y * w + x].z;
-                const float z = Z - base_min;
-                const long sz = (long)(unsigned long)(z / sigma_r + 0.5f) + 2;
-                float2& d = A[(sx + sw * sy) * sd + sz];
-                d.x += Z;
-                d.y += 1.0f;
-            }
+    const float sigma_s = 10.0f, sigma_r = 0.05f;
+    const long ncol = sw * sh;
+    const long col = (long)blockIdx.x * BIL_COLS + t;
+    if (col >= ncol) return;
+    for (long z = 0; z < sd; ++z) { cx[z][t] = 0.f; cy[z][t] = 0.f; }
+    const float4* cloud = cloud_all + (long)s * w * h;
+    const int sx = (int)(col % sw), sy = (int)(col / sw);
+    const int x0 = max(0, 10 * (sx - 2) - 6), x1 = min(w - 1, 10 * (sx - 2) + 6);
+    const int y0 = max(0, 10 * (sy - 2) - 6), y1 = min(h - 1, 10 * (sy - 2) + 6);
+    for (int x = x0; x <= x1; ++x) {
+        if ((long)(unsigned long)((float)x / sigma_s + 0.5f) + 2 != sx) continue;
+        for (int y = y0; y <= y1; ++y) {
+            if ((long)(unsigned long)((float)y / sigma_s + 0.5f) + 2 != sy) continue;
+            float Z = cloud[(long)y * w + x].z;
+            if (!isfin(Z)) Z = bmax;                           // NaN depths take the range maximum
+            const float z = Z - bmin;
+            const long sz = (long)(unsigned long)(z / sigma_r + 0.5f) + 2;
+            cx[sz][t] += Z;
+            cy[sz][t] += 1.0f;
         }
     }
-    __syncthreads();
-    // 3 axes x 2 iterations of [1 2 1]/4 over the interior; boundaries stay zero
-    const long off[3] = {sd, sw * sd, 1};
-    float2* src = A;
-    float2* dst = B;
-    const long inner = (sw - 2) * (sh - 2) * (sd - 2);
-    for (int pass = 0; pass < 6; ++pass) {
-        const long o = off[pass >> 1];
-        for (long t = threadIdx.x; t < inner; t += blockDim.x) {
-            const long z = t % (sd - 2) + 1;
-            const long rest = t / (sd - 2);
-            const long y = rest % (sh - 2) + 1;
-            const long x = rest / (sh - 2) + 1;
-            const long p = (x + sw * y) * sd + z;
-            const float2 a = src[p - o], b = src[p + o], c = src[p];
-            dst[p] = make_float2((a.x + b.x + 2.0f * c.x) / 4.0f, (a.y + b.y + 2.0f * c.y) / 4.0f);
-        }
-        __syncthreads();
-        float2* t = src; src = dst; dst = t;
+    float2* A = grids + (long)s * 2 * grid_cells;
+    for (long z = 0; z < sd; ++z) A[z * ncol + col] = make_float2(cx[z][t], cy[z][t]);
+}
+
+template <int AX>
+__global__ void k_bil_blur(float2* __restrict__ grids, long grid_cells, int src_slot, long sw, long sh,
+                           const int* __restrict__ zmm, int sd_max) {
+    const int s = blockIdx.y;
+    float bmin, bmax;
+    long sd;
+    bool over;
+    if (!bil_params(zmm, s, sd_max, bmin, bmax, sd, over)) return;
+    const long ncol = sw * sh, cells = sd * ncol;
+    const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= cells) return;
+    const float2* src = grids + (long)s * 2 * grid_cells + (long)src_slot * grid_cells;
+    float2* dst = grids + (long)s * 2 * grid_cells + (long)(1 - src_slot) * grid_cells;
+    const long z = c / ncol, col = c - z * ncol, y = col / sw, x = col - y * sw;
+    const long o = AX == 0 ? 1 : (AX == 1 ? sw : ncol);
+    const long a0 = AX == 0 ? x : (AX == 1 ? y : z);           // coordinate along the axis
+    const long an = AX == 0 ? sw : (AX == 1 ? sh : sd);
+    const bool other_bnd = AX == 0 ? (y <= 0 || y >= sh - 1 || z <= 0 || z >= sd - 1)
+                                   : AX == 1 ? (x <= 0 || x >= sw - 1 || z <= 0 || z >= sd - 1)
+                                             : (x <= 0 || x >= sw - 1 || y <= 0 || y >= sh - 1);
+    if (other_bnd || a0 <= 0 || a0 >= an - 1) { dst[c] = make_float2(0.f, 0.f); return; }
+    // first iteration at axis offsets -1, 0, +1 (zero on the boundary)
+    float2 b1[3];
+#pragma unroll
+    for (int k = -1; k <= 1; ++k) {
+        const long ak = a0 + k;
+        if (ak <= 0 || ak >= an - 1) { b1[k + 1] = make_float2(0.f, 0.f); continue; }
+        const long q = c + k * o;
+        const float2 a = src[q - o], b = src[q + o], m = src[q];
+        b1[k + 1] = make_float2((a.x + b.x + 2.0f * m.x) / 4.0f, (a.y + b.y + 2.0f * m.y) / 4.0f);
     }
-    // slice (trilinear) and z <- D0 / D1; src holds the result after 6 passes
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        const int y = i / w, x = i - (i / w) * w;
-        const float Z = cloud[i].z;
-        const float z = Z - base_min;
+    dst[c] = make_float2((b1[0].x + b1[2].x + 2.0f * b1[1].x) / 4.0f, (b1[0].y + b1[2].y + 2.0f * b1[1].y) / 4.0f);
+}
+
+__global__ void k_bil_slice(float4* __restrict__ cloud_all, int w, int h, long sw, long sh,
+                            const int* __restrict__ zmm, int sd_max, const float2* __restrict__ grids, long grid_cells,
+                            int slot) {
+    const long N = (long)w * h, total = 8 * N;
+    const float sigma_s = 10.0f, sigma_r = 0.05f;
+    const long ncol = sw * sh;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int s = (int)(i / N);
+        float bmin, bmax;
+        long sd;
+        bool over;
+        if (!bil_params(zmm, s, sd_max, bmin, bmax, sd, over)) continue;
+        const float2* G = grids + (long)s * 2 * grid_cells + (long)slot * grid_cells;
+        const int j = (int)(i - (long)s * N);
+        const int y = j / w, x = j - (j / w) * w;
+        float Z = cloud_all[i].z;
+        if (!isfin(Z)) Z = bmax;
+        const float z = Z - bmin;
         const float fx = (float)x / sigma_s + 2.0f, fy = (float)y / sigma_s + 2.0f, fz = z / sigma_r + 2.0f;
         long xi = (long)(unsigned long)fx, yi = (long)(unsigned long)fy, zi = (long)(unsigned long)fz;
         xi = xi < 0 ? 0 : (xi > sw - 1 ? sw - 1 : xi);
@@ -180,7 +260,7 @@ __global__ void __launch_bounds__(BIL_TPB) k_bilateral(float4* __restrict__ clou
         const long yyi = yi + 1 > sh - 1 ? sh - 1 : yi + 1;
         const long zzi = zi + 1 > sd - 1 ? sd - 1 : zi + 1;
         const float xa = fx - (float)xi, ya = fy - (float)yi, za = fz - (float)zi;
-        auto V = [&](long a, long b, long c) { return src[(a + sw * b) * sd + c]; };
+        auto V = [&](long a, long b, long c) { return G[c * ncol + a + sw * b]; };
         const float2 v000 = V(xi, yi, zi), v100 = V(xxi, yi, zi), v010 = V(xi, yyi, zi), v110 = V(xxi, yyi, zi);
         const float2 v001 = V(xi, yi, zzi), v101 = V(xxi, yi, zzi), v011 = V(xi, yyi, zzi), v111 = V(xxi, yyi, zzi);
         const float w000 = (1.0f - xa) * (1.0f - ya) * (1.0f - za), w100 = xa * (1.0f - ya) * (1.0f - za);
@@ -191,7 +271,7 @@ __global__ void __launch_bounds__(BIL_TPB) k_bilateral(float4* __restrict__ clou
                          w101 * v101.x + w011 * v011.x + w111 * v111.x;
         const float D1 = w000 * v000.y + w100 * v100.y + w010 * v010.y + w110 * v110.y + w001 * v001.y +
                          w101 * v101.y + w011 * v011.y + w111 * v111.y;
-        cloud[i].z = D0 / D1;
+        cloud_all[i].z = D0 / D1;
     }
 }
 
@@ -361,13 +441,32 @@ int launch_cloud_normals(r360_frame* f) {
     const float inv_f = 1.f / focal_length;
     const float ox = f->cols / 2 - 0.5, oy = f->rows / 2 - 0.5;
     int slot = timing_begin(f->ctx, "k_cloud");
+    R360_HIP(hipMemsetAsync(P.zmm, 0x7f, sizeof(int) * 8, st));
+    R360_HIP(hipMemsetAsync(P.zmm + 8, 0x80, sizeof(int) * 8, st));
     hipLaunchKernelGGL(k_cloud, dim3(blocks), dim3(256), 0, st, f->d_depth_m, f->d_bgr, f->rows, f->cols, inv_f, ox, oy,
-                       P.cloud, P.rgb);
+                       P.cloud, P.rgb, P.zmm, reinterpret_cast<int*>(P.dist0));
+    hipLaunchKernelGGL(k_zrange, dim3(8), dim3(1024), 0, st, reinterpret_cast<const int*>(P.dist0), (long)w * h, P.zmm);
     timing_end(f->ctx, slot);
     R360_HIP(hipGetLastError());
     slot = timing_begin(f->ctx, "k_bilateral");
-    hipLaunchKernelGGL(k_bilateral, dim3(8), dim3(BIL_TPB), 0, st, P.cloud, w, h, P.grids, P.grid_cells, P.sd_max,
-                       P.err);
+    {
+        // grid extent (FastBilateralFilter): sw, sh from the image size; sd per sensor on the device
+        const long sw = (long)(unsigned long)((float)(w - 1) / 10.0f) + 5;
+        const long sh = (long)(unsigned long)((float)(h - 1) / 10.0f) + 5;
+        if (P.sd_max != BIL_SD_MAX || sw * sh * P.sd_max > P.grid_cells) {
+            r360_set_error("bilateral grid configuration mismatch");
+            return -1;
+        }
+        const long ncol = sw * sh;
+        hipLaunchKernelGGL(k_bil_splat, dim3((ncol + BIL_COLS - 1) / BIL_COLS, 8), dim3(BIL_COLS), 0, st, P.cloud, w, h,
+                           sw, sh, P.zmm, P.sd_max, P.grids, P.grid_cells, P.err);
+        const dim3 gb((unsigned)((ncol * P.sd_max + 255) / 256), 8);
+        hipLaunchKernelGGL(k_bil_blur<0>, gb, dim3(256), 0, st, P.grids, P.grid_cells, 0, sw, sh, P.zmm, P.sd_max);
+        hipLaunchKernelGGL(k_bil_blur<1>, gb, dim3(256), 0, st, P.grids, P.grid_cells, 1, sw, sh, P.zmm, P.sd_max);
+        hipLaunchKernelGGL(k_bil_blur<2>, gb, dim3(256), 0, st, P.grids, P.grid_cells, 0, sw, sh, P.zmm, P.sd_max);
+        hipLaunchKernelGGL(k_bil_slice, dim3(blocks), dim3(256), 0, st, P.cloud, w, h, sw, sh, P.zmm, P.sd_max, P.grids,
+                           P.grid_cells, 1);
+    }
     timing_end(f->ctx, slot);
     R360_HIP(hipGetLastError());
     slot = timing_begin(f->ctx, "k_dcm");

@@ -142,21 +142,31 @@ __global__ void k_ccl_label(const int* __restrict__ root, const int* __restrict_
     }
 }
 
-// labels with more than min_inliers points, in increasing label order (one workgroup per sensor)
+// labels with more than min_inliers points, in increasing label order (one workgroup per sensor);
+// also the label -> large-label index map and each large label's offset in the grouped pixel list
 __global__ void __launch_bounds__(1024) k_big_list(const int* __restrict__ cnt, const int* __restrict__ nlab, int N,
                                                    int min_inliers, int* __restrict__ big, int* __restrict__ nbig,
-                                                   int maxbig, int* __restrict__ err) {
+                                                   int maxbig, int* __restrict__ err, int* __restrict__ bmap,
+                                                   int* __restrict__ boff) {
     __shared__ int sh[17];
     const int s = blockIdx.x;
     const int n = nlab[s];
-    int acc = 0;
+    int acc = 0, cacc = 0;
     for (int j0 = 0; j0 < n; j0 += blockDim.x) {
         const int j = j0 + threadIdx.x;
-        const int f = (j < n && cnt[(long)s * N + j] > min_inliers) ? 1 : 0;
-        int tot;
+        const int c = j < n ? cnt[(long)s * N + j] : 0;
+        const int f = c > min_inliers ? 1 : 0;
+        int tot, ctot;
         const int ex = block_exscan(f, sh, tot);
-        if (f && acc + ex < maxbig) big[s * maxbig + acc + ex] = j;
+        const int cex = block_exscan(f ? c : 0, sh, ctot);
+        const int b = acc + ex;
+        if (j < n) bmap[(long)s * N + j] = (f && b < maxbig) ? b : -1;
+        if (f && b < maxbig) {
+            big[s * maxbig + b] = j;
+            boff[s * maxbig + b] = cacc + cex;
+        }
         acc += tot;
+        cacc += ctot;
         __syncthreads();
     }
     if (threadIdx.x == 0) {
@@ -165,67 +175,167 @@ __global__ void __launch_bounds__(1024) k_big_list(const int* __restrict__ cnt, 
     }
 }
 
-// ------------------------------------------------------------------ moments
-constexpr int MOM_TPB = 256;
-
-struct alignas(16) MomShared {
-    r360p::i128 s2[MOM_TPB];
-    long long v[MOM_TPB];
-};
-
-// block reduction of a Moments struct, field by field (exact integer sums: order-free)
-__device__ void block_reduce_moments(r360p::Moments& m, MomShared* sh) {
-    auto red64 = [&](long long& x) {
-        sh->v[threadIdx.x] = x;
-        __syncthreads();
-        for (int o = MOM_TPB / 2; o > 0; o >>= 1) {
-            if ((int)threadIdx.x < o) sh->v[threadIdx.x] += sh->v[threadIdx.x + o];
-            __syncthreads();
-        }
-        x = sh->v[0];
-        __syncthreads();
-    };
-    auto red128 = [&](r360p::i128& x) {
-        sh->s2[threadIdx.x] = x;
-        __syncthreads();
-        for (int o = MOM_TPB / 2; o > 0; o >>= 1) {
-            if ((int)threadIdx.x < o) sh->s2[threadIdx.x] += sh->s2[threadIdx.x + o];
-            __syncthreads();
-        }
-        x = sh->s2[0];
-        __syncthreads();
-    };
-    red64(m.n);
-    for (int k = 0; k < 3; ++k) red64(m.s1[k]);
-    for (int k = 0; k < 6; ++k) red128(m.s2[k]);
-    for (int k = 0; k < 4; ++k) red64(m.c[k]);
+// Wave-aggregated counter increment: lanes with the same key share one atomic; returns each active
+// lane's slot.  Must be called by every lane of the wave (uniform control flow).
+__device__ __forceinline__ int agg_inc(int* __restrict__ ctr, int key, bool active) {
+    const int lane = threadIdx.x & 63;
+    unsigned long long pending = __ballot(active);
+    int res = 0;
+    while (pending) {
+        const int leader = __ffsll((long long)pending) - 1;
+        const int lkey = __shfl(key, leader, 64);
+        const unsigned long long grp = __ballot(active && key == lkey) & pending;
+        int base = 0;
+        if (lane == leader) base = atomicAdd(ctr + lkey, __popcll(grp));
+        base = __shfl(base, leader, 64);
+        if ((grp >> lane) & 1) res = base + __popcll(grp & ((1ull << lane) - 1));
+        pending &= ~grp;
+    }
+    return res;
 }
 
-__global__ void __launch_bounds__(MOM_TPB) k_label_moments(const float4* __restrict__ cloud, const int* __restrict__ lab,
+// pixels of every large label into its slice of the grouped list (order inside a slice is free: the
+// moments are exact integer sums and the first pixel is a minimum)
+__global__ void k_label_scatter(const int* __restrict__ lab, int N, const int* __restrict__ bmap,
+                                const int* __restrict__ boff, int* __restrict__ bcur, int* __restrict__ blist,
+                                int maxbig) {
+    const long total = 8L * N, stride = (long)gridDim.x * blockDim.x;
+    for (long i0 = blockIdx.x * (long)blockDim.x + (threadIdx.x & ~63); i0 < total; i0 += stride) {
+        const long i = i0 + (threadIdx.x & 63);
+        int key = -1, s = 0, j = 0;
+        if (i < total) {
+            s = (int)(i / N);
+            j = (int)(i - (long)s * N);
+            const int L = lab[i];
+            if (L >= 0) {
+                const int b = bmap[(long)s * N + L];
+                if (b >= 0) key = s * maxbig + b;
+            }
+        }
+        const int pos = agg_inc(bcur, key, key >= 0);
+        if (key >= 0) blist[(long)s * N + boff[key] + pos] = j;
+    }
+}
+
+// ------------------------------------------------------------------ moments
+constexpr int MOM_TPB = 1024;
+constexpr int MOM_NW = MOM_TPB / 64;
+constexpr int MOM_UNROLL = 4;           // independent list entries per thread in flight
+
+struct MomShared {
+    long long w[MOM_NW][20];
+};
+
+__device__ __forceinline__ long long wave_sum64(long long x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+    return x;
+}
+
+__device__ __forceinline__ r360p::i128 wave_sum128(r360p::i128 x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long lo = __shfl_xor((unsigned long long)x, o, 64);
+        const long long hi = __shfl_xor((long long)(x >> 64), o, 64);
+        x += (r360p::i128)(((unsigned __int128)(unsigned long long)hi << 64) | lo);
+    }
+    return x;
+}
+
+// block reduction of a Moments struct (exact integer sums: order-free): wave butterflies, then one
+// LDS stage; the total is valid in thread 0
+__device__ void block_reduce_moments(r360p::Moments& m, MomShared* sh) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    long long w[20];
+    w[0] = wave_sum64(m.n);
+    for (int k = 0; k < 3; ++k) w[1 + k] = wave_sum64(m.s1[k]);
+    for (int k = 0; k < 6; ++k) {
+        const r360p::i128 v = wave_sum128(m.s2[k]);
+        w[4 + 2 * k] = (long long)(unsigned long long)v;
+        w[5 + 2 * k] = (long long)(v >> 64);
+    }
+    for (int k = 0; k < 4; ++k) w[16 + k] = wave_sum64(m.c[k]);
+    if (lane == 0)
+        for (int k = 0; k < 20; ++k) sh->w[wid][k] = w[k];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        r360p::moments_zero(m);
+        for (int q = 0; q < (int)(blockDim.x >> 6); ++q) {
+            m.n += sh->w[q][0];
+            for (int k = 0; k < 3; ++k) m.s1[k] += sh->w[q][1 + k];
+            for (int k = 0; k < 6; ++k)
+                m.s2[k] += (r360p::i128)(((unsigned __int128)(unsigned long long)sh->w[q][5 + 2 * k] << 64) |
+                                         (unsigned long long)sh->w[q][4 + 2 * k]);
+            for (int k = 0; k < 4; ++k) m.c[k] += sh->w[q][16 + k];
+        }
+    }
+}
+
+__device__ __forceinline__ int block_min(int v, int* sh) {
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        for (int q = 1; q < (int)(blockDim.x >> 6); ++q) v = min(v, sh[q]);
+    return v;
+}
+
+__device__ __forceinline__ float block_fminmax(float v, bool mx, float* sh) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const float u = __shfl_xor(v, o, 64);
+        v = mx ? fmaxf(v, u) : fminf(v, u);
+    }
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        for (int q = 1; q < (int)(blockDim.x >> 6); ++q) v = mx ? fmaxf(v, sh[q]) : fminf(v, sh[q]);
+    return v;
+}
+
+__global__ void __launch_bounds__(MOM_TPB) k_label_moments(const float4* __restrict__ cloud, const int* __restrict__ cnt,
                                                           int N, const int* __restrict__ big,
                                                           const int* __restrict__ nbig, int maxbig,
-                                                          r360p::Moments* __restrict__ mom) {
+                                                          const int* __restrict__ boff, const int* __restrict__ blist,
+                                                          r360p::Moments* __restrict__ mom, int* __restrict__ bfirst) {
     __shared__ MomShared sh;
+    __shared__ int smin[MOM_NW];
     const int s = blockIdx.y, b = blockIdx.x;
     if (b >= nbig[s]) return;
     const int L = big[s * maxbig + b];
     const long base = (long)s * N;
+    const int n = cnt[base + L];
+    const int* li = blist + base + boff[s * maxbig + b];
     r360p::Moments m;
     r360p::moments_zero(m);
-    for (int j = threadIdx.x; j < N; j += MOM_TPB)
-        if (lab[base + j] == L) {
-            const float4 p = cloud[base + j];
-            if (isfin(p.x) && isfin(p.y) && isfin(p.z)) r360p::moments_add_xyz(m, p.x, p.y, p.z);
-        }
+    int first = N;
+    for (int k0 = threadIdx.x; k0 < n; k0 += MOM_UNROLL * MOM_TPB) {
+        int j[MOM_UNROLL];
+        float4 p[MOM_UNROLL];
+#pragma unroll
+        for (int u = 0; u < MOM_UNROLL; ++u) j[u] = k0 + u * MOM_TPB < n ? li[k0 + u * MOM_TPB] : -1;
+#pragma unroll
+        for (int u = 0; u < MOM_UNROLL; ++u) p[u] = j[u] >= 0 ? cloud[base + j[u]] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int u = 0; u < MOM_UNROLL; ++u)
+            if (j[u] >= 0) {
+                first = min(first, j[u]);
+                if (isfin(p[u].x) && isfin(p[u].y) && isfin(p[u].z)) r360p::moments_add_xyz(m, p[u].x, p[u].y, p[u].z);
+            }
+    }
+    first = block_min(first, smin);
     block_reduce_moments(m, &sh);
-    if (threadIdx.x == 0) mom[s * maxbig + b] = m;
+    if (threadIdx.x == 0) {
+        mom[s * maxbig + b] = m;
+        bfirst[s * maxbig + b] = first;
+    }
 }
 
 // OrganizedMultiPlaneSegmentation::segment plane fit, one thread per sensor over its large labels in
 // label order (the viewpoint vp accumulates across labels, as in PCL 1.7)
 __global__ void k_plane_fit(const r360p::Moments* __restrict__ mom, const int* __restrict__ big,
                             const int* __restrict__ nbig, int maxbig, float max_curvature, PlaneModel* __restrict__ models,
-                            int* __restrict__ nmodels, int* __restrict__ err) {
+                            int* __restrict__ nmodels, int* __restrict__ err, int N, int* __restrict__ mmap) {
     const int s = threadIdx.x;
     if (s >= 8) return;
     float vp[4] = {0, 0, 0, 0};
@@ -253,6 +363,8 @@ __global__ void k_plane_fit(const r360p::Moments* __restrict__ mom, const int* _
             if (nm >= R360_MAX_MODELS) { atomicOr(err, 4); break; }
             PlaneModel& M = models[s * R360_MAX_MODELS + nm];
             M.label = big[s * maxbig + b];
+            M.big = b;
+            mmap[(long)s * N + M.label] = nm;
             M.n_fit = (int)m.n;
             for (int k = 0; k < 4; ++k) M.v[k] = pp[k];
             for (int k = 0; k < 3; ++k) M.centroid[k] = centroid[k];
@@ -451,57 +563,113 @@ __global__ void k_refine_final(const int8_t* __restrict__ state, const int* __re
 }
 
 // ------------------------------------------------------------------ per-model statistics
+// refined regions grouped by model: counts, then scatter (order inside a slice is free, as above)
+__global__ void k_model_count(const int* __restrict__ labf, int N, const int* __restrict__ mmap, int* __restrict__ mcnt) {
+    const long total = 8L * N, stride = (long)gridDim.x * blockDim.x;
+    for (long i0 = blockIdx.x * (long)blockDim.x + (threadIdx.x & ~63); i0 < total; i0 += stride) {
+        const long i = i0 + (threadIdx.x & 63);
+        int key = -1;
+        if (i < total) {
+            const int s = (int)(i / N);
+            const int L = labf[i];
+            if (L >= 0) {
+                const int m = mmap[(long)s * N + L];
+                if (m >= 0) key = s * R360_MAX_MODELS + m;
+            }
+        }
+        agg_inc(mcnt, key, key >= 0);
+    }
+}
+
+__device__ __forceinline__ int model_offset(const int* __restrict__ mcnt, int s, int m) {
+    int o = 0;
+    for (int k = 0; k < m; ++k) o += mcnt[s * R360_MAX_MODELS + k];
+    return o;
+}
+
+__global__ void k_model_scatter(const int* __restrict__ labf, int N, const int* __restrict__ mmap,
+                                const int* __restrict__ mcnt, int* __restrict__ mcur, int* __restrict__ mlist) {
+    __shared__ int moff[8 * R360_MAX_MODELS];
+    for (int q = threadIdx.x; q < 8 * R360_MAX_MODELS; q += blockDim.x) moff[q] = mcnt[q];
+    __syncthreads();
+    if (threadIdx.x < 8) {   // exclusive prefix per sensor
+        int acc = 0;
+        for (int m = 0; m < R360_MAX_MODELS; ++m) {
+            const int c = moff[threadIdx.x * R360_MAX_MODELS + m];
+            moff[threadIdx.x * R360_MAX_MODELS + m] = acc;
+            acc += c;
+        }
+    }
+    __syncthreads();
+    const long total = 8L * N, stride = (long)gridDim.x * blockDim.x;
+    for (long i0 = blockIdx.x * (long)blockDim.x + (threadIdx.x & ~63); i0 < total; i0 += stride) {
+        const long i = i0 + (threadIdx.x & 63);
+        int key = -1, s = 0, j = 0;
+        if (i < total) {
+            s = (int)(i / N);
+            j = (int)(i - (long)s * N);
+            const int L = labf[i];
+            if (L >= 0) {
+                const int m = mmap[(long)s * N + L];
+                if (m >= 0) key = s * R360_MAX_MODELS + m;
+            }
+        }
+        const int pos = agg_inc(mcur, key, key >= 0);
+        if (key >= 0) mlist[(long)s * N + moff[key] + pos] = j;
+    }
+}
+
 __global__ void __launch_bounds__(MOM_TPB) k_model_stats(const float4* __restrict__ cloud, const uchar4* __restrict__ rgb,
-                                                        const int* __restrict__ lab, const int* __restrict__ labf,
                                                         int N, const PlaneModel* __restrict__ models,
                                                         const int* __restrict__ nmodels, const float* __restrict__ rt8,
+                                                        const int* __restrict__ mcnt, const int* __restrict__ mlist,
+                                                        const int* __restrict__ bfirst, int maxbig,
                                                         PlaneOut* __restrict__ out) {
     __shared__ MomShared sh;
-    __shared__ float sbox[6][MOM_TPB];
-    __shared__ int smin[MOM_TPB];
+    __shared__ float sred[MOM_NW];
     const int s = blockIdx.y, m = blockIdx.x;
     if (m >= nmodels[s]) return;
     const PlaneModel& M = models[s * R360_MAX_MODELS + m];
-    const int L = M.label;
     const float* T = rt8 + 16 * s;
     const long base = (long)s * N;
+    const int n = mcnt[s * R360_MAX_MODELS + m];
+    const int* li = mlist + base + model_offset(mcnt, s, m);
     r360p::Moments mo;
     r360p::moments_zero(mo);
-    int first = N;
     float bx[6] = {3.4e38f, 3.4e38f, 3.4e38f, -3.4e38f, -3.4e38f, -3.4e38f};   // local-frame bounds
-    for (int j = threadIdx.x; j < N; j += MOM_TPB) {
-        if (lab[base + j] == L && j < first) first = j;
-        if (labf[base + j] == L) {
-            const float4 p = cloud[base + j];
-            bx[0] = fminf(bx[0], p.x); bx[1] = fminf(bx[1], p.y); bx[2] = fminf(bx[2], p.z);
-            bx[3] = fmaxf(bx[3], p.x); bx[4] = fmaxf(bx[4], p.y); bx[5] = fmaxf(bx[5], p.z);
+    for (int k0 = threadIdx.x; k0 < n; k0 += MOM_UNROLL * MOM_TPB) {
+        int j[MOM_UNROLL];
+        float4 p[MOM_UNROLL];
+        uchar4 c[MOM_UNROLL];
+#pragma unroll
+        for (int u = 0; u < MOM_UNROLL; ++u) j[u] = k0 + u * MOM_TPB < n ? li[k0 + u * MOM_TPB] : -1;
+#pragma unroll
+        for (int u = 0; u < MOM_UNROLL; ++u) {
+            p[u] = j[u] >= 0 ? cloud[base + j[u]] : make_float4(0.f, 0.f, 0.f, 0.f);
+            c[u] = j[u] >= 0 ? rgb[base + j[u]] : make_uchar4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < MOM_UNROLL; ++u) {
+            if (j[u] < 0) continue;
+            const float4 q = p[u];
+            bx[0] = fminf(bx[0], q.x); bx[1] = fminf(bx[1], q.y); bx[2] = fminf(bx[2], q.z);
+            bx[3] = fmaxf(bx[3], q.x); bx[4] = fmaxf(bx[4], q.y); bx[5] = fmaxf(bx[5], q.z);
             // Eigen Affine3f * Vector3f (pcl::transformPointCloud), column-major T
-            const float x = T[0] * p.x + T[4] * p.y + T[8] * p.z + T[12];
-            const float y = T[1] * p.x + T[5] * p.y + T[9] * p.z + T[13];
-            const float z = T[2] * p.x + T[6] * p.y + T[10] * p.z + T[14];
+            const float x = T[0] * q.x + T[4] * q.y + T[8] * q.z + T[12];
+            const float y = T[1] * q.x + T[5] * q.y + T[9] * q.z + T[13];
+            const float z = T[2] * q.x + T[6] * q.y + T[10] * q.z + T[14];
             r360p::moments_add_xyz(mo, x, y, z);
-            const uchar4 c = rgb[base + j];
-            r360p::moments_add_rgb(mo, c.x, c.y, c.z);
+            r360p::moments_add_rgb(mo, c[u].x, c[u].y, c[u].z);
         }
     }
-    smin[threadIdx.x] = first;
-    for (int k = 0; k < 6; ++k) sbox[k][threadIdx.x] = bx[k];
-    __syncthreads();
-    for (int o = MOM_TPB / 2; o > 0; o >>= 1) {
-        if ((int)threadIdx.x < o) {
-            smin[threadIdx.x] = min(smin[threadIdx.x], smin[threadIdx.x + o]);
-            for (int k = 0; k < 3; ++k) sbox[k][threadIdx.x] = fminf(sbox[k][threadIdx.x], sbox[k][threadIdx.x + o]);
-            for (int k = 3; k < 6; ++k) sbox[k][threadIdx.x] = fmaxf(sbox[k][threadIdx.x], sbox[k][threadIdx.x + o]);
-        }
-        __syncthreads();
-    }
+    for (int k = 0; k < 6; ++k) bx[k] = block_fminmax(bx[k], k >= 3, sred);
     block_reduce_moments(mo, &sh);
     if (threadIdx.x == 0) {
         PlaneOut& O = out[s * R360_MAX_MODELS + m];
         O.model = M;
         O.stats = mo;
-        O.start = smin[0];
-        for (int k = 0; k < 3; ++k) { O.bmin[k] = sbox[k][0]; O.bmax[k] = sbox[k + 3][0]; }
+        O.start = bfirst[s * maxbig + M.big];
+        for (int k = 0; k < 3; ++k) { O.bmin[k] = bx[k]; O.bmax[k] = bx[k + 3]; }
         O.n_contour = 0;
         O.contour_off = 0;
         O.n_vox = 0;
@@ -794,11 +962,25 @@ int launch_segmentation(r360_frame* f) {
     timing_end(ctx, slot);
     R360_HIP(hipGetLastError());
     slot = timing_begin(ctx, "k_plane_fit");
-    hipLaunchKernelGGL(k_big_list, dim3(8), dim3(1024), 0, st, P.cnt, P.nlab, N, 80, P.big, P.nbig, R360_MAX_BIG, P.err);
-    hipLaunchKernelGGL(k_label_moments, dim3(R360_MAX_BIG, 8), dim3(MOM_TPB), 0, st, P.cloud, P.lab, N, P.big, P.nbig,
-                       R360_MAX_BIG, P.mom);
+    // aux: boff, bcur, bfirst [8][MAX_BIG]; mcnt, mcur [8][MAX_MODELS].  parent / root are free after
+    // the labelling and hold the label -> large-label and label -> model maps.
+    int* boff = P.aux;
+    int* bcur = boff + 8 * R360_MAX_BIG;
+    int* bfirst = bcur + 8 * R360_MAX_BIG;
+    int* mcnt = bfirst + 8 * R360_MAX_BIG;
+    int* mcur = mcnt + 8 * R360_MAX_MODELS;
+    int* bmap = P.parent;
+    int* mmap = P.root;
+    hipLaunchKernelGGL(k_big_list, dim3(8), dim3(1024), 0, st, P.cnt, P.nlab, N, 80, P.big, P.nbig, R360_MAX_BIG, P.err,
+                       bmap, boff);
+    R360_HIP(hipMemsetAsync(bcur, 0, sizeof(int) * 8 * R360_MAX_BIG, st));
+    hipLaunchKernelGGL(k_label_scatter, dim3(blocks), dim3(256), 0, st, P.lab, N, bmap, boff, bcur, P.blist,
+                       R360_MAX_BIG);
+    hipLaunchKernelGGL(k_label_moments, dim3(R360_MAX_BIG, 8), dim3(MOM_TPB), 0, st, P.cloud, P.cnt, N, P.big, P.nbig,
+                       R360_MAX_BIG, boff, P.blist, P.mom, bfirst);
+    R360_HIP(hipMemsetAsync(mmap, 0xff, sizeof(int) * total, st));
     hipLaunchKernelGGL(k_plane_fit, dim3(1), dim3(64), 0, st, P.mom, P.big, P.nbig, R360_MAX_BIG, 0.001f, P.models,
-                       P.nmodels, P.err);
+                       P.nmodels, P.err, N, mmap);
     timing_end(ctx, slot);
     R360_HIP(hipGetLastError());
     slot = timing_begin(ctx, "k_refine");
@@ -817,8 +999,11 @@ int launch_segmentation(r360_frame* f) {
     timing_end(ctx, slot);
     R360_HIP(hipGetLastError());
     slot = timing_begin(ctx, "k_model_stats");
-    hipLaunchKernelGGL(k_model_stats, dim3(R360_MAX_MODELS, 8), dim3(MOM_TPB), 0, st, P.cloud, P.rgb, P.lab, P.labf, N,
-                       P.models, P.nmodels, f->calib->d_rt, P.out);
+    R360_HIP(hipMemsetAsync(mcnt, 0, sizeof(int) * 16 * R360_MAX_MODELS, st));
+    hipLaunchKernelGGL(k_model_count, dim3(blocks), dim3(256), 0, st, P.labf, N, mmap, mcnt);
+    hipLaunchKernelGGL(k_model_scatter, dim3(blocks), dim3(256), 0, st, P.labf, N, mmap, mcnt, mcur, P.mlist);
+    hipLaunchKernelGGL(k_model_stats, dim3(R360_MAX_MODELS, 8), dim3(MOM_TPB), 0, st, P.cloud, P.rgb, N, P.models,
+                       P.nmodels, f->calib->d_rt, mcnt, P.mlist, bfirst, R360_MAX_BIG, P.out);
     // the refinement's closeness masks are dead here: their storage holds the neighbour masks
     uint8_t* nbm = reinterpret_cast<uint8_t*>(P.mask);
     hipLaunchKernelGGL(k_nbmask, dim3(blocks), dim3(256), 0, st, P.labf, w, h, nbm);

@@ -78,6 +78,7 @@ enum { R360_SUM_NVALID = 27, R360_SUM_NVIS = 28, R360_SUM_ERR2 = 31, R360_NSUMS 
 // One planar model of segment() (PlanarRegion statistics + ModelCoefficients)
 struct PlaneModel {
     int label, n_fit;
+    int big;                 // index of the label in the sensor's large-label list
     float v[4];
     float centroid[3];
     float cov[9];
@@ -116,11 +117,15 @@ struct PlaneBufs {
     float2* grids = nullptr;    // bilateral grids, 8 x 2 x grid_cells
     long grid_cells = 0;
     int sd_max = 0;
+    int* zmm = nullptr;         // per-sensor depth range for the bilateral grid: [8] min, [8] max (ordered ints)
     int* parent = nullptr;      // union-find parents, then root ranks
     int* root = nullptr;
     int* lab = nullptr;         // CCL labels (per-sensor ids, -1 none)
     int* labf = nullptr;        // labels after refinement
     int* cnt = nullptr;         // label sizes [8][N]
+    int* blist = nullptr;       // pixels of each large label, grouped by label [8][N]
+    int* mlist = nullptr;       // pixels of each refined model region, grouped by model [8][N]
+    int* aux = nullptr;         // per-sensor list offsets / cursors / first pixels (plane_seg.hip)
     int* nlab = nullptr;        // [8]
     int* big = nullptr;         // [8][R360_MAX_BIG]
     int* nbig = nullptr;        // [8]
