@@ -362,7 +362,7 @@ int plane_bufs_alloc(r360_frame* f) {
     R360_HIP(hipHostMalloc(&P.contour, sizeof(float4) * P.contour_cap));
     R360_HIP(hipHostMalloc(&P.vox, sizeof(VoxOut) * P.vox_cap));
     R360_HIP(hipEventCreateWithFlags(&P.done, hipEventDisableTiming | hipEventBlockingSync));
-    R360_HIP(hipMalloc(&P.totals, sizeof(long) * 2));
+    R360_HIP(hipMalloc(&P.totals, sizeof(long) * 4));
     R360_HIP(hipMalloc(&P.err, sizeof(int)));
     R360_HIP(hipHostMalloc(&P.h_out, sizeof(PlaneOut) * 8 * R360_MAX_MODELS));
     R360_HIP(hipHostMalloc(&P.h_nmodels, sizeof(int) * 16));

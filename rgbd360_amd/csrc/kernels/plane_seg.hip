@@ -841,13 +841,33 @@ __global__ void __launch_bounds__(TR_TPB) k_trace(const uint8_t* __restrict__ nb
     }
 }
 
-// contour total of the frame (profiling / pool accounting)
-__global__ void k_alloc(const int* __restrict__ nmodels, const PlaneOut* __restrict__ out, long* __restrict__ totals) {
+// contour total of the frame (profiling / pool accounting), and the voxel hash table size for this
+// frame: a power of two >= 2x the inliers of the regions without a contour (their refined region
+// sizes bound the number of distinct voxels), capped by the allocation
+__global__ void k_alloc(const int* __restrict__ nmodels, const PlaneOut* __restrict__ out, const int* __restrict__ mcnt,
+                        unsigned long long cap, long* __restrict__ totals) {
     if (threadIdx.x != 0) return;
-    long co = 0;
+    long co = 0, cand = 0;
     for (int s = 0; s < 8; ++s)
-        for (int m = 0; m < nmodels[s]; ++m) co += out[s * R360_MAX_MODELS + m].n_contour;
+        for (int m = 0; m < nmodels[s]; ++m) {
+            const int nc = out[s * R360_MAX_MODELS + m].n_contour;
+            co += nc;
+            if (nc == 0) cand += mcnt[s * R360_MAX_MODELS + m];
+        }
     totals[0] = co;
+    unsigned long long t = 1024;
+    while (t < 2ull * (unsigned long long)cand && t < cap) t <<= 1;
+    totals[2] = (long)(t - 1);   // hash mask
+}
+
+__global__ void k_vox_clear(VoxCell* __restrict__ tab, const long* __restrict__ totals) {
+    const unsigned long long used = (unsigned long long)totals[2] + 1;
+    for (unsigned long long c = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; c < used;
+         c += (unsigned long long)gridDim.x * blockDim.x) {
+        tab[c].tag = 0;
+        tab[c].s[0] = tab[c].s[1] = tab[c].s[2] = 0.0;
+        tab[c].cnt = 0;
+    }
 }
 
 // pcl::VoxelGrid (leaf 0.05) of the inliers of regions without a contour (Frame360.h:1017-1026):
@@ -857,38 +877,82 @@ __device__ __forceinline__ unsigned long long vhash(unsigned long long tag, unsi
     return (tag * 0x9E3779B97F4A7C15ull >> 20) & mask;
 }
 
-__global__ void k_vox_hash(const float4* __restrict__ cloud, const int8_t* __restrict__ state, int N,
-                           PlaneOut* __restrict__ out, VoxCell* __restrict__ tab, unsigned long long mask,
-                           int* __restrict__ err) {
+// Points are pre-summed per wave over lanes with the same (region, voxel) tag (consecutive pixels of
+// a row mostly share a voxel), so one insertion + four atomics serve a whole group; new voxels are
+// counted per region in LDS and flushed once per workgroup.
+constexpr int VOX_TPB = 256;
+
+__global__ void __launch_bounds__(VOX_TPB) k_vox_hash(const float4* __restrict__ cloud, const int8_t* __restrict__ state,
+                                                     int N, PlaneOut* __restrict__ out, VoxCell* __restrict__ tab,
+                                                     const long* __restrict__ totals, int* __restrict__ err) {
+    __shared__ int nnew[8 * R360_MAX_MODELS];
+    for (int q = threadIdx.x; q < 8 * R360_MAX_MODELS; q += VOX_TPB) nnew[q] = 0;
+    __syncthreads();
     const long total = 8L * N;
+    const unsigned long long mask = (unsigned long long)totals[2];
     const float inv = 1.0f / 0.05f;
-    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-        const int m = state[i];
-        if (m < 0) continue;
-        const int s = (int)(i / N);
-        PlaneOut& O = out[s * R360_MAX_MODELS + m];
-        if (O.n_contour != 0) continue;
-        const float4 p = cloud[i];
-        const long long b0 = (long long)floorf(O.bmin[0] * inv), b1 = (long long)floorf(O.bmin[1] * inv),
-                        b2 = (long long)floorf(O.bmin[2] * inv);
-        const long long d0 = (long long)floorf(O.bmax[0] * inv) - b0 + 1, d1 = (long long)floorf(O.bmax[1] * inv) - b1 + 1;
-        const long long key = ((long long)floorf(p.x * inv) - b0) + ((long long)floorf(p.y * inv) - b1) * d0 +
-                              ((long long)floorf(p.z * inv) - b2) * d0 * d1;
-        const unsigned long long tag = ((unsigned long long)(s * R360_MAX_MODELS + m + 1) << 48) | (unsigned long long)key;
-        unsigned long long hsh = vhash(tag, mask);
-        for (unsigned long long probe = 0;; ++probe) {
-            const unsigned long long prev = atomicCAS(&tab[hsh].tag, 0ull, tag);
-            if (prev == 0ull) { atomicAdd(&O.n_vox, 1); break; }
-            if (prev == tag) break;
-            hsh = (hsh + 1) & mask;
-            if (probe > mask) { atomicOr(err, 16); hsh = ~0ull; break; }
+    const int lane = threadIdx.x & 63;
+    const long stride = (long)gridDim.x * VOX_TPB;
+    for (long i0 = blockIdx.x * (long)VOX_TPB + (threadIdx.x & ~63); i0 < total; i0 += stride) {
+        const long i = i0 + lane;
+        unsigned long long tag = 0;
+        double px = 0, py = 0, pz = 0;
+        int sm = -1;
+        if (i < total) {
+            const int m = state[i];
+            if (m >= 0) {
+                const int s = (int)(i / N);
+                const PlaneOut& O = out[s * R360_MAX_MODELS + m];
+                if (O.n_contour == 0) {
+                    const float4 p = cloud[i];
+                    const long long b0 = (long long)floorf(O.bmin[0] * inv), b1 = (long long)floorf(O.bmin[1] * inv),
+                                    b2 = (long long)floorf(O.bmin[2] * inv);
+                    const long long d0 = (long long)floorf(O.bmax[0] * inv) - b0 + 1,
+                                    d1 = (long long)floorf(O.bmax[1] * inv) - b1 + 1;
+                    const long long key = ((long long)floorf(p.x * inv) - b0) + ((long long)floorf(p.y * inv) - b1) * d0 +
+                                          ((long long)floorf(p.z * inv) - b2) * d0 * d1;
+                    sm = s * R360_MAX_MODELS + m;
+                    tag = ((unsigned long long)(sm + 1) << 48) | (unsigned long long)key;
+                    px = p.x; py = p.y; pz = p.z;
+                }
+            }
         }
-        if (hsh == ~0ull) continue;
-        atomicAdd(&tab[hsh].s[0], (double)p.x);
-        atomicAdd(&tab[hsh].s[1], (double)p.y);
-        atomicAdd(&tab[hsh].s[2], (double)p.z);
-        atomicAdd(&tab[hsh].cnt, 1u);
+        unsigned long long pending = __ballot(tag != 0);
+        while (pending) {
+            const int leader = __ffsll((long long)pending) - 1;
+            const unsigned long long ltag = __shfl(tag, leader, 64);
+            const bool mine = tag == ltag && ((pending >> lane) & 1);
+            const unsigned long long grp = __ballot(mine);
+            // group sums (exact in double: order-free)
+            double gx = mine ? px : 0.0, gy = mine ? py : 0.0, gz = mine ? pz : 0.0;
+            for (int o = 32; o > 0; o >>= 1) {
+                gx += __shfl_xor(gx, o, 64);
+                gy += __shfl_xor(gy, o, 64);
+                gz += __shfl_xor(gz, o, 64);
+            }
+            if (lane == leader) {
+                unsigned long long hsh = vhash(ltag, mask);
+                bool ok = true;
+                for (unsigned long long probe = 0;; ++probe) {
+                    const unsigned long long prev = atomicCAS(&tab[hsh].tag, 0ull, ltag);
+                    if (prev == 0ull) { atomicAdd(&nnew[sm], 1); break; }
+                    if (prev == ltag) break;
+                    hsh = (hsh + 1) & mask;
+                    if (probe > mask) { atomicOr(err, 16); ok = false; break; }
+                }
+                if (ok) {
+                    atomicAdd(&tab[hsh].s[0], gx);
+                    atomicAdd(&tab[hsh].s[1], gy);
+                    atomicAdd(&tab[hsh].s[2], gz);
+                    atomicAdd(&tab[hsh].cnt, (unsigned)__popcll(grp));
+                }
+            }
+            pending &= ~grp;
+        }
     }
+    __syncthreads();
+    for (int q = threadIdx.x; q < 8 * R360_MAX_MODELS; q += VOX_TPB)
+        if (nnew[q]) atomicAdd(&out[q].n_vox, nnew[q]);
 }
 
 __global__ void k_vox_alloc(const int* __restrict__ nmodels, PlaneOut* __restrict__ out, long* __restrict__ totals,
@@ -905,36 +969,41 @@ __global__ void k_vox_alloc(const int* __restrict__ nmodels, PlaneOut* __restric
     if (vo > vox_cap) atomicOr(err, 16);
 }
 
-__global__ void k_vox_compact(const VoxCell* __restrict__ tab, unsigned long long cells, PlaneOut* __restrict__ out,
-                              VoxOut* __restrict__ pool, long pool_cap) {
-    for (unsigned long long c = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; c < cells;
-         c += (unsigned long long)gridDim.x * blockDim.x) {
+// one workgroup per contiguous range of table cells: valid cells are counted per region in LDS, one
+// global atomic per (workgroup, region) reserves the slots, then the cells are written
+constexpr int VOXC_TPB = 1024, VOXC_BLOCKS = 256;
+
+__global__ void __launch_bounds__(VOXC_TPB) k_vox_compact(const VoxCell* __restrict__ tab,
+                                                         const long* __restrict__ totals, PlaneOut* __restrict__ out,
+                                                         VoxOut* __restrict__ pool, long pool_cap) {
+    __shared__ int cnt[8 * R360_MAX_MODELS], base[8 * R360_MAX_MODELS];
+    for (int q = threadIdx.x; q < 8 * R360_MAX_MODELS; q += VOXC_TPB) cnt[q] = 0;
+    __syncthreads();
+    const unsigned long long cells = (unsigned long long)totals[2] + 1;
+    const unsigned long long per = (cells + gridDim.x - 1) / gridDim.x;
+    const unsigned long long c0 = blockIdx.x * per, c1 = c0 + per < cells ? c0 + per : cells;
+    for (unsigned long long c = c0 + threadIdx.x; c < c1; c += VOXC_TPB) {
         const unsigned long long tag = tab[c].tag;
-        const int sm = tag ? (int)(tag >> 48) - 1 : -1;
-        // one atomic per (wave, region): lanes of the same region take consecutive slots
-        int pos = 0;
-        bool pending = sm >= 0;
-        while (__any(pending)) {
-            const int leader = __ffsll((long long)__ballot(pending)) - 1;
-            const int lsm = __shfl(sm, leader, 64);
-            const bool mine = pending && sm == lsm;
-            const unsigned long long same = __ballot(mine);
-            int basepos = 0;
-            if ((int)(threadIdx.x & 63) == leader) basepos = atomicAdd(&out[lsm].vox_fill, __popcll(same));
-            basepos = __shfl(basepos, leader, 64);
-            if (mine) {
-                pos = basepos + __popcll(same & ((1ull << (threadIdx.x & 63)) - 1));
-                pending = false;
-            }
-        }
-        if (sm < 0) continue;
-        PlaneOut& O = out[sm];
-        const double cnt = (double)tab[c].cnt;
+        if (tag) atomicAdd(&cnt[(int)(tag >> 48) - 1], 1);
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < 8 * R360_MAX_MODELS; q += VOXC_TPB) {
+        base[q] = cnt[q] ? atomicAdd(&out[q].vox_fill, cnt[q]) : 0;
+        cnt[q] = 0;
+    }
+    __syncthreads();
+    for (unsigned long long c = c0 + threadIdx.x; c < c1; c += VOXC_TPB) {
+        const unsigned long long tag = tab[c].tag;
+        if (!tag) continue;
+        const int sm = (int)(tag >> 48) - 1;
+        const int pos = base[sm] + atomicAdd(&cnt[sm], 1);
+        const PlaneOut& O = out[sm];
+        const double n = (double)tab[c].cnt;
         VoxOut v;
         v.key = (long long)(tag & ((1ull << 48) - 1));
-        v.x = (float)(tab[c].s[0] / cnt);
-        v.y = (float)(tab[c].s[1] / cnt);
-        v.z = (float)(tab[c].s[2] / cnt);
+        v.x = (float)(tab[c].s[0] / n);
+        v.y = (float)(tab[c].s[1] / n);
+        v.z = (float)(tab[c].s[2] / n);
         v.pad = 0.f;
         if (O.vox_off + pos < pool_cap) pool[O.vox_off + pos] = v;
     }
@@ -1013,17 +1082,19 @@ int launch_segmentation(r360_frame* f) {
     else
         hipLaunchKernelGGL(k_trace<false>, dim3(8), dim3(TR_TPB), 0, st, nbm, P.cloud, w, h, P.nmodels, P.out,
                            P.contour, P.contour_cap, P.err);
-    hipLaunchKernelGGL(k_alloc, dim3(1), dim3(64), 0, st, P.nmodels, P.out, P.totals);
+    if (ctx_vhash_reserve(ctx, 12L * N)) return -1;
+    hipLaunchKernelGGL(k_alloc, dim3(1), dim3(64), 0, st, P.nmodels, P.out, mcnt,
+                       (unsigned long long)ctx->vhash_cap, P.totals);
     timing_end(ctx, slot);
     R360_HIP(hipGetLastError());
     slot = timing_begin(ctx, "k_voxel");
-    if (ctx_vhash_reserve(ctx, 12L * N)) return -1;
-    R360_HIP(hipMemsetAsync(ctx->d_vhash, 0, sizeof(VoxCell) * ctx->vhash_cap, st));
-    hipLaunchKernelGGL(k_vox_hash, dim3(blocks), dim3(256), 0, st, P.cloud, P.state, N, P.out, ctx->d_vhash,
-                       (unsigned long long)(ctx->vhash_cap - 1), P.err);
+    hipLaunchKernelGGL(k_vox_clear, dim3((unsigned)((ctx->vhash_cap + 255) / 256)), dim3(256), 0, st, ctx->d_vhash,
+                       P.totals);
+    hipLaunchKernelGGL(k_vox_hash, dim3(blocks), dim3(VOX_TPB), 0, st, P.cloud, P.state, N, P.out, ctx->d_vhash,
+                       P.totals, P.err);
     hipLaunchKernelGGL(k_vox_alloc, dim3(1), dim3(64), 0, st, P.nmodels, P.out, P.totals, P.vox_cap, P.err);
-    hipLaunchKernelGGL(k_vox_compact, dim3(2048), dim3(256), 0, st, ctx->d_vhash, (unsigned long long)ctx->vhash_cap,
-                       P.out, P.vox, P.vox_cap);
+    hipLaunchKernelGGL(k_vox_compact, dim3(VOXC_BLOCKS), dim3(VOXC_TPB), 0, st, ctx->d_vhash, P.totals, P.out, P.vox,
+                       P.vox_cap);
     timing_end(ctx, slot);
     R360_HIP(hipGetLastError());
     return 0;
