@@ -447,6 +447,9 @@ __device__ void resolve_chain(const int (&L)[K], const unsigned long long (&M)[K
     }
 }
 
+// One wave per sensor walks the rows.  Rows are loaded two ahead into three register sets used in
+// rotation (the loop is unrolled by three), so no loop-carried copy of an in-flight load forces a
+// vmcnt(0) per row, and every load is unconditional (clamped column, value masked afterwards).
 template <int K>
 __global__ void __launch_bounds__(64) k_refine(int8_t* __restrict__ state_all,
                                               const unsigned long long* __restrict__ mask_all, int w, int h) {
@@ -455,30 +458,34 @@ __global__ void __launch_bounds__(64) k_refine(int8_t* __restrict__ state_all,
     const long N = (long)w * h;
     int8_t* S = state_all + s * N;
     const unsigned long long* MK = mask_all + s * N;
+    auto col = [&](int k, int dir) { return dir > 0 ? lane * K + k : (63 - lane) * K + (K - 1 - k); };
     auto load = [&](int r, int (&L)[K], unsigned long long (&M)[K], int dir) {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             // walking order: dir>0 -> column lane*K + k; dir<0 -> column (63-lane)*K + (K-1-k)
-            const int c = dir > 0 ? lane * K + k : (63 - lane) * K + (K - 1 - k);
-            L[k] = c < w ? (int)S[(long)r * w + c] : -1;
-            M[k] = c < w ? MK[(long)r * w + c] : 0ull;
+            const int c = col(k, dir);
+            const int cc = c < w ? c : w - 1;
+            const int v = S[(long)r * w + cc];
+            const unsigned long long m = MK[(long)r * w + cc];
+            L[k] = c < w ? v : -1;
+            M[k] = c < w ? m : 0ull;
         }
     };
     auto store = [&](int r, const int (&L)[K], int dir) {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            const int c = dir > 0 ? lane * K + k : (63 - lane) * K + (K - 1 - k);
+            const int c = col(k, dir);
             if (c < w) S[(long)r * w + c] = (int8_t)L[k];
         }
     };
+    int A[K], B[K], C[K];
+    unsigned long long Am[K], Bm[K], Cm[K];
     // ---------------- first sweep: top->bottom, left->right; right and down checks
     {
-        int cur[K], nxt[K], nn[K], F[K];
-        unsigned long long cm[K], nm[K], nnm[K];
-        load(0, cur, cm, +1);
-        if (h > 1) load(1, nxt, nm, +1);
-        for (int r = 0; r < h - 1; ++r) {
-            if (r + 2 < h) load(r + 2, nn, nnm, +1);     // prefetch: consumed one row later
+        auto step = [&](int r, int (&cur)[K], unsigned long long (&cm)[K], int (&nxt)[K], unsigned long long (&nm)[K],
+                        int (&nn)[K], unsigned long long (&nnm)[K]) {
+            if (r + 2 < h) load(r + 2, nn, nnm, +1);     // consumed two steps later
+            int F[K];
             resolve_chain<K>(cur, cm, F);
             // original state of the column to the right of each of this lane's columns
             const int right_of_last = __shfl(cur[0], (lane + 1) & 63, 64);
@@ -492,24 +499,31 @@ __global__ void __launch_bounds__(64) k_refine(int8_t* __restrict__ state_all,
                 if (F[k] >= 0 && nxt[k] == -2 && ((nm[k] >> F[k]) & 1)) nxt[k] = F[k];
             }
             store(r, F, +1);
-#pragma unroll
-            for (int k = 0; k < K; ++k) { cur[k] = nxt[k]; cm[k] = nm[k]; nxt[k] = nn[k]; nm[k] = nnm[k]; }
+        };
+        load(0, A, Am, +1);
+        if (h > 1) load(1, B, Bm, +1);
+        int r = 0;
+        for (; r + 3 <= h - 1; r += 3) {
+            step(r, A, Am, B, Bm, C, Cm);
+            step(r + 1, B, Bm, C, Cm, A, Am);
+            step(r + 2, C, Cm, A, Am, B, Bm);
         }
-        store(h - 1, cur, +1);
+        const int rem = (h - 1) - r;
+        if (rem == 0) store(h - 1, A, +1);
+        else if (rem == 1) { step(r, A, Am, B, Bm, C, Cm); store(h - 1, B, +1); }
+        else { step(r, A, Am, B, Bm, C, Cm); step(r + 1, B, Bm, C, Cm, A, Am); store(h - 1, C, +1); }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     // ---------------- second sweep: bottom->top, right->left; left and up checks
     {
-        int cur[K], up[K], uu[K], F[K];
-        unsigned long long cm[K], um[K], uum[K];
-        load(h - 1, cur, cm, -1);
-        if (h > 1) load(h - 2, up, um, -1);
         const int cl = w - 1;                                    // owner of column w-1 (walking order)
         const int own_lane = 63 - cl / K, own_k = K - 1 - cl % K;
-        for (int r = h - 1; r >= 1; --r) {
-            if (r - 2 >= 0) load(r - 2, uu, uum, -1);    // prefetch: consumed one row later
+        auto step = [&](int r, int (&cur)[K], unsigned long long (&cm)[K], int (&up)[K], unsigned long long (&um)[K],
+                        int (&uu)[K], unsigned long long (&uum)[K]) {
+            if (r - 2 >= 0) load(r - 2, uu, uum, -1);    // consumed two steps later
+            int F[K];
             resolve_chain<K>(cur, cm, F);
             // original state of the column to the left (walking order: the next element)
             const int left_of_last = __shfl(cur[0], (lane + 1) & 63, 64);
@@ -545,10 +559,18 @@ __global__ void __launch_bounds__(64) k_refine(int8_t* __restrict__ state_all,
                 if (lane == 63 && k == K - 1) up[k] = new_up0;
             }
             store(r, F, -1);
-#pragma unroll
-            for (int k = 0; k < K; ++k) { cur[k] = up[k]; cm[k] = um[k]; up[k] = uu[k]; um[k] = uum[k]; }
+        };
+        load(h - 1, A, Am, -1);
+        if (h > 1) load(h - 2, B, Bm, -1);
+        int r = h - 1;
+        for (; r - 3 >= 0; r -= 3) {
+            step(r, A, Am, B, Bm, C, Cm);
+            step(r - 1, B, Bm, C, Cm, A, Am);
+            step(r - 2, C, Cm, A, Am, B, Bm);
         }
-        store(0, cur, -1);
+        if (r == 0) store(0, A, -1);
+        else if (r == 1) { step(1, A, Am, B, Bm, C, Cm); store(0, B, -1); }
+        else { step(2, A, Am, B, Bm, C, Cm); step(1, B, Bm, C, Cm, A, Am); store(0, C, -1); }
     }
 }
 
