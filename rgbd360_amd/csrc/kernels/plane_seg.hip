@@ -769,6 +769,8 @@ __global__ void __launch_bounds__(TR_TPB) k_trace(const uint8_t* __restrict__ nb
         }
     }
     if (threadIdx.x == 0) { s_nch = 0; s_over = 0; }
+    // a chain can end with an allocated but empty chunk (length a multiple of TR_CHUNK): unowned
+    for (int c = threadIdx.x; c < TR_NCH; c += TR_TPB) cown[c] = -1;
     __syncthreads();
     const uint8_t* nb = LDS ? sm : nbs;
     const int dxs[8] = {-1, -1, 0, 1, 1, 1, 0, -1}, dys[8] = {0, -1, -1, -1, 0, 1, 1, 1};
@@ -839,8 +841,10 @@ __global__ void __launch_bounds__(TR_TPB) k_trace(const uint8_t* __restrict__ nb
         const float4* P = cloud + (long)s * N;
         const long cap_end = (s + 1) * (pool_cap / 8);
         for (int e = threadIdx.x; e < s_nch * TR_CHUNK; e += TR_TPB) {
-            const int c = e / TR_CHUNK, k = cout_[c] + (e - c * TR_CHUNK);
+            const int c = e / TR_CHUNK;
             const int r = cown[c];
+            if (r < 0) continue;
+            const int k = cout_[c] + (e - c * TR_CHUNK);
             if (k < s_len[r]) {
                 const long dst = s_off[r] + k;
                 if (dst < cap_end) pool[dst] = P[list[e]];
