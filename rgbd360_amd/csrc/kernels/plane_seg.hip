@@ -1,17 +1,18 @@
 // plane_seg.hip — OrganizedMultiPlaneSegmentation::segmentAndRefine on gfx950 and the
 // per-plane statistics the PbMap descriptors need (A8):
-//   k_ccl_*        4-connected components under PlaneCoefficientComparator (lock-free union-find,
-//                  roots = smallest raster index, labels numbered in raster order of their roots — the
-//                  reference's run-id compaction order)
-//   k_label_count  label sizes (wave-aggregated atomics);  k_big_list: labels with > 80 points, in order
-//   k_label_moments  exact moments per large label (one workgroup per label, int64/int128 sums)
+//   k_ccl_*        4-connected components under PlaneCoefficientComparator (LDS union-find per row
+//                  band, then lock-free global union of the band-crossing edges; roots = smallest
+//                  raster index, labels numbered in raster order of their roots — the reference's
+//                  run-id compaction order)
+//   k_big_list     labels with > 80 points, in order; k_label_scatter groups their pixels
+//   k_label_moments  exact moments per large label (int64/int128 sums over its pixel list)
 //   k_plane_fit    eigen33 plane fit, curvature test and the accumulating viewpoint of segment()
 //   k_refine       the two raster sweeps of refine(): one wave per sensor walks the rows; within a row
 //                  the left-to-right (right-to-left) label chains are resolved with wave scans over
 //                  per-lane chunk summaries; closeness to every model is precomputed per pixel as a
 //                  bit mask (k_refine_init)
 //   k_model_stats  final inlier moments (rig frame) + colour sums + the region's first pixel
-//   k_trace        findLabeledRegionBoundary (Moore-neighbour trace) on an LDS membership bitmap
+//   k_trace        findLabeledRegionBoundary (Moore-neighbour trace) over per-pixel neighbour masks
 //   k_vox_*        VoxelGrid of regions without a contour (Frame360.h:1017-1026): (region, voxel) hash
 //                  table with exact double sums, compacted into per-region voxel lists
 // Arithmetic follows oracle/src/planes_oracle.cpp and pbmap_oracle.cpp; see rgbd360_amd/csrc/plane_math.h.
@@ -23,11 +24,6 @@ namespace {
 __device__ __forceinline__ bool isfin(float v) { return __builtin_isfinite(v); }
 
 // ------------------------------------------------------------------ CCL
-__global__ void k_ccl_init(const float4* __restrict__ cloud, long total, int* __restrict__ parent) {
-    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x)
-        parent[i] = isfin(cloud[i].x) ? (int)i : -1;
-}
-
 __device__ __forceinline__ int ld(const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
 __device__ int find_root(const int* parent, int x) {
@@ -60,16 +56,67 @@ __device__ __forceinline__ bool plane_cmp(const float4& pa, const float4& na, co
     return fabsf(na.w - nb.w) < thr && nd > ang_thr;
 }
 
-__global__ void k_ccl_merge(const float4* __restrict__ cloud, const float4* __restrict__ nrm, int w, int h,
-                            float ang_thr, int* __restrict__ parent) {
-    const long N = (long)w * h, total = 8 * N;
-    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-        if (ld(parent + i) < 0) continue;
-        const int j = (int)(i % N);
-        const int r = j / w, c = j - (j / w) * w;
-        const float4 p = cloud[i], n = nrm[i];
-        if (c >= 1 && plane_cmp(p, n, nrm[i - 1], ang_thr)) unite(parent, (int)i, (int)i - 1);
-        if (r >= 1 && plane_cmp(p, n, nrm[i - w], ang_thr)) unite(parent, (int)i, (int)(i - w));
+// Two-level CCL: each workgroup labels a band of CCL_ROWS full rows with an LDS union-find (min-index
+// roots, the same representative the global union-find produces), writes every pixel's parent as
+// the global index of its band-local root, then k_ccl_border unites only the edges that cross band
+// boundaries in global memory.
+constexpr int CCL_ROWS = 8, CCL_TPB = 1024;
+
+__device__ int lds_find(const int* lp, int x) {
+    int p = lp[x];
+    while (p != x) {
+        x = p;
+        p = lp[x];
+    }
+    return x;
+}
+
+__device__ void lds_unite(int* lp, int a, int b) {
+    while (true) {
+        a = lds_find(lp, a);
+        b = lds_find(lp, b);
+        if (a == b) return;
+        if (a < b) { const int t = a; a = b; b = t; }
+        const int old = atomicCAS(lp + a, a, b);
+        if (old == a) return;
+        a = old;
+    }
+}
+
+__global__ void __launch_bounds__(CCL_TPB) k_ccl_local(const float4* __restrict__ cloud, const float4* __restrict__ nrm,
+                                                      int w, int h, float ang_thr, int* __restrict__ parent) {
+    extern __shared__ int lp[];
+    const int s = blockIdx.y, r0 = blockIdx.x * CCL_ROWS;
+    if (r0 >= h) return;
+    const int rows = min(CCL_ROWS, h - r0), n = rows * w;
+    const long base = (long)s * w * h + (long)r0 * w;
+    for (int k = threadIdx.x; k < n; k += CCL_TPB) lp[k] = isfin(cloud[base + k].x) ? k : -1;
+    __syncthreads();
+    for (int k = threadIdx.x; k < n; k += CCL_TPB) {
+        if (lp[k] < 0) continue;                   // invalid pixels never change
+        const int rr = k / w, c = k - rr * w;
+        const float4 p = cloud[base + k], nn = nrm[base + k];
+        if (c >= 1 && lp[k - 1] >= 0 && plane_cmp(p, nn, nrm[base + k - 1], ang_thr)) lds_unite(lp, k, k - 1);
+        if (rr >= 1 && lp[k - w] >= 0 && plane_cmp(p, nn, nrm[base + k - w], ang_thr)) lds_unite(lp, k, k - w);
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < n; k += CCL_TPB) {
+        const int v = lp[k];
+        parent[base + k] = v < 0 ? -1 : (int)(base + lds_find(lp, k));
+    }
+}
+
+__global__ void k_ccl_border(const float4* __restrict__ cloud, const float4* __restrict__ nrm, int w, int h,
+                             float ang_thr, int* __restrict__ parent) {
+    const int nb = (h - 1) / CCL_ROWS;                          // band boundaries per sensor
+    const long total = 8L * nb * w;
+    for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+        const int s = (int)(t / ((long)nb * w));
+        const int q = (int)(t - (long)s * nb * w);
+        const int b = q / w, c = q - b * w;
+        const long i = (long)s * w * h + (long)(b + 1) * CCL_ROWS * w + c;
+        if (ld(parent + i) < 0 || ld(parent + i - w) < 0) continue;
+        if (plane_cmp(cloud[i], nrm[i], nrm[i - w], ang_thr)) unite(parent, (int)i, (int)(i - w));
     }
 }
 
@@ -1048,8 +1095,14 @@ int launch_segmentation(r360_frame* f) {
     // PlaneCoefficientComparator::setAngularThreshold stores cosf(angle) (angle 0.039812, Frame360.h:959)
     const float ang_thr = cosf((float)0.039812);
     int slot = timing_begin(ctx, "k_ccl");
-    hipLaunchKernelGGL(k_ccl_init, dim3(blocks), dim3(256), 0, st, P.cloud, total, P.parent);
-    hipLaunchKernelGGL(k_ccl_merge, dim3(blocks), dim3(256), 0, st, P.cloud, P.nrm, w, h, ang_thr, P.parent);
+    hipLaunchKernelGGL(k_ccl_local, dim3((h + CCL_ROWS - 1) / CCL_ROWS, 8), dim3(CCL_TPB), sizeof(int) * CCL_ROWS * w,
+                       st, P.cloud, P.nrm, w, h, ang_thr, P.parent);
+    {
+        const long edges = 8L * ((h - 1) / CCL_ROWS) * w;
+        if (edges > 0)
+            hipLaunchKernelGGL(k_ccl_border, dim3((unsigned)((edges + 255) / 256)), dim3(256), 0, st, P.cloud, P.nrm, w,
+                               h, ang_thr, P.parent);
+    }
     hipLaunchKernelGGL(k_ccl_flatten, dim3(blocks), dim3(256), 0, st, P.parent, total, P.root);
     hipLaunchKernelGGL(k_ccl_number, dim3(8), dim3(1024), 0, st, P.root, N, P.parent, P.nlab);
     R360_HIP(hipMemsetAsync(P.cnt, 0, sizeof(int) * total, st));
