@@ -19,8 +19,9 @@
 
 namespace {
 
-constexpr int TPB = 256;
+constexpr int TPB = 1024;     // 16 waves: one workgroup per CU at the kernel's occupancy, few records
 constexpr int NW = TPB / 64;
+constexpr int RG = TPB / 16;  // record-reduction groups (16 lanes x 16 B per record)
 
 struct Pose12 { float R[9]; float t[3]; };
 
@@ -76,6 +77,13 @@ __device__ __forceinline__ Proj project(const Pose12& P, float d, float gray_s, 
                                         int nRows, int nCols, float half_nRows, float angle_res_inv, const IcpConst& C) {
     Proj o;
     const bool valid = (C.min_d < d && d < C.max_d);                // LUT validity (:4578)
+    if (!__any(valid)) {        // whole chunk without depth (sphere rows outside the sensors' view)
+        o.X = o.Y = o.Z = o.dist = o.dist_inv = 0.f;
+        o.gray_s = gray_s;
+        o.t = 0;
+        o.vis = false;
+        return o;
+    }
     const float lx = d * sp;                                       // LUT_xyz_sphere (:4580-4582)
     const float ly = -d * cp * st;
     const float lz = -d * cp * ct;
@@ -131,6 +139,7 @@ __device__ __forceinline__ void contribute(Acc& A, const Proj& o, const float4 G
                                            const IcpConst& C) {
     constexpr bool photo = (METHOD == R360_PHOTO_CONSISTENCY || METHOD == R360_PHOTO_DEPTH);
     constexpr bool depth = (METHOD == R360_DEPTH_CONSISTENCY || METHOD == R360_PHOTO_DEPTH);
+    if (!__any(o.vis)) return;  // nothing visible in the chunk: every term below would be zero
     const float X = o.X, Y = o.Y, Z = o.Z, dist = o.dist, dist_inv = o.dist_inv;
     A.h[28] += o.vis ? 1.f : 0.f;                                               // numVisiblePixels
     // photo saliency fails -> 'continue' skips the depth term too (:3038-3039)
@@ -230,10 +239,6 @@ __device__ __forceinline__ double wave_sum_d(double x) {
 // ---------------------------------------------------------------- GN step (thread 0 of last block)
 #include "icp_gn.inc"
 
-__device__ __forceinline__ double ld_sc1(const double* p) {  // agent-scope (L1-bypassing) load
-    return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
-                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
 
 template <int METHOD, int PF>
 __global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src, const float2* __restrict__ trg,
@@ -244,7 +249,7 @@ __global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src
                                                  int eval_only) {
     __shared__ float s_red[NW][32];
     __shared__ double s_err[NW];
-    __shared__ double s_fin[8][32];
+    __shared__ double s_fin[RG][32];
     __shared__ int s_last;
     __shared__ GnShared s_gn;
     __shared__ IcpState s_state;
@@ -407,26 +412,33 @@ __global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src
     const unsigned long long t_ticket = __builtin_amdgcn_s_memrealtime();
 #endif
     {
-        // fixed-order reduction of the per-workgroup records; 8 independent accumulators per thread
-        // keep 8 loads in flight (the serial chain of dependent loads was the finalize's cost)
-        const int v = threadIdx.x & 31, grp = threadIdx.x >> 5;  // 8 groups of 32
-        double a8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        // fixed-order reduction of the per-workgroup records: lane q of a 16-lane group loads bytes
+        // 16q..16q+15 of records g, g+RG, ... with L1-bypassing (sc1) 16-B buffer loads, 8 in flight;
+        // then thread v sums slot v over the groups in order
+        const int q = threadIdx.x & 15, g = threadIdx.x >> 4;
         const int nb = (int)gridDim.x;
-        int bk = grp;
-        for (; bk + 56 < nb; bk += 64) {
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(partials, 0, nb * 256, 0x00020000);
+        double a0 = 0.0, a1 = 0.0;
+        auto add = [&](const decltype(__builtin_amdgcn_raw_buffer_load_b128(rs, 0, 0, 16))& x) {
+            a0 += __longlong_as_double((long long)(((unsigned long long)x[1] << 32) | x[0]));
+            a1 += __longlong_as_double((long long)(((unsigned long long)x[3] << 32) | x[2]));
+        };
+        int r = g;
+        for (; r + 7 * RG < nb; r += 8 * RG) {
+            decltype(__builtin_amdgcn_raw_buffer_load_b128(rs, 0, 0, 16)) x[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) a8[j] += ld_sc1(partials + (long)(bk + 8 * j) * 32 + v);
+            for (int j = 0; j < 8; ++j) x[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, ((r + j * RG) * 16 + q) * 16, 0, 16);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) add(x[j]);
         }
-        for (int j = 0; bk < nb; bk += 8, ++j) a8[j & 7] += ld_sc1(partials + (long)bk * 32 + v);
-        double acc = 0.0;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc += a8[j];
-        s_fin[grp][v] = acc;
+        for (; r < nb; r += RG) add(__builtin_amdgcn_raw_buffer_load_b128(rs, (r * 16 + q) * 16, 0, 16));
+        s_fin[g][2 * q] = a0;
+        s_fin[g][2 * q + 1] = a1;
     }
     __syncthreads();
     if (threadIdx.x < 32) {
         double t = 0.0;
-        for (int g = 0; g < 8; ++g) t += s_fin[g][threadIdx.x];
+        for (int g = 0; g < RG; ++g) t += s_fin[g][threadIdx.x];
         s_fin[0][threadIdx.x] = t;
     }
     __syncthreads();

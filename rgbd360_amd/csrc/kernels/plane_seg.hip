@@ -148,18 +148,27 @@ __device__ int block_exscan(int v, int* sh, int& total) {
 }
 
 // roots -> label ids in raster order (one workgroup per sensor); rank stored at the root's slot
+constexpr int SCAN_V = 8;   // consecutive elements per thread in the per-sensor scans
+
 __global__ void __launch_bounds__(1024) k_ccl_number(const int* __restrict__ root, int N, int* __restrict__ rank,
                                                      int* __restrict__ nlab) {
     __shared__ int sh[17];
     const int s = blockIdx.x;
     const long base = (long)s * N;
     int acc = 0;
-    for (int j0 = 0; j0 < N; j0 += blockDim.x) {
-        const int j = j0 + threadIdx.x;
-        const int is_root = (j < N && root[base + j] == (int)(base + j)) ? 1 : 0;
+    for (int j0 = 0; j0 < N; j0 += blockDim.x * SCAN_V) {
+        const int j = j0 + threadIdx.x * SCAN_V;
+        int isr[SCAN_V], c = 0;
+#pragma unroll
+        for (int v = 0; v < SCAN_V; ++v) {
+            isr[v] = (j + v < N && root[base + j + v] == (int)(base + j + v)) ? 1 : 0;
+            c += isr[v];
+        }
         int tot;
-        const int ex = block_exscan(is_root, sh, tot);
-        if (is_root) rank[base + j] = acc + ex;
+        int r = acc + block_exscan(c, sh, tot);
+#pragma unroll
+        for (int v = 0; v < SCAN_V; ++v)
+            if (isr[v]) rank[base + j + v] = r++;
         acc += tot;
         __syncthreads();
     }
@@ -199,18 +208,30 @@ __global__ void __launch_bounds__(1024) k_big_list(const int* __restrict__ cnt, 
     const int s = blockIdx.x;
     const int n = nlab[s];
     int acc = 0, cacc = 0;
-    for (int j0 = 0; j0 < n; j0 += blockDim.x) {
-        const int j = j0 + threadIdx.x;
-        const int c = j < n ? cnt[(long)s * N + j] : 0;
-        const int f = c > min_inliers ? 1 : 0;
+    for (int j0 = 0; j0 < n; j0 += blockDim.x * SCAN_V) {
+        const int j = j0 + threadIdx.x * SCAN_V;
+        int c[SCAN_V], nf = 0, nc = 0;
+#pragma unroll
+        for (int v = 0; v < SCAN_V; ++v) {
+            c[v] = j + v < n ? cnt[(long)s * N + j + v] : 0;
+            if (c[v] > min_inliers) { ++nf; nc += c[v]; }
+        }
         int tot, ctot;
-        const int ex = block_exscan(f, sh, tot);
-        const int cex = block_exscan(f ? c : 0, sh, ctot);
-        const int b = acc + ex;
-        if (j < n) bmap[(long)s * N + j] = (f && b < maxbig) ? b : -1;
-        if (f && b < maxbig) {
-            big[s * maxbig + b] = j;
-            boff[s * maxbig + b] = cacc + cex;
+        int b = acc + block_exscan(nf, sh, tot);
+        int co = cacc + block_exscan(nc, sh, ctot);
+#pragma unroll
+        for (int v = 0; v < SCAN_V; ++v) {
+            if (j + v >= n) break;
+            const bool f = c[v] > min_inliers;
+            bmap[(long)s * N + j + v] = (f && b < maxbig) ? b : -1;
+            if (f) {
+                if (b < maxbig) {
+                    big[s * maxbig + b] = j + v;
+                    boff[s * maxbig + b] = co;
+                }
+                ++b;
+                co += c[v];
+            }
         }
         acc += tot;
         cacc += ctot;
