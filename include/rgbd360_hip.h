@@ -218,6 +218,11 @@ int r360_ctx_timing(r360_ctx* ctx, int enable);
 /* Per-kernel accumulated device time (ms) and launch counts since the last reset. */
 int r360_ctx_timing_read(r360_ctx* ctx, const char* kernel, double* ms, long* launches);
 int r360_ctx_timing_reset(r360_ctx* ctx);
+/* In-kernel execution spans of the fused ICP passes at one pyramid level (earliest workgroup start to
+ * the end of the last workgroup, s_memrealtime), summed in microseconds, and the pass count, since the
+ * last reset.  Unlike stream events they exclude queueing behind other streams' kernels. */
+int r360_ctx_kernel_time(r360_ctx* ctx, int level, double* us_sum, long* passes);
+int r360_ctx_kernel_time_reset(r360_ctx* ctx);
 
 #ifdef __cplusplus
 }

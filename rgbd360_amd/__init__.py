@@ -132,6 +132,8 @@ _SIGS = [
     ("r360_proj_check", C.c_int, [_FP, _FP, _FP, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_ulonglong),
                                   C.POINTER(C.c_ulonglong)]),
     ("r360_ctx_debug_stamps", C.c_int, [_P, C.POINTER(C.c_ulonglong)]),
+    ("r360_ctx_kernel_time", C.c_int, [_P, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_long)]),
+    ("r360_ctx_kernel_time_reset", C.c_int, [_P]),
     ("r360_ctx_timing", C.c_int, [_P, C.c_int]),
     ("r360_ctx_timing_read", C.c_int, [_P, C.c_char_p, _DP, C.POINTER(C.c_long)]),
     ("r360_ctx_timing_reset", C.c_int, [_P]),
@@ -201,6 +203,15 @@ class Context:
 
     def timing_reset(self):
         _check(lib().r360_ctx_timing_reset(self.h), "timing_reset")
+
+    def kernel_time(self, level: int):
+        """(summed in-kernel execution span in us, pass count) of the ICP passes at `level`."""
+        us, n = C.c_double(), C.c_long()
+        _check(lib().r360_ctx_kernel_time(self.h, level, C.byref(us), C.byref(n)), "kernel_time")
+        return us.value, n.value
+
+    def kernel_time_reset(self):
+        _check(lib().r360_ctx_kernel_time_reset(self.h), "kernel_time_reset")
 
     def close(self):
         if self.h:

@@ -108,6 +108,9 @@ extern "C" int r360_ctx_create(int device, r360_ctx** out) {
     R360_HIP(hipMemset(c->d_state, 0, sizeof(IcpState)));
     c->partials_cap = 2048;
     R360_HIP(hipMalloc(&c->d_partials, sizeof(double) * 32 * c->partials_cap));
+    R360_HIP(hipMalloc(&c->d_ktime, sizeof(unsigned long long) * 17));
+    R360_HIP(hipMemset(c->d_ktime, 0, sizeof(unsigned long long) * 17));
+    R360_HIP(hipMemset(c->d_ktime, 0xff, sizeof(unsigned long long)));
     R360_HIP(hipHostMalloc(&c->h_state, sizeof(IcpState), hipHostMallocDefault));
     *out = c;
     return 0;
@@ -121,11 +124,30 @@ extern "C" void r360_ctx_destroy(r360_ctx* c) {
     hipEventDestroy(c->wait_ev);
     hipFree(c->d_state);
     hipFree(c->d_partials);
+    hipFree(c->d_ktime);
     hipHostFree(c->h_state);
     hipFree(c->d_match_desc); hipFree(c->d_unary); hipFree(c->d_bin); hipFree(c->d_vhash);
     hipHostFree(c->h_unary); hipHostFree(c->h_bin);
     hipStreamDestroy(c->stream);
     delete c;
+}
+
+extern "C" int r360_ctx_kernel_time(r360_ctx* ctx, int level, double* us_sum, long* passes) {
+    CHECK_ARG(ctx && level >= 0 && level < 8 && us_sum && passes, "invalid arguments");
+    unsigned long long k[17];
+    if (ctx_wait(ctx)) return -1;
+    R360_HIP(hipMemcpy(k, ctx->d_ktime, sizeof k, hipMemcpyDeviceToHost));
+    *us_sum = (double)k[1 + level] * 0.01;   // 100 MHz ticks
+    *passes = (long)k[9 + level];
+    return 0;
+}
+
+extern "C" int r360_ctx_kernel_time_reset(r360_ctx* ctx) {
+    CHECK_ARG(ctx, "null ctx");
+    if (ctx_wait(ctx)) return -1;
+    R360_HIP(hipMemset(ctx->d_ktime, 0, sizeof(unsigned long long) * 17));
+    R360_HIP(hipMemset(ctx->d_ktime, 0xff, sizeof(unsigned long long)));
+    return 0;
 }
 
 extern "C" int r360_ctx_sync(r360_ctx* c) {

@@ -240,13 +240,15 @@ __device__ __forceinline__ double wave_sum_d(double x) {
 #include "icp_gn.inc"
 
 
-template <int METHOD, int PF>
+// TOP = 1 only renames the level-0 instantiation, so traces (rocprofv3) separate level 0 from level 1,
+// which launch the same grid.
+template <int METHOD, int PF, int TOP>
 __global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src, const float2* __restrict__ trg,
                                                  const float4* __restrict__ tg, const float* __restrict__ sinphi,
                                                  const float* __restrict__ cosphi, const float* __restrict__ sinth,
                                                  const float* __restrict__ costh, int nRows, int nCols,
                                                  IcpConst C, IcpState* S, double* __restrict__ partials, int first,
-                                                 int eval_only) {
+                                                 int eval_only, unsigned long long* __restrict__ kt) {
     __shared__ float s_red[NW][32];
     __shared__ double s_err[NW];
     __shared__ double s_fin[RG][32];
@@ -259,6 +261,9 @@ __global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #endif
     if (!first && !S->active && !eval_only) return;
+    if (threadIdx.x == 0)   // execution span: earliest workgroup start of this pass
+        __hip_atomic_fetch_min(kt, (unsigned long long)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
 
     const float* pm = (first && !eval_only) ? S->pose : S->cand;
     Pose12 P;
@@ -488,6 +493,14 @@ __global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src
 #endif
         }
         if (eval_only && threadIdx.x == 0) S->ticket = 0;
+        if (threadIdx.x == 0) {   // the last workgroup closes the span
+            const unsigned long long t0 = __hip_atomic_load(kt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+            const int lv = C.level & 7;
+            kt[1 + lv] += t1 > t0 ? t1 - t0 : 0;
+            kt[9 + lv] += 1;
+            __hip_atomic_store(kt, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 
@@ -619,10 +632,11 @@ static int env_int(const char* name, int dflt) {
 
 template <int M, int PF>
 static void launch_pass(r360_ctx* ctx, int nb, const LevelBufs& Ls, const LevelBufs& Lt, const LevelTrig& T,
-                        const IcpConst& C, int first, int eval_only) {
-    hipLaunchKernelGGL((k_icp_pass<M, PF>), dim3(nb), dim3(TPB), 0, ctx->stream, Ls.p0, Lt.p0, Lt.tg, T.sinphi,
+                        const IcpConst& C, int first, int eval_only, bool top) {
+    auto kern = top ? k_icp_pass<M, PF, 1> : k_icp_pass<M, PF, 0>;
+    hipLaunchKernelGGL(kern, dim3(nb), dim3(TPB), 0, ctx->stream, Ls.p0, Lt.p0, Lt.tg, T.sinphi,
                        T.cosphi, T.sinth, T.costh, Ls.rows, Ls.cols, C, ctx->d_state, ctx->d_partials, first,
-                       eval_only);
+                       eval_only, ctx->d_ktime);
 }
 
 int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src, int level, int method,
@@ -641,9 +655,9 @@ int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src
         int dev = 0;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&o.cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[0], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 0>, TPB, 0);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[1], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 1>, TPB, 0);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[2], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 2>, TPB, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[0], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 0, 0>, TPB, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[1], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 1, 0>, TPB, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[2], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 2, 0>, TPB, 0);
         return o;
     }();
     const int npx = Ls.rows * Ls.cols;
@@ -656,9 +670,9 @@ int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src
     const int slot = timing_begin(ctx, name);
 #define R360_LAUNCH(M)                                                              \
     do {                                                                            \
-        if (pf == 1) launch_pass<M, 1>(ctx, nb, Ls, Lt, T, C, first, eval_only);   \
-        else if (pf == 2) launch_pass<M, 2>(ctx, nb, Ls, Lt, T, C, first, eval_only); \
-        else launch_pass<M, 0>(ctx, nb, Ls, Lt, T, C, first, eval_only);          \
+        if (pf == 1) launch_pass<M, 1>(ctx, nb, Ls, Lt, T, C, first, eval_only, level == 0);   \
+        else if (pf == 2) launch_pass<M, 2>(ctx, nb, Ls, Lt, T, C, first, eval_only, level == 0); \
+        else launch_pass<M, 0>(ctx, nb, Ls, Lt, T, C, first, eval_only, level == 0);          \
     } while (0)
     if (method == R360_PHOTO_CONSISTENCY) R360_LAUNCH(R360_PHOTO_CONSISTENCY);
     else if (method == R360_DEPTH_CONSISTENCY) R360_LAUNCH(R360_DEPTH_CONSISTENCY);

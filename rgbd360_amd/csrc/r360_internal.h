@@ -159,6 +159,9 @@ struct r360_ctx {
     hipEvent_t wait_ev = nullptr;   // blocking-sync event: host waits sleep instead of spinning
     IcpState* d_state = nullptr;
     double* d_partials = nullptr;
+    // in-kernel execution spans of the ICP passes (s_memrealtime, 100 MHz): [0] earliest workgroup start
+    // of the running pass, [1+l] summed spans at level l, [9+l] pass counts
+    unsigned long long* d_ktime = nullptr;
     int partials_cap = 0;
     IcpState* h_state = nullptr;  // pinned
     int timing = 0;

@@ -8,6 +8,7 @@ import csv
 import glob
 import json
 import os
+import re
 import shutil
 import sys
 
@@ -19,16 +20,23 @@ stats = glob.glob(os.path.join(src, "trace", "*kernel_stats.csv"))[0]
 shutil.copy(stats, os.path.join(dst, "kernel_stats.csv"))
 trace = glob.glob(os.path.join(src, "trace", "*kernel_trace.csv"))[0]
 rows = list(csv.DictReader(open(trace)))
-icp = [r for r in rows if "k_icp_pass" in r["Kernel_Name"]]
+
+
+def is_l0(name):
+    # the level-0 instantiation carries template tag TOP = 1: k_icp_pass<METHOD, PF, 1>
+    return re.search(r"k_icp_pass<\d+, \d+, 1>", name) is not None or re.search(r"k_icp_passILi\d+ELi\d+ELi1E", name) is not None
+
+
+icp = [r for r in rows if is_l0(r["Kernel_Name"])]
 gmax = max(int(r["Grid_Size_X"]) for r in icp)
-l0 = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in icp if int(r["Grid_Size_X"]) == gmax]
+l0 = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in icp]
 
 
 def pmc(name):
     vals = []
     for f in glob.glob(os.path.join(src, "pmc*", "*counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            if "k_icp_pass" in r["Kernel_Name"] and int(r["Grid_Size"]) == gmax and r["Counter_Name"] == name:
+            if is_l0(r["Kernel_Name"]) and r["Counter_Name"] == name:
                 vals.append(float(r["Counter_Value"]))
     return float(np.median(vals)) if vals else None
 
