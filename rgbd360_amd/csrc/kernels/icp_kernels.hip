@@ -19,7 +19,13 @@
 
 namespace {
 
-constexpr int TPB = 1024;     // 16 waves: one workgroup per CU at the kernel's occupancy, few records
+#ifndef R360_ICP_TPB
+#define R360_ICP_TPB 1024
+#endif
+#ifndef R360_ICP_MINB
+#define R360_ICP_MINB 1
+#endif
+constexpr int TPB = R360_ICP_TPB;  // 16 waves: one workgroup per CU at the kernel's occupancy, few records
 constexpr int NW = TPB / 64;
 constexpr int RG = TPB / 16;  // record-reduction groups (16 lanes x 16 B per record)
 
@@ -243,7 +249,7 @@ __device__ __forceinline__ double wave_sum_d(double x) {
 // TOP = 1 only renames the level-0 instantiation, so traces (rocprofv3) separate level 0 from level 1,
 // which launch the same grid.
 template <int METHOD, int PF, int TOP>
-__global__ __launch_bounds__(TPB) void k_icp_pass(const float2* __restrict__ src, const float2* __restrict__ trg,
+__global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const float2* __restrict__ src, const float2* __restrict__ trg,
                                                  const float4* __restrict__ tg, const float* __restrict__ sinphi,
                                                  const float* __restrict__ cosphi, const float* __restrict__ sinth,
                                                  const float* __restrict__ costh, int nRows, int nCols,
