@@ -71,6 +71,7 @@ struct Proj {
     float X, Y, Z, dist, dist_inv, gray_s;
     int t;          // target pixel index (0 when not visible)
     bool vis;       // valid source depth and projected inside the target image
+    bool fix;       // near a rounding boundary: project_fix decides the pixel exactly
 };
 
 // Guard bands (pixels) around the .5 rounding boundaries inside which the fast projection defers to the
@@ -79,17 +80,23 @@ struct Proj {
 // divisions in atan2 plus the float rounding of theta + pi); coarser levels scale them down.
 constexpr float kGuardRow = 6e-4f, kGuardCol = 1.5e-3f;
 
+// round() + int conversion + the (:2989) bounds test, on the float values so NaN and out-of-range
+// projections are rejected exactly as the x86 reference's (int) conversion does.
+__device__ __forceinline__ void set_pixel(Proj& o, float rr, float cc, bool valid, int nRows, int nCols) {
+    const float rf = roundf(rr);
+    const float cf = roundf(cc);
+    o.vis = valid && (rf >= 0.f && rf < (float)nRows) && cf < (float)nCols;
+    o.t = o.vis ? (int)rf * nCols + (int)cf : 0;
+}
+
+// Branch-free fast projection: the lanes whose coordinates land inside a guard band of a rounding
+// boundary (or whose fast path produced NaN, at the poles) are flagged in o.fix and re-projected
+// exactly by project_fix before their target pixel is used.  Keeping this part branch-free lets the
+// scheduler interleave it with the accumulation of the previous chunk.
 __device__ __forceinline__ Proj project(const Pose12& P, float d, float gray_s, float sp, float cp, float st, float ct,
                                         int nRows, int nCols, float half_nRows, float angle_res_inv, const IcpConst& C) {
     Proj o;
     const bool valid = (C.min_d < d && d < C.max_d);                // LUT validity (:4578)
-    if (!__any(valid)) {        // whole chunk without depth (sphere rows outside the sensors' view)
-        o.X = o.Y = o.Z = o.dist = o.dist_inv = 0.f;
-        o.gray_s = gray_s;
-        o.t = 0;
-        o.vis = false;
-        return o;
-    }
     const float lx = d * sp;                                       // LUT_xyz_sphere (:4580-4582)
     const float ly = -d * cp * st;
     const float lz = -d * cp * ct;
@@ -99,29 +106,37 @@ __device__ __forceinline__ Proj project(const Pose12& P, float d, float gray_s, 
     const float d2 = X * X + Y * Y + Z * Z;
     // |p'| is exact (it enters the depth residual); the projection itself uses hardware rsq/rcp
     const float dist = sqrtf(d2);
-    float dist_inv = __builtin_amdgcn_rsqf(d2);
-    float phi_trg = r360m::asinf_fast(X * dist_inv);
-    float theta_trg = (float)((double)r360m::atan2f_fast(Y, Z) + R360_PI);
-    float rr = half_nRows - phi_trg * angle_res_inv;
-    float cc = theta_trg * angle_res_inv;
+    const float dist_inv = __builtin_amdgcn_rsqf(d2);
+    const float phi_trg = r360m::asinf_fast(X * dist_inv);
+    const float theta_trg = (float)((double)r360m::atan2f_fast(Y, Z) + R360_PI);
+    const float rr = half_nRows - phi_trg * angle_res_inv;
+    const float cc = theta_trg * angle_res_inv;
     const float gr = fabsf(rr - floorf(rr) - 0.5f), gc = fabsf(cc - floorf(cc) - 0.5f);
-    if (valid && !(gr >= kGuardRow && gc >= kGuardCol)) {   // also catches a NaN of the fast path (poles)
-        // near a rounding boundary: the exact program (same float expressions as the reference,
-        // glibc-exact asinf/atan2f, IEEE sqrt/div) decides the pixel
-        dist_inv = 1.f / dist;
-        phi_trg = r360m::asinf(X * dist_inv);
-        theta_trg = (float)((double)r360m::atan2f_sel(Y, Z) + R360_PI);
-        rr = half_nRows - phi_trg * angle_res_inv;
-        cc = theta_trg * angle_res_inv;
-    }
-    // round() + int conversion + the (:2989) bounds test, on the float values so NaN and out-of-range
-    // projections are rejected exactly as the x86 reference's (int) conversion does.
-    const float rf = roundf(rr);
-    const float cf = roundf(cc);
-    o.vis = valid && (rf >= 0.f && rf < (float)nRows) && cf < (float)nCols;
-    o.t = o.vis ? (int)rf * nCols + (int)cf : 0;
+    o.fix = valid && !(gr >= kGuardRow && gc >= kGuardCol);          // also catches a NaN of the fast path
+    set_pixel(o, rr, cc, valid, nRows, nCols);
     o.X = X; o.Y = Y; o.Z = Z; o.dist = dist; o.dist_inv = dist_inv; o.gray_s = gray_s;
     return o;
+}
+
+// Exact re-projection of the flagged lanes: the reference's float expressions with glibc-exact
+// asinf/atan2f and IEEE sqrt/div decide the pixel.  Returns whether any lane of the wave changed
+// its target pixel (the caller then re-issues the gathers).
+__device__ __forceinline__ bool project_fix(Proj& o, int nRows, int nCols, float half_nRows, float angle_res_inv) {
+    if (!__any(o.fix)) return false;
+    bool changed = false;
+    if (o.fix) {
+        o.dist_inv = 1.f / o.dist;
+        const float phi_trg = r360m::asinf(o.X * o.dist_inv);
+        const float theta_trg = (float)((double)r360m::atan2f_sel(o.Y, o.Z) + R360_PI);
+        const float rr = half_nRows - phi_trg * angle_res_inv;
+        const float cc = theta_trg * angle_res_inv;
+        const int t0 = o.t;
+        const bool v0 = o.vis;
+        set_pixel(o, rr, cc, true, nRows, nCols);
+        o.fix = false;
+        changed = o.t != t0 || o.vis != v0;
+    }
+    return __any(changed);
 }
 
 __device__ __forceinline__ void acc_fma(Acc& A, const float J[6], float r) {
@@ -145,7 +160,6 @@ __device__ __forceinline__ void contribute(Acc& A, const Proj& o, const float4 G
                                            const IcpConst& C) {
     constexpr bool photo = (METHOD == R360_PHOTO_CONSISTENCY || METHOD == R360_PHOTO_DEPTH);
     constexpr bool depth = (METHOD == R360_DEPTH_CONSISTENCY || METHOD == R360_PHOTO_DEPTH);
-    if (!__any(o.vis)) return;  // nothing visible in the chunk: every term below would be zero
     const float X = o.X, Y = o.Y, Z = o.Z, dist = o.dist, dist_inv = o.dist_inv;
     A.h[28] += o.vis ? 1.f : 0.f;                                               // numVisiblePixels
     // photo saliency fails -> 'continue' skips the depth term too (:3038-3039)
@@ -294,7 +308,8 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const float2* _
     const float4* ct4 = reinterpret_cast<const float4*>(costh);
     const int cq = nCols >> 2;
     auto one = [&](float d, float g, float sp, float cp, float st, float ct) {
-        const Proj o = project(P, d, g, sp, cp, st, ct, nRows, nCols, half_nRows, angle_res_inv, C);
+        Proj o = project(P, d, g, sp, cp, st, ct, nRows, nCols, half_nRows, angle_res_inv, C);
+        project_fix(o, nRows, nCols, half_nRows, angle_res_inv);
         const float4 G = tg[o.t];
         const float2 T = trg[o.t];
         contribute<METHOD>(A, o, G, T, angle_res_inv, C);
@@ -302,8 +317,10 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const float2* _
     auto two = [&](float d0, float g0, float d1, float g1, float sp, float cp, float st0, float ct0, float st1,
                    float ct1) {
         // project both, issue both gathers, then the math (ILP + loads in flight)
-        const Proj o0 = project(P, d0, g0, sp, cp, st0, ct0, nRows, nCols, half_nRows, angle_res_inv, C);
-        const Proj o1 = project(P, d1, g1, sp, cp, st1, ct1, nRows, nCols, half_nRows, angle_res_inv, C);
+        Proj o0 = project(P, d0, g0, sp, cp, st0, ct0, nRows, nCols, half_nRows, angle_res_inv, C);
+        Proj o1 = project(P, d1, g1, sp, cp, st1, ct1, nRows, nCols, half_nRows, angle_res_inv, C);
+        project_fix(o0, nRows, nCols, half_nRows, angle_res_inv);
+        project_fix(o1, nRows, nCols, half_nRows, angle_res_inv);
         const float4 G0 = tg[o0.t], G1 = tg[o1.t];
         const float2 T0 = trg[o0.t], T1 = trg[o1.t];
         contribute<METHOD>(A, o0, G0, T0, angle_res_inv, C);
@@ -349,24 +366,30 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const float2* _
             // Per half-iteration h: load the source of chunk h+2, project chunk h+1 and issue its gathers,
             // accumulate chunk h.  Loads are issued in the order they are consumed, so the in-order
             // vmcnt lets each wait skip the five younger loads still in flight.
+            // The gathers of a chunk are issued speculatively from the fast projection; the rare
+            // guard-band lanes are re-projected at the next half-iteration boundary and, if a pixel
+            // changed, the chunk's gathers are re-issued before it is accumulated.
             Src sA = ld(base(0));
             Src sB = ld(base(1));
             Proj oA = prj(sA);
+            project_fix(oA, nRows, nCols, half_nRows, angle_res_inv);
             float4 GA = gt.g(oA.t);
             float2 TA = gt.T(oA.t);
             for (int k = 0;; k += 2) {
                 sA = ld(base(k + 2));
-                const Proj oB = prj(sB);
-                const float4 GB = gt.g(oB.t);
-                const float2 TB = gt.T(oB.t);
+                Proj oB = prj(sB);
+                float4 GB = gt.g(oB.t);
+                float2 TB = gt.T(oB.t);
                 contribute<METHOD>(A, oA, GA, TA, angle_res_inv, C);
                 if (k + 1 >= n_it) break;
+                if (project_fix(oB, nRows, nCols, half_nRows, angle_res_inv)) { GB = gt.g(oB.t); TB = gt.T(oB.t); }
                 sB = ld(base(k + 3));
                 oA = prj(sA);
                 GA = gt.g(oA.t);
                 TA = gt.T(oA.t);
                 contribute<METHOD>(A, oB, GB, TB, angle_res_inv, C);
                 if (k + 2 >= n_it) break;
+                if (project_fix(oA, nRows, nCols, half_nRows, angle_res_inv)) { GA = gt.g(oA.t); TA = gt.T(oA.t); }
             }
         }
     } else {
