@@ -132,6 +132,13 @@ int r360_align360_result(r360_ctx* ctx, float pose_out[16], float H_out[36], flo
 int r360_icp_eval(r360_ctx* ctx, r360_frame* trg, r360_frame* src, int level, const float pose[16],
                   int method, const r360_icp_params* p, double H[36], double g[6],
                   double* err2, int* n_valid, int* n_visible);
+/* Occlusion-aware pass at `pose` (alignFrames360 occlusion 1 / 2, :4598-4627): H / g of
+ * calcHessGrad_sphereOcc{occ} and the value errorPhotoICP_sphereOcc{occ} returns (:3232-3370,
+ * :3720-3855); occlusion 0 gives errorPhotoICP_sphere's value.  n_valid = the error's point count
+ * (Occ1: photo + depth terms; Occ2: nValidDepthPts), n_visible = the HessGrad's numVisiblePixels. */
+int r360_icp_eval_occ(r360_ctx* ctx, r360_frame* trg, r360_frame* src, int level, const float pose[16],
+                      int method, int occlusion, const r360_icp_params* p, double H[36], double g[6],
+                      double* error, int* n_valid, int* n_visible);
 
 /* CPose3D::exp(mu, pseudo) (MRPT; used at RegisterPhotoICP.h:4697). */
 void r360_exp_se3(const double mu[6], int pseudo, float T[16]);

@@ -91,6 +91,11 @@ def lib() -> C.CDLL:
             "orc_hessgrad_sphere": (None, [C.POINTER(Level), fp, C.c_int, C.POINTER(IcpParams), dp, dp, ip]),
             "orc_align360": (C.c_int, [vp, vp, vp, vp, C.c_int, C.c_int, fp, C.c_int, C.POINTER(IcpParams), fp,
                                        fp, fp, C.POINTER(IcpStats)]),
+            "orc_align360_occ": (C.c_int, [vp, vp, vp, vp, C.c_int, C.c_int, fp, C.c_int, C.c_int,
+                                           C.POINTER(IcpParams), fp, fp, fp, C.POINTER(IcpStats)]),
+            "orc_error_sphere_occ": (C.c_double, [C.POINTER(Level), fp, C.c_int, C.c_int, C.POINTER(IcpParams), ip]),
+            "orc_hessgrad_sphere_occ": (None, [C.POINTER(Level), fp, C.c_int, C.c_int, C.POINTER(IcpParams), dp, dp,
+                                               ip]),
             "orc_exp_se3": (None, [dp, C.c_int, fp]),
             "orc_huber": (C.c_float, [C.c_float, C.c_float]),
             "orc_libm": (None, [fp, fp, fp, C.c_int, fp, fp]),
@@ -275,14 +280,38 @@ def hessgrad_sphere(src: dict, trg: dict, pose, method=PHOTO_DEPTH, params: IcpP
     return H.reshape(6, 6), g, nvis.value
 
 
-def align360(trg_bgr, trg_dep, src_bgr, src_dep, init=None, method=PHOTO_DEPTH, params: IcpParams | None = None):
+def error_sphere_occ(src: dict, trg: dict, pose, method=PHOTO_DEPTH, occlusion=1,
+                     params: IcpParams | None = None):
+    """errorPhotoICP_sphereOcc{1,2} (occlusion 0 = errorPhotoICP_sphere): (error, n_valid)."""
+    L, keep = _level_struct(src, trg)
+    p = params or IcpParams.default()
+    nv = C.c_int()
+    e = lib().orc_error_sphere_occ(C.byref(L), _f(mat16(pose)), method, occlusion, C.byref(p), C.byref(nv))
+    return e, nv.value
+
+
+def hessgrad_sphere_occ(src: dict, trg: dict, pose, method=PHOTO_DEPTH, occlusion=2,
+                        params: IcpParams | None = None):
+    """calcHessGrad_sphereOcc2 (occlusion 0 / 1 = calcHessGrad_sphere): (H, g, n_visible)."""
+    L, keep = _level_struct(src, trg)
+    p = params or IcpParams.default()
+    H, g, nvis = np.zeros(36), np.zeros(6), C.c_int()
+    lib().orc_hessgrad_sphere_occ(C.byref(L), _f(mat16(pose)), method, occlusion, C.byref(p),
+                                  H.ctypes.data_as(C.POINTER(C.c_double)), g.ctypes.data_as(C.POINTER(C.c_double)),
+                                  C.byref(nvis))
+    return H.reshape(6, 6), g, nvis.value
+
+
+def align360(trg_bgr, trg_dep, src_bgr, src_dep, init=None, method=PHOTO_DEPTH, params: IcpParams | None = None,
+             occlusion=0):
     trg_bgr, trg_dep, src_bgr, src_dep = [np.ascontiguousarray(a) for a in (trg_bgr, trg_dep, src_bgr, src_dep)]
     p = params or IcpParams.default()
     init16 = mat16(np.eye(4) if init is None else init)
     po, Ho, go = np.zeros(16, np.float32), np.zeros(36, np.float32), np.zeros(6, np.float32)
     st = IcpStats()
-    rc = lib().orc_align360(_v(trg_bgr), _v(trg_dep), _v(src_bgr), _v(src_dep), src_dep.shape[0], src_dep.shape[1],
-                            _f(init16), method, C.byref(p), _f(po), _f(Ho), _f(go), C.byref(st))
+    rc = lib().orc_align360_occ(_v(trg_bgr), _v(trg_dep), _v(src_bgr), _v(src_dep), src_dep.shape[0],
+                                src_dep.shape[1], _f(init16), method, occlusion, C.byref(p), _f(po), _f(Ho), _f(go),
+                                C.byref(st))
     return rc, from16(po), Ho.reshape(6, 6).T.copy(), go, st
 
 

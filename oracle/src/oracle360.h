@@ -88,6 +88,16 @@ double orc_error_sphere(const orc_level* L, const float pose[16], int method,
 void   orc_hessgrad_sphere(const orc_level* L, const float pose[16], int method,
                            const orc_icp_params* p, double H[36], double g[6], int* n_visible);
 
+/* ---- §8(f)1: occlusion-aware variants (occ 1 / 2); occ 0 = the plain functions above */
+double orc_error_sphere_occ(const orc_level* L, const float pose[16], int method, int occ,
+                            const orc_icp_params* p, int* n_valid);
+void   orc_hessgrad_sphere_occ(const orc_level* L, const float pose[16], int method, int occ,
+                               const orc_icp_params* p, double H[36], double g[6], int* n_visible);
+int    orc_align360_occ(const uint8_t* trg_bgr, const uint16_t* trg_depth,
+                        const uint8_t* src_bgr, const uint16_t* src_depth, int rows, int cols,
+                        const float init[16], int method, int occlusion, const orc_icp_params* p,
+                        float pose_out[16], float H_out[36], float g_out[6], orc_icp_stats* st);
+
 /* ---- A15: full alignFrames360 from sphere images */
 int orc_align360(const uint8_t* trg_bgr, const uint16_t* trg_depth,
                  const uint8_t* src_bgr, const uint16_t* src_depth,

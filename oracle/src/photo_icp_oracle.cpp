@@ -306,6 +306,235 @@ static void hessgrad_sphere_lut(const orc_level* L, const Lut& lut, const float 
     *n_visible = (int)nvis;
 }
 
+// ---------------------------------------------------------------------------
+// §8(f)1 — occlusion-aware variants (alignFrames360 occlusion = 1 / 2, :4598-4627).  The reference
+// runs these loops under `omp parallel for` with unsynchronised Z-buffer and residual writes (a data
+// race); the restatement takes the single-thread order, LUT index i ascending, which is the only
+// deterministic reading.
+// ---------------------------------------------------------------------------
+static const float kThresDepthOutliers = 0.3f;   // alignFrames360 :4525
+
+// errorPhotoICP_sphereOcc1 (:3232-3370): Z-buffer on the TARGET pixel; an accepted point overwrites
+// the pixel's residual, every accepted point counts.  Returns avPhotoResidual + avDepthResidual.
+static double error_sphere_occ1(const orc_level* L, const Lut& lut, const float pose[16], int method,
+                                const orc_icp_params* p, int* n_valid) {
+    const int nRows = L->rows, nCols = L->cols;
+    const float angle_res = 2 * REF_PI / nCols;
+    const float angle_res_inv = 1 / angle_res;
+    const float half_nRows = 0.5 * nRows - 0.5;
+    const double stdDevPhoto_inv = 1. / p->std_dev_photo;
+    const Pose P = split_pose(pose);
+    const long N = (long)nRows * nCols;
+    std::vector<float> zbuf(N, 0.f), resP(N, 0.f), resD(N, 0.f);
+    long nP = 0, nD = 0;
+    for (long i = 0; i < N; ++i) {
+        if (lut.x[i] == INVALID_POINT) continue;
+        Proj o = project(P, lut.x[i], lut.y[i], lut.z[i], nRows, nCols, half_nRows, angle_res_inv);
+        if (!o.vis) continue;
+        const size_t ii = (size_t)o.r * nCols + o.c;
+        if (zbuf[ii] > 0 && o.dist_inv < zbuf[ii]) continue;      // occluded (:3292-3294)
+        zbuf[ii] = o.dist_inv;
+        if (method == ORC_PHOTO || method == ORC_PHOTO_DEPTH) {
+            if (std::fabs(L->gx[ii]) < p->thres_sal_int && std::fabs(L->gy[ii]) < p->thres_sal_int) continue;
+            float photoDiff = L->gray_trg[ii] - L->gray_src[i];
+            double weight_photo = orc_huber(photoDiff, p->std_dev_photo) * stdDevPhoto_inv;
+            float wE = (float)(weight_photo * photoDiff);
+            resP[ii] = wE * wE;
+            ++nP;
+        }
+        if (method == ORC_DEPTH || method == ORC_PHOTO_DEPTH) {
+            float depth2 = L->depth_trg[ii];
+            if (std::isfinite(depth2)) {
+                if (std::fabs(L->dgx[ii]) < p->thres_sal_depth && std::fabs(L->dgy[ii]) < p->thres_sal_depth) continue;
+                float depthDiff = depth2 - o.dist;
+                float sd = p->std_dev_depth * depth2;
+                double weight_depth = orc_huber(depthDiff, sd) / sd;
+                float wE = (float)(weight_depth * depthDiff);
+                resD[ii] = wE * wE;
+                ++nD;
+            }
+        }
+    }
+    double PR = 0.0, DR = 0.0;
+    for (long i = 0; i < N; ++i) { PR += resP[i]; DR += resD[i]; }
+    *n_valid = (int)(nP + nD);
+    return std::sqrt(PR / nP) + std::sqrt(DR / nD);
+}
+
+// errorPhotoICP_sphereOcc2 (:3720-3855): depth-outlier filter, then the target Z-buffer; residuals are
+// kept per SOURCE point, so every accepted point contributes.  Both averages use nValidDepthPts.
+static double error_sphere_occ2(const orc_level* L, const Lut& lut, const float pose[16], int method,
+                                const orc_icp_params* p, int* n_valid) {
+    const int nRows = L->rows, nCols = L->cols;
+    const float angle_res = 2 * REF_PI / nCols;
+    const float angle_res_inv = 1 / angle_res;
+    const float half_nRows = 0.5 * nRows - 0.5;
+    const double stdDevPhoto_inv = 1. / p->std_dev_photo;
+    const Pose P = split_pose(pose);
+    const long N = (long)nRows * nCols;
+    std::vector<float> zbuf(N, 0.f), resP(N, 0.f), resD(N, 0.f);
+    long nV = 0;
+    for (long i = 0; i < N; ++i) {
+        if (lut.x[i] == INVALID_POINT) continue;
+        Proj o = project(P, lut.x[i], lut.y[i], lut.z[i], nRows, nCols, half_nRows, angle_res_inv);
+        if (!o.vis) continue;
+        const size_t ii = (size_t)o.r * nCols + o.c;
+        float depth2 = L->depth_trg[ii];
+        float depthDiff = depth2 - o.dist;
+        if (std::fabs(depthDiff) > kThresDepthOutliers) continue;     // :3790-3791
+        if (zbuf[ii] > 0 && o.dist_inv < zbuf[ii]) continue;         // :3794-3796
+        zbuf[ii] = o.dist_inv;
+        ++nV;
+        if (method == ORC_PHOTO || method == ORC_PHOTO_DEPTH) {
+            if (std::fabs(L->gx[ii]) < p->thres_sal_int && std::fabs(L->gy[ii]) < p->thres_sal_int) continue;
+            float photoDiff = L->gray_trg[ii] - L->gray_src[i];
+            double weight_photo = orc_huber(photoDiff, p->std_dev_photo) * stdDevPhoto_inv;
+            float wE = (float)(weight_photo * photoDiff);
+            resP[i] = wE * wE;
+        }
+        if (method == ORC_DEPTH || method == ORC_PHOTO_DEPTH) {
+            if (std::isfinite(depth2)) {
+                if (std::fabs(L->dgx[ii]) < p->thres_sal_depth && std::fabs(L->dgy[ii]) < p->thres_sal_depth) continue;
+                float sd = p->std_dev_depth * depth2;
+                double weight_depth = orc_huber(depthDiff, sd) / sd;
+                float wE = (float)(weight_depth * depthDiff);
+                resD[i] = wE * wE;
+            }
+        }
+    }
+    double PR = 0.0, DR = 0.0;
+    for (long i = 0; i < N; ++i) { PR += resP[i]; DR += resD[i]; }
+    *n_valid = (int)nV;
+    return std::sqrt(PR / nV) + std::sqrt(DR / nV);
+}
+
+// calcHessGrad_sphereOcc2 (:3861-4250): depth-outlier filter; the LAST filtered point of each target
+// pixel (LUT order) owns that pixel's Jacobian rows and residuals.  A depth-saliency `continue` skips
+// the store of both rows.  numVisiblePixels counts target pixels hit by a filtered point.
+// (calcHessGrad_sphereOcc1 indexes its Z-buffer by the source index, :3486-3488, so it never occludes
+// and equals calcHessGrad_sphere.)
+static void hessgrad_sphere_occ2(const orc_level* L, const Lut& lut, const float pose[16], int method,
+                                 const orc_icp_params* p, double H[36], double g[6], int* n_visible) {
+    const int nRows = L->rows, nCols = L->cols;
+    const float angle_res = 2 * REF_PI / nCols;
+    const float angle_res_inv = 1 / angle_res;
+    const float half_nRows = 0.5 * nRows - 0.5;
+    const float stdDevPhoto_inv = 1. / p->std_dev_photo;
+    const Pose P = split_pose(pose);
+    const long N = (long)nRows * nCols;
+    std::vector<float> zbuf(N, 0.f), JP(6 * N), JD(6 * N), rP(N), rD(N);
+    std::vector<char> vP(N, 0), vD(N, 0);
+    long nvis = 0;
+    for (long i = 0; i < N; ++i) {
+        if (lut.x[i] == INVALID_POINT) continue;
+        Proj o = project(P, lut.x[i], lut.y[i], lut.z[i], nRows, nCols, half_nRows, angle_res_inv);
+        if (!o.vis) continue;
+        const size_t ii = (size_t)o.r * nCols + o.c;
+        float depth2 = L->depth_trg[ii];
+        float depthDiff = depth2 - o.dist;
+        if (std::fabs(depthDiff) > kThresDepthOutliers) continue;
+        if (zbuf[ii] == 0) ++nvis;
+        zbuf[ii] = o.dist_inv;
+        const float X = o.x, Y = o.y, Z = o.z;
+        float T[3][6] = {{1, 0, 0, 0, Z, -Y}, {0, 1, 0, -Z, 0, X}, {0, 0, 1, Y, -X, 0}};
+        float z_inv = 1.f / Z;
+        float z_inv2 = z_inv * z_inv;
+        float D_atan_theta = 1.f / (1 + Y * Y * z_inv2) * angle_res_inv;
+        float Pj[2][3];
+        Pj[0][0] = 0;
+        Pj[0][1] = D_atan_theta * z_inv;
+        Pj[0][2] = -Y * z_inv2 * D_atan_theta;
+        float dist_inv2 = o.dist_inv * o.dist_inv;
+        float x_dist_inv2 = X * dist_inv2;
+        float D_asin = 1.f / std::sqrt(1 - X * x_dist_inv2) * angle_res_inv;
+        Pj[1][0] = -D_asin * o.dist_inv * (1 - X * x_dist_inv2);
+        Pj[1][1] = D_asin * (x_dist_inv2 * Y * o.dist_inv);
+        Pj[1][2] = D_asin * (x_dist_inv2 * Z * o.dist_inv);
+        float Jw[2][6];
+        for (int r = 0; r < 2; ++r)
+            for (int c = 0; c < 6; ++c) Jw[r][c] = Pj[r][0] * T[0][c] + Pj[r][1] * T[1][c] + Pj[r][2] * T[2][c];
+        float Jp[6] = {0}, Jd[6] = {0}, wEP = 0, wED = 0;
+        if (method == ORC_PHOTO || method == ORC_PHOTO_DEPTH) {
+            float gx = L->gx[ii], gy = L->gy[ii];
+            if (std::fabs(gx) < p->thres_sal_int && std::fabs(gy) < p->thres_sal_int) continue;
+            float photoDiff = L->gray_trg[ii] - L->gray_src[i];
+            float weight_photo = orc_huber(photoDiff, p->std_dev_photo) * stdDevPhoto_inv;
+            wEP = weight_photo * photoDiff;
+            const float wgx = weight_photo * gx, wgy = weight_photo * gy;
+            for (int c = 0; c < 6; ++c) Jp[c] = wgx * Jw[0][c] + wgy * Jw[1][c];
+        }
+        if (method == ORC_DEPTH || method == ORC_PHOTO_DEPTH) {
+            if (std::isfinite(depth2)) {
+                float dgx = L->dgx[ii], dgy = L->dgy[ii];
+                if (std::fabs(dgx) < p->thres_sal_depth && std::fabs(dgy) < p->thres_sal_depth) continue;
+                float sd = p->std_dev_depth * depth2;
+                float weight_depth = orc_huber(depthDiff, sd) / sd;
+                wED = weight_depth * depthDiff;
+                float js0 = X * o.dist_inv, js1 = Y * o.dist_inv, js2 = Z * o.dist_inv;
+                for (int c = 0; c < 6; ++c) {
+                    float ga = dgx * Jw[0][c] + dgy * Jw[1][c];
+                    float gb = js0 * T[0][c] + js1 * T[1][c] + js2 * T[2][c];
+                    Jd[c] = weight_depth * (ga - gb);
+                }
+            }
+        }
+        if (method == ORC_PHOTO || method == ORC_PHOTO_DEPTH) {
+            for (int c = 0; c < 6; ++c) JP[6 * ii + c] = Jp[c];
+            rP[ii] = wEP;
+            vP[ii] = 1;
+        }
+        if ((method == ORC_DEPTH || method == ORC_PHOTO_DEPTH) && std::isfinite(depth2)) {
+            for (int c = 0; c < 6; ++c) JD[6 * ii + c] = Jd[c];
+            rD[ii] = wED;
+            vD[ii] = 1;
+        }
+    }
+    double acc[27] = {0};
+    for (int pass = 0; pass < 2; ++pass) {
+        const std::vector<float>& J = pass ? JD : JP;
+        const std::vector<float>& rr = pass ? rD : rP;
+        const std::vector<char>& v = pass ? vD : vP;
+        for (long i = 0; i < N; ++i) {
+            if (!v[i]) continue;
+            const float* j = &J[6 * i];
+            int k = 0;
+            for (int u = 0; u < 6; ++u)
+                for (int w = u; w < 6; ++w) acc[k++] += (double)(j[u] * j[w]);
+            for (int u = 0; u < 6; ++u) acc[21 + u] += (double)(j[u] * rr[i]);
+        }
+    }
+    int k = 0;
+    for (int u = 0; u < 6; ++u)
+        for (int w = u; w < 6; ++w) { H[u * 6 + w] = H[w * 6 + u] = acc[k++]; }
+    for (int u = 0; u < 6; ++u) g[u] = acc[21 + u];
+    *n_visible = (int)nvis;
+}
+
+static double error_any(const orc_level* L, const Lut& lut, const float pose[16], int method, int occ,
+                        const orc_icp_params* p, int* nv) {
+    if (occ == 1) return error_sphere_occ1(L, lut, pose, method, p, nv);
+    if (occ == 2) return error_sphere_occ2(L, lut, pose, method, p, nv);
+    return error_sphere_lut(L, lut, pose, method, p, nv, nullptr);
+}
+
+static void hessgrad_any(const orc_level* L, const Lut& lut, const float pose[16], int method, int occ,
+                         const orc_icp_params* p, double H[36], double g[6], int* nvis) {
+    if (occ == 2) hessgrad_sphere_occ2(L, lut, pose, method, p, H, g, nvis);
+    else hessgrad_sphere_lut(L, lut, pose, method, p, H, g, nvis);
+}
+
+extern "C" double orc_error_sphere_occ(const orc_level* L, const float pose[16], int method, int occ,
+                                       const orc_icp_params* p, int* n_valid) {
+    Lut lut; build_lut(L, p->min_depth, p->max_depth, lut);
+    return error_any(L, lut, pose, method, occ, p, n_valid);
+}
+
+extern "C" void orc_hessgrad_sphere_occ(const orc_level* L, const float pose[16], int method, int occ,
+                                        const orc_icp_params* p, double H[36], double g[6], int* n_visible) {
+    Lut lut; build_lut(L, p->min_depth, p->max_depth, lut);
+    hessgrad_any(L, lut, pose, method, occ, p, H, g, n_visible);
+}
+
 extern "C" double orc_error_sphere(const orc_level* L, const float pose[16], int method,
                                    const orc_icp_params* p, int* n_valid, double* err2) {
     Lut lut; build_lut(L, p->min_depth, p->max_depth, lut);
@@ -417,11 +646,11 @@ static bool solve6(const double H_in[36], const double g[6], double x[6]) {
 // ---------------------------------------------------------------------------
 // A15 — alignFrames360 (:4519-4784) preceded by setTargetFrame / setSourceFrame (:480-516)
 // ---------------------------------------------------------------------------
-extern "C" int orc_align360(const uint8_t* trg_bgr, const uint16_t* trg_depth,
-                            const uint8_t* src_bgr, const uint16_t* src_depth,
-                            int rows, int cols, const float init[16], int method,
-                            const orc_icp_params* p, float pose_out[16], float H_out[36],
-                            float g_out[6], orc_icp_stats* st) {
+extern "C" int orc_align360_occ(const uint8_t* trg_bgr, const uint16_t* trg_depth,
+                                const uint8_t* src_bgr, const uint16_t* src_depth,
+                                int rows, int cols, const float init[16], int method, int occlusion,
+                                const orc_icp_params* p, float pose_out[16], float H_out[36],
+                                float g_out[6], orc_icp_stats* st) {
     const int nL = p->n_pyr;
     std::vector<int> R(nL), C(nL);
     std::vector<std::vector<float>> gs(nL), ds(nL), gt(nL), dt(nL), gx(nL), gy(nL), dgx(nL), dgy(nL);
@@ -467,7 +696,7 @@ extern "C" int orc_align360(const uint8_t* trg_bgr, const uint16_t* trg_depth,
         int it = 0, nv = 0, evals = 0;
         const int maxIters = fixed ? p->fixed_iters_level0 : p->max_iters;
         float upd[6] = {1, 1, 1, 1, 1, 1};
-        double error = error_sphere_lut(&L, lut, pose, method, p, &nv, nullptr);
+        double error = error_any(&L, lut, pose, method, occlusion, p, &nv);
         double diff_error = error;
         int loops = 0;
         auto norm6 = [](const float* u) { float s = 0; for (int k = 0; k < 6; ++k) s += u[k] * u[k]; return std::sqrt(s); };
@@ -475,7 +704,7 @@ extern "C" int orc_align360(const uint8_t* trg_bgr, const uint16_t* trg_depth,
                      : (it < maxIters && norm6(upd) > p->tol_update && diff_error > p->tol_residual)) {
             ++loops;
             double H[36], g[6]; int nvis = 0;
-            hessgrad_sphere_lut(&L, lut, pose, method, p, H, g, &nvis);
+            hessgrad_any(&L, lut, pose, method, occlusion, p, H, g, &nvis);
             for (int k = 0; k < 36; ++k) Hf[k] = (float)H[k];
             for (int k = 0; k < 6; ++k) gf[k] = (float)g[k];
             if (st) st->sso = (float)nvis / (nRows * nCols);
@@ -497,7 +726,7 @@ extern "C" int orc_align360(const uint8_t* trg_bgr, const uint16_t* trg_depth,
             float E[16], cand[16];
             orc_exp_se3(ud, 1, E);                                        // :4697
             matmul4f(E, pose, cand);
-            double new_error = error_sphere_lut(&L, lut, cand, method, p, &nv, nullptr);
+            double new_error = error_any(&L, lut, cand, method, occlusion, p, &nv);
             ++evals;
             diff_error = error - new_error;                               // :4711
             if (diff_error > p->tol_residual) {                           // :4715-4722
@@ -513,6 +742,15 @@ done:
     if (H_out) memcpy(H_out, Hf, sizeof(Hf));
     if (g_out) memcpy(g_out, gf, sizeof(gf));
     return ret;
+}
+
+extern "C" int orc_align360(const uint8_t* trg_bgr, const uint16_t* trg_depth,
+                            const uint8_t* src_bgr, const uint16_t* src_depth,
+                            int rows, int cols, const float init[16], int method,
+                            const orc_icp_params* p, float pose_out[16], float H_out[36],
+                            float g_out[6], orc_icp_stats* st) {
+    return orc_align360_occ(trg_bgr, trg_depth, src_bgr, src_depth, rows, cols, init, method, 0, p, pose_out,
+                            H_out, g_out, st);
 }
 
 // glibc float asinf / atan2f as the reference calls them (std::asin(float), std::atan2(float, float))

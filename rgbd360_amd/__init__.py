@@ -113,6 +113,8 @@ _SIGS = [
     ("r360_align360_result", C.c_int, [_P, _FP, _FP, _FP, C.POINTER(IcpStats)]),
     ("r360_icp_eval", C.c_int, [_P, _P, _P, C.c_int, _FP, C.c_int, C.POINTER(IcpParams), _DP, _DP, _DP, _IP,
                                 _IP]),
+    ("r360_icp_eval_occ", C.c_int, [_P, _P, _P, C.c_int, _FP, C.c_int, C.c_int, C.POINTER(IcpParams), _DP, _DP,
+                                    _DP, _IP, _IP]),
     ("r360_exp_se3", None, [_DP, C.c_int, _FP]),
     ("r360_frame_get_planes", C.c_int, [_P, C.POINTER(Plane), C.c_int, _IP]),
     ("r360_frame_get_plane_hull", C.c_int, [_P, C.c_int, _FP, C.c_int, _IP]),
@@ -510,6 +512,17 @@ class RegisterPhotoICP:
                                    C.byref(self.params), H.ctypes.data_as(_DP), g.ctypes.data_as(_DP),
                                    C.byref(e2), C.byref(nv), C.byref(nvis)), "icp_eval")
         return H.reshape(6, 6), g, e2.value, nv.value, nvis.value
+
+    def eval_occ(self, level: int, pose, method: int = PHOTO_DEPTH, occlusion: int = 1):
+        """One occlusion-aware pass at a fixed pose: H, g of calcHessGrad_sphereOcc{occlusion}, the value
+        of errorPhotoICP_sphereOcc{occlusion}, its point count and numVisiblePixels."""
+        p = _mat16(pose)
+        H, g = np.zeros(36), np.zeros(6)
+        e, nv, nvis = C.c_double(), C.c_int(), C.c_int()
+        _check(lib().r360_icp_eval_occ(self.ctx.h, self.trg.h, self.src.h, level, _fptr(p), method, occlusion,
+                                       C.byref(self.params), H.ctypes.data_as(_DP), g.ctypes.data_as(_DP),
+                                       C.byref(e), C.byref(nv), C.byref(nvis)), "icp_eval_occ")
+        return H.reshape(6, 6), g, e.value, nv.value, nvis.value
 
 
 def libm_eval(x, y, z, on_device: bool = False):

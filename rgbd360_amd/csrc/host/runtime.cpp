@@ -521,7 +521,7 @@ extern "C" void r360_icp_default_params(r360_icp_params* p) {
     p->fixed_iters_level0 = 0;
 }
 
-static IcpConst make_const(const r360_icp_params* p, int level, int n_pixels) {
+static IcpConst make_const(const r360_icp_params* p, int level, int n_pixels, int occ = 0) {
     IcpConst C;
     memset(&C, 0, sizeof(C));
     C.min_d = p->min_depth; C.max_d = p->max_depth;
@@ -531,7 +531,7 @@ static IcpConst make_const(const r360_icp_params* p, int level, int n_pixels) {
     C.sd_photo_inv_d = 1. / p->std_dev_photo;
     C.tol_res = p->tol_residual; C.tol_upd = p->tol_update; C.lambda = p->lambda;
     C.max_iters = p->max_iters; C.fixed_iters0 = p->fixed_iters_level0;
-    C.n_pixels = n_pixels; C.level = level;
+    C.n_pixels = n_pixels; C.level = level; C.occ = occ;
     return C;
 }
 
@@ -552,7 +552,7 @@ extern "C" int r360_align360_async(r360_ctx* ctx, r360_frame* trg, r360_frame* s
     if (int rc = check_pair(ctx, trg, src, p)) return rc;
     CHECK_ARG(init, "null init pose");
     CHECK_ARG(method >= 0 && method <= 2, "invalid method");
-    CHECK_ARG(occlusion == 0, "occlusion variants (Occ1/Occ2) are not built in this version");
+    CHECK_ARG(occlusion >= 0 && occlusion <= 2, "occlusion must be 0, 1 or 2");
     IcpState* h = ctx->h_state;
     memset(h, 0, sizeof(IcpState));
     memcpy(h->pose, init, sizeof(float) * 16);
@@ -561,7 +561,7 @@ extern "C" int r360_align360_async(r360_ctx* ctx, r360_frame* trg, r360_frame* s
     R360_HIP(hipMemcpyAsync(ctx->d_state, h, sizeof(IcpState), hipMemcpyHostToDevice, ctx->stream));
     for (int l = p->n_pyr - 1; l >= 0; --l) {
         const int np = src->lv[l].rows * src->lv[l].cols;
-        const IcpConst C = make_const(p, l, np);
+        const IcpConst C = make_const(p, l, np, occlusion);
         const int passes = 1 + ((l == 0 && p->fixed_iters_level0 > 0) ? p->fixed_iters_level0 : p->max_iters);
         for (int k = 0; k < passes; ++k)
             if (launch_icp_level(ctx, trg, src, l, method, C, k == 0, 0)) return -1;
@@ -599,29 +599,58 @@ extern "C" int r360_align360(r360_ctx* ctx, r360_frame* trg, r360_frame* src, co
     return r360_align360_result(ctx, pose_out, H_out, g_out, st);
 }
 
-extern "C" int r360_icp_eval(r360_ctx* ctx, r360_frame* trg, r360_frame* src, int level, const float pose[16],
-                             int method, const r360_icp_params* p, double H[36], double g[6], double* err2,
-                             int* n_valid, int* n_visible) {
+// one eval-mode pass (no GN step): the raw pass sums at `pose`
+static int icp_eval_sums(r360_ctx* ctx, r360_frame* trg, r360_frame* src, int level, const float pose[16], int method,
+                         int occ, const r360_icp_params* p, double sums[R360_NSUMS]) {
     if (int rc = check_pair(ctx, trg, src, p)) return rc;
     CHECK_ARG(level >= 0 && level < src->n_levels, "level out of range");
     CHECK_ARG(method >= 0 && method <= 2, "invalid method");
+    CHECK_ARG(occ >= 0 && occ <= 2, "occlusion must be 0, 1 or 2");
     IcpState* h = ctx->h_state;
     memset(h, 0, sizeof(IcpState));
     memcpy(h->cand, pose, sizeof(float) * 16);
     memcpy(h->pose, pose, sizeof(float) * 16);
     h->dbg[8] = ~0ull;
     R360_HIP(hipMemcpyAsync(ctx->d_state, h, sizeof(IcpState), hipMemcpyHostToDevice, ctx->stream));
-    const IcpConst C = make_const(p, level, src->lv[level].rows * src->lv[level].cols);
+    const IcpConst C = make_const(p, level, src->lv[level].rows * src->lv[level].cols, occ);
     if (launch_icp_level(ctx, trg, src, level, method, C, 0, 1)) return -1;
     R360_HIP(hipMemcpyAsync(h, ctx->d_state, sizeof(IcpState), hipMemcpyDeviceToHost, ctx->stream));
-    R360_HIP(hipStreamSynchronize(ctx->stream));
-    const double* s = h->sums;
+    if (ctx_wait(ctx)) return -1;
+    memcpy(sums, h->sums, sizeof(double) * R360_NSUMS);
+    return 0;
+}
+
+static void sums_hg(const double* s, double H[36], double g[6]) {
     int k = 0;
     for (int u = 0; u < 6; ++u)
         for (int v = u; v < 6; ++v) { H[u * 6 + v] = H[v * 6 + u] = s[k++]; }
     for (int u = 0; u < 6; ++u) g[u] = s[21 + u];
+}
+
+extern "C" int r360_icp_eval(r360_ctx* ctx, r360_frame* trg, r360_frame* src, int level, const float pose[16],
+                             int method, const r360_icp_params* p, double H[36], double g[6], double* err2,
+                             int* n_valid, int* n_visible) {
+    double s[R360_NSUMS];
+    if (int rc = icp_eval_sums(ctx, trg, src, level, pose, method, 0, p, s)) return rc;
+    sums_hg(s, H, g);
     if (err2) *err2 = s[R360_SUM_ERR2];
     if (n_valid) *n_valid = (int)s[R360_SUM_NVALID];
+    if (n_visible) *n_visible = (int)s[R360_SUM_NVIS];
+    return 0;
+}
+
+extern "C" int r360_icp_eval_occ(r360_ctx* ctx, r360_frame* trg, r360_frame* src, int level, const float pose[16],
+                                 int method, int occlusion, const r360_icp_params* p, double H[36], double g[6],
+                                 double* error, int* n_valid, int* n_visible) {
+    double s[R360_NSUMS];
+    if (int rc = icp_eval_sums(ctx, trg, src, level, pose, method, occlusion, p, s)) return rc;
+    sums_hg(s, H, g);
+    const double e2 = s[R360_SUM_ERR2], nv = s[R360_SUM_NVALID];
+    if (error)
+        *error = occlusion == 0 ? std::sqrt(e2 / nv)
+               : occlusion == 1 ? std::sqrt(e2 / nv) + std::sqrt(s[R360_SUM_ERR2D] / s[R360_SUM_NDEPTH])
+                                : std::sqrt(e2 / nv) + std::sqrt(s[R360_SUM_ERR2D] / nv);
+    if (n_valid) *n_valid = (int)(nv + (occlusion == 1 ? s[R360_SUM_NDEPTH] : 0.0));
     if (n_visible) *n_visible = (int)s[R360_SUM_NVIS];
     return 0;
 }

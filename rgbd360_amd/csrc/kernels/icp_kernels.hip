@@ -60,8 +60,14 @@ __device__ __forceinline__ float huberf(float e, float reg) {  // weightHuber<fl
 // Accumulator slots: 0..20 upper-triangle H (row-major), 21..26 g, 27 n_valid, 28 n_visible.
 struct Acc {
     float h[32];
-    double err2;
+    double err2;    // squared weighted residuals (occlusion variants: photometric only)
+    double err2d;   // occlusion variants: depth squared weighted residuals
 };
+
+// occlusion flags per source pixel (k_occ_resolve): bit 0 accepted by the target Z-buffer (a prefix
+// maximum of 1/|p'| in LUT order), bit 1 the last accepted point of its target pixel, bit 2 the last
+// point (after the Occ2 depth-outlier filter) of its target pixel
+enum { OCC_ACC = 1, OCC_OWN = 2, OCC_WIN = 4 };
 
 // ---------------------------------------------------------------- per-pixel pipeline
 // Exact part: LUT point, transform and spherical projection, bit-identical to the reference
@@ -155,18 +161,18 @@ __device__ __forceinline__ void acc_fma(Acc& A, const float J[6], float r) {
 // Residuals, weights and Jacobian rows of one projected pixel, accumulated branch-free: a pixel that
 // the reference skips contributes through selects that zero its row (never a multiply by 0, which
 // would let a NaN of an invalid pixel through).
-template <int METHOD>
-__device__ __forceinline__ void contribute(Acc& A, const Proj& o, const float4 G, const float2 T, float angle_res_inv,
-                                           const IcpConst& C) {
+template <int METHOD, int OCC>
+__device__ __forceinline__ void contribute(Acc& A, const Proj& o, const float4 G, const float2 T, int fl,
+                                           float angle_res_inv, const IcpConst& C) {
     constexpr bool photo = (METHOD == R360_PHOTO_CONSISTENCY || METHOD == R360_PHOTO_DEPTH);
     constexpr bool depth = (METHOD == R360_DEPTH_CONSISTENCY || METHOD == R360_PHOTO_DEPTH);
     const float X = o.X, Y = o.Y, Z = o.Z, dist = o.dist, dist_inv = o.dist_inv;
-    A.h[28] += o.vis ? 1.f : 0.f;                                               // numVisiblePixels
     // photo saliency fails -> 'continue' skips the depth term too (:3038-3039)
     const bool sal_p = !(fabsf(G.x) < C.thr_int && fabsf(G.y) < C.thr_int);
+    const bool sal_d = !(fabsf(G.z) < C.thr_depth && fabsf(G.w) < C.thr_depth);
+    const bool fin_d = isfinite(T.y);
     const bool p_ok = photo && o.vis && sal_p;
-    const bool d_ok = depth && o.vis && (!photo || sal_p) && isfinite(T.y) &&
-                      !(fabsf(G.z) < C.thr_depth && fabsf(G.w) < C.thr_depth);  // (:3064-3073)
+    const bool d_ok = depth && o.vis && (!photo || sal_p) && fin_d && sal_d;   // (:3064-3073)
     // exact error terms (they steer the accept/reject test :4715)
     const float photoDiff = T.x - o.gray_s;
     const float whp = huberf(photoDiff, C.sd_photo);
@@ -175,8 +181,34 @@ __device__ __forceinline__ void contribute(Acc& A, const Proj& o, const float4 G
     const float sd = C.sd_depth * T.y;
     const float wd = huberf(depthDiff, sd) / sd;                                        // (:3077-3078)
     const float wEdep = (float)((double)wd * depthDiff);
-    if (photo) { A.err2 += p_ok ? (double)(wEd * wEd) : 0.0; A.h[27] += p_ok ? 1.f : 0.f; }
-    if (depth) { A.err2 += d_ok ? (double)(wEdep * wEdep) : 0.0; A.h[27] += d_ok ? 1.f : 0.f; }
+    // which terms enter the error and which Jacobian rows enter H / g
+    bool jp = p_ok, jd = d_ok;
+    if (OCC == 0) {
+        A.h[28] += o.vis ? 1.f : 0.f;                                               // numVisiblePixels
+        if (photo) { A.err2 += p_ok ? (double)(wEd * wEd) : 0.0; A.h[27] += p_ok ? 1.f : 0.f; }
+        if (depth) { A.err2 += d_ok ? (double)(wEdep * wEdep) : 0.0; A.h[27] += d_ok ? 1.f : 0.f; }
+    } else if (OCC == 1) {
+        // errorPhotoICP_sphereOcc1 (:3232-3370): accepted points count, the last accepted one of a
+        // target pixel owns its residual; H / g as calcHessGrad_sphere (its Z-buffer never occludes)
+        const bool acc = fl & OCC_ACC, own = fl & OCC_OWN;
+        A.h[28] += o.vis ? 1.f : 0.f;
+        if (photo) { A.err2 += (own && p_ok) ? (double)(wEd * wEd) : 0.0; A.h[27] += (acc && p_ok) ? 1.f : 0.f; }
+        if (depth) {
+            A.err2d += (own && d_ok) ? (double)(wEdep * wEdep) : 0.0;
+            A.h[29] += (acc && d_ok) ? 1.f : 0.f;
+        }
+    } else {
+        // errorPhotoICP_sphereOcc2 (:3720-3855): every accepted point counts and contributes;
+        // calcHessGrad_sphereOcc2 (:3861-4250): the last filtered point of a target pixel owns its rows,
+        // and a failed depth-saliency test skips the store of both rows
+        const bool acc = fl & OCC_ACC, win = fl & OCC_WIN;
+        A.h[27] += acc ? 1.f : 0.f;
+        if (photo) A.err2 += (acc && p_ok) ? (double)(wEd * wEd) : 0.0;
+        if (depth) A.err2d += (acc && d_ok) ? (double)(wEdep * wEdep) : 0.0;
+        A.h[28] += win ? 1.f : 0.f;
+        jp = win && p_ok && !(depth && fin_d && !sal_d);
+        jd = win && d_ok;
+    }
     // Jacobian of the spherical warp (:2995-3026), expanded with T36 = [I | -skew(p')]
     float Jw0[6], Jw1[6];
     {
@@ -201,8 +233,8 @@ __device__ __forceinline__ void contribute(Acc& A, const Proj& o, const float4 G
         const float wgx = w * G.x, wgy = w * G.y;
         float J[6];
 #pragma unroll
-        for (int k = 0; k < 6; ++k) J[k] = p_ok ? wgx * Jw0[k] + wgy * Jw1[k] : 0.f;
-        acc_fma(A, J, p_ok ? w * photoDiff : 0.f);
+        for (int k = 0; k < 6; ++k) J[k] = jp ? wgx * Jw0[k] + wgy * Jw1[k] : 0.f;
+        acc_fma(A, J, jp ? w * photoDiff : 0.f);
     }
     if (depth) {
 #pragma clang fp contract(fast)
@@ -216,8 +248,8 @@ __device__ __forceinline__ void contribute(Acc& A, const Proj& o, const float4 G
         J[4] = G.z * Jw0[4] + G.w * Jw1[4];
         J[5] = G.z * Jw0[5] + G.w * Jw1[5];
 #pragma unroll
-        for (int k = 0; k < 6; ++k) J[k] = d_ok ? wd * J[k] : 0.f;
-        acc_fma(A, J, d_ok ? wd * depthDiff : 0.f);
+        for (int k = 0; k < 6; ++k) J[k] = jd ? wd * J[k] : 0.f;
+        acc_fma(A, J, jd ? wd * depthDiff : 0.f);
     }
 }
 
@@ -262,15 +294,16 @@ __device__ __forceinline__ double wave_sum_d(double x) {
 
 // TOP = 1 only renames the level-0 instantiation, so traces (rocprofv3) separate level 0 from level 1,
 // which launch the same grid.
-template <int METHOD, int PF, int TOP>
+template <int METHOD, int PF, int TOP, int OCC>
 __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const float2* __restrict__ src, const float2* __restrict__ trg,
                                                  const float4* __restrict__ tg, const float* __restrict__ sinphi,
                                                  const float* __restrict__ cosphi, const float* __restrict__ sinth,
                                                  const float* __restrict__ costh, int nRows, int nCols,
                                                  IcpConst C, IcpState* S, double* __restrict__ partials, int first,
-                                                 int eval_only, unsigned long long* __restrict__ kt) {
+                                                 int eval_only, unsigned long long* __restrict__ kt,
+                                                 const uint8_t* __restrict__ occf) {
     __shared__ float s_red[NW][32];
-    __shared__ double s_err[NW];
+    __shared__ double s_err[NW], s_errd[NW];
     __shared__ double s_fin[RG][32];
     __shared__ int s_last;
     __shared__ GnShared s_gn;
@@ -301,21 +334,23 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const float2* _
 #pragma unroll
     for (int k = 0; k < 32; ++k) A.h[k] = 0.f;
     A.err2 = 0.0;
+    A.err2d = 0.0;
+    auto flag = [&](int i) { return OCC ? (int)occf[i] : 0; };
 
     const int units = (nRows * nCols) >> 2;  // 4 pixels of one row per unit (nCols % 4 == 0)
     const float4* src4 = reinterpret_cast<const float4*>(src);
     const float4* st4 = reinterpret_cast<const float4*>(sinth);
     const float4* ct4 = reinterpret_cast<const float4*>(costh);
     const int cq = nCols >> 2;
-    auto one = [&](float d, float g, float sp, float cp, float st, float ct) {
+    auto one = [&](float d, float g, float sp, float cp, float st, float ct, int fl) {
         Proj o = project(P, d, g, sp, cp, st, ct, nRows, nCols, half_nRows, angle_res_inv, C);
         project_fix(o, nRows, nCols, half_nRows, angle_res_inv);
         const float4 G = tg[o.t];
         const float2 T = trg[o.t];
-        contribute<METHOD>(A, o, G, T, angle_res_inv, C);
+        contribute<METHOD, OCC>(A, o, G, T, fl, angle_res_inv, C);
     };
     auto two = [&](float d0, float g0, float d1, float g1, float sp, float cp, float st0, float ct0, float st1,
-                   float ct1) {
+                   float ct1, int fl0, int fl1) {
         // project both, issue both gathers, then the math (ILP + loads in flight)
         Proj o0 = project(P, d0, g0, sp, cp, st0, ct0, nRows, nCols, half_nRows, angle_res_inv, C);
         Proj o1 = project(P, d1, g1, sp, cp, st1, ct1, nRows, nCols, half_nRows, angle_res_inv, C);
@@ -323,8 +358,8 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const float2* _
         project_fix(o1, nRows, nCols, half_nRows, angle_res_inv);
         const float4 G0 = tg[o0.t], G1 = tg[o1.t];
         const float2 T0 = trg[o0.t], T1 = trg[o1.t];
-        contribute<METHOD>(A, o0, G0, T0, angle_res_inv, C);
-        contribute<METHOD>(A, o1, G1, T1, angle_res_inv, C);
+        contribute<METHOD, OCC>(A, o0, G0, T0, fl0, angle_res_inv, C);
+        contribute<METHOD, OCC>(A, o1, G1, T1, fl1, angle_res_inv, C);
     };
     const int stride = gridDim.x * TPB;
     if (PF == 1) {
@@ -335,8 +370,8 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const float2* _
             const float4 a = src4[2 * u], b = src4[2 * u + 1];  // {g0,d0,g1,d1} {g2,d2,g3,d3}
             const float4 s = st4[c4], c = ct4[c4];
             const float sp = sinphi[r], cp = cosphi[r];
-            two(a.y, a.x, a.w, a.z, sp, cp, s.x, c.x, s.y, c.y);
-            two(b.y, b.x, b.w, b.z, sp, cp, s.z, c.z, s.w, c.w);
+            two(a.y, a.x, a.w, a.z, sp, cp, s.x, c.x, s.y, c.y, flag(4 * u), flag(4 * u + 1));
+            two(b.y, b.x, b.w, b.z, sp, cp, s.z, c.z, s.w, c.w, flag(4 * u + 2), flag(4 * u + 3));
         }
     } else if (PF == 2) {
         // software-pipelined pixel stream, one wave = 64 consecutive pixels of one row (nCols % 64 == 0,
@@ -344,12 +379,12 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const float2* _
         // chunk k is accumulated, chunk k+1's target gathers and chunk k+2's source loads are in flight
         const int npx = nRows * nCols;
         const int lane = threadIdx.x & 63;
-        struct Src { float d, g, sp, cp, st, ct; };
+        struct Src { float d, g, sp, cp, st, ct; int f; };
         auto ld = [&](int base) {                          // base: wave-uniform first pixel
             const int r = __builtin_amdgcn_readfirstlane(base / nCols);
             const int c = base - r * nCols + lane;
             const float2 a = src[base + lane];
-            return Src{a.y, a.x, sinphi[r], cosphi[r], sinth[c], costh[c]};
+            return Src{a.y, a.x, sinphi[r], cosphi[r], sinth[c], costh[c], flag(base + lane)};
         };
         const Gather gt{__builtin_amdgcn_make_buffer_rsrc(const_cast<float4*>(tg), 0, npx * 16, 0x00020000),
                         __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(trg), 0, npx * 8, 0x00020000)};
@@ -372,22 +407,25 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const float2* _
             Src sA = ld(base(0));
             Src sB = ld(base(1));
             Proj oA = prj(sA);
+            int fA = sA.f;
             project_fix(oA, nRows, nCols, half_nRows, angle_res_inv);
             float4 GA = gt.g(oA.t);
             float2 TA = gt.T(oA.t);
             for (int k = 0;; k += 2) {
                 sA = ld(base(k + 2));
                 Proj oB = prj(sB);
+                const int fB = sB.f;
                 float4 GB = gt.g(oB.t);
                 float2 TB = gt.T(oB.t);
-                contribute<METHOD>(A, oA, GA, TA, angle_res_inv, C);
+                contribute<METHOD, OCC>(A, oA, GA, TA, fA, angle_res_inv, C);
                 if (k + 1 >= n_it) break;
                 if (project_fix(oB, nRows, nCols, half_nRows, angle_res_inv)) { GB = gt.g(oB.t); TB = gt.T(oB.t); }
                 sB = ld(base(k + 3));
                 oA = prj(sA);
+                fA = sA.f;
                 GA = gt.g(oA.t);
                 TA = gt.T(oA.t);
-                contribute<METHOD>(A, oB, GB, TB, angle_res_inv, C);
+                contribute<METHOD, OCC>(A, oB, GB, TB, fB, angle_res_inv, C);
                 if (k + 2 >= n_it) break;
                 if (project_fix(oA, nRows, nCols, half_nRows, angle_res_inv)) { GA = gt.g(oA.t); TA = gt.T(oA.t); }
             }
@@ -399,7 +437,7 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const float2* _
             const int r = i / nCols;
             const int c = i - r * nCols;
             const float2 a = src[i];
-            one(a.y, a.x, sinphi[r], cosphi[r], sinth[c], costh[c]);
+            one(a.y, a.x, sinphi[r], cosphi[r], sinth[c], costh[c], flag(i));
         }
     }
 #ifdef R360_STAMPS
@@ -415,13 +453,16 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const float2* _
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const float mine = wave_reduce_scatter32(A.h, lane);
     const double e2 = wave_sum_d(A.err2);
+    const double e2d = OCC ? wave_sum_d(A.err2d) : 0.0;
     if ((lane & 1) == 0) s_red[wid][scatter_slot(lane)] = mine;
-    if (lane == 0) s_err[wid] = e2;
+    if (lane == 0) { s_err[wid] = e2; s_errd[wid] = e2d; }
     __syncthreads();
     if (threadIdx.x < 32) {
         double v;
         if (threadIdx.x == R360_SUM_ERR2) {
             v = 0; for (int w = 0; w < NW; ++w) v += s_err[w];
+        } else if (OCC && threadIdx.x == R360_SUM_ERR2D) {
+            v = 0; for (int w = 0; w < NW; ++w) v += s_errd[w];
         } else {
             v = 0; for (int w = 0; w < NW; ++w) v += (double)s_red[w][threadIdx.x];
         }
@@ -530,6 +571,179 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const float2* _
             kt[9 + lv] += 1;
             __hip_atomic_store(kt, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+    }
+}
+
+// ---------------------------------------------------------------- occlusion variants (§8(f)1)
+// Per pass, before the fused pass and at the same pose:
+//   k_occ_project  per source pixel: target pixel (the fused pass's exact decision), 1/|p'| with the
+//                  reference's IEEE division, the Occ2 depth-outlier filter; counts per target pixel
+//   k_occ_scan*    exclusive scan of the counts (per-target list offsets)
+//   k_occ_scatter  source indices grouped by target pixel (counts return to zero)
+//   k_occ_resolve  per target pixel, in LUT (source index) order: the Z-buffer's accepted points
+//                  (prefix maxima of 1/|p'|), the last accepted one, and the last point
+constexpr int OCC_SCAN_TPB = 1024, OCC_SCAN_V = 4, OCC_SCAN_ITEMS = OCC_SCAN_TPB * OCC_SCAN_V;
+
+__device__ __forceinline__ bool pass_skipped(const IcpState* S, int first, int eval_only) {
+    return S->stop || (!first && !S->active && !eval_only);
+}
+
+__device__ __forceinline__ Pose12 pass_pose(const IcpState* S, int first, int eval_only) {
+    const float* pm = (first && !eval_only) ? S->pose : S->cand;
+    Pose12 P;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) P.R[r * 3 + c] = pm[c * 4 + r];
+        P.t[r] = pm[12 + r];
+    }
+    return P;
+}
+
+template <int OCC>
+__global__ void __launch_bounds__(256) k_occ_project(const float2* __restrict__ src, const float2* __restrict__ trg,
+                                                    const float* __restrict__ sinphi, const float* __restrict__ cosphi,
+                                                    const float* __restrict__ sinth, const float* __restrict__ costh,
+                                                    int nRows, int nCols, IcpConst C, const IcpState* S, int first,
+                                                    int eval_only, int* __restrict__ tgt, float* __restrict__ dinv,
+                                                    uint8_t* __restrict__ flags, int* __restrict__ cnt) {
+    if (pass_skipped(S, first, eval_only)) return;
+    const Pose12 P = pass_pose(S, first, eval_only);
+    const float angle_res = (float)(2 * R360_PI / nCols);
+    const float angle_res_inv = 1 / angle_res;
+    const float half_nRows = (float)(0.5 * nRows - 0.5);
+    const int npx = nRows * nCols;
+    const int stride = gridDim.x * blockDim.x;
+    // wave-uniform trip count (project_fix votes across the wave)
+    for (int i0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63); i0 < npx; i0 += stride) {
+        const int i = min(i0 + (int)(threadIdx.x & 63), npx - 1);
+        const bool own = i0 + (int)(threadIdx.x & 63) < npx;
+        const int r = i / nCols, c = i - (i / nCols) * nCols;
+        const float2 a = src[i];
+        Proj o = project(P, a.y, a.x, sinphi[r], cosphi[r], sinth[c], costh[c], nRows, nCols, half_nRows,
+                         angle_res_inv, C);
+        project_fix(o, nRows, nCols, half_nRows, angle_res_inv);
+        if (!own) continue;
+        int t = -1;
+        float di = 0.f;
+        if (o.vis) {
+            di = 1.f / o.dist;                                  // the reference's dist_inv (IEEE)
+            bool keep = true;
+            if (OCC == 2) keep = !(fabsf(trg[o.t].y - o.dist) > 0.3f);   // thresDepthOutliers (:4525, :3790)
+            if (keep) {
+                t = o.t;
+                atomicAdd(cnt + t, 1);
+            }
+        }
+        tgt[i] = t;
+        dinv[i] = di;
+        flags[i] = 0;
+    }
+}
+
+// exclusive scan of cnt[0..n) into off[0..n] in three steps (workgroup scans, scan of the workgroup
+// totals, add); off[n] = total
+__device__ int occ_block_exscan(int v, int* sh, int& total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    int x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    __syncthreads();
+    if (lane == 63) sh[wid] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int acc = 0;
+        for (int k = 0; k < nw; ++k) { const int t = sh[k]; sh[k] = acc; acc += t; }
+        sh[nw] = acc;
+    }
+    __syncthreads();
+    total = sh[nw];
+    return sh[wid] + x - v;
+}
+
+__global__ void __launch_bounds__(OCC_SCAN_TPB) k_occ_scan1(const int* __restrict__ cnt, int n, int* __restrict__ off,
+                                                          int* __restrict__ bsum, const IcpState* S, int first,
+                                                          int eval_only) {
+    __shared__ int sh[17];
+    if (pass_skipped(S, first, eval_only)) return;
+    const int j = blockIdx.x * OCC_SCAN_ITEMS + threadIdx.x * OCC_SCAN_V;
+    int v[OCC_SCAN_V], t = 0;
+#pragma unroll
+    for (int k = 0; k < OCC_SCAN_V; ++k) { v[k] = j + k < n ? cnt[j + k] : 0; t += v[k]; }
+    int tot;
+    int e = occ_block_exscan(t, sh, tot);
+#pragma unroll
+    for (int k = 0; k < OCC_SCAN_V; ++k)
+        if (j + k < n) { off[j + k] = e; e += v[k]; }
+    if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(OCC_SCAN_TPB) k_occ_scan2(int* __restrict__ bsum, int nb, int* __restrict__ off,
+                                                          int n, const IcpState* S, int first, int eval_only) {
+    __shared__ int sh[17];
+    if (pass_skipped(S, first, eval_only)) return;
+    int acc = 0;
+    for (int b0 = 0; b0 < nb; b0 += OCC_SCAN_TPB) {
+        const int b = b0 + threadIdx.x;
+        const int v = b < nb ? bsum[b] : 0;
+        int tot;
+        const int e = occ_block_exscan(v, sh, tot);
+        if (b < nb) bsum[b] = acc + e;
+        acc += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) off[n] = acc;
+}
+
+__global__ void __launch_bounds__(OCC_SCAN_TPB) k_occ_scan3(const int* __restrict__ bsum, int n, int* __restrict__ off,
+                                                          const IcpState* S, int first, int eval_only) {
+    if (pass_skipped(S, first, eval_only)) return;
+    const int j = blockIdx.x * OCC_SCAN_ITEMS + threadIdx.x * OCC_SCAN_V;
+    const int add = bsum[blockIdx.x];
+#pragma unroll
+    for (int k = 0; k < OCC_SCAN_V; ++k)
+        if (j + k < n) off[j + k] += add;
+}
+
+__global__ void k_occ_scatter(const int* __restrict__ tgt, int n, const int* __restrict__ off, int* __restrict__ cnt,
+                              int* __restrict__ list, const IcpState* S, int first, int eval_only) {
+    if (pass_skipped(S, first, eval_only)) return;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int t = tgt[i];
+        if (t < 0) continue;
+        const int pos = atomicSub(cnt + t, 1) - 1;
+        list[off[t] + pos] = i;
+    }
+}
+
+__global__ void k_occ_resolve(const int* __restrict__ off, int n, const int* __restrict__ list,
+                              const float* __restrict__ dinv, uint8_t* __restrict__ flags, const IcpState* S,
+                              int first, int eval_only) {
+    if (pass_skipped(S, first, eval_only)) return;
+    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
+        const int b = off[t], m = off[t + 1] - b;
+        if (m == 0) continue;
+        if (m == 1) { flags[list[b]] = OCC_ACC | OCC_OWN | OCC_WIN; continue; }
+        // m points hit this target pixel: walk them in source-index order.  invDepthBuffer starts at 0
+        // and keeps the last accepted 1/|p'|, so a point is accepted iff 1/|p'| >= every earlier one
+        int prev = -1, last_acc = -1;
+        float zmax = 0.f;
+        for (int k = 0; k < m; ++k) {
+            int nxt = 0x7fffffff;                           // smallest source index above prev
+            for (int q = 0; q < m; ++q) {
+                const int i = list[b + q];
+                if (i > prev && i < nxt) nxt = i;
+            }
+            prev = nxt;
+            const float d = dinv[nxt];
+            const bool acc = !(zmax > 0.f && d < zmax);
+            if (acc) { zmax = d; last_acc = nxt; }
+            flags[nxt] = acc ? OCC_ACC : 0;
+        }
+        flags[last_acc] |= OCC_OWN;
+        flags[prev] |= OCC_WIN;                             // prev = largest source index
     }
 }
 
@@ -662,10 +876,12 @@ static int env_int(const char* name, int dflt) {
 template <int M, int PF>
 static void launch_pass(r360_ctx* ctx, int nb, const LevelBufs& Ls, const LevelBufs& Lt, const LevelTrig& T,
                         const IcpConst& C, int first, int eval_only, bool top) {
-    auto kern = top ? k_icp_pass<M, PF, 1> : k_icp_pass<M, PF, 0>;
+    auto kern = C.occ == 1 ? k_icp_pass<M, PF, 0, 1>
+              : C.occ == 2 ? k_icp_pass<M, PF, 0, 2>
+              : top        ? k_icp_pass<M, PF, 1, 0> : k_icp_pass<M, PF, 0, 0>;
     hipLaunchKernelGGL(kern, dim3(nb), dim3(TPB), 0, ctx->stream, Ls.p0, Lt.p0, Lt.tg, T.sinphi,
                        T.cosphi, T.sinth, T.costh, Ls.rows, Ls.cols, C, ctx->d_state, ctx->d_partials, first,
-                       eval_only, ctx->d_ktime);
+                       eval_only, ctx->d_ktime, ctx->occ_flags);
 }
 
 int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src, int level, int method,
@@ -684,9 +900,9 @@ int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src
         int dev = 0;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&o.cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[0], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 0, 0>, TPB, 0);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[1], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 1, 0>, TPB, 0);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[2], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 2, 0>, TPB, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[0], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 0, 0, 0>, TPB, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[1], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 1, 0, 0>, TPB, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[2], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 2, 0, 0>, TPB, 0);
         return o;
     }();
     const int npx = Ls.rows * Ls.cols;
@@ -695,6 +911,46 @@ int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src
     if (cap > ctx->partials_cap) cap = ctx->partials_cap;
     int nb = pf == 1 ? icp_blocks_for(npx) : (npx + TPB - 1) / TPB;
     if (nb > cap) nb = cap;
+    if (C.occ) {   // occlusion flags of this pass's pose (same stream, before the fused pass)
+        if (ctx->occ_cap < npx) {
+            (void)hipFree(ctx->occ_tgt); (void)hipFree(ctx->occ_dinv); (void)hipFree(ctx->occ_flags);
+            (void)hipFree(ctx->occ_cnt); (void)hipFree(ctx->occ_off); (void)hipFree(ctx->occ_list);
+            (void)hipFree(ctx->occ_bsum);
+            const long n = npx;
+            R360_HIP(hipMalloc(&ctx->occ_tgt, sizeof(int) * n));
+            R360_HIP(hipMalloc(&ctx->occ_dinv, sizeof(float) * n));
+            R360_HIP(hipMalloc(&ctx->occ_flags, n));
+            R360_HIP(hipMalloc(&ctx->occ_cnt, sizeof(int) * n));
+            R360_HIP(hipMalloc(&ctx->occ_off, sizeof(int) * (n + 1)));
+            R360_HIP(hipMalloc(&ctx->occ_list, sizeof(int) * n));
+            R360_HIP(hipMalloc(&ctx->occ_bsum, sizeof(int) * (n / OCC_SCAN_ITEMS + 2)));
+            R360_HIP(hipMemsetAsync(ctx->occ_cnt, 0, sizeof(int) * n, ctx->stream));
+            ctx->occ_cap = n;
+        }
+        const int b256 = (npx + 255) / 256, bscan = (npx + OCC_SCAN_ITEMS - 1) / OCC_SCAN_ITEMS;
+        const int slot = timing_begin(ctx, "k_occ");
+        hipStream_t st = ctx->stream;
+        if (C.occ == 1)
+            hipLaunchKernelGGL(k_occ_project<1>, dim3(b256), dim3(256), 0, st, Ls.p0, Lt.p0, T.sinphi, T.cosphi,
+                               T.sinth, T.costh, Ls.rows, Ls.cols, C, ctx->d_state, first, eval_only, ctx->occ_tgt,
+                               ctx->occ_dinv, ctx->occ_flags, ctx->occ_cnt);
+        else
+            hipLaunchKernelGGL(k_occ_project<2>, dim3(b256), dim3(256), 0, st, Ls.p0, Lt.p0, T.sinphi, T.cosphi,
+                               T.sinth, T.costh, Ls.rows, Ls.cols, C, ctx->d_state, first, eval_only, ctx->occ_tgt,
+                               ctx->occ_dinv, ctx->occ_flags, ctx->occ_cnt);
+        hipLaunchKernelGGL(k_occ_scan1, dim3(bscan), dim3(OCC_SCAN_TPB), 0, st, ctx->occ_cnt, npx, ctx->occ_off,
+                           ctx->occ_bsum, ctx->d_state, first, eval_only);
+        hipLaunchKernelGGL(k_occ_scan2, dim3(1), dim3(OCC_SCAN_TPB), 0, st, ctx->occ_bsum, bscan, ctx->occ_off, npx,
+                           ctx->d_state, first, eval_only);
+        hipLaunchKernelGGL(k_occ_scan3, dim3(bscan), dim3(OCC_SCAN_TPB), 0, st, ctx->occ_bsum, npx, ctx->occ_off,
+                           ctx->d_state, first, eval_only);
+        hipLaunchKernelGGL(k_occ_scatter, dim3(b256), dim3(256), 0, st, ctx->occ_tgt, npx, ctx->occ_off, ctx->occ_cnt,
+                           ctx->occ_list, ctx->d_state, first, eval_only);
+        hipLaunchKernelGGL(k_occ_resolve, dim3(b256), dim3(256), 0, st, ctx->occ_off, npx, ctx->occ_list,
+                           ctx->occ_dinv, ctx->occ_flags, ctx->d_state, first, eval_only);
+        timing_end(ctx, slot);
+        R360_HIP(hipGetLastError());
+    }
     const char* name = level == 0 ? "k_icp_pass_L0" : "k_icp_pass";
     const int slot = timing_begin(ctx, name);
 #define R360_LAUNCH(M)                                                              \

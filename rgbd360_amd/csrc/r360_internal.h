@@ -47,6 +47,8 @@ struct IcpConst {
     double sd_photo_inv_d;    // double stdDevPhoto_inv = 1./stdDevPhoto  (:2561)
     double tol_res, tol_upd, lambda;
     int max_iters, fixed_iters0, n_pixels, level;
+    int occ;                  // alignFrames360 occlusion: 0 plain, 1 Occ1, 2 Occ2 (:4598-4627)
+    int pad1;
 };
 
 // Device-resident Gauss-Newton state of one alignFrames360 call.
@@ -68,7 +70,10 @@ struct alignas(16) IcpState {
     unsigned long long dbg[12];  // s_memrealtime stamps of the diagnostic build (-DR360_STAMPS)
 };
 
-enum { R360_SUM_NVALID = 27, R360_SUM_NVIS = 28, R360_SUM_ERR2 = 31, R360_NSUMS = 32 };
+// Pass sums.  Occlusion variants: NVALID counts photo terms (Occ1) or accepted points (Occ2), NDEPTH
+// the depth terms (Occ1), ERR2 the photometric and ERR2D the depth squared residuals.
+enum { R360_SUM_NVALID = 27, R360_SUM_NVIS = 28, R360_SUM_NDEPTH = 29, R360_SUM_ERR2D = 30, R360_SUM_ERR2 = 31,
+       R360_NSUMS = 32 };
 
 // ------------------------------------------------------------------ plane half
 #include "plane_math.h"
@@ -162,6 +167,16 @@ struct r360_ctx {
     // in-kernel execution spans of the ICP passes (s_memrealtime, 100 MHz): [0] earliest workgroup start
     // of the running pass, [1+l] summed spans at level l, [9+l] pass counts
     unsigned long long* d_ktime = nullptr;
+    // occlusion variants: per-source target pixel / exact inverse range / flags, per-target counts,
+    // offsets (exclusive scan) and the grouped source lists (icp_kernels.hip, k_occ_*)
+    long occ_cap = 0;
+    int* occ_tgt = nullptr;
+    float* occ_dinv = nullptr;
+    uint8_t* occ_flags = nullptr;
+    int* occ_cnt = nullptr;
+    int* occ_off = nullptr;
+    int* occ_list = nullptr;
+    int* occ_bsum = nullptr;
     int partials_cap = 0;
     IcpState* h_state = nullptr;  // pinned
     int timing = 0;
