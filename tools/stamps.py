@@ -55,3 +55,16 @@ k = len(order)
 for part in range(4):
     sl = order[part * k // 4:(part + 1) * k // 4]
     print(f"start-quartile {part}: busy mean {busy[sl].mean():6.2f}")
+
+# align mode (device Gauss-Newton step in the last workgroup): stamps of the final pass
+if os.environ.get("ALIGN"):
+    reg.params.fixed_iters_level0 = 20
+    for rep in range(3):
+        reg.alignFrames360(P, R.PHOTO_DEPTH)
+    st = (C.c_ulonglong * 12)()
+    R.lib().r360_ctx_debug_stamps(ctx.h, st)
+    t = np.array(list(st), dtype=np.uint64).astype(np.float64)
+    base = t[5]
+    us = lambda x: (x - base) / 100.0
+    print(f"align last pass: all-blocks loop end {us(t[6]):7.2f} | last block: start {us(t[0]):7.2f} loop-end {us(t[1]):7.2f}"
+          f" ticket {us(t[2]):7.2f} records {us(t[3]):7.2f} end (after GN) {us(t[4]):7.2f}")
