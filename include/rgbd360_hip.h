@@ -70,8 +70,14 @@ void r360_frame_destroy(r360_frame* f);
 int  r360_frame_upload(r360_frame* f, const uint8_t* bgr8, const uint16_t* depth8);
 /* Device-resident images (already in HBM on the ctx's device); copied device-to-device. */
 int  r360_frame_upload_device(r360_frame* f, const void* d_bgr8, const void* d_depth8);
-/* Frame360::loadFrame(path) (Frame360.h:231-266): Boost binary archive of 8 x {RGB, depth}. */
+/* Frame360::loadFrame(path) (Frame360.h:231-266): Boost binary archive of 8 x {RGB, depth} and
+ * the timestamp digit matrix (get_uint64_t_ofMatrixRepresentation, SerializeFrameRGBD.h:77-89). */
 int  r360_frame_load_bin(r360_frame* f, const char* path);
+/* Frame360::serialize(fileName) (Frame360.h:332-345): writes the raw images as loaded/uploaded. */
+int  r360_frame_save_bin(r360_frame* f, const char* path);
+/* Frame360::setTimeStamp / timeStamp (Frame360.h:181-184). */
+int  r360_frame_set_timestamp(r360_frame* f, uint64_t ts);
+int  r360_frame_get_timestamp(const r360_frame* f, uint64_t* ts);
 int  r360_frame_build(r360_frame* f, unsigned flags);
 int  r360_frame_build_async(r360_frame* f, unsigned flags);
 int  r360_frame_dims(const r360_frame* f, int* rows, int* cols, int* sph_rows, int* sph_cols);
@@ -154,8 +160,34 @@ typedef struct {
 } r360_plane;
 
 int r360_frame_get_planes(r360_frame* f, r360_plane* out, int cap, int* n);
+/* Plane::label of plane i (set by the labelization tools, LabelizeFrame360.cpp).  get returns the
+ * label length and copies at most cap-1 bytes plus a terminator. */
+int r360_frame_set_plane_label(r360_frame* f, int i, const char* label);
+int r360_frame_get_plane_label(r360_frame* f, int i, char* buf, int cap);
 /* Closed convex hull polygon (polygonContourPtr) of plane i, xyz triples. */
 int r360_frame_get_plane_hull(r360_frame* f, int i, float* xyz, int cap, int* n);
+
+/* ---------------------------------------------------------------- keyframe persistence
+ * Frame360::sphereCloud (Frame360.h:120): buildSphereCloud's concatenation of the 8 filtered
+ * clouds in the rig frame (width = 8*rows/2, height = cols/2), or the cloud set by loadCloud.
+ * xyz [cap][3], rgba [cap] (PointXYZRGBA packing b | g<<8 | r<<16 | a<<24); either may be NULL. */
+int r360_frame_get_sphere_cloud(r360_frame* f, float* xyz, uint32_t* rgba, size_t cap, int* width, int* height);
+/* pcl::io::savePCDFile / PCDReader::read for PointXYZRGBA (Frame360.h:187-193, 326).
+ * mode 0 = DATA ascii (the reference's call), 1 = binary, 2 = binary_compressed (LZF). */
+int r360_pcd_write(const char* path, const float* xyz, const uint32_t* rgba, int width, int height, int mode);
+int r360_pcd_read(const char* path, float* xyz, uint32_t* rgba, size_t cap, size_t* n, int* width, int* height);
+int r360_frame_save_cloud(r360_frame* f, const char* path, int mode);
+/* loadCloud (Frame360.h:187-193): sets the frame's sphereCloud. */
+int r360_frame_load_cloud(r360_frame* f, const char* path);
+/* savePlanes / loadPbMap (Frame360.h:195-210, 312-318): gzip file of the frame's PbMap (format in
+ * DESIGN.md; MRPT's CSerializable layout is not restated).  A loaded PbMap replaces the frame's
+ * planes and registers (r360_register_pbmap) exactly as the one that was saved. */
+int r360_frame_save_planes(r360_frame* f, const char* path);
+int r360_frame_load_pbmap(r360_frame* f, const char* path);
+/* save(path, frame) (Frame360.h:320-330) and load_PbMap_Cloud(path, index) (:222-228):
+ * dir/sphereCloud_<i>.pcd + dir/spherePlanes_<i>.pbmap. */
+int r360_frame_save(r360_frame* f, const char* dir, unsigned index);
+int r360_frame_load_pbmap_cloud(r360_frame* f, const char* dir, unsigned index);
 
 /* ---------------------------------------------------------------- RegisterRGBD360
  * Replaces include/RegisterRGBD360.h:97-337.  registrationType (:260-266). */

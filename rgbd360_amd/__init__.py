@@ -35,6 +35,7 @@ REPO_ROOT = os.path.dirname(_HERE)
 
 PHOTO_CONSISTENCY, DEPTH_CONSISTENCY, PHOTO_DEPTH = 0, 1, 2
 BUILD_UNDISTORT, BUILD_SPHERE, BUILD_PYRAMID, BUILD_CLOUD, BUILD_PLANES = 1, 2, 4, 8, 16
+PCD_ASCII, PCD_BINARY, PCD_BINARY_COMPRESSED = 0, 1, 2
 
 
 class IcpParams(C.Structure):
@@ -100,6 +101,20 @@ _SIGS = [
     ("r360_frame_upload", C.c_int, [_P, _P, _P]),
     ("r360_frame_upload_device", C.c_int, [_P, _P, _P]),
     ("r360_frame_load_bin", C.c_int, [_P, C.c_char_p]),
+    ("r360_frame_save_bin", C.c_int, [_P, C.c_char_p]),
+    ("r360_frame_set_timestamp", C.c_int, [_P, C.c_uint64]),
+    ("r360_frame_get_timestamp", C.c_int, [_P, C.POINTER(C.c_uint64)]),
+    ("r360_frame_get_sphere_cloud", C.c_int, [_P, _FP, _P, C.c_size_t, _IP, _IP]),
+    ("r360_pcd_write", C.c_int, [C.c_char_p, _FP, _P, C.c_int, C.c_int, C.c_int]),
+    ("r360_pcd_read", C.c_int, [C.c_char_p, _FP, _P, C.c_size_t, C.POINTER(C.c_size_t), _IP, _IP]),
+    ("r360_frame_save_cloud", C.c_int, [_P, C.c_char_p, C.c_int]),
+    ("r360_frame_load_cloud", C.c_int, [_P, C.c_char_p]),
+    ("r360_frame_save_planes", C.c_int, [_P, C.c_char_p]),
+    ("r360_frame_load_pbmap", C.c_int, [_P, C.c_char_p]),
+    ("r360_frame_save", C.c_int, [_P, C.c_char_p, C.c_uint]),
+    ("r360_frame_load_pbmap_cloud", C.c_int, [_P, C.c_char_p, C.c_uint]),
+    ("r360_frame_set_plane_label", C.c_int, [_P, C.c_int, C.c_char_p]),
+    ("r360_frame_get_plane_label", C.c_int, [_P, C.c_int, C.c_char_p, C.c_int]),
     ("r360_frame_build", C.c_int, [_P, C.c_uint]),
     ("r360_frame_build_async", C.c_int, [_P, C.c_uint]),
     ("r360_frame_dims", C.c_int, [_P, _IP, _IP, _IP, _IP]),
@@ -164,6 +179,28 @@ def _check(rc: int, what: str) -> int:
     if rc < 0:
         raise RuntimeError(f"{what} failed ({rc}): {lib().r360_last_error().decode()}")
     return rc
+
+
+def pcd_write(path: str, xyz: np.ndarray, rgba: np.ndarray | None, width: int, height: int, mode: int = PCD_ASCII):
+    """pcl::io::savePCDFile of a PointXYZRGBA cloud (host-only codec)."""
+    xyz = np.ascontiguousarray(xyz, np.float32).reshape(-1, 3)
+    assert xyz.shape[0] == width * height
+    if rgba is not None:
+        rgba = np.ascontiguousarray(rgba, np.uint32).reshape(-1)
+        assert rgba.shape[0] == xyz.shape[0]
+    _check(lib().r360_pcd_write(path.encode(), _fptr(xyz), None if rgba is None else _vptr(rgba), width, height, mode),
+           "pcd_write")
+
+
+def pcd_read(path: str):
+    """PCDReader::read into (xyz [n,3] f32, rgba [n] u32, width, height)."""
+    n, w, h = C.c_size_t(), C.c_int(), C.c_int()
+    _check(lib().r360_pcd_read(path.encode(), None, None, 0, C.byref(n), C.byref(w), C.byref(h)), "pcd_read")
+    xyz = np.zeros((n.value, 3), np.float32)
+    rgba = np.zeros(n.value, np.uint32)
+    _check(lib().r360_pcd_read(path.encode(), _fptr(xyz), _vptr(rgba), n.value, C.byref(n), C.byref(w), C.byref(h)),
+           "pcd_read")
+    return xyz, rgba, w.value, h.value
 
 
 def _fptr(a: np.ndarray):
@@ -286,6 +323,64 @@ class Frame360:
 
     def loadFrame(self, path: str):
         _check(lib().r360_frame_load_bin(self.h, path.encode()), "loadFrame")
+
+    def serialize(self, fileName: str):
+        """Frame360::serialize (Frame360.h:332-345): the raw images + timestamp as a .bin archive."""
+        _check(lib().r360_frame_save_bin(self.h, fileName.encode()), "serialize")
+
+    def setTimeStamp(self, timestamp: int):
+        _check(lib().r360_frame_set_timestamp(self.h, int(timestamp)), "setTimeStamp")
+
+    @property
+    def timeStamp(self) -> int:
+        t = C.c_uint64()
+        _check(lib().r360_frame_get_timestamp(self.h, C.byref(t)), "timeStamp")
+        return t.value
+
+    def sphereCloud(self):
+        """Frame360::sphereCloud: (xyz [n,3] f32, rgba [n] u32, width, height)."""
+        w, h = C.c_int(), C.c_int()
+        _check(lib().r360_frame_get_sphere_cloud(self.h, None, None, 0, C.byref(w), C.byref(h)), "sphereCloud")
+        n = w.value * h.value
+        xyz = np.zeros((n, 3), np.float32)
+        rgba = np.zeros(n, np.uint32)
+        _check(lib().r360_frame_get_sphere_cloud(self.h, _fptr(xyz), _vptr(rgba), n, C.byref(w), C.byref(h)),
+               "sphereCloud")
+        return xyz, rgba, w.value, h.value
+
+    def loadCloud(self, pointCloudPath: str):
+        _check(lib().r360_frame_load_cloud(self.h, pointCloudPath.encode()), "loadCloud")
+
+    def loadPbMap(self, pbmapPath: str):
+        _check(lib().r360_frame_load_pbmap(self.h, pbmapPath.encode()), "loadPbMap")
+
+    def load_PbMap_Cloud(self, path: str, index_or_pbmap):
+        """load_PbMap_Cloud(cloudPath, pbmapPath) or load_PbMap_Cloud(dir, index) (Frame360.h:212-228)."""
+        if isinstance(index_or_pbmap, str):
+            self.loadCloud(path)
+            self.loadPbMap(index_or_pbmap)
+        else:
+            _check(lib().r360_frame_load_pbmap_cloud(self.h, path.encode(), int(index_or_pbmap)), "load_PbMap_Cloud")
+
+    def savePlanes(self, pathPbMap: str):
+        _check(lib().r360_frame_save_planes(self.h, pathPbMap.encode()), "savePlanes")
+
+    def saveCloud(self, path: str, mode: int = PCD_ASCII):
+        _check(lib().r360_frame_save_cloud(self.h, path.encode(), mode), "saveCloud")
+
+    def save(self, path: str, frame: int):
+        """Frame360::save (Frame360.h:320-330): path/sphereCloud_<frame>.pcd + path/spherePlanes_<frame>.pbmap."""
+        _check(lib().r360_frame_save(self.h, path.encode(), int(frame)), "save")
+
+    def setPlaneLabel(self, i: int, label: str):
+        _check(lib().r360_frame_set_plane_label(self.h, i, label.encode()), "setPlaneLabel")
+
+    def planeLabel(self, i: int) -> str:
+        n = lib().r360_frame_get_plane_label(self.h, i, None, 0)
+        _check(min(n, 0), "planeLabel")
+        buf = C.create_string_buffer(n + 1)
+        lib().r360_frame_get_plane_label(self.h, i, buf, n + 1)
+        return buf.value.decode()
 
     def upload(self, bgr8: np.ndarray, depth8: np.ndarray):
         bgr8 = np.ascontiguousarray(bgr8, np.uint8)

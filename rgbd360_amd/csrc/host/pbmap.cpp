@@ -20,6 +20,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <zlib.h>
 #include <set>
 #include <vector>
 
@@ -59,6 +60,7 @@ struct HPlane {
     float nrgb[3] = {0, 0, 0};
     float intensity = 0;
     int id = 0, sensor = 0;
+    std::string label;      // Plane::label (set by the labelization tools, kept by savePlanes)
     std::vector<P3> hull;   // closed polygon
     r360p::Moments st;
 };
@@ -441,6 +443,7 @@ void planes_join(r360_frame* f) {
 // Host part of getPlanes: waits for the assembly thread
 int planes_finish(r360_frame* f) {
     PlaneBufs& P = f->pl;
+    if (!P.cloud && f->pbmap) return 0;   // PbMap loaded from a file (loadPbMap)
     if (!P.cloud) { r360_set_error("planes were not built (R360_BUILD_PLANES)"); return -2; }
     planes_join(f);
     if (P.worker_rc) { r360_set_error("%s", P.worker_err.c_str()); return P.worker_rc; }
@@ -937,7 +940,7 @@ extern "C" int r360_register(r360_ctx* ctx, r360_frame* ref, r360_frame* trg, co
 
 // ------------------------------------------------------------------ inspection (parity tests)
 extern "C" int r360_frame_get_cloud(r360_frame* f, float* xyz4, uint8_t* rgb4, float* nrm4, float* dist) {
-    CHECK_ARG(f && (f->built & R360_BUILD_CLOUD), "frame cloud not built (R360_BUILD_CLOUD)");
+    CHECK_ARG(f && (f->built & R360_BUILD_CLOUD) && f->pl.cloud, "frame cloud not built (R360_BUILD_CLOUD)");
     PlaneBufs& P = f->pl;
     const size_t T = 8 * (size_t)P.w * P.h;
     hipStream_t st = f->ctx->stream;
@@ -950,7 +953,7 @@ extern "C" int r360_frame_get_cloud(r360_frame* f, float* xyz4, uint8_t* rgb4, f
 }
 
 extern "C" int r360_frame_get_labels(r360_frame* f, int* lab, int* labf) {
-    CHECK_ARG(f && (f->built & R360_BUILD_PLANES), "frame planes not built (R360_BUILD_PLANES)");
+    CHECK_ARG(f && (f->built & R360_BUILD_PLANES) && f->pl.cloud, "frame planes not built (R360_BUILD_PLANES)");
     PlaneBufs& P = f->pl;
     const size_t T = 8 * (size_t)P.w * P.h;
     hipStream_t st = f->ctx->stream;
@@ -962,6 +965,7 @@ extern "C" int r360_frame_get_labels(r360_frame* f, int* lab, int* labf) {
 
 extern "C" int r360_frame_get_regions(r360_frame* f, int sensor, r360_region* out, int cap, int* n) {
     if (int rc = ready(f)) return rc;
+    CHECK_ARG(f->pl.cloud, "frame planes were loaded, not built: no per-sensor regions");
     CHECK_ARG(sensor >= 0 && sensor < 8, "sensor out of range");
     PlaneBufs& P = f->pl;
     const int nm = P.h_nmodels[sensor];
@@ -980,4 +984,140 @@ extern "C" int r360_frame_get_regions(r360_frame* f, int sensor, r360_region* ou
         r.curvature = O.model.curvature;
     }
     return 0;
+}
+
+// ------------------------------------------------------------------ PbMap persistence
+// Frame360::savePlanes / loadPbMap (Frame360.h:195-210, 312-318) stream the mrpt::pbmap::PbMap
+// through MRPT's CSerializable into a gzip file.  MRPT is not vendored in the reference, so its byte
+// layout cannot be restated here (parity unpinned at the byte level); the file keeps the gzip
+// container and carries, per plane, every field the registration path reads, the exact-integer
+// moments the same-plane merges use, the label and the convex hull, so a PbMap saved and loaded
+// back registers bit-identically to the one built.  Layout (little-endian, inside gzip):
+//   "R360PBM1" | u32 version = 1 | u32 n_planes | n_planes x {
+//     i32 id, sensor | f32 normal[3], center[3], ppal[3], d, area, elongation, curvature,
+//     nrgb[3], intensity | i64 n, s1[3] | i128 s2[6] | i64 c[4] | u32 label_len, label bytes |
+//     u32 n_hull, f32 hull[n_hull][3] }
+namespace {
+const char kPbmMagic[8] = {'R', '3', '6', '0', 'P', 'B', 'M', '1'};
+
+struct GzOut {
+    gzFile g;
+    bool ok = true;
+    void put(const void* p, size_t n) { if (ok && n) ok = gzwrite(g, p, (unsigned)n) == (int)n; }
+    template <class T> void val(const T& v) { put(&v, sizeof(T)); }
+};
+struct GzIn {
+    gzFile g;
+    bool ok = true;
+    void get(void* p, size_t n) { if (ok && n) ok = gzread(g, p, (unsigned)n) == (int)n; }
+    template <class T> void val(T& v) { get(&v, sizeof(T)); }
+};
+}  // namespace
+
+extern "C" int r360_frame_save_planes(r360_frame* f, const char* path) {
+    CHECK_ARG(path, "null path");
+    if (int rc = ready(f)) return rc;
+    GzOut o{gzopen(path, "wb")};
+    if (!o.g) { r360_set_error("cannot create %s", path); return -1; }
+    const auto& P = f->pbmap->planes;
+    o.put(kPbmMagic, 8);
+    o.val(uint32_t(1));
+    o.val(uint32_t(P.size()));
+    for (const HPlane& p : P) {
+        o.val(int32_t(p.id)); o.val(int32_t(p.sensor));
+        for (const P3* v : {&p.normal, &p.center, &p.ppal}) { o.val(v->x); o.val(v->y); o.val(v->z); }
+        o.val(p.d); o.val(p.area); o.val(p.elongation); o.val(p.curvature);
+        o.put(p.nrgb, sizeof p.nrgb); o.val(p.intensity);
+        o.val(p.st.n); o.put(p.st.s1, sizeof p.st.s1); o.put(p.st.s2, sizeof p.st.s2); o.put(p.st.c, sizeof p.st.c);
+        o.val(uint32_t(p.label.size())); o.put(p.label.data(), p.label.size());
+        o.val(uint32_t(p.hull.size()));
+        for (const P3& q : p.hull) { o.val(q.x); o.val(q.y); o.val(q.z); }
+    }
+    const bool closed = gzclose(o.g) == Z_OK;
+    if (!o.ok || !closed) { r360_set_error("write failed: %s", path); return -1; }
+    return 0;
+}
+
+extern "C" int r360_frame_load_pbmap(r360_frame* f, const char* path) {
+    CHECK_ARG(f && path, "null arg");
+    GzIn in{gzopen(path, "rb")};
+    if (!in.g) { r360_set_error("cannot open %s", path); return -1; }
+    char magic[8] = {};
+    uint32_t version = 0, n = 0;
+    in.get(magic, 8); in.val(version); in.val(n);
+    auto fail = [&](const char* why) { gzclose(in.g); r360_set_error("%s: %s", path, why); return -1; };
+    if (!in.ok || memcmp(magic, kPbmMagic, 8) != 0) return fail("not an R360 PbMap file");
+    if (version != 1) return fail("unsupported PbMap file version");
+    if (n > (1u << 20)) return fail("implausible plane count");
+    auto* pm = new PbMapHost;
+    pm->planes.resize(n);
+    for (HPlane& p : pm->planes) {
+        int32_t id = 0, sensor = 0;
+        in.val(id); in.val(sensor);
+        p.id = id; p.sensor = sensor;
+        for (P3* v : {&p.normal, &p.center, &p.ppal}) { in.val(v->x); in.val(v->y); in.val(v->z); }
+        in.val(p.d); in.val(p.area); in.val(p.elongation); in.val(p.curvature);
+        in.get(p.nrgb, sizeof p.nrgb); in.val(p.intensity);
+        in.val(p.st.n); in.get(p.st.s1, sizeof p.st.s1); in.get(p.st.s2, sizeof p.st.s2); in.get(p.st.c, sizeof p.st.c);
+        uint32_t ll = 0, nh = 0;
+        in.val(ll);
+        if (!in.ok || ll > (1u << 20)) { delete pm; return fail("corrupt label"); }
+        p.label.resize(ll);
+        in.get(&p.label[0], ll);
+        in.val(nh);
+        if (!in.ok || nh > (1u << 24)) { delete pm; return fail("corrupt hull"); }
+        p.hull.resize(nh);
+        for (P3& q : p.hull) { in.val(q.x); in.val(q.y); in.val(q.z); }
+        if (!in.ok) { delete pm; return fail("truncated"); }
+    }
+    gzclose(in.g);
+    // like `serialize_planes >> planes`, the loaded map replaces the frame's planes
+    planes_join(f);
+    f->pl.worker_rc = 0;
+    delete f->pbmap;
+    f->pbmap = pm;
+    f->built |= R360_BUILD_PLANES;
+    return 0;
+}
+
+extern "C" int r360_frame_set_plane_label(r360_frame* f, int i, const char* label) {
+    if (int rc = ready(f)) return rc;
+    CHECK_ARG(label && i >= 0 && i < int(f->pbmap->planes.size()), "plane index out of range");
+    f->pbmap->planes[i].label = label;
+    return 0;
+}
+
+extern "C" int r360_frame_get_plane_label(r360_frame* f, int i, char* buf, int cap) {
+    if (int rc = ready(f)) return rc;
+    CHECK_ARG(i >= 0 && i < int(f->pbmap->planes.size()), "plane index out of range");
+    const std::string& s = f->pbmap->planes[i].label;
+    if (buf && cap > 0) {
+        const int k = std::min(cap - 1, int(s.size()));
+        memcpy(buf, s.data(), k);
+        buf[k] = 0;
+    }
+    return int(s.size());
+}
+
+// Frame360::save(path, frame) (Frame360.h:320-330): path/sphereCloud_%d.pcd (savePCDFile, ascii)
+// and path/spherePlanes_%d.pbmap.
+extern "C" int r360_frame_save(r360_frame* f, const char* dir, unsigned index) {
+    CHECK_ARG(f && dir, "null arg");
+    if (int rc = ready(f)) return rc;
+    CHECK_ARG(!f->pbmap->planes.empty(), "save: the frame has no planes (Frame360.h:323 asserts)");
+    char a[4096], b[4096];
+    snprintf(a, sizeof a, "%s/sphereCloud_%d.pcd", dir, (int)index);
+    snprintf(b, sizeof b, "%s/spherePlanes_%d.pbmap", dir, (int)index);
+    if (int rc = r360_frame_save_cloud(f, a, 0)) return rc;
+    return r360_frame_save_planes(f, b);
+}
+
+// Frame360::load_PbMap_Cloud(path, index) (Frame360.h:222-228): %u in the file names.
+extern "C" int r360_frame_load_pbmap_cloud(r360_frame* f, const char* dir, unsigned index) {
+    CHECK_ARG(f && dir, "null arg");
+    char a[4096], b[4096];
+    snprintf(a, sizeof a, "%s/sphereCloud_%u.pcd", dir, index);
+    snprintf(b, sizeof b, "%s/spherePlanes_%u.pbmap", dir, index);
+    if (int rc = r360_frame_load_cloud(f, a)) return rc;
+    return r360_frame_load_pbmap(f, b);
 }

@@ -390,6 +390,7 @@ extern "C" void r360_frame_destroy(r360_frame* f) {
     hipFree(f->d_bgr); hipFree(f->d_depth); hipFree(f->d_depth_m); hipFree(f->d_sph_bgr); hipFree(f->d_sph_depth);
     for (int l = 0; l < f->n_levels; ++l) { hipFree(f->lv[l].p0); hipFree(f->lv[l].tg); }
     plane_bufs_free(f);
+    delete f->sphere_cloud;
     delete f;
 }
 
@@ -412,16 +413,6 @@ extern "C" int r360_frame_upload_device(r360_frame* f, const void* d_bgr8, const
     return 0;
 }
 
-int parse_bin_file(const char* path, int rows, int cols, std::vector<uint8_t>& bgr, std::vector<uint16_t>& depth);
-
-extern "C" int r360_frame_load_bin(r360_frame* f, const char* path) {
-    CHECK_ARG(f && path, "null arg");
-    std::vector<uint8_t> bgr;
-    std::vector<uint16_t> depth;
-    if (parse_bin_file(path, f->rows, f->cols, bgr, depth)) return -1;
-    return r360_frame_upload(f, bgr.data(), depth.data());
-}
-
 extern "C" int r360_frame_build_async(r360_frame* f, unsigned flags) {
     CHECK_ARG(f, "null frame");
     if (flags & (R360_BUILD_UNDISTORT | R360_BUILD_CLOUD | R360_BUILD_PLANES)) {
@@ -441,6 +432,8 @@ extern "C" int r360_frame_build_async(r360_frame* f, unsigned flags) {
         // here; the per-plane PbMap assembly runs on the host when the planes are first needed
         if (planes_enqueue(f)) return -1;
         f->built |= R360_BUILD_CLOUD | R360_BUILD_PLANES;
+        delete f->sphere_cloud;  // a cloud set by loadCloud is replaced by the built one
+        f->sphere_cloud = nullptr;
     }
     return 0;
 }

@@ -231,6 +231,13 @@ struct r360_calib {
     LevelTrig trig[R360_MAX_PYR];
 };
 
+// Host copy of Frame360::sphereCloud as loadCloud leaves it (io.cpp)
+struct SphereCloudHost {
+    int width = 0, height = 0;
+    std::vector<float> xyz;      // [n][3]
+    std::vector<uint32_t> rgba;  // PCL PointXYZRGBA packing: b | g<<8 | r<<16 | a<<24
+};
+
 struct r360_frame {
     r360_ctx* ctx = nullptr;
     const r360_calib* calib = nullptr;
@@ -244,6 +251,8 @@ struct r360_frame {
     unsigned built = 0;
     PlaneBufs pl;
     PbMapHost* pbmap = nullptr;
+    uint64_t timestamp = 0;            // Frame360::timeStamp (Frame360.h:181-184)
+    SphereCloudHost* sphere_cloud = nullptr;  // sphereCloud set by loadCloud (Frame360.h:187-193)
 };
 
 // ------------------------------------------------------------------ kernel launchers
