@@ -121,6 +121,7 @@ struct Plane {                          // mrpt::pbmap::Plane fields used on the
     int sensor;
     size_t n_inliers;
     std::vector<float> polygonContour;  // closed hull polygon, xyz triples
+    std::string label;                  // Plane::label (labelization tools), kept by savePlanes
 };
 
 class Frame360 {
@@ -141,6 +142,40 @@ class Frame360 {
         check(r360_frame_build(h_, R360_BUILD_UNDISTORT | R360_BUILD_PLANES), "getPlanes");
         fetch_planes();
     }
+    // ---- keyframe persistence (Frame360.h:181-228, 312-345)
+    void serialize(const std::string& fileName) { check(r360_frame_save_bin(h_, fileName.c_str()), "serialize"); }
+    void setTimeStamp(uint64_t t) { check(r360_frame_set_timestamp(h_, t), "setTimeStamp"); }
+    uint64_t timeStamp() const { uint64_t t = 0; check(r360_frame_get_timestamp(h_, &t), "timeStamp"); return t; }
+    void loadCloud(const std::string& pointCloudPath) { check(r360_frame_load_cloud(h_, pointCloudPath.c_str()), "loadCloud"); }
+    void loadPbMap(const std::string& pbmapPath) {
+        check(r360_frame_load_pbmap(h_, pbmapPath.c_str()), "loadPbMap");
+        fetch_planes();
+    }
+    void load_PbMap_Cloud(const std::string& pointCloudPath, const std::string& pbmapPath) {
+        loadCloud(pointCloudPath);
+        loadPbMap(pbmapPath);
+    }
+    void load_PbMap_Cloud(const std::string& path, unsigned index) {
+        check(r360_frame_load_pbmap_cloud(h_, path.c_str(), index), "load_PbMap_Cloud");
+        fetch_planes();
+    }
+    // labels edited in `planes` are written with the map
+    void savePlanes(const std::string& pathPbMap) {
+        push_labels();
+        check(r360_frame_save_planes(h_, pathPbMap.c_str()), "savePlanes");
+    }
+    void save(const std::string& path, unsigned frame) {
+        push_labels();
+        check(r360_frame_save(h_, path.c_str(), frame), "save");
+    }
+    // sphereCloud as xyz triples + PointXYZRGBA-packed colours
+    void sphereCloud(std::vector<float>& xyz, std::vector<uint32_t>& rgba, int& width, int& height) {
+        check(r360_frame_get_sphere_cloud(h_, nullptr, nullptr, 0, &width, &height), "sphereCloud");
+        const size_t n = size_t(width) * size_t(height);
+        xyz.resize(3 * n);
+        rgba.resize(n);
+        check(r360_frame_get_sphere_cloud(h_, xyz.data(), rgba.data(), n, &width, &height), "sphereCloud");
+    }
     // Frame360::getPlanarArea (Frame360.h:157)
     float getPlanarArea() const {
         float a = 0.f;
@@ -153,6 +188,10 @@ class Frame360 {
     r360_frame* get() const { return h_; }
 
   private:
+    void push_labels() {
+        for (size_t i = 0; i < planes.size(); ++i)
+            check(r360_frame_set_plane_label(h_, int(i), planes[i].label.c_str()), "plane label");
+    }
     void fetch_planes() {
         int n = 0;
         check(r360_frame_get_planes(h_, nullptr, 0, &n), "getPlanes");
@@ -172,6 +211,12 @@ class Frame360 {
             p.polygonContour.resize(3 * size_t(r.n_hull));
             int m = 0;
             check(r360_frame_get_plane_hull(h_, i, p.polygonContour.data(), r.n_hull, &m), "getPlanes");
+            const int ll = r360_frame_get_plane_label(h_, i, nullptr, 0);
+            if (ll > 0) {
+                std::vector<char> buf(size_t(ll) + 1);
+                r360_frame_get_plane_label(h_, i, buf.data(), ll + 1);
+                p.label = buf.data();
+            }
             planes.push_back(p);
         }
     }
