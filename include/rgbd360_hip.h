@@ -63,6 +63,7 @@ enum {
     R360_BUILD_PYRAMID   = 1u << 2,  /* RegisterPhotoICP::set{Source,Target}Frame :480-516 */
     R360_BUILD_CLOUD     = 1u << 3,  /* Frame360::buildSphereCloud()     Frame360.h:467   */
     R360_BUILD_PLANES    = 1u << 4,  /* Frame360::getPlanes()            Frame360.h:615   */
+    R360_BUILD_SENSOR_PYRAMID = 1u << 5, /* per-sensor setSource/TargetFrame (pinhole alignFrames) */
 };
 int  r360_frame_create(r360_ctx* ctx, const r360_calib* calib, r360_frame** out);
 void r360_frame_destroy(r360_frame* f);
@@ -89,6 +90,9 @@ int  r360_frame_get_depth_m(r360_frame* f, float* depth8);
  * gradients with the alignFrames360 seam mask applied).  Any pointer may be NULL. */
 int  r360_frame_get_level(r360_frame* f, int level, int* rows, int* cols, float* gray, float* depth,
                           float* gx, float* gy, float* dgx, float* dgy);
+/* Sensor k's pinhole pyramid level (R360_BUILD_SENSOR_PYRAMID; no seam mask). */
+int  r360_frame_get_sensor_level(r360_frame* f, int sensor, int level, int* rows, int* cols, float* gray,
+                                 float* depth, float* gx, float* gy, float* dgx, float* dgy);
 
 /* ---------------------------------------------------------------- RegisterPhotoICP
  * Replaces include/RegisterPhotoICP.h:85-4784 (spherical path). */
@@ -145,6 +149,28 @@ int r360_icp_eval(r360_ctx* ctx, r360_frame* trg, r360_frame* src, int level, co
 int r360_icp_eval_occ(r360_ctx* ctx, r360_frame* trg, r360_frame* src, int level, const float pose[16],
                       int method, int occlusion, const r360_icp_params* p, double H[36], double g[6],
                       double* error, int* n_valid, int* n_visible);
+
+/* ---------------------------------------------------------------- pinhole alignFrames (per sensor)
+ * RegisterPhotoICP::alignFrames(pose_guess, method) (:4254-4512) with errorPhotoICP (:560-761) and
+ * calcHessGrad (:767-1100), after setTargetFrame / setSourceFrame on sensor k's raw images of two
+ * frames (MethodsRegisterRGBD360.cpp:320-345).  Frames need R360_BUILD_SENSOR_PYRAMID.
+ * K = {fx, fy, ox, oy} of level 0 (setCameraMatrix); NULL = the calibration's cameraMatrix.
+ * Uses p->n_pyr, depth range, std devs and saliency thresholds; the Levenberg-Marquardt constants are
+ * alignFrames' own (lambda 0.01, step 10, 10 iterations, tolerances 1e-4).  Returns 1 if ILL-POSED. */
+int r360_align_pinhole(r360_ctx* ctx, r360_frame* trg, r360_frame* src, int sensor, const float init[16],
+                       int method, const float* K, const r360_icp_params* p, float pose_out[16], float H_out[36],
+                       float g_out[6], r360_icp_stats* st);
+/* Up to 8 alignments at once (one per listed sensor, init = n x float[16]); _result fills n poses /
+ * H / g / stats and returns the number of ILL-POSED jobs. */
+int r360_align_pinhole_async(r360_ctx* ctx, r360_frame* trg, r360_frame* src, int n, const int* sensors,
+                             const float* init, int method, const float* K, const r360_icp_params* p);
+int r360_align_pinhole_result(r360_ctx* ctx, float* poses, float* H, float* g, r360_icp_stats* st);
+/* One errorPhotoICP + calcHessGrad pass at `pose` (parity hook): error = avResidual (NaN for
+ * PHOTO_CONSISTENCY, as the reference), res = {PhotoResidual, DepthResidual},
+ * counts = {nValidPhotoPts, nValidDepthPts, visible}. */
+int r360_pinhole_eval(r360_ctx* ctx, r360_frame* trg, r360_frame* src, int sensor, int level, const float pose[16],
+                      int method, const float* K, const r360_icp_params* p, double H[36], double g[6],
+                      double* error, double res[2], int counts[3]);
 
 /* CPose3D::exp(mu, pseudo) (MRPT; used at RegisterPhotoICP.h:4697). */
 void r360_exp_se3(const double mu[6], int pseudo, float T[16]);

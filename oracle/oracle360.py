@@ -46,6 +46,16 @@ class Level(C.Structure):
         (n, C.POINTER(C.c_float)) for n in ("gray_src", "depth_src", "gray_trg", "depth_trg", "gx", "gy", "dgx", "dgy")]
 
 
+class Pinhole(C.Structure):
+    _fields_ = [("fx", C.c_float), ("fy", C.c_float), ("ox", C.c_float), ("oy", C.c_float)]
+
+    @classmethod
+    def rgbd360(cls, rows: int, cols: int):
+        """MethodsRegisterRGBD360.cpp:323-330: f = 525*w/640, c = (w/2 - 0.5, h/2 - 0.5), float."""
+        f = np.float32(525) * (np.float32(cols) / np.float32(640.0))
+        return cls(f, f, np.float32(cols) / 2 - np.float32(0.5), np.float32(rows) / 2 - np.float32(0.5))
+
+
 class Region(C.Structure):
     _fields_ = [("label", C.c_int), ("count", C.c_int), ("start_idx", C.c_int), ("n_contour", C.c_int),
                 ("contour_off", C.c_int), ("centroid", C.c_float * 3), ("cov", C.c_float * 9),
@@ -96,6 +106,12 @@ def lib() -> C.CDLL:
             "orc_error_sphere_occ": (C.c_double, [C.POINTER(Level), fp, C.c_int, C.c_int, C.POINTER(IcpParams), ip]),
             "orc_hessgrad_sphere_occ": (None, [C.POINTER(Level), fp, C.c_int, C.c_int, C.POINTER(IcpParams), dp, dp,
                                                ip]),
+            "orc_error_pinhole": (C.c_double, [C.POINTER(Level), C.POINTER(Pinhole), C.c_int, fp, C.c_int,
+                                               C.POINTER(IcpParams), ip, ip, dp, dp]),
+            "orc_hessgrad_pinhole": (None, [C.POINTER(Level), C.POINTER(Pinhole), C.c_int, fp, C.c_int,
+                                            C.POINTER(IcpParams), dp, dp, ip]),
+            "orc_align_pinhole": (C.c_int, [vp, vp, vp, vp, C.c_int, C.c_int, C.POINTER(Pinhole), fp, C.c_int,
+                                            C.POINTER(IcpParams), fp, fp, fp, C.POINTER(IcpStats)]),
             "orc_exp_se3": (None, [dp, C.c_int, fp]),
             "orc_huber": (C.c_float, [C.c_float, C.c_float]),
             "orc_libm": (None, [fp, fp, fp, C.c_int, fp, fp]),
@@ -312,6 +328,50 @@ def align360(trg_bgr, trg_dep, src_bgr, src_dep, init=None, method=PHOTO_DEPTH, 
     rc = lib().orc_align360_occ(_v(trg_bgr), _v(trg_dep), _v(src_bgr), _v(src_dep), src_dep.shape[0],
                                 src_dep.shape[1], _f(init16), method, occlusion, C.byref(p), _f(po), _f(Ho), _f(go),
                                 C.byref(st))
+    return rc, from16(po), Ho.reshape(6, 6).T.copy(), go, st
+
+
+# ---------------------------------------------------------------- §8(f)3 pinhole per-sensor path
+def sensor_pyramid(bgr, dep, n_levels: int):
+    """setTargetFrame / setSourceFrame (:480-516) on one sensor's raw images: no seam mask."""
+    return sphere_pyramid(bgr, dep, n_levels, mask=False)
+
+
+def error_pinhole(src: dict, trg: dict, K: Pinhole, level: int, pose, method=PHOTO_DEPTH,
+                  params: IcpParams | None = None):
+    """errorPhotoICP (:560-761) -> (avResidual, n_photo, n_depth, photo_sum, depth_sum)."""
+    L, keep = _level_struct(src, trg)
+    p = params or IcpParams.default()
+    nP, nD, rP, rD = C.c_int(), C.c_int(), C.c_double(), C.c_double()
+    e = lib().orc_error_pinhole(C.byref(L), C.byref(K), level, _f(mat16(pose)), method, C.byref(p), C.byref(nP),
+                                C.byref(nD), C.byref(rP), C.byref(rD))
+    return e, nP.value, nD.value, rP.value, rD.value
+
+
+def hessgrad_pinhole(src: dict, trg: dict, K: Pinhole, level: int, pose, method=PHOTO_DEPTH,
+                     params: IcpParams | None = None):
+    """calcHessGrad (:767-1100) -> (H, g, n_visible)."""
+    L, keep = _level_struct(src, trg)
+    p = params or IcpParams.default()
+    H, g, nvis = np.zeros(36), np.zeros(6), C.c_int()
+    lib().orc_hessgrad_pinhole(C.byref(L), C.byref(K), level, _f(mat16(pose)), method, C.byref(p),
+                               H.ctypes.data_as(C.POINTER(C.c_double)), g.ctypes.data_as(C.POINTER(C.c_double)),
+                               C.byref(nvis))
+    return H.reshape(6, 6), g, nvis.value
+
+
+def align_pinhole(trg_bgr, trg_dep, src_bgr, src_dep, K: Pinhole | None = None, init=None, method=PHOTO_DEPTH,
+                  params: IcpParams | None = None):
+    """alignFrames (:4254-4512) on one sensor -> (rc, pose, H, g, stats)."""
+    trg_bgr, trg_dep, src_bgr, src_dep = [np.ascontiguousarray(a) for a in (trg_bgr, trg_dep, src_bgr, src_dep)]
+    rows, cols = src_dep.shape
+    K = K or Pinhole.rgbd360(rows, cols)
+    p = params or IcpParams.default()
+    init16 = mat16(np.eye(4) if init is None else init)
+    po, Ho, go = np.zeros(16, np.float32), np.zeros(36, np.float32), np.zeros(6, np.float32)
+    st = IcpStats()
+    rc = lib().orc_align_pinhole(_v(trg_bgr), _v(trg_dep), _v(src_bgr), _v(src_dep), rows, cols, C.byref(K),
+                                 _f(init16), method, C.byref(p), _f(po), _f(Ho), _f(go), C.byref(st))
     return rc, from16(po), Ho.reshape(6, 6).T.copy(), go, st
 
 

@@ -105,6 +105,21 @@ int orc_align360(const uint8_t* trg_bgr, const uint16_t* trg_depth,
                  const orc_icp_params* p, float pose_out[16], float H_out[36],
                  float g_out[6], orc_icp_stats* st);
 
+/* ---- §8(f)3: per-sensor pinhole dense path (RegisterPhotoICP.h:560-1100, 4254-4512).
+ * Level-0 intrinsics (setCameraMatrix); each level scales them by 1/2^l (:4273-4279). */
+typedef struct { float fx, fy, ox, oy; } orc_pinhole;
+/* errorPhotoICP -> avResidual (NaN for PHOTO_CONSISTENCY, as the reference: it divides by nValidDepthPts) */
+double orc_error_pinhole(const orc_level* L, const orc_pinhole* K, int level, const float pose[16], int method,
+                         const orc_icp_params* p, int* n_photo, int* n_depth, double* res_photo, double* res_depth);
+void   orc_hessgrad_pinhole(const orc_level* L, const orc_pinhole* K, int level, const float pose[16], int method,
+                            const orc_icp_params* p, double H[36], double g[6], int* n_visible);
+/* alignFrames (occlusion 0) on one sensor's raw images; params: n_pyr, depth range, std devs and
+ * saliency thresholds (the LM constants are alignFrames' own).  Returns 1 when ILL-POSED. */
+int    orc_align_pinhole(const uint8_t* trg_bgr, const uint16_t* trg_depth, const uint8_t* src_bgr,
+                         const uint16_t* src_depth, int rows, int cols, const orc_pinhole* K,
+                         const float init[16], int method, const orc_icp_params* p, float pose_out[16],
+                         float H_out[36], float g_out[6], orc_icp_stats* st);
+
 /* ---- A18: CPose3D::exp(mu, pseudo) */
 void orc_exp_se3(const double mu[6], int pseudo, float T[16]);
 

@@ -35,6 +35,7 @@ REPO_ROOT = os.path.dirname(_HERE)
 
 PHOTO_CONSISTENCY, DEPTH_CONSISTENCY, PHOTO_DEPTH = 0, 1, 2
 BUILD_UNDISTORT, BUILD_SPHERE, BUILD_PYRAMID, BUILD_CLOUD, BUILD_PLANES = 1, 2, 4, 8, 16
+BUILD_SENSOR_PYRAMID = 32
 PCD_ASCII, PCD_BINARY, PCD_BINARY_COMPRESSED = 0, 1, 2
 
 
@@ -121,6 +122,7 @@ _SIGS = [
     ("r360_frame_get_sphere", C.c_int, [_P, _P, _P]),
     ("r360_frame_get_depth_m", C.c_int, [_P, _P]),
     ("r360_frame_get_level", C.c_int, [_P, C.c_int, _IP, _IP, _P, _P, _P, _P, _P, _P]),
+    ("r360_frame_get_sensor_level", C.c_int, [_P, C.c_int, C.c_int, _IP, _IP, _P, _P, _P, _P, _P, _P]),
     ("r360_icp_default_params", None, [C.POINTER(IcpParams)]),
     ("r360_align360", C.c_int, [_P, _P, _P, _FP, C.c_int, C.c_int, C.POINTER(IcpParams), _FP, _FP, _FP,
                                 C.POINTER(IcpStats)]),
@@ -131,6 +133,12 @@ _SIGS = [
     ("r360_icp_eval_occ", C.c_int, [_P, _P, _P, C.c_int, _FP, C.c_int, C.c_int, C.POINTER(IcpParams), _DP, _DP,
                                     _DP, _IP, _IP]),
     ("r360_exp_se3", None, [_DP, C.c_int, _FP]),
+    ("r360_align_pinhole", C.c_int, [_P, _P, _P, C.c_int, _FP, C.c_int, _FP, C.POINTER(IcpParams), _FP, _FP, _FP,
+                                     C.POINTER(IcpStats)]),
+    ("r360_align_pinhole_async", C.c_int, [_P, _P, _P, C.c_int, _IP, _FP, C.c_int, _FP, C.POINTER(IcpParams)]),
+    ("r360_align_pinhole_result", C.c_int, [_P, _FP, _FP, _FP, C.POINTER(IcpStats)]),
+    ("r360_pinhole_eval", C.c_int, [_P, _P, _P, C.c_int, C.c_int, _FP, C.c_int, _FP, C.POINTER(IcpParams), _DP, _DP,
+                                    _DP, _DP, _IP]),
     ("r360_frame_get_planes", C.c_int, [_P, C.POINTER(Plane), C.c_int, _IP]),
     ("r360_frame_get_plane_hull", C.c_int, [_P, C.c_int, _FP, C.c_int, _IP]),
     ("r360_register_pbmap", C.c_int, [_P, _P, _P, C.c_size_t, C.c_int, _FP, _FP, _IP, C.c_int, _IP, _FP, _FP, _FP]),
@@ -470,6 +478,16 @@ class Frame360:
                "get_level")
         return dict(zip(["gray", "depth", "gx", "gy", "dgx", "dgy"], arrs))
 
+    def sensor_level(self, sensor: int, level: int):
+        """Sensor k's pinhole pyramid level (BUILD_SENSOR_PYRAMID)."""
+        r, c = C.c_int(), C.c_int()
+        _check(lib().r360_frame_get_sensor_level(self.h, sensor, level, C.byref(r), C.byref(c), None, None, None,
+                                                 None, None, None), "get_sensor_level")
+        arrs = [np.zeros((r.value, c.value), np.float32) for _ in range(6)]
+        _check(lib().r360_frame_get_sensor_level(self.h, sensor, level, C.byref(r), C.byref(c),
+                                                 *[_vptr(a) for a in arrs]), "get_sensor_level")
+        return dict(zip(["gray", "depth", "gx", "gy", "dgx", "dgy"], arrs))
+
     def close(self):
         if self.h:
             lib().r360_frame_destroy(self.h)
@@ -597,6 +615,66 @@ class RegisterPhotoICP:
     def getOptimalPose(self): return self.relPose
     def getHessian(self): return self.hessian
     def getGradient(self): return self.gradient
+
+    # ---- pinhole per-sensor path (§8(f) rank 3): alignFrames (:4254-4512) on sensor images
+    def setCameraMatrix(self, K):
+        """cameraMatrix (3x3); None = the calibration's (f = 525*cols/640, c = (cols/2-0.5, rows/2-0.5))."""
+        self.K = None if K is None else np.array([K[0][0], K[1][1], K[0][2], K[1][2]], np.float32)
+
+    def setSourceSensor(self, f: Frame360, sensor: int):
+        """setSourceFrame(frameRGBD_[sensor].getRGBImage(), getDepthImage()) (:496-516)."""
+        self.src, self.src_sensor = f, sensor
+
+    def setTargetSensor(self, f: Frame360, sensor: int):
+        """setTargetFrame(frameRGBD_[sensor].getRGBImage(), getDepthImage()) (:480-494)."""
+        self.trg, self.trg_sensor = f, sensor
+
+    def _K(self):
+        k = getattr(self, "K", None)
+        return None if k is None else _fptr(k)
+
+    def alignFrames(self, pose_guess=None, method: int = PHOTO_CONSISTENCY, occlusion: int = 0) -> int:
+        if occlusion:
+            raise NotImplementedError("pinhole alignFrames: occlusion variants 1/2 are not built")
+        if self.src_sensor != self.trg_sensor:
+            raise ValueError("source and target sensors differ")
+        init = _mat16(np.eye(4) if pose_guess is None else pose_guess)
+        po, Ho, go = np.zeros(16, np.float32), np.zeros(36, np.float32), np.zeros(6, np.float32)
+        rc = _check(lib().r360_align_pinhole(self.ctx.h, self.trg.h, self.src.h, self.src_sensor, _fptr(init), method,
+                                             self._K(), C.byref(self.params), _fptr(po), _fptr(Ho), _fptr(go),
+                                             C.byref(self.stats)), "alignFrames")
+        self.relPose = _from16(po)
+        self.hessian = Ho.reshape(6, 6).T.copy()
+        self.gradient = go.copy()
+        return rc
+
+    def alignSensors(self, trg: Frame360, src: Frame360, sensors, pose_guesses, method: int = PHOTO_DEPTH):
+        """alignFrames on several sensors of one pair at once (one batched pass sequence).
+        Returns (poses [n,4,4], hessians [n,6,6], stats list, n_illposed)."""
+        sensors = np.ascontiguousarray(sensors, np.int32)
+        n = len(sensors)
+        init = np.concatenate([_mat16(P) for P in pose_guesses]).astype(np.float32)
+        _check(lib().r360_align_pinhole_async(self.ctx.h, trg.h, src.h, n, sensors.ctypes.data_as(_IP), _fptr(init),
+                                              method, self._K(), C.byref(self.params)), "alignSensors")
+        po, Ho, go = np.zeros(16 * n, np.float32), np.zeros(36 * n, np.float32), np.zeros(6 * n, np.float32)
+        st = (IcpStats * n)()
+        ill = _check(lib().r360_align_pinhole_result(self.ctx.h, _fptr(po), _fptr(Ho), _fptr(go), st),
+                     "alignSensors")
+        poses = np.stack([_from16(po[16 * j:16 * j + 16]) for j in range(n)])
+        Hs = np.stack([Ho[36 * j:36 * j + 36].reshape(6, 6).T for j in range(n)])
+        return poses, Hs, list(st), ill
+
+    def eval_pinhole(self, level: int, pose, method: int = PHOTO_DEPTH):
+        """One errorPhotoICP + calcHessGrad pass -> dict(H, g, error, res_photo, res_depth, n_photo, n_depth, n_vis)."""
+        H, g = np.zeros(36), np.zeros(6)
+        err, res = C.c_double(), np.zeros(2)
+        cnt = np.zeros(3, np.int32)
+        _check(lib().r360_pinhole_eval(self.ctx.h, self.trg.h, self.src.h, self.src_sensor, level, _fptr(_mat16(pose)),
+                                       method, self._K(), C.byref(self.params), H.ctypes.data_as(_DP),
+                                       g.ctypes.data_as(_DP), C.byref(err), res.ctypes.data_as(_DP),
+                                       cnt.ctypes.data_as(_IP)), "eval_pinhole")
+        return dict(H=H.reshape(6, 6), g=g, error=err.value, res_photo=res[0], res_depth=res[1], n_photo=int(cnt[0]),
+                    n_depth=int(cnt[1]), n_vis=int(cnt[2]))
 
     def eval(self, level: int, pose, method: int = PHOTO_DEPTH):
         """One fused errorPhotoICP_sphere + calcHessGrad_sphere pass at a fixed pose."""

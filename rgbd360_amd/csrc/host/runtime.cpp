@@ -126,6 +126,7 @@ extern "C" void r360_ctx_destroy(r360_ctx* c) {
     hipFree(c->d_partials);
     hipFree(c->d_ktime);
     hipHostFree(c->h_state);
+    hipFree(c->d_pin_state); hipFree(c->d_pin_partials); hipHostFree(c->h_pin_state);
     hipFree(c->d_match_desc); hipFree(c->d_unary); hipFree(c->d_bin); hipFree(c->d_vhash);
     hipHostFree(c->h_unary); hipHostFree(c->h_bin);
     hipStreamDestroy(c->stream);
@@ -389,6 +390,7 @@ extern "C" void r360_frame_destroy(r360_frame* f) {
     // outlive their context at interpreter shutdown.
     hipFree(f->d_bgr); hipFree(f->d_depth); hipFree(f->d_depth_m); hipFree(f->d_sph_bgr); hipFree(f->d_sph_depth);
     for (int l = 0; l < f->n_levels; ++l) { hipFree(f->lv[l].p0); hipFree(f->lv[l].tg); }
+    for (int l = 0; l < f->n_slevels; ++l) { hipFree(f->sp[l].p0); hipFree(f->sp[l].tg); }
     plane_bufs_free(f);
     delete f->sphere_cloud;
     delete f;
@@ -426,6 +428,10 @@ extern "C" int r360_frame_build_async(r360_frame* f, unsigned flags) {
     if (flags & R360_BUILD_PYRAMID) {
         if (launch_pyramid(f)) return -1;
         f->built |= R360_BUILD_PYRAMID;
+    }
+    if (flags & R360_BUILD_SENSOR_PYRAMID) {
+        if (launch_sensor_pyramid(f)) return -1;
+        f->built |= R360_BUILD_SENSOR_PYRAMID;
     }
     if (flags & (R360_BUILD_CLOUD | R360_BUILD_PLANES)) {
         // buildSphereCloud + getPlanes (Frame360.h:467-510, 615-640): the per-pixel part is enqueued
@@ -473,20 +479,16 @@ extern "C" int r360_frame_get_depth_m(r360_frame* f, float* depth8) {
     return 0;
 }
 
-extern "C" int r360_frame_get_level(r360_frame* f, int level, int* rows, int* cols, float* gray, float* depth,
-                                    float* gx, float* gy, float* dgx, float* dgy) {
-    CHECK_ARG(f, "null frame");
-    CHECK_ARG(level >= 0 && level < f->n_levels, "level out of range");
-    CHECK_ARG(f->built & R360_BUILD_PYRAMID, "pyramid not built");
-    const LevelBufs& L = f->lv[level];
-    if (rows) *rows = L.rows;
-    if (cols) *cols = L.cols;
-    const size_t n = (size_t)L.rows * L.cols;
+static int copy_level(r360_frame* f, const float2* d_p0, const float4* d_tg, int R, int C, int* rows, int* cols,
+                      float* gray, float* depth, float* gx, float* gy, float* dgx, float* dgy) {
+    if (rows) *rows = R;
+    if (cols) *cols = C;
+    const size_t n = (size_t)R * C;
     R360_HIP(hipStreamSynchronize(f->ctx->stream));
     std::vector<float2> p0(n);
     std::vector<float4> tg(n);
-    R360_HIP(hipMemcpy(p0.data(), L.p0, n * sizeof(float2), hipMemcpyDeviceToHost));
-    R360_HIP(hipMemcpy(tg.data(), L.tg, n * sizeof(float4), hipMemcpyDeviceToHost));
+    R360_HIP(hipMemcpy(p0.data(), d_p0, n * sizeof(float2), hipMemcpyDeviceToHost));
+    R360_HIP(hipMemcpy(tg.data(), d_tg, n * sizeof(float4), hipMemcpyDeviceToHost));
     for (size_t i = 0; i < n; ++i) {
         if (gray) gray[i] = p0[i].x;
         if (depth) depth[i] = p0[i].y;
@@ -496,6 +498,26 @@ extern "C" int r360_frame_get_level(r360_frame* f, int level, int* rows, int* co
         if (dgy) dgy[i] = tg[i].w;
     }
     return 0;
+}
+
+extern "C" int r360_frame_get_level(r360_frame* f, int level, int* rows, int* cols, float* gray, float* depth,
+                                    float* gx, float* gy, float* dgx, float* dgy) {
+    CHECK_ARG(f, "null frame");
+    CHECK_ARG(level >= 0 && level < f->n_levels, "level out of range");
+    CHECK_ARG(f->built & R360_BUILD_PYRAMID, "pyramid not built");
+    const LevelBufs& L = f->lv[level];
+    return copy_level(f, L.p0, L.tg, L.rows, L.cols, rows, cols, gray, depth, gx, gy, dgx, dgy);
+}
+
+extern "C" int r360_frame_get_sensor_level(r360_frame* f, int sensor, int level, int* rows, int* cols, float* gray,
+                                           float* depth, float* gx, float* gy, float* dgx, float* dgy) {
+    CHECK_ARG(f, "null frame");
+    CHECK_ARG(f->built & R360_BUILD_SENSOR_PYRAMID, "sensor pyramid not built (R360_BUILD_SENSOR_PYRAMID)");
+    CHECK_ARG(level >= 0 && level < f->n_slevels, "level out of range");
+    CHECK_ARG(sensor >= 0 && sensor < 8, "sensor out of range");
+    const LevelBufs& L = f->sp[level];
+    const size_t off = (size_t)sensor * L.rows * L.cols;
+    return copy_level(f, L.p0 + off, L.tg + off, L.rows, L.cols, rows, cols, gray, depth, gx, gy, dgx, dgy);
 }
 
 // ------------------------------------------------------------------ RegisterPhotoICP

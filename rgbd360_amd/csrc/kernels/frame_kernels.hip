@@ -88,11 +88,16 @@ __device__ __forceinline__ int refl101(int p, int n) {
 }
 
 // ------------------------------------------------------------------ pyramid (level l -> l+1)
-__global__ void k_pyramid(const float2* __restrict__ in, int R, int C, float2* __restrict__ out, float min_d,
-                          float max_d) {
+// nimg images of R x C stored back to back (the sphere: 1; the per-sensor pyramids: 8)
+__global__ void k_pyramid(const float2* __restrict__ in_all, int R, int C, float2* __restrict__ out_all, float min_d,
+                          float max_d, int nimg) {
     const int dr = R / 2, dc = C / 2;
-    const long n = (long)dr * dc;
-    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long per = (long)dr * dc, n = per * nimg;
+    for (long j = blockIdx.x * (long)blockDim.x + threadIdx.x; j < n; j += (long)gridDim.x * blockDim.x) {
+        const int img = (int)(j / per);
+        const long i = j - (long)img * per;
+        const float2* in = in_all + (long)img * R * C;
+        float2* out = out_all + (long)img * per;
         const int y = (int)(i / dc), x = (int)(i - (long)y * dc);
         // cv::pyrDown: horizontal [1 4 6 4 1] per source row, then the vertical SSE order.
         const int sx = 2 * x;
@@ -129,15 +134,18 @@ __device__ __forceinline__ float harm(float fl, float f, float fr) {
     return 0.f;
 }
 
-__global__ void k_gradient(const float2* __restrict__ p0, int R, int C, float4* __restrict__ tg) {
-    const long n = (long)R * C;
+// seam = 1: the sphere (alignFrames360's seam mask); 0: per-sensor images (alignFrames has none)
+__global__ void k_gradient(const float2* __restrict__ p0, int R, int C, float4* __restrict__ tg, int nimg,
+                           int mask_seams) {
+    const long per = (long)R * C, n = per * nimg;
     const int ws = C / 8;
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-        const int r = (int)(i / C), c = (int)(i - (long)r * C);
+        const long li = i % per;
+        const int r = (int)(li / C), c = (int)(li - (long)r * C);
         float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
         // seam columns s*ws-1 and s*ws, s = 1..7, are zeroed by alignFrames360 (:4538-4549)
         const int m = c % ws;
-        const bool seam = (c >= ws - 1) && (c < 7 * ws + 1) && (m == 0 || m == ws - 1);
+        const bool seam = mask_seams && (c >= ws - 1) && (c < 7 * ws + 1) && (m == 0 || m == ws - 1);
         if (!seam && r >= 1 && r < R - 1 && c >= 1 && c < C - 1) {
             const float2 f = p0[i], fl = p0[i - 1], fr = p0[i + 1], fu = p0[i - C], fd = p0[i + C];
             o.x = harm(fl.x, f.x, fr.x);
@@ -146,6 +154,17 @@ __global__ void k_gradient(const float2* __restrict__ p0, int R, int C, float4* 
             o.w = harm(fu.y, f.y, fd.y);
         }
         tg[i] = o;
+    }
+}
+
+// setSourceFrame / setTargetFrame level 0 of each sensor's raw images (:480-516): CV_RGB2GRAY on the
+// BGR-stored data /255, and the u16 depth * 0.001 (buildPyramidRange :316-317)
+__global__ void k_sensor_level0(const uint8_t* __restrict__ bgr8, const uint16_t* __restrict__ depth8, long n,
+                                float2* __restrict__ p0) {
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+        const int b = bgr8[3 * i], g = bgr8[3 * i + 1], r = bgr8[3 * i + 2];
+        const int y = (b * 4899 + g * 9617 + r * 1868 + (1 << 13)) >> 14;
+        p0[i] = make_float2((float)y * (float)(1. / 255), (float)depth8[i] * 0.001f);
     }
 }
 
@@ -187,12 +206,46 @@ int launch_pyramid(r360_frame* f) {
     for (int l = 1; l < f->n_levels; ++l) {
         const long n = (long)f->lv[l].rows * f->lv[l].cols;
         hipLaunchKernelGGL(k_pyramid, dim3(grid_for(n)), dim3(TPB), 0, f->ctx->stream, f->lv[l - 1].p0,
-                           f->lv[l - 1].rows, f->lv[l - 1].cols, f->lv[l].p0, min_d, max_d);
+                           f->lv[l - 1].rows, f->lv[l - 1].cols, f->lv[l].p0, min_d, max_d, 1);
     }
     for (int l = 0; l < f->n_levels; ++l) {
         const long n = (long)f->lv[l].rows * f->lv[l].cols;
         hipLaunchKernelGGL(k_gradient, dim3(grid_for(n)), dim3(TPB), 0, f->ctx->stream, f->lv[l].p0, f->lv[l].rows,
-                           f->lv[l].cols, f->lv[l].tg);
+                           f->lv[l].cols, f->lv[l].tg, 1, 1);
+    }
+    R360_HIP(hipGetLastError());
+    return 0;
+}
+
+// The 8 sensors' pinhole pyramids (RegisterPhotoICP::setSourceFrame / setTargetFrame on
+// frameRGBD_[k].getRGBImage() / getDepthImage(), MethodsRegisterRGBD360.cpp:337-338), all sensors per
+// launch.  Levels are allocated on first use.
+int launch_sensor_pyramid(r360_frame* f) {
+    const float min_d = 0.3f, max_d = 6.0f;
+    if (!f->n_slevels) {
+        int R = f->rows, C = f->cols, nl = 0;
+        while (nl < R360_MAX_PYR) {
+            f->sp[nl].rows = R; f->sp[nl].cols = C;
+            R360_HIP(hipMalloc(&f->sp[nl].p0, sizeof(float2) * 8 * (size_t)R * C));
+            R360_HIP(hipMalloc(&f->sp[nl].tg, sizeof(float4) * 8 * (size_t)R * C));
+            ++nl;
+            if ((R & 1) || (C & 1) || R < 8 || C < 8) break;   // cv::pyrDown halves exactly only even sizes
+            R /= 2; C /= 2;
+        }
+        f->n_slevels = nl;
+    }
+    hipStream_t st = f->ctx->stream;
+    const long n0 = 8L * f->rows * f->cols;
+    hipLaunchKernelGGL(k_sensor_level0, dim3(grid_for(n0)), dim3(TPB), 0, st, f->d_bgr, f->d_depth, n0, f->sp[0].p0);
+    for (int l = 1; l < f->n_slevels; ++l) {
+        const long n = 8L * f->sp[l].rows * f->sp[l].cols;
+        hipLaunchKernelGGL(k_pyramid, dim3(grid_for(n)), dim3(TPB), 0, st, f->sp[l - 1].p0, f->sp[l - 1].rows,
+                           f->sp[l - 1].cols, f->sp[l].p0, min_d, max_d, 8);
+    }
+    for (int l = 0; l < f->n_slevels; ++l) {
+        const long n = 8L * f->sp[l].rows * f->sp[l].cols;
+        hipLaunchKernelGGL(k_gradient, dim3(grid_for(n)), dim3(TPB), 0, st, f->sp[l].p0, f->sp[l].rows, f->sp[l].cols,
+                           f->sp[l].tg, 8, 0);
     }
     R360_HIP(hipGetLastError());
     return 0;

@@ -51,18 +51,7 @@ struct Gather {
 __device__ unsigned long long g_blk_stamps[2][8192];  // per-workgroup start / loop end (diagnostic build)
 #endif
 
-__device__ __forceinline__ float huberf(float e, float reg) {  // weightHuber<float> (:545-554)
-    const float a = fabsf(e);
-    if (a < reg) return 1.f;
-    return sqrtf(2 * reg * a - reg * reg) / a;
-}
-
-// Accumulator slots: 0..20 upper-triangle H (row-major), 21..26 g, 27 n_valid, 28 n_visible.
-struct Acc {
-    float h[32];
-    double err2;    // squared weighted residuals (occlusion variants: photometric only)
-    double err2d;   // occlusion variants: depth squared weighted residuals
-};
+#include "icp_common.inc"
 
 // occlusion flags per source pixel (k_occ_resolve): bit 0 accepted by the target Z-buffer (a prefix
 // maximum of 1/|p'| in LUT order), bit 1 the last accepted point of its target pixel, bit 2 the last
@@ -143,19 +132,6 @@ __device__ __forceinline__ bool project_fix(Proj& o, int nRows, int nCols, float
         changed = o.t != t0 || o.vis != v0;
     }
     return __any(changed);
-}
-
-__device__ __forceinline__ void acc_fma(Acc& A, const float J[6], float r) {
-#pragma clang fp contract(fast)
-    A.h[0] += J[0] * J[0]; A.h[1] += J[0] * J[1]; A.h[2] += J[0] * J[2];
-    A.h[3] += J[0] * J[3]; A.h[4] += J[0] * J[4]; A.h[5] += J[0] * J[5];
-    A.h[6] += J[1] * J[1]; A.h[7] += J[1] * J[2]; A.h[8] += J[1] * J[3];
-    A.h[9] += J[1] * J[4]; A.h[10] += J[1] * J[5]; A.h[11] += J[2] * J[2];
-    A.h[12] += J[2] * J[3]; A.h[13] += J[2] * J[4]; A.h[14] += J[2] * J[5];
-    A.h[15] += J[3] * J[3]; A.h[16] += J[3] * J[4]; A.h[17] += J[3] * J[5];
-    A.h[18] += J[4] * J[4]; A.h[19] += J[4] * J[5]; A.h[20] += J[5] * J[5];
-    A.h[21] += J[0] * r; A.h[22] += J[1] * r; A.h[23] += J[2] * r;
-    A.h[24] += J[3] * r; A.h[25] += J[4] * r; A.h[26] += J[5] * r;
 }
 
 // Residuals, weights and Jacobian rows of one projected pixel, accumulated branch-free: a pixel that
@@ -251,41 +227,6 @@ __device__ __forceinline__ void contribute(Acc& A, const Proj& o, const float4 G
         for (int k = 0; k < 6; ++k) J[k] = jd ? wd * J[k] : 0.f;
         acc_fma(A, J, jd ? wd * depthDiff : 0.f);
     }
-}
-
-// Butterfly reduce-scatter of 32 floats across a 64-lane wave: 32 shuffles instead of 32*6.
-// On return lane L holds the wave total of slot idx(L) = (bit5 bit4 bit3 bit2 bit1 of L) in a
-// fixed bit order, identical for lanes L and L^1.
-template <int M, int HALF>
-__device__ __forceinline__ void bfly_step(float (&v)[32], int lane) {
-    const bool hi = (lane & M) != 0;
-#pragma unroll
-    for (int j = 0; j < HALF; ++j) {
-        const float keep = hi ? v[j + HALF] : v[j];
-        const float send = hi ? v[j] : v[j + HALF];
-        v[j] = keep + __shfl_xor(send, M, 64);
-    }
-}
-
-__device__ __forceinline__ float wave_reduce_scatter32(float (&v)[32], int lane) {
-    bfly_step<32, 16>(v, lane);
-    bfly_step<16, 8>(v, lane);
-    bfly_step<8, 4>(v, lane);
-    bfly_step<4, 2>(v, lane);
-    bfly_step<2, 1>(v, lane);
-    return v[0] + __shfl_xor(v[0], 1, 64);
-}
-
-__device__ __forceinline__ int scatter_slot(int lane) {
-    // step with mask 32 selects the upper half (+16), mask 16 -> +8, ... mask 2 -> +1
-    return ((lane >> 5) & 1) * 16 + ((lane >> 4) & 1) * 8 + ((lane >> 3) & 1) * 4 + ((lane >> 2) & 1) * 2 +
-           ((lane >> 1) & 1);
-}
-
-__device__ __forceinline__ double wave_sum_d(double x) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) x += __shfl_xor(x, m, 64);
-    return x;
 }
 
 // ---------------------------------------------------------------- GN step (thread 0 of last block)

@@ -66,6 +66,9 @@ struct alignas(16) IcpState {
     int iters[8], evals_l[8];
     unsigned ticket;
     int pad1;
+    double lm_lambda;   // alignFrames (pinhole) Levenberg-Marquardt lambda (:4301)
+    int lm_phase;       // 0: the pending candidate is the undamped step, 1: the LM retry (:4381-4412)
+    int pad2;
     double sums[32];    // last pass sums (eval mode)
     unsigned long long dbg[12];  // s_memrealtime stamps of the diagnostic build (-DR360_STAMPS)
 };
@@ -188,6 +191,11 @@ struct r360_ctx {
     std::vector<std::pair<std::string, Acc>> acc;
     // async-align bookkeeping
     int async_nL = 0, async_pending = 0;
+    // pinhole alignFrames (pinhole_kernels.hip): one state and one record area per job (sensor)
+    IcpState* d_pin_state = nullptr;
+    double* d_pin_partials = nullptr;
+    IcpState* h_pin_state = nullptr;   // pinned
+    int pin_pending = 0;
     // PbMap matcher scratch (k_match_tables)
     int match_cap = 0;                       // planes per subgraph
     float* d_match_desc = nullptr;
@@ -248,6 +256,9 @@ struct r360_frame {
     uint8_t* d_sph_bgr = nullptr;  // [H][W][3]
     uint16_t* d_sph_depth = nullptr;
     LevelBufs lv[R360_MAX_PYR];
+    // per-sensor pinhole pyramids (R360_BUILD_SENSOR_PYRAMID): level l = [8][rows>>l][cols>>l], no seam mask
+    LevelBufs sp[R360_MAX_PYR];
+    int n_slevels = 0;
     unsigned built = 0;
     PlaneBufs pl;
     PbMapHost* pbmap = nullptr;
@@ -259,6 +270,12 @@ struct r360_frame {
 int launch_undistort(r360_frame* f);
 int launch_stitch(r360_frame* f);
 int launch_pyramid(r360_frame* f);
+int launch_sensor_pyramid(r360_frame* f);
+// pinhole alignFrames: intrinsics of level 0 (setCameraMatrix) and the jobs of one batched launch
+struct PinJobs { int sensor[8]; int n; };
+constexpr int R360_PIN_MAX_BLOCKS = 256;   // workgroups per job and pass (record area per job)
+int launch_pin_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src, int level, int method,
+                     const IcpConst& C, const float K[4], const PinJobs& J, int first, int eval_only);
 int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src, int level,
                      int method, const IcpConst& C, int first, int eval_only);
 int icp_blocks_for(int n_pixels);
