@@ -11,6 +11,7 @@
 //                                                  RegisterPbMap :276, getPose :199, getCovMat :208,
 //                                                  getInfoMat :219, getMatchedPlanes :242,
 //                                                  getAreaMatched :251, areaSource/areaTarget :91-94,
+//                                                  RegisterDensePhotoICP :344,
 //                                                  Register() = OdometryKeyFrame360.cpp:205-254
 //
 // Header-only; every body is a call into the C-ABI (include/rgbd360_hip.h).  Matrices are the
@@ -310,8 +311,25 @@ class RegisterRGBD360 {
                              "Register");
         return rc == 0;
     }
+    // RegisterDensePhotoICP (RegisterRGBD360.h:344-520): frame2's 8 sensor images aligned to frame1's, the
+    // Jacobians in the rig frame (calcPhotoICPError_robot / calcHessianGradient_robot).  As in the reference,
+    // rigidTransf = pose_estim and informationM = the last level's Hessian; false = ILL-POSED.
+    bool RegisterDensePhotoICP(Frame360* frame1, Frame360* frame2, Matrix4f pose_estim = Matrix4f::Identity(),
+                               RegisterPhotoICP::costFuncType method = RegisterPhotoICP::PHOTO_CONSISTENCY,
+                               registrationType registMode = DEFAULT_6DoF) {
+        check(r360_frame_build(frame1->get(), R360_BUILD_SENSOR_PYRAMID), "setTargetFrame (sensor pyramids)");
+        check(r360_frame_build(frame2->get(), R360_BUILD_SENSOR_PYRAMID), "setSourceFrame (sensor pyramids)");
+        const int rc = check(r360_register_dense(ctx_.get(), frame1->get(), frame2->get(), pose_estim.data(), method,
+                                                 registMode, nullptr, rigidTransf_.data(), informationM_.data(),
+                                                 &dense_st_),
+                             "RegisterDensePhotoICP");
+        done_ = true;                   // bRegistrationDone (:509)
+        return rc == 1;
+    }
+    const r360_dense_stats& denseStats() const { return dense_st_; }
     float areaSource = 0.f, areaTarget = 0.f;
   private:
+    r360_dense_stats dense_st_{};
     Context& ctx_;
     std::string config_;
     Frame360* ref_ = nullptr;

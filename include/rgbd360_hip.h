@@ -172,6 +172,36 @@ int r360_pinhole_eval(r360_ctx* ctx, r360_frame* trg, r360_frame* src, int senso
                       int method, const float* K, const r360_icp_params* p, double H[36], double g[6],
                       double* error, double res[2], int counts[3]);
 
+/* ---------------------------------------------------------------- RegisterDensePhotoICP (A19)
+ * RegisterRGBD360::RegisterDensePhotoICP(frame1, frame2, pose_estim, method, registMode)
+ * (RegisterRGBD360.h:344-520): the 8 sensors' pinhole images of frame2 (source) against frame1's
+ * (target), Jacobians in the rig frame (calcPhotoICPError_robot, RegisterPhotoICP.h:4905-5076;
+ * calcHessianGradient_robot, :5083-5407), sensors summed, LM per level (lambda 1e-3, step 10,
+ * tol_residual 0.1).  Frames need R360_BUILD_SENSOR_PYRAMID; p = NULL uses RegisterPhotoICP()'s
+ * defaults (4 levels).  As in the reference, the "new" error is evaluated at the unchanged pose, so
+ * pose_out = pose_estim and info_out = the Hessian of the last level whose loop ran.
+ * Returns 1 (the reference's true) or 0 (ILL-POSED: false, info_out untouched). */
+typedef struct {
+    double error[8];            /* per level: sum over sensors of calcPhotoICPError_robot   */
+    int    ran[8];              /* 1 if the level's LM loop ran (error > tol_residual 0.1)   */
+    int    n_visible[8];        /* HessGrad visible pixels per level, 8 sensors             */
+    int    n_error[8];          /* error-term visible pixels per level, 8 sensors           */
+    int    illposed_level;      /* -1, or the level whose rank test failed                  */
+    int    levels;
+    int    info_set;            /* 0 if no level ran (the reference's Hessian is then undefined; info = 0) */
+    int    pad;
+    float  gradient[6];         /* the summed gradient of that level                        */
+} r360_dense_stats;
+int r360_register_dense(r360_ctx* ctx, r360_frame* frame1, r360_frame* frame2, const float pose_estim[16],
+                        int method, int mode, const r360_icp_params* p, float pose_out[16], float info_out[36],
+                        r360_dense_stats* st);
+/* Parity hook: one level's 8 sensors at `pose`: err[2k] / err[2k+1] = sensor k's photometric / depth
+ * part of calcPhotoICPError_robot, H / g = calcHessianGradient_robot's (double sums of the float
+ * terms), counts[3k..] = {error visible, error depth terms, HessGrad visible}. */
+int r360_dense_robot_eval(r360_ctx* ctx, r360_frame* frame1, r360_frame* frame2, int level, const float pose[16],
+                          int method, const r360_icp_params* p, double err[16], double H[8 * 36], double g[8 * 6],
+                          int counts[8 * 3]);
+
 /* CPose3D::exp(mu, pseudo) (MRPT; used at RegisterPhotoICP.h:4697). */
 void r360_exp_se3(const double mu[6], int pseudo, float T[16]);
 

@@ -41,6 +41,11 @@ class IcpStats(C.Structure):
                 ("error", C.c_double)]
 
 
+class DenseStats(C.Structure):
+    _fields_ = [("error", C.c_double * 8), ("ran", C.c_int * 8), ("iters", C.c_int * 8), ("illposed_level", C.c_int),
+                ("info_set", C.c_int), ("gradient", C.c_float * 6)]
+
+
 class Level(C.Structure):
     _fields_ = [("rows", C.c_int), ("cols", C.c_int)] + [
         (n, C.POINTER(C.c_float)) for n in ("gray_src", "depth_src", "gray_trg", "depth_trg", "gx", "gy", "dgx", "dgy")]
@@ -112,6 +117,12 @@ def lib() -> C.CDLL:
                                             C.POINTER(IcpParams), dp, dp, ip]),
             "orc_align_pinhole": (C.c_int, [vp, vp, vp, vp, C.c_int, C.c_int, C.POINTER(Pinhole), fp, C.c_int,
                                             C.POINTER(IcpParams), fp, fp, fp, C.POINTER(IcpStats)]),
+            "orc_error_robot": (C.c_double, [C.POINTER(Level), C.c_int, C.c_int, C.c_int, fp, fp, fp, C.c_int,
+                                             C.POINTER(IcpParams), dp, dp, ip]),
+            "orc_hessgrad_robot": (None, [C.POINTER(Level), C.c_int, C.c_int, C.c_int, fp, fp, fp, C.c_int,
+                                          C.POINTER(IcpParams), fp, fp, dp, dp, ip]),
+            "orc_register_dense_robot": (C.c_int, [vp, vp, vp, vp, C.c_int, C.c_int, fp, fp, fp, C.c_int,
+                                                   C.POINTER(IcpParams), fp, fp, C.POINTER(DenseStats)]),
             "orc_exp_se3": (None, [dp, C.c_int, fp]),
             "orc_huber": (C.c_float, [C.c_float, C.c_float]),
             "orc_libm": (None, [fp, fp, fp, C.c_int, fp, fp]),
@@ -373,6 +384,49 @@ def align_pinhole(trg_bgr, trg_dep, src_bgr, src_dep, K: Pinhole | None = None, 
     rc = lib().orc_align_pinhole(_v(trg_bgr), _v(trg_dep), _v(src_bgr), _v(src_dep), rows, cols, C.byref(K),
                                  _f(init16), method, C.byref(p), _f(po), _f(Ho), _f(go), C.byref(st))
     return rc, from16(po), Ho.reshape(6, 6).T.copy(), go, st
+
+
+# ---------------------------------------------------------------- A19 RegisterDensePhotoICP (robot frame)
+def error_robot(src: dict, trg: dict, rows0: int, cols0: int, level: int, pose, rt, rt_inv, method=PHOTO,
+                params: IcpParams | None = None):
+    """calcPhotoICPError_robot (:4905-5076) of one sensor -> (error2, photo_sum, depth_sum, n_visible, n_depth)."""
+    L, keep = _level_struct(src, trg)
+    p = params or IcpParams.default()
+    eP, eD, cnt = C.c_double(), C.c_double(), np.zeros(2, np.int32)
+    e = lib().orc_error_robot(C.byref(L), rows0, cols0, level, _f(mat16(pose)), _f(mat16(rt)), _f(mat16(rt_inv)),
+                              method, C.byref(p), C.byref(eP), C.byref(eD), cnt.ctypes.data_as(C.POINTER(C.c_int)))
+    return e, eP.value, eD.value, int(cnt[0]), int(cnt[1])
+
+
+def hessgrad_robot(src: dict, trg: dict, rows0: int, cols0: int, level: int, pose, rt, rt_inv,
+                   method=PHOTO, params: IcpParams | None = None):
+    """calcHessianGradient_robot (:5083-5407) of one sensor -> (Hf, gf (float, raster order, the reference's),
+    Hd, gd (the same terms summed in double), n_visible)."""
+    L, keep = _level_struct(src, trg)
+    p = params or IcpParams.default()
+    Hf, gf, Hd, gd, nv = np.zeros(36, np.float32), np.zeros(6, np.float32), np.zeros(36), np.zeros(6), C.c_int()
+    dp = C.POINTER(C.c_double)
+    lib().orc_hessgrad_robot(C.byref(L), rows0, cols0, level, _f(mat16(pose)), _f(mat16(rt)), _f(mat16(rt_inv)),
+                             method, C.byref(p), _f(Hf), _f(gf), Hd.ctypes.data_as(dp), gd.ctypes.data_as(dp),
+                             C.byref(nv))
+    return Hf.reshape(6, 6), gf, Hd.reshape(6, 6), gd, nv.value
+
+
+def register_dense_robot(bgr1, dep1, bgr2, dep2, rt8, rt_inv8, init=None, method=PHOTO,
+                         params: IcpParams | None = None):
+    """RegisterDensePhotoICP(frame1, frame2, pose_estim, method) (RegisterRGBD360.h:344-520).
+    rt8 / rt_inv8: [8,4,4].  Returns (ok, pose, informationM, DenseStats)."""
+    bgr1, dep1, bgr2, dep2 = [np.ascontiguousarray(a) for a in (bgr1, dep1, bgr2, dep2)]
+    rows, cols = dep1.shape[1], dep1.shape[2]
+    p = params or IcpParams.default()
+    r8 = np.concatenate([mat16(m) for m in rt8]).astype(np.float32)
+    ri8 = np.concatenate([mat16(m) for m in rt_inv8]).astype(np.float32)
+    init16 = mat16(np.eye(4) if init is None else init)
+    po, info = np.zeros(16, np.float32), np.zeros(36, np.float32)
+    st = DenseStats()
+    ok = lib().orc_register_dense_robot(_v(bgr1), _v(dep1), _v(bgr2), _v(dep2), rows, cols, _f(r8), _f(ri8),
+                                        _f(init16), method, C.byref(p), _f(po), _f(info), C.byref(st))
+    return ok == 1, from16(po), info.reshape(6, 6).T.copy(), st
 
 
 def exp_se3(mu, pseudo=True) -> np.ndarray:

@@ -127,6 +127,28 @@ void orc_exp_se3(const double mu[6], int pseudo, float T[16]);
 void orc_libm(const float* x, const float* y, const float* z, int n, float* asin_out, float* atan2_out);
 
 /* Huber weight (RegisterPhotoICP.h:545-554), float instantiation */
+/* ---- A19: RegisterDensePhotoICP (RegisterRGBD360.h:344-520) with calcPhotoICPError_robot
+ * (RegisterPhotoICP.h:4905-5076) / calcHessianGradient_robot (:5083-5407).  rows0/cols0 = level-0 image
+ * size (camIntrinsicMat).  Returns error2; photo/depth parts and {visible, depth terms} on the side. */
+double orc_error_robot(const orc_level* L, int rows0, int cols0, int level, const float pose[16],
+                       const float rt[16], const float rt_inv[16], int method, const orc_icp_params* p,
+                       double* photo_sum, double* depth_sum, int counts[2]);
+/* Hf / gf: float accumulation in raster order (the reference's); Hd / gd: the same terms summed in double. */
+void   orc_hessgrad_robot(const orc_level* L, int rows0, int cols0, int level, const float pose[16],
+                          const float rt[16], const float rt_inv[16], int method, const orc_icp_params* p,
+                          float Hf[36], float gf[6], double Hd[36], double gd[6], int* n_vis);
+typedef struct {
+    double error[8];
+    int    ran[8], iters[8];
+    int    illposed_level, info_set;
+    float  gradient[6];
+} orc_dense_stats;
+/* frame1 = target, frame2 = source; [8][rows][cols](x3) raw images; returns 1 (true) / 0 (ILL-POSED). */
+int    orc_register_dense_robot(const uint8_t* bgr1, const uint16_t* dep1, const uint8_t* bgr2,
+                                const uint16_t* dep2, int rows, int cols, const float* rt8, const float* rt_inv8,
+                                const float init[16], int method, const orc_icp_params* p, float pose_out[16],
+                                float info_out[36], orc_dense_stats* st);
+
 float orc_huber(float err, float reg);
 
 /* =============================== plane half (A3-A9, A11-A13) ===============================

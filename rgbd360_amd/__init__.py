@@ -62,6 +62,13 @@ class IcpStats(C.Structure):
     ]
 
 
+class DenseStats(C.Structure):
+    """r360_dense_stats — RegisterDensePhotoICP per-level diagnostics."""
+    _fields_ = [("error", C.c_double * 8), ("ran", C.c_int * 8), ("n_visible", C.c_int * 8), ("n_error", C.c_int * 8),
+                ("illposed_level", C.c_int), ("levels", C.c_int), ("info_set", C.c_int), ("pad", C.c_int),
+                ("gradient", C.c_float * 6)]
+
+
 class Plane(C.Structure):
     """r360_plane — the mrpt::pbmap::Plane fields used on the path (rig frame)."""
     _fields_ = [("normal", C.c_float * 3), ("center", C.c_float * 3), ("d", C.c_float), ("area", C.c_float),
@@ -139,6 +146,10 @@ _SIGS = [
     ("r360_align_pinhole_result", C.c_int, [_P, _FP, _FP, _FP, C.POINTER(IcpStats)]),
     ("r360_pinhole_eval", C.c_int, [_P, _P, _P, C.c_int, C.c_int, _FP, C.c_int, _FP, C.POINTER(IcpParams), _DP, _DP,
                                     _DP, _DP, _IP]),
+    ("r360_register_dense", C.c_int, [_P, _P, _P, _FP, C.c_int, C.c_int, C.POINTER(IcpParams), _FP, _FP,
+                                      C.POINTER(DenseStats)]),
+    ("r360_dense_robot_eval", C.c_int, [_P, _P, _P, C.c_int, _FP, C.c_int, C.POINTER(IcpParams), _DP, _DP, _DP,
+                                        _IP]),
     ("r360_frame_get_planes", C.c_int, [_P, C.POINTER(Plane), C.c_int, _IP]),
     ("r360_frame_get_plane_hull", C.c_int, [_P, C.c_int, _FP, C.c_int, _IP]),
     ("r360_register_pbmap", C.c_int, [_P, _P, _P, C.c_size_t, C.c_int, _FP, _FP, _IP, C.c_int, _IP, _FP, _FP, _FP]),
@@ -540,6 +551,36 @@ class RegisterRGBD360:
             self.informationM = info.reshape(6, 6).T.copy()
             self.areaSource, self.areaTarget = as_.value, at.value
         return rc == 1
+
+    def RegisterDensePhotoICP(self, frame1, frame2, pose_estim=None, method: int = PHOTO_CONSISTENCY,
+                              registMode: int = DEFAULT_6DoF, params: "IcpParams | None" = None) -> bool:
+        """RegisterDensePhotoICP (RegisterRGBD360.h:344-520): frame2's 8 sensor images aligned to frame1's in
+        the rig frame.  Frames need BUILD_SENSOR_PYRAMID.  params None = RegisterPhotoICP()'s defaults."""
+        init = _mat16(np.eye(4) if pose_estim is None else pose_estim)
+        po = np.zeros(16, np.float32)
+        info = np.ascontiguousarray(self.informationM.T).reshape(36).copy()
+        self.dense_stats = DenseStats()
+        rc = _check(lib().r360_register_dense(self.ctx.h, frame1.h, frame2.h, _fptr(init), method, registMode,
+                                              None if params is None else C.byref(params), _fptr(po), _fptr(info),
+                                              C.byref(self.dense_stats)), "RegisterDensePhotoICP")
+        self.rigidTransf = _from16(po)
+        if rc == 1:
+            self.informationM = info.reshape(6, 6).T.copy()
+        return rc == 1
+
+    def eval_dense_robot(self, frame1, frame2, level: int, pose, method: int = PHOTO_CONSISTENCY,
+                         params: "IcpParams | None" = None):
+        """Per-sensor calcPhotoICPError_robot / calcHessianGradient_robot at `pose` on one level ->
+        dict(err_photo[8], err_depth[8], H[8,6,6], g[8,6], n_error[8], n_depth[8], n_vis[8])."""
+        err, H, g = np.zeros(16), np.zeros(8 * 36), np.zeros(8 * 6)
+        cnt = np.zeros(24, np.int32)
+        _check(lib().r360_dense_robot_eval(self.ctx.h, frame1.h, frame2.h, level, _fptr(_mat16(pose)), method,
+                                           None if params is None else C.byref(params), err.ctypes.data_as(_DP),
+                                           H.ctypes.data_as(_DP), g.ctypes.data_as(_DP), cnt.ctypes.data_as(_IP)),
+               "eval_dense_robot")
+        c = cnt.reshape(8, 3)
+        return dict(err_photo=err[0::2].copy(), err_depth=err[1::2].copy(), H=H.reshape(8, 6, 6), g=g.reshape(8, 6),
+                    n_error=c[:, 0].copy(), n_depth=c[:, 1].copy(), n_vis=c[:, 2].copy())
 
     def getPose(self): return self.rigidTransf
     def getInfoMat(self): return self.informationM

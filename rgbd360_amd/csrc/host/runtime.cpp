@@ -127,6 +127,8 @@ extern "C" void r360_ctx_destroy(r360_ctx* c) {
     hipFree(c->d_ktime);
     hipHostFree(c->h_state);
     hipFree(c->d_pin_state); hipFree(c->d_pin_partials); hipHostFree(c->h_pin_state);
+    hipFree(c->d_rob_jobs); hipFree(c->d_rob_partials); hipFree(c->d_rob_sums); hipFree(c->d_rob_tickets);
+    hipFree(c->d_rob_out); hipHostFree(c->h_rob_jobs); hipHostFree(c->h_rob_sums); hipHostFree(c->h_rob_out);
     hipFree(c->d_match_desc); hipFree(c->d_unary); hipFree(c->d_bin); hipFree(c->d_vhash);
     hipHostFree(c->h_unary); hipHostFree(c->h_bin);
     hipStreamDestroy(c->stream);

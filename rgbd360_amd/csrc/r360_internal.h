@@ -196,6 +196,15 @@ struct r360_ctx {
     double* d_pin_partials = nullptr;
     IcpState* h_pin_state = nullptr;   // pinned
     int pin_pending = 0;
+    // RegisterDensePhotoICP (robot_kernels.hip): job table, per-job records / sums / tickets, result
+    struct RobotJob* d_rob_jobs = nullptr;
+    struct RobotJob* h_rob_jobs = nullptr;     // pinned
+    double* d_rob_partials = nullptr;
+    double* d_rob_sums = nullptr;
+    double* h_rob_sums = nullptr;              // pinned
+    unsigned* d_rob_tickets = nullptr;
+    struct RobotOut* d_rob_out = nullptr;
+    struct RobotOut* h_rob_out = nullptr;      // pinned
     // PbMap matcher scratch (k_match_tables)
     int match_cap = 0;                       // planes per subgraph
     float* d_match_desc = nullptr;
@@ -276,6 +285,29 @@ struct PinJobs { int sensor[8]; int n; };
 constexpr int R360_PIN_MAX_BLOCKS = 256;   // workgroups per job and pass (record area per job)
 int launch_pin_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src, int level, int method,
                      const IcpConst& C, const float K[4], const PinJobs& J, int first, int eval_only);
+// RegisterDensePhotoICP (A19): one job = (pyramid level, sensor); matrices col-major
+struct RobotJob {
+    const float2* src;        // source sensor level {gray, depth}
+    const float2* trg;        // target sensor level {gray, depth}
+    const float4* tg;         // target gradients {gx, gy, dgx, dgy}
+    int rows, cols;
+    float fx, fy, ox, oy, inv_fx, inv_fy;          // calcPhotoICPError_robot's float intrinsics
+    double fxd, fyd, oxd, oyd, inv_fxd, inv_fyd;   // calcHessianGradient_robot's double intrinsics
+    float Mrel[16];           // relPoseCam = Rt^-1 * pose * Rt (float products)
+    float Rt[16], P[16], Rti[16];
+};
+constexpr int R360_ROBOT_MAX_JOBS = 8 * R360_MAX_PYR;
+constexpr int R360_ROBOT_MAX_BLOCKS = 256;
+constexpr int TPB_ROBOT = 256;   // k_robot_pass workgroup size
+struct RobotGrid { int block0[R360_ROBOT_MAX_JOBS + 1]; int njobs; };
+struct RobotOut {
+    float info[36], grad[6];
+    double error[8];
+    int ran[8], n_visible[8], n_error[8];
+    int ok, illposed_level, any, pad;
+};
+int launch_robot(r360_ctx* ctx, const RobotJob* d_jobs, const RobotGrid& grid, int method, const IcpConst& C,
+                 int finalize_levels);
 int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src, int level,
                      int method, const IcpConst& C, int first, int eval_only);
 int icp_blocks_for(int n_pixels);
