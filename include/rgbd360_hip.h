@@ -298,10 +298,16 @@ int r360_synth_path_pose(uint32_t seed, int frame, float pose_out[16]);
 /* ---------------------------------------------------------------- test hooks
  * The float asinf/atan2f program used by the projection (libm_f32.h, bit-identical to x86-64 glibc)
  * evaluated on the host (on_device = 0) or on the GPU (on_device = 1). */
-/* Fast-guarded vs exact spherical projection of points (X, Y, Z) for an nRows x nCols sphere:
- * pixel-decision mismatches (must be 0) and exact fallbacks taken. */
+/* The ICP pass's fast-guarded vs the exact spherical projection of points (X, Y, Z) for an
+ * nRows x nCols sphere: pixel-decision mismatches (must be 0) and deferred (exact) lanes.  _pose:
+ * LUT points (lx, ly, lz) transformed by pose (col-major 4x4) first, fast and exact transforms. */
 int r360_proj_check(const float* X, const float* Y, const float* Z, int n, int nRows, int nCols,
                     unsigned long long* mismatches, unsigned long long* fallbacks);
+int r360_proj_check_pose(const float* lx, const float* ly, const float* lz, int n, const float pose[16], int nRows,
+                         int nCols, unsigned long long* mismatches, unsigned long long* fallbacks);
+/* sqrt_rn / div_rn (the pass's correctly rounded f32 sqrt / division) against the compiler's IEEE
+ * operations on n hashed operands: out = {sqrt mismatches, division mismatches}, both must be 0. */
+int r360_rn_check(unsigned n, unsigned seed, unsigned long long out[2]);
 int r360_libm_eval(const float* x, const float* y, const float* z, int n, float* asin_out, float* atan2_out,
                    int on_device);
 

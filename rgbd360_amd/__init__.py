@@ -165,6 +165,9 @@ _SIGS = [
     ("r360_synth_frame_rt", C.c_int, [C.c_int, C.c_int, _FP, C.c_uint32, _FP, _P, _P]),
     ("r360_synth_path_pose", C.c_int, [C.c_uint32, C.c_int, _FP]),
     ("r360_libm_eval", C.c_int, [_FP, _FP, _FP, C.c_int, _FP, _FP, C.c_int]),
+    ("r360_rn_check", C.c_int, [C.c_uint, C.c_uint, C.POINTER(C.c_ulonglong)]),
+    ("r360_proj_check_pose", C.c_int, [_FP, _FP, _FP, C.c_int, _FP, C.c_int, C.c_int, C.POINTER(C.c_ulonglong),
+                                       C.POINTER(C.c_ulonglong)]),
     ("r360_proj_check", C.c_int, [_FP, _FP, _FP, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_ulonglong),
                                   C.POINTER(C.c_ulonglong)]),
     ("r360_ctx_debug_stamps", C.c_int, [_P, C.POINTER(C.c_ulonglong)]),

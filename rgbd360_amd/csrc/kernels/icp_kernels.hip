@@ -37,6 +37,10 @@ struct Pose12 { float R[9]; float t[3]; };
 // which had moved every gather next to its use and exposed its full latency once per pixel.
 struct Gather {
     __amdgpu_buffer_rsrc_t tg, trg;
+#ifdef R360_EXP_NOGATHER   // experiment builds only (tools/exp_variants.sh): no target loads
+    __device__ __forceinline__ float4 g(int t) const { const float v = (float)(t & 1023) * 1e-3f; return make_float4(v, -v, v, 0.5f * v); }
+    __device__ __forceinline__ float2 T(int t) const { return make_float2((float)(t & 255) * 4e-3f, 2.f); }
+#else
     __device__ __forceinline__ float4 g(int t) const {
         const auto v = __builtin_amdgcn_raw_buffer_load_b128(tg, t * 16, 0, 0);
         return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
@@ -45,6 +49,7 @@ struct Gather {
         const auto v = __builtin_amdgcn_raw_buffer_load_b64(trg, t * 8, 0, 0);
         return make_float2(__uint_as_float(v[0]), __uint_as_float(v[1]));
     }
+#endif
 };
 
 #ifdef R360_STAMPS
@@ -88,6 +93,7 @@ __device__ __forceinline__ void set_pixel(Proj& o, float rr, float cc, bool vali
 // boundary (or whose fast path produced NaN, at the poles) are flagged in o.fix and re-projected
 // exactly by project_fix before their target pixel is used.  Keeping this part branch-free lets the
 // scheduler interleave it with the accumulation of the previous chunk.
+template <bool FASTD = false>
 __device__ __forceinline__ Proj project(const Pose12& P, float d, float gray_s, float sp, float cp, float st, float ct,
                                         int nRows, int nCols, float half_nRows, float angle_res_inv, const IcpConst& C) {
     Proj o;
@@ -100,7 +106,7 @@ __device__ __forceinline__ Proj project(const Pose12& P, float d, float gray_s, 
     float Z = P.R[6] * lx + P.R[7] * ly + P.R[8] * lz; Z = Z + P.t[2];
     const float d2 = X * X + Y * Y + Z * Z;
     // |p'| is exact (it enters the depth residual); the projection itself uses hardware rsq/rcp
-    const float dist = sqrtf(d2);
+    const float dist = FASTD ? __builtin_amdgcn_sqrtf(d2) : sqrtf(d2);
     const float dist_inv = __builtin_amdgcn_rsqf(d2);
     const float phi_trg = r360m::asinf_fast(X * dist_inv);
     const float theta_trg = (float)((double)r360m::atan2f_fast(Y, Z) + R360_PI);
@@ -134,12 +140,85 @@ __device__ __forceinline__ bool project_fix(Proj& o, int nRows, int nCols, float
     return __any(changed);
 }
 
+// LUT_xyz_sphere point of a source pixel (:4578-4582), the reference's float expressions
+struct Lut3 { float x, y, z; bool valid; };
+__device__ __forceinline__ Lut3 lut_point(float d, float sp, float cp, float st, float ct, const IcpConst& C) {
+    Lut3 l;
+    l.valid = (C.min_d < d && d < C.max_d);
+    l.x = d * sp;
+    l.y = -d * cp * st;
+    l.z = -d * cp * ct;
+    return l;
+}
+
+// The reference's projection of one LUT point, start to finish (the deferred lanes of the PF 3 loop):
+// the transform as written, IEEE sqrt / division, glibc-exact asinf / atan2f, theta + pi in double.
+__device__ __forceinline__ Proj project_exact(const Pose12& P, const Lut3& l, float gray_s, int nRows, int nCols,
+                                              float half_nRows, float angle_res_inv) {
+    Proj o;
+    float X = P.R[0] * l.x + P.R[1] * l.y + P.R[2] * l.z; X = X + P.t[0];
+    float Y = P.R[3] * l.x + P.R[4] * l.y + P.R[5] * l.z; Y = Y + P.t[1];
+    float Z = P.R[6] * l.x + P.R[7] * l.y + P.R[8] * l.z; Z = Z + P.t[2];
+    const float dist = sqrtf(X * X + Y * Y + Z * Z);
+    const float dist_inv = 1.f / dist;
+    const float phi_trg = r360m::asinf(X * dist_inv);
+    const float theta_trg = (float)((double)r360m::atan2f_sel(Y, Z) + R360_PI);
+    set_pixel(o, half_nRows - phi_trg * angle_res_inv, theta_trg * angle_res_inv, l.valid, nRows, nCols);
+    o.X = X; o.Y = Y; o.Z = Z; o.dist = dist; o.dist_inv = dist_inv; o.gray_s = gray_s;
+    o.fix = false;
+    return o;
+}
+
+// PF 3 fast projection (never the final word near a rounding boundary): the reference's p' and |p'|
+// (correctly rounded sqrt), then hardware rsq, theta + pi in float, atan2 with one reciprocal, and floor(x + 0.5) rounding
+// (= roundf away from the .5 boundaries, which are all inside the guard bands) that shares its
+// floor with the guard test.  A lane inside a guard band, or NaN, is flagged in o.fix.
+__device__ __forceinline__ Proj project_fast(const Pose12& P, const Lut3& l, float gray_s, int nRows, int nCols,
+                                             float angle_res_inv) {
+    Proj o;
+    // p' and |p'| exactly as the reference (they enter the error terms, which steer the GN decisions)
+    float X = P.R[0] * l.x + P.R[1] * l.y + P.R[2] * l.z; X = X + P.t[0];
+    float Y = P.R[3] * l.x + P.R[4] * l.y + P.R[5] * l.z; Y = Y + P.t[1];
+    float Z = P.R[6] * l.x + P.R[7] * l.y + P.R[8] * l.z; Z = Z + P.t[2];
+    const float d2 = X * X + Y * Y + Z * Z;
+    const float dist_inv = __builtin_amdgcn_rsqf(d2);
+    const float phi_trg = r360m::asinf_fast(X * dist_inv);
+    const float theta_trg = r360m::atan2f_fast1(Y, Z) + 3.14159265358979f;
+    // u = rr + 0.5, v = cc + 0.5 (half_nRows + 0.5 = nRows / 2 exactly)
+    const float u = fmaf(-phi_trg, angle_res_inv, 0.5f * (float)nRows);
+    const float v = fmaf(theta_trg, angle_res_inv, 0.5f);
+    const float fu = floorf(u), fv = floorf(v);
+    const float eu = fabsf(u - fu - 0.5f), ev = fabsf(v - fv - 0.5f);
+    o.fix = l.valid && !(eu <= 0.5f - kGuardRow && ev <= 0.5f - kGuardCol);   // NaN -> flagged
+    o.vis = l.valid && fu >= 0.f && fu < (float)nRows && fv < (float)nCols;
+    o.t = o.vis ? (int)fu * nCols + (int)fv : 0;
+    o.X = X; o.Y = Y; o.Z = Z; o.dist = r360m::sqrt_rn(d2); o.dist_inv = dist_inv; o.gray_s = gray_s;
+    return o;
+}
+
+__device__ __forceinline__ float huber_rn(float e, float reg) {    // weightHuber<float>, bit-exact
+    const float a = fabsf(e);
+    const float w = r360m::div_rn(r360m::sqrt_rn(2 * reg * a - reg * reg), a);
+    return a < reg ? 1.f : w;
+}
+
+__device__ __forceinline__ float huber_fast(float e, float reg) {   // weightHuber with hardware sqrt / rcp
+    const float a = fabsf(e);
+    const float w = __builtin_amdgcn_sqrtf(2 * reg * a - reg * reg) * __builtin_amdgcn_rcpf(a);
+    return a < reg ? 1.f : w;
+}
+
 // Residuals, weights and Jacobian rows of one projected pixel, accumulated branch-free: a pixel that
 // the reference skips contributes through selects that zero its row (never a multiply by 0, which
 // would let a NaN of an invalid pixel through).
-template <int METHOD, int OCC>
+template <int METHOD, int OCC, bool FAST = false>
 __device__ __forceinline__ void contribute(Acc& A, const Proj& o, const float4 G, const float2 T, int fl,
                                            float angle_res_inv, const IcpConst& C) {
+#ifdef R360_EXP_NOACC   // experiment builds only: keep the operands alive, skip the math
+    A.h[0] += o.vis ? G.x + G.y + G.z + G.w + T.x + T.y + o.X + o.dist : 0.f;
+    A.h[28] += o.vis ? 1.f : 0.f;
+    return;
+#endif
     constexpr bool photo = (METHOD == R360_PHOTO_CONSISTENCY || METHOD == R360_PHOTO_DEPTH);
     constexpr bool depth = (METHOD == R360_DEPTH_CONSISTENCY || METHOD == R360_PHOTO_DEPTH);
     const float X = o.X, Y = o.Y, Z = o.Z, dist = o.dist, dist_inv = o.dist_inv;
@@ -150,13 +229,17 @@ __device__ __forceinline__ void contribute(Acc& A, const Proj& o, const float4 G
     const bool p_ok = photo && o.vis && sal_p;
     const bool d_ok = depth && o.vis && (!photo || sal_p) && fin_d && sal_d;   // (:3064-3073)
     // exact error terms (they steer the accept/reject test :4715)
+    // FAST: hardware sqrt / rcp and float products (~1-2 ulp per term; the error and H / g sums keep
+    // their fp64 / summation-order tolerances)
     const float photoDiff = T.x - o.gray_s;
-    const float whp = huberf(photoDiff, C.sd_photo);
-    const float wEd = (float)((double)whp * C.sd_photo_inv_d * photoDiff);            // (:2699-2700)
+    const float whp = FAST ? huber_fast(photoDiff, C.sd_photo) : huberf(photoDiff, C.sd_photo);
+    const float wEd = FAST ? whp * C.sd_photo_inv_f * photoDiff
+                           : (float)((double)whp * C.sd_photo_inv_d * photoDiff);         // (:2699-2700)
     const float depthDiff = T.y - dist;
     const float sd = C.sd_depth * T.y;
-    const float wd = huberf(depthDiff, sd) / sd;                                        // (:3077-3078)
-    const float wEdep = (float)((double)wd * depthDiff);
+    const float wd = FAST ? huber_fast(depthDiff, sd) * __builtin_amdgcn_rcpf(sd)
+                          : huberf(depthDiff, sd) / sd;                                   // (:3077-3078)
+    const float wEdep = wd * depthDiff;   // == (float)((double)wd * depthDiff): the f32 product is exact in f64
     // which terms enter the error and which Jacobian rows enter H / g
     bool jp = p_ok, jd = d_ok;
     if (OCC == 0) {
@@ -229,6 +312,105 @@ __device__ __forceinline__ void contribute(Acc& A, const Proj& o, const float4 G
     }
 }
 
+// PF 3's residuals, weights and Jacobian rows: contribute<..>'s terms (exact error terms, fast
+// Jacobian) for every occlusion variant, with the skips applied to the weights instead of the rows (a
+// lane that contributes nothing has its coordinates replaced by finite ones, so a zero weight zeroes
+// its rows exactly) and the counts taken per wave from ballots (SALU).  The depth Huber weight is 1
+// for almost every pixel (sigma = 0.2 m per metre of range): its exact sqrt / division run only in
+// waves where some lane needs them.
+struct WaveCnt { int c27 = 0, c28 = 0, c29 = 0; };
+
+__device__ __forceinline__ int wave_count(bool b) { return __popcll(__ballot(b)); }
+
+template <int METHOD, int OCC>
+__device__ __forceinline__ void contribute_fast(Acc& A, WaveCnt& W, const Proj& o, const float4 G, const float2 T,
+                                                int fl, float angle_res_inv, const IcpConst& C) {
+    constexpr bool photo = (METHOD == R360_PHOTO_CONSISTENCY || METHOD == R360_PHOTO_DEPTH);
+    constexpr bool depth = (METHOD == R360_DEPTH_CONSISTENCY || METHOD == R360_PHOTO_DEPTH);
+    const bool sal_p = !(fabsf(G.x) < C.thr_int && fabsf(G.y) < C.thr_int);
+    const bool sal_d = !(fabsf(G.z) < C.thr_depth && fabsf(G.w) < C.thr_depth);
+    const bool fin_d = isfinite(T.y);
+    const bool p_ok = photo && o.vis && sal_p;
+    const bool d_ok = depth && o.vis && (!photo || sal_p) && fin_d && sal_d;   // (:3064-3073)
+    // error terms exactly as the reference's (correctly rounded sqrt / division, no contraction): they
+    // steer the GN accept / stop decisions, which must not flip on a rounding difference
+    const float photoDiff = T.x - o.gray_s;
+    const float whp = huber_rn(photoDiff, C.sd_photo);
+    const float wEd = (float)((double)whp * C.sd_photo_inv_d * photoDiff);                 // (:2699-2700)
+    const float depthDiff = T.y - o.dist;
+    const float sd = C.sd_depth * T.y;
+    float hd = 1.f;
+    if (__any(d_ok && !(fabsf(depthDiff) < sd))) hd = huber_rn(depthDiff, sd);
+    const float wd_ = r360m::div_rn(hd, sd);                                               // (:3077-3078)
+    const float wEdep = wd_ * depthDiff;   // == (float)((double)wd * depthDiff)
+    const float ep = wEd * wEd, ed = wEdep * wEdep;
+    bool jp = p_ok, jd = d_ok;
+    if (OCC == 0) {
+        W.c28 += wave_count(o.vis);                                                        // numVisiblePixels
+        W.c27 += (photo ? wave_count(p_ok) : 0) + (depth ? wave_count(d_ok) : 0);
+        A.err2 += (p_ok ? (double)ep : 0.0) + (d_ok ? (double)ed : 0.0);
+    } else if (OCC == 1) {
+        // errorPhotoICP_sphereOcc1 (:3232-3370): accepted points count, the last accepted one of a target
+        // pixel owns its residual; H / g as calcHessGrad_sphere (its Z-buffer never occludes)
+        const bool acc = fl & OCC_ACC, own = fl & OCC_OWN;
+        W.c28 += wave_count(o.vis);
+        if (photo) { A.err2 += (own && p_ok) ? (double)ep : 0.0; W.c27 += wave_count(acc && p_ok); }
+        if (depth) { A.err2d += (own && d_ok) ? (double)ed : 0.0; W.c29 += wave_count(acc && d_ok); }
+    } else {
+        // errorPhotoICP_sphereOcc2 (:3720-3855): every accepted point counts and contributes;
+        // calcHessGrad_sphereOcc2 (:3861-4250): the last filtered point of a target pixel owns its rows,
+        // and a failed depth-saliency test skips the store of both rows
+        const bool acc = fl & OCC_ACC, win = fl & OCC_WIN;
+        W.c27 += wave_count(acc);
+        if (photo) A.err2 += (acc && p_ok) ? (double)ep : 0.0;
+        if (depth) A.err2d += (acc && d_ok) ? (double)ed : 0.0;
+        W.c28 += wave_count(win);
+        jp = win && p_ok && !(depth && fin_d && !sal_d);
+        jd = win && d_ok;
+    }
+    const float wp = jp ? whp * C.sd_photo_inv_f : 0.f;                                    // (:3047)
+    const float rp = wp * photoDiff;
+    const float wd = jd ? wd_ : 0.f;
+    const float rd = jd ? wEdep : 0.f;   // |p'| of a lane without a point can be NaN
+    const float X = o.vis ? o.X : 1.f, Y = o.vis ? o.Y : 1.f, Z = o.vis ? o.Z : 1.f;
+    const float dist_inv = o.vis ? o.dist_inv : 0.5f;
+    {
+#pragma clang fp contract(fast)
+        // Jacobian of the spherical warp (:2995-3026), expanded with T36 = [I | -skew(p')]
+        const float z_inv = __builtin_amdgcn_rcpf(Z);
+        const float z_inv2 = z_inv * z_inv;
+        const float D_atan = __builtin_amdgcn_rcpf(1 + Y * Y * z_inv2) * angle_res_inv;
+        const float P01 = D_atan * z_inv;
+        const float P02 = -Y * z_inv2 * D_atan;
+        const float x_dist_inv2 = X * (dist_inv * dist_inv);
+        const float q = 1 - X * x_dist_inv2;
+        const float D_asin = __builtin_amdgcn_rsqf(q) * angle_res_inv;
+        const float P10 = -D_asin * dist_inv * q;
+        const float kk = D_asin * x_dist_inv2 * dist_inv;
+        const float P11 = kk * Y, P12 = kk * Z;
+        const float Jw0[6] = {0.f, P01, P02, P02 * Y - P01 * Z, -P02 * X, P01 * X};
+        const float Jw1[6] = {P10, P11, P12, P12 * Y - P11 * Z, P10 * Z - P12 * X, P11 * X - P10 * Y};
+        if (photo) {
+            const float wgx = wp * G.x, wgy = wp * G.y;
+            float J[6];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) J[k] = wgx * Jw0[k] + wgy * Jw1[k];
+            acc_fma(A, J, rp);
+        }
+        if (depth) {
+            // (dgrad * Jw - (p'/|p'|)^T T36): the rotational part of (p'/|p'|)^T T36 is p' x p' / |p'| = 0
+            const float wz = wd * G.z, ww = wd * G.w, wdi = wd * dist_inv;
+            float J[6];
+            J[0] = wz * Jw0[0] + ww * Jw1[0] - wdi * X;
+            J[1] = wz * Jw0[1] + ww * Jw1[1] - wdi * Y;
+            J[2] = wz * Jw0[2] + ww * Jw1[2] - wdi * Z;
+#pragma unroll
+            for (int k = 3; k < 6; ++k) J[k] = wz * Jw0[k] + ww * Jw1[k];
+            acc_fma(A, J, rd);
+        }
+    }
+}
+
 // ---------------------------------------------------------------- GN step (thread 0 of last block)
 #include "icp_gn.inc"
 
@@ -242,20 +424,26 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const float2* _
                                                  const float* __restrict__ costh, int nRows, int nCols,
                                                  IcpConst C, IcpState* S, double* __restrict__ partials, int first,
                                                  int eval_only, unsigned long long* __restrict__ kt,
-                                                 const uint8_t* __restrict__ occf) {
+                                                 const uint8_t* __restrict__ occf, unsigned* __restrict__ gcnt) {
     __shared__ float s_red[NW][32];
     __shared__ double s_err[NW], s_errd[NW];
     __shared__ double s_fin[RG][32];
     __shared__ int s_last;
     __shared__ GnShared s_gn;
     __shared__ IcpState s_state;
+    constexpr int QCAP = 128;   // PF 3: deferred pixels per wave (<= 63 + 64 between drains)
+    __shared__ int s_queue[PF == 3 ? NW * QCAP : 1];
 
     if (S->stop) return;
 #ifdef R360_STAMPS
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #endif
     if (!first && !S->active && !eval_only) return;
+#ifndef R360_EXP_NOKT
     if (threadIdx.x == 0)   // execution span: earliest workgroup start of this pass
+#else
+    if (false)
+#endif
         __hip_atomic_fetch_min(kt, (unsigned long long)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
 
@@ -277,6 +465,7 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const float2* _
     A.err2 = 0.0;
     A.err2d = 0.0;
     auto flag = [&](int i) { return OCC ? (int)occf[i] : 0; };
+    WaveCnt W;   // PF 3: wave-uniform counts
 
     const int units = (nRows * nCols) >> 2;  // 4 pixels of one row per unit (nCols % 4 == 0)
     const float4* src4 = reinterpret_cast<const float4*>(src);
@@ -371,6 +560,95 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const float2* _
                 if (project_fix(oA, nRows, nCols, half_nRows, angle_res_inv)) { GA = gt.g(oA.t); TA = gt.T(oA.t); }
             }
         }
+    } else if (PF == 3) {
+        // PF 2's pipelined wave stream with the guard-band lanes DEFERRED instead of fixed in place: a
+        // lane whose fast projection lands near a rounding boundary drops out of its chunk (no
+        // contribution) and its pixel index goes to a per-wave LDS queue; full waves of queued pixels
+        // run the exact projection (project_exact) later, at every lane.  The chunk loop then has one
+        // straight-line path (no re-issued gathers), and the exact code runs at full lane occupancy
+        // instead of once per chunk that has any flagged lane (about a quarter of them at level 0).
+        const int npx = nRows * nCols;
+        const int lane = threadIdx.x & 63;
+        int* q = s_queue + (threadIdx.x >> 6) * QCAP;
+        int qn = 0;   // wave-uniform queue length
+        auto acc = [&](const Proj& o, const float4 G, const float2 T, int fl) {
+            contribute_fast<METHOD, OCC>(A, W, o, G, T, fl, angle_res_inv, C);
+        };
+        struct Src { float d, g, sp, cp, st, ct; int f; };
+        auto ld = [&](int base) {
+            const int r = __builtin_amdgcn_readfirstlane(base / nCols);
+            const int c = base - r * nCols + lane;
+            const float2 a = src[base + lane];
+            return Src{a.y, a.x, sinphi[r], cosphi[r], sinth[c], costh[c], flag(base + lane)};
+        };
+        const Gather gt{__builtin_amdgcn_make_buffer_rsrc(const_cast<float4*>(tg), 0, npx * 16, 0x00020000),
+                        __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(trg), 0, npx * 8, 0x00020000)};
+        auto prj = [&](const Src& x) {
+            return project_fast(P, lut_point(x.d, x.sp, x.cp, x.st, x.ct, C), x.g, nRows, nCols, angle_res_inv);
+        };
+        // queue the flagged lanes of a chunk and take them out of it
+        auto defer = [&](Proj& o, int& fl, int base) {
+            const unsigned long long m = __ballot(o.fix);
+            if (m) {
+                const int pos = qn + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                                   __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+                if (o.fix) { q[pos] = base + lane; o.vis = false; o.t = 0; fl = 0; }   // Occ2 counts read the flags
+                qn += __popcll(m);
+            }
+        };
+        // exact pass over queue entries [0, n), one pixel per lane, then the queue moves down by n
+        auto drain = [&](int n) {
+            const bool act = lane < n;
+            const int i = q[act ? lane : 0];
+            const int r = i / nCols, c = i - r * nCols;
+            const float2 a = src[i];
+            Proj o = project_exact(P, lut_point(a.y, sinphi[r], cosphi[r], sinth[c], costh[c], C), a.x, nRows, nCols,
+                                   half_nRows, angle_res_inv);
+            o.vis = o.vis && act;
+            o.t = o.vis ? o.t : 0;
+            acc(o, gt.g(o.t), gt.T(o.t), act ? flag(i) : 0);
+            const int rest = qn - n;
+            const int moved = lane < rest ? q[n + lane] : 0;
+            if (lane < rest) q[lane] = moved;
+            qn = rest;
+        };
+        const int b0 = __builtin_amdgcn_readfirstlane((blockIdx.x * TPB + (threadIdx.x & ~63)));
+#ifdef R360_EXP_NOLOOP   // experiment builds only: the pass without its pixel loop (fixed costs)
+        if (false) {
+#else
+        if (b0 < npx) {
+#endif
+            const int n_it = (npx - 1 - b0) / stride + 1;
+            auto base = [&](int k) { return b0 + (k < n_it ? k : n_it - 1) * stride; };
+            Src sA = ld(base(0));
+            Src sB = ld(base(1));
+            Proj oA = prj(sA);
+            int fA = sA.f;
+            defer(oA, fA, base(0));
+            float4 GA = gt.g(oA.t);
+            float2 TA = gt.T(oA.t);
+            for (int k = 0;; k += 2) {
+                sA = ld(base(k + 2));
+                Proj oB = prj(sB);
+                int fB = sB.f;
+                if (k + 1 < n_it) defer(oB, fB, base(k + 1));   // a clamped tail chunk is never accumulated
+                const float4 GB = gt.g(oB.t);
+                const float2 TB = gt.T(oB.t);
+                acc(oA, GA, TA, fA);
+                if (k + 1 >= n_it) break;
+                if (qn >= 64) drain(64);
+                sB = ld(base(k + 3));
+                oA = prj(sA);
+                fA = sA.f;
+                if (k + 2 < n_it) defer(oA, fA, base(k + 2));
+                GA = gt.g(oA.t);
+                TA = gt.T(oA.t);
+                acc(oB, GB, TB, fB);
+                if (k + 2 >= n_it) break;
+                if (qn >= 64) drain(64);
+            }
+            while (qn > 0) drain(qn < 64 ? qn : 64);
+        }
     } else {
         // small levels: one pixel per thread, so the latency chain per thread is a quarter as long
         const int npx = nRows * nCols;
@@ -392,9 +670,19 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const float2* _
 
     // ---- stage 1: wave butterfly (f32) -> LDS -> per-workgroup fp64 record
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (PF == 3 && lane == 0) { A.h[27] += (float)W.c27; A.h[28] += (float)W.c28; A.h[29] += (float)W.c29; }
+#ifdef R360_EXP_NOEPI   // experiment builds only
+    if (A.h[0] == 1.2345f) S->dbg[7] = 1;
+    return;
+#endif
+#ifdef R360_EXP_NOBFLY   // experiment builds only
+    const float mine = A.h[lane & 31];
+    const double e2 = A.err2, e2d = A.err2d;
+#else
     const float mine = wave_reduce_scatter32(A.h, lane);
     const double e2 = wave_sum_d(A.err2);
     const double e2d = OCC ? wave_sum_d(A.err2d) : 0.0;
+#endif
     if ((lane & 1) == 0) s_red[wid][scatter_slot(lane)] = mine;
     if (lane == 0) { s_err[wid] = e2; s_errd[wid] = e2d; }
     __syncthreads();
@@ -418,12 +706,26 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const float2* _
     // its wave (vmcnt(0) above) before the barrier; one relaxed agent-scope add per workgroup; the
     // last adder reads every record with sc1 loads.  No buffer_wbl2 / buffer_inv fences: a release
     // fence per workgroup wrote back each XCD's dirty L2 (tens of us per pass).
+    // Two-level ticket: agent-scope atomics on one address serialise at the memory side (~50 ns each,
+    // 256 of them were ~13 us of every level-0 pass), so workgroups first count in 16 group counters
+    // (256 B apart) and only the last of each group takes the pass ticket: 16 + 16 deep instead of 256.
     if (threadIdx.x == 0) {
-        const unsigned prev = __hip_atomic_fetch_add(&S->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = (prev == gridDim.x - 1);
+        const int nb = (int)gridDim.x;
+        const int ng = nb < R360_TICKET_GROUPS ? nb : R360_TICKET_GROUPS;
+        const int g = (int)blockIdx.x % R360_TICKET_GROUPS;
+        const unsigned gsz = (unsigned)((nb - g + R360_TICKET_GROUPS - 1) / R360_TICKET_GROUPS);
+        const unsigned prev = __hip_atomic_fetch_add(gcnt + g * 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int last = 0;
+        if (prev == gsz - 1) {
+            const unsigned p2 = __hip_atomic_fetch_add(&S->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last = (p2 == (unsigned)ng - 1);
+        }
+        s_last = last;
     }
     __syncthreads();
     if (!s_last) return;
+    if (threadIdx.x < R360_TICKET_GROUPS)   // every group is complete: reset its counter for the next pass
+        __hip_atomic_store(gcnt + threadIdx.x * 64, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #ifdef R360_STAMPS
     const unsigned long long t_ticket = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -727,54 +1029,36 @@ int icp_blocks_for(int n_pixels) {
 }
 
 namespace {
-// Test hook: fast-guarded vs exact projection of arbitrary transformed points (pose = identity,
-// LUT bypassed): counts pixel-decision mismatches (must be 0) and exact fallbacks.
+// Test hook: the PF 3 pass's decision for LUT points (lx, ly, lz) at pose P — the fast projection, or
+// the exact one for a flagged (deferred) lane — against the exact program alone: pixel-decision
+// mismatches (must be 0) and deferrals.
 __global__ void k_proj_check(const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
-                             int n, int nRows, int nCols, unsigned long long* __restrict__ out) {
+                             int n, Pose12 P, int nRows, int nCols, unsigned long long* __restrict__ out) {
     const float angle_res = (float)(2 * R360_PI / nCols);
     const float angle_res_inv = 1 / angle_res;
     const float half_nRows = (float)(0.5 * nRows - 0.5);
     unsigned long long mism = 0, fb = 0;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const float x = X[i], y = Y[i], z = Z[i];
-        const float d2 = x * x + y * y + z * z;
-        // exact
-        const float dist = sqrtf(d2);
-        const float dinv = 1.f / dist;
-        const float rr_e = half_nRows - r360m::asinf(x * dinv) * angle_res_inv;
-        const float cc_e = (float)((double)r360m::atan2f_sel(y, z) + R360_PI) * angle_res_inv;
-        // fast + guard (as project())
-        const float fi = __builtin_amdgcn_rsqf(d2);
-        float rr = half_nRows - r360m::asinf_fast(x * fi) * angle_res_inv;
-        float cc = (float)((double)r360m::atan2f_fast(y, z) + R360_PI) * angle_res_inv;
-        const float gr = fabsf(rr - floorf(rr) - 0.5f), gc = fabsf(cc - floorf(cc) - 0.5f);
-        const float rr_f = rr, cc_f = cc;
-        if (!(gr >= kGuardRow && gc >= kGuardCol)) { rr = rr_e; cc = cc_e; ++fb; }
-        // the decision the pass takes: visible or not, and which target pixel
-        auto decide = [&](float a, float b, long long& t) {
-            const float rf = roundf(a), cf = roundf(b);
-            const bool vis = (rf >= 0.f && rf < (float)nRows) && cf < (float)nCols;
-            t = vis ? (long long)rf * nCols + (long long)cf : -1;
-            return vis;
-        };
-        long long tf, te;
-        const bool vf = decide(rr, cc, tf), ve = decide(rr_e, cc_e, te);
-        const bool same = vf == ve && tf == te;
+        Lut3 l;
+        l.x = X[i]; l.y = Y[i]; l.z = Z[i]; l.valid = true;
+        const Proj e = project_exact(P, l, 0.f, nRows, nCols, half_nRows, angle_res_inv);
+        Proj f = project_fast(P, l, 0.f, nRows, nCols, angle_res_inv);
+        if (f.fix) { f = e; ++fb; }
+        const bool same = f.vis == e.vis && f.t == e.t;
         mism += same ? 0 : 1;
-        if (!same) {
-            out[2] = (unsigned long long)i;
-            out[3] = __float_as_uint(rr_f); out[4] = __float_as_uint(rr_e);
-            out[5] = __float_as_uint(cc_f); out[6] = __float_as_uint(cc_e);
-        }
+        if (!same) { out[2] = (unsigned long long)i; out[3] = (unsigned long long)f.t; out[4] = (unsigned long long)e.t; }
     }
     atomicAdd(out, mism);
     atomicAdd(out + 1, fb);
 }
 
-}  // namespace
-
-extern "C" int r360_proj_check(const float* X, const float* Y, const float* Z, int n, int nRows, int nCols,
-                               unsigned long long* mismatches, unsigned long long* fallbacks) {
+int proj_check(const float* X, const float* Y, const float* Z, int n, const float* pose, int nRows, int nCols,
+               unsigned long long* mismatches, unsigned long long* fallbacks) {
+    Pose12 P;
+    for (int r = 0; r < 3; ++r) {
+        for (int c = 0; c < 3; ++c) P.R[r * 3 + c] = pose ? pose[c * 4 + r] : (r == c ? 1.f : 0.f);
+        P.t[r] = pose ? pose[12 + r] : 0.f;
+    }
     float *dx, *dy, *dz;
     unsigned long long* dout;
     R360_HIP(hipMalloc(&dx, sizeof(float) * n));
@@ -785,18 +1069,63 @@ extern "C" int r360_proj_check(const float* X, const float* Y, const float* Z, i
     R360_HIP(hipMemcpy(dy, Y, sizeof(float) * n, hipMemcpyHostToDevice));
     R360_HIP(hipMemcpy(dz, Z, sizeof(float) * n, hipMemcpyHostToDevice));
     R360_HIP(hipMemset(dout, 0, 64));
-    hipLaunchKernelGGL(k_proj_check, dim3(1024), dim3(256), 0, 0, dx, dy, dz, n, nRows, nCols, dout);
+    hipLaunchKernelGGL(k_proj_check, dim3(1024), dim3(256), 0, 0, dx, dy, dz, n, P, nRows, nCols, dout);
     R360_HIP(hipGetLastError());
     unsigned long long h[8];
     R360_HIP(hipMemcpy(h, dout, 64, hipMemcpyDeviceToHost));
     if (h[0] && getenv("R360_PROJ_DEBUG"))
-        fprintf(stderr, "proj mismatch at %llu: rr fast %.9g exact %.9g, cc fast %.9g exact %.9g\n", h[2],
-                (double)__builtin_bit_cast(float, (unsigned)h[3]), (double)__builtin_bit_cast(float, (unsigned)h[4]),
-                (double)__builtin_bit_cast(float, (unsigned)h[5]), (double)__builtin_bit_cast(float, (unsigned)h[6]));
+        fprintf(stderr, "proj mismatch at %llu: fast pixel %lld exact pixel %lld\n", h[2], (long long)h[3], (long long)h[4]);
     (void)hipFree(dx); (void)hipFree(dy); (void)hipFree(dz); (void)hipFree(dout);
     *mismatches = h[0];
     *fallbacks = h[1];
     return 0;
+}
+
+}  // namespace
+
+namespace {
+// Test hook: sqrt_rn / div_rn against the compiler's IEEE sqrtf and '/' on hashed operands spanning the
+// ranges the pass feeds them (squared ranges 1e-4..1e4, weights and residuals 1e-5..1e3).
+__device__ __forceinline__ float hash_unit(unsigned x) {
+    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+    return (float)(x >> 8) * (1.f / 16777216.f);
+}
+__global__ void k_rn_check(unsigned n, unsigned seed, unsigned long long* __restrict__ out) {
+    unsigned long long ms = 0, md = 0;
+    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const unsigned k = i * 3u + seed * 0x9e3779b9u;
+        const float x = exp2f(hash_unit(k) * 26.6f - 13.3f);            // 1e-4 .. 1e4
+        const float a = exp2f(hash_unit(k + 1) * 26.6f - 16.6f);        // 1e-5 .. 1e3
+        const float b = exp2f(hash_unit(k + 2) * 26.6f - 16.6f);
+        volatile float xs = x, as = a, bs = b;
+        ms += __float_as_uint(r360m::sqrt_rn(x)) != __float_as_uint(sqrtf(xs));
+        md += __float_as_uint(r360m::div_rn(a, b)) != __float_as_uint(as / bs);
+    }
+    atomicAdd(out, ms);
+    atomicAdd(out + 1, md);
+}
+}  // namespace
+
+extern "C" int r360_rn_check(unsigned n, unsigned seed, unsigned long long out[2]) {
+    unsigned long long* d;
+    R360_HIP(hipMalloc(&d, 16));
+    R360_HIP(hipMemset(d, 0, 16));
+    hipLaunchKernelGGL(k_rn_check, dim3(1024), dim3(256), 0, 0, n, seed, d);
+    R360_HIP(hipGetLastError());
+    R360_HIP(hipMemcpy(out, d, 16, hipMemcpyDeviceToHost));
+    (void)hipFree(d);
+    return 0;
+}
+
+extern "C" int r360_proj_check(const float* X, const float* Y, const float* Z, int n, int nRows, int nCols,
+                               unsigned long long* mismatches, unsigned long long* fallbacks) {
+    return proj_check(X, Y, Z, n, nullptr, nRows, nCols, mismatches, fallbacks);
+}
+
+extern "C" int r360_proj_check_pose(const float* lx, const float* ly, const float* lz, int n, const float pose[16],
+                                    int nRows, int nCols, unsigned long long* mismatches,
+                                    unsigned long long* fallbacks) {
+    return proj_check(lx, ly, lz, n, pose, nRows, nCols, mismatches, fallbacks);
 }
 
 #ifdef R360_STAMPS
@@ -822,7 +1151,7 @@ static void launch_pass(r360_ctx* ctx, int nb, const LevelBufs& Ls, const LevelB
               : top        ? k_icp_pass<M, PF, 1, 0> : k_icp_pass<M, PF, 0, 0>;
     hipLaunchKernelGGL(kern, dim3(nb), dim3(TPB), 0, ctx->stream, Ls.p0, Lt.p0, Lt.tg, T.sinphi,
                        T.cosphi, T.sinth, T.costh, Ls.rows, Ls.cols, C, ctx->d_state, ctx->d_partials, first,
-                       eval_only, ctx->d_ktime, ctx->occ_flags);
+                       eval_only, ctx->d_ktime, ctx->occ_flags, ctx->d_gticket);
 }
 
 int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src, int level, int method,
@@ -835,7 +1164,7 @@ int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src
     static const int pf_env = env_int("R360_ICP_PF", -1);
     static const int cap_env = env_int("R360_ICP_CAP", -1);
     // one resident round: CUs x workgroups per CU of the launched form (grid-stride beyond it)
-    struct Occ { int cus = 0, per[3] = {0, 0, 0}; };
+    struct Occ { int cus = 0, per[4] = {0, 0, 0, 0}; };
     static const Occ occ = [] {   // thread-safe one-time query (contexts may be driven from several threads)
         Occ o;
         int dev = 0;
@@ -844,10 +1173,11 @@ int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[0], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 0, 0, 0>, TPB, 0);
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[1], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 1, 0, 0>, TPB, 0);
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[2], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 2, 0, 0>, TPB, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[3], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 3, 0, 0>, TPB, 0);
         return o;
     }();
     const int npx = Ls.rows * Ls.cols;
-    const int pf = pf_env >= 0 ? pf_env : ((Ls.cols % 64 == 0) ? 2 : 0);
+    const int pf = pf_env >= 0 ? pf_env : ((Ls.cols % 64 == 0) ? 3 : 0);
     int cap = cap_env > 0 ? cap_env : occ.cus * (occ.per[pf] > 0 ? occ.per[pf] : 4);
     if (cap > ctx->partials_cap) cap = ctx->partials_cap;
     int nb = pf == 1 ? icp_blocks_for(npx) : (npx + TPB - 1) / TPB;
@@ -898,6 +1228,7 @@ int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src
     do {                                                                            \
         if (pf == 1) launch_pass<M, 1>(ctx, nb, Ls, Lt, T, C, first, eval_only, level == 0);   \
         else if (pf == 2) launch_pass<M, 2>(ctx, nb, Ls, Lt, T, C, first, eval_only, level == 0); \
+        else if (pf == 3) launch_pass<M, 3>(ctx, nb, Ls, Lt, T, C, first, eval_only, level == 0); \
         else launch_pass<M, 0>(ctx, nb, Ls, Lt, T, C, first, eval_only, level == 0);          \
     } while (0)
     if (method == R360_PHOTO_CONSISTENCY) R360_LAUNCH(R360_PHOTO_CONSISTENCY);

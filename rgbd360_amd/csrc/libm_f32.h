@@ -240,6 +240,46 @@ __device__ __forceinline__ float atan2f_fast(float y, float x) {
     r = (fbits(x) >> 31) ? 3.14159265f - r : r;
     return (fbits(y) >> 31) ? -r : r;
 }
+
+// Correctly rounded f32 square root and division for NORMAL operands and results (no scaling, no
+// special-value fix-up): the compiler's own IEEE sequences (v_sqrt + neighbour tests; v_rcp + Newton +
+// two fma corrections) without their range handling.  The ICP pass's error terms go through them, so
+// they equal the reference's sqrtf / '/' bit for bit (tests/test_gpu_dense.py checks both against the
+// compiler's IEEE operations).  sqrt_rn(0) = 0.
+__device__ __forceinline__ float sqrt_rn(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sm = __uint_as_float(__float_as_uint(s) - 1u), sp = __uint_as_float(__float_as_uint(s) + 1u);
+    const float vm = __builtin_fmaf(-sm, s, x), vp = __builtin_fmaf(-sp, s, x);
+    float r = vm <= 0.f ? sm : s;
+    r = vp > 0.f ? sp : r;
+    return r;
+}
+__device__ __forceinline__ float div_rn(float a, float b) {
+    float r = __builtin_amdgcn_rcpf(b);
+    r = __builtin_fmaf(__builtin_fmaf(-b, r, 1.0f), r, r);
+    float q = a * r;
+    q = __builtin_fmaf(__builtin_fmaf(-b, q, a), r, q);
+    return __builtin_fmaf(__builtin_fmaf(-b, q, a), r, q);
+}
+
+// atan2 as atan2f_fast with a single reciprocal: the reduction t = (mn - mx) / (mn + mx) above
+// tan(pi/8) (= (a - 1) / (a + 1) for a = mn / mx) and t = mn / mx below share one division.
+__device__ __forceinline__ float atan2f_fast1(float y, float x) {
+    const float ay = fabs_(y), ax = fabs_(x);
+    const float mx = ay > ax ? ay : ax, mn = ay > ax ? ax : ay;
+    const bool big = mn > 0.41421356f * mx;
+    const float t = (big ? mn - mx : mn) * fast_rcp(big ? mn + mx : mx);
+    const float z = t * t, w = z * z;
+    const float s1 = z * (3.3333334327e-01f + w * (1.4285714924e-01f + w * (9.0908870101e-02f +
+                     w * (6.6610731184e-02f + w * (4.9768779427e-02f + w * 1.6285819933e-02f)))));
+    const float s2 = w * (-2.0000000298e-01f + w * (-1.1111110449e-01f + w * (-7.6918758452e-02f +
+                     w * (-5.8335702866e-02f + w * -3.6531571299e-02f))));
+    float r = t - t * (s1 + s2);
+    r = big ? r + 0.78539816f : r;
+    r = ay > ax ? 1.57079633f - r : r;
+    r = (fbits(x) >> 31) ? 3.14159265f - r : r;
+    return (fbits(y) >> 31) ? -r : r;
+}
 #endif
 
 }  // namespace r360m

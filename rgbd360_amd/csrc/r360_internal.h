@@ -73,6 +73,8 @@ struct alignas(16) IcpState {
     unsigned long long dbg[12];  // s_memrealtime stamps of the diagnostic build (-DR360_STAMPS)
 };
 
+constexpr int R360_TICKET_GROUPS = 16;
+
 // Pass sums.  Occlusion variants: NVALID counts photo terms (Occ1) or accepted points (Occ2), NDEPTH
 // the depth terms (Occ1), ERR2 the photometric and ERR2D the depth squared residuals.
 enum { R360_SUM_NVALID = 27, R360_SUM_NVIS = 28, R360_SUM_NDEPTH = 29, R360_SUM_ERR2D = 30, R360_SUM_ERR2 = 31,
@@ -167,6 +169,7 @@ struct r360_ctx {
     hipEvent_t wait_ev = nullptr;   // blocking-sync event: host waits sleep instead of spinning
     IcpState* d_state = nullptr;
     double* d_partials = nullptr;
+    unsigned* d_gticket = nullptr;   // group arrival counters of the ICP pass (R360_TICKET_GROUPS x 256 B)
     // in-kernel execution spans of the ICP passes (s_memrealtime, 100 MHz): [0] earliest workgroup start
     // of the running pass, [1+l] summed spans at level l, [9+l] pass counts
     unsigned long long* d_ktime = nullptr;

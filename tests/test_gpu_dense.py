@@ -211,3 +211,22 @@ def test_fast_projection_guard_never_changes_a_pixel(rows, cols):
                                      R.C.byref(fb)), "proj_check")
     assert mism.value == 0, mism.value
     assert fb.value < n // 3          # the fast path decides most points
+    # the same with a pose: LUT points whose TRANSFORMED position is random or on a rounding boundary,
+    # so the fast (FMA-contracted) transform is covered too
+    for seed in range(3):
+        P = O.exp_se3(rng.normal(scale=[0.2, 0.2, 0.2, 0.1, 0.1, 0.1]), pseudo=False).astype(np.float32)
+        lut = ((v - P[:3, 3]) @ P[:3, :3]).astype(np.float32)   # R^T (p' - t)
+        lx, ly, lz = (np.ascontiguousarray(lut[:, k]) for k in range(3))
+        p16 = np.ascontiguousarray(P.T).reshape(16)
+        R._check(R.lib().r360_proj_check_pose(R._fptr(lx), R._fptr(ly), R._fptr(lz), n, R._fptr(p16), rows, cols,
+                                              R.C.byref(mism), R.C.byref(fb)), "proj_check_pose")
+        assert mism.value == 0, (seed, mism.value)
+        assert fb.value < n // 3
+
+
+def test_correctly_rounded_sqrt_div():
+    """The pass's error terms use sqrt_rn / div_rn (libm_f32.h): they must equal IEEE sqrtf and '/' bit for
+    bit over the operand ranges the pass feeds them (64M operands each)."""
+    out = (R.C.c_ulonglong * 2)()
+    R._check(R.lib().r360_rn_check(1 << 26, 7, out), "rn_check")
+    assert out[0] == 0 and out[1] == 0, (out[0], out[1])
