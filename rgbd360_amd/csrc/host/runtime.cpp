@@ -108,8 +108,8 @@ extern "C" int r360_ctx_create(int device, r360_ctx** out) {
     R360_HIP(hipMemset(c->d_state, 0, sizeof(IcpState)));
     c->partials_cap = 2048;
     R360_HIP(hipMalloc(&c->d_partials, sizeof(double) * 32 * c->partials_cap));
-    R360_HIP(hipMalloc(&c->d_gticket, sizeof(unsigned) * 64 * R360_TICKET_GROUPS));
-    R360_HIP(hipMemset(c->d_gticket, 0, sizeof(unsigned) * 64 * R360_TICKET_GROUPS));
+    R360_HIP(hipMalloc(&c->d_gticket, sizeof(unsigned) * R360_TICKET_STRIDE * R360_TICKET_GROUPS));
+    R360_HIP(hipMemset(c->d_gticket, 0, sizeof(unsigned) * R360_TICKET_STRIDE * R360_TICKET_GROUPS));
     R360_HIP(hipMalloc(&c->d_ktime, sizeof(unsigned long long) * 17));
     R360_HIP(hipMemset(c->d_ktime, 0, sizeof(unsigned long long) * 17));
     R360_HIP(hipMemset(c->d_ktime, 0xff, sizeof(unsigned long long)));
@@ -127,6 +127,7 @@ extern "C" void r360_ctx_destroy(r360_ctx* c) {
     hipFree(c->d_state);
     hipFree(c->d_partials);
     hipFree(c->d_gticket);
+    hipFree(c->d_defer);
     hipFree(c->d_ktime);
     hipHostFree(c->h_state);
     hipFree(c->d_pin_state); hipFree(c->d_pin_partials); hipHostFree(c->h_pin_state);

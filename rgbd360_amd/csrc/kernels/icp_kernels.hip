@@ -20,10 +20,10 @@
 namespace {
 
 #ifndef R360_ICP_TPB
-#define R360_ICP_TPB 1024
+#define R360_ICP_TPB 512
 #endif
 #ifndef R360_ICP_MINB
-#define R360_ICP_MINB 1
+#define R360_ICP_MINB 4   // waves per SIMD (HIP launch_bounds 2nd arg): caps the pass at 128 VGPRs
 #endif
 constexpr int TPB = R360_ICP_TPB;  // 16 waves: one workgroup per CU at the kernel's occupancy, few records
 constexpr int NW = TPB / 64;
@@ -325,6 +325,11 @@ __device__ __forceinline__ int wave_count(bool b) { return __popcll(__ballot(b))
 template <int METHOD, int OCC>
 __device__ __forceinline__ void contribute_fast(Acc& A, WaveCnt& W, const Proj& o, const float4 G, const float2 T,
                                                 int fl, float angle_res_inv, const IcpConst& C) {
+#ifdef R360_EXP_NOACC   // experiment builds only: keep the operands alive, skip the math
+    A.h[0] += o.vis ? G.x + G.y + G.z + G.w + T.x + T.y + o.X + o.dist : 0.f;
+    W.c28 += wave_count(o.vis);
+    return;
+#endif
     constexpr bool photo = (METHOD == R360_PHOTO_CONSISTENCY || METHOD == R360_PHOTO_DEPTH);
     constexpr bool depth = (METHOD == R360_DEPTH_CONSISTENCY || METHOD == R360_PHOTO_DEPTH);
     const bool sal_p = !(fabsf(G.x) < C.thr_int && fabsf(G.y) < C.thr_int);
@@ -424,28 +429,26 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const float2* _
                                                  const float* __restrict__ costh, int nRows, int nCols,
                                                  IcpConst C, IcpState* S, double* __restrict__ partials, int first,
                                                  int eval_only, unsigned long long* __restrict__ kt,
-                                                 const uint8_t* __restrict__ occf, unsigned* __restrict__ gcnt) {
+                                                 const uint8_t* __restrict__ occf, unsigned* __restrict__ gcnt,
+                                                 int* __restrict__ dq) {
     __shared__ float s_red[NW][32];
     __shared__ double s_err[NW], s_errd[NW];
     __shared__ double s_fin[RG][32];
     __shared__ int s_last;
     __shared__ GnShared s_gn;
     __shared__ IcpState s_state;
-    constexpr int QCAP = 128;   // PF 3: deferred pixels per wave (<= 63 + 64 between drains)
-    __shared__ int s_queue[PF == 3 ? NW * QCAP : 1];
 
     if (S->stop) return;
 #ifdef R360_STAMPS
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #endif
     if (!first && !S->active && !eval_only) return;
-#ifndef R360_EXP_NOKT
-    if (threadIdx.x == 0)   // execution span: earliest workgroup start of this pass
-#else
-    if (false)
-#endif
-        __hip_atomic_fetch_min(kt, (unsigned long long)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+    // execution span: the start of workgroup 0 (dispatched first).  One store, not an atomic-min per
+    // workgroup: same-address atomics serialise at the memory side (~25 ns each), and 512 of them
+    // outlasted a short pass.
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_store(kt, (unsigned long long)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
 
     const float* pm = (first && !eval_only) ? S->pose : S->cand;
     Pose12 P;
@@ -563,13 +566,16 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const float2* _
     } else if (PF == 3) {
         // PF 2's pipelined wave stream with the guard-band lanes DEFERRED instead of fixed in place: a
         // lane whose fast projection lands near a rounding boundary drops out of its chunk (no
-        // contribution) and its pixel index goes to a per-wave LDS queue; full waves of queued pixels
-        // run the exact projection (project_exact) later, at every lane.  The chunk loop then has one
-        // straight-line path (no re-issued gathers), and the exact code runs at full lane occupancy
-        // instead of once per chunk that has any flagged lane (about a quarter of them at level 0).
+        // contribution) and its pixel index goes to the wave's queue in global memory (room for every
+        // pixel of the wave, so it never overflows); after the stream the wave runs the exact
+        // projection (project_exact) over its queue, 64 pixels at a time.  The chunk loop keeps one
+        // straight-line path (no re-issued gathers, no conditional accumulation that would make the
+        // compiler copy the accumulators), and the exact code runs at full lane occupancy instead of
+        // once per chunk that has any flagged lane (about a quarter of them at level 0).
         const int npx = nRows * nCols;
         const int lane = threadIdx.x & 63;
-        int* q = s_queue + (threadIdx.x >> 6) * QCAP;
+        const int qcap = ((npx + stride - 1) / stride) * 64;
+        int* q = dq + ((long)blockIdx.x * NW + (threadIdx.x >> 6)) * qcap;
         int qn = 0;   // wave-uniform queue length
         auto acc = [&](const Proj& o, const float4 G, const float2 T, int fl) {
             contribute_fast<METHOD, OCC>(A, W, o, G, T, fl, angle_res_inv, C);
@@ -596,22 +602,6 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const float2* _
                 qn += __popcll(m);
             }
         };
-        // exact pass over queue entries [0, n), one pixel per lane, then the queue moves down by n
-        auto drain = [&](int n) {
-            const bool act = lane < n;
-            const int i = q[act ? lane : 0];
-            const int r = i / nCols, c = i - r * nCols;
-            const float2 a = src[i];
-            Proj o = project_exact(P, lut_point(a.y, sinphi[r], cosphi[r], sinth[c], costh[c], C), a.x, nRows, nCols,
-                                   half_nRows, angle_res_inv);
-            o.vis = o.vis && act;
-            o.t = o.vis ? o.t : 0;
-            acc(o, gt.g(o.t), gt.T(o.t), act ? flag(i) : 0);
-            const int rest = qn - n;
-            const int moved = lane < rest ? q[n + lane] : 0;
-            if (lane < rest) q[lane] = moved;
-            qn = rest;
-        };
         const int b0 = __builtin_amdgcn_readfirstlane((blockIdx.x * TPB + (threadIdx.x & ~63)));
 #ifdef R360_EXP_NOLOOP   // experiment builds only: the pass without its pixel loop (fixed costs)
         if (false) {
@@ -636,7 +626,6 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const float2* _
                 const float2 TB = gt.T(oB.t);
                 acc(oA, GA, TA, fA);
                 if (k + 1 >= n_it) break;
-                if (qn >= 64) drain(64);
                 sB = ld(base(k + 3));
                 oA = prj(sA);
                 fA = sA.f;
@@ -645,9 +634,22 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const float2* _
                 TA = gt.T(oA.t);
                 acc(oB, GB, TB, fB);
                 if (k + 2 >= n_it) break;
-                if (qn >= 64) drain(64);
             }
-            while (qn > 0) drain(qn < 64 ? qn : 64);
+        }
+        if (qn > 0) {
+            // the queue was written by other lanes of this wave: order those stores before the reads
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            for (int s0 = 0; s0 < qn; s0 += 64) {
+                const bool act = s0 + lane < qn;
+                const int i = act ? q[s0 + lane] : 0;
+                const int r = i / nCols, c = i - r * nCols;
+                const float2 a = src[i];
+                Proj o = project_exact(P, lut_point(a.y, sinphi[r], cosphi[r], sinth[c], costh[c], C), a.x, nRows,
+                                       nCols, half_nRows, angle_res_inv);
+                o.vis = o.vis && act;
+                o.t = o.vis ? o.t : 0;
+                acc(o, gt.g(o.t), gt.T(o.t), act ? flag(i) : 0);
+            }
         }
     } else {
         // small levels: one pixel per thread, so the latency chain per thread is a quarter as long
@@ -686,6 +688,10 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const float2* _
     if ((lane & 1) == 0) s_red[wid][scatter_slot(lane)] = mine;
     if (lane == 0) { s_err[wid] = e2; s_errd[wid] = e2d; }
     __syncthreads();
+#ifdef R360_EXP_NOREC   // experiment builds only: no record, no ticket
+    if (s_red[0][0] == 1.2345f) S->dbg[7] = 1;
+    return;
+#endif
     if (threadIdx.x < 32) {
         double v;
         if (threadIdx.x == R360_SUM_ERR2) {
@@ -708,13 +714,13 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const float2* _
     // fence per workgroup wrote back each XCD's dirty L2 (tens of us per pass).
     // Two-level ticket: agent-scope atomics on one address serialise at the memory side (~50 ns each,
     // 256 of them were ~13 us of every level-0 pass), so workgroups first count in 16 group counters
-    // (256 B apart) and only the last of each group takes the pass ticket: 16 + 16 deep instead of 256.
+    // (4 KB apart) and only the last of each group takes the pass ticket: 32 + 16 deep instead of 512.
     if (threadIdx.x == 0) {
         const int nb = (int)gridDim.x;
         const int ng = nb < R360_TICKET_GROUPS ? nb : R360_TICKET_GROUPS;
         const int g = (int)blockIdx.x % R360_TICKET_GROUPS;
         const unsigned gsz = (unsigned)((nb - g + R360_TICKET_GROUPS - 1) / R360_TICKET_GROUPS);
-        const unsigned prev = __hip_atomic_fetch_add(gcnt + g * 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned prev = __hip_atomic_fetch_add(gcnt + g * R360_TICKET_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         int last = 0;
         if (prev == gsz - 1) {
             const unsigned p2 = __hip_atomic_fetch_add(&S->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -725,7 +731,7 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const float2* _
     __syncthreads();
     if (!s_last) return;
     if (threadIdx.x < R360_TICKET_GROUPS)   // every group is complete: reset its counter for the next pass
-        __hip_atomic_store(gcnt + threadIdx.x * 64, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(gcnt + threadIdx.x * R360_TICKET_STRIDE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #ifdef R360_STAMPS
     const unsigned long long t_ticket = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -812,7 +818,6 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const float2* _
             const int lv = C.level & 7;
             kt[1 + lv] += t1 > t0 ? t1 - t0 : 0;
             kt[9 + lv] += 1;
-            __hip_atomic_store(kt, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
@@ -1151,7 +1156,7 @@ static void launch_pass(r360_ctx* ctx, int nb, const LevelBufs& Ls, const LevelB
               : top        ? k_icp_pass<M, PF, 1, 0> : k_icp_pass<M, PF, 0, 0>;
     hipLaunchKernelGGL(kern, dim3(nb), dim3(TPB), 0, ctx->stream, Ls.p0, Lt.p0, Lt.tg, T.sinphi,
                        T.cosphi, T.sinth, T.costh, Ls.rows, Ls.cols, C, ctx->d_state, ctx->d_partials, first,
-                       eval_only, ctx->d_ktime, ctx->occ_flags, ctx->d_gticket);
+                       eval_only, ctx->d_ktime, ctx->occ_flags, ctx->d_gticket, ctx->d_defer);
 }
 
 int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src, int level, int method,
@@ -1182,6 +1187,15 @@ int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src
     if (cap > ctx->partials_cap) cap = ctx->partials_cap;
     int nb = pf == 1 ? icp_blocks_for(npx) : (npx + TPB - 1) / TPB;
     if (nb > cap) nb = cap;
+    if (pf == 3) {   // deferred-pixel queues: one per wave, room for every pixel the wave streams
+        const long stride = (long)nb * TPB;
+        const long need = (long)nb * (TPB / 64) * (((npx + stride - 1) / stride) * 64);
+        if (ctx->defer_cap < need) {
+            (void)hipFree(ctx->d_defer);
+            R360_HIP(hipMalloc(&ctx->d_defer, sizeof(int) * need));
+            ctx->defer_cap = need;
+        }
+    }
     if (C.occ) {   // occlusion flags of this pass's pose (same stream, before the fused pass)
         if (ctx->occ_cap < npx) {
             (void)hipFree(ctx->occ_tgt); (void)hipFree(ctx->occ_dinv); (void)hipFree(ctx->occ_flags);

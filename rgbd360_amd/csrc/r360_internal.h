@@ -74,6 +74,7 @@ struct alignas(16) IcpState {
 };
 
 constexpr int R360_TICKET_GROUPS = 16;
+constexpr int R360_TICKET_STRIDE = 1024;   // uints between group counters (4 KB)
 
 // Pass sums.  Occlusion variants: NVALID counts photo terms (Occ1) or accepted points (Occ2), NDEPTH
 // the depth terms (Occ1), ERR2 the photometric and ERR2D the depth squared residuals.
@@ -169,7 +170,9 @@ struct r360_ctx {
     hipEvent_t wait_ev = nullptr;   // blocking-sync event: host waits sleep instead of spinning
     IcpState* d_state = nullptr;
     double* d_partials = nullptr;
-    unsigned* d_gticket = nullptr;   // group arrival counters of the ICP pass (R360_TICKET_GROUPS x 256 B)
+    unsigned* d_gticket = nullptr;   // group arrival counters of the ICP pass (R360_TICKET_GROUPS x 4 KB)
+    int* d_defer = nullptr;          // ICP pass (PF 3): per-wave queues of deferred (exactly re-projected) pixels
+    long defer_cap = 0;
     // in-kernel execution spans of the ICP passes (s_memrealtime, 100 MHz): [0] earliest workgroup start
     // of the running pass, [1+l] summed spans at level l, [9+l] pass counts
     unsigned long long* d_ktime = nullptr;
