@@ -23,8 +23,8 @@ rows = list(csv.DictReader(open(trace)))
 
 
 def is_l0(name):
-    # the level-0 instantiation carries template tag TOP = 1: k_icp_pass<METHOD, PF, 1>
-    return re.search(r"k_icp_pass<\d+, \d+, 1>", name) is not None or re.search(r"k_icp_passILi\d+ELi\d+ELi1E", name) is not None
+    # the level-0 instantiation carries template tag TOP = 1: k_icp_pass<METHOD, PF, 1, OCC>
+    return re.search(r"k_icp_pass<\d+, \d+, 1[,>]", name) is not None or re.search(r"k_icp_passILi\d+ELi\d+ELi1E", name) is not None
 
 
 icp = [r for r in rows if is_l0(r["Kernel_Name"])]
