@@ -275,6 +275,68 @@ int r360_pbmap_match_tables(r360_ctx* ctx, r360_frame* ref, r360_frame* trg, siz
                             int mode, int* ns, int* nt, int* sid, int* tid, uint8_t* unary,
                             uint64_t* binary, int cap);
 
+/* ---------------------------------------------------------------- batched registrations (§8f-4)
+ * Many independent pair registrations on one GPU, as SphereGraphSLAM's tracking loop
+ * (SLAM/SphereGraphSLAM.cpp:169-231: RegisterPbMap against up to numCheckRegistration = 5 previous
+ * keyframes) and LoopClosure360's candidate checks (include/LoopClosure360.h:280-366: RegisterPbMap
+ * PLANAR_3DoF, gate on matches/area, alignFrames360 refinement) issue them.  A batch owns `lanes`
+ * worker contexts (own HIP stream, ICP state and matcher scratch) and runs the jobs of one call
+ * concurrently, one host thread per lane.  Every job computes exactly what the sequential reference
+ * call computes: the result of a batched job is identical to r360_register_pbmap / r360_align360 on
+ * the same frames.  Frames may belong to any ctx of the same device; each lane's stream waits for
+ * the frames' build work before reading them.  The caller must not modify or destroy a frame while a
+ * batch call that names it runs. */
+typedef struct r360_batch r360_batch;
+int  r360_batch_create(int device, int lanes, r360_batch** out);
+void r360_batch_destroy(r360_batch* b);
+int  r360_batch_lanes(const r360_batch* b);
+
+/* dense stage of one job */
+enum {
+    R360_JOB_PBMAP_ONLY = 0,  /* RegisterPbMap only (SphereGraphSLAM tracking)                          */
+    R360_JOB_GATED = 1,       /* alignFrames360 only when RegisterPbMap succeeded with n_match > min_matches
+                                 and area_matched > min_area (LoopClosure360.h:298, 342)                */
+    R360_JOB_ALWAYS = 2       /* Register(): alignFrames360 from the PbMap pose, or from `guess` when the
+                                 PbMap stage failed (OdometryKeyFrame360.cpp:205-254)                   */
+};
+typedef struct {
+    r360_frame* ref;          /* RegisterPbMap(ref, trg, ...): pRef360 (RegisterRGBD360.h:276)           */
+    r360_frame* trg;
+    int   dense;              /* R360_JOB_*                                                               */
+    int   ref_is_source;      /* dense roles. 0: setTargetFrame(ref), setSourceFrame(trg)
+                                 (OdometryKeyFrame360.cpp:248-249, LoopClosure360.h:348-349).
+                                 1: setSourceFrame(ref), setTargetFrame(trg) (LoopClosure360.h:309-310) */
+    float guess[16];          /* R360_JOB_ALWAYS fallback pose (rig frame)                               */
+} r360_pair_job;
+typedef struct {
+    int   good;               /* RegisterPbMap's return value (1 / 0)                                    */
+    int   n_match;            /* getMatchedPlanes().size()                                               */
+    float area_matched, area_src, area_trg, sso_pbmap;   /* getAreaMatched(), areaSource, areaTarget,
+                                 areaMatched / areaSource (SphereGraphSLAM.cpp:214-215; 0 if not good)   */
+    float pbmap_pose[16];     /* getPose() (identity if not good)                                        */
+    float pbmap_info[36];     /* getInfoMat() (zeros if not good)                                        */
+    int   dense_rc;           /* -1: dense stage not run; 0 ok; 1 ill-posed (R360_ILLPOSED)               */
+    float pose[16];           /* rotOffset^-1 * getOptimalPose() * rotOffset (LoopClosure360.h:313, 352) */
+    float hessian[36];        /* getHessian()                                                            */
+    r360_icp_stats stats;     /* SSO, accepted error, iterations                                         */
+} r360_pair_result;
+
+/* Runs the n jobs.  max_match_planes/mode apply to every RegisterPbMap; min_matches/min_area gate
+ * R360_JOB_GATED jobs; p = the dense stage's RegisterPhotoICP parameters (PHOTO_DEPTH, occlusion 0).
+ * Returns 0, or the first job error (< 0, message in r360_last_error()). */
+int r360_batch_register(r360_batch* b, const r360_pair_job* jobs, int n, size_t max_match_planes, int mode,
+                        int min_matches, float min_area, const r360_icp_params* p, r360_pair_result* out);
+
+/* SphereGraphSLAM tracking step (SphereGraphSLAM.cpp:169-231): RegisterPbMap(kfs[j], frame,
+ * max_match_planes, mode) for j = n_kf-1, n_kf-2, ... (newest keyframe first) while fewer than
+ * num_check candidates and fewer than no_assoc_threshold failures were tried; the first good one wins.
+ * All candidates are registered at once; *chosen = index into kfs of the winner, or -1 ("No
+ * registration available").  result (optional) = the winner's r360_pair_result; cand (optional,
+ * min(n_kf, num_check, no_assoc_threshold) entries) = every candidate's result in reference order. */
+int r360_track_frame(r360_batch* b, r360_frame* const* kfs, int n_kf, r360_frame* frame, int num_check,
+                     int no_assoc_threshold, size_t max_match_planes, int mode, int* chosen,
+                     r360_pair_result* result, r360_pair_result* cand);
+
 /* Inspection hooks of the per-pixel plane half (parity tests).  Sizes: 8 x (rows/2) x (cols/2). */
 typedef struct {
     int   label, count, start_idx, n_contour, n_fit;

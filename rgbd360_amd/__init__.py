@@ -26,7 +26,7 @@ C = C  # re-exported for callers that drive the C-ABI directly (bench.py)
 __all__ = [
     "lib", "Context", "Calib360", "Frame360", "RegisterPhotoICP", "RegisterRGBD360", "IcpParams", "IcpStats",
     "PHOTO_CONSISTENCY", "DEPTH_CONSISTENCY", "PHOTO_DEPTH", "synth_path_pose", "exp_se3",
-    "LIB_PATH", "ABI_SYMBOLS",
+    "LIB_PATH", "ABI_SYMBOLS", "Batch", "PairJob", "PairResult", "JOB_PBMAP_ONLY", "JOB_GATED", "JOB_ALWAYS",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -60,6 +60,32 @@ class IcpStats(C.Structure):
         ("iters", C.c_int * 8), ("evals", C.c_int * 8), ("illposed", C.c_int), ("sso", C.c_float),
         ("error", C.c_double), ("passes", C.c_int), ("pad", C.c_int),
     ]
+
+
+class PairJob(C.Structure):
+    """r360_pair_job — one pair of a batched registration call (include/rgbd360_hip.h, §8f-4)."""
+    _fields_ = [("ref", C.c_void_p), ("trg", C.c_void_p), ("dense", C.c_int), ("ref_is_source", C.c_int),
+                ("guess", C.c_float * 16)]
+
+
+class PairResult(C.Structure):
+    """r360_pair_result — RegisterPbMap outputs and the dense refinement of one batched pair."""
+    _fields_ = [("good", C.c_int), ("n_match", C.c_int), ("area_matched", C.c_float), ("area_src", C.c_float),
+                ("area_trg", C.c_float), ("sso_pbmap", C.c_float), ("pbmap_pose", C.c_float * 16),
+                ("pbmap_info", C.c_float * 36), ("dense_rc", C.c_int), ("pose", C.c_float * 16),
+                ("hessian", C.c_float * 36), ("stats", IcpStats)]
+
+    def as_dict(self) -> dict:
+        return {"good": self.good, "n_match": self.n_match, "area_matched": self.area_matched,
+                "area_src": self.area_src, "area_trg": self.area_trg, "sso_pbmap": self.sso_pbmap,
+                "pbmap_pose": _from16(np.array(self.pbmap_pose, np.float32)),
+                "pbmap_info": np.array(self.pbmap_info, np.float32).reshape(6, 6).T.copy(),
+                "dense_rc": self.dense_rc, "pose": _from16(np.array(self.pose, np.float32)),
+                "hessian": np.array(self.hessian, np.float32).reshape(6, 6).T.copy(),
+                "sso": self.stats.sso, "error": self.stats.error}
+
+
+JOB_PBMAP_ONLY, JOB_GATED, JOB_ALWAYS = 0, 1, 2
 
 
 class DenseStats(C.Structure):
@@ -158,6 +184,13 @@ _SIGS = [
     ("r360_register_async", C.c_int, [_P, _P, _P, _FP, C.POINTER(IcpParams), C.c_size_t, C.c_int]),
     ("r360_register_result", C.c_int, [_P, _FP, _FP, C.POINTER(IcpStats)]),
     ("r360_pbmap_match_tables", C.c_int, [_P, _P, _P, C.c_size_t, C.c_int, _IP, _IP, _IP, _IP, _P, _P, C.c_int]),
+    ("r360_batch_create", C.c_int, [C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
+    ("r360_batch_destroy", None, [_P]),
+    ("r360_batch_lanes", C.c_int, [_P]),
+    ("r360_batch_register", C.c_int, [_P, C.POINTER(PairJob), C.c_int, C.c_size_t, C.c_int, C.c_int, C.c_float,
+                                      C.POINTER(IcpParams), C.POINTER(PairResult)]),
+    ("r360_track_frame", C.c_int, [_P, C.POINTER(C.c_void_p), C.c_int, _P, C.c_int, C.c_int, C.c_size_t, C.c_int,
+                                   _IP, C.POINTER(PairResult), C.POINTER(PairResult)]),
     ("r360_frame_get_cloud", C.c_int, [_P, _FP, _P, _FP, _FP]),
     ("r360_frame_get_labels", C.c_int, [_P, _IP, _IP]),
     ("r360_frame_get_regions", C.c_int, [_P, C.c_int, C.POINTER(Region), C.c_int, _IP]),
@@ -617,6 +650,70 @@ def register(ctx: "Context", ref: "Frame360", trg: "Frame360", guess=None, param
     rc = _check(lib().r360_register(ctx.h, ref.h, trg.h, _fptr(g), C.byref(p), max_match_planes, mode, _fptr(pose),
                                     _fptr(info), C.byref(st)), "register")
     return _from16(pose), info.reshape(6, 6).T.copy(), st, rc == 0
+
+
+class Batch:
+    """Batched pair registrations (r360_batch, §8f-4): `lanes` worker contexts on one GPU run the jobs of a
+    call concurrently.  Each job is the single-pair code path, so results equal the sequential calls.
+
+    * ``register_pairs`` — generic jobs (RegisterPbMap, optionally gated / always refined by alignFrames360).
+    * ``track`` — SphereGraphSLAM's tracking step (SLAM/SphereGraphSLAM.cpp:169-231).
+    * ``loop_closures`` — LoopClosure360's candidate checks (include/LoopClosure360.h:280-366).
+    """
+
+    def __init__(self, device: int = 0, lanes: int = 8):
+        h = C.c_void_p()
+        _check(lib().r360_batch_create(device, lanes, C.byref(h)), "r360_batch_create")
+        self.h = h
+        self.lanes = lib().r360_batch_lanes(h)
+
+    def register_pairs(self, jobs, max_match_planes: int = 25, mode: int = PLANAR_3DoF, min_matches: int = 0,
+                       min_area: float = 0.0, params: "IcpParams | None" = None) -> list[dict]:
+        """jobs: iterable of dicts {ref, trg, dense=JOB_PBMAP_ONLY, ref_is_source=False, guess=None}."""
+        jobs = list(jobs)
+        arr = (PairJob * max(1, len(jobs)))()
+        for a, j in zip(arr, jobs):
+            a.ref, a.trg = j["ref"].h.value, j["trg"].h.value
+            a.dense = int(j.get("dense", JOB_PBMAP_ONLY))
+            a.ref_is_source = int(bool(j.get("ref_is_source", False)))
+            g = j.get("guess")
+            a.guess[:] = [float(v) for v in _mat16(np.eye(4) if g is None else g)]
+        out = (PairResult * max(1, len(jobs)))()
+        p = params if params is not None else IcpParams.default()
+        _check(lib().r360_batch_register(self.h, arr, len(jobs), max_match_planes, mode, min_matches, min_area,
+                                         C.byref(p), out), "r360_batch_register")
+        return [out[i].as_dict() for i in range(len(jobs))]
+
+    def track(self, keyframes, frame, num_check: int = 5, no_assoc_threshold: int = 40, max_match_planes: int = 25,
+              mode: int = PLANAR_ODOMETRY_3DoF):
+        """Register `frame` against the newest keyframes (list, oldest first) -> (index into keyframes or -1,
+        winner's result dict or None, every candidate's result in the reference's order)."""
+        kfs = list(keyframes)
+        ptrs = (C.c_void_p * max(1, len(kfs)))(*[k.h.value for k in kfs])
+        m = min(len(kfs), num_check, no_assoc_threshold)
+        res, cand = PairResult(), (PairResult * max(1, m))()
+        chosen = C.c_int()
+        _check(lib().r360_track_frame(self.h, ptrs, len(kfs), frame.h, num_check, no_assoc_threshold,
+                                      max_match_planes, mode, C.byref(chosen), C.byref(res), cand), "r360_track_frame")
+        return chosen.value, (res.as_dict() if chosen.value >= 0 else None), [cand[i].as_dict() for i in range(m)]
+
+    def loop_closures(self, pairs, min_matches: int = 5, min_area: float = 15.0, ref_is_source: bool = True,
+                      params: "IcpParams | None" = None, max_match_planes: int = 25) -> list[dict]:
+        """pairs: [(keyframe, new_keyframe)].  RegisterPbMap PLANAR_3DoF, the matches/area gate
+        (LoopClosure360.h:114-115, 298) and the alignFrames360 refinement of the pairs that pass."""
+        jobs = [{"ref": a, "trg": b, "dense": JOB_GATED, "ref_is_source": ref_is_source} for a, b in pairs]
+        return self.register_pairs(jobs, max_match_planes, PLANAR_3DoF, min_matches, min_area, params)
+
+    def close(self):
+        if self.h:
+            lib().r360_batch_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class RegisterPhotoICP:

@@ -875,9 +875,8 @@ extern "C" int r360_register_pbmap(r360_ctx* ctx, r360_frame* ref, r360_frame* t
 // Register(): PbMap registration, then the dense refinement initialised with the rotOffset-conjugated
 // PbMap pose (OdometryKeyFrame360.cpp:167-171, 205, 244-254).  guess = fallback initial pose in the rig
 // frame when the PbMap registration fails (the caller's previous relative pose).
-namespace {
 // rotOffset: rotation of angleOffset = 157.5 deg about x (OdometryRGBD360.cpp:138-139), column-major
-void rot_offset(float Ro[16], float Ri[16]) {
+void r360_rot_offset(float Ro[16], float Ri[16]) {
     const float a = 157.5f;
     const float c = (float)cos(a * R360_PI / 180), s = (float)sin(a * R360_PI / 180);
     const float o[16] = {1, 0, 0, 0, 0, c, -s, 0, 0, s, c, 0, 0, 0, 0, 1};   // (1,2) = s, (2,1) = -s
@@ -885,7 +884,7 @@ void rot_offset(float Ro[16], float Ri[16]) {
     memcpy(Ro, o, sizeof o);
     memcpy(Ri, t, sizeof t);
 }
-void mul4(const float* A, const float* B, float* C) {   // Eigen Matrix4f product order
+void r360_mul4(const float* A, const float* B, float* C) {   // Eigen Matrix4f product order
     float out[16];
     for (int col = 0; col < 4; ++col)
         for (int r = 0; r < 4; ++r) {
@@ -895,7 +894,6 @@ void mul4(const float* A, const float* B, float* C) {   // Eigen Matrix4f produc
         }
     memcpy(C, out, sizeof out);
 }
-}  // namespace
 
 extern "C" int r360_register_async(r360_ctx* ctx, r360_frame* ref, r360_frame* trg, const float guess[16],
                                    const r360_icp_params* p, size_t max_match_planes, int mode) {
@@ -907,9 +905,9 @@ extern "C" int r360_register_async(r360_ctx* ctx, r360_frame* ref, r360_frame* t
                                          nullptr, nullptr);
     if (good < 0) return good;
     float Ro[16], Ri[16], t1[16], init[16];
-    rot_offset(Ro, Ri);
-    mul4(Ro, pb, t1);
-    mul4(t1, Ri, init);                             // rotOffset * pose * rotOffset^-1
+    r360_rot_offset(Ro, Ri);
+    r360_mul4(Ro, pb, t1);
+    r360_mul4(t1, Ri, init);                             // rotOffset * pose * rotOffset^-1
     if (int rc = r360_align360_async(ctx, ref, trg, init, R360_PHOTO_DEPTH, 0, p)) return rc;
     ctx->reg_pending = 1;
     ctx->reg_good = good;
@@ -924,9 +922,9 @@ extern "C" int r360_register_result(r360_ctx* ctx, float pose[16], float info[36
     const int rc = r360_align360_result(ctx, dense, nullptr, nullptr, st);
     if (rc < 0) return rc;
     float Ro[16], Ri[16], t2[16];
-    rot_offset(Ro, Ri);
-    mul4(Ri, dense, t2);
-    mul4(t2, Ro, pose);                             // rotOffset^-1 * dense * rotOffset
+    r360_rot_offset(Ro, Ri);
+    r360_mul4(Ri, dense, t2);
+    r360_mul4(t2, Ro, pose);                             // rotOffset^-1 * dense * rotOffset
     if (info) memcpy(info, ctx->reg_info, sizeof ctx->reg_info);
     return ctx->reg_good ? 0 : 1;
 }

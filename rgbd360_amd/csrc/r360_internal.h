@@ -324,6 +324,9 @@ void plane_bufs_free(r360_frame* f);
 int planes_enqueue(r360_frame* f);
 int ctx_vhash_reserve(r360_ctx* ctx, long min_cells);
 int planes_finish(r360_frame* f);
+// rotOffset (157.5 deg about x, OdometryRGBD360.cpp:138-139) and its inverse; column-major 4x4 product C = A*B
+void r360_rot_offset(float Ro[16], float Ri[16]);
+void r360_mul4(const float* A, const float* B, float* C);
 int planes_assemble(r360_frame* f);
 void planes_join(r360_frame* f);
 
