@@ -13,6 +13,9 @@
 //                                                  getAreaMatched :251, areaSource/areaTarget :91-94,
 //                                                  RegisterDensePhotoICP :344,
 //                                                  Register() = OdometryKeyFrame360.cpp:205-254
+//   BatchRegistration  many independent pair registrations on one GPU (§8f-4): SphereGraphSLAM's
+//                      tracking loop (SLAM/SphereGraphSLAM.cpp:169-231) and LoopClosure360's candidate
+//                      checks (include/LoopClosure360.h:280-366)
 //
 // Header-only; every body is a call into the C-ABI (include/rgbd360_hip.h).  Matrices are the
 // column-major Eigen layout; r360::Matrix4f / Matrix6f are minimal stand-ins with Eigen's (row, col)
@@ -341,6 +344,59 @@ class RegisterRGBD360 {
     Matrix6f informationM_;
     std::map<unsigned, unsigned> bestMatch_;
     float areaMatched_ = 0.f;
+};
+
+// ------------------------------------------------------------------ batched registrations (§8f-4)
+// Worker lanes (own HIP streams and ICP state) run the pairs of one call concurrently; each pair is the
+// single-pair code path, so results equal sequential RegisterRGBD360 / RegisterPhotoICP calls.
+class BatchRegistration {
+  public:
+    BatchRegistration(int device = 0, int lanes = 8) { check(r360_batch_create(device, lanes, &h_), "r360_batch_create"); }
+    ~BatchRegistration() { r360_batch_destroy(h_); }
+    BatchRegistration(const BatchRegistration&) = delete;
+    BatchRegistration& operator=(const BatchRegistration&) = delete;
+    // generic jobs: RegisterPbMap(ref, trg) and the dense stage each job asks for (R360_JOB_*)
+    std::vector<r360_pair_result> registerPairs(const std::vector<r360_pair_job>& jobs, size_t max_match_planes,
+                                                RegisterRGBD360::registrationType mode, const r360_icp_params* icp,
+                                                int min_matches = 0, float min_area = 0.f) {
+        std::vector<r360_pair_result> out(jobs.size());
+        check(r360_batch_register(h_, jobs.data(), int(jobs.size()), max_match_planes, mode, min_matches, min_area,
+                                  icp, out.data()),
+              "registerPairs");
+        return out;
+    }
+    // SphereGraphSLAM tracking step: keyframes oldest first; returns the index of the keyframe the sequential
+    // loop registers against (-1: "No registration available"), its result in *winner
+    int track(const std::vector<Frame360*>& keyframes, Frame360* frame, r360_pair_result* winner = nullptr,
+              int numCheckRegistration = 5, int noAssoc_threshold = 40, size_t max_match_planes = 25,
+              RegisterRGBD360::registrationType mode = RegisterRGBD360::PLANAR_ODOMETRY_3DoF) {
+        std::vector<r360_frame*> kf;
+        for (auto f : keyframes) kf.push_back(f->get());
+        int chosen = -1;
+        check(r360_track_frame(h_, kf.data(), int(kf.size()), frame->get(), numCheckRegistration, noAssoc_threshold,
+                               max_match_planes, mode, &chosen, winner, nullptr),
+              "track");
+        return chosen;
+    }
+    // LoopClosure360 candidate checks: RegisterPbMap PLANAR_3DoF, gate n_match > minMatchesThreshold and
+    // area_matched > areaThreshold (LoopClosure360.h:114-115), then alignFrames360 (keyframe as source,
+    // :309-313) of the pairs that pass
+    std::vector<r360_pair_result> loopClosures(const std::vector<std::pair<Frame360*, Frame360*> >& pairs,
+                                               const r360_icp_params& icp, int minMatchesThreshold = 5,
+                                               float areaThreshold = 15.f) {
+        std::vector<r360_pair_job> jobs(pairs.size());
+        for (size_t i = 0; i < pairs.size(); ++i) {
+            std::memset(&jobs[i], 0, sizeof(r360_pair_job));
+            jobs[i].ref = pairs[i].first->get();
+            jobs[i].trg = pairs[i].second->get();
+            jobs[i].dense = R360_JOB_GATED;
+            jobs[i].ref_is_source = 1;
+        }
+        return registerPairs(jobs, 25, RegisterRGBD360::PLANAR_3DoF, &icp, minMatchesThreshold, areaThreshold);
+    }
+    r360_batch* get() const { return h_; }
+  private:
+    r360_batch* h_ = nullptr;
 };
 
 }  // namespace r360
