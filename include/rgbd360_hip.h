@@ -285,7 +285,7 @@ int r360_pbmap_match_tables(r360_ctx* ctx, r360_frame* ref, r360_frame* trg, siz
  * call computes: the result of a batched job is identical to r360_register_pbmap / r360_align360 on
  * the same frames.  Frames may belong to any ctx of the same device; each lane's stream waits for
  * the frames' build work before reading them.  The caller must not modify or destroy a frame while a
- * batch call that names it runs. */
+ * batch call that names it runs.  A batch is driven by one host thread at a time. */
 typedef struct r360_batch r360_batch;
 int  r360_batch_create(int device, int lanes, r360_batch** out);
 void r360_batch_destroy(r360_batch* b);

@@ -3,12 +3,15 @@
 // (SLAM/SphereGraphSLAM.cpp:169-231, include/LoopClosure360.h:280-366).  The reference runs them one
 // after another on one RegisterRGBD360 / RegisterPhotoICP object.  Here a batch owns `lanes` worker
 // contexts (each with its own HIP stream, device GN state and matcher scratch) and one host thread per
-// lane, so the host interpretation-tree searches of different pairs overlap each other and the dense
+// lane (persistent workers), so the host interpretation-tree searches of different pairs overlap each other and the dense
 // refinements of different pairs run side by side on the GPU.  Every job is the unchanged single-pair
 // code path (r360_register_pbmap, r360_align360_async/_result), so batched results are identical to
 // sequential ones.
 #include <atomic>
+#include <condition_variable>
 #include <cstring>
+#include <functional>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -28,6 +31,45 @@ struct r360_batch {
     int device = 0;
     std::vector<r360_ctx*> lane;
     std::vector<hipEvent_t> dep;   // one "frame built" event per distinct frame of a call (grown on demand)
+    // persistent workers for lanes 1..L-1 (the calling thread drives lane 0): a call publishes `task` under a
+    // new generation number and waits until every worker has run it
+    std::vector<std::thread> th;
+    std::mutex m;
+    std::condition_variable go, done;
+    unsigned long gen = 0;
+    int busy = 0;
+    bool stop = false;
+    std::function<void(int)> task;
+
+    void worker(int l) {
+        hipSetDevice(device);
+        unsigned long seen = 0;
+        for (;;) {
+            std::function<void(int)> t;
+            {
+                std::unique_lock<std::mutex> lk(m);
+                go.wait(lk, [&] { return stop || gen != seen; });
+                if (stop) return;
+                seen = gen;
+                t = task;
+            }
+            t(l);
+            std::lock_guard<std::mutex> lk(m);
+            if (--busy == 0) done.notify_all();
+        }
+    }
+    void run(const std::function<void(int)>& fn) {
+        {
+            std::lock_guard<std::mutex> lk(m);
+            task = fn;
+            busy = int(th.size());
+            ++gen;
+        }
+        go.notify_all();
+        fn(0);
+        std::unique_lock<std::mutex> lk(m);
+        done.wait(lk, [&] { return busy == 0; });
+    }
 };
 
 extern "C" int r360_batch_create(int device, int lanes, r360_batch** out) {
@@ -40,12 +82,19 @@ extern "C" int r360_batch_create(int device, int lanes, r360_batch** out) {
         if (int rc = r360_ctx_create(device, &c)) { r360_batch_destroy(b); return rc; }
         b->lane.push_back(c);
     }
+    for (int l = 1; l < lanes; ++l) b->th.emplace_back(&r360_batch::worker, b, l);
     *out = b;
     return 0;
 }
 
 extern "C" void r360_batch_destroy(r360_batch* b) {
     if (!b) return;
+    {
+        std::lock_guard<std::mutex> lk(b->m);
+        b->stop = true;
+    }
+    b->go.notify_all();
+    for (auto& t : b->th) t.join();
     for (auto c : b->lane) r360_ctx_destroy(c);
     hipSetDevice(b->device);
     for (auto e : b->dep) hipEventDestroy(e);
@@ -153,21 +202,15 @@ extern "C" int r360_batch_register(r360_batch* b, const r360_pair_job* jobs, int
     FrameDeps D;
     if (int rc = prepare_frames(b, frames, true, D)) return rc;
 
-    const int L = std::min<int>(int(b->lane.size()), n);
     std::atomic<int> next{0};
     std::vector<int> rcs(n, 0);
     std::vector<std::string> errs(n);
-    auto worker = [&](int l) {
-        hipSetDevice(b->device);
+    b->run([&](int l) {
         for (int i = next++; i < n; i = next++) {
             rcs[i] = run_job(b->lane[l], D, jobs[i], max_match_planes, mode, min_matches, min_area, p, out[i]);
             if (rcs[i] < 0) errs[i] = r360_last_error();
         }
-    };
-    std::vector<std::thread> th;
-    for (int l = 1; l < L; ++l) th.emplace_back(worker, l);
-    worker(0);
-    for (auto& t : th) t.join();
+    });
     for (int i = 0; i < n; ++i)
         if (rcs[i] < 0) {
             r360_set_error("job %d: %s", i, errs[i].c_str());
