@@ -298,18 +298,20 @@ def main():
     # command (tools/profile.sh + tools/profile_summary.py, committed under profiles/)
     traffic = None
     tf = os.path.join(ROOT, "profiles", "latest", "l0_pass.json")
-    if os.path.exists(tf):
-        traffic = json.load(open(tf)).get("hbm_bytes_per_launch")
+    if os.path.exists(tf) and (args.rows, args.cols, args.workload) == (480, 640, "full"):
+        traffic = json.load(open(tf)).get("hbm_bytes_per_launch")   # profiled on the default workload only
     pairs_timed = args.steps * P
     if args.workload == "full":
-        workload = ("config2+3 (run as config4's sequence): per pair, the new synthetic 8x640x480 Frame360 is "
+        workload = ("config2+3 (run as config4's sequence): per pair, the new synthetic "
+                    f"8x{args.cols}x{args.rows} Frame360 is "
                     "built on the GPU (undistort, cloud + median downsample, bilateral, normals, plane "
                     "segmentation + refinement, PbMap descriptors/grouping, stitch, 5-level pyramid), then "
                     "RegisterPbMap(25 planes, PLANAR_3DoF) + alignFrames360(PHOTO_DEPTH) initialised with the "
                     f"rotOffset-conjugated PbMap pose: levels 4..1 reference schedule + {args.iters0} GN "
                     "iterations at level 0")
     else:
-        workload = ("config3: synthetic 8x640x480 Frame360 pair -> stitch + 5-level pyramid x2 -> "
+        workload = (("config5" if args.rows == 960 else "config3") + f": synthetic 8x{args.cols}x{args.rows} "
+                    "Frame360 pair -> stitch + 5-level pyramid x2 -> "
                     f"alignFrames360(PHOTO_DEPTH) levels 4..1 reference schedule + {args.iters0} GN iterations "
                     "at level 0")
     out = {
