@@ -636,6 +636,9 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const float2* _
                 if (k + 2 >= n_it) break;
             }
         }
+#ifdef R360_EXP_NODRAIN   // experiment builds only: deferred lanes dropped
+        qn = 0;
+#endif
         if (qn > 0) {
             // the queue was written by other lanes of this wave: order those stores before the reads
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
