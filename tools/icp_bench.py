@@ -21,6 +21,9 @@ reg = R.RegisterPhotoICP(ctx)
 reg.setNumPyr(5); reg.setGrayVariance(3.0 / 255)
 reg.setTargetFrame(fr[0]); reg.setSourceFrame(fr[1])
 P = np.eye(4, dtype=np.float32)
+if os.environ.get("POSE") == "path":   # the synthetic path's true relative motion between the two frames
+    P0, P1 = (np.asarray(R.synth_path_pose(seed, i), dtype=np.float64).reshape(4, 4) for i in range(2))
+    P = (np.linalg.inv(P0) @ P1).astype(np.float32)
 tag = f"PF={os.environ.get('R360_ICP_PF', 'dflt')} CAP={os.environ.get('R360_ICP_CAP', 'dflt')}"
 for lv in [int(x) for x in os.environ.get("LEVELS", "0,1,2").split(",")]:
     for _ in range(3):
