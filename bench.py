@@ -128,6 +128,7 @@ def main():
     ap.add_argument("--streams", type=int, default=16, help="pairs in flight per GPU (one pipeline = host thread + HIP stream each)")
     ap.add_argument("--window", type=int, default=16, help="sequence frames resident per pipeline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--eval-probe", action="store_true", help="diagnostic: also time the level-0 pass in eval mode")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -294,6 +295,21 @@ def main():
     us, n = ctxs[0].kernel_time(0)
     iso_ms = us / max(n, 1) * 1e-3
     iso_ach = alg_bytes / (iso_ms * 1e-3) / 1e9 if n else None
+    probe = None
+    if args.eval_probe:   # opt-in diagnostic: the level-0 pass in eval mode (no GN step) at identity, alone
+        j = (args.warmup + args.steps + 2) % (F - 1)
+        reg = R.RegisterPhotoICP(ctxs[0])
+        reg.setNumPyr(5); reg.setGrayVariance(3.0 / 255)
+        reg.setTargetFrame(frames[0][j]); reg.setSourceFrame(frames[0][j + 1])
+        for _ in range(3):
+            reg.eval(0, np.eye(4, dtype=np.float32), R.PHOTO_DEPTH)
+        ctxs[0].kernel_time_reset()
+        for _ in range(30):
+            reg.eval(0, np.eye(4, dtype=np.float32), R.PHOTO_DEPTH)
+        ctxs[0].sync()
+        pu, pn = ctxs[0].kernel_time(0)
+        probe = {"avg_launch_ms": pu / max(pn, 1) * 1e-3, "launches": pn,
+                 "note": "eval mode at identity pose, pipeline 0's last pair, in-kernel span"}
     # HBM bytes per level-0 launch from the rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes of this same
     # command (tools/profile.sh + tools/profile_summary.py, committed under profiles/)
     traffic = None
@@ -332,6 +348,7 @@ def main():
             "isolated": {"avg_launch_ms": iso_ms, "launches": n, "achieved": iso_ach,
                          "frac": (iso_ach / HBM_PEAK_GBS) if iso_ach else None,
                          "note": "same pass, pipeline 0 alone on the GPU (3 pairs after the timed region)"},
+            **({"eval_probe": probe} if probe else {}),
         },
         "stage_ms_per_pair": {k: v / max(pairs_timed, 1) for k, v in stage.items()},
     }
