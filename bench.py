@@ -1,32 +1,36 @@
 """bench.py — registered Frame360 pairs/sec on MI355X (BASELINE.json metric) + ICP-reduce roofline.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload full|dense]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload sequence|dense]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-Workload "full" (default; BASELINE.json configs[1]+[2] as one registration, run the way configs[3]
-runs them): the synthetic 256-frame OdometryRGBD360 sequence (procedural room, seed 360, 8 x 480x640
-sensors).  One step registers, on each of P pipelines of each GPU, the next consecutive pair of the
-rank's shard (pipelines run free on their own host threads and HIP streams; the timed region covers
-`steps` pairs per pipeline): the new Frame360 is built end to end on the GPU (undistort, cloud + 2x2 median
-downsample, bilateral filter, normals, plane segmentation + refinement, PbMap descriptors and
-grouping, spherical stitch, 5-level pyramid with gradients), then RegisterRGBD360::RegisterPbMap
-(25 planes, PLANAR_3DoF) and RegisterPhotoICP::alignFrames360(PHOTO_DEPTH) initialised with the
-rotOffset-conjugated PbMap pose (OdometryKeyFrame360.cpp:205-254), with the reference schedule on
-levels 4..1 and exactly 20 Gauss-Newton iterations at level 0 (timing mode).
-Workload "dense" (configs[2] alone): stitch + pyramid of both frames + alignFrames360.
-Raw sensor images are resident in HBM before the timed region.  Multi-GPU: each rank registers its
-own contiguous shard of the sequence (weak scaling, no data-path collective) and the 4x4 poses are
-gathered with one RCCL all_gather over xGMI.
+Workload "sequence" (default; BASELINE.json configs[3], whose per-pair work is configs[1] + configs[2]):
+OdometryRGBD360 over the synthetic 256-frame sequence (procedural room, seed 360, 8 x 480x640 sensors).
+One step registers each of the 255 consecutive pairs exactly once (rgbd360_amd/odometry.py):
+  * the pairs are split contiguously over the ranks (one process per GPU) and, within a rank, over P
+    pipelines (host thread + HIP stream each, running free);
+  * per pair the new frame's raw 8-sensor images are uploaded from page-locked host memory (inside the
+    timed region, BASELINE.md §3 "from input upload"), the Frame360 is built on the GPU (undistort, cloud
+    + 2x2 median downsample, bilateral filter, normals, plane segmentation + refinement, PbMap
+    descriptors and grouping, spherical stitch, 5-level pyramid with gradients), then
+    RegisterRGBD360::RegisterPbMap(25 planes, PLANAR_3DoF) and RegisterPhotoICP::alignFrames360(PHOTO_DEPTH)
+    initialised with the rotOffset-conjugated PbMap pose (OdometryKeyFrame360.cpp:205-254): the reference
+    schedule on levels 4..1 and exactly 20 Gauss-Newton iterations at level 0 (timing mode);
+  * the per-pair records {pose, information, status, SSO, error} of every rank are gathered with one RCCL
+    all_gather over xGMI and rank 0 composes the trajectory (OdometryRGBD360.cpp:257) — inside the timed
+    region.
+Strong scaling: the sequence is the same at every N.  Workload "dense" (configs[2]; configs[4] with
+--rows 960 --cols 1280 --iters0 50): stitch + pyramid of every frame and alignFrames360 per pair, no planes.
 
 Prints ONE JSON line on rank 0.
 """
 import argparse
+import ctypes
+import hashlib
 import json
 import os
 import sys
 import time
-from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
@@ -34,42 +38,110 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 # Hardware queues per process (HIP's default is 4): the per-frame plane kernels are latency-bound
 # (one workgroup or wave per sensor), so throughput comes from many pipelines' kernels running at
-# once; 16 queues let 16+ streams reach the hardware side by side.  Must precede HIP initialisation.
+# once; 16 queues let 16 streams reach the hardware side by side.  Must precede HIP initialisation.
 os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 
 METRIC = "registered Frame360 pairs/sec @ 8×640×480; ICP-reduce HBM GB/s vs roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
-SEQ_LEN = 256
+SEED = 360 << 16
+ICP_SOURCES = ["rgbd360_amd/csrc/kernels/icp_kernels.hip", "rgbd360_amd/csrc/kernels/icp_common.inc",
+               "rgbd360_amd/csrc/kernels/icp_gn.inc", "rgbd360_amd/csrc/kernels/icp_la.inc",
+               "rgbd360_amd/csrc/libm_f32.h", "rgbd360_amd/csrc/r360_internal.h"]
 
 
-def shard_windows(rank, world, pipelines, window, seq_len=SEQ_LEN):
-    """Frame indices each pipeline of this rank walks: the rank owns a contiguous shard of the sequence
-    (pairs are independent); pipeline p takes a window of `window` consecutive frames in it."""
-    shard = seq_len // world
-    first = rank * shard
-    span = max(1, shard - window)
-    return [list(range(first + (p * window) % span, first + (p * window) % span + window)) for p in range(pipelines)]
+def icp_source_hash():
+    """Hash of the ICP pass's sources: a profile's PMC traffic is reported only for the kernel it measured."""
+    h = hashlib.sha256()
+    for p in ICP_SOURCES:
+        with open(os.path.join(ROOT, p), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
 
 
-def gather_poses(dist, poses, device):
-    """One all_gather of every rank's poses (RCCL over xGMI with backend nccl; gloo on CPU in the tests)."""
-    import torch
-    t = torch.from_numpy(np.ascontiguousarray(poses, np.float32).reshape(-1, 16)).to(device)
-    out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
-    dist.all_gather(out, t)
-    return torch.cat(out).cpu().numpy()
+def gather_records(allgather, rec, pad_to):
+    """Every rank's pair records (K, n, REC), padded to the largest shard and all-gathered in one call (RCCL
+    over xGMI through rgbd360_amd.Comm on the GPU; gloo in the CPU tests).  Returns the records of the whole
+    sequence in rank order and the shard sizes."""
+    k, n, w = rec.shape
+    buf = np.zeros((k, pad_to, w), np.float32)
+    buf[:, :n] = rec
+    buf[:, :, w - 1] = n                # the record's last slot is unused: it carries the shard size
+    allr = allgather(buf)               # (world, K, pad, REC)
+    sizes = [int(x[0, 0, w - 1]) for x in allr]
+    return np.concatenate([x[:, :m] for x, m in zip(allr, sizes)], axis=1), sizes
 
 
-def max_over_ranks(dist, value, device):
-    import torch
-    e = torch.tensor([value], device=device, dtype=torch.float64)
-    dist.all_reduce(e, op=dist.ReduceOp.MAX)
-    return float(e.item())
+class RankGroup:
+    """One process per GPU: torch.distributed's gloo group (host only, never touches the GPU) for the
+    rendezvous and barriers, and an RCCL communicator of the library (rgbd360_amd.Comm) for the device
+    collectives over xGMI."""
+
+    def __init__(self, device, rehearsal=False):
+        import torch.distributed as dist
+        import rgbd360_amd as R
+        dist.init_process_group("gloo")
+        self.dist = dist
+        self.world, self.rank = dist.get_world_size(), dist.get_rank()
+        self.comm = None
+        if not rehearsal:
+            uid = [R.Comm.unique_id() if self.rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            self.comm = R.Comm(device, self.world, self.rank, uid[0])
+
+    def barrier(self, ctxs=()):
+        for c in ctxs:
+            c.sync()
+        self.dist.barrier()
+
+    def allgather(self, a):
+        if self.comm is not None:
+            return self.comm.allgather(a)
+        import torch     # rehearsal of N ranks on one GPU (R360_BENCH_REHEARSAL=1): host gloo gather
+        t = torch.from_numpy(np.ascontiguousarray(a))
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t)
+        return np.stack([o.numpy() for o in out])
+
+    def max(self, v):
+        if self.comm is not None:
+            return self.comm.allreduce_max(v)
+        import torch
+        t = torch.tensor([v], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        if self.comm is not None:
+            self.comm.close()
+        self.dist.destroy_process_group()
 
 
-def cpu_baseline(R, cal, seed, first, workload, iters0, budget_s=15.0):
-    """The CPU oracle (C++ restatement, OpenMP over the 8 sensors / rows) on a bounded sample of the
-    same workload: consecutive pairs of the same synthetic sequence."""
+def host_cpu_info():
+    """Host cores usable by this process (affinity and cgroup quota) and the CPU model string."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except Exception:
+        pass
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    return {"affinity": aff, "cgroup_quota": quota, "usable": min(aff, quota) if quota else aff, "model": model}
+
+
+def cpu_baseline(cal, frames_of, first, last, workload, iters0, budget_s=10.0):
+    """The CPU oracle (C++ restatement, OpenMP where the reference parallelises: the 8 sensors, the ICP
+    rows) on a bounded sample of the same workload: consecutive pairs of the same synthetic sequence,
+    each = PbMap build of the new frame + RegisterPbMap + stitch + alignFrames360.  Timed at 8 threads
+    (the reference's num_threads(8), Frame360.h:620) and at every usable host core."""
     from oracle import oracle360 as O
     rt, rti, K = cal.extrinsics()
     Km = K.reshape(3, 3).T
@@ -81,181 +153,135 @@ def cpu_baseline(R, cal, seed, first, workload, iters0, budget_s=15.0):
     Ro[1, 2], Ro[2, 1] = np.float32(np.sin(a)), -np.float32(np.sin(a))
     Ri = Ro.T.copy()
 
-    def frame(i):
-        b, d = cal.synth_frame(seed, R.synth_path_pose(seed, i))
-        return b, d
-
-    def build(b, d):
+    def build(i):
+        b, d = frames_of(i)
         sb, sd = O.stitch(b, d, rti, Km)
-        pm = O.PbMap(d.astype(np.float32) * np.float32(0.001), b, rt8) if workload == "full" else None
+        pm = O.PbMap(d.astype(np.float32) * np.float32(0.001), b, rt8) if workload == "sequence" else None
         return sb, sd, pm
 
-    raw = [frame(first + j) for j in range(6)]
-    prev = build(*raw[0])
-    n, t0 = 0, time.perf_counter()
-    while True:
-        b, d = raw[(n + 1) % len(raw)]
-        cur = build(b, d)
-        if workload == "full":
-            r = O.register_pbmap(prev[2], cur[2], 25, O.PLANAR_3DoF)
-            init = Ro @ (r["pose"] if r["good"] else np.eye(4, dtype=np.float32)) @ Ri
-        else:
-            prev = build(*raw[n % len(raw)])     # dense: both frames per pair
-            init = None
-        O.align360(prev[0], prev[1], cur[0], cur[1], init, O.PHOTO_DEPTH, prm)
-        prev = cur
-        n += 1
-        if time.perf_counter() - t0 > budget_s:
-            break
-    dt = time.perf_counter() - t0
-    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    what = ("PbMap build of the new frame + RegisterPbMap + stitch + alignFrames360" if workload == "full"
-            else "stitch x2 + alignFrames360")
-    return {"value": n / dt, "unit": "pairs/s", "cores": cores, "kind": "port",
-            "sample": f"{n} consecutive synthetic 8x480x640 pairs ({what}, nPyr=5, {iters0} level-0 iterations), "
-                      f"oracle/liboracle360.so, {dt:.1f} s"}
+    gomp = None
+    try:
+        gomp = ctypes.CDLL("libgomp.so.1")
+    except OSError:
+        pass
+    info = host_cpu_info()
+    runs = []
+    for threads in sorted({min(8, info["usable"]), info["usable"]}):
+        if gomp is not None:
+            gomp.omp_set_num_threads(threads)
+        prev = build(first)
+        n, t0 = 0, time.perf_counter()
+        while True:
+            cur = build(first + n + 1)
+            if workload == "sequence":
+                r = O.register_pbmap(prev[2], cur[2], 25, O.PLANAR_3DoF)
+                init = Ro @ (r["pose"] if r["good"] else np.eye(4, dtype=np.float32)) @ Ri
+            else:
+                init = None
+            O.align360(prev[0], prev[1], cur[0], cur[1], init, O.PHOTO_DEPTH, prm)
+            prev = cur
+            n += 1
+            if time.perf_counter() - t0 > budget_s or first + n + 1 > last:
+                break
+        dt = time.perf_counter() - t0
+        runs.append({"threads": threads, "value": n / dt, "pairs": n, "seconds": round(dt, 2)})
+    what = ("PbMap build of the new frame + RegisterPbMap + stitch + alignFrames360" if workload == "sequence"
+            else "stitch + alignFrames360")
+    best = max(runs, key=lambda r: r["value"])
+    return {"value": best["value"], "unit": "pairs/s", "cores": best["threads"], "kind": "port",
+            "runs": runs, "cpu_model": info["model"], "host_cores": info,
+            "sample": f"consecutive synthetic pairs from frame {first} of the same sequence ({what}, nPyr=5, "
+                      f"{iters0} level-0 iterations), oracle/liboracle360.so (g++ -O3 -fopenmp), ~{budget_s:.0f} s per "
+                      "thread count; value = the faster run"}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--rows", type=int, default=480)
     ap.add_argument("--cols", type=int, default=640)
     ap.add_argument("--iters0", type=int, default=20)
-    ap.add_argument("--workload", choices=["full", "dense"], default="full")
-    ap.add_argument("--streams", type=int, default=16, help="pairs in flight per GPU (one pipeline = host thread + HIP stream each)")
-    ap.add_argument("--window", type=int, default=16, help="sequence frames resident per pipeline")
+    ap.add_argument("--frames", type=int, default=256, help="sequence length (frames)")
+    ap.add_argument("--workload", choices=["sequence", "dense"], default="sequence")
+    ap.add_argument("--streams", type=int, default=16, help="max pipelines per GPU (host thread + HIP stream each)")
+    ap.add_argument("--min-run", type=int, default=4, help="min pairs per pipeline run (each run rebuilds a halo frame)")
+    ap.add_argument("--emulate", type=str, default=None,
+                    help="RANK/WORLD: run that rank's shard alone (single-GPU rehearsal of an N-GPU shard)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-resident", action="store_true", help="skip the HBM-resident-input secondary run")
     ap.add_argument("--eval-probe", action="store_true", help="diagnostic: also time the level-0 pass in eval mode")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+    rehearsal = os.environ.get("R360_BENCH_REHEARSAL") == "1"   # N ranks sharing one GPU (gloo records)
+    if rehearsal:
+        local = 0
+    group = RankGroup(local, rehearsal) if world > 1 else None
+    shard_rank, shard_world = rank, world
+    if args.emulate:
+        shard_rank, shard_world = (int(x) for x in args.emulate.split("/"))
 
     import rgbd360_amd as R
+    from rgbd360_amd import odometry as OD
 
-    # P independent pipelines (one r360_ctx = one HIP stream + device GN state each) keep several pairs
-    # in flight: one pipeline's host-side PbMap work and latency-bound coarse ICP levels overlap the
-    # other pipelines' kernels
-    P = max(1, args.streams)
-    F = max(3, args.window)
-    ctxs = [R.Context(local) for _ in range(P)]
-    cals = []
-    for c in ctxs:
-        cal = R.Calib360(c, args.rows, args.cols)
-        cal.loadExtrinsicCalibration(R.EXTRINSICS_DIR)
-        cals.append(cal)
-    cal = cals[0]
-    seed = 360 << 16
-    # this rank's shard of the 256-frame sequence; pipeline p walks its own contiguous window of it
-    windows = shard_windows(rank, world, P, F)
-    first = windows[0][0]
-    flags = R.BUILD_UNDISTORT | R.BUILD_SPHERE | R.BUILD_PYRAMID
-    if args.workload == "full":
-        flags |= R.BUILD_PLANES
-    frames = []
-    raw = {}
-    for p, c in enumerate(cals):
-        fl = []
-        for idx in windows[p]:
-            if idx not in raw:
-                raw[idx] = cal.synth_frame(seed, R.synth_path_pose(seed, idx))
-            b, d = raw[idx]
-            f = R.Frame360(c)
-            f.upload(b, d)          # raw 8-sensor images resident in HBM before timing
-            f.build(flags)          # allocates every device buffer outside the timed region
-            fl.append(f)
-        frames.append(fl)
+    p0, p1 = OD.shard_pairs(shard_rank, shard_world, args.frames)
+    P = OD.pipelines_for(p1 - p0, args.streams, args.min_run)
+    runs = OD.split_range(p0, p1, P)
+    P = len(runs)
+
+    # raw frames p0..p1 of this rank, rendered on the host, in page-locked memory (uploaded per pair
+    # inside the timed region)
+    t_gen = time.perf_counter()
+    rt8 = np.stack([np.loadtxt(os.path.join(R.EXTRINSICS_DIR, f"Rt_0{k + 1}.txt"), dtype=np.float32)
+                    for k in range(8)])
+    nf = p1 - p0 + 1
+    BGR = np.zeros((nf, 8, args.rows, args.cols, 3), np.uint8)
+    DEP = np.zeros((nf, 8, args.rows, args.cols), np.uint16)
+    for j in range(nf):
+        b, d = R.synth_frame_rt(args.rows, args.cols, rt8, SEED, R.synth_path_pose(SEED, p0 + j))
+        BGR[j], DEP[j] = b, d
+    gen_s = time.perf_counter() - t_gen
+    pinned = R.HostPinned(BGR, DEP)
+
+    def frames_of(i):
+        return BGR[i - p0], DEP[i - p0]
+
     params = R.IcpParams.default()
     params.n_pyr = 5
     params.std_dev_photo = np.float32(3.0 / 255)       # OdometryRGBD360.cpp:92-95
     params.fixed_iters_level0 = args.iters0
-    L = R.lib()
-    eye16 = np.eye(4, dtype=np.float32).reshape(16)
-    pout = np.zeros((P, 16), np.float32)
-    stats = [R.IcpStats() for _ in range(P)]
-
-    prof = os.environ.get("BENCH_PROFILE") is not None
-    tacc = np.zeros((P, 4))
-
-    def pair(p, k, out):
-        """Pipeline p registers its k-th pair (frames j, j+1 of its window) and writes the pose to out."""
-        ta = time.perf_counter()
-        j = k % (F - 1)
-        if args.workload == "dense" or j == 0:
-            frames[p][j].build(flags, sync=False)
-        frames[p][j + 1].build(flags, sync=False)
-        ref, trg = frames[p][j], frames[p][j + 1]
-        tb = time.perf_counter()
-        if args.workload == "full":   # PbMap stage on this host thread, then the dense stage is enqueued
-            rc = L.r360_register_async(ctxs[p].h, ref.h, trg.h, R._fptr(eye16), R.C.byref(params), 25,
-                                       R.PLANAR_3DoF)
-        else:
-            rc = L.r360_align360_async(ctxs[p].h, ref.h, trg.h, R._fptr(eye16), R.PHOTO_DEPTH, 0,
-                                       R.C.byref(params))
-        assert rc == 0, L.r360_last_error()
-        tc = time.perf_counter()
-        if args.workload == "full":
-            rc = L.r360_register_result(ctxs[p].h, R._fptr(out), None, R.C.byref(stats[p]))
-        else:
-            rc = L.r360_align360_result(ctxs[p].h, R._fptr(out), None, None, R.C.byref(stats[p]))
-        assert rc >= 0, L.r360_last_error()
-        if prof:
-            tacc[p] += (tb - ta, tc - tb, time.perf_counter() - tc, 1)
-
-    # Each pipeline runs free on its own host thread (ctypes drops the GIL inside the library), so one
-    # pipeline's host PbMap stage and its wait for results never stall the others' GPU work.
-    pool = ThreadPoolExecutor(max_workers=P)
-
-    def run(k0, n, poses):
-        def worker(p):
-            for i in range(n):
-                pair(p, k0 + i, poses[i, p])
-        for f in [pool.submit(worker, p) for p in range(P)]:
-            f.result()
-
-    run(0, args.warmup, np.zeros((max(args.warmup, 1), P, 16), np.float32))
-    for c in ctxs:
-        c.sync()
+    runner = OD.SequenceRunner(local, args.rows, args.cols, P, params, planes=args.workload == "sequence",
+                               dense_only=args.workload == "dense")
+    ctxs = runner.ctxs
 
     def barrier():
-        if dist is not None:
-            import torch
-            torch.cuda.synchronize()
-            dist.barrier()
+        if group is not None:
+            group.barrier(ctxs)
 
-    poses = np.zeros((args.steps, P, 16), np.float32)
+    # warmup: every buffer (frames, queues, records) is allocated here, outside the timed region
+    runner.run(p0, p1, frames_of, np.zeros((max(args.warmup, 1), p1 - p0, OD.REC), np.float32),
+               repeats=max(args.warmup, 1), runs=runs)
+
+    rec = np.zeros((args.steps, p1 - p0, OD.REC), np.float32)
     barrier()
     for c in ctxs:
         c.timing(True)
         c.timing_reset()
         c.kernel_time_reset()
     t0 = time.perf_counter()
-    run(args.warmup, args.steps, poses)
-    for c in ctxs:
-        c.sync()
-    if dist is not None:  # RCCL pose gather over xGMI (SURVEY.md §8(e))
-        import torch
-        gather_poses(dist, poses, "cuda")
-        torch.cuda.synchronize()
+    runner.run(p0, p1, frames_of, rec, repeats=args.steps, runs=runs)
+    if group is not None:   # RCCL gather of the pair records over xGMI
+        allrec, sizes = gather_records(group.allgather, rec, -(-(args.frames - 1) // shard_world))
+    else:
+        allrec, sizes = rec, [p1 - p0]
+    traj = OD.compose(allrec[-1]) if rank == 0 else None   # OdometryRGBD360.cpp:257
     elapsed = time.perf_counter() - t0
-    if prof:
-        n = max(tacc[:, 3].sum(), 1)
-        print(f"per pair (ms): build-enqueue {1e3 * tacc[:, 0].sum() / n:.2f}  pbmap-stage {1e3 * tacc[:, 1].sum() / n:.2f}"
-              f"  dense-wait {1e3 * tacc[:, 2].sum() / n:.2f}", file=sys.stderr)
     barrier()
-    l0_ms, l0_n = 0.0, 0        # stream events around each level-0 pass
-    k0_us, k0_n = 0.0, 0        # in-kernel execution spans of the same passes
-    stage = {}
+    l0_ms, l0_n, k0_us, k0_n, stage = 0.0, 0, 0.0, 0, {}
     for c in ctxs:
         c.timing(False)
         ms, n = c.timing_read("k_icp_pass_L0")
@@ -264,43 +290,67 @@ def main():
         us, n = c.kernel_time(0)
         k0_us += us
         k0_n += n
-        for name in ("k_cloud", "k_bilateral", "k_distmap", "k_normals", "k_ccl", "k_plane_fit", "k_refine",
-                     "k_model_stats", "k_icp_pass", "k_icp_pass_L0"):
+        for name in ("k_undistort", "k_stitch", "k_pyramid", "k_cloud", "k_bilateral", "k_distmap", "k_normals",
+                     "k_ccl", "k_plane_fit", "k_refine", "k_model_stats", "k_icp_pass", "k_icp_pass_L0"):
             ms, n = c.timing_read(name)
             stage[name] = stage.get(name, 0.0) + ms
-    if dist is not None:
-        elapsed = max_over_ranks(dist, elapsed, "cuda")
+    if group is not None:
+        elapsed = group.max(elapsed)
+    pairs_job = args.steps * sum(sizes)
+    value = pairs_job / elapsed
 
-    total_pairs = args.steps * world * P
-    value = total_pairs / elapsed
+    # secondary: the same steps with the raw images already resident in HBM (device-to-device copies
+    # into the frames instead of PCIe uploads)
+    resident = None
+    if not args.no_resident:
+        dB, dD = R.DeviceArray(local, BGR), R.DeviceArray(local, DEP)
+
+        def dev_of(i):
+            return dB.ptr(i - p0), dD.ptr(i - p0)
+        rec2 = np.zeros((args.steps, p1 - p0, OD.REC), np.float32)
+        for c in ctxs:
+            c.timing(True)       # same per-launch event instrumentation as the headline run
+        barrier()
+        t1 = time.perf_counter()
+        runner.run(p0, p1, dev_of, rec2, repeats=args.steps, runs=runs, device_inputs=True)
+        e2 = time.perf_counter() - t1
+        for c in ctxs:
+            c.timing(False)
+            c.timing_reset()
+        if group is not None:
+            e2 = group.max(e2)
+        resident = pairs_job / e2
+        dB.close()
+        dD.close()
+
     W0 = args.rows * 8
     H0 = int(W0 * 0.5 * 60.0 / 180)               # Frame360.h:391-392 (640 x 3840 at VGA)
     N0 = H0 * W0
-    sso = float(stats[0].sso)
+    sso = float(np.mean(rec[:, :, OD.R_SSO]))
     V = sso * N0
-    alg_bytes = 8.0 * N0 + 24.0 * V            # B = 8 N + 24 V per pass
+    alg_bytes = 8.0 * N0 + 24.0 * V               # B = 8 N + 24 V per pass
     # The pass's duration is its in-kernel execution span (earliest workgroup start to the end of the
     # last workgroup, s_memrealtime), which is what rocprofv3's kernel trace reports; stream events
     # around a launch also count the time it waits behind the other pipelines' kernels.
     avg_ms = k0_us / max(k0_n, 1) * 1e-3
     event_ms = l0_ms / max(l0_n, 1)
     achieved = alg_bytes / (avg_ms * 1e-3) / 1e9 if k0_n else None
-    # the same pass with the GPU to itself: pipeline 0 registers a few more pairs alone
+    # the same pass with the GPU to itself: pipeline 0 registers its run once more, alone
     for c in ctxs:
         c.kernel_time_reset()
-    iso = np.zeros((3, P, 16), np.float32)
-    for i in range(3):
-        pair(0, args.warmup + args.steps + i, iso[i, 0])
-    ctxs[0].sync()
+    iso_rec = np.zeros((1, p1 - p0, OD.REC), np.float32)
+    runner.run(p0, p1, frames_of, iso_rec, repeats=1, runs=runs[:1])
     us, n = ctxs[0].kernel_time(0)
     iso_ms = us / max(n, 1) * 1e-3
     iso_ach = alg_bytes / (iso_ms * 1e-3) / 1e9 if n else None
     probe = None
     if args.eval_probe:   # opt-in diagnostic: the level-0 pass in eval mode (no GN step) at identity, alone
-        j = (args.warmup + args.steps + 2) % (F - 1)
+        fa, fb = runner.frames[0]
         reg = R.RegisterPhotoICP(ctxs[0])
-        reg.setNumPyr(5); reg.setGrayVariance(3.0 / 255)
-        reg.setTargetFrame(frames[0][j]); reg.setSourceFrame(frames[0][j + 1])
+        reg.setNumPyr(5)
+        reg.setGrayVariance(3.0 / 255)
+        reg.setTargetFrame(fa)
+        reg.setSourceFrame(fb)
         for _ in range(3):
             reg.eval(0, np.eye(4, dtype=np.float32), R.PHOTO_DEPTH)
         ctxs[0].kernel_time_reset()
@@ -311,53 +361,70 @@ def main():
         probe = {"avg_launch_ms": pu / max(pn, 1) * 1e-3, "launches": pn,
                  "note": "eval mode at identity pose, pipeline 0's last pair, in-kernel span"}
     # HBM bytes per level-0 launch from the rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes of this same
-    # command (tools/profile.sh + tools/profile_summary.py, committed under profiles/)
-    traffic = None
+    # command (tools/profile.sh + tools/profile_summary.py, committed under profiles/); reported only when
+    # the profile measured the current ICP sources
+    traffic, traffic_src = None, None
     tf = os.path.join(ROOT, "profiles", "latest", "l0_pass.json")
-    if os.path.exists(tf) and (args.rows, args.cols, args.workload) == (480, 640, "full"):
-        traffic = json.load(open(tf)).get("hbm_bytes_per_launch")   # profiled on the default workload only
-    pairs_timed = args.steps * P
-    if args.workload == "full":
-        workload = ("config2+3 (run as config4's sequence): per pair, the new synthetic "
-                    f"8x{args.cols}x{args.rows} Frame360 is "
-                    "built on the GPU (undistort, cloud + median downsample, bilateral, normals, plane "
-                    "segmentation + refinement, PbMap descriptors/grouping, stitch, 5-level pyramid), then "
-                    "RegisterPbMap(25 planes, PLANAR_3DoF) + alignFrames360(PHOTO_DEPTH) initialised with the "
-                    f"rotOffset-conjugated PbMap pose: levels 4..1 reference schedule + {args.iters0} GN "
-                    "iterations at level 0")
+    if os.path.exists(tf) and (args.rows, args.cols, args.workload) == (480, 640, "sequence"):
+        prof = json.load(open(tf))
+        if prof.get("icp_source_hash") == icp_source_hash():
+            traffic, traffic_src = prof.get("hbm_bytes_per_launch"), prof.get("tag")
+    steps_pairs = p1 - p0
+    if args.workload == "sequence":
+        workload = ("config4 (per pair configs 1+2's work): OdometryRGBD360 over the synthetic "
+                    f"{args.frames}-frame sequence, 8x{args.cols}x{args.rows}; each step registers every "
+                    "consecutive pair once: upload of the new frame's raw images, Frame360 build on the GPU "
+                    "(undistort, cloud + median downsample, bilateral, normals, plane segmentation + "
+                    "refinement, PbMap descriptors/grouping, stitch, 5-level pyramid), RegisterPbMap(25 planes, "
+                    "PLANAR_3DoF) + alignFrames360(PHOTO_DEPTH) from the rotOffset-conjugated PbMap pose "
+                    f"(levels 4..1 reference schedule + {args.iters0} GN iterations at level 0), pose gather + "
+                    "trajectory composition on rank 0")
     else:
         workload = (("config5" if args.rows == 960 else "config3") + f": synthetic 8x{args.cols}x{args.rows} "
-                    "Frame360 pair -> stitch + 5-level pyramid x2 -> "
+                    f"{args.frames}-frame sequence; per pair: upload, stitch + 5-level pyramid, "
                     f"alignFrames360(PHOTO_DEPTH) levels 4..1 reference schedule + {args.iters0} GN iterations "
                     "at level 0")
     out = {
         "metric": METRIC, "value": value, "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {
             "workload": workload, "sensors": f"8x{args.cols}x{args.rows}", "sphere": f"{H0}x{W0}",
-            "n_pyr": 5, "parallelism": f"pair-per-GPU dp{world}", "pairs_in_flight_per_gpu": P,
-            "pairs_per_step_per_gpu": P,
+            "n_pyr": 5, "parallelism": f"pair-shard dp{world}", "pairs_per_step": pairs_job // args.steps,
+            "pairs_per_step_this_rank": steps_pairs, "pipelines_per_gpu": P,
+            **({"emulated_shard": f"{shard_rank}/{shard_world}"} if args.emulate else {}),
         },
+        "value_hbm_resident_inputs": resident,
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
+            "traffic_profile": traffic_src,
             "kernel": "k_icp_pass<PHOTO_DEPTH> (level 0)", "avg_launch_ms": avg_ms, "launches": k0_n,
             "timing": "in-kernel execution span (s_memrealtime) over the timed region, all pipelines running",
             "event_avg_launch_ms": event_ms, "bytes_per_launch": alg_bytes, "visible_frac": sso,
             "isolated": {"avg_launch_ms": iso_ms, "launches": n, "achieved": iso_ach,
                          "frac": (iso_ach / HBM_PEAK_GBS) if iso_ach else None,
-                         "note": "same pass, pipeline 0 alone on the GPU (3 pairs after the timed region)"},
+                         "note": "same pass, pipeline 0 alone on the GPU (its run once more after the timed region)"},
             **({"eval_probe": probe} if probe else {}),
         },
-        "stage_ms_per_pair": {k: v / max(pairs_timed, 1) for k, v in stage.items()},
+        "stage_ms_per_pair": {k: v / max(args.steps * steps_pairs, 1) for k, v in stage.items()},
+        "frame_generation_s": round(gen_s, 1),
     }
+    if rank == 0 and traj is not None:
+        gt = np.stack([R.synth_path_pose(SEED, k).astype(np.float64) for k in range(args.frames)])
+        if allrec.shape[1] == args.frames - 1:
+            out["trajectory"] = OD.trajectory_error(traj, gt)
+            st = allrec[-1, :, OD.R_STATUS]
+            out["trajectory"].update({"pairs": int(allrec.shape[1]), "pbmap_failed": int((st == 1).sum()),
+                                      "illposed": int((st == 2).sum())})
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(R, cal, seed, first, args.workload, args.iters0)
+        out["cpu_baseline"] = cpu_baseline(runner.cals[0], frames_of, p0, p1, args.workload, args.iters0)
+    pinned.close()
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+    runner.close()
+    if group is not None:
+        group.close()
 
 
 if __name__ == "__main__":

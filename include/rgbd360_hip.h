@@ -69,6 +69,13 @@ int  r360_frame_create(r360_ctx* ctx, const r360_calib* calib, r360_frame** out)
 void r360_frame_destroy(r360_frame* f);
 /* Host images -> HBM (8 sensors contiguous).  Replaces loadFrame's decode step. */
 int  r360_frame_upload(r360_frame* f, const uint8_t* bgr8, const uint16_t* depth8);
+/* Same copy, enqueued on the ctx stream without waiting (OdometryRGBD360's per-frame input upload in
+ * the pipelined sequence driver).  The host buffers must stay valid until the stream has consumed
+ * them; page-locked buffers (r360_host_register) make the copy asynchronous to the host. */
+int  r360_frame_upload_async(r360_frame* f, const uint8_t* bgr8, const uint16_t* depth8);
+/* Page-lock / release host memory for asynchronous uploads (hipHostRegister). */
+int  r360_host_register(void* p, size_t bytes);
+int  r360_host_unregister(void* p);
 /* Device-resident images (already in HBM on the ctx's device); copied device-to-device. */
 int  r360_frame_upload_device(r360_frame* f, const void* d_bgr8, const void* d_depth8);
 /* Frame360::loadFrame(path) (Frame360.h:231-266): Boost binary archive of 8 x {RGB, depth} and
@@ -285,7 +292,8 @@ int r360_pbmap_match_tables(r360_ctx* ctx, r360_frame* ref, r360_frame* trg, siz
  * call computes: the result of a batched job is identical to r360_register_pbmap / r360_align360 on
  * the same frames.  Frames may belong to any ctx of the same device; each lane's stream waits for
  * the frames' build work before reading them.  The caller must not modify or destroy a frame while a
- * batch call that names it runs.  A batch is driven by one host thread at a time. */
+ * batch call that names it runs.  Calls on one batch are serialised: a call made while another thread's
+ * call runs waits for it. */
 typedef struct r360_batch r360_batch;
 int  r360_batch_create(int device, int lanes, r360_batch** out);
 void r360_batch_destroy(r360_batch* b);
@@ -345,6 +353,26 @@ typedef struct {
 int r360_frame_get_cloud(r360_frame* f, float* xyz4, uint8_t* rgb4, float* nrm4, float* dist);
 int r360_frame_get_labels(r360_frame* f, int* lab, int* labf);
 int r360_frame_get_regions(r360_frame* f, int sensor, r360_region* out, int cap, int* n);
+
+/* ---------------------------------------------------------------- multi-GPU sequence driver (§8(e))
+ * Pairs of a sequence shard one contiguous run per GPU (one process per GPU); the per-pair records
+ * {pose, information, status, ...} are all-gathered to every rank over RCCL (xGMI) and rank 0 composes the
+ * trajectory (Registration/OdometryRGBD360.cpp:257).  Rank 0 creates the id; the caller distributes it.
+ * Host buffers in and out; each call returns when its result is on the host. */
+typedef struct r360_comm r360_comm;
+int  r360_comm_unique_id(uint8_t id[128]);
+int  r360_comm_init(int device, int nranks, int rank, const uint8_t id[128], r360_comm** out);
+void r360_comm_destroy(r360_comm* c);
+/* recv[r * bytes .. (r + 1) * bytes) = rank r's send (ncclAllGather). */
+int  r360_comm_allgather(r360_comm* c, const void* send, void* recv, size_t bytes);
+/* v[i] = max over the ranks of v[i] (ncclAllReduce / ncclMax, f64). */
+int  r360_comm_allreduce_max(r360_comm* c, double* v, int n);
+
+/* Plain device buffers (inputs kept resident in HBM, r360_frame_upload_device).  kind: 0 host->device,
+ * 1 device->host, 2 device->device; synchronous. */
+int  r360_dev_alloc(int device, size_t bytes, void** out);
+int  r360_dev_free(void* p);
+int  r360_dev_copy(void* dst, const void* src, size_t bytes, int kind);
 
 /* ---------------------------------------------------------------- synthetic scenes
  * Procedural indoor room rendered by the 8 rig cameras.  Deterministic in

@@ -134,6 +134,9 @@ _SIGS = [
     ("r360_frame_destroy", None, [_P]),
     ("r360_frame_upload", C.c_int, [_P, _P, _P]),
     ("r360_frame_upload_device", C.c_int, [_P, _P, _P]),
+    ("r360_frame_upload_async", C.c_int, [_P, _P, _P]),
+    ("r360_host_register", C.c_int, [_P, C.c_size_t]),
+    ("r360_host_unregister", C.c_int, [_P]),
     ("r360_frame_load_bin", C.c_int, [_P, C.c_char_p]),
     ("r360_frame_save_bin", C.c_int, [_P, C.c_char_p]),
     ("r360_frame_set_timestamp", C.c_int, [_P, C.c_uint64]),
@@ -194,6 +197,14 @@ _SIGS = [
     ("r360_frame_get_cloud", C.c_int, [_P, _FP, _P, _FP, _FP]),
     ("r360_frame_get_labels", C.c_int, [_P, _IP, _IP]),
     ("r360_frame_get_regions", C.c_int, [_P, C.c_int, C.POINTER(Region), C.c_int, _IP]),
+    ("r360_comm_unique_id", C.c_int, [_P]),
+    ("r360_comm_init", C.c_int, [C.c_int, C.c_int, C.c_int, _P, C.POINTER(_P)]),
+    ("r360_comm_destroy", None, [_P]),
+    ("r360_comm_allgather", C.c_int, [_P, _P, _P, C.c_size_t]),
+    ("r360_comm_allreduce_max", C.c_int, [_P, _DP, C.c_int]),
+    ("r360_dev_alloc", C.c_int, [C.c_int, C.c_size_t, C.POINTER(_P)]),
+    ("r360_dev_free", C.c_int, [_P]),
+    ("r360_dev_copy", C.c_int, [_P, _P, C.c_size_t, C.c_int]),
     ("r360_synth_frame", C.c_int, [_P, C.c_uint32, _FP, _P, _P]),
     ("r360_synth_frame_rt", C.c_int, [C.c_int, C.c_int, _FP, C.c_uint32, _FP, _P, _P]),
     ("r360_synth_path_pose", C.c_int, [C.c_uint32, C.c_int, _FP]),
@@ -442,6 +453,14 @@ class Frame360:
         depth8 = np.ascontiguousarray(depth8, np.uint16)
         assert bgr8.shape == (8, self.rows, self.cols, 3) and depth8.shape == (8, self.rows, self.cols)
         _check(lib().r360_frame_upload(self.h, _vptr(bgr8), _vptr(depth8)), "upload")
+
+    def upload_async(self, bgr8: np.ndarray, depth8: np.ndarray):
+        """Enqueue the upload on the frame's stream; the arrays must stay alive (and should be page-locked,
+        see HostPinned) until the stream has consumed them."""
+        assert bgr8.dtype == np.uint8 and depth8.dtype == np.uint16
+        assert bgr8.flags.c_contiguous and depth8.flags.c_contiguous
+        assert bgr8.shape == (8, self.rows, self.cols, 3) and depth8.shape == (8, self.rows, self.cols)
+        _check(lib().r360_frame_upload_async(self.h, _vptr(bgr8), _vptr(depth8)), "upload_async")
 
     def upload_device(self, d_bgr: int, d_depth: int):
         _check(lib().r360_frame_upload_device(self.h, C.c_void_p(d_bgr), C.c_void_p(d_depth)), "upload_device")
@@ -846,6 +865,89 @@ def libm_eval(x, y, z, on_device: bool = False):
     _check(lib().r360_libm_eval(_fptr(x), _fptr(y), _fptr(z), x.size, _fptr(a), _fptr(t), int(on_device)),
            "libm_eval")
     return a, t
+
+
+class Comm:
+    """RCCL communicator of one rank (r360_comm): the sequence driver's record all_gather over xGMI.
+    Rank 0 calls unique_id() and hands the bytes to the other ranks (e.g. over a gloo process group)."""
+
+    @staticmethod
+    def unique_id() -> bytes:
+        b = (C.c_uint8 * 128)()
+        _check(lib().r360_comm_unique_id(b), "comm_unique_id")
+        return bytes(b)
+
+    def __init__(self, device: int, nranks: int, rank: int, uid: bytes):
+        assert len(uid) == 128
+        self.nranks = nranks
+        self.h = C.c_void_p()
+        b = (C.c_uint8 * 128).from_buffer_copy(uid)
+        _check(lib().r360_comm_init(device, nranks, rank, b, C.byref(self.h)), "comm_init")
+
+    def allgather(self, a: np.ndarray) -> np.ndarray:
+        """(nranks,) + a.shape: every rank's array, in rank order."""
+        a = np.ascontiguousarray(a)
+        out = np.zeros((self.nranks,) + a.shape, a.dtype)
+        _check(lib().r360_comm_allgather(self.h, _vptr(a), _vptr(out), a.nbytes), "comm_allgather")
+        return out
+
+    def allreduce_max(self, v: float) -> float:
+        x = np.array([v], np.float64)
+        _check(lib().r360_comm_allreduce_max(self.h, x.ctypes.data_as(_DP), 1), "comm_allreduce_max")
+        return float(x[0])
+
+    def close(self):
+        if self.h:
+            lib().r360_comm_destroy(self.h)
+            self.h = None
+
+
+class DeviceArray:
+    """A host array's copy resident in HBM (r360_dev_alloc); ptr(i) = device address of element i along
+    the first axis."""
+
+    def __init__(self, device: int, a: np.ndarray):
+        a = np.ascontiguousarray(a)
+        self.nbytes, self.row = a.nbytes, a[0].nbytes if a.ndim else a.nbytes
+        self.p = C.c_void_p()
+        _check(lib().r360_dev_alloc(device, self.nbytes, C.byref(self.p)), "dev_alloc")
+        _check(lib().r360_dev_copy(self.p, _vptr(a), self.nbytes, 0), "dev_copy")
+
+    def ptr(self, i: int = 0) -> int:
+        return self.p.value + i * self.row
+
+    def close(self):
+        if self.p:
+            lib().r360_dev_free(self.p)
+            self.p = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class HostPinned:
+    """Page-locks numpy arrays for asynchronous uploads (hipHostRegister); released by close()."""
+
+    def __init__(self, *arrays):
+        self.arrays = []
+        for a in arrays:
+            assert a.flags.c_contiguous
+            _check(lib().r360_host_register(_vptr(a), a.nbytes), "host_register")
+            self.arrays.append(a)
+
+    def close(self):
+        for a in self.arrays:
+            lib().r360_host_unregister(_vptr(a))
+        self.arrays = []
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def synth_frame_rt(rows: int, cols: int, rt8: np.ndarray, seed: int, rig_pose: np.ndarray):

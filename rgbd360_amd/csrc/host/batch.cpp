@@ -40,6 +40,7 @@ struct r360_batch {
     int busy = 0;
     bool stop = false;
     std::function<void(int)> task;
+    std::recursive_mutex call;   // one call at a time (r360_track_frame re-enters r360_batch_register): a second caller waits instead of overwriting task / lane state
 
     void worker(int l) {
         hipSetDevice(device);
@@ -188,6 +189,7 @@ extern "C" int r360_batch_register(r360_batch* b, const r360_pair_job* jobs, int
                                    r360_pair_result* out) {
     CHECK_ARG(b && (n == 0 || (jobs && out)), "null arg");
     CHECK_ARG(n >= 0, "negative job count");
+    std::lock_guard<std::recursive_mutex> serial(b->call);
     CHECK_ARG(mode >= 0 && mode <= 3, "registrationType must be 0..3");
     bool any_dense = false;
     std::vector<r360_frame*> frames;
@@ -224,6 +226,7 @@ extern "C" int r360_track_frame(r360_batch* b, r360_frame* const* kfs, int n_kf,
                                 r360_pair_result* result, r360_pair_result* cand) {
     CHECK_ARG(b && frame && chosen && (n_kf == 0 || kfs), "null arg");
     CHECK_ARG(n_kf >= 0 && num_check >= 0 && no_assoc_threshold >= 0, "negative count");
+    std::lock_guard<std::recursive_mutex> serial(b->call);
     // while(compareLocalIdx >= 0 && compareLocalIdx >= newLocalFrameID - numCheckRegistration &&
     //       noAssoc < noAssoc_threshold): every failed candidate increments noAssoc, so at most
     // min(n_kf, num_check, no_assoc_threshold) candidates are tried, newest first

@@ -412,6 +412,29 @@ extern "C" int r360_frame_upload(r360_frame* f, const uint8_t* bgr8, const uint1
     return 0;
 }
 
+// Enqueued on the ctx stream; the host buffers must stay valid until the stream reaches the copies
+// (page-locked buffers, r360_host_register, make the copies truly asynchronous).
+extern "C" int r360_frame_upload_async(r360_frame* f, const uint8_t* bgr8, const uint16_t* depth8) {
+    CHECK_ARG(f && bgr8 && depth8, "null arg");
+    const size_t ns = (size_t)8 * f->rows * f->cols;
+    R360_HIP(hipMemcpyAsync(f->d_bgr, bgr8, ns * 3, hipMemcpyHostToDevice, f->ctx->stream));
+    R360_HIP(hipMemcpyAsync(f->d_depth, depth8, ns * 2, hipMemcpyHostToDevice, f->ctx->stream));
+    f->built = 0;
+    return 0;
+}
+
+extern "C" int r360_host_register(void* p, size_t bytes) {
+    CHECK_ARG(p && bytes, "null arg");
+    R360_HIP(hipHostRegister(p, bytes, hipHostRegisterDefault));
+    return 0;
+}
+
+extern "C" int r360_host_unregister(void* p) {
+    CHECK_ARG(p, "null arg");
+    R360_HIP(hipHostUnregister(p));
+    return 0;
+}
+
 extern "C" int r360_frame_upload_device(r360_frame* f, const void* d_bgr8, const void* d_depth8) {
     CHECK_ARG(f && d_bgr8 && d_depth8, "null arg");
     const size_t ns = (size_t)8 * f->rows * f->cols;
@@ -574,6 +597,7 @@ extern "C" int r360_align360_async(r360_ctx* ctx, r360_frame* trg, r360_frame* s
     CHECK_ARG(init, "null init pose");
     CHECK_ARG(method >= 0 && method <= 2, "invalid method");
     CHECK_ARG(occlusion >= 0 && occlusion <= 2, "occlusion must be 0, 1 or 2");
+    if (ensure_defer(ctx, src->lv[0].rows * src->lv[0].cols)) return -1;
     IcpState* h = ctx->h_state;
     memset(h, 0, sizeof(IcpState));
     memcpy(h->pose, init, sizeof(float) * 16);
@@ -627,6 +651,7 @@ static int icp_eval_sums(r360_ctx* ctx, r360_frame* trg, r360_frame* src, int le
     CHECK_ARG(level >= 0 && level < src->n_levels, "level out of range");
     CHECK_ARG(method >= 0 && method <= 2, "invalid method");
     CHECK_ARG(occ >= 0 && occ <= 2, "occlusion must be 0, 1 or 2");
+    if (ensure_defer(ctx, src->lv[level].rows * src->lv[level].cols)) return -1;
     IcpState* h = ctx->h_state;
     memset(h, 0, sizeof(IcpState));
     memcpy(h->cand, pose, sizeof(float) * 16);

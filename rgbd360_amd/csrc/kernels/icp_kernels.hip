@@ -1162,6 +1162,20 @@ static void launch_pass(r360_ctx* ctx, int nb, const LevelBufs& Ls, const LevelB
                        eval_only, ctx->d_ktime, ctx->occ_flags, ctx->d_gticket, ctx->d_defer);
 }
 
+int ensure_defer(r360_ctx* ctx, long n_pixels) {
+    // per wave ceil(npx / stride) * 64 entries over nb * NW waves: <= npx + nb * TPB for any nb
+    const long need = n_pixels + (long)ctx->partials_cap * TPB;
+    if (ctx->defer_cap >= need) return 0;
+    R360_HIP(hipSetDevice(ctx->device));
+    R360_HIP(hipStreamSynchronize(ctx->stream));
+    if (ctx->d_defer) R360_HIP(hipFree(ctx->d_defer));
+    ctx->d_defer = nullptr;
+    ctx->defer_cap = 0;
+    R360_HIP(hipMalloc(&ctx->d_defer, sizeof(int) * need));
+    ctx->defer_cap = need;
+    return 0;
+}
+
 int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src, int level, int method,
                      const IcpConst& C, int first, int eval_only) {
     const LevelBufs& Ls = src->lv[level];
@@ -1194,9 +1208,8 @@ int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src
         const long stride = (long)nb * TPB;
         const long need = (long)nb * (TPB / 64) * (((npx + stride - 1) / stride) * 64);
         if (ctx->defer_cap < need) {
-            (void)hipFree(ctx->d_defer);
-            R360_HIP(hipMalloc(&ctx->d_defer, sizeof(int) * need));
-            ctx->defer_cap = need;
+            r360_set_error("deferred-pixel queue not sized for %d pixels (ensure_defer)", npx);
+            return -1;
         }
     }
     if (C.occ) {   // occlusion flags of this pass's pose (same stream, before the fused pass)

@@ -317,6 +317,9 @@ int launch_robot(r360_ctx* ctx, const RobotJob* d_jobs, const RobotGrid& grid, i
 int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src, int level,
                      int method, const IcpConst& C, int first, int eval_only);
 int icp_blocks_for(int n_pixels);
+// sizes ctx->d_defer for passes over up to n_pixels pixels (synchronises the ctx stream when it grows,
+// so it never frees a queue an enqueued pass still uses); call before enqueuing a level sequence
+int ensure_defer(r360_ctx* ctx, long n_pixels);
 int launch_cloud_normals(r360_frame* f);
 int launch_segmentation(r360_frame* f);
 int plane_bufs_alloc(r360_frame* f);

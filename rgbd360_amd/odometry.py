@@ -1,0 +1,186 @@
+"""OdometryRGBD360 over a Frame360 sequence, sharded by pair (BASELINE config 4).
+
+The reference's loop (Registration/OdometryRGBD360.cpp:141-257) walks a sequence, registers each new
+Frame360 against the previous one (RegisterPbMap, then alignFrames360) and composes the trajectory with
+``currentPose = currentPose * rigidTransf`` (:257).  Registering pair (i, i+1) needs only frames i and
+i+1, so the 255 pairs of a 256-frame sequence are split into contiguous shards, one per rank (one
+process per GPU), and each rank's shard into contiguous runs, one per pipeline (one ``r360_ctx`` =
+host thread + HIP stream).  A pipeline builds the first frame of its run (the halo frame, also built by
+the previous run) and then, per pair, uploads and builds the new frame and registers it with the
+``Register()`` alias (PbMap -> rotOffset conjugation -> alignFrames360, OdometryKeyFrame360.cpp:205-254).
+Every pair is registered exactly once; rank 0 gathers the per-pair records and forms the prefix product.
+
+Deviation, by construction of the sharding: the reference's ``dist < 0.4`` keyframe skip (:230-238)
+makes pair i depend on earlier results (the reference frame only advances after a far-enough frame), so
+a sharded run registers consecutive pairs.  ``apps/OdometryRGBD360`` keeps the skip for sequential runs.
+"""
+from __future__ import annotations
+
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+from . import (BUILD_PLANES, BUILD_PYRAMID, BUILD_SPHERE, BUILD_UNDISTORT, PHOTO_DEPTH, PLANAR_3DoF, Calib360,
+               Context, Frame360, IcpParams, IcpStats, EXTRINSICS_DIR, C, _fptr, lib)
+
+SEQ_FRAMES = 256
+# one pair record: pose (16, column-major, rig frame of the pair's first frame), the PbMap information
+# matrix (36), status (0: PbMap stage good, 1: PbMap failed and the dense stage started from the guess,
+# 2: alignFrames360 ill-posed), SSO, the accepted level-0 error
+REC = 56
+
+# rotOffset of OdometryRGBD360.cpp:136-139 (the sphere's frame vs the rig's), float angle, double PI
+_A = float(np.float32(157.5)) * 3.14159265359 / 180
+ROT_OFFSET = np.eye(4)
+ROT_OFFSET[1, 1] = ROT_OFFSET[2, 2] = np.float32(np.cos(_A))
+ROT_OFFSET[1, 2], ROT_OFFSET[2, 1] = np.float32(np.sin(_A)), -np.float32(np.sin(_A))
+ROT_OFFSET_INV = ROT_OFFSET.T.copy()
+R_POSE, R_INFO, R_STATUS, R_SSO, R_ERR = 0, 16, 52, 53, 54
+
+
+def split_range(a: int, b: int, parts: int) -> list[tuple[int, int]]:
+    """[a, b) in `parts` contiguous pieces whose sizes differ by at most one (empty pieces dropped)."""
+    n = b - a
+    parts = max(1, min(parts, n)) if n > 0 else 1
+    base, extra = divmod(n, parts)
+    out, s = [], a
+    for k in range(parts):
+        e = s + base + (1 if k < extra else 0)
+        if e > s:
+            out.append((s, e))
+        s = e
+    return out
+
+
+def shard_pairs(rank: int, world: int, n_frames: int = SEQ_FRAMES) -> tuple[int, int]:
+    """Pairs [p0, p1) of rank `rank`: pair i registers frames (i, i+1); the n_frames-1 pairs are split
+    contiguously over the ranks.  The rank needs frames p0..p1."""
+    n = n_frames - 1
+    base, extra = divmod(n, world)
+    p0 = rank * base + min(rank, extra)
+    return p0, p0 + base + (1 if rank < extra else 0)
+
+
+def pipelines_for(n_pairs: int, streams: int, min_run: int) -> int:
+    """Pipelines for a shard: at most `streams`, each with a run of at least `min_run` pairs (every run
+    rebuilds its halo frame, so short runs cost extra frame builds)."""
+    return max(1, min(streams, n_pairs // max(1, min_run)))
+
+
+def compose(records: np.ndarray) -> np.ndarray:
+    """Trajectory of the sequence: T[0] = I, T[k+1] = T[k] * pose_k (OdometryRGBD360.cpp:257), in float64."""
+    n = records.shape[0]
+    T = np.zeros((n + 1, 4, 4))
+    T[0] = np.eye(4)
+    for k in range(n):
+        T[k + 1] = T[k] @ records[k, R_POSE:R_POSE + 16].reshape(4, 4).T.astype(np.float64)
+    return T
+
+
+def trajectory_error(T: np.ndarray, gt: np.ndarray) -> dict:
+    """Per-frame error of a composed trajectory against ground-truth rig poses gt[k] (composed from gt[0])."""
+    g0 = np.linalg.inv(gt[0])
+    rot, trans = [], []
+    for k in range(T.shape[0]):
+        G = g0 @ gt[k]
+        D = np.linalg.inv(G) @ T[k]
+        rot.append(float(np.degrees(np.arccos(np.clip((np.trace(D[:3, :3]) - 1) / 2, -1, 1)))))
+        trans.append(float(np.linalg.norm(T[k][:3, 3] - G[:3, 3])))
+    path = float(sum(np.linalg.norm(gt[k + 1][:3, 3] - gt[k][:3, 3]) for k in range(len(gt) - 1)))
+    return {"frames": int(T.shape[0]), "max_rot_err_deg": max(rot), "max_trans_err_m": max(trans),
+            "final_rot_err_deg": rot[-1], "final_trans_err_m": trans[-1], "path_length_m": path}
+
+
+class SequenceRunner:
+    """P pipelines on one GPU, each an r360_ctx (HIP stream + device GN state) driven by its own host thread
+    (ctypes drops the GIL inside the library), each with two Frame360 buffers used in turn."""
+
+    def __init__(self, device: int, rows: int, cols: int, pipelines: int, params: IcpParams,
+                 planes: bool = True, max_match_planes: int = 25, mode: int = PLANAR_3DoF, dense_only: bool = False):
+        self.P = pipelines
+        self.dense_only = dense_only
+        self.params = params
+        self.max_match_planes, self.mode = max_match_planes, mode
+        self.flags = BUILD_UNDISTORT | BUILD_SPHERE | BUILD_PYRAMID | (BUILD_PLANES if planes else 0)
+        self.ctxs = [Context(device) for _ in range(pipelines)]
+        self.cals, self.frames = [], []
+        for c in self.ctxs:
+            cal = Calib360(c, rows, cols)
+            cal.loadExtrinsicCalibration(EXTRINSICS_DIR)
+            self.cals.append(cal)
+            self.frames.append([Frame360(cal), Frame360(cal)])
+        self.stats = [IcpStats() for _ in range(pipelines)]
+        self.pool = ThreadPoolExecutor(max_workers=pipelines)
+        self.eye = np.eye(4, dtype=np.float32).reshape(16)
+
+    def _pipeline(self, p: int, run: tuple[int, int], frames_of, out: np.ndarray, p0: int, device_inputs: bool):
+        """Pipeline p registers pairs run[0]..run[1]-1; out[i - p0] = the record of pair i.  Frame i's raw
+        images come from frames_of(i): host arrays (uploaded over PCIe) or, with device_inputs, device
+        pointers of images already resident in HBM (copied device to device)."""
+        L = lib()
+        ctx = self.ctxs[p]
+        fa, fb = self.frames[p]
+        a, b = run
+
+        def load(f, i):
+            if device_inputs:
+                f.upload_device(*frames_of(i))
+            else:
+                f.upload_async(*frames_of(i))
+        load(fa, a)
+        fa.build(self.flags, sync=False)
+        for i in range(a, b):
+            load(fb, i + 1)
+            fb.build(self.flags, sync=False)
+            rec = out[i - p0]
+            pose, info = np.zeros(16, np.float32), np.zeros(36, np.float32)
+            if self.dense_only:   # alignFrames360 from identity (configs 3 / 5), pose conjugated back to the rig
+                rc = L.r360_align360_async(ctx.h, fa.h, fb.h, _fptr(self.eye), PHOTO_DEPTH, 0, C.byref(self.params))
+                if rc != 0:
+                    raise RuntimeError(f"r360_align360_async: {L.r360_last_error()}")
+                dense = np.zeros(16, np.float32)
+                rc = L.r360_align360_result(ctx.h, _fptr(dense), None, None, C.byref(self.stats[p]))
+                if rc < 0:
+                    raise RuntimeError(f"r360_align360_result: {L.r360_last_error()}")
+                pose = (ROT_OFFSET_INV @ dense.reshape(4, 4).T.astype(np.float64) @ ROT_OFFSET).T.reshape(16)
+                rc = 0
+            else:
+                rc = L.r360_register_async(ctx.h, fa.h, fb.h, _fptr(self.eye), C.byref(self.params),
+                                           self.max_match_planes, self.mode)
+                if rc != 0:
+                    raise RuntimeError(f"r360_register_async: {L.r360_last_error()}")
+                rc = L.r360_register_result(ctx.h, _fptr(pose), _fptr(info), C.byref(self.stats[p]))
+                if rc < 0:
+                    raise RuntimeError(f"r360_register_result: {L.r360_last_error()}")
+            rec[R_POSE:R_POSE + 16] = pose
+            rec[R_INFO:R_INFO + 36] = info
+            rec[R_STATUS] = 2 if self.stats[p].illposed else rc
+            rec[R_SSO] = self.stats[p].sso
+            rec[R_ERR] = self.stats[p].error
+            fa, fb = fb, fa
+
+    def run(self, p0: int, p1: int, frames_of, out: np.ndarray, repeats: int = 1, runs=None,
+            device_inputs: bool = False):
+        """Registers pairs [p0, p1) `repeats` times (out: (repeats, p1 - p0, REC)); frames_of(i) returns
+        frame i's (bgr, depth) host arrays, which must outlive the call.  runs: the pipelines' pair runs
+        (default: [p0, p1) split over the pipelines)."""
+        runs = runs or split_range(p0, p1, self.P)
+        assert len(runs) <= self.P
+
+        def worker(p):
+            for r in range(repeats):
+                self._pipeline(p, runs[p], frames_of, out[r], p0, device_inputs)
+        for f in [self.pool.submit(worker, p) for p in range(len(runs))]:
+            f.result()
+        for c in self.ctxs:
+            c.sync()
+
+    def close(self):
+        self.pool.shutdown()
+        for fr in self.frames:
+            for f in fr:
+                f.close()
+        for c in self.cals:
+            c.close()
+        for c in self.ctxs:
+            c.close()

@@ -1,0 +1,117 @@
+"""BASELINE config 4 on one GPU: OdometryRGBD360 over the synthetic 256-frame sequence, sharded by pair
+(rgbd360_amd/odometry.py, the bench's default workload).
+
+* the first 16 pairs of the pipelined run equal the oracle chain (PbMap -> RegisterPbMap -> rotOffset
+  conjugation -> alignFrames360 with the bench's 20 level-0 iterations) to the north-star tolerance;
+* the records of all 255 pairs do not depend on how the pairs are sharded (ranks x pipelines): the N = 2 and
+  N = 8 rank shards, each run alone, reproduce the single-GPU run bit for bit;
+* the composed trajectory follows the synthetic ground truth (synth_path_pose)."""
+import numpy as np
+import pytest
+
+import rgbd360_amd as R
+from rgbd360_amd import odometry as OD
+
+pytestmark = pytest.mark.gpu
+
+SEED = 360 << 16
+
+
+@pytest.fixture(scope="module")
+def seq():
+    rt8 = np.stack([np.loadtxt(f"{R.EXTRINSICS_DIR}/Rt_0{k + 1}.txt", dtype=np.float32) for k in range(8)])
+    bgr = np.zeros((256, 8, 480, 640, 3), np.uint8)
+    dep = np.zeros((256, 8, 480, 640), np.uint16)
+    for i in range(256):
+        bgr[i], dep[i] = R.synth_frame_rt(480, 640, rt8, SEED, R.synth_path_pose(SEED, i))
+    pin = R.HostPinned(bgr, dep)
+    p = R.IcpParams.default()
+    p.n_pyr = 5
+    p.std_dev_photo = np.float32(3.0 / 255)
+    p.fixed_iters_level0 = 20
+    runner = OD.SequenceRunner(0, 480, 640, 16, p)
+    rec = np.zeros((1, 255, OD.REC), np.float32)
+    runner.run(0, 255, lambda i: (bgr[i], dep[i]), rec)
+    yield dict(bgr=bgr, dep=dep, runner=runner, rec=rec[0], params=p, rt8=rt8)
+    runner.close()
+    pin.close()
+
+
+def test_first_pairs_match_oracle_chain(seq):
+    from oracle import oracle360 as O
+    bgr, dep, rec = seq["bgr"], seq["dep"], seq["rec"]
+    cal = seq["runner"].cals[0]
+    rt, rti, K = cal.extrinsics()
+    Km = K.reshape(3, 3).T
+    rt8 = np.stack([rt[16 * k:16 * k + 16].reshape(4, 4).T for k in range(8)])
+    prm = O.IcpParams.default(n_pyr=5, std_dev_photo=np.float32(3.0 / 255), fixed_iters_level0=20)
+    Ro = OD.ROT_OFFSET.astype(np.float32)
+    Ri = OD.ROT_OFFSET_INV.astype(np.float32)
+
+    def build(i):
+        sb, sd = O.stitch(bgr[i], dep[i], rti, Km)
+        return sb, sd, O.PbMap(dep[i].astype(np.float32) * np.float32(0.001), bgr[i], rt8)
+
+    prev = build(0)
+    for i in range(16):
+        cur = build(i + 1)
+        r = O.register_pbmap(prev[2], cur[2], 25, O.PLANAR_3DoF)
+        assert r["good"] == (rec[i, OD.R_STATUS] == 0), i
+        init = Ro @ (r["pose"] if r["good"] else np.eye(4, dtype=np.float32)) @ Ri
+        _, dense, _, _, _ = O.align360(prev[0], prev[1], cur[0], cur[1], init, O.PHOTO_DEPTH, prm)
+        ref = Ri.astype(np.float64) @ dense.astype(np.float64) @ Ro.astype(np.float64)
+        pose = rec[i, :16].reshape(4, 4).T
+        assert O.rot_angle(pose[:3, :3], ref[:3, :3]) <= 1e-4, i
+        assert np.linalg.norm(pose[:3, 3] - ref[:3, 3]) <= 1e-3, i
+        prev = cur
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_sharded_runs_reproduce_the_single_gpu_records(seq, world):
+    bgr, dep = seq["bgr"], seq["dep"]
+    runner = seq["runner"]
+    parts = []
+    for r in range(world):
+        p0, p1 = OD.shard_pairs(r, world)
+        runs = OD.split_range(p0, p1, OD.pipelines_for(p1 - p0, 16, 4))
+        out = np.zeros((1, p1 - p0, OD.REC), np.float32)
+        runner.run(p0, p1, lambda i: (bgr[i], dep[i]), out, runs=runs)
+        parts.append(out[0])
+    assert np.array_equal(np.concatenate(parts), seq["rec"])
+
+
+def test_device_resident_inputs_give_the_same_records(seq):
+    bgr, dep = seq["bgr"], seq["dep"]
+    dB, dD = R.DeviceArray(0, bgr[:33]), R.DeviceArray(0, dep[:33])
+    out = np.zeros((1, 32, OD.REC), np.float32)
+    seq["runner"].run(0, 32, lambda i: (dB.ptr(i), dD.ptr(i)), out, device_inputs=True)
+    dB.close()
+    dD.close()
+    assert np.array_equal(out[0], seq["rec"][:32])
+
+
+def test_rccl_comm_single_rank():
+    """The record gather's RCCL path (r360_comm) with one rank: all_gather returns the rank's own buffer,
+    the max is the value (multi-rank RCCL needs one GPU per rank: exercised by the driver's N > 1 runs)."""
+    c = R.Comm(0, 1, 0, R.Comm.unique_id())
+    a = np.arange(3 * 5 * 56, dtype=np.float32).reshape(3, 5, 56)
+    assert np.array_equal(c.allgather(a), a[None])
+    assert c.allreduce_max(2.5) == 2.5
+    c.close()
+
+
+def test_trajectory_follows_ground_truth(seq):
+    rec = seq["rec"]
+    assert (rec[:, OD.R_STATUS] == 0).all()                   # every PbMap stage succeeded, none ill-posed
+    gt = np.stack([R.synth_path_pose(SEED, k).astype(np.float64) for k in range(256)])
+    # every pair: the relative pose of the synthetic path
+    for i in range(255):
+        rel = np.linalg.inv(gt[i]) @ gt[i + 1]
+        pose = rec[i, :16].reshape(4, 4).T.astype(np.float64)
+        D = np.linalg.inv(rel) @ pose
+        assert np.degrees(np.arccos(np.clip((np.trace(D[:3, :3]) - 1) / 2, -1, 1))) < 0.2, i
+        assert np.linalg.norm(pose[:3, 3] - rel[:3, 3]) < 0.02, i
+    e = OD.trajectory_error(OD.compose(rec), gt)
+    print(e)
+    # drift of the composed odometry over the closed 256-frame loop
+    assert e["max_rot_err_deg"] < 2.0 and e["max_trans_err_m"] < 0.02 * e["path_length_m"], e
