@@ -182,7 +182,7 @@ __device__ __forceinline__ Proj project_fast(const Pose12& P, const Lut3& l, flo
     float Z = P.R[6] * l.x + P.R[7] * l.y + P.R[8] * l.z; Z = Z + P.t[2];
     const float d2 = X * X + Y * Y + Z * Z;
     const float dist_inv = __builtin_amdgcn_rsqf(d2);
-    const float phi_trg = r360m::asinf_fast(X * dist_inv);
+    const float phi_trg = r360m::asinf_fast_view(X * dist_inv);
     const float theta_trg = r360m::atan2f_fast1(Y, Z) + 3.14159265358979f;
     // u = rr + 0.5, v = cc + 0.5 (half_nRows + 0.5 = nRows / 2 exactly)
     const float u = fmaf(-phi_trg, angle_res_inv, 0.5f * (float)nRows);
@@ -353,7 +353,10 @@ __device__ __forceinline__ void contribute_fast(Acc& A, WaveCnt& W, const Proj& 
     if (OCC == 0) {
         W.c28 += wave_count(o.vis);                                                        // numVisiblePixels
         W.c27 += (photo ? wave_count(p_ok) : 0) + (depth ? wave_count(d_ok) : 0);
-        A.err2 += (p_ok ? (double)ep : 0.0) + (d_ok ? (double)ed : 0.0);
+        // one f64 add per pixel: the pixel's two squared terms are summed in f32 first (2^-24 relative per
+        // pixel, far below the accept test's resolution; the summation order differs from the
+        // reference's OpenMP reduction anyway)
+        A.err2 += (double)((p_ok ? ep : 0.f) + (d_ok ? ed : 0.f));
     } else if (OCC == 1) {
         // errorPhotoICP_sphereOcc1 (:3232-3370): accepted points count, the last accepted one of a target
         // pixel owns its residual; H / g as calcHessGrad_sphere (its Z-buffer never occludes)
@@ -381,37 +384,36 @@ __device__ __forceinline__ void contribute_fast(Acc& A, WaveCnt& W, const Proj& 
     const float dist_inv = o.vis ? o.dist_inv : 0.5f;
     {
 #pragma clang fp contract(fast)
-        // Jacobian of the spherical warp (:2995-3026), expanded with T36 = [I | -skew(p')]
-        const float z_inv = __builtin_amdgcn_rcpf(Z);
-        const float z_inv2 = z_inv * z_inv;
-        const float D_atan = __builtin_amdgcn_rcpf(1 + Y * Y * z_inv2) * angle_res_inv;
-        const float P01 = D_atan * z_inv;
-        const float P02 = -Y * z_inv2 * D_atan;
-        const float x_dist_inv2 = X * (dist_inv * dist_inv);
-        const float q = 1 - X * x_dist_inv2;
-        const float D_asin = __builtin_amdgcn_rsqf(q) * angle_res_inv;
-        const float P10 = -D_asin * dist_inv * q;
-        const float kk = D_asin * x_dist_inv2 * dist_inv;
-        const float P11 = kk * Y, P12 = kk * Z;
-        const float Jw0[6] = {0.f, P01, P02, P02 * Y - P01 * Z, -P02 * X, P01 * X};
-        const float Jw1[6] = {P10, P11, P12, P12 * Y - P11 * Z, P10 * Z - P12 * X, P11 * X - P10 * Y};
+        // Jacobian of the spherical warp (:2995-3026): row = [gx gy] J_proj [I | -skew(p')] = [u, p' x u]
+        // with u = J_proj^T [gx gy]^T (the 3-vector of the translation part; u^T (-skew(p')) = (p' x u)^T).
+        // J_proj in closed form, with r2 = Y^2 + Z^2, d2 = |p'|^2 and a = 1 / angle_res:
+        //   theta row (0, a Z / r2, -a Y / r2);  phi row (-a r2 / (sqrt(r2) d2), a X Y / (sqrt(r2) d2),
+        //   a X Z / (sqrt(r2) d2)) — the reference's D_atan / D_asin products (:3000-3016) simplified.
+        const float r2 = Y * Y + Z * Z;
+        const float s = __builtin_amdgcn_rcpf(r2) * angle_res_inv;                        // theta row scale
+        const float t = __builtin_amdgcn_rsqf(r2) * (dist_inv * dist_inv) * angle_res_inv; // phi row scale
+        auto row = [&](float gx, float gy, float& u0, float& u1, float& u2) {
+            const float A = gx * s, B = gy * t, BX = B * X;
+            u0 = -B * r2;
+            u1 = A * Z + BX * Y;
+            u2 = BX * Z - A * Y;
+        };
+        auto acc_row = [&](float u0, float u1, float u2, float r) {
+            const float J[6] = {u0, u1, u2, Y * u2 - Z * u1, Z * u0 - X * u2, X * u1 - Y * u0};
+            acc_fma(A, J, r);
+        };
         if (photo) {
-            const float wgx = wp * G.x, wgy = wp * G.y;
-            float J[6];
-#pragma unroll
-            for (int k = 0; k < 6; ++k) J[k] = wgx * Jw0[k] + wgy * Jw1[k];
-            acc_fma(A, J, rp);
+            float u0, u1, u2;
+            row(wp * G.x, wp * G.y, u0, u1, u2);
+            acc_row(u0, u1, u2, rp);
         }
         if (depth) {
-            // (dgrad * Jw - (p'/|p'|)^T T36): the rotational part of (p'/|p'|)^T T36 is p' x p' / |p'| = 0
-            const float wz = wd * G.z, ww = wd * G.w, wdi = wd * dist_inv;
-            float J[6];
-            J[0] = wz * Jw0[0] + ww * Jw1[0] - wdi * X;
-            J[1] = wz * Jw0[1] + ww * Jw1[1] - wdi * Y;
-            J[2] = wz * Jw0[2] + ww * Jw1[2] - wdi * Z;
-#pragma unroll
-            for (int k = 3; k < 6; ++k) J[k] = wz * Jw0[k] + ww * Jw1[k];
-            acc_fma(A, J, rd);
+            // (dgrad * J_w - (p'/|p'|)^T T36): the rotational part of (p'/|p'|)^T T36 is p' x p' / |p'| = 0,
+            // so the unit-vector term enters u only
+            float u0, u1, u2;
+            row(wd * G.z, wd * G.w, u0, u1, u2);
+            const float wdi = wd * dist_inv;
+            acc_row(u0 - wdi * X, u1 - wdi * Y, u2 - wdi * Z, rd);
         }
     }
 }

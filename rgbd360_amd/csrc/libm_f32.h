@@ -221,6 +221,19 @@ __device__ __forceinline__ float asinf_fast(float x) {
     return x > 0 ? r : -r;
 }
 
+// asin for the spherical projection's row decision only: the sphere spans |phi| <= 30 deg (H = W / 6,
+// Frame360.h:391-392), so |x| >= 0.53 (|phi| >= 32 deg) always projects outside the image, at every
+// pyramid level (>= 1.3 rows beyond the border).  There the result is a constant that projects outside
+// as well; below it the |x| < 0.5 polynomial of asinf (accurate to 1 ulp up to 0.53), with contraction.
+__device__ __forceinline__ float asinf_fast_view(float x) {
+#pragma clang fp contract(fast)
+    const float p0 = 1.666675248e-1f, p1 = 7.495297643e-2f, p2 = 4.547037598e-2f, p3 = 2.417951451e-2f,
+                p4 = 4.216630880e-2f;
+    const float t = x * x;
+    const float r = x + x * (t * (p0 + t * (p1 + t * (p2 + t * (p3 + t * p4)))));
+    return fabs_(x) < 0.53f ? r : __builtin_copysignf(1.0f, x);
+}
+
 // atan2 with a two-way argument reduction (|t| <= tan(pi/8) < 7/16, fdlibm's polynomial domain):
 // atan(a) = a poly for a <= tan(pi/8), pi/4 + atan((a-1)/(a+1)) above; octants by selects.
 __device__ __forceinline__ float atan2f_fast(float y, float x) {
@@ -265,6 +278,7 @@ __device__ __forceinline__ float div_rn(float a, float b) {
 // atan2 as atan2f_fast with a single reciprocal: the reduction t = (mn - mx) / (mn + mx) above
 // tan(pi/8) (= (a - 1) / (a + 1) for a = mn / mx) and t = mn / mx below share one division.
 __device__ __forceinline__ float atan2f_fast1(float y, float x) {
+#pragma clang fp contract(fast)
     const float ay = fabs_(y), ax = fabs_(x);
     const float mx = ay > ax ? ay : ax, mn = ay > ax ? ax : ay;
     const bool big = mn > 0.41421356f * mx;
