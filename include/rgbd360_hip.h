@@ -97,6 +97,9 @@ int  r360_frame_get_depth_m(r360_frame* f, float* depth8);
  * gradients with the alignFrames360 seam mask applied).  Any pointer may be NULL. */
 int  r360_frame_get_level(r360_frame* f, int level, int* rows, int* cols, float* gray, float* depth,
                           float* gx, float* gy, float* dgx, float* dgy);
+/* The level's compacted ICP source points (valid depth, raster order) as {x, y, z, gray} quadruples:
+ * LUT_xyz_sphere (RegisterPhotoICP.h:4553-4587) and the gray value.  *n = their count; copies min(n, cap). */
+int  r360_frame_get_points(r360_frame* f, int level, float* xyzg, int cap, int* n);
 /* Sensor k's pinhole pyramid level (R360_BUILD_SENSOR_PYRAMID; no seam mask). */
 int  r360_frame_get_sensor_level(r360_frame* f, int sensor, int level, int* rows, int* cols, float* gray,
                                  float* depth, float* gx, float* gy, float* dgx, float* dgy);

@@ -158,6 +158,7 @@ _SIGS = [
     ("r360_frame_get_sphere", C.c_int, [_P, _P, _P]),
     ("r360_frame_get_depth_m", C.c_int, [_P, _P]),
     ("r360_frame_get_level", C.c_int, [_P, C.c_int, _IP, _IP, _P, _P, _P, _P, _P, _P]),
+    ("r360_frame_get_points", C.c_int, [_P, C.c_int, _FP, C.c_int, _IP]),
     ("r360_frame_get_sensor_level", C.c_int, [_P, C.c_int, C.c_int, _IP, _IP, _P, _P, _P, _P, _P, _P]),
     ("r360_icp_default_params", None, [C.POINTER(IcpParams)]),
     ("r360_align360", C.c_int, [_P, _P, _P, _FP, C.c_int, C.c_int, C.POINTER(IcpParams), _FP, _FP, _FP,
@@ -543,6 +544,14 @@ class Frame360:
         _check(lib().r360_frame_get_level(self.h, level, C.byref(r), C.byref(c), *[_vptr(a) for a in arrs]),
                "get_level")
         return dict(zip(["gray", "depth", "gx", "gy", "dgx", "dgy"], arrs))
+
+    def points(self, level: int) -> np.ndarray:
+        """The level's compacted ICP source points: (n, 4) {x, y, z, gray} (valid depth, raster order)."""
+        n = C.c_int()
+        _check(lib().r360_frame_get_points(self.h, level, None, 0, C.byref(n)), "get_points")
+        out = np.zeros((max(n.value, 1), 4), np.float32)
+        _check(lib().r360_frame_get_points(self.h, level, _fptr(out), n.value, C.byref(n)), "get_points")
+        return out[:n.value]
 
     def sensor_level(self, sensor: int, level: int):
         """Sensor k's pinhole pyramid level (BUILD_SENSOR_PYRAMID)."""

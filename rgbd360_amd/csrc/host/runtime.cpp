@@ -384,8 +384,13 @@ extern "C" int r360_frame_create(r360_ctx* ctx, const r360_calib* calib, r360_fr
         f->lv[l].rows = R; f->lv[l].cols = C;
         R360_HIP(hipMalloc(&f->lv[l].p0, sizeof(float2) * (size_t)R * C));
         R360_HIP(hipMalloc(&f->lv[l].tg, sizeof(float4) * (size_t)R * C));
+        R360_HIP(hipMalloc(&f->lv[l].pts, sizeof(float4) * (size_t)R * C));
         R /= 2; C /= 2;
     }
+    f->src_blocks = (int)((nsph + R360_SRC_BLOCK - 1) / R360_SRC_BLOCK);
+    R360_HIP(hipMalloc(&f->d_npts, sizeof(int) * R360_MAX_PYR));
+    R360_HIP(hipMemset(f->d_npts, 0, sizeof(int) * R360_MAX_PYR));
+    R360_HIP(hipMalloc(&f->d_src_cnt, sizeof(int) * R360_MAX_PYR * (size_t)f->src_blocks));
     *out = f;
     return 0;
 }
@@ -395,7 +400,8 @@ extern "C" void r360_frame_destroy(r360_frame* f) {
     // hipFree synchronises the device; the frame never dereferences its ctx here so frames may
     // outlive their context at interpreter shutdown.
     hipFree(f->d_bgr); hipFree(f->d_depth); hipFree(f->d_depth_m); hipFree(f->d_sph_bgr); hipFree(f->d_sph_depth);
-    for (int l = 0; l < f->n_levels; ++l) { hipFree(f->lv[l].p0); hipFree(f->lv[l].tg); }
+    for (int l = 0; l < f->n_levels; ++l) { hipFree(f->lv[l].p0); hipFree(f->lv[l].tg); hipFree(f->lv[l].pts); }
+    hipFree(f->d_npts); hipFree(f->d_src_cnt);
     for (int l = 0; l < f->n_slevels; ++l) { hipFree(f->sp[l].p0); hipFree(f->sp[l].tg); }
     plane_bufs_free(f);
     delete f->sphere_cloud;
@@ -536,6 +542,21 @@ extern "C" int r360_frame_get_level(r360_frame* f, int level, int* rows, int* co
     CHECK_ARG(f->built & R360_BUILD_PYRAMID, "pyramid not built");
     const LevelBufs& L = f->lv[level];
     return copy_level(f, L.p0, L.tg, L.rows, L.cols, rows, cols, gray, depth, gx, gy, dgx, dgy);
+}
+
+extern "C" int r360_frame_get_points(r360_frame* f, int level, float* xyzg, int cap, int* n) {
+    CHECK_ARG(f && n, "null arg");
+    CHECK_ARG(level >= 0 && level < f->n_levels, "level out of range");
+    CHECK_ARG(f->built & R360_BUILD_PYRAMID, "pyramid not built");
+    int np = 0;
+    R360_HIP(hipMemcpyAsync(&np, f->d_npts + level, sizeof(int), hipMemcpyDeviceToHost, f->ctx->stream));
+    R360_HIP(hipStreamSynchronize(f->ctx->stream));
+    *n = np;
+    if (xyzg && cap > 0) {
+        const int m = np < cap ? np : cap;
+        R360_HIP(hipMemcpy(xyzg, f->lv[level].pts, sizeof(float4) * (size_t)m, hipMemcpyDeviceToHost));
+    }
+    return 0;
 }
 
 extern "C" int r360_frame_get_sensor_level(r360_frame* f, int sensor, int level, int* rows, int* cols, float* gray,

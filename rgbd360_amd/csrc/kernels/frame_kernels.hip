@@ -200,6 +200,91 @@ int launch_stitch(r360_frame* f) {
     return 0;
 }
 
+// ------------------------------------------------------------------ ICP source points
+// The source side of errorPhotoICP_sphere / calcHessGrad_sphere reads, per pixel with
+// minDepth < depth < maxDepth, the LUT_xyz_sphere point (RegisterPhotoICP.h:4553-4587, the same float
+// expressions) and the gray value; both are fixed for a source frame.  They are compacted here once per
+// frame, in raster order (a deterministic two-kernel scan), so the pass streams only valid pixels.
+// blockIdx.y = pyramid level; a block covers R360_SRC_BLOCK consecutive pixels, 4 per thread.
+struct SrcLevel { const float2* p0; float4* pts; const float* sinphi; const float* cosphi; const float* sinth;
+                  const float* costh; int rows, cols; };
+struct SrcLevels { SrcLevel l[R360_MAX_PYR]; };
+constexpr int SRC_TPB = R360_SRC_BLOCK / 4;
+
+__device__ __forceinline__ bool src_valid(float d, float min_d, float max_d) { return min_d < d && d < max_d; }
+
+__global__ void __launch_bounds__(SRC_TPB) k_src_count(SrcLevels L, float min_d, float max_d, int* __restrict__ cnt,
+                                                      int stride) {
+    const SrcLevel& S = L.l[blockIdx.y];
+    const long n = (long)S.rows * S.cols;
+    const long b0 = (long)blockIdx.x * R360_SRC_BLOCK;
+    if (b0 >= n) return;
+    int c = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const long i = b0 + k * SRC_TPB + threadIdx.x;
+        c += (i < n && src_valid(S.p0[i].y, min_d, max_d)) ? 1 : 0;
+    }
+    __shared__ int sh[SRC_TPB / 64];
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int t = 0;
+        for (int w = 0; w < SRC_TPB / 64; ++w) t += sh[w];
+        cnt[blockIdx.y * stride + blockIdx.x] = t;
+    }
+}
+
+__global__ void __launch_bounds__(SRC_TPB) k_src_compact(SrcLevels L, float min_d, float max_d, const int* __restrict__ cnt,
+                                                        int stride, int* __restrict__ npts) {
+    const SrcLevel& S = L.l[blockIdx.y];
+    const long n = (long)S.rows * S.cols;
+    const long b0 = (long)blockIdx.x * R360_SRC_BLOCK;
+    if (b0 >= n) return;
+    __shared__ int sh[SRC_TPB / 64 + 1];
+    // this block's output offset: the counts of the blocks before it
+    int base = 0;
+    for (int b = threadIdx.x; b < (int)blockIdx.x; b += SRC_TPB) base += cnt[blockIdx.y * stride + b];
+    for (int o = 32; o > 0; o >>= 1) base += __shfl_xor(base, o, 64);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = base;
+    __syncthreads();
+    base = 0;
+    for (int w = 0; w < SRC_TPB / 64; ++w) base += sh[w];
+    __syncthreads();
+    // raster order: pixel b0 + 4t + k is the k-th of thread t
+    const long i0 = b0 + 4L * threadIdx.x;
+    bool v[4];
+    int c = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        v[k] = i0 + k < n && src_valid(S.p0[i0 + k].y, min_d, max_d);
+        c += v[k] ? 1 : 0;
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int x = c;                                           // inclusive wave scan
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) sh[wid] = x;
+    __syncthreads();
+    int wbase = 0;
+    for (int w = 0; w < wid; ++w) wbase += sh[w];
+    int pos = base + wbase + x - c;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (!v[k]) continue;
+        const long i = i0 + k;
+        const int r = (int)(i / S.cols), cc = (int)(i - (long)r * S.cols);
+        const float2 a = S.p0[i];
+        const float d = a.y;
+        // LUT_xyz_sphere (:4580-4582): x = d sin(phi), y = -d cos(phi) sin(theta), z = -d cos(phi) cos(theta)
+        S.pts[pos++] = make_float4(d * S.sinphi[r], -d * S.cosphi[r] * S.sinth[cc], -d * S.cosphi[r] * S.costh[cc], a.x);
+    }
+    if (blockIdx.x == (unsigned)((n - 1) / R360_SRC_BLOCK) && threadIdx.x == SRC_TPB - 1) npts[blockIdx.y] = pos;
+}
+
 int launch_pyramid(r360_frame* f) {
     // RegisterPhotoICP constructor defaults minDepth 0.3 / maxDepth 6.0 (:202-203)
     const float min_d = 0.3f, max_d = 6.0f;
@@ -213,6 +298,15 @@ int launch_pyramid(r360_frame* f) {
         hipLaunchKernelGGL(k_gradient, dim3(grid_for(n)), dim3(TPB), 0, f->ctx->stream, f->lv[l].p0, f->lv[l].rows,
                            f->lv[l].cols, f->lv[l].tg, 1, 1);
     }
+    SrcLevels L{};
+    for (int l = 0; l < f->n_levels; ++l) {
+        const LevelTrig& T = f->calib->trig[l];
+        L.l[l] = SrcLevel{f->lv[l].p0, f->lv[l].pts, T.sinphi, T.cosphi, T.sinth, T.costh, f->lv[l].rows, f->lv[l].cols};
+    }
+    const dim3 g(f->src_blocks, f->n_levels);
+    hipLaunchKernelGGL(k_src_count, g, dim3(SRC_TPB), 0, f->ctx->stream, L, min_d, max_d, f->d_src_cnt, f->src_blocks);
+    hipLaunchKernelGGL(k_src_compact, g, dim3(SRC_TPB), 0, f->ctx->stream, L, min_d, max_d, f->d_src_cnt,
+                       f->src_blocks, f->d_npts);
     R360_HIP(hipGetLastError());
     return 0;
 }

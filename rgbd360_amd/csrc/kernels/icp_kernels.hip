@@ -432,7 +432,8 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const float2* _
                                                  IcpConst C, IcpState* S, double* __restrict__ partials, int first,
                                                  int eval_only, unsigned long long* __restrict__ kt,
                                                  const uint8_t* __restrict__ occf, unsigned* __restrict__ gcnt,
-                                                 int* __restrict__ dq) {
+                                                 int* __restrict__ dq, const float4* __restrict__ pts,
+                                                 const int* __restrict__ npts) {
     __shared__ float s_red[NW][32];
     __shared__ double s_err[NW], s_errd[NW];
     __shared__ double s_fin[RG][32];
@@ -656,6 +657,79 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const float2* _
                 acc(o, gt.g(o.t), gt.T(o.t), act ? flag(i) : 0);
             }
         }
+    } else if (PF == 4) {
+        // PF 3's wave stream over the level's COMPACTED source points (LevelBufs::pts, built once per frame):
+        // only pixels with minDepth < depth < maxDepth, as {LUT point, gray}, in raster order.  No row/column
+        // tables, no LUT arithmetic and no lanes spent on pixels without depth.  Deferred lanes queue their
+        // point index and are re-projected exactly after the stream.
+        const int nv = __builtin_amdgcn_readfirstlane(*npts);
+        const int lane = threadIdx.x & 63;
+        const int qcap = ((nv + stride - 1) / stride) * 64;
+        int* q = dq + ((long)blockIdx.x * NW + (threadIdx.x >> 6)) * qcap;
+        int qn = 0;
+        auto acc = [&](const Proj& o, const float4 G, const float2 T) {
+            contribute_fast<METHOD, 0>(A, W, o, G, T, 0, angle_res_inv, C);
+        };
+        const Gather gt{__builtin_amdgcn_make_buffer_rsrc(const_cast<float4*>(tg), 0, nRows * nCols * 16, 0x00020000),
+                        __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(trg), 0, nRows * nCols * 8, 0x00020000)};
+        const auto prs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float4*>(pts), 0, nv * 16, 0x00020000);
+        struct Src { float4 p; bool valid; };
+        auto ld = [&](int base) {        // out-of-range lanes read 0 (buffer bounds) and are not valid
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(prs, (base + lane) * 16, 0, 0);
+            return Src{make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]),
+                                   __uint_as_float(v[3])), base + lane < nv};
+        };
+        auto prj = [&](const Src& x) {
+            return project_fast(P, Lut3{x.p.x, x.p.y, x.p.z, x.valid}, x.p.w, nRows, nCols, angle_res_inv);
+        };
+        auto defer = [&](Proj& o, int base) {
+            const unsigned long long m = __ballot(o.fix);
+            if (m) {
+                const int pos = qn + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                                   __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+                if (o.fix) { q[pos] = base + lane; o.vis = false; o.t = 0; }
+                qn += __popcll(m);
+            }
+        };
+        const int b0 = __builtin_amdgcn_readfirstlane((blockIdx.x * TPB + (threadIdx.x & ~63)));
+        if (b0 < nv) {
+            const int n_it = (nv - 1 - b0) / stride + 1;
+            auto base = [&](int k) { return b0 + (k < n_it ? k : n_it - 1) * stride; };
+            Src sA = ld(base(0));
+            Src sB = ld(base(1));
+            Proj oA = prj(sA);
+            defer(oA, base(0));
+            float4 GA = gt.g(oA.t);
+            float2 TA = gt.T(oA.t);
+            for (int k = 0;; k += 2) {
+                sA = ld(base(k + 2));
+                Proj oB = prj(sB);
+                if (k + 1 < n_it) defer(oB, base(k + 1));   // a clamped tail chunk is never accumulated
+                const float4 GB = gt.g(oB.t);
+                const float2 TB = gt.T(oB.t);
+                acc(oA, GA, TA);
+                if (k + 1 >= n_it) break;
+                sB = ld(base(k + 3));
+                oA = prj(sA);
+                if (k + 2 < n_it) defer(oA, base(k + 2));
+                GA = gt.g(oA.t);
+                TA = gt.T(oA.t);
+                acc(oB, GB, TB);
+                if (k + 2 >= n_it) break;
+            }
+        }
+        if (qn > 0) {
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            for (int s0 = 0; s0 < qn; s0 += 64) {
+                const bool act = s0 + lane < qn;
+                const int i = act ? q[s0 + lane] : 0;
+                const float4 a = pts[i];
+                Proj o = project_exact(P, Lut3{a.x, a.y, a.z, true}, a.w, nRows, nCols, half_nRows, angle_res_inv);
+                o.vis = o.vis && act;
+                o.t = o.vis ? o.t : 0;
+                acc(o, gt.g(o.t), gt.T(o.t));
+            }
+        }
     } else {
         // small levels: one pixel per thread, so the latency chain per thread is a quarter as long
         const int npx = nRows * nCols;
@@ -677,7 +751,7 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const float2* _
 
     // ---- stage 1: wave butterfly (f32) -> LDS -> per-workgroup fp64 record
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    if (PF == 3 && lane == 0) { A.h[27] += (float)W.c27; A.h[28] += (float)W.c28; A.h[29] += (float)W.c29; }
+    if (PF >= 3 && lane == 0) { A.h[27] += (float)W.c27; A.h[28] += (float)W.c28; A.h[29] += (float)W.c29; }
 #ifdef R360_EXP_NOEPI   // experiment builds only
     if (A.h[0] == 1.2345f) S->dbg[7] = 1;
     return;
@@ -1155,13 +1229,15 @@ static int env_int(const char* name, int dflt) {
 
 template <int M, int PF>
 static void launch_pass(r360_ctx* ctx, int nb, const LevelBufs& Ls, const LevelBufs& Lt, const LevelTrig& T,
-                        const IcpConst& C, int first, int eval_only, bool top) {
-    auto kern = C.occ == 1 ? k_icp_pass<M, PF, 0, 1>
-              : C.occ == 2 ? k_icp_pass<M, PF, 0, 2>
+                        const IcpConst& C, int first, int eval_only, bool top, const int* npts) {
+    // PF 4 (compacted source points) has no occlusion form: the occlusion flags are per source pixel
+    constexpr int PFO = PF == 4 ? 3 : PF;
+    auto kern = C.occ == 1 ? k_icp_pass<M, PFO, 0, 1>
+              : C.occ == 2 ? k_icp_pass<M, PFO, 0, 2>
               : top        ? k_icp_pass<M, PF, 1, 0> : k_icp_pass<M, PF, 0, 0>;
     hipLaunchKernelGGL(kern, dim3(nb), dim3(TPB), 0, ctx->stream, Ls.p0, Lt.p0, Lt.tg, T.sinphi,
                        T.cosphi, T.sinth, T.costh, Ls.rows, Ls.cols, C, ctx->d_state, ctx->d_partials, first,
-                       eval_only, ctx->d_ktime, ctx->occ_flags, ctx->d_gticket, ctx->d_defer);
+                       eval_only, ctx->d_ktime, ctx->occ_flags, ctx->d_gticket, ctx->d_defer, Ls.pts, npts);
 }
 
 int ensure_defer(r360_ctx* ctx, long n_pixels) {
@@ -1188,7 +1264,7 @@ int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src
     static const int pf_env = env_int("R360_ICP_PF", -1);
     static const int cap_env = env_int("R360_ICP_CAP", -1);
     // one resident round: CUs x workgroups per CU of the launched form (grid-stride beyond it)
-    struct Occ { int cus = 0, per[4] = {0, 0, 0, 0}; };
+    struct Occ { int cus = 0, per[5] = {0, 0, 0, 0, 0}; };
     static const Occ occ = [] {   // thread-safe one-time query (contexts may be driven from several threads)
         Occ o;
         int dev = 0;
@@ -1198,15 +1274,18 @@ int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[1], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 1, 0, 0>, TPB, 0);
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[2], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 2, 0, 0>, TPB, 0);
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[3], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 3, 0, 0>, TPB, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[4], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 4, 0, 0>, TPB, 0);
         return o;
     }();
     const int npx = Ls.rows * Ls.cols;
-    const int pf = pf_env >= 0 ? pf_env : ((Ls.cols % 64 == 0) ? 3 : 0);
+    // PF 4 (compacted source points) for the plain pass; the occlusion variants index their flags by source
+    // pixel and keep the image stream (PF 3 where rows split into whole waves)
+    const int pf = pf_env >= 0 && !(pf_env == 4 && C.occ) ? pf_env : (C.occ ? ((Ls.cols % 64 == 0) ? 3 : 0) : 4);
     int cap = cap_env > 0 ? cap_env : occ.cus * (occ.per[pf] > 0 ? occ.per[pf] : 4);
     if (cap > ctx->partials_cap) cap = ctx->partials_cap;
     int nb = pf == 1 ? icp_blocks_for(npx) : (npx + TPB - 1) / TPB;
     if (nb > cap) nb = cap;
-    if (pf == 3) {   // deferred-pixel queues: one per wave, room for every pixel the wave streams
+    if (pf >= 3) {   // deferred-pixel queues: one per wave, room for every pixel the wave streams
         const long stride = (long)nb * TPB;
         const long need = (long)nb * (TPB / 64) * (((npx + stride - 1) / stride) * 64);
         if (ctx->defer_cap < need) {
@@ -1255,13 +1334,15 @@ int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src
         R360_HIP(hipGetLastError());
     }
     const char* name = level == 0 ? "k_icp_pass_L0" : "k_icp_pass";
+    const int* np = src->d_npts + level;
     const int slot = timing_begin(ctx, name);
 #define R360_LAUNCH(M)                                                              \
     do {                                                                            \
-        if (pf == 1) launch_pass<M, 1>(ctx, nb, Ls, Lt, T, C, first, eval_only, level == 0);   \
-        else if (pf == 2) launch_pass<M, 2>(ctx, nb, Ls, Lt, T, C, first, eval_only, level == 0); \
-        else if (pf == 3) launch_pass<M, 3>(ctx, nb, Ls, Lt, T, C, first, eval_only, level == 0); \
-        else launch_pass<M, 0>(ctx, nb, Ls, Lt, T, C, first, eval_only, level == 0);          \
+        if (pf == 1) launch_pass<M, 1>(ctx, nb, Ls, Lt, T, C, first, eval_only, level == 0, np);   \
+        else if (pf == 2) launch_pass<M, 2>(ctx, nb, Ls, Lt, T, C, first, eval_only, level == 0, np); \
+        else if (pf == 3) launch_pass<M, 3>(ctx, nb, Ls, Lt, T, C, first, eval_only, level == 0, np); \
+        else if (pf == 4) launch_pass<M, 4>(ctx, nb, Ls, Lt, T, C, first, eval_only, level == 0, np); \
+        else launch_pass<M, 0>(ctx, nb, Ls, Lt, T, C, first, eval_only, level == 0, np);          \
     } while (0)
     if (method == R360_PHOTO_CONSISTENCY) R360_LAUNCH(R360_PHOTO_CONSISTENCY);
     else if (method == R360_DEPTH_CONSISTENCY) R360_LAUNCH(R360_DEPTH_CONSISTENCY);

@@ -29,7 +29,12 @@ struct LevelBufs {
     int rows = 0, cols = 0;
     float2* p0 = nullptr;
     float4* tg = nullptr;
+    // the level's valid source pixels (minDepth < depth < maxDepth, RegisterPhotoICP.h:4578) in raster
+    // order as {LUT_xyz_sphere point (:4580-4582), gray}: the ICP pass streams these instead of the image
+    // (launch_pyramid builds them; the count is the frame's d_npts[level])
+    float4* pts = nullptr;
 };
+constexpr int R360_SRC_BLOCK = 4096;   // pixels per block of the source-point compaction
 
 // Per-geometry trigonometric tables, computed on the host with the same float expressions
 // as the reference (RegisterPhotoICP.h:4555-4569), so the device LUT is bit-identical.
@@ -268,6 +273,9 @@ struct r360_frame {
     uint8_t* d_bgr = nullptr;      // [8][rows][cols][3]
     uint16_t* d_depth = nullptr;   // [8][rows][cols] mm
     float* d_depth_m = nullptr;    // [8][rows][cols] undistorted metres
+    int* d_npts = nullptr;         // [R360_MAX_PYR] valid source points per level (LevelBufs::pts)
+    int* d_src_cnt = nullptr;      // [R360_MAX_PYR][blocks] compaction scratch
+    int src_blocks = 0;
     uint8_t* d_sph_bgr = nullptr;  // [H][W][3]
     uint16_t* d_sph_depth = nullptr;
     LevelBufs lv[R360_MAX_PYR];

@@ -88,6 +88,26 @@ def test_pyramid_bitexact(qvga):
                 assert np.array_equal(got[k], ref[l][k]), (l, k)
 
 
+def test_source_points_compaction(qvga):
+    """The ICP pass streams each level's valid source pixels (0.3 < depth < 6, RegisterPhotoICP.h:4578) as
+    compacted {LUT point, gray} records in raster order (frame_kernels.hip k_src_*): same count, same gray
+    values in the same order, and LUT points at the pixel's depth along its viewing ray."""
+    for f in (qvga["f1"], qvga["f2"]):
+        for l in range(6):
+            lv = f.level(l)
+            d, gray = lv["depth"].reshape(-1), lv["gray"].reshape(-1)
+            valid = (d > np.float32(0.3)) & (d < np.float32(6.0))
+            pts = f.points(l)
+            assert pts.shape[0] == int(valid.sum()), l
+            assert np.array_equal(pts[:, 3], gray[valid]), l
+            np.testing.assert_allclose(np.linalg.norm(pts[:, :3].astype(np.float64), axis=1), d[valid], rtol=2e-6)
+            rows, cols = lv["depth"].shape
+            r, c = np.nonzero(valid.reshape(rows, cols))
+            ares = 2 * np.pi / cols
+            phi = (rows / 2 - 0.5 - r) * ares
+            np.testing.assert_allclose(pts[:, 0], d[valid] * np.sin(phi), atol=2e-5)
+
+
 def _icp_check(H, g, e2, nv, nvis, Hr, gr, e2r, nvr, nvisr, npx):
     """The projection is bit-identical (glibc-exact asinf/atan2f port), so pixel sets and counts
     match exactly; the sums differ only by summation order (GPU: per-thread f32 partials over a few

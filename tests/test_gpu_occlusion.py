@@ -66,14 +66,18 @@ def test_occlusion_pass_parity(ctx, qvga, method, occ):
 
 def test_occ1_hessgrad_equals_plain(ctx, qvga):
     """calcHessGrad_sphereOcc1 indexes its Z-buffer by the source pixel (:3486-3488), so it never
-    occludes: its H / g / numVisiblePixels are calcHessGrad_sphere's."""
+    occludes: its H / g / numVisiblePixels are calcHessGrad_sphere's.  (The plain pass streams the compacted
+    source points, the occlusion pass the image, so the f32 partial sums group pixels differently: equal
+    counts, sums equal to summation-order rounding.)"""
     reg = R.RegisterPhotoICP(ctx)
     reg.setTargetFrame(qvga["f1"]); reg.setSourceFrame(qvga["f2"])
     P = POSES[1]
     H1, g1, _, _, nvis1 = reg.eval_occ(1, P, R.PHOTO_DEPTH, 1)
     H0, g0, _, _, nvis0 = reg.eval(1, P, R.PHOTO_DEPTH)
     assert nvis1 == nvis0
-    assert np.array_equal(H1, H0) and np.array_equal(g1, g0)
+    sH = np.abs(H0).max()
+    assert np.abs(H1 - H0).max() <= 1e-6 * sH
+    assert (np.abs(g1 - g0) <= 1e-6 * np.sqrt(np.abs(np.diag(H0)) * sH)).all()
 
 
 def test_occ2_filters_and_occludes(ctx, qvga):

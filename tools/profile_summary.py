@@ -55,5 +55,10 @@ for k in ("SQ_INSTS_VALU", "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_W
     v = pmc(k)
     if v is not None:
         out[k] = v
+# the ICP sources this profile measured (bench.py reports the traffic only while they are unchanged)
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+out["icp_source_hash"] = bench.icp_source_hash()
+out["tag"] = os.path.basename(os.path.normpath(dst))
 json.dump(out, open(os.path.join(dst, "l0_pass.json"), "w"), indent=1)
 print(json.dumps(out, indent=1))
