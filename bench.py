@@ -245,7 +245,7 @@ def main():
         b, d = R.synth_frame_rt(args.rows, args.cols, rt8, SEED, R.synth_path_pose(SEED, p0 + j))
         BGR[j], DEP[j] = b, d
     gen_s = time.perf_counter() - t_gen
-    pinned = R.HostPinned(BGR, DEP)
+    pinned = R.HostPinned(BGR, DEP) if os.environ.get("R360_NO_PIN") != "1" else R.HostPinned()
 
     def frames_of(i):
         return BGR[i - p0], DEP[i - p0]

@@ -9,9 +9,41 @@
 // created by rank 0 and handed to the other ranks by the caller (the bench uses torch.distributed's gloo
 // group, which never touches the GPU).
 #include <cstring>
+#include <dlfcn.h>
+#include <mutex>
 #include <rccl/rccl.h>
 
 #include "../r360_internal.h"
+
+// RCCL is loaded on first use (dlopen), so single-GPU users of the library never load it.
+namespace {
+struct Rccl {
+    decltype(&ncclGetUniqueId) getUniqueId = nullptr;
+    decltype(&ncclCommInitRank) commInitRank = nullptr;
+    decltype(&ncclCommDestroy) commDestroy = nullptr;
+    decltype(&ncclAllGather) allGather = nullptr;
+    decltype(&ncclAllReduce) allReduce = nullptr;
+    decltype(&ncclGetErrorString) errorString = nullptr;
+    bool ok = false;
+};
+const Rccl& rccl() {
+    static Rccl r;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) return;
+        r.getUniqueId = (decltype(r.getUniqueId))dlsym(h, "ncclGetUniqueId");
+        r.commInitRank = (decltype(r.commInitRank))dlsym(h, "ncclCommInitRank");
+        r.commDestroy = (decltype(r.commDestroy))dlsym(h, "ncclCommDestroy");
+        r.allGather = (decltype(r.allGather))dlsym(h, "ncclAllGather");
+        r.allReduce = (decltype(r.allReduce))dlsym(h, "ncclAllReduce");
+        r.errorString = (decltype(r.errorString))dlsym(h, "ncclGetErrorString");
+        r.ok = r.getUniqueId && r.commInitRank && r.commDestroy && r.allGather && r.allReduce && r.errorString;
+    });
+    return r;
+}
+}  // namespace
 
 #define CHECK_ARG(cond, msg)                  \
     do {                                      \
@@ -25,7 +57,7 @@
     do {                                                                                 \
         ncclResult_t _r = (call);                                                        \
         if (_r != ncclSuccess) {                                                         \
-            r360_set_error("%s failed: %s (%s:%d)", #call, ncclGetErrorString(_r), __FILE__, __LINE__); \
+            r360_set_error("%s failed: %s (%s:%d)", #call, rccl().errorString(_r), __FILE__, __LINE__); \
             return -1;                                                                   \
         }                                                                                \
     } while (0)
@@ -40,10 +72,13 @@ struct r360_comm {
 
 static_assert(sizeof(ncclUniqueId) == 128, "RCCL unique id size");
 
+#define REQUIRE_RCCL() CHECK_ARG(rccl().ok, "librccl.so.1 could not be loaded")
+
 extern "C" int r360_comm_unique_id(uint8_t id[128]) {
     CHECK_ARG(id, "null id");
+    REQUIRE_RCCL();
     ncclUniqueId u;
-    R360_NCCL(ncclGetUniqueId(&u));
+    R360_NCCL(rccl().getUniqueId(&u));
     memcpy(id, &u, sizeof u);
     return 0;
 }
@@ -51,6 +86,7 @@ extern "C" int r360_comm_unique_id(uint8_t id[128]) {
 extern "C" int r360_comm_init(int device, int nranks, int rank, const uint8_t id[128], r360_comm** out) {
     CHECK_ARG(id && out, "null arg");
     CHECK_ARG(nranks >= 1 && rank >= 0 && rank < nranks, "invalid rank / nranks");
+    REQUIRE_RCCL();
     R360_HIP(hipSetDevice(device));
     r360_comm* c = new r360_comm;
     c->device = device;
@@ -58,13 +94,13 @@ extern "C" int r360_comm_init(int device, int nranks, int rank, const uint8_t id
     c->rank = rank;
     ncclUniqueId u;
     memcpy(&u, id, sizeof u);
-    if (ncclCommInitRank(&c->comm, nranks, u, rank) != ncclSuccess) {
+    if (rccl().commInitRank(&c->comm, nranks, u, rank) != ncclSuccess) {
         r360_set_error("ncclCommInitRank failed (rank %d of %d)", rank, nranks);
         delete c;
         return -1;
     }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
-        ncclCommDestroy(c->comm);
+        rccl().commDestroy(c->comm);
         delete c;
         r360_set_error("hipStreamCreate failed");
         return -1;
@@ -77,7 +113,7 @@ extern "C" void r360_comm_destroy(r360_comm* c) {
     if (!c) return;
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
-    ncclCommDestroy(c->comm);
+    rccl().commDestroy(c->comm);
     hipFree(c->d_buf);
     hipStreamDestroy(c->stream);
     delete c;
@@ -104,7 +140,7 @@ extern "C" int r360_comm_allgather(r360_comm* c, const void* send, void* recv, s
     char* d_recv = d_send + slot;
     R360_HIP(hipMemcpyAsync(d_send, send, bytes, hipMemcpyHostToDevice, c->stream));
     // the receive slices are `bytes` apart (ncclAllGather's layout)
-    R360_NCCL(ncclAllGather(d_send, d_recv, bytes, ncclUint8, c->comm, c->stream));
+    R360_NCCL(rccl().allGather(d_send, d_recv, bytes, ncclUint8, c->comm, c->stream));
     R360_HIP(hipMemcpyAsync(recv, d_recv, bytes * c->nranks, hipMemcpyDeviceToHost, c->stream));
     R360_HIP(hipStreamSynchronize(c->stream));
     return 0;
@@ -117,7 +153,7 @@ extern "C" int r360_comm_allreduce_max(r360_comm* c, double* v, int n) {
     const size_t bytes = sizeof(double) * (size_t)n;
     if (int rc = comm_reserve(c, bytes)) return rc;
     R360_HIP(hipMemcpyAsync(c->d_buf, v, bytes, hipMemcpyHostToDevice, c->stream));
-    R360_NCCL(ncclAllReduce(c->d_buf, c->d_buf, (size_t)n, ncclFloat64, ncclMax, c->comm, c->stream));
+    R360_NCCL(rccl().allReduce(c->d_buf, c->d_buf, (size_t)n, ncclFloat64, ncclMax, c->comm, c->stream));
     R360_HIP(hipMemcpyAsync(v, c->d_buf, bytes, hipMemcpyDeviceToHost, c->stream));
     R360_HIP(hipStreamSynchronize(c->stream));
     return 0;

@@ -391,6 +391,13 @@ extern "C" int r360_frame_create(r360_ctx* ctx, const r360_calib* calib, r360_fr
     R360_HIP(hipMalloc(&f->d_npts, sizeof(int) * R360_MAX_PYR));
     R360_HIP(hipMemset(f->d_npts, 0, sizeof(int) * R360_MAX_PYR));
     R360_HIP(hipMalloc(&f->d_src_cnt, sizeof(int) * R360_MAX_PYR * (size_t)f->src_blocks));
+    SrcLevel sl[R360_MAX_PYR];
+    for (int l = 0; l < f->n_levels; ++l) {
+        const LevelTrig& T = calib->trig[l];
+        sl[l] = SrcLevel{f->lv[l].p0, f->lv[l].pts, T.sinphi, T.cosphi, T.sinth, T.costh, f->lv[l].rows, f->lv[l].cols};
+    }
+    R360_HIP(hipMalloc(&f->d_src_levels, sizeof(SrcLevel) * R360_MAX_PYR));
+    R360_HIP(hipMemcpy(f->d_src_levels, sl, sizeof(SrcLevel) * f->n_levels, hipMemcpyHostToDevice));
     *out = f;
     return 0;
 }
@@ -401,7 +408,7 @@ extern "C" void r360_frame_destroy(r360_frame* f) {
     // outlive their context at interpreter shutdown.
     hipFree(f->d_bgr); hipFree(f->d_depth); hipFree(f->d_depth_m); hipFree(f->d_sph_bgr); hipFree(f->d_sph_depth);
     for (int l = 0; l < f->n_levels; ++l) { hipFree(f->lv[l].p0); hipFree(f->lv[l].tg); hipFree(f->lv[l].pts); }
-    hipFree(f->d_npts); hipFree(f->d_src_cnt);
+    hipFree(f->d_npts); hipFree(f->d_src_cnt); hipFree(f->d_src_levels);
     for (int l = 0; l < f->n_slevels; ++l) { hipFree(f->sp[l].p0); hipFree(f->sp[l].tg); }
     plane_bufs_free(f);
     delete f->sphere_cloud;

@@ -206,16 +206,13 @@ int launch_stitch(r360_frame* f) {
 // expressions) and the gray value; both are fixed for a source frame.  They are compacted here once per
 // frame, in raster order (a deterministic two-kernel scan), so the pass streams only valid pixels.
 // blockIdx.y = pyramid level; a block covers R360_SRC_BLOCK consecutive pixels, 4 per thread.
-struct SrcLevel { const float2* p0; float4* pts; const float* sinphi; const float* cosphi; const float* sinth;
-                  const float* costh; int rows, cols; };
-struct SrcLevels { SrcLevel l[R360_MAX_PYR]; };
 constexpr int SRC_TPB = R360_SRC_BLOCK / 4;
 
 __device__ __forceinline__ bool src_valid(float d, float min_d, float max_d) { return min_d < d && d < max_d; }
 
-__global__ void __launch_bounds__(SRC_TPB) k_src_count(SrcLevels L, float min_d, float max_d, int* __restrict__ cnt,
-                                                      int stride) {
-    const SrcLevel& S = L.l[blockIdx.y];
+__global__ void __launch_bounds__(SRC_TPB) k_src_count(const SrcLevel* __restrict__ L, float min_d, float max_d,
+                                                      int* __restrict__ cnt, int stride) {
+    const SrcLevel S = L[blockIdx.y];
     const long n = (long)S.rows * S.cols;
     const long b0 = (long)blockIdx.x * R360_SRC_BLOCK;
     if (b0 >= n) return;
@@ -236,9 +233,9 @@ __global__ void __launch_bounds__(SRC_TPB) k_src_count(SrcLevels L, float min_d,
     }
 }
 
-__global__ void __launch_bounds__(SRC_TPB) k_src_compact(SrcLevels L, float min_d, float max_d, const int* __restrict__ cnt,
-                                                        int stride, int* __restrict__ npts) {
-    const SrcLevel& S = L.l[blockIdx.y];
+__global__ void __launch_bounds__(SRC_TPB) k_src_compact(const SrcLevel* __restrict__ L, float min_d, float max_d,
+                                                        const int* __restrict__ cnt, int stride, int* __restrict__ npts) {
+    const SrcLevel S = L[blockIdx.y];
     const long n = (long)S.rows * S.cols;
     const long b0 = (long)blockIdx.x * R360_SRC_BLOCK;
     if (b0 >= n) return;
@@ -298,15 +295,11 @@ int launch_pyramid(r360_frame* f) {
         hipLaunchKernelGGL(k_gradient, dim3(grid_for(n)), dim3(TPB), 0, f->ctx->stream, f->lv[l].p0, f->lv[l].rows,
                            f->lv[l].cols, f->lv[l].tg, 1, 1);
     }
-    SrcLevels L{};
-    for (int l = 0; l < f->n_levels; ++l) {
-        const LevelTrig& T = f->calib->trig[l];
-        L.l[l] = SrcLevel{f->lv[l].p0, f->lv[l].pts, T.sinphi, T.cosphi, T.sinth, T.costh, f->lv[l].rows, f->lv[l].cols};
-    }
     const dim3 g(f->src_blocks, f->n_levels);
-    hipLaunchKernelGGL(k_src_count, g, dim3(SRC_TPB), 0, f->ctx->stream, L, min_d, max_d, f->d_src_cnt, f->src_blocks);
-    hipLaunchKernelGGL(k_src_compact, g, dim3(SRC_TPB), 0, f->ctx->stream, L, min_d, max_d, f->d_src_cnt,
-                       f->src_blocks, f->d_npts);
+    hipLaunchKernelGGL(k_src_count, g, dim3(SRC_TPB), 0, f->ctx->stream, f->d_src_levels, min_d, max_d, f->d_src_cnt,
+                       f->src_blocks);
+    hipLaunchKernelGGL(k_src_compact, g, dim3(SRC_TPB), 0, f->ctx->stream, f->d_src_levels, min_d, max_d,
+                       f->d_src_cnt, f->src_blocks, f->d_npts);
     R360_HIP(hipGetLastError());
     return 0;
 }

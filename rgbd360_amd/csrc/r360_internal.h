@@ -35,6 +35,9 @@ struct LevelBufs {
     float4* pts = nullptr;
 };
 constexpr int R360_SRC_BLOCK = 4096;   // pixels per block of the source-point compaction
+// one level's inputs / output of the compaction (a device-side table per frame, fixed at creation)
+struct SrcLevel { const float2* p0; float4* pts; const float* sinphi; const float* cosphi; const float* sinth;
+                  const float* costh; int rows, cols; };
 
 // Per-geometry trigonometric tables, computed on the host with the same float expressions
 // as the reference (RegisterPhotoICP.h:4555-4569), so the device LUT is bit-identical.
@@ -275,6 +278,7 @@ struct r360_frame {
     float* d_depth_m = nullptr;    // [8][rows][cols] undistorted metres
     int* d_npts = nullptr;         // [R360_MAX_PYR] valid source points per level (LevelBufs::pts)
     int* d_src_cnt = nullptr;      // [R360_MAX_PYR][blocks] compaction scratch
+    SrcLevel* d_src_levels = nullptr;  // [n_levels]
     int src_blocks = 0;
     uint8_t* d_sph_bgr = nullptr;  // [H][W][3]
     uint16_t* d_sph_depth = nullptr;
