@@ -267,6 +267,7 @@ def main():
                repeats=max(args.warmup, 1), runs=runs)
 
     rec = np.zeros((args.steps, p1 - p0, OD.REC), np.float32)
+    runner.host_s[:] = 0
     barrier()
     for c in ctxs:
         c.timing(True)
@@ -294,6 +295,8 @@ def main():
                      "k_ccl", "k_plane_fit", "k_refine", "k_model_stats", "k_icp_pass", "k_icp_pass_L0"):
             ms, n = c.timing_read(name)
             stage[name] = stage.get(name, 0.0) + ms
+    hs = runner.host_s.sum(axis=0)
+    host_ms = {k: 1e3 * v / max(hs[3], 1) for k, v in zip(("load_build_enqueue", "pbmap_stage", "dense_wait"), hs[:3])}
     if group is not None:
         elapsed = group.max(elapsed)
     pairs_job = args.steps * sum(sizes)
@@ -408,6 +411,7 @@ def main():
             **({"eval_probe": probe} if probe else {}),
         },
         "stage_ms_per_pair": {k: v / max(args.steps * steps_pairs, 1) for k, v in stage.items()},
+        "pipeline_host_ms_per_pair": host_ms,
         "frame_generation_s": round(gen_s, 1),
     }
     if rank == 0 and traj is not None:

@@ -18,6 +18,8 @@ from __future__ import annotations
 
 from concurrent.futures import ThreadPoolExecutor
 
+import time
+
 import numpy as np
 
 from . import (BUILD_PLANES, BUILD_PYRAMID, BUILD_SPHERE, BUILD_UNDISTORT, PHOTO_DEPTH, PLANAR_3DoF, Calib360,
@@ -110,6 +112,8 @@ class SequenceRunner:
             self.cals.append(cal)
             self.frames.append([Frame360(cal), Frame360(cal)])
         self.stats = [IcpStats() for _ in range(pipelines)]
+        # host-side time per pipeline: [load + build enqueue, PbMap stage (register_async), dense wait, pairs]
+        self.host_s = np.zeros((pipelines, 4))
         self.pool = ThreadPoolExecutor(max_workers=pipelines)
         self.eye = np.eye(4, dtype=np.float32).reshape(16)
 
@@ -127,11 +131,14 @@ class SequenceRunner:
                 f.upload_device(*frames_of(i))
             else:
                 f.upload_async(*frames_of(i))
+        hs = self.host_s[p]
         load(fa, a)
         fa.build(self.flags, sync=False)
         for i in range(a, b):
+            t0 = time.perf_counter()
             load(fb, i + 1)
             fb.build(self.flags, sync=False)
+            t1 = time.perf_counter()
             rec = out[i - p0]
             pose, info = np.zeros(16, np.float32), np.zeros(36, np.float32)
             if self.dense_only:   # alignFrames360 from identity (configs 3 / 5), pose conjugated back to the rig
@@ -149,9 +156,11 @@ class SequenceRunner:
                                            self.max_match_planes, self.mode)
                 if rc != 0:
                     raise RuntimeError(f"r360_register_async: {L.r360_last_error()}")
+                t2 = time.perf_counter()
                 rc = L.r360_register_result(ctx.h, _fptr(pose), _fptr(info), C.byref(self.stats[p]))
                 if rc < 0:
                     raise RuntimeError(f"r360_register_result: {L.r360_last_error()}")
+                hs += (t1 - t0, t2 - t1, time.perf_counter() - t2, 1)
             rec[R_POSE:R_POSE + 16] = pose
             rec[R_INFO:R_INFO + 36] = info
             rec[R_STATUS] = 2 if self.stats[p].illposed else rc
