@@ -401,6 +401,8 @@ int r360_proj_check_pose(const float* lx, const float* ly, const float* lz, int 
 /* sqrt_rn / div_rn (the pass's correctly rounded f32 sqrt / division) against the compiler's IEEE
  * operations on n hashed operands: out = {sqrt mismatches, division mismatches}, both must be 0. */
 int r360_rn_check(unsigned n, unsigned seed, unsigned long long out[2]);
+/* The device ILL-POSED test: Eigen FullPivLU<Matrix<float,6,6>>::rank() of n row-major matrices. */
+int r360_rank6(const float* M, int n, int* ranks);
 int r360_libm_eval(const float* x, const float* y, const float* z, int n, float* asin_out, float* atan2_out,
                    int on_device);
 

@@ -124,6 +124,7 @@ def lib() -> C.CDLL:
             "orc_register_dense_robot": (C.c_int, [vp, vp, vp, vp, C.c_int, C.c_int, fp, fp, fp, C.c_int,
                                                    C.POINTER(IcpParams), fp, fp, C.POINTER(DenseStats)]),
             "orc_exp_se3": (None, [dp, C.c_int, fp]),
+            "orc_rank6f": (C.c_int, [fp]),
             "orc_huber": (C.c_float, [C.c_float, C.c_float]),
             "orc_libm": (None, [fp, fp, fp, C.c_int, fp, fp]),
             "orc_cloud_downsample": (None, [fp, vp, C.c_int, C.c_int, fp, vp]),
@@ -434,6 +435,12 @@ def exp_se3(mu, pseudo=True) -> np.ndarray:
     T = np.zeros(16, np.float32)
     lib().orc_exp_se3(m.ctypes.data_as(C.POINTER(C.c_double)), int(pseudo), _f(T))
     return from16(T)
+
+
+def rank6f(M) -> int:
+    """Eigen FullPivLU<Matrix<float,6,6>>::rank() of M (the alignFrames360 ILL-POSED test, :4682)."""
+    m = np.ascontiguousarray(np.asarray(M, np.float32).reshape(6, 6))
+    return int(lib().orc_rank6f(_f(m)))
 
 
 def libm(x, y, z):

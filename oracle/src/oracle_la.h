@@ -19,28 +19,34 @@ static inline void matmul4f(const float A[16], const float B[16], float C[16]) {
     memcpy(C, out, sizeof(out));
 }
 
-// Eigen FullPivLU::rank() with the default threshold (eps * diagonalSize) (:4682)
+// Eigen FullPivLU<Matrix<float,6,6>>::rank() with the default threshold (:4682, :4345, RegisterRGBD360.h:443):
+// the reference's matrices are float, so the decomposition runs in float.  Per step the biggest |.| of the
+// remaining corner is found in Eigen's visiting order (column-major, first strictly greater, starting at the
+// corner's first coefficient); m_maxpivot is the largest of those maxima; rank = #pivots with
+// |pivot| > |maxpivot| * (FLT_EPSILON * 6).  M_in: row-major, values already rounded to float.
 static inline int rank6(const double M_in[36]) {
-    double M[36]; memcpy(M, M_in, sizeof(M));
-    double maxpiv = 0; int rk = 0;
-    double piv[6];
+    float M[36];
+    for (int k = 0; k < 36; ++k) M[k] = (float)M_in[k];
+    float maxpiv = 0.f, piv[6];
+    int nz = 6;
     for (int k = 0; k < 6; ++k) {
-        int br = k, bc = k; double bv = -1;
-        for (int r = k; r < 6; ++r)
-            for (int c = k; c < 6; ++c)
+        int br = k, bc = k;
+        float bv = std::fabs(M[k * 6 + k]);
+        for (int c = k; c < 6; ++c)
+            for (int r = (c == k ? k + 1 : k); r < 6; ++r)
                 if (std::fabs(M[r * 6 + c]) > bv) { bv = std::fabs(M[r * 6 + c]); br = r; bc = c; }
+        if (bv == 0.f) { nz = k; break; }
+        if (bv > maxpiv) maxpiv = bv;
         for (int c = 0; c < 6; ++c) std::swap(M[k * 6 + c], M[br * 6 + c]);
         for (int r = 0; r < 6; ++r) std::swap(M[r * 6 + k], M[r * 6 + bc]);
         piv[k] = M[k * 6 + k];
-        if (piv[k] != 0)
-            for (int r = k + 1; r < 6; ++r) {
-                double f = M[r * 6 + k] / piv[k];
-                for (int c = k; c < 6; ++c) M[r * 6 + c] -= f * M[k * 6 + c];
-            }
+        for (int r = k + 1; r < 6; ++r) M[r * 6 + k] = M[r * 6 + k] / piv[k];
+        for (int r = k + 1; r < 6; ++r)
+            for (int c = k + 1; c < 6; ++c) M[r * 6 + c] = M[r * 6 + c] - M[r * 6 + k] * M[k * 6 + c];
     }
-    maxpiv = std::fabs(piv[0]);
-    const double thr = 1.1920928955078125e-07 * 6;
-    for (int k = 0; k < 6; ++k) if (std::fabs(piv[k]) > thr * maxpiv) ++rk;
+    const float thr = maxpiv * (1.1920928955078125e-07f * 6.0f);
+    int rk = 0;
+    for (int k = 0; k < nz; ++k) if (std::fabs(piv[k]) > thr) ++rk;
     return rk;
 }
 

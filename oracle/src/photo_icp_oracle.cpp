@@ -635,6 +635,7 @@ extern "C" int orc_align360_occ(const uint8_t* trg_bgr, const uint16_t* trg_dept
         Lut lut; build_lut(&L, p->min_depth, p->max_depth, lut);
         const bool fixed = (l == 0 && p->fixed_iters_level0 > 0);
         int it = 0, nv = 0, evals = 0;
+        double lambda = p->lambda;                                        // :4589
         const int maxIters = fixed ? p->fixed_iters_level0 : p->max_iters;
         float upd[6] = {1, 1, 1, 1, 1, 1};
         double error = error_any(&L, lut, pose, method, occlusion, p, &nv);
@@ -652,8 +653,10 @@ extern "C" int orc_align360_occ(const uint8_t* trg_bgr, const uint16_t* trg_dept
             double Hd[36], HL[36], gd[6];
             for (int k = 0; k < 36; ++k) Hd[k] = Hf[k];
             for (int k = 0; k < 6; ++k) gd[k] = gf[k];
+            // hessian + lambda * diag(hessian): float matrices, the double lambda enters as a float scalar;
+            // lambda = 1 at each level start, divided by step = 5 on every accepted update (:4589-4590, :4718)
             memcpy(HL, Hd, sizeof(HL));
-            for (int k = 0; k < 6; ++k) HL[k * 7] += p->lambda * Hd[k * 7];
+            for (int k = 0; k < 6; ++k) HL[k * 7] = (float)(Hf[k * 7] + (float)lambda * Hf[k * 7]);
             if (rank6(HL) != 6) {                                       // :4682-4690
                 memcpy(pose_out, pose, sizeof(float) * 16);
                 if (st) st->illposed = 1;
@@ -671,6 +674,7 @@ extern "C" int orc_align360_occ(const uint8_t* trg_bgr, const uint16_t* trg_dept
             ++evals;
             diff_error = error - new_error;                               // :4711
             if (diff_error > p->tol_residual) {                           // :4715-4722
+                lambda /= 5.0;                                            // lambda /= step (:4718)
                 memcpy(pose, cand, sizeof(pose));
                 error = new_error;
                 it = it + 1;
@@ -692,6 +696,13 @@ extern "C" int orc_align360(const uint8_t* trg_bgr, const uint16_t* trg_depth,
                             float g_out[6], orc_icp_stats* st) {
     return orc_align360_occ(trg_bgr, trg_depth, src_bgr, src_depth, rows, cols, init, method, 0, p, pose_out,
                             H_out, g_out, st);
+}
+
+// (M).rank() of Eigen::Matrix<float,6,6> (row-major M), the ILL-POSED test of alignFrames360 (:4682)
+extern "C" int orc_rank6f(const float* M) {
+    double Md[36];
+    for (int k = 0; k < 36; ++k) Md[k] = M[k];
+    return rank6(Md);
 }
 
 // glibc float asinf / atan2f as the reference calls them (std::asin(float), std::atan2(float, float))

@@ -211,6 +211,7 @@ _SIGS = [
     ("r360_synth_path_pose", C.c_int, [C.c_uint32, C.c_int, _FP]),
     ("r360_libm_eval", C.c_int, [_FP, _FP, _FP, C.c_int, _FP, _FP, C.c_int]),
     ("r360_rn_check", C.c_int, [C.c_uint, C.c_uint, C.POINTER(C.c_ulonglong)]),
+    ("r360_rank6", C.c_int, [_FP, C.c_int, _IP]),
     ("r360_proj_check_pose", C.c_int, [_FP, _FP, _FP, C.c_int, _FP, C.c_int, C.c_int, C.POINTER(C.c_ulonglong),
                                        C.POINTER(C.c_ulonglong)]),
     ("r360_proj_check", C.c_int, [_FP, _FP, _FP, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_ulonglong),

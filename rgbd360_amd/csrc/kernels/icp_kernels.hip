@@ -1190,6 +1190,32 @@ __global__ void k_rn_check(unsigned n, unsigned seed, unsigned long long* __rest
 }
 }  // namespace
 
+namespace {
+__global__ void k_rank6(const float* __restrict__ M, int n, int* __restrict__ out) {
+    const int m = blockIdx.x, lane = threadIdx.x;
+    if (m >= n) return;
+    const float a = lane < 36 ? M[m * 36 + lane] : 0.f;
+    const int rk = wave_rank6(a, lane);
+    if (lane == 0) out[m] = rk;
+}
+}  // namespace
+
+// Test hook: the device rank test (wave_rank6, the ILL-POSED check of alignFrames360 :4682 / alignFrames
+// :4345 / RegisterDensePhotoICP :443) on n row-major 6x6 float matrices.
+extern "C" int r360_rank6(const float* M, int n, int* ranks) {
+    if (!M || !ranks || n <= 0) { r360_set_error("r360_rank6: bad arguments"); return -2; }
+    float* dM;
+    int* dr;
+    R360_HIP(hipMalloc(&dM, sizeof(float) * 36 * (size_t)n));
+    R360_HIP(hipMalloc(&dr, sizeof(int) * (size_t)n));
+    R360_HIP(hipMemcpy(dM, M, sizeof(float) * 36 * (size_t)n, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_rank6, dim3(n), dim3(64), 0, 0, dM, n, dr);
+    R360_HIP(hipGetLastError());
+    R360_HIP(hipMemcpy(ranks, dr, sizeof(int) * (size_t)n, hipMemcpyDeviceToHost));
+    (void)hipFree(dM); (void)hipFree(dr);
+    return 0;
+}
+
 extern "C" int r360_rn_check(unsigned n, unsigned seed, unsigned long long out[2]) {
     unsigned long long* d;
     R360_HIP(hipMalloc(&d, 16));

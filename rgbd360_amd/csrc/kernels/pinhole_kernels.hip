@@ -223,7 +223,7 @@ __device__ void lm_step_wave(IcpState* S, const double* sums, const IcpConst& C,
         return i == j ? h + G->lam * h : h;
     };
     if (mode == 1) {                                     // (H + lambda diag H).rank() != 6 -> ILL-POSED
-        const double hl = lane < 36 ? (double)damped(lane / 6, lane - (lane / 6) * 6) : 0.0;
+        const float hl = lane < 36 ? damped(lane / 6, lane - (lane / 6) * 6) : 0.f;
         if (wave_rank6(hl, lane) != 6) {
             if (lane == 0) {
                 S->illposed = 1; S->stop = 1; S->active = 0;

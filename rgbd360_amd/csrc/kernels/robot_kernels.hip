@@ -280,10 +280,10 @@ __global__ __launch_bounds__(64) void k_robot_finalize(const double* __restrict_
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         // (Hessian + lambda * diag(Hessian)).rank() != 6 -> ILL-POSED, return false (:427-434);
         // lambda = 0.001 enters as a float scalar
-        double hl = 0.0;
+        float hl = 0.f;
         if (lane < 36) {
             const float h = sH[lane];
-            hl = (lane % 7 == 0) ? (double)(h + 0.001f * h) : (double)h;
+            hl = (lane % 7 == 0) ? h + 0.001f * h : h;
         }
         const int rk = wave_rank6(hl, lane);
         if (rk != 6) {

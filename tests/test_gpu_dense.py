@@ -250,3 +250,17 @@ def test_correctly_rounded_sqrt_div():
     out = (R.C.c_ulonglong * 2)()
     R._check(R.lib().r360_rn_check(1 << 26, 7, out), "rn_check")
     assert out[0] == 0 and out[1] == 0, (out[0], out[1])
+
+
+def test_rank_test_matches_oracle_over_lambda_schedule():
+    """The device ILL-POSED test (icp_la.inc wave_rank6: Eigen's float FullPivLU rank) gives the oracle's
+    verdict on near-singular Hessians over alignFrames360's decaying lambda (1, /5 per accepted update,
+    RegisterPhotoICP.h:4589, :4718), including the ones where the decay flips it."""
+    from _cases import lambda_family
+    fam = lambda_family()
+    M = np.ascontiguousarray(np.stack([m for _, _, m in fam]), np.float32)
+    out = np.zeros(len(fam), np.int32)
+    R._check(R.lib().r360_rank6(R._fptr(M), len(fam), out.ctypes.data_as(R.C.POINTER(R.C.c_int))), "rank6")
+    ref = np.array([O.rank6f(m) for _, _, m in fam])
+    assert np.array_equal(out, ref)
+    assert (ref < 6).any() and (ref == 6).any()

@@ -8,6 +8,7 @@ import numpy as np
 import pytest
 
 from oracle import oracle360 as O
+from _cases import lambda_family
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden", "oracle_samples.npz")
 
@@ -207,3 +208,53 @@ def test_align_golden_and_descent(samples, gold):
     e0 = O.error_sphere(ls[1], lt[1], np.eye(4))[0]
     e1 = O.error_sphere(ls[1], lt[1], pose)[0]
     assert e1 < e0
+
+
+def _eigen_fullpivlu_rank_f32(M):
+    """Independent pure-Python statement of Eigen FullPivLU<Matrix<float,6,6>>::rank() (Eigen 3 FullPivLU.h
+    computeInPlace / rank): float arithmetic; the corner's biggest |.| in column-major visiting order (first
+    strictly greater, starting at the corner's first coefficient); maxpivot = the largest corner maximum;
+    pivots counted above |maxpivot| * (epsilon * 6)."""
+    a = [[np.float32(M[r][c]) for c in range(6)] for r in range(6)]
+    f = np.float32
+    maxpiv, pivs, nz = f(0), [], 6
+    for k in range(6):
+        br, bc, bv = k, k, abs(a[k][k])
+        for c in range(k, 6):
+            for r in range(k, 6):
+                if (r, c) != (k, k) and abs(a[r][c]) > bv:
+                    br, bc, bv = r, c, abs(a[r][c])
+        if bv == 0:
+            nz = k
+            break
+        maxpiv = max(maxpiv, bv)
+        a[k], a[br] = a[br], a[k]
+        for row in a:
+            row[k], row[bc] = row[bc], row[k]
+        p = a[k][k]
+        pivs.append(p)
+        for r in range(k + 1, 6):
+            a[r][k] = f(a[r][k] / p)
+        for r in range(k + 1, 6):
+            for c in range(k + 1, 6):
+                a[r][c] = f(a[r][c] - f(a[r][k] * a[k][c]))
+    thr = f(maxpiv * f(f(1.1920928955078125e-07) * f(6)))
+    return sum(1 for k in range(nz) if abs(pivs[k]) > thr)
+
+
+def test_rank6_is_eigens_float_fullpivlu():
+    """The oracle's ILL-POSED test (oracle_la.h rank6) equals an independent statement of Eigen's float
+    FullPivLU rank on near-singular matrices, and lambda's decay changes the verdict on some of them."""
+    ranks = {}
+    for trial, it, M in lambda_family():
+        r = O.rank6f(M)
+        assert r == _eigen_fullpivlu_rank_f32(M), (trial, it)
+        ranks.setdefault(trial, []).append(r)
+    flips = [t for t, rs in ranks.items() if rs[0] == 6 and min(rs) < 6]
+    assert len(flips) >= 5, ranks          # lambda = 1 passes, a decayed lambda fails
+    # singular and zero matrices
+    Z = np.zeros((6, 6), np.float32)
+    assert O.rank6f(Z) == 0 and _eigen_fullpivlu_rank_f32(Z) == 0
+    E = np.eye(6, dtype=np.float32)
+    E[5, 5] = 0
+    assert O.rank6f(E) == 5 == _eigen_fullpivlu_rank_f32(E)
