@@ -2,8 +2,12 @@
 // the MI355X library: for each new Frame360, PbMap registration against the previous keyframe, dense
 // RegisterPhotoICP refinement initialised with the rotOffset-conjugated PbMap pose (Register()), the
 // |t| < 0.4 m frame skip (:230-238) and the trajectory prefix product currentPose *= rigidTransf (:257).
+// As in the reference, the keyframe (frame360_1) advances only after a registration whose PbMap stage
+// succeeded and whose dense translation reached 0.4 m (bGoodRegistration, :145-148, :189, :230-238).
 //   usage: OdometryRGBD360 <dir with sphere_images_<n>.bin> [first] [step] [calib_dir]
-//          OdometryRGBD360 --synthetic <n_frames>        (procedural room, 8 x 480x640, no I/O)
+//          OdometryRGBD360 --synthetic <n_frames> [skip]  (procedural room, 8 x 480x640, no I/O; skip = 1
+//                                                          applies the |t| < 0.4 m frame skip, 0 registers
+//                                                          every consecutive pair)
 #include <rgbd360/rgbd360.h>
 
 #include <cmath>
@@ -23,6 +27,7 @@ int main(int argc, char** argv) {
     }
     const bool synthetic = std::string(argv[1]) == "--synthetic";
     const int n_synth = synthetic && argc > 2 ? std::atoi(argv[2]) : 32;
+    const bool skip = !synthetic || (argc > 3 && std::atoi(argv[3]) != 0);
     const std::string dir = argv[1];
     int frame = !synthetic && argc > 2 ? std::atoi(argv[2]) : 1;
     const int step = !synthetic && argc > 3 ? std::atoi(argv[3]) : 1;
@@ -62,7 +67,7 @@ int main(int argc, char** argv) {
         std::unique_ptr<r360::Frame360> f1(new r360::Frame360(&calib));
         if (!load(*f1, frame)) { std::fprintf(stderr, "no first frame\n"); return 3; }
         build(*f1);
-        r360::RegisterRGBD360 registerer(ctx, "config_files/configLocaliser_sphericalOdometry.ini");
+        r360::RegisterRGBD360 registerer(ctx, std::string(RGBD360_DATA_DIR) + "/config_files/configLocaliser_sphericalOdometry.ini");
         r360::Matrix4f currentPose, prevRel;
         int n_kf = 1;
         for (int idx = frame + step;; idx += step) {
@@ -75,12 +80,17 @@ int main(int argc, char** argv) {
             const float dist = std::sqrt(rigidTransf(0, 3) * rigidTransf(0, 3) + rigidTransf(1, 3) * rigidTransf(1, 3) +
                                          rigidTransf(2, 3) * rigidTransf(2, 3));
             std::printf("frame %d: PbMap %s, dist %.3f\n", idx, pbmap_ok ? "ok" : "failed (dense from prior)", dist);
-            if (dist < 0.4f && !synthetic) continue;         // skip frames too close to the keyframe (:230-238)
+            if (dist < 0.4f && skip) continue;                // skip frames too close to the keyframe (:230-238)
             currentPose = currentPose * rigidTransf;          // :257
             prevRel = rigidTransf;
-            f1 = std::move(f2);
-            ++n_kf;
-            std::printf("  pose t = (%.3f %.3f %.3f)\n", currentPose(0, 3), currentPose(1, 3), currentPose(2, 3));
+            if (pbmap_ok) {                                   // frame360_1 = frame360_2 only if bGoodRegistration
+                f1 = std::move(f2);
+                ++n_kf;
+            }
+            std::printf("  pose %d:", idx);
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 4; ++c) std::printf(" %.6f", currentPose(r, c));
+            std::printf("\n");
         }
         std::printf("%d keyframes\n", n_kf);
     } catch (const std::exception& e) {

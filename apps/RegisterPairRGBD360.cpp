@@ -32,7 +32,7 @@ int main(int argc, char** argv) {
         frame360_2.undistort();
         frame360_2.buildSphereCloud();
         frame360_2.getPlanes();
-        r360::RegisterRGBD360 registerer(ctx, "config_files/configLocaliser_sphericalOdometry.ini");
+        r360::RegisterRGBD360 registerer(ctx, std::string(RGBD360_DATA_DIR) + "/config_files/configLocaliser_sphericalOdometry.ini");
         const bool good = registerer.RegisterPbMap(&frame360_1, &frame360_2, 25, r360::RegisterRGBD360::PLANAR_3DoF);
         std::printf("planes %zu / %zu, registration %s\n", frame360_1.planes.size(), frame360_2.planes.size(),
                     good ? "good" : "insufficient");

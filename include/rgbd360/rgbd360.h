@@ -9,9 +9,9 @@
 //                                                  getHessian/getGradient :279-288
 //   RegisterRGBD360   include/RegisterRGBD360.h    ctor(ini) :97, setReference/setTarget :111/:161,
 //                                                  RegisterPbMap :276, getPose :199, getCovMat :208,
-//                                                  getInfoMat :219, getMatchedPlanes :242,
+//                                                  getInfoMat :219, calcEntropy :230, getMatchedPlanes :242,
 //                                                  getAreaMatched :251, areaSource/areaTarget :91-94,
-//                                                  RegisterDensePhotoICP :344,
+//                                                  RegisterDensePhotoICP :344, trackingScore :526,
 //                                                  Register() = OdometryKeyFrame360.cpp:205-254
 //   BatchRegistration  many independent pair registrations on one GPU (§8f-4): SphereGraphSLAM's
 //                      tracking loop (SLAM/SphereGraphSLAM.cpp:169-231) and LoopClosure360's candidate
@@ -21,13 +21,17 @@
 // column-major Eigen layout; r360::Matrix4f / Matrix6f are minimal stand-ins with Eigen's (row, col)
 // accessors and data() — define RGBD360_WITH_EIGEN to use Eigen::Matrix4f / Matrix<float,6,6>.
 // Differences from the reference surface, all forced by the GPU-resident design:
-//   * RegisterPhotoICP::setSourceFrame/setTargetFrame take the Frame360 (its sphere and pyramid live
-//     in HBM) instead of the cv::Mat sphereRGB/sphereDepth pair;
+//   * images are r360::Mat (rows, cols, channels, bytes) instead of cv::Mat.  Frame360::sphereRGB /
+//     sphereDepth are views of the frame's sphere in HBM: RegisterPhotoICP::setSourceFrame(
+//     frame->sphereRGB, frame->sphereDepth) uses the frame's device pyramid without a copy; other images
+//     are uploaded and pyramided on the GPU (r360_frame_set_sphere);
 //   * objects are bound to an r360::Context (one GPU + HIP stream); errors throw r360::Error.
 #pragma once
 #include <rgbd360_hip.h>
 
+#include <cmath>
 #include <cstring>
+#include <limits>
 #include <map>
 #include <stdexcept>
 #include <string>
@@ -74,6 +78,21 @@ struct MatrixNf {                       // column-major, Eigen's (row, col) and 
 typedef MatrixNf<4> Matrix4f;
 typedef MatrixNf<6> Matrix6f;
 #endif
+
+class Frame360;
+
+// Host image (cv::Mat stand-in: CV_8UC3 BGR sphereRGB, CV_16UC1 range-mm sphereDepth).  A Mat whose `frame`
+// is set is a view of that Frame360's sphere in HBM (no host pixels until Frame360::downloadSphere()).
+struct Mat {
+    int rows = 0, cols = 0, channels = 1, elem = 1;   // elem: bytes per channel
+    std::vector<uint8_t> bytes;
+    const Frame360* frame = nullptr;
+    Mat() = default;
+    Mat(int r, int c, int ch, int e) : rows(r), cols(c), channels(ch), elem(e), bytes(size_t(r) * c * ch * e) {}
+    uint8_t* data() { return bytes.data(); }
+    const uint8_t* data() const { return bytes.data(); }
+    bool empty() const { return rows == 0 || cols == 0; }
+};
 
 class Context {
   public:
@@ -132,6 +151,13 @@ class Frame360 {
   public:
     explicit Frame360(Calib360* calib) : calib_(calib) {
         check(r360_frame_create(calib->ctx().get(), calib->get(), &h_), "r360_frame_create");
+        int r, c, sr, sc;
+        check(r360_frame_dims(h_, &r, &c, &sr, &sc), "r360_frame_dims");
+        sphereRGB.rows = sphereDepth.rows = sr;
+        sphereRGB.cols = sphereDepth.cols = sc;
+        sphereRGB.channels = 3; sphereRGB.elem = 1;
+        sphereDepth.channels = 1; sphereDepth.elem = 2;
+        sphereRGB.frame = sphereDepth.frame = this;
     }
     ~Frame360() { r360_frame_destroy(h_); }
     Frame360(const Frame360&) = delete;
@@ -186,6 +212,15 @@ class Frame360 {
         for (const Plane& p : planes) a += p.areaHull;
         return a;
     }
+    // sphereRGB / sphereDepth (Frame360.h:104-107): views of the stitched sphere in HBM
+    Mat sphereRGB, sphereDepth;
+    // copies the sphere's pixels into sphereRGB / sphereDepth (they stay views of this frame)
+    void downloadSphere() {
+        sphereRGB.bytes.resize(size_t(sphereRGB.rows) * sphereRGB.cols * 3);
+        sphereDepth.bytes.resize(size_t(sphereDepth.rows) * sphereDepth.cols * 2);
+        check(r360_frame_get_sphere(h_, sphereRGB.data(), reinterpret_cast<uint16_t*>(sphereDepth.data())),
+              "downloadSphere");
+    }
     std::vector<Plane> planes;          // the frame's PbMap ("planes.vPlanes")
     Matrix4f pose;
     unsigned id = 0;
@@ -233,41 +268,86 @@ class RegisterPhotoICP {
   public:
     enum costFuncType { PHOTO_CONSISTENCY = 0, DEPTH_CONSISTENCY = 1, PHOTO_DEPTH = 2 };
     explicit RegisterPhotoICP(Context& ctx) : ctx_(ctx) { r360_icp_default_params(&p_); }
+    ~RegisterPhotoICP() {
+        for (auto& o : own_) { r360_frame_destroy(o.frame); r360_calib_destroy(o.calib); }
+    }
+    RegisterPhotoICP(const RegisterPhotoICP&) = delete;
+    RegisterPhotoICP& operator=(const RegisterPhotoICP&) = delete;
     void setNumPyr(int n) { p_.n_pyr = n; }
     void setMinDepth(float d) { p_.min_depth = d; }
     void setMaxDepth(float d) { p_.max_depth = d; }
     void setGrayVariance(float s) { p_.std_dev_photo = s; }   // sets stdDevPhoto (RegisterPhotoICP.h:242-245)
     void setDepthVariance(float s) { p_.std_dev_depth = s; }
-    void setSourceFrame(Frame360& f) { ensure_pyramid(f); src_ = &f; }
-    void setTargetFrame(Frame360& f) { ensure_pyramid(f); trg_ = &f; }
+    void useSaliency(bool b) {           // the sphere path never subsamples (the saliency code is commented out)
+        if (b) throw std::invalid_argument("useSaliency(true) is not supported on the spherical path");
+    }
+    void setVisualization(bool) {}      // visualizeIterations: OpenCV windows, no display here
+    void setSourceFrame(Frame360& f) { ensure_pyramid(f); src_ = f.get(); }
+    void setTargetFrame(Frame360& f) { ensure_pyramid(f); trg_ = f.get(); }
+    // setSourceFrame / setTargetFrame(cv::Mat& imgRGB, cv::Mat& imgDepth) (:480-516): a frame's own
+    // sphereRGB / sphereDepth use its device pyramid; other images (BGR u8, range u16 mm) are uploaded
+    void setSourceFrame(Mat& imgRGB, Mat& imgDepth) { src_ = sphere_frame(0, imgRGB, imgDepth); }
+    void setTargetFrame(Mat& imgRGB, Mat& imgDepth) { trg_ = sphere_frame(1, imgRGB, imgDepth); }
     // benchmark timing mode: exactly K level-0 iterations (0 = reference schedule)
     void setFixedIterationsLevel0(int k) { p_.fixed_iters_level0 = k; }
     // returns false where the reference prints "ILL-POSED" and returns early (:4682-4690)
     bool alignFrames360(const Matrix4f& pose_guess = Matrix4f::Identity(), costFuncType method = PHOTO_CONSISTENCY,
                         int occlusion = 0) {
         float g[6];
-        const int rc = check(r360_align360(ctx_.get(), trg_->get(), src_->get(), pose_guess.data(), method, occlusion,
+        const int rc = check(r360_align360(ctx_.get(), trg_, src_, pose_guess.data(), method, occlusion,
                                            &p_, relPose_.data(), hessian_.data(), g, &st_),
                              "alignFrames360");
         std::memcpy(gradient_, g, sizeof g);
         SSO = st_.sso;
+        // the residual members keep their previous value unless the error function assigns them (:183-189)
+        if (st_.residuals_set & 1) { avPhotoResidual = st_.av_photo_residual; avDepthResidual = st_.av_depth_residual; }
+        if (st_.residuals_set & 2) avResidual = st_.av_residual;
         return rc == 0;
     }
     Matrix4f getOptimalPose() const { return relPose_; }
     Matrix6f getHessian() const { return hessian_; }
     const float* getGradient() const { return gradient_; }
     float SSO = 0.f;
+    // public residual members (RegisterPhotoICP.h:183-189; uninitialised in the reference until assigned)
+    float avResidual = std::numeric_limits<float>::quiet_NaN();
+    double avPhotoResidual = std::numeric_limits<double>::quiet_NaN();
+    double avDepthResidual = std::numeric_limits<double>::quiet_NaN();
     const r360_icp_stats& stats() const { return st_; }
     r360_icp_params& params() { return p_; }
   private:
     static void ensure_pyramid(Frame360& f) {
         check(r360_frame_build(f.get(), R360_BUILD_UNDISTORT | R360_BUILD_SPHERE | R360_BUILD_PYRAMID), "pyramid");
     }
+    r360_frame* sphere_frame(int role, Mat& rgb, Mat& depth) {
+        if (rgb.frame && rgb.frame == depth.frame) {       // the frame's own sphere views
+            Frame360& f = const_cast<Frame360&>(*rgb.frame);
+            ensure_pyramid(f);
+            return f.get();
+        }
+        if (rgb.channels != 3 || rgb.elem != 1 || depth.channels != 1 || depth.elem != 2 || rgb.rows != depth.rows ||
+            rgb.cols != depth.cols || rgb.bytes.size() < size_t(rgb.rows) * rgb.cols * 3 ||
+            depth.bytes.size() < size_t(depth.rows) * depth.cols * 2)
+            throw std::invalid_argument("sphere images: BGR u8 x 3 and range u16 of the same size");
+        Own* o = nullptr;
+        for (auto& x : own_)
+            if (x.role == role && x.rows == rgb.rows && x.cols == rgb.cols) o = &x;
+        if (!o) {
+            own_.push_back(Own{role, rgb.rows, rgb.cols, nullptr, nullptr});
+            o = &own_.back();
+            check(r360_calib_create_sphere(ctx_.get(), rgb.rows, rgb.cols, &o->calib), "sphere calibration");
+            check(r360_frame_create(ctx_.get(), o->calib, &o->frame), "sphere frame");
+        }
+        check(r360_frame_set_sphere(o->frame, rgb.data(), reinterpret_cast<const uint16_t*>(depth.data()), rgb.rows,
+                                    rgb.cols), "setSourceFrame / setTargetFrame");
+        return o->frame;
+    }
+    struct Own { int role, rows, cols; r360_calib* calib; r360_frame* frame; };
+    std::vector<Own> own_;
     Context& ctx_;
     r360_icp_params p_;
     r360_icp_stats st_{};
-    Frame360* src_ = nullptr;
-    Frame360* trg_ = nullptr;
+    r360_frame* src_ = nullptr;
+    r360_frame* trg_ = nullptr;
     Matrix4f relPose_;
     Matrix6f hessian_;
     float gradient_[6] = {0, 0, 0, 0, 0, 0};
@@ -277,10 +357,14 @@ class RegisterPhotoICP {
 class RegisterRGBD360 {
   public:
     enum registrationType { DEFAULT_6DoF = 0, PLANAR_3DoF = 1, ODOMETRY_6DoF = 2, PLANAR_ODOMETRY_3DoF = 3 };
-    // the matcher thresholds are those of config_files/configLocaliser_sphericalOdometry.ini
+    // matcher.configLocaliser.load_params(configFile) (:97-100): the [global]/[unary]/[binary] thresholds of
+    // the mrpt-pbmap ini; without a file, configLocaliser_sphericalOdometry.ini's values
     RegisterRGBD360(Context& ctx, const std::string& configFile = "") : ctx_(ctx), config_(configFile) {
         std::memset(informationM_.data(), 0, sizeof(float) * 36);
+        r360_match_params_default(&match_);
+        if (!configFile.empty()) check(r360_match_params_load_ini(configFile.c_str(), &match_), "load_params");
     }
+    r360_match_params& matchParams() { return match_; }
     void setReference(Frame360* ref, size_t max_match_planes = 0) { ref_ = ref; max_ = max_match_planes; done_ = false; }
     void setTarget(Frame360* trg, size_t max_match_planes = 0) { trg_ = trg; max_ = max_match_planes; done_ = false; }
     bool RegisterPbMap(Frame360* frame1 = nullptr, Frame360* frame2 = nullptr, size_t max_match_planes = 0,
@@ -291,6 +375,7 @@ class RegisterRGBD360 {
         done_ = true;
         std::vector<int> pairs(512);
         int n = 0;
+        check(r360_ctx_set_match_params(ctx_.get(), &match_), "matcher thresholds");
         const int rc = check(r360_register_pbmap(ctx_.get(), ref_->get(), trg_->get(), max_, registMode,
                                                  rigidTransf_.data(), informationM_.data(), pairs.data(), 256, &n,
                                                  &areaMatched_, &areaSource, &areaTarget),
@@ -301,6 +386,25 @@ class RegisterRGBD360 {
     }
     Matrix4f getPose() { if (!done_) RegisterPbMap(); return rigidTransf_; }
     Matrix6f& getInfoMat() { if (!done_) RegisterPbMap(); return informationM_; }
+    // covarianceM = informationM.inverse() (:208-215)
+    Matrix6f getCovMat() {
+        if (!done_) RegisterPbMap();
+        return inverse6(informationM_);
+    }
+    // differential entropy of the matched planes' Gaussian, 0.5 (DOF (1 + log 2 pi) + log det cov) (:230-238)
+    float calcEntropy() {
+        const Matrix6f cov = getCovMat();
+        double A[36];
+        for (int i = 0; i < 36; ++i) A[i] = cov.data()[i];
+        return float(0.5 * (6 * (1 + std::log(2 * 3.14159265359)) + std::log(float(det6(A)))));
+    }
+    // tracking quality from the matched-area ratio (:526-540): 0 GOOD (>= 0.7), 1 WEAK (>= 0.3), 2 BAD
+    int trackingScore(float& score) {
+        score = getAreaMatched() / areaSource;
+        if (score >= 0.7) return 0;
+        if (score >= 0.3) return 1;
+        return 2;
+    }
     std::map<unsigned, unsigned> getMatchedPlanes() { if (!done_) RegisterPbMap(); return bestMatch_; }
     float getAreaMatched() { if (!done_) RegisterPbMap(); return areaMatched_; }
     // Register(): PbMap -> rotOffset conjugation -> alignFrames360 -> back (OdometryKeyFrame360.cpp:205-254);
@@ -309,6 +413,7 @@ class RegisterRGBD360 {
                   const Matrix4f& guess = Matrix4f::Identity(), size_t max_match_planes = 25,
                   registrationType registMode = PLANAR_3DoF) {
         r360_icp_stats st;
+        check(r360_ctx_set_match_params(ctx_.get(), &match_), "matcher thresholds");
         const int rc = check(r360_register(ctx_.get(), frame1->get(), frame2->get(), guess.data(), &icp,
                                            max_match_planes, registMode, pose.data(), informationM_.data(), &st),
                              "Register");
@@ -344,6 +449,41 @@ class RegisterRGBD360 {
     Matrix6f informationM_;
     std::map<unsigned, unsigned> bestMatch_;
     float areaMatched_ = 0.f;
+    r360_match_params match_{};
+    // 6x6 inverse / determinant by Gaussian elimination with partial pivoting (double)
+    static double det6(double A[36]) {
+        double d = 1.0;
+        for (int k = 0; k < 6; ++k) {
+            int p = k;
+            for (int r = k + 1; r < 6; ++r) if (std::fabs(A[r * 6 + k]) > std::fabs(A[p * 6 + k])) p = r;
+            if (A[p * 6 + k] == 0) return 0.0;
+            if (p != k) { for (int c = 0; c < 6; ++c) std::swap(A[k * 6 + c], A[p * 6 + c]); d = -d; }
+            d *= A[k * 6 + k];
+            for (int r = k + 1; r < 6; ++r) {
+                const double f = A[r * 6 + k] / A[k * 6 + k];
+                for (int c = k; c < 6; ++c) A[r * 6 + c] -= f * A[k * 6 + c];
+            }
+        }
+        return d;
+    }
+    static Matrix6f inverse6(const Matrix6f& M) {
+        double A[6][12];
+        for (int r = 0; r < 6; ++r)
+            for (int c = 0; c < 12; ++c) A[r][c] = c < 6 ? M(r, c) : (c - 6 == r ? 1.0 : 0.0);
+        for (int k = 0; k < 6; ++k) {
+            int p = k;
+            for (int r = k + 1; r < 6; ++r) if (std::fabs(A[r][k]) > std::fabs(A[p][k])) p = r;
+            for (int c = 0; c < 12; ++c) std::swap(A[k][c], A[p][c]);
+            const double piv = A[k][k];
+            for (int c = 0; c < 12; ++c) A[k][c] /= piv;
+            for (int r = 0; r < 6; ++r)
+                if (r != k) { const double f = A[r][k]; for (int c = 0; c < 12; ++c) A[r][c] -= f * A[k][c]; }
+        }
+        Matrix6f out;
+        for (int r = 0; r < 6; ++r)
+            for (int c = 0; c < 6; ++c) out(r, c) = float(A[r][c + 6]);
+        return out;
+    }
 };
 
 // ------------------------------------------------------------------ batched registrations (§8f-4)
@@ -352,6 +492,8 @@ class RegisterRGBD360 {
 class BatchRegistration {
   public:
     BatchRegistration(int device = 0, int lanes = 8) { check(r360_batch_create(device, lanes, &h_), "r360_batch_create"); }
+    // the matcher thresholds of every lane (e.g. RegisterRGBD360::matchParams() of an ini file)
+    void setMatchParams(const r360_match_params& m) { check(r360_batch_set_match_params(h_, &m), "setMatchParams"); }
     ~BatchRegistration() { r360_batch_destroy(h_); }
     BatchRegistration(const BatchRegistration&) = delete;
     BatchRegistration& operator=(const BatchRegistration&) = delete;

@@ -54,6 +54,10 @@ int  r360_calib_load_extrinsics(r360_calib* c, const char* dir);
 /* loadIntrinsicCalibration(dir): CLAMS dir/distortion_model{1..8} + downsampleParams(2)
  * (Calib360.h:104-119).  Without intrinsics undistort() is the identity. */
 int  r360_calib_load_intrinsics(r360_calib* c, const char* dir);
+/* A calibration without sensors for spheres given as images (setSourceFrame / setTargetFrame(cv::Mat&,
+ * cv::Mat&), RegisterPhotoICP.h:480-516): the ICP tables of an sph_rows x sph_cols sphere
+ * (sph_cols % 8 == 0).  Its frames only take r360_frame_set_sphere. */
+int  r360_calib_create_sphere(r360_ctx* ctx, int sph_rows, int sph_cols, r360_calib** out);
 
 /* ---------------------------------------------------------------- Frame360
  * Replaces include/Frame360.h:93-1150. */
@@ -73,6 +77,10 @@ int  r360_frame_upload(r360_frame* f, const uint8_t* bgr8, const uint16_t* depth
  * the pipelined sequence driver).  The host buffers must stay valid until the stream has consumed
  * them; page-locked buffers (r360_host_register) make the copy asynchronous to the host. */
 int  r360_frame_upload_async(r360_frame* f, const uint8_t* bgr8, const uint16_t* depth8);
+/* setSourceFrame / setTargetFrame(cv::Mat& imgRGB, cv::Mat& imgDepth) (RegisterPhotoICP.h:480-516): the
+ * sphere as images (BGR u8 [sph_rows][sph_cols][3], range u16 mm [sph_rows][sph_cols], as sphereRGB /
+ * sphereDepth) replaces the frame's and its pyramid is rebuilt.  The size must be the frame's. */
+int  r360_frame_set_sphere(r360_frame* f, const uint8_t* bgr, const uint16_t* range_mm, int sph_rows, int sph_cols);
 /* Page-lock / release host memory for asynchronous uploads (hipHostRegister). */
 int  r360_host_register(void* p, size_t bytes);
 int  r360_host_unregister(void* p);
@@ -132,6 +140,17 @@ typedef struct {
     double error;               /* accepted error at level 0                 */
     int    passes;              /* fused residual/Jacobian/JtJ passes run     */
     int    pad;
+    /* The public residual members RegisterPhotoICP leaves after the call (RegisterPhotoICP.h:183-189).
+     * alignFrames360 with occlusion 1 / 2: avPhotoResidual / avDepthResidual of the last error evaluation
+     * (errorPhotoICP_sphereOcc1 :3360-3362, Occ2 :3852-3853); avResidual is set only when ILL-POSED (= 0,
+     * :4688).  alignFrames360 with occlusion 0 assigns none of them (errorPhotoICP_sphere does not).
+     * alignFrames (pinhole): the values copied at the start of the last loop iteration (:4329-4332,
+     * :4507-4509; errorPhotoICP :759-762).  residuals_set: bit 0 = avPhotoResidual / avDepthResidual
+     * assigned, bit 1 = avResidual assigned; unassigned members keep their previous value in the façades. */
+    double av_photo_residual;
+    double av_depth_residual;
+    float  av_residual;
+    int    residuals_set;
 } r360_icp_stats;
 
 void r360_icp_default_params(r360_icp_params* p);
@@ -259,6 +278,32 @@ int r360_frame_load_pbmap_cloud(r360_frame* f, const char* dir, unsigned index);
  * Replaces include/RegisterRGBD360.h:97-337.  registrationType (:260-266). */
 enum { R360_DEFAULT_6DoF = 0, R360_PLANAR_3DoF = 1, R360_ODOMETRY_6DoF = 2, R360_PLANAR_ODOMETRY_3DoF = 3 };
 
+/* SubgraphMatcher thresholds: the [global]/[unary]/[binary] keys of the mrpt-pbmap config file that
+ * RegisterRGBD360(configFile) loads (RegisterRGBD360.h:97-100, config_files/configLocaliser_*.ini).  A ctx
+ * (and each lane of a batch) holds one set; r360_register_pbmap, r360_register* and the batch use it. */
+typedef struct {
+    int   min_planes_recognition;   /* [global]; RegisterPbMap itself requires 3 matches (:306)            */
+    float dist_d;                   /* [unary] plane offset difference (m)                                  */
+    float angle;                    /* [unary] normal angle (deg), odometry modes                           */
+    float color_threshold;          /* [unary] normalised-rgb difference                                    */
+    float intensity_threshold;      /* [unary]                                                              */
+    float elongation_threshold;     /* [unary] ratio                                                        */
+    float area_threshold;           /* [unary] ratio                                                        */
+    float dist_threshold;           /* [binary] centroid-distance ratio                                     */
+    float angle_threshold;          /* [binary] relative-normal-angle difference (deg)                      */
+    float height_threshold;         /* [binary] relative height of parallel planes (m)                      */
+    float cos_angle_parallel;       /* [binary]                                                             */
+    float planar_normal_angle;      /* planar modes: vertical-normal tolerance (deg; not an ini key, 10)    */
+    long  max_nodes;                /* interpretation-tree node budget (deterministic cut-off)              */
+} r360_match_params;
+/* The configLocaliser_sphericalOdometry.ini values (the odometry apps' file). */
+void r360_match_params_default(r360_match_params* m);
+/* Reads an mrpt-pbmap ini file into m (keys absent from the file keep m's values).  Returns 0, <0 if the
+ * file cannot be read. */
+int  r360_match_params_load_ini(const char* path, r360_match_params* m);
+int  r360_ctx_set_match_params(r360_ctx* ctx, const r360_match_params* m);
+int  r360_ctx_get_match_params(const r360_ctx* ctx, r360_match_params* m);
+
 /* RegisterPbMap(ref, trg, max_match_planes, mode) (:276-337): returns 1 (good alignment) or 0
  * (insufficient matching / ill-conditioned; pose and info are then left untouched, :306-310).
  * pose = getPose() (target as seen from the reference), info = getInfoMat(), match_pairs =
@@ -301,6 +346,8 @@ typedef struct r360_batch r360_batch;
 int  r360_batch_create(int device, int lanes, r360_batch** out);
 void r360_batch_destroy(r360_batch* b);
 int  r360_batch_lanes(const r360_batch* b);
+/* The matcher thresholds of every lane (r360_ctx_set_match_params). */
+int  r360_batch_set_match_params(r360_batch* b, const r360_match_params* m);
 
 /* dense stage of one job */
 enum {

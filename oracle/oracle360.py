@@ -38,7 +38,8 @@ class IcpParams(C.Structure):
 
 class IcpStats(C.Structure):
     _fields_ = [("iters", C.c_int * 8), ("evals", C.c_int * 8), ("illposed", C.c_int), ("sso", C.c_float),
-                ("error", C.c_double)]
+                ("error", C.c_double), ("av_photo_residual", C.c_double), ("av_depth_residual", C.c_double),
+                ("av_residual", C.c_float), ("residuals_set", C.c_int)]
 
 
 class DenseStats(C.Structure):
@@ -135,8 +136,8 @@ def lib() -> C.CDLL:
             "orc_pbmap_free": (None, [vp]),
             "orc_pbmap_count": (C.c_int, [vp]),
             "orc_pbmap_get": (C.c_int, [vp, C.c_int, C.POINTER(Plane), fp, C.c_int]),
-            "orc_match_tables": (C.c_int, [vp, vp, C.c_size_t, C.c_int, ip, ip, ip, ip, vp, vp, C.c_int]),
-            "orc_register_pbmap": (C.c_int, [vp, vp, C.c_size_t, C.c_int, fp, fp, ip, C.c_int, ip, fp, fp, fp]),
+            "orc_match_tables": (C.c_int, [vp, vp, C.c_size_t, C.c_int, ip, ip, ip, ip, vp, vp, C.c_int, vp]),
+            "orc_register_pbmap": (C.c_int, [vp, vp, C.c_size_t, C.c_int, fp, fp, ip, C.c_int, ip, fp, fp, fp, vp]),
         }
         for k, (r, a) in sig.items():
             f = getattr(L, k)
@@ -555,7 +556,46 @@ class PbMap:
             self.h = None
 
 
-def match_tables(ref: PbMap, trg: PbMap, max_match_planes=25, mode=PLANAR_3DoF, cap=128):
+class MatchParams(C.Structure):
+    """orc_match_params: SubgraphMatcher thresholds (the mrpt-pbmap ini keys, angles in degrees)."""
+    _fields_ = [("min_planes_recognition", C.c_int), ("dist_d", C.c_float), ("angle", C.c_float),
+                ("color_threshold", C.c_float), ("intensity_threshold", C.c_float),
+                ("elongation_threshold", C.c_float), ("area_threshold", C.c_float), ("dist_threshold", C.c_float),
+                ("angle_threshold", C.c_float), ("height_threshold", C.c_float), ("cos_angle_parallel", C.c_float),
+                ("planar_normal_angle", C.c_float), ("max_nodes", C.c_long)]
+
+    @classmethod
+    def odometry_default(cls) -> "MatchParams":
+        """config_files/configLocaliser_sphericalOdometry.ini"""
+        return cls(3, 0.5, 50.0, 0.07, 100.0, 2.5, 3.0, 3.0, 10.0, 0.33, 0.985, 10.0, 4000000)
+
+
+def load_match_ini(path, base: "MatchParams | None" = None) -> MatchParams:
+    """mrpt-pbmap config_heuristics::load_params: the [global]/[unary]/[binary] keys the matcher uses
+    (INI 'key=value', '//' and '%' comments); keys absent from the file keep base's values."""
+    m = MatchParams.odometry_default() if base is None else base
+    keys = {("global", "min_planes_recognition"): int, ("unary", "dist_d"): float, ("unary", "angle"): float,
+            ("unary", "color_threshold"): float, ("unary", "intensity_threshold"): float,
+            ("unary", "elongation_threshold"): float, ("unary", "area_threshold"): float,
+            ("binary", "dist_threshold"): float, ("binary", "angle_threshold"): float,
+            ("binary", "height_threshold"): float, ("binary", "cos_angle_parallel"): float}
+    sec = ""
+    for raw in open(path):
+        line = raw.split("//")[0].split("%")[0].strip()
+        if not line:
+            continue
+        if line.startswith("["):
+            sec = line[1:line.index("]")].strip()
+            continue
+        if "=" not in line:
+            continue
+        k, v = (x.strip() for x in line.split("=", 1))
+        if (sec, k) in keys:
+            setattr(m, k, keys[(sec, k)](float(v)))
+    return m
+
+
+def match_tables(ref: PbMap, trg: PbMap, max_match_planes=25, mode=PLANAR_3DoF, cap=128, params=None):
     ns, nt = C.c_int(), C.c_int()
     sid = np.zeros(cap, np.int32)
     tid = np.zeros(cap, np.int32)
@@ -564,20 +604,22 @@ def match_tables(ref: PbMap, trg: PbMap, max_match_planes=25, mode=PLANAR_3DoF, 
     bi = np.zeros(cap * cap * words, np.uint64)
     ip = C.POINTER(C.c_int)
     w = lib().orc_match_tables(ref.h, trg.h, max_match_planes, mode, C.byref(ns), C.byref(nt), sid.ctypes.data_as(ip),
-                               tid.ctypes.data_as(ip), _v(un), _v(bi), cap)
+                               tid.ctypes.data_as(ip), _v(un), _v(bi), cap,
+                               C.byref(params) if params is not None else None)
     n, m = ns.value, nt.value
     return dict(sid=sid[:n].copy(), tid=tid[:m].copy(), unary=un[:n * m].reshape(n, m).copy(),
                 binary=bi[:n * m * w].reshape(n * m, w).copy(), words=w)
 
 
-def register_pbmap(ref: PbMap, trg: PbMap, max_match_planes=25, mode=PLANAR_3DoF):
+def register_pbmap(ref: PbMap, trg: PbMap, max_match_planes=25, mode=PLANAR_3DoF, params=None):
     pose = np.zeros(16, np.float32)
     info = np.zeros(36, np.float32)
     pairs = np.zeros(2 * 256, np.int32)
     n, am, as_, at = C.c_int(), C.c_float(), C.c_float(), C.c_float()
     ip = C.POINTER(C.c_int)
     rc = lib().orc_register_pbmap(ref.h, trg.h, max_match_planes, mode, _f(pose), _f(info), pairs.ctypes.data_as(ip),
-                                  256, C.byref(n), C.byref(am), C.byref(as_), C.byref(at))
+                                  256, C.byref(n), C.byref(am), C.byref(as_), C.byref(at),
+                                  C.byref(params) if params is not None else None)
     return dict(good=rc, pose=from16(pose), info=info.reshape(6, 6).T.copy(),
                 matches={int(pairs[2 * k]): int(pairs[2 * k + 1]) for k in range(min(n.value, 256))},
                 area_matched=am.value, area_src=as_.value, area_trg=at.value)

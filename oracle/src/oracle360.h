@@ -50,6 +50,10 @@ typedef struct {
     int    illposed;            /* 1 if the rank test stopped the solve */
     float  sso;                 /* SSO from the last calcHessGrad       */
     double error;               /* last accepted error (level 0)        */
+    /* the residual members left after the call (RegisterPhotoICP.h:183-189), as r360_icp_stats */
+    double av_photo_residual, av_depth_residual;
+    float  av_residual;
+    int    residuals_set;       /* bit 0 photo/depth assigned, bit 1 avResidual assigned */
 } orc_icp_stats;
 
 /* One pyramid level of the spherical frames (RegisterPhotoICP.h:197-198). */
@@ -200,13 +204,21 @@ void* orc_pbmap_build(const float* depth_m8, const uint8_t* bgr8, int rows, int 
 void  orc_pbmap_free(void* h);
 int   orc_pbmap_count(const void* h);
 int   orc_pbmap_get(const void* h, int i, orc_plane* out, float* hull_xyz, int hull_cap);
+/* SubgraphMatcher thresholds: the [global]/[unary]/[binary] keys of config_files/configLocaliser_*.ini
+ * (RegisterRGBD360.h:97-100); angles in degrees.  NULL = configLocaliser_sphericalOdometry.ini. */
+typedef struct {
+    int   min_planes_recognition;
+    float dist_d, angle, color_threshold, intensity_threshold, elongation_threshold, area_threshold;
+    float dist_threshold, angle_threshold, height_threshold, cos_angle_parallel, planar_normal_angle;
+    long  max_nodes;
+} orc_match_params;
 /* A11+A12 tables: subgraph ids, unary [ns][nt] and binary [(i*nt+j)][words] bitsets; returns words. */
 int   orc_match_tables(const void* href, const void* htrg, size_t max_match_planes, int mode, int* ns, int* nt,
-                       int* sid, int* tid, uint8_t* unary, uint64_t* binary, int cap);
+                       int* sid, int* tid, uint8_t* unary, uint64_t* binary, int cap, const orc_match_params* mp);
 /* A11-A13: RegisterRGBD360::RegisterPbMap.  Returns 1 good, 0 insufficient / ill-conditioned. */
 int   orc_register_pbmap(const void* href, const void* htrg, size_t max_match_planes, int mode, float pose[16],
                          float info[36], int* pairs, int pair_cap, int* n_match, float* area_matched,
-                         float* area_src, float* area_trg);
+                         float* area_src, float* area_trg, const orc_match_params* mp);
 
 #ifdef __cplusplus
 }

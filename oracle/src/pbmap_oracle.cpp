@@ -519,6 +519,24 @@ struct MatchCfg {                       // config_files/configLocaliser_spherica
           cos_angle_parallel = 0.985f, planar_normal_tol = 0.17364818f /* sin 10 deg */;
     int min_planes_recognition = 3;
     long max_nodes = 4000000;           // interpretation-tree node budget (deterministic cut-off)
+    MatchCfg() = default;
+    explicit MatchCfg(const orc_match_params* p) {
+        if (!p) return;
+        const double PI = 3.14159265359;        // include/Miscellaneous.h:44
+        dist_d = p->dist_d;
+        cos_angle_unary = (float)std::cos(p->angle * PI / 180);
+        color_threshold = p->color_threshold;
+        intensity_threshold = p->intensity_threshold;
+        elongation_threshold = p->elongation_threshold;
+        area_threshold = p->area_threshold;
+        dist_threshold = p->dist_threshold;
+        cos_angle_binary = (float)std::cos(p->angle_threshold * PI / 180);
+        height_threshold = p->height_threshold;
+        cos_angle_parallel = p->cos_angle_parallel;
+        planar_normal_tol = (float)std::sin(p->planar_normal_angle * PI / 180);
+        min_planes_recognition = p->min_planes_recognition;
+        max_nodes = p->max_nodes;
+    }
 };
 
 enum { DEFAULT_6DoF = 0, PLANAR_3DoF = 1, ODOMETRY_6DoF = 2, PLANAR_ODOMETRY_3DoF = 3 };
@@ -789,10 +807,10 @@ int orc_pbmap_get(const void* h, int i, orc_plane* out, float* hull_xyz, int hul
 }
 
 int orc_match_tables(const void* href, const void* htrg, size_t max_match_planes, int mode, int* ns, int* nt,
-                     int* sid, int* tid, uint8_t* unary, uint64_t* binary, int cap) {
+                     int* sid, int* tid, uint8_t* unary, uint64_t* binary, int cap, const orc_match_params* mp) {
     const auto& S = static_cast<const orc_pbmap_s*>(href)->m.planes;
     const auto& T = static_cast<const orc_pbmap_s*>(htrg)->m.planes;
-    MatchCfg c;
+    MatchCfg c(mp);
     const std::vector<int> si = select_planes(S, max_match_planes), ti = select_planes(T, max_match_planes);
     *ns = int(si.size());
     *nt = int(ti.size());
@@ -807,10 +825,10 @@ int orc_match_tables(const void* href, const void* htrg, size_t max_match_planes
 
 int orc_register_pbmap(const void* href, const void* htrg, size_t max_match_planes, int mode, float pose[16],
                        float info[36], int* pairs, int pair_cap, int* n_match, float* area_matched, float* area_src,
-                       float* area_trg) {
+                       float* area_trg, const orc_match_params* mp) {
     const auto& S = static_cast<const orc_pbmap_s*>(href)->m.planes;
     const auto& T = static_cast<const orc_pbmap_s*>(htrg)->m.planes;
-    MatchCfg c;
+    MatchCfg c(mp);
     const std::vector<int> si = select_planes(S, max_match_planes), ti = select_planes(T, max_match_planes);
     const Tables tb = build_tables(S, si, T, ti, mode, c);
     Search sr;

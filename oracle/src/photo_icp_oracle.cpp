@@ -313,6 +313,8 @@ static void hessgrad_sphere_lut(const orc_level* L, const Lut& lut, const float 
 // deterministic reading.
 // ---------------------------------------------------------------------------
 static const float kThresDepthOutliers = 0.3f;   // alignFrames360 :4525
+// the members errorPhotoICP_sphereOcc1/2 assign (avPhotoResidual / avDepthResidual, :3360-3362, :3852-3853)
+static thread_local double g_avPhoto = 0.0, g_avDepth = 0.0;
 
 // errorPhotoICP_sphereOcc1 (:3232-3370): Z-buffer on the TARGET pixel; an accepted point overwrites
 // the pixel's residual, every accepted point counts.  Returns avPhotoResidual + avDepthResidual.
@@ -358,7 +360,9 @@ static double error_sphere_occ1(const orc_level* L, const Lut& lut, const float 
     double PR = 0.0, DR = 0.0;
     for (long i = 0; i < N; ++i) { PR += resP[i]; DR += resD[i]; }
     *n_valid = (int)(nP + nD);
-    return std::sqrt(PR / nP) + std::sqrt(DR / nD);
+    g_avPhoto = std::sqrt(PR / nP);
+    g_avDepth = std::sqrt(DR / nD);
+    return g_avPhoto + g_avDepth;
 }
 
 // errorPhotoICP_sphereOcc2 (:3720-3855): depth-outlier filter, then the target Z-buffer; residuals are
@@ -405,7 +409,9 @@ static double error_sphere_occ2(const orc_level* L, const Lut& lut, const float 
     double PR = 0.0, DR = 0.0;
     for (long i = 0; i < N; ++i) { PR += resP[i]; DR += resD[i]; }
     *n_valid = (int)nV;
-    return std::sqrt(PR / nV) + std::sqrt(DR / nV);
+    g_avPhoto = std::sqrt(PR / nV);
+    g_avDepth = std::sqrt(DR / nV);
+    return g_avPhoto + g_avDepth;
 }
 
 // calcHessGrad_sphereOcc2 (:3861-4250): depth-outlier filter; the LAST filtered point of each target
@@ -638,7 +644,11 @@ extern "C" int orc_align360_occ(const uint8_t* trg_bgr, const uint16_t* trg_dept
         double lambda = p->lambda;                                        // :4589
         const int maxIters = fixed ? p->fixed_iters_level0 : p->max_iters;
         float upd[6] = {1, 1, 1, 1, 1, 1};
+        auto note_residuals = [&]() {
+            if (st && occlusion) { st->av_photo_residual = g_avPhoto; st->av_depth_residual = g_avDepth; st->residuals_set |= 1; }
+        };
         double error = error_any(&L, lut, pose, method, occlusion, p, &nv);
+        note_residuals();
         double diff_error = error;
         int loops = 0;
         auto norm6 = [](const float* u) { float s = 0; for (int k = 0; k < 6; ++k) s += u[k] * u[k]; return std::sqrt(s); };
@@ -659,7 +669,7 @@ extern "C" int orc_align360_occ(const uint8_t* trg_bgr, const uint16_t* trg_dept
             for (int k = 0; k < 6; ++k) HL[k * 7] = (float)(Hf[k * 7] + (float)lambda * Hf[k * 7]);
             if (rank6(HL) != 6) {                                       // :4682-4690
                 memcpy(pose_out, pose, sizeof(float) * 16);
-                if (st) st->illposed = 1;
+                if (st) { st->illposed = 1; st->av_residual = 0.f; st->residuals_set |= 2; }   // avResidual = 0
                 ret = 1;
                 goto done;
             }
@@ -671,6 +681,7 @@ extern "C" int orc_align360_occ(const uint8_t* trg_bgr, const uint16_t* trg_dept
             orc_exp_se3(ud, 1, E);                                        // :4697
             matmul4f(E, pose, cand);
             double new_error = error_any(&L, lut, cand, method, occlusion, p, &nv);
+            note_residuals();
             ++evals;
             diff_error = error - new_error;                               // :4711
             if (diff_error > p->tol_residual) {                           // :4715-4722

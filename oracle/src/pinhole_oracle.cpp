@@ -266,6 +266,9 @@ extern "C" int orc_align_pinhole(const uint8_t* trg_bgr, const uint16_t* trg_dep
         matmul4f(E, pose, cand);
     };
     int ret = 0;
+    double av[2] = {0, 0}, av_t[2] = {0, 0};
+    float av_res = 0.f, av_res_t = 0.f;
+    bool have_t = false;
     const bool trace = getenv("R360_ORACLE_TRACE") != nullptr;   // debugging aid: LM trace on stderr
     for (int l = nL - 1; l >= 0; --l) {
         orc_level L = {R[l], C[l], gs[l].data(), ds[l].data(), gt[l].data(), dt[l].data(),
@@ -276,9 +279,20 @@ extern "C" int orc_align_pinhole(const uint8_t* trg_bgr, const uint16_t* trg_dep
         double lambda = 0.01;
         int it = 0, evals = 0;
         float upd[6] = {1, 1, 1, 1, 1, 1};
-        double error = error_pin(&L, lut, I, pose, method, p, nullptr, nullptr, nullptr, nullptr);
+        // the members errorPhotoICP assigns (:759-762) and alignFrames' copies of them (:4329-4332)
+        auto eval = [&](const float* P) {
+            int nP = 0, nD = 0;
+            double rp = 0, rd = 0;
+            const double e = error_pin(&L, lut, I, P, method, p, &nP, &nD, &rp, &rd);
+            av[0] = std::sqrt(rp / nD);
+            av[1] = std::sqrt(rd / nD);
+            av_res = (float)(av[0] + av[1]);
+            return e;
+        };
+        double error = eval(pose);
         double diff_error = error;
         while (it < maxIters && norm6(upd) > tol_update && diff_error > tol_residual) {   // :4324
+            av_t[0] = av[0]; av_t[1] = av[1]; av_res_t = av_res; have_t = true;
             double H[36], g[6];
             hessgrad_pin(&L, lut, I, pose, method, p, H, g, nullptr);
             for (int k = 0; k < 36; ++k) Hf[k] = (float)H[k];
@@ -288,14 +302,18 @@ extern "C" int orc_align_pinhole(const uint8_t* trg_bgr, const uint16_t* trg_dep
             for (int k = 0; k < 6; ++k) HL[k * 7] = (float)(Hf[k * 7] + (float)lambda * Hf[k * 7]);
             if (rank6(HL) != 6) {                                                          // :4345-4353
                 memcpy(pose_out, pose, sizeof(pose));
-                if (st) { st->illposed = 1; st->iters[l] = it; st->evals[l] = evals; }
+                if (st) {
+                    st->illposed = 1; st->iters[l] = it; st->evals[l] = evals;
+                    st->av_photo_residual = av[0]; st->av_depth_residual = av[1]; st->av_residual = av_res;
+                    st->residuals_set = 3;
+                }
                 ret = 1;
                 goto done;
             }
             solve(0.f, upd);                                                               // :4355
             float cand[16];
             candidate(upd, cand);                                                          // :4358
-            double new_error = error_pin(&L, lut, I, cand, method, p, nullptr, nullptr, nullptr, nullptr);
+            double new_error = eval(cand);
             ++evals;
             diff_error = error - new_error;
             if (trace) fprintf(stderr, "L%d it%d err %.17g new %.17g diff %.3e lam %g |upd| %.3e\n", l, it, error, new_error, diff_error, lambda, (double)norm6(upd));
@@ -308,7 +326,7 @@ extern "C" int orc_align_pinhole(const uint8_t* trg_bgr, const uint16_t* trg_dep
                 lambda = lambda * step;
                 solve((float)lambda, upd);
                 candidate(upd, cand);
-                new_error = error_pin(&L, lut, I, cand, method, p, nullptr, nullptr, nullptr, nullptr);
+                new_error = eval(cand);
                 ++evals;
                 diff_error = error - new_error;
                 if (diff_error > 0) {
@@ -321,6 +339,10 @@ extern "C" int orc_align_pinhole(const uint8_t* trg_bgr, const uint16_t* trg_dep
         if (st) { st->iters[l] = it; st->evals[l] = evals; st->error = error; }
     }
     memcpy(pose_out, pose, sizeof(pose));
+    if (st && have_t) {                                  // :4507-4509
+        st->av_photo_residual = av_t[0]; st->av_depth_residual = av_t[1]; st->av_residual = av_res_t;
+        st->residuals_set = 3;
+    }
 done:
     if (H_out) memcpy(H_out, Hf, sizeof(Hf));
     if (g_out) memcpy(g_out, gf, sizeof(gf));

@@ -55,10 +55,35 @@ class IcpParams(C.Structure):
         return p
 
 
+class MatchParams(C.Structure):
+    """r360_match_params — SubgraphMatcher thresholds, the keys of config_files/configLocaliser_*.ini that
+    RegisterRGBD360(configFile) loads (RegisterRGBD360.h:97-100); angles in degrees."""
+    _fields_ = [("min_planes_recognition", C.c_int), ("dist_d", C.c_float), ("angle", C.c_float),
+                ("color_threshold", C.c_float), ("intensity_threshold", C.c_float),
+                ("elongation_threshold", C.c_float), ("area_threshold", C.c_float), ("dist_threshold", C.c_float),
+                ("angle_threshold", C.c_float), ("height_threshold", C.c_float), ("cos_angle_parallel", C.c_float),
+                ("planar_normal_angle", C.c_float), ("max_nodes", C.c_long)]
+
+    @classmethod
+    def default(cls) -> "MatchParams":
+        """configLocaliser_sphericalOdometry.ini (the odometry apps' file)."""
+        m = cls()
+        lib().r360_match_params_default(C.byref(m))
+        return m
+
+    @classmethod
+    def load_ini(cls, path: str, base: "MatchParams | None" = None) -> "MatchParams":
+        m = cls.default() if base is None else base
+        _check(lib().r360_match_params_load_ini(path.encode(), C.byref(m)), "match_params_load_ini")
+        return m
+
+
 class IcpStats(C.Structure):
     _fields_ = [
         ("iters", C.c_int * 8), ("evals", C.c_int * 8), ("illposed", C.c_int), ("sso", C.c_float),
         ("error", C.c_double), ("passes", C.c_int), ("pad", C.c_int),
+        ("av_photo_residual", C.c_double), ("av_depth_residual", C.c_double), ("av_residual", C.c_float),
+        ("residuals_set", C.c_int),
     ]
 
 
@@ -135,6 +160,8 @@ _SIGS = [
     ("r360_frame_upload", C.c_int, [_P, _P, _P]),
     ("r360_frame_upload_device", C.c_int, [_P, _P, _P]),
     ("r360_frame_upload_async", C.c_int, [_P, _P, _P]),
+    ("r360_frame_set_sphere", C.c_int, [_P, _P, _P, C.c_int, C.c_int]),
+    ("r360_calib_create_sphere", C.c_int, [_P, C.c_int, C.c_int, C.POINTER(_P)]),
     ("r360_host_register", C.c_int, [_P, C.c_size_t]),
     ("r360_host_unregister", C.c_int, [_P]),
     ("r360_frame_load_bin", C.c_int, [_P, C.c_char_p]),
@@ -182,6 +209,11 @@ _SIGS = [
                                         _IP]),
     ("r360_frame_get_planes", C.c_int, [_P, C.POINTER(Plane), C.c_int, _IP]),
     ("r360_frame_get_plane_hull", C.c_int, [_P, C.c_int, _FP, C.c_int, _IP]),
+    ("r360_match_params_default", None, [C.POINTER(MatchParams)]),
+    ("r360_match_params_load_ini", C.c_int, [C.c_char_p, C.POINTER(MatchParams)]),
+    ("r360_ctx_set_match_params", C.c_int, [_P, C.POINTER(MatchParams)]),
+    ("r360_ctx_get_match_params", C.c_int, [_P, C.POINTER(MatchParams)]),
+    ("r360_batch_set_match_params", C.c_int, [_P, C.POINTER(MatchParams)]),
     ("r360_register_pbmap", C.c_int, [_P, _P, _P, C.c_size_t, C.c_int, _FP, _FP, _IP, C.c_int, _IP, _FP, _FP, _FP]),
     ("r360_register", C.c_int, [_P, _P, _P, _FP, C.POINTER(IcpParams), C.c_size_t, C.c_int, _FP, _FP,
                                 C.POINTER(IcpStats)]),
@@ -335,10 +367,20 @@ class Context:
 class Calib360:
     """Calib360 (include/Calib360.h:44-132): Rt_[8], Rt_inv[8], cameraMatrix, CLAMS models."""
 
-    def __init__(self, ctx: Context, rows: int = 240, cols: int = 320):
+    def __init__(self, ctx: Context, rows: int = 240, cols: int = 320, _sphere: tuple | None = None):
         h = C.c_void_p()
-        _check(lib().r360_calib_create(ctx.h, rows, cols, C.byref(h)), "r360_calib_create")
+        if _sphere is None:
+            _check(lib().r360_calib_create(ctx.h, rows, cols, C.byref(h)), "r360_calib_create")
+        else:
+            _check(lib().r360_calib_create_sphere(ctx.h, _sphere[0], _sphere[1], C.byref(h)), "r360_calib_create_sphere")
+            rows = cols = 0
         self.h, self.ctx, self.rows, self.cols = h, ctx, rows, cols
+
+    @classmethod
+    def for_sphere(cls, ctx: Context, sph_rows: int, sph_cols: int) -> "Calib360":
+        """A calibration without sensors for spheres given as images (setSourceFrame / setTargetFrame(cv::Mat&,
+        cv::Mat&), RegisterPhotoICP.h:480-516)."""
+        return cls(ctx, _sphere=(sph_rows, sph_cols))
 
     def loadExtrinsicCalibration(self, path: str):
         _check(lib().r360_calib_load_extrinsics(self.h, path.encode()), "loadExtrinsicCalibration")
@@ -455,6 +497,15 @@ class Frame360:
         depth8 = np.ascontiguousarray(depth8, np.uint16)
         assert bgr8.shape == (8, self.rows, self.cols, 3) and depth8.shape == (8, self.rows, self.cols)
         _check(lib().r360_frame_upload(self.h, _vptr(bgr8), _vptr(depth8)), "upload")
+
+    def set_sphere(self, bgr: np.ndarray, range_mm: np.ndarray):
+        """The sphere as images (BGR u8 [H, W, 3], range u16 mm [H, W]; sphereRGB / sphereDepth) replaces the
+        frame's; its ICP pyramid is rebuilt (setSourceFrame / setTargetFrame(cv::Mat&, cv::Mat&))."""
+        bgr = np.ascontiguousarray(bgr, np.uint8)
+        range_mm = np.ascontiguousarray(range_mm, np.uint16)
+        H, W = range_mm.shape
+        assert bgr.shape == (H, W, 3)
+        _check(lib().r360_frame_set_sphere(self.h, _vptr(bgr), _vptr(range_mm), H, W), "set_sphere")
 
     def upload_async(self, bgr8: np.ndarray, depth8: np.ndarray):
         """Enqueue the upload on the frame's stream; the arrays must stay alive (and should be page-locked,
@@ -580,9 +631,11 @@ class RegisterRGBD360:
     """RegisterRGBD360 (include/RegisterRGBD360.h:47-340): PbMap registration of two Frame360."""
 
     def __init__(self, ctx: "Context", config_file: str | None = None):
-        # the matcher thresholds are those of config_files/configLocaliser_sphericalOdometry.ini
+        # RegisterRGBD360(configFile): matcher.configLocaliser.load_params(configFile) (:97-100); without a
+        # file, the configLocaliser_sphericalOdometry.ini values
         self.ctx = ctx
         self.config_file = config_file
+        self.match = MatchParams.load_ini(config_file) if config_file else MatchParams.default()
         self.rigidTransf = np.eye(4, dtype=np.float32)
         self.informationM = np.zeros((6, 6), np.float32)
         self.bestMatch: dict[int, int] = {}
@@ -606,6 +659,7 @@ class RegisterRGBD360:
         pairs = np.zeros(512, np.int32)
         n = C.c_int()
         am, as_, at = C.c_float(), C.c_float(self.areaSource), C.c_float(self.areaTarget)
+        _check(lib().r360_ctx_set_match_params(self.ctx.h, C.byref(self.match)), "set_match_params")
         rc = _check(lib().r360_register_pbmap(self.ctx.h, self.ref.h, self.trg.h, self.max_match_planes, registMode,
                                               _fptr(pose), _fptr(info), pairs.ctypes.data_as(_IP), 256, C.byref(n),
                                               C.byref(am), C.byref(as_), C.byref(at)), "RegisterPbMap")
@@ -649,7 +703,22 @@ class RegisterRGBD360:
 
     def getPose(self): return self.rigidTransf
     def getInfoMat(self): return self.informationM
-    def getCovMat(self): return np.linalg.inv(self.informationM.astype(np.float64)).astype(np.float32)
+    def getCovMat(self):
+        """covarianceM = informationM.inverse() (:208-215)."""
+        return np.linalg.inv(self.informationM.astype(np.float64)).astype(np.float32)
+
+    def calcEntropy(self) -> float:
+        """0.5 (DOF (1 + log 2 pi) + log det(covariance)) (:230-238), DOF = 6, PI = 3.14159265359."""
+        det = np.float32(np.linalg.det(self.getCovMat().astype(np.float64)))
+        return float(np.float32(0.5 * (6 * (1 + np.log(2 * 3.14159265359)) + np.log(det))))
+
+    def trackingScore(self):
+        """(quality, score) of trackingScore(float& score) (:526-540): score = areaMatched / areaSource;
+        0 GOOD (>= 0.7), 1 WEAK (>= 0.3), 2 BAD."""
+        score = float(np.float32(np.float32(self.getAreaMatched()) / np.float32(self.areaSource))) \
+            if self.areaSource else float("nan")
+        return (0 if score >= 0.7 else 1 if score >= 0.3 else 2), score
+
     def getMatchedPlanes(self): return dict(self.bestMatch)
     def getAreaMatched(self): return self.areaMatched
 
@@ -660,6 +729,7 @@ class RegisterRGBD360:
         un = np.zeros(cap * cap, np.uint8)
         words = (cap * cap + 63) // 64
         bi = np.zeros(cap * cap * words, np.uint64)
+        _check(lib().r360_ctx_set_match_params(self.ctx.h, C.byref(self.match)), "set_match_params")
         w = _check(lib().r360_pbmap_match_tables(self.ctx.h, self.ref.h, self.trg.h, self.max_match_planes, mode,
                                                  C.byref(ns), C.byref(nt), sid.ctypes.data_as(_IP),
                                                  tid.ctypes.data_as(_IP), _vptr(un), _vptr(bi), cap), "match_tables")
@@ -756,6 +826,23 @@ class RegisterPhotoICP:
         self.hessian = np.zeros((6, 6), np.float32)
         self.gradient = np.zeros(6, np.float32)
         self.stats = IcpStats()
+        # public members (:180-192); the reference leaves the residuals uninitialised until an error function
+        # that assigns them runs (NaN here)
+        self.avResidual = self.avPhotoResidual = self.avDepthResidual = float("nan")
+        self.SSO = 0.0
+        self._own = {}         # sphere-only frames for spheres given as images, per (role, size)
+
+    def _residuals(self):
+        if self.stats.residuals_set & 1:
+            self.avPhotoResidual = self.stats.av_photo_residual
+            self.avDepthResidual = self.stats.av_depth_residual
+        if self.stats.residuals_set & 2:
+            self.avResidual = self.stats.av_residual
+        self.SSO = self.stats.sso
+
+    def setVisualization(self, b: bool):
+        """visualizeIterations (OpenCV windows): no display here."""
+        self.visualize = bool(b)
 
     # setters (:224-269)
     def setNumPyr(self, n: int): self.params.n_pyr = n
@@ -768,8 +855,24 @@ class RegisterPhotoICP:
         if b:
             raise NotImplementedError("saliency subsampling is commented out in the reference's sphere path")
 
-    def setSourceFrame(self, f: Frame360): self.src = f
-    def setTargetFrame(self, f: Frame360): self.trg = f
+    def _sphere_frame(self, role: str, bgr, range_mm) -> Frame360:
+        H, W = np.asarray(range_mm).shape
+        key = (role, H, W)
+        if key not in self._own:
+            cal = Calib360.for_sphere(self.ctx, H, W)
+            self._own[key] = (cal, Frame360(cal))
+        f = self._own[key][1]
+        f.set_sphere(bgr, range_mm)
+        return f
+
+    def setSourceFrame(self, f, imgDepth=None):
+        """setSourceFrame(Frame360) — the frame's sphere and pyramid in HBM — or setSourceFrame(imgRGB,
+        imgDepth) with the sphere as images (BGR u8 [H, W, 3], range u16 mm [H, W]; :496-516)."""
+        self.src = f if imgDepth is None else self._sphere_frame("src", f, imgDepth)
+
+    def setTargetFrame(self, f, imgDepth=None):
+        """setTargetFrame(Frame360) or setTargetFrame(imgRGB, imgDepth) (:480-494)."""
+        self.trg = f if imgDepth is None else self._sphere_frame("trg", f, imgDepth)
 
     def alignFrames360(self, pose_guess=None, method: int = PHOTO_CONSISTENCY, occlusion: int = 0) -> int:
         init = _mat16(np.eye(4) if pose_guess is None else pose_guess)
@@ -777,6 +880,7 @@ class RegisterPhotoICP:
         rc = _check(lib().r360_align360(self.ctx.h, self.trg.h, self.src.h, _fptr(init), method, occlusion,
                                         C.byref(self.params), _fptr(po), _fptr(Ho), _fptr(go),
                                         C.byref(self.stats)), "alignFrames360")
+        self._residuals()
         self.relPose = _from16(po)
         self.hessian = Ho.reshape(6, 6).T.copy()
         self.gradient = go.copy()
@@ -813,6 +917,7 @@ class RegisterPhotoICP:
         rc = _check(lib().r360_align_pinhole(self.ctx.h, self.trg.h, self.src.h, self.src_sensor, _fptr(init), method,
                                              self._K(), C.byref(self.params), _fptr(po), _fptr(Ho), _fptr(go),
                                              C.byref(self.stats)), "alignFrames")
+        self._residuals()
         self.relPose = _from16(po)
         self.hessian = Ho.reshape(6, 6).T.copy()
         self.gradient = go.copy()

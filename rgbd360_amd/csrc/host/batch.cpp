@@ -104,6 +104,14 @@ extern "C" void r360_batch_destroy(r360_batch* b) {
 
 extern "C" int r360_batch_lanes(const r360_batch* b) { return b ? int(b->lane.size()) : 0; }
 
+extern "C" int r360_batch_set_match_params(r360_batch* b, const r360_match_params* m) {
+    CHECK_ARG(b && m, "null arg");
+    std::lock_guard<std::recursive_mutex> serial(b->call);
+    for (auto c : b->lane)
+        if (int rc = r360_ctx_set_match_params(c, m)) return rc;
+    return 0;
+}
+
 namespace {
 
 void identity16(float* m) {

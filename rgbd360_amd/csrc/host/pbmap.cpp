@@ -840,6 +840,7 @@ extern "C" int r360_register_pbmap(r360_ctx* ctx, r360_frame* ref, r360_frame* t
     if (gpu_tables(ctx, S, si, T, ti, mode, tb)) return -1;
     Tree tr;
     tr.tb = &tb;
+    tr.budget = ctx->match.max_nodes;
     tr.area.resize(si.size());
     tr.rest.assign(si.size() + 1, 0.0);
     for (size_t i = 0; i < si.size(); ++i) tr.area[i] = S[si[i]].area;
@@ -870,6 +871,75 @@ extern "C" int r360_register_pbmap(r360_ctx* ctx, r360_frame* ref, r360_frame* t
     if (area_src) *area_src = as;
     if (area_trg) *area_trg = at;
     return 1;
+}
+
+// ------------------------------------------------------------------ matcher configuration
+extern "C" void r360_match_params_default(r360_match_params* m) {
+    if (!m) return;
+    // config_files/configLocaliser_sphericalOdometry.ini ([global], [unary], [binary])
+    m->min_planes_recognition = 3;
+    m->dist_d = 0.5f; m->angle = 50.f; m->color_threshold = 0.07f; m->intensity_threshold = 100.f;
+    m->elongation_threshold = 2.5f; m->area_threshold = 3.0f;
+    m->dist_threshold = 3.0f; m->angle_threshold = 10.f; m->height_threshold = 0.33f; m->cos_angle_parallel = 0.985f;
+    m->planar_normal_angle = 10.f;
+    m->max_nodes = 4000000;
+}
+
+// mrpt-pbmap's config_heuristics::load_params reads the keys of [global], [unary] and [binary] with
+// CConfigFile (INI: "key=value", '//' and '%' comments; keys absent from the file keep their defaults)
+extern "C" int r360_match_params_load_ini(const char* path, r360_match_params* m) {
+    CHECK_ARG(path && m, "null arg");
+    FILE* fp = fopen(path, "r");
+    if (!fp) { r360_set_error("cannot open %s", path); return -1; }
+    char line[1024];
+    std::string section;
+    while (fgets(line, sizeof line, fp)) {
+        std::string l(line);
+        const size_t cpos = l.find("//");
+        if (cpos != std::string::npos) l.erase(cpos);
+        const size_t pct = l.find('%');
+        if (pct != std::string::npos) l.erase(pct);
+        auto trim = [](std::string x) {
+            const size_t a = x.find_first_not_of(" \t\r\n"), b = x.find_last_not_of(" \t\r\n");
+            return a == std::string::npos ? std::string() : x.substr(a, b - a + 1);
+        };
+        l = trim(l);
+        if (l.empty()) continue;
+        if (l[0] == '[') { section = trim(l.substr(1, l.find(']') - 1)); continue; }
+        const size_t eq = l.find('=');
+        if (eq == std::string::npos) continue;
+        const std::string k = trim(l.substr(0, eq)), v = trim(l.substr(eq + 1));
+        const double x = atof(v.c_str());
+        if (section == "global" && k == "min_planes_recognition") m->min_planes_recognition = (int)x;
+        else if (section == "unary") {
+            if (k == "dist_d") m->dist_d = (float)x;
+            else if (k == "angle") m->angle = (float)x;
+            else if (k == "color_threshold") m->color_threshold = (float)x;
+            else if (k == "intensity_threshold") m->intensity_threshold = (float)x;
+            else if (k == "elongation_threshold") m->elongation_threshold = (float)x;
+            else if (k == "area_threshold") m->area_threshold = (float)x;
+        } else if (section == "binary") {
+            if (k == "dist_threshold") m->dist_threshold = (float)x;
+            else if (k == "angle_threshold") m->angle_threshold = (float)x;
+            else if (k == "height_threshold") m->height_threshold = (float)x;
+            else if (k == "cos_angle_parallel") m->cos_angle_parallel = (float)x;
+        }
+    }
+    fclose(fp);
+    return 0;
+}
+
+extern "C" int r360_ctx_set_match_params(r360_ctx* ctx, const r360_match_params* m) {
+    CHECK_ARG(ctx && m, "null arg");
+    CHECK_ARG(m->max_nodes > 0, "max_nodes must be positive");
+    ctx->match = *m;
+    return 0;
+}
+
+extern "C" int r360_ctx_get_match_params(const r360_ctx* ctx, r360_match_params* m) {
+    CHECK_ARG(ctx && m, "null arg");
+    *m = ctx->match;
+    return 0;
 }
 
 // Register(): PbMap registration, then the dense refinement initialised with the rotOffset-conjugated

@@ -113,6 +113,13 @@ extern "C" int r360_align_pinhole_result(r360_ctx* ctx, float* poses, float* H, 
             s.illposed = h[j].illposed;
             s.error = h[j].error;
             s.passes = h[j].passes;
+            // alignFrames restores the copies of the last loop iteration's start (:4507-4509); an ILL-POSED
+            // return skips that, leaving the last evaluation's values (equal to those copies)
+            const bool t = (h[j].av_set & 12) != 0;
+            s.av_photo_residual = (t && !h[j].illposed) ? h[j].av_photo_t : h[j].av_photo;
+            s.av_depth_residual = (t && !h[j].illposed) ? h[j].av_depth_t : h[j].av_depth;
+            s.av_residual = (t && !h[j].illposed) ? h[j].av_res_t : h[j].av_res;
+            s.residuals_set = (t || h[j].illposed) ? 3 : 0;
         }
         ill += h[j].illposed;
     }

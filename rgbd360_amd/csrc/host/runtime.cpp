@@ -114,6 +114,7 @@ extern "C" int r360_ctx_create(int device, r360_ctx** out) {
     R360_HIP(hipMemset(c->d_ktime, 0, sizeof(unsigned long long) * 17));
     R360_HIP(hipMemset(c->d_ktime, 0xff, sizeof(unsigned long long)));
     R360_HIP(hipHostMalloc(&c->h_state, sizeof(IcpState), hipHostMallocDefault));
+    r360_match_params_default(&c->match);
     *out = c;
     return 0;
 }
@@ -196,10 +197,14 @@ static int upload_floats(float** dptr, const std::vector<float>& h) {
 
 // Trigonometric tables with the reference's exact float expressions:
 //   stitchImage (Frame360.h:1104-1129) and the alignFrames360 LUT (RegisterPhotoICP.h:4555-4569).
-static int calib_build_tables(r360_calib* c) {
-    const int W = c->rows * 8;
-    const int H = (int)(W * 0.5 * 60.0 / 180);
+// sph_rows / sph_cols: the sphere size; 0 = the one stitchSphericalImage produces from the sensors
+// (width 8 * rows, height width / 6, Frame360.h:391-392)
+static int calib_build_tables(r360_calib* c, int sph_rows = 0, int sph_cols = 0) {
+    const int W = sph_cols ? sph_cols : c->rows * 8;
+    const int H = sph_rows ? sph_rows : (int)(W * 0.5 * 60.0 / 180);
     c->sph_rows = H; c->sph_cols = W;
+    if (c->rows == 0) goto levels;   // sphere-only calibration: no stitch tables
+    {
     const float offsetPhi = H / 2 - 0.5;
     const float offsetTheta = -c->rows * 15 / 2 + 0.5;
     const float angle_pixel = 2 * R360_PI / W;
@@ -209,6 +214,8 @@ static int calib_build_tables(r360_calib* c) {
     if (upload_floats(&c->d_st_sinphi, sp) || upload_floats(&c->d_st_cosphi, cp) ||
         upload_floats(&c->d_st_sinth, st) || upload_floats(&c->d_st_costh, ct))
         return -1;
+    }
+levels:
     // pyramid levels of the sphere
     int R = H, C = W, nl = 0;
     for (; nl < R360_MAX_PYR; ++nl) {
@@ -248,6 +255,21 @@ extern "C" int r360_calib_create(r360_ctx* ctx, int rows, int cols, r360_calib**
     R360_HIP(hipMalloc(&c->d_rt, sizeof(float) * 128));
     R360_HIP(hipMemcpy(c->d_rt, c->rt, sizeof(float) * 128, hipMemcpyHostToDevice));
     if (calib_build_tables(c)) { delete c; return -1; }
+    *out = c;
+    return 0;
+}
+
+// A calibration for spheres given as images (RegisterPhotoICP::setSourceFrame / setTargetFrame(cv::Mat&,
+// cv::Mat&), :480-516): no sensors, only the ICP tables of an sph_rows x sph_cols sphere.
+extern "C" int r360_calib_create_sphere(r360_ctx* ctx, int sph_rows, int sph_cols, r360_calib** out) {
+    CHECK_ARG(ctx && out, "null arg");
+    CHECK_ARG(sph_rows >= 2 && sph_cols >= 8 && sph_cols % 8 == 0, "sphere size: rows >= 2, cols a multiple of 8");
+    R360_HIP(hipSetDevice(ctx->device));
+    r360_calib* c = new r360_calib;
+    c->ctx = ctx; c->rows = 0; c->cols = 0;
+    for (int k = 0; k < 8; ++k)
+        for (int i = 0; i < 16; ++i) c->rt[k][i] = c->rt_inv[k][i] = (i % 5 == 0) ? 1.f : 0.f;
+    if (calib_build_tables(c, sph_rows, sph_cols)) { delete c; return -1; }
     *out = c;
     return 0;
 }
@@ -374,9 +396,11 @@ extern "C" int r360_frame_create(r360_ctx* ctx, const r360_calib* calib, r360_fr
     f->sph_rows = calib->sph_rows; f->sph_cols = calib->sph_cols;
     f->n_levels = calib->n_levels;
     const size_t ns = (size_t)8 * f->rows * f->cols, nsph = (size_t)f->sph_rows * f->sph_cols;
-    R360_HIP(hipMalloc(&f->d_bgr, ns * 3));
-    R360_HIP(hipMalloc(&f->d_depth, ns * 2));
-    R360_HIP(hipMalloc(&f->d_depth_m, ns * 4));
+    if (ns) {                        // a sphere-only frame (r360_calib_create_sphere) has no sensor images
+        R360_HIP(hipMalloc(&f->d_bgr, ns * 3));
+        R360_HIP(hipMalloc(&f->d_depth, ns * 2));
+        R360_HIP(hipMalloc(&f->d_depth_m, ns * 4));
+    }
     R360_HIP(hipMalloc(&f->d_sph_bgr, nsph * 3));
     R360_HIP(hipMalloc(&f->d_sph_depth, nsph * 2));
     int R = f->sph_rows, C = f->sph_cols;
@@ -417,6 +441,7 @@ extern "C" void r360_frame_destroy(r360_frame* f) {
 
 extern "C" int r360_frame_upload(r360_frame* f, const uint8_t* bgr8, const uint16_t* depth8) {
     CHECK_ARG(f && bgr8 && depth8, "null arg");
+    CHECK_ARG(f->rows > 0, "a sphere-only frame has no sensor images");
     const size_t ns = (size_t)8 * f->rows * f->cols;
     R360_HIP(hipMemcpyAsync(f->d_bgr, bgr8, ns * 3, hipMemcpyHostToDevice, f->ctx->stream));
     R360_HIP(hipMemcpyAsync(f->d_depth, depth8, ns * 2, hipMemcpyHostToDevice, f->ctx->stream));
@@ -429,6 +454,7 @@ extern "C" int r360_frame_upload(r360_frame* f, const uint8_t* bgr8, const uint1
 // (page-locked buffers, r360_host_register, make the copies truly asynchronous).
 extern "C" int r360_frame_upload_async(r360_frame* f, const uint8_t* bgr8, const uint16_t* depth8) {
     CHECK_ARG(f && bgr8 && depth8, "null arg");
+    CHECK_ARG(f->rows > 0, "a sphere-only frame has no sensor images");
     const size_t ns = (size_t)8 * f->rows * f->cols;
     R360_HIP(hipMemcpyAsync(f->d_bgr, bgr8, ns * 3, hipMemcpyHostToDevice, f->ctx->stream));
     R360_HIP(hipMemcpyAsync(f->d_depth, depth8, ns * 2, hipMemcpyHostToDevice, f->ctx->stream));
@@ -448,8 +474,26 @@ extern "C" int r360_host_unregister(void* p) {
     return 0;
 }
 
+// setSourceFrame / setTargetFrame(cv::Mat& imgRGB, cv::Mat& imgDepth) (RegisterPhotoICP.h:480-516): a sphere
+// given as images (BGR u8 sph_rows x sph_cols x 3, range u16 mm) replaces the frame's sphere; its pyramid
+// (gray, depth, gradients with the seam mask, source points) is rebuilt.
+extern "C" int r360_frame_set_sphere(r360_frame* f, const uint8_t* bgr, const uint16_t* range_mm, int sph_rows,
+                                     int sph_cols) {
+    CHECK_ARG(f && bgr && range_mm, "null arg");
+    CHECK_ARG(sph_rows == f->sph_rows && sph_cols == f->sph_cols,
+              "sphere size differs from the frame's (create it from r360_calib_create_sphere)");
+    const size_t n = (size_t)sph_rows * sph_cols;
+    R360_HIP(hipMemcpyAsync(f->d_sph_bgr, bgr, n * 3, hipMemcpyHostToDevice, f->ctx->stream));
+    R360_HIP(hipMemcpyAsync(f->d_sph_depth, range_mm, n * 2, hipMemcpyHostToDevice, f->ctx->stream));
+    if (launch_sphere_level0(f) || launch_pyramid(f)) return -1;
+    R360_HIP(hipStreamSynchronize(f->ctx->stream));
+    f->built = (f->built & ~(unsigned)(R360_BUILD_SPHERE | R360_BUILD_PYRAMID)) | R360_BUILD_SPHERE | R360_BUILD_PYRAMID;
+    return 0;
+}
+
 extern "C" int r360_frame_upload_device(r360_frame* f, const void* d_bgr8, const void* d_depth8) {
     CHECK_ARG(f && d_bgr8 && d_depth8, "null arg");
+    CHECK_ARG(f->rows > 0, "a sphere-only frame has no sensor images");
     const size_t ns = (size_t)8 * f->rows * f->cols;
     R360_HIP(hipMemcpyAsync(f->d_bgr, d_bgr8, ns * 3, hipMemcpyDeviceToDevice, f->ctx->stream));
     R360_HIP(hipMemcpyAsync(f->d_depth, d_depth8, ns * 2, hipMemcpyDeviceToDevice, f->ctx->stream));
@@ -459,6 +503,7 @@ extern "C" int r360_frame_upload_device(r360_frame* f, const void* d_bgr8, const
 
 extern "C" int r360_frame_build_async(r360_frame* f, unsigned flags) {
     CHECK_ARG(f, "null frame");
+    CHECK_ARG(f->rows > 0 || flags == 0, "a sphere-only frame has no sensor images to build from (r360_frame_set_sphere)");
     if (flags & (R360_BUILD_UNDISTORT | R360_BUILD_CLOUD | R360_BUILD_PLANES)) {
         if (launch_undistort(f)) return -1;
         f->built |= R360_BUILD_UNDISTORT;
@@ -661,6 +706,10 @@ extern "C" int r360_align360_result(r360_ctx* ctx, float pose_out[16], float H_o
         st->sso = h->sso;
         st->error = h->error;
         st->passes = h->passes;
+        st->av_photo_residual = h->av_photo;
+        st->av_depth_residual = h->av_depth;
+        st->av_residual = h->av_res;
+        st->residuals_set = h->av_set & 3;
     }
     return h->illposed ? 1 : 0;
 }

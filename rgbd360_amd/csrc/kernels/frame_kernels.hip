@@ -282,6 +282,15 @@ __global__ void __launch_bounds__(SRC_TPB) k_src_compact(const SrcLevel* __restr
     if (blockIdx.x == (unsigned)((n - 1) / R360_SRC_BLOCK) && threadIdx.x == SRC_TPB - 1) npts[blockIdx.y] = pos;
 }
 
+int launch_sphere_level0(r360_frame* f) {
+    const long n = (long)f->sph_rows * f->sph_cols;
+    // cvtColor(CV_RGB2GRAY) / 255 and convertTo(CV_32F, 0.001): the stitch kernel's level-0 expressions
+    hipLaunchKernelGGL(k_sensor_level0, dim3(grid_for(n)), dim3(TPB), 0, f->ctx->stream, f->d_sph_bgr, f->d_sph_depth,
+                       n, f->lv[0].p0);
+    R360_HIP(hipGetLastError());
+    return 0;
+}
+
 int launch_pyramid(r360_frame* f) {
     // RegisterPhotoICP constructor defaults minDepth 0.3 / maxDepth 6.0 (:202-203)
     const float min_d = 0.3f, max_d = 6.0f;

@@ -154,6 +154,11 @@ __device__ void lm_step_wave(IcpState* S, const double* sums, const IcpConst& C,
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     if (lane == 0) {
         S->passes++;
+        // errorPhotoICP assigns the residual members (:759-762); avResidual is float
+        S->av_photo = sqrt(sums[R360_SUM_ERR2] / nD);
+        S->av_depth = sqrt(sums[R360_SUM_ERR2D] / nD);
+        S->av_res = (float)(S->av_photo + S->av_depth);
+        S->av_set |= 3;
         bool check = false;
         int mode = 0;
         auto accept = [&]() {
@@ -200,6 +205,9 @@ __device__ void lm_step_wave(IcpState* S, const double* sums, const IcpConst& C,
                 S->evals_l[C.level] = S->evals;
             } else {
                 S->loops++;
+                // "Assign the temporal values for the residuals" at the loop iteration's start (:4329-4332)
+                S->av_photo_t = S->av_photo; S->av_depth_t = S->av_depth; S->av_res_t = S->av_res;
+                S->av_set |= 12;
                 for (int k = 0; k < 36; ++k) S->Hout[k] = S->Hcur[k];   // `hessian` of this iteration
                 for (int k = 0; k < 6; ++k) S->gout[k] = S->gcur[k];
                 mode = 1;

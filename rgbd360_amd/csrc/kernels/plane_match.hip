@@ -89,7 +89,13 @@ __global__ void k_match_tables(const float* __restrict__ desc, int ns, int nt, i
 
 int launch_match_tables(r360_ctx* ctx, const float* d_desc, int ns, int nt, int mode, uint8_t* d_unary,
                         unsigned long long* d_bin, int words) {
-    const MatchCfg cfg = {0.5f, 0.64278761f, 0.07f, 100.f, 2.5f, 3.0f, 3.0f, 0.98480775f, 0.33f, 0.985f, 0.17364818f};
+    // the ctx's thresholds (r360_match_params, the ini keys); angles become the cosines / sine the
+    // constraints compare against (configLocaliser_sphericalOdometry.ini: cos 50, cos 10, sin 10 deg)
+    const r360_match_params& m = ctx->match;
+    const MatchCfg cfg = {m.dist_d, (float)cos(m.angle * R360_PI / 180), m.color_threshold, m.intensity_threshold,
+                          m.elongation_threshold, m.area_threshold, m.dist_threshold,
+                          (float)cos(m.angle_threshold * R360_PI / 180), m.height_threshold, m.cos_angle_parallel,
+                          (float)sin(m.planar_normal_angle * R360_PI / 180)};
     const long total = (long)ns * nt * words * 64;
     if (total == 0) return 0;
     const int blocks = (int)std::min<long>((total + 255) / 256, 4096);

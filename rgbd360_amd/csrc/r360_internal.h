@@ -77,6 +77,11 @@ struct alignas(16) IcpState {
     double lm_lambda;   // alignFrames (pinhole) Levenberg-Marquardt lambda (:4301)
     int lm_phase;       // 0: the pending candidate is the undamped step, 1: the LM retry (:4381-4412)
     int pad2;
+    // the residual members the error functions assign (RegisterPhotoICP.h:183-189): of the last evaluated
+    // pass (av_*) and, for alignFrames, the copies taken at each loop iteration's start (av_*_t, :4329-4332)
+    double av_photo, av_depth, av_photo_t, av_depth_t;
+    float av_res, av_res_t;
+    int av_set;         // bit 0 photo/depth of the last pass assigned, bit 1 av_res assigned, bits 2/3 the copies
     double sums[32];    // last pass sums (eval mode)
     unsigned long long dbg[12];  // s_memrealtime stamps of the diagnostic build (-DR360_STAMPS)
 };
@@ -221,6 +226,7 @@ struct r360_ctx {
     struct RobotOut* h_rob_out = nullptr;      // pinned
     // PbMap matcher scratch (k_match_tables)
     int match_cap = 0;                       // planes per subgraph
+    r360_match_params match{};               // SubgraphMatcher thresholds (r360_ctx_set_match_params)
     float* d_match_desc = nullptr;
     uint8_t* d_unary = nullptr;
     unsigned long long* d_bin = nullptr;
@@ -297,6 +303,7 @@ struct r360_frame {
 int launch_undistort(r360_frame* f);
 int launch_stitch(r360_frame* f);
 int launch_pyramid(r360_frame* f);
+int launch_sphere_level0(r360_frame* f);   // level 0 {gray, depth m} from the frame's sphere images
 int launch_sensor_pyramid(r360_frame* f);
 // pinhole alignFrames: intrinsics of level 0 (setCameraMatrix) and the jobs of one batched launch
 struct PinJobs { int sensor[8]; int n; };

@@ -82,3 +82,34 @@ def test_context_without_gpu_fails_loudly():
         return
     ctx.close()
     pytest.skip("GPU present: the no-GPU error path is not reachable here")
+
+
+@pytest.mark.parametrize("ini", ["configLocaliser_spherical.ini", "configLocaliser_sphericalOdometry.ini"])
+def test_matcher_ini_parsers_agree(ini):
+    """RegisterRGBD360(configFile) reads the mrpt-pbmap thresholds (RegisterRGBD360.h:97-100): the
+    library's parser (r360_match_params_load_ini) and the oracle's independent one give the same values;
+    the sphericalOdometry file reproduces the library's defaults."""
+    from oracle import oracle360 as O
+    path = os.path.join(R.DATA_DIR, "config_files", ini)
+    lib_m = R.MatchParams.load_ini(path)
+    orc_m = O.load_match_ini(path)
+    vals = lambda m, F: [getattr(m, f) for f, _ in F._fields_]
+    assert vals(lib_m, R.MatchParams) == vals(orc_m, O.MatchParams)
+    if ini.endswith("Odometry.ini"):
+        assert vals(lib_m, R.MatchParams) == vals(R.MatchParams.default(), R.MatchParams)
+    else:
+        assert lib_m.area_threshold == 4.0 and lib_m.angle_threshold == 9.0 and lib_m.intensity_threshold == 150.0
+    with pytest.raises(RuntimeError):
+        R.MatchParams.load_ini(path + ".missing")
+
+
+def test_facade_translation_units_compile(root, tmp_path):
+    """The C++ façade compiles against calls written the way the reference's applications make them
+    (apps/*.cpp: OdometryRGBD360, RegisterPairRGBD360, SphereGraphSLAM, KFsphere_SLAM), with g++ alone."""
+    import subprocess
+    for app in ("KFsphereTracking", "OdometryRGBD360", "RegisterPairRGBD360", "SphereGraphTracking"):
+        out = tmp_path / app
+        p = subprocess.run(["g++", "-std=c++17", "-O0", "-fsyntax-only", "-Wall", "-Werror",
+                            f"-I{root}/include", f'-DRGBD360_DATA_DIR="{root}/data"', f"{root}/apps/{app}.cpp"],
+                           capture_output=True, text=True)
+        assert p.returncode == 0, (app, p.stderr[-3000:])

@@ -264,3 +264,29 @@ def test_rank_test_matches_oracle_over_lambda_schedule():
     ref = np.array([O.rank6f(m) for _, _, m in fam])
     assert np.array_equal(out, ref)
     assert (ref < 6).any() and (ref == 6).any()
+
+
+def test_set_frames_from_sphere_images(ctx, qvga):
+    """setSourceFrame / setTargetFrame(imgRGB, imgDepth) (RegisterPhotoICP.h:480-516): the stitched spheres
+    handed over as images (downloaded, then uploaded into sphere-only frames) give the same pyramid and the
+    same alignment as the frames themselves."""
+    f1, f2 = qvga["f1"], qvga["f2"]
+    s1b, s1d = f1.sphere()
+    s2b, s2d = f2.sphere()
+    a = R.RegisterPhotoICP(ctx)
+    b = R.RegisterPhotoICP(ctx)
+    for reg in (a, b):
+        reg.setNumPyr(5)
+        reg.setGrayVariance(3.0 / 255)
+    a.setTargetFrame(f1); a.setSourceFrame(f2)
+    b.setTargetFrame(s1b, s1d); b.setSourceFrame(s2b, s2d)
+    for l in range(5):
+        la, lb = f2.level(l), b.src.level(l)
+        for k in ("gray", "depth", "gx", "gy", "dgx", "dgy"):
+            assert np.array_equal(la[k], lb[k]), (l, k)
+        assert np.array_equal(f2.points(l), b.src.points(l)), l
+    ra = a.alignFrames360(np.eye(4), R.PHOTO_DEPTH)
+    rb = b.alignFrames360(np.eye(4), R.PHOTO_DEPTH)
+    assert ra == rb
+    assert np.array_equal(a.getOptimalPose(), b.getOptimalPose())
+    assert np.array_equal(a.getHessian(), b.getHessian())

@@ -107,3 +107,24 @@ def test_align360_occlusion_parity_samples(ctx, qvga, occ):
     dt = float(np.linalg.norm(np.asarray(reg.getOptimalPose())[:3, 3] - pose[:3, 3]))
     assert dr <= ROT_TOL and dt <= TRANS_TOL, (dr, dt)
     assert list(reg.stats.iters)[:5] == list(st.iters)[:5]
+    # the residual members errorPhotoICP_sphereOcc1/2 leave (RegisterPhotoICP.h:3360-3362, :3852-3853)
+    assert reg.stats.residuals_set & 1 and st.residuals_set & 1
+    # evaluated at the final poses, which agree to the north-star tolerance (not bit for bit): 1e-3 relative
+    assert _close(reg.avPhotoResidual, st.av_photo_residual, 1e-3), (reg.avPhotoResidual, st.av_photo_residual)
+    assert _close(reg.avDepthResidual, st.av_depth_residual, 1e-3), (reg.avDepthResidual, st.av_depth_residual)
+    assert (reg.stats.residuals_set & 2) == (st.residuals_set & 2)        # avResidual only when ILL-POSED
+
+
+def test_plain_align_leaves_residual_members(ctx, qvga):
+    """errorPhotoICP_sphere assigns no residual member: after an occlusion-0 alignment they keep the values
+    of the previous occlusion-2 one (uninitialised in a fresh reference object: NaN here)."""
+    reg = R.RegisterPhotoICP(ctx)
+    reg.setNumPyr(4)
+    reg.setTargetFrame(qvga["f1"]); reg.setSourceFrame(qvga["f2"])
+    reg.alignFrames360(np.eye(4), R.PHOTO_DEPTH, 0)
+    assert np.isnan(reg.avPhotoResidual) and np.isnan(reg.avDepthResidual) and np.isnan(reg.avResidual)
+    reg.alignFrames360(np.eye(4), R.PHOTO_DEPTH, 2)
+    a, b = reg.avPhotoResidual, reg.avDepthResidual
+    assert np.isfinite(a) and np.isfinite(b)
+    reg.alignFrames360(np.eye(4), R.PHOTO_DEPTH, 0)
+    assert (reg.avPhotoResidual, reg.avDepthResidual) == (a, b)

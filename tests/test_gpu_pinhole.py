@@ -154,6 +154,13 @@ def test_align_sensors_parity_qvga(ctx, qvga, method):
         checked += 1
         dr, dtr = _pose_err(poses[k], Po)
         assert dr <= 1e-4 and dtr <= 1e-3, (k, dr, dtr, list(stats[k].iters[:4]), list(st.iters[:4]))
+        # the residual members alignFrames leaves (:4329-4332, :4507-4509; errorPhotoICP :759-762)
+        assert stats[k].residuals_set == st.residuals_set, k
+        if st.residuals_set:
+            for a, b in ((stats[k].av_photo_residual, st.av_photo_residual),
+                         (stats[k].av_depth_residual, st.av_depth_residual), (stats[k].av_residual, st.av_residual)):
+                # at poses equal to the north-star tolerance: 1e-3 relative
+                assert (np.isnan(a) and np.isnan(b)) or abs(a - b) <= 1e-3 * abs(b), (k, a, b)
     assert checked >= 5, checked
     # the single-sensor entry point is the same computation
     f_t, f_s = qvga["frames"]

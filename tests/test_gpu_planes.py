@@ -129,25 +129,58 @@ def test_pbmap_planes_identical(request, which):
     D["oracle_maps"] = maps
 
 
+CONFIG_DIR = os.path.join(R.DATA_DIR, "config_files")
+
+
 @pytest.mark.parametrize("which", ["qvga", "vga"])
-def test_match_tables_and_register_pbmap(ctx, request, which):
+@pytest.mark.parametrize("mode", [R.DEFAULT_6DoF, R.PLANAR_3DoF, R.ODOMETRY_6DoF, R.PLANAR_ODOMETRY_3DoF])
+@pytest.mark.parametrize("ini", [None, "configLocaliser_spherical.ini"])
+def test_match_tables_and_register_pbmap(ctx, request, which, mode, ini):
+    """SubgraphMatcher tables, matches, pose and information for every registrationType
+    (RegisterRGBD360.h:260-266), with the default (sphericalOdometry) thresholds and with those of
+    configLocaliser_spherical.ini loaded the way RegisterRGBD360(configFile) does (:97-100)."""
     D = request.getfixturevalue(which)
     maps = D.get("oracle_maps") or [O.PbMap(dm, b, D["rt"]) for (b, dm) in D["inputs"]]
-    reg = R.RegisterRGBD360(ctx)
+    path = os.path.join(CONFIG_DIR, ini) if ini else None
+    reg = R.RegisterRGBD360(ctx, path)
+    op = O.load_match_ini(path) if path else None
+    if op is not None:                       # the two independent ini parsers agree
+        assert [getattr(op, f) for f, _ in O.MatchParams._fields_] == [getattr(reg.match, f) for f, _ in R.MatchParams._fields_]
     reg.setReference(D["frames"][0], 25)
     reg.setTarget(D["frames"][1], 25)
-    gt = reg.match_tables(R.PLANAR_3DoF)
-    ot = O.match_tables(maps[0], maps[1], 25, O.PLANAR_3DoF)
+    gt = reg.match_tables(mode)
+    ot = O.match_tables(maps[0], maps[1], 25, mode, params=op)
     for key in ("sid", "tid", "unary", "binary"):
         assert np.array_equal(gt[key], ot[key]), key
-    ok = reg.RegisterPbMap(D["frames"][0], D["frames"][1], 25, R.PLANAR_3DoF)
-    r = O.register_pbmap(maps[0], maps[1], 25, O.PLANAR_3DoF)
+    D.setdefault("tables", {})[(mode, ini)] = ot
+    ok = reg.RegisterPbMap(D["frames"][0], D["frames"][1], 25, mode)
+    r = O.register_pbmap(maps[0], maps[1], 25, mode, params=op)
     assert ok == bool(r["good"])
     assert reg.getMatchedPlanes() == r["matches"]
     assert reg.getAreaMatched() == r["area_matched"]
     if ok:
         assert np.array_equal(reg.getPose(), r["pose"])
         assert np.array_equal(reg.getInfoMat(), r["info"])
+        # getCovMat / calcEntropy / trackingScore (:208-238, :526-540) from the same information matrix
+        cov = np.linalg.inv(r["info"].astype(np.float64))
+        np.testing.assert_allclose(reg.getCovMat(), cov, rtol=1e-5, atol=1e-12)
+        ent = 0.5 * (6 * (1 + np.log(2 * 3.14159265359)) + np.log(np.linalg.det(cov)))
+        assert abs(reg.calcEntropy() - ent) <= 1e-4 * max(1.0, abs(ent))
+        q, score = reg.trackingScore()
+        assert score == np.float32(np.float32(r["area_matched"]) / np.float32(r["area_src"]))
+        assert q == (0 if score >= 0.7 else 1 if score >= 0.3 else 2)
+
+
+def test_ini_thresholds_change_the_tables(request):
+    """configLocaliser_spherical.ini's thresholds (wider area / elongation / distance ratios, other angles)
+    give other unary tables than the default file for at least one registrationType, as in the oracle."""
+    for which in ("qvga", "vga"):
+        T = request.getfixturevalue(which).get("tables", {})
+        if not T:
+            pytest.skip("runs after test_match_tables_and_register_pbmap")
+        diff = [m for m in range(4) if (m, None) in T and (m, "configLocaliser_spherical.ini") in T
+                and not np.array_equal(T[(m, None)]["unary"], T[(m, "configLocaliser_spherical.ini")]["unary"])]
+        assert diff, which
 
 
 def test_register_pbmap_synthetic_accuracy(ctx, vga):
