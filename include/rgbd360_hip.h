@@ -166,6 +166,19 @@ int r360_align360_async(r360_ctx* ctx, r360_frame* trg, r360_frame* src, const f
 int r360_align360_result(r360_ctx* ctx, float pose_out[16], float H_out[36], float g_out[6],
                          r360_icp_stats* st);
 
+/* Batched alignFrames360 (occlusion 0): n <= R360_MAX_BATCH independent alignments of pairs
+ * (trg[j], src[j]) from init[16 j..], each exactly the computation r360_align360 performs on that pair
+ * (same passes, same per-pair Gauss-Newton state and decisions; results bit-identical), run as one launch
+ * per pass over all pairs.  This is how the reference's callers' many alignFrames360 calls (one per
+ * consecutive pair in OdometryRGBD360.cpp:141-257, per keyframe candidate in SphereGraphSLAM /
+ * LoopClosure360) fill the GPU.  Frames must share one sphere size and may belong to any ctx of the device:
+ * ctx's stream waits for the work already enqueued on their contexts' streams.  _result fills n poses /
+ * H / g / stats (NULL skips) and returns the number of ILL-POSED alignments.  One batch per ctx at a time. */
+#define R360_MAX_BATCH_ALIGN 16
+int r360_align360_batch_async(r360_ctx* ctx, int n, r360_frame* const* trg, r360_frame* const* src,
+                              const float* init, int method, const r360_icp_params* p);
+int r360_align360_batch_result(r360_ctx* ctx, float* pose_out, float* H_out, float* g_out, r360_icp_stats* st);
+
 /* One fused pass at a fixed pose: errorPhotoICP_sphere (:2545-2739) + calcHessGrad_sphere
  * (:2745-3228) at pyramid level `level`.  H/g in double (sum of the float per-pixel terms). */
 int r360_icp_eval(r360_ctx* ctx, r360_frame* trg, r360_frame* src, int level, const float pose[16],

@@ -192,6 +192,9 @@ _SIGS = [
                                 C.POINTER(IcpStats)]),
     ("r360_align360_async", C.c_int, [_P, _P, _P, _FP, C.c_int, C.c_int, C.POINTER(IcpParams)]),
     ("r360_align360_result", C.c_int, [_P, _FP, _FP, _FP, C.POINTER(IcpStats)]),
+    ("r360_align360_batch_async", C.c_int, [_P, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), _FP, C.c_int,
+                                            C.POINTER(IcpParams)]),
+    ("r360_align360_batch_result", C.c_int, [_P, _FP, _FP, _FP, C.POINTER(IcpStats)]),
     ("r360_icp_eval", C.c_int, [_P, _P, _P, C.c_int, _FP, C.c_int, C.POINTER(IcpParams), _DP, _DP, _DP, _IP,
                                 _IP]),
     ("r360_icp_eval_occ", C.c_int, [_P, _P, _P, C.c_int, _FP, C.c_int, C.c_int, C.POINTER(IcpParams), _DP, _DP,
@@ -813,6 +816,31 @@ class Batch:
             self.close()
         except Exception:
             pass
+
+
+MAX_BATCH_ALIGN = 16
+
+
+def align360_batch(ctx: "Context", pairs, inits=None, method: int = PHOTO_CONSISTENCY, params: "IcpParams" = None):
+    """Batched alignFrames360 (r360_align360_batch_*): pairs = [(target Frame360, source Frame360), ...] (at most
+    MAX_BATCH_ALIGN), inits = per-pair 4x4 guesses (identity if None).  Every pair's result equals
+    RegisterPhotoICP.alignFrames360 on that pair alone.  Returns (poses [n,4,4], H [n,6,6], g [n,6], stats list,
+    illposed count)."""
+    n = len(pairs)
+    p = params or IcpParams.default()
+    trg = (C.c_void_p * n)(*[t.h for t, _ in pairs])
+    src = (C.c_void_p * n)(*[s.h for _, s in pairs])
+    init = np.concatenate([_mat16(np.eye(4) if inits is None or inits[j] is None else inits[j]) for j in range(n)])
+    init = np.ascontiguousarray(init, np.float32)
+    _check(lib().r360_align360_batch_async(ctx.h, n, trg, src, _fptr(init), method, C.byref(p)),
+           "r360_align360_batch_async")
+    po, Ho, go = np.zeros(16 * n, np.float32), np.zeros(36 * n, np.float32), np.zeros(6 * n, np.float32)
+    st = (IcpStats * n)()
+    ill = _check(lib().r360_align360_batch_result(ctx.h, _fptr(po), _fptr(Ho), _fptr(go), st),
+                 "r360_align360_batch_result")
+    poses = np.stack([_from16(po[16 * j:16 * j + 16]) for j in range(n)])
+    H = np.stack([Ho[36 * j:36 * j + 36].reshape(6, 6).T.copy() for j in range(n)])
+    return poses, H, go.reshape(n, 6).copy(), list(st), ill
 
 
 class RegisterPhotoICP:

@@ -110,8 +110,8 @@ extern "C" int r360_ctx_create(int device, r360_ctx** out) {
     R360_HIP(hipMalloc(&c->d_partials, sizeof(double) * 32 * c->partials_cap));
     R360_HIP(hipMalloc(&c->d_gticket, sizeof(unsigned) * R360_TICKET_STRIDE * R360_TICKET_GROUPS));
     R360_HIP(hipMemset(c->d_gticket, 0, sizeof(unsigned) * R360_TICKET_STRIDE * R360_TICKET_GROUPS));
-    R360_HIP(hipMalloc(&c->d_ktime, sizeof(unsigned long long) * 17));
-    R360_HIP(hipMemset(c->d_ktime, 0, sizeof(unsigned long long) * 17));
+    R360_HIP(hipMalloc(&c->d_ktime, sizeof(unsigned long long) * 18));
+    R360_HIP(hipMemset(c->d_ktime, 0, sizeof(unsigned long long) * 18));
     R360_HIP(hipMemset(c->d_ktime, 0xff, sizeof(unsigned long long)));
     R360_HIP(hipHostMalloc(&c->h_state, sizeof(IcpState), hipHostMallocDefault));
     r360_match_params_default(&c->match);
@@ -131,6 +131,9 @@ extern "C" void r360_ctx_destroy(r360_ctx* c) {
     hipFree(c->d_defer);
     hipFree(c->d_ktime);
     hipHostFree(c->h_state);
+    hipFree(c->d_bstate); hipFree(c->d_bpartials); hipFree(c->d_bgticket); hipFree(c->d_bdefer);
+    hipHostFree(c->h_bstate);
+    for (auto e : c->sync_ev) hipEventDestroy(e);
     hipFree(c->d_pin_state); hipFree(c->d_pin_partials); hipHostFree(c->h_pin_state);
     hipFree(c->d_rob_jobs); hipFree(c->d_rob_partials); hipFree(c->d_rob_sums); hipFree(c->d_rob_tickets);
     hipFree(c->d_rob_out); hipHostFree(c->h_rob_jobs); hipHostFree(c->h_rob_sums); hipHostFree(c->h_rob_out);
@@ -153,7 +156,7 @@ extern "C" int r360_ctx_kernel_time(r360_ctx* ctx, int level, double* us_sum, lo
 extern "C" int r360_ctx_kernel_time_reset(r360_ctx* ctx) {
     CHECK_ARG(ctx, "null ctx");
     if (ctx_wait(ctx)) return -1;
-    R360_HIP(hipMemset(ctx->d_ktime, 0, sizeof(unsigned long long) * 17));
+    R360_HIP(hipMemset(ctx->d_ktime, 0, sizeof(unsigned long long) * 18));
     R360_HIP(hipMemset(ctx->d_ktime, 0xff, sizeof(unsigned long long)));
     return 0;
 }
@@ -689,6 +692,19 @@ extern "C" int r360_align360_async(r360_ctx* ctx, r360_frame* trg, r360_frame* s
     return 0;
 }
 
+static void fill_stats(const IcpState* h, r360_icp_stats* st) {
+    memset(st, 0, sizeof(*st));
+    for (int l = 0; l < 8; ++l) { st->iters[l] = h->iters[l]; st->evals[l] = h->evals_l[l]; }
+    st->illposed = h->illposed;
+    st->sso = h->sso;
+    st->error = h->error;
+    st->passes = h->passes;
+    st->av_photo_residual = h->av_photo;
+    st->av_depth_residual = h->av_depth;
+    st->av_residual = h->av_res;
+    st->residuals_set = h->av_set & 3;
+}
+
 extern "C" int r360_align360_result(r360_ctx* ctx, float pose_out[16], float H_out[36], float g_out[6],
                                     r360_icp_stats* st) {
     CHECK_ARG(ctx && ctx->async_pending, "no alignment pending");
@@ -699,18 +715,7 @@ extern "C" int r360_align360_result(r360_ctx* ctx, float pose_out[16], float H_o
     if (pose_out) memcpy(pose_out, h->pose, sizeof(float) * 16);
     if (H_out) memcpy(H_out, h->Hout, sizeof(float) * 36);
     if (g_out) memcpy(g_out, h->gout, sizeof(float) * 6);
-    if (st) {
-        memset(st, 0, sizeof(*st));
-        for (int l = 0; l < 8; ++l) { st->iters[l] = h->iters[l]; st->evals[l] = h->evals_l[l]; }
-        st->illposed = h->illposed;
-        st->sso = h->sso;
-        st->error = h->error;
-        st->passes = h->passes;
-        st->av_photo_residual = h->av_photo;
-        st->av_depth_residual = h->av_depth;
-        st->av_residual = h->av_res;
-        st->residuals_set = h->av_set & 3;
-    }
+    if (st) fill_stats(h, st);
     return h->illposed ? 1 : 0;
 }
 
@@ -719,6 +724,94 @@ extern "C" int r360_align360(r360_ctx* ctx, r360_frame* trg, r360_frame* src, co
                              float g_out[6], r360_icp_stats* st) {
     if (int rc = r360_align360_async(ctx, trg, src, init, method, occlusion, p)) return rc;
     return r360_align360_result(ctx, pose_out, H_out, g_out, st);
+}
+
+// Makes ctx's stream wait for the work already enqueued on the streams of the frames' contexts (their builds)
+int ctx_wait_frames(r360_ctx* ctx, r360_frame* const* frames, int n) {
+    std::vector<hipStream_t> seen;
+    for (int i = 0; i < n; ++i) {
+        hipStream_t s = frames[i]->ctx->stream;
+        if (s == ctx->stream) continue;
+        bool dup = false;
+        for (hipStream_t t : seen) dup = dup || t == s;
+        if (dup) continue;
+        seen.push_back(s);
+    }
+    while (ctx->sync_ev.size() < seen.size()) {
+        hipEvent_t e;
+        R360_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        ctx->sync_ev.push_back(e);
+    }
+    for (size_t i = 0; i < seen.size(); ++i) {
+        R360_HIP(hipEventRecord(ctx->sync_ev[i], seen[i]));
+        R360_HIP(hipStreamWaitEvent(ctx->stream, ctx->sync_ev[i], 0));
+    }
+    return 0;
+}
+
+extern "C" int r360_align360_batch_async(r360_ctx* ctx, int n, r360_frame* const* trg, r360_frame* const* src,
+                                         const float* init, int method, const r360_icp_params* p) {
+    CHECK_ARG(ctx && trg && src && init && p, "null arg");
+    CHECK_ARG(n >= 1 && n <= R360_MAX_BATCH, "batch size must be 1..R360_MAX_BATCH");
+    CHECK_ARG(!ctx->batch_pending, "a batch is pending on this ctx (r360_align360_batch_result)");
+    CHECK_ARG(method >= 0 && method <= 2, "invalid method");
+    for (int j = 0; j < n; ++j) {
+        if (int rc = check_pair(ctx, trg[j], src[j], p)) return rc;
+        CHECK_ARG(src[j]->sph_rows == src[0]->sph_rows && src[j]->sph_cols == src[0]->sph_cols,
+                  "batched alignments need frames of one sphere size");
+    }
+    if (ensure_batch(ctx, n, (long)src[0]->lv[0].rows * src[0]->lv[0].cols)) return -1;
+    std::vector<r360_frame*> fr;
+    for (int j = 0; j < n; ++j) { fr.push_back(trg[j]); fr.push_back(src[j]); }
+    if (ctx_wait_frames(ctx, fr.data(), 2 * n)) return -1;
+    for (int j = 0; j < n; ++j) {
+        IcpState* h = ctx->h_bstate + j;
+        memset(h, 0, sizeof(IcpState));
+        memcpy(h->pose, init + 16 * j, sizeof(float) * 16);
+        memcpy(h->cand, init + 16 * j, sizeof(float) * 16);
+        h->dbg[8] = ~0ull;
+    }
+    R360_HIP(hipMemcpyAsync(ctx->d_bstate, ctx->h_bstate, sizeof(IcpState) * n, hipMemcpyHostToDevice, ctx->stream));
+    const size_t tk = (size_t)R360_TICKET_GROUPS * R360_TICKET_STRIDE;
+    for (int l = p->n_pyr - 1; l >= 0; --l) {
+        IcpJobs jobs;
+        for (int j = 0; j < n; ++j) {
+            IcpJob& J = jobs.j[j];
+            J.src = src[j]->lv[l].p0; J.trg = trg[j]->lv[l].p0; J.tg = trg[j]->lv[l].tg;
+            J.pts = src[j]->lv[l].pts; J.npts = src[j]->d_npts + l;
+            J.S = ctx->d_bstate + j;
+            J.partials = ctx->d_bpartials + (size_t)j * 32 * ctx->partials_cap;
+            J.gcnt = ctx->d_bgticket + (size_t)j * tk;
+            J.dq = ctx->d_bdefer + (size_t)j * ctx->bdefer_cap;
+        }
+        const int np = src[0]->lv[l].rows * src[0]->lv[l].cols;
+        const IcpConst C = make_const(p, l, np, 0);
+        const int passes = 1 + ((l == 0 && p->fixed_iters_level0 > 0) ? p->fixed_iters_level0 : p->max_iters);
+        for (int k = 0; k < passes; ++k)
+            if (int rc = launch_icp_jobs(ctx, jobs, n, src[0], l, method, C, k == 0, 0)) return rc;
+    }
+    ctx->batch_n = n;
+    ctx->batch_pending = 1;
+    return 0;
+}
+
+extern "C" int r360_align360_batch_result(r360_ctx* ctx, float* pose_out, float* H_out, float* g_out,
+                                          r360_icp_stats* st) {
+    CHECK_ARG(ctx && ctx->batch_pending, "no batched alignment pending");
+    const int n = ctx->batch_n;
+    R360_HIP(hipMemcpyAsync(ctx->h_bstate, ctx->d_bstate, sizeof(IcpState) * n, hipMemcpyDeviceToHost, ctx->stream));
+    if (ctx_wait(ctx)) return -1;
+    ctx->batch_pending = 0;
+    int ill = 0;
+    for (int j = 0; j < n; ++j) {
+        const IcpState* h = ctx->h_bstate + j;
+        if (pose_out) memcpy(pose_out + 16 * j, h->pose, sizeof(float) * 16);
+        if (H_out) memcpy(H_out + 36 * j, h->Hout, sizeof(float) * 36);
+        if (g_out) memcpy(g_out + 6 * j, h->gout, sizeof(float) * 6);
+        if (st) fill_stats(h, st + j);
+        ill += h->illposed ? 1 : 0;
+    }
+    return ill;
 }
 
 // one eval-mode pass (no GN step): the raw pass sums at `pose`

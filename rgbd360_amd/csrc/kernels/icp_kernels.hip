@@ -422,18 +422,32 @@ __device__ __forceinline__ void contribute_fast(Acc& A, WaveCnt& W, const Proj& 
 #include "icp_gn.inc"
 
 
+// The last arrival of a pass's jobs (a job's last workgroup, or block 0 of a job that exits at entry) closes
+// the pass's in-kernel execution span, if any job ran.
+__device__ __forceinline__ void pass_arrive(unsigned long long* kt, bool ran, int level) {
+    const unsigned long long prev = __hip_atomic_fetch_add(kt + 17, 1ull + (ran ? (1ull << 32) : 0ull),
+                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((unsigned)prev != gridDim.y - 1) return;
+    __hip_atomic_store(kt + 17, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((prev >> 32) + (ran ? 1 : 0) == 0) return;
+    const unsigned long long t0 = __hip_atomic_load(kt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+    const int lv = level & 7;
+    kt[1 + lv] += t1 > t0 ? t1 - t0 : 0;
+    kt[9 + lv] += 1;
+}
+
 // TOP = 1 only renames the level-0 instantiation, so traces (rocprofv3) separate level 0 from level 1,
-// which launch the same grid.
+// which launch the same grid.  One launch runs gridDim.y independent alignments (jobs.j[blockIdx.y]), each
+// on gridDim.x workgroups with its own records, tickets and GN state: a job's sums and step are exactly
+// those of the same job launched alone.
 template <int METHOD, int PF, int TOP, int OCC>
-__global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const float2* __restrict__ src, const float2* __restrict__ trg,
-                                                 const float4* __restrict__ tg, const float* __restrict__ sinphi,
+__global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs jobs, const float* __restrict__ sinphi,
                                                  const float* __restrict__ cosphi, const float* __restrict__ sinth,
                                                  const float* __restrict__ costh, int nRows, int nCols,
-                                                 IcpConst C, IcpState* S, double* __restrict__ partials, int first,
-                                                 int eval_only, unsigned long long* __restrict__ kt,
-                                                 const uint8_t* __restrict__ occf, unsigned* __restrict__ gcnt,
-                                                 int* __restrict__ dq, const float4* __restrict__ pts,
-                                                 const int* __restrict__ npts) {
+                                                 IcpConst C, int first, int eval_only,
+                                                 unsigned long long* __restrict__ kt,
+                                                 const uint8_t* __restrict__ occf) {
     __shared__ float s_red[NW][32];
     __shared__ double s_err[NW], s_errd[NW];
     __shared__ double s_fin[RG][32];
@@ -441,17 +455,30 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const float2* _
     __shared__ GnShared s_gn;
     __shared__ IcpState s_state;
 
-    if (S->stop) return;
+    const IcpJob& J = jobs.j[blockIdx.y];
+    const float2* __restrict__ src = J.src;
+    const float2* __restrict__ trg = J.trg;
+    const float4* __restrict__ tg = J.tg;
+    const float4* __restrict__ pts = J.pts;
+    const int* __restrict__ npts = J.npts;
+    IcpState* S = J.S;
+    double* __restrict__ partials = J.partials;
+    unsigned* __restrict__ gcnt = J.gcnt;
+    int* __restrict__ dq = J.dq;
+
+    // execution span: the start of the launch's first workgroup (dispatched first).  One store, not an
+    // atomic-min per workgroup: same-address atomics serialise at the memory side (~25 ns each), and 512
+    // of them outlasted a short pass.
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+        __hip_atomic_store(kt, (unsigned long long)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    if (S->stop || (!first && !S->active && !eval_only)) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) pass_arrive(kt, false, C.level);
+        return;
+    }
 #ifdef R360_STAMPS
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #endif
-    if (!first && !S->active && !eval_only) return;
-    // execution span: the start of workgroup 0 (dispatched first).  One store, not an atomic-min per
-    // workgroup: same-address atomics serialise at the memory side (~25 ns each), and 512 of them
-    // outlasted a short pass.
-    if (blockIdx.x == 0 && threadIdx.x == 0)
-        __hip_atomic_store(kt, (unsigned long long)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
 
     const float* pm = (first && !eval_only) ? S->pose : S->cand;
     Pose12 P;
@@ -891,13 +918,7 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const float2* _
 #endif
         }
         if (eval_only && threadIdx.x == 0) S->ticket = 0;
-        if (threadIdx.x == 0) {   // the last workgroup closes the span
-            const unsigned long long t0 = __hip_atomic_load(kt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
-            const int lv = C.level & 7;
-            kt[1 + lv] += t1 > t0 ? t1 - t0 : 0;
-            kt[9 + lv] += 1;
-        }
+        if (threadIdx.x == 0) pass_arrive(kt, true, C.level);   // the job's last workgroup
     }
 }
 
@@ -1254,16 +1275,15 @@ static int env_int(const char* name, int dflt) {
 }
 
 template <int M, int PF>
-static void launch_pass(r360_ctx* ctx, int nb, const LevelBufs& Ls, const LevelBufs& Lt, const LevelTrig& T,
-                        const IcpConst& C, int first, int eval_only, bool top, const int* npts) {
+static void launch_pass(r360_ctx* ctx, int nb, int njobs, const IcpJobs& jobs, const LevelBufs& Ls,
+                        const LevelTrig& T, const IcpConst& C, int first, int eval_only, bool top) {
     // PF 4 (compacted source points) has no occlusion form: the occlusion flags are per source pixel
     constexpr int PFO = PF == 4 ? 3 : PF;
     auto kern = C.occ == 1 ? k_icp_pass<M, PFO, 0, 1>
               : C.occ == 2 ? k_icp_pass<M, PFO, 0, 2>
               : top        ? k_icp_pass<M, PF, 1, 0> : k_icp_pass<M, PF, 0, 0>;
-    hipLaunchKernelGGL(kern, dim3(nb), dim3(TPB), 0, ctx->stream, Ls.p0, Lt.p0, Lt.tg, T.sinphi,
-                       T.cosphi, T.sinth, T.costh, Ls.rows, Ls.cols, C, ctx->d_state, ctx->d_partials, first,
-                       eval_only, ctx->d_ktime, ctx->occ_flags, ctx->d_gticket, ctx->d_defer, Ls.pts, npts);
+    hipLaunchKernelGGL(kern, dim3(nb, njobs), dim3(TPB), 0, ctx->stream, jobs, T.sinphi, T.cosphi, T.sinth,
+                       T.costh, Ls.rows, Ls.cols, C, first, eval_only, ctx->d_ktime, ctx->occ_flags);
 }
 
 int ensure_defer(r360_ctx* ctx, long n_pixels) {
@@ -1280,18 +1300,43 @@ int ensure_defer(r360_ctx* ctx, long n_pixels) {
     return 0;
 }
 
-int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src, int level, int method,
-                     const IcpConst& C, int first, int eval_only) {
-    const LevelBufs& Ls = src->lv[level];
-    const LevelBufs& Lt = trg->lv[level];
-    const LevelTrig& T = src->calib->trig[level];
+// Sizes the batch buffers of ctx for n jobs over frames of up to n_pixels level-0 pixels (synchronises the
+// ctx stream when they grow).  Job j: state j, partials_cap records, its own ticket groups and queue.
+int ensure_batch(r360_ctx* ctx, int n, long n_pixels) {
+    const long dneed = n_pixels + (long)ctx->partials_cap * TPB;
+    if (ctx->batch_cap >= n && ctx->bdefer_cap >= dneed) return 0;
+    const int cap = n > ctx->batch_cap ? n : ctx->batch_cap;
+    const long dcap = dneed > ctx->bdefer_cap ? dneed : ctx->bdefer_cap;
+    R360_HIP(hipSetDevice(ctx->device));
+    R360_HIP(hipStreamSynchronize(ctx->stream));
+    (void)hipFree(ctx->d_bstate); (void)hipFree(ctx->d_bpartials); (void)hipFree(ctx->d_bgticket);
+    (void)hipFree(ctx->d_bdefer); (void)hipHostFree(ctx->h_bstate);
+    ctx->d_bstate = nullptr; ctx->d_bpartials = nullptr; ctx->d_bgticket = nullptr; ctx->d_bdefer = nullptr;
+    ctx->h_bstate = nullptr;
+    ctx->batch_cap = 0; ctx->bdefer_cap = 0;
+    const size_t tk = (size_t)R360_TICKET_GROUPS * R360_TICKET_STRIDE;
+    R360_HIP(hipMalloc(&ctx->d_bstate, sizeof(IcpState) * cap));
+    R360_HIP(hipMalloc(&ctx->d_bpartials, sizeof(double) * 32 * (size_t)ctx->partials_cap * cap));
+    R360_HIP(hipMalloc(&ctx->d_bgticket, sizeof(unsigned) * tk * cap));
+    R360_HIP(hipMemset(ctx->d_bgticket, 0, sizeof(unsigned) * tk * cap));
+    R360_HIP(hipMalloc(&ctx->d_bdefer, sizeof(int) * (size_t)dcap * cap));
+    R360_HIP(hipHostMalloc(&ctx->h_bstate, sizeof(IcpState) * cap, hipHostMallocDefault));
+    ctx->batch_cap = cap;
+    ctx->bdefer_cap = dcap;
+    return 0;
+}
+
+// grid of one job's pass at level `level` of `geom` (the same for every job of a batch): the pass form and
+// the number of workgroups
+struct PassGrid { int pf, nb; };
+static PassGrid pass_grid(const r360_ctx* ctx, const LevelBufs& Ls, int occ) {
     // 4-pixel units on the large levels, one pixel per thread where that still fits one resident
     // round (latency-bound small levels); R360_ICP_PF=0/1 forces one form (experiments)
     static const int pf_env = env_int("R360_ICP_PF", -1);
     static const int cap_env = env_int("R360_ICP_CAP", -1);
     // one resident round: CUs x workgroups per CU of the launched form (grid-stride beyond it)
     struct Occ { int cus = 0, per[5] = {0, 0, 0, 0, 0}; };
-    static const Occ occ = [] {   // thread-safe one-time query (contexts may be driven from several threads)
+    static const Occ occ_q = [] {   // thread-safe one-time query (contexts may be driven from several threads)
         Occ o;
         int dev = 0;
         (void)hipGetDevice(&dev);
@@ -1306,18 +1351,66 @@ int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src
     const int npx = Ls.rows * Ls.cols;
     // PF 4 (compacted source points) for the plain pass; the occlusion variants index their flags by source
     // pixel and keep the image stream (PF 3 where rows split into whole waves)
-    const int pf = pf_env >= 0 && !(pf_env == 4 && C.occ) ? pf_env : (C.occ ? ((Ls.cols % 64 == 0) ? 3 : 0) : 4);
-    int cap = cap_env > 0 ? cap_env : occ.cus * (occ.per[pf] > 0 ? occ.per[pf] : 4);
+    const int pf = pf_env >= 0 && !(pf_env == 4 && occ) ? pf_env : (occ ? ((Ls.cols % 64 == 0) ? 3 : 0) : 4);
+    int cap = cap_env > 0 ? cap_env : occ_q.cus * (occ_q.per[pf] > 0 ? occ_q.per[pf] : 4);
     if (cap > ctx->partials_cap) cap = ctx->partials_cap;
     int nb = pf == 1 ? icp_blocks_for(npx) : (npx + TPB - 1) / TPB;
     if (nb > cap) nb = cap;
-    if (pf >= 3) {   // deferred-pixel queues: one per wave, room for every pixel the wave streams
-        const long stride = (long)nb * TPB;
-        const long need = (long)nb * (TPB / 64) * (((npx + stride - 1) / stride) * 64);
-        if (ctx->defer_cap < need) {
-            r360_set_error("deferred-pixel queue not sized for %d pixels (ensure_defer)", npx);
-            return -1;
-        }
+    return {pf, nb};
+}
+
+// deferred-queue entries one job's PF 3 / PF 4 pass needs: per wave ceil(npx / stride) * 64
+static long defer_need(int npx, int nb) {
+    const long stride = (long)nb * TPB;
+    return (long)nb * (TPB / 64) * (((npx + stride - 1) / stride) * 64);
+}
+
+static int launch_jobs(r360_ctx* ctx, const IcpJobs& jobs, int njobs, const LevelBufs& Ls, const LevelTrig& T,
+                       int level, int method, const IcpConst& C, int first, int eval_only, const PassGrid& G) {
+    const char* name = level == 0 ? "k_icp_pass_L0" : "k_icp_pass";
+    const int slot = timing_begin(ctx, name);
+    const int pf = G.pf, nb = G.nb;
+    const bool top = level == 0;
+#define R360_LAUNCH(M)                                                                                   \
+    do {                                                                                                 \
+        if (pf == 1) launch_pass<M, 1>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top);           \
+        else if (pf == 2) launch_pass<M, 2>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top);      \
+        else if (pf == 3) launch_pass<M, 3>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top);      \
+        else if (pf == 4) launch_pass<M, 4>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top);      \
+        else launch_pass<M, 0>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top);                   \
+    } while (0)
+    if (method == R360_PHOTO_CONSISTENCY) R360_LAUNCH(R360_PHOTO_CONSISTENCY);
+    else if (method == R360_DEPTH_CONSISTENCY) R360_LAUNCH(R360_DEPTH_CONSISTENCY);
+    else R360_LAUNCH(R360_PHOTO_DEPTH);
+#undef R360_LAUNCH
+    timing_end(ctx, slot);
+    R360_HIP(hipGetLastError());
+    return 0;
+}
+
+int launch_icp_jobs(r360_ctx* ctx, const IcpJobs& jobs, int n, const r360_frame* geom, int level, int method,
+                    const IcpConst& C, int first, int eval_only) {
+    if (C.occ) { r360_set_error("batched passes: occlusion variants run one alignment per launch"); return -2; }
+    if (n < 1 || n > R360_MAX_BATCH) { r360_set_error("batched passes: %d jobs (1..%d)", n, R360_MAX_BATCH); return -2; }
+    const LevelBufs& Ls = geom->lv[level];
+    const PassGrid G = pass_grid(ctx, Ls, 0);
+    if (G.pf >= 3 && ctx->bdefer_cap < defer_need(Ls.rows * Ls.cols, G.nb)) {
+        r360_set_error("batched passes: deferred-pixel queues not sized for %d pixels", Ls.rows * Ls.cols);
+        return -1;
+    }
+    return launch_jobs(ctx, jobs, n, Ls, geom->calib->trig[level], level, method, C, first, eval_only, G);
+}
+
+int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src, int level, int method,
+                     const IcpConst& C, int first, int eval_only) {
+    const LevelBufs& Ls = src->lv[level];
+    const LevelBufs& Lt = trg->lv[level];
+    const LevelTrig& T = src->calib->trig[level];
+    const PassGrid G = pass_grid(ctx, Ls, C.occ);
+    const int npx = Ls.rows * Ls.cols;
+    if (G.pf >= 3 && ctx->defer_cap < defer_need(npx, G.nb)) {   // one queue per wave, room for every pixel
+        r360_set_error("deferred-pixel queue not sized for %d pixels (ensure_defer)", npx);
+        return -1;
     }
     if (C.occ) {   // occlusion flags of this pass's pose (same stream, before the fused pass)
         if (ctx->occ_cap < npx) {
@@ -1359,22 +1452,9 @@ int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src
         timing_end(ctx, slot);
         R360_HIP(hipGetLastError());
     }
-    const char* name = level == 0 ? "k_icp_pass_L0" : "k_icp_pass";
-    const int* np = src->d_npts + level;
-    const int slot = timing_begin(ctx, name);
-#define R360_LAUNCH(M)                                                              \
-    do {                                                                            \
-        if (pf == 1) launch_pass<M, 1>(ctx, nb, Ls, Lt, T, C, first, eval_only, level == 0, np);   \
-        else if (pf == 2) launch_pass<M, 2>(ctx, nb, Ls, Lt, T, C, first, eval_only, level == 0, np); \
-        else if (pf == 3) launch_pass<M, 3>(ctx, nb, Ls, Lt, T, C, first, eval_only, level == 0, np); \
-        else if (pf == 4) launch_pass<M, 4>(ctx, nb, Ls, Lt, T, C, first, eval_only, level == 0, np); \
-        else launch_pass<M, 0>(ctx, nb, Ls, Lt, T, C, first, eval_only, level == 0, np);          \
-    } while (0)
-    if (method == R360_PHOTO_CONSISTENCY) R360_LAUNCH(R360_PHOTO_CONSISTENCY);
-    else if (method == R360_DEPTH_CONSISTENCY) R360_LAUNCH(R360_DEPTH_CONSISTENCY);
-    else R360_LAUNCH(R360_PHOTO_DEPTH);
-#undef R360_LAUNCH
-    timing_end(ctx, slot);
-    R360_HIP(hipGetLastError());
-    return 0;
+    IcpJobs jobs;
+    IcpJob& J = jobs.j[0];
+    J.src = Ls.p0; J.trg = Lt.p0; J.tg = Lt.tg; J.pts = Ls.pts; J.npts = src->d_npts + level;
+    J.S = ctx->d_state; J.partials = ctx->d_partials; J.gcnt = ctx->d_gticket; J.dq = ctx->d_defer;
+    return launch_jobs(ctx, jobs, 1, Ls, T, level, method, C, first, eval_only, G);
 }

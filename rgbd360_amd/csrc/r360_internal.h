@@ -86,6 +86,22 @@ struct alignas(16) IcpState {
     unsigned long long dbg[12];  // s_memrealtime stamps of the diagnostic build (-DR360_STAMPS)
 };
 
+// One alignment of a batched ICP launch (blockIdx.y = job): the pair's level buffers and its own GN state,
+// record area, arrival counters and deferred-pixel queue.  A single alignment is a batch of one.
+constexpr int R360_MAX_BATCH = R360_MAX_BATCH_ALIGN;
+struct IcpJob {
+    const float2* src;          // source level {gray, depth}
+    const float2* trg;          // target level {gray, depth}
+    const float4* tg;           // target level gradients
+    const float4* pts;          // source level compacted points (PF 4)
+    const int* npts;            // their count
+    IcpState* S;
+    double* partials;           // per-workgroup records
+    unsigned* gcnt;             // group arrival counters (R360_TICKET_GROUPS x R360_TICKET_STRIDE)
+    int* dq;                    // deferred-pixel queues
+};
+struct IcpJobs { IcpJob j[R360_MAX_BATCH]; };   // passed by value (kernel arguments, 1152 B)
+
 constexpr int R360_TICKET_GROUPS = 16;
 constexpr int R360_TICKET_STRIDE = 1024;   // uints between group counters (4 KB)
 
@@ -187,7 +203,8 @@ struct r360_ctx {
     int* d_defer = nullptr;          // ICP pass (PF 3): per-wave queues of deferred (exactly re-projected) pixels
     long defer_cap = 0;
     // in-kernel execution spans of the ICP passes (s_memrealtime, 100 MHz): [0] earliest workgroup start
-    // of the running pass, [1+l] summed spans at level l, [9+l] pass counts
+    // of the running pass, [1+l] summed spans at level l, [9+l] pass counts, [17] job arrivals of the running
+    // pass (low 32 bits: jobs arrived, high: jobs that ran; the last arrival closes the span)
     unsigned long long* d_ktime = nullptr;
     // occlusion variants: per-source target pixel / exact inverse range / flags, per-target counts,
     // offsets (exclusive scan) and the grouped source lists (icp_kernels.hip, k_occ_*)
@@ -210,6 +227,16 @@ struct r360_ctx {
     std::vector<std::pair<std::string, Acc>> acc;
     // async-align bookkeeping
     int async_nL = 0, async_pending = 0;
+    // batched alignFrames360 (r360_align360_batch_*): per-job state / records / counters / queues
+    int batch_cap = 0;               // jobs the batch buffers hold
+    long bdefer_cap = 0;             // deferred-queue entries per job
+    IcpState* d_bstate = nullptr;
+    double* d_bpartials = nullptr;   // [batch_cap][partials_cap][32]
+    unsigned* d_bgticket = nullptr;  // [batch_cap][R360_TICKET_GROUPS * R360_TICKET_STRIDE]
+    int* d_bdefer = nullptr;         // [batch_cap][bdefer_cap]
+    IcpState* h_bstate = nullptr;    // pinned
+    int batch_n = 0, batch_pending = 0;
+    std::vector<hipEvent_t> sync_ev; // producer-stream events the batch waits on
     // pinhole alignFrames (pinhole_kernels.hip): one state and one record area per job (sensor)
     IcpState* d_pin_state = nullptr;
     double* d_pin_partials = nullptr;
@@ -335,10 +362,18 @@ int launch_robot(r360_ctx* ctx, const RobotJob* d_jobs, const RobotGrid& grid, i
                  int finalize_levels);
 int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src, int level,
                      int method, const IcpConst& C, int first, int eval_only);
+// One pass over n jobs at pyramid level `level` (plain alignFrames360 only: C.occ == 0); the jobs' frames
+// share the level geometry of `geom`.  kt: the ctx's in-kernel span counters.
+int launch_icp_jobs(r360_ctx* ctx, const IcpJobs& jobs, int n, const r360_frame* geom, int level, int method,
+                    const IcpConst& C, int first, int eval_only);
 int icp_blocks_for(int n_pixels);
 // sizes ctx->d_defer for passes over up to n_pixels pixels (synchronises the ctx stream when it grows,
 // so it never frees a queue an enqueued pass still uses); call before enqueuing a level sequence
 int ensure_defer(r360_ctx* ctx, long n_pixels);
+// sizes ctx's batch buffers for n jobs over frames of up to n_pixels level-0 pixels (synchronises when growing)
+int ensure_batch(r360_ctx* ctx, int n, long n_pixels);
+// ctx's stream waits for the work enqueued so far on the streams of the frames' contexts
+int ctx_wait_frames(r360_ctx* ctx, r360_frame* const* frames, int n);
 int launch_cloud_normals(r360_frame* f);
 int launch_segmentation(r360_frame* f);
 int plane_bufs_alloc(r360_frame* f);

@@ -1,0 +1,135 @@
+"""GPU tests of the batched alignFrames360 (r360_align360_batch_async / _result): n pairs' passes run as one
+launch per pass, each pair with its own device Gauss-Newton state.
+
+The bar is identity with the single-pair path: every output of a batched pair (pose, Hessian, gradient,
+iteration counts, passes, SSO, error) is bit-identical to r360_align360 on that pair alone, under both the
+bench's timing schedule (exactly 20 level-0 iterations) and the reference schedule (RegisterPhotoICP.h:4611,
+where pairs converge after different numbers of iterations, so jobs of one launch exit at entry at different
+passes).  The single path itself is checked against the CPU oracle in test_gpu_dense.py; one pair of the batch
+is checked against the oracle here too."""
+import numpy as np
+import pytest
+
+import rgbd360_amd as R
+
+pytestmark = pytest.mark.gpu
+
+SEED = 360 << 16
+
+
+def _params(iters0):
+    p = R.IcpParams.default()
+    p.n_pyr = 5
+    p.std_dev_photo = np.float32(3.0 / 255)
+    p.fixed_iters_level0 = iters0
+    return p
+
+
+@pytest.fixture(scope="module")
+def seq():
+    """Seven VGA frames along the bench's camera path, built on two contexts (the batch ctx's stream must
+    wait for both), and one frame of an unrelated scene."""
+    ctxs = [R.Context(0), R.Context(0)]
+    cals = []
+    for c in ctxs:
+        cal = R.Calib360(c, 480, 640)
+        cal.loadExtrinsicCalibration(R.EXTRINSICS_DIR)
+        cals.append(cal)
+    frames = []
+    for i in range(7):
+        cal = cals[i % 2]
+        b, d = cal.synth_frame(SEED, R.synth_path_pose(SEED, 3 * i))
+        f = R.Frame360(cal)
+        f.upload(b, d)
+        f.build(R.BUILD_UNDISTORT | R.BUILD_SPHERE | R.BUILD_PYRAMID, sync=False)
+        frames.append(f)
+    b, d = cals[0].synth_frame(SEED + 7919, R.synth_path_pose(SEED + 7919, 40))
+    other = R.Frame360(cals[0])
+    other.upload(b, d)
+    other.build(R.BUILD_UNDISTORT | R.BUILD_SPHERE | R.BUILD_PYRAMID)
+    for c in ctxs:
+        c.sync()
+    yield dict(ctxs=ctxs, cals=cals, frames=frames, other=other)
+    for f in frames + [other]:
+        f.close()
+
+
+def _single(ctx, trg, src, init, params):
+    reg = R.RegisterPhotoICP(ctx)
+    reg.params = params
+    reg.setTargetFrame(trg)
+    reg.setSourceFrame(src)
+    rc = reg.alignFrames360(init, R.PHOTO_DEPTH)
+    return reg.getOptimalPose(), reg.getHessian(), reg.getGradient(), reg.stats, rc
+
+
+def _same(a_stats, b_stats):
+    for k in ("iters", "evals"):
+        assert list(getattr(a_stats, k)) == list(getattr(b_stats, k)), k
+    for k in ("illposed", "sso", "error", "passes"):
+        assert getattr(a_stats, k) == getattr(b_stats, k), k
+
+
+def _inits(frames, pairs):
+    # the true relative motion perturbed, as a PbMap initialisation would give it
+    out = []
+    for j, (t, s) in enumerate(pairs):
+        out.append(np.eye(4, dtype=np.float32) if j % 2 else None)
+    return out
+
+
+@pytest.mark.parametrize("iters0", [20, 0])
+def test_batch_equals_single(seq, iters0):
+    fr = seq["frames"]
+    pairs = [(fr[i], fr[i + 1]) for i in range(6)] + [(fr[0], seq["other"]), (fr[2], fr[5])]
+    inits = _inits(fr, pairs)
+    p = _params(iters0)
+    bctx = R.Context(0)
+    poses, H, g, st, ill = R.align360_batch(bctx, pairs, inits, R.PHOTO_DEPTH, p)
+    n_ill = 0
+    for j, (t, s) in enumerate(pairs):
+        sp, sH, sg, sst, rc = _single(seq["ctxs"][j % 2], t, s, inits[j], _params(iters0))
+        assert np.array_equal(poses[j], sp), j
+        assert np.array_equal(H[j], sH), j
+        assert np.array_equal(g[j], sg), j
+        _same(st[j], sst)
+        n_ill += rc
+    assert ill == n_ill
+    if iters0 == 0:   # the reference schedule: the pairs do not all stop at the same pass
+        assert len({tuple(s.iters[:5]) for s in st}) > 1
+    bctx.close()
+
+
+def test_batch_of_one_and_reuse(seq):
+    fr = seq["frames"]
+    p = _params(20)
+    bctx = R.Context(0)
+    for k in range(2):    # the ctx's batch buffers are reused across calls
+        poses, H, g, st, ill = R.align360_batch(bctx, [(fr[1], fr[2])], None, R.PHOTO_DEPTH, p)
+        sp, sH, sg, sst, rc = _single(seq["ctxs"][0], fr[1], fr[2], None, _params(20))
+        assert np.array_equal(poses[0], sp) and np.array_equal(H[0], sH)
+        _same(st[0], sst)
+    full = [(fr[i % 6], fr[i % 6 + 1]) for i in range(R.MAX_BATCH_ALIGN)]
+    poses, H, g, st, ill = R.align360_batch(bctx, full, None, R.PHOTO_DEPTH, p)
+    for j in range(6, R.MAX_BATCH_ALIGN):   # repeated pairs give repeated results
+        assert np.array_equal(poses[j], poses[j % 6])
+    with pytest.raises(RuntimeError):
+        R.align360_batch(bctx, full + full[:1], None, R.PHOTO_DEPTH, p)
+    bctx.close()
+
+
+def test_batch_pair_matches_oracle(seq):
+    """One batched pair against the CPU oracle's alignFrames360 on the same spheres (north-star tolerance)."""
+    from oracle import oracle360 as O
+    fr = seq["frames"]
+    p = _params(20)
+    bctx = R.Context(0)
+    poses, *_ = R.align360_batch(bctx, [(fr[3], fr[4]), (fr[4], fr[5])], None, R.PHOTO_DEPTH, p)
+    bctx.close()
+    for j, (t, s) in enumerate([(fr[3], fr[4]), (fr[4], fr[5])]):
+        tb, td = t.sphere()
+        sb, sd = s.sphere()
+        prm = O.IcpParams.default(n_pyr=5, std_dev_photo=np.float32(3.0 / 255), fixed_iters_level0=20)
+        _, opose, _, _, _ = O.align360(tb, td, sb, sd, None, O.PHOTO_DEPTH, prm)
+        assert O.rot_angle(poses[j], opose) <= 1e-4, j
+        assert np.linalg.norm(poses[j][:3, 3] - opose[:3, 3]) <= 1e-3, j
