@@ -207,6 +207,9 @@ def main():
     ap.add_argument("--workload", choices=["sequence", "dense"], default="sequence")
     ap.add_argument("--streams", type=int, default=16, help="max pipelines per GPU (host thread + HIP stream each)")
     ap.add_argument("--min-run", type=int, default=4, help="min pairs per pipeline run (each run rebuilds a halo frame)")
+    ap.add_argument("--queue", type=int, default=16,
+                    help="dense queue batch size (alignFrames360 of up to N pairs per launch); 0 = one launch per pair "
+                         "on each pipeline's stream")
     ap.add_argument("--emulate", type=str, default=None,
                     help="RANK/WORLD: run that rank's shard alone (single-GPU rehearsal of an N-GPU shard)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -255,8 +258,9 @@ def main():
     params.std_dev_photo = np.float32(3.0 / 255)       # OdometryRGBD360.cpp:92-95
     params.fixed_iters_level0 = args.iters0
     runner = OD.SequenceRunner(local, args.rows, args.cols, P, params, planes=args.workload == "sequence",
-                               dense_only=args.workload == "dense")
-    ctxs = runner.ctxs
+                               dense_only=args.workload == "dense", queue=args.queue)
+    ctxs = runner.ctxs + ([runner.queue.ctx] if runner.queue else [])
+    dense_ctx = runner.queue.ctx if runner.queue else ctxs[0]   # where pipeline 0's alignments run
 
     def barrier():
         if group is not None:
@@ -273,6 +277,7 @@ def main():
         c.timing(True)
         c.timing_reset()
         c.kernel_time_reset()
+    q0 = runner.queue.stats() if runner.queue else None
     t0 = time.perf_counter()
     runner.run(p0, p1, frames_of, rec, repeats=args.steps, runs=runs)
     if group is not None:   # RCCL gather of the pair records over xGMI
@@ -282,15 +287,20 @@ def main():
     traj = OD.compose(allrec[-1]) if rank == 0 else None   # OdometryRGBD360.cpp:257
     elapsed = time.perf_counter() - t0
     barrier()
-    l0_ms, l0_n, k0_us, k0_n, stage = 0.0, 0, 0.0, 0, {}
+    l0_ms, l0_n, k0_us, k0_n, k0_jobs, stage = 0.0, 0, 0.0, 0, 0, {}
+    qstats = None
+    if runner.queue:   # batches of the timed run
+        q1 = runner.queue.stats()
+        qstats = {"batches": q1["batches"] - q0["batches"], "jobs": q1["jobs"] - q0["jobs"], "max_batch": q1["max_batch"]}
     for c in ctxs:
         c.timing(False)
         ms, n = c.timing_read("k_icp_pass_L0")
         l0_ms += ms
         l0_n += n
-        us, n = c.kernel_time(0)
+        us, n, nj = c.kernel_stats(0)
         k0_us += us
         k0_n += n
+        k0_jobs += nj
         for name in ("k_undistort", "k_stitch", "k_pyramid", "k_cloud", "k_bilateral", "k_distmap", "k_normals",
                      "k_ccl", "k_plane_fit", "k_refine", "k_model_stats", "k_icp_pass", "k_icp_pass_L0"):
             ms, n = c.timing_read(name)
@@ -337,15 +347,16 @@ def main():
     # around a launch also count the time it waits behind the other pipelines' kernels.
     avg_ms = k0_us / max(k0_n, 1) * 1e-3
     event_ms = l0_ms / max(l0_n, 1)
-    achieved = alg_bytes / (avg_ms * 1e-3) / 1e9 if k0_n else None
+    pairs_per_launch = k0_jobs / max(k0_n, 1)      # a batched launch runs one level-0 pass per pair
+    achieved = pairs_per_launch * alg_bytes / (avg_ms * 1e-3) / 1e9 if k0_n else None
     # the same pass with the GPU to itself: pipeline 0 registers its run once more, alone
     for c in ctxs:
         c.kernel_time_reset()
     iso_rec = np.zeros((1, p1 - p0, OD.REC), np.float32)
     runner.run(p0, p1, frames_of, iso_rec, repeats=1, runs=runs[:1])
-    us, n = ctxs[0].kernel_time(0)
+    us, n, nj = dense_ctx.kernel_stats(0)
     iso_ms = us / max(n, 1) * 1e-3
-    iso_ach = alg_bytes / (iso_ms * 1e-3) / 1e9 if n else None
+    iso_ach = (nj / max(n, 1)) * alg_bytes / (iso_ms * 1e-3) / 1e9 if n else None
     probe = None
     if args.eval_probe:   # opt-in diagnostic: the level-0 pass in eval mode (no GN step) at identity, alone
         fa, fb = runner.frames[0]
@@ -395,6 +406,7 @@ def main():
             "workload": workload, "sensors": f"8x{args.cols}x{args.rows}", "sphere": f"{H0}x{W0}",
             "n_pyr": 5, "parallelism": f"pair-shard dp{world}", "pairs_per_step": pairs_job // args.steps,
             "pairs_per_step_this_rank": steps_pairs, "pipelines_per_gpu": P,
+            "dense_batch": args.queue,
             **({"emulated_shard": f"{shard_rank}/{shard_world}"} if args.emulate else {}),
         },
         "value_hbm_resident_inputs": resident,
@@ -403,8 +415,10 @@ def main():
             "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
             "traffic_profile": traffic_src,
             "kernel": "k_icp_pass<PHOTO_DEPTH> (level 0)", "avg_launch_ms": avg_ms, "launches": k0_n,
+            "pairs_per_launch": pairs_per_launch,
             "timing": "in-kernel execution span (s_memrealtime) over the timed region, all pipelines running",
-            "event_avg_launch_ms": event_ms, "bytes_per_launch": alg_bytes, "visible_frac": sso,
+            "event_avg_launch_ms": event_ms, "bytes_per_launch": pairs_per_launch * alg_bytes,
+            "bytes_per_pair_pass": alg_bytes, "visible_frac": sso,
             "isolated": {"avg_launch_ms": iso_ms, "launches": n, "achieved": iso_ach,
                          "frac": (iso_ach / HBM_PEAK_GBS) if iso_ach else None,
                          "note": "same pass, pipeline 0 alone on the GPU (its run once more after the timed region)"},
@@ -412,6 +426,7 @@ def main():
         },
         "stage_ms_per_pair": {k: v / max(args.steps * steps_pairs, 1) for k, v in stage.items()},
         "pipeline_host_ms_per_pair": host_ms,
+        **({"dense_queue": {**qstats, "mean_batch": qstats["jobs"] / max(qstats["batches"], 1)}} if qstats else {}),
         "frame_generation_s": round(gen_s, 1),
     }
     if rank == 0 and traj is not None:

@@ -179,6 +179,24 @@ int r360_align360_batch_async(r360_ctx* ctx, int n, r360_frame* const* trg, r360
                               const float* init, int method, const r360_icp_params* p);
 int r360_align360_batch_result(r360_ctx* ctx, float* pose_out, float* H_out, float* g_out, r360_icp_stats* st);
 
+/* Dense queue: the alignFrames360 calls of many concurrent registrations (one producer thread per pipeline
+ * of frame builds + PbMap stages, e.g. OdometryRGBD360.cpp:141-257 sharded over pipelines) batched on one
+ * stream.  A dispatcher thread runs every pending job (up to max_batch of one method / parameter set) as one
+ * r360_align360_batch call; the next batch accumulates while one runs.  submit records the frames' build
+ * work (their contexts' streams) and returns a ticket at once; collect waits for that job and returns
+ * what r360_align360_result would (0, 1 = ILL-POSED, < 0 error).  The frames must stay unmodified until
+ * their job is collected.  Every ticket must be collected once.  Thread-safe. */
+typedef struct r360_dense_queue r360_dense_queue;
+int  r360_dense_queue_create(int device, int max_batch, r360_dense_queue** out);
+void r360_dense_queue_destroy(r360_dense_queue* q);
+/* the queue's own context (stream, in-kernel span counters, per-launch timing) */
+r360_ctx* r360_dense_queue_ctx(r360_dense_queue* q);
+int  r360_dense_queue_stats(r360_dense_queue* q, long* batches, long* jobs, int* max_batch_seen);
+int  r360_dense_queue_submit(r360_dense_queue* q, r360_frame* trg, r360_frame* src, const float init[16],
+                             int method, const r360_icp_params* p, long* ticket);
+int  r360_dense_queue_collect(r360_dense_queue* q, long ticket, float pose_out[16], float H_out[36],
+                              float g_out[6], r360_icp_stats* st);
+
 /* One fused pass at a fixed pose: errorPhotoICP_sphere (:2545-2739) + calcHessGrad_sphere
  * (:2745-3228) at pyramid level `level`.  H/g in double (sum of the float per-pixel terms). */
 int r360_icp_eval(r360_ctx* ctx, r360_frame* trg, r360_frame* src, int level, const float pose[16],
@@ -337,6 +355,12 @@ int r360_register(r360_ctx* ctx, r360_frame* ref, r360_frame* trg, const float g
 int r360_register_async(r360_ctx* ctx, r360_frame* ref, r360_frame* trg, const float guess[16],
                         const r360_icp_params* p, size_t max_match_planes, int mode);
 int r360_register_result(r360_ctx* ctx, float pose[16], float info[36], r360_icp_stats* st);
+/* Register() with the dense stage on a dense queue: the PbMap stage runs at the call on ctx (waiting for the
+ * frames' plane builds), the rotOffset-conjugated alignFrames360 is submitted to q; collect waits for it and
+ * returns what r360_register_result returns. */
+int r360_register_submit(r360_ctx* ctx, r360_dense_queue* q, r360_frame* ref, r360_frame* trg, const float guess[16],
+                         const r360_icp_params* p, size_t max_match_planes, int mode, long* ticket);
+int r360_register_collect(r360_dense_queue* q, long ticket, float pose[16], float info[36], r360_icp_stats* st);
 /* SubgraphMatcher constraint tables (k_match_tables): unary [ns][nt], binary [(i*nt+j)][words]
  * bitsets over (k*nt+l).  Returns words.  Inspection/parity hook. */
 int r360_pbmap_match_tables(r360_ctx* ctx, r360_frame* ref, r360_frame* trg, size_t max_match_planes,
@@ -478,6 +502,8 @@ int r360_ctx_timing_reset(r360_ctx* ctx);
  * the end of the last workgroup, s_memrealtime), summed in microseconds, and the pass count, since the
  * last reset.  Unlike stream events they exclude queueing behind other streams' kernels. */
 int r360_ctx_kernel_time(r360_ctx* ctx, int level, double* us_sum, long* passes);
+/* the same, plus the job passes those launches ran (a batched launch runs one per pair; NULL skips) */
+int r360_ctx_kernel_stats(r360_ctx* ctx, int level, double* us_sum, long* launches, long* job_passes);
 int r360_ctx_kernel_time_reset(r360_ctx* ctx);
 
 #ifdef __cplusplus

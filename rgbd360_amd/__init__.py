@@ -195,6 +195,15 @@ _SIGS = [
     ("r360_align360_batch_async", C.c_int, [_P, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), _FP, C.c_int,
                                             C.POINTER(IcpParams)]),
     ("r360_align360_batch_result", C.c_int, [_P, _FP, _FP, _FP, C.POINTER(IcpStats)]),
+    ("r360_dense_queue_create", C.c_int, [C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
+    ("r360_dense_queue_destroy", None, [_P]),
+    ("r360_dense_queue_ctx", C.c_void_p, [_P]),
+    ("r360_dense_queue_stats", C.c_int, [_P, C.POINTER(C.c_long), C.POINTER(C.c_long), _IP]),
+    ("r360_dense_queue_submit", C.c_int, [_P, _P, _P, _FP, C.c_int, C.POINTER(IcpParams), C.POINTER(C.c_long)]),
+    ("r360_dense_queue_collect", C.c_int, [_P, C.c_long, _FP, _FP, _FP, C.POINTER(IcpStats)]),
+    ("r360_register_submit", C.c_int, [_P, _P, _P, _P, _FP, C.POINTER(IcpParams), C.c_size_t, C.c_int,
+                                       C.POINTER(C.c_long)]),
+    ("r360_register_collect", C.c_int, [_P, C.c_long, _FP, _FP, C.POINTER(IcpStats)]),
     ("r360_icp_eval", C.c_int, [_P, _P, _P, C.c_int, _FP, C.c_int, C.POINTER(IcpParams), _DP, _DP, _DP, _IP,
                                 _IP]),
     ("r360_icp_eval_occ", C.c_int, [_P, _P, _P, C.c_int, _FP, C.c_int, C.c_int, C.POINTER(IcpParams), _DP, _DP,
@@ -254,6 +263,8 @@ _SIGS = [
     ("r360_ctx_debug_stamps", C.c_int, [_P, C.POINTER(C.c_ulonglong)]),
     ("r360_ctx_kernel_time", C.c_int, [_P, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_long)]),
     ("r360_ctx_kernel_time_reset", C.c_int, [_P]),
+    ("r360_ctx_kernel_stats", C.c_int, [_P, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_long),
+                                        C.POINTER(C.c_long)]),
     ("r360_ctx_timing", C.c_int, [_P, C.c_int]),
     ("r360_ctx_timing_read", C.c_int, [_P, C.c_char_p, _DP, C.POINTER(C.c_long)]),
     ("r360_ctx_timing_reset", C.c_int, [_P]),
@@ -351,6 +362,12 @@ class Context:
         us, n = C.c_double(), C.c_long()
         _check(lib().r360_ctx_kernel_time(self.h, level, C.byref(us), C.byref(n)), "kernel_time")
         return us.value, n.value
+
+    def kernel_stats(self, level: int):
+        """(summed in-kernel span in us, launches, job passes) of the ICP passes at `level`."""
+        us, n, j = C.c_double(), C.c_long(), C.c_long()
+        _check(lib().r360_ctx_kernel_stats(self.h, level, C.byref(us), C.byref(n), C.byref(j)), "kernel_stats")
+        return us.value, n.value, j.value
 
     def kernel_time_reset(self):
         _check(lib().r360_ctx_kernel_time_reset(self.h), "kernel_time_reset")
@@ -841,6 +858,51 @@ def align360_batch(ctx: "Context", pairs, inits=None, method: int = PHOTO_CONSIS
     poses = np.stack([_from16(po[16 * j:16 * j + 16]) for j in range(n)])
     H = np.stack([Ho[36 * j:36 * j + 36].reshape(6, 6).T.copy() for j in range(n)])
     return poses, H, go.reshape(n, 6).copy(), list(st), ill
+
+
+class DenseQueue:
+    """The alignFrames360 stage of many concurrent registrations batched on one stream (r360_dense_queue):
+    submit from any thread, collect by ticket; a job's result equals the single-pair alignment."""
+
+    def __init__(self, device: int = 0, max_batch: int = MAX_BATCH_ALIGN):
+        h = C.c_void_p()
+        _check(lib().r360_dense_queue_create(device, max_batch, C.byref(h)), "r360_dense_queue_create")
+        self.h, self.device = h, device
+        ctx = Context.__new__(Context)      # non-owning view of the queue's own context (timing reads)
+        ctx.h, ctx.device = C.c_void_p(lib().r360_dense_queue_ctx(h)), device
+        ctx.close = lambda: None
+        self.ctx = ctx
+
+    def submit(self, trg: "Frame360", src: "Frame360", init=None, method: int = PHOTO_DEPTH,
+               params: "IcpParams" = None) -> int:
+        t = C.c_long()
+        i16 = _mat16(np.eye(4) if init is None else init)
+        _check(lib().r360_dense_queue_submit(self.h, trg.h, src.h, _fptr(i16), method,
+                                             C.byref(params or IcpParams.default()), C.byref(t)), "dense submit")
+        return t.value
+
+    def collect(self, ticket: int):
+        po, Ho, go = np.zeros(16, np.float32), np.zeros(36, np.float32), np.zeros(6, np.float32)
+        st = IcpStats()
+        rc = _check(lib().r360_dense_queue_collect(self.h, ticket, _fptr(po), _fptr(Ho), _fptr(go), C.byref(st)),
+                    "dense collect")
+        return _from16(po), Ho.reshape(6, 6).T.copy(), go, st, rc
+
+    def stats(self):
+        b, j, m = C.c_long(), C.c_long(), C.c_int()
+        _check(lib().r360_dense_queue_stats(self.h, C.byref(b), C.byref(j), C.byref(m)), "dense stats")
+        return {"batches": b.value, "jobs": j.value, "max_batch": m.value}
+
+    def close(self):
+        if self.h:
+            lib().r360_dense_queue_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class RegisterPhotoICP:

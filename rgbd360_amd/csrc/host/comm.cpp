@@ -45,13 +45,6 @@ const Rccl& rccl() {
 }
 }  // namespace
 
-#define CHECK_ARG(cond, msg)                  \
-    do {                                      \
-        if (!(cond)) {                        \
-            r360_set_error("%s", msg);        \
-            return -2;                        \
-        }                                     \
-    } while (0)
 
 #define R360_NCCL(call)                                                                  \
     do {                                                                                 \

@@ -1,0 +1,262 @@
+// dense_queue.cpp — the dense stage of many concurrent registrations, batched on one stream.
+//
+// OdometryRGBD360 registers every consecutive pair (OdometryRGBD360.cpp:141-257), and SphereGraphSLAM /
+// LoopClosure360 register a frame against several keyframes; each registration ends in one alignFrames360
+// (RegisterPhotoICP.h:4519-4784).  Producers (pipelines of frame builds + PbMap stages, one host thread each)
+// submit their alignments here; a dispatcher thread takes every pending alignment (up to R360_MAX_BATCH of
+// one method / parameter set) and runs them as ONE batched alignment (r360_align360_batch_async): one launch
+// per pass over all pairs instead of one small launch per pair and stream.  While a batch runs, the next one
+// accumulates, so the batch size follows the load.  A job's result is exactly the single-pair result.
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <mutex>
+#include "../r360_internal.h"
+
+extern "C" int r360_align360_batch_async(r360_ctx* ctx, int n, r360_frame* const* trg, r360_frame* const* src,
+                                         const float* init, int method, const r360_icp_params* p);
+int align360_batch_enqueue(r360_ctx* ctx, int n, r360_frame* const* trg, r360_frame* const* src, const float* init,
+                           int method, const r360_icp_params* p, bool wait_frames);
+
+struct r360_dense_queue {
+    r360_ctx* ctx = nullptr;           // the queue's own stream, GN states and batch buffers
+    int max_batch = R360_MAX_BATCH;
+    std::mutex m;
+    std::condition_variable cv_work, cv_done;
+    struct Job {
+        r360_frame* trg = nullptr;
+        r360_frame* src = nullptr;
+        float init[16];
+        int method = 0;
+        r360_icp_params p{};
+        hipEvent_t ev[2] = {nullptr, nullptr};   // the producers' streams up to the submit (frame builds)
+        int nev = 0;
+        int reg = 0, good = 0;                   // Register(): PbMap outcome and information
+        float info[36];
+        int done = 0, rc = 0;
+        std::string err;
+        float pose[16], H[36], g[6];
+        r360_icp_stats st{};
+    };
+    std::map<long, Job> jobs;
+    std::deque<long> pending;
+    long next = 1;
+    bool quit = false;
+    std::thread worker;
+    std::vector<hipEvent_t> ev_free;
+    long batches = 0, batched = 0;
+    int max_seen = 0;
+};
+
+static bool same_params(const r360_dense_queue::Job& a, const r360_dense_queue::Job& b) {
+    return a.method == b.method && memcmp(&a.p, &b.p, sizeof(r360_icp_params)) == 0;
+}
+
+static void dispatcher(r360_dense_queue* q) {
+    (void)hipSetDevice(q->ctx->device);
+    std::vector<long> take;
+    std::vector<r360_frame*> trg, src;
+    std::vector<float> init;
+    for (;;) {
+        std::unique_lock<std::mutex> lk(q->m);
+        q->cv_work.wait(lk, [&] { return q->quit || !q->pending.empty(); });
+        if (q->pending.empty()) break;   // quit with nothing pending
+        take.clear();
+        const r360_dense_queue::Job& first = q->jobs[q->pending.front()];
+        for (auto it = q->pending.begin(); it != q->pending.end() && (int)take.size() < q->max_batch;) {
+            if (same_params(q->jobs[*it], first)) { take.push_back(*it); it = q->pending.erase(it); }
+            else ++it;
+        }
+        const int n = (int)take.size();
+        trg.resize(n); src.resize(n); init.resize(16 * (size_t)n);
+        for (int j = 0; j < n; ++j) {
+            r360_dense_queue::Job& J = q->jobs[take[j]];
+            trg[j] = J.trg; src[j] = J.src;
+            memcpy(init.data() + 16 * j, J.init, sizeof J.init);
+        }
+        const int method = first.method;
+        const r360_icp_params p = first.p;
+        std::vector<hipEvent_t> evs;
+        for (long t : take) {
+            const r360_dense_queue::Job& J = q->jobs[t];
+            for (int e = 0; e < J.nev; ++e) evs.push_back(J.ev[e]);
+        }
+        lk.unlock();
+
+        int rc = 0;
+        for (hipEvent_t e : evs)
+            if (hipStreamWaitEvent(q->ctx->stream, e, 0) != hipSuccess) { r360_set_error("hipStreamWaitEvent failed"); rc = -1; }
+        if (rc == 0) rc = align360_batch_enqueue(q->ctx, n, trg.data(), src.data(), init.data(), method, &p, false);
+        std::vector<float> po(16 * (size_t)n), Ho(36 * (size_t)n), go(6 * (size_t)n);
+        std::vector<r360_icp_stats> st(n);
+        if (rc == 0) rc = r360_align360_batch_result(q->ctx, po.data(), Ho.data(), go.data(), st.data());
+        const std::string err = rc < 0 ? r360_last_error() : "";
+
+        lk.lock();
+        for (int j = 0; j < n; ++j) {
+            r360_dense_queue::Job& J = q->jobs[take[j]];
+            if (rc < 0) { J.rc = rc; J.err = err; }
+            else {
+                memcpy(J.pose, po.data() + 16 * j, sizeof J.pose);
+                memcpy(J.H, Ho.data() + 36 * j, sizeof J.H);
+                memcpy(J.g, go.data() + 6 * j, sizeof J.g);
+                J.st = st[j];
+                J.rc = st[j].illposed ? 1 : 0;
+            }
+            for (int e = 0; e < J.nev; ++e) q->ev_free.push_back(J.ev[e]);
+            J.nev = 0;
+            J.done = 1;
+        }
+        q->batches++;
+        q->batched += n;
+        if (n > q->max_seen) q->max_seen = n;
+        lk.unlock();
+        q->cv_done.notify_all();
+    }
+}
+
+extern "C" int r360_dense_queue_create(int device, int max_batch, r360_dense_queue** out) {
+    CHECK_ARG(out, "null out");
+    CHECK_ARG(max_batch >= 1 && max_batch <= R360_MAX_BATCH, "max_batch must be 1..R360_MAX_BATCH_ALIGN");
+    r360_ctx* ctx = nullptr;
+    if (int rc = r360_ctx_create(device, &ctx)) return rc;
+    auto* q = new r360_dense_queue;
+    q->ctx = ctx;
+    q->max_batch = max_batch;
+    q->worker = std::thread(dispatcher, q);
+    *out = q;
+    return 0;
+}
+
+extern "C" void r360_dense_queue_destroy(r360_dense_queue* q) {
+    if (!q) return;
+    {
+        std::lock_guard<std::mutex> lk(q->m);
+        q->quit = true;
+    }
+    q->cv_work.notify_all();
+    q->worker.join();
+    (void)hipSetDevice(q->ctx->device);
+    for (auto& kv : q->jobs)
+        for (int e = 0; e < kv.second.nev; ++e) hipEventDestroy(kv.second.ev[e]);
+    for (hipEvent_t e : q->ev_free) hipEventDestroy(e);
+    r360_ctx_destroy(q->ctx);
+    delete q;
+}
+
+extern "C" r360_ctx* r360_dense_queue_ctx(r360_dense_queue* q) { return q ? q->ctx : nullptr; }
+
+extern "C" int r360_dense_queue_stats(r360_dense_queue* q, long* batches, long* jobs, int* max_batch_seen) {
+    CHECK_ARG(q, "null queue");
+    std::lock_guard<std::mutex> lk(q->m);
+    if (batches) *batches = q->batches;
+    if (jobs) *jobs = q->batched;
+    if (max_batch_seen) *max_batch_seen = q->max_seen;
+    return 0;
+}
+
+static int queue_submit(r360_dense_queue* q, r360_frame* trg, r360_frame* src, const float init[16], int method,
+                        const r360_icp_params* p, int reg, int good, const float* info, long* ticket) {
+    CHECK_ARG(q && trg && src && init && p && ticket, "null arg");
+    CHECK_ARG(method >= 0 && method <= 2, "invalid method");
+    CHECK_ARG(trg->ctx->device == q->ctx->device && src->ctx->device == q->ctx->device,
+              "frames and queue on different devices");
+    CHECK_ARG((trg->built & R360_BUILD_PYRAMID) && (src->built & R360_BUILD_PYRAMID),
+              "frames need R360_BUILD_PYRAMID");
+    // events on the producers' streams: the batch waits for the frames' builds enqueued so far
+    hipStream_t streams[2] = {trg->ctx->stream, src->ctx->stream};
+    const int ns = streams[0] == streams[1] ? 1 : 2;
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    {
+        std::lock_guard<std::mutex> lk(q->m);
+        for (int i = 0; i < ns; ++i)
+            if (!q->ev_free.empty()) { ev[i] = q->ev_free.back(); q->ev_free.pop_back(); }
+    }
+    for (int i = 0; i < ns; ++i) {
+        if (!ev[i]) R360_HIP(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
+        R360_HIP(hipEventRecord(ev[i], streams[i]));
+    }
+    {
+        std::lock_guard<std::mutex> lk(q->m);
+        const long t = q->next++;
+        r360_dense_queue::Job& J = q->jobs[t];
+        J.trg = trg; J.src = src;
+        memcpy(J.init, init, sizeof J.init);
+        J.method = method;
+        J.p = *p;
+        J.ev[0] = ev[0]; J.ev[1] = ev[1]; J.nev = ns;
+        J.reg = reg; J.good = good;
+        if (info) memcpy(J.info, info, sizeof J.info);
+        q->pending.push_back(t);
+        *ticket = t;
+    }
+    q->cv_work.notify_one();
+    return 0;
+}
+
+// waits for job t and removes it; returns its rc (0, 1 = ILL-POSED, < 0 error)
+static int queue_collect(r360_dense_queue* q, long t, r360_dense_queue::Job& out) {
+    CHECK_ARG(q, "null queue");
+    std::unique_lock<std::mutex> lk(q->m);
+    auto it = q->jobs.find(t);
+    CHECK_ARG(it != q->jobs.end(), "unknown or already collected ticket");
+    q->cv_done.wait(lk, [&] { return it->second.done != 0; });
+    out = it->second;
+    q->jobs.erase(it);
+    lk.unlock();
+    if (out.rc < 0) { r360_set_error("%s", out.err.c_str()); return out.rc; }
+    return out.rc;
+}
+
+extern "C" int r360_dense_queue_submit(r360_dense_queue* q, r360_frame* trg, r360_frame* src, const float init[16],
+                                       int method, const r360_icp_params* p, long* ticket) {
+    return queue_submit(q, trg, src, init, method, p, 0, 0, nullptr, ticket);
+}
+
+extern "C" int r360_dense_queue_collect(r360_dense_queue* q, long ticket, float pose_out[16], float H_out[36],
+                                        float g_out[6], r360_icp_stats* st) {
+    r360_dense_queue::Job J;
+    const int rc = queue_collect(q, ticket, J);
+    if (rc < 0) return rc;
+    if (pose_out) memcpy(pose_out, J.pose, sizeof J.pose);
+    if (H_out) memcpy(H_out, J.H, sizeof J.H);
+    if (g_out) memcpy(g_out, J.g, sizeof J.g);
+    if (st) *st = J.st;
+    return rc;
+}
+
+// Register() with the dense stage on the queue: RegisterPbMap on the calling thread (ctx's matcher), the
+// rotOffset-conjugated initialisation (OdometryKeyFrame360.cpp:205-254), then the alignment is submitted.
+extern "C" int r360_register_submit(r360_ctx* ctx, r360_dense_queue* q, r360_frame* ref, r360_frame* trg,
+                                    const float guess[16], const r360_icp_params* p, size_t max_match_planes,
+                                    int mode, long* ticket) {
+    CHECK_ARG(ctx && q && ref && trg && p && ticket, "null arg");
+    float pb[16], inf[36];
+    for (int i = 0; i < 16; ++i) pb[i] = guess ? guess[i] : ((i % 5 == 0) ? 1.f : 0.f);
+    for (int i = 0; i < 36; ++i) inf[i] = 0.f;
+    const int good = r360_register_pbmap(ctx, ref, trg, max_match_planes, mode, pb, inf, nullptr, 0, nullptr, nullptr,
+                                         nullptr, nullptr);
+    if (good < 0) return good;
+    float Ro[16], Ri[16], t1[16], init[16];
+    r360_rot_offset(Ro, Ri);
+    r360_mul4(Ro, pb, t1);
+    r360_mul4(t1, Ri, init);                             // rotOffset * pose * rotOffset^-1
+    return queue_submit(q, ref, trg, init, R360_PHOTO_DEPTH, p, 1, good, inf, ticket);
+}
+
+extern "C" int r360_register_collect(r360_dense_queue* q, long ticket, float pose[16], float info[36],
+                                     r360_icp_stats* st) {
+    CHECK_ARG(pose, "null pose");
+    r360_dense_queue::Job J;
+    const int rc = queue_collect(q, ticket, J);
+    if (rc < 0) return rc;
+    CHECK_ARG(J.reg, "ticket is not a Register() job (r360_dense_queue_collect)");
+    float Ro[16], Ri[16], t2[16];
+    r360_rot_offset(Ro, Ri);
+    r360_mul4(Ri, J.pose, t2);
+    r360_mul4(t2, Ro, pose);                             // rotOffset^-1 * dense * rotOffset
+    if (info) memcpy(info, J.info, sizeof J.info);
+    if (st) *st = J.st;
+    return J.good ? 0 : 1;
+}

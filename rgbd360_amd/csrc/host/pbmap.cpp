@@ -26,13 +26,6 @@
 
 #include "../r360_internal.h"
 
-#define CHECK_ARG(cond, msg)                  \
-    do {                                      \
-        if (!(cond)) {                        \
-            r360_set_error("%s", msg);        \
-            return -2;                        \
-        }                                     \
-    } while (0)
 
 int launch_match_tables(r360_ctx* ctx, const float* d_desc, int ns, int nt, int mode, uint8_t* d_unary,
                         unsigned long long* d_bin, int words);

@@ -8,13 +8,6 @@
 
 #include "../r360_internal.h"
 
-#define CHECK_ARG(cond, msg)                  \
-    do {                                      \
-        if (!(cond)) {                        \
-            r360_set_error("%s", msg);        \
-            return -2;                        \
-        }                                     \
-    } while (0)
 
 namespace {
 

@@ -24,13 +24,6 @@ void r360_set_error(const char* fmt, ...) {
 extern "C" const char* r360_last_error(void) { return g_err.c_str(); }
 extern "C" const char* r360_version(void) { return "rgbd360_amd 0.1 (gfx950)"; }
 
-#define CHECK_ARG(cond, msg)                 \
-    do {                                     \
-        if (!(cond)) {                       \
-            r360_set_error("%s", msg);       \
-            return -2;                       \
-        }                                    \
-    } while (0)
 
 // ------------------------------------------------------------------ timing (HIP events on the ctx stream)
 int ctx_wait(r360_ctx* ctx) {
@@ -110,8 +103,8 @@ extern "C" int r360_ctx_create(int device, r360_ctx** out) {
     R360_HIP(hipMalloc(&c->d_partials, sizeof(double) * 32 * c->partials_cap));
     R360_HIP(hipMalloc(&c->d_gticket, sizeof(unsigned) * R360_TICKET_STRIDE * R360_TICKET_GROUPS));
     R360_HIP(hipMemset(c->d_gticket, 0, sizeof(unsigned) * R360_TICKET_STRIDE * R360_TICKET_GROUPS));
-    R360_HIP(hipMalloc(&c->d_ktime, sizeof(unsigned long long) * 18));
-    R360_HIP(hipMemset(c->d_ktime, 0, sizeof(unsigned long long) * 18));
+    R360_HIP(hipMalloc(&c->d_ktime, sizeof(unsigned long long) * R360_KT_SLOTS));
+    R360_HIP(hipMemset(c->d_ktime, 0, sizeof(unsigned long long) * R360_KT_SLOTS));
     R360_HIP(hipMemset(c->d_ktime, 0xff, sizeof(unsigned long long)));
     R360_HIP(hipHostMalloc(&c->h_state, sizeof(IcpState), hipHostMallocDefault));
     r360_match_params_default(&c->match);
@@ -143,20 +136,25 @@ extern "C" void r360_ctx_destroy(r360_ctx* c) {
     delete c;
 }
 
-extern "C" int r360_ctx_kernel_time(r360_ctx* ctx, int level, double* us_sum, long* passes) {
-    CHECK_ARG(ctx && level >= 0 && level < 8 && us_sum && passes, "invalid arguments");
-    unsigned long long k[17];
+extern "C" int r360_ctx_kernel_stats(r360_ctx* ctx, int level, double* us_sum, long* launches, long* job_passes) {
+    CHECK_ARG(ctx && level >= 0 && level < 8 && us_sum && launches, "invalid arguments");
+    unsigned long long k[R360_KT_SLOTS];
     if (ctx_wait(ctx)) return -1;
     R360_HIP(hipMemcpy(k, ctx->d_ktime, sizeof k, hipMemcpyDeviceToHost));
     *us_sum = (double)k[1 + level] * 0.01;   // 100 MHz ticks
-    *passes = (long)k[9 + level];
+    *launches = (long)k[9 + level];
+    if (job_passes) *job_passes = (long)k[18 + level];
     return 0;
+}
+
+extern "C" int r360_ctx_kernel_time(r360_ctx* ctx, int level, double* us_sum, long* passes) {
+    return r360_ctx_kernel_stats(ctx, level, us_sum, passes, nullptr);
 }
 
 extern "C" int r360_ctx_kernel_time_reset(r360_ctx* ctx) {
     CHECK_ARG(ctx, "null ctx");
     if (ctx_wait(ctx)) return -1;
-    R360_HIP(hipMemset(ctx->d_ktime, 0, sizeof(unsigned long long) * 18));
+    R360_HIP(hipMemset(ctx->d_ktime, 0, sizeof(unsigned long long) * R360_KT_SLOTS));
     R360_HIP(hipMemset(ctx->d_ktime, 0xff, sizeof(unsigned long long)));
     return 0;
 }
@@ -726,6 +724,9 @@ extern "C" int r360_align360(r360_ctx* ctx, r360_frame* trg, r360_frame* src, co
     return r360_align360_result(ctx, pose_out, H_out, g_out, st);
 }
 
+int align360_batch_enqueue(r360_ctx* ctx, int n, r360_frame* const* trg, r360_frame* const* src, const float* init,
+                           int method, const r360_icp_params* p, bool wait_frames);
+
 // Makes ctx's stream wait for the work already enqueued on the streams of the frames' contexts (their builds)
 int ctx_wait_frames(r360_ctx* ctx, r360_frame* const* frames, int n) {
     std::vector<hipStream_t> seen;
@@ -751,6 +752,12 @@ int ctx_wait_frames(r360_ctx* ctx, r360_frame* const* frames, int n) {
 
 extern "C" int r360_align360_batch_async(r360_ctx* ctx, int n, r360_frame* const* trg, r360_frame* const* src,
                                          const float* init, int method, const r360_icp_params* p) {
+    return align360_batch_enqueue(ctx, n, trg, src, init, method, p, true);
+}
+
+// wait_frames = false: the caller has already ordered ctx's stream after the frames' builds (dense queue)
+int align360_batch_enqueue(r360_ctx* ctx, int n, r360_frame* const* trg, r360_frame* const* src, const float* init,
+                           int method, const r360_icp_params* p, bool wait_frames) {
     CHECK_ARG(ctx && trg && src && init && p, "null arg");
     CHECK_ARG(n >= 1 && n <= R360_MAX_BATCH, "batch size must be 1..R360_MAX_BATCH");
     CHECK_ARG(!ctx->batch_pending, "a batch is pending on this ctx (r360_align360_batch_result)");
@@ -763,7 +770,7 @@ extern "C" int r360_align360_batch_async(r360_ctx* ctx, int n, r360_frame* const
     if (ensure_batch(ctx, n, (long)src[0]->lv[0].rows * src[0]->lv[0].cols)) return -1;
     std::vector<r360_frame*> fr;
     for (int j = 0; j < n; ++j) { fr.push_back(trg[j]); fr.push_back(src[j]); }
-    if (ctx_wait_frames(ctx, fr.data(), 2 * n)) return -1;
+    if (wait_frames && ctx_wait_frames(ctx, fr.data(), 2 * n)) return -1;
     for (int j = 0; j < n; ++j) {
         IcpState* h = ctx->h_bstate + j;
         memset(h, 0, sizeof(IcpState));

@@ -435,6 +435,7 @@ __device__ __forceinline__ void pass_arrive(unsigned long long* kt, bool ran, in
     const int lv = level & 7;
     kt[1 + lv] += t1 > t0 ? t1 - t0 : 0;
     kt[9 + lv] += 1;
+    kt[18 + lv] += (prev >> 32) + (ran ? 1 : 0);   // job passes (pairs) the launch ran
 }
 
 // TOP = 1 only renames the level-0 instantiation, so traces (rocprofv3) separate level 0 from level 1,

@@ -21,6 +21,15 @@ void r360_set_error(const char* fmt, ...);
         }                                                                               \
     } while (0)
 
+// argument check of a C-ABI entry point: sets the thread's error and returns -2
+#define CHECK_ARG(cond, msg)                 \
+    do {                                     \
+        if (!(cond)) {                       \
+            r360_set_error("%s", msg);       \
+            return -2;                       \
+        }                                    \
+    } while (0)
+
 // ------------------------------------------------------------------ device layouts
 // One pyramid level of a frame's sphere, as the fused ICP pass reads it:
 //   p0[i] = {gray, depth}          (source stream AND target gather)   8 B/px
@@ -102,6 +111,7 @@ struct IcpJob {
 };
 struct IcpJobs { IcpJob j[R360_MAX_BATCH]; };   // passed by value (kernel arguments, 1152 B)
 
+constexpr int R360_KT_SLOTS = 26;
 constexpr int R360_TICKET_GROUPS = 16;
 constexpr int R360_TICKET_STRIDE = 1024;   // uints between group counters (4 KB)
 
@@ -204,7 +214,8 @@ struct r360_ctx {
     long defer_cap = 0;
     // in-kernel execution spans of the ICP passes (s_memrealtime, 100 MHz): [0] earliest workgroup start
     // of the running pass, [1+l] summed spans at level l, [9+l] pass counts, [17] job arrivals of the running
-    // pass (low 32 bits: jobs arrived, high: jobs that ran; the last arrival closes the span)
+    // pass (low 32 bits: jobs arrived, high: jobs that ran; the last arrival closes the span), [18+l] job
+    // passes run at level l (a batched launch runs one per pair); R360_KT_SLOTS entries
     unsigned long long* d_ktime = nullptr;
     // occlusion variants: per-source target pixel / exact inverse range / flags, per-target counts,
     // offsets (exclusive scan) and the grouped source lists (icp_kernels.hip, k_occ_*)

@@ -23,7 +23,7 @@ import time
 import numpy as np
 
 from . import (BUILD_PLANES, BUILD_PYRAMID, BUILD_SPHERE, BUILD_UNDISTORT, PHOTO_DEPTH, PLANAR_3DoF, Calib360,
-               Context, Frame360, IcpParams, IcpStats, EXTRINSICS_DIR, C, _fptr, lib)
+               Context, DenseQueue, Frame360, IcpParams, IcpStats, EXTRINSICS_DIR, C, _fptr, lib)
 
 SEQ_FRAMES = 256
 # one pair record: pose (16, column-major, rig frame of the pair's first frame), the PbMap information
@@ -95,12 +95,19 @@ def trajectory_error(T: np.ndarray, gt: np.ndarray) -> dict:
 
 class SequenceRunner:
     """P pipelines on one GPU, each an r360_ctx (HIP stream + device GN state) driven by its own host thread
-    (ctypes drops the GIL inside the library), each with two Frame360 buffers used in turn."""
+    (ctypes drops the GIL inside the library), each with two Frame360 buffers used in turn.
+
+    queue > 0: the pipelines' alignFrames360 calls go to one dense queue (r360_dense_queue, batches of up to
+    `queue` pairs per launch on the queue's stream) and each pipeline keeps one alignment in flight while it
+    builds and PbMap-registers the next frame (three Frame360 buffers in turn).  Every record is identical to
+    the unqueued run's (a batched alignment equals the single-pair one bit for bit)."""
 
     def __init__(self, device: int, rows: int, cols: int, pipelines: int, params: IcpParams,
-                 planes: bool = True, max_match_planes: int = 25, mode: int = PLANAR_3DoF, dense_only: bool = False):
+                 planes: bool = True, max_match_planes: int = 25, mode: int = PLANAR_3DoF, dense_only: bool = False,
+                 queue: int = 0):
         self.P = pipelines
         self.dense_only = dense_only
+        self.queue = DenseQueue(device, queue) if queue > 0 else None
         self.params = params
         self.max_match_planes, self.mode = max_match_planes, mode
         self.flags = BUILD_UNDISTORT | BUILD_SPHERE | BUILD_PYRAMID | (BUILD_PLANES if planes else 0)
@@ -110,7 +117,7 @@ class SequenceRunner:
             cal = Calib360(c, rows, cols)
             cal.loadExtrinsicCalibration(EXTRINSICS_DIR)
             self.cals.append(cal)
-            self.frames.append([Frame360(cal), Frame360(cal)])
+            self.frames.append([Frame360(cal) for _ in range(3 if self.queue else 2)])
         self.stats = [IcpStats() for _ in range(pipelines)]
         # host-side time per pipeline: [load + build enqueue, PbMap stage (register_async), dense wait, pairs]
         self.host_s = np.zeros((pipelines, 4))
@@ -168,6 +175,73 @@ class SequenceRunner:
             rec[R_ERR] = self.stats[p].error
             fa, fb = fb, fa
 
+    def _pipeline_queued(self, p: int, run: tuple[int, int], frames_of, out: np.ndarray, p0: int,
+                         device_inputs: bool):
+        """_pipeline with the dense stage on the queue: submit pair i, then collect pair i-1 (so one alignment
+        per pipeline is in flight while the next frame is built and PbMap-registered).  Frame i+1 goes into
+        the buffer of frame i-2, whose pair (i-2, i-1) was collected in the previous iteration."""
+        L = lib()
+        ctx = self.ctxs[p]
+        fr = self.frames[p]
+        a, b = run
+        q = self.queue
+        hs = self.host_s[p]
+
+        def load(f, i):
+            if device_inputs:
+                f.upload_device(*frames_of(i))
+            else:
+                f.upload_async(*frames_of(i))
+
+        def finish(ticket, i, st):
+            rec = out[i - p0]
+            pose, info = np.zeros(16, np.float32), np.zeros(36, np.float32)
+            if self.dense_only:
+                dense = np.zeros(16, np.float32)
+                rc = L.r360_dense_queue_collect(q.h, ticket, _fptr(dense), None, None, C.byref(st))
+                if rc < 0:
+                    raise RuntimeError(f"r360_dense_queue_collect: {L.r360_last_error()}")
+                pose = (ROT_OFFSET_INV @ dense.reshape(4, 4).T.astype(np.float64) @ ROT_OFFSET).T.reshape(16)
+                rc = 0
+            else:
+                rc = L.r360_register_collect(q.h, ticket, _fptr(pose), _fptr(info), C.byref(st))
+                if rc < 0:
+                    raise RuntimeError(f"r360_register_collect: {L.r360_last_error()}")
+            rec[R_POSE:R_POSE + 16] = pose
+            rec[R_INFO:R_INFO + 36] = info
+            rec[R_STATUS] = 2 if st.illposed else rc
+            rec[R_SSO] = st.sso
+            rec[R_ERR] = st.error
+
+        load(fr[0], a)
+        fr[0].build(self.flags, sync=False)
+        pending = None
+        sts = [IcpStats(), IcpStats()]
+        for i in range(a, b):
+            t0 = time.perf_counter()
+            cur, nxt = fr[(i - a) % 3], fr[(i + 1 - a) % 3]
+            load(nxt, i + 1)
+            nxt.build(self.flags, sync=False)
+            t1 = time.perf_counter()
+            ticket = C.c_long()
+            if self.dense_only:
+                rc = L.r360_dense_queue_submit(q.h, cur.h, nxt.h, _fptr(self.eye), PHOTO_DEPTH, C.byref(self.params),
+                                               C.byref(ticket))
+            else:
+                rc = L.r360_register_submit(ctx.h, q.h, cur.h, nxt.h, _fptr(self.eye), C.byref(self.params),
+                                            self.max_match_planes, self.mode, C.byref(ticket))
+            if rc != 0:
+                raise RuntimeError(f"submit: {L.r360_last_error()}")
+            t2 = time.perf_counter()
+            if pending is not None:
+                finish(*pending)
+            pending = (ticket.value, i, sts[i % 2])
+            hs += (t1 - t0, t2 - t1, time.perf_counter() - t2, 1)
+        if pending is not None:
+            t2 = time.perf_counter()
+            finish(*pending)
+            hs[2] += time.perf_counter() - t2
+
     def run(self, p0: int, p1: int, frames_of, out: np.ndarray, repeats: int = 1, runs=None,
             device_inputs: bool = False):
         """Registers pairs [p0, p1) `repeats` times (out: (repeats, p1 - p0, REC)); frames_of(i) returns
@@ -176,9 +250,11 @@ class SequenceRunner:
         runs = runs or split_range(p0, p1, self.P)
         assert len(runs) <= self.P
 
+        body = self._pipeline_queued if self.queue else self._pipeline
+
         def worker(p):
             for r in range(repeats):
-                self._pipeline(p, runs[p], frames_of, out[r], p0, device_inputs)
+                body(p, runs[p], frames_of, out[r], p0, device_inputs)
         for f in [self.pool.submit(worker, p) for p in range(len(runs))]:
             f.result()
         for c in self.ctxs:
@@ -186,6 +262,8 @@ class SequenceRunner:
 
     def close(self):
         self.pool.shutdown()
+        if self.queue:
+            self.queue.close()
         for fr in self.frames:
             for f in fr:
                 f.close()

@@ -115,3 +115,18 @@ def test_trajectory_follows_ground_truth(seq):
     print(e)
     # drift of the composed odometry over the closed 256-frame loop
     assert e["max_rot_err_deg"] < 2.0 and e["max_trans_err_m"] < 0.02 * e["path_length_m"], e
+
+
+def test_queued_dense_stage_reproduces_the_records(seq):
+    """The same 255 pairs with the alignments batched on a dense queue (r360_dense_queue, up to 16 pairs per
+    launch, one alignment in flight per pipeline): every record is bit-identical to the unqueued run's."""
+    bgr, dep = seq["bgr"], seq["dep"]
+    runner = OD.SequenceRunner(0, 480, 640, 16, seq["params"], queue=16)
+    try:
+        rec = np.zeros((1, 255, OD.REC), np.float32)
+        runner.run(0, 255, lambda i: (bgr[i], dep[i]), rec)
+        st = runner.queue.stats()
+    finally:
+        runner.close()
+    assert st["jobs"] == 255 and st["batches"] < 255
+    assert np.array_equal(rec[0], seq["rec"])
