@@ -116,6 +116,20 @@ class RankGroup:
         self.dist.destroy_process_group()
 
 
+def thread_cpu_s():
+    """CPU seconds (user + system) per live OS thread of this process: {tid: seconds}."""
+    out = {}
+    tck = os.sysconf("SC_CLK_TCK")
+    for t in os.listdir("/proc/self/task"):
+        try:
+            f = open(f"/proc/self/task/{t}/stat").read()
+            fields = f[f.rindex(")") + 2:].split()
+            out[int(t)] = (int(fields[11]) + int(fields[12])) / tck
+        except (OSError, ValueError, IndexError):
+            pass
+    return out
+
+
 def host_cpu_info():
     """Host cores usable by this process (affinity and cgroup quota) and the CPU model string."""
     aff = len(os.sched_getaffinity(0))
@@ -204,9 +218,11 @@ def main():
     ap.add_argument("--cols", type=int, default=640)
     ap.add_argument("--iters0", type=int, default=20)
     ap.add_argument("--frames", type=int, default=256, help="sequence length (frames)")
-    ap.add_argument("--workload", choices=["sequence", "dense"], default="sequence")
+    ap.add_argument("--workload", choices=["sequence", "dense", "planes"], default="sequence")
     ap.add_argument("--streams", type=int, default=16, help="max pipelines per GPU (host thread + HIP stream each)")
     ap.add_argument("--min-run", type=int, default=4, help="min pairs per pipeline run (each run rebuilds a halo frame)")
+    ap.add_argument("--stage-timing", action="store_true",
+                    help="diagnostic: HIP events around EVERY launch of the timed run (per-stage times; slows the run)")
     ap.add_argument("--queue", type=int, default=16,
                     help="dense queue batch size (alignFrames360 of up to N pairs per launch); 0 = one launch per pair "
                          "on each pipeline's stream")
@@ -257,8 +273,9 @@ def main():
     params.n_pyr = 5
     params.std_dev_photo = np.float32(3.0 / 255)       # OdometryRGBD360.cpp:92-95
     params.fixed_iters_level0 = args.iters0
-    runner = OD.SequenceRunner(local, args.rows, args.cols, P, params, planes=args.workload == "sequence",
-                               dense_only=args.workload == "dense", queue=args.queue)
+    runner = OD.SequenceRunner(local, args.rows, args.cols, P, params, planes=args.workload != "dense",
+                               dense_only=args.workload == "dense", queue=args.queue,
+                               planes_only=args.workload == "planes")
     ctxs = runner.ctxs + ([runner.queue.ctx] if runner.queue else [])
     dense_ctx = runner.queue.ctx if runner.queue else ctxs[0]   # where pipeline 0's alignments run
 
@@ -273,11 +290,15 @@ def main():
     rec = np.zeros((args.steps, p1 - p0, OD.REC), np.float32)
     runner.host_s[:] = 0
     barrier()
+    # HIP events around the level-0 passes (on the stream they are launched on); every launch only with
+    # --stage-timing (events around every plane kernel of 16 streams cost throughput)
     for c in ctxs:
-        c.timing(True)
+        c.timing(1 if args.stage_timing else 2)
         c.timing_reset()
         c.kernel_time_reset()
     q0 = runner.queue.stats() if runner.queue else None
+    ru0 = os.times()
+    th0 = thread_cpu_s()
     t0 = time.perf_counter()
     runner.run(p0, p1, frames_of, rec, repeats=args.steps, runs=runs)
     if group is not None:   # RCCL gather of the pair records over xGMI
@@ -286,6 +307,15 @@ def main():
         allrec, sizes = rec, [p1 - p0]
     traj = OD.compose(allrec[-1]) if rank == 0 else None   # OdometryRGBD360.cpp:257
     elapsed = time.perf_counter() - t0
+    ru1 = os.times()
+    th1 = thread_cpu_s()
+    host_cores_busy = ((ru1.user - ru0.user) + (ru1.system - ru0.system)) / elapsed   # this rank's process
+    pipe_s = sum(th1[t] - th0.get(t, 0.0) for t in th1 if t in runner.native_ids)
+    live_s = sum(th1[t] - th0.get(t, 0.0) for t in th1 if t not in runner.native_ids)
+    host_split = {"pipeline_threads": round(pipe_s / elapsed, 2), "other_live_threads": round(live_s / elapsed, 2),
+                  "exited_threads": round(host_cores_busy - (pipe_s + live_s) / elapsed, 2),
+                  "other_live_top": sorted((round((th1[t] - th0.get(t, 0.0)) / elapsed, 2) for t in th1
+                                            if t not in runner.native_ids), reverse=True)[:6]}
     barrier()
     l0_ms, l0_n, k0_us, k0_n, k0_jobs, stage = 0.0, 0, 0.0, 0, 0, {}
     qstats = None
@@ -322,7 +352,7 @@ def main():
             return dB.ptr(i - p0), dD.ptr(i - p0)
         rec2 = np.zeros((args.steps, p1 - p0, OD.REC), np.float32)
         for c in ctxs:
-            c.timing(True)       # same per-launch event instrumentation as the headline run
+            c.timing(1 if args.stage_timing else 2)   # same event instrumentation as the headline run
         barrier()
         t1 = time.perf_counter()
         runner.run(p0, p1, dev_of, rec2, repeats=args.steps, runs=runs, device_inputs=True)
@@ -393,6 +423,9 @@ def main():
                     "PLANAR_3DoF) + alignFrames360(PHOTO_DEPTH) from the rotOffset-conjugated PbMap pose "
                     f"(levels 4..1 reference schedule + {args.iters0} GN iterations at level 0), pose gather + "
                     "trajectory composition on rank 0")
+    elif args.workload == "planes":
+        workload = ("config2 over the config4 sequence: per pair upload + Frame360 build with planes (PbMap) + "
+                    "RegisterPbMap(25 planes, PLANAR_3DoF), no alignFrames360")
     else:
         workload = (("config5" if args.rows == 960 else "config3") + f": synthetic 8x{args.cols}x{args.rows} "
                     f"{args.frames}-frame sequence; per pair: upload, stitch + 5-level pyramid, "
@@ -424,8 +457,11 @@ def main():
                          "note": "same pass, pipeline 0 alone on the GPU (its run once more after the timed region)"},
             **({"eval_probe": probe} if probe else {}),
         },
-        "stage_ms_per_pair": {k: v / max(args.steps * steps_pairs, 1) for k, v in stage.items()},
+        **({"stage_ms_per_pair": {k: v / max(args.steps * steps_pairs, 1) for k, v in stage.items()}}
+           if args.stage_timing else {}),
         "pipeline_host_ms_per_pair": host_ms,
+        "host_cores_busy": round(host_cores_busy, 2),
+        "host_cores_split": host_split,
         **({"dense_queue": {**qstats, "mean_batch": qstats["jobs"] / max(qstats["batches"], 1)}} if qstats else {}),
         "frame_generation_s": round(gen_s, 1),
     }

@@ -494,6 +494,7 @@ int r360_libm_eval(const float* x, const float* y, const float* z, int n, float*
 int r360_ctx_debug_stamps(r360_ctx* ctx, unsigned long long* out12);
 
 /* ---------------------------------------------------------------- timing hooks (bench) */
+/* enable: 0 off, 1 every launch on ctx's stream, 2 the level-0 ICP passes only (HIP events around each) */
 int r360_ctx_timing(r360_ctx* ctx, int enable);
 /* Per-kernel accumulated device time (ms) and launch counts since the last reset. */
 int r360_ctx_timing_read(r360_ctx* ctx, const char* kernel, double* ms, long* launches);

@@ -346,7 +346,8 @@ class Context:
     def sync(self):
         _check(lib().r360_ctx_sync(self.h), "r360_ctx_sync")
 
-    def timing(self, enable: bool):
+    def timing(self, enable):
+        """0/False off, 1/True HIP events around every launch, 2 around the level-0 ICP passes only."""
         _check(lib().r360_ctx_timing(self.h, int(enable)), "timing")
 
     def timing_read(self, kernel: str):

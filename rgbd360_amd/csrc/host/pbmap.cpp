@@ -413,7 +413,7 @@ int planes_enqueue(r360_frame* f) {
     P.worker_err.clear();
     P.worker = new std::thread([f] {
         PlaneBufs& Q = f->pl;
-        if (hipEventSynchronize(Q.done) != hipSuccess) {
+        if (event_wait(Q.done) != 0) {
             Q.worker_rc = -1;
             Q.worker_err = "plane build: GPU work failed";
             return;

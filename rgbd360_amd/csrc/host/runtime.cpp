@@ -1,7 +1,9 @@
 // runtime.cpp — host side of librgbd360_hip.so: contexts, Calib360, Frame360 and the
 // RegisterPhotoICP::alignFrames360 driver.  Everything here is plumbing around the HIP kernels
 // (frame_kernels.hip, icp_kernels.hip); the per-pixel work never runs on the CPU.
+#include <chrono>
 #include <cmath>
+#include <thread>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -26,14 +28,30 @@ extern "C" const char* r360_version(void) { return "rgbd360_amd 0.1 (gfx950)"; }
 
 
 // ------------------------------------------------------------------ timing (HIP events on the ctx stream)
+// Waits for a recorded event by polling it with short sleeps.  hipEventSynchronize spins a core for the
+// whole wait even on a blocking-sync event (measured: every per-frame assembly thread and pipeline thread
+// of the bench burned its wait, 15 of 16 host cores at 16 pipelines), and a sleeping poll gives the cores
+// back to the PbMap host stages; the added latency is at most one sleep (<= 100 us) on ms-scale waits.
+int event_wait(hipEvent_t e) {
+    for (int k = 0;; ++k) {
+        const hipError_t r = hipEventQuery(e);
+        if (r == hipSuccess) return 0;
+        if (r != hipErrorNotReady) {
+            r360_set_error("hipEventQuery -> %s", hipGetErrorString(r));
+            return -1;
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(k < 8 ? 20 : k < 32 ? 50 : 100));
+    }
+}
+
 int ctx_wait(r360_ctx* ctx) {
     R360_HIP(hipEventRecord(ctx->wait_ev, ctx->stream));
-    R360_HIP(hipEventSynchronize(ctx->wait_ev));
-    return 0;
+    return event_wait(ctx->wait_ev);
 }
 
 int timing_begin(r360_ctx* ctx, const char* name) {
     if (!ctx || !ctx->timing) return -1;
+    if (ctx->timing == 2 && strcmp(name, "k_icp_pass_L0") != 0) return -1;   // level-0 passes only
     if (ctx->ev_used + 2 > (int)ctx->ev_pool.size()) {
         for (int i = 0; i < 64; ++i) {
             hipEvent_t e;

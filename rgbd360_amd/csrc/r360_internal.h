@@ -403,4 +403,6 @@ int  timing_begin(r360_ctx* ctx, const char* name);
 // Wait for everything enqueued on the context's stream, sleeping (blocking-sync event) rather than
 // spinning, so many pipelines' host threads can wait while plane assembly threads keep the cores.
 int  ctx_wait(r360_ctx* ctx);
+// waits for a recorded event, polling it with short sleeps (no core spins for the wait)
+int  event_wait(hipEvent_t e);
 void timing_end(r360_ctx* ctx, int slot);

@@ -104,9 +104,12 @@ class SequenceRunner:
 
     def __init__(self, device: int, rows: int, cols: int, pipelines: int, params: IcpParams,
                  planes: bool = True, max_match_planes: int = 25, mode: int = PLANAR_3DoF, dense_only: bool = False,
-                 queue: int = 0):
+                 queue: int = 0, planes_only: bool = False):
         self.P = pipelines
         self.dense_only = dense_only
+        self.planes_only = planes_only
+        if planes_only:
+            queue = 0
         self.queue = DenseQueue(device, queue) if queue > 0 else None
         self.params = params
         self.max_match_planes, self.mode = max_match_planes, mode
@@ -122,6 +125,7 @@ class SequenceRunner:
         # host-side time per pipeline: [load + build enqueue, PbMap stage (register_async), dense wait, pairs]
         self.host_s = np.zeros((pipelines, 4))
         self.pool = ThreadPoolExecutor(max_workers=pipelines)
+        self.native_ids = set()   # OS thread ids of the pipeline threads (host CPU accounting)
         self.eye = np.eye(4, dtype=np.float32).reshape(16)
 
     def _pipeline(self, p: int, run: tuple[int, int], frames_of, out: np.ndarray, p0: int, device_inputs: bool):
@@ -148,7 +152,14 @@ class SequenceRunner:
             t1 = time.perf_counter()
             rec = out[i - p0]
             pose, info = np.zeros(16, np.float32), np.zeros(36, np.float32)
-            if self.dense_only:   # alignFrames360 from identity (configs 3 / 5), pose conjugated back to the rig
+            if self.planes_only:   # configs[1]: the PbMap stage alone (RegisterPbMap), no alignFrames360
+                rc = L.r360_register_pbmap(ctx.h, fa.h, fb.h, self.max_match_planes, self.mode, _fptr(pose),
+                                           _fptr(info), None, 0, None, None, None, None)
+                if rc < 0:
+                    raise RuntimeError(f"r360_register_pbmap: {L.r360_last_error()}")
+                rc = 0 if rc == 1 else 1
+                hs += (t1 - t0, time.perf_counter() - t1, 0, 1)
+            elif self.dense_only:   # alignFrames360 from identity (configs 3 / 5), pose conjugated back to the rig
                 rc = L.r360_align360_async(ctx.h, fa.h, fb.h, _fptr(self.eye), PHOTO_DEPTH, 0, C.byref(self.params))
                 if rc != 0:
                     raise RuntimeError(f"r360_align360_async: {L.r360_last_error()}")
@@ -253,6 +264,8 @@ class SequenceRunner:
         body = self._pipeline_queued if self.queue else self._pipeline
 
         def worker(p):
+            import threading
+            self.native_ids.add(threading.get_native_id())
             for r in range(repeats):
                 body(p, runs[p], frames_of, out[r], p0, device_inputs)
         for f in [self.pool.submit(worker, p) for p in range(len(runs))]:
