@@ -361,6 +361,11 @@ int r360_register_result(r360_ctx* ctx, float pose[16], float info[36], r360_icp
 int r360_register_submit(r360_ctx* ctx, r360_dense_queue* q, r360_frame* ref, r360_frame* trg, const float guess[16],
                          const r360_icp_params* p, size_t max_match_planes, int mode, long* ticket);
 int r360_register_collect(r360_dense_queue* q, long ticket, float pose[16], float info[36], r360_icp_stats* st);
+/* Parity hook: the two raster sweeps of OrganizedMultiPlaneSegmentation::refine as k_refine* run them, on
+ * 8 sensors' refinement states (-1 no label, -2 non-planar label, m >= 0 planar model m) and closeness
+ * masks (bit m: the pixel is within 0.02 of model m), w x h each; rb rows per band (0 = one wave per sensor
+ * walks all rows).  out = the swept states. */
+int r360_refine_eval(const int8_t* state, const uint64_t* mask, int w, int h, int rb, int8_t* out);
 /* SubgraphMatcher constraint tables (k_match_tables): unary [ns][nt], binary [(i*nt+j)][words]
  * bitsets over (k*nt+l).  Returns words.  Inspection/parity hook. */
 int r360_pbmap_match_tables(r360_ctx* ctx, r360_frame* ref, r360_frame* trg, size_t max_match_planes,

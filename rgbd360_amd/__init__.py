@@ -195,6 +195,7 @@ _SIGS = [
     ("r360_align360_batch_async", C.c_int, [_P, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), _FP, C.c_int,
                                             C.POINTER(IcpParams)]),
     ("r360_align360_batch_result", C.c_int, [_P, _FP, _FP, _FP, C.POINTER(IcpStats)]),
+    ("r360_refine_eval", C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, _P]),
     ("r360_dense_queue_create", C.c_int, [C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
     ("r360_dense_queue_destroy", None, [_P]),
     ("r360_dense_queue_ctx", C.c_void_p, [_P]),
@@ -1062,6 +1063,16 @@ class RegisterPhotoICP:
                                        C.byref(self.params), H.ctypes.data_as(_DP), g.ctypes.data_as(_DP),
                                        C.byref(e), C.byref(nv), C.byref(nvis)), "icp_eval_occ")
         return H.reshape(6, 6), g, e.value, nv.value, nvis.value
+
+
+def refine_eval(state: np.ndarray, mask: np.ndarray, rb: int = 0) -> np.ndarray:
+    """refine()'s two sweeps on the device (parity hook): state int8 (8, h, w), mask uint64 (8, h, w)."""
+    state = np.ascontiguousarray(state, np.int8)
+    mask = np.ascontiguousarray(mask, np.uint64)
+    _, h, w = state.shape
+    out = np.zeros_like(state)
+    _check(lib().r360_refine_eval(state.ctypes.data, mask.ctypes.data, w, h, rb, out.ctypes.data), "r360_refine_eval")
+    return out
 
 
 def libm_eval(x, y, z, on_device: bool = False):

@@ -642,6 +642,170 @@ __global__ void __launch_bounds__(64) k_refine(int8_t* __restrict__ state_all,
     }
 }
 
+// ------------------------------------------------------------------ banded refine
+// The sweeps are sequential along rows (row r's swept states change row r+1 in the first sweep, row r-1
+// in the second), but the change only travels through non-planar (-2) pixels close to a model, so it dies
+// out within a few rows.  Each sweep therefore runs in two phases over row bands of rb rows:
+//   phase 1  every (sensor, band) in parallel, one wave each, assuming no incoming assignment into the
+//            band's first row; the band's assignments into the next band's first row are kept (rbnd) with
+//            a flag telling whether they changed that row;
+//   phase 2  one wave per sensor walks the bands in sweep order: a band whose incoming row was changed
+//            (flag of the previous band) is swept again from the true incoming row until a swept row equals
+//            its phase-1 result — every later row of the band (and its boundary) is then unchanged.
+// The result is the sequential sweep's, bit for bit.  The sweeps read Sin (unchanged) and write Sout.
+//
+// One band of one sweep: DIR = +1 rows top->bottom, columns left->right, right/down checks (rows 0..h-2
+// swept, row h-1 only receives); DIR = -1 rows bottom->top, columns right->left, left/up checks with the
+// flat-index wrap of column 0 (rows h-1..1 swept, row 0 only receives).
+template <int K, int DIR>
+__device__ void refine_band(const int8_t* __restrict__ Sin, int8_t* __restrict__ Sout,
+                            const unsigned long long* __restrict__ MK, int w, int h, int r0, int r1,
+                            const int8_t* __restrict__ init, int8_t* __restrict__ bnd_out, int* __restrict__ flag_out,
+                            bool conv) {
+    const int lane = threadIdx.x & 63;
+    auto col = [&](int k) { return DIR > 0 ? lane * K + k : (63 - lane) * K + (K - 1 - k); };
+    auto load = [&](const int8_t* src, int r, int (&L)[K], unsigned long long (&M)[K]) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int c = col(k);
+            const int cc = c < w ? c : w - 1;
+            const int v = src[(long)r * w + cc];
+            const unsigned long long m = MK[(long)r * w + cc];
+            L[k] = c < w ? v : -1;
+            M[k] = c < w ? m : 0ull;
+        }
+    };
+    const int first = DIR > 0 ? r0 : r1 - 1, last = DIR > 0 ? r1 - 1 : r0;
+    int cur[K];
+    unsigned long long cm[K];
+    if (init) {
+        int dummy[K];
+        load(Sin, first, dummy, cm);
+#pragma unroll
+        for (int k = 0; k < K; ++k) { const int c = col(k); cur[k] = c < w ? (int)init[c] : -1; }
+    } else {
+        load(Sin, first, cur, cm);
+    }
+    const int cl = w - 1;                                    // owner of column w-1 in walking order (DIR < 0)
+    const int own_lane = 63 - cl / K, own_k = K - 1 - cl % K;
+    for (int r = first;; r += DIR) {
+        const int nr = r + DIR;
+        const bool has_nr = nr >= 0 && nr < h;
+        int nxt[K], nxt0[K];
+        unsigned long long nm[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) { nxt[k] = -1; nm[k] = 0ull; }
+        if (has_nr) load(Sin, nr, nxt, nm);
+#pragma unroll
+        for (int k = 0; k < K; ++k) nxt0[k] = nxt[k];
+        int F[K];
+        const bool swept = DIR > 0 ? r <= h - 2 : r >= 1;
+        if (swept) {
+            resolve_chain<K>(cur, cm, F);
+            // original state of the next column in walking order (right in the first sweep, left in the second)
+            const int next_of_last = __shfl(cur[0], (lane + 1) & 63, 64);
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int c = col(k);
+                if (DIR > 0 ? c >= w - 1 : (c >= w || c == 0)) continue;
+                const int nl = k + 1 < K ? cur[k + 1] : (lane < 63 ? next_of_last : -1);
+                if (F[k] == -1 || nl == -1) continue;
+                if (nxt[k] == -1) continue;
+                if (F[k] >= 0 && nxt[k] == -2 && ((nm[k] >> F[k]) & 1)) nxt[k] = F[k];
+            }
+            if (DIR < 0) {
+                // column 0: its "left" neighbour is the last pixel of the row above (flat-index wrap)
+                int upw = -1;
+                unsigned long long upw_m = 0;
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    if (k == own_k) { upw = nxt[k]; upw_m = nm[k]; }
+                upw = __shfl(upw, own_lane, 64);
+                upw_m = __shfl(upw_m, own_lane, 64);
+                const int f0 = __shfl(F[K - 1], 63, 64);     // column 0 = lane 63, k = K-1
+                const int up0 = __shfl(nxt[K - 1], 63, 64);
+                const unsigned long long um0 = __shfl(nm[K - 1], 63, 64);
+                int new_upw = upw, new_up0 = up0;
+                if (f0 != -1 && upw != -1) {
+                    if (f0 >= 0 && upw == -2 && ((upw_m >> f0) & 1)) new_upw = f0;
+                    if (up0 != -1 && f0 >= 0 && up0 == -2 && ((um0 >> f0) & 1)) new_up0 = f0;
+                }
+                if (w - 1 == 0) new_upw = new_up0;           // degenerate single-column image
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    if (lane == own_lane && k == own_k) nxt[k] = new_upw;
+                    if (lane == 63 && k == K - 1) nxt[k] = new_up0;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < K; ++k) F[k] = cur[k];
+        }
+        if (conv) {   // converged onto the phase-1 sweep: the rest of the band is unchanged
+            bool same = true;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int c = col(k);
+                if (c < w) same = same && (int)Sout[(long)r * w + c] == F[k];
+            }
+            if (__all(same)) return;
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int c = col(k);
+            if (c < w) Sout[(long)r * w + c] = (int8_t)F[k];
+        }
+        if (r == last) {
+            if (has_nr && bnd_out) {
+                bool diff = false;
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const int c = col(k);
+                    if (c < w) { bnd_out[c] = (int8_t)nxt[k]; diff = diff || nxt[k] != nxt0[k]; }
+                }
+                const bool any = __any(diff);
+                if (lane == 0) *flag_out = any ? 1 : 0;
+            }
+            return;
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) { cur[k] = nxt[k]; cm[k] = nm[k]; }
+    }
+}
+
+template <int K, int DIR>
+__global__ void __launch_bounds__(64) k_refine_p1(const int8_t* __restrict__ Sin, int8_t* __restrict__ Sout,
+                                                 const unsigned long long* __restrict__ MK, int w, int h, int rb,
+                                                 int8_t* __restrict__ bnd, int* __restrict__ flag) {
+    const int b = blockIdx.x, s = blockIdx.y;
+    const long N = (long)w * h;
+    const int r0 = b * rb, r1 = min(h, r0 + rb);
+    refine_band<K, DIR>(Sin + s * N, Sout + s * N, MK + s * N, w, h, r0, r1, nullptr,
+                        bnd + ((long)s * R360_REFINE_BANDS + b) * w, flag + s * R360_REFINE_BANDS + b, false);
+}
+
+template <int K, int DIR>
+__global__ void __launch_bounds__(64) k_refine_p2(const int8_t* __restrict__ Sin, int8_t* __restrict__ Sout,
+                                                 const unsigned long long* __restrict__ MK, int w, int h, int rb,
+                                                 int nb, int8_t* __restrict__ bnd, int* __restrict__ flag) {
+    const int s = blockIdx.x;
+    const long N = (long)w * h;
+    int8_t* B = bnd + (long)s * R360_REFINE_BANDS * w;
+    int* Fl = flag + s * R360_REFINE_BANDS;
+    for (int i = 1; i < nb; ++i) {
+        const int b = DIR > 0 ? i : nb - 1 - i;
+        const int prev = b - DIR;
+        // flags and boundary rows were written by phase 1 or by this wave's previous band
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        if (!__builtin_amdgcn_readfirstlane(Fl[prev])) continue;
+        const int r0 = b * rb, r1 = min(h, r0 + rb);
+        refine_band<K, DIR>(Sin + s * N, Sout + s * N, MK + s * N, w, h, r0, r1, B + (long)prev * w, B + (long)b * w,
+                            Fl + b, true);
+    }
+}
+
 __global__ void k_refine_final(const int8_t* __restrict__ state, const int* __restrict__ lab, int N,
                                const PlaneModel* __restrict__ models, int* __restrict__ labf) {
     const long total = 8L * N;
@@ -1105,6 +1269,39 @@ __global__ void __launch_bounds__(VOXC_TPB) k_vox_compact(const VoxCell* __restr
 
 }  // namespace
 
+// rows per band of the banded refinement (R360_REFINE_ROWS overrides; 0 = the single-wave sweeps)
+int refine_band_rows(int h) {
+    static const int env = getenv("R360_REFINE_ROWS") ? atoi(getenv("R360_REFINE_ROWS")) : -1;
+    int rb = env >= 0 ? env : 16;
+    if (rb > 0 && (h + rb - 1) / rb > R360_REFINE_BANDS) rb = (h + R360_REFINE_BANDS - 1) / R360_REFINE_BANDS;
+    return rb;
+}
+
+// refine()'s two sweeps over 8 sensors' states S (in place), closeness masks MK.  rb > 0: banded (phases 1 and
+// 2 per sweep; S2 holds the first sweep's output); rb = 0: one wave per sensor walks every row (k_refine).
+int launch_refine_sweeps(hipStream_t st, int8_t* S, int8_t* S2, const unsigned long long* MK, int8_t* bnd, int* flag,
+                         int w, int h, int rb) {
+    const int K = (w + 63) / 64;
+    if (rb > 0 && (h + rb - 1) / rb > R360_REFINE_BANDS) { r360_set_error("refine: %d rows per band too few", rb); return -2; }
+    const int nb = rb > 0 ? (h + rb - 1) / rb : 0;
+    switch (K) {
+#define R360_REFINE_CASE(k)                                                                                     \
+    case k:                                                                                                     \
+        if (rb == 0) { hipLaunchKernelGGL(k_refine<k>, dim3(8), dim3(64), 0, st, S, MK, w, h); break; }          \
+        hipLaunchKernelGGL((k_refine_p1<k, 1>), dim3(nb, 8), dim3(64), 0, st, S, S2, MK, w, h, rb, bnd, flag);   \
+        hipLaunchKernelGGL((k_refine_p2<k, 1>), dim3(8), dim3(64), 0, st, S, S2, MK, w, h, rb, nb, bnd, flag);   \
+        hipLaunchKernelGGL((k_refine_p1<k, -1>), dim3(nb, 8), dim3(64), 0, st, S2, S, MK, w, h, rb, bnd, flag);  \
+        hipLaunchKernelGGL((k_refine_p2<k, -1>), dim3(8), dim3(64), 0, st, S2, S, MK, w, h, rb, nb, bnd, flag);  \
+        break;
+        R360_REFINE_CASE(1) R360_REFINE_CASE(2) R360_REFINE_CASE(3) R360_REFINE_CASE(4) R360_REFINE_CASE(5)
+        R360_REFINE_CASE(6) R360_REFINE_CASE(7) R360_REFINE_CASE(8) R360_REFINE_CASE(9) R360_REFINE_CASE(10)
+#undef R360_REFINE_CASE
+        default: r360_set_error("refine: cloud width %d > 640 unsupported", w); return -1;
+    }
+    R360_HIP(hipGetLastError());
+    return 0;
+}
+
 // ------------------------------------------------------------------ launcher
 int launch_segmentation(r360_frame* f) {
     PlaneBufs& P = f->pl;
@@ -1155,15 +1352,7 @@ int launch_segmentation(r360_frame* f) {
     slot = timing_begin(ctx, "k_refine");
     hipLaunchKernelGGL(k_refine_init, dim3(blocks), dim3(256), 0, st, P.cloud, P.lab, N, P.models, P.nmodels, P.state,
                        P.mask);
-    const int K = (w + 63) / 64;
-    switch (K) {
-#define R360_REFINE_CASE(k) \
-    case k: hipLaunchKernelGGL(k_refine<k>, dim3(8), dim3(64), 0, st, P.state, P.mask, w, h); break;
-        R360_REFINE_CASE(1) R360_REFINE_CASE(2) R360_REFINE_CASE(3) R360_REFINE_CASE(4) R360_REFINE_CASE(5)
-        R360_REFINE_CASE(6) R360_REFINE_CASE(7) R360_REFINE_CASE(8) R360_REFINE_CASE(9) R360_REFINE_CASE(10)
-#undef R360_REFINE_CASE
-        default: r360_set_error("refine: cloud width %d > 640 unsupported", w); return -1;
-    }
+    if (launch_refine_sweeps(st, P.state, P.state2, P.mask, P.rbnd, P.rflag, w, h, refine_band_rows(h))) return -1;
     hipLaunchKernelGGL(k_refine_final, dim3(blocks), dim3(256), 0, st, P.state, P.lab, N, P.models, P.labf);
     timing_end(ctx, slot);
     R360_HIP(hipGetLastError());
@@ -1198,4 +1387,25 @@ int launch_segmentation(r360_frame* f) {
     timing_end(ctx, slot);
     R360_HIP(hipGetLastError());
     return 0;
+}
+
+// Test hook: refine()'s two sweeps on given states / closeness masks of 8 sensors (w x h each), banded with
+// rb rows per band (0 = the single-wave sweeps); out receives the swept states.
+extern "C" int r360_refine_eval(const int8_t* state, const uint64_t* mask, int w, int h, int rb, int8_t* out) {
+    if (!state || !mask || !out || w < 1 || h < 1 || w > 640) { r360_set_error("r360_refine_eval: bad arguments"); return -2; }
+    const size_t T = 8 * (size_t)w * h;
+    int8_t *S, *S2, *bnd;
+    unsigned long long* MK;
+    int* flag;
+    R360_HIP(hipMalloc(&S, T));
+    R360_HIP(hipMalloc(&S2, T));
+    R360_HIP(hipMalloc(&MK, sizeof(unsigned long long) * T));
+    R360_HIP(hipMalloc(&bnd, 8L * R360_REFINE_BANDS * w));
+    R360_HIP(hipMalloc(&flag, sizeof(int) * 8 * R360_REFINE_BANDS));
+    R360_HIP(hipMemcpy(S, state, T, hipMemcpyHostToDevice));
+    R360_HIP(hipMemcpy(MK, mask, sizeof(unsigned long long) * T, hipMemcpyHostToDevice));
+    const int rc = launch_refine_sweeps(0, S, S2, MK, bnd, flag, w, h, rb);
+    if (rc == 0) R360_HIP(hipMemcpy(out, S, T, hipMemcpyDeviceToHost));
+    (void)hipFree(S); (void)hipFree(S2); (void)hipFree(MK); (void)hipFree(bnd); (void)hipFree(flag);
+    return rc;
 }

@@ -124,6 +124,7 @@ enum { R360_SUM_NVALID = 27, R360_SUM_NVIS = 28, R360_SUM_NDEPTH = 29, R360_SUM_
 #include "plane_math.h"
 #define R360_MAX_MODELS 64     // planar models per sensor (refinement closeness bit masks are 64-bit)
 #define R360_MAX_BIG 512       // labels with > 80 points per sensor
+#define R360_REFINE_BANDS 64   // row bands per sensor of the banded refinement sweeps
 
 // One planar model of segment() (PlanarRegion statistics + ModelCoefficients)
 struct PlaneModel {
@@ -183,6 +184,9 @@ struct PlaneBufs {
     PlaneModel* models = nullptr;    // [8][R360_MAX_MODELS]
     int* nmodels = nullptr;          // [8]
     int8_t* state = nullptr;         // refinement state [8][N]
+    int8_t* state2 = nullptr;        // refinement state after the first sweep [8][N]
+    int8_t* rbnd = nullptr;          // banded refinement: each band's assignments into the next band's first row
+    int* rflag = nullptr;            //   [8][R360_REFINE_BANDS][w] and whether they changed that row [8][..]
     unsigned long long* mask = nullptr;  // closeness masks [8][N]
     PlaneOut* out = nullptr;         // [8][R360_MAX_MODELS]
     float4* contour = nullptr;       // contour pool
