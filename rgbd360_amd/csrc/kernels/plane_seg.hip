@@ -688,14 +688,25 @@ __device__ void refine_band(const int8_t* __restrict__ Sin, int8_t* __restrict__
     }
     const int cl = w - 1;                                    // owner of column w-1 in walking order (DIR < 0)
     const int own_lane = 63 - cl / K, own_k = K - 1 - cl % K;
+    // conv: the phase-1 states of the current row, loaded one row ahead like the inputs
+    auto load_out = [&](int r, int (&P)[K]) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int c = col(k);
+            P[k] = (int)Sout[(long)r * w + (c < w ? c : w - 1)];
+        }
+    };
+    int po[K];
+    if (conv) load_out(first, po);
     for (int r = first;; r += DIR) {
         const int nr = r + DIR;
         const bool has_nr = nr >= 0 && nr < h;
-        int nxt[K], nxt0[K];
+        int nxt[K], nxt0[K], pn[K];
         unsigned long long nm[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) { nxt[k] = -1; nm[k] = 0ull; }
+        for (int k = 0; k < K; ++k) { nxt[k] = -1; nm[k] = 0ull; pn[k] = 0; }
         if (has_nr) load(Sin, nr, nxt, nm);
+        if (conv && has_nr && r != last) load_out(nr, pn);
 #pragma unroll
         for (int k = 0; k < K; ++k) nxt0[k] = nxt[k];
         int F[K];
@@ -746,7 +757,7 @@ __device__ void refine_band(const int8_t* __restrict__ Sin, int8_t* __restrict__
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 const int c = col(k);
-                if (c < w) same = same && (int)Sout[(long)r * w + c] == F[k];
+                if (c < w) same = same && po[k] == F[k];
             }
             if (__all(same)) return;
         }
@@ -769,7 +780,7 @@ __device__ void refine_band(const int8_t* __restrict__ Sin, int8_t* __restrict__
             return;
         }
 #pragma unroll
-        for (int k = 0; k < K; ++k) { cur[k] = nxt[k]; cm[k] = nm[k]; }
+        for (int k = 0; k < K; ++k) { cur[k] = nxt[k]; cm[k] = nm[k]; po[k] = pn[k]; }
     }
 }
 
