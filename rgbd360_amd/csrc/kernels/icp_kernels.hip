@@ -20,12 +20,15 @@
 namespace {
 
 #ifndef R360_ICP_TPB
-#define R360_ICP_TPB 512
+#define R360_ICP_TPB 256
 #endif
 #ifndef R360_ICP_MINB
-#define R360_ICP_MINB 4   // waves per SIMD (HIP launch_bounds 2nd arg): caps the pass at 128 VGPRs
+#define R360_ICP_MINB 5   // waves per SIMD (HIP launch_bounds 2nd arg): caps the pass at 102 VGPRs (94 used)
 #endif
-constexpr int TPB = R360_ICP_TPB;  // 16 waves: one workgroup per CU at the kernel's occupancy, few records
+// 4 waves per workgroup, 5 workgroups per CU: 5 waves per SIMD (a 512-thread workgroup holds 2 waves per
+// SIMD, so 94 VGPRs still gave 4); with 512 workgroups per pass each wave streams twice the chunks, and a
+// batched launch (16 pairs) keeps every SIMD at 5 waves (17.8 vs 20.4 us per pair-pass, profiles/r2_v2)
+constexpr int TPB = R360_ICP_TPB;
 constexpr int NW = TPB / 64;
 constexpr int RG = TPB / 16;  // record-reduction groups (16 lanes x 16 B per record)
 
@@ -1353,7 +1356,9 @@ static PassGrid pass_grid(const r360_ctx* ctx, const LevelBufs& Ls, int occ) {
     // PF 4 (compacted source points) for the plain pass; the occlusion variants index their flags by source
     // pixel and keep the image stream (PF 3 where rows split into whole waves)
     const int pf = pf_env >= 0 && !(pf_env == 4 && occ) ? pf_env : (occ ? ((Ls.cols % 64 == 0) ? 3 : 0) : 4);
-    int cap = cap_env > 0 ? cap_env : occ_q.cus * (occ_q.per[pf] > 0 ? occ_q.per[pf] : 4);
+    // workgroups per job and pass: 2 per CU (one resident round holds occ_q.per[pf] per CU; a batched launch
+    // fills the rest with other jobs, and fewer records per job shorten the reduction tail)
+    int cap = cap_env > 0 ? cap_env : 2 * occ_q.cus;
     if (cap > ctx->partials_cap) cap = ctx->partials_cap;
     int nb = pf == 1 ? icp_blocks_for(npx) : (npx + TPB - 1) / TPB;
     if (nb > cap) nb = cap;
