@@ -411,8 +411,9 @@ def main():
     tf = os.path.join(ROOT, "profiles", "latest", "l0_pass.json")
     if os.path.exists(tf) and (args.rows, args.cols, args.workload) == (480, 640, "sequence"):
         prof = json.load(open(tf))
-        if prof.get("icp_source_hash") == icp_source_hash():
-            traffic, traffic_src = prof.get("hbm_bytes_per_launch"), prof.get("tag")
+        if prof.get("icp_source_hash") == icp_source_hash() and prof.get("hbm_bytes_per_pair_pass"):
+            # the profile's HBM bytes per pair-pass, scaled to this run's pairs per launch
+            traffic, traffic_src = prof["hbm_bytes_per_pair_pass"] * pairs_per_launch, prof.get("tag")
     steps_pairs = p1 - p0
     if args.workload == "sequence":
         workload = ("config4 (per pair configs 1+2's work): OdometryRGBD360 over the synthetic "
@@ -447,6 +448,7 @@ def main():
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
             "traffic_profile": traffic_src,
+            "traffic_per_pair_pass": (traffic / pairs_per_launch) if traffic else None,
             "kernel": "k_icp_pass<PHOTO_DEPTH> (level 0)", "avg_launch_ms": avg_ms, "launches": k0_n,
             "pairs_per_launch": pairs_per_launch,
             "timing": "in-kernel execution span (s_memrealtime) over the timed region, all pipelines running",

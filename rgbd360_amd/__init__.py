@@ -1065,14 +1065,17 @@ class RegisterPhotoICP:
         return H.reshape(6, 6), g, e.value, nv.value, nvis.value
 
 
-def refine_eval(state: np.ndarray, mask: np.ndarray, rb: int = 0) -> np.ndarray:
-    """refine()'s two sweeps on the device (parity hook): state int8 (8, h, w), mask uint64 (8, h, w)."""
+def refine_eval(state: np.ndarray, mask: np.ndarray, rb: int = 0, return_fallbacks: bool = False):
+    """refine()'s two sweeps on the device (parity hook): state int8 (8, h, w), mask uint64 (8, h, w); rb < 0 the
+    wavefront sweeps (the default path), 0 the single-wave sweeps, rb > 0 banded.  With return_fallbacks, also the
+    number of sensors whose wavefront second sweep needed wrap-push corrections (re-runs or the fallback)."""
     state = np.ascontiguousarray(state, np.int8)
     mask = np.ascontiguousarray(mask, np.uint64)
     _, h, w = state.shape
     out = np.zeros_like(state)
-    _check(lib().r360_refine_eval(state.ctypes.data, mask.ctypes.data, w, h, rb, out.ctypes.data), "r360_refine_eval")
-    return out
+    nfb = _check(lib().r360_refine_eval(state.ctypes.data, mask.ctypes.data, w, h, rb, out.ctypes.data),
+                 "r360_refine_eval")
+    return (out, nfb) if return_fallbacks else out
 
 
 def libm_eval(x, y, z, on_device: bool = False):

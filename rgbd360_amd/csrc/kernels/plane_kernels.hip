@@ -376,15 +376,64 @@ __global__ void __launch_bounds__(DM_TPB) k_distmap(const float* __restrict__ in
 // Window sums of the central differences are sums of floats whose ulps are >= 2^-36 and whose
 // magnitudes stay far below 2^17, so they are exact in double in any order: a direct sum over the
 // (<= 9 x 9) window equals the reference's integral-image differences bit for bit.
-__global__ void k_normals(const float4* __restrict__ cloud, const float* __restrict__ dist, int w, int h,
-                          float4* __restrict__ nrm) {
-    const long N = (long)w * h, total = 8 * N;
+//
+// One workgroup = a tile of NT_R x NT_C output pixels of one sensor.  The central differences of the tile
+// plus a NT_H-pixel halo are computed once into LDS as {dx, finite}, {dy, finite} (a non-finite difference is
+// stored as zero and not counted, which is what skipping it does to an exact sum); each pixel then sums its
+// window from LDS.  Windows wider than the halo (smoothing >= 10, only for points beyond ~20 m) are summed from
+// global memory as before.
+constexpr int NT_R = 16, NT_C = 64, NT_H = 4, NT_TPB = 256;
+constexpr int NT_SR = NT_R + 2 * NT_H, NT_SC = NT_C + 2 * NT_H;
+
+__device__ __forceinline__ void normal_out(const double (&gx)[3], const double (&gy)[3], unsigned cx, unsigned cy,
+                                           const float4& p, float4& o) {
+    if (cx != 0 && cy != 0) {
+        const double n0 = gy[1] * gx[2] - gy[2] * gx[1];
+        const double n1 = gy[2] * gx[0] - gy[0] * gx[2];
+        const double n2 = gy[0] * gx[1] - gy[1] * gx[0];
+        const double len = n0 * n0 + n1 * n1 + n2 * n2;
+        if (len != 0.0) {
+            const double sl = sqrt(len);
+            float nx = (float)(n0 / sl), ny = (float)(n1 / sl), nz = (float)(n2 / sl);
+            const float vx = 0.f - p.x, vy = 0.f - p.y, vz = 0.f - p.z;
+            if (vx * nx + vy * ny + vz * nz < 0) { nx *= -1; ny *= -1; nz *= -1; }
+            o = make_float4(nx, ny, nz, p.x * nx + p.y * ny + p.z * nz);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(NT_TPB) k_normals(const float4* __restrict__ cloud, const float* __restrict__ dist,
+                                                   int w, int h, float4* __restrict__ nrm) {
+    __shared__ float4 sdx[NT_SR * NT_SC], sdy[NT_SR * NT_SC];
+    const int s = blockIdx.z;
+    const int r0 = blockIdx.y * NT_R, c0 = blockIdx.x * NT_C;
+    const long N = (long)w * h;
+    const float4* P = cloud + (long)s * N;
+    // differences of the staged pixels (image rows r0 - NT_H .., columns c0 - NT_H ..); positions outside
+    // [1, h-2] x [1, w-2] are zero and counted, as the reference's border handling (never read by pixels that
+    // pass the 8-pixel border test)
+    for (int k = threadIdx.x; k < NT_SR * NT_SC; k += NT_TPB) {
+        const int yy = r0 - NT_H + k / NT_SC, xx = c0 - NT_H + k % NT_SC;
+        float4 a = make_float4(0.f, 0.f, 0.f, 1.f), b = a;
+        if (yy >= 1 && yy <= h - 2 && xx >= 1 && xx <= w - 2) {
+            const int q = yy * w + xx;
+            const float4 pr = P[q + 1], pl = P[q - 1], pu = P[q - w], pd = P[q + w];
+            const float dx0 = pr.x - pl.x, dx1 = pr.y - pl.y, dx2 = pr.z - pl.z;
+            const float dy0 = pd.x - pu.x, dy1 = pd.y - pu.y, dy2 = pd.z - pu.z;
+            a = isfin(dx0 + dx1 + dx2) ? make_float4(dx0, dx1, dx2, 1.f) : make_float4(0.f, 0.f, 0.f, 0.f);
+            b = isfin(dy0 + dy1 + dy2) ? make_float4(dy0, dy1, dy2, 1.f) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        sdx[k] = a;
+        sdy[k] = b;
+    }
+    __syncthreads();
     const float nan = __builtin_nanf("");
-    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-        const int s = (int)(i / N);
-        const int j = (int)(i - (long)s * N);
-        const int r = j / w, c = j - (j / w) * w;
-        const float4* P = cloud + (long)s * N;
+    const int c = c0 + (threadIdx.x & (NT_C - 1));
+    for (int rr = threadIdx.x / NT_C; rr < NT_R; rr += NT_TPB / NT_C) {
+        const int r = r0 + rr;
+        if (r >= h || c >= w) continue;
+        const int j = r * w + c;
+        const long i = (long)s * N + j;
         float4 o = make_float4(nan, nan, nan, nan);
         const int border = 8;
         const float4 p = P[j];
@@ -397,29 +446,31 @@ __global__ void k_normals(const float4* __restrict__ cloud, const float* __restr
                 const int sx = c - rs2, sy = r - rs2;
                 double gx[3] = {0, 0, 0}, gy[3] = {0, 0, 0};
                 unsigned cx = 0, cy = 0;
-                for (int yy = sy; yy < sy + rs; ++yy)
-                    for (int xx = sx; xx < sx + rs; ++xx) {
-                        if (yy < 1 || yy > h - 2 || xx < 1 || xx > w - 2) { ++cx; ++cy; continue; }  // zero, finite
-                        const int q = yy * w + xx;
-                        const float4 a = P[q + 1], b = P[q - 1], u = P[q - w], d = P[q + w];
-                        const float dx0 = a.x - b.x, dx1 = a.y - b.y, dx2 = a.z - b.z;
-                        const float dy0 = d.x - u.x, dy1 = d.y - u.y, dy2 = d.z - u.z;
-                        if (isfin(dx0 + dx1 + dx2)) { gx[0] += dx0; gx[1] += dx1; gx[2] += dx2; ++cx; }
-                        if (isfin(dy0 + dy1 + dy2)) { gy[0] += dy0; gy[1] += dy1; gy[2] += dy2; ++cy; }
+                if (rs <= 2 * NT_H + 1) {
+                    float fcx = 0.f, fcy = 0.f;   // counts of <= 81 ones: exact in float
+                    for (int yy = sy; yy < sy + rs; ++yy) {
+                        const int rowb = (yy - (r0 - NT_H)) * NT_SC - (c0 - NT_H);
+                        for (int xx = sx; xx < sx + rs; ++xx) {
+                            const float4 a = sdx[rowb + xx], b = sdy[rowb + xx];
+                            gx[0] += a.x; gx[1] += a.y; gx[2] += a.z; fcx += a.w;
+                            gy[0] += b.x; gy[1] += b.y; gy[2] += b.z; fcy += b.w;
+                        }
                     }
-                if (cx != 0 && cy != 0) {
-                    const double n0 = gy[1] * gx[2] - gy[2] * gx[1];
-                    const double n1 = gy[2] * gx[0] - gy[0] * gx[2];
-                    const double n2 = gy[0] * gx[1] - gy[1] * gx[0];
-                    const double len = n0 * n0 + n1 * n1 + n2 * n2;
-                    if (len != 0.0) {
-                        const double sl = sqrt(len);
-                        float nx = (float)(n0 / sl), ny = (float)(n1 / sl), nz = (float)(n2 / sl);
-                        const float vx = 0.f - p.x, vy = 0.f - p.y, vz = 0.f - p.z;
-                        if (vx * nx + vy * ny + vz * nz < 0) { nx *= -1; ny *= -1; nz *= -1; }
-                        o = make_float4(nx, ny, nz, p.x * nx + p.y * ny + p.z * nz);
-                    }
+                    cx = (unsigned)fcx;
+                    cy = (unsigned)fcy;
+                } else {
+                    for (int yy = sy; yy < sy + rs; ++yy)
+                        for (int xx = sx; xx < sx + rs; ++xx) {
+                            if (yy < 1 || yy > h - 2 || xx < 1 || xx > w - 2) { ++cx; ++cy; continue; }  // zero, finite
+                            const int q = yy * w + xx;
+                            const float4 a = P[q + 1], b = P[q - 1], u = P[q - w], d = P[q + w];
+                            const float dx0 = a.x - b.x, dx1 = a.y - b.y, dx2 = a.z - b.z;
+                            const float dy0 = d.x - u.x, dy1 = d.y - u.y, dy2 = d.z - u.z;
+                            if (isfin(dx0 + dx1 + dx2)) { gx[0] += dx0; gx[1] += dx1; gx[2] += dx2; ++cx; }
+                            if (isfin(dy0 + dy1 + dy2)) { gy[0] += dy0; gy[1] += dy1; gy[2] += dy2; ++cy; }
+                        }
                 }
+                normal_out(gx, gy, cx, cy, p, o);
             }
         }
         nrm[i] = o;
@@ -482,7 +533,8 @@ int launch_cloud_normals(r360_frame* f) {
     timing_end(f->ctx, slot);
     R360_HIP(hipGetLastError());
     slot = timing_begin(f->ctx, "k_normals");
-    hipLaunchKernelGGL(k_normals, dim3(blocks), dim3(256), 0, st, P.cloud, P.dist, w, h, P.nrm);
+    hipLaunchKernelGGL(k_normals, dim3((w + NT_C - 1) / NT_C, (h + NT_R - 1) / NT_R, 8), dim3(NT_TPB), 0, st, P.cloud,
+                       P.dist, w, h, P.nrm);
     timing_end(f->ctx, slot);
     R360_HIP(hipGetLastError());
     return 0;

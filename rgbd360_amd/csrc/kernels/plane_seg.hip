@@ -16,6 +16,8 @@
 //   k_vox_*        VoxelGrid of regions without a contour (Frame360.h:1017-1026): (region, voxel) hash
 //                  table with exact double sums, compacted into per-region voxel lists
 // Arithmetic follows oracle/src/planes_oracle.cpp and pbmap_oracle.cpp; see rgbd360_amd/csrc/plane_math.h.
+#include <cstdio>
+#include <cstdlib>
 #include "../r360_internal.h"
 #include "../plane_math.h"
 
@@ -519,10 +521,10 @@ __device__ void resolve_chain(const int (&L)[K], const unsigned long long (&M)[K
 // rotation (the loop is unrolled by three), so no loop-carried copy of an in-flight load forces a
 // vmcnt(0) per row, and every load is unconditional (clamped column, value masked afterwards).
 template <int K>
-__global__ void __launch_bounds__(64) k_refine(int8_t* __restrict__ state_all,
-                                              const unsigned long long* __restrict__ mask_all, int w, int h) {
-    const int s = blockIdx.x;
-    const int lane = threadIdx.x;
+__device__ void refine_sweeps(int8_t* __restrict__ state_all, const unsigned long long* __restrict__ mask_all, int w,
+                              int h, int s, int sweeps, int r_top = -1) {
+    if (r_top < 0) r_top = h - 1;   // the second sweep's first source row (rows above it are already swept)
+    const int lane = threadIdx.x & 63;
     const long N = (long)w * h;
     int8_t* S = state_all + s * N;
     const unsigned long long* MK = mask_all + s * N;
@@ -549,7 +551,7 @@ __global__ void __launch_bounds__(64) k_refine(int8_t* __restrict__ state_all,
     int A[K], B[K], C[K];
     unsigned long long Am[K], Bm[K], Cm[K];
     // ---------------- first sweep: top->bottom, left->right; right and down checks
-    {
+    if (sweeps & 1) {
         auto step = [&](int r, int (&cur)[K], unsigned long long (&cm)[K], int (&nxt)[K], unsigned long long (&nm)[K],
                         int (&nn)[K], unsigned long long (&nnm)[K]) {
             if (r + 2 < h) load(r + 2, nn, nnm, +1);     // consumed two steps later
@@ -585,7 +587,7 @@ __global__ void __launch_bounds__(64) k_refine(int8_t* __restrict__ state_all,
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     // ---------------- second sweep: bottom->top, right->left; left and up checks
-    {
+    if (sweeps & 2) {
         const int cl = w - 1;                                    // owner of column w-1 (walking order)
         const int own_lane = 63 - cl / K, own_k = K - 1 - cl % K;
         auto step = [&](int r, int (&cur)[K], unsigned long long (&cm)[K], int (&up)[K], unsigned long long (&um)[K],
@@ -628,9 +630,9 @@ __global__ void __launch_bounds__(64) k_refine(int8_t* __restrict__ state_all,
             }
             store(r, F, -1);
         };
-        load(h - 1, A, Am, -1);
-        if (h > 1) load(h - 2, B, Bm, -1);
-        int r = h - 1;
+        load(r_top, A, Am, -1);
+        if (r_top >= 1) load(r_top - 1, B, Bm, -1);
+        int r = r_top;
         for (; r - 3 >= 0; r -= 3) {
             step(r, A, Am, B, Bm, C, Cm);
             step(r - 1, B, Bm, C, Cm, A, Am);
@@ -640,6 +642,12 @@ __global__ void __launch_bounds__(64) k_refine(int8_t* __restrict__ state_all,
         else if (r == 1) { step(1, A, Am, B, Bm, C, Cm); store(0, B, -1); }
         else { step(2, A, Am, B, Bm, C, Cm); step(1, B, Bm, C, Cm, A, Am); store(0, C, -1); }
     }
+}
+
+template <int K>
+__global__ void __launch_bounds__(64) k_refine(int8_t* __restrict__ state_all,
+                                              const unsigned long long* __restrict__ mask_all, int w, int h) {
+    refine_sweeps<K>(state_all, mask_all, w, h, blockIdx.x, 3);
 }
 
 // ------------------------------------------------------------------ banded refine
@@ -815,6 +823,232 @@ __global__ void __launch_bounds__(64) k_refine_p2(const int8_t* __restrict__ Sin
         refine_band<K, DIR>(Sin + s * N, Sout + s * N, MK + s * N, w, h, r0, r1, B + (long)prev * w, B + (long)b * w,
                             Fl + b, true);
     }
+}
+
+// ------------------------------------------------------------------ wavefront refine
+// The sweeps as anti-diagonal wavefronts.  In the first sweep a pixel's state depends only on the pixel above
+// (the down push of the row above, applied first) and the pixel to its left (the row's chain), both on the
+// previous anti-diagonal k - 1 (k = row + column); the second sweep mirrors it (the pixel below, the pixel to
+// the right; diagonals in decreasing order).  So one thread per row walks its row while the diagonals advance:
+// at step k thread r handles column k - r, takes the left/right neighbour from its own previous step and the
+// upper/lower neighbour's from thread r -/+ 1 (DPP wave shift inside a wave, LDS between waves, one barrier
+// per diagonal).  h + w - 1 steps instead of h dependent row scans.
+//
+// Per pixel (O = state before the sweep, only O == -2 pixels change, M = closeness mask):
+//   sweep 1   D = up push:  r >= 1, c <= w-2, O(r-1, c+1) != -1, a = F(r-1, c) >= 0, M bit a  -> a
+//             chain:        D == -2, r <= h-2, c >= 1, b = F(r, c-1) >= 0, M bit b           -> b
+//   sweep 2   D = push:     r <= h-2, O(r+1, c-1) != -1 (c >= 1) or O(r, w-1) != -1 (c == 0),
+//                           a = F(r+1, c) >= 0, M bit a                                        -> a
+//             chain:        D == -2, r >= 1, c <= w-2, b = F(r, c+1) >= 0, M bit b            -> b
+// The second sweep has one edge the wavefront cannot order: column 0 of row r+1 also pushes into (r, w-1)
+// when the push from below left it at -2 (the flat-index wrap of PCL's "left" neighbour), but (r+1, 0) is
+// reached only after row r has started.  The wavefront runs as if that push never happens and checks it when
+// thread r reaches column 0 (where a = F(r+1, 0)); if it would have fired for any row, the sensor's fallback
+// flag is set and k_refine_fb redoes the second sweep with the single-wave kernel.  Without such a row every
+// pixel satisfies the sequential recurrences, so the states are the sequential sweep's bit for bit.
+//
+// Inputs in skewed layout (k_refine_skew): slot k * h + r of diagonal k holds pixel (r, k - r), so a step's
+// loads are coalesced; code = state | static push conditions << 8.
+constexpr int RW_PF = 8;   // diagonals prefetched ahead
+
+__global__ void k_refine_skew(const int8_t* __restrict__ S, const unsigned long long* __restrict__ MK, int w, int h,
+                              uint16_t* __restrict__ code, unsigned long long* __restrict__ msk, int* __restrict__ fb) {
+    // one thread per skewed slot (coalesced stores; the raster reads walk down-left diagonals, which reuse
+    // each cache line for the next diagonals); slots outside the image are never used
+    const long N = (long)w * h, SK = (long)(h + w - 1) * h, total = 8 * SK;
+    if (blockIdx.x == 0 && threadIdx.x < 16) fb[threadIdx.x] = 0;
+    for (long d = blockIdx.x * (long)blockDim.x + threadIdx.x; d < total; d += (long)gridDim.x * blockDim.x) {
+        const int s = (int)(d / SK);
+        const long q = d - (long)s * SK;
+        const int k = (int)(q / h), r = (int)(q - (long)k * h);
+        const int c = k - r;
+        if (c < 0 || c >= w) continue;
+        const int j = r * w + c;
+        const long i = (long)s * N + j;
+        const int8_t* O = S + (long)s * N;
+        const bool c1 = r >= 1 && c <= w - 2 && O[(r - 1) * w + c + 1] != -1;
+        const bool c2 = r <= h - 2 && (c >= 1 ? O[(r + 1) * w + c - 1] != -1 : O[r * w + w - 1] != -1);
+        code[d] = (uint16_t)((uint8_t)O[j] | (c1 ? 0x100 : 0) | (c2 ? 0x200 : 0));
+        msk[d] = MK[i];
+    }
+}
+
+__device__ __forceinline__ bool mbit(unsigned long long m, int v) { return v >= 0 && ((m >> v) & 1ull); }
+
+// DIR = +1: first sweep, F written to f1 (skewed).  DIR = -1: second sweep over f1, F written to S (raster).
+// blockDim.x = 64 * ceil(h / 64), grid = 8 sensors.
+//
+// Second sweep, wrap pushes: the wavefront runs with an assumed wrap value per row (none at first); when thread
+// r reaches column 0 it records the value the wrap push into (r, w-1) really takes given the states now known
+// (wdet[r]).  Rows are swept bottom-up, so the last row (largest r) whose record differs from its assumption is
+// the earliest point where the sweep went wrong: everything on diagonals above r + w - 1 is exact.  Every
+// differing row takes its record as the new assumption (that row's record is exact, the others are the best
+// guess) and the wavefront is re-run from diagonal r + w - 1 downwards, comparing every state with the
+// previous pass's; once it is below the lowest changed assumption, a whole diagonal that comes out unchanged
+// means every later diagonal would too, and the pass stops.  Repeat until no row's record differs from its
+// assumption: then every pixel satisfies the sequential recurrences and the states are the sequential sweep's
+// (each pass makes the last differing row exact, so this ends).  After RW_MAX_REDO re-runs the sensor is handed
+// to k_refine_fb (fb[s] = first differing row + 1).
+constexpr int RW_MAX_REDO = 64;
+
+template <int DIR>
+__global__ void __launch_bounds__(1024) k_refine_wave(const uint16_t* __restrict__ code_all,
+                                                      const unsigned long long* __restrict__ msk_all,
+                                                      int8_t* __restrict__ f1_all, int8_t* __restrict__ S_all,
+                                                      int* __restrict__ fb, int w, int h) {
+    __shared__ int xch[2][16];
+    __shared__ int8_t wasm[1024], wdet[1024];   // DIR < 0: assumed / detected wrap value per row (-2: none)
+    __shared__ int s_red, s_min;
+    __shared__ int chg[2][16];   // re-runs: whether a wave changed any state at a step
+    const int s = blockIdx.x;
+    const int r = threadIdx.x, lane = r & 63, wv = r >> 6, nw = blockDim.x >> 6;
+    const long SK = (long)(h + w - 1) * h;
+    const uint16_t* code = code_all + s * SK;
+    const unsigned long long* msk = msk_all + s * SK;
+    int8_t* f1 = f1_all + s * SK;
+    int8_t* S = S_all + (long)s * w * h;
+    const int KS = h + w - 1;
+    const int rr = r < h ? r : h - 1;             // loads of rows >= h are clamped (never used)
+    auto kof = [&](int t) { return DIR > 0 ? t : KS - 1 - t; };
+    auto tc = [&](int t) { return t < KS ? t : KS - 1; };
+    // inputs of RW_PF diagonals per chunk: the next chunk's loads are issued when a chunk starts and consumed
+    // RW_PF steps later (kept as loaded; combining them at load time would wait for them there): code = state |
+    // push conditions, the mask, for DIR < 0 the first sweep's state and, in a re-run, the previous pass's
+    struct In { unsigned short code; unsigned char f1, old; unsigned long long m; };
+    auto ld = [&](int t, bool redo, In& x) {
+        const int k = kof(tc(t));
+        const long q = (long)k * h + rr;
+        x.code = code[q];
+        x.m = msk[q];
+        if (DIR < 0) x.f1 = (unsigned char)f1[q];
+        if (DIR < 0 && redo) {
+            const int c = k - rr;
+            x.old = (unsigned char)S[(long)rr * w + (c < 0 ? 0 : c >= w ? w - 1 : c)];
+        }
+    };
+    if (DIR < 0) {
+        for (int q = threadIdx.x; q < 1024; q += blockDim.x) { wasm[q] = -2; wdet[q] = -2; }
+    }
+    bool upw_free = false;     // DIR < 0: (r, w-1) was left at -2 by the push from below
+    unsigned long long mw = 0; //   and its mask
+    int t_start = 0, t_guard = 0;   // re-runs may stop only at steps after t_guard
+    for (int pass = 0;; ++pass) {
+        const bool redo = pass > 0;
+        int prev = -1;         // this row's state at the previous step
+        if (redo) {            // resume from the previous pass's states on the diagonal before t_start
+            const int c = kof(t_start - 1) - r;
+            if (r < h && c >= 0 && c < w) prev = S[(long)r * w + c];
+        }
+        In cur[RW_PF];
+#pragma unroll
+        for (int d = 0; d < RW_PF; ++d) ld(t_start + d, redo, cur[d]);
+        __syncthreads();
+        if (lane == (DIR > 0 ? 63 : 0)) xch[(t_start + 1) & 1][wv] = prev;
+        if (threadIdx.x < 16) { chg[0][threadIdx.x] = 1; chg[1][threadIdx.x] = 1; }
+        __syncthreads();
+        bool stop = false;
+        for (int t0 = t_start; t0 < KS && !stop; t0 += RW_PF) {
+            In nxt[RW_PF];
+#pragma unroll
+            for (int d = 0; d < RW_PF; ++d) ld(t0 + RW_PF + d, redo, nxt[d]);
+#pragma unroll
+            for (int d = 0; d < RW_PF; ++d) {
+                const int t = t0 + d;
+                if (t >= KS) break;
+                if (DIR < 0 && redo && t - 1 > t_guard) {
+                    // the previous diagonal came out equal to the previous pass's: so would every later one
+                    int any = 0;
+                    for (int q = 0; q < nw; ++q) any |= chg[(t + 1) & 1][q];
+                    if (!any) { stop = true; break; }
+                }
+                const int k = kof(t);
+                const int c = k - r;
+                const bool act = r < h && c >= 0 && c < w;
+                const int o = DIR > 0 ? (int)(int8_t)(cur[d].code & 0xff) : (int)(int8_t)cur[d].f1;
+                const bool cond = (cur[d].code >> (DIR > 0 ? 8 : 9)) & 1;
+                const unsigned long long m = cur[d].m;
+                // the neighbour row's state at the previous step: thread r - 1 (DIR > 0) / r + 1 (DIR < 0)
+                const int pw = DIR > 0 ? (wv > 0 ? xch[(t + 1) & 1][wv - 1] : -1)
+                                       : (wv + 1 < nw ? xch[(t + 1) & 1][wv + 1] : -1);
+                int a = DIR > 0 ? __builtin_amdgcn_update_dpp(pw, prev, 0x138, 0xf, 0xf, false)    // wave_shr:1
+                                : __builtin_amdgcn_update_dpp(pw, prev, 0x130, 0xf, 0xf, false);   // wave_shl:1
+                if (DIR < 0 && r == h - 1) a = -1;
+                int F = o;
+                if (o == -2) {
+                    int D = (cond && mbit(m, a)) ? a : -2;
+                    if (DIR < 0 && c == w - 1) {
+                        upw_free = D == -2 && r <= h - 2;
+                        mw = m;
+                        if (upw_free && act) D = wasm[r];   // the assumed wrap push (-2: none)
+                    }
+                    const bool ch = DIR > 0 ? (r <= h - 2 && c >= 1) : (r >= 1 && c <= w - 2);
+                    if (D == -2 && ch && mbit(m, prev)) D = prev;
+                    F = D;
+                }
+                if (DIR < 0 && act && c == 0 && r <= h - 2) wdet[r] = (upw_free && mbit(mw, a)) ? (int8_t)a : (int8_t)-2;
+                bool changed = false;
+                if (act) {
+                    if (DIR > 0) f1[(long)k * h + r] = (int8_t)F;
+                    else {
+                        changed = redo && F != (int)(int8_t)cur[d].old;
+                        S[(long)r * w + c] = (int8_t)F;
+                    }
+                    prev = F;
+                }
+                if (lane == (DIR > 0 ? 63 : 0)) xch[t & 1][wv] = prev;
+                if (DIR < 0 && redo) {
+                    const bool wchg = __any(changed);
+                    if (lane == 0) chg[t & 1][wv] = wchg;
+                }
+                // LDS-only barrier: the exchange slots are the only shared state (no wait for the prefetches)
+                __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
+                __builtin_amdgcn_s_barrier();
+            }
+#pragma unroll
+            for (int d = 0; d < RW_PF; ++d) cur[d] = nxt[d];
+        }
+        if (DIR > 0) break;
+        // the last row (first in sweep order) whose detected wrap push differs from the assumed one
+        if (threadIdx.x == 0) { s_red = -1; s_min = h; }
+        __syncthreads();
+        const bool mis = r <= h - 2 && wdet[r] != wasm[r];
+        if (mis) { atomicMax(&s_red, r); atomicMin(&s_min, r); }
+        __syncthreads();
+        const int rs = s_red;
+        if (rs < 0) {
+            if (threadIdx.x == 0 && pass > 0) fb[8 + s] = pass;   // re-runs this sensor needed (inspection)
+            break;
+        }
+        if (pass >= RW_MAX_REDO) {   // give up: the single-wave kernel finishes the sweep from that row
+            if (threadIdx.x == 0) { fb[s] = rs + 1; fb[8 + s] = pass; }
+            break;
+        }
+        if (mis) wasm[r] = wdet[r];
+        t_start = KS - 1 - (rs + w - 1);      // the step of diagonal rs + w - 1
+        t_guard = KS - 1 - (s_min + w - 1);   // the step of the lowest changed assumption
+        __syncthreads();
+    }
+}
+
+// The exact second sweep for a sensor whose wavefront saw the wrap push fire, first at target row r0 = fb - 1:
+// rows below r0 are exact (nothing they depend on fired), so rows 0..r0 get the first sweep's states back and
+// the single-wave sweep resumes at source row r0 + 1 (re-chaining a swept row leaves it unchanged).
+template <int K>
+__global__ void __launch_bounds__(64) k_refine_fb(const int8_t* __restrict__ f1_all, int8_t* __restrict__ S_all,
+                                                 const unsigned long long* __restrict__ MK, const int* __restrict__ fb,
+                                                 int w, int h) {
+    const int s = blockIdx.x;
+    const int r0 = fb[s] - 1;
+    if (r0 < 0) return;
+    const long N = (long)w * h, SK = (long)(h + w - 1) * h;
+    for (long j = threadIdx.x; j < (long)(r0 + 1) * w; j += 64) {
+        const int r = (int)(j / w), c = (int)(j - (long)r * w);
+        S_all[s * N + j] = f1_all[s * SK + (long)(r + c) * h + r];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    refine_sweeps<K>(S_all, MK, w, h, s, 2, r0 + 1);
 }
 
 __global__ void k_refine_final(const int8_t* __restrict__ state, const int* __restrict__ lab, int N,
@@ -1127,9 +1361,11 @@ __global__ void k_alloc(const int* __restrict__ nmodels, const PlaneOut* __restr
     unsigned long long t = 1024;
     while (t < 2ull * (unsigned long long)cand && t < cap) t <<= 1;
     totals[2] = (long)(t - 1);   // hash mask
+    totals[3] = cand;            // inliers of the regions without a contour (0: the voxel stage has no work)
 }
 
 __global__ void k_vox_clear(VoxCell* __restrict__ tab, const long* __restrict__ totals) {
+    if (totals[3] == 0) return;
     const unsigned long long used = (unsigned long long)totals[2] + 1;
     for (unsigned long long c = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; c < used;
          c += (unsigned long long)gridDim.x * blockDim.x) {
@@ -1146,82 +1382,106 @@ __device__ __forceinline__ unsigned long long vhash(unsigned long long tag, unsi
     return (tag * 0x9E3779B97F4A7C15ull >> 20) & mask;
 }
 
-// Points are pre-summed per wave over lanes with the same (region, voxel) tag (consecutive pixels of
-// a row mostly share a voxel), so one insertion + four atomics serve a whole group; new voxels are
-// counted per region in LDS and flushed once per workgroup.
-constexpr int VOX_TPB = 256;
+// Only the inliers of regions without a contour are hashed.  A workgroup takes VOX_PX consecutive pixels (a few
+// rows of a sensor, so its points fall into a few dozen voxels), sums them per (region, voxel) in an LDS hash
+// table (exact double sums: order-free), then flushes one update per voxel it touched into the global table.
+// New voxels are counted per region in LDS and flushed once per workgroup.
+constexpr int VOX_TPB = 256, VOX_PX = 1024, VOX_LT = 256;
+
+__device__ __forceinline__ void vox_global_add(VoxCell* __restrict__ tab, unsigned long long mask,
+                                               unsigned long long tag, double x, double y, double z, unsigned n,
+                                               int* __restrict__ nnew_slot, int* __restrict__ err) {
+    unsigned long long hsh = vhash(tag, mask);
+    for (unsigned long long probe = 0;; ++probe) {
+        const unsigned long long prev = atomicCAS(&tab[hsh].tag, 0ull, tag);
+        if (prev == 0ull) { atomicAdd(nnew_slot, 1); break; }
+        if (prev == tag) break;
+        hsh = (hsh + 1) & mask;
+        if (probe > mask) { atomicOr(err, 16); return; }
+    }
+    atomicAdd(&tab[hsh].s[0], x);
+    atomicAdd(&tab[hsh].s[1], y);
+    atomicAdd(&tab[hsh].s[2], z);
+    atomicAdd(&tab[hsh].cnt, n);
+}
 
 __global__ void __launch_bounds__(VOX_TPB) k_vox_hash(const float4* __restrict__ cloud, const int8_t* __restrict__ state,
-                                                     int N, PlaneOut* __restrict__ out, VoxCell* __restrict__ tab,
-                                                     const long* __restrict__ totals, int* __restrict__ err) {
+                                                     int N, const int* __restrict__ nmodels, PlaneOut* __restrict__ out,
+                                                     VoxCell* __restrict__ tab, const long* __restrict__ totals,
+                                                     int* __restrict__ err) {
+    if (totals[3] == 0) return;
     __shared__ int nnew[8 * R360_MAX_MODELS];
-    for (int q = threadIdx.x; q < 8 * R360_MAX_MODELS; q += VOX_TPB) nnew[q] = 0;
-    __syncthreads();
+    __shared__ unsigned char cand[8 * R360_MAX_MODELS];
+    __shared__ long long bnd[8 * R360_MAX_MODELS][5];   // voxel origin b0..b2 and extents d0, d1 of a region
+    __shared__ unsigned long long ltag[VOX_LT];
+    __shared__ double lsum[3][VOX_LT];
+    __shared__ unsigned lcnt[VOX_LT];
+    __shared__ int any;
     const long total = 8L * N;
-    const unsigned long long mask = (unsigned long long)totals[2];
+    const long i0 = (long)blockIdx.x * VOX_PX;
+    const int s0 = (int)(i0 / N), s1 = (int)(min(total, i0 + VOX_PX) - 1) / N;   // sensors of this block
     const float inv = 1.0f / 0.05f;
-    const int lane = threadIdx.x & 63;
-    const long stride = (long)gridDim.x * VOX_TPB;
-    for (long i0 = blockIdx.x * (long)VOX_TPB + (threadIdx.x & ~63); i0 < total; i0 += stride) {
-        const long i = i0 + lane;
-        unsigned long long tag = 0;
-        double px = 0, py = 0, pz = 0;
-        int sm = -1;
-        if (i < total) {
-            const int m = state[i];
-            if (m >= 0) {
-                const int s = (int)(i / N);
-                const PlaneOut& O = out[s * R360_MAX_MODELS + m];
-                if (O.n_contour == 0) {
-                    const float4 p = cloud[i];
-                    const long long b0 = (long long)floorf(O.bmin[0] * inv), b1 = (long long)floorf(O.bmin[1] * inv),
-                                    b2 = (long long)floorf(O.bmin[2] * inv);
-                    const long long d0 = (long long)floorf(O.bmax[0] * inv) - b0 + 1,
-                                    d1 = (long long)floorf(O.bmax[1] * inv) - b1 + 1;
-                    const long long key = ((long long)floorf(p.x * inv) - b0) + ((long long)floorf(p.y * inv) - b1) * d0 +
-                                          ((long long)floorf(p.z * inv) - b2) * d0 * d1;
-                    sm = s * R360_MAX_MODELS + m;
-                    tag = ((unsigned long long)(sm + 1) << 48) | (unsigned long long)key;
-                    px = p.x; py = p.y; pz = p.z;
-                }
-            }
-        }
-        unsigned long long pending = __ballot(tag != 0);
-        while (pending) {
-            const int leader = __ffsll((long long)pending) - 1;
-            const unsigned long long ltag = __shfl(tag, leader, 64);
-            const bool mine = tag == ltag && ((pending >> lane) & 1);
-            const unsigned long long grp = __ballot(mine);
-            // group sums (exact in double: order-free)
-            double gx = mine ? px : 0.0, gy = mine ? py : 0.0, gz = mine ? pz : 0.0;
-            for (int o = 32; o > 0; o >>= 1) {
-                gx += __shfl_xor(gx, o, 64);
-                gy += __shfl_xor(gy, o, 64);
-                gz += __shfl_xor(gz, o, 64);
-            }
-            if (lane == leader) {
-                unsigned long long hsh = vhash(ltag, mask);
-                bool ok = true;
-                for (unsigned long long probe = 0;; ++probe) {
-                    const unsigned long long prev = atomicCAS(&tab[hsh].tag, 0ull, ltag);
-                    if (prev == 0ull) { atomicAdd(&nnew[sm], 1); break; }
-                    if (prev == ltag) break;
-                    hsh = (hsh + 1) & mask;
-                    if (probe > mask) { atomicOr(err, 16); ok = false; break; }
-                }
-                if (ok) {
-                    atomicAdd(&tab[hsh].s[0], gx);
-                    atomicAdd(&tab[hsh].s[1], gy);
-                    atomicAdd(&tab[hsh].s[2], gz);
-                    atomicAdd(&tab[hsh].cnt, (unsigned)__popcll(grp));
-                }
-            }
-            pending &= ~grp;
+    if (threadIdx.x == 0) any = 0;
+    for (int q = threadIdx.x; q < VOX_LT; q += VOX_TPB) {
+        ltag[q] = 0ull; lsum[0][q] = 0.0; lsum[1][q] = 0.0; lsum[2][q] = 0.0; lcnt[q] = 0u;
+    }
+    for (int q = threadIdx.x; q < (s1 - s0 + 1) * R360_MAX_MODELS; q += VOX_TPB) {
+        const int sm = s0 * R360_MAX_MODELS + q;
+        const PlaneOut& O = out[sm];
+        const bool c = (q % R360_MAX_MODELS) < nmodels[sm / R360_MAX_MODELS] && O.n_contour == 0;
+        cand[sm] = c;
+        nnew[sm] = 0;
+        if (c) {
+            bnd[sm][0] = (long long)floorf(O.bmin[0] * inv);
+            bnd[sm][1] = (long long)floorf(O.bmin[1] * inv);
+            bnd[sm][2] = (long long)floorf(O.bmin[2] * inv);
+            bnd[sm][3] = (long long)floorf(O.bmax[0] * inv) - bnd[sm][0] + 1;
+            bnd[sm][4] = (long long)floorf(O.bmax[1] * inv) - bnd[sm][1] + 1;
+            any = 1;
         }
     }
     __syncthreads();
-    for (int q = threadIdx.x; q < 8 * R360_MAX_MODELS; q += VOX_TPB)
-        if (nnew[q]) atomicAdd(&out[q].n_vox, nnew[q]);
+    if (!any) return;
+    const unsigned long long mask = (unsigned long long)totals[2];
+    for (int k = threadIdx.x; k < VOX_PX; k += VOX_TPB) {
+        const long i = i0 + k;
+        if (i >= total) break;
+        const int m = state[i];
+        if (m < 0) continue;
+        const int s = (int)(i / N);
+        const int sm = s * R360_MAX_MODELS + m;
+        if (!cand[sm]) continue;
+        const float4 p = cloud[i];
+        const long long* B = bnd[sm];
+        const long long key = ((long long)floorf(p.x * inv) - B[0]) + ((long long)floorf(p.y * inv) - B[1]) * B[3] +
+                              ((long long)floorf(p.z * inv) - B[2]) * B[3] * B[4];
+        const unsigned long long tag = ((unsigned long long)(sm + 1) << 48) | (unsigned long long)key;
+        unsigned q = (unsigned)vhash(tag, VOX_LT - 1);
+        bool ok = false;
+        for (int probe = 0; probe < VOX_LT; ++probe) {
+            const unsigned long long prev = atomicCAS(&ltag[q], 0ull, tag);
+            if (prev == 0ull || prev == tag) { ok = true; break; }
+            q = (q + 1) & (VOX_LT - 1);
+        }
+        if (ok) {
+            atomicAdd(&lsum[0][q], (double)p.x);
+            atomicAdd(&lsum[1][q], (double)p.y);
+            atomicAdd(&lsum[2][q], (double)p.z);
+            atomicAdd(&lcnt[q], 1u);
+        } else {   // more distinct voxels than VOX_LT in one block: straight to the global table
+            vox_global_add(tab, mask, tag, p.x, p.y, p.z, 1u, &nnew[sm], err);
+        }
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < VOX_LT; q += VOX_TPB) {
+        const unsigned long long tag = ltag[q];
+        if (tag) vox_global_add(tab, mask, tag, lsum[0][q], lsum[1][q], lsum[2][q], lcnt[q], &nnew[(int)(tag >> 48) - 1], err);
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < (s1 - s0 + 1) * R360_MAX_MODELS; q += VOX_TPB) {
+        const int sm = s0 * R360_MAX_MODELS + q;
+        if (nnew[sm]) atomicAdd(&out[sm].n_vox, nnew[sm]);
+    }
 }
 
 __global__ void k_vox_alloc(const int* __restrict__ nmodels, PlaneOut* __restrict__ out, long* __restrict__ totals,
@@ -1245,6 +1505,7 @@ constexpr int VOXC_TPB = 1024, VOXC_BLOCKS = 256;
 __global__ void __launch_bounds__(VOXC_TPB) k_vox_compact(const VoxCell* __restrict__ tab,
                                                          const long* __restrict__ totals, PlaneOut* __restrict__ out,
                                                          VoxOut* __restrict__ pool, long pool_cap) {
+    if (totals[3] == 0) return;
     __shared__ int cnt[8 * R360_MAX_MODELS], base[8 * R360_MAX_MODELS];
     for (int q = threadIdx.x; q < 8 * R360_MAX_MODELS; q += VOXC_TPB) cnt[q] = 0;
     __syncthreads();
@@ -1280,10 +1541,15 @@ __global__ void __launch_bounds__(VOXC_TPB) k_vox_compact(const VoxCell* __restr
 
 }  // namespace
 
-// rows per band of the banded refinement (R360_REFINE_ROWS overrides; 0 = the single-wave sweeps)
+// buffers of the wavefront refinement (skewed layout, [8][h + w - 1][h] each)
+struct RefineWaveBufs { uint16_t* code; unsigned long long* msk; int8_t* f1; };
+
+// refinement mode: -1 the wavefront sweeps (default), 0 the single-wave sweeps, rb > 0 banded with rb rows per
+// band (R360_REFINE_ROWS overrides)
 int refine_band_rows(int h) {
-    static const int env = getenv("R360_REFINE_ROWS") ? atoi(getenv("R360_REFINE_ROWS")) : -1;
-    int rb = env >= 0 ? env : 16;
+    static const int env = getenv("R360_REFINE_ROWS") ? atoi(getenv("R360_REFINE_ROWS")) : -2;
+    int rb = env >= -1 ? env : -1;
+    if (rb < 0) return h <= 1024 ? -1 : 0;
     if (rb > 0 && (h + rb - 1) / rb > R360_REFINE_BANDS) rb = (h + R360_REFINE_BANDS - 1) / R360_REFINE_BANDS;
     return rb;
 }
@@ -1291,8 +1557,26 @@ int refine_band_rows(int h) {
 // refine()'s two sweeps over 8 sensors' states S (in place), closeness masks MK.  rb > 0: banded (phases 1 and
 // 2 per sweep; S2 holds the first sweep's output); rb = 0: one wave per sensor walks every row (k_refine).
 int launch_refine_sweeps(hipStream_t st, int8_t* S, int8_t* S2, const unsigned long long* MK, int8_t* bnd, int* flag,
-                         int w, int h, int rb) {
+                         int w, int h, int rb, const RefineWaveBufs* wb) {
     const int K = (w + 63) / 64;
+    if (rb < 0 && (w < 2 || h > 1024 || !wb)) rb = 0;
+    if (rb < 0) {
+        const long slots = 8L * (h + w - 1) * h;
+        hipLaunchKernelGGL(k_refine_skew, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, st, S, MK, w, h, wb->code,
+                           wb->msk, flag);
+        const int tpb = 64 * ((h + 63) / 64);
+        hipLaunchKernelGGL(k_refine_wave<1>, dim3(8), dim3(tpb), 0, st, wb->code, wb->msk, wb->f1, S, flag, w, h);
+        hipLaunchKernelGGL(k_refine_wave<-1>, dim3(8), dim3(tpb), 0, st, wb->code, wb->msk, wb->f1, S, flag, w, h);
+        switch (K) {
+#define R360_FB_CASE(k) case k: hipLaunchKernelGGL(k_refine_fb<k>, dim3(8), dim3(64), 0, st, wb->f1, S, MK, flag, w, h); break;
+            R360_FB_CASE(1) R360_FB_CASE(2) R360_FB_CASE(3) R360_FB_CASE(4) R360_FB_CASE(5)
+            R360_FB_CASE(6) R360_FB_CASE(7) R360_FB_CASE(8) R360_FB_CASE(9) R360_FB_CASE(10)
+#undef R360_FB_CASE
+            default: r360_set_error("refine: cloud width %d > 640 unsupported", w); return -1;
+        }
+        R360_HIP(hipGetLastError());
+        return 0;
+    }
     if (rb > 0 && (h + rb - 1) / rb > R360_REFINE_BANDS) { r360_set_error("refine: %d rows per band too few", rb); return -2; }
     const int nb = rb > 0 ? (h + rb - 1) / rb : 0;
     switch (K) {
@@ -1363,7 +1647,8 @@ int launch_segmentation(r360_frame* f) {
     slot = timing_begin(ctx, "k_refine");
     hipLaunchKernelGGL(k_refine_init, dim3(blocks), dim3(256), 0, st, P.cloud, P.lab, N, P.models, P.nmodels, P.state,
                        P.mask);
-    if (launch_refine_sweeps(st, P.state, P.state2, P.mask, P.rbnd, P.rflag, w, h, refine_band_rows(h))) return -1;
+    const RefineWaveBufs wb{P.rcode, P.rmsk, P.rf1};
+    if (launch_refine_sweeps(st, P.state, P.state2, P.mask, P.rbnd, P.rflag, w, h, refine_band_rows(h), &wb)) return -1;
     hipLaunchKernelGGL(k_refine_final, dim3(blocks), dim3(256), 0, st, P.state, P.lab, N, P.models, P.labf);
     timing_end(ctx, slot);
     R360_HIP(hipGetLastError());
@@ -1388,10 +1673,10 @@ int launch_segmentation(r360_frame* f) {
     timing_end(ctx, slot);
     R360_HIP(hipGetLastError());
     slot = timing_begin(ctx, "k_voxel");
-    hipLaunchKernelGGL(k_vox_clear, dim3((unsigned)((ctx->vhash_cap + 255) / 256)), dim3(256), 0, st, ctx->d_vhash,
-                       P.totals);
-    hipLaunchKernelGGL(k_vox_hash, dim3(blocks), dim3(VOX_TPB), 0, st, P.cloud, P.state, N, P.out, ctx->d_vhash,
-                       P.totals, P.err);
+    // the voxel kernels exit at entry when no region lacks a contour (totals[3] == 0, the usual case)
+    hipLaunchKernelGGL(k_vox_clear, dim3(256), dim3(256), 0, st, ctx->d_vhash, P.totals);
+    hipLaunchKernelGGL(k_vox_hash, dim3((unsigned)((total + VOX_PX - 1) / VOX_PX)), dim3(VOX_TPB), 0, st, P.cloud,
+                       P.state, N, P.nmodels, P.out, ctx->d_vhash, P.totals, P.err);
     hipLaunchKernelGGL(k_vox_alloc, dim3(1), dim3(64), 0, st, P.nmodels, P.out, P.totals, P.vox_cap, P.err);
     hipLaunchKernelGGL(k_vox_compact, dim3(VOXC_BLOCKS), dim3(VOXC_TPB), 0, st, ctx->d_vhash, P.totals, P.out, P.vox,
                        P.vox_cap);
@@ -1400,8 +1685,10 @@ int launch_segmentation(r360_frame* f) {
     return 0;
 }
 
-// Test hook: refine()'s two sweeps on given states / closeness masks of 8 sensors (w x h each), banded with
-// rb rows per band (0 = the single-wave sweeps); out receives the swept states.
+// Test hook: refine()'s two sweeps on given states / closeness masks of 8 sensors (w x h each): rb < 0 the
+// wavefront sweeps, 0 the single-wave sweeps, rb > 0 banded with rb rows per band; out receives the swept
+// states.  Returns the number of sensors whose wavefront second sweep needed wrap-push corrections (re-runs
+// or the single-wave fallback; rb < 0), else 0.
 extern "C" int r360_refine_eval(const int8_t* state, const uint64_t* mask, int w, int h, int rb, int8_t* out) {
     if (!state || !mask || !out || w < 1 || h < 1 || w > 640) { r360_set_error("r360_refine_eval: bad arguments"); return -2; }
     const size_t T = 8 * (size_t)w * h;
@@ -1415,8 +1702,23 @@ extern "C" int r360_refine_eval(const int8_t* state, const uint64_t* mask, int w
     R360_HIP(hipMalloc(&flag, sizeof(int) * 8 * R360_REFINE_BANDS));
     R360_HIP(hipMemcpy(S, state, T, hipMemcpyHostToDevice));
     R360_HIP(hipMemcpy(MK, mask, sizeof(unsigned long long) * T, hipMemcpyHostToDevice));
-    const int rc = launch_refine_sweeps(0, S, S2, MK, bnd, flag, w, h, rb);
-    if (rc == 0) R360_HIP(hipMemcpy(out, S, T, hipMemcpyDeviceToHost));
+    RefineWaveBufs wb{};
+    const size_t SK = 8 * (size_t)(h + w - 1) * h;
+    R360_HIP(hipMalloc(&wb.code, sizeof(uint16_t) * SK));
+    R360_HIP(hipMalloc(&wb.msk, sizeof(unsigned long long) * SK));
+    R360_HIP(hipMalloc(&wb.f1, SK));
+    int rc = launch_refine_sweeps(0, S, S2, MK, bnd, flag, w, h, rb, &wb);
+    if (rc == 0) {
+        R360_HIP(hipMemcpy(out, S, T, hipMemcpyDeviceToHost));
+        if (rb < 0 && w >= 2 && h <= 1024) {
+            int fbh[16];
+            R360_HIP(hipMemcpy(fbh, flag, sizeof(fbh), hipMemcpyDeviceToHost));
+            for (int k = 0; k < 8; ++k) rc += (fbh[k] != 0 || fbh[8 + k] != 0);
+            if (getenv("R360_REFINE_TRACE"))
+                for (int k = 0; k < 8; ++k) fprintf(stderr, "refine sensor %d: re-runs %d fallback row %d\n", k, fbh[8 + k], fbh[k] - 1);
+        }
+    }
     (void)hipFree(S); (void)hipFree(S2); (void)hipFree(MK); (void)hipFree(bnd); (void)hipFree(flag);
+    (void)hipFree(wb.code); (void)hipFree(wb.msk); (void)hipFree(wb.f1);
     return rc;
 }

@@ -188,6 +188,9 @@ struct PlaneBufs {
     int8_t* rbnd = nullptr;          // banded refinement: each band's assignments into the next band's first row
     int* rflag = nullptr;            //   [8][R360_REFINE_BANDS][w] and whether they changed that row [8][..]
     unsigned long long* mask = nullptr;  // closeness masks [8][N]
+    uint16_t* rcode = nullptr;           // wavefront refinement, skewed [8][h + w - 1][h]: state | push conditions
+    unsigned long long* rmsk = nullptr;  //   closeness masks, skewed
+    int8_t* rf1 = nullptr;               //   first sweep's states, skewed
     PlaneOut* out = nullptr;         // [8][R360_MAX_MODELS]
     float4* contour = nullptr;       // contour pool
     long contour_cap = 0;

@@ -95,7 +95,7 @@ def test_banded_sweeps_equal_python_restatement(seed, dense):
     S, M = _inputs(h, w, seed, dense)
     ref = np.stack([_refine_ref(S[s], M[s]) for s in range(8)])
     assert not np.array_equal(ref, S)            # the sweeps changed something
-    for rb in (0, 1, 3, 8, 16, 37):
+    for rb in (-1, 0, 1, 3, 8, 16, 37):
         out = R.refine_eval(S, M, rb)
         assert np.array_equal(out, ref), (rb, np.argwhere(out != ref)[:5])
 
@@ -105,5 +105,33 @@ def test_banded_sweeps_equal_single_wave(h, w):
     for seed in (11, 12):
         S, M = _inputs(h, w, seed)
         one = R.refine_eval(S, M, 0)
-        for rb in [r for r in (4, 16, 32) if -(-h // r) <= 64]:
+        for rb in [r for r in (-1, 4, 16, 32) if -(-h // r) <= 64]:
             assert np.array_equal(R.refine_eval(S, M, rb), one), (h, w, rb, seed)
+
+
+def _no_wrap(S):
+    """The same states with the last column unlabelled (-1): the second sweep's flat-index wrap push (column 0
+    of row r+1 into (r, w-1)) can then never fire, so the wavefront needs no fallback."""
+    S = S.copy()
+    S[:, :, -1] = -1
+    return S
+
+
+@pytest.mark.parametrize("h,w", [(37, 70), (240, 320), (480, 640)])
+def test_wavefront_sweeps_both_paths(h, w):
+    """The wavefront sweeps (the default refinement path) on both of its paths: no wrap push (pure wavefront,
+    checked against the sequential restatement / single-wave kernel) and wrap pushes firing (the fallback
+    sensor(s) redo the second sweep)."""
+    seen_fb = 0
+    for seed in (21, 22, 23):
+        S, M = _inputs(h, w, seed)
+        for St, want_fb in ((_no_wrap(S), False), (S, None)):
+            ref = (np.stack([_refine_ref(St[s], M[s]) for s in range(8)]) if h * w <= 37 * 70
+                   else R.refine_eval(St, M, 0))
+            out, nfb = R.refine_eval(St, M, -1, return_fallbacks=True)
+            assert np.array_equal(out, ref), (h, w, seed, np.argwhere(out != ref)[:5])
+            if want_fb is False:
+                assert nfb == 0
+            else:
+                seen_fb += nfb
+    assert seen_fb > 0   # the random fields do make the wrap push fire somewhere

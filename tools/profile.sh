@@ -18,8 +18,8 @@ TARGS="--streams 4 $ARGS"
 rc=0
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o trace -- python3 $R/bench.py $TARGS > $OUT/trace_bench.json 2> $OUT/trace.err || rc=1
 [ $rc = 0 ] && { timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE -d $OUT/pmc1 -o pmc1 -- python3 $R/bench.py $ARGS > /dev/null 2> $OUT/pmc1.err || rc=2; }
-[ $rc = 0 ] && { timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv --pmc FETCH_SIZE -d $OUT/pmc2 -o pmc2 -- python3 $R/bench.py $ARGS > /dev/null 2> $OUT/pmc2.err || rc=3; }
-[ $rc = 0 ] && { timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv --pmc WRITE_SIZE TCC_HIT_sum TCC_MISS_sum -d $OUT/pmc3 -o pmc3 -- python3 $R/bench.py $ARGS > /dev/null 2> $OUT/pmc3.err || rc=4; }
+[ $rc = 0 ] && { timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv --pmc FETCH_SIZE SQ_WAVES -d $OUT/pmc2 -o pmc2 -- python3 $R/bench.py $ARGS > /dev/null 2> $OUT/pmc2.err || rc=3; }
+[ $rc = 0 ] && { timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv --pmc WRITE_SIZE TCC_HIT_sum TCC_MISS_sum SQ_WAVES -d $OUT/pmc3 -o pmc3 -- python3 $R/bench.py $ARGS > /dev/null 2> $OUT/pmc3.err || rc=4; }
 # the traced command's bench line without the profiler (its in-kernel spans vs the trace's durations)
 [ $rc = 0 ] && { timeout -k 10 300 python3 $R/bench.py $TARGS > $OUT/bench_streams4.json 2> $OUT/bench_streams4.err || rc=5; }
 cd $R

@@ -41,7 +41,26 @@ def pmc(name):
     return float(np.median(vals)) if vals else None
 
 
+def pmc_per_job(name, waves_per_job):
+    """median over level-0 dispatches of counter / jobs (a batched launch runs one pass per pair: jobs =
+    SQ_WAVES of the same dispatch, collected in the same --pmc pass, / waves of one job's grid)"""
+    vals = []
+    for f in glob.glob(os.path.join(src, "pmc*", "*counter_collection.csv")):
+        per = {}
+        for r in csv.DictReader(open(f)):
+            if is_l0(r["Kernel_Name"]):
+                per.setdefault(r["Dispatch_Id"], {})[r["Counter_Name"]] = float(r["Counter_Value"])
+        for d in per.values():
+            if name in d and d.get("SQ_WAVES"):
+                vals.append(d[name] / (d["SQ_WAVES"] / waves_per_job))
+    return float(np.median(vals)) if vals else None
+
+
 fetch, write = pmc("FETCH_SIZE"), pmc("WRITE_SIZE")
+# one job's grid: the level-0 launch's x extent in workgroups x waves per workgroup
+waves_per_job = (gmax // 64) if gmax else None
+fetch_j = pmc_per_job("FETCH_SIZE", waves_per_job) if waves_per_job else None
+write_j = pmc_per_job("WRITE_SIZE", waves_per_job) if waves_per_job else None
 out = {
     "kernel": "k_icp_pass<PHOTO_DEPTH> level 0", "grid_threads": gmax, "launches": len(l0),
     "avg_duration_us": float(np.mean(l0)), "median_duration_us": float(np.median(l0)),
@@ -49,6 +68,10 @@ out = {
     # MI355X_MICROARCH.md §HBM: FETCH_SIZE counts 64 B per 128-B request on gfx950 -> double it
     "hbm_bytes_per_launch": (2 * fetch * 1024 + write * 1024) if fetch is not None and write is not None else None,
     "note": "FETCH_SIZE doubled per the gfx950 correction; Infinity-Cache hits are counted by the counter",
+    # per pair-pass (a batched launch runs one level-0 pass per pair): the figure bench.py scales by its own
+    # pairs per launch
+    "waves_per_job": waves_per_job, "FETCH_SIZE_kB_per_pair_pass": fetch_j, "WRITE_SIZE_kB_per_pair_pass": write_j,
+    "hbm_bytes_per_pair_pass": (2 * fetch_j * 1024 + write_j * 1024) if fetch_j is not None and write_j is not None else None,
 }
 for k in ("SQ_INSTS_VALU", "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_INST_ANY", "GRBM_GUI_ACTIVE",
           "TCC_HIT_sum", "TCC_MISS_sum", "SQ_ACTIVE_INST_VALU", "SQ_INSTS_VMEM_RD"):
