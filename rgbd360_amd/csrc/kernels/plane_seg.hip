@@ -205,7 +205,8 @@ __global__ void k_ccl_label(const int* __restrict__ root, const int* __restrict_
 __global__ void __launch_bounds__(1024) k_big_list(const int* __restrict__ cnt, const int* __restrict__ nlab, int N,
                                                    int min_inliers, int* __restrict__ big, int* __restrict__ nbig,
                                                    int maxbig, int* __restrict__ err, int* __restrict__ bmap,
-                                                   int* __restrict__ boff) {
+                                                   int* __restrict__ boff, r360p::Moments* __restrict__ mom,
+                                                   int* __restrict__ bfirst) {
     __shared__ int sh[17];
     const int s = blockIdx.x;
     const int n = nlab[s];
@@ -242,6 +243,12 @@ __global__ void __launch_bounds__(1024) k_big_list(const int* __restrict__ cnt, 
     if (threadIdx.x == 0) {
         nbig[s] = acc < maxbig ? acc : maxbig;
         if (acc > maxbig) atomicOr(err, 2);
+    }
+    // k_label_moments merges its workgroups' partial sums into zeroed accumulators
+    const int nb = acc < maxbig ? acc : maxbig;
+    for (int q = threadIdx.x; q < nb; q += blockDim.x) {
+        r360p::moments_zero(mom[s * maxbig + q]);
+        bfirst[s * maxbig + q] = N;
     }
 }
 
@@ -363,27 +370,64 @@ __device__ __forceinline__ float block_fminmax(float v, bool mx, float* sh) {
     return v;
 }
 
-__global__ void __launch_bounds__(MOM_TPB) k_label_moments(const float4* __restrict__ cloud, const int* __restrict__ cnt,
+// Exact merge of a workgroup's partial moments into global accumulators: 64-bit atomic adds (two's complement,
+// order-free); an int128 sum is a low/high pair whose carry each adder derives from the old low word it got back,
+// so the pair ends at the exact total whatever the order.
+__device__ void moments_atomic_merge(r360p::Moments* dst, const r360p::Moments& m) {
+    auto add64 = [](long long* p, long long v) {
+        atomicAdd(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v);
+    };
+    add64(&dst->n, m.n);
+    for (int k = 0; k < 3; ++k) add64(&dst->s1[k], m.s1[k]);
+    for (int k = 0; k < 4; ++k) add64(&dst->c[k], m.c[k]);
+    for (int k = 0; k < 6; ++k) {
+        unsigned long long* w = reinterpret_cast<unsigned long long*>(&dst->s2[k]);
+        const unsigned long long lo = (unsigned long long)m.s2[k];
+        const unsigned long long hi = (unsigned long long)(m.s2[k] >> 64);
+        const unsigned long long old = atomicAdd(w, lo);
+        atomicAdd(w + 1, hi + (old + lo < old ? 1ull : 0ull));
+    }
+}
+
+// float min / max through integer atomics (the accumulators start at +inf / -inf; -0 orders below +0)
+__device__ __forceinline__ void atomic_fmin(float* p, float v) {
+    if (v >= 0.f) atomicMin(reinterpret_cast<int*>(p), __float_as_int(v));
+    else atomicMax(reinterpret_cast<unsigned*>(p), __float_as_uint(v));
+}
+__device__ __forceinline__ void atomic_fmax(float* p, float v) {
+    if (v >= 0.f) atomicMax(reinterpret_cast<int*>(p), __float_as_int(v));
+    else atomicMin(reinterpret_cast<unsigned*>(p), __float_as_uint(v));
+}
+
+// grid (LMOM_GX, 8, LMOM_SPLIT): workgroup x walks labels x, x + LMOM_GX, ...; blockIdx.z takes every LMOM_SPLIT-th
+// slice of MOM_UNROLL * LMOM_TPB list entries, so a large label's pixels are summed by several workgroups at once
+// (exact merges into the sums k_big_list zeroed)
+
+constexpr int LMOM_TPB = 256, LMOM_GX = 128, LMOM_SPLIT = 4;   // labels are mostly small: 4 waves each
+
+__global__ void __launch_bounds__(LMOM_TPB) k_label_moments(const float4* __restrict__ cloud, const int* __restrict__ cnt,
                                                           int N, const int* __restrict__ big,
                                                           const int* __restrict__ nbig, int maxbig,
                                                           const int* __restrict__ boff, const int* __restrict__ blist,
                                                           r360p::Moments* __restrict__ mom, int* __restrict__ bfirst) {
     __shared__ MomShared sh;
     __shared__ int smin[MOM_NW];
-    const int s = blockIdx.y, b = blockIdx.x;
-    if (b >= nbig[s]) return;
+    const int s = blockIdx.y;
+    const int nb = nbig[s];
+    for (int b = blockIdx.x; b < nb; b += gridDim.x) {
     const int L = big[s * maxbig + b];
     const long base = (long)s * N;
     const int n = cnt[base + L];
     const int* li = blist + base + boff[s * maxbig + b];
+    if ((int)blockIdx.z * MOM_UNROLL * LMOM_TPB >= n) continue;
     r360p::Moments m;
     r360p::moments_zero(m);
     int first = N;
-    for (int k0 = threadIdx.x; k0 < n; k0 += MOM_UNROLL * MOM_TPB) {
+    for (int k0 = blockIdx.z * MOM_UNROLL * LMOM_TPB + threadIdx.x; k0 < n; k0 += LMOM_SPLIT * MOM_UNROLL * LMOM_TPB) {
         int j[MOM_UNROLL];
         float4 p[MOM_UNROLL];
 #pragma unroll
-        for (int u = 0; u < MOM_UNROLL; ++u) j[u] = k0 + u * MOM_TPB < n ? li[k0 + u * MOM_TPB] : -1;
+        for (int u = 0; u < MOM_UNROLL; ++u) j[u] = k0 + u * LMOM_TPB < n ? li[k0 + u * LMOM_TPB] : -1;
 #pragma unroll
         for (int u = 0; u < MOM_UNROLL; ++u) p[u] = j[u] >= 0 ? cloud[base + j[u]] : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
@@ -396,8 +440,10 @@ __global__ void __launch_bounds__(MOM_TPB) k_label_moments(const float4* __restr
     first = block_min(first, smin);
     block_reduce_moments(m, &sh);
     if (threadIdx.x == 0) {
-        mom[s * maxbig + b] = m;
-        bfirst[s * maxbig + b] = first;
+        moments_atomic_merge(mom + s * maxbig + b, m);
+        atomicMin(bfirst + s * maxbig + b, first);
+    }
+    __syncthreads();   // the LDS reduction scratch is reused by the next label
     }
 }
 
@@ -1063,7 +1109,14 @@ __global__ void k_refine_final(const int8_t* __restrict__ state, const int* __re
 
 // ------------------------------------------------------------------ per-model statistics
 // refined regions grouped by model: counts, then scatter (order inside a slice is free, as above)
-__global__ void k_model_count(const int* __restrict__ labf, int N, const int* __restrict__ mmap, int* __restrict__ mcnt) {
+__global__ void k_model_count(const int* __restrict__ labf, int N, const int* __restrict__ mmap, int* __restrict__ mcnt,
+                              PlaneOut* __restrict__ out) {
+    // k_model_stats merges its workgroups' partial sums and bounds into these
+    if (blockIdx.x == 0)
+        for (int q = threadIdx.x; q < 8 * R360_MAX_MODELS; q += blockDim.x) {
+            r360p::moments_zero(out[q].stats);
+            for (int k = 0; k < 3; ++k) { out[q].bmin[k] = __builtin_inff(); out[q].bmax[k] = -__builtin_inff(); }
+        }
     const long total = 8L * N, stride = (long)gridDim.x * blockDim.x;
     for (long i0 = blockIdx.x * (long)blockDim.x + (threadIdx.x & ~63); i0 < total; i0 += stride) {
         const long i = i0 + (threadIdx.x & 63);
@@ -1118,7 +1171,9 @@ __global__ void k_model_scatter(const int* __restrict__ labf, int N, const int* 
     }
 }
 
-__global__ void __launch_bounds__(MOM_TPB) k_model_stats(const float4* __restrict__ cloud, const uchar4* __restrict__ rgb,
+constexpr int MS_TPB = 256, MS_SPLIT = 16;   // model lists: 16 workgroups of 4 waves per model
+
+__global__ void __launch_bounds__(MS_TPB) k_model_stats(const float4* __restrict__ cloud, const uchar4* __restrict__ rgb,
                                                         int N, const PlaneModel* __restrict__ models,
                                                         const int* __restrict__ nmodels, const float* __restrict__ rt8,
                                                         const int* __restrict__ mcnt, const int* __restrict__ mlist,
@@ -1126,22 +1181,24 @@ __global__ void __launch_bounds__(MOM_TPB) k_model_stats(const float4* __restric
                                                         PlaneOut* __restrict__ out) {
     __shared__ MomShared sh;
     __shared__ float sred[MOM_NW];
-    const int s = blockIdx.y, m = blockIdx.x;
-    if (m >= nmodels[s]) return;
+    const int s = blockIdx.y;
+    const int nmod = nmodels[s];
+    for (int m = blockIdx.x; m < nmod; m += gridDim.x) {
     const PlaneModel& M = models[s * R360_MAX_MODELS + m];
     const float* T = rt8 + 16 * s;
     const long base = (long)s * N;
     const int n = mcnt[s * R360_MAX_MODELS + m];
     const int* li = mlist + base + model_offset(mcnt, s, m);
+    if (blockIdx.z > 0 && (int)blockIdx.z * MOM_UNROLL * MS_TPB >= n) continue;
     r360p::Moments mo;
     r360p::moments_zero(mo);
     float bx[6] = {3.4e38f, 3.4e38f, 3.4e38f, -3.4e38f, -3.4e38f, -3.4e38f};   // local-frame bounds
-    for (int k0 = threadIdx.x; k0 < n; k0 += MOM_UNROLL * MOM_TPB) {
+    for (int k0 = blockIdx.z * MOM_UNROLL * MS_TPB + threadIdx.x; k0 < n; k0 += MS_SPLIT * MOM_UNROLL * MS_TPB) {
         int j[MOM_UNROLL];
         float4 p[MOM_UNROLL];
         uchar4 c[MOM_UNROLL];
 #pragma unroll
-        for (int u = 0; u < MOM_UNROLL; ++u) j[u] = k0 + u * MOM_TPB < n ? li[k0 + u * MOM_TPB] : -1;
+        for (int u = 0; u < MOM_UNROLL; ++u) j[u] = k0 + u * MS_TPB < n ? li[k0 + u * MS_TPB] : -1;
 #pragma unroll
         for (int u = 0; u < MOM_UNROLL; ++u) {
             p[u] = j[u] >= 0 ? cloud[base + j[u]] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1165,15 +1222,22 @@ __global__ void __launch_bounds__(MOM_TPB) k_model_stats(const float4* __restric
     block_reduce_moments(mo, &sh);
     if (threadIdx.x == 0) {
         PlaneOut& O = out[s * R360_MAX_MODELS + m];
-        O.model = M;
-        O.stats = mo;
-        O.start = bfirst[s * maxbig + M.big];
-        for (int k = 0; k < 3; ++k) { O.bmin[k] = bx[k]; O.bmax[k] = bx[k + 3]; }
-        O.n_contour = 0;
-        O.contour_off = 0;
-        O.n_vox = 0;
-        O.vox_fill = 0;
-        O.vox_off = 0;
+        moments_atomic_merge(&O.stats, mo);
+        if (n > 0)
+            for (int k = 0; k < 3; ++k) { atomic_fmin(&O.bmin[k], bx[k]); atomic_fmax(&O.bmax[k], bx[k + 3]); }
+        if (blockIdx.z == 0) {
+            O.model = M;
+            O.start = bfirst[s * maxbig + M.big];
+            if (n == 0)
+                for (int k = 0; k < 3; ++k) { O.bmin[k] = bx[k]; O.bmax[k] = bx[k + 3]; }
+            O.n_contour = 0;
+            O.contour_off = 0;
+            O.n_vox = 0;
+            O.vox_fill = 0;
+            O.vox_off = 0;
+        }
+    }
+    __syncthreads();   // the LDS reduction scratch is reused by the next model
     }
 }
 
@@ -1633,11 +1697,11 @@ int launch_segmentation(r360_frame* f) {
     int* bmap = P.parent;
     int* mmap = P.root;
     hipLaunchKernelGGL(k_big_list, dim3(8), dim3(1024), 0, st, P.cnt, P.nlab, N, 80, P.big, P.nbig, R360_MAX_BIG, P.err,
-                       bmap, boff);
+                       bmap, boff, P.mom, bfirst);
     R360_HIP(hipMemsetAsync(bcur, 0, sizeof(int) * 8 * R360_MAX_BIG, st));
     hipLaunchKernelGGL(k_label_scatter, dim3(blocks), dim3(256), 0, st, P.lab, N, bmap, boff, bcur, P.blist,
                        R360_MAX_BIG);
-    hipLaunchKernelGGL(k_label_moments, dim3(R360_MAX_BIG, 8), dim3(MOM_TPB), 0, st, P.cloud, P.cnt, N, P.big, P.nbig,
+    hipLaunchKernelGGL(k_label_moments, dim3(LMOM_GX, 8, LMOM_SPLIT), dim3(LMOM_TPB), 0, st, P.cloud, P.cnt, N, P.big, P.nbig,
                        R360_MAX_BIG, boff, P.blist, P.mom, bfirst);
     R360_HIP(hipMemsetAsync(mmap, 0xff, sizeof(int) * total, st));
     hipLaunchKernelGGL(k_plane_fit, dim3(1), dim3(64), 0, st, P.mom, P.big, P.nbig, R360_MAX_BIG, 0.001f, P.models,
@@ -1654,9 +1718,9 @@ int launch_segmentation(r360_frame* f) {
     R360_HIP(hipGetLastError());
     slot = timing_begin(ctx, "k_model_stats");
     R360_HIP(hipMemsetAsync(mcnt, 0, sizeof(int) * 16 * R360_MAX_MODELS, st));
-    hipLaunchKernelGGL(k_model_count, dim3(blocks), dim3(256), 0, st, P.labf, N, mmap, mcnt);
+    hipLaunchKernelGGL(k_model_count, dim3(blocks), dim3(256), 0, st, P.labf, N, mmap, mcnt, P.out);
     hipLaunchKernelGGL(k_model_scatter, dim3(blocks), dim3(256), 0, st, P.labf, N, mmap, mcnt, mcur, P.mlist);
-    hipLaunchKernelGGL(k_model_stats, dim3(R360_MAX_MODELS, 8), dim3(MOM_TPB), 0, st, P.cloud, P.rgb, N, P.models,
+    hipLaunchKernelGGL(k_model_stats, dim3(16, 8, MS_SPLIT), dim3(MS_TPB), 0, st, P.cloud, P.rgb, N, P.models,
                        P.nmodels, f->calib->d_rt, mcnt, P.mlist, bfirst, R360_MAX_BIG, P.out);
     // the refinement's closeness masks are dead here: their storage holds the neighbour masks
     uint8_t* nbm = reinterpret_cast<uint8_t*>(P.mask);
