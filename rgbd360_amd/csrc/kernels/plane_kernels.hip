@@ -304,7 +304,7 @@ __global__ void k_dcm(const float4* __restrict__ cloud, int w, int h, float* __r
 // and a 10-term window for the within-row chain reproduce every value below the cap bit for bit
 // (rounding is monotone: fl(min(a,b)+1) = min(fl(a+1), fl(b+1))).  Values at or above the cap are
 // upper bounds of the true ones and never win the min.
-constexpr int DM_BAND = 16, DM_HALO = 10, DM_TPB = 256;
+constexpr int DM_BAND = 4, DM_HALO = 10, DM_TPB = 256;   // short bands: the halo rows run in parallel
 
 __global__ void __launch_bounds__(DM_TPB) k_distmap(const float* __restrict__ init, int w, int h,
                                                    float* __restrict__ out) {

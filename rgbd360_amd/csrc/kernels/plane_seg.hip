@@ -149,32 +149,46 @@ __device__ int block_exscan(int v, int* sh, int& total) {
     return sh[wid] + x - v;
 }
 
-// roots -> label ids in raster order (one workgroup per sensor); rank stored at the root's slot
-constexpr int SCAN_V = 8;   // consecutive elements per thread in the per-sensor scans
+// roots -> label ids in raster order (one workgroup per sensor); rank stored at the root's slot.
+// Pass 1 loads the sensor coalesced, 8 elements per thread and round, all rounds in flight (no barrier between
+// them), and keeps one flag byte per 8 elements in LDS; pass 2 gives each thread a contiguous run of flag bytes,
+// one block scan of their popcounts, then the ranks in raster order.
+constexpr int SCAN_V = 8;   // elements per flag byte
+constexpr int NUM_TPB = 1024;
+constexpr int NUM_MAXQ = 40960;   // flag bytes per sensor (N / 8; HiRes 38400)
 
-__global__ void __launch_bounds__(1024) k_ccl_number(const int* __restrict__ root, int N, int* __restrict__ rank,
-                                                     int* __restrict__ nlab) {
+__global__ void __launch_bounds__(NUM_TPB) k_ccl_number(const int* __restrict__ root, int N, int* __restrict__ rank,
+                                                        int* __restrict__ nlab) {
     __shared__ int sh[17];
+    __shared__ unsigned char F[NUM_MAXQ];
     const int s = blockIdx.x;
     const long base = (long)s * N;
-    int acc = 0;
-    for (int j0 = 0; j0 < N; j0 += blockDim.x * SCAN_V) {
-        const int j = j0 + threadIdx.x * SCAN_V;
-        int isr[SCAN_V], c = 0;
+    const int nq = (N + SCAN_V - 1) / SCAN_V;
+    for (int q = threadIdx.x; q < nq; q += NUM_TPB) {
+        unsigned f = 0;
 #pragma unroll
         for (int v = 0; v < SCAN_V; ++v) {
-            isr[v] = (j + v < N && root[base + j + v] == (int)(base + j + v)) ? 1 : 0;
-            c += isr[v];
+            const int j = q * SCAN_V + v;
+            if (j < N && root[base + j] == (int)(base + j)) f |= 1u << v;
         }
-        int tot;
-        int r = acc + block_exscan(c, sh, tot);
-#pragma unroll
-        for (int v = 0; v < SCAN_V; ++v)
-            if (isr[v]) rank[base + j + v] = r++;
-        acc += tot;
-        __syncthreads();
+        F[q] = (unsigned char)f;
     }
-    if (threadIdx.x == 0) nlab[s] = acc;
+    __syncthreads();
+    const int per = (nq + NUM_TPB - 1) / NUM_TPB;
+    const int q0 = threadIdx.x * per, q1 = min(nq, q0 + per);
+    int c = 0;
+    for (int q = q0; q < q1; ++q) c += __popc(F[q]);
+    int tot;
+    int r = block_exscan(c, sh, tot);
+    for (int q = q0; q < q1; ++q) {
+        unsigned f = F[q];
+        while (f) {
+            const int v = __ffs(f) - 1;
+            f &= f - 1;
+            rank[base + q * SCAN_V + v] = r++;
+        }
+    }
+    if (threadIdx.x == 0) nlab[s] = tot;
 }
 
 __global__ void k_ccl_label(const int* __restrict__ root, const int* __restrict__ rank, int N, int* __restrict__ lab,
@@ -201,51 +215,68 @@ __global__ void k_ccl_label(const int* __restrict__ root, const int* __restrict_
 }
 
 // labels with more than min_inliers points, in increasing label order (one workgroup per sensor);
-// also the label -> large-label index map and each large label's offset in the grouped pixel list
-__global__ void __launch_bounds__(1024) k_big_list(const int* __restrict__ cnt, const int* __restrict__ nlab, int N,
-                                                   int min_inliers, int* __restrict__ big, int* __restrict__ nbig,
-                                                   int maxbig, int* __restrict__ err, int* __restrict__ bmap,
-                                                   int* __restrict__ boff, r360p::Moments* __restrict__ mom,
-                                                   int* __restrict__ bfirst) {
+// also the label -> large-label index map and each large label's offset in the grouped pixel list.  Same two
+// passes as k_ccl_number: flag bytes of the labels' counts, then contiguous runs per thread.
+__global__ void __launch_bounds__(NUM_TPB) k_big_list(const int* __restrict__ cnt, const int* __restrict__ nlab, int N,
+                                                      int min_inliers, int* __restrict__ big, int* __restrict__ nbig,
+                                                      int maxbig, int* __restrict__ err, int* __restrict__ bmap,
+                                                      int* __restrict__ boff, r360p::Moments* __restrict__ mom,
+                                                      int* __restrict__ bfirst) {
     __shared__ int sh[17];
+    __shared__ unsigned char F[NUM_MAXQ];
     const int s = blockIdx.x;
     const int n = nlab[s];
-    int acc = 0, cacc = 0;
-    for (int j0 = 0; j0 < n; j0 += blockDim.x * SCAN_V) {
-        const int j = j0 + threadIdx.x * SCAN_V;
-        int c[SCAN_V], nf = 0, nc = 0;
+    const long base = (long)s * N;
+    const int nq = (n + SCAN_V - 1) / SCAN_V;
+    for (int q = threadIdx.x; q < nq; q += NUM_TPB) {
+        unsigned f = 0;
 #pragma unroll
         for (int v = 0; v < SCAN_V; ++v) {
-            c[v] = j + v < n ? cnt[(long)s * N + j + v] : 0;
-            if (c[v] > min_inliers) { ++nf; nc += c[v]; }
-        }
-        int tot, ctot;
-        int b = acc + block_exscan(nf, sh, tot);
-        int co = cacc + block_exscan(nc, sh, ctot);
-#pragma unroll
-        for (int v = 0; v < SCAN_V; ++v) {
-            if (j + v >= n) break;
-            const bool f = c[v] > min_inliers;
-            bmap[(long)s * N + j + v] = (f && b < maxbig) ? b : -1;
-            if (f) {
-                if (b < maxbig) {
-                    big[s * maxbig + b] = j + v;
-                    boff[s * maxbig + b] = co;
-                }
-                ++b;
-                co += c[v];
+            const int j = q * SCAN_V + v;
+            if (j < n) {
+                if (cnt[base + j] > min_inliers) f |= 1u << v;
+                else bmap[base + j] = -1;
             }
         }
-        acc += tot;
-        cacc += ctot;
-        __syncthreads();
+        F[q] = (unsigned char)f;
+    }
+    __syncthreads();
+    const int per = (nq + NUM_TPB - 1) / NUM_TPB;
+    const int q0 = threadIdx.x * per, q1 = min(nq, q0 + per);
+    int nf = 0, nc = 0;
+    for (int q = q0; q < q1; ++q) {
+        unsigned f = F[q];
+        nf += __popc(f);
+        while (f) {
+            const int v = __ffs(f) - 1;
+            f &= f - 1;
+            nc += cnt[base + q * SCAN_V + v];
+        }
+    }
+    int tot, ctot;
+    int b = block_exscan(nf, sh, tot);
+    int co = block_exscan(nc, sh, ctot);
+    for (int q = q0; q < q1; ++q) {
+        unsigned f = F[q];
+        while (f) {
+            const int v = __ffs(f) - 1;
+            f &= f - 1;
+            const int j = q * SCAN_V + v;
+            bmap[base + j] = b < maxbig ? b : -1;
+            if (b < maxbig) {
+                big[s * maxbig + b] = j;
+                boff[s * maxbig + b] = co;
+            }
+            ++b;
+            co += cnt[base + j];
+        }
     }
     if (threadIdx.x == 0) {
-        nbig[s] = acc < maxbig ? acc : maxbig;
-        if (acc > maxbig) atomicOr(err, 2);
+        nbig[s] = tot < maxbig ? tot : maxbig;
+        if (tot > maxbig) atomicOr(err, 2);
     }
     // k_label_moments merges its workgroups' partial sums into zeroed accumulators
-    const int nb = acc < maxbig ? acc : maxbig;
+    const int nb = tot < maxbig ? tot : maxbig;
     for (int q = threadIdx.x; q < nb; q += blockDim.x) {
         r360p::moments_zero(mom[s * maxbig + q]);
         bfirst[s * maxbig + q] = N;
@@ -449,14 +480,22 @@ __global__ void __launch_bounds__(LMOM_TPB) k_label_moments(const float4* __rest
 
 // OrganizedMultiPlaneSegmentation::segment plane fit, one thread per sensor over its large labels in
 // label order (the viewpoint vp accumulates across labels, as in PCL 1.7)
-__global__ void k_plane_fit(const r360p::Moments* __restrict__ mom, const int* __restrict__ big,
-                            const int* __restrict__ nbig, int maxbig, float max_curvature, PlaneModel* __restrict__ models,
-                            int* __restrict__ nmodels, int* __restrict__ err, int N, int* __restrict__ mmap) {
-    const int s = threadIdx.x;
-    if (s >= 8) return;
-    float vp[4] = {0, 0, 0, 0};
-    int nm = 0;
-    for (int b = 0; b < nbig[s]; ++b) {
+// One workgroup per sensor.  The eigen33 fits of the large labels are independent (one thread each); the only
+// order dependence of segment() is the viewpoint vp, which accumulates the centroids of all previous labels in
+// float — four sequential subtraction chains, one lane per component — and decides each label's flip; the
+// planar labels are then numbered in label order.
+constexpr int PF_TPB = 256;
+
+__global__ void __launch_bounds__(PF_TPB) k_plane_fit(const r360p::Moments* __restrict__ mom, const int* __restrict__ big,
+                                                     const int* __restrict__ nbig, int maxbig, float max_curvature,
+                                                     PlaneModel* __restrict__ models, int* __restrict__ nmodels,
+                                                     int* __restrict__ err, int N, int* __restrict__ mmap) {
+    __shared__ float s_c[R360_MAX_BIG][4], s_pp[R360_MAX_BIG][4], s_vp[R360_MAX_BIG][4];
+    __shared__ float s_curv[R360_MAX_BIG];
+    __shared__ int s_idx[R360_MAX_BIG];
+    const int s = blockIdx.x;
+    const int nb = min(nbig[s], maxbig);
+    for (int b = threadIdx.x; b < nb; b += PF_TPB) {
         const r360p::Moments m = mom[s * maxbig + b];
         double mean[3], cv[9];
         r360p::moments_mean_cov(m, mean, cv);
@@ -467,29 +506,47 @@ __global__ void k_plane_fit(const r360p::Moments* __restrict__ mom, const int* _
         r360p::eigen33_min(cov, eval, evec);
         float pp[4] = {evec[0], evec[1], evec[2], 0};
         pp[3] = -1 * r360p::dot4(pp, centroid);
-        for (int k = 0; k < 4; ++k) vp[k] -= centroid[k];
+        const float eig_sum = cov[0] + cov[4] + cov[8];
+        s_curv[b] = eig_sum != 0 ? fabsf(eval / eig_sum) : 0.f;
+        for (int k = 0; k < 4; ++k) { s_c[b][k] = centroid[k]; s_pp[b][k] = pp[k]; }
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {   // vp after label b: vp -= centroid, in label order
+        const int k = threadIdx.x;
+        float v = 0.f;
+        for (int b = 0; b < nb; ++b) { v -= s_c[b][k]; s_vp[b][k] = v; }
+    }
+    if (threadIdx.x == 32) {   // planar labels numbered in label order (wave 0, lane 32: beside the vp chains)
+        int nm = 0;
+        for (int b = 0; b < nb; ++b) s_idx[b] = s_curv[b] < max_curvature ? nm++ : -1;
+        if (nm > R360_MAX_MODELS) atomicOr(err, 4);
+        nmodels[s] = nm < R360_MAX_MODELS ? nm : R360_MAX_MODELS;
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < nb; b += PF_TPB) {
+        const int nm = s_idx[b];
+        if (nm < 0 || nm >= R360_MAX_MODELS) continue;
+        float centroid[4], pp[4], vp[4];
+        for (int k = 0; k < 4; ++k) { centroid[k] = s_c[b][k]; pp[k] = s_pp[b][k]; vp[k] = s_vp[b][k]; }
         const float cos_theta = r360p::dot4(vp, pp);
         if (cos_theta < 0) {
             for (int k = 0; k < 4; ++k) pp[k] *= -1;
             pp[3] = -1 * r360p::dot4(pp, centroid);
         }
-        const float eig_sum = cov[0] + cov[4] + cov[8];
-        const float curv = eig_sum != 0 ? fabsf(eval / eig_sum) : 0.f;
-        if (curv < max_curvature) {
-            if (nm >= R360_MAX_MODELS) { atomicOr(err, 4); break; }
-            PlaneModel& M = models[s * R360_MAX_MODELS + nm];
-            M.label = big[s * maxbig + b];
-            M.big = b;
-            mmap[(long)s * N + M.label] = nm;
-            M.n_fit = (int)m.n;
-            for (int k = 0; k < 4; ++k) M.v[k] = pp[k];
-            for (int k = 0; k < 3; ++k) M.centroid[k] = centroid[k];
-            for (int k = 0; k < 9; ++k) M.cov[k] = cov[k];
-            M.curvature = curv;
-            ++nm;
-        }
+        // the label's covariance again (cheap next to the eigen solve; keeps the LDS small)
+        const r360p::Moments m = mom[s * maxbig + b];
+        double mean[3], cv[9];
+        r360p::moments_mean_cov(m, mean, cv);
+        PlaneModel& M = models[s * R360_MAX_MODELS + nm];
+        M.label = big[s * maxbig + b];
+        M.big = b;
+        mmap[(long)s * N + M.label] = nm;
+        M.n_fit = (int)m.n;
+        for (int k = 0; k < 4; ++k) M.v[k] = pp[k];
+        for (int k = 0; k < 3; ++k) M.centroid[k] = centroid[k];
+        for (int k = 0; k < 9; ++k) M.cov[k] = (float)cv[k];
+        M.curvature = s_curv[b];
     }
-    nmodels[s] = nm;
 }
 
 // ------------------------------------------------------------------ refine
@@ -1314,7 +1371,10 @@ __global__ void __launch_bounds__(TR_TPB) k_trace(const uint8_t* __restrict__ nb
     for (int c = threadIdx.x; c < TR_NCH; c += TR_TPB) cown[c] = -1;
     __syncthreads();
     const uint8_t* nb = LDS ? sm : nbs;
-    const int dxs[8] = {-1, -1, 0, 1, 1, 1, 0, -1}, dys[8] = {0, -1, -1, -1, 0, 1, 1, 1};
+    // Moore directions {W, NW, N, NE, E, SE, S, SW} as 2-bit fields of two constants (a dynamically indexed
+    // local table would be a global-memory load on the trace's dependency chain)
+    auto dxs = [](int d) { return (int)((0x1A90U >> (2 * d)) & 3u) - 1; };
+    auto dys = [](int d) { return (int)((0xA901U >> (2 * d)) & 3u) - 1; };
     const long max_len = 8L * N;
     const int m = threadIdx.x;
     int dir0 = -1, start = 0;
@@ -1324,7 +1384,7 @@ __global__ void __launch_bounds__(TR_TPB) k_trace(const uint8_t* __restrict__ nb
         const int cx = start % w, cy = start / w;
         const unsigned m8 = nb[start];
         for (int d = 0; d < 8; ++d) {
-            const int x = cx + dxs[d], y = cy + dys[d];
+            const int x = cx + dxs(d), y = cy + dys(d);
             if (x >= 0 && x < w && y >= 0 && y < h && !((m8 >> d) & 1)) { dir0 = d; break; }
         }
         long n = 0;
@@ -1346,7 +1406,7 @@ __global__ void __launch_bounds__(TR_TPB) k_trace(const uint8_t* __restrict__ nb
             do {
                 const int nd = trace_next(nb[cidx], dir);
                 dir = (nd + 4) & 7;
-                cidx += dys[nd] * w + dxs[nd];
+                cidx += dys(nd) * w + dxs(nd);
                 append(cidx);
                 if (++n > max_len) { atomicOr(err, 8); break; }
             } while (cidx != start);
@@ -1402,7 +1462,7 @@ __global__ void __launch_bounds__(TR_TPB) k_trace(const uint8_t* __restrict__ nb
         do {
             const int nd = trace_next(nb[cidx], dir);
             dir = (nd + 4) & 7;
-            cidx += dys[nd] * w + dxs[nd];
+            cidx += dys(nd) * w + dxs(nd);
             if (dst + n < cap_end) pool[dst + n] = P[cidx];
         } while (++n <= max_len && cidx != start);
     }
@@ -1411,16 +1471,24 @@ __global__ void __launch_bounds__(TR_TPB) k_trace(const uint8_t* __restrict__ nb
 // contour total of the frame (profiling / pool accounting), and the voxel hash table size for this
 // frame: a power of two >= 2x the inliers of the regions without a contour (their refined region
 // sizes bound the number of distinct voxels), capped by the allocation
-__global__ void k_alloc(const int* __restrict__ nmodels, const PlaneOut* __restrict__ out, const int* __restrict__ mcnt,
-                        unsigned long long cap, long* __restrict__ totals) {
-    if (threadIdx.x != 0) return;
+// one workgroup of 512 threads, thread = (sensor, model)
+__global__ void __launch_bounds__(512) k_alloc(const int* __restrict__ nmodels, const PlaneOut* __restrict__ out,
+                                               const int* __restrict__ mcnt, unsigned long long cap,
+                                               long* __restrict__ totals) {
+    __shared__ long sco[8], sca[8];
+    const int q = threadIdx.x, s = q / R360_MAX_MODELS, m = q % R360_MAX_MODELS;
     long co = 0, cand = 0;
-    for (int s = 0; s < 8; ++s)
-        for (int m = 0; m < nmodels[s]; ++m) {
-            const int nc = out[s * R360_MAX_MODELS + m].n_contour;
-            co += nc;
-            if (nc == 0) cand += mcnt[s * R360_MAX_MODELS + m];
-        }
+    if (m < nmodels[s]) {
+        const int nc = out[q].n_contour;
+        co = nc;
+        if (nc == 0) cand = mcnt[q];
+    }
+    for (int o = 32; o > 0; o >>= 1) { co += __shfl_xor(co, o, 64); cand += __shfl_xor(cand, o, 64); }
+    if ((q & 63) == 0) { sco[q >> 6] = co; sca[q >> 6] = cand; }
+    __syncthreads();
+    if (q != 0) return;
+    co = 0; cand = 0;
+    for (int w = 0; w < 8; ++w) { co += sco[w]; cand += sca[w]; }
     totals[0] = co;
     unsigned long long t = 1024;
     while (t < 2ull * (unsigned long long)cand && t < cap) t <<= 1;
@@ -1548,18 +1616,27 @@ __global__ void __launch_bounds__(VOX_TPB) k_vox_hash(const float4* __restrict__
     }
 }
 
-__global__ void k_vox_alloc(const int* __restrict__ nmodels, PlaneOut* __restrict__ out, long* __restrict__ totals,
-                            long vox_cap, int* __restrict__ err) {
-    if (threadIdx.x != 0) return;
-    long vo = 0;
-    for (int s = 0; s < 8; ++s)
-        for (int m = 0; m < nmodels[s]; ++m) {
-            PlaneOut& O = out[s * R360_MAX_MODELS + m];
-            O.vox_off = vo;
-            vo += O.n_vox;
-        }
-    totals[1] = vo;
-    if (vo > vox_cap) atomicOr(err, 16);
+// voxel list offsets per region in (sensor, model) order: one workgroup of 512 threads, exclusive scan
+__global__ void __launch_bounds__(512) k_vox_alloc(const int* __restrict__ nmodels, PlaneOut* __restrict__ out,
+                                                   long* __restrict__ totals, long vox_cap, int* __restrict__ err) {
+    __shared__ long sw[8];
+    const int q = threadIdx.x, lane = q & 63, wid = q >> 6;
+    const bool live = (q % R360_MAX_MODELS) < nmodels[q / R360_MAX_MODELS];
+    const long v = live ? out[q].n_vox : 0;
+    long x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const long y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) sw[wid] = x;
+    __syncthreads();
+    long pre = 0;
+    for (int w = 0; w < wid; ++w) pre += sw[w];
+    if (live) out[q].vox_off = pre + x - v;
+    if (q == 511) {
+        totals[1] = pre + x;
+        if (pre + x > vox_cap) atomicOr(err, 16);
+    }
 }
 
 // one workgroup per contiguous range of table cells: valid cells are counted per region in LDS, one
@@ -1681,7 +1758,8 @@ int launch_segmentation(r360_frame* f) {
                                h, ang_thr, P.parent);
     }
     hipLaunchKernelGGL(k_ccl_flatten, dim3(blocks), dim3(256), 0, st, P.parent, total, P.root);
-    hipLaunchKernelGGL(k_ccl_number, dim3(8), dim3(1024), 0, st, P.root, N, P.parent, P.nlab);
+    if ((N + SCAN_V - 1) / SCAN_V > NUM_MAXQ) { r360_set_error("segmentation: sensor of %d points too large", N); return -1; }
+    hipLaunchKernelGGL(k_ccl_number, dim3(8), dim3(NUM_TPB), 0, st, P.root, N, P.parent, P.nlab);
     R360_HIP(hipMemsetAsync(P.cnt, 0, sizeof(int) * total, st));
     hipLaunchKernelGGL(k_ccl_label, dim3(blocks), dim3(256), 0, st, P.root, P.parent, N, P.lab, P.cnt);
     timing_end(ctx, slot);
@@ -1704,7 +1782,7 @@ int launch_segmentation(r360_frame* f) {
     hipLaunchKernelGGL(k_label_moments, dim3(LMOM_GX, 8, LMOM_SPLIT), dim3(LMOM_TPB), 0, st, P.cloud, P.cnt, N, P.big, P.nbig,
                        R360_MAX_BIG, boff, P.blist, P.mom, bfirst);
     R360_HIP(hipMemsetAsync(mmap, 0xff, sizeof(int) * total, st));
-    hipLaunchKernelGGL(k_plane_fit, dim3(1), dim3(64), 0, st, P.mom, P.big, P.nbig, R360_MAX_BIG, 0.001f, P.models,
+    hipLaunchKernelGGL(k_plane_fit, dim3(8), dim3(PF_TPB), 0, st, P.mom, P.big, P.nbig, R360_MAX_BIG, 0.001f, P.models,
                        P.nmodels, P.err, N, mmap);
     timing_end(ctx, slot);
     R360_HIP(hipGetLastError());
@@ -1732,7 +1810,7 @@ int launch_segmentation(r360_frame* f) {
         hipLaunchKernelGGL(k_trace<false>, dim3(8), dim3(TR_TPB), 0, st, nbm, P.cloud, w, h, P.nmodels, P.out,
                            P.contour, P.contour_cap, P.err);
     if (ctx_vhash_reserve(ctx, 12L * N)) return -1;
-    hipLaunchKernelGGL(k_alloc, dim3(1), dim3(64), 0, st, P.nmodels, P.out, mcnt,
+    hipLaunchKernelGGL(k_alloc, dim3(1), dim3(512), 0, st, P.nmodels, P.out, mcnt,
                        (unsigned long long)ctx->vhash_cap, P.totals);
     timing_end(ctx, slot);
     R360_HIP(hipGetLastError());
@@ -1741,7 +1819,7 @@ int launch_segmentation(r360_frame* f) {
     hipLaunchKernelGGL(k_vox_clear, dim3(256), dim3(256), 0, st, ctx->d_vhash, P.totals);
     hipLaunchKernelGGL(k_vox_hash, dim3((unsigned)((total + VOX_PX - 1) / VOX_PX)), dim3(VOX_TPB), 0, st, P.cloud,
                        P.state, N, P.nmodels, P.out, ctx->d_vhash, P.totals, P.err);
-    hipLaunchKernelGGL(k_vox_alloc, dim3(1), dim3(64), 0, st, P.nmodels, P.out, P.totals, P.vox_cap, P.err);
+    hipLaunchKernelGGL(k_vox_alloc, dim3(1), dim3(512), 0, st, P.nmodels, P.out, P.totals, P.vox_cap, P.err);
     hipLaunchKernelGGL(k_vox_compact, dim3(VOXC_BLOCKS), dim3(VOXC_TPB), 0, st, ctx->d_vhash, P.totals, P.out, P.vox,
                        P.vox_cap);
     timing_end(ctx, slot);

@@ -1,6 +1,6 @@
 """GPU occupancy of a rocprofv3 kernel trace: wall span, time with >= 1 kernel running, mean kernel
 concurrency, and per-kernel totals, over the last <window_ms> of the trace (the bench's timed region).
-usage: python tools/busy.py <kernel_trace.csv> <window_ms>"""
+usage: python tools/busy.py <kernel_trace.csv> <window_ms> [top kernels, default 25]"""
 import csv
 import collections
 import re
@@ -36,7 +36,8 @@ cnt = collections.Counter()
 for s, e, n in ev:
     tot[n] += e - s
     cnt[n] += 1
-for n, v in tot.most_common(25):
+TOP = int(sys.argv[3]) if len(sys.argv) > 3 else 25
+for n, v in tot.most_common(TOP):
     print(f"{v / 1e6:9.2f} ms  {cnt[n]:6d} x {v / cnt[n] / 1e3:8.2f} us  {n}")
 
 # per-kernel grid sizes (workgroups) of the window, to tell full-GPU kernels from latency-bound ones
@@ -50,5 +51,5 @@ for r in rows:
         except (KeyError, ValueError):
             pass
 print("workgroups per launch:")
-for n, v in tot.most_common(25):
+for n, v in tot.most_common(TOP):
     print(f"  {n:28s} {sorted(wg[n])[:6]}")
