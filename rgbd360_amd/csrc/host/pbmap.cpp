@@ -356,6 +356,7 @@ int plane_bufs_alloc(r360_frame* f) {
     R360_HIP(hipMalloc(&P.rcode, sizeof(uint16_t) * SK));
     R360_HIP(hipMalloc(&P.rmsk, sizeof(unsigned long long) * SK));
     R360_HIP(hipMalloc(&P.rf1, SK));
+    R360_HIP(hipMalloc(&P.rf2, SK));
     R360_HIP(hipMalloc(&P.out, sizeof(PlaneOut) * 8 * R360_MAX_MODELS));
     P.contour_cap = 2 * T;
     P.vox_cap = T;
@@ -375,7 +376,7 @@ void plane_bufs_free(r360_frame* f) {
     PlaneBufs& P = f->pl;
     planes_join(f);
     void* dev[] = {P.cloud, P.rgb, P.nrm, P.dist0, P.dist, P.grids, P.zmm, P.parent, P.root, P.lab, P.labf, P.cnt, P.blist, P.mlist, P.aux, P.nlab,
-                   P.big, P.nbig, P.mom, P.models, P.nmodels, P.state, P.state2, P.rbnd, P.rflag, P.mask, P.rcode, P.rmsk, P.rf1, P.out, P.totals, P.err};
+                   P.big, P.nbig, P.mom, P.models, P.nmodels, P.state, P.state2, P.rbnd, P.rflag, P.mask, P.rcode, P.rmsk, P.rf1, P.rf2, P.out, P.totals, P.err};
     for (void* p : dev) hipFree(p);
     hipHostFree(P.contour);
     hipHostFree(P.vox);

@@ -18,6 +18,7 @@
 // Arithmetic follows oracle/src/planes_oracle.cpp and pbmap_oracle.cpp; see rgbd360_amd/csrc/plane_math.h.
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 #include "../r360_internal.h"
 #include "../plane_math.h"
 
@@ -976,7 +977,7 @@ __global__ void k_refine_skew(const int8_t* __restrict__ S, const unsigned long 
     }
 }
 
-__device__ __forceinline__ bool mbit(unsigned long long m, int v) { return v >= 0 && ((m >> v) & 1ull); }
+__device__ __forceinline__ bool mbit(unsigned long long m, int v) { return (v >= 0) & (((m >> (v & 63)) & 1ull) != 0); }
 
 // DIR = +1: first sweep, F written to f1 (skewed).  DIR = -1: second sweep over f1, F written to S (raster).
 // blockDim.x = 64 * ceil(h / 64), grid = 8 sensors.
@@ -997,7 +998,7 @@ constexpr int RW_MAX_REDO = 64;
 template <int DIR>
 __global__ void __launch_bounds__(1024) k_refine_wave(const uint16_t* __restrict__ code_all,
                                                       const unsigned long long* __restrict__ msk_all,
-                                                      int8_t* __restrict__ f1_all, int8_t* __restrict__ S_all,
+                                                      int8_t* __restrict__ f1_all, int8_t* __restrict__ f2_all,
                                                       int* __restrict__ fb, int w, int h) {
     __shared__ int xch[2][16];
     __shared__ int8_t wasm[1024], wdet[1024];   // DIR < 0: assumed / detected wrap value per row (-2: none)
@@ -1009,7 +1010,7 @@ __global__ void __launch_bounds__(1024) k_refine_wave(const uint16_t* __restrict
     const uint16_t* code = code_all + s * SK;
     const unsigned long long* msk = msk_all + s * SK;
     int8_t* f1 = f1_all + s * SK;
-    int8_t* S = S_all + (long)s * w * h;
+    int8_t* f2 = f2_all + s * SK;                 // DIR < 0: the second sweep's states, skewed (coalesced stores)
     const int KS = h + w - 1;
     const int rr = r < h ? r : h - 1;             // loads of rows >= h are clamped (never used)
     auto kof = [&](int t) { return DIR > 0 ? t : KS - 1 - t; };
@@ -1024,10 +1025,7 @@ __global__ void __launch_bounds__(1024) k_refine_wave(const uint16_t* __restrict
         x.code = code[q];
         x.m = msk[q];
         if (DIR < 0) x.f1 = (unsigned char)f1[q];
-        if (DIR < 0 && redo) {
-            const int c = k - rr;
-            x.old = (unsigned char)S[(long)rr * w + (c < 0 ? 0 : c >= w ? w - 1 : c)];
-        }
+        if (DIR < 0 && redo) x.old = (unsigned char)f2[q];
     };
     if (DIR < 0) {
         for (int q = threadIdx.x; q < 1024; q += blockDim.x) { wasm[q] = -2; wdet[q] = -2; }
@@ -1035,16 +1033,19 @@ __global__ void __launch_bounds__(1024) k_refine_wave(const uint16_t* __restrict
     bool upw_free = false;     // DIR < 0: (r, w-1) was left at -2 by the push from below
     unsigned long long mw = 0; //   and its mask
     int t_start = 0, t_guard = 0;   // re-runs may stop only at steps after t_guard
-    for (int pass = 0;; ++pass) {
-        const bool redo = pass > 0;
+    // one pass of the wavefront from step t_start; REDO: a re-run (compares with the previous pass, may stop)
+    auto run = [&](auto redo_tag) {
+        constexpr bool REDO = decltype(redo_tag)::value;
         int prev = -1;         // this row's state at the previous step
-        if (redo) {            // resume from the previous pass's states on the diagonal before t_start
-            const int c = kof(t_start - 1) - r;
-            if (r < h && c >= 0 && c < w) prev = S[(long)r * w + c];
+        if (REDO) {            // resume from the previous pass's states on the diagonal before t_start
+            const int k = kof(t_start - 1), c = k - r;
+            if (r < h && c >= 0 && c < w) prev = f2[(long)k * h + r];
         }
+        const int my_wasm = DIR < 0 && r < h ? (int)wasm[r] : -2;   // this row's assumed wrap push
+        int my_wdet = DIR < 0 && r < h ? (int)wdet[r] : -2;         // and the one it detects
         In cur[RW_PF];
 #pragma unroll
-        for (int d = 0; d < RW_PF; ++d) ld(t_start + d, redo, cur[d]);
+        for (int d = 0; d < RW_PF; ++d) ld(t_start + d, REDO, cur[d]);
         __syncthreads();
         if (lane == (DIR > 0 ? 63 : 0)) xch[(t_start + 1) & 1][wv] = prev;
         if (threadIdx.x < 16) { chg[0][threadIdx.x] = 1; chg[1][threadIdx.x] = 1; }
@@ -1053,12 +1054,12 @@ __global__ void __launch_bounds__(1024) k_refine_wave(const uint16_t* __restrict
         for (int t0 = t_start; t0 < KS && !stop; t0 += RW_PF) {
             In nxt[RW_PF];
 #pragma unroll
-            for (int d = 0; d < RW_PF; ++d) ld(t0 + RW_PF + d, redo, nxt[d]);
+            for (int d = 0; d < RW_PF; ++d) ld(t0 + RW_PF + d, REDO, nxt[d]);
 #pragma unroll
             for (int d = 0; d < RW_PF; ++d) {
                 const int t = t0 + d;
                 if (t >= KS) break;
-                if (DIR < 0 && redo && t - 1 > t_guard) {
+                if (REDO && t - 1 > t_guard) {
                     // the previous diagonal came out equal to the previous pass's: so would every later one
                     int any = 0;
                     for (int q = 0; q < nw; ++q) any |= chg[(t + 1) & 1][q];
@@ -1066,7 +1067,7 @@ __global__ void __launch_bounds__(1024) k_refine_wave(const uint16_t* __restrict
                 }
                 const int k = kof(t);
                 const int c = k - r;
-                const bool act = r < h && c >= 0 && c < w;
+                const bool act = (r < h) & (c >= 0) & (c < w);
                 const int o = DIR > 0 ? (int)(int8_t)(cur[d].code & 0xff) : (int)(int8_t)cur[d].f1;
                 const bool cond = (cur[d].code >> (DIR > 0 ? 8 : 9)) & 1;
                 const unsigned long long m = cur[d].m;
@@ -1076,30 +1077,30 @@ __global__ void __launch_bounds__(1024) k_refine_wave(const uint16_t* __restrict
                 int a = DIR > 0 ? __builtin_amdgcn_update_dpp(pw, prev, 0x138, 0xf, 0xf, false)    // wave_shr:1
                                 : __builtin_amdgcn_update_dpp(pw, prev, 0x130, 0xf, 0xf, false);   // wave_shl:1
                 if (DIR < 0 && r == h - 1) a = -1;
-                int F = o;
-                if (o == -2) {
-                    int D = (cond && mbit(m, a)) ? a : -2;
-                    if (DIR < 0 && c == w - 1) {
-                        upw_free = D == -2 && r <= h - 2;
-                        mw = m;
-                        if (upw_free && act) D = wasm[r];   // the assumed wrap push (-2: none)
-                    }
-                    const bool ch = DIR > 0 ? (r <= h - 2 && c >= 1) : (r >= 1 && c <= w - 2);
-                    if (D == -2 && ch && mbit(m, prev)) D = prev;
-                    F = D;
+                // branch-free: only o == -2 pixels change
+                int D = (cond & mbit(m, a)) ? a : -2;
+                if (DIR < 0) {
+                    const bool first = (c == w - 1) & (o == -2);   // (r, w-1): the wrap push's target
+                    const bool uf = (D == -2) & (r <= h - 2);
+                    upw_free = first ? uf : upw_free;
+                    mw = first ? m : mw;
+                    D = (first & uf & act) ? my_wasm : D;          // the assumed wrap push (-2: none)
                 }
-                if (DIR < 0 && act && c == 0 && r <= h - 2) wdet[r] = (upw_free && mbit(mw, a)) ? (int8_t)a : (int8_t)-2;
-                bool changed = false;
+                const bool ch = DIR > 0 ? ((r <= h - 2) & (c >= 1)) : ((r >= 1) & (c <= w - 2));
+                D = ((D == -2) & ch & mbit(m, prev)) ? prev : D;
+                const int F = o == -2 ? D : o;
+                if (DIR < 0) {
+                    const bool last = act & (c == 0) & (r <= h - 2);  // a = F(r+1, 0): the wrap push's source
+                    my_wdet = last ? ((upw_free & mbit(mw, a)) ? a : -2) : my_wdet;
+                }
                 if (act) {
                     if (DIR > 0) f1[(long)k * h + r] = (int8_t)F;
-                    else {
-                        changed = redo && F != (int)(int8_t)cur[d].old;
-                        S[(long)r * w + c] = (int8_t)F;
-                    }
-                    prev = F;
+                    else f2[(long)k * h + r] = (int8_t)F;
                 }
+                const bool changed = REDO & act & (F != (int)(int8_t)cur[d].old);
+                prev = act ? F : prev;
                 if (lane == (DIR > 0 ? 63 : 0)) xch[t & 1][wv] = prev;
-                if (DIR < 0 && redo) {
+                if (REDO) {
                     const bool wchg = __any(changed);
                     if (lane == 0) chg[t & 1][wv] = wchg;
                 }
@@ -1110,6 +1111,12 @@ __global__ void __launch_bounds__(1024) k_refine_wave(const uint16_t* __restrict
 #pragma unroll
             for (int d = 0; d < RW_PF; ++d) cur[d] = nxt[d];
         }
+        if (DIR < 0 && r < h) wdet[r] = (int8_t)my_wdet;
+        __syncthreads();
+    };
+    for (int pass = 0;; ++pass) {
+        if (pass == 0) run(std::integral_constant<bool, false>{});
+        else run(std::integral_constant<bool, true>{});
         if (DIR > 0) break;
         // the last row (first in sweep order) whose detected wrap push differs from the assumed one
         if (threadIdx.x == 0) { s_red = -1; s_min = h; }
@@ -1133,20 +1140,34 @@ __global__ void __launch_bounds__(1024) k_refine_wave(const uint16_t* __restrict
     }
 }
 
+// the second sweep's states back to raster order (sensors handed to k_refine_fb are written by it)
+__global__ void k_refine_unskew(const int8_t* __restrict__ f2_all, int8_t* __restrict__ S_all,
+                                const int* __restrict__ fb, int w, int h) {
+    const long N = (long)w * h, SK = (long)(h + w - 1) * h, total = 8 * N;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int s = (int)(i / N);
+        if (fb[s]) continue;
+        const int j = (int)(i - (long)s * N), r = j / w, c = j - r * w;
+        S_all[i] = f2_all[s * SK + (long)(r + c) * h + r];
+    }
+}
+
 // The exact second sweep for a sensor whose wavefront saw the wrap push fire, first at target row r0 = fb - 1:
 // rows below r0 are exact (nothing they depend on fired), so rows 0..r0 get the first sweep's states back and
 // the single-wave sweep resumes at source row r0 + 1 (re-chaining a swept row leaves it unchanged).
 template <int K>
-__global__ void __launch_bounds__(64) k_refine_fb(const int8_t* __restrict__ f1_all, int8_t* __restrict__ S_all,
+__global__ void __launch_bounds__(64) k_refine_fb(const int8_t* __restrict__ f1_all, const int8_t* __restrict__ f2_all,
+                                                 int8_t* __restrict__ S_all,
                                                  const unsigned long long* __restrict__ MK, const int* __restrict__ fb,
                                                  int w, int h) {
     const int s = blockIdx.x;
     const int r0 = fb[s] - 1;
     if (r0 < 0) return;
     const long N = (long)w * h, SK = (long)(h + w - 1) * h;
-    for (long j = threadIdx.x; j < (long)(r0 + 1) * w; j += 64) {
+    // rows 0..r0 from the first sweep, rows below from the wavefront's (exact) second sweep
+    for (long j = threadIdx.x; j < N; j += 64) {
         const int r = (int)(j / w), c = (int)(j - (long)r * w);
-        S_all[s * N + j] = f1_all[s * SK + (long)(r + c) * h + r];
+        S_all[s * N + j] = (r <= r0 ? f1_all : f2_all)[s * SK + (long)(r + c) * h + r];
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
@@ -1683,7 +1704,7 @@ __global__ void __launch_bounds__(VOXC_TPB) k_vox_compact(const VoxCell* __restr
 }  // namespace
 
 // buffers of the wavefront refinement (skewed layout, [8][h + w - 1][h] each)
-struct RefineWaveBufs { uint16_t* code; unsigned long long* msk; int8_t* f1; };
+struct RefineWaveBufs { uint16_t* code; unsigned long long* msk; int8_t* f1; int8_t* f2; };
 
 // refinement mode: -1 the wavefront sweeps (default), 0 the single-wave sweeps, rb > 0 banded with rb rows per
 // band (R360_REFINE_ROWS overrides)
@@ -1707,9 +1728,11 @@ int launch_refine_sweeps(hipStream_t st, int8_t* S, int8_t* S2, const unsigned l
                            wb->msk, flag);
         const int tpb = 64 * ((h + 63) / 64);
         hipLaunchKernelGGL(k_refine_wave<1>, dim3(8), dim3(tpb), 0, st, wb->code, wb->msk, wb->f1, S, flag, w, h);
-        hipLaunchKernelGGL(k_refine_wave<-1>, dim3(8), dim3(tpb), 0, st, wb->code, wb->msk, wb->f1, S, flag, w, h);
+        hipLaunchKernelGGL(k_refine_wave<-1>, dim3(8), dim3(tpb), 0, st, wb->code, wb->msk, wb->f1, wb->f2, flag, w, h);
+        hipLaunchKernelGGL(k_refine_unskew, dim3((unsigned)((8L * w * h + 255) / 256)), dim3(256), 0, st, wb->f2, S, flag,
+                           w, h);
         switch (K) {
-#define R360_FB_CASE(k) case k: hipLaunchKernelGGL(k_refine_fb<k>, dim3(8), dim3(64), 0, st, wb->f1, S, MK, flag, w, h); break;
+#define R360_FB_CASE(k) case k: hipLaunchKernelGGL(k_refine_fb<k>, dim3(8), dim3(64), 0, st, wb->f1, wb->f2, S, MK, flag, w, h); break;
             R360_FB_CASE(1) R360_FB_CASE(2) R360_FB_CASE(3) R360_FB_CASE(4) R360_FB_CASE(5)
             R360_FB_CASE(6) R360_FB_CASE(7) R360_FB_CASE(8) R360_FB_CASE(9) R360_FB_CASE(10)
 #undef R360_FB_CASE
@@ -1789,7 +1812,7 @@ int launch_segmentation(r360_frame* f) {
     slot = timing_begin(ctx, "k_refine");
     hipLaunchKernelGGL(k_refine_init, dim3(blocks), dim3(256), 0, st, P.cloud, P.lab, N, P.models, P.nmodels, P.state,
                        P.mask);
-    const RefineWaveBufs wb{P.rcode, P.rmsk, P.rf1};
+    const RefineWaveBufs wb{P.rcode, P.rmsk, P.rf1, P.rf2};
     if (launch_refine_sweeps(st, P.state, P.state2, P.mask, P.rbnd, P.rflag, w, h, refine_band_rows(h), &wb)) return -1;
     hipLaunchKernelGGL(k_refine_final, dim3(blocks), dim3(256), 0, st, P.state, P.lab, N, P.models, P.labf);
     timing_end(ctx, slot);
@@ -1849,6 +1872,7 @@ extern "C" int r360_refine_eval(const int8_t* state, const uint64_t* mask, int w
     R360_HIP(hipMalloc(&wb.code, sizeof(uint16_t) * SK));
     R360_HIP(hipMalloc(&wb.msk, sizeof(unsigned long long) * SK));
     R360_HIP(hipMalloc(&wb.f1, SK));
+    R360_HIP(hipMalloc(&wb.f2, SK));
     int rc = launch_refine_sweeps(0, S, S2, MK, bnd, flag, w, h, rb, &wb);
     if (rc == 0) {
         R360_HIP(hipMemcpy(out, S, T, hipMemcpyDeviceToHost));
@@ -1861,6 +1885,6 @@ extern "C" int r360_refine_eval(const int8_t* state, const uint64_t* mask, int w
         }
     }
     (void)hipFree(S); (void)hipFree(S2); (void)hipFree(MK); (void)hipFree(bnd); (void)hipFree(flag);
-    (void)hipFree(wb.code); (void)hipFree(wb.msk); (void)hipFree(wb.f1);
+    (void)hipFree(wb.code); (void)hipFree(wb.msk); (void)hipFree(wb.f1); (void)hipFree(wb.f2);
     return rc;
 }

@@ -191,6 +191,7 @@ struct PlaneBufs {
     uint16_t* rcode = nullptr;           // wavefront refinement, skewed [8][h + w - 1][h]: state | push conditions
     unsigned long long* rmsk = nullptr;  //   closeness masks, skewed
     int8_t* rf1 = nullptr;               //   first sweep's states, skewed
+    int8_t* rf2 = nullptr;               //   second sweep's states, skewed
     PlaneOut* out = nullptr;         // [8][R360_MAX_MODELS]
     float4* contour = nullptr;       // contour pool
     long contour_cap = 0;
