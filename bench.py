@@ -226,6 +226,8 @@ def main():
     ap.add_argument("--queue", type=int, default=16,
                     help="dense queue batch size (alignFrames360 of up to N pairs per launch); 0 = one launch per pair "
                          "on each pipeline's stream")
+    ap.add_argument("--depth", type=int, default=1,
+                    help="dense queue: alignments in flight per pipeline (each needs one more Frame360 buffer)")
     ap.add_argument("--emulate", type=str, default=None,
                     help="RANK/WORLD: run that rank's shard alone (single-GPU rehearsal of an N-GPU shard)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -275,7 +277,7 @@ def main():
     params.fixed_iters_level0 = args.iters0
     runner = OD.SequenceRunner(local, args.rows, args.cols, P, params, planes=args.workload != "dense",
                                dense_only=args.workload == "dense", queue=args.queue,
-                               planes_only=args.workload == "planes")
+                               planes_only=args.workload == "planes", depth=args.depth)
     ctxs = runner.ctxs + ([runner.queue.ctx] if runner.queue else [])
     dense_ctx = runner.queue.ctx if runner.queue else ctxs[0]   # where pipeline 0's alignments run
 
@@ -389,7 +391,7 @@ def main():
     iso_ach = (nj / max(n, 1)) * alg_bytes / (iso_ms * 1e-3) / 1e9 if n else None
     probe = None
     if args.eval_probe:   # opt-in diagnostic: the level-0 pass in eval mode (no GN step) at identity, alone
-        fa, fb = runner.frames[0]
+        fa, fb = runner.frames[0][:2]
         reg = R.RegisterPhotoICP(ctxs[0])
         reg.setNumPyr(5)
         reg.setGrayVariance(3.0 / 255)
@@ -440,7 +442,7 @@ def main():
             "workload": workload, "sensors": f"8x{args.cols}x{args.rows}", "sphere": f"{H0}x{W0}",
             "n_pyr": 5, "parallelism": f"pair-shard dp{world}", "pairs_per_step": pairs_job // args.steps,
             "pairs_per_step_this_rank": steps_pairs, "pipelines_per_gpu": P,
-            "dense_batch": args.queue,
+            "dense_batch": args.queue, "dense_in_flight_per_pipeline": args.depth if args.queue else 1,
             **({"emulated_shard": f"{shard_rank}/{shard_world}"} if args.emulate else {}),
         },
         "value_hbm_resident_inputs": resident,

@@ -104,13 +104,14 @@ class SequenceRunner:
 
     def __init__(self, device: int, rows: int, cols: int, pipelines: int, params: IcpParams,
                  planes: bool = True, max_match_planes: int = 25, mode: int = PLANAR_3DoF, dense_only: bool = False,
-                 queue: int = 0, planes_only: bool = False):
+                 queue: int = 0, planes_only: bool = False, depth: int = 1):
         self.P = pipelines
         self.dense_only = dense_only
         self.planes_only = planes_only
         if planes_only:
             queue = 0
         self.queue = DenseQueue(device, queue) if queue > 0 else None
+        self.depth = max(1, depth)   # queued mode: alignments in flight per pipeline
         self.params = params
         self.max_match_planes, self.mode = max_match_planes, mode
         self.flags = BUILD_UNDISTORT | BUILD_SPHERE | BUILD_PYRAMID | (BUILD_PLANES if planes else 0)
@@ -120,7 +121,7 @@ class SequenceRunner:
             cal = Calib360(c, rows, cols)
             cal.loadExtrinsicCalibration(EXTRINSICS_DIR)
             self.cals.append(cal)
-            self.frames.append([Frame360(cal) for _ in range(3 if self.queue else 2)])
+            self.frames.append([Frame360(cal) for _ in range(self.depth + 2 if self.queue else 2)])
         self.stats = [IcpStats() for _ in range(pipelines)]
         # host-side time per pipeline: [load + build enqueue, PbMap stage (register_async), dense wait, pairs]
         self.host_s = np.zeros((pipelines, 4))
@@ -188,9 +189,9 @@ class SequenceRunner:
 
     def _pipeline_queued(self, p: int, run: tuple[int, int], frames_of, out: np.ndarray, p0: int,
                          device_inputs: bool):
-        """_pipeline with the dense stage on the queue: submit pair i, then collect pair i-1 (so one alignment
-        per pipeline is in flight while the next frame is built and PbMap-registered).  Frame i+1 goes into
-        the buffer of frame i-2, whose pair (i-2, i-1) was collected in the previous iteration."""
+        """_pipeline with the dense stage on the queue: submit pair i, then collect pair i-depth (so `depth`
+        alignments per pipeline are in flight while the next frame is built and PbMap-registered).  Frame i+1
+        goes into the buffer of frame i+1-(depth+2), whose pairs were collected in earlier iterations."""
         L = lib()
         ctx = self.ctxs[p]
         fr = self.frames[p]
@@ -224,13 +225,15 @@ class SequenceRunner:
             rec[R_SSO] = st.sso
             rec[R_ERR] = st.error
 
+        nbuf = len(fr)
+        depth = nbuf - 2
         load(fr[0], a)
         fr[0].build(self.flags, sync=False)
-        pending = None
-        sts = [IcpStats(), IcpStats()]
+        pending = []
+        sts = [IcpStats() for _ in range(depth + 1)]
         for i in range(a, b):
             t0 = time.perf_counter()
-            cur, nxt = fr[(i - a) % 3], fr[(i + 1 - a) % 3]
+            cur, nxt = fr[(i - a) % nbuf], fr[(i + 1 - a) % nbuf]
             load(nxt, i + 1)
             nxt.build(self.flags, sync=False)
             t1 = time.perf_counter()
@@ -244,14 +247,14 @@ class SequenceRunner:
             if rc != 0:
                 raise RuntimeError(f"submit: {L.r360_last_error()}")
             t2 = time.perf_counter()
-            if pending is not None:
-                finish(*pending)
-            pending = (ticket.value, i, sts[i % 2])
+            pending.append((ticket.value, i, sts[(i - a) % (depth + 1)]))
+            if len(pending) > depth:
+                finish(*pending.pop(0))
             hs += (t1 - t0, t2 - t1, time.perf_counter() - t2, 1)
-        if pending is not None:
-            t2 = time.perf_counter()
-            finish(*pending)
-            hs[2] += time.perf_counter() - t2
+        t2 = time.perf_counter()
+        while pending:
+            finish(*pending.pop(0))
+        hs[2] += time.perf_counter() - t2
 
     def run(self, p0: int, p1: int, frames_of, out: np.ndarray, repeats: int = 1, runs=None,
             device_inputs: bool = False):
