@@ -284,46 +284,74 @@ __global__ void __launch_bounds__(NUM_TPB) k_big_list(const int* __restrict__ cn
     }
 }
 
-// Wave-aggregated counter increment: lanes with the same key share one atomic; returns each active
-// lane's slot.  Must be called by every lane of the wave (uniform control flow).
-__device__ __forceinline__ int agg_inc(int* __restrict__ ctr, int key, bool active) {
-    const int lane = threadIdx.x & 63;
-    unsigned long long pending = __ballot(active);
-    int res = 0;
-    while (pending) {
-        const int leader = __ffsll((long long)pending) - 1;
-        const int lkey = __shfl(key, leader, 64);
-        const unsigned long long grp = __ballot(active && key == lkey) & pending;
-        int base = 0;
-        if (lane == leader) base = atomicAdd(ctr + lkey, __popcll(grp));
-        base = __shfl(base, leader, 64);
-        if ((grp >> lane) & 1) res = base + __popcll(grp & ((1ull << lane) - 1));
-        pending &= ~grp;
+// Block-privatised grouping: a workgroup takes PS_PX consecutive pixels (4 per thread; they cover at most
+// two sensors, PS_PX <= N), counts its keys in an LDS histogram over the keys of those sensors, reserves one
+// slot range per key with a single global atomic, and places its pixels with LDS atomics.  Replaces a global
+// returning atomic per (wave, key).  Order inside a key's slice is free (see the users).
+constexpr int PS_TPB = 256, PS_PX = 4 * PS_TPB;
+
+template <int BINS>   // keys per sensor
+__device__ void priv_count(const int (&key)[4], int s0, int* __restrict__ hist, int* __restrict__ gcnt) {
+    for (int q = threadIdx.x; q < 2 * BINS; q += PS_TPB) hist[q] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (key[k] >= 0) atomicAdd(&hist[key[k] - s0 * BINS], 1);
+    __syncthreads();
+    for (int q = threadIdx.x; q < 2 * BINS; q += PS_TPB)
+        if (hist[q] && s0 * BINS + q < 8 * BINS) atomicAdd(gcnt + s0 * BINS + q, hist[q]);
+}
+
+// returns each pixel's slot inside its key's slice (gcur: running fill per key, zeroed beforehand)
+template <int BINS>
+__device__ void priv_slots(const int (&key)[4], int s0, int* __restrict__ hist, int* __restrict__ base,
+                           int* __restrict__ gcur, int (&pos)[4]) {
+    for (int q = threadIdx.x; q < 2 * BINS; q += PS_TPB) hist[q] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (key[k] >= 0) atomicAdd(&hist[key[k] - s0 * BINS], 1);
+    __syncthreads();
+    for (int q = threadIdx.x; q < 2 * BINS; q += PS_TPB) {
+        base[q] = (hist[q] && s0 * BINS + q < 8 * BINS) ? atomicAdd(gcur + s0 * BINS + q, hist[q]) : 0;
+        hist[q] = 0;
     }
-    return res;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int q = key[k] - s0 * BINS;
+        pos[k] = key[k] >= 0 ? base[q] + atomicAdd(&hist[q], 1) : 0;
+    }
 }
 
 // pixels of every large label into its slice of the grouped list (order inside a slice is free: the
 // moments are exact integer sums and the first pixel is a minimum)
-__global__ void k_label_scatter(const int* __restrict__ lab, int N, const int* __restrict__ bmap,
-                                const int* __restrict__ boff, int* __restrict__ bcur, int* __restrict__ blist,
-                                int maxbig) {
-    const long total = 8L * N, stride = (long)gridDim.x * blockDim.x;
-    for (long i0 = blockIdx.x * (long)blockDim.x + (threadIdx.x & ~63); i0 < total; i0 += stride) {
-        const long i = i0 + (threadIdx.x & 63);
-        int key = -1, s = 0, j = 0;
+__global__ void __launch_bounds__(PS_TPB) k_label_scatter(const int* __restrict__ lab, int N, const int* __restrict__ bmap,
+                                                          const int* __restrict__ boff, int* __restrict__ bcur,
+                                                          int* __restrict__ blist) {
+    __shared__ int hist[2 * R360_MAX_BIG], base[2 * R360_MAX_BIG];
+    const long total = 8L * N, b0 = (long)blockIdx.x * PS_PX;
+    const int s0 = (int)(b0 / N);
+    int key[4], j[4], s[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const long i = b0 + k * PS_TPB + threadIdx.x;
+        key[k] = -1; j[k] = 0; s[k] = 0;
         if (i < total) {
-            s = (int)(i / N);
-            j = (int)(i - (long)s * N);
+            s[k] = (int)(i / N);
+            j[k] = (int)(i - (long)s[k] * N);
             const int L = lab[i];
             if (L >= 0) {
-                const int b = bmap[(long)s * N + L];
-                if (b >= 0) key = s * maxbig + b;
+                const int b = bmap[(long)s[k] * N + L];
+                if (b >= 0) key[k] = s[k] * R360_MAX_BIG + b;
             }
         }
-        const int pos = agg_inc(bcur, key, key >= 0);
-        if (key >= 0) blist[(long)s * N + boff[key] + pos] = j;
     }
+    int pos[4];
+    priv_slots<R360_MAX_BIG>(key, s0, hist, base, bcur, pos);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (key[k] >= 0) blist[(long)s[k] * N + boff[key[k]] + pos[k]] = j[k];
 }
 
 // ------------------------------------------------------------------ moments
@@ -1187,28 +1215,38 @@ __global__ void k_refine_final(const int8_t* __restrict__ state, const int* __re
 
 // ------------------------------------------------------------------ per-model statistics
 // refined regions grouped by model: counts, then scatter (order inside a slice is free, as above)
-__global__ void k_model_count(const int* __restrict__ labf, int N, const int* __restrict__ mmap, int* __restrict__ mcnt,
-                              PlaneOut* __restrict__ out) {
+__device__ __forceinline__ void model_keys(const int* __restrict__ labf, int N, const int* __restrict__ mmap, long b0,
+                                           int (&key)[4], int (&j)[4], int (&s)[4]) {
+    const long total = 8L * N;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const long i = b0 + k * PS_TPB + threadIdx.x;
+        key[k] = -1; j[k] = 0; s[k] = 0;
+        if (i < total) {
+            s[k] = (int)(i / N);
+            j[k] = (int)(i - (long)s[k] * N);
+            const int L = labf[i];
+            if (L >= 0) {
+                const int m = mmap[(long)s[k] * N + L];
+                if (m >= 0) key[k] = s[k] * R360_MAX_MODELS + m;
+            }
+        }
+    }
+}
+
+__global__ void __launch_bounds__(PS_TPB) k_model_count(const int* __restrict__ labf, int N, const int* __restrict__ mmap,
+                                                       int* __restrict__ mcnt, PlaneOut* __restrict__ out) {
+    __shared__ int hist[2 * R360_MAX_MODELS];
     // k_model_stats merges its workgroups' partial sums and bounds into these
     if (blockIdx.x == 0)
         for (int q = threadIdx.x; q < 8 * R360_MAX_MODELS; q += blockDim.x) {
             r360p::moments_zero(out[q].stats);
             for (int k = 0; k < 3; ++k) { out[q].bmin[k] = __builtin_inff(); out[q].bmax[k] = -__builtin_inff(); }
         }
-    const long total = 8L * N, stride = (long)gridDim.x * blockDim.x;
-    for (long i0 = blockIdx.x * (long)blockDim.x + (threadIdx.x & ~63); i0 < total; i0 += stride) {
-        const long i = i0 + (threadIdx.x & 63);
-        int key = -1;
-        if (i < total) {
-            const int s = (int)(i / N);
-            const int L = labf[i];
-            if (L >= 0) {
-                const int m = mmap[(long)s * N + L];
-                if (m >= 0) key = s * R360_MAX_MODELS + m;
-            }
-        }
-        agg_inc(mcnt, key, key >= 0);
-    }
+    const long b0 = (long)blockIdx.x * PS_PX;
+    int key[4], j[4], s[4];
+    model_keys(labf, N, mmap, b0, key, j, s);
+    priv_count<R360_MAX_MODELS>(key, (int)(b0 / N), hist, mcnt);
 }
 
 __device__ __forceinline__ int model_offset(const int* __restrict__ mcnt, int s, int m) {
@@ -1217,9 +1255,10 @@ __device__ __forceinline__ int model_offset(const int* __restrict__ mcnt, int s,
     return o;
 }
 
-__global__ void k_model_scatter(const int* __restrict__ labf, int N, const int* __restrict__ mmap,
-                                const int* __restrict__ mcnt, int* __restrict__ mcur, int* __restrict__ mlist) {
-    __shared__ int moff[8 * R360_MAX_MODELS];
+__global__ void __launch_bounds__(PS_TPB) k_model_scatter(const int* __restrict__ labf, int N, const int* __restrict__ mmap,
+                                                         const int* __restrict__ mcnt, int* __restrict__ mcur,
+                                                         int* __restrict__ mlist) {
+    __shared__ int moff[8 * R360_MAX_MODELS], hist[2 * R360_MAX_MODELS], base[2 * R360_MAX_MODELS];
     for (int q = threadIdx.x; q < 8 * R360_MAX_MODELS; q += blockDim.x) moff[q] = mcnt[q];
     __syncthreads();
     if (threadIdx.x < 8) {   // exclusive prefix per sensor
@@ -1230,23 +1269,13 @@ __global__ void k_model_scatter(const int* __restrict__ labf, int N, const int* 
             acc += c;
         }
     }
-    __syncthreads();
-    const long total = 8L * N, stride = (long)gridDim.x * blockDim.x;
-    for (long i0 = blockIdx.x * (long)blockDim.x + (threadIdx.x & ~63); i0 < total; i0 += stride) {
-        const long i = i0 + (threadIdx.x & 63);
-        int key = -1, s = 0, j = 0;
-        if (i < total) {
-            s = (int)(i / N);
-            j = (int)(i - (long)s * N);
-            const int L = labf[i];
-            if (L >= 0) {
-                const int m = mmap[(long)s * N + L];
-                if (m >= 0) key = s * R360_MAX_MODELS + m;
-            }
-        }
-        const int pos = agg_inc(mcur, key, key >= 0);
-        if (key >= 0) mlist[(long)s * N + moff[key] + pos] = j;
-    }
+    const long b0 = (long)blockIdx.x * PS_PX;
+    int key[4], j[4], s[4], pos[4];
+    model_keys(labf, N, mmap, b0, key, j, s);
+    priv_slots<R360_MAX_MODELS>(key, (int)(b0 / N), hist, base, mcur, pos);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (key[k] >= 0) mlist[(long)s[k] * N + moff[key[k]] + pos[k]] = j[k];
 }
 
 constexpr int MS_TPB = 256, MS_SPLIT = 16;   // model lists: 16 workgroups of 4 waves per model
@@ -1800,8 +1829,9 @@ int launch_segmentation(r360_frame* f) {
     hipLaunchKernelGGL(k_big_list, dim3(8), dim3(1024), 0, st, P.cnt, P.nlab, N, 80, P.big, P.nbig, R360_MAX_BIG, P.err,
                        bmap, boff, P.mom, bfirst);
     R360_HIP(hipMemsetAsync(bcur, 0, sizeof(int) * 8 * R360_MAX_BIG, st));
-    hipLaunchKernelGGL(k_label_scatter, dim3(blocks), dim3(256), 0, st, P.lab, N, bmap, boff, bcur, P.blist,
-                       R360_MAX_BIG);
+    if (N < PS_PX) { r360_set_error("segmentation: sensor of %d points too small", N); return -1; }
+    const int pblocks = (int)((total + PS_PX - 1) / PS_PX);
+    hipLaunchKernelGGL(k_label_scatter, dim3(pblocks), dim3(PS_TPB), 0, st, P.lab, N, bmap, boff, bcur, P.blist);
     hipLaunchKernelGGL(k_label_moments, dim3(LMOM_GX, 8, LMOM_SPLIT), dim3(LMOM_TPB), 0, st, P.cloud, P.cnt, N, P.big, P.nbig,
                        R360_MAX_BIG, boff, P.blist, P.mom, bfirst);
     R360_HIP(hipMemsetAsync(mmap, 0xff, sizeof(int) * total, st));
@@ -1819,8 +1849,8 @@ int launch_segmentation(r360_frame* f) {
     R360_HIP(hipGetLastError());
     slot = timing_begin(ctx, "k_model_stats");
     R360_HIP(hipMemsetAsync(mcnt, 0, sizeof(int) * 16 * R360_MAX_MODELS, st));
-    hipLaunchKernelGGL(k_model_count, dim3(blocks), dim3(256), 0, st, P.labf, N, mmap, mcnt, P.out);
-    hipLaunchKernelGGL(k_model_scatter, dim3(blocks), dim3(256), 0, st, P.labf, N, mmap, mcnt, mcur, P.mlist);
+    hipLaunchKernelGGL(k_model_count, dim3(pblocks), dim3(PS_TPB), 0, st, P.labf, N, mmap, mcnt, P.out);
+    hipLaunchKernelGGL(k_model_scatter, dim3(pblocks), dim3(PS_TPB), 0, st, P.labf, N, mmap, mcnt, mcur, P.mlist);
     hipLaunchKernelGGL(k_model_stats, dim3(16, 8, MS_SPLIT), dim3(MS_TPB), 0, st, P.cloud, P.rgb, N, P.models,
                        P.nmodels, f->calib->d_rt, mcnt, P.mlist, bfirst, R360_MAX_BIG, P.out);
     // the refinement's closeness masks are dead here: their storage holds the neighbour masks
