@@ -1360,8 +1360,14 @@ static PassGrid pass_grid(const r360_ctx* ctx, const LevelBufs& Ls, int occ) {
     // fills the rest with other jobs, and fewer records per job shorten the reduction tail)
     int cap = cap_env > 0 ? cap_env : 2 * occ_q.cus;
     if (cap > ctx->partials_cap) cap = ctx->partials_cap;
-    int nb = pf == 1 ? icp_blocks_for(npx) : (npx + TPB - 1) / TPB;
+    // at least R360_ICP_PXT points per thread (default 1; 8 measured no faster): the coarse levels (a quarter, ... of
+    // level 0) then run on a few hundred / dozen workgroups per pair instead of one thread per point, which
+    // shortens their record / ticket / final-sum tail (level 0 at VGA has ~19 per thread on the capped grid)
+    static const int pxt_env = env_int("R360_ICP_PXT", -1);
+    const int pxt = pxt_env > 0 ? pxt_env : 1;
+    int nb = pf == 1 ? icp_blocks_for(npx) : (npx + TPB * pxt - 1) / (TPB * pxt);
     if (nb > cap) nb = cap;
+    if (nb < 1) nb = 1;
     return {pf, nb};
 }
 

@@ -135,10 +135,10 @@ def _oracle_stable(D, k, init, method, n_pyr, ref_pose):
     (bt, dt), (bs, ds) = D["raw"]
     tweak = O.exp_se3([0, 0, 0, 1e-7, 0, 0], pseudo=False).astype(np.float32)
     p = O.IcpParams.default(n_pyr=n_pyr)
-    _, Pp, _, _, _ = O.align_pinhole(bt[k], dt[k], bs[k], ds[k], init=(tweak @ init).astype(np.float32),
-                                     method=method, params=p)
+    _, Pp, _, _, stp = O.align_pinhole(bt[k], dt[k], bs[k], ds[k], init=(tweak @ init).astype(np.float32),
+                                       method=method, params=p)
     dr, dtr = _pose_err(Pp, ref_pose)
-    return dr <= 1e-4 and dtr <= 1e-3
+    return dr <= 1e-4 and dtr <= 1e-3, dr, dtr, stp.error
 
 
 @pytest.mark.parametrize("method", [R.PHOTO_DEPTH, R.DEPTH_CONSISTENCY])
@@ -149,10 +149,17 @@ def test_align_sensors_parity_qvga(ctx, qvga, method):
     for k in range(8):
         rc, Po, Ho, go, st = ref[k]
         assert stats[k].illposed == rc
-        if not _oracle_stable(qvga, k, inits[k], method, 4, Po):
+        stable, sdr, sdt, serr = _oracle_stable(qvga, k, inits[k], method, 4, Po)
+        dr, dtr = _pose_err(poses[k], Po)
+        if not stable:
+            # the reference's own answer moves by (sdr, sdt) under a 1e-7 rad nudge of the initial pose (a flat
+            # valley), so the pose is not comparable; the solve must still reach the same quality: its final
+            # error within 2 % of the oracle's, or within twice the oracle's own change under the nudge (a solve
+            # that regressed still fails)
+            tol = max(0.02 * abs(st.error), 2 * abs(serr - st.error))
+            assert abs(stats[k].error - st.error) <= tol, (k, stats[k].error, st.error, serr, sdr, sdt)
             continue
         checked += 1
-        dr, dtr = _pose_err(poses[k], Po)
         assert dr <= 1e-4 and dtr <= 1e-3, (k, dr, dtr, list(stats[k].iters[:4]), list(st.iters[:4]))
         # the residual members alignFrames leaves (:4329-4332, :4507-4509; errorPhotoICP :759-762)
         assert stats[k].residuals_set == st.residuals_set, k
