@@ -219,14 +219,14 @@ def main():
     ap.add_argument("--iters0", type=int, default=20)
     ap.add_argument("--frames", type=int, default=256, help="sequence length (frames)")
     ap.add_argument("--workload", choices=["sequence", "dense", "planes"], default="sequence")
-    ap.add_argument("--streams", type=int, default=16, help="max pipelines per GPU (host thread + HIP stream each)")
+    ap.add_argument("--streams", type=int, default=12, help="max pipelines per GPU (host thread + HIP stream each)")
     ap.add_argument("--min-run", type=int, default=4, help="min pairs per pipeline run (each run rebuilds a halo frame)")
     ap.add_argument("--stage-timing", action="store_true",
                     help="diagnostic: HIP events around EVERY launch of the timed run (per-stage times; slows the run)")
     ap.add_argument("--queue", type=int, default=16,
                     help="dense queue batch size (alignFrames360 of up to N pairs per launch); 0 = one launch per pair "
                          "on each pipeline's stream")
-    ap.add_argument("--depth", type=int, default=1,
+    ap.add_argument("--depth", type=int, default=2,
                     help="dense queue: alignments in flight per pipeline (each needs one more Frame360 buffer)")
     ap.add_argument("--emulate", type=str, default=None,
                     help="RANK/WORLD: run that rank's shard alone (single-GPU rehearsal of an N-GPU shard)")

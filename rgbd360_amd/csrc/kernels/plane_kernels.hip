@@ -305,10 +305,13 @@ __global__ void k_dcm(const float4* __restrict__ cloud, int w, int h, float* __r
 // (rounding is monotone: fl(min(a,b)+1) = min(fl(a+1), fl(b+1))).  Values at or above the cap are
 // upper bounds of the true ones and never win the min.
 constexpr int DM_BAND = 4, DM_HALO = 10, DM_TPB = 256;   // short bands: the halo rows run in parallel
+// (one wave per band measured 2.3x slower: the 10-term chain windows of 5 columns per lane serialise)
+
+__device__ __forceinline__ void dm_sync() { __syncthreads(); }
 
 __global__ void __launch_bounds__(DM_TPB) k_distmap(const float* __restrict__ init, int w, int h,
                                                    float* __restrict__ out) {
-    extern __shared__ float sm[];   // (DM_BAND + 2*DM_HALO + 2) rows x w, plus one temp row
+    extern __shared__ float sm[];   // (DM_BAND + 2*DM_HALO + 2) rows x w, plus two temp rows
     const int s = blockIdx.y;
     const int r0 = blockIdx.x * DM_BAND;
     if (r0 >= h) return;
@@ -318,9 +321,10 @@ __global__ void __launch_bounds__(DM_TPB) k_distmap(const float* __restrict__ in
     const int base = R1 - 1;                       // LDS row 0 = image row R1-1
     const int nrows = R2 - base + 1;
     float* tmp = sm + (long)nrows * w;
+    float* tmp2 = tmp + w;                         // the chain's results before they replace the row
     auto L = [&](int row) { return sm + (long)(row - base) * w; };
     for (int k = threadIdx.x; k < nrows * w; k += blockDim.x) sm[k] = I[(long)base * w + k];
-    __syncthreads();
+    dm_sync();
     // forward pass rows R1..R2
     for (int r = R1; r <= R2; ++r) {
         const float* prev = L(r - 1);
@@ -330,19 +334,16 @@ __global__ void __launch_bounds__(DM_TPB) k_distmap(const float* __restrict__ in
             float m = fminf(fminf(prev[c - 1] + 1.4f, prev[c] + 1.0f), upRight);
             tmp[c] = fminf(cur[c], m);
         }
-        __syncthreads();
-        float res[4];
-        int nres = 0;
+        dm_sync();
         for (int c = 1 + threadIdx.x; c < w; c += blockDim.x) {
             const int k0 = c - 10 > 1 ? c - 10 : 1;
             float v = (k0 == 1) ? cur[0] : 1e30f;          // chain start (cur[0] is never updated)
             for (int k = k0; k <= c; ++k) v = fminf(tmp[k], v + 1.0f);
-            res[nres++] = v;
+            tmp2[c] = v;
         }
-        __syncthreads();
-        nres = 0;
-        for (int c = 1 + threadIdx.x; c < w; c += blockDim.x) cur[c] = res[nres++];
-        __syncthreads();
+        dm_sync();
+        for (int c = 1 + threadIdx.x; c < w; c += blockDim.x) cur[c] = tmp2[c];
+        dm_sync();
     }
     // backward pass rows Rb..r0
     const int Rb = min(h - 2, r0 + DM_BAND + DM_HALO - 1);
@@ -354,19 +355,16 @@ __global__ void __launch_bounds__(DM_TPB) k_distmap(const float* __restrict__ in
             const float m = fminf(fminf(lowerLeft, next[c] + 1.0f), next[c + 1] + 1.4f);
             tmp[c] = fminf(cur[c], m);
         }
-        __syncthreads();
-        float res[4];
-        int nres = 0;
+        dm_sync();
         for (int c = threadIdx.x; c <= w - 2; c += blockDim.x) {
             const int k0 = c + 10 < w - 2 ? c + 10 : w - 2;
             float v = (k0 == w - 2) ? cur[w - 1] : 1e30f;
             for (int k = k0; k >= c; --k) v = fminf(tmp[k], v + 1.0f);
-            res[nres++] = v;
+            tmp2[c] = v;
         }
-        __syncthreads();
-        nres = 0;
-        for (int c = threadIdx.x; c <= w - 2; c += blockDim.x) cur[c] = res[nres++];
-        __syncthreads();
+        dm_sync();
+        for (int c = threadIdx.x; c <= w - 2; c += blockDim.x) cur[c] = tmp2[c];
+        dm_sync();
     }
     const int rend = min(h, r0 + DM_BAND);
     for (int k = threadIdx.x; k < (rend - r0) * w; k += blockDim.x) out[s * N + (long)r0 * w + k] = L(r0)[k];
@@ -526,7 +524,7 @@ int launch_cloud_normals(r360_frame* f) {
     R360_HIP(hipGetLastError());
     const int nb = (h + DM_BAND - 1) / DM_BAND;
     const int max_rows = DM_BAND + 2 * DM_HALO + 2;
-    const size_t lds = sizeof(float) * ((size_t)max_rows + 1) * w;
+    const size_t lds = sizeof(float) * ((size_t)max_rows + 2) * w;
     if (lds > 160 * 1024) { r360_set_error("distance map: cloud width %d too large", w); return -1; }
     slot = timing_begin(f->ctx, "k_distmap");
     hipLaunchKernelGGL(k_distmap, dim3(nb, 8), dim3(DM_TPB), lds, st, P.dist0, w, h, P.dist);
