@@ -113,7 +113,16 @@ extern "C" int r360_ctx_create(int device, r360_ctx** out) {
     R360_HIP(hipSetDevice(device));
     r360_ctx* c = new r360_ctx;
     c->device = device;
-    R360_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    // R360_CTX_PRIORITY=1: contexts' streams at the device's highest priority (the dense queue keeps the normal
+    // one, r360_dense_queue_create); an experiment knob, off by default
+    static const int ctx_prio = getenv("R360_CTX_PRIORITY") ? atoi(getenv("R360_CTX_PRIORITY")) : 0;
+    if (ctx_prio) {
+        int least = 0, greatest = 0;
+        R360_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        R360_HIP(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, greatest));
+    } else {
+        R360_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    }
     R360_HIP(hipEventCreateWithFlags(&c->wait_ev, hipEventDisableTiming | hipEventBlockingSync));
     R360_HIP(hipMalloc(&c->d_state, sizeof(IcpState)));
     R360_HIP(hipMemset(c->d_state, 0, sizeof(IcpState)));
