@@ -220,7 +220,8 @@ def main():
     ap.add_argument("--frames", type=int, default=256, help="sequence length (frames)")
     ap.add_argument("--workload", choices=["sequence", "dense", "planes"], default="sequence")
     ap.add_argument("--streams", type=int, default=12, help="max pipelines per GPU (host thread + HIP stream each)")
-    ap.add_argument("--min-run", type=int, default=4, help="min pairs per pipeline run (each run rebuilds a halo frame)")
+    ap.add_argument("--min-run", type=int, default=8,
+                    help="min pairs per pipeline run (each run rebuilds a halo frame; 8 beat 4 and 16 on 1/4- and 1/8-size shards)")
     ap.add_argument("--stage-timing", action="store_true",
                     help="diagnostic: HIP events around EVERY launch of the timed run (per-stage times; slows the run)")
     ap.add_argument("--queue", type=int, default=16,
