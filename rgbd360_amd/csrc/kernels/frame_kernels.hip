@@ -82,6 +82,61 @@ __global__ void k_stitch(const uint8_t* __restrict__ bgr8, const uint16_t* __res
     }
 }
 
+// k_stitch with 4 consecutive sphere pixels of one row per thread (W % 4 == 0): the same per-pixel expressions,
+// with the 4 pixels' BGR bytes, ranges and level-0 {gray, depth} written as 3 + 2 + 8 dwords (byte-granular
+// stores of one pixel per lane were a third of the kernel's memory instructions)
+__global__ void k_stitch4(const uint8_t* __restrict__ bgr8, const uint16_t* __restrict__ depth8, int rows, int cols,
+                          int H, int W, const float* __restrict__ sinphi, const float* __restrict__ cosphi,
+                          const float* __restrict__ sinth, const float* __restrict__ costh,
+                          const float* __restrict__ rt_inv, float fx, float fy, float cx, float cy,
+                          uint8_t* __restrict__ sph_bgr, uint16_t* __restrict__ sph_depth, float2* __restrict__ p0) {
+    const long nq = (long)H * W / 4;
+    for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < nq; q += (long)gridDim.x * blockDim.x) {
+        const long i0 = 4 * q;
+        const int row = (int)(i0 / W), col0 = (int)(i0 - (long)row * W);
+        const float v0 = sinphi[row], cos_phi = cosphi[row];
+        unsigned char px[12];
+        unsigned short dd4[4];
+        float2 o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int col = col0 + e;
+            const int k = 7 - col / rows;
+            const float* T = rt_inv + 16 * k;
+            const float v1 = cos_phi * sinth[col];
+            const float v2 = cos_phi * costh[col];
+            float p0x = T[0] * v0 + T[4] * v1 + T[8] * v2;
+            float p1 = T[1] * v0 + T[5] * v1 + T[9] * v2;
+            float p2 = T[2] * v0 + T[6] * v1 + T[10] * v2;
+            p0x = p0x + T[12]; p1 = p1 + T[13]; p2 = p2 + T[14];
+            const float u = fx * p0x / p2 + cx;                          // :1133
+            const float v = fy * p1 / p2 + cy;                           // :1134
+            uint8_t b = 0, g = 0, r = 0;
+            uint16_t dd = 0;
+            if (u >= 0 && u < cols && v >= 0 && v < rows) {
+                const int iu = (int)u, iv = (int)v;
+                const long si = (long)k * rows * cols + (long)iv * cols + iu;
+                b = bgr8[si * 3 + 0]; g = bgr8[si * 3 + 1]; r = bgr8[si * 3 + 2];
+                const double du = (double)((u - cx) / fx), dv = (double)((v - cy) / fy);
+                dd = (uint16_t)(depth8[si] * sqrt(1 + du * du + dv * dv));  // :1142 (range in mm)
+            }
+            px[3 * e] = b; px[3 * e + 1] = g; px[3 * e + 2] = r;
+            dd4[e] = dd;
+            const int y = (b * 4899 + g * 9617 + r * 1868 + (1 << 13)) >> 14;
+            o[e] = make_float2((float)y * (float)(1. / 255), (float)dd * 0.001f);
+        }
+        uint3 wb;
+        wb.x = px[0] | (px[1] << 8) | (px[2] << 16) | ((unsigned)px[3] << 24);
+        wb.y = px[4] | (px[5] << 8) | (px[6] << 16) | ((unsigned)px[7] << 24);
+        wb.z = px[8] | (px[9] << 8) | (px[10] << 16) | ((unsigned)px[11] << 24);
+        *reinterpret_cast<uint3*>(sph_bgr + 12 * q) = wb;
+        *reinterpret_cast<uint2*>(sph_depth + i0) = make_uint2(dd4[0] | ((unsigned)dd4[1] << 16),
+                                                                 dd4[2] | ((unsigned)dd4[3] << 16));
+        *reinterpret_cast<float4*>(p0 + i0) = make_float4(o[0].x, o[0].y, o[1].x, o[1].y);
+        *reinterpret_cast<float4*>(p0 + i0 + 2) = make_float4(o[2].x, o[2].y, o[3].x, o[3].y);
+    }
+}
+
 __device__ __forceinline__ int refl101(int p, int n) {
     p = p < 0 ? -p : p;
     return p >= n ? 2 * n - p - 2 : p;
@@ -191,10 +246,16 @@ int launch_stitch(r360_frame* f) {
     const r360_calib* c = f->calib;
     const long n = (long)f->sph_rows * f->sph_cols;
     const int slot = timing_begin(f->ctx, "k_stitch");
-    hipLaunchKernelGGL(k_stitch, dim3(grid_for(n)), dim3(TPB), 0, f->ctx->stream, f->d_bgr, f->d_depth, f->rows,
-                       f->cols, f->sph_rows, f->sph_cols, c->d_st_sinphi, c->d_st_cosphi, c->d_st_sinth,
-                       c->d_st_costh, c->d_rt_inv, c->K[0], c->K[4], c->K[6], c->K[7], f->d_sph_bgr,
-                       f->d_sph_depth, f->lv[0].p0);
+    if (f->sph_cols % 4 == 0)
+        hipLaunchKernelGGL(k_stitch4, dim3(grid_for(n / 4)), dim3(TPB), 0, f->ctx->stream, f->d_bgr, f->d_depth,
+                           f->rows, f->cols, f->sph_rows, f->sph_cols, c->d_st_sinphi, c->d_st_cosphi, c->d_st_sinth,
+                           c->d_st_costh, c->d_rt_inv, c->K[0], c->K[4], c->K[6], c->K[7], f->d_sph_bgr,
+                           f->d_sph_depth, f->lv[0].p0);
+    else
+        hipLaunchKernelGGL(k_stitch, dim3(grid_for(n)), dim3(TPB), 0, f->ctx->stream, f->d_bgr, f->d_depth, f->rows,
+                           f->cols, f->sph_rows, f->sph_cols, c->d_st_sinphi, c->d_st_cosphi, c->d_st_sinth,
+                           c->d_st_costh, c->d_rt_inv, c->K[0], c->K[4], c->K[6], c->K[7], f->d_sph_bgr,
+                           f->d_sph_depth, f->lv[0].p0);
     timing_end(f->ctx, slot);
     R360_HIP(hipGetLastError());
     return 0;
@@ -208,13 +269,25 @@ int launch_stitch(r360_frame* f) {
 // blockIdx.y = pyramid level; a block covers R360_SRC_BLOCK consecutive pixels, 4 per thread.
 constexpr int SRC_TPB = R360_SRC_BLOCK / 4;
 
+// flattened (level, block) grid: level l owns blocks [blk0[l], blk0[l + 1]) (the coarse levels need a quarter, a
+// sixteenth ... of level 0's blocks; a 2D grid sized for level 0 dispatched thousands of empty workgroups)
+struct SrcGrid { int blk0[R360_MAX_PYR + 1]; int nl; };
+__device__ __forceinline__ void src_block(const SrcGrid& G, int& level, int& b) {
+    const int bid = blockIdx.x;
+    level = 0;
+    while (level + 1 < G.nl && bid >= G.blk0[level + 1]) ++level;
+    b = bid - G.blk0[level];
+}
+
 __device__ __forceinline__ bool src_valid(float d, float min_d, float max_d) { return min_d < d && d < max_d; }
 
-__global__ void __launch_bounds__(SRC_TPB) k_src_count(const SrcLevel* __restrict__ L, float min_d, float max_d,
+__global__ void __launch_bounds__(SRC_TPB) k_src_count(const SrcLevel* __restrict__ L, SrcGrid G, float min_d, float max_d,
                                                       int* __restrict__ cnt, int stride) {
-    const SrcLevel S = L[blockIdx.y];
+    int lvl, bx;
+    src_block(G, lvl, bx);
+    const SrcLevel S = L[lvl];
     const long n = (long)S.rows * S.cols;
-    const long b0 = (long)blockIdx.x * R360_SRC_BLOCK;
+    const long b0 = (long)bx * R360_SRC_BLOCK;
     if (b0 >= n) return;
     int c = 0;
 #pragma unroll
@@ -229,20 +302,23 @@ __global__ void __launch_bounds__(SRC_TPB) k_src_count(const SrcLevel* __restric
     if (threadIdx.x == 0) {
         int t = 0;
         for (int w = 0; w < SRC_TPB / 64; ++w) t += sh[w];
-        cnt[blockIdx.y * stride + blockIdx.x] = t;
+        cnt[lvl * stride + bx] = t;
     }
 }
 
-__global__ void __launch_bounds__(SRC_TPB) k_src_compact(const SrcLevel* __restrict__ L, float min_d, float max_d,
-                                                        const int* __restrict__ cnt, int stride, int* __restrict__ npts) {
-    const SrcLevel S = L[blockIdx.y];
+__global__ void __launch_bounds__(SRC_TPB) k_src_compact(const SrcLevel* __restrict__ L, SrcGrid G, float min_d,
+                                                        float max_d, const int* __restrict__ cnt, int stride,
+                                                        int* __restrict__ npts) {
+    int lvl, bx;
+    src_block(G, lvl, bx);
+    const SrcLevel S = L[lvl];
     const long n = (long)S.rows * S.cols;
-    const long b0 = (long)blockIdx.x * R360_SRC_BLOCK;
+    const long b0 = (long)bx * R360_SRC_BLOCK;
     if (b0 >= n) return;
     __shared__ int sh[SRC_TPB / 64 + 1];
     // this block's output offset: the counts of the blocks before it
     int base = 0;
-    for (int b = threadIdx.x; b < (int)blockIdx.x; b += SRC_TPB) base += cnt[blockIdx.y * stride + b];
+    for (int b = threadIdx.x; b < bx; b += SRC_TPB) base += cnt[lvl * stride + b];
     for (int o = 32; o > 0; o >>= 1) base += __shfl_xor(base, o, 64);
     if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = base;
     __syncthreads();
@@ -279,7 +355,7 @@ __global__ void __launch_bounds__(SRC_TPB) k_src_compact(const SrcLevel* __restr
         // LUT_xyz_sphere (:4580-4582): x = d sin(phi), y = -d cos(phi) sin(theta), z = -d cos(phi) cos(theta)
         S.pts[pos++] = make_float4(d * S.sinphi[r], -d * S.cosphi[r] * S.sinth[cc], -d * S.cosphi[r] * S.costh[cc], a.x);
     }
-    if (blockIdx.x == (unsigned)((n - 1) / R360_SRC_BLOCK) && threadIdx.x == SRC_TPB - 1) npts[blockIdx.y] = pos;
+    if (bx == (int)((n - 1) / R360_SRC_BLOCK) && threadIdx.x == SRC_TPB - 1) npts[lvl] = pos;
 }
 
 int launch_sphere_level0(r360_frame* f) {
@@ -304,10 +380,14 @@ int launch_pyramid(r360_frame* f) {
         hipLaunchKernelGGL(k_gradient, dim3(grid_for(n)), dim3(TPB), 0, f->ctx->stream, f->lv[l].p0, f->lv[l].rows,
                            f->lv[l].cols, f->lv[l].tg, 1, 1);
     }
-    const dim3 g(f->src_blocks, f->n_levels);
-    hipLaunchKernelGGL(k_src_count, g, dim3(SRC_TPB), 0, f->ctx->stream, f->d_src_levels, min_d, max_d, f->d_src_cnt,
+    SrcGrid G{};
+    G.nl = f->n_levels;
+    for (int l = 0; l < f->n_levels; ++l)
+        G.blk0[l + 1] = G.blk0[l] + (int)(((long)f->lv[l].rows * f->lv[l].cols + R360_SRC_BLOCK - 1) / R360_SRC_BLOCK);
+    const dim3 g(G.blk0[f->n_levels]);
+    hipLaunchKernelGGL(k_src_count, g, dim3(SRC_TPB), 0, f->ctx->stream, f->d_src_levels, G, min_d, max_d, f->d_src_cnt,
                        f->src_blocks);
-    hipLaunchKernelGGL(k_src_compact, g, dim3(SRC_TPB), 0, f->ctx->stream, f->d_src_levels, min_d, max_d,
+    hipLaunchKernelGGL(k_src_compact, g, dim3(SRC_TPB), 0, f->ctx->stream, f->d_src_levels, G, min_d, max_d,
                        f->d_src_cnt, f->src_blocks, f->d_npts);
     R360_HIP(hipGetLastError());
     return 0;
