@@ -363,8 +363,9 @@ int r360_register_submit(r360_ctx* ctx, r360_dense_queue* q, r360_frame* ref, r3
 int r360_register_collect(r360_dense_queue* q, long ticket, float pose[16], float info[36], r360_icp_stats* st);
 /* Parity hook: the two raster sweeps of OrganizedMultiPlaneSegmentation::refine as k_refine* run them, on
  * 8 sensors' refinement states (-1 no label, -2 non-planar label, m >= 0 planar model m) and closeness
- * masks (bit m: the pixel is within 0.02 of model m), w x h each; rb < 0: the wavefront sweeps (the
- * default path), 0: one wave per sensor walks all rows, rb > 0: rb rows per band.  out = the swept states.
+ * masks (bit m: the pixel is within 0.02 of model m), w x h each; rb = -1: the wavefront sweeps (the
+ * default path: 64-row bands pipelined through LDS for h <= 512), -2: the wavefront with a workgroup barrier
+ * per diagonal, 0: one wave per sensor walks all rows, rb > 0: rb rows per band.  out = the swept states.
  * Returns the number of sensors whose wavefront second sweep needed corrections of the flat-index wrap push
  * (re-runs or the single-wave fallback; rb < 0), else 0; < 0 on error. */
 int r360_refine_eval(const int8_t* state, const uint64_t* mask, int w, int h, int rb, int8_t* out);

@@ -1066,8 +1066,9 @@ class RegisterPhotoICP:
 
 
 def refine_eval(state: np.ndarray, mask: np.ndarray, rb: int = 0, return_fallbacks: bool = False):
-    """refine()'s two sweeps on the device (parity hook): state int8 (8, h, w), mask uint64 (8, h, w); rb < 0 the
-    wavefront sweeps (the default path), 0 the single-wave sweeps, rb > 0 banded.  With return_fallbacks, also the
+    """refine()'s two sweeps on the device (parity hook): state int8 (8, h, w), mask uint64 (8, h, w); rb = -1 the
+    wavefront sweeps (the default path; LDS-pipelined 64-row bands for h <= 512), -2 the barrier-per-diagonal
+    wavefront, 0 the single-wave sweeps, rb > 0 banded.  With return_fallbacks, also the
     number of sensors whose wavefront second sweep needed wrap-push corrections (re-runs or the fallback)."""
     state = np.ascontiguousarray(state, np.int8)
     mask = np.ascontiguousarray(mask, np.uint64)

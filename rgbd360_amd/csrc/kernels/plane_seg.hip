@@ -988,7 +988,7 @@ __global__ void k_refine_skew(const int8_t* __restrict__ S, const unsigned long 
     // one thread per skewed slot (coalesced stores; the raster reads walk down-left diagonals, which reuse
     // each cache line for the next diagonals); slots outside the image are never used
     const long N = (long)w * h, SK = (long)(h + w - 1) * h, total = 8 * SK;
-    if (blockIdx.x == 0 && threadIdx.x < 16) fb[threadIdx.x] = 0;
+    if (blockIdx.x == 0 && threadIdx.x < 24) fb[threadIdx.x] = 0;
     for (long d = blockIdx.x * (long)blockDim.x + threadIdx.x; d < total; d += (long)gridDim.x * blockDim.x) {
         const int s = (int)(d / SK);
         const long q = d - (long)s * SK;
@@ -1168,6 +1168,328 @@ __global__ void __launch_bounds__(1024) k_refine_wave(const uint16_t* __restrict
     }
 }
 
+// ------------------------------------------------------------------ pipelined wavefront
+// The same wavefront with no workgroup barrier per diagonal: wave g owns the 64-row band r0 = 64 g .. r0 + 63
+// and walks its own diagonals r0 .. r0 + 63 + w - 1 at its own pace (inside the band the neighbour row's state
+// still comes by DPP from the neighbouring lane).  The one row that crosses a band edge is handed over in LDS:
+// the producing band (DIR > 0 the band above, DIR < 0 the band below) writes its edge row's states, in sweep
+// order u, to bnd[band][u] and publishes how many are valid (prog); the consuming band waits, every RP_BC steps,
+// until the values of its next RP_BC steps are there.  A band's step then costs its own dependency chain only,
+// not an LDS round trip plus a barrier over all bands, and the bands run as a pipeline one band's lead apart.
+//
+// Re-runs (DIR < 0, wrap pushes, as k_refine_wave): a band may stop early once its previous diagonal came out
+// unchanged, the lowest changed wrap assumption is behind it, and the band it consumes from has finished this
+// pass with every value it changed already consumed (lchg).  Values a band does not recompute in a re-run stay
+// in bnd from the previous pass, so prog starts at the band's first recomputed u.
+constexpr int RP_BC = 8;           // steps per chunk (hand-off check); loads run two chunks ahead
+constexpr int RP_MAXB = 8;         // bands (waves): h <= 512
+constexpr int RP_MAXW = 640;       // widest sensor
+constexpr int RP_PAD = 8;          // bnd rows are padded on both sides: a chunk stores its RP_BC edge values whole
+constexpr unsigned RP_SPIN = 1u << 22;
+
+struct PipeShared {
+    int8_t bnd[RP_MAXB][RP_MAXW + 2 * RP_PAD];   // each band's edge row (DIR > 0 its last, DIR < 0 its first), by u
+    int prog[RP_MAXB];              // bnd[g][u] valid this pass for u < prog[g] (w: the band is done)
+    int lchg[RP_MAXB];              // re-runs: the largest u of bnd[g] changed this pass (-1: none)
+    int8_t wasm[64 * RP_MAXB], wdet[64 * RP_MAXB];   // DIR < 0: assumed / detected wrap value per row
+    int s_red, s_min, s_fail;
+};
+
+// NARROW: every label and closeness bit of the sensor is below 30, so a mask test is one 32-bit bit-field
+// extract whose offset wraps -1 / -2 onto the always-clear bits 31 / 30 (no sign test), and the step's
+// dependency chain is DPP -> extract -> compare -> select.  The skewed arrays are read and written through
+// buffer resources: a step's diagonal offset is wave-uniform (scalar), the lane's row the vector offset.
+template <int DIR, bool NARROW>
+__device__ __forceinline__ void refine_pipe_body(const uint16_t* __restrict__ code_all,
+                                                 const unsigned long long* __restrict__ msk_all,
+                                                 int8_t* __restrict__ f1_all, int8_t* __restrict__ f2_all,
+                                                 int* __restrict__ fb, int w, int h, PipeShared& P) {
+    auto& bnd = P.bnd;
+    auto& prog = P.prog;
+    auto& lchg = P.lchg;
+    auto& wasm = P.wasm;
+    auto& wdet = P.wdet;
+    const int s = blockIdx.x;
+    const int r = threadIdx.x, lane = r & 63, nw = blockDim.x >> 6;
+    const int g = __builtin_amdgcn_readfirstlane(r >> 6);
+    const int SK = (h + w - 1) * h;
+    const auto rcode = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(code_all) + (long)s * SK, 0, SK * 2, 0x00020000);
+    const auto rmsk = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned long long*>(msk_all) + (long)s * SK, 0, SK * 8,
+                                                        0x00020000);
+    const auto rf1 = __builtin_amdgcn_make_buffer_rsrc(f1_all + (long)s * SK, 0, SK, 0x00020000);
+    const auto rf2 = __builtin_amdgcn_make_buffer_rsrc(f2_all + (long)s * SK, 0, SK, 0x00020000);
+    const int KS = h + w - 1;
+    const int rr = r < h ? r : h - 1;             // loads of rows >= h are clamped (never used)
+    const int r0 = g * 64, nr = min(64, h - r0);
+    // this band's diagonals r0 .. r0 + nr + w - 2 as steps [tlo, thi]
+    const int tlo = DIR > 0 ? r0 : KS - 1 - (r0 + nr + w - 2), thi = DIR > 0 ? r0 + nr + w - 2 : KS - 1 - r0;
+    const int up = DIR > 0 ? g - 1 : g + 1;       // the band whose edge row this one consumes
+    const bool has_up = up >= 0 && up < nw;
+    const bool has_out = DIR > 0 ? g < nw - 1 : g > 0;   // a band consumes this one's edge row
+    const int plane = DIR > 0 ? 63 : 0;           // the lane whose row is this band's edge row
+    // u of the consuming lane (DIR > 0 lane 0, DIR < 0 lane 63) and of the edge lane at step t
+    auto ucons = [&](int t) { return DIR > 0 ? t - r0 : t + r0 + 64 - h; };
+    auto uprod = [&](int t) { return DIR > 0 ? t - r0 - 63 : t + r0 + 1 - h; };
+    auto kof = [&](int t) { return DIR > 0 ? t : KS - 1 - t; };
+    struct In { unsigned code, f1, old; unsigned long long m; };
+    // DIR < 0 keeps fewer scalar registers live with plain 32-bit-offset loads (its wrap bookkeeping needs them)
+    constexpr bool BUF = DIR > 0;
+    const uint16_t* cs = code_all + (long)s * SK;
+    const unsigned long long* ms = msk_all + (long)s * SK;
+    const int8_t* f1s = f1_all + (long)s * SK;
+    int8_t* f2s = f2_all + (long)s * SK;
+    auto ld = [&](int t, bool redo, In& x) {
+        const int so = kof(t <= thi ? t : thi) * h;   // the diagonal's first slot
+        if (!BUF) {
+            const unsigned q = (unsigned)(so + rr);
+            x.code = cs[q];
+            x.m = NARROW ? (unsigned long long)reinterpret_cast<const unsigned*>(ms)[2 * q] : ms[q];
+            x.f1 = (unsigned char)f1s[q];
+            if (redo) x.old = (unsigned char)f2s[q];
+            return;
+        }
+        x.code = __builtin_amdgcn_raw_buffer_load_b16(rcode, rr * 2, so * 2, 0);
+        if (NARROW) {
+            x.m = __builtin_amdgcn_raw_buffer_load_b32(rmsk, rr * 8, so * 8, 0);
+        } else {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b64(rmsk, rr * 8, so * 8, 0);
+            x.m = (unsigned long long)v[0] | ((unsigned long long)v[1] << 32);
+        }
+        if (DIR < 0) x.f1 = __builtin_amdgcn_raw_buffer_load_b8(rf1, rr, so, 0);
+        if (DIR < 0 && redo) x.old = __builtin_amdgcn_raw_buffer_load_b8(rf2, rr, so, 0);
+    };
+    if (DIR < 0) {
+        for (int q = threadIdx.x; q < 64 * RP_MAXB; q += blockDim.x) { wasm[q] = -2; wdet[q] = -2; }
+    }
+    if (threadIdx.x == 0) P.s_fail = 0;
+    bool upw_free = false;     // DIR < 0: (r, w-1) was left at -2 by the push from below
+    unsigned long long mw = 0; //   and its mask
+    int t_start = 0, t_guard = 0;   // re-runs may stop only at steps after t_guard
+    auto run = [&](auto redo_tag) {
+        constexpr bool REDO = decltype(redo_tag)::value;
+        const int tb = max(t_start, tlo);
+        int prev = -1;         // this row's state at the previous step
+        if (REDO) {            // resume from the previous pass's states on the diagonal before tb
+            const int k = kof(tb - 1), c = k - r;
+            if (r < h && c >= 0 && c < w) prev = f2_all[(long)s * SK + (long)k * h + r];
+        }
+        const int my_wasm = DIR < 0 && r < h ? (int)wasm[r] : -2;   // this row's assumed wrap push
+        int my_wdet = DIR < 0 && r < h ? (int)wdet[r] : -2;         // and the one it detects
+        // three register sets of RP_BC diagonals used in rotation: a chunk's loads are issued two chunks ahead and
+        // no loop-carried copy of an in-flight load forces a wait
+        In A[RP_BC], B[RP_BC], C[RP_BC];
+#pragma unroll
+        for (int d = 0; d < RP_BC; ++d) { ld(tb + d, REDO, A[d]); ld(tb + RP_BC + d, REDO, B[d]); }
+        if (lane == 0) { lchg[g] = -1; prog[g] = min(max(uprod(tb), 0), w); }
+        __syncthreads();
+        bool pchg = true;
+        int lchg_r = -1;       // edge lane: the largest u it changed this pass
+        unsigned spins = 0;
+        // one chunk of RP_BC steps from t0 over inputs cur, issuing the loads of chunk t0 + 2 RP_BC into nn; FULL:
+        // every step is inside the band's range.  True when the pass ends in it.
+        auto chunk = [&](int t0, In (&cur)[RP_BC], In (&nn)[RP_BC], auto full_tag) -> bool {
+            constexpr bool FULL = decltype(full_tag)::value;
+#pragma unroll
+            for (int d = 0; d < RP_BC; ++d) ld(t0 + 2 * RP_BC + d, REDO, nn[d]);
+            // the upstream band's edge values of these steps
+            int bv[RP_BC];
+            if (has_up) {
+                const int need = min(ucons(t0 + RP_BC - 1), w - 1);
+                if (need >= 0) {
+                    while (__hip_atomic_load(&prog[up], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <= need) {
+                        if (++spins > RP_SPIN) { P.s_fail = 1; break; }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                }
+                asm volatile("" ::: "memory");
+#pragma unroll
+                for (int e = 0; e < RP_BC; ++e) {
+                    const int u = ucons(t0 + e);
+                    bv[e] = bnd[up][RP_PAD + (u < 0 ? 0 : (u < w ? u : w - 1))];
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < RP_BC; ++e) bv[e] = -1;
+            }
+            int Fv[RP_BC];     // the edge lane's states of this chunk (pass 0: stored to bnd at its end)
+            bool ended = false;
+#pragma unroll
+            for (int d = 0; d < RP_BC; ++d) {
+                const int t = t0 + d;
+                if (!FULL && t > thi) {
+                    ended = true;
+#pragma unroll
+                    for (int e = d; e < RP_BC; ++e) Fv[e] = -1;   // lands in the row's back padding
+                    break;
+                }
+                if (REDO && t > tb && !pchg && t - 1 > t_guard) {
+                    // the previous diagonal came out as in the previous pass: so does every later one once the
+                    // upstream band is done and its changed values are consumed
+                    if (!has_up || (__hip_atomic_load(&prog[up], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= w &&
+                                    __hip_atomic_load(&lchg[up], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < ucons(t)))
+                        return true;
+                }
+                const int k = kof(t);
+                const int c = k - r;
+                const bool act = (r < h) & ((unsigned)c < (unsigned)w);
+                // this step's inputs become visible here, not earlier: otherwise the scheduler hoists their uses
+                // to the chunk start and waits there for loads issued for two chunks later
+                unsigned xcode = cur[d].code, xf1 = cur[d].f1, xold = cur[d].old;
+                unsigned long long xm = cur[d].m;
+                asm volatile("" : "+v"(xcode), "+v"(xm));
+                if (DIR < 0) asm volatile("" : "+v"(xf1));
+                if (REDO) asm volatile("" : "+v"(xold));
+                const int o = DIR > 0 ? (int)(int8_t)(xcode & 0xff) : (int)(int8_t)xf1;
+                const bool cond = (xcode >> (DIR > 0 ? 8 : 9)) & 1;
+                const bool ch = DIR > 0 ? ((r <= h - 2) & (c >= 1)) : ((r >= 1) & (c <= w - 2));
+                const int pw = bv[d];
+                int F;
+                if (NARROW) {
+                    // off the chain: the candidate masks of the push (from the neighbour row) and of the chain
+                    // (from the left / right), and the value when neither applies
+                    const unsigned mlo = (unsigned)xm;
+                    const bool fixed = o != -2;
+                    const unsigned mp = (cond & !fixed) ? mlo : 0u, mc = (ch & !fixed) ? mlo : 0u;
+                    int base = o;
+                    bool first = false;
+                    if (DIR < 0) {
+                        first = (c == w - 1) & !fixed;                          // (r, w-1): the wrap push's target
+                        base = (first & (r <= h - 2) & act) ? my_wasm : base;  // the assumed wrap push
+                    }
+                    const int a = DIR > 0 ? __builtin_amdgcn_update_dpp(pw, prev, 0x138, 0xf, 0xf, false)
+                                          : __builtin_amdgcn_update_dpp(pw, prev, 0x130, 0xf, 0xf, false);
+                    const int alt = __builtin_amdgcn_ubfe(mc, (unsigned)prev, 1) ? prev : base;
+                    const bool pok = __builtin_amdgcn_ubfe(mp, (unsigned)a, 1) != 0;
+                    F = pok ? a : alt;
+                    if (DIR < 0) {
+                        upw_free = first ? (!pok & (r <= h - 2)) : upw_free;
+                        mw = first ? (unsigned long long)mlo : mw;
+                        const bool last = act & (c == 0) & (r <= h - 2);  // a = F(r+1, 0): the wrap push's source
+                        my_wdet = last ? ((upw_free & (__builtin_amdgcn_ubfe((unsigned)mw, (unsigned)a, 1) != 0)) ? a : -2)
+                                       : my_wdet;
+                    }
+                } else {
+                    const unsigned long long m = xm;
+                    int a = DIR > 0 ? __builtin_amdgcn_update_dpp(pw, prev, 0x138, 0xf, 0xf, false)    // wave_shr:1
+                                    : __builtin_amdgcn_update_dpp(pw, prev, 0x130, 0xf, 0xf, false);   // wave_shl:1
+                    if (DIR < 0 && r == h - 1) a = -1;
+                    int D = (cond & mbit(m, a)) ? a : -2;
+                    if (DIR < 0) {
+                        const bool first = (c == w - 1) & (o == -2);   // (r, w-1): the wrap push's target
+                        const bool uf = (D == -2) & (r <= h - 2);
+                        upw_free = first ? uf : upw_free;
+                        mw = first ? m : mw;
+                        D = (first & uf & act) ? my_wasm : D;          // the assumed wrap push (-2: none)
+                    }
+                    D = ((D == -2) & ch & mbit(m, prev)) ? prev : D;
+                    F = o == -2 ? D : o;
+                    if (DIR < 0) {
+                        const bool last = act & (c == 0) & (r <= h - 2);  // a = F(r+1, 0): the wrap push's source
+                        my_wdet = last ? ((upw_free & mbit(mw, a)) ? a : -2) : my_wdet;
+                    }
+                }
+                if (act) {
+                    if (BUF) __builtin_amdgcn_raw_buffer_store_b8((unsigned char)F, rf1, r, k * h, 0);
+                    else f2s[(unsigned)(k * h + r)] = (int8_t)F;
+                }
+                Fv[d] = F;
+                prev = act ? F : prev;
+                if (REDO || DIR < 0) {   // DIR < 0: per-step edge stores keep fewer registers live
+                    const bool changed = REDO & act & (F != (int)(int8_t)xold);
+                    if (lane == plane && act) {
+                        const int u = uprod(t);
+                        bnd[g][RP_PAD + u] = (int8_t)F;
+                        if (changed) lchg_r = u;
+                    }
+                    if (REDO) pchg = __any(changed);
+                }
+            }
+            if (lane == plane) {   // publish this chunk's edge values
+                if (!REDO && DIR > 0 && has_out) {
+                    const int u0 = uprod(t0);
+                    if (u0 + RP_BC - 1 >= 0) {
+#pragma unroll
+                        for (int d = 0; d < RP_BC; ++d) bnd[g][RP_PAD + u0 + d] = (int8_t)Fv[d];
+                    }
+                }
+                __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the values before their count
+                lchg[g] = lchg_r;
+                __hip_atomic_store(&prog[g], min(max(uprod(min(t0 + RP_BC - 1, thi)) + 1, 0), w), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            return ended;
+        };
+        using T = std::integral_constant<bool, true>;
+        using Fl = std::integral_constant<bool, false>;
+        int t0 = tb;
+        bool ended = false;
+        for (; DIR > 0 && t0 + 3 * RP_BC - 1 <= thi; t0 += 3 * RP_BC) {   // whole rotations inside the range
+            if (chunk(t0, A, C, T{}) || chunk(t0 + RP_BC, B, A, T{}) || chunk(t0 + 2 * RP_BC, C, B, T{})) {
+                ended = true;
+                break;
+            }
+        }
+        if (DIR > 0) {
+            if (!ended && t0 <= thi && !chunk(t0, A, C, Fl{}) && t0 + RP_BC <= thi && !chunk(t0 + RP_BC, B, A, Fl{}) &&
+                t0 + 2 * RP_BC <= thi)
+                chunk(t0 + 2 * RP_BC, C, B, Fl{});
+        } else {   // DIR < 0: every chunk checks the range end (one copy of the step code per rotation slot)
+            for (; t0 <= thi; t0 += 3 * RP_BC) {
+                if (chunk(t0, A, C, Fl{}) || chunk(t0 + RP_BC, B, A, Fl{}) || chunk(t0 + 2 * RP_BC, C, B, Fl{})) break;
+            }
+        }
+        if (lane == plane) {   // done: every value of bnd[g] is this pass's
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            lchg[g] = lchg_r;
+            __hip_atomic_store(&prog[g], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if (DIR < 0 && r < h) wdet[r] = (int8_t)my_wdet;
+        __syncthreads();
+    };
+    for (int pass = 0;; ++pass) {
+        if (pass == 0) run(std::integral_constant<bool, false>{});
+        else run(std::integral_constant<bool, true>{});
+        if (P.s_fail) {   // a hand-off wait gave up: k_refine_fb redoes this sensor (both sweeps after a first-sweep failure)
+            if (threadIdx.x == 0) {
+                fb[s] = h - 1;
+                if (DIR > 0) fb[16 + s] = 1;
+            }
+            break;
+        }
+        if (DIR > 0) break;
+        if (threadIdx.x == 0) { P.s_red = -1; P.s_min = h; }
+        __syncthreads();
+        const bool mis = r <= h - 2 && wdet[r] != wasm[r];
+        if (mis) { atomicMax(&P.s_red, r); atomicMin(&P.s_min, r); }
+        __syncthreads();
+        const int rs = __builtin_amdgcn_readfirstlane(P.s_red);
+        if (rs < 0) {
+            if (threadIdx.x == 0 && pass > 0) fb[8 + s] = pass;
+            break;
+        }
+        if (pass >= RW_MAX_REDO) {
+            if (threadIdx.x == 0) { fb[s] = rs + 1; fb[8 + s] = pass; }
+            break;
+        }
+        if (mis) wasm[r] = wdet[r];
+        t_start = KS - 1 - (rs + w - 1);
+        t_guard = KS - 1 - (__builtin_amdgcn_readfirstlane(P.s_min) + w - 1);
+        __syncthreads();
+    }
+}
+
+// NW: the most waves (bands) it is launched with; 4 (h <= 256) leaves each wave up to 512 VGPRs
+template <int DIR, int NW>
+__global__ void __launch_bounds__(64 * NW) k_refine_pipe(const uint16_t* __restrict__ code_all,
+                                                             const unsigned long long* __restrict__ msk_all,
+                                                             int8_t* __restrict__ f1_all, int8_t* __restrict__ f2_all,
+                                                             const int* __restrict__ nmodels, int* __restrict__ fb,
+                                                             int w, int h, int narrow_max) {
+    __shared__ PipeShared P;
+    if (nmodels[blockIdx.x] <= narrow_max) refine_pipe_body<DIR, true>(code_all, msk_all, f1_all, f2_all, fb, w, h, P);
+    else refine_pipe_body<DIR, false>(code_all, msk_all, f1_all, f2_all, fb, w, h, P);
+}
+
 // the second sweep's states back to raster order (sensors handed to k_refine_fb are written by it)
 __global__ void k_refine_unskew(const int8_t* __restrict__ f2_all, int8_t* __restrict__ S_all,
                                 const int* __restrict__ fb, int w, int h) {
@@ -1189,6 +1511,10 @@ __global__ void __launch_bounds__(64) k_refine_fb(const int8_t* __restrict__ f1_
                                                  const unsigned long long* __restrict__ MK, const int* __restrict__ fb,
                                                  int w, int h) {
     const int s = blockIdx.x;
+    if (fb[16 + s]) {   // the pipelined first sweep gave up: both sweeps from the original states
+        refine_sweeps<K>(S_all, MK, w, h, s, 3);
+        return;
+    }
     const int r0 = fb[s] - 1;
     if (r0 < 0) return;
     const long N = (long)w * h, SK = (long)(h + w - 1) * h;
@@ -1735,12 +2061,12 @@ __global__ void __launch_bounds__(VOXC_TPB) k_vox_compact(const VoxCell* __restr
 // buffers of the wavefront refinement (skewed layout, [8][h + w - 1][h] each)
 struct RefineWaveBufs { uint16_t* code; unsigned long long* msk; int8_t* f1; int8_t* f2; };
 
-// refinement mode: -1 the wavefront sweeps (default), 0 the single-wave sweeps, rb > 0 banded with rb rows per
-// band (R360_REFINE_ROWS overrides)
+// refinement mode: -1 the wavefront sweeps (default; pipelined bands for h <= 512), -2 the wavefront sweeps with a
+// barrier per diagonal, 0 the single-wave sweeps, rb > 0 banded with rb rows per band (R360_REFINE_ROWS overrides)
 int refine_band_rows(int h) {
-    static const int env = getenv("R360_REFINE_ROWS") ? atoi(getenv("R360_REFINE_ROWS")) : -2;
-    int rb = env >= -1 ? env : -1;
-    if (rb < 0) return h <= 1024 ? -1 : 0;
+    static const int env = getenv("R360_REFINE_ROWS") ? atoi(getenv("R360_REFINE_ROWS")) : -99;
+    int rb = env >= -2 ? env : -1;
+    if (rb < 0) return h <= 1024 ? rb : 0;
     if (rb > 0 && (h + rb - 1) / rb > R360_REFINE_BANDS) rb = (h + R360_REFINE_BANDS - 1) / R360_REFINE_BANDS;
     return rb;
 }
@@ -1748,7 +2074,7 @@ int refine_band_rows(int h) {
 // refine()'s two sweeps over 8 sensors' states S (in place), closeness masks MK.  rb > 0: banded (phases 1 and
 // 2 per sweep; S2 holds the first sweep's output); rb = 0: one wave per sensor walks every row (k_refine).
 int launch_refine_sweeps(hipStream_t st, int8_t* S, int8_t* S2, const unsigned long long* MK, int8_t* bnd, int* flag,
-                         int w, int h, int rb, const RefineWaveBufs* wb) {
+                         int w, int h, int rb, const RefineWaveBufs* wb, const int* nmodels) {
     const int K = (w + 63) / 64;
     if (rb < 0 && (w < 2 || h > 1024 || !wb)) rb = 0;
     if (rb < 0) {
@@ -1756,8 +2082,24 @@ int launch_refine_sweeps(hipStream_t st, int8_t* S, int8_t* S2, const unsigned l
         hipLaunchKernelGGL(k_refine_skew, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, st, S, MK, w, h, wb->code,
                            wb->msk, flag);
         const int tpb = 64 * ((h + 63) / 64);
-        hipLaunchKernelGGL(k_refine_wave<1>, dim3(8), dim3(tpb), 0, st, wb->code, wb->msk, wb->f1, S, flag, w, h);
-        hipLaunchKernelGGL(k_refine_wave<-1>, dim3(8), dim3(tpb), 0, st, wb->code, wb->msk, wb->f1, wb->f2, flag, w, h);
+        // R360_REFINE_NARROW=0: the 64-bit mask path for every sensor (inspection)
+        static const int narrow_max = getenv("R360_REFINE_NARROW") && !atoi(getenv("R360_REFINE_NARROW")) ? -1 : 30;
+        if (rb == -1 && h <= 64 * RP_MAXB && w <= RP_MAXW && nmodels) {
+            if (h <= 256) {
+                hipLaunchKernelGGL((k_refine_pipe<1, 4>), dim3(8), dim3(tpb), 0, st, wb->code, wb->msk, wb->f1, wb->f2,
+                                   nmodels, flag, w, h, narrow_max);
+                hipLaunchKernelGGL((k_refine_pipe<-1, 4>), dim3(8), dim3(tpb), 0, st, wb->code, wb->msk, wb->f1, wb->f2,
+                                   nmodels, flag, w, h, narrow_max);
+            } else {
+                hipLaunchKernelGGL((k_refine_pipe<1, RP_MAXB>), dim3(8), dim3(tpb), 0, st, wb->code, wb->msk, wb->f1,
+                                   wb->f2, nmodels, flag, w, h, narrow_max);
+                hipLaunchKernelGGL((k_refine_pipe<-1, RP_MAXB>), dim3(8), dim3(tpb), 0, st, wb->code, wb->msk, wb->f1,
+                                   wb->f2, nmodels, flag, w, h, narrow_max);
+            }
+        } else {
+            hipLaunchKernelGGL(k_refine_wave<1>, dim3(8), dim3(tpb), 0, st, wb->code, wb->msk, wb->f1, S, flag, w, h);
+            hipLaunchKernelGGL(k_refine_wave<-1>, dim3(8), dim3(tpb), 0, st, wb->code, wb->msk, wb->f1, wb->f2, flag, w, h);
+        }
         hipLaunchKernelGGL(k_refine_unskew, dim3((unsigned)((8L * w * h + 255) / 256)), dim3(256), 0, st, wb->f2, S, flag,
                            w, h);
         switch (K) {
@@ -1843,7 +2185,8 @@ int launch_segmentation(r360_frame* f) {
     hipLaunchKernelGGL(k_refine_init, dim3(blocks), dim3(256), 0, st, P.cloud, P.lab, N, P.models, P.nmodels, P.state,
                        P.mask);
     const RefineWaveBufs wb{P.rcode, P.rmsk, P.rf1, P.rf2};
-    if (launch_refine_sweeps(st, P.state, P.state2, P.mask, P.rbnd, P.rflag, w, h, refine_band_rows(h), &wb)) return -1;
+    if (launch_refine_sweeps(st, P.state, P.state2, P.mask, P.rbnd, P.rflag, w, h, refine_band_rows(h), &wb, P.nmodels))
+        return -1;
     hipLaunchKernelGGL(k_refine_final, dim3(blocks), dim3(256), 0, st, P.state, P.lab, N, P.models, P.labf);
     timing_end(ctx, slot);
     R360_HIP(hipGetLastError());
@@ -1880,8 +2223,8 @@ int launch_segmentation(r360_frame* f) {
     return 0;
 }
 
-// Test hook: refine()'s two sweeps on given states / closeness masks of 8 sensors (w x h each): rb < 0 the
-// wavefront sweeps, 0 the single-wave sweeps, rb > 0 banded with rb rows per band; out receives the swept
+// Test hook: refine()'s two sweeps on given states / closeness masks of 8 sensors (w x h each): rb = -1 the
+// wavefront sweeps (pipelined bands for h <= 512), -2 the barrier-per-diagonal wavefront, 0 the single-wave sweeps, rb > 0 banded with rb rows per band; out receives the swept
 // states.  Returns the number of sensors whose wavefront second sweep needed wrap-push corrections (re-runs
 // or the single-wave fallback; rb < 0), else 0.
 extern "C" int r360_refine_eval(const int8_t* state, const uint64_t* mask, int w, int h, int rb, int8_t* out) {
@@ -1903,7 +2246,19 @@ extern "C" int r360_refine_eval(const int8_t* state, const uint64_t* mask, int w
     R360_HIP(hipMalloc(&wb.msk, sizeof(unsigned long long) * SK));
     R360_HIP(hipMalloc(&wb.f1, SK));
     R360_HIP(hipMalloc(&wb.f2, SK));
-    int rc = launch_refine_sweeps(0, S, S2, MK, bnd, flag, w, h, rb, &wb);
+    // models per sensor as the pipeline's k_plane_fit counts them: above every label and closeness bit
+    int nmh[8], *nm;
+    for (int s = 0; s < 8; ++s) {
+        int top = 0;
+        for (size_t i = (size_t)s * w * h; i < (size_t)(s + 1) * w * h; ++i) {
+            if (state[i] + 1 > top) top = state[i] + 1;
+            if (mask[i]) top = std::max(top, 64 - __builtin_clzll(mask[i]));
+        }
+        nmh[s] = top;
+    }
+    R360_HIP(hipMalloc(&nm, sizeof(nmh)));
+    R360_HIP(hipMemcpy(nm, nmh, sizeof(nmh), hipMemcpyHostToDevice));
+    int rc = launch_refine_sweeps(0, S, S2, MK, bnd, flag, w, h, rb, &wb, nm);
     if (rc == 0) {
         R360_HIP(hipMemcpy(out, S, T, hipMemcpyDeviceToHost));
         if (rb < 0 && w >= 2 && h <= 1024) {
@@ -1914,7 +2269,7 @@ extern "C" int r360_refine_eval(const int8_t* state, const uint64_t* mask, int w
                 for (int k = 0; k < 8; ++k) fprintf(stderr, "refine sensor %d: re-runs %d fallback row %d\n", k, fbh[8 + k], fbh[k] - 1);
         }
     }
-    (void)hipFree(S); (void)hipFree(S2); (void)hipFree(MK); (void)hipFree(bnd); (void)hipFree(flag);
+    (void)hipFree(S); (void)hipFree(S2); (void)hipFree(MK); (void)hipFree(bnd); (void)hipFree(flag); (void)hipFree(nm);
     (void)hipFree(wb.code); (void)hipFree(wb.msk); (void)hipFree(wb.f1); (void)hipFree(wb.f2);
     return rc;
 }

@@ -95,17 +95,17 @@ def test_banded_sweeps_equal_python_restatement(seed, dense):
     S, M = _inputs(h, w, seed, dense)
     ref = np.stack([_refine_ref(S[s], M[s]) for s in range(8)])
     assert not np.array_equal(ref, S)            # the sweeps changed something
-    for rb in (-1, 0, 1, 3, 8, 16, 37):
+    for rb in (-1, -2, 0, 1, 3, 8, 16, 37):
         out = R.refine_eval(S, M, rb)
         assert np.array_equal(out, ref), (rb, np.argwhere(out != ref)[:5])
 
 
-@pytest.mark.parametrize("h,w", [(240, 320), (480, 640), (120, 160)])
+@pytest.mark.parametrize("h,w", [(240, 320), (480, 640), (120, 160), (65, 97), (200, 333), (512, 640)])
 def test_banded_sweeps_equal_single_wave(h, w):
     for seed in (11, 12):
         S, M = _inputs(h, w, seed)
         one = R.refine_eval(S, M, 0)
-        for rb in [r for r in (-1, 4, 16, 32) if -(-h // r) <= 64]:
+        for rb in [r for r in (-1, -2, 4, 16, 32) if r < 0 or -(-h // r) <= 64]:
             assert np.array_equal(R.refine_eval(S, M, rb), one), (h, w, rb, seed)
 
 
@@ -117,7 +117,7 @@ def _no_wrap(S):
     return S
 
 
-@pytest.mark.parametrize("h,w", [(37, 70), (240, 320), (480, 640)])
+@pytest.mark.parametrize("h,w", [(37, 70), (130, 203), (240, 320), (480, 640)])
 def test_wavefront_sweeps_both_paths(h, w):
     """The wavefront sweeps (the default refinement path) on both of its paths: no wrap push (pure wavefront,
     checked against the sequential restatement / single-wave kernel) and wrap pushes firing (the fallback
@@ -128,10 +128,28 @@ def test_wavefront_sweeps_both_paths(h, w):
         for St, want_fb in ((_no_wrap(S), False), (S, None)):
             ref = (np.stack([_refine_ref(St[s], M[s]) for s in range(8)]) if h * w <= 37 * 70
                    else R.refine_eval(St, M, 0))
-            out, nfb = R.refine_eval(St, M, -1, return_fallbacks=True)
-            assert np.array_equal(out, ref), (h, w, seed, np.argwhere(out != ref)[:5])
-            if want_fb is False:
-                assert nfb == 0
-            else:
-                seen_fb += nfb
+            for rb in (-1, -2):   # LDS-pipelined bands (default) and barrier per diagonal
+                out, nfb = R.refine_eval(St, M, rb, return_fallbacks=True)
+                assert np.array_equal(out, ref), (h, w, seed, rb, np.argwhere(out != ref)[:5])
+                if want_fb is False:
+                    assert nfb == 0
+                else:
+                    seen_fb += nfb
     assert seen_fb > 0   # the random fields do make the wrap push fire somewhere
+
+
+@pytest.mark.parametrize("h,w", [(37, 70), (240, 320)])
+def test_wavefront_sweeps_wide_labels(h, w):
+    """Labels and closeness bits above 30 (sensors with more than 30 models): the pipelined sweeps take their
+    64-bit mask path there, checked like the narrow one."""
+    for seed in (31, 32):
+        S, M = _inputs(h, w, seed)
+        S = np.where(S >= 0, S + 40, S).astype(np.int8)
+        M = M << np.uint64(40)
+        S[3] = np.where(S[3] >= 0, S[3] - 40, S[3])   # one narrow sensor beside the wide ones
+        M[3] = M[3] >> np.uint64(40)
+        ref = (np.stack([_refine_ref(S[s], M[s]) for s in range(8)]) if h * w <= 37 * 70
+               else R.refine_eval(S, M, 0))
+        for rb in (-1, -2):
+            out = R.refine_eval(S, M, rb)
+            assert np.array_equal(out, ref), (h, w, seed, rb, np.argwhere(out != ref)[:5])
