@@ -1354,7 +1354,7 @@ __device__ __forceinline__ void refine_pipe_body(const uint16_t* __restrict__ co
                     bool first = false;
                     if (DIR < 0) {
                         first = (c == w - 1) & !fixed;                          // (r, w-1): the wrap push's target
-                        base = (first & (r <= h - 2) & act) ? my_wasm : base;  // the assumed wrap push
+                        base = (first & (r <= h - 2)) ? my_wasm : base;        // the assumed wrap push
                     }
                     const int a = DIR > 0 ? __builtin_amdgcn_update_dpp(pw, prev, 0x138, 0xf, 0xf, false)
                                           : __builtin_amdgcn_update_dpp(pw, prev, 0x130, 0xf, 0xf, false);
@@ -1362,11 +1362,13 @@ __device__ __forceinline__ void refine_pipe_body(const uint16_t* __restrict__ co
                     const bool pok = __builtin_amdgcn_ubfe(mp, (unsigned)a, 1) != 0;
                     F = pok ? a : alt;
                     if (DIR < 0) {
-                        upw_free = first ? (!pok & (r <= h - 2)) : upw_free;
-                        mw = first ? (unsigned long long)mlo : mw;
-                        const bool last = act & (c == 0) & (r <= h - 2);  // a = F(r+1, 0): the wrap push's source
-                        my_wdet = last ? ((upw_free & (__builtin_amdgcn_ubfe((unsigned)mw, (unsigned)a, 1) != 0)) ? a : -2)
-                                       : my_wdet;
+                        // the wrap bookkeeping touches one lane per step at most: branches, not selects per step
+                        if (first) {
+                            upw_free = !pok & (r <= h - 2);
+                            mw = mlo;
+                        }
+                        if (act & (c == 0) & (r <= h - 2))   // a = F(r+1, 0): the wrap push's source
+                            my_wdet = (upw_free & (__builtin_amdgcn_ubfe((unsigned)mw, (unsigned)a, 1) != 0)) ? a : -2;
                     }
                 } else {
                     const unsigned long long m = xm;
