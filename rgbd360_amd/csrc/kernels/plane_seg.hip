@@ -29,10 +29,13 @@ __device__ __forceinline__ bool isfin(float v) { return __builtin_isfinite(v); }
 // ------------------------------------------------------------------ CCL
 __device__ __forceinline__ int ld(const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
-__device__ int find_root(const int* parent, int x) {
+// with path halving (see lds_find); the re-points are agent-scope atomic stores, like the CAS links
+__device__ int find_root(int* parent, int x) {
     int p = ld(parent + x);
     while (p != x) {
-        x = p;
+        const int gp = ld(parent + p);
+        if (gp != p) __hip_atomic_store(parent + x, gp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        x = gp;
         p = ld(parent + x);
     }
     return x;
@@ -65,10 +68,15 @@ __device__ __forceinline__ bool plane_cmp(const float4& pa, const float4& na, co
 // boundaries in global memory.
 constexpr int CCL_ROWS = 8, CCL_TPB = 1024;
 
-__device__ int lds_find(const int* lp, int x) {
+// path halving: every other node on the walk is re-pointed at its grandparent.  Parents only ever point at
+// smaller indices of the same component, so a racing re-point installs another ancestor and the roots (the
+// components' smallest indices) are unchanged.
+__device__ int lds_find(int* lp, int x) {
     int p = lp[x];
     while (p != x) {
-        x = p;
+        const int gp = lp[p];
+        if (gp != p) lp[x] = gp;
+        x = gp;
         p = lp[x];
     }
     return x;
@@ -123,7 +131,7 @@ __global__ void k_ccl_border(const float4* __restrict__ cloud, const float4* __r
     }
 }
 
-__global__ void k_ccl_flatten(const int* __restrict__ parent, long total, int* __restrict__ root) {
+__global__ void k_ccl_flatten(int* __restrict__ parent, long total, int* __restrict__ root) {
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x)
         root[i] = parent[i] < 0 ? -1 : find_root(parent, (int)i);
 }
@@ -165,7 +173,18 @@ __global__ void __launch_bounds__(NUM_TPB) k_ccl_number(const int* __restrict__ 
     const int s = blockIdx.x;
     const long base = (long)s * N;
     const int nq = (N + SCAN_V - 1) / SCAN_V;
-    for (int q = threadIdx.x; q < nq; q += NUM_TPB) {
+    // whole flag bytes with two 16-byte loads (the sensor's slice starts 32-byte aligned when N % 8 == 0)
+    const int nq_vec = (N % SCAN_V) == 0 ? nq : 0;
+    for (int q = threadIdx.x; q < nq_vec; q += NUM_TPB) {
+        const int4* p4 = reinterpret_cast<const int4*>(root + base + (long)q * SCAN_V);
+        const int4 a = p4[0], b = p4[1];
+        const int j0 = (int)(base + (long)q * SCAN_V);
+        const unsigned f = (unsigned)(a.x == j0) | (unsigned)(a.y == j0 + 1) << 1 | (unsigned)(a.z == j0 + 2) << 2 |
+                           (unsigned)(a.w == j0 + 3) << 3 | (unsigned)(b.x == j0 + 4) << 4 | (unsigned)(b.y == j0 + 5) << 5 |
+                           (unsigned)(b.z == j0 + 6) << 6 | (unsigned)(b.w == j0 + 7) << 7;
+        F[q] = (unsigned char)f;
+    }
+    for (int q = nq_vec + threadIdx.x; q < nq; q += NUM_TPB) {
         unsigned f = 0;
 #pragma unroll
         for (int v = 0; v < SCAN_V; ++v) {
