@@ -248,7 +248,21 @@ __global__ void __launch_bounds__(NUM_TPB) k_big_list(const int* __restrict__ cn
     const int n = nlab[s];
     const long base = (long)s * N;
     const int nq = (n + SCAN_V - 1) / SCAN_V;
-    for (int q = threadIdx.x; q < nq; q += NUM_TPB) {
+    // whole flag bytes with two 16-byte loads (the sensor's slice starts 32-byte aligned when N % 8 == 0)
+    const int nq_vec = (N % SCAN_V) == 0 ? n / SCAN_V : 0;
+    for (int q = threadIdx.x; q < nq_vec; q += NUM_TPB) {
+        const int4* p4 = reinterpret_cast<const int4*>(cnt + base + (long)q * SCAN_V);
+        const int4 a = p4[0], b = p4[1];
+        const int c8[SCAN_V] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        unsigned f = 0;
+#pragma unroll
+        for (int v = 0; v < SCAN_V; ++v) {
+            if (c8[v] > min_inliers) f |= 1u << v;
+            else bmap[base + q * SCAN_V + v] = -1;
+        }
+        F[q] = (unsigned char)f;
+    }
+    for (int q = nq_vec + threadIdx.x; q < nq; q += NUM_TPB) {
         unsigned f = 0;
 #pragma unroll
         for (int v = 0; v < SCAN_V; ++v) {
