@@ -1751,8 +1751,11 @@ constexpr int TR_NB_MAX = 96 * 1024;          // largest sensor (w*h) whose mask
 // Moore step: next direction = first neighbour in the mask clockwise after dir (the d = 1..8 scan of
 // the reference loop); an empty mask keeps nd = dir (the scan's last candidate), as the reference does.
 __device__ __forceinline__ int trace_next(unsigned m8, int dir) {
-    const unsigned r = ((m8 | (m8 << 8)) >> ((dir + 1) & 7)) & 0xffu;
-    return r ? (dir + 1 + __builtin_ctz(r)) & 7 : dir;
+    const unsigned r = ((m8 * 0x101u) >> ((dir + 1) & 7)) & 0xffu;
+    // v_ffbl of 0 is -1, which leaves nd = dir for an empty mask with no compare / select
+    int tz;
+    asm("v_ffbl_b32 %0, %1" : "=v"(tz) : "v"(r));
+    return (dir + 1 + tz) & 7;
 }
 
 template <bool LDS>
@@ -1786,7 +1789,12 @@ __global__ void __launch_bounds__(TR_TPB) k_trace(const uint8_t* __restrict__ nb
     // local table would be a global-memory load on the trace's dependency chain)
     auto dxs = [](int d) { return (int)((0x1A90U >> (2 * d)) & 3u) - 1; };
     auto dys = [](int d) { return (int)((0xA901U >> (2 * d)) & 3u) - 1; };
-    const long max_len = 8L * N;
+    // the step's index offset dy * w + dx with a 24-bit multiply of the raw (0..2) fields
+    const int wp1 = w + 1;
+    auto step_off = [&](int d) {
+        return (int)__umul24((0xA901U >> (2 * d)) & 3u, (unsigned)w) + (int)((0x1A90U >> (2 * d)) & 3u) - wp1;
+    };
+    const int max_len = 8 * N;
     const int m = threadIdx.x;
     int dir0 = -1, start = 0;
     if (m < nm) {
@@ -1798,7 +1806,7 @@ __global__ void __launch_bounds__(TR_TPB) k_trace(const uint8_t* __restrict__ nb
             const int x = cx + dxs(d), y = cy + dys(d);
             if (x >= 0 && x < w && y >= 0 && y < h && !((m8 >> d) & 1)) { dir0 = d; break; }
         }
-        long n = 0;
+        int n = 0;
         if (dir0 >= 0) {
             int chunk = atomicAdd(&s_nch, 1), pos = 0;
             s_head[m] = chunk;
@@ -1817,7 +1825,7 @@ __global__ void __launch_bounds__(TR_TPB) k_trace(const uint8_t* __restrict__ nb
             do {
                 const int nd = trace_next(nb[cidx], dir);
                 dir = (nd + 4) & 7;
-                cidx += dys(nd) * w + dxs(nd);
+                cidx += step_off(nd);
                 append(cidx);
                 if (++n > max_len) { atomicOr(err, 8); break; }
             } while (cidx != start);
@@ -1873,7 +1881,7 @@ __global__ void __launch_bounds__(TR_TPB) k_trace(const uint8_t* __restrict__ nb
         do {
             const int nd = trace_next(nb[cidx], dir);
             dir = (nd + 4) & 7;
-            cidx += dys(nd) * w + dxs(nd);
+            cidx += step_off(nd);
             if (dst + n < cap_end) pool[dst + n] = P[cidx];
         } while (++n <= max_len && cidx != start);
     }
