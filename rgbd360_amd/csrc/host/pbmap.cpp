@@ -404,14 +404,10 @@ int planes_enqueue(r360_frame* f) {
     if (plane_bufs_alloc(f)) return -1;
     planes_join(f);
     PlaneBufs& P = f->pl;
-    R360_HIP(hipMemsetAsync(P.err, 0, sizeof(int), f->ctx->stream));
+    // k_plane_begin (first kernel of launch_cloud_normals) zeroes the error word
     if (launch_cloud_normals(f)) return -1;
     if (launch_segmentation(f)) return -1;
-    R360_HIP(hipMemcpyAsync(P.h_out, P.out, sizeof(PlaneOut) * 8 * R360_MAX_MODELS, hipMemcpyDeviceToHost,
-                            f->ctx->stream));
-    R360_HIP(hipMemcpyAsync(P.h_nmodels, P.nmodels, sizeof(int) * 8, hipMemcpyDeviceToHost, f->ctx->stream));
-    R360_HIP(hipMemcpyAsync(P.h_nmodels + 8, P.err, sizeof(int), hipMemcpyDeviceToHost, f->ctx->stream));
-    R360_HIP(hipMemcpyAsync(P.h_nmodels + 10, P.totals, sizeof(long) * 2, hipMemcpyDeviceToHost, f->ctx->stream));
+    if (launch_plane_publish(f)) return -1;
     R360_HIP(hipEventRecord(P.done, f->ctx->stream));
     delete f->pbmap;
     f->pbmap = nullptr;

@@ -109,6 +109,14 @@ __global__ void k_cloud(const float* __restrict__ depth_m, const uint8_t* __rest
 }
 
 
+// the frame's plane stage starts: depth-range accumulators and the error word (one launch instead of memsets)
+__global__ void k_plane_begin(int* __restrict__ zmm, int* __restrict__ err) {
+    const int t = threadIdx.x;
+    if (t < 8) zmm[t] = kOrdMinInit;
+    else if (t < 16) zmm[t] = kOrdMaxInit;
+    if (t == 0) *err = 0;
+}
+
 // per-sensor depth range from k_cloud's per-wave partials (waves inside one sensor)
 __global__ void __launch_bounds__(1024) k_zrange(const int* __restrict__ wmm, long N, int* __restrict__ zmm) {
     __shared__ int smin[16], smax[16];
@@ -490,8 +498,7 @@ int launch_cloud_normals(r360_frame* f) {
     const float inv_f = 1.f / focal_length;
     const float ox = f->cols / 2 - 0.5, oy = f->rows / 2 - 0.5;
     int slot = timing_begin(f->ctx, "k_cloud");
-    R360_HIP(hipMemsetAsync(P.zmm, 0x7f, sizeof(int) * 8, st));
-    R360_HIP(hipMemsetAsync(P.zmm + 8, 0x80, sizeof(int) * 8, st));
+    hipLaunchKernelGGL(k_plane_begin, dim3(1), dim3(64), 0, st, P.zmm, P.err);
     hipLaunchKernelGGL(k_cloud, dim3(blocks), dim3(256), 0, st, f->d_depth_m, f->d_bgr, f->rows, f->cols, inv_f, ox, oy,
                        P.cloud, P.rgb, P.zmm, reinterpret_cast<int*>(P.dist0));
     hipLaunchKernelGGL(k_zrange, dim3(8), dim3(1024), 0, st, reinterpret_cast<const int*>(P.dist0), (long)w * h, P.zmm);

@@ -131,9 +131,12 @@ __global__ void k_ccl_border(const float4* __restrict__ cloud, const float4* __r
     }
 }
 
-__global__ void k_ccl_flatten(int* __restrict__ parent, long total, int* __restrict__ root) {
-    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x)
+// also zeroes the label counts k_ccl_label accumulates (one launch instead of a memset)
+__global__ void k_ccl_flatten(int* __restrict__ parent, long total, int* __restrict__ root, int* __restrict__ cnt) {
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
         root[i] = parent[i] < 0 ? -1 : find_root(parent, (int)i);
+        cnt[i] = 0;
+    }
 }
 
 // block-wide exclusive scan of one int per thread (blockDim.x = 1024)
@@ -241,11 +244,12 @@ __global__ void __launch_bounds__(NUM_TPB) k_big_list(const int* __restrict__ cn
                                                       int min_inliers, int* __restrict__ big, int* __restrict__ nbig,
                                                       int maxbig, int* __restrict__ err, int* __restrict__ bmap,
                                                       int* __restrict__ boff, r360p::Moments* __restrict__ mom,
-                                                      int* __restrict__ bfirst) {
+                                                      int* __restrict__ bfirst, int* __restrict__ bcur) {
     __shared__ int sh[17];
     __shared__ unsigned char F[NUM_MAXQ];
     const int s = blockIdx.x;
     const int n = nlab[s];
+    for (int q = threadIdx.x; q < maxbig; q += NUM_TPB) bcur[s * maxbig + q] = 0;   // k_label_scatter's cursors
     const long base = (long)s * N;
     const int nq = (n + SCAN_V - 1) / SCAN_V;
     // whole flag bytes with two 16-byte loads (the sensor's slice starts 32-byte aligned when N % 8 == 0)
@@ -359,9 +363,10 @@ __device__ void priv_slots(const int (&key)[4], int s0, int* __restrict__ hist, 
 
 // pixels of every large label into its slice of the grouped list (order inside a slice is free: the
 // moments are exact integer sums and the first pixel is a minimum)
+// also clears the label -> model map k_plane_fit fills (its storage, root, is dead after k_ccl_label)
 __global__ void __launch_bounds__(PS_TPB) k_label_scatter(const int* __restrict__ lab, int N, const int* __restrict__ bmap,
                                                           const int* __restrict__ boff, int* __restrict__ bcur,
-                                                          int* __restrict__ blist) {
+                                                          int* __restrict__ blist, int* __restrict__ mmap) {
     __shared__ int hist[2 * R360_MAX_BIG], base[2 * R360_MAX_BIG];
     const long total = 8L * N, b0 = (long)blockIdx.x * PS_PX;
     const int s0 = (int)(b0 / N);
@@ -371,6 +376,7 @@ __global__ void __launch_bounds__(PS_TPB) k_label_scatter(const int* __restrict_
         const long i = b0 + k * PS_TPB + threadIdx.x;
         key[k] = -1; j[k] = 0; s[k] = 0;
         if (i < total) {
+            mmap[i] = -1;
             s[k] = (int)(i / N);
             j[k] = (int)(i - (long)s[k] * N);
             const int L = lab[i];
@@ -551,11 +557,17 @@ constexpr int PF_TPB = 256;
 __global__ void __launch_bounds__(PF_TPB) k_plane_fit(const r360p::Moments* __restrict__ mom, const int* __restrict__ big,
                                                      const int* __restrict__ nbig, int maxbig, float max_curvature,
                                                      PlaneModel* __restrict__ models, int* __restrict__ nmodels,
-                                                     int* __restrict__ err, int N, int* __restrict__ mmap) {
+                                                     int* __restrict__ err, int N, int* __restrict__ mmap,
+                                                     int* __restrict__ mcnt) {
     __shared__ float s_c[R360_MAX_BIG][4], s_pp[R360_MAX_BIG][4], s_vp[R360_MAX_BIG][4];
     __shared__ float s_curv[R360_MAX_BIG];
     __shared__ int s_idx[R360_MAX_BIG];
     const int s = blockIdx.x;
+    // the model counts and cursors of k_model_count / k_model_scatter ([8][MAX_MODELS] each)
+    for (int q = threadIdx.x; q < R360_MAX_MODELS; q += PF_TPB) {
+        mcnt[s * R360_MAX_MODELS + q] = 0;
+        mcnt[(8 + s) * R360_MAX_MODELS + q] = 0;
+    }
     const int nb = min(nbig[s], maxbig);
     for (int b = threadIdx.x; b < nb; b += PF_TPB) {
         const r360p::Moments m = mom[s * maxbig + b];
@@ -2194,10 +2206,9 @@ int launch_segmentation(r360_frame* f) {
             hipLaunchKernelGGL(k_ccl_border, dim3((unsigned)((edges + 255) / 256)), dim3(256), 0, st, P.cloud, P.nrm, w,
                                h, ang_thr, P.parent);
     }
-    hipLaunchKernelGGL(k_ccl_flatten, dim3(blocks), dim3(256), 0, st, P.parent, total, P.root);
+    hipLaunchKernelGGL(k_ccl_flatten, dim3(blocks), dim3(256), 0, st, P.parent, total, P.root, P.cnt);
     if ((N + SCAN_V - 1) / SCAN_V > NUM_MAXQ) { r360_set_error("segmentation: sensor of %d points too large", N); return -1; }
     hipLaunchKernelGGL(k_ccl_number, dim3(8), dim3(NUM_TPB), 0, st, P.root, N, P.parent, P.nlab);
-    R360_HIP(hipMemsetAsync(P.cnt, 0, sizeof(int) * total, st));
     hipLaunchKernelGGL(k_ccl_label, dim3(blocks), dim3(256), 0, st, P.root, P.parent, N, P.lab, P.cnt);
     timing_end(ctx, slot);
     R360_HIP(hipGetLastError());
@@ -2212,16 +2223,14 @@ int launch_segmentation(r360_frame* f) {
     int* bmap = P.parent;
     int* mmap = P.root;
     hipLaunchKernelGGL(k_big_list, dim3(8), dim3(1024), 0, st, P.cnt, P.nlab, N, 80, P.big, P.nbig, R360_MAX_BIG, P.err,
-                       bmap, boff, P.mom, bfirst);
-    R360_HIP(hipMemsetAsync(bcur, 0, sizeof(int) * 8 * R360_MAX_BIG, st));
+                       bmap, boff, P.mom, bfirst, bcur);
     if (N < PS_PX) { r360_set_error("segmentation: sensor of %d points too small", N); return -1; }
     const int pblocks = (int)((total + PS_PX - 1) / PS_PX);
-    hipLaunchKernelGGL(k_label_scatter, dim3(pblocks), dim3(PS_TPB), 0, st, P.lab, N, bmap, boff, bcur, P.blist);
+    hipLaunchKernelGGL(k_label_scatter, dim3(pblocks), dim3(PS_TPB), 0, st, P.lab, N, bmap, boff, bcur, P.blist, mmap);
     hipLaunchKernelGGL(k_label_moments, dim3(LMOM_GX, 8, LMOM_SPLIT), dim3(LMOM_TPB), 0, st, P.cloud, P.cnt, N, P.big, P.nbig,
                        R360_MAX_BIG, boff, P.blist, P.mom, bfirst);
-    R360_HIP(hipMemsetAsync(mmap, 0xff, sizeof(int) * total, st));
     hipLaunchKernelGGL(k_plane_fit, dim3(8), dim3(PF_TPB), 0, st, P.mom, P.big, P.nbig, R360_MAX_BIG, 0.001f, P.models,
-                       P.nmodels, P.err, N, mmap);
+                       P.nmodels, P.err, N, mmap, mcnt);
     timing_end(ctx, slot);
     R360_HIP(hipGetLastError());
     slot = timing_begin(ctx, "k_refine");
@@ -2234,7 +2243,6 @@ int launch_segmentation(r360_frame* f) {
     timing_end(ctx, slot);
     R360_HIP(hipGetLastError());
     slot = timing_begin(ctx, "k_model_stats");
-    R360_HIP(hipMemsetAsync(mcnt, 0, sizeof(int) * 16 * R360_MAX_MODELS, st));
     hipLaunchKernelGGL(k_model_count, dim3(pblocks), dim3(PS_TPB), 0, st, P.labf, N, mmap, mcnt, P.out);
     hipLaunchKernelGGL(k_model_scatter, dim3(pblocks), dim3(PS_TPB), 0, st, P.labf, N, mmap, mcnt, mcur, P.mlist);
     hipLaunchKernelGGL(k_model_stats, dim3(16, 8, MS_SPLIT), dim3(MS_TPB), 0, st, P.cloud, P.rgb, N, P.models,
@@ -2262,6 +2270,32 @@ int launch_segmentation(r360_frame* f) {
     hipLaunchKernelGGL(k_vox_compact, dim3(VOXC_BLOCKS), dim3(VOXC_TPB), 0, st, ctx->d_vhash, P.totals, P.out, P.vox,
                        P.vox_cap);
     timing_end(ctx, slot);
+    R360_HIP(hipGetLastError());
+    return 0;
+}
+
+namespace {
+// the plane stage's outputs for the host assembly, written straight into pinned host memory (one launch
+// instead of four device-to-host copies): the region records, models per sensor, error word, totals
+__global__ void k_plane_publish(const PlaneOut* __restrict__ out, const int* __restrict__ nmodels,
+                                const int* __restrict__ err, const long* __restrict__ totals, PlaneOut* __restrict__ h_out,
+                                int* __restrict__ h_nm, int nwords) {
+    const int* src = reinterpret_cast<const int*>(out);
+    int* dst = reinterpret_cast<int*>(h_out);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nwords; i += gridDim.x * blockDim.x) dst[i] = src[i];
+    if (blockIdx.x == 0 && threadIdx.x < 14 && threadIdx.x != 9) {
+        const int t = threadIdx.x;
+        h_nm[t] = t < 8 ? nmodels[t] : t == 8 ? *err : reinterpret_cast<const int*>(totals)[t - 10];
+    }
+}
+}  // namespace
+
+int launch_plane_publish(r360_frame* f) {
+    PlaneBufs& P = f->pl;
+    static_assert(sizeof(PlaneOut) % 4 == 0, "PlaneOut is copied as 32-bit words");
+    const int nwords = (int)(sizeof(PlaneOut) * 8 * R360_MAX_MODELS / 4);
+    hipLaunchKernelGGL(k_plane_publish, dim3((nwords + 255) / 256), dim3(256), 0, f->ctx->stream, P.out, P.nmodels, P.err,
+                       P.totals, P.h_out, P.h_nmodels, nwords);
     R360_HIP(hipGetLastError());
     return 0;
 }

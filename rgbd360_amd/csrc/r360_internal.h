@@ -395,6 +395,7 @@ int ensure_batch(r360_ctx* ctx, int n, long n_pixels);
 int ctx_wait_frames(r360_ctx* ctx, r360_frame* const* frames, int n);
 int launch_cloud_normals(r360_frame* f);
 int launch_segmentation(r360_frame* f);
+int launch_plane_publish(r360_frame* f);   // plane outputs -> pinned host buffers (h_out, h_nmodels)
 int plane_bufs_alloc(r360_frame* f);
 void plane_bufs_free(r360_frame* f);
 int planes_enqueue(r360_frame* f);
