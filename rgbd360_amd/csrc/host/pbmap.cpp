@@ -646,10 +646,8 @@ int gpu_tables(r360_ctx* ctx, const std::vector<HPlane>& S, const std::vector<in
     for (int j = 0; j < nt; ++j) pack_desc(T[ti[j]], &desc[16 * (ns + j)]);
     hipStream_t st = ctx->stream;
     R360_HIP(hipMemcpyAsync(ctx->d_match_desc, desc.data(), sizeof(float) * desc.size(), hipMemcpyHostToDevice, st));
-    if (launch_match_tables(ctx, ctx->d_match_desc, ns, nt, mode, ctx->d_unary, ctx->d_bin, tb.words)) return -1;
-    R360_HIP(hipMemcpyAsync(ctx->h_unary, ctx->d_unary, (size_t)ns * nt, hipMemcpyDeviceToHost, st));
-    R360_HIP(hipMemcpyAsync(ctx->h_bin, ctx->d_bin, sizeof(unsigned long long) * (size_t)ns * nt * tb.words,
-                            hipMemcpyDeviceToHost, st));
+    // the kernel writes the tables straight into the pinned host buffers (no device-to-host copies)
+    if (launch_match_tables(ctx, ctx->d_match_desc, ns, nt, mode, ctx->h_unary, ctx->h_bin, tb.words)) return -1;
     if (ctx_wait(ctx)) return -1;
     return 0;
 }
