@@ -193,9 +193,15 @@ __global__ void __launch_bounds__(BIL_COLS) k_bil_splat(const float4* __restrict
     const int y0 = max(0, 10 * (sy - 2) - 6), y1 = min(h - 1, 10 * (sy - 2) + 6);
     for (int x = x0; x <= x1; ++x) {
         if ((long)(unsigned long)((float)x / sigma_s + 0.5f) + 2 != sx) continue;
-        for (int y = y0; y <= y1; ++y) {
-            if ((long)(unsigned long)((float)y / sigma_s + 0.5f) + 2 != sy) continue;
-            float Z = cloud[(long)y * w + x].z;
+        // the column's depths of this x, all loads in flight before the ordered accumulation (y1 - y0 <= 12)
+        float zr[13];
+#pragma unroll
+        for (int k = 0; k < 13; ++k) zr[k] = y0 + k <= y1 ? cloud[(long)(y0 + k) * w + x].z : 0.f;
+#pragma unroll
+        for (int k = 0; k < 13; ++k) {
+            const int y = y0 + k;
+            if (y > y1 || (long)(unsigned long)((float)y / sigma_s + 0.5f) + 2 != sy) continue;
+            float Z = zr[k];
             if (!isfin(Z)) Z = bmax;                           // NaN depths take the range maximum
             const float z = Z - bmin;
             const long sz = (long)(unsigned long)(z / sigma_r + 0.5f) + 2;
