@@ -335,7 +335,6 @@ __global__ void __launch_bounds__(DM_TPB) k_distmap(const float* __restrict__ in
     const int base = R1 - 1;                       // LDS row 0 = image row R1-1
     const int nrows = R2 - base + 1;
     float* tmp = sm + (long)nrows * w;
-    float* tmp2 = tmp + w;                         // the chain's results before they replace the row
     auto L = [&](int row) { return sm + (long)(row - base) * w; };
     for (int k = threadIdx.x; k < nrows * w; k += blockDim.x) sm[k] = I[(long)base * w + k];
     dm_sync();
@@ -349,14 +348,13 @@ __global__ void __launch_bounds__(DM_TPB) k_distmap(const float* __restrict__ in
             tmp[c] = fminf(cur[c], m);
         }
         dm_sync();
+        // the chain reads tmp (and cur[0], never updated), so its results go straight into the row
         for (int c = 1 + threadIdx.x; c < w; c += blockDim.x) {
             const int k0 = c - 10 > 1 ? c - 10 : 1;
             float v = (k0 == 1) ? cur[0] : 1e30f;          // chain start (cur[0] is never updated)
             for (int k = k0; k <= c; ++k) v = fminf(tmp[k], v + 1.0f);
-            tmp2[c] = v;
+            cur[c] = v;
         }
-        dm_sync();
-        for (int c = 1 + threadIdx.x; c < w; c += blockDim.x) cur[c] = tmp2[c];
         dm_sync();
     }
     // backward pass rows Rb..r0
@@ -372,12 +370,10 @@ __global__ void __launch_bounds__(DM_TPB) k_distmap(const float* __restrict__ in
         dm_sync();
         for (int c = threadIdx.x; c <= w - 2; c += blockDim.x) {
             const int k0 = c + 10 < w - 2 ? c + 10 : w - 2;
-            float v = (k0 == w - 2) ? cur[w - 1] : 1e30f;
+            float v = (k0 == w - 2) ? cur[w - 1] : 1e30f;   // cur[w-1] is never updated
             for (int k = k0; k >= c; --k) v = fminf(tmp[k], v + 1.0f);
-            tmp2[c] = v;
+            cur[c] = v;
         }
-        dm_sync();
-        for (int c = threadIdx.x; c <= w - 2; c += blockDim.x) cur[c] = tmp2[c];
         dm_sync();
     }
     const int rend = min(h, r0 + DM_BAND);
