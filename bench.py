@@ -219,7 +219,7 @@ def main():
     ap.add_argument("--iters0", type=int, default=20)
     ap.add_argument("--frames", type=int, default=256, help="sequence length (frames)")
     ap.add_argument("--workload", choices=["sequence", "dense", "planes"], default="sequence")
-    ap.add_argument("--streams", type=int, default=12, help="max pipelines per GPU (host thread + HIP stream each)")
+    ap.add_argument("--streams", type=int, default=8, help="max pipelines per GPU (host thread + HIP stream each)")
     ap.add_argument("--min-run", type=int, default=8,
                     help="min pairs per pipeline run (each run rebuilds a halo frame; 8 beat 4 and 16 on 1/4- and 1/8-size shards)")
     ap.add_argument("--stage-timing", action="store_true",
@@ -227,7 +227,7 @@ def main():
     ap.add_argument("--queue", type=int, default=16,
                     help="dense queue batch size (alignFrames360 of up to N pairs per launch); 0 = one launch per pair "
                          "on each pipeline's stream")
-    ap.add_argument("--depth", type=int, default=2,
+    ap.add_argument("--depth", type=int, default=3,
                     help="dense queue: alignments in flight per pipeline (each needs one more Frame360 buffer)")
     ap.add_argument("--emulate", type=str, default=None,
                     help="RANK/WORLD: run that rank's shard alone (single-GPU rehearsal of an N-GPU shard)")
