@@ -212,6 +212,38 @@ __global__ void k_gradient(const float2* __restrict__ p0, int R, int C, float4* 
     }
 }
 
+// all sphere levels' gradients in one launch (the levels are independent once the pyramid is built): block b
+// belongs to the level l with blk0[l] <= b < blk0[l + 1], one pixel per thread
+struct GradLevels {
+    const float2* p0[R360_MAX_PYR];
+    float4* tg[R360_MAX_PYR];
+    int rows[R360_MAX_PYR], cols[R360_MAX_PYR];
+    int blk0[R360_MAX_PYR + 1];
+    int nl;
+};
+
+__global__ void k_gradient_levels(GradLevels G) {
+    int l = 0;
+    while (l + 1 < G.nl && (int)blockIdx.x >= G.blk0[l + 1]) ++l;
+    const int R = G.rows[l], C = G.cols[l];
+    const long i = (long)(blockIdx.x - G.blk0[l]) * blockDim.x + threadIdx.x;
+    if (i >= (long)R * C) return;
+    const float2* p0 = G.p0[l];
+    const int ws = C / 8;
+    const int r = (int)(i / C), c = (int)(i - (long)r * C);
+    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int m = c % ws;   // seam columns as k_gradient (alignFrames360 :4538-4549)
+    const bool seam = (c >= ws - 1) && (c < 7 * ws + 1) && (m == 0 || m == ws - 1);
+    if (!seam && r >= 1 && r < R - 1 && c >= 1 && c < C - 1) {
+        const float2 f = p0[i], fl = p0[i - 1], fr = p0[i + 1], fu = p0[i - C], fd = p0[i + C];
+        o.x = harm(fl.x, f.x, fr.x);
+        o.y = harm(fu.x, f.x, fd.x);
+        o.z = harm(fl.y, f.y, fr.y);
+        o.w = harm(fu.y, f.y, fd.y);
+    }
+    G.tg[l][i] = o;
+}
+
 // setSourceFrame / setTargetFrame level 0 of each sensor's raw images (:480-516): CV_RGB2GRAY on the
 // BGR-stored data /255, and the u16 depth * 0.001 (buildPyramidRange :316-317)
 __global__ void k_sensor_level0(const uint8_t* __restrict__ bgr8, const uint16_t* __restrict__ depth8, long n,
@@ -375,10 +407,17 @@ int launch_pyramid(r360_frame* f) {
         hipLaunchKernelGGL(k_pyramid, dim3(grid_for(n)), dim3(TPB), 0, f->ctx->stream, f->lv[l - 1].p0,
                            f->lv[l - 1].rows, f->lv[l - 1].cols, f->lv[l].p0, min_d, max_d, 1);
     }
-    for (int l = 0; l < f->n_levels; ++l) {
-        const long n = (long)f->lv[l].rows * f->lv[l].cols;
-        hipLaunchKernelGGL(k_gradient, dim3(grid_for(n)), dim3(TPB), 0, f->ctx->stream, f->lv[l].p0, f->lv[l].rows,
-                           f->lv[l].cols, f->lv[l].tg, 1, 1);
+    {
+        GradLevels GL{};
+        GL.nl = f->n_levels;
+        for (int l = 0; l < f->n_levels; ++l) {
+            GL.p0[l] = f->lv[l].p0;
+            GL.tg[l] = f->lv[l].tg;
+            GL.rows[l] = f->lv[l].rows;
+            GL.cols[l] = f->lv[l].cols;
+            GL.blk0[l + 1] = GL.blk0[l] + (int)(((long)f->lv[l].rows * f->lv[l].cols + TPB - 1) / TPB);
+        }
+        hipLaunchKernelGGL(k_gradient_levels, dim3(GL.blk0[f->n_levels]), dim3(TPB), 0, f->ctx->stream, GL);
     }
     SrcGrid G{};
     G.nl = f->n_levels;
