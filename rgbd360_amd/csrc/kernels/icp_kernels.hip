@@ -722,7 +722,12 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
                 qn += __popcll(m);
             }
         };
-        const int b0 = __builtin_amdgcn_readfirstlane((blockIdx.x * TPB + (threadIdx.x & ~63)));
+        // XCD-aware stream order: workgroups are dispatched round-robin over the 8 XCDs, so with nb % 8 == 0
+        // workgroup x runs on XCD x % 8; give each XCD one contiguous nb/8-workgroup slice of every stride
+        // period, so a neighbourhood of the target's rows is gathered through one L2 instead of eight
+        const int nbx = (int)gridDim.x;
+        const int bx = (nbx & 7) ? (int)blockIdx.x : ((int)blockIdx.x & 7) * (nbx >> 3) + ((int)blockIdx.x >> 3);
+        const int b0 = __builtin_amdgcn_readfirstlane((bx * TPB + (threadIdx.x & ~63)));
         if (b0 < nv) {
             const int n_it = (nv - 1 - b0) / stride + 1;
             auto base = [&](int k) { return b0 + (k < n_it ? k : n_it - 1) * stride; };
