@@ -36,6 +36,7 @@ struct r360_dense_queue {
         int reg = 0, good = 0;                   // Register(): PbMap outcome and information
         float info[36];
         int done = 0, rc = 0;
+        bool claimed = false;                    // a collector waits on it (a second one is refused)
         std::string err;
         float pose[16], H[36], g[6];
         r360_icp_stats st{};
@@ -50,8 +51,12 @@ struct r360_dense_queue {
     int max_seen = 0;
 };
 
+// One batch = one method, one parameter set and one sphere geometry (r360_align360_batch_async rejects a
+// batch whose frames differ in size, which would fail every job of it)
 static bool same_params(const r360_dense_queue::Job& a, const r360_dense_queue::Job& b) {
-    return a.method == b.method && memcmp(&a.p, &b.p, sizeof(r360_icp_params)) == 0;
+    return a.method == b.method && memcmp(&a.p, &b.p, sizeof(r360_icp_params)) == 0 &&
+           a.src->sph_rows == b.src->sph_rows && a.src->sph_cols == b.src->sph_cols &&
+           a.src->n_levels == b.src->n_levels && a.trg->n_levels == b.trg->n_levels;
 }
 
 static void dispatcher(r360_dense_queue* q) {
@@ -209,13 +214,21 @@ static int queue_submit(r360_dense_queue* q, r360_frame* trg, r360_frame* src, c
     return 0;
 }
 
-// waits for job t and removes it; returns its rc (0, 1 = ILL-POSED, < 0 error)
-static int queue_collect(r360_dense_queue* q, long t, r360_dense_queue::Job& out) {
+// waits for job t and removes it; returns its rc (0, 1 = ILL-POSED, < 0 error).  want_reg: 1 = only a
+// Register() ticket, 0 = only a plain alignment ticket, -1 = either; a ticket of the other kind is left in
+// the queue for the right collector.  The ticket is claimed under the lock, so a second collector of the
+// same ticket is refused instead of waiting on a job the first one erases.
+static int queue_collect(r360_dense_queue* q, long t, r360_dense_queue::Job& out, int want_reg = -1) {
     CHECK_ARG(q, "null queue");
     std::unique_lock<std::mutex> lk(q->m);
     auto it = q->jobs.find(t);
     CHECK_ARG(it != q->jobs.end(), "unknown or already collected ticket");
-    q->cv_done.wait(lk, [&] { return it->second.done != 0; });
+    CHECK_ARG(!it->second.claimed, "ticket is being collected by another thread");
+    CHECK_ARG(want_reg < 0 || (it->second.reg != 0) == (want_reg != 0),
+              want_reg ? "ticket is not a Register() job (r360_dense_queue_collect)"
+                       : "ticket is a Register() job (r360_register_collect)");
+    it->second.claimed = true;
+    q->cv_done.wait(lk, [&] { return it->second.done != 0; });   // std::map nodes stay put while others erase
     out = it->second;
     q->jobs.erase(it);
     lk.unlock();
@@ -231,7 +244,7 @@ extern "C" int r360_dense_queue_submit(r360_dense_queue* q, r360_frame* trg, r36
 extern "C" int r360_dense_queue_collect(r360_dense_queue* q, long ticket, float pose_out[16], float H_out[36],
                                         float g_out[6], r360_icp_stats* st) {
     r360_dense_queue::Job J;
-    const int rc = queue_collect(q, ticket, J);
+    const int rc = queue_collect(q, ticket, J, 0);
     if (rc < 0) return rc;
     if (pose_out) memcpy(pose_out, J.pose, sizeof J.pose);
     if (H_out) memcpy(H_out, J.H, sizeof J.H);
@@ -263,9 +276,8 @@ extern "C" int r360_register_collect(r360_dense_queue* q, long ticket, float pos
                                      r360_icp_stats* st) {
     CHECK_ARG(pose, "null pose");
     r360_dense_queue::Job J;
-    const int rc = queue_collect(q, ticket, J);
+    const int rc = queue_collect(q, ticket, J, 1);
     if (rc < 0) return rc;
-    CHECK_ARG(J.reg, "ticket is not a Register() job (r360_dense_queue_collect)");
     float Ro[16], Ri[16], t2[16];
     r360_rot_offset(Ro, Ri);
     r360_mul4(Ri, J.pose, t2);

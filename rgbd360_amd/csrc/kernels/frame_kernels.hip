@@ -193,14 +193,14 @@ __device__ __forceinline__ float harm(float fl, float f, float fr) {
 __global__ void k_gradient(const float2* __restrict__ p0, int R, int C, float4* __restrict__ tg, int nimg,
                            int mask_seams) {
     const long per = (long)R * C, n = per * nimg;
-    const int ws = C / 8;
+    const int ws = C / 8;   // >= 1: calib_build_tables stops the pyramid before a level narrower than 8
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
         const long li = i % per;
         const int r = (int)(li / C), c = (int)(li - (long)r * C);
         float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
         // seam columns s*ws-1 and s*ws, s = 1..7, are zeroed by alignFrames360 (:4538-4549)
-        const int m = c % ws;
-        const bool seam = mask_seams && (c >= ws - 1) && (c < 7 * ws + 1) && (m == 0 || m == ws - 1);
+        const int m = ws > 0 ? c % ws : 1;
+        const bool seam = mask_seams && ws > 0 && (c >= ws - 1) && (c < 7 * ws + 1) && (m == 0 || m == ws - 1);
         if (!seam && r >= 1 && r < R - 1 && c >= 1 && c < C - 1) {
             const float2 f = p0[i], fl = p0[i - 1], fr = p0[i + 1], fu = p0[i - C], fd = p0[i + C];
             o.x = harm(fl.x, f.x, fr.x);
@@ -229,11 +229,11 @@ __global__ void k_gradient_levels(GradLevels G) {
     const long i = (long)(blockIdx.x - G.blk0[l]) * blockDim.x + threadIdx.x;
     if (i >= (long)R * C) return;
     const float2* p0 = G.p0[l];
-    const int ws = C / 8;
+    const int ws = C / 8;   // >= 1: calib_build_tables stops the pyramid before a level narrower than 8
     const int r = (int)(i / C), c = (int)(i - (long)r * C);
     float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
-    const int m = c % ws;   // seam columns as k_gradient (alignFrames360 :4538-4549)
-    const bool seam = (c >= ws - 1) && (c < 7 * ws + 1) && (m == 0 || m == ws - 1);
+    const int m = ws > 0 ? c % ws : 1;   // seam columns as k_gradient (alignFrames360 :4538-4549)
+    const bool seam = ws > 0 && (c >= ws - 1) && (c < 7 * ws + 1) && (m == 0 || m == ws - 1);
     if (!seam && r >= 1 && r < R - 1 && c >= 1 && c < C - 1) {
         const float2 f = p0[i], fl = p0[i - 1], fr = p0[i + 1], fu = p0[i - C], fd = p0[i + C];
         o.x = harm(fl.x, f.x, fr.x);

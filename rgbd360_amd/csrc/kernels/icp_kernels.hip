@@ -83,6 +83,14 @@ struct Proj {
 // divisions in atan2 plus the float rounding of theta + pi); coarser levels scale them down.
 constexpr float kGuardRow = 6e-4f, kGuardCol = 1.5e-3f;
 
+// What asinf_fast_view returns for |x| >= 0.53 (|phi| >= 32 deg): 1 (a row outside the image) when the
+// sphere's half-height nRows * pi / nCols stays below 0.55 rad (the stitched sphere's 30 deg, at every
+// pyramid level), NaN otherwise (a taller r360_calib_create_sphere sphere: the lane is deferred to the
+// exact projection).
+__device__ __forceinline__ float asin_out_for(int nRows, int nCols) {
+    return (float)nRows * 3.14159265f < 0.55f * (float)nCols ? 1.0f : __builtin_nanf("");
+}
+
 // round() + int conversion + the (:2989) bounds test, on the float values so NaN and out-of-range
 // projections are rejected exactly as the x86 reference's (int) conversion does.
 __device__ __forceinline__ void set_pixel(Proj& o, float rr, float cc, bool valid, int nRows, int nCols) {
@@ -177,7 +185,7 @@ __device__ __forceinline__ Proj project_exact(const Pose12& P, const Lut3& l, fl
 // (= roundf away from the .5 boundaries, which are all inside the guard bands) that shares its
 // floor with the guard test.  A lane inside a guard band, or NaN, is flagged in o.fix.
 __device__ __forceinline__ Proj project_fast(const Pose12& P, const Lut3& l, float gray_s, int nRows, int nCols,
-                                             float angle_res_inv) {
+                                             float angle_res_inv, float asin_out) {
     Proj o;
     // p' and |p'| exactly as the reference (they enter the error terms, which steer the GN decisions)
     float X = P.R[0] * l.x + P.R[1] * l.y + P.R[2] * l.z; X = X + P.t[0];
@@ -185,7 +193,7 @@ __device__ __forceinline__ Proj project_fast(const Pose12& P, const Lut3& l, flo
     float Z = P.R[6] * l.x + P.R[7] * l.y + P.R[8] * l.z; Z = Z + P.t[2];
     const float d2 = X * X + Y * Y + Z * Z;
     const float dist_inv = __builtin_amdgcn_rsqf(d2);
-    const float phi_trg = r360m::asinf_fast_view(X * dist_inv);
+    const float phi_trg = r360m::asinf_fast_view(X * dist_inv, asin_out);
     const float theta_trg = r360m::atan2f_fast1(Y, Z) + 3.14159265358979f;
     // u = rr + 0.5, v = cc + 0.5 (half_nRows + 0.5 = nRows / 2 exactly)
     const float u = fmaf(-phi_trg, angle_res_inv, 0.5f * (float)nRows);
@@ -495,6 +503,7 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
     const float angle_res = (float)(2 * R360_PI / nCols);
     const float angle_res_inv = 1 / angle_res;
     const float half_nRows = (float)(0.5 * nRows - 0.5);
+    const float asin_out = asin_out_for(nRows, nCols);
 
     Acc A;
 #pragma unroll
@@ -624,7 +633,7 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
         const Gather gt{__builtin_amdgcn_make_buffer_rsrc(const_cast<float4*>(tg), 0, npx * 16, 0x00020000),
                         __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(trg), 0, npx * 8, 0x00020000)};
         auto prj = [&](const Src& x) {
-            return project_fast(P, lut_point(x.d, x.sp, x.cp, x.st, x.ct, C), x.g, nRows, nCols, angle_res_inv);
+            return project_fast(P, lut_point(x.d, x.sp, x.cp, x.st, x.ct, C), x.g, nRows, nCols, angle_res_inv, asin_out);
         };
         // queue the flagged lanes of a chunk and take them out of it
         auto defer = [&](Proj& o, int& fl, int base) {
@@ -711,7 +720,7 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
                                    __uint_as_float(v[3])), base + lane < nv};
         };
         auto prj = [&](const Src& x) {
-            return project_fast(P, Lut3{x.p.x, x.p.y, x.p.z, x.valid}, x.p.w, nRows, nCols, angle_res_inv);
+            return project_fast(P, Lut3{x.p.x, x.p.y, x.p.z, x.valid}, x.p.w, nRows, nCols, angle_res_inv, asin_out);
         };
         auto defer = [&](Proj& o, int base) {
             const unsigned long long m = __ballot(o.fix);
@@ -1156,7 +1165,7 @@ __global__ void k_proj_check(const float* __restrict__ X, const float* __restric
         Lut3 l;
         l.x = X[i]; l.y = Y[i]; l.z = Z[i]; l.valid = true;
         const Proj e = project_exact(P, l, 0.f, nRows, nCols, half_nRows, angle_res_inv);
-        Proj f = project_fast(P, l, 0.f, nRows, nCols, angle_res_inv);
+        Proj f = project_fast(P, l, 0.f, nRows, nCols, angle_res_inv, asin_out_for(nRows, nCols));
         if (f.fix) { f = e; ++fb; }
         const bool same = f.vis == e.vis && f.t == e.t;
         mism += same ? 0 : 1;

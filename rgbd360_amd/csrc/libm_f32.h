@@ -221,17 +221,19 @@ __device__ __forceinline__ float asinf_fast(float x) {
     return x > 0 ? r : -r;
 }
 
-// asin for the spherical projection's row decision only: the sphere spans |phi| <= 30 deg (H = W / 6,
-// Frame360.h:391-392), so |x| >= 0.53 (|phi| >= 32 deg) always projects outside the image, at every
-// pyramid level (>= 1.3 rows beyond the border).  There the result is a constant that projects outside
-// as well; below it the |x| < 0.5 polynomial of asinf (accurate to 1 ulp up to 0.53), with contraction.
-__device__ __forceinline__ float asinf_fast_view(float x) {
+// asin for the spherical projection's row decision only: below |x| = 0.53 the |x| < 0.5 polynomial of
+// asinf (accurate to 1 ulp up to 0.53), with contraction; at and above it the caller's `out`.  The
+// stitched sphere spans |phi| <= 30 deg (H = W / 6, Frame360.h:391-392), so there |x| >= 0.53 (|phi| >= 32
+// deg) always projects outside the image at every pyramid level and out = 1 (a row outside as well) is
+// exact in effect.  A taller sphere (r360_calib_create_sphere with H > 0.175 W) passes out = NaN: those
+// lanes are flagged by the guard test and re-projected exactly (project_exact).
+__device__ __forceinline__ float asinf_fast_view(float x, float out = 1.0f) {
 #pragma clang fp contract(fast)
     const float p0 = 1.666675248e-1f, p1 = 7.495297643e-2f, p2 = 4.547037598e-2f, p3 = 2.417951451e-2f,
                 p4 = 4.216630880e-2f;
     const float t = x * x;
     const float r = x + x * (t * (p0 + t * (p1 + t * (p2 + t * (p3 + t * p4)))));
-    return fabs_(x) < 0.53f ? r : __builtin_copysignf(1.0f, x);
+    return fabs_(x) < 0.53f ? r : __builtin_copysignf(out, x);
 }
 
 // atan2 with a two-way argument reduction (|t| <= tan(pi/8) < 7/16, fdlibm's polynomial domain):
