@@ -209,6 +209,78 @@ def cpu_baseline(cal, frames_of, first, last, workload, iters0, budget_s=10.0):
                       "thread count; value = the faster run"}
 
 
+def config5_leg(device, rt8, pairs=48, iters0=50, pipelines=8, depth=2, repeats=3):
+    """BASELINE configs[4], the HBM stress case, as a secondary block of the default line: the dense stage
+    (upload, stitch + 5-level pyramid, alignFrames360(PHOTO_DEPTH) with the reference schedule on levels 4..1
+    and exactly `iters0` GN iterations at level 0) over `pairs` consecutive pairs of the synthetic sequence at
+    8 x 1280x960 (1280 x 7680 sphere), batched like the headline run (pipelines x depth alignments in flight on
+    the dense queue).  Its level-0 working set (~268 MB per pair-pass) exceeds the 256 MB Infinity Cache, so
+    this is the one configuration whose roofline is an HBM roofline."""
+    import rgbd360_amd as R
+    from rgbd360_amd import odometry as OD
+    rows, cols = 960, 1280
+    t_gen = time.perf_counter()
+    nf = pairs + 1
+    BGR = np.zeros((nf, 8, rows, cols, 3), np.uint8)
+    DEP = np.zeros((nf, 8, rows, cols), np.uint16)
+    for j in range(nf):
+        BGR[j], DEP[j] = R.synth_frame_rt(rows, cols, rt8, SEED, R.synth_path_pose(SEED, j))
+    gen_s = time.perf_counter() - t_gen
+    pinned = R.HostPinned(BGR, DEP)
+    params = R.IcpParams.default()
+    params.n_pyr = 5
+    params.std_dev_photo = np.float32(3.0 / 255)
+    params.fixed_iters_level0 = iters0
+    runs = OD.split_range(0, pairs, pipelines)
+    runner = OD.SequenceRunner(device, rows, cols, len(runs), params, planes=False, dense_only=True, queue=16,
+                               depth=depth)
+
+    def frames_of(i):
+        return BGR[i], DEP[i]
+    runner.run(0, pairs, frames_of, np.zeros((1, pairs, OD.REC), np.float32), repeats=1, runs=runs)   # warmup
+    qctx = runner.queue.ctx
+    q0 = runner.queue.stats()
+    qctx.kernel_time_reset()
+    rec = np.zeros((repeats, pairs, OD.REC), np.float32)
+    t0 = time.perf_counter()
+    runner.run(0, pairs, frames_of, rec, repeats=repeats, runs=runs)
+    elapsed = time.perf_counter() - t0
+    us, n, nj = qctx.kernel_stats(0)
+    q1 = runner.queue.stats()
+    runner.close()
+    pinned.close()
+    W0 = rows * 8
+    H0 = int(W0 * 0.5 * 60.0 / 180)
+    N0 = H0 * W0
+    sso = float(np.mean(rec[:, :, OD.R_SSO]))
+    alg = 8.0 * N0 + 24.0 * sso * N0
+    avg_ms = us / max(n, 1) * 1e-3
+    ppl = nj / max(n, 1)
+    ach = ppl * alg / (avg_ms * 1e-3) / 1e9 if n else None
+    # per-pair accuracy against the synthetic ground truth (the dense stage starts from identity)
+    gt = [R.synth_path_pose(SEED, k).astype(np.float64) for k in range(nf)]
+    rot_err = []
+    for i in range(pairs):
+        G = np.linalg.inv(gt[i]) @ gt[i + 1]
+        D = np.linalg.inv(G) @ rec[-1, i, OD.R_POSE:OD.R_POSE + 16].reshape(4, 4).T.astype(np.float64)
+        rot_err.append(float(np.degrees(np.arccos(np.clip((np.trace(D[:3, :3]) - 1) / 2, -1, 1)))))
+    return {
+        "workload": (f"config5: synthetic 8x{cols}x{rows} sequence, {pairs} consecutive pairs x {repeats} repeats; per "
+                     f"pair: upload, stitch + 5-level pyramid, alignFrames360(PHOTO_DEPTH) levels 4..1 reference "
+                     f"schedule + {iters0} GN iterations at level 0 ({len(runs)} pipelines x {depth} in flight, dense "
+                     "queue batches of up to 16 pairs)"),
+        "sphere": f"{H0}x{W0}", "value": pairs * repeats / elapsed, "unit": "pairs/s",
+        "ms_per_pair": elapsed / (pairs * repeats) * 1e3,
+        "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": (ach / HBM_PEAK_GBS) if ach else None, "traffic": None,
+                     "kernel": "k_icp_pass<PHOTO_DEPTH> (level 0)", "avg_launch_ms": avg_ms, "launches": n,
+                     "pairs_per_launch": ppl, "bytes_per_pair_pass": alg, "visible_frac": sso,
+                     "timing": "in-kernel execution span (s_memrealtime) of every level-0 launch of the timed repeats"},
+        "dense_queue": {"batches": q1["batches"] - q0["batches"], "jobs": q1["jobs"] - q0["jobs"]},
+        "max_pair_rot_err_deg": max(rot_err), "frame_generation_s": round(gen_s, 1),
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -233,6 +305,10 @@ def main():
                     help="RANK/WORLD: run that rank's shard alone (single-GPU rehearsal of an N-GPU shard)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-resident", action="store_true", help="skip the HBM-resident-input secondary run")
+    ap.add_argument("--no-config5", action="store_true", help="skip the config-5 (8x1280x960, 50 iterations) leg")
+    ap.add_argument("--no-isolated", action="store_true",
+                    help="skip the lone-pipeline rerun after the timed region (profiling: the trace then holds only "
+                         "the warmup and timed launches)")
     ap.add_argument("--eval-probe", action="store_true", help="diagnostic: also time the level-0 pass in eval mode")
     args = ap.parse_args()
 
@@ -386,7 +462,8 @@ def main():
     for c in ctxs:
         c.kernel_time_reset()
     iso_rec = np.zeros((1, p1 - p0, OD.REC), np.float32)
-    runner.run(p0, p1, frames_of, iso_rec, repeats=1, runs=runs[:1])
+    if not args.no_isolated:
+        runner.run(p0, p1, frames_of, iso_rec, repeats=1, runs=runs[:1])
     us, n, nj = dense_ctx.kernel_stats(0)
     iso_ms = us / max(n, 1) * 1e-3
     iso_ach = (nj / max(n, 1)) * alg_bytes / (iso_ms * 1e-3) / 1e9 if n else None
@@ -480,9 +557,12 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(runner.cals[0], frames_of, p0, p1, args.workload, args.iters0)
     pinned.close()
+    runner.close()
+    if rank == 0 and world == 1 and not args.no_config5 and args.workload == "sequence" and args.rows == 480:
+        del BGR, DEP
+        out["config5"] = config5_leg(local, rt8)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    runner.close()
     if group is not None:
         group.close()
 

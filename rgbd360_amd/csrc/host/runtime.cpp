@@ -437,6 +437,7 @@ extern "C" int r360_frame_create(r360_ctx* ctx, const r360_calib* calib, r360_fr
         R360_HIP(hipMalloc(&f->lv[l].p0, sizeof(float2) * (size_t)R * C));
         R360_HIP(hipMalloc(&f->lv[l].tg, sizeof(float4) * (size_t)R * C));
         R360_HIP(hipMalloc(&f->lv[l].pts, sizeof(float4) * (size_t)R * C));
+        if (l == 0) R360_HIP(hipMalloc(&f->lv[l].pk, sizeof(uint32_t) * (size_t)R * C));
         R /= 2; C /= 2;
     }
     f->src_blocks = (int)((nsph + R360_SRC_BLOCK - 1) / R360_SRC_BLOCK);
@@ -459,7 +460,7 @@ extern "C" void r360_frame_destroy(r360_frame* f) {
     // hipFree synchronises the device; the frame never dereferences its ctx here so frames may
     // outlive their context at interpreter shutdown.
     hipFree(f->d_bgr); hipFree(f->d_depth); hipFree(f->d_depth_m); hipFree(f->d_sph_bgr); hipFree(f->d_sph_depth);
-    for (int l = 0; l < f->n_levels; ++l) { hipFree(f->lv[l].p0); hipFree(f->lv[l].tg); hipFree(f->lv[l].pts); }
+    for (int l = 0; l < f->n_levels; ++l) { hipFree(f->lv[l].p0); hipFree(f->lv[l].tg); hipFree(f->lv[l].pts); hipFree(f->lv[l].pk); }
     hipFree(f->d_npts); hipFree(f->d_src_cnt); hipFree(f->d_src_levels);
     for (int l = 0; l < f->n_slevels; ++l) { hipFree(f->sp[l].p0); hipFree(f->sp[l].tg); }
     plane_bufs_free(f);
@@ -813,6 +814,7 @@ int align360_batch_enqueue(r360_ctx* ctx, int n, r360_frame* const* trg, r360_fr
             IcpJob& J = jobs.j[j];
             J.src = src[j]->lv[l].p0; J.trg = trg[j]->lv[l].p0; J.tg = trg[j]->lv[l].tg;
             J.pts = src[j]->lv[l].pts; J.npts = src[j]->d_npts + l;
+            J.spk = src[j]->lv[l].pk; J.tpk = trg[j]->lv[l].pk;
             J.S = ctx->d_bstate + j;
             J.partials = ctx->d_bpartials + (size_t)j * 32 * ctx->partials_cap;
             J.gcnt = ctx->d_bgticket + (size_t)j * tk;

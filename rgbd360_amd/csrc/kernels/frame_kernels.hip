@@ -50,7 +50,8 @@ __global__ void k_stitch(const uint8_t* __restrict__ bgr8, const uint16_t* __res
                          int H, int W, const float* __restrict__ sinphi, const float* __restrict__ cosphi,
                          const float* __restrict__ sinth, const float* __restrict__ costh,
                          const float* __restrict__ rt_inv, float fx, float fy, float cx, float cy,
-                         uint8_t* __restrict__ sph_bgr, uint16_t* __restrict__ sph_depth, float2* __restrict__ p0) {
+                         uint8_t* __restrict__ sph_bgr, uint16_t* __restrict__ sph_depth, float2* __restrict__ p0,
+                         uint32_t* __restrict__ pk) {
     const long n = (long)H * W;
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
         const int row = (int)(i / W), col = (int)(i - (long)row * W);
@@ -79,6 +80,7 @@ __global__ void k_stitch(const uint8_t* __restrict__ bgr8, const uint16_t* __res
         // setSourceFrame / setTargetFrame level 0: CV_RGB2GRAY on BGR data, /255; depth *0.001
         const int y = (b * 4899 + g * 9617 + r * 1868 + (1 << 13)) >> 14;
         p0[i] = make_float2((float)y * (float)(1. / 255), (float)dd * 0.001f);
+        pk[i] = dd | ((unsigned)y << 16);
     }
 }
 
@@ -89,7 +91,8 @@ __global__ void k_stitch4(const uint8_t* __restrict__ bgr8, const uint16_t* __re
                           int H, int W, const float* __restrict__ sinphi, const float* __restrict__ cosphi,
                           const float* __restrict__ sinth, const float* __restrict__ costh,
                           const float* __restrict__ rt_inv, float fx, float fy, float cx, float cy,
-                          uint8_t* __restrict__ sph_bgr, uint16_t* __restrict__ sph_depth, float2* __restrict__ p0) {
+                          uint8_t* __restrict__ sph_bgr, uint16_t* __restrict__ sph_depth, float2* __restrict__ p0,
+                          uint32_t* __restrict__ pk) {
     const long nq = (long)H * W / 4;
     for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < nq; q += (long)gridDim.x * blockDim.x) {
         const long i0 = 4 * q;
@@ -97,6 +100,7 @@ __global__ void k_stitch4(const uint8_t* __restrict__ bgr8, const uint16_t* __re
         const float v0 = sinphi[row], cos_phi = cosphi[row];
         unsigned char px[12];
         unsigned short dd4[4];
+        unsigned pk4[4];
         float2 o[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -124,6 +128,7 @@ __global__ void k_stitch4(const uint8_t* __restrict__ bgr8, const uint16_t* __re
             dd4[e] = dd;
             const int y = (b * 4899 + g * 9617 + r * 1868 + (1 << 13)) >> 14;
             o[e] = make_float2((float)y * (float)(1. / 255), (float)dd * 0.001f);
+            pk4[e] = dd | ((unsigned)y << 16);
         }
         uint3 wb;
         wb.x = px[0] | (px[1] << 8) | (px[2] << 16) | ((unsigned)px[3] << 24);
@@ -134,6 +139,7 @@ __global__ void k_stitch4(const uint8_t* __restrict__ bgr8, const uint16_t* __re
                                                                  dd4[2] | ((unsigned)dd4[3] << 16));
         *reinterpret_cast<float4*>(p0 + i0) = make_float4(o[0].x, o[0].y, o[1].x, o[1].y);
         *reinterpret_cast<float4*>(p0 + i0 + 2) = make_float4(o[2].x, o[2].y, o[3].x, o[3].y);
+        *reinterpret_cast<uint4*>(pk + i0) = make_uint4(pk4[0], pk4[1], pk4[2], pk4[3]);
     }
 }
 
@@ -246,12 +252,14 @@ __global__ void k_gradient_levels(GradLevels G) {
 
 // setSourceFrame / setTargetFrame level 0 of each sensor's raw images (:480-516): CV_RGB2GRAY on the
 // BGR-stored data /255, and the u16 depth * 0.001 (buildPyramidRange :316-317)
+// pk (optional): the packed level-0 image of the sphere (LevelBufs::pk)
 __global__ void k_sensor_level0(const uint8_t* __restrict__ bgr8, const uint16_t* __restrict__ depth8, long n,
-                                float2* __restrict__ p0) {
+                                float2* __restrict__ p0, uint32_t* __restrict__ pk) {
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
         const int b = bgr8[3 * i], g = bgr8[3 * i + 1], r = bgr8[3 * i + 2];
         const int y = (b * 4899 + g * 9617 + r * 1868 + (1 << 13)) >> 14;
         p0[i] = make_float2((float)y * (float)(1. / 255), (float)depth8[i] * 0.001f);
+        if (pk) pk[i] = depth8[i] | ((unsigned)y << 16);
     }
 }
 
@@ -282,12 +290,12 @@ int launch_stitch(r360_frame* f) {
         hipLaunchKernelGGL(k_stitch4, dim3(grid_for(n / 4)), dim3(TPB), 0, f->ctx->stream, f->d_bgr, f->d_depth,
                            f->rows, f->cols, f->sph_rows, f->sph_cols, c->d_st_sinphi, c->d_st_cosphi, c->d_st_sinth,
                            c->d_st_costh, c->d_rt_inv, c->K[0], c->K[4], c->K[6], c->K[7], f->d_sph_bgr,
-                           f->d_sph_depth, f->lv[0].p0);
+                           f->d_sph_depth, f->lv[0].p0, f->lv[0].pk);
     else
         hipLaunchKernelGGL(k_stitch, dim3(grid_for(n)), dim3(TPB), 0, f->ctx->stream, f->d_bgr, f->d_depth, f->rows,
                            f->cols, f->sph_rows, f->sph_cols, c->d_st_sinphi, c->d_st_cosphi, c->d_st_sinth,
                            c->d_st_costh, c->d_rt_inv, c->K[0], c->K[4], c->K[6], c->K[7], f->d_sph_bgr,
-                           f->d_sph_depth, f->lv[0].p0);
+                           f->d_sph_depth, f->lv[0].p0, f->lv[0].pk);
     timing_end(f->ctx, slot);
     R360_HIP(hipGetLastError());
     return 0;
@@ -394,7 +402,7 @@ int launch_sphere_level0(r360_frame* f) {
     const long n = (long)f->sph_rows * f->sph_cols;
     // cvtColor(CV_RGB2GRAY) / 255 and convertTo(CV_32F, 0.001): the stitch kernel's level-0 expressions
     hipLaunchKernelGGL(k_sensor_level0, dim3(grid_for(n)), dim3(TPB), 0, f->ctx->stream, f->d_sph_bgr, f->d_sph_depth,
-                       n, f->lv[0].p0);
+                       n, f->lv[0].p0, f->lv[0].pk);
     R360_HIP(hipGetLastError());
     return 0;
 }
@@ -451,7 +459,8 @@ int launch_sensor_pyramid(r360_frame* f) {
     }
     hipStream_t st = f->ctx->stream;
     const long n0 = 8L * f->rows * f->cols;
-    hipLaunchKernelGGL(k_sensor_level0, dim3(grid_for(n0)), dim3(TPB), 0, st, f->d_bgr, f->d_depth, n0, f->sp[0].p0);
+    hipLaunchKernelGGL(k_sensor_level0, dim3(grid_for(n0)), dim3(TPB), 0, st, f->d_bgr, f->d_depth, n0, f->sp[0].p0,
+                       (uint32_t*)nullptr);
     for (int l = 1; l < f->n_slevels; ++l) {
         const long n = 8L * f->sp[l].rows * f->sp[l].cols;
         hipLaunchKernelGGL(k_pyramid, dim3(grid_for(n)), dim3(TPB), 0, st, f->sp[l - 1].p0, f->sp[l - 1].rows,

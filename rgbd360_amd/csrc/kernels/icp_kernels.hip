@@ -184,13 +184,24 @@ __device__ __forceinline__ Proj project_exact(const Pose12& P, const Lut3& l, fl
 // (correctly rounded sqrt), then hardware rsq, theta + pi in float, atan2 with one reciprocal, and floor(x + 0.5) rounding
 // (= roundf away from the .5 boundaries, which are all inside the guard bands) that shares its
 // floor with the guard test.  A lane inside a guard band, or NaN, is flagged in o.fix.
+// LEAN (PF 5): p' by three fused multiply-adds per coordinate instead of the reference's six rounded
+// operations (|p'| then differs from the reference's by about an ulp; the projection's guard bands are three
+// orders of magnitude wider than that, and deferred lanes are re-projected from the exact p').
+template <bool LEAN = false>
 __device__ __forceinline__ Proj project_fast(const Pose12& P, const Lut3& l, float gray_s, int nRows, int nCols,
                                              float angle_res_inv, float asin_out) {
     Proj o;
-    // p' and |p'| exactly as the reference (they enter the error terms, which steer the GN decisions)
-    float X = P.R[0] * l.x + P.R[1] * l.y + P.R[2] * l.z; X = X + P.t[0];
-    float Y = P.R[3] * l.x + P.R[4] * l.y + P.R[5] * l.z; Y = Y + P.t[1];
-    float Z = P.R[6] * l.x + P.R[7] * l.y + P.R[8] * l.z; Z = Z + P.t[2];
+    float X, Y, Z;
+    if (LEAN) {
+        X = __builtin_fmaf(P.R[0], l.x, __builtin_fmaf(P.R[1], l.y, __builtin_fmaf(P.R[2], l.z, P.t[0])));
+        Y = __builtin_fmaf(P.R[3], l.x, __builtin_fmaf(P.R[4], l.y, __builtin_fmaf(P.R[5], l.z, P.t[1])));
+        Z = __builtin_fmaf(P.R[6], l.x, __builtin_fmaf(P.R[7], l.y, __builtin_fmaf(P.R[8], l.z, P.t[2])));
+    } else {
+        // p' and |p'| exactly as the reference (they enter the error terms, which steer the GN decisions)
+        X = P.R[0] * l.x + P.R[1] * l.y + P.R[2] * l.z; X = X + P.t[0];
+        Y = P.R[3] * l.x + P.R[4] * l.y + P.R[5] * l.z; Y = Y + P.t[1];
+        Z = P.R[6] * l.x + P.R[7] * l.y + P.R[8] * l.z; Z = Z + P.t[2];
+    }
     const float d2 = X * X + Y * Y + Z * Z;
     const float dist_inv = __builtin_amdgcn_rsqf(d2);
     const float phi_trg = r360m::asinf_fast_view(X * dist_inv, asin_out);
@@ -429,6 +440,82 @@ __device__ __forceinline__ void contribute_fast(Acc& A, WaveCnt& W, const Proj& 
     }
 }
 
+// PF 5's residuals, weights and Jacobian rows (plain pass, OCC 0): contribute_fast with the error terms in
+// fast single precision instead of the reference's exact float / double mix.
+//  * Huber weights without a square root or a division: for |e| >= k, sqrt(2 k |e| - k^2) / |e| = t rsq(t e^2)
+//    with t = 2 k |e| - k^2; the depth weight's 1 / sigma folds into the same reciprocal square root
+//    (w_d = rsq(sigma^2) below sigma, t rsq(t e^2 sigma^2) above).  One hardware rsq per term (~1 ulp)
+//    replaces sqrt_rn + div_rn (photo), div_rn and a wave-wide exact Huber branch (depth).
+//  * Photo residual w e / sigma in float (the reference's double product, :2699-2700, rounds to float anyway).
+//  * The squared residuals are summed per lane in float and in double across lanes and workgroups (~1e-7
+//    relative; the error value's bar is 1e-5).
+// The weights are continuous at |e| = k (both branches give 1), so the comparison needs no guard band.
+template <int METHOD>
+__device__ __forceinline__ void contribute_lean(Acc& A, WaveCnt& W, float& errf, const Proj& o, const float4 G,
+                                                const float2 T, float angle_res_inv, const IcpConst& C) {
+    constexpr bool photo = (METHOD == R360_PHOTO_CONSISTENCY || METHOD == R360_PHOTO_DEPTH);
+    constexpr bool depth = (METHOD == R360_DEPTH_CONSISTENCY || METHOD == R360_PHOTO_DEPTH);
+    const bool sal_p = !(fabsf(G.x) < C.thr_int && fabsf(G.y) < C.thr_int);
+    const bool sal_d = !(fabsf(G.z) < C.thr_depth && fabsf(G.w) < C.thr_depth);
+    const bool fin_d = isfinite(T.y);
+    const bool p_ok = photo && o.vis && sal_p;
+    const bool d_ok = depth && o.vis && (!photo || sal_p) && fin_d && sal_d;   // (:3064-3073)
+    float wp = 0.f, rp = 0.f, wd = 0.f, rd = 0.f;
+    {
+#pragma clang fp contract(fast)
+        if (photo) {
+            const float e = T.x - o.gray_s;
+            const float a = fabsf(e), k = C.sd_photo;
+            const float t = 2.f * k * a - k * k;
+            const float h = a < k ? 1.f : t * __builtin_amdgcn_rsqf(t * a * a);   // weightHuber (:545-554)
+            wp = p_ok ? h * C.sd_photo_inv_f : 0.f;                                 // (:3047)
+            rp = wp * e;
+        }
+        if (depth) {
+            const float e = T.y - o.dist;
+            const float a = fabsf(e), k = C.sd_depth * T.y, k2 = k * k;
+            const float t = 2.f * k * a - k2;
+            const bool in = a < k;
+            const float w = (in ? 1.f : t) * __builtin_amdgcn_rsqf(in ? k2 : t * a * a * k2);   // (:3077-3078)
+            wd = d_ok ? w : 0.f;
+            rd = d_ok ? w * e : 0.f;   // |p'| of a lane without a point can be NaN
+        }
+        errf += rp * rp + rd * rd;
+    }
+    W.c28 += wave_count(o.vis);                                                            // numVisiblePixels
+    W.c27 += (photo ? wave_count(p_ok) : 0) + (depth ? wave_count(d_ok) : 0);
+    const float X = o.vis ? o.X : 1.f, Y = o.vis ? o.Y : 1.f, Z = o.vis ? o.Z : 1.f;
+    const float dist_inv = o.vis ? o.dist_inv : 0.5f;
+    {
+#pragma clang fp contract(fast)
+        // the closed-form Jacobian rows of contribute_fast: row = [u, p' x u], u = J_proj^T [gx gy]^T
+        const float r2 = Y * Y + Z * Z;
+        const float s = __builtin_amdgcn_rcpf(r2) * angle_res_inv;
+        const float t = __builtin_amdgcn_rsqf(r2) * (dist_inv * dist_inv) * angle_res_inv;
+        auto row = [&](float gx, float gy, float& u0, float& u1, float& u2) {
+            const float A = gx * s, B = gy * t, BX = B * X;
+            u0 = -B * r2;
+            u1 = A * Z + BX * Y;
+            u2 = BX * Z - A * Y;
+        };
+        auto acc_row = [&](float u0, float u1, float u2, float r) {
+            const float J[6] = {u0, u1, u2, Y * u2 - Z * u1, Z * u0 - X * u2, X * u1 - Y * u0};
+            acc_fma(A, J, r);
+        };
+        if (photo) {
+            float u0, u1, u2;
+            row(wp * G.x, wp * G.y, u0, u1, u2);
+            acc_row(u0, u1, u2, rp);
+        }
+        if (depth) {
+            float u0, u1, u2;
+            row(wd * G.z, wd * G.w, u0, u1, u2);
+            const float wdi = wd * dist_inv;
+            acc_row(u0 - wdi * X, u1 - wdi * Y, u2 - wdi * Z, rd);
+        }
+    }
+}
+
 // ---------------------------------------------------------------- GN step (thread 0 of last block)
 #include "icp_gn.inc"
 
@@ -464,6 +551,7 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
     __shared__ double s_err[NW], s_errd[NW];
     __shared__ double s_fin[RG][32];
     __shared__ int s_last;
+    __shared__ int s_qn[NW];   // PF 5: deferred entries per wave
     __shared__ GnShared s_gn;
     __shared__ IcpState s_state;
 
@@ -512,6 +600,7 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
     A.err2d = 0.0;
     auto flag = [&](int i) { return OCC ? (int)occf[i] : 0; };
     WaveCnt W;   // PF 3: wave-uniform counts
+    float errf = 0.f;   // PF 5: the lane's squared residuals in float
 
     const int units = (nRows * nCols) >> 2;  // 4 pixels of one row per unit (nCols % 4 == 0)
     const float4* src4 = reinterpret_cast<const float4*>(src);
@@ -697,18 +786,23 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
                 acc(o, gt.g(o.t), gt.T(o.t), act ? flag(i) : 0);
             }
         }
-    } else if (PF == 4) {
+    } else if (PF == 4 || PF == 5) {
         // PF 3's wave stream over the level's COMPACTED source points (LevelBufs::pts, built once per frame):
         // only pixels with minDepth < depth < maxDepth, as {LUT point, gray}, in raster order.  No row/column
         // tables, no LUT arithmetic and no lanes spent on pixels without depth.  Deferred lanes queue their
         // point index and are re-projected exactly after the stream.
+        // PF 5 (default): the same stream with contribute_lean's single-precision error terms and a contracted
+        // transform, and the deferred lanes of the workgroup's four waves drained together (a wave defers ~0.4 %
+        // of its points, a few per pass: one drain chunk per workgroup instead of one mostly idle chunk per wave).
+        constexpr bool LEAN = PF == 5;
         const int nv = __builtin_amdgcn_readfirstlane(*npts);
         const int lane = threadIdx.x & 63;
         const int qcap = ((nv + stride - 1) / stride) * 64;
         int* q = dq + ((long)blockIdx.x * NW + (threadIdx.x >> 6)) * qcap;
         int qn = 0;
         auto acc = [&](const Proj& o, const float4 G, const float2 T) {
-            contribute_fast<METHOD, 0>(A, W, o, G, T, 0, angle_res_inv, C);
+            if (LEAN) contribute_lean<METHOD>(A, W, errf, o, G, T, angle_res_inv, C);
+            else contribute_fast<METHOD, 0>(A, W, o, G, T, 0, angle_res_inv, C);
         };
         const Gather gt{__builtin_amdgcn_make_buffer_rsrc(const_cast<float4*>(tg), 0, nRows * nCols * 16, 0x00020000),
                         __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(trg), 0, nRows * nCols * 8, 0x00020000)};
@@ -720,7 +814,7 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
                                    __uint_as_float(v[3])), base + lane < nv};
         };
         auto prj = [&](const Src& x) {
-            return project_fast(P, Lut3{x.p.x, x.p.y, x.p.z, x.valid}, x.p.w, nRows, nCols, angle_res_inv, asin_out);
+            return project_fast<LEAN>(P, Lut3{x.p.x, x.p.y, x.p.z, x.valid}, x.p.w, nRows, nCols, angle_res_inv, asin_out);
         };
         auto defer = [&](Proj& o, int base) {
             const unsigned long long m = __ballot(o.fix);
@@ -763,7 +857,7 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
                 if (k + 2 >= n_it) break;
             }
         }
-        if (qn > 0) {
+        if (!LEAN && qn > 0) {
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
             for (int s0 = 0; s0 < qn; s0 += 64) {
                 const bool act = s0 + lane < qn;
@@ -774,6 +868,153 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
                 o.t = o.vis ? o.t : 0;
                 acc(o, gt.g(o.t), gt.T(o.t));
             }
+        }
+        if (LEAN) {
+            // the workgroup's queues as one list (wave w's entries after those of waves < w), 64 entries per
+            // drain chunk, chunk j on wave j % NW; the queue stores of other waves are ordered before the loads
+            // by the workgroup-scope release / acquire of the barrier (one CU, one L1)
+            if (lane == 0) s_qn[threadIdx.x >> 6] = qn;
+            __syncthreads();
+            int pre[NW + 1];
+            pre[0] = 0;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) pre[w + 1] = pre[w] + s_qn[w];
+            const int tot = pre[NW];
+            const int* qb = dq + (long)blockIdx.x * NW * qcap;
+            for (int s0 = (threadIdx.x >> 6) * 64; s0 < tot; s0 += NW * 64) {
+                const int g = s0 + lane;
+                const bool act = g < tot;
+                int w = 0;
+#pragma unroll
+                for (int v = 1; v < NW; ++v) w += g >= pre[v] ? 1 : 0;
+                const int i = act ? qb[w * qcap + (g - pre[w])] : 0;
+                const float4 a = pts[i];
+                Proj o = project_exact(P, Lut3{a.x, a.y, a.z, true}, a.w, nRows, nCols, half_nRows, angle_res_inv);
+                o.vis = o.vis && act;
+                o.t = o.vis ? o.t : 0;
+                acc(o, gt.g(o.t), gt.T(o.t));
+            }
+        }
+    } else if (PF == 6) {
+        // Level 0 from the PACKED level-0 images (LevelBufs::pk, 4 B per pixel: range mm | luma << 16): the
+        // source is streamed as the image itself, one wave = 64 consecutive pixels of one row (nCols % 64 == 0),
+        // and the target {gray, depth} is gathered from the target's packed image (4 B instead of 8).  Per pass
+        // and pair that reads 4 N + 20 V bytes instead of PF 5's 16 N_valid + 24 V, with the LUT point computed
+        // from the row / column tables by the compaction's own float expressions (lut_point) and gray / depth by
+        // the stitch's (luma * (float)(1/255), range * 0.001f): bit for bit the values PF 5 reads.  Pixels
+        // without a valid depth ride along as invisible lanes (~10 % at level 0).  Projection, lean terms and the
+        // workgroup drain as PF 5.
+        const int npx = nRows * nCols;
+        const int lane = threadIdx.x & 63;
+        const int qcap = ((npx + stride - 1) / stride) * 64;
+        int* q = dq + ((long)blockIdx.x * NW + (threadIdx.x >> 6)) * qcap;
+        int qn = 0;
+        const uint32_t* __restrict__ spk = J.spk;
+        const auto rs_s = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(spk), 0, npx * 4, 0x00020000);
+        const auto rs_g = __builtin_amdgcn_make_buffer_rsrc(const_cast<float4*>(tg), 0, npx * 16, 0x00020000);
+        const auto rs_t = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(J.tpk), 0, npx * 4, 0x00020000);
+        auto gray_of = [](unsigned v) { return (float)(v >> 16) * (float)(1. / 255); };   // k_stitch4's expressions
+        auto depth_of = [](unsigned v) { return (float)(v & 0xffffu) * 0.001f; };
+#ifdef R360_EXP_NOGATHER   // experiment builds only (tools/exp_variants.sh): no target loads
+        auto gG = [&](int t) { const float v = (float)(t & 1023) * 1e-3f; return make_float4(v, -v, v, 0.5f * v); };
+        auto gT = [&](int t) { return (unsigned)(t & 0xffffff); };
+#else
+        auto gG = [&](int t) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs_g, t * 16, 0, 0);
+            return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+        };
+        auto gT = [&](int t) { return __builtin_amdgcn_raw_buffer_load_b32(rs_t, t * 4, 0, 0); };
+#endif
+        auto acc = [&](const Proj& o, const float4 G, unsigned tv) {
+#ifdef R360_EXP_NOACC   // experiment builds only: keep the operands alive, skip the math
+            A.h[0] += o.vis ? G.x + G.y + G.z + G.w + gray_of(tv) + depth_of(tv) + o.X + o.dist : 0.f;
+            W.c28 += wave_count(o.vis);
+            return;
+#endif
+            contribute_lean<METHOD>(A, W, errf, o, G, make_float2(gray_of(tv), depth_of(tv)), angle_res_inv, C);
+        };
+        // row of a wave-uniform pixel index: a float estimate corrected by one step either way (exact for
+        // pixel indices below 2^24, every level-0 size here)
+        const float inv_cols = 1.f / (float)nCols;
+        auto row_of = [&](int i) {
+            int r = (int)((float)i * inv_cols);
+            r -= (r * nCols > i) ? 1 : 0;
+            r += ((r + 1) * nCols <= i) ? 1 : 0;
+            return r;
+        };
+        struct Src { unsigned v; float sp, cp, st, ct; };
+        auto ld = [&](int base) {                          // base: wave-uniform first pixel of a 64-pixel run
+            const int r = __builtin_amdgcn_readfirstlane(row_of(base));
+            const int c = base - r * nCols + lane;
+            return Src{__builtin_amdgcn_raw_buffer_load_b32(rs_s, (base + lane) * 4, 0, 0), sinphi[r], cosphi[r],
+                       sinth[c], costh[c]};
+        };
+        auto prj = [&](const Src& x) {
+            const float d = depth_of(x.v);
+            return project_fast<true>(P, lut_point(d, x.sp, x.cp, x.st, x.ct, C), gray_of(x.v), nRows, nCols,
+                                      angle_res_inv, asin_out);
+        };
+        auto defer = [&](Proj& o, int base) {
+            const unsigned long long m = __ballot(o.fix);
+            if (m) {
+                const int pos = qn + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                                   __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+                if (o.fix) { q[pos] = base + lane; o.vis = false; o.t = 0; }
+                qn += __popcll(m);
+            }
+        };
+        const int nbx = (int)gridDim.x;   // XCD-aware stream order (as PF 4 / 5)
+        const int bx = (nbx & 7) ? (int)blockIdx.x : ((int)blockIdx.x & 7) * (nbx >> 3) + ((int)blockIdx.x >> 3);
+        const int b0 = __builtin_amdgcn_readfirstlane((bx * TPB + (threadIdx.x & ~63)));
+        if (b0 < npx) {
+            const int n_it = (npx - 1 - b0) / stride + 1;
+            auto base = [&](int k) { return b0 + (k < n_it ? k : n_it - 1) * stride; };
+            Src sA = ld(base(0));
+            Src sB = ld(base(1));
+            Proj oA = prj(sA);
+            defer(oA, base(0));
+            float4 GA = gG(oA.t);
+            unsigned TA = gT(oA.t);
+            for (int k = 0;; k += 2) {
+                sA = ld(base(k + 2));
+                Proj oB = prj(sB);
+                if (k + 1 < n_it) defer(oB, base(k + 1));   // a clamped tail chunk is never accumulated
+                const float4 GB = gG(oB.t);
+                const unsigned TB = gT(oB.t);
+                acc(oA, GA, TA);
+                if (k + 1 >= n_it) break;
+                sB = ld(base(k + 3));
+                oA = prj(sA);
+                if (k + 2 < n_it) defer(oA, base(k + 2));
+                GA = gG(oA.t);
+                TA = gT(oA.t);
+                acc(oB, GB, TB);
+                if (k + 2 >= n_it) break;
+            }
+        }
+        // the workgroup's deferred lanes, drained together (as PF 5)
+        if (lane == 0) s_qn[threadIdx.x >> 6] = qn;
+        __syncthreads();
+        int pre[NW + 1];
+        pre[0] = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) pre[w + 1] = pre[w] + s_qn[w];
+        const int tot = pre[NW];
+        const int* qb = dq + (long)blockIdx.x * NW * qcap;
+        for (int s0 = (threadIdx.x >> 6) * 64; s0 < tot; s0 += NW * 64) {
+            const int g = s0 + lane;
+            const bool act = g < tot;
+            int w = 0;
+#pragma unroll
+            for (int v = 1; v < NW; ++v) w += g >= pre[v] ? 1 : 0;
+            const int i = act ? qb[w * qcap + (g - pre[w])] : 0;
+            const unsigned v = spk[i];
+            const int r = i / nCols, c = i - r * nCols;
+            Proj o = project_exact(P, lut_point(depth_of(v), sinphi[r], cosphi[r], sinth[c], costh[c], C), gray_of(v),
+                                   nRows, nCols, half_nRows, angle_res_inv);
+            o.vis = o.vis && act;
+            o.t = o.vis ? o.t : 0;
+            acc(o, gG(o.t), gT(o.t));
         }
     } else {
         // small levels: one pixel per thread, so the latency chain per thread is a quarter as long
@@ -797,6 +1038,7 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
     // ---- stage 1: wave butterfly (f32) -> LDS -> per-workgroup fp64 record
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     if (PF >= 3 && lane == 0) { A.h[27] += (float)W.c27; A.h[28] += (float)W.c28; A.h[29] += (float)W.c29; }
+    if (PF >= 5) A.err2 = (double)errf;
 #ifdef R360_EXP_NOEPI   // experiment builds only
     if (A.h[0] == 1.2345f) S->dbg[7] = 1;
     return;
@@ -1154,7 +1396,8 @@ int icp_blocks_for(int n_pixels) {
 namespace {
 // Test hook: the PF 3 pass's decision for LUT points (lx, ly, lz) at pose P — the fast projection, or
 // the exact one for a flagged (deferred) lane — against the exact program alone: pixel-decision
-// mismatches (must be 0) and deferrals.
+// mismatches (must be 0; the PF 5 form with the contracted transform is checked on the same points) and
+// deferrals.
 __global__ void k_proj_check(const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
                              int n, Pose12 P, int nRows, int nCols, unsigned long long* __restrict__ out) {
     const float angle_res = (float)(2 * R360_PI / nCols);
@@ -1166,8 +1409,10 @@ __global__ void k_proj_check(const float* __restrict__ X, const float* __restric
         l.x = X[i]; l.y = Y[i]; l.z = Z[i]; l.valid = true;
         const Proj e = project_exact(P, l, 0.f, nRows, nCols, half_nRows, angle_res_inv);
         Proj f = project_fast(P, l, 0.f, nRows, nCols, angle_res_inv, asin_out_for(nRows, nCols));
+        Proj fl = project_fast<true>(P, l, 0.f, nRows, nCols, angle_res_inv, asin_out_for(nRows, nCols));  // PF 5
         if (f.fix) { f = e; ++fb; }
-        const bool same = f.vis == e.vis && f.t == e.t;
+        if (fl.fix) fl = e;
+        const bool same = f.vis == e.vis && f.t == e.t && fl.vis == e.vis && fl.t == e.t;
         mism += same ? 0 : 1;
         if (!same) { out[2] = (unsigned long long)i; out[3] = (unsigned long long)f.t; out[4] = (unsigned long long)e.t; }
     }
@@ -1295,8 +1540,8 @@ static int env_int(const char* name, int dflt) {
 template <int M, int PF>
 static void launch_pass(r360_ctx* ctx, int nb, int njobs, const IcpJobs& jobs, const LevelBufs& Ls,
                         const LevelTrig& T, const IcpConst& C, int first, int eval_only, bool top) {
-    // PF 4 (compacted source points) has no occlusion form: the occlusion flags are per source pixel
-    constexpr int PFO = PF == 4 ? 3 : PF;
+    // PF 4 / 5 (compacted source points) have no occlusion form: the occlusion flags are per source pixel
+    constexpr int PFO = PF >= 4 ? 3 : PF;
     auto kern = C.occ == 1 ? k_icp_pass<M, PFO, 0, 1>
               : C.occ == 2 ? k_icp_pass<M, PFO, 0, 2>
               : top        ? k_icp_pass<M, PF, 1, 0> : k_icp_pass<M, PF, 0, 0>;
@@ -1353,7 +1598,7 @@ static PassGrid pass_grid(const r360_ctx* ctx, const LevelBufs& Ls, int occ) {
     static const int pf_env = env_int("R360_ICP_PF", -1);
     static const int cap_env = env_int("R360_ICP_CAP", -1);
     // one resident round: CUs x workgroups per CU of the launched form (grid-stride beyond it)
-    struct Occ { int cus = 0, per[5] = {0, 0, 0, 0, 0}; };
+    struct Occ { int cus = 0, per[7] = {0, 0, 0, 0, 0, 0, 0}; };
     static const Occ occ_q = [] {   // thread-safe one-time query (contexts may be driven from several threads)
         Occ o;
         int dev = 0;
@@ -1364,12 +1609,17 @@ static PassGrid pass_grid(const r360_ctx* ctx, const LevelBufs& Ls, int occ) {
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[2], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 2, 0, 0>, TPB, 0);
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[3], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 3, 0, 0>, TPB, 0);
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[4], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 4, 0, 0>, TPB, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[5], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 5, 0, 0>, TPB, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[6], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 6, 0, 0>, TPB, 0);
         return o;
     }();
     const int npx = Ls.rows * Ls.cols;
     // PF 4 (compacted source points) for the plain pass; the occlusion variants index their flags by source
     // pixel and keep the image stream (PF 3 where rows split into whole waves)
-    const int pf = pf_env >= 0 && !(pf_env == 4 && occ) ? pf_env : (occ ? ((Ls.cols % 64 == 0) ? 3 : 0) : 4);
+    // level 0 (the only level with a packed image) streams the packed images where rows split into whole waves
+    const bool pk_ok = Ls.pk != nullptr && Ls.cols % 64 == 0;
+    const int pf_dflt = occ ? ((Ls.cols % 64 == 0) ? 3 : 0) : (pk_ok ? 6 : 5);
+    const int pf = pf_env >= 0 && !(pf_env >= 4 && occ) && !(pf_env == 6 && !pk_ok) ? pf_env : pf_dflt;
     // workgroups per job and pass: 2 per CU (one resident round holds occ_q.per[pf] per CU; a batched launch
     // fills the rest with other jobs, and fewer records per job shorten the reduction tail)
     int cap = cap_env > 0 ? cap_env : 2 * occ_q.cus;
@@ -1403,6 +1653,8 @@ static int launch_jobs(r360_ctx* ctx, const IcpJobs& jobs, int njobs, const Leve
         else if (pf == 2) launch_pass<M, 2>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top);      \
         else if (pf == 3) launch_pass<M, 3>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top);      \
         else if (pf == 4) launch_pass<M, 4>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top);      \
+        else if (pf == 5) launch_pass<M, 5>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top);      \
+        else if (pf == 6) launch_pass<M, 6>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top);      \
         else launch_pass<M, 0>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top);                   \
     } while (0)
     if (method == R360_PHOTO_CONSISTENCY) R360_LAUNCH(R360_PHOTO_CONSISTENCY);
@@ -1481,6 +1733,7 @@ int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src
     IcpJobs jobs;
     IcpJob& J = jobs.j[0];
     J.src = Ls.p0; J.trg = Lt.p0; J.tg = Lt.tg; J.pts = Ls.pts; J.npts = src->d_npts + level;
+    J.spk = Ls.pk; J.tpk = Lt.pk;
     J.S = ctx->d_state; J.partials = ctx->d_partials; J.gcnt = ctx->d_gticket; J.dq = ctx->d_defer;
     return launch_jobs(ctx, jobs, 1, Ls, T, level, method, C, first, eval_only, G);
 }

@@ -42,6 +42,10 @@ struct LevelBufs {
     // order as {LUT_xyz_sphere point (:4580-4582), gray}: the ICP pass streams these instead of the image
     // (launch_pyramid builds them; the count is the frame's d_npts[level])
     float4* pts = nullptr;
+    // level 0 only: the level's {gray, depth} as the stitch produced them, 4 B per pixel: range in mm (u16) |
+    // luma (u8) << 16.  gray = luma * (float)(1/255), depth = range * 0.001f reproduce p0 bit for bit; the
+    // level-0 ICP pass (PF 6) streams the source and gathers the target {gray, depth} from these.
+    uint32_t* pk = nullptr;
 };
 constexpr int R360_SRC_BLOCK = 4096;   // pixels per block of the source-point compaction
 // one level's inputs / output of the compaction (a device-side table per frame, fixed at creation)
@@ -102,8 +106,10 @@ struct IcpJob {
     const float2* src;          // source level {gray, depth}
     const float2* trg;          // target level {gray, depth}
     const float4* tg;           // target level gradients
-    const float4* pts;          // source level compacted points (PF 4)
+    const float4* pts;          // source level compacted points (PF 4 / 5)
     const int* npts;            // their count
+    const uint32_t* spk;        // level 0: source packed {range mm, luma} image (PF 6)
+    const uint32_t* tpk;        // level 0: target packed image
     IcpState* S;
     double* partials;           // per-workgroup records
     unsigned* gcnt;             // group arrival counters (R360_TICKET_GROUPS x R360_TICKET_STRIDE)

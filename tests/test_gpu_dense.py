@@ -232,7 +232,7 @@ def test_fast_projection_guard_never_changes_a_pixel(rows, cols):
     R._check(R.lib().r360_proj_check(R._fptr(x), R._fptr(y), R._fptr(z), n, rows, cols, R.C.byref(mism),
                                      R.C.byref(fb)), "proj_check")
     assert mism.value == 0, mism.value
-    fb_cap = n // 3 if rows * 6 <= cols else (3 * n) // 5   # tall spheres: |x| >= 0.53 always deferred
+    fb_cap = n // 3 if rows * 6 <= cols else (2 * n) // 3   # tall spheres: |x| >= 0.53 always deferred
     assert fb.value < fb_cap          # the fast path decides most points
     # the same with a pose: LUT points whose TRANSFORMED position is random or on a rounding boundary,
     # so the fast (FMA-contracted) transform is covered too

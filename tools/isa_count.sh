@@ -20,7 +20,7 @@ body = s[start:end]
 best = None
 for h in [i for i, l in enumerate(body) if "Inner Loop Header" in l]:
     lab = body[h].split(":")[0]
-    back = max((i for i, l in enumerate(body) if re.search(r"s_cbranch\w* " + re.escape(lab) + r"$", l.strip())),
+    back = max((i for i, l in enumerate(body) if re.search(r"s_(?:c)?branch\w* " + re.escape(lab) + r"$", l.strip())),
                default=None)
     if back is None:
         continue

@@ -30,6 +30,7 @@ def is_l0(name):
 icp = [r for r in rows if is_l0(r["Kernel_Name"])]
 gmax = max(int(r["Grid_Size_X"]) for r in icp)
 l0 = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in icp]
+l0_pairs = [int(r["Grid_Size_Y"]) for r in icp]   # blockIdx.y = pair: pairs per batched launch
 
 
 def pmc(name):
@@ -64,6 +65,7 @@ write_j = pmc_per_job("WRITE_SIZE", waves_per_job) if waves_per_job else None
 out = {
     "kernel": "k_icp_pass<PHOTO_DEPTH> level 0", "grid_threads": gmax, "launches": len(l0),
     "avg_duration_us": float(np.mean(l0)), "median_duration_us": float(np.median(l0)),
+    "avg_pairs_per_launch": float(np.mean(l0_pairs)),
     "FETCH_SIZE_kB_per_launch": fetch, "WRITE_SIZE_kB_per_launch": write,
     # MI355X_MICROARCH.md §HBM: FETCH_SIZE counts 64 B per 128-B request on gfx950 -> double it
     "hbm_bytes_per_launch": (2 * fetch * 1024 + write * 1024) if fetch is not None and write is not None else None,
@@ -77,7 +79,22 @@ for k in ("SQ_INSTS_VALU", "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_W
           "TCC_HIT_sum", "TCC_MISS_sum", "SQ_ACTIVE_INST_VALU", "SQ_INSTS_VMEM_RD"):
     v = pmc(k)
     if v is not None:
-        out[k] = v
+        out[k] = v   # median over dispatches of the raw counter (dispatches differ in pairs per launch)
+    if k != "SQ_WAVES" and waves_per_job:
+        vj = pmc_per_job(k, waves_per_job)   # per dispatch: counter / its own pairs, then the median
+        if vj is not None:
+            out[k + "_per_pair_pass"] = vj
+# the traced command's own bench line: its in-kernel-span roofline against the trace's durations and pairs
+try:
+    line = [l for l in open(os.path.join(src, "trace.out")) if l.startswith("{")][-1]
+    b = json.loads(line)["roofline"]
+    B = b["bytes_per_pair_pass"]
+    out["traced_line"] = {"avg_launch_ms": b["avg_launch_ms"], "pairs_per_launch": b["pairs_per_launch"],
+                          "frac": b["frac"], "bytes_per_pair_pass": B}
+    out["trace_frac"] = out["avg_pairs_per_launch"] * B / (out["avg_duration_us"] * 1e-6) / 1e9 / 8000.0
+    out["trace_frac_over_line_frac"] = out["trace_frac"] / b["frac"]
+except Exception as e:   # noqa: BLE001
+    out["traced_line_error"] = str(e)
 # the ICP sources this profile measured (bench.py reports the traffic only while they are unchanged)
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
