@@ -140,6 +140,13 @@ extern "C" int r360_dense_queue_create(int device, int max_batch, r360_dense_que
         R360_HIP(hipStreamDestroy(ctx->stream));
         ctx->stream = hs;
     }
+    uint32_t mask[R360_CU_MASK_WORDS];
+    if (r360_cu_mask(device, 1, mask)) {   // CU partition experiment: the queue's stream off the excluded CUs
+        hipStream_t hs = nullptr;
+        R360_HIP(hipExtStreamCreateWithCUMask(&hs, R360_CU_MASK_WORDS * 32, mask));
+        R360_HIP(hipStreamDestroy(ctx->stream));
+        ctx->stream = hs;
+    }
     auto* q = new r360_dense_queue;
     q->ctx = ctx;
     q->max_batch = max_batch;

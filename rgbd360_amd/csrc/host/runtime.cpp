@@ -105,6 +105,27 @@ extern "C" int r360_ctx_timing_reset(r360_ctx* ctx) {
 }
 
 // ------------------------------------------------------------------ context
+// CU partition experiment (off by default).  R360_QUEUE_CU_EXCL=n keeps n CUs out of the dense queue's stream
+// (R360_QUEUE_CU_PAT=spread: every (CUs / n)-th CU, =high: the last n); R360_PIPE_CU=excl puts every other context's
+// stream on exactly those n CUs.  Returns true and fills mask when the stream of that kind gets a CU mask.
+bool r360_cu_mask(int device, int for_queue, uint32_t* mask) {
+    static const int excl = getenv("R360_QUEUE_CU_EXCL") ? atoi(getenv("R360_QUEUE_CU_EXCL")) : 0;
+    static const bool high = getenv("R360_QUEUE_CU_PAT") && strcmp(getenv("R360_QUEUE_CU_PAT"), "high") == 0;
+    static const bool pipe = getenv("R360_PIPE_CU") && strcmp(getenv("R360_PIPE_CU"), "excl") == 0;
+    if (excl <= 0 || (!for_queue && !pipe)) return false;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= excl ||
+        cus > 32 * R360_CU_MASK_WORDS)
+        return false;
+    for (int w = 0; w < R360_CU_MASK_WORDS; ++w) mask[w] = 0;
+    const int step = cus / excl;
+    for (int i = 0; i < cus; ++i) {
+        const bool ex = high ? i >= cus - excl : (i % step == step - 1 && i / step < excl);
+        if (ex != (bool)for_queue) mask[i / 32] |= 1u << (i % 32);
+    }
+    return true;
+}
+
 extern "C" int r360_ctx_create(int device, r360_ctx** out) {
     CHECK_ARG(out, "null out");
     int n = 0;
@@ -116,10 +137,13 @@ extern "C" int r360_ctx_create(int device, r360_ctx** out) {
     // R360_CTX_PRIORITY=1: contexts' streams at the device's highest priority (the dense queue keeps the normal
     // one, r360_dense_queue_create); an experiment knob, off by default
     static const int ctx_prio = getenv("R360_CTX_PRIORITY") ? atoi(getenv("R360_CTX_PRIORITY")) : 0;
+    uint32_t mask[R360_CU_MASK_WORDS];
     if (ctx_prio) {
         int least = 0, greatest = 0;
         R360_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
         R360_HIP(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, greatest));
+    } else if (r360_cu_mask(device, 0, mask)) {   // R360_PIPE_CU=excl: contexts on the dense queue's excluded CUs
+        R360_HIP(hipExtStreamCreateWithCUMask(&c->stream, R360_CU_MASK_WORDS * 32, mask));
     } else {
         R360_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     }
@@ -629,6 +653,10 @@ extern "C" int r360_frame_get_points(r360_frame* f, int level, float* xyzg, int 
     CHECK_ARG(f && n, "null arg");
     CHECK_ARG(level >= 0 && level < f->n_levels, "level out of range");
     CHECK_ARG(f->built & R360_BUILD_PYRAMID, "pyramid not built");
+    if (level == 0 && !f->lv0_compacted) {   // level 0 streams its packed image; compact it on request
+        if (int rc = launch_src_compaction(f, 0, 1)) return rc;
+        f->lv0_compacted = true;
+    }
     int np = 0;
     R360_HIP(hipMemcpyAsync(&np, f->d_npts + level, sizeof(int), hipMemcpyDeviceToHost, f->ctx->stream));
     R360_HIP(hipStreamSynchronize(f->ctx->stream));

@@ -427,11 +427,24 @@ int launch_pyramid(r360_frame* f) {
         }
         hipLaunchKernelGGL(k_gradient_levels, dim3(GL.blk0[f->n_levels]), dim3(TPB), 0, f->ctx->stream, GL);
     }
+    // level 0 streams its packed image (PF 6) where rows split into whole waves: its compacted points are built
+    // only on request (r360_frame_get_points, or a pass form forced by R360_ICP_PF)
+    static const int pf_env = getenv("R360_ICP_PF") ? atoi(getenv("R360_ICP_PF")) : -1;
+    const bool skip0 = f->lv[0].pk && f->lv[0].cols % 64 == 0 && !(pf_env == 4 || pf_env == 5);
+    f->lv0_compacted = !skip0;
+    return launch_src_compaction(f, skip0 ? 1 : 0, f->n_levels);
+}
+
+// The compaction of levels [l0, l1) (one count + one compact launch over a flattened (level, block) grid)
+int launch_src_compaction(r360_frame* f, int l0, int l1) {
+    const float min_d = 0.3f, max_d = 6.0f;
+    if (l0 >= l1) return 0;
     SrcGrid G{};
-    G.nl = f->n_levels;
-    for (int l = 0; l < f->n_levels; ++l)
-        G.blk0[l + 1] = G.blk0[l] + (int)(((long)f->lv[l].rows * f->lv[l].cols + R360_SRC_BLOCK - 1) / R360_SRC_BLOCK);
-    const dim3 g(G.blk0[f->n_levels]);
+    G.nl = l1;
+    for (int l = 0; l < l1; ++l)
+        G.blk0[l + 1] = G.blk0[l] +
+                        (l < l0 ? 0 : (int)(((long)f->lv[l].rows * f->lv[l].cols + R360_SRC_BLOCK - 1) / R360_SRC_BLOCK));
+    const dim3 g(G.blk0[l1]);
     hipLaunchKernelGGL(k_src_count, g, dim3(SRC_TPB), 0, f->ctx->stream, f->d_src_levels, G, min_d, max_d, f->d_src_cnt,
                        f->src_blocks);
     hipLaunchKernelGGL(k_src_compact, g, dim3(SRC_TPB), 0, f->ctx->stream, f->d_src_levels, G, min_d, max_d,

@@ -966,7 +966,11 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
         const int nbx = (int)gridDim.x;   // XCD-aware stream order (as PF 4 / 5)
         const int bx = (nbx & 7) ? (int)blockIdx.x : ((int)blockIdx.x & 7) * (nbx >> 3) + ((int)blockIdx.x >> 3);
         const int b0 = __builtin_amdgcn_readfirstlane((bx * TPB + (threadIdx.x & ~63)));
+#ifdef R360_EXP_NOLOOP   // experiment builds only: the pass without its pixel loop (fixed costs)
+        if (false) {
+#else
         if (b0 < npx) {
+#endif
             const int n_it = (npx - 1 - b0) / stride + 1;
             auto base = [&](int k) { return b0 + (k < n_it ? k : n_it - 1) * stride; };
             Src sA = ld(base(0));
@@ -990,6 +994,152 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
                 TA = gT(oA.t);
                 acc(oB, GB, TB);
                 if (k + 2 >= n_it) break;
+            }
+        }
+        // the workgroup's deferred lanes, drained together (as PF 5)
+        if (lane == 0) s_qn[threadIdx.x >> 6] = qn;
+        __syncthreads();
+        int pre[NW + 1];
+        pre[0] = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) pre[w + 1] = pre[w] + s_qn[w];
+        const int tot = pre[NW];
+        const int* qb = dq + (long)blockIdx.x * NW * qcap;
+        for (int s0 = (threadIdx.x >> 6) * 64; s0 < tot; s0 += NW * 64) {
+            const int g = s0 + lane;
+            const bool act = g < tot;
+            int w = 0;
+#pragma unroll
+            for (int v = 1; v < NW; ++v) w += g >= pre[v] ? 1 : 0;
+            const int i = act ? qb[w * qcap + (g - pre[w])] : 0;
+            const unsigned v = spk[i];
+            const int r = i / nCols, c = i - r * nCols;
+            Proj o = project_exact(P, lut_point(depth_of(v), sinphi[r], cosphi[r], sinth[c], costh[c], C), gray_of(v),
+                                   nRows, nCols, half_nRows, angle_res_inv);
+            o.vis = o.vis && act;
+            o.t = o.vis ? o.t : 0;
+            acc(o, gG(o.t), gT(o.t));
+        }
+    } else if (PF == 7) {
+        // PF 6 with a deeper software pipeline (sources two steps ahead of their projection, gathers two steps
+        // ahead of their accumulation): the level-0 pass is bound by memory latency, not by VALU or bytes
+        // Level 0 from the PACKED level-0 images (LevelBufs::pk, 4 B per pixel: range mm | luma << 16): the
+        // source is streamed as the image itself, one wave = 64 consecutive pixels of one row (nCols % 64 == 0),
+        // and the target {gray, depth} is gathered from the target's packed image (4 B instead of 8).  Per pass
+        // and pair that reads 4 N + 20 V bytes instead of PF 5's 16 N_valid + 24 V, with the LUT point computed
+        // from the row / column tables by the compaction's own float expressions (lut_point) and gray / depth by
+        // the stitch's (luma * (float)(1/255), range * 0.001f): bit for bit the values PF 5 reads.  Pixels
+        // without a valid depth ride along as invisible lanes (~10 % at level 0).  Projection, lean terms and the
+        // workgroup drain as PF 5.
+        const int npx = nRows * nCols;
+        const int lane = threadIdx.x & 63;
+        const int qcap = ((npx + stride - 1) / stride) * 64;
+        int* q = dq + ((long)blockIdx.x * NW + (threadIdx.x >> 6)) * qcap;
+        int qn = 0;
+        const uint32_t* __restrict__ spk = J.spk;
+        const auto rs_s = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(spk), 0, npx * 4, 0x00020000);
+        const auto rs_g = __builtin_amdgcn_make_buffer_rsrc(const_cast<float4*>(tg), 0, npx * 16, 0x00020000);
+        const auto rs_t = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(J.tpk), 0, npx * 4, 0x00020000);
+        auto gray_of = [](unsigned v) { return (float)(v >> 16) * (float)(1. / 255); };   // k_stitch4's expressions
+        auto depth_of = [](unsigned v) { return (float)(v & 0xffffu) * 0.001f; };
+#ifdef R360_EXP_NOGATHER   // experiment builds only (tools/exp_variants.sh): no target loads
+        auto gG = [&](int t) { const float v = (float)(t & 1023) * 1e-3f; return make_float4(v, -v, v, 0.5f * v); };
+        auto gT = [&](int t) { return (unsigned)(t & 0xffffff); };
+#else
+        auto gG = [&](int t) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs_g, t * 16, 0, 0);
+            return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+        };
+        auto gT = [&](int t) { return __builtin_amdgcn_raw_buffer_load_b32(rs_t, t * 4, 0, 0); };
+#endif
+        auto acc = [&](const Proj& o, const float4 G, unsigned tv) {
+#ifdef R360_EXP_NOACC   // experiment builds only: keep the operands alive, skip the math
+            A.h[0] += o.vis ? G.x + G.y + G.z + G.w + gray_of(tv) + depth_of(tv) + o.X + o.dist : 0.f;
+            W.c28 += wave_count(o.vis);
+            return;
+#endif
+            contribute_lean<METHOD>(A, W, errf, o, G, make_float2(gray_of(tv), depth_of(tv)), angle_res_inv, C);
+        };
+        // row of a wave-uniform pixel index: a float estimate corrected by one step either way (exact for
+        // pixel indices below 2^24, every level-0 size here)
+        const float inv_cols = 1.f / (float)nCols;
+        auto row_of = [&](int i) {
+            int r = (int)((float)i * inv_cols);
+            r -= (r * nCols > i) ? 1 : 0;
+            r += ((r + 1) * nCols <= i) ? 1 : 0;
+            return r;
+        };
+        struct Src { unsigned v; float sp, cp, st, ct; };
+        auto ld = [&](int base) {                          // base: wave-uniform first pixel of a 64-pixel run
+            const int r = __builtin_amdgcn_readfirstlane(row_of(base));
+            const int c = base - r * nCols + lane;
+            return Src{__builtin_amdgcn_raw_buffer_load_b32(rs_s, (base + lane) * 4, 0, 0), sinphi[r], cosphi[r],
+                       sinth[c], costh[c]};
+        };
+        auto prj = [&](const Src& x) {
+            const float d = depth_of(x.v);
+            return project_fast<true>(P, lut_point(d, x.sp, x.cp, x.st, x.ct, C), gray_of(x.v), nRows, nCols,
+                                      angle_res_inv, asin_out);
+        };
+        auto defer = [&](Proj& o, int base) {
+            const unsigned long long m = __ballot(o.fix);
+            if (m) {
+                const int pos = qn + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                                   __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+                if (o.fix) { q[pos] = base + lane; o.vis = false; o.t = 0; }
+                qn += __popcll(m);
+            }
+        };
+        const int nbx = (int)gridDim.x;   // XCD-aware stream order (as PF 4 / 5)
+        const int bx = (nbx & 7) ? (int)blockIdx.x : ((int)blockIdx.x & 7) * (nbx >> 3) + ((int)blockIdx.x >> 3);
+        const int b0 = __builtin_amdgcn_readfirstlane((bx * TPB + (threadIdx.x & ~63)));
+        if (b0 < npx) {
+            // three-step pipeline over chunk slots 0..2 (chunk h in slot h % 3, source slot (h + 1) % 3 refilled
+            // with chunk h + 4): each step loads the source of chunk h + 4, projects chunk h + 2 (its source
+            // loaded two steps earlier) and issues its gathers, and accumulates chunk h (gathered two steps
+            // earlier).  A projected chunk keeps only its key {p', gray, target pixel}; |p'| and 1/|p'| are
+            // recomputed by the same expressions when it is accumulated.
+            const int n_it = (npx - 1 - b0) / stride + 1;
+            auto base = [&](int k) { return b0 + (k < n_it ? k : n_it - 1) * stride; };
+            struct Key { float X, Y, Z, g; int t; };   // t = target pixel, -1 when not visible
+            auto stage_b = [&](const Src& x, int k, Key& K, float4& G, unsigned& T) {
+                Proj o = prj(x);
+                if (k < n_it) defer(o, base(k));   // a clamped tail chunk is never accumulated
+                K = Key{o.X, o.Y, o.Z, o.gray_s, o.vis ? o.t : -1};
+                G = gG(o.t);
+                T = gT(o.t);
+            };
+            auto stage_c = [&](const Key& K, const float4 G, unsigned T) {
+                Proj o;
+                o.X = K.X; o.Y = K.Y; o.Z = K.Z; o.gray_s = K.g;
+                const float d2 = K.X * K.X + K.Y * K.Y + K.Z * K.Z;   // project_fast's expressions
+                o.dist_inv = __builtin_amdgcn_rsqf(d2);
+                o.dist = r360m::sqrt_rn(d2);
+                o.vis = K.t >= 0;
+                o.t = o.vis ? K.t : 0;
+                o.fix = false;
+                acc(o, G, T);
+            };
+            Src S0 = ld(base(0)), S1 = ld(base(1)), S2 = ld(base(2));
+            Key K0, K1, K2;
+            float4 G0, G1, G2;
+            unsigned T0, T1, T2;
+            stage_b(S0, 0, K0, G0, T0);
+            S0 = ld(base(3));
+            stage_b(S1, 1, K1, G1, T1);
+            for (int h = 0;; h += 3) {
+                S1 = ld(base(h + 4));
+                stage_b(S2, h + 2, K2, G2, T2);
+                stage_c(K0, G0, T0);
+                if (h + 1 >= n_it) break;
+                S2 = ld(base(h + 5));
+                stage_b(S0, h + 3, K0, G0, T0);
+                stage_c(K1, G1, T1);
+                if (h + 2 >= n_it) break;
+                S0 = ld(base(h + 6));
+                stage_b(S1, h + 4, K1, G1, T1);
+                stage_c(K2, G2, T2);
+                if (h + 3 >= n_it) break;
             }
         }
         // the workgroup's deferred lanes, drained together (as PF 5)
@@ -1592,13 +1742,13 @@ int ensure_batch(r360_ctx* ctx, int n, long n_pixels) {
 // grid of one job's pass at level `level` of `geom` (the same for every job of a batch): the pass form and
 // the number of workgroups
 struct PassGrid { int pf, nb; };
-static PassGrid pass_grid(const r360_ctx* ctx, const LevelBufs& Ls, int occ) {
+static PassGrid pass_grid(const r360_ctx* ctx, const LevelBufs& Ls, int occ, int njobs = 1) {
     // 4-pixel units on the large levels, one pixel per thread where that still fits one resident
     // round (latency-bound small levels); R360_ICP_PF=0/1 forces one form (experiments)
     static const int pf_env = env_int("R360_ICP_PF", -1);
     static const int cap_env = env_int("R360_ICP_CAP", -1);
     // one resident round: CUs x workgroups per CU of the launched form (grid-stride beyond it)
-    struct Occ { int cus = 0, per[7] = {0, 0, 0, 0, 0, 0, 0}; };
+    struct Occ { int cus = 0, per[8] = {0, 0, 0, 0, 0, 0, 0, 0}; };
     static const Occ occ_q = [] {   // thread-safe one-time query (contexts may be driven from several threads)
         Occ o;
         int dev = 0;
@@ -1611,6 +1761,7 @@ static PassGrid pass_grid(const r360_ctx* ctx, const LevelBufs& Ls, int occ) {
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[4], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 4, 0, 0>, TPB, 0);
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[5], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 5, 0, 0>, TPB, 0);
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[6], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 6, 0, 0>, TPB, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[7], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 7, 0, 0>, TPB, 0);
         return o;
     }();
     const int npx = Ls.rows * Ls.cols;
@@ -1619,10 +1770,14 @@ static PassGrid pass_grid(const r360_ctx* ctx, const LevelBufs& Ls, int occ) {
     // level 0 (the only level with a packed image) streams the packed images where rows split into whole waves
     const bool pk_ok = Ls.pk != nullptr && Ls.cols % 64 == 0;
     const int pf_dflt = occ ? ((Ls.cols % 64 == 0) ? 3 : 0) : (pk_ok ? 6 : 5);
-    const int pf = pf_env >= 0 && !(pf_env >= 4 && occ) && !(pf_env == 6 && !pk_ok) ? pf_env : pf_dflt;
+    const int pf = pf_env >= 0 && !(pf_env >= 4 && occ) && !(pf_env >= 6 && !pk_ok) ? pf_env : pf_dflt;
     // workgroups per job and pass: 2 per CU (one resident round holds occ_q.per[pf] per CU; a batched launch
     // fills the rest with other jobs, and fewer records per job shorten the reduction tail)
     int cap = cap_env > 0 ? cap_env : 2 * occ_q.cus;
+    // R360_ICP_WG_TOTAL (experiment): workgroups per LAUNCH, split over its jobs (multiple of 8 per job for the
+    // XCD slice order)
+    static const int tot_env = env_int("R360_ICP_WG_TOTAL", -1);
+    if (tot_env > 0) cap = ((tot_env / (njobs > 0 ? njobs : 1) + 7) / 8) * 8;
     if (cap > ctx->partials_cap) cap = ctx->partials_cap;
     // at least R360_ICP_PXT points per thread (default 1; 8 measured no faster): the coarse levels (a quarter, ... of
     // level 0) then run on a few hundred / dozen workgroups per pair instead of one thread per point, which
@@ -1655,6 +1810,7 @@ static int launch_jobs(r360_ctx* ctx, const IcpJobs& jobs, int njobs, const Leve
         else if (pf == 4) launch_pass<M, 4>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top);      \
         else if (pf == 5) launch_pass<M, 5>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top);      \
         else if (pf == 6) launch_pass<M, 6>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top);      \
+        else if (pf == 7) launch_pass<M, 7>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top);      \
         else launch_pass<M, 0>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top);                   \
     } while (0)
     if (method == R360_PHOTO_CONSISTENCY) R360_LAUNCH(R360_PHOTO_CONSISTENCY);
@@ -1671,7 +1827,7 @@ int launch_icp_jobs(r360_ctx* ctx, const IcpJobs& jobs, int n, const r360_frame*
     if (C.occ) { r360_set_error("batched passes: occlusion variants run one alignment per launch"); return -2; }
     if (n < 1 || n > R360_MAX_BATCH) { r360_set_error("batched passes: %d jobs (1..%d)", n, R360_MAX_BATCH); return -2; }
     const LevelBufs& Ls = geom->lv[level];
-    const PassGrid G = pass_grid(ctx, Ls, 0);
+    const PassGrid G = pass_grid(ctx, Ls, 0, n);
     if (G.pf >= 3 && ctx->bdefer_cap < defer_need(Ls.rows * Ls.cols, G.nb)) {
         r360_set_error("batched passes: deferred-pixel queues not sized for %d pixels", Ls.rows * Ls.cols);
         return -1;

@@ -348,6 +348,7 @@ struct r360_frame {
     PlaneBufs pl;
     PbMapHost* pbmap = nullptr;
     uint64_t timestamp = 0;            // Frame360::timeStamp (Frame360.h:181-184)
+    bool lv0_compacted = false;        // lv[0].pts / d_npts[0] hold level 0's compacted points
     SphereCloudHost* sphere_cloud = nullptr;  // sphereCloud set by loadCloud (Frame360.h:187-193)
 };
 
@@ -355,6 +356,9 @@ struct r360_frame {
 int launch_undistort(r360_frame* f);
 int launch_stitch(r360_frame* f);
 int launch_pyramid(r360_frame* f);
+int launch_src_compaction(r360_frame* f, int l0, int l1);   // compacted source points of levels [l0, l1)
+constexpr int R360_CU_MASK_WORDS = 8;
+bool r360_cu_mask(int device, int for_queue, uint32_t* mask);   // CU partition experiment (runtime.cpp)
 int launch_sphere_level0(r360_frame* f);   // level 0 {gray, depth m} from the frame's sphere images
 int launch_sensor_pyramid(r360_frame* f);
 // pinhole alignFrames: intrinsics of level 0 (setCameraMatrix) and the jobs of one batched launch

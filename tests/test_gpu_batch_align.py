@@ -133,3 +133,21 @@ def test_batch_pair_matches_oracle(seq):
         _, opose, _, _, _ = O.align360(tb, td, sb, sd, None, O.PHOTO_DEPTH, prm)
         assert O.rot_angle(poses[j], opose) <= 1e-4, j
         assert np.linalg.norm(poses[j][:3, 3] - opose[:3, 3]) <= 1e-3, j
+
+
+def test_batched_alignment_is_deterministic(seq):
+    """The same batch twice, on fresh contexts: every output bit-identical.  The sums are order-fixed (pixels to
+    waves by index, wave butterflies, per-workgroup records summed in workgroup order), so a pose does not depend
+    on which workgroup finished first."""
+    fr = seq["frames"]
+    pairs = [(fr[i], fr[i + 1]) for i in range(6)]
+    outs = []
+    for _ in range(2):
+        bctx = R.Context(0)
+        outs.append(R.align360_batch(bctx, pairs, None, R.PHOTO_DEPTH, _params(20)))
+        bctx.close()
+    (pa, Ha, ga, sa, ia), (pb, Hb, gb, sb, ib) = outs
+    assert ia == ib
+    for j in range(len(pairs)):
+        assert np.array_equal(pa[j], pb[j]) and np.array_equal(Ha[j], Hb[j]) and np.array_equal(ga[j], gb[j]), j
+        _same(sa[j], sb[j])

@@ -7,6 +7,7 @@ Against the CPU oracle on the same synthetic pair (two consecutive frames of the
   1e-5 of scale;
 * alignFrames360(PHOTO_DEPTH) with the reference schedule on levels 4..1 and exactly 50 iterations at level 0:
   the pose to the north-star tolerance (1e-4 rad / 1e-3 m), the coarse levels' iteration counts equal;
+* three consecutive pairs of the path, and the Register() alias (PbMap-seeded, non-identity start) on one of them;
 plus the size-independent properties: source-point compaction counts and the accuracy of the registered
 motion against the synthetic ground truth."""
 import numpy as np
@@ -27,7 +28,7 @@ def hires():
     cal = R.Calib360(ctx, 960, 1280)
     cal.loadExtrinsicCalibration(R.EXTRINSICS_DIR)
     raw, frames = [], []
-    for i in (0, 1):
+    for i in (0, 1, 2, 3):
         b, d = cal.synth_frame(SEED, R.synth_path_pose(SEED, i))
         f = R.Frame360(cal)
         f.upload(b, d)
@@ -56,7 +57,7 @@ def test_hires_stitch_and_pyramid_bitexact(hires):
 
 
 def test_hires_icp_pass_level0(hires):
-    f1, f2 = hires["frames"]
+    f1, f2 = hires["frames"][:2]
     reg = R.RegisterPhotoICP(hires["ctx"])
     reg.setTargetFrame(f1); reg.setSourceFrame(f2)
     lt, ls = f1.level(0), f2.level(0)
@@ -72,8 +73,71 @@ def test_hires_icp_pass_level0(hires):
         assert abs(e2 - e2r) <= 1e-6 * e2r
 
 
+def _oracle_align(f1, f2, init=None):
+    s1b, s1d = f1.sphere()
+    s2b, s2d = f2.sphere()
+    p = O.IcpParams.default(n_pyr=5, std_dev_photo=np.float32(3.0 / 255), fixed_iters_level0=50)
+    return O.align360(s1b, s1d, s2b, s2d, init, O.PHOTO_DEPTH, p)
+
+
+def _gt_rel(i, j):
+    return np.linalg.inv(R.synth_path_pose(SEED, i).astype(np.float64)) @ R.synth_path_pose(SEED, j).astype(np.float64)
+
+
+def _rot_deg(D):
+    return np.degrees(np.arccos(np.clip((np.trace(D[:3, :3]) - 1) / 2, -1, 1)))
+
+
+@pytest.mark.parametrize("pair", [(1, 2), (2, 3)])
+def test_hires_consecutive_pairs(hires, pair):
+    """Pairs (1, 2) and (2, 3) of the path (with (0, 1) below: three consecutive pairs), alignFrames360 from identity
+    with 50 level-0 iterations, against the oracle; the level-0 pass there streams the packed level-0 images."""
+    f1, f2 = (hires["frames"][k] for k in pair)
+    reg = R.RegisterPhotoICP(hires["ctx"])
+    reg.setNumPyr(5)
+    reg.setGrayVariance(3.0 / 255)
+    reg.params.fixed_iters_level0 = 50
+    reg.setTargetFrame(f1); reg.setSourceFrame(f2)
+    rc = reg.alignFrames360(np.eye(4), R.PHOTO_DEPTH)
+    rco, pose, H, g, st = _oracle_align(f1, f2)
+    assert rc == rco
+    assert O.rot_angle(reg.getOptimalPose(), pose) <= ROT_TOL
+    assert float(np.linalg.norm(reg.getOptimalPose()[:3, 3] - pose[:3, 3])) <= TRANS_TOL
+    assert list(reg.stats.iters)[1:5] == list(st.iters)[1:5]
+
+
+def test_hires_register_pbmap_seeded(hires):
+    """The Register() alias at 8 x 1280x960: PbMap plane extraction of both frames (480 x 640 clouds),
+    RegisterPbMap(25, PLANAR_3DoF), the rotOffset-conjugated PbMap pose as alignFrames360's (non-identity)
+    initialisation and 50 level-0 iterations, against the oracle's chain on the same raw frames."""
+    from rgbd360_amd.odometry import ROT_OFFSET, ROT_OFFSET_INV
+    f1, f2 = hires["frames"][2:4]
+    p = R.IcpParams.default()
+    p.n_pyr = 5
+    p.std_dev_photo = np.float32(3.0 / 255)
+    p.fixed_iters_level0 = 50
+    for f in (f1, f2):
+        f.getPlanes()
+    pose, info, st, ok = R.register(hires["ctx"], f1, f2, params=p)
+    rt, rti, K = hires["cal"].extrinsics()
+    rt8 = np.stack([rt[16 * k:16 * k + 16].reshape(4, 4).T for k in range(8)])
+    maps = [O.PbMap(d.astype(np.float32) * np.float32(0.001), b, rt8) for (b, d) in hires["raw"][2:4]]
+    r = O.register_pbmap(maps[0], maps[1], 25, O.PLANAR_3DoF)
+    assert ok == bool(r["good"])
+    assert ok, "the synthetic room's planes register"
+    assert not np.allclose(r["pose"], np.eye(4), atol=1e-3)          # a non-identity start
+    Ro, Ri = ROT_OFFSET.astype(np.float32), ROT_OFFSET_INV.astype(np.float32)
+    init = Ro @ r["pose"] @ Ri
+    _, dense, _, _, _ = _oracle_align(f1, f2, init)
+    ref = Ri.astype(np.float64) @ dense.astype(np.float64) @ Ro.astype(np.float64)
+    assert O.rot_angle(pose[:3, :3], ref[:3, :3]) <= ROT_TOL
+    assert np.linalg.norm(pose[:3, 3] - ref[:3, 3]) <= TRANS_TOL
+    D = np.linalg.inv(_gt_rel(2, 3)) @ pose.astype(np.float64)
+    assert _rot_deg(D) < 0.2 and np.linalg.norm(pose[:3, 3] - _gt_rel(2, 3)[:3, 3]) < 0.02
+
+
 def test_hires_align360_50_iterations(hires):
-    f1, f2 = hires["frames"]
+    f1, f2 = hires["frames"][:2]
     reg = R.RegisterPhotoICP(hires["ctx"])
     reg.setNumPyr(5)
     reg.setGrayVariance(3.0 / 255)
