@@ -368,6 +368,8 @@ def main():
 
     rec = np.zeros((args.steps, p1 - p0, OD.REC), np.float32)
     runner.host_s[:] = 0
+    for c in runner.ctxs:
+        c.host_times(reset=True)
     barrier()
     # HIP events around the level-0 passes (on the stream they are launched on); every launch only with
     # --stage-timing (events around every plane kernel of 16 streams cost throughput)
@@ -416,6 +418,10 @@ def main():
             stage[name] = stage.get(name, 0.0) + ms
     hs = runner.host_s.sum(axis=0)
     host_ms = {k: 1e3 * v / max(hs[3], 1) for k, v in zip(("load_build_enqueue", "pbmap_stage", "dense_wait"), hs[:3])}
+    ht = np.sum([c.host_times() for c in runner.ctxs], axis=0)   # inside RegisterPbMap
+    host_ms["pbmap_stage_split"] = {k: 1e3 * v / max(ht[3], 1) for k, v in
+                                    zip(("wait_frame_pbmaps", "match_tables", "tree_and_pose"), ht[:3])}
+    host_ms["pbmap_assembly_per_frame"] = 1e3 * ht[4] / max(ht[5], 1)
     if group is not None:
         elapsed = group.max(elapsed)
     pairs_job = args.steps * sum(sizes)
@@ -458,15 +464,26 @@ def main():
     event_ms = l0_ms / max(l0_n, 1)
     pairs_per_launch = k0_jobs / max(k0_n, 1)      # a batched launch runs one level-0 pass per pair
     achieved = pairs_per_launch * alg_bytes / (avg_ms * 1e-3) / 1e9 if k0_n else None
-    # the same pass with the GPU to itself: pipeline 0 registers its run once more, alone
-    for c in ctxs:
-        c.kernel_time_reset()
-    iso_rec = np.zeros((1, p1 - p0, OD.REC), np.float32)
+    # a lone pair on an idle GPU (OdometryRGBD360's sequential caller registers one pair at a time): two frames
+    # pipeline 0 has built, alignFrames360 with the same schedule, nothing else running
+    iso_ms, n, iso_ach, lone_ms = 0.0, 0, None, None
     if not args.no_isolated:
-        runner.run(p0, p1, frames_of, iso_rec, repeats=1, runs=runs[:1])
-    us, n, nj = dense_ctx.kernel_stats(0)
-    iso_ms = us / max(n, 1) * 1e-3
-    iso_ach = (nj / max(n, 1)) * alg_bytes / (iso_ms * 1e-3) / 1e9 if n else None
+        fa, fb = runner.frames[0][:2]
+        reg = R.RegisterPhotoICP(ctxs[0])
+        reg.params = params
+        reg.setTargetFrame(fa)
+        reg.setSourceFrame(fb)
+        for _ in range(2):
+            reg.alignFrames360(np.eye(4, dtype=np.float32), R.PHOTO_DEPTH)
+        ctxs[0].sync()
+        ctxs[0].kernel_time_reset()
+        t_l = time.perf_counter()
+        for _ in range(5):
+            reg.alignFrames360(np.eye(4, dtype=np.float32), R.PHOTO_DEPTH)
+        lone_ms = (time.perf_counter() - t_l) / 5 * 1e3
+        us, n, nj = ctxs[0].kernel_stats(0)
+        iso_ms = us / max(n, 1) * 1e-3
+        iso_ach = (nj / max(n, 1)) * alg_bytes / (iso_ms * 1e-3) / 1e9 if n else None
     probe = None
     if args.eval_probe:   # opt-in diagnostic: the level-0 pass in eval mode (no GN step) at identity, alone
         fa, fb = runner.frames[0][:2]
@@ -535,8 +552,9 @@ def main():
             "event_avg_launch_ms": event_ms, "bytes_per_launch": pairs_per_launch * alg_bytes,
             "bytes_per_pair_pass": alg_bytes, "visible_frac": sso,
             "isolated": {"avg_launch_ms": iso_ms, "launches": n, "achieved": iso_ach,
-                         "frac": (iso_ach / HBM_PEAK_GBS) if iso_ach else None,
-                         "note": "same pass, pipeline 0 alone on the GPU (its run once more after the timed region)"},
+                         "frac": (iso_ach / HBM_PEAK_GBS) if iso_ach else None, "align_ms_per_pair": lone_ms,
+                         "note": "a lone pair on an idle GPU: alignFrames360 (same schedule) of two built frames, "
+                                 "one pair per launch, 5 calls after 2 warm-up calls"},
             **({"eval_probe": probe} if probe else {}),
         },
         **({"stage_ms_per_pair": {k: v / max(args.steps * steps_pairs, 1) for k, v in stage.items()}}

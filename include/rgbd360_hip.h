@@ -513,6 +513,11 @@ int r360_ctx_timing_reset(r360_ctx* ctx);
 int r360_ctx_kernel_time(r360_ctx* ctx, int level, double* us_sum, long* passes);
 /* the same, plus the job passes those launches ran (a batched launch runs one per pair; NULL skips) */
 int r360_ctx_kernel_stats(r360_ctx* ctx, int level, double* us_sum, long* launches, long* job_passes);
+/* Profiling: host time of the ctx's RegisterPbMap calls: out[0] s waiting for the frames' PbMaps (GPU plane
+ * stage + host assembly), out[1] s in the match tables, out[2] s in the interpretation tree + ConsistencyTest,
+ * out[3] calls; out[4] s of PbMap assembly (the frames' host threads), out[5] frames; reset != 0 zeroes them.
+ * (No reference counterpart: instrumentation of r360_register_pbmap and the frames' assembly.) */
+int r360_ctx_host_times(r360_ctx* ctx, double out[6], int reset);
 int r360_ctx_kernel_time_reset(r360_ctx* ctx);
 
 #ifdef __cplusplus

@@ -264,6 +264,7 @@ _SIGS = [
     ("r360_ctx_debug_stamps", C.c_int, [_P, C.POINTER(C.c_ulonglong)]),
     ("r360_ctx_kernel_time", C.c_int, [_P, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_long)]),
     ("r360_ctx_kernel_time_reset", C.c_int, [_P]),
+    ("r360_ctx_host_times", C.c_int, [_P, C.POINTER(C.c_double), C.c_int]),
     ("r360_ctx_kernel_stats", C.c_int, [_P, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_long),
                                         C.POINTER(C.c_long)]),
     ("r360_ctx_timing", C.c_int, [_P, C.c_int]),
@@ -370,6 +371,13 @@ class Context:
         us, n, j = C.c_double(), C.c_long(), C.c_long()
         _check(lib().r360_ctx_kernel_stats(self.h, level, C.byref(us), C.byref(n), C.byref(j)), "kernel_stats")
         return us.value, n.value, j.value
+
+    def host_times(self, reset: bool = False):
+        """Host seconds of this ctx's RegisterPbMap calls: (waiting for the frames' PbMaps, match tables, tree search +
+        ConsistencyTest, calls, PbMap assembly of its frames, frames)."""
+        out = (C.c_double * 6)()
+        _check(lib().r360_ctx_host_times(self.h, out, 1 if reset else 0), "host_times")
+        return tuple(out)
 
     def kernel_time_reset(self):
         _check(lib().r360_ctx_kernel_time_reset(self.h), "kernel_time_reset")

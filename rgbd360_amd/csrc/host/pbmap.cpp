@@ -27,8 +27,8 @@
 #include "../r360_internal.h"
 
 
-int launch_match_tables(r360_ctx* ctx, const float* d_desc, int ns, int nt, int mode, uint8_t* d_unary,
-                        unsigned long long* d_bin, int words);
+int launch_match_tables(r360_ctx* ctx, hipStream_t stream, const float* d_desc, int ns, int nt, int mode,
+                        uint8_t* d_unary, unsigned long long* d_bin, int words);
 
 namespace {
 
@@ -422,8 +422,11 @@ int planes_enqueue(r360_frame* f) {
             Q.worker_err = "plane build: GPU work failed";
             return;
         }
+        const auto a0 = std::chrono::steady_clock::now();
         Q.worker_rc = planes_assemble(f);
         if (Q.worker_rc) Q.worker_err = r360_last_error();
+        f->ctx->host_ns[4] += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - a0).count();
+        f->ctx->host_ns[5] += 1;
     });
     return 0;
 }
@@ -644,12 +647,21 @@ int gpu_tables(r360_ctx* ctx, const std::vector<HPlane>& S, const std::vector<in
     std::vector<float> desc(16 * (size_t)(ns + nt));
     for (int i = 0; i < ns; ++i) pack_desc(S[si[i]], &desc[16 * i]);
     for (int j = 0; j < nt; ++j) pack_desc(T[ti[j]], &desc[16 * (ns + j)]);
-    hipStream_t st = ctx->stream;
+    if (!ctx->mstream) {
+        // the device's highest priority: a few microseconds of work that the calling thread waits for, which
+        // at normal priority queued for milliseconds behind the dense queue's launches (2.4 ms per call in the
+        // default bench, profiles/r3_host)
+        int least = 0, greatest = 0;
+        R360_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        R360_HIP(hipStreamCreateWithPriority(&ctx->mstream, hipStreamNonBlocking, greatest));
+        R360_HIP(hipEventCreateWithFlags(&ctx->mwait_ev, hipEventDisableTiming | hipEventBlockingSync));
+    }
+    hipStream_t st = ctx->mstream;
     R360_HIP(hipMemcpyAsync(ctx->d_match_desc, desc.data(), sizeof(float) * desc.size(), hipMemcpyHostToDevice, st));
     // the kernel writes the tables straight into the pinned host buffers (no device-to-host copies)
-    if (launch_match_tables(ctx, ctx->d_match_desc, ns, nt, mode, ctx->h_unary, ctx->h_bin, tb.words)) return -1;
-    if (ctx_wait(ctx)) return -1;
-    return 0;
+    if (launch_match_tables(ctx, st, ctx->d_match_desc, ns, nt, mode, ctx->h_unary, ctx->h_bin, tb.words)) return -1;
+    R360_HIP(hipEventRecord(ctx->mwait_ev, st));
+    return event_wait(ctx->mwait_ev);
 }
 
 // interpretation tree: depth-first over reference planes; largest consistent set, ties by matched
@@ -826,13 +838,27 @@ extern "C" int r360_register_pbmap(r360_ctx* ctx, r360_frame* ref, r360_frame* t
                                    float* area_matched, float* area_src, float* area_trg) {
     CHECK_ARG(ctx && pose && info, "null arg");
     CHECK_ARG(mode >= 0 && mode <= 3, "registrationType must be 0..3");
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
     if (int rc = ready(ref)) return rc;
     if (int rc = ready(trg)) return rc;
+    const auto t1 = clk::now();
     const auto& S = ref->pbmap->planes;
     const auto& T = trg->pbmap->planes;
     const std::vector<int> si = subgraph(S, max_match_planes), ti = subgraph(T, max_match_planes);
     Tables tb;
     if (gpu_tables(ctx, S, si, T, ti, mode, tb)) return -1;
+    const auto t2 = clk::now();
+    struct Acct {   // tree + pose time, accounted on every return path
+        r360_ctx* c; clk::time_point a, b, s;
+        ~Acct() {
+            const auto e = clk::now();
+            c->host_ns[0] += std::chrono::duration_cast<std::chrono::nanoseconds>(a - s).count();
+            c->host_ns[1] += std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count();
+            c->host_ns[2] += std::chrono::duration_cast<std::chrono::nanoseconds>(e - b).count();
+            c->host_ns[3] += 1;
+        }
+    } acct{ctx, t1, t2, t0};
     Tree tr;
     tr.tb = &tb;
     tr.budget = ctx->match.max_nodes;

@@ -169,6 +169,7 @@ extern "C" void r360_ctx_destroy(r360_ctx* c) {
     hipStreamSynchronize(c->stream);
     for (auto e : c->ev_pool) hipEventDestroy(e);
     hipEventDestroy(c->wait_ev);
+    if (c->mstream) { hipStreamDestroy(c->mstream); hipEventDestroy(c->mwait_ev); }
     hipFree(c->d_state);
     hipFree(c->d_partials);
     hipFree(c->d_gticket);
@@ -200,6 +201,18 @@ extern "C" int r360_ctx_kernel_stats(r360_ctx* ctx, int level, double* us_sum, l
 
 extern "C" int r360_ctx_kernel_time(r360_ctx* ctx, int level, double* us_sum, long* passes) {
     return r360_ctx_kernel_stats(ctx, level, us_sum, passes, nullptr);
+}
+
+// Host time of the ctx's RegisterPbMap calls (profiling): out[0..2] seconds waiting for the frames' PbMaps,
+// in the match tables, in the tree search + ConsistencyTest; out[3] calls; out[4] seconds of PbMap assembly of
+// the ctx's frames, out[5] frames.  reset != 0 zeroes the counters.
+extern "C" int r360_ctx_host_times(r360_ctx* ctx, double out[6], int reset) {
+    CHECK_ARG(ctx && out, "null arg");
+    for (int k = 0; k < 6; ++k) {
+        const long long v = reset ? ctx->host_ns[k].exchange(0) : ctx->host_ns[k].load();
+        out[k] = (k == 3 || k == 5) ? (double)v : (double)v * 1e-9;
+    }
+    return 0;
 }
 
 extern "C" int r360_ctx_kernel_time_reset(r360_ctx* ctx) {
@@ -561,6 +574,16 @@ extern "C" int r360_frame_build_async(r360_frame* f, unsigned flags) {
         if (launch_undistort(f)) return -1;
         f->built |= R360_BUILD_UNDISTORT;
     }
+    // the plane stage first: its results go to the host (PbMap assembly, then RegisterPbMap), which the dense
+    // stage waits for anyway, so the stitch and pyramid run on the GPU while the host assembles and matches
+    if (flags & (R360_BUILD_CLOUD | R360_BUILD_PLANES)) {
+        // buildSphereCloud + getPlanes (Frame360.h:467-510, 615-640): the per-pixel part is enqueued
+        // here; the per-plane PbMap assembly runs on the host when the planes are first needed
+        if (planes_enqueue(f)) return -1;
+        f->built |= R360_BUILD_CLOUD | R360_BUILD_PLANES;
+        delete f->sphere_cloud;  // a cloud set by loadCloud is replaced by the built one
+        f->sphere_cloud = nullptr;
+    }
     if (flags & (R360_BUILD_SPHERE | R360_BUILD_PYRAMID)) {
         if (launch_stitch(f)) return -1;
         f->built |= R360_BUILD_SPHERE;
@@ -572,14 +595,6 @@ extern "C" int r360_frame_build_async(r360_frame* f, unsigned flags) {
     if (flags & R360_BUILD_SENSOR_PYRAMID) {
         if (launch_sensor_pyramid(f)) return -1;
         f->built |= R360_BUILD_SENSOR_PYRAMID;
-    }
-    if (flags & (R360_BUILD_CLOUD | R360_BUILD_PLANES)) {
-        // buildSphereCloud + getPlanes (Frame360.h:467-510, 615-640): the per-pixel part is enqueued
-        // here; the per-plane PbMap assembly runs on the host when the planes are first needed
-        if (planes_enqueue(f)) return -1;
-        f->built |= R360_BUILD_CLOUD | R360_BUILD_PLANES;
-        delete f->sphere_cloud;  // a cloud set by loadCloud is replaced by the built one
-        f->sphere_cloud = nullptr;
     }
     return 0;
 }

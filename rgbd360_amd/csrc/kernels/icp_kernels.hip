@@ -1773,9 +1773,11 @@ static PassGrid pass_grid(const r360_ctx* ctx, const LevelBufs& Ls, int occ, int
     const int pf = pf_env >= 0 && !(pf_env >= 4 && occ) && !(pf_env >= 6 && !pk_ok) ? pf_env : pf_dflt;
     // workgroups per job and pass: 2 per CU (one resident round holds occ_q.per[pf] per CU; a batched launch
     // fills the rest with other jobs, and fewer records per job shorten the reduction tail)
+    // workgroups per job and pass: a fixed number per level size, never a function of the batch, so that a
+    // pair's sums (pixels to waves, records in workgroup order) and thus its pose are the same in any batch
+    // and on any number of ranks.  R360_ICP_WG_TOTAL (experiment only: breaks that) splits a per-launch total
+    // over the launch's jobs.
     int cap = cap_env > 0 ? cap_env : 2 * occ_q.cus;
-    // R360_ICP_WG_TOTAL (experiment): workgroups per LAUNCH, split over its jobs (multiple of 8 per job for the
-    // XCD slice order)
     static const int tot_env = env_int("R360_ICP_WG_TOTAL", -1);
     if (tot_env > 0) cap = ((tot_env / (njobs > 0 ? njobs : 1) + 7) / 8) * 8;
     if (cap > ctx->partials_cap) cap = ctx->partials_cap;

@@ -87,8 +87,8 @@ __global__ void k_match_tables(const float* __restrict__ desc, int ns, int nt, i
 
 }  // namespace
 
-int launch_match_tables(r360_ctx* ctx, const float* d_desc, int ns, int nt, int mode, uint8_t* d_unary,
-                        unsigned long long* d_bin, int words) {
+int launch_match_tables(r360_ctx* ctx, hipStream_t stream, const float* d_desc, int ns, int nt, int mode,
+                        uint8_t* d_unary, unsigned long long* d_bin, int words) {
     // the ctx's thresholds (r360_match_params, the ini keys); angles become the cosines / sine the
     // constraints compare against (configLocaliser_sphericalOdometry.ini: cos 50, cos 10, sin 10 deg)
     const r360_match_params& m = ctx->match;
@@ -99,7 +99,7 @@ int launch_match_tables(r360_ctx* ctx, const float* d_desc, int ns, int nt, int 
     const long total = (long)ns * nt * words * 64;
     if (total == 0) return 0;
     const int blocks = (int)std::min<long>((total + 255) / 256, 4096);
-    hipLaunchKernelGGL(k_match_tables, dim3(blocks), dim3(256), 0, ctx->stream, d_desc, ns, nt, mode, cfg, d_unary,
+    hipLaunchKernelGGL(k_match_tables, dim3(blocks), dim3(256), 0, stream, d_desc, ns, nt, mode, cfg, d_unary,
                        d_bin, words);
     R360_HIP(hipGetLastError());
     return 0;

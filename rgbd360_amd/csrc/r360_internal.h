@@ -1,6 +1,7 @@
 // r360_internal.h — internal types shared by the HIP kernels and the host runtime of
 // librgbd360_hip.so.  Not part of the ABI.
 #pragma once
+#include <atomic>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string>
@@ -221,6 +222,14 @@ struct r360_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t wait_ev = nullptr;   // blocking-sync event: host waits sleep instead of spinning
+    // RegisterPbMap's match tables run on a stream of their own (created on first use): on the ctx's stream
+    // they would queue behind the new frame's stitch and pyramid, which the host does not need yet
+    hipStream_t mstream = nullptr;
+    hipEvent_t mwait_ev = nullptr;
+    // host time of the ctx's RegisterPbMap calls (ns): 0 waiting for the frames' PbMaps (GPU plane stage + host
+    // assembly), 1 match tables (upload, kernel, wait), 2 interpretation tree + ConsistencyTest, 3 calls; of its
+    // frames' assembly threads: 4 PbMap assembly after the GPU part, 5 frames
+    std::atomic<long long> host_ns[6] = {};
     IcpState* d_state = nullptr;
     double* d_partials = nullptr;
     unsigned* d_gticket = nullptr;   // group arrival counters of the ICP pass (R360_TICKET_GROUPS x 4 KB)
