@@ -456,35 +456,52 @@ __device__ __forceinline__ int block_min(int v, int* sh) {
     return v;
 }
 
-__device__ __forceinline__ float block_fminmax(float v, bool mx, float* sh) {
-    for (int o = 32; o > 0; o >>= 1) {
-        const float u = __shfl_xor(v, o, 64);
-        v = mx ? fmaxf(v, u) : fminf(v, u);
-    }
+// block min of v[0..2] and max of v[3..5] (one LDS round for all six); the result is valid in thread 0
+__device__ __forceinline__ void block_fminmax6(float (&v)[6], float (*sh)[6]) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+        for (int o = 32; o > 0; o >>= 1) {
+            const float u = __shfl_xor(v[k], o, 64);
+            v[k] = k >= 3 ? fmaxf(v[k], u) : fminf(v[k], u);
+        }
     __syncthreads();
-    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+    if ((threadIdx.x & 63) == 0)
+        for (int k = 0; k < 6; ++k) sh[threadIdx.x >> 6][k] = v[k];
     __syncthreads();
     if (threadIdx.x == 0)
-        for (int q = 1; q < (int)(blockDim.x >> 6); ++q) v = mx ? fmaxf(v, sh[q]) : fminf(v, sh[q]);
-    return v;
+        for (int q = 1; q < (int)(blockDim.x >> 6); ++q)
+            for (int k = 0; k < 6; ++k) v[k] = k >= 3 ? fmaxf(v[k], sh[q][k]) : fminf(v[k], sh[q][k]);
 }
 
 // Exact merge of a workgroup's partial moments into global accumulators: 64-bit atomic adds (two's complement,
 // order-free); an int128 sum is a low/high pair whose carry each adder derives from the old low word it got back,
-// so the pair ends at the exact total whatever the order.
-__device__ void moments_atomic_merge(r360p::Moments* dst, const r360p::Moments& m) {
-    auto add64 = [](long long* p, long long v) {
-        atomicAdd(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v);
-    };
-    add64(&dst->n, m.n);
-    for (int k = 0; k < 3; ++k) add64(&dst->s1[k], m.s1[k]);
-    for (int k = 0; k < 4; ++k) add64(&dst->c[k], m.c[k]);
-    for (int k = 0; k < 6; ++k) {
-        unsigned long long* w = reinterpret_cast<unsigned long long*>(&dst->s2[k]);
-        const unsigned long long lo = (unsigned long long)m.s2[k];
-        const unsigned long long hi = (unsigned long long)(m.s2[k] >> 64);
+// so the pair ends at the exact total whatever the order.  Called by every thread with the block total of
+// block_reduce_moments in thread 0: the 20 words go through LDS and 14 lanes of wave 0 add one word each (the six
+// returning low-word adds in one instruction: one memory round trip instead of six in sequence, which is what a
+// single lane walking the words cost, the compiler waiting for each returned value).
+__device__ void moments_atomic_merge(r360p::Moments* dst, const r360p::Moments& m, MomShared* sh) {
+    if (threadIdx.x == 0) {
+        sh->w[0][0] = m.n;
+        for (int k = 0; k < 3; ++k) sh->w[0][1 + k] = m.s1[k];
+        for (int k = 0; k < 6; ++k) {
+            sh->w[0][4 + 2 * k] = (long long)(unsigned long long)m.s2[k];
+            sh->w[0][5 + 2 * k] = (long long)(m.s2[k] >> 64);
+        }
+        for (int k = 0; k < 4; ++k) sh->w[0][16 + k] = m.c[k];
+    }
+    __syncthreads();
+    const int l = threadIdx.x;
+    if (l < 6) {
+        unsigned long long* w = reinterpret_cast<unsigned long long*>(&dst->s2[l]);
+        const unsigned long long lo = (unsigned long long)sh->w[0][4 + 2 * l];
+        const unsigned long long hi = (unsigned long long)sh->w[0][5 + 2 * l];
         const unsigned long long old = atomicAdd(w, lo);
         atomicAdd(w + 1, hi + (old + lo < old ? 1ull : 0ull));
+    } else if (l < 14) {
+        const int k = l - 6;   // n, s1[0..2], c[0..3]
+        long long* p = k == 0 ? &dst->n : k < 4 ? &dst->s1[k - 1] : &dst->c[k - 4];
+        const long long v = sh->w[0][k == 0 ? 0 : k < 4 ? k : 12 + k];
+        atomicAdd(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v);
     }
 }
 
@@ -538,10 +555,8 @@ __global__ void __launch_bounds__(LMOM_TPB) k_label_moments(const float4* __rest
     }
     first = block_min(first, smin);
     block_reduce_moments(m, &sh);
-    if (threadIdx.x == 0) {
-        moments_atomic_merge(mom + s * maxbig + b, m);
-        atomicMin(bfirst + s * maxbig + b, first);
-    }
+    if (threadIdx.x == 0) atomicMin(bfirst + s * maxbig + b, first);
+    moments_atomic_merge(mom + s * maxbig + b, m, &sh);
     __syncthreads();   // the LDS reduction scratch is reused by the next label
     }
 }
@@ -1660,7 +1675,7 @@ __global__ void __launch_bounds__(MS_TPB) k_model_stats(const float4* __restrict
                                                         const int* __restrict__ bfirst, int maxbig,
                                                         PlaneOut* __restrict__ out) {
     __shared__ MomShared sh;
-    __shared__ float sred[MOM_NW];
+    __shared__ float sred6[MOM_NW][6];
     const int s = blockIdx.y;
     const int nmod = nmodels[s];
     for (int m = blockIdx.x; m < nmod; m += gridDim.x) {
@@ -1698,11 +1713,11 @@ __global__ void __launch_bounds__(MS_TPB) k_model_stats(const float4* __restrict
             r360p::moments_add_rgb(mo, c[u].x, c[u].y, c[u].z);
         }
     }
-    for (int k = 0; k < 6; ++k) bx[k] = block_fminmax(bx[k], k >= 3, sred);
+    block_fminmax6(bx, sred6);
     block_reduce_moments(mo, &sh);
+    moments_atomic_merge(&out[s * R360_MAX_MODELS + m].stats, mo, &sh);
     if (threadIdx.x == 0) {
         PlaneOut& O = out[s * R360_MAX_MODELS + m];
-        moments_atomic_merge(&O.stats, mo);
         if (n > 0)
             for (int k = 0; k < 3; ++k) { atomic_fmin(&O.bmin[k], bx[k]); atomic_fmax(&O.bmax[k], bx[k + 3]); }
         if (blockIdx.z == 0) {

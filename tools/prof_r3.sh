@@ -37,6 +37,7 @@ python3 tools/profile_summary.py $OUT $OUT/summary > $OUT/summary.txt 2>&1
 python3 tools/hires_summary.py $OUT/hires $OUT/hires_bench.out > $OUT/summary/hires_pmc.json 2>&1
 T=$(ls $OUT/trace/*kernel_trace.csv 2>/dev/null | head -1)
 [ -n "$T" ] && python3 tools/busy.py $T 1000 > $OUT/summary/busy.txt 2>&1
+[ -n "$T" ] && python3 tools/kernel_area.py $T > $OUT/summary/area.txt 2>&1
 find $OUT -name "*kernel_trace.csv" -delete; find $OUT -name "*counter_collection.csv" -delete
 find $OUT -name "*.csv" -size +4M -delete
 echo profile rc=$rc
