@@ -485,6 +485,148 @@ __global__ void __launch_bounds__(NT_TPB) k_normals(const float4* __restrict__ c
     }
 }
 
+
+// k_normals with the window sums read from summed-area tables of the staged tile instead of summed over the
+// window: a table entry is a sum of at most (NT_SR x NT_SC) = 1728 central differences, each a multiple of 2^-36
+// below 2^5 in magnitude, so every entry (< 2^16) and every rectangle of entries is exact in double, and a window
+// sum S(y1,x1) - S(y0,x1) - S(y1,x0) + S(y0,x0) equals the direct sum bit for bit.  Per output pixel that is 4
+// lookups per channel instead of up to 81 float4 reads per difference image.  The tables (3 doubles + a count per
+// entry, leading zero row / column) are built for dx, used, then rebuilt for dy in the same 51 KB.
+constexpr int NS_W = NT_SC + 1, NS_H = NT_SR + 1;   // table size with the leading zero row / column
+struct SatShared { double v[3][NS_H * NS_W]; int c[NS_H * NS_W]; };
+
+__global__ void __launch_bounds__(NT_TPB) k_normals_sat(const float4* __restrict__ cloud, const float* __restrict__ dist,
+                                                       int w, int h, float4* __restrict__ nrm) {
+    __shared__ SatShared T;
+    const int s = blockIdx.z;
+    const int r0 = blockIdx.y * NT_R, c0 = blockIdx.x * NT_C;
+    const long N = (long)w * h;
+    const float4* P = cloud + (long)s * N;
+    const float nan = __builtin_nanf("");
+    // the thread's output pixels (column c, rows r0 + rr, rr = thread / NT_C + 4 j) and their windows
+    constexpr int PER = NT_R / (NT_TPB / NT_C);
+    const int c = c0 + (threadIdx.x & (NT_C - 1));
+    int rs_[PER];         // window size (0: no normal from the table path; -1: the global-memory path)
+    float4 pt[PER];
+    double g[2][PER][3];
+    unsigned cnt[2][PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int r = r0 + threadIdx.x / NT_C + j * (NT_TPB / NT_C);
+        rs_[j] = 0;
+        pt[j] = make_float4(nan, nan, nan, nan);
+        if (r >= h || c >= w) continue;
+        const int border = 8;
+        const float4 p = P[r * w + c];
+        pt[j] = p;
+        if (r >= border && r < h - border && c >= border && c < w - border && isfin(p.z)) {
+            const float dm = dist[(long)s * N + r * w + c];
+            const float lim = 8.0f + p.z / 10.0f;
+            const float smoothing = dm < lim ? dm : lim;
+            if (smoothing > 2.0f) {
+                const int rs = (int)smoothing;
+                rs_[j] = rs <= 2 * NT_H + 1 ? rs : -1;
+            }
+        }
+    }
+#pragma unroll
+    for (int ph = 0; ph < 2; ++ph) {   // 0: x differences (right - left), 1: y differences (down - up)
+        // stage the differences at table position (y + 1, x + 1); row 0 and column 0 are zero
+        for (int k = threadIdx.x; k < NS_H * NS_W; k += NT_TPB) {
+            const int ty = k / NS_W, tx = k - ty * NS_W;
+            double d0 = 0.0, d1 = 0.0, d2 = 0.0;
+            int n = 0;
+            if (ty > 0 && tx > 0) {
+                const int yy = r0 - NT_H + ty - 1, xx = c0 - NT_H + tx - 1;
+                n = 1;   // outside [1, h-2] x [1, w-2]: zero and counted, as k_normals
+                if (yy >= 1 && yy <= h - 2 && xx >= 1 && xx <= w - 2) {
+                    const int q = yy * w + xx;
+                    const float4 a = ph ? P[q + w] : P[q + 1], b = ph ? P[q - w] : P[q - 1];
+                    const float e0 = a.x - b.x, e1 = a.y - b.y, e2 = a.z - b.z;
+                    if (isfin(e0 + e1 + e2)) { d0 = e0; d1 = e1; d2 = e2; } else n = 0;
+                }
+            }
+            T.v[0][k] = d0; T.v[1][k] = d1; T.v[2][k] = d2; T.c[k] = n;
+        }
+        __syncthreads();
+        // row prefix sums (one thread per (row, channel)), then column prefix sums (one per (column, channel))
+        for (int t = threadIdx.x; t < NS_H * 4; t += NT_TPB) {
+            const int row = t >> 2, ch = t & 3;
+            if (ch < 3) {
+                double* v = T.v[ch] + row * NS_W;
+                double acc = 0.0;
+                for (int x = 0; x < NS_W; ++x) { acc += v[x]; v[x] = acc; }
+            } else {
+                int* v = T.c + row * NS_W;
+                int acc = 0;
+                for (int x = 0; x < NS_W; ++x) { acc += v[x]; v[x] = acc; }
+            }
+        }
+        __syncthreads();
+        for (int t = threadIdx.x; t < NS_W * 4; t += NT_TPB) {
+            const int col = t >> 2, ch = t & 3;
+            if (ch < 3) {
+                double* v = T.v[ch] + col;
+                double acc = 0.0;
+                for (int y = 0; y < NS_H; ++y) { acc += v[y * NS_W]; v[y * NS_W] = acc; }
+            } else {
+                int* v = T.c + col;
+                int acc = 0;
+                for (int y = 0; y < NS_H; ++y) { acc += v[y * NS_W]; v[y * NS_W] = acc; }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            g[ph][j][0] = g[ph][j][1] = g[ph][j][2] = 0.0;
+            cnt[ph][j] = 0;
+            const int rs = rs_[j];
+            if (rs <= 0) continue;
+            const int r = r0 + threadIdx.x / NT_C + j * (NT_TPB / NT_C);
+            // window rows [r - rs/2, +rs), columns [c - rs/2, +rs) in table coordinates (+ NT_H - r0 / c0)
+            const int y0 = r - rs / 2 - (r0 - NT_H), x0 = c - rs / 2 - (c0 - NT_H);
+            const int i00 = y0 * NS_W + x0, i01 = y0 * NS_W + x0 + rs, i10 = (y0 + rs) * NS_W + x0,
+                      i11 = (y0 + rs) * NS_W + x0 + rs;
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) {
+                const double* v = T.v[ch];
+                g[ph][j][ch] = ((v[i11] - v[i01]) - v[i10]) + v[i00];
+            }
+            cnt[ph][j] = (unsigned)(((T.c[i11] - T.c[i01]) - T.c[i10]) + T.c[i00]);
+        }
+        __syncthreads();   // the tables are rebuilt for the next phase
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const int r = r0 + threadIdx.x / NT_C + j * (NT_TPB / NT_C);
+        if (r >= h || c >= w) continue;
+        float4 o = make_float4(nan, nan, nan, nan);
+        const float4 p = pt[j];
+        if (rs_[j] > 0) {
+            normal_out(g[0][j], g[1][j], cnt[0][j], cnt[1][j], p, o);
+        } else if (rs_[j] < 0) {   // window wider than the halo: summed from global memory as k_normals
+            const float dm = dist[(long)s * N + r * w + c];
+            const float lim = 8.0f + p.z / 10.0f;
+            const int rs = (int)(dm < lim ? dm : lim), rs2 = rs / 2;
+            const int sx = c - rs2, sy = r - rs2;
+            double gx[3] = {0, 0, 0}, gy[3] = {0, 0, 0};
+            unsigned cx = 0, cy = 0;
+            for (int yy = sy; yy < sy + rs; ++yy)
+                for (int xx = sx; xx < sx + rs; ++xx) {
+                    if (yy < 1 || yy > h - 2 || xx < 1 || xx > w - 2) { ++cx; ++cy; continue; }  // zero, finite
+                    const int q = yy * w + xx;
+                    const float4 a = P[q + 1], b = P[q - 1], u = P[q - w], d = P[q + w];
+                    const float dx0 = a.x - b.x, dx1 = a.y - b.y, dx2 = a.z - b.z;
+                    const float dy0 = d.x - u.x, dy1 = d.y - u.y, dy2 = d.z - u.z;
+                    if (isfin(dx0 + dx1 + dx2)) { gx[0] += dx0; gx[1] += dx1; gx[2] += dx2; ++cx; }
+                    if (isfin(dy0 + dy1 + dy2)) { gy[0] += dy0; gy[1] += dy1; gy[2] += dy2; ++cy; }
+                }
+            normal_out(gx, gy, cx, cy, p, o);
+        }
+        nrm[(long)s * N + r * w + c] = o;
+    }
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ launchers
@@ -540,7 +682,13 @@ int launch_cloud_normals(r360_frame* f) {
     timing_end(f->ctx, slot);
     R360_HIP(hipGetLastError());
     slot = timing_begin(f->ctx, "k_normals");
-    hipLaunchKernelGGL(k_normals, dim3((w + NT_C - 1) / NT_C, (h + NT_R - 1) / NT_R, 8), dim3(NT_TPB), 0, st, P.cloud,
+    // summed-area-table windows (default; R360_NORMALS_SAT=0: the direct window sums of k_normals)
+    static const int nsat = getenv("R360_NORMALS_SAT") ? atoi(getenv("R360_NORMALS_SAT")) : 1;
+    if (nsat)
+        hipLaunchKernelGGL(k_normals_sat, dim3((w + NT_C - 1) / NT_C, (h + NT_R - 1) / NT_R, 8), dim3(NT_TPB), 0, st, P.cloud,
+                       P.dist, w, h, P.nrm);
+    else
+        hipLaunchKernelGGL(k_normals, dim3((w + NT_C - 1) / NT_C, (h + NT_R - 1) / NT_R, 8), dim3(NT_TPB), 0, st, P.cloud,
                        P.dist, w, h, P.nrm);
     timing_end(f->ctx, slot);
     R360_HIP(hipGetLastError());

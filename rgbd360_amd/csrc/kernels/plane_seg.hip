@@ -539,7 +539,7 @@ __global__ void __launch_bounds__(LMOM_TPB) k_label_moments(const float4* __rest
     r360p::Moments m;
     r360p::moments_zero(m);
     int first = N;
-    for (int k0 = blockIdx.z * MOM_UNROLL * LMOM_TPB + threadIdx.x; k0 < n; k0 += LMOM_SPLIT * MOM_UNROLL * LMOM_TPB) {
+    for (int k0 = blockIdx.z * MOM_UNROLL * LMOM_TPB + threadIdx.x; k0 < n; k0 += gridDim.z * MOM_UNROLL * LMOM_TPB) {
         int j[MOM_UNROLL];
         float4 p[MOM_UNROLL];
 #pragma unroll
@@ -1688,7 +1688,7 @@ __global__ void __launch_bounds__(MS_TPB) k_model_stats(const float4* __restrict
     r360p::Moments mo;
     r360p::moments_zero(mo);
     float bx[6] = {3.4e38f, 3.4e38f, 3.4e38f, -3.4e38f, -3.4e38f, -3.4e38f};   // local-frame bounds
-    for (int k0 = blockIdx.z * MOM_UNROLL * MS_TPB + threadIdx.x; k0 < n; k0 += MS_SPLIT * MOM_UNROLL * MS_TPB) {
+    for (int k0 = blockIdx.z * MOM_UNROLL * MS_TPB + threadIdx.x; k0 < n; k0 += gridDim.z * MOM_UNROLL * MS_TPB) {
         int j[MOM_UNROLL];
         float4 p[MOM_UNROLL];
         uchar4 c[MOM_UNROLL];
@@ -1915,8 +1915,8 @@ __global__ void __launch_bounds__(TR_TPB) k_trace(const uint8_t* __restrict__ nb
 }
 
 // contour total of the frame (profiling / pool accounting), and the voxel hash table size for this
-// frame: a power of two >= 2x the inliers of the regions without a contour (their refined region
-// sizes bound the number of distinct voxels), capped by the allocation
+// frame: a power of two >= 2x a bound on the distinct voxels of the regions without a contour (per region the
+// smaller of its inliers and its bounding box's voxels), capped by the allocation
 // one workgroup of 512 threads, thread = (sensor, model)
 __global__ void __launch_bounds__(512) k_alloc(const int* __restrict__ nmodels, const PlaneOut* __restrict__ out,
                                                const int* __restrict__ mcnt, unsigned long long cap,
@@ -1927,7 +1927,15 @@ __global__ void __launch_bounds__(512) k_alloc(const int* __restrict__ nmodels, 
     if (m < nmodels[s]) {
         const int nc = out[q].n_contour;
         co = nc;
-        if (nc == 0) cand = mcnt[q];
+        if (nc == 0) {
+            // distinct voxels of the region: at most its inliers and at most the voxels of its bounding box
+            const float inv = 1.0f / 0.05f;
+            double vol = 1.0;
+            for (int k = 0; k < 3; ++k)
+                vol *= (double)((long long)floorf(out[q].bmax[k] * inv) - (long long)floorf(out[q].bmin[k] * inv) + 1);
+            cand = mcnt[q];
+            if (vol >= 1.0 && vol < (double)cand) cand = (long)vol;
+        }
     }
     for (int o = 32; o > 0; o >>= 1) { co += __shfl_xor(co, o, 64); cand += __shfl_xor(cand, o, 64); }
     if ((q & 63) == 0) { sco[q >> 6] = co; sca[q >> 6] = cand; }
@@ -1939,7 +1947,7 @@ __global__ void __launch_bounds__(512) k_alloc(const int* __restrict__ nmodels, 
     unsigned long long t = 1024;
     while (t < 2ull * (unsigned long long)cand && t < cap) t <<= 1;
     totals[2] = (long)(t - 1);   // hash mask
-    totals[3] = cand;            // inliers of the regions without a contour (0: the voxel stage has no work)
+    totals[3] = cand;            // bound on the voxels of the regions without a contour (0: no voxel stage work)
 }
 
 __global__ void k_vox_clear(VoxCell* __restrict__ tab, const long* __restrict__ totals) {
@@ -1964,7 +1972,8 @@ __device__ __forceinline__ unsigned long long vhash(unsigned long long tag, unsi
 // rows of a sensor, so its points fall into a few dozen voxels), sums them per (region, voxel) in an LDS hash
 // table (exact double sums: order-free), then flushes one update per voxel it touched into the global table.
 // New voxels are counted per region in LDS and flushed once per workgroup.
-constexpr int VOX_TPB = 256, VOX_PX = 1024, VOX_LT = 256;
+constexpr int VOX_TPB = 256, VOX_PX = 1024, VOX_LT = 512;   // VOX_PX: default pixels per workgroup (2048: 3.4x, 4096:
+                                                            // 15x slower, profiles/r3_planes)
 
 __device__ __forceinline__ void vox_global_add(VoxCell* __restrict__ tab, unsigned long long mask,
                                                unsigned long long tag, double x, double y, double z, unsigned n,
@@ -1986,18 +1995,22 @@ __device__ __forceinline__ void vox_global_add(VoxCell* __restrict__ tab, unsign
 __global__ void __launch_bounds__(VOX_TPB) k_vox_hash(const float4* __restrict__ cloud, const int8_t* __restrict__ state,
                                                      int N, const int* __restrict__ nmodels, PlaneOut* __restrict__ out,
                                                      VoxCell* __restrict__ tab, const long* __restrict__ totals,
-                                                     int* __restrict__ err) {
+                                                     int* __restrict__ err, int px) {
     if (totals[3] == 0) return;
-    __shared__ int nnew[8 * R360_MAX_MODELS];
-    __shared__ unsigned char cand[8 * R360_MAX_MODELS];
-    __shared__ long long bnd[8 * R360_MAX_MODELS][5];   // voxel origin b0..b2 and extents d0, d1 of a region
+    __shared__ int nnew_[2 * R360_MAX_MODELS];
+    __shared__ unsigned char cand_[2 * R360_MAX_MODELS];
+    __shared__ long long bnd_[2 * R360_MAX_MODELS][5];   // voxel origin b0..b2 and extents d0, d1 of a region
     __shared__ unsigned long long ltag[VOX_LT];
     __shared__ double lsum[3][VOX_LT];
     __shared__ unsigned lcnt[VOX_LT];
     __shared__ int any;
     const long total = 8L * N;
-    const long i0 = (long)blockIdx.x * VOX_PX;
-    const int s0 = (int)(i0 / N), s1 = (int)(min(total, i0 + VOX_PX) - 1) / N;   // sensors of this block
+    const long i0 = (long)blockIdx.x * px;
+    const int s0 = (int)(i0 / N), s1 = (int)(min(total, i0 + px) - 1) / N;   // sensors of this block (px <= N)
+    // the block's regions, indexed by (sensor, model) - s0 * R360_MAX_MODELS
+    int* nnew = nnew_ - s0 * R360_MAX_MODELS;
+    unsigned char* cand = cand_ - s0 * R360_MAX_MODELS;
+    long long (*bnd)[5] = bnd_ - s0 * R360_MAX_MODELS;
     const float inv = 1.0f / 0.05f;
     if (threadIdx.x == 0) any = 0;
     for (int q = threadIdx.x; q < VOX_LT; q += VOX_TPB) {
@@ -2021,7 +2034,7 @@ __global__ void __launch_bounds__(VOX_TPB) k_vox_hash(const float4* __restrict__
     __syncthreads();
     if (!any) return;
     const unsigned long long mask = (unsigned long long)totals[2];
-    for (int k = threadIdx.x; k < VOX_PX; k += VOX_TPB) {
+    for (int k = threadIdx.x; k < px; k += VOX_TPB) {
         const long i = i0 + k;
         if (i >= total) break;
         const int m = state[i];
@@ -2242,7 +2255,12 @@ int launch_segmentation(r360_frame* f) {
     if (N < PS_PX) { r360_set_error("segmentation: sensor of %d points too small", N); return -1; }
     const int pblocks = (int)((total + PS_PX - 1) / PS_PX);
     hipLaunchKernelGGL(k_label_scatter, dim3(pblocks), dim3(PS_TPB), 0, st, P.lab, N, bmap, boff, bcur, P.blist, mmap);
-    hipLaunchKernelGGL(k_label_moments, dim3(LMOM_GX, 8, LMOM_SPLIT), dim3(LMOM_TPB), 0, st, P.cloud, P.cnt, N, P.big, P.nbig,
+    // grid shapes of the two moment kernels (R360_LMOM_GX / _SPLIT, R360_MS_GX / _SPLIT: experiments)
+    static const int lm_gx = getenv("R360_LMOM_GX") ? atoi(getenv("R360_LMOM_GX")) : LMOM_GX;
+    static const int lm_sp = getenv("R360_LMOM_SPLIT") ? atoi(getenv("R360_LMOM_SPLIT")) : LMOM_SPLIT;
+    static const int ms_gx = getenv("R360_MS_GX") ? atoi(getenv("R360_MS_GX")) : 16;
+    static const int ms_sp = getenv("R360_MS_SPLIT") ? atoi(getenv("R360_MS_SPLIT")) : MS_SPLIT;
+    hipLaunchKernelGGL(k_label_moments, dim3(lm_gx, 8, lm_sp), dim3(LMOM_TPB), 0, st, P.cloud, P.cnt, N, P.big, P.nbig,
                        R360_MAX_BIG, boff, P.blist, P.mom, bfirst);
     hipLaunchKernelGGL(k_plane_fit, dim3(8), dim3(PF_TPB), 0, st, P.mom, P.big, P.nbig, R360_MAX_BIG, 0.001f, P.models,
                        P.nmodels, P.err, N, mmap, mcnt);
@@ -2260,7 +2278,7 @@ int launch_segmentation(r360_frame* f) {
     slot = timing_begin(ctx, "k_model_stats");
     hipLaunchKernelGGL(k_model_count, dim3(pblocks), dim3(PS_TPB), 0, st, P.labf, N, mmap, mcnt, P.out);
     hipLaunchKernelGGL(k_model_scatter, dim3(pblocks), dim3(PS_TPB), 0, st, P.labf, N, mmap, mcnt, mcur, P.mlist);
-    hipLaunchKernelGGL(k_model_stats, dim3(16, 8, MS_SPLIT), dim3(MS_TPB), 0, st, P.cloud, P.rgb, N, P.models,
+    hipLaunchKernelGGL(k_model_stats, dim3(ms_gx, 8, ms_sp), dim3(MS_TPB), 0, st, P.cloud, P.rgb, N, P.models,
                        P.nmodels, f->calib->d_rt, mcnt, P.mlist, bfirst, R360_MAX_BIG, P.out);
     // the refinement's closeness masks are dead here: their storage holds the neighbour masks
     uint8_t* nbm = reinterpret_cast<uint8_t*>(P.mask);
@@ -2279,8 +2297,10 @@ int launch_segmentation(r360_frame* f) {
     slot = timing_begin(ctx, "k_voxel");
     // the voxel kernels exit at entry when no region lacks a contour (totals[3] == 0, the usual case)
     hipLaunchKernelGGL(k_vox_clear, dim3(256), dim3(256), 0, st, ctx->d_vhash, P.totals);
-    hipLaunchKernelGGL(k_vox_hash, dim3((unsigned)((total + VOX_PX - 1) / VOX_PX)), dim3(VOX_TPB), 0, st, P.cloud,
-                       P.state, N, P.nmodels, P.out, ctx->d_vhash, P.totals, P.err);
+    static const int vox_px_env = getenv("R360_VOX_PX") ? atoi(getenv("R360_VOX_PX")) : VOX_PX;   // experiments
+    const int vox_px = std::min(vox_px_env, N);   // a block spans at most two sensors
+    hipLaunchKernelGGL(k_vox_hash, dim3((unsigned)((total + vox_px - 1) / vox_px)), dim3(VOX_TPB), 0, st, P.cloud,
+                       P.state, N, P.nmodels, P.out, ctx->d_vhash, P.totals, P.err, vox_px);
     hipLaunchKernelGGL(k_vox_alloc, dim3(1), dim3(512), 0, st, P.nmodels, P.out, P.totals, P.vox_cap, P.err);
     hipLaunchKernelGGL(k_vox_compact, dim3(VOXC_BLOCKS), dim3(VOXC_TPB), 0, st, ctx->d_vhash, P.totals, P.out, P.vox,
                        P.vox_cap);
