@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <cmath>
@@ -648,12 +649,20 @@ int gpu_tables(r360_ctx* ctx, const std::vector<HPlane>& S, const std::vector<in
     for (int i = 0; i < ns; ++i) pack_desc(S[si[i]], &desc[16 * i]);
     for (int j = 0; j < nt; ++j) pack_desc(T[ti[j]], &desc[16 * (ns + j)]);
     if (!ctx->mstream) {
-        // the device's highest priority: a few microseconds of work that the calling thread waits for, which
-        // at normal priority queued for milliseconds behind the dense queue's launches (2.4 ms per call in the
-        // default bench, profiles/r3_host)
-        int least = 0, greatest = 0;
-        R360_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-        R360_HIP(hipStreamCreateWithPriority(&ctx->mstream, hipStreamNonBlocking, greatest));
+        // one stream per device at the highest priority, shared by every context: a few microseconds of work that
+        // the calling thread waits for, which at normal priority queued for milliseconds behind the dense queue's
+        // launches (2.4 ms per call in the default bench, profiles/r3_host).  Shared, not one per context: a
+        // second stream per pipeline would take more hardware queues than GPU_MAX_HW_QUEUES provides.
+        static std::mutex m;
+        static hipStream_t dev_stream[64] = {};
+        std::lock_guard<std::mutex> lk(m);
+        if (ctx->device < 0 || ctx->device >= 64) { r360_set_error("device ordinal out of range"); return -2; }
+        if (!dev_stream[ctx->device]) {
+            int least = 0, greatest = 0;
+            R360_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+            R360_HIP(hipStreamCreateWithPriority(&dev_stream[ctx->device], hipStreamNonBlocking, greatest));
+        }
+        ctx->mstream = dev_stream[ctx->device];
         R360_HIP(hipEventCreateWithFlags(&ctx->mwait_ev, hipEventDisableTiming | hipEventBlockingSync));
     }
     hipStream_t st = ctx->mstream;

@@ -169,7 +169,7 @@ extern "C" void r360_ctx_destroy(r360_ctx* c) {
     hipStreamSynchronize(c->stream);
     for (auto e : c->ev_pool) hipEventDestroy(e);
     hipEventDestroy(c->wait_ev);
-    if (c->mstream) { hipStreamDestroy(c->mstream); hipEventDestroy(c->mwait_ev); }
+    if (c->mwait_ev) hipEventDestroy(c->mwait_ev);   // mstream is the device's shared match stream
     hipFree(c->d_state);
     hipFree(c->d_partials);
     hipFree(c->d_gticket);

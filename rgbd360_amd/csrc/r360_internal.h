@@ -222,8 +222,8 @@ struct r360_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t wait_ev = nullptr;   // blocking-sync event: host waits sleep instead of spinning
-    // RegisterPbMap's match tables run on a stream of their own (created on first use): on the ctx's stream
-    // they would queue behind the new frame's stitch and pyramid, which the host does not need yet
+    // RegisterPbMap's match tables run on the device's shared high-priority match stream (pbmap.cpp): on the
+    // ctx's stream they would queue behind the new frame's stitch and pyramid, which the host does not need yet
     hipStream_t mstream = nullptr;
     hipEvent_t mwait_ev = nullptr;
     // host time of the ctx's RegisterPbMap calls (ns): 0 waiting for the frames' PbMaps (GPU plane stage + host
