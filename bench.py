@@ -281,7 +281,10 @@ def config5_leg(device, rt8, pairs=48, iters0=50, pipelines=8, depth=2, repeats=
     }
 
 
-def main():
+def main(argv=None, runner_factory=None):
+    """argv: the command line (sys.argv[1:] by default).  runner_factory(device, rows, cols, P, params, **kw): the
+    pipelines' runner (odometry.SequenceRunner by default; the CPU tests pass a stand-in that fills the pair records
+    without a GPU, to drive this function's shard / gather / max-over-ranks / composition path over gloo)."""
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -310,7 +313,7 @@ def main():
                     help="skip the lone-pipeline rerun after the timed region (profiling: the trace then holds only "
                          "the warmup and timed launches)")
     ap.add_argument("--eval-probe", action="store_true", help="diagnostic: also time the level-0 pass in eval mode")
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -352,9 +355,10 @@ def main():
     params.n_pyr = 5
     params.std_dev_photo = np.float32(3.0 / 255)       # OdometryRGBD360.cpp:92-95
     params.fixed_iters_level0 = args.iters0
-    runner = OD.SequenceRunner(local, args.rows, args.cols, P, params, planes=args.workload != "dense",
-                               dense_only=args.workload == "dense", queue=args.queue,
-                               planes_only=args.workload == "planes", depth=args.depth)
+    runner = (runner_factory or OD.SequenceRunner)(local, args.rows, args.cols, P, params,
+                                                   planes=args.workload != "dense", dense_only=args.workload == "dense",
+                                                   queue=args.queue, planes_only=args.workload == "planes",
+                                                   depth=args.depth)
     ctxs = runner.ctxs + ([runner.queue.ctx] if runner.queue else [])
     dense_ctx = runner.queue.ctx if runner.queue else ctxs[0]   # where pipeline 0's alignments run
 

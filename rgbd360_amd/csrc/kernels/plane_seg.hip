@@ -4,14 +4,14 @@
 //                  band, then lock-free global union of the band-crossing edges; roots = smallest
 //                  raster index, labels numbered in raster order of their roots — the reference's
 //                  run-id compaction order)
-//   k_big_list     labels with > 80 points, in order; k_label_scatter groups their pixels
-//   k_label_moments  exact moments per large label (int64/int128 sums over its pixel list)
+//   k_big_list     labels with > 80 points, in order
+//   k_gm<false>    exact moments per large label (int64/int128 sums), pixel order, no pixel lists
 //   k_plane_fit    eigen33 plane fit, curvature test and the accumulating viewpoint of segment()
 //   k_refine       the two raster sweeps of refine(): one wave per sensor walks the rows; within a row
 //                  the left-to-right (right-to-left) label chains are resolved with wave scans over
 //                  per-lane chunk summaries; closeness to every model is precomputed per pixel as a
 //                  bit mask (k_refine_init)
-//   k_model_stats  final inlier moments (rig frame) + colour sums + the region's first pixel
+//   k_gm<true>     final inlier moments (rig frame) + colour sums + bounds per refined region (folded by k_nbmask)
 //   k_trace        findLabeledRegionBoundary (Moore-neighbour trace) over per-pixel neighbour masks
 //   k_vox_*        VoxelGrid of regions without a contour (Frame360.h:1017-1026): (region, voxel) hash
 //                  table with exact double sums, compacted into per-region voxel lists
@@ -237,19 +237,34 @@ __global__ void k_ccl_label(const int* __restrict__ root, const int* __restrict_
     }
 }
 
-// labels with more than min_inliers points, in increasing label order (one workgroup per sensor);
-// also the label -> large-label index map and each large label's offset in the grouped pixel list.  Same two
-// passes as k_ccl_number: flag bytes of the labels' counts, then contiguous runs per thread.
+// ------------------------------------------------------------------ moments
+// float min / max through integer atomics (the accumulators start at +inf / -inf; -0 orders below +0)
+__device__ __forceinline__ void atomic_fmin(float* p, float v) {
+    if (v >= 0.f) atomicMin(reinterpret_cast<int*>(p), __float_as_int(v));
+    else atomicMax(reinterpret_cast<unsigned*>(p), __float_as_uint(v));
+}
+__device__ __forceinline__ void atomic_fmax(float* p, float v) {
+    if (v >= 0.f) atomicMax(reinterpret_cast<int*>(p), __float_as_int(v));
+    else atomicMin(reinterpret_cast<unsigned*>(p), __float_as_uint(v));
+}
+
+__device__ __forceinline__ void add128(unsigned long long* p, r360p::i128 v) {
+    const unsigned long long lo = (unsigned long long)v, hi = (unsigned long long)(v >> 64);
+    const unsigned long long old = atomicAdd(p, lo);
+    atomicAdd(p + 1, hi + (old + lo < old ? 1ull : 0ull));
+}
+
+// labels with more than min_inliers points, in increasing label order (one workgroup per sensor), and the
+// label -> large-label index map.  Same two passes as k_ccl_number: flag bytes of the labels' counts, then
+// contiguous runs per thread.  Also zeroes the large labels' moment accumulators k_gm<false> adds into.
 __global__ void __launch_bounds__(NUM_TPB) k_big_list(const int* __restrict__ cnt, const int* __restrict__ nlab, int N,
                                                       int min_inliers, int* __restrict__ big, int* __restrict__ nbig,
                                                       int maxbig, int* __restrict__ err, int* __restrict__ bmap,
-                                                      int* __restrict__ boff, r360p::Moments* __restrict__ mom,
-                                                      int* __restrict__ bfirst, int* __restrict__ bcur) {
+                                                      r360p::Moments* __restrict__ mom, int* __restrict__ bfirst) {
     __shared__ int sh[17];
     __shared__ unsigned char F[NUM_MAXQ];
     const int s = blockIdx.x;
     const int n = nlab[s];
-    for (int q = threadIdx.x; q < maxbig; q += NUM_TPB) bcur[s * maxbig + q] = 0;   // k_label_scatter's cursors
     const long base = (long)s * N;
     const int nq = (n + SCAN_V - 1) / SCAN_V;
     // whole flag bytes with two 16-byte loads (the sensor's slice starts 32-byte aligned when N % 8 == 0)
@@ -281,19 +296,10 @@ __global__ void __launch_bounds__(NUM_TPB) k_big_list(const int* __restrict__ cn
     __syncthreads();
     const int per = (nq + NUM_TPB - 1) / NUM_TPB;
     const int q0 = threadIdx.x * per, q1 = min(nq, q0 + per);
-    int nf = 0, nc = 0;
-    for (int q = q0; q < q1; ++q) {
-        unsigned f = F[q];
-        nf += __popc(f);
-        while (f) {
-            const int v = __ffs(f) - 1;
-            f &= f - 1;
-            nc += cnt[base + q * SCAN_V + v];
-        }
-    }
-    int tot, ctot;
+    int nf = 0;
+    for (int q = q0; q < q1; ++q) nf += __popc((unsigned)F[q]);
+    int tot;
     int b = block_exscan(nf, sh, tot);
-    int co = block_exscan(nc, sh, ctot);
     for (int q = q0; q < q1; ++q) {
         unsigned f = F[q];
         while (f) {
@@ -301,19 +307,14 @@ __global__ void __launch_bounds__(NUM_TPB) k_big_list(const int* __restrict__ cn
             f &= f - 1;
             const int j = q * SCAN_V + v;
             bmap[base + j] = b < maxbig ? b : -1;
-            if (b < maxbig) {
-                big[s * maxbig + b] = j;
-                boff[s * maxbig + b] = co;
-            }
+            if (b < maxbig) big[s * maxbig + b] = j;
             ++b;
-            co += cnt[base + j];
         }
     }
     if (threadIdx.x == 0) {
         nbig[s] = tot < maxbig ? tot : maxbig;
         if (tot > maxbig) atomicOr(err, 2);
     }
-    // k_label_moments merges its workgroups' partial sums into zeroed accumulators
     const int nb = tot < maxbig ? tot : maxbig;
     for (int q = threadIdx.x; q < nb; q += blockDim.x) {
         r360p::moments_zero(mom[s * maxbig + q]);
@@ -321,243 +322,263 @@ __global__ void __launch_bounds__(NUM_TPB) k_big_list(const int* __restrict__ cn
     }
 }
 
-// Block-privatised grouping: a workgroup takes PS_PX consecutive pixels (4 per thread; they cover at most
-// two sensors, PS_PX <= N), counts its keys in an LDS histogram over the keys of those sensors, reserves one
-// slot range per key with a single global atomic, and places its pixels with LDS atomics.  Replaces a global
-// returning atomic per (wave, key).  Order inside a key's slice is free (see the users).
-constexpr int PS_TPB = 256, PS_PX = 4 * PS_TPB;
+// ------------------------------------------------------------------ pixel-order grouped moments
+// The moments of every large label (k_gm<false>) and of every refined model region (k_gm<true>) straight from the
+// label images, with no grouped pixel list: a workgroup streams a contiguous pixel range, each wave a contiguous
+// quarter of it in chunks of 64 consecutive pixels, whose labels, keys and points it loads up front.  A chunk's
+// pixels form runs of equal keys (raster order: a few per chunk); one segmented inclusive scan across the wave sums
+// every run at once, and the last lane of each run adds the run's sums into a workgroup table in LDS (so one LDS
+// deposit per run instead of a conflicting atomic per pixel).  The table (GM_SLOTS open-addressed slots) goes to
+// the global accumulators at the end, 14 lanes per slot; a key that finds no free slot is merged into the global
+// accumulators directly.  Global atomics execute at the memory side, and a planar region spans hundreds of
+// workgroups: the region accumulators are kept in GM_COPIES copies (workgroup x adds into copy x % GM_COPIES) that
+// k_nbmask folds into the region records, so that no word takes more than 1/8 of the adds.  Exact integer sums
+// (int128 as a low / high pair whose carry each adder derives from the old low word it got back) and min / max: the
+// result is independent of the grouping, bit for bit the same as summing each region's pixels in any order.
+constexpr int GM_TPB = 256, GM_SLOTS = 64, GM_PX = 512, GM_COPIES = R360_GM_COPIES;
 
-template <int BINS>   // keys per sensor
-__device__ void priv_count(const int (&key)[4], int s0, int* __restrict__ hist, int* __restrict__ gcnt) {
-    for (int q = threadIdx.x; q < 2 * BINS; q += PS_TPB) hist[q] = 0;
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-        if (key[k] >= 0) atomicAdd(&hist[key[k] - s0 * BINS], 1);
-    __syncthreads();
-    for (int q = threadIdx.x; q < 2 * BINS; q += PS_TPB)
-        if (hist[q] && s0 * BINS + q < 8 * BINS) atomicAdd(gcnt + s0 * BINS + q, hist[q]);
-}
 
-// returns each pixel's slot inside its key's slice (gcur: running fill per key, zeroed beforehand)
-template <int BINS>
-__device__ void priv_slots(const int (&key)[4], int s0, int* __restrict__ hist, int* __restrict__ base,
-                           int* __restrict__ gcur, int (&pos)[4]) {
-    for (int q = threadIdx.x; q < 2 * BINS; q += PS_TPB) hist[q] = 0;
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-        if (key[k] >= 0) atomicAdd(&hist[key[k] - s0 * BINS], 1);
-    __syncthreads();
-    for (int q = threadIdx.x; q < 2 * BINS; q += PS_TPB) {
-        base[q] = (hist[q] && s0 * BINS + q < 8 * BINS) ? atomicAdd(gcur + s0 * BINS + q, hist[q]) : 0;
-        hist[q] = 0;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int q = key[k] - s0 * BINS;
-        pos[k] = key[k] >= 0 ? base[q] + atomicAdd(&hist[q], 1) : 0;
-    }
-}
-
-// pixels of every large label into its slice of the grouped list (order inside a slice is free: the
-// moments are exact integer sums and the first pixel is a minimum)
-// also clears the label -> model map k_plane_fit fills (its storage, root, is dead after k_ccl_label)
-__global__ void __launch_bounds__(PS_TPB) k_label_scatter(const int* __restrict__ lab, int N, const int* __restrict__ bmap,
-                                                          const int* __restrict__ boff, int* __restrict__ bcur,
-                                                          int* __restrict__ blist, int* __restrict__ mmap) {
-    __shared__ int hist[2 * R360_MAX_BIG], base[2 * R360_MAX_BIG];
-    const long total = 8L * N, b0 = (long)blockIdx.x * PS_PX;
-    const int s0 = (int)(b0 / N);
-    int key[4], j[4], s[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const long i = b0 + k * PS_TPB + threadIdx.x;
-        key[k] = -1; j[k] = 0; s[k] = 0;
-        if (i < total) {
-            mmap[i] = -1;
-            s[k] = (int)(i / N);
-            j[k] = (int)(i - (long)s[k] * N);
-            const int L = lab[i];
-            if (L >= 0) {
-                const int b = bmap[(long)s[k] * N + L];
-                if (b >= 0) key[k] = s[k] * R360_MAX_BIG + b;
-            }
-        }
-    }
-    int pos[4];
-    priv_slots<R360_MAX_BIG>(key, s0, hist, base, bcur, pos);
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-        if (key[k] >= 0) blist[(long)s[k] * N + boff[key[k]] + pos[k]] = j[k];
-}
-
-// ------------------------------------------------------------------ moments
-constexpr int MOM_TPB = 1024;
-constexpr int MOM_NW = MOM_TPB / 64;
-constexpr int MOM_UNROLL = 4;           // independent list entries per thread in flight
-
-struct MomShared {
-    long long w[MOM_NW][20];
+struct GmShared {
+    int key[GM_SLOTS];
+    unsigned long long w[GM_SLOTS][20];   // n, s1[3], s2 (lo, hi) x 6, c[4]
+    float b[GM_SLOTS][6];                 // model regions: local-frame min xyz, max xyz
+    int first[GM_SLOTS];                  // large labels: first pixel
 };
 
-__device__ __forceinline__ long long wave_sum64(long long x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-    return x;
+struct GmAcc {   // one lane's sums for one key
+    long long n, s1[3], c[4];
+    r360p::i128 s2[6];
+    float b[6];
+    int first;
+};
+
+__device__ __forceinline__ void gm_zero(GmAcc& a) {
+    a.n = 0;
+    a.first = 0x7fffffff;
+    for (int k = 0; k < 3; ++k) a.s1[k] = 0;
+    for (int k = 0; k < 4; ++k) a.c[k] = 0;
+    for (int k = 0; k < 6; ++k) { a.s2[k] = 0; a.b[k] = k < 3 ? 3.4e38f : -3.4e38f; }
 }
 
-__device__ __forceinline__ r360p::i128 wave_sum128(r360p::i128 x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long lo = __shfl_xor((unsigned long long)x, o, 64);
-        const long long hi = __shfl_xor((long long)(x >> 64), o, 64);
-        x += (r360p::i128)(((unsigned __int128)(unsigned long long)hi << 64) | lo);
+
+// one lane's sums of key into the workgroup table (or, with the table full, into the global accumulators)
+template <bool MODEL>
+__device__ __forceinline__ void gm_deposit(GmShared* sh, int key, const GmAcc& a, r360p::Moments* gmom, int* gfirst,
+                                           RegionPart* gout) {
+    int h = key & (GM_SLOTS - 1), t = 0;
+#pragma unroll 1
+    for (; t < GM_SLOTS; ++t, h = (h + 1) & (GM_SLOTS - 1)) {
+        const int old = atomicCAS(&sh->key[h], -1, key);
+        if (old == -1 || old == key) break;
     }
-    return x;
+    if (t < GM_SLOTS) {
+        unsigned long long* d = sh->w[h];
+        if (a.n) {
+            atomicAdd(d + 0, (unsigned long long)a.n);
+            for (int k = 0; k < 3; ++k) atomicAdd(d + 1 + k, (unsigned long long)a.s1[k]);
+            for (int k = 0; k < 6; ++k) add128(d + 4 + 2 * k, a.s2[k]);
+        }
+        if (MODEL) {
+            for (int k = 0; k < 4; ++k) atomicAdd(d + 16 + k, (unsigned long long)a.c[k]);
+            for (int k = 0; k < 3; ++k) { atomic_fmin(&sh->b[h][k], a.b[k]); atomic_fmax(&sh->b[h][k + 3], a.b[k + 3]); }
+        } else {
+            atomicMin(&sh->first[h], a.first);
+        }
+        return;
+    }
+    r360p::Moments* dst = MODEL ? &gout[key].m : &gmom[key];
+    if (a.n) {
+        atomicAdd(reinterpret_cast<unsigned long long*>(&dst->n), (unsigned long long)a.n);
+        for (int k = 0; k < 3; ++k) atomicAdd(reinterpret_cast<unsigned long long*>(&dst->s1[k]), (unsigned long long)a.s1[k]);
+        for (int k = 0; k < 6; ++k) add128(reinterpret_cast<unsigned long long*>(&dst->s2[k]), a.s2[k]);
+    }
+    if (MODEL) {
+        for (int k = 0; k < 4; ++k) atomicAdd(reinterpret_cast<unsigned long long*>(&dst->c[k]), (unsigned long long)a.c[k]);
+        for (int k = 0; k < 3; ++k) { atomic_fmin(&gout[key].bmin[k], a.b[k]); atomic_fmax(&gout[key].bmax[k], a.b[k + 3]); }
+    } else {
+        atomicMin(gfirst + key, a.first);
+    }
 }
 
-// block reduction of a Moments struct (exact integer sums: order-free): wave butterflies, then one
-// LDS stage; the total is valid in thread 0
-__device__ void block_reduce_moments(r360p::Moments& m, MomShared* sh) {
+// Segmented inclusive scan of the lanes' contributions within runs of lanes (head: the first lane of this lane's
+// run), on DPP lane moves (no LDS): row_shr 1, 2, 4, 8 inside each row of 16 lanes, then row_bcast:15 (rows 1 and 3
+// take the last lane of the row before) and row_bcast:31 (rows 2 and 3 take lane 31); a lane takes a moved value
+// only when the source lane lies in its run.  The pixel counts and first pixels are not scanned (run lengths and
+// ballots give them).
+template <int CTRL>
+__device__ __forceinline__ unsigned dpp32(unsigned v) {
+    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
+}
+template <int CTRL>
+__device__ __forceinline__ long long dpp64(long long v) {
+    const unsigned lo = dpp32<CTRL>((unsigned)(unsigned long long)v), hi = dpp32<CTRL>((unsigned)((unsigned long long)v >> 32));
+    return (long long)(((unsigned long long)hi << 32) | lo);
+}
+template <int CTRL>
+__device__ __forceinline__ r360p::i128 dpp128(r360p::i128 v) {
+    const unsigned long long lo = (unsigned long long)dpp64<CTRL>((long long)(unsigned long long)v);
+    const unsigned long long hi = (unsigned long long)dpp64<CTRL>((long long)(unsigned long long)(v >> 64));
+    return (r360p::i128)(((unsigned __int128)hi << 64) | lo);
+}
+template <bool MODEL, int CTRL>
+__device__ __forceinline__ void gm_scan_step(GmAcc& v, bool take) {
+    long long s1[3];
+    r360p::i128 s2[6];
+    for (int k = 0; k < 3; ++k) s1[k] = dpp64<CTRL>(v.s1[k]);
+    for (int k = 0; k < 6; ++k) s2[k] = dpp128<CTRL>(v.s2[k]);
+    if (MODEL) {
+        long long c[4];
+        float b[6];
+        for (int k = 0; k < 4; ++k) c[k] = dpp64<CTRL>(v.c[k]);
+        for (int k = 0; k < 6; ++k) b[k] = __uint_as_float(dpp32<CTRL>(__float_as_uint(v.b[k])));
+        if (take) {
+            for (int k = 0; k < 4; ++k) v.c[k] += c[k];
+            for (int k = 0; k < 3; ++k) { v.b[k] = fminf(v.b[k], b[k]); v.b[k + 3] = fmaxf(v.b[k + 3], b[k + 3]); }
+        }
+    }
+    if (take) {
+        for (int k = 0; k < 3; ++k) v.s1[k] += s1[k];
+        for (int k = 0; k < 6; ++k) v.s2[k] += s2[k];
+    }
+}
+template <bool MODEL>
+__device__ __forceinline__ void gm_seg_scan(GmAcc& v, int lane, int head) {
+    const int r = lane & 15, row = lane >> 4;
+    gm_scan_step<MODEL, 0x111>(v, r >= 1 && head <= lane - 1);   // row_shr:1
+    gm_scan_step<MODEL, 0x112>(v, r >= 2 && head <= lane - 2);   // row_shr:2
+    gm_scan_step<MODEL, 0x114>(v, r >= 4 && head <= lane - 4);   // row_shr:4
+    gm_scan_step<MODEL, 0x118>(v, r >= 8 && head <= lane - 8);   // row_shr:8
+    gm_scan_step<MODEL, 0x142>(v, (row & 1) && head <= (lane & ~15) - 1);   // row_bcast:15
+    gm_scan_step<MODEL, 0x143>(v, row >= 2 && head <= 31);                   // row_bcast:31
+}
+
+// MODEL = false (large labels): key = s * R360_MAX_BIG + bmap[label], moments of the finite points, first pixel into
+//   bfirst; also clears the label -> model map (mmap) k_plane_fit fills.
+// MODEL = true (refined regions): key = s * R360_MAX_MODELS + mmap[labf], moments of the points in the rig frame
+//   (Eigen Affine3f * Vector3f with the sensor's column-major pose, pcl::transformPointCloud) and of the colours, and
+//   the local-frame bounds, into copy blockIdx.x % GM_COPIES.  The accumulators were zeroed (bounds at -+3.4e38) by
+//   k_big_list / k_plane_fit.
+template <bool MODEL, int CPW>   // CPW: chunks of 64 pixels per wave (a workgroup takes 256 * CPW pixels)
+__global__ void __launch_bounds__(GM_TPB) k_gm(const float4* __restrict__ cloud, const uchar4* __restrict__ rgb,
+                                             const int* __restrict__ lab, int N, const int* __restrict__ kmap,
+                                             int* __restrict__ mmap_clear, const float* __restrict__ rt8,
+                                             r360p::Moments* __restrict__ gmom, int* __restrict__ gfirst,
+                                             RegionPart* __restrict__ gpart, int exp) {
+    __shared__ GmShared sh;
+    RegionPart* const gout = MODEL ? gpart + (blockIdx.x % GM_COPIES) * 8 * R360_MAX_MODELS : nullptr;
+    for (int q = threadIdx.x; q < GM_SLOTS; q += GM_TPB) {
+        sh.key[q] = -1;
+        sh.first[q] = 0x7fffffff;
+        for (int k = 0; k < 20; ++k) sh.w[q][k] = 0;
+        for (int k = 0; k < 6; ++k) sh.b[q][k] = k < 3 ? 3.4e38f : -3.4e38f;
+    }
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    long long w[20];
-    w[0] = wave_sum64(m.n);
-    for (int k = 0; k < 3; ++k) w[1 + k] = wave_sum64(m.s1[k]);
-    for (int k = 0; k < 6; ++k) {
-        const r360p::i128 v = wave_sum128(m.s2[k]);
-        w[4 + 2 * k] = (long long)(unsigned long long)v;
-        w[5 + 2 * k] = (long long)(v >> 64);
-    }
-    for (int k = 0; k < 4; ++k) w[16 + k] = wave_sum64(m.c[k]);
-    if (lane == 0)
-        for (int k = 0; k < 20; ++k) sh->w[wid][k] = w[k];
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        r360p::moments_zero(m);
-        for (int q = 0; q < (int)(blockDim.x >> 6); ++q) {
-            m.n += sh->w[q][0];
-            for (int k = 0; k < 3; ++k) m.s1[k] += sh->w[q][1 + k];
-            for (int k = 0; k < 6; ++k)
-                m.s2[k] += (r360p::i128)(((unsigned __int128)(unsigned long long)sh->w[q][5 + 2 * k] << 64) |
-                                         (unsigned long long)sh->w[q][4 + 2 * k]);
-            for (int k = 0; k < 4; ++k) m.c[k] += sh->w[q][16 + k];
-        }
-    }
-}
-
-__device__ __forceinline__ int block_min(int v, int* sh) {
-    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
-    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
-    __syncthreads();
-    if (threadIdx.x == 0)
-        for (int q = 1; q < (int)(blockDim.x >> 6); ++q) v = min(v, sh[q]);
-    return v;
-}
-
-// block min of v[0..2] and max of v[3..5] (one LDS round for all six); the result is valid in thread 0
-__device__ __forceinline__ void block_fminmax6(float (&v)[6], float (*sh)[6]) {
+    const long total = 8L * N;
+    const long w0 = ((long)blockIdx.x * GM_TPB * CPW) + (long)wid * 64 * CPW + lane;   // this lane's first pixel
+    // the wave's chunks' labels, keys and points loaded up front (three rounds of CPW independent loads)
+    int key[CPW];
 #pragma unroll
-    for (int k = 0; k < 6; ++k)
-        for (int o = 32; o > 0; o >>= 1) {
-            const float u = __shfl_xor(v[k], o, 64);
-            v[k] = k >= 3 ? fmaxf(v[k], u) : fminf(v[k], u);
-        }
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0)
-        for (int k = 0; k < 6; ++k) sh[threadIdx.x >> 6][k] = v[k];
-    __syncthreads();
-    if (threadIdx.x == 0)
-        for (int q = 1; q < (int)(blockDim.x >> 6); ++q)
-            for (int k = 0; k < 6; ++k) v[k] = k >= 3 ? fmaxf(v[k], sh[q][k]) : fminf(v[k], sh[q][k]);
-}
-
-// Exact merge of a workgroup's partial moments into global accumulators: 64-bit atomic adds (two's complement,
-// order-free); an int128 sum is a low/high pair whose carry each adder derives from the old low word it got back,
-// so the pair ends at the exact total whatever the order.  Called by every thread with the block total of
-// block_reduce_moments in thread 0: the 20 words go through LDS and 14 lanes of wave 0 add one word each (the six
-// returning low-word adds in one instruction: one memory round trip instead of six in sequence, which is what a
-// single lane walking the words cost, the compiler waiting for each returned value).
-__device__ void moments_atomic_merge(r360p::Moments* dst, const r360p::Moments& m, MomShared* sh) {
-    if (threadIdx.x == 0) {
-        sh->w[0][0] = m.n;
-        for (int k = 0; k < 3; ++k) sh->w[0][1 + k] = m.s1[k];
-        for (int k = 0; k < 6; ++k) {
-            sh->w[0][4 + 2 * k] = (long long)(unsigned long long)m.s2[k];
-            sh->w[0][5 + 2 * k] = (long long)(m.s2[k] >> 64);
-        }
-        for (int k = 0; k < 4; ++k) sh->w[0][16 + k] = m.c[k];
+    for (int c = 0; c < CPW; ++c) {
+        const long i = w0 + 64 * c;
+        key[c] = i < total ? lab[i] : -1;
+        if (!MODEL && i < total) mmap_clear[i] = -1;
+    }
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) {
+        const long i = w0 + 64 * c;
+        const int s = (int)(i / N);
+        const int m = key[c] >= 0 ? kmap[(long)s * N + key[c]] : -1;
+        key[c] = m >= 0 ? s * (MODEL ? R360_MAX_MODELS : R360_MAX_BIG) + m : -1;
+    }
+    float4 pt[CPW];
+    uchar4 col[CPW];
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) {
+        const long i = w0 + 64 * c;
+        pt[c] = key[c] >= 0 ? cloud[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (MODEL) col[c] = key[c] >= 0 ? rgb[i] : make_uchar4(0, 0, 0, 0);
     }
     __syncthreads();
-    const int l = threadIdx.x;
-    if (l < 6) {
-        unsigned long long* w = reinterpret_cast<unsigned long long*>(&dst->s2[l]);
-        const unsigned long long lo = (unsigned long long)sh->w[0][4 + 2 * l];
-        const unsigned long long hi = (unsigned long long)sh->w[0][5 + 2 * l];
-        const unsigned long long old = atomicAdd(w, lo);
-        atomicAdd(w + 1, hi + (old + lo < old ? 1ull : 0ull));
-    } else if (l < 14) {
-        const int k = l - 6;   // n, s1[0..2], c[0..3]
-        long long* p = k == 0 ? &dst->n : k < 4 ? &dst->s1[k - 1] : &dst->c[k - 4];
-        const long long v = sh->w[0][k == 0 ? 0 : k < 4 ? k : 12 + k];
-        atomicAdd(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v);
-    }
-}
-
-// float min / max through integer atomics (the accumulators start at +inf / -inf; -0 orders below +0)
-__device__ __forceinline__ void atomic_fmin(float* p, float v) {
-    if (v >= 0.f) atomicMin(reinterpret_cast<int*>(p), __float_as_int(v));
-    else atomicMax(reinterpret_cast<unsigned*>(p), __float_as_uint(v));
-}
-__device__ __forceinline__ void atomic_fmax(float* p, float v) {
-    if (v >= 0.f) atomicMax(reinterpret_cast<int*>(p), __float_as_int(v));
-    else atomicMin(reinterpret_cast<unsigned*>(p), __float_as_uint(v));
-}
-
-// grid (LMOM_GX, 8, LMOM_SPLIT): workgroup x walks labels x, x + LMOM_GX, ...; blockIdx.z takes every LMOM_SPLIT-th
-// slice of MOM_UNROLL * LMOM_TPB list entries, so a large label's pixels are summed by several workgroups at once
-// (exact merges into the sums k_big_list zeroed)
-
-constexpr int LMOM_TPB = 256, LMOM_GX = 128, LMOM_SPLIT = 4;   // labels are mostly small: 4 waves each
-
-__global__ void __launch_bounds__(LMOM_TPB) k_label_moments(const float4* __restrict__ cloud, const int* __restrict__ cnt,
-                                                          int N, const int* __restrict__ big,
-                                                          const int* __restrict__ nbig, int maxbig,
-                                                          const int* __restrict__ boff, const int* __restrict__ blist,
-                                                          r360p::Moments* __restrict__ mom, int* __restrict__ bfirst) {
-    __shared__ MomShared sh;
-    __shared__ int smin[MOM_NW];
-    const int s = blockIdx.y;
-    const int nb = nbig[s];
-    for (int b = blockIdx.x; b < nb; b += gridDim.x) {
-    const int L = big[s * maxbig + b];
-    const long base = (long)s * N;
-    const int n = cnt[base + L];
-    const int* li = blist + base + boff[s * maxbig + b];
-    if ((int)blockIdx.z * MOM_UNROLL * LMOM_TPB >= n) continue;
-    r360p::Moments m;
-    r360p::moments_zero(m);
-    int first = N;
-    for (int k0 = blockIdx.z * MOM_UNROLL * LMOM_TPB + threadIdx.x; k0 < n; k0 += gridDim.z * MOM_UNROLL * LMOM_TPB) {
-        int j[MOM_UNROLL];
-        float4 p[MOM_UNROLL];
 #pragma unroll
-        for (int u = 0; u < MOM_UNROLL; ++u) j[u] = k0 + u * LMOM_TPB < n ? li[k0 + u * LMOM_TPB] : -1;
-#pragma unroll
-        for (int u = 0; u < MOM_UNROLL; ++u) p[u] = j[u] >= 0 ? cloud[base + j[u]] : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-        for (int u = 0; u < MOM_UNROLL; ++u)
-            if (j[u] >= 0) {
-                first = min(first, j[u]);
-                if (isfin(p[u].x) && isfin(p[u].y) && isfin(p[u].z)) r360p::moments_add_xyz(m, p[u].x, p[u].y, p[u].z);
+    for (int c = 0; c < CPW; ++c) {
+        const long i = w0 + 64 * c;
+        const int s = (int)(i / N);
+        GmAcc p;                       // this pixel's contribution
+        gm_zero(p);
+        if (key[c] >= 0) {
+            const float4 q = pt[c];
+            float x = q.x, y = q.y, z = q.z;
+            bool add = true;
+            if (MODEL) {
+                p.b[0] = q.x; p.b[1] = q.y; p.b[2] = q.z; p.b[3] = q.x; p.b[4] = q.y; p.b[5] = q.z;
+                const float* T = rt8 + 16 * s;
+                x = T[0] * q.x + T[4] * q.y + T[8] * q.z + T[12];
+                y = T[1] * q.x + T[5] * q.y + T[9] * q.z + T[13];
+                z = T[2] * q.x + T[6] * q.y + T[10] * q.z + T[14];
+                const uchar4 cc = col[c];
+                const int sum = cc.x + cc.y + cc.z;
+                if (sum != 0) {   // r360p::moments_add_rgb
+                    const float inv = 1.0f / float(sum);
+                    p.c[0] = (long long)((double)(float(cc.x) * inv) * 8589934592.0);
+                    p.c[1] = (long long)((double)(float(cc.y) * inv) * 8589934592.0);
+                    p.c[2] = (long long)((double)(float(cc.z) * inv) * 8589934592.0);
+                }
+                p.c[3] = sum;
+            } else {
+                p.first = (int)(i - (long)s * N);
+                add = isfin(q.x) && isfin(q.y) && isfin(q.z);
             }
+            if (add) {   // r360p::moments_add_xyz
+                const long long qv[3] = {r360p::q36(x), r360p::q36(y), r360p::q36(z)};
+                p.n = 1;
+                for (int k = 0; k < 3; ++k) p.s1[k] = qv[k];
+                p.s2[0] = (r360p::i128)qv[0] * qv[0];
+                p.s2[1] = (r360p::i128)qv[0] * qv[1];
+                p.s2[2] = (r360p::i128)qv[0] * qv[2];
+                p.s2[3] = (r360p::i128)qv[1] * qv[1];
+                p.s2[4] = (r360p::i128)qv[1] * qv[2];
+                p.s2[5] = (r360p::i128)qv[2] * qv[2];
+            }
+        }
+        // one segmented inclusive scan over the chunk's runs of equal keys; the last lane of a run deposits it
+        const unsigned long long heads = __ballot(lane == 0 || key[c] != __shfl_up(key[c], 1, 64));
+        const unsigned long long le = lane == 63 ? ~0ull : (2ull << lane) - 1;
+        const int head = 63 - __clzll((long long)(heads & le));
+        const unsigned long long fin = __ballot(p.n != 0);   // pixels with moments (labels: finite points)
+        if (!(exp & 4)) gm_seg_scan<MODEL>(p, lane, head);
+        const bool tail = lane == 63 || ((heads >> (lane + 1)) & 1ull);
+        if (!(exp & 2) && tail && key[c] >= 0) {
+            const unsigned long long run = le & ~((1ull << head) - 1);
+            p.n = __popcll(fin & run);
+            p.first -= lane - head;   // the run's first pixel (consecutive pixels of one sensor)
+            gm_deposit<MODEL>(&sh, key[c], p, gmom, gfirst, gout);
+        }
     }
-    first = block_min(first, smin);
-    block_reduce_moments(m, &sh);
-    if (threadIdx.x == 0) atomicMin(bfirst + s * maxbig + b, first);
-    moments_atomic_merge(mom + s * maxbig + b, m, &sh);
-    __syncthreads();   // the LDS reduction scratch is reused by the next label
+    __syncthreads();
+    // the table into the global accumulators: slot q by 32 lanes (14 words, 6 bounds or the first pixel)
+    for (int q = threadIdx.x >> 5; q < GM_SLOTS; q += GM_TPB / 32) {
+        const int key = sh.key[q];
+        if (key < 0 || (exp & 1)) continue;
+        const int l = threadIdx.x & 31;
+        r360p::Moments* dst = MODEL ? &gout[key].m : &gmom[key];
+        if (l < 6) {
+            unsigned long long* d = reinterpret_cast<unsigned long long*>(&dst->s2[l]);
+            const unsigned long long lo = sh.w[q][4 + 2 * l], hi = sh.w[q][5 + 2 * l];
+            const unsigned long long old = atomicAdd(d, lo);
+            atomicAdd(d + 1, hi + (old + lo < old ? 1ull : 0ull));
+        } else if (l < 14) {
+            const int k = l - 6;   // n, s1[0..2], c[0..3]
+            if (k < 4 || MODEL) {
+                long long* d = k == 0 ? &dst->n : k < 4 ? &dst->s1[k - 1] : &dst->c[k - 4];
+                atomicAdd(reinterpret_cast<unsigned long long*>(d), sh.w[q][k == 0 ? 0 : k < 4 ? k : 12 + k]);
+            }
+        } else if (MODEL && l < 20) {
+            const int k = l - 14;
+            if (k < 3) atomic_fmin(&gout[key].bmin[k], sh.b[q][k]);
+            else atomic_fmax(&gout[key].bmax[k - 3], sh.b[q][k]);
+        } else if (!MODEL && l == 14) {
+            atomicMin(gfirst + key, sh.first[q]);
+        }
     }
 }
 
@@ -573,16 +594,12 @@ __global__ void __launch_bounds__(PF_TPB) k_plane_fit(const r360p::Moments* __re
                                                      const int* __restrict__ nbig, int maxbig, float max_curvature,
                                                      PlaneModel* __restrict__ models, int* __restrict__ nmodels,
                                                      int* __restrict__ err, int N, int* __restrict__ mmap,
-                                                     int* __restrict__ mcnt) {
+                                                     const int* __restrict__ bfirst, PlaneOut* __restrict__ out,
+                                                     RegionPart* __restrict__ gpart) {
     __shared__ float s_c[R360_MAX_BIG][4], s_pp[R360_MAX_BIG][4], s_vp[R360_MAX_BIG][4];
     __shared__ float s_curv[R360_MAX_BIG];
     __shared__ int s_idx[R360_MAX_BIG];
     const int s = blockIdx.x;
-    // the model counts and cursors of k_model_count / k_model_scatter ([8][MAX_MODELS] each)
-    for (int q = threadIdx.x; q < R360_MAX_MODELS; q += PF_TPB) {
-        mcnt[s * R360_MAX_MODELS + q] = 0;
-        mcnt[(8 + s) * R360_MAX_MODELS + q] = 0;
-    }
     const int nb = min(nbig[s], maxbig);
     for (int b = threadIdx.x; b < nb; b += PF_TPB) {
         const r360p::Moments m = mom[s * maxbig + b];
@@ -635,6 +652,21 @@ __global__ void __launch_bounds__(PF_TPB) k_plane_fit(const r360p::Moments* __re
         for (int k = 0; k < 3; ++k) M.centroid[k] = centroid[k];
         for (int k = 0; k < 9; ++k) M.cov[k] = (float)cv[k];
         M.curvature = s_curv[b];
+        // the region record, and the copies of its accumulators k_gm<true> adds into (bounds at -+3.4e38: a region
+        // left without pixels after the refinement keeps them, as the reference's min / max over an empty cloud)
+        PlaneOut& O = out[s * R360_MAX_MODELS + nm];
+        O.model = M;
+        O.start = bfirst[s * maxbig + b];
+        for (int c = 0; c < GM_COPIES; ++c) {
+            RegionPart& G = gpart[(c * 8 + s) * R360_MAX_MODELS + nm];
+            r360p::moments_zero(G.m);
+            for (int k = 0; k < 3; ++k) { G.bmin[k] = 3.4e38f; G.bmax[k] = -3.4e38f; }
+        }
+        O.n_contour = 0;
+        O.contour_off = 0;
+        O.n_vox = 0;
+        O.vox_fill = 0;
+        O.vox_off = 0;
     }
 }
 
@@ -1601,141 +1633,6 @@ __global__ void k_refine_final(const int8_t* __restrict__ state, const int* __re
     }
 }
 
-// ------------------------------------------------------------------ per-model statistics
-// refined regions grouped by model: counts, then scatter (order inside a slice is free, as above)
-__device__ __forceinline__ void model_keys(const int* __restrict__ labf, int N, const int* __restrict__ mmap, long b0,
-                                           int (&key)[4], int (&j)[4], int (&s)[4]) {
-    const long total = 8L * N;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const long i = b0 + k * PS_TPB + threadIdx.x;
-        key[k] = -1; j[k] = 0; s[k] = 0;
-        if (i < total) {
-            s[k] = (int)(i / N);
-            j[k] = (int)(i - (long)s[k] * N);
-            const int L = labf[i];
-            if (L >= 0) {
-                const int m = mmap[(long)s[k] * N + L];
-                if (m >= 0) key[k] = s[k] * R360_MAX_MODELS + m;
-            }
-        }
-    }
-}
-
-__global__ void __launch_bounds__(PS_TPB) k_model_count(const int* __restrict__ labf, int N, const int* __restrict__ mmap,
-                                                       int* __restrict__ mcnt, PlaneOut* __restrict__ out) {
-    __shared__ int hist[2 * R360_MAX_MODELS];
-    // k_model_stats merges its workgroups' partial sums and bounds into these
-    if (blockIdx.x == 0)
-        for (int q = threadIdx.x; q < 8 * R360_MAX_MODELS; q += blockDim.x) {
-            r360p::moments_zero(out[q].stats);
-            for (int k = 0; k < 3; ++k) { out[q].bmin[k] = __builtin_inff(); out[q].bmax[k] = -__builtin_inff(); }
-        }
-    const long b0 = (long)blockIdx.x * PS_PX;
-    int key[4], j[4], s[4];
-    model_keys(labf, N, mmap, b0, key, j, s);
-    priv_count<R360_MAX_MODELS>(key, (int)(b0 / N), hist, mcnt);
-}
-
-__device__ __forceinline__ int model_offset(const int* __restrict__ mcnt, int s, int m) {
-    int o = 0;
-    for (int k = 0; k < m; ++k) o += mcnt[s * R360_MAX_MODELS + k];
-    return o;
-}
-
-__global__ void __launch_bounds__(PS_TPB) k_model_scatter(const int* __restrict__ labf, int N, const int* __restrict__ mmap,
-                                                         const int* __restrict__ mcnt, int* __restrict__ mcur,
-                                                         int* __restrict__ mlist) {
-    __shared__ int moff[8 * R360_MAX_MODELS], hist[2 * R360_MAX_MODELS], base[2 * R360_MAX_MODELS];
-    for (int q = threadIdx.x; q < 8 * R360_MAX_MODELS; q += blockDim.x) moff[q] = mcnt[q];
-    __syncthreads();
-    if (threadIdx.x < 8) {   // exclusive prefix per sensor
-        int acc = 0;
-        for (int m = 0; m < R360_MAX_MODELS; ++m) {
-            const int c = moff[threadIdx.x * R360_MAX_MODELS + m];
-            moff[threadIdx.x * R360_MAX_MODELS + m] = acc;
-            acc += c;
-        }
-    }
-    const long b0 = (long)blockIdx.x * PS_PX;
-    int key[4], j[4], s[4], pos[4];
-    model_keys(labf, N, mmap, b0, key, j, s);
-    priv_slots<R360_MAX_MODELS>(key, (int)(b0 / N), hist, base, mcur, pos);
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-        if (key[k] >= 0) mlist[(long)s[k] * N + moff[key[k]] + pos[k]] = j[k];
-}
-
-constexpr int MS_TPB = 256, MS_SPLIT = 16;   // model lists: 16 workgroups of 4 waves per model
-
-__global__ void __launch_bounds__(MS_TPB) k_model_stats(const float4* __restrict__ cloud, const uchar4* __restrict__ rgb,
-                                                        int N, const PlaneModel* __restrict__ models,
-                                                        const int* __restrict__ nmodels, const float* __restrict__ rt8,
-                                                        const int* __restrict__ mcnt, const int* __restrict__ mlist,
-                                                        const int* __restrict__ bfirst, int maxbig,
-                                                        PlaneOut* __restrict__ out) {
-    __shared__ MomShared sh;
-    __shared__ float sred6[MOM_NW][6];
-    const int s = blockIdx.y;
-    const int nmod = nmodels[s];
-    for (int m = blockIdx.x; m < nmod; m += gridDim.x) {
-    const PlaneModel& M = models[s * R360_MAX_MODELS + m];
-    const float* T = rt8 + 16 * s;
-    const long base = (long)s * N;
-    const int n = mcnt[s * R360_MAX_MODELS + m];
-    const int* li = mlist + base + model_offset(mcnt, s, m);
-    if (blockIdx.z > 0 && (int)blockIdx.z * MOM_UNROLL * MS_TPB >= n) continue;
-    r360p::Moments mo;
-    r360p::moments_zero(mo);
-    float bx[6] = {3.4e38f, 3.4e38f, 3.4e38f, -3.4e38f, -3.4e38f, -3.4e38f};   // local-frame bounds
-    for (int k0 = blockIdx.z * MOM_UNROLL * MS_TPB + threadIdx.x; k0 < n; k0 += gridDim.z * MOM_UNROLL * MS_TPB) {
-        int j[MOM_UNROLL];
-        float4 p[MOM_UNROLL];
-        uchar4 c[MOM_UNROLL];
-#pragma unroll
-        for (int u = 0; u < MOM_UNROLL; ++u) j[u] = k0 + u * MS_TPB < n ? li[k0 + u * MS_TPB] : -1;
-#pragma unroll
-        for (int u = 0; u < MOM_UNROLL; ++u) {
-            p[u] = j[u] >= 0 ? cloud[base + j[u]] : make_float4(0.f, 0.f, 0.f, 0.f);
-            c[u] = j[u] >= 0 ? rgb[base + j[u]] : make_uchar4(0, 0, 0, 0);
-        }
-#pragma unroll
-        for (int u = 0; u < MOM_UNROLL; ++u) {
-            if (j[u] < 0) continue;
-            const float4 q = p[u];
-            bx[0] = fminf(bx[0], q.x); bx[1] = fminf(bx[1], q.y); bx[2] = fminf(bx[2], q.z);
-            bx[3] = fmaxf(bx[3], q.x); bx[4] = fmaxf(bx[4], q.y); bx[5] = fmaxf(bx[5], q.z);
-            // Eigen Affine3f * Vector3f (pcl::transformPointCloud), column-major T
-            const float x = T[0] * q.x + T[4] * q.y + T[8] * q.z + T[12];
-            const float y = T[1] * q.x + T[5] * q.y + T[9] * q.z + T[13];
-            const float z = T[2] * q.x + T[6] * q.y + T[10] * q.z + T[14];
-            r360p::moments_add_xyz(mo, x, y, z);
-            r360p::moments_add_rgb(mo, c[u].x, c[u].y, c[u].z);
-        }
-    }
-    block_fminmax6(bx, sred6);
-    block_reduce_moments(mo, &sh);
-    moments_atomic_merge(&out[s * R360_MAX_MODELS + m].stats, mo, &sh);
-    if (threadIdx.x == 0) {
-        PlaneOut& O = out[s * R360_MAX_MODELS + m];
-        if (n > 0)
-            for (int k = 0; k < 3; ++k) { atomic_fmin(&O.bmin[k], bx[k]); atomic_fmax(&O.bmax[k], bx[k + 3]); }
-        if (blockIdx.z == 0) {
-            O.model = M;
-            O.start = bfirst[s * maxbig + M.big];
-            if (n == 0)
-                for (int k = 0; k < 3; ++k) { O.bmin[k] = bx[k]; O.bmax[k] = bx[k + 3]; }
-            O.n_contour = 0;
-            O.contour_off = 0;
-            O.n_vox = 0;
-            O.vox_fill = 0;
-            O.vox_off = 0;
-        }
-    }
-    __syncthreads();   // the LDS reduction scratch is reused by the next model
-    }
-}
-
 // findLabeledRegionBoundary (Moore-neighbour trace), all regions of a sensor in one workgroup.
 // k_nbmask first stores, per pixel, the 8-bit mask of the neighbours carrying the same refined label
 // (bit d = direction d of {W, NW, N, NE, E, SE, S, SW}; out-of-image neighbours are 0).  A trace only
@@ -1744,9 +1641,46 @@ __global__ void __launch_bounds__(MS_TPB) k_model_stats(const float4* __restrict
 // find-first-set.  k_trace loads the masks of its sensor into LDS, lane m of wave 0 walks region m
 // (all regions of the sensor in parallel), appending the visited pixel indices to 32-entry chunks of
 // an LDS list; then the whole workgroup writes the contour points to the pool in trace order.
-__global__ void k_nbmask(const int* __restrict__ labf, int w, int h, uint8_t* __restrict__ nb) {
+// Threads 0 .. 20 * 8 * R360_MAX_MODELS - 1 also fold the region accumulators' copies of k_gm<true> into the region
+// records, one word each (exact integer sums, min / max), for k_alloc and the host.
+__global__ void k_nbmask(const int* __restrict__ labf, int w, int h, uint8_t* __restrict__ nb,
+                         const RegionPart* __restrict__ gpart, const int* __restrict__ nmodels,
+                         PlaneOut* __restrict__ out) {
     const int N = w * h;
     const long total = 8L * N;
+    {   // thread (q, w): word w of region q summed over the copies
+        const long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
+        const int q = (int)(t / 20), w = (int)(t % 20);
+        if (q < 8 * R360_MAX_MODELS && q % R360_MAX_MODELS < nmodels[q / R360_MAX_MODELS]) {
+            const RegionPart* G = gpart + q;
+            PlaneOut& O = out[q];
+            constexpr int C = GM_COPIES, S = 8 * R360_MAX_MODELS;
+            if (w < 6) {
+                r360p::i128 v = 0;
+#pragma unroll
+                for (int c = 0; c < C; ++c) v += G[c * S].m.s2[w];
+                O.stats.s2[w] = v;
+            } else if (w < 14) {
+                const int k = w - 6;   // n, s1[0..2], c[0..3]
+                long long v = 0;
+#pragma unroll
+                for (int c = 0; c < C; ++c) {
+                    const r360p::Moments& m = G[c * S].m;
+                    v += k == 0 ? m.n : k < 4 ? m.s1[k - 1] : m.c[k - 4];
+                }
+                if (k == 0) O.stats.n = v;
+                else if (k < 4) O.stats.s1[k - 1] = v;
+                else O.stats.c[k - 4] = v;
+            } else {
+                const int k = w - 14;   // bmin[0..2], bmax[0..2]
+                float v = k < 3 ? 3.4e38f : -3.4e38f;
+#pragma unroll
+                for (int c = 0; c < C; ++c) v = k < 3 ? fminf(v, G[c * S].bmin[k]) : fmaxf(v, G[c * S].bmax[k - 3]);
+                if (k < 3) O.bmin[k] = v;
+                else O.bmax[k - 3] = v;
+            }
+        }
+    }
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
         const int s = (int)(i / N), p = (int)(i - (long)s * N);
         const int* Lb = labf + (long)s * N;
@@ -1919,7 +1853,7 @@ __global__ void __launch_bounds__(TR_TPB) k_trace(const uint8_t* __restrict__ nb
 // smaller of its inliers and its bounding box's voxels), capped by the allocation
 // one workgroup of 512 threads, thread = (sensor, model)
 __global__ void __launch_bounds__(512) k_alloc(const int* __restrict__ nmodels, const PlaneOut* __restrict__ out,
-                                               const int* __restrict__ mcnt, unsigned long long cap,
+                                               unsigned long long cap,
                                                long* __restrict__ totals) {
     __shared__ long sco[8], sca[8];
     const int q = threadIdx.x, s = q / R360_MAX_MODELS, m = q % R360_MAX_MODELS;
@@ -1933,7 +1867,7 @@ __global__ void __launch_bounds__(512) k_alloc(const int* __restrict__ nmodels, 
             double vol = 1.0;
             for (int k = 0; k < 3; ++k)
                 vol *= (double)((long long)floorf(out[q].bmax[k] * inv) - (long long)floorf(out[q].bmin[k] * inv) + 1);
-            cand = mcnt[q];
+            cand = out[q].stats.n;
             if (vol >= 1.0 && vol < (double)cand) cand = (long)vol;
         }
     }
@@ -2216,6 +2150,24 @@ int launch_refine_sweeps(hipStream_t st, int8_t* S, int8_t* S2, const unsigned l
 }
 
 // ------------------------------------------------------------------ launcher
+template <bool MODEL>
+int launch_gm(int px, long total, hipStream_t st, const float4* cloud, const uchar4* rgb, const int* lab, int N,
+              const int* kmap, int* mmap_clear, const float* rt8, r360p::Moments* gmom, int* gfirst, RegionPart* gpart) {
+    const unsigned blocks = (unsigned)((total + px - 1) / px);
+    static const int exp = getenv("R360_EXP_GM") ? atoi(getenv("R360_EXP_GM")) : 0;   // timing experiments only
+    switch (px) {
+#define R360_GM_CASE(cpw)                                                                                         \
+    case 256 * cpw:                                                                                               \
+        hipLaunchKernelGGL((k_gm<MODEL, cpw>), dim3(blocks), dim3(GM_TPB), 0, st, cloud, rgb, lab, N, kmap,        \
+                           mmap_clear, rt8, gmom, gfirst, gpart, exp);                                            \
+        return 0;
+        R360_GM_CASE(1) R360_GM_CASE(2) R360_GM_CASE(4) R360_GM_CASE(8) R360_GM_CASE(16)
+#undef R360_GM_CASE
+    }
+    r360_set_error("segmentation: R360_GM_PX=%d (256, 512, 1024, 2048 or 4096)", px);
+    return -1;
+}
+
 int launch_segmentation(r360_frame* f) {
     PlaneBufs& P = f->pl;
     r360_ctx* ctx = f->ctx;
@@ -2241,29 +2193,19 @@ int launch_segmentation(r360_frame* f) {
     timing_end(ctx, slot);
     R360_HIP(hipGetLastError());
     slot = timing_begin(ctx, "k_plane_fit");
-    // aux: boff, bcur, bfirst [8][MAX_BIG]; mcnt, mcur [8][MAX_MODELS].  parent / root are free after
-    // the labelling and hold the label -> large-label and label -> model maps.
-    int* boff = P.aux;
-    int* bcur = boff + 8 * R360_MAX_BIG;
-    int* bfirst = bcur + 8 * R360_MAX_BIG;
-    int* mcnt = bfirst + 8 * R360_MAX_BIG;
-    int* mcur = mcnt + 8 * R360_MAX_MODELS;
+    // aux: the large labels' first pixels [8][MAX_BIG].  parent / root are free after the labelling and hold the
+    // label -> large-label and label -> model maps.
+    int* bfirst = P.aux;
     int* bmap = P.parent;
     int* mmap = P.root;
     hipLaunchKernelGGL(k_big_list, dim3(8), dim3(1024), 0, st, P.cnt, P.nlab, N, 80, P.big, P.nbig, R360_MAX_BIG, P.err,
-                       bmap, boff, P.mom, bfirst, bcur);
-    if (N < PS_PX) { r360_set_error("segmentation: sensor of %d points too small", N); return -1; }
-    const int pblocks = (int)((total + PS_PX - 1) / PS_PX);
-    hipLaunchKernelGGL(k_label_scatter, dim3(pblocks), dim3(PS_TPB), 0, st, P.lab, N, bmap, boff, bcur, P.blist, mmap);
-    // grid shapes of the two moment kernels (R360_LMOM_GX / _SPLIT, R360_MS_GX / _SPLIT: experiments)
-    static const int lm_gx = getenv("R360_LMOM_GX") ? atoi(getenv("R360_LMOM_GX")) : LMOM_GX;
-    static const int lm_sp = getenv("R360_LMOM_SPLIT") ? atoi(getenv("R360_LMOM_SPLIT")) : LMOM_SPLIT;
-    static const int ms_gx = getenv("R360_MS_GX") ? atoi(getenv("R360_MS_GX")) : 16;
-    static const int ms_sp = getenv("R360_MS_SPLIT") ? atoi(getenv("R360_MS_SPLIT")) : MS_SPLIT;
-    hipLaunchKernelGGL(k_label_moments, dim3(lm_gx, 8, lm_sp), dim3(LMOM_TPB), 0, st, P.cloud, P.cnt, N, P.big, P.nbig,
-                       R360_MAX_BIG, boff, P.blist, P.mom, bfirst);
+                       bmap, P.mom, bfirst);
+    // pixels per workgroup of the grouped-moment kernels (R360_GM_PX, experiments)
+    static const int gm_px = getenv("R360_GM_PX") ? atoi(getenv("R360_GM_PX")) : GM_PX;
+    if (launch_gm<false>(gm_px, total, st, P.cloud, nullptr, P.lab, N, bmap, mmap, nullptr, P.mom, bfirst, nullptr))
+        return -1;
     hipLaunchKernelGGL(k_plane_fit, dim3(8), dim3(PF_TPB), 0, st, P.mom, P.big, P.nbig, R360_MAX_BIG, 0.001f, P.models,
-                       P.nmodels, P.err, N, mmap, mcnt);
+                       P.nmodels, P.err, N, mmap, bfirst, P.out, P.gpart);
     timing_end(ctx, slot);
     R360_HIP(hipGetLastError());
     slot = timing_begin(ctx, "k_refine");
@@ -2276,13 +2218,13 @@ int launch_segmentation(r360_frame* f) {
     timing_end(ctx, slot);
     R360_HIP(hipGetLastError());
     slot = timing_begin(ctx, "k_model_stats");
-    hipLaunchKernelGGL(k_model_count, dim3(pblocks), dim3(PS_TPB), 0, st, P.labf, N, mmap, mcnt, P.out);
-    hipLaunchKernelGGL(k_model_scatter, dim3(pblocks), dim3(PS_TPB), 0, st, P.labf, N, mmap, mcnt, mcur, P.mlist);
-    hipLaunchKernelGGL(k_model_stats, dim3(ms_gx, 8, ms_sp), dim3(MS_TPB), 0, st, P.cloud, P.rgb, N, P.models,
-                       P.nmodels, f->calib->d_rt, mcnt, P.mlist, bfirst, R360_MAX_BIG, P.out);
+    if (launch_gm<true>(gm_px, total, st, P.cloud, P.rgb, P.labf, N, mmap, nullptr, f->calib->d_rt, nullptr, nullptr,
+                        P.gpart))
+        return -1;
     // the refinement's closeness masks are dead here: their storage holds the neighbour masks
     uint8_t* nbm = reinterpret_cast<uint8_t*>(P.mask);
-    hipLaunchKernelGGL(k_nbmask, dim3(blocks), dim3(256), 0, st, P.labf, w, h, nbm);
+    hipLaunchKernelGGL(k_nbmask, dim3(std::max(blocks, 20 * 8 * R360_MAX_MODELS / 256)), dim3(256), 0, st, P.labf, w, h, nbm,
+                       P.gpart, P.nmodels, P.out);
     if (N <= TR_NB_MAX)
         hipLaunchKernelGGL(k_trace<true>, dim3(8), dim3(TR_TPB), 0, st, nbm, P.cloud, w, h, P.nmodels, P.out,
                            P.contour, P.contour_cap, P.err);
@@ -2290,7 +2232,7 @@ int launch_segmentation(r360_frame* f) {
         hipLaunchKernelGGL(k_trace<false>, dim3(8), dim3(TR_TPB), 0, st, nbm, P.cloud, w, h, P.nmodels, P.out,
                            P.contour, P.contour_cap, P.err);
     if (ctx_vhash_reserve(ctx, 12L * N)) return -1;
-    hipLaunchKernelGGL(k_alloc, dim3(1), dim3(512), 0, st, P.nmodels, P.out, mcnt,
+    hipLaunchKernelGGL(k_alloc, dim3(1), dim3(512), 0, st, P.nmodels, P.out,
                        (unsigned long long)ctx->vhash_cap, P.totals);
     timing_end(ctx, slot);
     R360_HIP(hipGetLastError());

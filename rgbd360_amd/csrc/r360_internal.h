@@ -164,6 +164,14 @@ struct VoxOut {
     float x, y, z, pad;
 };
 
+// Global accumulators of the refined regions' grouped-moment kernel (plane_seg.hip): exact moments in the rig frame +
+// colour sums and local-frame bounds, in R360_GM_COPIES copies.
+#define R360_GM_COPIES 8
+struct RegionPart {
+    r360p::Moments m;
+    float bmin[3], bmax[3];
+};
+
 // Device buffers of a frame's plane half (allocated on the first CLOUD/PLANES build)
 struct PlaneBufs {
     int w = 0, h = 0;
@@ -181,13 +189,11 @@ struct PlaneBufs {
     int* lab = nullptr;         // CCL labels (per-sensor ids, -1 none)
     int* labf = nullptr;        // labels after refinement
     int* cnt = nullptr;         // label sizes [8][N]
-    int* blist = nullptr;       // pixels of each large label, grouped by label [8][N]
-    int* mlist = nullptr;       // pixels of each refined model region, grouped by model [8][N]
-    int* aux = nullptr;         // per-sensor list offsets / cursors / first pixels (plane_seg.hip)
+    int* aux = nullptr;         // the large labels' first pixels [8][R360_MAX_BIG] (plane_seg.hip)
     int* nlab = nullptr;        // [8]
     int* big = nullptr;         // [8][R360_MAX_BIG]
     int* nbig = nullptr;        // [8]
-    r360p::Moments* mom = nullptr;   // [8][R360_MAX_BIG]
+    r360p::Moments* mom = nullptr;   // [8][R360_MAX_BIG] the large labels' moments
     PlaneModel* models = nullptr;    // [8][R360_MAX_MODELS]
     int* nmodels = nullptr;          // [8]
     int8_t* state = nullptr;         // refinement state [8][N]
@@ -200,6 +206,7 @@ struct PlaneBufs {
     int8_t* rf1 = nullptr;               //   first sweep's states, skewed
     int8_t* rf2 = nullptr;               //   second sweep's states, skewed
     PlaneOut* out = nullptr;         // [8][R360_MAX_MODELS]
+    RegionPart* gpart = nullptr;     // [R360_GM_COPIES][8][R360_MAX_MODELS] region accumulators (k_gm<true>)
     float4* contour = nullptr;       // contour pool
     long contour_cap = 0;
     VoxOut* vox = nullptr;           // voxel-fallback centroids

@@ -102,3 +102,81 @@ def test_two_rank_gather_and_trajectory(tmp_path):
     assert list(allrec[1, :, OD.R_STATUS]) == [0] * 128 + [1] * 127
     # rank 0's prefix product: y translations add up
     assert np.allclose(traj[-1][1, 3], 0.001 * 255 * 256 / 2, rtol=1e-6)
+
+
+class _StubCtx:
+    """Context stand-in: the timing / sync calls bench.main makes on the pipelines' contexts."""
+
+    def sync(self): pass
+    def timing(self, on): pass
+    def timing_reset(self): pass
+    def kernel_time_reset(self): pass
+    def timing_read(self, name): return 0.0, 0
+    def kernel_stats(self, level): return 0.0, 0, 0
+    def host_times(self, reset=False): return np.zeros(6)
+
+
+class _StubRunner:
+    """odometry.SequenceRunner stand-in for the CPU: each pair's record is the ground-truth relative motion of the
+    synthetic path (so the composed trajectory is exact), its status the rank that registered it; every pair's raw
+    frames are fetched through frames_of, as the pipelines do."""
+
+    def __init__(self, device, rows, cols, P, params, **kw):
+        import rgbd360_amd as R
+        self.R, self.rows, self.cols = R, rows, cols
+        self.ctxs, self.queue, self.cals, self.frames = [_StubCtx() for _ in range(P)], None, [], []
+        self.host_s = np.zeros((P, 4))
+        self.native_ids = set()
+        self.rank = int(os.environ["RANK"])
+
+    def run(self, p0, p1, frames_of, out, repeats=1, runs=None, device_inputs=False):
+        assert runs[0][0] == p0 and runs[-1][1] == p1
+        for i in range(p0, p1):
+            for f in (i, i + 1):
+                b, d = frames_of(f)
+                assert b.shape == (8, self.rows, self.cols, 3) and d.shape == (8, self.rows, self.cols)
+            rel = np.linalg.inv(self.R.synth_path_pose(bench.SEED, i).astype(np.float64)) @ \
+                self.R.synth_path_pose(bench.SEED, i + 1).astype(np.float64)
+            out[:repeats, i - p0, OD.R_POSE:OD.R_POSE + 16] = rel.T.reshape(16)
+            out[:repeats, i - p0, OD.R_STATUS] = self.rank
+            out[:repeats, i - p0, OD.R_SSO] = 0.8
+        self.host_s[0, 3] += repeats * (p1 - p0)
+
+    def close(self): pass
+
+
+def _main_worker(rank, world, port, out_dir):
+    import contextlib
+    import io
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), R360_BENCH_REHEARSAL="1", R360_NO_PIN="1")
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        bench.main(["--gpus", str(world), "--steps", "2", "--warmup", "1", "--frames", "24", "--rows", "24",
+                    "--cols", "32", "--streams", "3", "--min-run", "2", "--no-cpu-baseline", "--no-resident",
+                    "--no-config5", "--no-isolated"], runner_factory=_StubRunner)
+    with open(os.path.join(out_dir, f"out{rank}.txt"), "w") as f:
+        f.write(buf.getvalue())
+
+
+def test_bench_main_two_ranks(tmp_path):
+    """bench.main itself at world size 2 over gloo (R360_BENCH_REHEARSAL: records gathered by gloo instead of the
+    library's RCCL communicator), with a CPU stand-in for the GPU pipelines: each rank registers only its shard,
+    rank 0 gathers every rank's records, composes the whole trajectory and prints the one JSON line with the
+    whole-job pair count; the other rank prints nothing."""
+    import json
+    world = 2
+    mp.spawn(_main_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    assert (tmp_path / "out1.txt").read_text() == ""
+    lines = (tmp_path / "out0.txt").read_text().strip().splitlines()
+    assert len(lines) == 1
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["steps"] == 2 and out["scaling"] == "strong"
+    assert out["config"]["parallelism"] == "pair-shard dp2"
+    assert out["config"]["pairs_per_step"] == 23 and out["config"]["pairs_per_step_this_rank"] == 12
+    tr = out["trajectory"]
+    assert tr["pairs"] == 23 and tr["frames"] == 24
+    # every pair composed once, in order (the floor: f32 records, arccos of a trace within 1e-7 of 3)
+    assert tr["max_rot_err_deg"] < 0.05 and tr["max_trans_err_m"] < 1e-5
+    assert tr["pbmap_failed"] == 11 and tr["illposed"] == 0                  # status = rank: rank 1's 11 pairs arrived
+    assert out["value"] > 0 and abs(out["value"] - 46 / (out["ms_per_step"] * 2e-3)) < 1e-6 * out["value"]
