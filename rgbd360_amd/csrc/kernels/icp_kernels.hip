@@ -943,11 +943,22 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
             return r;
         };
         struct Src { unsigned v; float sp, cp, st, ct; };
-        auto ld = [&](int base) {                          // base: wave-uniform first pixel of a 64-pixel run
-            const int r = __builtin_amdgcn_readfirstlane(row_of(base));
-            const int c = base - r * nCols + lane;
-            return Src{__builtin_amdgcn_raw_buffer_load_b32(rs_s, (base + lane) * 4, 0, 0), sinphi[r], cosphi[r],
-                       sinth[c], costh[c]};
+        int n_it_ = 0;
+        // the source cursor: chunk k's first pixel, row and column, advanced by the stride in scalar registers
+        // (SALU) and clamped at the last chunk, as base(k)
+        int cur_k = 0, cur_i = 0, cur_r = 0, cur_c = 0;
+        const int st_r = stride / nCols, st_c = stride - (stride / nCols) * nCols;
+        auto ld = [&]() {
+            const Src x{__builtin_amdgcn_raw_buffer_load_b32(rs_s, (cur_i + lane) * 4, 0, 0), sinphi[cur_r],
+                        cosphi[cur_r], sinth[cur_c + lane], costh[cur_c + lane]};
+            if (cur_k + 1 < n_it_) {
+                ++cur_k;
+                cur_i += stride;
+                cur_r += st_r;
+                cur_c += st_c;
+                if (cur_c >= nCols) { cur_c -= nCols; ++cur_r; }
+            }
+            return x;
         };
         auto prj = [&](const Src& x) {
             const float d = depth_of(x.v);
@@ -972,22 +983,26 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
         if (b0 < npx) {
 #endif
             const int n_it = (npx - 1 - b0) / stride + 1;
+            n_it_ = n_it;
+            cur_i = b0;
+            cur_r = __builtin_amdgcn_readfirstlane(row_of(b0));
+            cur_c = b0 - cur_r * nCols;
             auto base = [&](int k) { return b0 + (k < n_it ? k : n_it - 1) * stride; };
-            Src sA = ld(base(0));
-            Src sB = ld(base(1));
+            Src sA = ld();
+            Src sB = ld();
             Proj oA = prj(sA);
             defer(oA, base(0));
             float4 GA = gG(oA.t);
             unsigned TA = gT(oA.t);
             for (int k = 0;; k += 2) {
-                sA = ld(base(k + 2));
+                sA = ld();
                 Proj oB = prj(sB);
                 if (k + 1 < n_it) defer(oB, base(k + 1));   // a clamped tail chunk is never accumulated
                 const float4 GB = gG(oB.t);
                 const unsigned TB = gT(oB.t);
                 acc(oA, GA, TA);
                 if (k + 1 >= n_it) break;
-                sB = ld(base(k + 3));
+                sB = ld();
                 oA = prj(sA);
                 if (k + 2 < n_it) defer(oA, base(k + 2));
                 GA = gG(oA.t);
