@@ -295,8 +295,10 @@ def main(argv=None, runner_factory=None):
     ap.add_argument("--frames", type=int, default=256, help="sequence length (frames)")
     ap.add_argument("--workload", choices=["sequence", "dense", "planes"], default="sequence")
     ap.add_argument("--streams", type=int, default=8, help="max pipelines per GPU (host thread + HIP stream each)")
-    ap.add_argument("--min-run", type=int, default=8,
-                    help="min pairs per pipeline run (each run rebuilds a halo frame; 8 beat 4 and 16 on 1/4- and 1/8-size shards)")
+    ap.add_argument("--min-run", type=int, default=6,
+                    help="min pairs per pipeline run (each run rebuilds a halo frame): 6 gives a 1/8 shard (31-32 pairs) "
+                         "5 pipelines, 8-10 %% faster than 8 (3-4 pipelines) and 4 (8); N=1 and 1/4 shards keep 8 "
+                         "pipelines either way (profiles/r3_shards)")
     ap.add_argument("--stage-timing", action="store_true",
                     help="diagnostic: HIP events around EVERY launch of the timed run (per-stage times; slows the run)")
     ap.add_argument("--queue", type=int, default=16,
