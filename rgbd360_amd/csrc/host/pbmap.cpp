@@ -395,6 +395,8 @@ int ctx_vhash_reserve(r360_ctx* ctx, long min_cells) {
     hipFree(ctx->d_vhash);
     ctx->d_vhash = nullptr;
     R360_HIP(hipMalloc(&ctx->d_vhash, sizeof(VoxCell) * cap));
+    // zero once: k_vox_compact leaves every cell it used zero again (stream order: before the frame's kernels)
+    R360_HIP(hipMemsetAsync(ctx->d_vhash, 0, sizeof(VoxCell) * cap, ctx->stream));
     ctx->vhash_cap = cap;
     return 0;
 }

@@ -1884,16 +1884,6 @@ __global__ void __launch_bounds__(512) k_alloc(const int* __restrict__ nmodels, 
     totals[3] = cand;            // bound on the voxels of the regions without a contour (0: no voxel stage work)
 }
 
-__global__ void k_vox_clear(VoxCell* __restrict__ tab, const long* __restrict__ totals) {
-    if (totals[3] == 0) return;
-    const unsigned long long used = (unsigned long long)totals[2] + 1;
-    for (unsigned long long c = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; c < used;
-         c += (unsigned long long)gridDim.x * blockDim.x) {
-        tab[c].tag = 0;
-        tab[c].s[0] = tab[c].s[1] = tab[c].s[2] = 0.0;
-        tab[c].cnt = 0;
-    }
-}
 
 // pcl::VoxelGrid (leaf 0.05) of the inliers of regions without a contour (Frame360.h:1017-1026):
 // points are hashed by (region, voxel index); voxel sums of <= a few hundred coordinates with ulps
@@ -2032,23 +2022,43 @@ __global__ void __launch_bounds__(512) k_vox_alloc(const int* __restrict__ nmode
     }
 }
 
-// one workgroup per contiguous range of table cells: valid cells are counted per region in LDS, one
-// global atomic per (workgroup, region) reserves the slots, then the cells are written
+// one workgroup per contiguous range of table cells: valid cells are counted per region in LDS (one LDS atomic per
+// (wave, region): the cells of a region are spread over the whole table, so per-cell atomics all hit a few
+// counters), one global atomic per (workgroup, region) reserves the slots, then the cells are written — and
+// cleared, so that the table is all zero again for the next frame of this context (no clearing kernel).
 constexpr int VOXC_TPB = 1024, VOXC_BLOCKS = 256;
 
-__global__ void __launch_bounds__(VOXC_TPB) k_vox_compact(const VoxCell* __restrict__ tab,
+// runs of equal region keys within a wave: per distinct key the lanes' mask (the leader adds the count)
+template <typename F>
+__device__ __forceinline__ void wave_by_key(int key, F&& f) {
+    bool pending = key >= 0;
+    while (__any(pending)) {
+        const unsigned long long act = __ballot(pending);
+        const int leader = __ffsll((long long)act) - 1;
+        const int lk = __shfl(key, leader, 64);
+        const bool mine = pending && key == lk;
+        f(lk, __ballot(mine), leader, mine);
+        if (mine) pending = false;
+    }
+}
+
+__global__ void __launch_bounds__(VOXC_TPB) k_vox_compact(VoxCell* __restrict__ tab,
                                                          const long* __restrict__ totals, PlaneOut* __restrict__ out,
                                                          VoxOut* __restrict__ pool, long pool_cap) {
     if (totals[3] == 0) return;
     __shared__ int cnt[8 * R360_MAX_MODELS], base[8 * R360_MAX_MODELS];
     for (int q = threadIdx.x; q < 8 * R360_MAX_MODELS; q += VOXC_TPB) cnt[q] = 0;
     __syncthreads();
+    const int lane = threadIdx.x & 63;
     const unsigned long long cells = (unsigned long long)totals[2] + 1;
     const unsigned long long per = (cells + gridDim.x - 1) / gridDim.x;
     const unsigned long long c0 = blockIdx.x * per, c1 = c0 + per < cells ? c0 + per : cells;
-    for (unsigned long long c = c0 + threadIdx.x; c < c1; c += VOXC_TPB) {
-        const unsigned long long tag = tab[c].tag;
-        if (tag) atomicAdd(&cnt[(int)(tag >> 48) - 1], 1);
+    for (unsigned long long cb = c0; cb < c1; cb += VOXC_TPB) {
+        const unsigned long long c = cb + threadIdx.x;
+        const unsigned long long tag = c < c1 ? tab[c].tag : 0ull;
+        wave_by_key(tag ? (int)(tag >> 48) - 1 : -1, [&](int k, unsigned long long m, int leader, bool) {
+            if (lane == leader) atomicAdd(&cnt[k], __popcll(m));
+        });
     }
     __syncthreads();
     for (int q = threadIdx.x; q < 8 * R360_MAX_MODELS; q += VOXC_TPB) {
@@ -2056,11 +2066,19 @@ __global__ void __launch_bounds__(VOXC_TPB) k_vox_compact(const VoxCell* __restr
         cnt[q] = 0;
     }
     __syncthreads();
-    for (unsigned long long c = c0 + threadIdx.x; c < c1; c += VOXC_TPB) {
-        const unsigned long long tag = tab[c].tag;
-        if (!tag) continue;
-        const int sm = (int)(tag >> 48) - 1;
-        const int pos = base[sm] + atomicAdd(&cnt[sm], 1);
+    for (unsigned long long cb = c0; cb < c1; cb += VOXC_TPB) {
+        const unsigned long long c = cb + threadIdx.x;
+        const unsigned long long tag = c < c1 ? tab[c].tag : 0ull;
+        const int sm = tag ? (int)(tag >> 48) - 1 : -1;
+        int pos = 0;
+        wave_by_key(sm, [&](int k, unsigned long long m, int leader, bool mine) {
+            int o = 0;
+            if (lane == leader) o = atomicAdd(&cnt[k], __popcll(m));
+            o = __shfl(o, leader, 64);
+            if (mine) pos = base[k] + o + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                                          __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+        });
+        if (sm < 0) continue;
         const PlaneOut& O = out[sm];
         const double n = (double)tab[c].cnt;
         VoxOut v;
@@ -2070,6 +2088,9 @@ __global__ void __launch_bounds__(VOXC_TPB) k_vox_compact(const VoxCell* __restr
         v.z = (float)(tab[c].s[2] / n);
         v.pad = 0.f;
         if (O.vox_off + pos < pool_cap) pool[O.vox_off + pos] = v;
+        tab[c].tag = 0;
+        tab[c].s[0] = tab[c].s[1] = tab[c].s[2] = 0.0;
+        tab[c].cnt = 0;
     }
 }
 
@@ -2237,8 +2258,8 @@ int launch_segmentation(r360_frame* f) {
     timing_end(ctx, slot);
     R360_HIP(hipGetLastError());
     slot = timing_begin(ctx, "k_voxel");
-    // the voxel kernels exit at entry when no region lacks a contour (totals[3] == 0, the usual case)
-    hipLaunchKernelGGL(k_vox_clear, dim3(256), dim3(256), 0, st, ctx->d_vhash, P.totals);
+    // the voxel kernels exit at entry when no region lacks a contour (totals[3] == 0, the usual case); the table is
+    // zero on allocation and k_vox_compact clears every cell it reads
     static const int vox_px_env = getenv("R360_VOX_PX") ? atoi(getenv("R360_VOX_PX")) : VOX_PX;   // experiments
     const int vox_px = std::min(vox_px_env, N);   // a block spans at most two sensors
     hipLaunchKernelGGL(k_vox_hash, dim3((unsigned)((total + vox_px - 1) / vox_px)), dim3(VOX_TPB), 0, st, P.cloud,
