@@ -340,6 +340,7 @@ int plane_bufs_alloc(r360_frame* f) {
     R360_HIP(hipMalloc(&P.labf, sizeof(int) * T));
     R360_HIP(hipMalloc(&P.cnt, sizeof(int) * T));
     R360_HIP(hipMalloc(&P.aux, sizeof(int) * 8 * R360_MAX_BIG));
+    R360_HIP(hipMalloc(&P.chunk, sizeof(int) * 8 * ((N + 255) / 256)));
     R360_HIP(hipMalloc(&P.gpart, sizeof(RegionPart) * R360_GM_COPIES * 8 * R360_MAX_MODELS));
     R360_HIP(hipMalloc(&P.nlab, sizeof(int) * 8));
     R360_HIP(hipMalloc(&P.big, sizeof(int) * 8 * R360_MAX_BIG));
@@ -375,7 +376,7 @@ int plane_bufs_alloc(r360_frame* f) {
 void plane_bufs_free(r360_frame* f) {
     PlaneBufs& P = f->pl;
     planes_join(f);
-    void* dev[] = {P.cloud, P.rgb, P.nrm, P.dist0, P.dist, P.grids, P.zmm, P.parent, P.root, P.lab, P.labf, P.cnt, P.gpart, P.aux, P.nlab,
+    void* dev[] = {P.cloud, P.rgb, P.nrm, P.dist0, P.dist, P.grids, P.zmm, P.parent, P.root, P.lab, P.labf, P.cnt, P.gpart, P.aux, P.chunk, P.nlab,
                    P.big, P.nbig, P.mom, P.models, P.nmodels, P.state, P.state2, P.rbnd, P.rflag, P.mask, P.rcode, P.rmsk, P.rf1, P.rf2, P.out, P.totals, P.err};
     for (void* p : dev) hipFree(p);
     hipHostFree(P.contour);

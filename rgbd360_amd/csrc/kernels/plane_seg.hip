@@ -131,87 +131,54 @@ __global__ void k_ccl_border(const float4* __restrict__ cloud, const float4* __r
     }
 }
 
-// also zeroes the label counts k_ccl_label accumulates (one launch instead of a memset)
-__global__ void k_ccl_flatten(int* __restrict__ parent, long total, int* __restrict__ root, int* __restrict__ cnt) {
-    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-        root[i] = parent[i] < 0 ? -1 : find_root(parent, (int)i);
+// Roots, and the root count of every chunk of NUMC pixels of a sensor (grid (chunks, 8)) for k_ccl_number; also
+// zeroes the label counts k_ccl_label accumulates (one launch instead of a memset).
+constexpr int NUMC = 256;   // elements per chunk = threads per workgroup of the chunked numbering kernels
+
+__global__ void __launch_bounds__(NUMC) k_ccl_flatten(int* __restrict__ parent, int N, int* __restrict__ root,
+                                                     int* __restrict__ cnt, int* __restrict__ ccnt) {
+    const int s = blockIdx.y, j = blockIdx.x * NUMC + threadIdx.x;
+    const long i = (long)s * N + j;
+    bool is_root = false;
+    if (j < N) {
+        const int r = parent[i] < 0 ? -1 : find_root(parent, (int)i);
+        root[i] = r;
         cnt[i] = 0;
+        is_root = r == (int)i;
     }
+    const int c = __syncthreads_count(is_root);
+    if (threadIdx.x == 0) ccnt[s * gridDim.x + blockIdx.x] = c;
 }
 
-// block-wide exclusive scan of one int per thread (blockDim.x = 1024)
-__device__ int block_exscan(int v, int* sh, int& total) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    int x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
+// Exclusive rank of this thread's flag within its chunk, the chunk's offset (the sum of the counts of the chunks
+// before it in the sensor) and the chunk's total; one workgroup of NUMC threads per chunk.
+__device__ __forceinline__ int chunk_rank(bool flag, const int* __restrict__ ccnt_s, int chunk, int& off, int& tot) {
+    __shared__ int s_w[NUMC / 64], s_off[NUMC / 64];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int a = 0;
+    for (int k = threadIdx.x; k < chunk; k += NUMC) a += ccnt_s[k];
+    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+    const unsigned long long m = __ballot(flag);
+    if (lane == 0) { s_off[wid] = a; s_w[wid] = __popcll(m); }
     __syncthreads();
-    if (lane == 63) sh[wid] = x;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int acc = 0;
-        for (int k = 0; k < nw; ++k) { const int t = sh[k]; sh[k] = acc; acc += t; }
-        sh[nw] = acc;
-    }
-    __syncthreads();
-    total = sh[nw];
-    return sh[wid] + x - v;
+    int o = 0, before = 0, t = 0;
+    for (int w = 0; w < NUMC / 64; ++w) { o += s_off[w]; before += w < wid ? s_w[w] : 0; t += s_w[w]; }
+    off = o;
+    tot = t;
+    return before + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
 
-// roots -> label ids in raster order (one workgroup per sensor); rank stored at the root's slot.
-// Pass 1 loads the sensor coalesced, 8 elements per thread and round, all rounds in flight (no barrier between
-// them), and keeps one flag byte per 8 elements in LDS; pass 2 gives each thread a contiguous run of flag bytes,
-// one block scan of their popcounts, then the ranks in raster order.
-constexpr int SCAN_V = 8;   // elements per flag byte
-constexpr int NUM_TPB = 1024;
-constexpr int NUM_MAXQ = 40960;   // flag bytes per sensor (N / 8; HiRes 38400)
-
-__global__ void __launch_bounds__(NUM_TPB) k_ccl_number(const int* __restrict__ root, int N, int* __restrict__ rank,
-                                                        int* __restrict__ nlab) {
-    __shared__ int sh[17];
-    __shared__ unsigned char F[NUM_MAXQ];
-    const int s = blockIdx.x;
-    const long base = (long)s * N;
-    const int nq = (N + SCAN_V - 1) / SCAN_V;
-    // whole flag bytes with two 16-byte loads (the sensor's slice starts 32-byte aligned when N % 8 == 0)
-    const int nq_vec = (N % SCAN_V) == 0 ? nq : 0;
-    for (int q = threadIdx.x; q < nq_vec; q += NUM_TPB) {
-        const int4* p4 = reinterpret_cast<const int4*>(root + base + (long)q * SCAN_V);
-        const int4 a = p4[0], b = p4[1];
-        const int j0 = (int)(base + (long)q * SCAN_V);
-        const unsigned f = (unsigned)(a.x == j0) | (unsigned)(a.y == j0 + 1) << 1 | (unsigned)(a.z == j0 + 2) << 2 |
-                           (unsigned)(a.w == j0 + 3) << 3 | (unsigned)(b.x == j0 + 4) << 4 | (unsigned)(b.y == j0 + 5) << 5 |
-                           (unsigned)(b.z == j0 + 6) << 6 | (unsigned)(b.w == j0 + 7) << 7;
-        F[q] = (unsigned char)f;
-    }
-    for (int q = nq_vec + threadIdx.x; q < nq; q += NUM_TPB) {
-        unsigned f = 0;
-#pragma unroll
-        for (int v = 0; v < SCAN_V; ++v) {
-            const int j = q * SCAN_V + v;
-            if (j < N && root[base + j] == (int)(base + j)) f |= 1u << v;
-        }
-        F[q] = (unsigned char)f;
-    }
-    __syncthreads();
-    const int per = (nq + NUM_TPB - 1) / NUM_TPB;
-    const int q0 = threadIdx.x * per, q1 = min(nq, q0 + per);
-    int c = 0;
-    for (int q = q0; q < q1; ++q) c += __popc(F[q]);
-    int tot;
-    int r = block_exscan(c, sh, tot);
-    for (int q = q0; q < q1; ++q) {
-        unsigned f = F[q];
-        while (f) {
-            const int v = __ffs(f) - 1;
-            f &= f - 1;
-            rank[base + q * SCAN_V + v] = r++;
-        }
-    }
-    if (threadIdx.x == 0) nlab[s] = tot;
+// roots -> label ids in raster order; rank stored at the root's slot.  Grid (chunks, 8): a chunk's offset is the
+// sum of k_ccl_flatten's root counts of the chunks before it, its roots are ranked with a ballot scan.
+__global__ void __launch_bounds__(NUMC) k_ccl_number(const int* __restrict__ root, int N, const int* __restrict__ ccnt,
+                                                    int* __restrict__ rank, int* __restrict__ nlab) {
+    const int s = blockIdx.y, j = blockIdx.x * NUMC + threadIdx.x;
+    const long i = (long)s * N + j;
+    const bool is_root = j < N && root[i] == (int)i;
+    int off, tot;
+    const int r = chunk_rank(is_root, ccnt + s * gridDim.x, blockIdx.x, off, tot);
+    if (is_root) rank[i] = off + r;
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) nlab[s] = off + tot;
 }
 
 __global__ void k_ccl_label(const int* __restrict__ root, const int* __restrict__ rank, int N, int* __restrict__ lab,
@@ -254,71 +221,48 @@ __device__ __forceinline__ void add128(unsigned long long* p, r360p::i128 v) {
     atomicAdd(p + 1, hi + (old + lo < old ? 1ull : 0ull));
 }
 
-// labels with more than min_inliers points, in increasing label order (one workgroup per sensor), and the
-// label -> large-label index map.  Same two passes as k_ccl_number: flag bytes of the labels' counts, then
-// contiguous runs per thread.  Also zeroes the large labels' moment accumulators k_gm<false> adds into.
-__global__ void __launch_bounds__(NUM_TPB) k_big_list(const int* __restrict__ cnt, const int* __restrict__ nlab, int N,
-                                                      int min_inliers, int* __restrict__ big, int* __restrict__ nbig,
-                                                      int maxbig, int* __restrict__ err, int* __restrict__ bmap,
-                                                      r360p::Moments* __restrict__ mom, int* __restrict__ bfirst) {
-    __shared__ int sh[17];
-    __shared__ unsigned char F[NUM_MAXQ];
-    const int s = blockIdx.x;
-    const int n = nlab[s];
-    const long base = (long)s * N;
-    const int nq = (n + SCAN_V - 1) / SCAN_V;
-    // whole flag bytes with two 16-byte loads (the sensor's slice starts 32-byte aligned when N % 8 == 0)
-    const int nq_vec = (N % SCAN_V) == 0 ? n / SCAN_V : 0;
-    for (int q = threadIdx.x; q < nq_vec; q += NUM_TPB) {
-        const int4* p4 = reinterpret_cast<const int4*>(cnt + base + (long)q * SCAN_V);
-        const int4 a = p4[0], b = p4[1];
-        const int c8[SCAN_V] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-        unsigned f = 0;
-#pragma unroll
-        for (int v = 0; v < SCAN_V; ++v) {
-            if (c8[v] > min_inliers) f |= 1u << v;
-            else bmap[base + q * SCAN_V + v] = -1;
+// labels with more than min_inliers points, in increasing label order, and the label -> large-label index map
+// (-1 for the others).  Grid (chunks of label ids, 8): k_big_count counts each chunk's large labels, k_big_list
+// ranks them after the chunks before; the sensor's last chunk also zeroes the large labels' moment accumulators
+// k_gm<false> adds into.
+__global__ void __launch_bounds__(NUMC) k_big_count(const int* __restrict__ cnt, const int* __restrict__ nlab, int N,
+                                                   int min_inliers, int* __restrict__ bmap, int* __restrict__ ccnt) {
+    const int s = blockIdx.y, j = blockIdx.x * NUMC + threadIdx.x;
+    const long i = (long)s * N + j;
+    bool big = false;
+    if (j < nlab[s]) {
+        big = cnt[i] > min_inliers;
+        if (!big) bmap[i] = -1;
+    }
+    const int c = __syncthreads_count(big);
+    if (threadIdx.x == 0) ccnt[s * gridDim.x + blockIdx.x] = c;
+}
+
+__global__ void __launch_bounds__(NUMC) k_big_list(const int* __restrict__ cnt, const int* __restrict__ nlab, int N,
+                                                  int min_inliers, const int* __restrict__ ccnt, int* __restrict__ big,
+                                                  int* __restrict__ nbig, int maxbig, int* __restrict__ err,
+                                                  int* __restrict__ bmap, r360p::Moments* __restrict__ mom,
+                                                  int* __restrict__ bfirst) {
+    const int s = blockIdx.y, j = blockIdx.x * NUMC + threadIdx.x;
+    const long i = (long)s * N + j;
+    const bool is_big = j < nlab[s] && cnt[i] > min_inliers;
+    int off, tot;
+    const int r = chunk_rank(is_big, ccnt + s * gridDim.x, blockIdx.x, off, tot);
+    if (is_big) {
+        const int b = off + r;
+        bmap[i] = b < maxbig ? b : -1;
+        if (b < maxbig) big[s * maxbig + b] = j;
+    }
+    if (blockIdx.x == gridDim.x - 1) {
+        const int all = off + tot, nb = all < maxbig ? all : maxbig;
+        if (threadIdx.x == 0) {
+            nbig[s] = nb;
+            if (all > maxbig) atomicOr(err, 2);
         }
-        F[q] = (unsigned char)f;
-    }
-    for (int q = nq_vec + threadIdx.x; q < nq; q += NUM_TPB) {
-        unsigned f = 0;
-#pragma unroll
-        for (int v = 0; v < SCAN_V; ++v) {
-            const int j = q * SCAN_V + v;
-            if (j < n) {
-                if (cnt[base + j] > min_inliers) f |= 1u << v;
-                else bmap[base + j] = -1;
-            }
+        for (int q = threadIdx.x; q < nb; q += NUMC) {
+            r360p::moments_zero(mom[s * maxbig + q]);
+            bfirst[s * maxbig + q] = N;
         }
-        F[q] = (unsigned char)f;
-    }
-    __syncthreads();
-    const int per = (nq + NUM_TPB - 1) / NUM_TPB;
-    const int q0 = threadIdx.x * per, q1 = min(nq, q0 + per);
-    int nf = 0;
-    for (int q = q0; q < q1; ++q) nf += __popc((unsigned)F[q]);
-    int tot;
-    int b = block_exscan(nf, sh, tot);
-    for (int q = q0; q < q1; ++q) {
-        unsigned f = F[q];
-        while (f) {
-            const int v = __ffs(f) - 1;
-            f &= f - 1;
-            const int j = q * SCAN_V + v;
-            bmap[base + j] = b < maxbig ? b : -1;
-            if (b < maxbig) big[s * maxbig + b] = j;
-            ++b;
-        }
-    }
-    if (threadIdx.x == 0) {
-        nbig[s] = tot < maxbig ? tot : maxbig;
-        if (tot > maxbig) atomicOr(err, 2);
-    }
-    const int nb = tot < maxbig ? tot : maxbig;
-    for (int q = threadIdx.x; q < nb; q += blockDim.x) {
-        r360p::moments_zero(mom[s * maxbig + q]);
-        bfirst[s * maxbig + q] = N;
     }
 }
 
@@ -2207,9 +2151,9 @@ int launch_segmentation(r360_frame* f) {
             hipLaunchKernelGGL(k_ccl_border, dim3((unsigned)((edges + 255) / 256)), dim3(256), 0, st, P.cloud, P.nrm, w,
                                h, ang_thr, P.parent);
     }
-    hipLaunchKernelGGL(k_ccl_flatten, dim3(blocks), dim3(256), 0, st, P.parent, total, P.root, P.cnt);
-    if ((N + SCAN_V - 1) / SCAN_V > NUM_MAXQ) { r360_set_error("segmentation: sensor of %d points too large", N); return -1; }
-    hipLaunchKernelGGL(k_ccl_number, dim3(8), dim3(NUM_TPB), 0, st, P.root, N, P.parent, P.nlab);
+    const int nch = (N + NUMC - 1) / NUMC;   // numbering chunks per sensor; their counts in P.chunk [8][nch]
+    hipLaunchKernelGGL(k_ccl_flatten, dim3(nch, 8), dim3(NUMC), 0, st, P.parent, N, P.root, P.cnt, P.chunk);
+    hipLaunchKernelGGL(k_ccl_number, dim3(nch, 8), dim3(NUMC), 0, st, P.root, N, P.chunk, P.parent, P.nlab);
     hipLaunchKernelGGL(k_ccl_label, dim3(blocks), dim3(256), 0, st, P.root, P.parent, N, P.lab, P.cnt);
     timing_end(ctx, slot);
     R360_HIP(hipGetLastError());
@@ -2219,8 +2163,9 @@ int launch_segmentation(r360_frame* f) {
     int* bfirst = P.aux;
     int* bmap = P.parent;
     int* mmap = P.root;
-    hipLaunchKernelGGL(k_big_list, dim3(8), dim3(1024), 0, st, P.cnt, P.nlab, N, 80, P.big, P.nbig, R360_MAX_BIG, P.err,
-                       bmap, P.mom, bfirst);
+    hipLaunchKernelGGL(k_big_count, dim3(nch, 8), dim3(NUMC), 0, st, P.cnt, P.nlab, N, 80, bmap, P.chunk);
+    hipLaunchKernelGGL(k_big_list, dim3(nch, 8), dim3(NUMC), 0, st, P.cnt, P.nlab, N, 80, P.chunk, P.big, P.nbig,
+                       R360_MAX_BIG, P.err, bmap, P.mom, bfirst);
     // pixels per workgroup of the grouped-moment kernels (R360_GM_PX, experiments)
     static const int gm_px = getenv("R360_GM_PX") ? atoi(getenv("R360_GM_PX")) : GM_PX;
     if (launch_gm<false>(gm_px, total, st, P.cloud, nullptr, P.lab, N, bmap, mmap, nullptr, P.mom, bfirst, nullptr))

@@ -190,6 +190,7 @@ struct PlaneBufs {
     int* labf = nullptr;        // labels after refinement
     int* cnt = nullptr;         // label sizes [8][N]
     int* aux = nullptr;         // the large labels' first pixels [8][R360_MAX_BIG] (plane_seg.hip)
+    int* chunk = nullptr;       // per-chunk counts of the numbering kernels [8][ceil(N / 256)]
     int* nlab = nullptr;        // [8]
     int* big = nullptr;         // [8][R360_MAX_BIG]
     int* nbig = nullptr;        // [8]
