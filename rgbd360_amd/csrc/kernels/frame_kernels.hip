@@ -98,6 +98,17 @@ __global__ void k_stitch4(const uint8_t* __restrict__ bgr8, const uint16_t* __re
         const long i0 = 4 * q;
         const int row = (int)(i0 / W), col0 = (int)(i0 - (long)row * W);
         const float v0 = sinphi[row], cos_phi = cosphi[row];
+        // the four columns' tables as 16-byte loads (col0 % 4 == 0), and the sensor's pose loaded once when the four
+        // pixels share a sensor (every sensor width that is a multiple of 4)
+        const float4 st4 = *reinterpret_cast<const float4*>(sinth + col0);
+        const float4 ct4 = *reinterpret_cast<const float4*>(costh + col0);
+        const float st_[4] = {st4.x, st4.y, st4.z, st4.w}, ct_[4] = {ct4.x, ct4.y, ct4.z, ct4.w};
+        const int kA = 7 - col0 / rows;
+        const bool one_sensor = kA == 7 - (col0 + 3) / rows;
+        const float4* TA4 = reinterpret_cast<const float4*>(rt_inv + 16 * kA);
+        const float4 ta0 = TA4[0], ta1 = TA4[1], ta2 = TA4[2], ta3 = TA4[3];
+        const float TA[16] = {ta0.x, ta0.y, ta0.z, ta0.w, ta1.x, ta1.y, ta1.z, ta1.w,
+                              ta2.x, ta2.y, ta2.z, ta2.w, ta3.x, ta3.y, ta3.z, ta3.w};
         unsigned char px[12];
         unsigned short dd4[4];
         unsigned pk4[4];
@@ -106,9 +117,16 @@ __global__ void k_stitch4(const uint8_t* __restrict__ bgr8, const uint16_t* __re
         for (int e = 0; e < 4; ++e) {
             const int col = col0 + e;
             const int k = 7 - col / rows;
-            const float* T = rt_inv + 16 * k;
-            const float v1 = cos_phi * sinth[col];
-            const float v2 = cos_phi * costh[col];
+            float T[16];
+            if (one_sensor) {
+#pragma unroll
+                for (int t = 0; t < 16; ++t) T[t] = TA[t];
+            } else {
+#pragma unroll
+                for (int t = 0; t < 16; ++t) T[t] = rt_inv[16 * k + t];
+            }
+            const float v1 = cos_phi * st_[e];
+            const float v2 = cos_phi * ct_[e];
             float p0x = T[0] * v0 + T[4] * v1 + T[8] * v2;
             float p1 = T[1] * v0 + T[5] * v1 + T[9] * v2;
             float p2 = T[2] * v0 + T[6] * v1 + T[10] * v2;

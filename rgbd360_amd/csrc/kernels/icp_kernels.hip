@@ -56,7 +56,7 @@ struct Gather {
 };
 
 #ifdef R360_STAMPS
-__device__ unsigned long long g_blk_stamps[2][8192];  // per-workgroup start / loop end (diagnostic build)
+__device__ unsigned long long g_blk_stamps[3][8192];  // per-workgroup start / loop end / XCC_ID:HW_ID (diagnostic build)
 #endif
 
 #include "icp_common.inc"
@@ -1194,7 +1194,14 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
 #ifdef R360_STAMPS
     const unsigned long long t_loop = __builtin_amdgcn_s_memrealtime();
     if (threadIdx.x == 0) {   // earliest block start / latest loop end over the grid
-        if (blockIdx.x < 8192) { g_blk_stamps[0][blockIdx.x] = t_start; g_blk_stamps[1][blockIdx.x] = t_loop; }
+        if (blockIdx.x < 8192) {
+            g_blk_stamps[0][blockIdx.x] = t_start;
+            g_blk_stamps[1][blockIdx.x] = t_loop;
+            unsigned hw, xcc;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            g_blk_stamps[2][blockIdx.x] = ((unsigned long long)xcc << 32) | hw;
+        }
         __hip_atomic_fetch_min(&S->dbg[8], t_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_fetch_max(&S->dbg[9], t_loop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -1688,11 +1695,11 @@ extern "C" int r360_proj_check_pose(const float* lx, const float* ly, const floa
 }
 
 #ifdef R360_STAMPS
-// Diagnostic build only: per-workgroup start / loop-end stamps of the last pass.
+// Diagnostic build only: per-workgroup start / loop-end stamps and hardware ids of the last pass (out: 3 x 8192).
 extern "C" int r360_debug_block_stamps(unsigned long long* out, int n) {
     if (n > 8192) n = 8192;
     R360_HIP(hipDeviceSynchronize());
-    R360_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_blk_stamps), sizeof(unsigned long long) * 8192 * 2));
+    R360_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_blk_stamps), sizeof(unsigned long long) * 8192 * 3));
     return n;
 }
 #endif

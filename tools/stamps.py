@@ -34,9 +34,10 @@ for lv in (4, 3, 2, 1, 0):
 
 # per-workgroup start / loop-end distribution of the last level-0 pass
 nb = int(os.environ.get("NB", "768"))
-buf = (C.c_ulonglong * (2 * 8192))()
+buf = (C.c_ulonglong * (3 * 8192))()
 R.lib().r360_debug_block_stamps(buf, 8192)
-a = np.array(list(buf), dtype=np.float64).reshape(2, 8192)[:, :nb]
+a = np.array(list(buf), dtype=np.float64).reshape(3, 8192)[:2, :nb]
+hwid = np.array(list(buf), dtype=np.uint64).reshape(3, 8192)[2, :nb]
 t0 = a[0].min()
 st, en = (a[0] - t0) / 100.0, (a[1] - t0) / 100.0
 q = lambda x: " ".join(f"{v:6.2f}" for v in np.percentile(x, [0, 10, 50, 90, 100]))
@@ -50,6 +51,14 @@ print("blocks used", len(b))
 for x in range(8):
     sel = (b % 8) == x
     print(f"xcd {x}: busy pct 0/50/100 {np.percentile(busy[sel], [0, 50, 100]).round(2)}")
+# workgroups per CU (HW_ID: CU_ID bits 8-11, SH_ID 12, SE_ID 13-15; XCC_ID in the high word) and busy time
+hw = hwid[m]
+cu_key = ((hw >> np.uint64(32)) << np.uint64(8)) | ((hw >> np.uint64(8)) & np.uint64(0xff))
+keys, inv, counts = np.unique(cu_key, return_inverse=True, return_counts=True)
+per_blk = counts[inv]
+print(f"CUs used {len(keys)}; workgroups per CU: " + ", ".join(f"{k}: {int((counts == k).sum())} CUs" for k in np.unique(counts)))
+for k in np.unique(per_blk):
+    print(f"  blocks on CUs holding {k}: busy mean {busy[per_blk == k].mean():6.2f} max {busy[per_blk == k].max():6.2f}")
 order = np.argsort(a[0][m])
 k = len(order)
 for part in range(4):
