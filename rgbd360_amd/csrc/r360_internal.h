@@ -119,8 +119,11 @@ struct IcpJob {
 struct IcpJobs { IcpJob j[R360_MAX_BATCH]; };   // passed by value (kernel arguments, 1152 B)
 
 constexpr int R360_KT_SLOTS = 26;
-constexpr int R360_TICKET_GROUPS = 16;
-constexpr int R360_TICKET_STRIDE = 1024;   // uints between group counters (4 KB)
+#ifndef R360_TICKET_GROUPS_N   // experiment builds may regroup the same 16384 counter words
+#define R360_TICKET_GROUPS_N 16
+#endif
+constexpr int R360_TICKET_GROUPS = R360_TICKET_GROUPS_N;
+constexpr int R360_TICKET_STRIDE = 16384 / R360_TICKET_GROUPS_N;   // uints between group counters (4 KB at 16)
 
 // Pass sums.  Occlusion variants: NVALID counts photo terms (Occ1) or accepted points (Occ2), NDEPTH
 // the depth terms (Occ1), ERR2 the photometric and ERR2D the depth squared residuals.
