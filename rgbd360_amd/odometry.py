@@ -121,7 +121,8 @@ class SequenceRunner:
             cal = Calib360(c, rows, cols)
             cal.loadExtrinsicCalibration(EXTRINSICS_DIR)
             self.cals.append(cal)
-            self.frames.append([Frame360(cal) for _ in range(self.depth + 2 if self.queue else 2)])
+            # queued: depth alignments in flight, the pair being registered, and the next frame's prefetched upload
+            self.frames.append([Frame360(cal) for _ in range(self.depth + 3 if self.queue else 2)])
         self.stats = [IcpStats() for _ in range(pipelines)]
         # host-side time per pipeline: [load + build enqueue, PbMap stage (register_async), dense wait, pairs]
         self.host_s = np.zeros((pipelines, 4))
@@ -190,8 +191,10 @@ class SequenceRunner:
     def _pipeline_queued(self, p: int, run: tuple[int, int], frames_of, out: np.ndarray, p0: int,
                          device_inputs: bool):
         """_pipeline with the dense stage on the queue: submit pair i, then collect pair i-depth (so `depth`
-        alignments per pipeline are in flight while the next frame is built and PbMap-registered).  Frame i+1
-        goes into the buffer of frame i+1-(depth+2), whose pairs were collected in earlier iterations."""
+        alignments per pipeline are in flight while the next frame is built and PbMap-registered).  The upload of
+        frame i+2 is issued right after frame i+1's build (same stream: it runs when that build is done, while the
+        host assembles and matches frame i+1's planes), so the next iteration's build does not wait for its copy.
+        Frame i+2 goes into the buffer of frame i+2-(depth+3), whose pairs were collected in earlier iterations."""
         L = lib()
         ctx = self.ctxs[p]
         fr = self.frames[p]
@@ -226,16 +229,18 @@ class SequenceRunner:
             rec[R_ERR] = st.error
 
         nbuf = len(fr)
-        depth = nbuf - 2
+        depth = nbuf - 3
         load(fr[0], a)
         fr[0].build(self.flags, sync=False)
+        load(fr[1 % nbuf], a + 1)
         pending = []
         sts = [IcpStats() for _ in range(depth + 1)]
         for i in range(a, b):
             t0 = time.perf_counter()
             cur, nxt = fr[(i - a) % nbuf], fr[(i + 1 - a) % nbuf]
-            load(nxt, i + 1)
-            nxt.build(self.flags, sync=False)
+            nxt.build(self.flags, sync=False)   # its upload was issued one iteration earlier
+            if i + 2 <= b:
+                load(fr[(i + 2 - a) % nbuf], i + 2)
             t1 = time.perf_counter()
             ticket = C.c_long()
             if self.dense_only:
