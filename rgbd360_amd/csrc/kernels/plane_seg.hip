@@ -66,7 +66,7 @@ __device__ __forceinline__ bool plane_cmp(const float4& pa, const float4& na, co
 // roots, the same representative the global union-find produces), writes every pixel's parent as
 // the global index of its band-local root, then k_ccl_border unites only the edges that cross band
 // boundaries in global memory.
-constexpr int CCL_ROWS = 8, CCL_TPB = 1024;
+constexpr int CCL_ROWS = 16, CCL_TPB = 1024;
 
 // path halving: every other node on the walk is re-pointed at its grandparent.  Parents only ever point at
 // smaller indices of the same component, so a racing re-point installs another ancestor and the roots (the
