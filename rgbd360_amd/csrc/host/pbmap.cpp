@@ -389,7 +389,17 @@ void plane_bufs_free(r360_frame* f) {
     f->pbmap = nullptr;
 }
 
-int ctx_vhash_reserve(r360_ctx* ctx, long min_cells) {
+int ctx_vhash_reserve(r360_ctx* ctx, long min_cells, long list_entries, long list_groups) {
+    if (ctx->vlist_cap < list_entries || ctx->vcnt_cap < list_groups) {
+        hipFree(ctx->d_vlist);
+        hipFree(ctx->d_vcnt);
+        ctx->d_vlist = nullptr;
+        ctx->d_vcnt = nullptr;
+        R360_HIP(hipMalloc(&ctx->d_vlist, sizeof(int) * list_entries));
+        R360_HIP(hipMalloc(&ctx->d_vcnt, sizeof(int) * list_groups));
+        ctx->vlist_cap = list_entries;
+        ctx->vcnt_cap = list_groups;
+    }
     long cap = 1;
     while (cap < min_cells) cap <<= 1;
     if (ctx->vhash_cap >= cap) return 0;
@@ -583,8 +593,9 @@ int planes_assemble(r360_frame* f) {
     }
     f->pbmap = pm;
     if (prof)
-        fprintf(stderr, "[pbmap] gpu wait %.0f us, pools %ld+%ld pts D2H %.0f us, descriptors %.0f us, group/merge %.0f us\n",
-                us(t0, t1), totals[0], totals[1], us(t1, t2), us(t2, t3), us(t3, now()));
+        fprintf(stderr, "[pbmap] gpu wait %.0f us, pools %ld+%ld pts (voxel table %ld cells, bound %ld) D2H %.0f us, "
+                "descriptors %.0f us, group/merge %.0f us\n", us(t0, t1), totals[0], totals[1], totals[2] + 1, totals[3],
+                us(t1, t2), us(t2, t3), us(t3, now()));
     return 0;
 }
 

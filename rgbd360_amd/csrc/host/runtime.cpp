@@ -183,6 +183,7 @@ extern "C" void r360_ctx_destroy(r360_ctx* c) {
     hipFree(c->d_rob_jobs); hipFree(c->d_rob_partials); hipFree(c->d_rob_sums); hipFree(c->d_rob_tickets);
     hipFree(c->d_rob_out); hipHostFree(c->h_rob_jobs); hipHostFree(c->h_rob_sums); hipHostFree(c->h_rob_out);
     hipFree(c->d_match_desc); hipFree(c->d_unary); hipFree(c->d_bin); hipFree(c->d_vhash);
+    hipFree(c->d_vlist); hipFree(c->d_vcnt);
     hipHostFree(c->h_unary); hipHostFree(c->h_bin);
     hipStreamDestroy(c->stream);
     delete c;

@@ -1843,13 +1843,19 @@ __device__ __forceinline__ unsigned long long vhash(unsigned long long tag, unsi
 constexpr int VOX_TPB = 256, VOX_PX = 1024, VOX_LT = 512;   // VOX_PX: default pixels per workgroup (2048: 3.4x, 4096:
                                                             // 15x slower, profiles/r3_planes)
 
+// a cell this workgroup claims is appended to its list (vlist_b, count in LDS *nclaim) for k_vox_compact
 __device__ __forceinline__ void vox_global_add(VoxCell* __restrict__ tab, unsigned long long mask,
                                                unsigned long long tag, double x, double y, double z, unsigned n,
-                                               int* __restrict__ nnew_slot, int* __restrict__ err) {
+                                               int* __restrict__ nnew_slot, int* __restrict__ err,
+                                               int* __restrict__ nclaim, int* __restrict__ vlist_b) {
     unsigned long long hsh = vhash(tag, mask);
     for (unsigned long long probe = 0;; ++probe) {
         const unsigned long long prev = atomicCAS(&tab[hsh].tag, 0ull, tag);
-        if (prev == 0ull) { atomicAdd(nnew_slot, 1); break; }
+        if (prev == 0ull) {
+            atomicAdd(nnew_slot, 1);
+            vlist_b[atomicAdd(nclaim, 1)] = (int)hsh;
+            break;
+        }
         if (prev == tag) break;
         hsh = (hsh + 1) & mask;
         if (probe > mask) { atomicOr(err, 16); return; }
@@ -1863,8 +1869,11 @@ __device__ __forceinline__ void vox_global_add(VoxCell* __restrict__ tab, unsign
 __global__ void __launch_bounds__(VOX_TPB) k_vox_hash(const float4* __restrict__ cloud, const int8_t* __restrict__ state,
                                                      int N, const int* __restrict__ nmodels, PlaneOut* __restrict__ out,
                                                      VoxCell* __restrict__ tab, const long* __restrict__ totals,
-                                                     int* __restrict__ err, int px) {
+                                                     int* __restrict__ err, int px, int* __restrict__ vlist,
+                                                     int* __restrict__ vcnt) {
     if (totals[3] == 0) return;
+    __shared__ int s_nclaim;
+    int* const vlist_b = vlist + (long)blockIdx.x * px;
     __shared__ int nnew_[2 * R360_MAX_MODELS];
     __shared__ unsigned char cand_[2 * R360_MAX_MODELS];
     __shared__ long long bnd_[2 * R360_MAX_MODELS][5];   // voxel origin b0..b2 and extents d0, d1 of a region
@@ -1880,7 +1889,7 @@ __global__ void __launch_bounds__(VOX_TPB) k_vox_hash(const float4* __restrict__
     unsigned char* cand = cand_ - s0 * R360_MAX_MODELS;
     long long (*bnd)[5] = bnd_ - s0 * R360_MAX_MODELS;
     const float inv = 1.0f / 0.05f;
-    if (threadIdx.x == 0) any = 0;
+    if (threadIdx.x == 0) { any = 0; s_nclaim = 0; }
     for (int q = threadIdx.x; q < VOX_LT; q += VOX_TPB) {
         ltag[q] = 0ull; lsum[0][q] = 0.0; lsum[1][q] = 0.0; lsum[2][q] = 0.0; lcnt[q] = 0u;
     }
@@ -1900,7 +1909,10 @@ __global__ void __launch_bounds__(VOX_TPB) k_vox_hash(const float4* __restrict__
         }
     }
     __syncthreads();
-    if (!any) return;
+    if (!any) {
+        if (threadIdx.x == 0) vcnt[blockIdx.x] = 0;
+        return;
+    }
     const unsigned long long mask = (unsigned long long)totals[2];
     for (int k = threadIdx.x; k < px; k += VOX_TPB) {
         const long i = i0 + k;
@@ -1928,15 +1940,17 @@ __global__ void __launch_bounds__(VOX_TPB) k_vox_hash(const float4* __restrict__
             atomicAdd(&lsum[2][q], (double)p.z);
             atomicAdd(&lcnt[q], 1u);
         } else {   // more distinct voxels than VOX_LT in one block: straight to the global table
-            vox_global_add(tab, mask, tag, p.x, p.y, p.z, 1u, &nnew[sm], err);
+            vox_global_add(tab, mask, tag, p.x, p.y, p.z, 1u, &nnew[sm], err, &s_nclaim, vlist_b);
         }
     }
     __syncthreads();
     for (int q = threadIdx.x; q < VOX_LT; q += VOX_TPB) {
         const unsigned long long tag = ltag[q];
-        if (tag) vox_global_add(tab, mask, tag, lsum[0][q], lsum[1][q], lsum[2][q], lcnt[q], &nnew[(int)(tag >> 48) - 1], err);
+        if (tag) vox_global_add(tab, mask, tag, lsum[0][q], lsum[1][q], lsum[2][q], lcnt[q], &nnew[(int)(tag >> 48) - 1], err,
+                                &s_nclaim, vlist_b);
     }
     __syncthreads();
+    if (threadIdx.x == 0) vcnt[blockIdx.x] = s_nclaim;
     for (int q = threadIdx.x; q < (s1 - s0 + 1) * R360_MAX_MODELS; q += VOX_TPB) {
         const int sm = s0 * R360_MAX_MODELS + q;
         if (nnew[sm]) atomicAdd(&out[sm].n_vox, nnew[sm]);
@@ -1966,11 +1980,11 @@ __global__ void __launch_bounds__(512) k_vox_alloc(const int* __restrict__ nmode
     }
 }
 
-// one workgroup per contiguous range of table cells: valid cells are counted per region in LDS (one LDS atomic per
-// (wave, region): the cells of a region are spread over the whole table, so per-cell atomics all hit a few
-// counters), one global atomic per (workgroup, region) reserves the slots, then the cells are written — and
-// cleared, so that the table is all zero again for the next frame of this context (no clearing kernel).
-constexpr int VOXC_TPB = 1024, VOXC_BLOCKS = 256;
+// one workgroup per k_vox_hash workgroup: the cells that workgroup claimed (its list) are counted per region in LDS
+// (one LDS atomic per (wave, region)), one global atomic per (workgroup, region) reserves the slots, then the cells
+// are written — and cleared, so that the table is all zero again for the next frame of this context (no clearing
+// kernel, and no pass over the cells nobody claimed).
+constexpr int VOXC_TPB = 256;
 
 // runs of equal region keys within a wave: per distinct key the lanes' mask (the leader adds the count)
 template <typename F>
@@ -1988,20 +2002,22 @@ __device__ __forceinline__ void wave_by_key(int key, F&& f) {
 
 __global__ void __launch_bounds__(VOXC_TPB) k_vox_compact(VoxCell* __restrict__ tab,
                                                          const long* __restrict__ totals, PlaneOut* __restrict__ out,
-                                                         VoxOut* __restrict__ pool, long pool_cap) {
+                                                         VoxOut* __restrict__ pool, long pool_cap,
+                                                         const int* __restrict__ vlist, const int* __restrict__ vcnt,
+                                                         int px) {
     if (totals[3] == 0) return;
+    const int n = vcnt[blockIdx.x];
+    if (n == 0) return;
     __shared__ int cnt[8 * R360_MAX_MODELS], base[8 * R360_MAX_MODELS];
     for (int q = threadIdx.x; q < 8 * R360_MAX_MODELS; q += VOXC_TPB) cnt[q] = 0;
     __syncthreads();
     const int lane = threadIdx.x & 63;
-    const unsigned long long cells = (unsigned long long)totals[2] + 1;
-    const unsigned long long per = (cells + gridDim.x - 1) / gridDim.x;
-    const unsigned long long c0 = blockIdx.x * per, c1 = c0 + per < cells ? c0 + per : cells;
-    for (unsigned long long cb = c0; cb < c1; cb += VOXC_TPB) {
-        const unsigned long long c = cb + threadIdx.x;
-        const unsigned long long tag = c < c1 ? tab[c].tag : 0ull;
-        wave_by_key(tag ? (int)(tag >> 48) - 1 : -1, [&](int k, unsigned long long m, int leader, bool) {
-            if (lane == leader) atomicAdd(&cnt[k], __popcll(m));
+    const int* L = vlist + (long)blockIdx.x * px;
+    for (int kb = 0; kb < n; kb += VOXC_TPB) {
+        const int k = kb + threadIdx.x;
+        const unsigned long long tag = k < n ? tab[L[k]].tag : 0ull;
+        wave_by_key(tag ? (int)(tag >> 48) - 1 : -1, [&](int key, unsigned long long m, int leader, bool) {
+            if (lane == leader) atomicAdd(&cnt[key], __popcll(m));
         });
     }
     __syncthreads();
@@ -2010,26 +2026,27 @@ __global__ void __launch_bounds__(VOXC_TPB) k_vox_compact(VoxCell* __restrict__ 
         cnt[q] = 0;
     }
     __syncthreads();
-    for (unsigned long long cb = c0; cb < c1; cb += VOXC_TPB) {
-        const unsigned long long c = cb + threadIdx.x;
-        const unsigned long long tag = c < c1 ? tab[c].tag : 0ull;
+    for (int kb = 0; kb < n; kb += VOXC_TPB) {
+        const int k = kb + threadIdx.x;
+        const int c = k < n ? L[k] : 0;
+        const unsigned long long tag = k < n ? tab[c].tag : 0ull;
         const int sm = tag ? (int)(tag >> 48) - 1 : -1;
         int pos = 0;
-        wave_by_key(sm, [&](int k, unsigned long long m, int leader, bool mine) {
+        wave_by_key(sm, [&](int key, unsigned long long m, int leader, bool mine) {
             int o = 0;
-            if (lane == leader) o = atomicAdd(&cnt[k], __popcll(m));
+            if (lane == leader) o = atomicAdd(&cnt[key], __popcll(m));
             o = __shfl(o, leader, 64);
-            if (mine) pos = base[k] + o + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
-                                                                          __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+            if (mine) pos = base[key] + o + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                                            __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
         });
         if (sm < 0) continue;
         const PlaneOut& O = out[sm];
-        const double n = (double)tab[c].cnt;
+        const double cn = (double)tab[c].cnt;
         VoxOut v;
         v.key = (long long)(tag & ((1ull << 48) - 1));
-        v.x = (float)(tab[c].s[0] / n);
-        v.y = (float)(tab[c].s[1] / n);
-        v.z = (float)(tab[c].s[2] / n);
+        v.x = (float)(tab[c].s[0] / cn);
+        v.y = (float)(tab[c].s[1] / cn);
+        v.z = (float)(tab[c].s[2] / cn);
         v.pad = 0.f;
         if (O.vox_off + pos < pool_cap) pool[O.vox_off + pos] = v;
         tab[c].tag = 0;
@@ -2197,7 +2214,10 @@ int launch_segmentation(r360_frame* f) {
     else
         hipLaunchKernelGGL(k_trace<false>, dim3(8), dim3(TR_TPB), 0, st, nbm, P.cloud, w, h, P.nmodels, P.out,
                            P.contour, P.contour_cap, P.err);
-    if (ctx_vhash_reserve(ctx, 12L * N)) return -1;
+    static const int vox_px_env = getenv("R360_VOX_PX") ? atoi(getenv("R360_VOX_PX")) : VOX_PX;   // experiments
+    const int vox_px = std::min(vox_px_env, N);   // a block spans at most two sensors
+    const long vox_blocks = (total + vox_px - 1) / vox_px;
+    if (ctx_vhash_reserve(ctx, 12L * N, vox_blocks * vox_px, vox_blocks)) return -1;
     hipLaunchKernelGGL(k_alloc, dim3(1), dim3(512), 0, st, P.nmodels, P.out,
                        (unsigned long long)ctx->vhash_cap, P.totals);
     timing_end(ctx, slot);
@@ -2205,13 +2225,11 @@ int launch_segmentation(r360_frame* f) {
     slot = timing_begin(ctx, "k_voxel");
     // the voxel kernels exit at entry when no region lacks a contour (totals[3] == 0, the usual case); the table is
     // zero on allocation and k_vox_compact clears every cell it reads
-    static const int vox_px_env = getenv("R360_VOX_PX") ? atoi(getenv("R360_VOX_PX")) : VOX_PX;   // experiments
-    const int vox_px = std::min(vox_px_env, N);   // a block spans at most two sensors
-    hipLaunchKernelGGL(k_vox_hash, dim3((unsigned)((total + vox_px - 1) / vox_px)), dim3(VOX_TPB), 0, st, P.cloud,
-                       P.state, N, P.nmodels, P.out, ctx->d_vhash, P.totals, P.err, vox_px);
+    hipLaunchKernelGGL(k_vox_hash, dim3((unsigned)vox_blocks), dim3(VOX_TPB), 0, st, P.cloud, P.state, N, P.nmodels,
+                       P.out, ctx->d_vhash, P.totals, P.err, vox_px, ctx->d_vlist, ctx->d_vcnt);
     hipLaunchKernelGGL(k_vox_alloc, dim3(1), dim3(512), 0, st, P.nmodels, P.out, P.totals, P.vox_cap, P.err);
-    hipLaunchKernelGGL(k_vox_compact, dim3(VOXC_BLOCKS), dim3(VOXC_TPB), 0, st, ctx->d_vhash, P.totals, P.out, P.vox,
-                       P.vox_cap);
+    hipLaunchKernelGGL(k_vox_compact, dim3((unsigned)vox_blocks), dim3(VOXC_TPB), 0, st, ctx->d_vhash, P.totals, P.out,
+                       P.vox, P.vox_cap, ctx->d_vlist, ctx->d_vcnt, vox_px);
     timing_end(ctx, slot);
     R360_HIP(hipGetLastError());
     return 0;

@@ -307,6 +307,9 @@ struct r360_ctx {
     // VoxelGrid hash table (plane builds of the frames on this ctx)
     VoxCell* d_vhash = nullptr;
     long vhash_cap = 0;
+    int* d_vlist = nullptr;          // cells each k_vox_hash workgroup claimed [vlist_cap], its count per workgroup
+    int* d_vcnt = nullptr;           //   [vcnt_cap] (k_vox_compact walks these instead of the whole table)
+    long vlist_cap = 0, vcnt_cap = 0;
     // Register() in flight (r360_register_async)
     int reg_pending = 0, reg_good = 0;
     float reg_info[36];
@@ -429,7 +432,7 @@ int launch_plane_publish(r360_frame* f);   // plane outputs -> pinned host buffe
 int plane_bufs_alloc(r360_frame* f);
 void plane_bufs_free(r360_frame* f);
 int planes_enqueue(r360_frame* f);
-int ctx_vhash_reserve(r360_ctx* ctx, long min_cells);
+int ctx_vhash_reserve(r360_ctx* ctx, long min_cells, long list_entries, long list_groups);
 int planes_finish(r360_frame* f);
 // rotOffset (157.5 deg about x, OdometryRGBD360.cpp:138-139) and its inverse; column-major 4x4 product C = A*B
 void r360_rot_offset(float Ro[16], float Ri[16]);
