@@ -318,8 +318,9 @@ __global__ void k_dcm(const float4* __restrict__ cloud, int w, int h, float* __r
 // and a 10-term window for the within-row chain reproduce every value below the cap bit for bit
 // (rounding is monotone: fl(min(a,b)+1) = min(fl(a+1), fl(b+1))).  Values at or above the cap are
 // upper bounds of the true ones and never win the min.
-constexpr int DM_BAND = 4, DM_HALO = 10, DM_TPB = 256;   // short bands: the halo rows run in parallel
-// (one wave per band measured 2.3x slower: the 10-term chain windows of 5 columns per lane serialise)
+constexpr int DM_BAND = 4, DM_HALO = 10, DM_TPB = 512;   // short bands: the halo rows run in parallel
+// (one wave per band measured 2.3x slower: the 10-term chain windows of 5 columns per lane serialise); a thread per
+// column at VGA (w = 320): 256 threads 64 us, 320 41 us, 512 39 us per frame; bands of 2 / 3 / 6 / 8 rows slower
 
 __device__ __forceinline__ void dm_sync() { __syncthreads(); }
 
