@@ -8,6 +8,7 @@
 // one method / parameter set) and runs them as ONE batched alignment (r360_align360_batch_async): one launch
 // per pass over all pairs instead of one small launch per pair and stream.  While a batch runs, the next one
 // accumulates, so the batch size follows the load.  A job's result is exactly the single-pair result.
+#include <chrono>
 #include <condition_variable>
 #include <cstring>
 #include <deque>
@@ -68,6 +69,13 @@ static void dispatcher(r360_dense_queue* q) {
         std::unique_lock<std::mutex> lk(q->m);
         q->cv_work.wait(lk, [&] { return q->quit || !q->pending.empty(); });
         if (q->pending.empty()) break;   // quit with nothing pending
+        // optional batch floor (R360_QUEUE_MIN jobs, waiting at most R360_QUEUE_WAIT_US): larger batches fill the
+        // level-0 pass better at the cost of latency (experiment knob, off by default)
+        static const int min_jobs = getenv("R360_QUEUE_MIN") ? atoi(getenv("R360_QUEUE_MIN")) : 0;
+        static const int wait_us = getenv("R360_QUEUE_WAIT_US") ? atoi(getenv("R360_QUEUE_WAIT_US")) : 2000;
+        if (min_jobs > 1 && (int)q->pending.size() < min_jobs)
+            q->cv_work.wait_for(lk, std::chrono::microseconds(wait_us),
+                                [&] { return q->quit || (int)q->pending.size() >= min_jobs; });
         take.clear();
         const r360_dense_queue::Job& first = q->jobs[q->pending.front()];
         for (auto it = q->pending.begin(); it != q->pending.end() && (int)take.size() < q->max_batch;) {
