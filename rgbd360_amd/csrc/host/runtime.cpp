@@ -170,6 +170,7 @@ extern "C" void r360_ctx_destroy(r360_ctx* c) {
     for (auto e : c->ev_pool) hipEventDestroy(e);
     hipEventDestroy(c->wait_ev);
     if (c->mwait_ev) hipEventDestroy(c->mwait_ev);   // mstream is the device's shared match stream
+    for (auto& g : c->graphs) hipGraphExecDestroy(g.exec);
     hipFree(c->d_state);
     hipFree(c->d_partials);
     hipFree(c->d_gticket);
@@ -737,6 +738,64 @@ static int check_pair(r360_ctx* ctx, r360_frame* trg, r360_frame* src, const r36
     return 0;
 }
 
+// Replays the captured pass sequence of (trg, src, method, p) on ctx's stream, capturing it on first use.  The key
+// holds everything the launches read besides device memory contents: the frames' level buffers and sizes, the
+// sphere tables, the ctx's state / record / counter / queue buffers, the method and the parameters.
+template <class Enqueue>
+static int align_graph_launch(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src, int method,
+                              const r360_icp_params* p, Enqueue&& enqueue) {
+    std::vector<uintptr_t> key;
+    key.reserve(16 + 20 * p->n_pyr);
+    auto put = [&](const void* q) { key.push_back((uintptr_t)q); };
+    put(trg); put(src); key.push_back((uintptr_t)method);
+    put(ctx->d_state); put(ctx->d_partials); put(ctx->d_gticket); put(ctx->d_defer);
+    key.push_back((uintptr_t)ctx->defer_cap); key.push_back((uintptr_t)ctx->partials_cap); put(ctx->d_ktime);
+    put(src->d_npts); put(src->calib);
+    {
+        uintptr_t w[(sizeof(r360_icp_params) + sizeof(uintptr_t) - 1) / sizeof(uintptr_t)] = {};
+        memcpy(w, p, sizeof(r360_icp_params));
+        for (uintptr_t x : w) key.push_back(x);
+    }
+    for (int l = 0; l < p->n_pyr; ++l) {
+        for (const r360_frame* f : {trg, src}) {
+            const LevelBufs& L = f->lv[l];
+            key.push_back(((uintptr_t)(unsigned)L.rows << 32) | (unsigned)L.cols);
+            put(L.p0); put(L.tg); put(L.pts); put(L.pk);
+        }
+        const LevelTrig& T = src->calib->trig[l];
+        put(T.sinphi); put(T.cosphi); put(T.sinth); put(T.costh);
+    }
+    ++ctx->graph_clock;
+    for (auto& g : ctx->graphs)
+        if (g.key == key) {
+            g.used = ctx->graph_clock;
+            R360_HIP(hipGraphLaunch(g.exec, ctx->stream));
+            return 0;
+        }
+    hipGraph_t graph = nullptr;
+    R360_HIP(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeRelaxed));
+    const int rc = enqueue();
+    const hipError_t ec = hipStreamEndCapture(ctx->stream, &graph);
+    if (rc) { if (graph) (void)hipGraphDestroy(graph); return rc; }
+    R360_HIP(ec);
+    hipGraphExec_t exec = nullptr;
+    const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    R360_HIP(ei);
+    constexpr size_t kMaxGraphs = 8;   // e.g. the ordered pairs of three rotating frame buffers
+    if (ctx->graphs.size() >= kMaxGraphs) {
+        size_t lru = 0;
+        for (size_t i = 1; i < ctx->graphs.size(); ++i)
+            if (ctx->graphs[i].used < ctx->graphs[lru].used) lru = i;
+        R360_HIP(hipStreamSynchronize(ctx->stream));   // the evicted graph may still be running
+        (void)hipGraphExecDestroy(ctx->graphs[lru].exec);
+        ctx->graphs.erase(ctx->graphs.begin() + (long)lru);
+    }
+    ctx->graphs.push_back({std::move(key), exec, ctx->graph_clock});
+    R360_HIP(hipGraphLaunch(exec, ctx->stream));
+    return 0;
+}
+
 extern "C" int r360_align360_async(r360_ctx* ctx, r360_frame* trg, r360_frame* src, const float init[16], int method,
                                    int occlusion, const r360_icp_params* p) {
     if (int rc = check_pair(ctx, trg, src, p)) return rc;
@@ -750,12 +809,23 @@ extern "C" int r360_align360_async(r360_ctx* ctx, r360_frame* trg, r360_frame* s
     memcpy(h->cand, init, sizeof(float) * 16);
     h->dbg[8] = ~0ull;
     R360_HIP(hipMemcpyAsync(ctx->d_state, h, sizeof(IcpState), hipMemcpyHostToDevice, ctx->stream));
-    for (int l = p->n_pyr - 1; l >= 0; --l) {
-        const int np = src->lv[l].rows * src->lv[l].cols;
-        const IcpConst C = make_const(p, l, np, occlusion);
-        const int passes = 1 + ((l == 0 && p->fixed_iters_level0 > 0) ? p->fixed_iters_level0 : p->max_iters);
-        for (int k = 0; k < passes; ++k)
-            if (launch_icp_level(ctx, trg, src, l, method, C, k == 0, 0)) return -1;
+    auto passes_of = [&]() -> int {
+        for (int l = p->n_pyr - 1; l >= 0; --l) {
+            const int np = src->lv[l].rows * src->lv[l].cols;
+            const IcpConst C = make_const(p, l, np, occlusion);
+            const int passes = 1 + ((l == 0 && p->fixed_iters_level0 > 0) ? p->fixed_iters_level0 : p->max_iters);
+            for (int k = 0; k < passes; ++k)
+                if (launch_icp_level(ctx, trg, src, l, method, C, k == 0, 0)) return -1;
+        }
+        return 0;
+    };
+    // graphs for the plain pass (occlusion passes size their buffers on first use) without per-launch timing
+    // events; R360_NO_GRAPH=1 launches one by one (A/B)
+    static const bool no_graph = getenv("R360_NO_GRAPH") && atoi(getenv("R360_NO_GRAPH")) != 0;
+    if (no_graph || R360_POLL || occlusion || ctx->timing) {
+        if (passes_of()) return -1;
+    } else {
+        if (align_graph_launch(ctx, trg, src, method, p, passes_of)) return -1;
     }
     ctx->async_nL = p->n_pyr;
     ctx->async_pending = 1;

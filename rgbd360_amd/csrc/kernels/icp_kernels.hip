@@ -550,7 +550,9 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
     __shared__ float s_red[NW][32];
     __shared__ double s_err[NW], s_errd[NW];
     __shared__ double s_fin[RG][32];
+#if !R360_POLL
     __shared__ int s_last;
+#endif
     __shared__ int s_qn[NW];   // PF 5: deferred entries per wave
     __shared__ GnShared s_gn;
     __shared__ IcpState s_state;
@@ -1202,8 +1204,9 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
             asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
             g_blk_stamps[2][blockIdx.x] = ((unsigned long long)xcc << 32) | hw;
         }
-        __hip_atomic_fetch_min(&S->dbg[8], t_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_max(&S->dbg[9], t_loop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // no grid-wide min / max here: 2 x 512 same-address atomics at the loop end serialised for ~10 us when
+        // every workgroup finishes at once (coarse levels) and showed up as a ticket delay; the host takes
+        // them from the per-workgroup stamps
     }
 #endif
 
@@ -1245,6 +1248,27 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
+#if R360_POLL
+    // ---- stage 2: record flags; the job's last workgroup polls them, reduces all records and runs the GN step
+    // Every workgroup but the last stores this launch's sequence number (C.seq, unique per launch on the ctx)
+    // into its own flag word once its record is drained (the sc1 record stores and the barrier as below); the
+    // last workgroup of the job (dispatched after all the others, so it waits only on workgroups that have
+    // started) reads the nb - 1 flags in parallel until every one holds C.seq.  No same-address
+    // atomics: the arrival ticket serialised 512 simultaneous arrivals at the memory side (a coarse level's
+    // workgroups all finish within a microsecond, and their ticket took ~12 us of the pass; profiles/r3_lone).
+    {
+        const int nb = (int)gridDim.x;
+        if ((int)blockIdx.x != nb - 1) {
+            if (threadIdx.x == 0)
+                __hip_atomic_store(gcnt + blockIdx.x, C.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+        for (int b = threadIdx.x; b < nb - 1; b += TPB)
+            while (__hip_atomic_load(gcnt + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != C.seq)
+                __builtin_amdgcn_s_sleep(1);
+        __syncthreads();
+    }
+#else
     // ---- stage 2: arrival ticket; the last workgroup reduces all records and runs the GN step
     // Hand-off (MI355X_MICROARCH.md 'Valid forms', row 1): every record store is sc1 and drained by
     // its wave (vmcnt(0) above) before the barrier; one relaxed agent-scope add per workgroup; the
@@ -1270,6 +1294,7 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
     if (!s_last) return;
     if (threadIdx.x < R360_TICKET_GROUPS)   // every group is complete: reset its counter for the next pass
         __hip_atomic_store(gcnt + threadIdx.x * R360_TICKET_STRIDE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
 #ifdef R360_STAMPS
     const unsigned long long t_ticket = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1821,7 +1846,10 @@ static long defer_need(int npx, int nb) {
 }
 
 static int launch_jobs(r360_ctx* ctx, const IcpJobs& jobs, int njobs, const LevelBufs& Ls, const LevelTrig& T,
-                       int level, int method, const IcpConst& C, int first, int eval_only, const PassGrid& G) {
+                       int level, int method, const IcpConst& C0, int first, int eval_only, const PassGrid& G) {
+    IcpConst C = C0;
+    if (++ctx->icp_seq == 0) ++ctx->icp_seq;   // the record flags start (and may stale) at 0
+    C.seq = ctx->icp_seq;
     const char* name = level == 0 ? "k_icp_pass_L0" : "k_icp_pass";
     const int slot = timing_begin(ctx, name);
     const int pf = G.pf, nb = G.nb;

@@ -70,7 +70,7 @@ struct IcpConst {
     double tol_res, tol_upd, lambda;
     int max_iters, fixed_iters0, n_pixels, level;
     int occ;                  // alignFrames360 occlusion: 0 plain, 1 Occ1, 2 Occ2 (:4598-4627)
-    int pad1;
+    unsigned seq;             // ICP pass: launch sequence number on the ctx (never 0), the record flags' value
 };
 
 // Device-resident Gauss-Newton state of one alignFrames360 call.
@@ -113,12 +113,15 @@ struct IcpJob {
     const uint32_t* tpk;        // level 0: target packed image
     IcpState* S;
     double* partials;           // per-workgroup records
-    unsigned* gcnt;             // group arrival counters (R360_TICKET_GROUPS x R360_TICKET_STRIDE)
+    unsigned* gcnt;             // per-workgroup record flags (R360_POLL) / group arrival counters (16384 words)
     int* dq;                    // deferred-pixel queues
 };
 struct IcpJobs { IcpJob j[R360_MAX_BATCH]; };   // passed by value (kernel arguments, 1152 B)
 
 constexpr int R360_KT_SLOTS = 26;
+#ifndef R360_POLL   // 0: arrival tickets; 1 (experiment builds): record flags polled by the job's last workgroup
+#define R360_POLL 0
+#endif
 #ifndef R360_TICKET_GROUPS_N   // experiment builds may regroup the same 16384 counter words
 #define R360_TICKET_GROUPS_N 16
 #endif
@@ -262,6 +265,13 @@ struct r360_ctx {
     int* occ_list = nullptr;
     int* occ_bsum = nullptr;
     int partials_cap = 0;
+    unsigned icp_seq = 0;            // ICP launches on this ctx (IcpConst::seq)
+    // alignFrames360's fixed pass sequence (levels n_pyr-1..0, every GN pass) captured once per pair of frame
+    // buffers and replayed as one graph launch (r360_align360_async): the key lists every pointer, size and
+    // parameter the launches read, so a replay issues exactly the launches the loop would
+    struct AlignGraph { std::vector<uintptr_t> key; hipGraphExec_t exec = nullptr; unsigned long long used = 0; };
+    std::vector<AlignGraph> graphs;
+    unsigned long long graph_clock = 0;
     IcpState* h_state = nullptr;  // pinned
     int timing = 0;
     std::vector<hipEvent_t> ev_pool;

@@ -27,9 +27,14 @@ for lv in (4, 3, 2, 1, 0):
     st = (C.c_ulonglong * 12)()
     R.lib().r360_ctx_debug_stamps(ctx.h, st)
     t = np.array(list(st), dtype=np.uint64).astype(np.float64)
-    base = t[5]
+    # grid-wide first start / last loop end from the per-workgroup stamps of this level's last pass
+    nbl = min(512, -(-fr[0].level(lv)["gray"].size // 256))
+    bs = (C.c_ulonglong * (3 * 8192))()
+    R.lib().r360_debug_block_stamps(bs, 8192)
+    ab = np.array(list(bs), dtype=np.float64).reshape(3, 8192)[:2, :nbl]
+    base = ab[0].min()
     us = lambda x: (x - base) / 100.0
-    print(f"level {lv}: all-blocks loop end {us(t[6]):7.2f} | last block: start {us(t[0]):7.2f} loop-end {us(t[1]):7.2f}"
+    print(f"level {lv} ({nbl} wg): all-blocks loop end {us(ab[1].max()):7.2f} | last block: start {us(t[0]):7.2f} loop-end {us(t[1]):7.2f}"
           f" ticket {us(t[2]):7.2f} records {us(t[3]):7.2f} end {us(t[4]):7.2f}  (us from first block start)")
 
 # per-workgroup start / loop-end distribution of the last level-0 pass
