@@ -1277,6 +1277,61 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
     // Two-level ticket: agent-scope atomics on one address serialise at the memory side (~50 ns each,
     // 256 of them were ~13 us of every level-0 pass), so workgroups first count in 16 group counters
     // (4 KB apart) and only the last of each group takes the pass ticket: 32 + 16 deep instead of 512.
+#if R360_GROUP_SUM
+    // Two-level record sum along the two-level ticket: the last workgroup of ticket group g (records g, g + 16,
+    // ...) sums its group's records into a group record (slot nb + g) while other groups are still arriving, and
+    // the last group's workgroup then sums only the 16 group records.  Group sum: thread (s, q) adds records
+    // j = s, s + 16 of the group (16 B of each, sc1 loads), then slot v is summed over s in order; the final sum
+    // adds the group records in group order.  Fixed order for a given grid, so a job's sums are the same in any
+    // batch; one load round on the last group's path instead of four (512 records, 8 in flight per lane).
+    const int nb = (int)gridDim.x;
+    const int ng = nb < R360_TICKET_GROUPS ? nb : R360_TICKET_GROUPS;
+    if (threadIdx.x == 0) {
+        const int g = (int)blockIdx.x % R360_TICKET_GROUPS;
+        const unsigned gsz = (unsigned)((nb - g + R360_TICKET_GROUPS - 1) / R360_TICKET_GROUPS);
+        const unsigned prev = __hip_atomic_fetch_add(gcnt + g * R360_TICKET_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = prev == gsz - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    {
+        const int g = (int)blockIdx.x % R360_TICKET_GROUPS;
+        const int gsz = (nb - g + R360_TICKET_GROUPS - 1) / R360_TICKET_GROUPS;
+        const int q = threadIdx.x & 15, sj = threadIdx.x >> 4;
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(partials, 0, (nb + R360_TICKET_GROUPS) * 256, 0x00020000);
+        double a0 = 0.0, a1 = 0.0;
+        for (int j = sj; j < gsz; j += 2 * RG) {
+            const int j2 = j + RG < gsz ? j + RG : j;   // two loads in flight
+            const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, ((g + j * R360_TICKET_GROUPS) * 16 + q) * 16, 0, 16);
+            const auto y = __builtin_amdgcn_raw_buffer_load_b128(rs, ((g + j2 * R360_TICKET_GROUPS) * 16 + q) * 16, 0, 16);
+            a0 += __longlong_as_double((long long)(((unsigned long long)x[1] << 32) | x[0]));
+            a1 += __longlong_as_double((long long)(((unsigned long long)x[3] << 32) | x[2]));
+            if (j2 != j) {
+                a0 += __longlong_as_double((long long)(((unsigned long long)y[1] << 32) | y[0]));
+                a1 += __longlong_as_double((long long)(((unsigned long long)y[3] << 32) | y[2]));
+            }
+        }
+        s_fin[sj][2 * q] = a0;
+        s_fin[sj][2 * q + 1] = a1;
+        __syncthreads();
+        if (threadIdx.x < 32) {
+            double t = 0.0;
+            for (int k = 0; k < RG; ++k) t += s_fin[k][threadIdx.x];
+            __hip_atomic_store(reinterpret_cast<unsigned long long*>(partials) + (long)(nb + g) * 32 + threadIdx.x,
+                               (unsigned long long)__double_as_longlong(t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const unsigned p2 = __hip_atomic_fetch_add(&S->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = p2 == (unsigned)ng - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    if (threadIdx.x < R360_TICKET_GROUPS)   // every group is complete: reset its counter for the next pass
+        __hip_atomic_store(gcnt + threadIdx.x * R360_TICKET_STRIDE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
     if (threadIdx.x == 0) {
         const int nb = (int)gridDim.x;
         const int ng = nb < R360_TICKET_GROUPS ? nb : R360_TICKET_GROUPS;
@@ -1295,9 +1350,24 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
     if (threadIdx.x < R360_TICKET_GROUPS)   // every group is complete: reset its counter for the next pass
         __hip_atomic_store(gcnt + threadIdx.x * R360_TICKET_STRIDE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #endif
+#endif
 #ifdef R360_STAMPS
     const unsigned long long t_ticket = __builtin_amdgcn_s_memrealtime();
 #endif
+#if !R360_POLL && R360_GROUP_SUM
+    if (threadIdx.x < 16 * R360_TICKET_GROUPS) {   // the group records, 16 B per lane
+        const int q = threadIdx.x & 15, g = threadIdx.x >> 4;
+        double a0 = 0.0, a1 = 0.0;
+        if (g < ng) {
+            const auto rs = __builtin_amdgcn_make_buffer_rsrc(partials, 0, (nb + R360_TICKET_GROUPS) * 256, 0x00020000);
+            const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, ((nb + g) * 16 + q) * 16, 0, 16);
+            a0 = __longlong_as_double((long long)(((unsigned long long)x[1] << 32) | x[0]));
+            a1 = __longlong_as_double((long long)(((unsigned long long)x[3] << 32) | x[2]));
+        }
+        s_fin[g][2 * q] = a0;
+        s_fin[g][2 * q + 1] = a1;
+    }
+#else
     {
         // fixed-order reduction of the per-workgroup records: lane q of a 16-lane group loads bytes
         // 16q..16q+15 of records g, g+RG, ... with L1-bypassing (sc1) 16-B buffer loads, 8 in flight;
@@ -1322,6 +1392,7 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
         s_fin[g][2 * q] = a0;
         s_fin[g][2 * q + 1] = a1;
     }
+#endif
     __syncthreads();
     if (threadIdx.x < 32) {
         double t = 0.0;
@@ -1827,7 +1898,7 @@ static PassGrid pass_grid(const r360_ctx* ctx, const LevelBufs& Ls, int occ, int
     int cap = cap_env > 0 ? cap_env : 2 * occ_q.cus;
     static const int tot_env = env_int("R360_ICP_WG_TOTAL", -1);
     if (tot_env > 0) cap = ((tot_env / (njobs > 0 ? njobs : 1) + 7) / 8) * 8;
-    if (cap > ctx->partials_cap) cap = ctx->partials_cap;
+    if (cap > ctx->partials_cap - R360_TICKET_GROUPS) cap = ctx->partials_cap - R360_TICKET_GROUPS;   // + group records
     // at least R360_ICP_PXT points per thread (default 1; 8 measured no faster): the coarse levels (a quarter, ... of
     // level 0) then run on a few hundred / dozen workgroups per pair instead of one thread per point, which
     // shortens their record / ticket / final-sum tail (level 0 at VGA has ~19 per thread on the capped grid)

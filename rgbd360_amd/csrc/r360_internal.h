@@ -119,6 +119,9 @@ struct IcpJob {
 struct IcpJobs { IcpJob j[R360_MAX_BATCH]; };   // passed by value (kernel arguments, 1152 B)
 
 constexpr int R360_KT_SLOTS = 26;
+#ifndef R360_GROUP_SUM   // 1: group records summed by each ticket group's last workgroup; 0 (experiment builds): flat sum
+#define R360_GROUP_SUM 1
+#endif
 #ifndef R360_POLL   // 0: arrival tickets; 1 (experiment builds): record flags polled by the job's last workgroup
 #define R360_POLL 0
 #endif
