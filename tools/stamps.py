@@ -70,15 +70,28 @@ for part in range(4):
     sl = order[part * k // 4:(part + 1) * k // 4]
     print(f"start-quartile {part}: busy mean {busy[sl].mean():6.2f}")
 
-# align mode (device Gauss-Newton step in the last workgroup): stamps of the final pass
+# align mode (device Gauss-Newton step in the last workgroup): stamps of the final level-0 pass, beside an eval pass
+# at the aligned pose (same pixels, no GN step)
+def last_pass(label, nbl=512):
+    st = (C.c_ulonglong * 12)()
+    R.lib().r360_ctx_debug_stamps(ctx.h, st)
+    t = np.array(list(st), dtype=np.uint64).astype(np.float64)
+    bs = (C.c_ulonglong * (3 * 8192))()
+    R.lib().r360_debug_block_stamps(bs, 8192)
+    ab = np.array(list(bs), dtype=np.float64).reshape(3, 8192)[:2, :nbl]
+    base = ab[0].min()
+    us = lambda x: (x - base) / 100.0
+    le = (ab[1] - base) / 100.0
+    print(f"{label}: loop end pct 0/50/90/100 {np.percentile(le, [0, 50, 90, 100]).round(2)} | last block: start"
+          f" {us(t[0]):6.2f} loop-end {us(t[1]):6.2f} ticket {us(t[2]):6.2f} records {us(t[3]):6.2f} end {us(t[4]):6.2f}")
+
+
 if os.environ.get("ALIGN"):
     reg.params.fixed_iters_level0 = 20
     for rep in range(3):
         reg.alignFrames360(P, R.PHOTO_DEPTH)
-    st = (C.c_ulonglong * 12)()
-    R.lib().r360_ctx_debug_stamps(ctx.h, st)
-    t = np.array(list(st), dtype=np.uint64).astype(np.float64)
-    base = t[5]
-    us = lambda x: (x - base) / 100.0
-    print(f"align last pass: all-blocks loop end {us(t[6]):7.2f} | last block: start {us(t[0]):7.2f} loop-end {us(t[1]):7.2f}"
-          f" ticket {us(t[2]):7.2f} records {us(t[3]):7.2f} end (after GN) {us(t[4]):7.2f}")
+    last_pass("align last L0 pass")
+    Pa = np.asarray(reg.getOptimalPose(), dtype=np.float32)
+    for rep in range(4):
+        reg.eval(0, Pa, R.PHOTO_DEPTH)
+    last_pass("eval at aligned pose")
