@@ -574,11 +574,17 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
         __hip_atomic_store(kt, (unsigned long long)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
+#ifdef R360_STAMPS
+    // R360_STAMP_ENTRY: the start stamp before the state read (default: after it)
+#ifdef R360_STAMP_ENTRY
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+#endif
+#endif
     if (S->stop || (!first && !S->active && !eval_only)) {
         if (blockIdx.x == 0 && threadIdx.x == 0) pass_arrive(kt, false, C.level);
         return;
     }
-#ifdef R360_STAMPS
+#if defined(R360_STAMPS) && !defined(R360_STAMP_ENTRY)
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #endif
 
