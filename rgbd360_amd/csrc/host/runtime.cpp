@@ -722,6 +722,10 @@ static IcpConst make_const(const r360_icp_params* p, int level, int n_pixels, in
     C.sd_photo_inv_d = 1. / p->std_dev_photo;
     C.tol_res = p->tol_residual; C.tol_upd = p->tol_update; C.lambda = p->lambda;
     C.max_iters = p->max_iters; C.fixed_iters0 = p->fixed_iters_level0;
+    // diagnostic only (tools/stamps.py ALIGN=1): the device GN expects more level-0 iterations than are launched,
+    // so the last launched pass is a continuing one
+    static const int diag_extra = getenv("R360_DIAG_EXTRA_ITERS") ? atoi(getenv("R360_DIAG_EXTRA_ITERS")) : 0;
+    if (C.fixed_iters0 > 0) C.fixed_iters0 += diag_extra;
     C.n_pixels = n_pixels; C.level = level; C.occ = occ;
     return C;
 }
