@@ -475,6 +475,10 @@ def main(argv=None, runner_factory=None):
     iso_ms, n, iso_ach, lone_ms = 0.0, 0, None, None
     if not args.no_isolated:
         fa, fb = runner.frames[0][:2]
+        # two consecutive frames of the sequence (the pipeline's ring buffers hold frames up to depth + 2 apart)
+        for f, j in ((fa, p0), (fb, p0 + 1)):
+            f.upload(*frames_of(j))
+            f.build()
         reg = R.RegisterPhotoICP(ctxs[0])
         reg.params = params
         reg.setTargetFrame(fa)

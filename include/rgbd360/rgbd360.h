@@ -25,13 +25,20 @@
 //     sphereDepth are views of the frame's sphere in HBM: RegisterPhotoICP::setSourceFrame(
 //     frame->sphereRGB, frame->sphereDepth) uses the frame's device pyramid without a copy; other images
 //     are uploaded and pyramided on the GPU (r360_frame_set_sphere);
-//   * objects are bound to an r360::Context (one GPU + HIP stream); errors throw r360::Error.
+//   * objects are bound to an r360::Context (one GPU + HIP stream); errors throw r360::Error.  The constructors with
+//     the reference's signatures (Calib360(Resolution), RegisterPhotoICP(), RegisterRGBD360(configFile)) bind to
+//     r360::default_context(): one context per host thread on device $R360_DEVICE (default 0), created on first
+//     use.  include/rgbd360/compat.h brings the class names into the global namespace for unchanged call sites.
 #pragma once
 #include <rgbd360_hip.h>
 
 #include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <ostream>
 #include <map>
 #include <stdexcept>
 #include <string>
@@ -74,7 +81,49 @@ struct MatrixNf {                       // column-major, Eigen's (row, col) and 
             }
         return o;
     }
+    // inverse by Gauss-Jordan elimination with partial pivoting in double (Eigen's Matrix4f::inverse() uses
+    // cofactors in float: the two agree to float rounding)
+    MatrixNf inverse() const {
+        double A[N][2 * N];
+        for (int r = 0; r < N; ++r)
+            for (int c = 0; c < 2 * N; ++c) A[r][c] = c < N ? (*this)(r, c) : (c - N == r ? 1.0 : 0.0);
+        for (int k = 0; k < N; ++k) {
+            int p = k;
+            for (int r = k + 1; r < N; ++r) if (std::fabs(A[r][k]) > std::fabs(A[p][k])) p = r;
+            for (int c = 0; c < 2 * N; ++c) { const double t = A[k][c]; A[k][c] = A[p][c]; A[p][c] = t; }
+            const double piv = A[k][k];
+            for (int c = 0; c < 2 * N; ++c) A[k][c] /= piv;
+            for (int r = 0; r < N; ++r)
+                if (r != k) { const double f = A[r][k]; for (int c = 0; c < 2 * N; ++c) A[r][c] -= f * A[k][c]; }
+        }
+        MatrixNf o;
+        for (int r = 0; r < N; ++r)
+            for (int c = 0; c < N; ++c) o(r, c) = float(A[r][c + N]);
+        return o;
+    }
+    // block(r0, c0, rows, cols) as a read-only view with Eigen's norm() (e.g. the translation's length,
+    // rigidTransf.block(0,3,3,1).norm(), OdometryRGBD360.cpp:228)
+    struct Block {
+        const MatrixNf* m;
+        int r0, c0, rows, cols;
+        float operator()(int r, int c) const { return (*m)(r0 + r, c0 + c); }
+        float norm() const {
+            float s = 0.f;
+            for (int c = 0; c < cols; ++c)
+                for (int r = 0; r < rows; ++r) s += (*this)(r, c) * (*this)(r, c);
+            return std::sqrt(s);
+        }
+    };
+    Block block(int r0, int c0, int rows, int cols) const { return Block{this, r0, c0, rows, cols}; }
 };
+template <int N>
+inline std::ostream& operator<<(std::ostream& os, const MatrixNf<N>& m) {
+    for (int r = 0; r < N; ++r) {
+        for (int c = 0; c < N; ++c) os << (c ? " " : "") << m(r, c);
+        if (r + 1 < N) os << "\n";
+    }
+    return os;
+}
 typedef MatrixNf<4> Matrix4f;
 typedef MatrixNf<6> Matrix6f;
 #endif
@@ -106,22 +155,53 @@ class Context {
     r360_ctx* h_ = nullptr;
 };
 
+// The context the reference-signature constructors bind to: one per host thread (its own HIP stream), on device
+// $R360_DEVICE (default 0), created on first use and destroyed at thread exit — objects built on a thread must not
+// outlive it.
+inline int default_device() {
+    const char* e = std::getenv("R360_DEVICE");
+    return e ? std::atoi(e) : 0;
+}
+inline Context& default_context() {
+    thread_local Context ctx(default_device());
+    return ctx;
+}
+
+// printf-style std::string (the callers' mrpt::format for file names)
+inline std::string format(const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    char buf[4096];
+    std::vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    return std::string(buf);
+}
+inline std::string data_dir() { return r360_data_dir(); }
+
 // ------------------------------------------------------------------ Calib360
 class Calib360 {
   public:
+    // Resolution mode of the device (Calib360.h:62-67): per-sensor images of 480/res x 640/res
+    enum Resolution { VGA = 1, QVGA = 2, QQVGA = 4 };
+    // Calib360(Resolution res = QVGA) (Calib360.h:70), on the thread's default context
+    explicit Calib360(Resolution res = QVGA) : Calib360(default_context(), 480 / int(res), 640 / int(res)) {}
     // rows x cols per sensor (the reference's QVGA default, Calib360.h:73-77)
     explicit Calib360(Context& ctx, int rows = 240, int cols = 320) : ctx_(ctx) {
         check(r360_calib_create(ctx.get(), rows, cols, &h_), "r360_calib_create");
+        resolution = Resolution(cols > 0 && 640 % cols == 0 ? 640 / cols : 0);
     }
     ~Calib360() { r360_calib_destroy(h_); }
     Calib360(const Calib360&) = delete;
     Calib360& operator=(const Calib360&) = delete;
-    void loadExtrinsicCalibration(const std::string& dir) {
+    // "" = the shipped calibration (data/calib/Extrinsics), as the reference's default argument (Calib360.h:122-125)
+    void loadExtrinsicCalibration(const std::string& dir = "") {
         check(r360_calib_load_extrinsics(h_, dir.c_str()), "loadExtrinsicCalibration");
     }
-    void loadIntrinsicCalibration(const std::string& dir) {
+    // "" = data/calib/Intrinsics (Calib360.h:104-107)
+    void loadIntrinsicCalibration(const std::string& dir = "") {
         check(r360_calib_load_intrinsics(h_, dir.c_str()), "loadIntrinsicCalibration");
     }
+    Resolution resolution;
     Matrix4f getRt_id(int sensor_id) const {
         float rt[128];
         check(r360_calib_get_extrinsics(h_, rt, nullptr, nullptr), "getRt_id");
@@ -268,6 +348,8 @@ class RegisterPhotoICP {
   public:
     enum costFuncType { PHOTO_CONSISTENCY = 0, DEPTH_CONSISTENCY = 1, PHOTO_DEPTH = 2 };
     explicit RegisterPhotoICP(Context& ctx) : ctx_(ctx) { r360_icp_default_params(&p_); }
+    // RegisterPhotoICP() (RegisterPhotoICP.h:201), on the thread's default context
+    RegisterPhotoICP() : RegisterPhotoICP(default_context()) {}
     ~RegisterPhotoICP() {
         for (auto& o : own_) { r360_frame_destroy(o.frame); r360_calib_destroy(o.calib); }
     }
@@ -359,6 +441,8 @@ class RegisterRGBD360 {
     enum registrationType { DEFAULT_6DoF = 0, PLANAR_3DoF = 1, ODOMETRY_6DoF = 2, PLANAR_ODOMETRY_3DoF = 3 };
     // matcher.configLocaliser.load_params(configFile) (:97-100): the [global]/[unary]/[binary] thresholds of
     // the mrpt-pbmap ini; without a file, configLocaliser_sphericalOdometry.ini's values
+    // RegisterRGBD360(configFile) (RegisterRGBD360.h:97), on the thread's default context
+    explicit RegisterRGBD360(const std::string& configFile = "") : RegisterRGBD360(default_context(), configFile) {}
     RegisterRGBD360(Context& ctx, const std::string& configFile = "") : ctx_(ctx), config_(configFile) {
         std::memset(informationM_.data(), 0, sizeof(float) * 36);
         r360_match_params_default(&match_);

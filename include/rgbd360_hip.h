@@ -39,6 +39,9 @@ int         r360_ctx_sync(r360_ctx* ctx);
 void*       r360_ctx_stream(r360_ctx* ctx);        /* hipStream_t of the ctx */
 const char* r360_last_error(void);
 const char* r360_version(void);
+/* The shipped data directory (calib/, config_files/, samples/): $R360_DATA_DIR, else <tree>/data of the tree the
+ * library sits in — the files the reference finds under PROJECT_SOURCE_PATH (Calib360.h:107, :125). */
+const char* r360_data_dir(void);
 
 /* ---------------------------------------------------------------- Calib360
  * Replaces include/Calib360.h:44-132.  rows/cols = per-sensor image size; the pinhole
@@ -49,10 +52,12 @@ void r360_calib_destroy(r360_calib* c);
 /* Rt_[8] (Calib360.h:53), column-major 8 x float[16]; Rt_inv is derived (Calib360.h:129). */
 int  r360_calib_set_extrinsics(r360_calib* c, const float* rt8);
 int  r360_calib_get_extrinsics(const r360_calib* c, float* rt8, float* rt_inv8, float K[9]);
-/* loadExtrinsicCalibration(dir): reads dir/Rt_0{1..8}.txt (Calib360.h:122-131). */
+/* loadExtrinsicCalibration(dir): reads dir/Rt_0{1..8}.txt (Calib360.h:122-131); dir NULL or "" = the shipped
+ * r360_data_dir()/calib/Extrinsics (the reference's "" default, :124-125). */
 int  r360_calib_load_extrinsics(r360_calib* c, const char* dir);
 /* loadIntrinsicCalibration(dir): CLAMS dir/distortion_model{1..8} + downsampleParams(2)
- * (Calib360.h:104-119).  Without intrinsics undistort() is the identity. */
+ * (Calib360.h:104-119); dir NULL or "" = r360_data_dir()/calib/Intrinsics (:106-107).  Without intrinsics
+ * undistort() is the identity. */
 int  r360_calib_load_intrinsics(r360_calib* c, const char* dir);
 /* A calibration without sensors for spheres given as images (setSourceFrame / setTargetFrame(cv::Mat&,
  * cv::Mat&), RegisterPhotoICP.h:480-516): the ICP tables of an sph_rows x sph_cols sphere
@@ -495,6 +500,9 @@ int r360_proj_check_pose(const float* lx, const float* ly, const float* lz, int 
 int r360_rn_check(unsigned n, unsigned seed, unsigned long long out[2]);
 /* The device ILL-POSED test: Eigen FullPivLU<Matrix<float,6,6>>::rank() of n row-major matrices. */
 int r360_rank6(const float* M, int n, int* ranks);
+/* The device GN solve x = -H^-1 g (RegisterPhotoICP.h:4693; Gaussian elimination with partial pivoting in
+ * double) of n systems: H row-major n x 36, g n x 6, x n x 6. */
+int r360_solve6(const double* H, const double* g, int n, double* x);
 int r360_libm_eval(const float* x, const float* y, const float* z, int n, float* asin_out, float* atan2_out,
                    int on_device);
 

@@ -126,6 +126,7 @@ def lib() -> C.CDLL:
                                                    C.POINTER(IcpParams), fp, fp, C.POINTER(DenseStats)]),
             "orc_exp_se3": (None, [dp, C.c_int, fp]),
             "orc_rank6f": (C.c_int, [fp]),
+            "orc_solve6": (C.c_int, [dp, dp, dp]),
             "orc_huber": (C.c_float, [C.c_float, C.c_float]),
             "orc_libm": (None, [fp, fp, fp, C.c_int, fp, fp]),
             "orc_cloud_downsample": (None, [fp, vp, C.c_int, C.c_int, fp, vp]),
@@ -442,6 +443,16 @@ def rank6f(M) -> int:
     """Eigen FullPivLU<Matrix<float,6,6>>::rank() of M (the alignFrames360 ILL-POSED test, :4682)."""
     m = np.ascontiguousarray(np.asarray(M, np.float32).reshape(6, 6))
     return int(lib().orc_rank6f(_f(m)))
+
+
+def solve6(H, g):
+    """x = -H^-1 g by the GN step's Gaussian elimination with partial pivoting (double, :4693)."""
+    h = np.ascontiguousarray(np.asarray(H, np.float64).reshape(36))
+    gg = np.ascontiguousarray(np.asarray(g, np.float64).reshape(6))
+    x = np.zeros(6, np.float64)
+    dp_ = C.POINTER(C.c_double)
+    lib().orc_solve6(h.ctypes.data_as(dp_), gg.ctypes.data_as(dp_), x.ctypes.data_as(dp_))
+    return x
 
 
 def libm(x, y, z):

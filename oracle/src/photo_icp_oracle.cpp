@@ -716,6 +716,11 @@ extern "C" int orc_rank6f(const float* M) {
     return rank6(Md);
 }
 
+// x = -H^-1 g by the GN step's Gaussian elimination (:4693), H row-major double; 0 when singular
+extern "C" int orc_solve6(const double* H, const double* g, double* x) {
+    return solve6(H, g, x) ? 1 : 0;
+}
+
 // glibc float asinf / atan2f as the reference calls them (std::asin(float), std::atan2(float, float))
 extern "C" void orc_libm(const float* x, const float* y, const float* z, int n, float* as, float* at) {
     for (int i = 0; i < n; ++i) { as[i] = std::asin(x[i]); at[i] = std::atan2(y[i], z[i]); }

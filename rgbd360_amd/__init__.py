@@ -257,6 +257,8 @@ _SIGS = [
     ("r360_libm_eval", C.c_int, [_FP, _FP, _FP, C.c_int, _FP, _FP, C.c_int]),
     ("r360_rn_check", C.c_int, [C.c_uint, C.c_uint, C.POINTER(C.c_ulonglong)]),
     ("r360_rank6", C.c_int, [_FP, C.c_int, _IP]),
+    ("r360_data_dir", C.c_char_p, []),
+    ("r360_solve6", C.c_int, [_DP, _DP, C.c_int, _DP]),
     ("r360_proj_check_pose", C.c_int, [_FP, _FP, _FP, C.c_int, _FP, C.c_int, C.c_int, C.POINTER(C.c_ulonglong),
                                        C.POINTER(C.c_ulonglong)]),
     ("r360_proj_check", C.c_int, [_FP, _FP, _FP, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_ulonglong),
@@ -321,6 +323,10 @@ def pcd_read(path: str):
 
 def _fptr(a: np.ndarray):
     return a.ctypes.data_as(_FP)
+
+
+def _dptr(a: np.ndarray):
+    return a.ctypes.data_as(_DP)
 
 
 def _vptr(a: np.ndarray):

@@ -71,8 +71,8 @@ static void dispatcher(r360_dense_queue* q) {
         if (q->pending.empty()) break;   // quit with nothing pending
         // optional batch floor (R360_QUEUE_MIN jobs, waiting at most R360_QUEUE_WAIT_US): larger batches fill the
         // level-0 pass better at the cost of latency (experiment knob, off by default)
-        static const int min_jobs = getenv("R360_QUEUE_MIN") ? atoi(getenv("R360_QUEUE_MIN")) : 0;
-        static const int wait_us = getenv("R360_QUEUE_WAIT_US") ? atoi(getenv("R360_QUEUE_WAIT_US")) : 2000;
+        static const int min_jobs = R360_KNOB("R360_QUEUE_MIN", 0);
+        static const int wait_us = R360_KNOB("R360_QUEUE_WAIT_US", 2000);
         if (min_jobs > 1 && (int)q->pending.size() < min_jobs)
             q->cv_work.wait_for(lk, std::chrono::microseconds(wait_us),
                                 [&] { return q->quit || (int)q->pending.size() >= min_jobs; });
@@ -138,9 +138,9 @@ extern "C" int r360_dense_queue_create(int device, int max_batch, r360_dense_que
     // stream priority experiments (off by default): R360_QUEUE_PRIORITY=1 puts the queue's stream at the device's
     // highest priority (batched passes dispatched ahead of the plane kernels: 603 vs 820 pairs/s, the plane half
     // starves); with R360_CTX_PRIORITY=1 (pipelines high) the queue stays at the normal priority
-    static const int prio_env = getenv("R360_QUEUE_PRIORITY") ? atoi(getenv("R360_QUEUE_PRIORITY")) : 0;
-    static const int ctx_prio = getenv("R360_CTX_PRIORITY") ? atoi(getenv("R360_CTX_PRIORITY")) : 0;
-    if (prio_env || ctx_prio) {
+    static const int prio_env = R360_KNOB("R360_QUEUE_PRIORITY", 0);
+    static const int ctx_prio = R360_KNOB("R360_CTX_PRIORITY", 0);
+    if (prio_env != 0 || ctx_prio != 0) {
         int least = 0, greatest = 0;
         R360_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
         hipStream_t hs = nullptr;

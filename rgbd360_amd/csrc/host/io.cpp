@@ -77,6 +77,7 @@ int parse_bin_file(const char* path, int rows, int cols, std::vector<uint8_t>& b
 }
 
 extern "C" int r360_frame_load_bin(r360_frame* f, const char* path) {
+    if (f && bind_device(f->ctx->device)) return -1;
     if (!f || !path) { r360_set_error("null arg"); return -2; }
     std::vector<uint8_t> bgr;
     std::vector<uint16_t> depth;

@@ -468,7 +468,7 @@ int planes_finish(r360_frame* f) {
 // (including the pinned contour/voxel outputs) is complete
 int planes_assemble(r360_frame* f) {
     PlaneBufs& P = f->pl;
-    static const bool prof = getenv("R360_PBMAP_PROFILE") != nullptr;
+    static const bool prof = R360_KNOB_STR("R360_PBMAP_PROFILE") != nullptr;
     auto now = [] { return std::chrono::steady_clock::now(); };
     auto us = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
         return std::chrono::duration<double, std::micro>(b - a).count();
@@ -859,6 +859,7 @@ extern "C" int r360_register_pbmap(r360_ctx* ctx, r360_frame* ref, r360_frame* t
                                    float pose[16], float info[36], int* match_pairs, int pair_cap, int* n_match,
                                    float* area_matched, float* area_src, float* area_trg) {
     CHECK_ARG(ctx && pose && info, "null arg");
+    if (ctx && bind_device(ctx->device)) return -1;
     CHECK_ARG(mode >= 0 && mode <= 3, "registrationType must be 0..3");
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
@@ -1045,6 +1046,7 @@ extern "C" int r360_register_result(r360_ctx* ctx, float pose[16], float info[36
 extern "C" int r360_register(r360_ctx* ctx, r360_frame* ref, r360_frame* trg, const float guess[16],
                              const r360_icp_params* p, size_t max_match_planes, int mode, float pose[16],
                              float info[36], r360_icp_stats* st) {
+    if (ctx && bind_device(ctx->device)) return -1;
     if (int rc = r360_register_async(ctx, ref, trg, guess, p, max_match_planes, mode)) return rc;
     return r360_register_result(ctx, pose, info, st);
 }

@@ -57,6 +57,7 @@ void intrinsics(const r360_frame* f, const float* K_in, float K[4]) {
 
 extern "C" int r360_align_pinhole_async(r360_ctx* ctx, r360_frame* trg, r360_frame* src, int n, const int* sensors,
                                         const float* init, int method, const float* K_in, const r360_icp_params* p) {
+    if (ctx && bind_device(ctx->device)) return -1;
     if (int rc = check_pin_pair(ctx, trg, src, p)) return rc;
     CHECK_ARG(n >= 1 && n <= 8 && sensors && init, "1..8 jobs with sensors and init poses");
     CHECK_ARG(method >= 0 && method <= 2, "invalid method");

@@ -115,6 +115,7 @@ int enqueue_jobs(r360_ctx* ctx, r360_frame* f1, r360_frame* f2, int l_lo, int l_
 extern "C" int r360_register_dense(r360_ctx* ctx, r360_frame* frame1, r360_frame* frame2, const float pose_estim[16],
                                    int method, int mode, const r360_icp_params* p_in, float pose_out[16],
                                    float info_out[36], r360_dense_stats* st) {
+    if (ctx && bind_device(ctx->device)) return -1;
     (void)mode;   // registMode is accepted and unused by the reference (RegisterRGBD360.h:344-520)
     r360_icp_params pd;
     r360_icp_default_params(&pd);                  // the RegisterPhotoICP() the function constructs

@@ -2,6 +2,7 @@
 // RegisterPhotoICP::alignFrames360 driver.  Everything here is plumbing around the HIP kernels
 // (frame_kernels.hip, icp_kernels.hip); the per-pixel work never runs on the CPU.
 #include <chrono>
+#include <dlfcn.h>
 #include <cmath>
 #include <thread>
 #include <cstdarg>
@@ -25,6 +26,32 @@ void r360_set_error(const char* fmt, ...) {
 }
 extern "C" const char* r360_last_error(void) { return g_err.c_str(); }
 extern "C" const char* r360_version(void) { return "rgbd360_amd 0.1 (gfx950)"; }
+
+// The shipped data directory (calibration, matcher ini files, samples): $R360_DATA_DIR, else data/ of the tree the
+// library was built in (<tree>/rgbd360_amd/lib/librgbd360_hip.so -> <tree>/data).  The reference's callers rely on
+// PROJECT_SOURCE_PATH for the same files (Calib360.h:107, :125; OdometryRGBD360.cpp:68).
+extern "C" const char* r360_data_dir(void) {
+    static const std::string dir = [] {
+        if (const char* e = getenv("R360_DATA_DIR")) return std::string(e);
+        Dl_info info;
+        if (dladdr((void*)&r360_data_dir, &info) && info.dli_fname) {
+            std::string p(info.dli_fname);
+            for (int up = 0; up < 3; ++up) {            // strip the file name, lib/, rgbd360_amd/
+                const size_t s = p.find_last_of('/');
+                p = s == std::string::npos ? std::string(".") : p.substr(0, s);
+            }
+            return p + "/data";
+        }
+        return std::string("data");
+    }();
+    return dir.c_str();
+}
+
+// dir, or the shipped calibration's sub-directory where dir is NULL / "" (the reference's "" default argument)
+static std::string calib_dir_or_default(const char* dir, const char* sub) {
+    if (dir && *dir) return dir;
+    return std::string(r360_data_dir()) + "/calib/" + sub;
+}
 
 
 // ------------------------------------------------------------------ timing (HIP events on the ctx stream)
@@ -109,9 +136,9 @@ extern "C" int r360_ctx_timing_reset(r360_ctx* ctx) {
 // (R360_QUEUE_CU_PAT=spread: every (CUs / n)-th CU, =high: the last n); R360_PIPE_CU=excl puts every other context's
 // stream on exactly those n CUs.  Returns true and fills mask when the stream of that kind gets a CU mask.
 bool r360_cu_mask(int device, int for_queue, uint32_t* mask) {
-    static const int excl = getenv("R360_QUEUE_CU_EXCL") ? atoi(getenv("R360_QUEUE_CU_EXCL")) : 0;
-    static const bool high = getenv("R360_QUEUE_CU_PAT") && strcmp(getenv("R360_QUEUE_CU_PAT"), "high") == 0;
-    static const bool pipe = getenv("R360_PIPE_CU") && strcmp(getenv("R360_PIPE_CU"), "excl") == 0;
+    static const int excl = R360_KNOB("R360_QUEUE_CU_EXCL", 0);
+    static const bool high = R360_KNOB_STR("R360_QUEUE_CU_PAT") && strcmp(R360_KNOB_STR("R360_QUEUE_CU_PAT"), "high") == 0;
+    static const bool pipe = R360_KNOB_STR("R360_PIPE_CU") && strcmp(R360_KNOB_STR("R360_PIPE_CU"), "excl") == 0;
     if (excl <= 0 || (!for_queue && !pipe)) return false;
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= excl ||
@@ -136,7 +163,7 @@ extern "C" int r360_ctx_create(int device, r360_ctx** out) {
     c->device = device;
     // R360_CTX_PRIORITY=1: contexts' streams at the device's highest priority (the dense queue keeps the normal
     // one, r360_dense_queue_create); an experiment knob, off by default
-    static const int ctx_prio = getenv("R360_CTX_PRIORITY") ? atoi(getenv("R360_CTX_PRIORITY")) : 0;
+    static const int ctx_prio = R360_KNOB("R360_CTX_PRIORITY", 0);
     uint32_t mask[R360_CU_MASK_WORDS];
     if (ctx_prio) {
         int least = 0, greatest = 0;
@@ -372,8 +399,10 @@ extern "C" int r360_calib_get_extrinsics(const r360_calib* c, float* rt8, float*
     return 0;
 }
 
-extern "C" int r360_calib_load_extrinsics(r360_calib* c, const char* dir) {
-    CHECK_ARG(c && dir, "null arg");
+extern "C" int r360_calib_load_extrinsics(r360_calib* c, const char* dir_in) {
+    CHECK_ARG(c, "null arg");
+    const std::string dirs = calib_dir_or_default(dir_in, "Extrinsics");
+    const char* dir = dirs.c_str();
     float rt[8 * 16];
     for (int k = 0; k < 8; ++k) {
         char path[4096];
@@ -443,8 +472,10 @@ static int read_clams(const char* dir, int k, ClamsDev& M, std::vector<float>& m
     return 0;
 }
 
-extern "C" int r360_calib_load_intrinsics(r360_calib* c, const char* dir) {
-    CHECK_ARG(c && dir, "null arg");
+extern "C" int r360_calib_load_intrinsics(r360_calib* c, const char* dir_in) {
+    CHECK_ARG(c, "null arg");
+    const std::string dirs = calib_dir_or_default(dir_in, "Intrinsics");
+    const char* dir = dirs.c_str();
     std::vector<float> mult, counts;
     for (int k = 0; k < 8; ++k)
         if (read_clams(dir, k, c->clams, mult, counts)) return -1;
@@ -509,6 +540,7 @@ extern "C" void r360_frame_destroy(r360_frame* f) {
 
 extern "C" int r360_frame_upload(r360_frame* f, const uint8_t* bgr8, const uint16_t* depth8) {
     CHECK_ARG(f && bgr8 && depth8, "null arg");
+    if (f && bind_device(f->ctx->device)) return -1;
     CHECK_ARG(f->rows > 0, "a sphere-only frame has no sensor images");
     const size_t ns = (size_t)8 * f->rows * f->cols;
     R360_HIP(hipMemcpyAsync(f->d_bgr, bgr8, ns * 3, hipMemcpyHostToDevice, f->ctx->stream));
@@ -522,6 +554,7 @@ extern "C" int r360_frame_upload(r360_frame* f, const uint8_t* bgr8, const uint1
 // (page-locked buffers, r360_host_register, make the copies truly asynchronous).
 extern "C" int r360_frame_upload_async(r360_frame* f, const uint8_t* bgr8, const uint16_t* depth8) {
     CHECK_ARG(f && bgr8 && depth8, "null arg");
+    if (f && bind_device(f->ctx->device)) return -1;
     CHECK_ARG(f->rows > 0, "a sphere-only frame has no sensor images");
     const size_t ns = (size_t)8 * f->rows * f->cols;
     R360_HIP(hipMemcpyAsync(f->d_bgr, bgr8, ns * 3, hipMemcpyHostToDevice, f->ctx->stream));
@@ -548,6 +581,7 @@ extern "C" int r360_host_unregister(void* p) {
 extern "C" int r360_frame_set_sphere(r360_frame* f, const uint8_t* bgr, const uint16_t* range_mm, int sph_rows,
                                      int sph_cols) {
     CHECK_ARG(f && bgr && range_mm, "null arg");
+    if (f && bind_device(f->ctx->device)) return -1;
     CHECK_ARG(sph_rows == f->sph_rows && sph_cols == f->sph_cols,
               "sphere size differs from the frame's (create it from r360_calib_create_sphere)");
     const size_t n = (size_t)sph_rows * sph_cols;
@@ -561,6 +595,7 @@ extern "C" int r360_frame_set_sphere(r360_frame* f, const uint8_t* bgr, const ui
 
 extern "C" int r360_frame_upload_device(r360_frame* f, const void* d_bgr8, const void* d_depth8) {
     CHECK_ARG(f && d_bgr8 && d_depth8, "null arg");
+    if (f && bind_device(f->ctx->device)) return -1;
     CHECK_ARG(f->rows > 0, "a sphere-only frame has no sensor images");
     const size_t ns = (size_t)8 * f->rows * f->cols;
     R360_HIP(hipMemcpyAsync(f->d_bgr, d_bgr8, ns * 3, hipMemcpyDeviceToDevice, f->ctx->stream));
@@ -571,6 +606,7 @@ extern "C" int r360_frame_upload_device(r360_frame* f, const void* d_bgr8, const
 
 extern "C" int r360_frame_build_async(r360_frame* f, unsigned flags) {
     CHECK_ARG(f, "null frame");
+    if (f && bind_device(f->ctx->device)) return -1;
     CHECK_ARG(f->rows > 0 || flags == 0, "a sphere-only frame has no sensor images to build from (r360_frame_set_sphere)");
     if (flags & (R360_BUILD_UNDISTORT | R360_BUILD_CLOUD | R360_BUILD_PLANES)) {
         if (launch_undistort(f)) return -1;
@@ -724,7 +760,7 @@ static IcpConst make_const(const r360_icp_params* p, int level, int n_pixels, in
     C.max_iters = p->max_iters; C.fixed_iters0 = p->fixed_iters_level0;
     // diagnostic only (tools/stamps.py ALIGN=1): the device GN expects more level-0 iterations than are launched,
     // so the last launched pass is a continuing one
-    static const int diag_extra = getenv("R360_DIAG_EXTRA_ITERS") ? atoi(getenv("R360_DIAG_EXTRA_ITERS")) : 0;
+    static const int diag_extra = R360_KNOB("R360_DIAG_EXTRA_ITERS", 0);
     if (C.fixed_iters0 > 0) C.fixed_iters0 += diag_extra;
     C.n_pixels = n_pixels; C.level = level; C.occ = occ;
     return C;
@@ -802,6 +838,7 @@ static int align_graph_launch(r360_ctx* ctx, const r360_frame* trg, const r360_f
 
 extern "C" int r360_align360_async(r360_ctx* ctx, r360_frame* trg, r360_frame* src, const float init[16], int method,
                                    int occlusion, const r360_icp_params* p) {
+    if (ctx && bind_device(ctx->device)) return -1;
     if (int rc = check_pair(ctx, trg, src, p)) return rc;
     CHECK_ARG(init, "null init pose");
     CHECK_ARG(method >= 0 && method <= 2, "invalid method");
@@ -825,7 +862,7 @@ extern "C" int r360_align360_async(r360_ctx* ctx, r360_frame* trg, r360_frame* s
     };
     // graphs for the plain pass (occlusion passes size their buffers on first use) without per-launch timing
     // events; R360_NO_GRAPH=1 launches one by one (A/B)
-    static const bool no_graph = getenv("R360_NO_GRAPH") && atoi(getenv("R360_NO_GRAPH")) != 0;
+    static const bool no_graph = R360_KNOB("R360_NO_GRAPH", 0) != 0;
     if (no_graph || R360_POLL || occlusion || ctx->timing) {
         if (passes_of()) return -1;
     } else {
@@ -898,6 +935,7 @@ int ctx_wait_frames(r360_ctx* ctx, r360_frame* const* frames, int n) {
 
 extern "C" int r360_align360_batch_async(r360_ctx* ctx, int n, r360_frame* const* trg, r360_frame* const* src,
                                          const float* init, int method, const r360_icp_params* p) {
+    if (ctx && bind_device(ctx->device)) return -1;
     return align360_batch_enqueue(ctx, n, trg, src, init, method, p, true);
 }
 

@@ -447,7 +447,7 @@ int launch_pyramid(r360_frame* f) {
     }
     // level 0 streams its packed image (PF 6) where rows split into whole waves: its compacted points are built
     // only on request (r360_frame_get_points, or a pass form forced by R360_ICP_PF)
-    static const int pf_env = getenv("R360_ICP_PF") ? atoi(getenv("R360_ICP_PF")) : -1;
+    static const int pf_env = R360_KNOB("R360_ICP_PF", -1);
     const bool skip0 = f->lv[0].pk && f->lv[0].cols % 64 == 0 && !(pf_env == 4 || pf_env == 5);
     f->lv0_compacted = !skip0;
     return launch_src_compaction(f, skip0 ? 1 : 0, f->n_levels);

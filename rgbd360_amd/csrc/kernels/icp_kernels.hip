@@ -31,6 +31,8 @@ namespace {
 constexpr int TPB = R360_ICP_TPB;
 constexpr int NW = TPB / 64;
 constexpr int RG = TPB / 16;  // record-reduction groups (16 lanes x 16 B per record)
+// the two-level record sum maps ticket group g to the final-stage row g (threadIdx.x >> 4) and sums rows k < RG
+static_assert(!R360_GROUP_SUM || R360_TICKET_GROUPS == RG, "R360_GROUP_SUM needs R360_TICKET_GROUPS == TPB / 16");
 
 struct Pose12 { float R[9]; float t[3]; };
 
@@ -1715,7 +1717,7 @@ int proj_check(const float* X, const float* Y, const float* Z, int n, const floa
     R360_HIP(hipGetLastError());
     unsigned long long h[8];
     R360_HIP(hipMemcpy(h, dout, 64, hipMemcpyDeviceToHost));
-    if (h[0] && getenv("R360_PROJ_DEBUG"))
+    if (h[0] && R360_KNOB_STR("R360_PROJ_DEBUG"))
         fprintf(stderr, "proj mismatch at %llu: fast pixel %lld exact pixel %lld\n", h[2], (long long)h[3], (long long)h[4]);
     (void)hipFree(dx); (void)hipFree(dy); (void)hipFree(dz); (void)hipFree(dout);
     *mismatches = h[0];
@@ -1749,14 +1751,52 @@ __global__ void k_rn_check(unsigned n, unsigned seed, unsigned long long* __rest
 }  // namespace
 
 namespace {
+// the register form (the GN step's) and the wave form (pinhole / robot steps) must agree: -1 where they do not
 __global__ void k_rank6(const float* __restrict__ M, int n, int* __restrict__ out) {
     const int m = blockIdx.x, lane = threadIdx.x;
     if (m >= n) return;
     const float a = lane < 36 ? M[m * 36 + lane] : 0.f;
-    const int rk = wave_rank6(a, lane);
-    if (lane == 0) out[m] = rk;
+    const int rw = wave_rank6(a, lane);
+    if (lane == 0) {
+        float W[36];
+#pragma unroll
+        for (int l = 0; l < 36; ++l) W[l] = M[m * 36 + l];
+        const int rr = rank6_reg(W);
+        out[m] = rr == rw ? rr : -1;
+    }
+}
+
+// x = -H^-1 g by the GN step's row-per-lane solve (solve6_rows); one wave per system
+__global__ void k_solve6(const double* __restrict__ H, const double* __restrict__ g, int n, double* __restrict__ x) {
+    const int m = blockIdx.x, lane = threadIdx.x;
+    if (m >= n) return;
+    const int i = lane < 6 ? lane : 0;
+    double a[7], xs[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) a[j] = H[m * 36 + i * 6 + j];
+    a[6] = -g[m * 6 + i];
+    solve6_rows(a, lane, xs);
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) x[m * 6 + k] = xs[k];
 }
 }  // namespace
+
+// Test hook: the GN step's solve (icp_la.inc solve6_rows) on n systems (H row-major n x 36, g n x 6) -> x n x 6.
+extern "C" int r360_solve6(const double* H, const double* g, int n, double* x) {
+    if (!H || !g || !x || n <= 0) { r360_set_error("r360_solve6: bad arguments"); return -2; }
+    double *dH, *dg, *dx;
+    R360_HIP(hipMalloc(&dH, sizeof(double) * 36 * (size_t)n));
+    R360_HIP(hipMalloc(&dg, sizeof(double) * 6 * (size_t)n));
+    R360_HIP(hipMalloc(&dx, sizeof(double) * 6 * (size_t)n));
+    R360_HIP(hipMemcpy(dH, H, sizeof(double) * 36 * (size_t)n, hipMemcpyHostToDevice));
+    R360_HIP(hipMemcpy(dg, g, sizeof(double) * 6 * (size_t)n, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_solve6, dim3(n), dim3(64), 0, 0, dH, dg, n, dx);
+    R360_HIP(hipGetLastError());
+    R360_HIP(hipMemcpy(x, dx, sizeof(double) * 6 * (size_t)n, hipMemcpyDeviceToHost));
+    (void)hipFree(dH); (void)hipFree(dg); (void)hipFree(dx);
+    return 0;
+}
 
 // Test hook: the device rank test (wave_rank6, the ILL-POSED check of alignFrames360 :4682 / alignFrames
 // :4345 / RegisterDensePhotoICP :443) on n row-major 6x6 float matrices.
@@ -1806,21 +1846,32 @@ extern "C" int r360_debug_block_stamps(unsigned long long* out, int n) {
 }
 #endif
 
-static int env_int(const char* name, int dflt) {
-    const char* v = getenv(name);
-    return v ? atoi(v) : dflt;
-}
-
+// The pass forms the product library holds (each covered by the parity suite): PF 6 at level 0 (TOP = 1), PF 5 on
+// the other levels (and at level 0 where the packed image is not streamable), PF 3 / PF 0 for the occlusion
+// variants (PF 0 where rows do not split into whole waves).  PF 1 / 2 / 4 / 7 and the forced-form knobs exist only
+// in the experiment builds (R360_EXPERIMENTS, make exp).
 template <int M, int PF>
-static void launch_pass(r360_ctx* ctx, int nb, int njobs, const IcpJobs& jobs, const LevelBufs& Ls,
+static int launch_pass(r360_ctx* ctx, int nb, int njobs, const IcpJobs& jobs, const LevelBufs& Ls,
                         const LevelTrig& T, const IcpConst& C, int first, int eval_only, bool top) {
-    // PF 4 / 5 (compacted source points) have no occlusion form: the occlusion flags are per source pixel
-    constexpr int PFO = PF >= 4 ? 3 : PF;
-    auto kern = C.occ == 1 ? k_icp_pass<M, PFO, 0, 1>
-              : C.occ == 2 ? k_icp_pass<M, PFO, 0, 2>
-              : top        ? k_icp_pass<M, PF, 1, 0> : k_icp_pass<M, PF, 0, 0>;
+    void (*kern)(const IcpJobs, const float*, const float*, const float*, const float*, int, int, IcpConst, int, int,
+                 unsigned long long*, const uint8_t*) = nullptr;
+    if (C.occ) {
+        // PF 4 / 5 / 6 (compacted or packed source) have no occlusion form: the occlusion flags are per source pixel
+        constexpr int PFO = PF >= 4 ? 3 : PF;
+        if constexpr (PFO == 0 || PFO == 3 || R360_EXPERIMENTS)
+            kern = C.occ == 1 ? k_icp_pass<M, PFO, 0, 1> : k_icp_pass<M, PFO, 0, 2>;
+    } else if constexpr (PF == 5 || R360_EXPERIMENTS) {
+        kern = top ? k_icp_pass<M, PF, 1, 0> : k_icp_pass<M, PF, 0, 0>;
+    } else if constexpr (PF == 6) {
+        kern = k_icp_pass<M, PF, 1, 0>;   // level 0 only
+    }
+    if (!kern) {
+        r360_set_error("k_icp_pass: form PF %d (occlusion %d, top %d) is not in this build", PF, C.occ, (int)top);
+        return -1;
+    }
     hipLaunchKernelGGL(kern, dim3(nb, njobs), dim3(TPB), 0, ctx->stream, jobs, T.sinphi, T.cosphi, T.sinth,
                        T.costh, Ls.rows, Ls.cols, C, first, eval_only, ctx->d_ktime, ctx->occ_flags);
+    return 0;
 }
 
 int ensure_defer(r360_ctx* ctx, long n_pixels) {
@@ -1869,24 +1920,14 @@ struct PassGrid { int pf, nb; };
 static PassGrid pass_grid(const r360_ctx* ctx, const LevelBufs& Ls, int occ, int njobs = 1) {
     // 4-pixel units on the large levels, one pixel per thread where that still fits one resident
     // round (latency-bound small levels); R360_ICP_PF=0/1 forces one form (experiments)
-    static const int pf_env = env_int("R360_ICP_PF", -1);
-    static const int cap_env = env_int("R360_ICP_CAP", -1);
+    static const int pf_env = R360_KNOB("R360_ICP_PF", -1);
+    static const int cap_env = R360_KNOB("R360_ICP_CAP", -1);
     // one resident round: CUs x workgroups per CU of the launched form (grid-stride beyond it)
-    struct Occ { int cus = 0, per[8] = {0, 0, 0, 0, 0, 0, 0, 0}; };
-    static const Occ occ_q = [] {   // thread-safe one-time query (contexts may be driven from several threads)
-        Occ o;
-        int dev = 0;
+    static const int cus = [] {   // thread-safe one-time query (contexts may be driven from several threads)
+        int dev = 0, n = 0;
         (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&o.cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[0], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 0, 0, 0>, TPB, 0);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[1], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 1, 0, 0>, TPB, 0);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[2], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 2, 0, 0>, TPB, 0);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[3], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 3, 0, 0>, TPB, 0);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[4], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 4, 0, 0>, TPB, 0);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[5], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 5, 0, 0>, TPB, 0);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[6], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 6, 0, 0>, TPB, 0);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&o.per[7], (const void*)k_icp_pass<R360_PHOTO_DEPTH, 7, 0, 0>, TPB, 0);
-        return o;
+        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+        return n;
     }();
     const int npx = Ls.rows * Ls.cols;
     // PF 4 (compacted source points) for the plain pass; the occlusion variants index their flags by source
@@ -1894,21 +1935,21 @@ static PassGrid pass_grid(const r360_ctx* ctx, const LevelBufs& Ls, int occ, int
     // level 0 (the only level with a packed image) streams the packed images where rows split into whole waves
     const bool pk_ok = Ls.pk != nullptr && Ls.cols % 64 == 0;
     const int pf_dflt = occ ? ((Ls.cols % 64 == 0) ? 3 : 0) : (pk_ok ? 6 : 5);
-    const int pf = pf_env >= 0 && !(pf_env >= 4 && occ) && !(pf_env >= 6 && !pk_ok) ? pf_env : pf_dflt;
+    const int pf = R360_EXPERIMENTS && pf_env >= 0 && !(pf_env >= 4 && occ) && !(pf_env >= 6 && !pk_ok) ? pf_env : pf_dflt;
     // workgroups per job and pass: 2 per CU (one resident round holds occ_q.per[pf] per CU; a batched launch
     // fills the rest with other jobs, and fewer records per job shorten the reduction tail)
     // workgroups per job and pass: a fixed number per level size, never a function of the batch, so that a
     // pair's sums (pixels to waves, records in workgroup order) and thus its pose are the same in any batch
     // and on any number of ranks.  R360_ICP_WG_TOTAL (experiment only: breaks that) splits a per-launch total
     // over the launch's jobs.
-    int cap = cap_env > 0 ? cap_env : 2 * occ_q.cus;
-    static const int tot_env = env_int("R360_ICP_WG_TOTAL", -1);
+    int cap = cap_env > 0 ? cap_env : 2 * cus;
+    static const int tot_env = R360_KNOB("R360_ICP_WG_TOTAL", -1);
     if (tot_env > 0) cap = ((tot_env / (njobs > 0 ? njobs : 1) + 7) / 8) * 8;
     if (cap > ctx->partials_cap - R360_TICKET_GROUPS) cap = ctx->partials_cap - R360_TICKET_GROUPS;   // + group records
     // at least R360_ICP_PXT points per thread (default 1; 8 measured no faster): the coarse levels (a quarter, ... of
     // level 0) then run on a few hundred / dozen workgroups per pair instead of one thread per point, which
     // shortens their record / ticket / final-sum tail (level 0 at VGA has ~19 per thread on the capped grid)
-    static const int pxt_env = env_int("R360_ICP_PXT", -1);
+    static const int pxt_env = R360_KNOB("R360_ICP_PXT", -1);
     const int pxt = pxt_env > 0 ? pxt_env : 1;
     int nb = pf == 1 ? icp_blocks_for(npx) : (npx + TPB * pxt - 1) / (TPB * pxt);
     if (nb > cap) nb = cap;
@@ -1931,22 +1972,31 @@ static int launch_jobs(r360_ctx* ctx, const IcpJobs& jobs, int njobs, const Leve
     const int slot = timing_begin(ctx, name);
     const int pf = G.pf, nb = G.nb;
     const bool top = level == 0;
+#if R360_EXPERIMENTS
+#define R360_LAUNCH_EXP(M)                                                                               \
+        else if (pf == 1) rc = launch_pass<M, 1>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top); \
+        else if (pf == 2) rc = launch_pass<M, 2>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top); \
+        else if (pf == 4) rc = launch_pass<M, 4>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top); \
+        else if (pf == 7) rc = launch_pass<M, 7>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top);
+#else
+#define R360_LAUNCH_EXP(M)
+#endif
 #define R360_LAUNCH(M)                                                                                   \
     do {                                                                                                 \
-        if (pf == 1) launch_pass<M, 1>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top);           \
-        else if (pf == 2) launch_pass<M, 2>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top);      \
-        else if (pf == 3) launch_pass<M, 3>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top);      \
-        else if (pf == 4) launch_pass<M, 4>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top);      \
-        else if (pf == 5) launch_pass<M, 5>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top);      \
-        else if (pf == 6) launch_pass<M, 6>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top);      \
-        else if (pf == 7) launch_pass<M, 7>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top);      \
-        else launch_pass<M, 0>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top);                   \
+        if (pf == 3) rc = launch_pass<M, 3>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top);      \
+        else if (pf == 5) rc = launch_pass<M, 5>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top); \
+        else if (pf == 6) rc = launch_pass<M, 6>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top); \
+        R360_LAUNCH_EXP(M)                                                                               \
+        else rc = launch_pass<M, 0>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top);              \
     } while (0)
+    int rc = 0;
     if (method == R360_PHOTO_CONSISTENCY) R360_LAUNCH(R360_PHOTO_CONSISTENCY);
     else if (method == R360_DEPTH_CONSISTENCY) R360_LAUNCH(R360_DEPTH_CONSISTENCY);
     else R360_LAUNCH(R360_PHOTO_DEPTH);
 #undef R360_LAUNCH
+#undef R360_LAUNCH_EXP
     timing_end(ctx, slot);
+    if (rc) return rc;
     R360_HIP(hipGetLastError());
     return 0;
 }

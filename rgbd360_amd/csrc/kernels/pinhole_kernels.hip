@@ -387,10 +387,6 @@ __global__ __launch_bounds__(TPB) void k_pin_pass(const float2* __restrict__ src
     }
 }
 
-inline int env_int(const char* name, int dflt) {
-    const char* v = getenv(name);
-    return v ? atoi(v) : dflt;
-}
 
 }  // namespace
 
@@ -404,7 +400,7 @@ int launch_pin_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src
     Intr I;
     I.fx = K[0] * sc; I.fy = K[1] * sc; I.ox = K[2] * sc; I.oy = K[3] * sc;
     I.inv_fx = (float)(1. / I.fx); I.inv_fy = (float)(1. / I.fy);
-    static const int ppt = env_int("R360_PIN_PPT", 4);   // pixels per thread
+    static const int ppt = R360_KNOB("R360_PIN_PPT", 4);   // pixels per thread
     const int npx = Ls.rows * Ls.cols;
     int nb = (npx + TPB * ppt - 1) / (TPB * ppt);
     if (nb < 1) nb = 1;

@@ -684,7 +684,7 @@ int launch_cloud_normals(r360_frame* f) {
     R360_HIP(hipGetLastError());
     slot = timing_begin(f->ctx, "k_normals");
     // summed-area-table windows (default; R360_NORMALS_SAT=0: the direct window sums of k_normals)
-    static const int nsat = getenv("R360_NORMALS_SAT") ? atoi(getenv("R360_NORMALS_SAT")) : 1;
+    static const int nsat = R360_KNOB("R360_NORMALS_SAT", 1);
     if (nsat)
         hipLaunchKernelGGL(k_normals_sat, dim3((w + NT_C - 1) / NT_C, (h + NT_R - 1) / NT_R, 8), dim3(NT_TPB), 0, st, P.cloud,
                        P.dist, w, h, P.nrm);

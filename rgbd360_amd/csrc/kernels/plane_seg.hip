@@ -2063,7 +2063,7 @@ struct RefineWaveBufs { uint16_t* code; unsigned long long* msk; int8_t* f1; int
 // refinement mode: -1 the wavefront sweeps (default; pipelined bands for h <= 512), -2 the wavefront sweeps with a
 // barrier per diagonal, 0 the single-wave sweeps, rb > 0 banded with rb rows per band (R360_REFINE_ROWS overrides)
 int refine_band_rows(int h) {
-    static const int env = getenv("R360_REFINE_ROWS") ? atoi(getenv("R360_REFINE_ROWS")) : -99;
+    static const int env = R360_KNOB("R360_REFINE_ROWS", -99);
     int rb = env >= -2 ? env : -1;
     if (rb < 0) return h <= 1024 ? rb : 0;
     if (rb > 0 && (h + rb - 1) / rb > R360_REFINE_BANDS) rb = (h + R360_REFINE_BANDS - 1) / R360_REFINE_BANDS;
@@ -2082,7 +2082,7 @@ int launch_refine_sweeps(hipStream_t st, int8_t* S, int8_t* S2, const unsigned l
                            wb->msk, flag);
         const int tpb = 64 * ((h + 63) / 64);
         // R360_REFINE_NARROW=0: the 64-bit mask path for every sensor (inspection)
-        static const int narrow_max = getenv("R360_REFINE_NARROW") && !atoi(getenv("R360_REFINE_NARROW")) ? -1 : 30;
+        static const int narrow_max = R360_KNOB("R360_REFINE_NARROW", 1) == 0 ? -1 : 30;
         if (rb == -1 && h <= 64 * RP_MAXB && w <= RP_MAXW && nmodels) {
             if (h <= 256) {
                 hipLaunchKernelGGL((k_refine_pipe<1, 4>), dim3(8), dim3(tpb), 0, st, wb->code, wb->msk, wb->f1, wb->f2,
@@ -2136,7 +2136,7 @@ template <bool MODEL>
 int launch_gm(int px, long total, hipStream_t st, const float4* cloud, const uchar4* rgb, const int* lab, int N,
               const int* kmap, int* mmap_clear, const float* rt8, r360p::Moments* gmom, int* gfirst, RegionPart* gpart) {
     const unsigned blocks = (unsigned)((total + px - 1) / px);
-    static const int exp = getenv("R360_EXP_GM") ? atoi(getenv("R360_EXP_GM")) : 0;   // timing experiments only
+    static const int exp = R360_KNOB("R360_EXP_GM", 0);   // timing experiments only
     switch (px) {
 #define R360_GM_CASE(cpw)                                                                                         \
     case 256 * cpw:                                                                                               \
@@ -2184,7 +2184,7 @@ int launch_segmentation(r360_frame* f) {
     hipLaunchKernelGGL(k_big_list, dim3(nch, 8), dim3(NUMC), 0, st, P.cnt, P.nlab, N, 80, P.chunk, P.big, P.nbig,
                        R360_MAX_BIG, P.err, bmap, P.mom, bfirst);
     // pixels per workgroup of the grouped-moment kernels (R360_GM_PX, experiments)
-    static const int gm_px = getenv("R360_GM_PX") ? atoi(getenv("R360_GM_PX")) : GM_PX;
+    static const int gm_px = R360_KNOB("R360_GM_PX", GM_PX);
     if (launch_gm<false>(gm_px, total, st, P.cloud, nullptr, P.lab, N, bmap, mmap, nullptr, P.mom, bfirst, nullptr))
         return -1;
     hipLaunchKernelGGL(k_plane_fit, dim3(8), dim3(PF_TPB), 0, st, P.mom, P.big, P.nbig, R360_MAX_BIG, 0.001f, P.models,
@@ -2214,7 +2214,7 @@ int launch_segmentation(r360_frame* f) {
     else
         hipLaunchKernelGGL(k_trace<false>, dim3(8), dim3(TR_TPB), 0, st, nbm, P.cloud, w, h, P.nmodels, P.out,
                            P.contour, P.contour_cap, P.err);
-    static const int vox_px_env = getenv("R360_VOX_PX") ? atoi(getenv("R360_VOX_PX")) : VOX_PX;   // experiments
+    static const int vox_px_env = R360_KNOB("R360_VOX_PX", VOX_PX);   // experiments
     const int vox_px = std::min(vox_px_env, N);   // a block spans at most two sensors
     const long vox_blocks = (total + vox_px - 1) / vox_px;
     if (ctx_vhash_reserve(ctx, 12L * N, vox_blocks * vox_px, vox_blocks)) return -1;
@@ -2303,7 +2303,7 @@ extern "C" int r360_refine_eval(const int8_t* state, const uint64_t* mask, int w
             int fbh[16];
             R360_HIP(hipMemcpy(fbh, flag, sizeof(fbh), hipMemcpyDeviceToHost));
             for (int k = 0; k < 8; ++k) rc += (fbh[k] != 0 || fbh[8 + k] != 0);
-            if (getenv("R360_REFINE_TRACE"))
+            if (R360_KNOB_STR("R360_REFINE_TRACE"))
                 for (int k = 0; k < 8; ++k) fprintf(stderr, "refine sensor %d: re-runs %d fallback row %d\n", k, fbh[8 + k], fbh[k] - 1);
         }
     }

@@ -11,6 +11,22 @@
 
 #define R360_PI 3.14159265359  // include/Miscellaneous.h:44 (double literal)
 
+// Experiment knobs (pass forms, grid caps, CU masks, priorities, A/B switches) read the environment only in the
+// experiment builds (make exp / stamps, -DR360_EXPERIMENTS=1, lib/librgbd360_hip_exp.so): in the product library
+// R360_KNOB is its default and the variable's name is not even in the binary, so no environment variable can
+// change a registration.
+#ifndef R360_EXPERIMENTS
+#define R360_EXPERIMENTS 0
+#endif
+#if R360_EXPERIMENTS
+#include <cstdlib>
+#define R360_KNOB(name, dflt) (std::getenv(name) ? std::atoi(std::getenv(name)) : (dflt))
+#define R360_KNOB_STR(name) (std::getenv(name))
+#else
+#define R360_KNOB(name, dflt) (dflt)
+#define R360_KNOB_STR(name) ((const char*)nullptr)
+#endif
+
 // ------------------------------------------------------------------ error plumbing
 void r360_set_error(const char* fmt, ...);
 #define R360_HIP(call)                                                                  \
@@ -21,6 +37,15 @@ void r360_set_error(const char* fmt, ...);
             return -1;                                                                  \
         }                                                                               \
     } while (0)
+
+// Binds the calling thread to `device` (HIP's current device is per host thread): every entry point that enqueues
+// work or creates streams / events calls it first, so contexts of any device can be driven from any thread (the
+// pipelines' pool threads of a rank with LOCAL_RANK >= 1 never call hipSetDevice themselves).
+inline int bind_device(int device) {
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess || cur != device) R360_HIP(hipSetDevice(device));
+    return 0;
+}
 
 // argument check of a C-ABI entry point: sets the thread's error and returns -2
 #define CHECK_ARG(cond, msg)                 \
@@ -91,6 +116,8 @@ struct alignas(16) IcpState {
     double lm_lambda;   // alignFrames (pinhole) Levenberg-Marquardt lambda (:4301)
     int lm_phase;       // 0: the pending candidate is the undamped step, 1: the LM retry (:4381-4412)
     int pad2;
+    double gn_lambda;   // alignFrames360 lambda of the current level: 1 at the level start, /= 5 per accepted update
+    double pad3;
     // the residual members the error functions assign (RegisterPhotoICP.h:183-189): of the last evaluated
     // pass (av_*) and, for alignFrames, the copies taken at each loop iteration's start (av_*_t, :4329-4332)
     double av_photo, av_depth, av_photo_t, av_depth_t;

@@ -113,3 +113,41 @@ def test_facade_translation_units_compile(root, tmp_path):
                             f"-I{root}/include", f'-DRGBD360_DATA_DIR="{root}/data"', f"{root}/apps/{app}.cpp"],
                            capture_output=True, text=True)
         assert p.returncode == 0, (app, p.stderr[-3000:])
+
+
+def test_reference_call_sequence_compiles_unchanged(root):
+    """Source-level drop-in: tests/dropin/odometry_dropin.cpp makes the reference's OdometryRGBD360 calls
+    (Registration/OdometryRGBD360.cpp:60-257) with the reference's constructors and default arguments —
+    Calib360 calib; loadExtrinsicCalibration(); RegisterRGBD360 registerer(mrpt::format(..., PROJECT_SOURCE_PATH));
+    RegisterPhotoICP align360; Eigen::Matrix4f poses — through include/rgbd360/compat.h, with g++ alone."""
+    import subprocess
+    p = subprocess.run(["g++", "-std=c++17", "-O0", "-fsyntax-only", "-Wall", "-Wextra", "-Werror", f"-I{root}/include",
+                        f"{root}/tests/dropin/odometry_dropin.cpp"], capture_output=True, text=True)
+    assert p.returncode == 0, p.stderr[-3000:]
+
+
+def test_data_dir_is_the_shipped_tree(root):
+    """r360_data_dir() (the reference's PROJECT_SOURCE_PATH for calib/ and config_files/) resolves to this tree's
+    data/ from the library's own location, so default-argument loads find the shipped calibration."""
+    d = R.lib().r360_data_dir().decode()
+    assert os.path.realpath(d) == os.path.realpath(os.path.join(root, "data")), d
+    for sub in ("calib/Extrinsics/Rt_01.txt", "calib/Intrinsics/distortion_model1.r360",
+                "config_files/configLocaliser_sphericalOdometry.ini"):
+        assert os.path.exists(os.path.join(d, sub)), sub
+
+
+def test_product_library_holds_only_covered_pass_forms_and_no_knobs():
+    """The shipped library contains only the k_icp_pass forms the parity suite covers — PF 6 at level 0, PF 5 on the
+    other levels, PF 3 / PF 0 for the occlusion variants, for the three cost functions — and reads no experiment
+    knob from the environment (R360_ICP_PF / _CAP / _WG_TOTAL / _PXT, R360_DIAG_EXTRA_ITERS, ...: experiment builds
+    only, make exp), so no environment variable can change a registration."""
+    blob = open(R.LIB_PATH, "rb").read()
+    forms = set(re.findall(rb"k_icp_passILi([0-2])ELi([0-9])ELi([01])ELi([0-2])E", blob))
+    forms = {tuple(int(x) for x in f) for f in forms}
+    covered = set()
+    for m in (0, 1, 2):
+        covered |= {(m, 6, 1, 0), (m, 5, 0, 0), (m, 5, 1, 0)}
+        covered |= {(m, pf, 0, occ) for pf in (0, 3) for occ in (1, 2)}
+    assert forms == covered, sorted(forms ^ covered)
+    env_names = set(re.findall(rb"\x00(R360_[A-Z0-9_]+)\x00", blob))
+    assert env_names <= {b"R360_DATA_DIR"}, sorted(env_names)

@@ -269,6 +269,29 @@ def test_rank_test_matches_oracle_over_lambda_schedule():
     assert (ref < 6).any() and (ref == 6).any()
 
 
+def test_gn_solve_matches_oracle():
+    """The GN step's solve (icp_la.inc solve6_rows: row per lane, pivot rows broadcast by readlane) gives the
+    oracle's x = -H^-1 g (oracle_la.h solve6) bit for bit: SPD Hessians of the scales the passes produce, badly
+    conditioned ones, and matrices whose pivot order differs from the diagonal's."""
+    rng = np.random.default_rng(7)
+    Hs, gs = [], []
+    for k in range(256):
+        J = rng.normal(size=(6, 40)) * (10.0 ** rng.uniform(-3, 3, size=(6, 1)))
+        H = (J @ J.T).astype(np.float32).astype(np.float64)   # the passes' H / g are float sums
+        if k % 4 == 1:
+            H = rng.normal(size=(6, 6)).astype(np.float32).astype(np.float64)   # non-symmetric: row swaps
+        if k % 4 == 2:
+            H[5] = H[4] * (1 + 1e-6)                                          # nearly singular
+        Hs.append(H)
+        gs.append(rng.normal(size=6).astype(np.float32).astype(np.float64) * 10.0 ** rng.uniform(-3, 3))
+    H = np.ascontiguousarray(np.stack(Hs))
+    g = np.ascontiguousarray(np.stack(gs))
+    x = np.zeros((len(Hs), 6))
+    R._check(R.lib().r360_solve6(R._dptr(H), R._dptr(g), len(Hs), R._dptr(x)), "solve6")
+    ref = np.stack([O.solve6(h, gg) for h, gg in zip(Hs, gs)])
+    assert np.array_equal(x.view(np.uint64), ref.view(np.uint64))
+
+
 def test_set_frames_from_sphere_images(ctx, qvga):
     """setSourceFrame / setTargetFrame(imgRGB, imgDepth) (RegisterPhotoICP.h:480-516): the stitched spheres
     handed over as images (downloaded, then uploaded into sphere-only frames) give the same pyramid and the

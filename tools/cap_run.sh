@@ -1,6 +1,7 @@
 #!/bin/bash
 # GPU box: kernel-trace duration of the level-0 ICP pass (eval mode, tools/icp_bench.py) per grid cap.
 # usage: CAPS="512 1024" tools/cap_run.sh
+export R360_LIB=${R360_LIB:-${GRAFT_REPO_ROOT:-.}/rgbd360_amd/lib/librgbd360_hip_exp.so}   # knobs: experiment build (make -C rgbd360_amd/csrc exp)
 R=$GRAFT_REPO_ROOT
 cd /tmp && export TMPDIR=/tmp
 for cap in ${CAPS:-512 768 1024 1536 2048}; do

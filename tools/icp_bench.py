@@ -1,5 +1,6 @@
 """Micro-benchmark of the fused ICP pass at each pyramid level (eval mode, HIP-event timed).
-usage: python tools/icp_bench.py [reps]   (env R360_ICP_PF / R360_ICP_CAP select variants)"""
+usage: R360_LIB=rgbd360_amd/lib/librgbd360_hip_exp.so python tools/icp_bench.py [reps]   (env R360_ICP_PF /
+R360_ICP_CAP select variants; experiment build only: make -C rgbd360_amd/csrc exp)"""
 import os
 import sys
 

@@ -3,6 +3,7 @@
 # the ICP pass forms given in PFS (in-kernel spans), their level-0 VALU / HBM counters, and the default bench.
 # usage: PFS="4 5" tools/r3_iter.sh <tag> [skip-tests]
 set -o pipefail
+export R360_LIB=${R360_LIB:-${GRAFT_REPO_ROOT:-.}/rgbd360_amd/lib/librgbd360_hip_exp.so}   # knobs: experiment build (make -C rgbd360_amd/csrc exp)
 TAG=${1:-it}; R=$GRAFT_REPO_ROOT; OUT=$R/gpurun_out/it_$TAG; mkdir -p $OUT
 DARGS="--workload dense --steps 2 --warmup 1 --no-cpu-baseline --no-resident --no-config5 --no-isolated"
 if [ "$2" != "skip-tests" ]; then

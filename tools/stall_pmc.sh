@@ -1,6 +1,7 @@
 #!/bin/bash
 # GPU box: stall-attribution counters of the level-0 ICP pass in the dense-alone VGA bench (PF from the env).
 # usage: [R360_ICP_PF=6] tools/stall_pmc.sh <tag>
+export R360_LIB=${R360_LIB:-${GRAFT_REPO_ROOT:-.}/rgbd360_amd/lib/librgbd360_hip_exp.so}   # knobs: experiment build (make -C rgbd360_amd/csrc exp)
 R=$GRAFT_REPO_ROOT; TAG=${1:-st}; OUT=$R/gpurun_out/stall_$TAG; mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 DARGS="--workload dense --steps 1 --warmup 1 --no-cpu-baseline --no-resident --no-config5 --no-isolated"
