@@ -446,13 +446,14 @@ def rank6f(M) -> int:
 
 
 def solve6(H, g):
-    """x = -H^-1 g by the GN step's Gaussian elimination with partial pivoting (double, :4693)."""
+    """x = -H^-1 g by the GN step's Gaussian elimination with partial pivoting (double, :4693); None where a pivot is
+    exactly 0 (unreachable in alignFrames360: the rank test returns ILL-POSED first)."""
     h = np.ascontiguousarray(np.asarray(H, np.float64).reshape(36))
     gg = np.ascontiguousarray(np.asarray(g, np.float64).reshape(6))
     x = np.zeros(6, np.float64)
     dp_ = C.POINTER(C.c_double)
-    lib().orc_solve6(h.ctypes.data_as(dp_), gg.ctypes.data_as(dp_), x.ctypes.data_as(dp_))
-    return x
+    ok = lib().orc_solve6(h.ctypes.data_as(dp_), gg.ctypes.data_as(dp_), x.ctypes.data_as(dp_))
+    return x if ok else None
 
 
 def libm(x, y, z):

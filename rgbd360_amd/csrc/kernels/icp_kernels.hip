@@ -216,7 +216,8 @@ __device__ __forceinline__ Proj project_fast(const Pose12& P, const Lut3& l, flo
     o.fix = l.valid && !(eu <= 0.5f - kGuardRow && ev <= 0.5f - kGuardCol);   // NaN -> flagged
     o.vis = l.valid && fu >= 0.f && fu < (float)nRows && fv < (float)nCols;
     o.t = o.vis ? (int)fu * nCols + (int)fv : 0;
-    o.X = X; o.Y = Y; o.Z = Z; o.dist = r360m::sqrt_rn(d2); o.dist_inv = dist_inv; o.gray_s = gray_s;
+    // LEAN: |p'| = d2 rsq(d2) (within ~2 ulp of the correctly rounded root, like the lean error terms it enters)
+    o.X = X; o.Y = Y; o.Z = Z; o.dist = LEAN ? d2 * dist_inv : r360m::sqrt_rn(d2); o.dist_inv = dist_inv; o.gray_s = gray_s;
     return o;
 }
 
@@ -344,7 +345,9 @@ __device__ __forceinline__ void contribute(Acc& A, const Proj& o, const float4 G
 // waves where some lane needs them.
 struct WaveCnt { int c27 = 0, c28 = 0, c29 = 0; };
 
-__device__ __forceinline__ int wave_count(bool b) { return __popcll(__ballot(b)); }
+// the ballot of an i1 straight to its SGPR mask (HIP's int __ballot() materialised every predicate as 0 / 1 in a
+// VGPR and compared it again: 2 VALU per count)
+__device__ __forceinline__ int wave_count(bool b) { return __builtin_popcountll(__builtin_amdgcn_ballot_w64(b)); }
 
 template <int METHOD, int OCC>
 __device__ __forceinline__ void contribute_fast(Acc& A, WaveCnt& W, const Proj& o, const float4 G, const float2 T,
@@ -452,14 +455,15 @@ __device__ __forceinline__ void contribute_fast(Acc& A, WaveCnt& W, const Proj& 
 //  * The squared residuals are summed per lane in float and in double across lanes and workgroups (~1e-7
 //    relative; the error value's bar is 1e-5).
 // The weights are continuous at |e| = k (both branches give 1), so the comparison needs no guard band.
-template <int METHOD>
+// FIN = false: the target depth is known finite (PF 6 unpacks it from the packed image's millimetres).
+template <int METHOD, bool FIN = true>
 __device__ __forceinline__ void contribute_lean(Acc& A, WaveCnt& W, float& errf, const Proj& o, const float4 G,
                                                 const float2 T, float angle_res_inv, const IcpConst& C) {
     constexpr bool photo = (METHOD == R360_PHOTO_CONSISTENCY || METHOD == R360_PHOTO_DEPTH);
     constexpr bool depth = (METHOD == R360_DEPTH_CONSISTENCY || METHOD == R360_PHOTO_DEPTH);
     const bool sal_p = !(fabsf(G.x) < C.thr_int && fabsf(G.y) < C.thr_int);
     const bool sal_d = !(fabsf(G.z) < C.thr_depth && fabsf(G.w) < C.thr_depth);
-    const bool fin_d = isfinite(T.y);
+    const bool fin_d = !FIN || isfinite(T.y);
     const bool p_ok = photo && o.vis && sal_p;
     const bool d_ok = depth && o.vis && (!photo || sal_p) && fin_d && sal_d;   // (:3064-3073)
     float wp = 0.f, rp = 0.f, wd = 0.f, rd = 0.f;
@@ -486,12 +490,14 @@ __device__ __forceinline__ void contribute_lean(Acc& A, WaveCnt& W, float& errf,
     }
     W.c28 += wave_count(o.vis);                                                            // numVisiblePixels
     W.c27 += (photo ? wave_count(p_ok) : 0) + (depth ? wave_count(d_ok) : 0);
-    const float X = o.vis ? o.X : 1.f, Y = o.vis ? o.Y : 1.f, Z = o.vis ? o.Z : 1.f;
+    // p' of a lane without a point is finite (a LUT point, transformed), but r2 and |p'| may be 0 there: the lane's
+    // zero weights must not meet an infinite scale
+    const float X = o.X, Y = o.Y, Z = o.Z;
     const float dist_inv = o.vis ? o.dist_inv : 0.5f;
     {
 #pragma clang fp contract(fast)
         // the closed-form Jacobian rows of contribute_fast: row = [u, p' x u], u = J_proj^T [gx gy]^T
-        const float r2 = Y * Y + Z * Z;
+        const float r2 = o.vis ? Y * Y + Z * Z : 1.f;
         const float s = __builtin_amdgcn_rcpf(r2) * angle_res_inv;
         const float t = __builtin_amdgcn_rsqf(r2) * (dist_inv * dist_inv) * angle_res_inv;
         auto row = [&](float gx, float gy, float& u0, float& u1, float& u2) {
@@ -941,7 +947,7 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
             W.c28 += wave_count(o.vis);
             return;
 #endif
-            contribute_lean<METHOD>(A, W, errf, o, G, make_float2(gray_of(tv), depth_of(tv)), angle_res_inv, C);
+            contribute_lean<METHOD, false>(A, W, errf, o, G, make_float2(gray_of(tv), depth_of(tv)), angle_res_inv, C);
         };
         // row of a wave-uniform pixel index: a float estimate corrected by one step either way (exact for
         // pixel indices below 2^24, every level-0 size here)
@@ -958,9 +964,14 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
         // (SALU) and clamped at the last chunk, as base(k)
         int cur_k = 0, cur_i = 0, cur_r = 0, cur_c = 0;
         const int st_r = stride / nCols, st_c = stride - (stride / nCols) * nCols;
+        // the column tables through buffer resources (32-bit offsets: one address VALU for both loads)
+        const auto rs_st = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(sinth), 0, nCols * 4, 0x00020000);
+        const auto rs_ct = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(costh), 0, nCols * 4, 0x00020000);
         auto ld = [&]() {
+            const int co = (cur_c + lane) * 4;
             const Src x{__builtin_amdgcn_raw_buffer_load_b32(rs_s, (cur_i + lane) * 4, 0, 0), sinphi[cur_r],
-                        cosphi[cur_r], sinth[cur_c + lane], costh[cur_c + lane]};
+                        cosphi[cur_r], __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_st, co, 0, 0)),
+                        __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_ct, co, 0, 0))};
             if (cur_k + 1 < n_it_) {
                 ++cur_k;
                 cur_i += stride;

@@ -288,8 +288,10 @@ def test_gn_solve_matches_oracle():
     g = np.ascontiguousarray(np.stack(gs))
     x = np.zeros((len(Hs), 6))
     R._check(R.lib().r360_solve6(R._dptr(H), R._dptr(g), len(Hs), R._dptr(x)), "solve6")
-    ref = np.stack([O.solve6(h, gg) for h, gg in zip(Hs, gs)])
-    assert np.array_equal(x.view(np.uint64), ref.view(np.uint64))
+    ref = [O.solve6(h, gg) for h, gg in zip(Hs, gs)]
+    ok = [k for k, r in enumerate(ref) if r is not None]     # exactly singular systems: no oracle answer
+    assert len(ok) > 240
+    assert np.array_equal(x[ok].view(np.uint64), np.stack([ref[k] for k in ok]).view(np.uint64))
 
 
 def test_set_frames_from_sphere_images(ctx, qvga):

@@ -83,7 +83,8 @@ def last_pass(label, nbl=512):
     us = lambda x: (x - base) / 100.0
     le = (ab[1] - base) / 100.0
     print(f"{label}: loop end pct 0/50/90/100 {np.percentile(le, [0, 50, 90, 100]).round(2)} | last block: start"
-          f" {us(t[0]):6.2f} loop-end {us(t[1]):6.2f} ticket {us(t[2]):6.2f} records {us(t[3]):6.2f} end {us(t[4]):6.2f}")
+          f" {us(t[0]):6.2f} loop-end {us(t[1]):6.2f} ticket {us(t[2]):6.2f} records {us(t[3]):6.2f} end {us(t[4]):6.2f}"
+          f" | GN state {us(t[7]):6.2f} rank {us(t[10]):6.2f} solve {us(t[11]):6.2f}")
 
 
 if os.environ.get("ALIGN"):
