@@ -209,6 +209,55 @@ def cpu_baseline(cal, frames_of, first, last, workload, iters0, budget_s=10.0):
                       "thread count; value = the faster run"}
 
 
+def half_leg(kind, device, rows, cols, p0, p1, frames_of, params, pipelines, queue, depth, min_run, repeats=3):
+    """BASELINE configs[1] / configs[2] as secondary blocks of the default line: one half of the headline workload
+    over the same synthetic sequence, same pipelines, batched like the headline run.
+      kind "planes" (configs[1]): per pair the upload + Frame360 build with planes (PbMap) + RegisterPbMap(25,
+                                  PLANAR_3DoF), no alignFrames360;
+      kind "dense"  (configs[2]): per pair the upload + stitch + 5-level pyramid + alignFrames360(PHOTO_DEPTH) with
+                                  the reference schedule on levels 4..1 and exactly params.fixed_iters_level0 (20) GN
+                                  iterations at level 0, the dense queue batching the pipelines' alignments.
+    Returns pairs/s (whole sequence x repeats after one warm-up pass) and, for the dense half, its level-0 pass."""
+    from rgbd360_amd import odometry as OD
+    P = OD.pipelines_for(p1 - p0, pipelines, min_run)
+    runs = OD.split_range(p0, p1, P)
+    runner = OD.SequenceRunner(device, rows, cols, len(runs), params, planes=kind == "planes",
+                               dense_only=kind == "dense", queue=queue, planes_only=kind == "planes", depth=depth)
+    runner.run(p0, p1, frames_of, np.zeros((1, p1 - p0, OD.REC), np.float32), repeats=1, runs=runs)   # warm-up
+    qctx = runner.queue.ctx if runner.queue else None
+    if qctx:
+        qctx.kernel_time_reset()
+    rec = np.zeros((repeats, p1 - p0, OD.REC), np.float32)
+    t0 = time.perf_counter()
+    runner.run(p0, p1, frames_of, rec, repeats=repeats, runs=runs)
+    elapsed = time.perf_counter() - t0
+    out = {"value": (p1 - p0) * repeats / elapsed, "unit": "pairs/s", "pairs": p1 - p0, "repeats": repeats,
+           "ms_per_pair": elapsed / ((p1 - p0) * repeats) * 1e3, "pipelines": len(runs)}
+    if kind == "planes":
+        st = rec[-1, :, OD.R_STATUS]
+        out["workload"] = ("config2 over the config4 sequence: per pair upload + Frame360 build with planes (PbMap) + "
+                           "RegisterPbMap(25 planes, PLANAR_3DoF), no alignFrames360")
+        out["pbmap_failed"] = int((st == 1).sum())
+    else:
+        us, n, nj = qctx.kernel_stats(0)
+        W0 = cols * 8
+        N0 = int(W0 * 0.5 * 60.0 / 180) * W0
+        sso = float(np.mean(rec[:, :, OD.R_SSO]))
+        alg = 8.0 * N0 + 24.0 * sso * N0
+        avg_ms = us / max(n, 1) * 1e-3
+        ppl = nj / max(n, 1)
+        ach = ppl * alg / (avg_ms * 1e-3) / 1e9 if n else None
+        out["workload"] = ("config3 over the config4 sequence: per pair upload, stitch + 5-level pyramid, "
+                           f"alignFrames360(PHOTO_DEPTH) levels 4..1 reference schedule + {params.fixed_iters_level0} GN "
+                           "iterations at level 0 (dense queue batches of up to 16 pairs)")
+        out["roofline"] = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": (ach / HBM_PEAK_GBS) if ach else None, "avg_launch_ms": avg_ms, "launches": n,
+                           "pairs_per_launch": ppl, "bytes_per_pair_pass": alg,
+                           "kernel": "k_icp_pass<PHOTO_DEPTH> (level 0)", "timing": "in-kernel execution span"}
+    runner.close()
+    return out
+
+
 def config5_leg(device, rt8, pairs=48, iters0=50, pipelines=8, depth=2, repeats=3):
     """BASELINE configs[4], the HBM stress case, as a secondary block of the default line: the dense stage
     (upload, stitch + 5-level pyramid, alignFrames360(PHOTO_DEPTH) with the reference schedule on levels 4..1
@@ -311,6 +360,7 @@ def main(argv=None, runner_factory=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-resident", action="store_true", help="skip the HBM-resident-input secondary run")
     ap.add_argument("--no-config5", action="store_true", help="skip the config-5 (8x1280x960, 50 iterations) leg")
+    ap.add_argument("--no-halves", action="store_true", help="skip the config-2 (planes) and config-3 (dense) legs")
     ap.add_argument("--no-isolated", action="store_true",
                     help="skip the lone-pipeline rerun after the timed region (profiling: the trace then holds only "
                          "the warmup and timed launches)")
@@ -388,10 +438,13 @@ def main(argv=None, runner_factory=None):
     th0 = thread_cpu_s()
     t0 = time.perf_counter()
     runner.run(p0, p1, frames_of, rec, repeats=args.steps, runs=runs)
+    t_run = time.perf_counter() - t0
+    t_g = time.perf_counter()
     if group is not None:   # RCCL gather of the pair records over xGMI
         allrec, sizes = gather_records(group.allgather, rec, -(-(args.frames - 1) // shard_world))
     else:
         allrec, sizes = rec, [p1 - p0]
+    gather_s = time.perf_counter() - t_g
     traj = OD.compose(allrec[-1]) if rank == 0 else None   # OdometryRGBD360.cpp:257
     elapsed = time.perf_counter() - t0
     ru1 = os.times()
@@ -428,7 +481,15 @@ def main(argv=None, runner_factory=None):
     host_ms["pbmap_stage_split"] = {k: 1e3 * v / max(ht[3], 1) for k, v in
                                     zip(("wait_frame_pbmaps", "match_tables", "tree_and_pose"), ht[:3])}
     host_ms["pbmap_assembly_per_frame"] = 1e3 * ht[4] / max(ht[5], 1)
+    per_rank = None
     if group is not None:
+        # per-rank figures for diagnosing a scaling run from its own line: pairs, time to the end of its shard, the
+        # record gather's share of the timed region, and the halo frames (one per pipeline run) it rebuilt
+        mine = np.array([rank, p1 - p0, elapsed, t_run, gather_s, len(runs), P], np.float64)
+        allm = group.allgather(mine.astype(np.float32))
+        per_rank = [{"rank": int(m[0]), "pairs_per_step": int(m[1]), "pairs_per_s": float(m[1] * args.steps / m[2]),
+                     "shard_s": float(m[3]), "timed_s": float(m[2]), "gather_ms": float(m[4] * 1e3),
+                     "halo_frames_per_step": int(m[5]), "pipelines": int(m[6])} for m in allm]
         elapsed = group.max(elapsed)
     pairs_job = args.steps * sum(sizes)
     value = pairs_job / elapsed
@@ -573,6 +634,7 @@ def main(argv=None, runner_factory=None):
         "host_cores_busy": round(host_cores_busy, 2),
         "host_cores_split": host_split,
         **({"dense_queue": {**qstats, "mean_batch": qstats["jobs"] / max(qstats["batches"], 1)}} if qstats else {}),
+        **({"per_rank": per_rank} if per_rank else {"gather_ms": gather_s * 1e3}),
         "frame_generation_s": round(gen_s, 1),
     }
     if rank == 0 and traj is not None:
@@ -584,8 +646,14 @@ def main(argv=None, runner_factory=None):
                                       "illposed": int((st == 2).sum())})
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(runner.cals[0], frames_of, p0, p1, args.workload, args.iters0)
-    pinned.close()
     runner.close()
+    # configs[1] and configs[2] (the two halves of each pair's work) over the same sequence, after the timed region
+    if rank == 0 and world == 1 and not args.no_halves and args.workload == "sequence":
+        out["config2"] = half_leg("planes", local, args.rows, args.cols, p0, p1, frames_of, params, args.streams,
+                                  args.queue, args.depth, args.min_run)
+        out["config3"] = half_leg("dense", local, args.rows, args.cols, p0, p1, frames_of, params, args.streams,
+                                  args.queue, args.depth, args.min_run)
+    pinned.close()
     if rank == 0 and world == 1 and not args.no_config5 and args.workload == "sequence" and args.rows == 480:
         del BGR, DEP
         out["config5"] = config5_leg(local, rt8)

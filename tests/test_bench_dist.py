@@ -180,3 +180,8 @@ def test_bench_main_two_ranks(tmp_path):
     assert tr["max_rot_err_deg"] < 0.05 and tr["max_trans_err_m"] < 1e-5
     assert tr["pbmap_failed"] == 11 and tr["illposed"] == 0                  # status = rank: rank 1's 11 pairs arrived
     assert out["value"] > 0 and abs(out["value"] - 46 / (out["ms_per_step"] * 2e-3)) < 1e-6 * out["value"]
+    # per-rank diagnostics of the N > 1 line: shard sizes, rates, the gather's time, halo frames
+    pr = out["per_rank"]
+    assert [r["rank"] for r in pr] == [0, 1] and [r["pairs_per_step"] for r in pr] == [12, 11]
+    assert all(r["pairs_per_s"] > 0 and r["gather_ms"] >= 0 and r["halo_frames_per_step"] >= 1 for r in pr)
+    assert max(r["timed_s"] for r in pr) == pytest.approx(out["ms_per_step"] * 2e-3, rel=1e-5)

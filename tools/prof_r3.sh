@@ -13,7 +13,7 @@ R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-ARGS="--steps 2 --warmup 1 --no-cpu-baseline --no-resident --no-config5 --no-isolated $*"
+ARGS="--steps 2 --warmup 1 --no-cpu-baseline --no-resident --no-config5 --no-isolated --no-halves $*"
 HARGS="--workload dense --rows 960 --cols 1280 --iters0 50 --frames 33 --steps 1 --warmup 1 --no-cpu-baseline --no-resident --no-isolated --streams 8 --depth 2 --min-run 4"
 step() {   # step <name> <timeout> <cmd...>: stops the script on the first failure
     local name=$1 to=$2; shift 2
