@@ -355,6 +355,8 @@ def main(argv=None, runner_factory=None):
                          "on each pipeline's stream")
     ap.add_argument("--depth", type=int, default=3,
                     help="dense queue: alignments in flight per pipeline (each needs one more Frame360 buffer)")
+    ap.add_argument("--lookahead", type=int, default=1,
+                    help="dense queue: frames whose build is enqueued ahead of the pair being registered")
     ap.add_argument("--emulate", type=str, default=None,
                     help="RANK/WORLD: run that rank's shard alone (single-GPU rehearsal of an N-GPU shard)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -410,7 +412,7 @@ def main(argv=None, runner_factory=None):
     runner = (runner_factory or OD.SequenceRunner)(local, args.rows, args.cols, P, params,
                                                    planes=args.workload != "dense", dense_only=args.workload == "dense",
                                                    queue=args.queue, planes_only=args.workload == "planes",
-                                                   depth=args.depth)
+                                                   depth=args.depth, lookahead=args.lookahead)
     ctxs = runner.ctxs + ([runner.queue.ctx] if runner.queue else [])
     dense_ctx = runner.queue.ctx if runner.queue else ctxs[0]   # where pipeline 0's alignments run
 
@@ -609,6 +611,7 @@ def main(argv=None, runner_factory=None):
             "n_pyr": 5, "parallelism": f"pair-shard dp{world}", "pairs_per_step": pairs_job // args.steps,
             "pairs_per_step_this_rank": steps_pairs, "pipelines_per_gpu": P,
             "dense_batch": args.queue, "dense_in_flight_per_pipeline": args.depth if args.queue else 1,
+            "frames_built_ahead": args.lookahead if args.queue else 1,
             **({"emulated_shard": f"{shard_rank}/{shard_world}"} if args.emulate else {}),
         },
         "value_hbm_resident_inputs": resident,

@@ -1422,51 +1422,47 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
 #ifdef R360_STAMPS
     const unsigned long long t_recs = __builtin_amdgcn_s_memrealtime();
 #endif
-    if (threadIdx.x < 64) {
-        if (eval_only) {
-            if (threadIdx.x < 32) S->sums[threadIdx.x] = s_fin[0][threadIdx.x];
+    if (eval_only) {
+        if (threadIdx.x < 32) S->sums[threadIdx.x] = s_fin[0][threadIdx.x];
 #ifdef R360_STAMPS
-            if (threadIdx.x == 0) {
-                const unsigned long long mn = __hip_atomic_load(&S->dbg[8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const unsigned long long mx = __hip_atomic_load(&S->dbg[9], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                S->dbg[5] = mn; S->dbg[6] = mx; S->dbg[8] = ~0ull; S->dbg[9] = 0;
-                S->dbg[0] = t_start; S->dbg[1] = t_loop; S->dbg[2] = t_ticket; S->dbg[3] = t_recs;
-                S->dbg[4] = __builtin_amdgcn_s_memrealtime();
-            }
-#endif
-        } else {
-            // Stage the whole state in LDS with one coalesced 16-B access per lane, run the step on
-            // the LDS copy (a single lane walking global memory serialises ~150 dependent accesses,
-            // ~35 us), then write it back the same way.
-            constexpr int NQ = (int)(sizeof(IcpState) / 16);
-            uint4* sq = reinterpret_cast<uint4*>(&s_state);
-            const uint4* gq = reinterpret_cast<const uint4*>(S);
-            for (int q = threadIdx.x; q < NQ; q += 64) sq[q] = gq[q];
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-            gn_step_wave(&s_state, s_fin[0], C, first, &s_gn, threadIdx.x);
-            if (threadIdx.x == 0) s_state.ticket = 0;
-#ifdef R360_STAMPS
-            if (threadIdx.x == 0) {
-                s_state.dbg[5] = s_state.dbg[8]; s_state.dbg[6] = s_state.dbg[9];
-                s_state.dbg[8] = ~0ull; s_state.dbg[9] = 0;
-            }
-#endif
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-            uint4* wq = reinterpret_cast<uint4*>(S);
-            for (int q = threadIdx.x; q < NQ; q += 64) wq[q] = sq[q];
-#ifdef R360_STAMPS
-            if (threadIdx.x == 0) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
-                S->dbg[0] = t_start; S->dbg[1] = t_loop; S->dbg[2] = t_ticket; S->dbg[3] = t_recs; S->dbg[4] = t_end;
-            }
-#endif
+        if (threadIdx.x == 0) {
+            const unsigned long long mn = __hip_atomic_load(&S->dbg[8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long mx = __hip_atomic_load(&S->dbg[9], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            S->dbg[5] = mn; S->dbg[6] = mx; S->dbg[8] = ~0ull; S->dbg[9] = 0;
+            S->dbg[0] = t_start; S->dbg[1] = t_loop; S->dbg[2] = t_ticket; S->dbg[3] = t_recs;
+            S->dbg[4] = __builtin_amdgcn_s_memrealtime();
         }
-        if (eval_only && threadIdx.x == 0) S->ticket = 0;
-        if (threadIdx.x == 0) pass_arrive(kt, true, C.level);   // the job's last workgroup
+#endif
+        if (threadIdx.x == 0) {
+            S->ticket = 0;
+            pass_arrive(kt, true, C.level);   // the job's last workgroup
+        }
+        return;
     }
+    // Stage the whole state in LDS with one coalesced 16-B access per thread, run the step on the LDS copy (one
+    // lane walking global memory serialises ~150 dependent accesses, ~35 us), then write it back the same way.
+    constexpr int NQ = (int)(sizeof(IcpState) / 16);
+    uint4* sq = reinterpret_cast<uint4*>(&s_state);
+    for (int q = threadIdx.x; q < NQ; q += TPB) sq[q] = reinterpret_cast<const uint4*>(S)[q];
+    __syncthreads();
+    gn_step_block(&s_state, s_fin[0], C, first, &s_gn, threadIdx.x);
+    if (threadIdx.x == 0) {
+        s_state.ticket = 0;
+#ifdef R360_STAMPS
+        s_state.dbg[5] = s_state.dbg[8]; s_state.dbg[6] = s_state.dbg[9];
+        s_state.dbg[8] = ~0ull; s_state.dbg[9] = 0;
+#endif
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < NQ; q += TPB) reinterpret_cast<uint4*>(S)[q] = sq[q];
+#ifdef R360_STAMPS
+    if (threadIdx.x == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+        S->dbg[0] = t_start; S->dbg[1] = t_loop; S->dbg[2] = t_ticket; S->dbg[3] = t_recs; S->dbg[4] = t_end;
+    }
+#endif
+    if (threadIdx.x == 0) pass_arrive(kt, true, C.level);   // the job's last workgroup
 }
 
 // ---------------------------------------------------------------- occlusion variants (§8(f)1)
@@ -1762,22 +1758,21 @@ __global__ void k_rn_check(unsigned n, unsigned seed, unsigned long long* __rest
 }  // namespace
 
 namespace {
-// the register form (the GN step's) and the wave form (pinhole / robot steps) must agree: -1 where they do not
+// the row form (the GN step's) and the wave form (pinhole / robot steps) must agree: -1 where they do not
 __global__ void k_rank6(const float* __restrict__ M, int n, int* __restrict__ out) {
     const int m = blockIdx.x, lane = threadIdx.x;
     if (m >= n) return;
     const float a = lane < 36 ? M[m * 36 + lane] : 0.f;
     const int rw = wave_rank6(a, lane);
-    if (lane == 0) {
-        float W[36];
+    float r[6];
+    const int i = lane < 6 ? lane : 0;
 #pragma unroll
-        for (int l = 0; l < 36; ++l) W[l] = M[m * 36 + l];
-        const int rr = rank6_reg(W);
-        out[m] = rr == rw ? rr : -1;
-    }
+    for (int j = 0; j < 6; ++j) r[j] = M[m * 36 + i * 6 + j];
+    const int rr = rank6_rows(r, lane);
+    if (lane == 0) out[m] = rr == rw ? rr : -1;
 }
 
-// x = -H^-1 g by the GN step's row-per-lane solve (solve6_rows); one wave per system
+// x = -H^-1 g by the GN step's row-per-lane solve (solve6_rows_dpp); one wave per system
 __global__ void k_solve6(const double* __restrict__ H, const double* __restrict__ g, int n, double* __restrict__ x) {
     const int m = blockIdx.x, lane = threadIdx.x;
     if (m >= n) return;
@@ -1786,14 +1781,14 @@ __global__ void k_solve6(const double* __restrict__ H, const double* __restrict_
 #pragma unroll
     for (int j = 0; j < 6; ++j) a[j] = H[m * 36 + i * 6 + j];
     a[6] = -g[m * 6 + i];
-    solve6_rows(a, lane, xs);
+    solve6_rows_dpp(a, lane, xs);
     if (lane == 0)
 #pragma unroll
         for (int k = 0; k < 6; ++k) x[m * 6 + k] = xs[k];
 }
 }  // namespace
 
-// Test hook: the GN step's solve (icp_la.inc solve6_rows) on n systems (H row-major n x 36, g n x 6) -> x n x 6.
+// Test hook: the GN step's solve (icp_la.inc solve6_rows_dpp) on n systems (H row-major n x 36, g n x 6) -> x n x 6.
 extern "C" int r360_solve6(const double* H, const double* g, int n, double* x) {
     if (!H || !g || !x || n <= 0) { r360_set_error("r360_solve6: bad arguments"); return -2; }
     double *dH, *dg, *dx;

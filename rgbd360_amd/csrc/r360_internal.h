@@ -146,9 +146,6 @@ struct IcpJob {
 struct IcpJobs { IcpJob j[R360_MAX_BATCH]; };   // passed by value (kernel arguments, 1152 B)
 
 constexpr int R360_KT_SLOTS = 26;
-#ifndef R360_GN_SERIAL   // 1: the GN step's rank test and solve on one lane; 0 (experiment builds): wave-parallel
-#define R360_GN_SERIAL 1
-#endif
 #ifndef R360_GROUP_SUM   // 1: group records summed by each ticket group's last workgroup; 0 (experiment builds): flat sum
 #define R360_GROUP_SUM 1
 #endif

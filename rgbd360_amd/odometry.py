@@ -104,8 +104,9 @@ class SequenceRunner:
 
     def __init__(self, device: int, rows: int, cols: int, pipelines: int, params: IcpParams,
                  planes: bool = True, max_match_planes: int = 25, mode: int = PLANAR_3DoF, dense_only: bool = False,
-                 queue: int = 0, planes_only: bool = False, depth: int = 1):
+                 queue: int = 0, planes_only: bool = False, depth: int = 1, lookahead: int = 1):
         self.P = pipelines
+        self.lookahead = max(1, lookahead)   # queued mode: frames whose build is enqueued ahead of the pair in hand
         self.dense_only = dense_only
         self.planes_only = planes_only
         if planes_only:
@@ -121,8 +122,9 @@ class SequenceRunner:
             cal = Calib360(c, rows, cols)
             cal.loadExtrinsicCalibration(EXTRINSICS_DIR)
             self.cals.append(cal)
-            # queued: depth alignments in flight, the pair being registered, and the next frame's prefetched upload
-            self.frames.append([Frame360(cal) for _ in range(self.depth + 3 if self.queue else 2)])
+            # queued: depth alignments in flight, the pair being registered, the frames built ahead and the next
+            # frame's prefetched upload
+            self.frames.append([Frame360(cal) for _ in range(self.depth + self.lookahead + 2 if self.queue else 2)])
         self.stats = [IcpStats() for _ in range(pipelines)]
         # host-side time per pipeline: [load + build enqueue, PbMap stage (register_async), dense wait, pairs]
         self.host_s = np.zeros((pipelines, 4))
@@ -191,10 +193,12 @@ class SequenceRunner:
     def _pipeline_queued(self, p: int, run: tuple[int, int], frames_of, out: np.ndarray, p0: int,
                          device_inputs: bool):
         """_pipeline with the dense stage on the queue: submit pair i, then collect pair i-depth (so `depth`
-        alignments per pipeline are in flight while the next frame is built and PbMap-registered).  The upload of
-        frame i+2 is issued right after frame i+1's build (same stream: it runs when that build is done, while the
-        host assembles and matches frame i+1's planes), so the next iteration's build does not wait for its copy.
-        Frame i+2 goes into the buffer of frame i+2-(depth+3), whose pairs were collected in earlier iterations."""
+        alignments per pipeline are in flight while the next frame is built and PbMap-registered).  Frames are
+        built `lookahead` ahead of the pair in hand: iteration i enqueues frame i+L's build (L = lookahead) before
+        RegisterPbMap(i, i+1) waits for frame i+1's planes, so with L = 2 the GPU works on frame i+2 while the host
+        assembles and matches frame i+1's.  The upload of frame i+L+1 is issued right after frame i+L's build (same
+        stream), so the next iteration's build does not wait for its copy.  Frame j lives in buffer (j - a) % nbuf,
+        nbuf = depth + L + 2: the buffer's previous frame j - nbuf belonged to pairs collected earlier."""
         L = lib()
         ctx = self.ctxs[p]
         fr = self.frames[p]
@@ -229,18 +233,22 @@ class SequenceRunner:
             rec[R_ERR] = st.error
 
         nbuf = len(fr)
-        depth = nbuf - 3
-        load(fr[0], a)
-        fr[0].build(self.flags, sync=False)
-        load(fr[1 % nbuf], a + 1)
+        L = self.lookahead
+        depth = nbuf - L - 2
+        for j in range(a, min(a + L, b + 1)):   # frames a .. a+L-1 built, frame a+L uploaded
+            load(fr[(j - a) % nbuf], j)
+            fr[(j - a) % nbuf].build(self.flags, sync=False)
+        if a + L <= b:
+            load(fr[L % nbuf], a + L)
         pending = []
         sts = [IcpStats() for _ in range(depth + 1)]
         for i in range(a, b):
             t0 = time.perf_counter()
             cur, nxt = fr[(i - a) % nbuf], fr[(i + 1 - a) % nbuf]
-            nxt.build(self.flags, sync=False)   # its upload was issued one iteration earlier
-            if i + 2 <= b:
-                load(fr[(i + 2 - a) % nbuf], i + 2)
+            if i + L <= b:
+                fr[(i + L - a) % nbuf].build(self.flags, sync=False)   # its upload was issued one iteration earlier
+            if i + L + 1 <= b:
+                load(fr[(i + L + 1 - a) % nbuf], i + L + 1)
             t1 = time.perf_counter()
             ticket = C.c_long()
             if self.dense_only:

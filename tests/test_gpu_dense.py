@@ -256,9 +256,10 @@ def test_correctly_rounded_sqrt_div():
 
 
 def test_rank_test_matches_oracle_over_lambda_schedule():
-    """The device ILL-POSED test (icp_la.inc wave_rank6: Eigen's float FullPivLU rank) gives the oracle's
-    verdict on near-singular Hessians over alignFrames360's decaying lambda (1, /5 per accepted update,
-    RegisterPhotoICP.h:4589, :4718), including the ones where the decay flips it."""
+    """The device ILL-POSED tests (icp_la.inc rank6_rows of the GN step and wave_rank6 of the pinhole / robot steps:
+    Eigen's float FullPivLU rank; r360_rank6 returns -1 where the two disagree) give the oracle's verdict on
+    near-singular Hessians over alignFrames360's decaying lambda (1, /5 per accepted update, RegisterPhotoICP.h:4589,
+    :4718), including the ones where the decay flips it."""
     from _cases import lambda_family
     fam = lambda_family()
     M = np.ascontiguousarray(np.stack([m for _, _, m in fam]), np.float32)
@@ -270,7 +271,7 @@ def test_rank_test_matches_oracle_over_lambda_schedule():
 
 
 def test_gn_solve_matches_oracle():
-    """The GN step's solve (icp_la.inc solve6_rows: row per lane, pivot rows broadcast by readlane) gives the
+    """The GN step's solve (icp_la.inc solve6_rows_dpp: row per lane, DPP pivot search) gives the
     oracle's x = -H^-1 g (oracle_la.h solve6) bit for bit: SPD Hessians of the scales the passes produce, badly
     conditioned ones, and matrices whose pivot order differs from the diagonal's."""
     rng = np.random.default_rng(7)
