@@ -144,7 +144,8 @@ typedef struct {
     float  sso;                 /* SSO (:3226)                               */
     double error;               /* accepted error at level 0                 */
     int    passes;              /* fused residual/Jacobian/JtJ passes run     */
-    int    pad;
+    int    persistent;          /* r360_align360: 1 = each level ran as ONE launch (k_icp_level) instead of
+                                   one launch per pass; same results either way */
     /* The public residual members RegisterPhotoICP leaves after the call (RegisterPhotoICP.h:183-189).
      * alignFrames360 with occlusion 1 / 2: avPhotoResidual / avDepthResidual of the last error evaluation
      * (errorPhotoICP_sphereOcc1 :3360-3362, Occ2 :3852-3853); avResidual is set only when ILL-POSED (= 0,

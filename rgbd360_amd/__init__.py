@@ -81,7 +81,7 @@ class MatchParams(C.Structure):
 class IcpStats(C.Structure):
     _fields_ = [
         ("iters", C.c_int * 8), ("evals", C.c_int * 8), ("illposed", C.c_int), ("sso", C.c_float),
-        ("error", C.c_double), ("passes", C.c_int), ("pad", C.c_int),
+        ("error", C.c_double), ("passes", C.c_int), ("persistent", C.c_int),
         ("av_photo_residual", C.c_double), ("av_depth_residual", C.c_double), ("av_residual", C.c_float),
         ("residuals_set", C.c_int),
     ]

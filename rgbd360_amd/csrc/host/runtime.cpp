@@ -1,6 +1,7 @@
 // runtime.cpp — host side of librgbd360_hip.so: contexts, Calib360, Frame360 and the
 // RegisterPhotoICP::alignFrames360 driver.  Everything here is plumbing around the HIP kernels
 // (frame_kernels.hip, icp_kernels.hip); the per-pixel work never runs on the CPU.
+#include <atomic>
 #include <chrono>
 #include <dlfcn.h>
 #include <cmath>
@@ -190,10 +191,13 @@ extern "C" int r360_ctx_create(int device, r360_ctx** out) {
     return 0;
 }
 
+void persist_release(r360_ctx* ctx);
+
 extern "C" void r360_ctx_destroy(r360_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
+    persist_release(c);
     for (auto e : c->ev_pool) hipEventDestroy(e);
     hipEventDestroy(c->wait_ev);
     if (c->mwait_ev) hipEventDestroy(c->mwait_ev);   // mstream is the device's shared match stream
@@ -783,11 +787,11 @@ static int check_pair(r360_ctx* ctx, r360_frame* trg, r360_frame* src, const r36
 // sphere tables, the ctx's state / record / counter / queue buffers, the method and the parameters.
 template <class Enqueue>
 static int align_graph_launch(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src, int method,
-                              const r360_icp_params* p, Enqueue&& enqueue) {
+                              const r360_icp_params* p, bool persist, Enqueue&& enqueue) {
     std::vector<uintptr_t> key;
     key.reserve(16 + 20 * p->n_pyr);
     auto put = [&](const void* q) { key.push_back((uintptr_t)q); };
-    put(trg); put(src); key.push_back((uintptr_t)method);
+    put(trg); put(src); key.push_back((uintptr_t)method); key.push_back((uintptr_t)persist);
     put(ctx->d_state); put(ctx->d_partials); put(ctx->d_gticket); put(ctx->d_defer);
     key.push_back((uintptr_t)ctx->defer_cap); key.push_back((uintptr_t)ctx->partials_cap); put(ctx->d_ktime);
     put(src->d_npts); put(src->calib);
@@ -836,6 +840,24 @@ static int align_graph_launch(r360_ctx* ctx, const r360_frame* trg, const r360_f
     return 0;
 }
 
+// One persistent level launch in flight per process: its grid must be resident whole (k_icp_level), and two of
+// them leave room per CU (icp_level_persist_ok keeps one workgroup per CU spare); the slot is taken when an
+// alignment is enqueued that way and given back when its result is read (or the ctx is destroyed).  Another
+// alignment enqueued meanwhile launches its passes one by one.
+static std::atomic<int> g_persist_slot{0};
+static bool persist_take(r360_ctx* ctx) {
+    if (ctx->persist_held) return true;
+    int z = 0;
+    if (!g_persist_slot.compare_exchange_strong(z, 1)) return false;
+    ctx->persist_held = 1;
+    return true;
+}
+void persist_release(r360_ctx* ctx) {
+    if (!ctx->persist_held) return;
+    ctx->persist_held = 0;
+    g_persist_slot.store(0);
+}
+
 extern "C" int r360_align360_async(r360_ctx* ctx, r360_frame* trg, r360_frame* src, const float init[16], int method,
                                    int occlusion, const r360_icp_params* p) {
     if (ctx && bind_device(ctx->device)) return -1;
@@ -850,11 +872,22 @@ extern "C" int r360_align360_async(r360_ctx* ctx, r360_frame* trg, r360_frame* s
     memcpy(h->cand, init, sizeof(float) * 16);
     h->dbg[8] = ~0ull;
     R360_HIP(hipMemcpyAsync(ctx->d_state, h, sizeof(IcpState), hipMemcpyHostToDevice, ctx->stream));
+    // the plain pass without per-launch timing events runs each level as one persistent launch (k_icp_level)
+    // when every level's grid fits; otherwise (occlusion variants, timing, another persistent launch in
+    // flight) one launch per pass.  R360_NO_PERSIST=1 (experiment builds) forces the per-pass launches.
+    static const bool no_persist = R360_KNOB("R360_NO_PERSIST", 0) != 0;
+    bool persist = !no_persist && !occlusion && !ctx->timing && !R360_POLL;
+    for (int l = 0; persist && l < p->n_pyr; ++l) persist = icp_level_persist_ok(ctx, src, l, method);
+    if (persist) persist = persist_take(ctx);
     auto passes_of = [&]() -> int {
         for (int l = p->n_pyr - 1; l >= 0; --l) {
             const int np = src->lv[l].rows * src->lv[l].cols;
             const IcpConst C = make_const(p, l, np, occlusion);
             const int passes = 1 + ((l == 0 && p->fixed_iters_level0 > 0) ? p->fixed_iters_level0 : p->max_iters);
+            if (persist) {
+                if (launch_icp_level_persist(ctx, trg, src, l, method, C, passes)) return -1;
+                continue;
+            }
             for (int k = 0; k < passes; ++k)
                 if (launch_icp_level(ctx, trg, src, l, method, C, k == 0, 0)) return -1;
         }
@@ -863,12 +896,15 @@ extern "C" int r360_align360_async(r360_ctx* ctx, r360_frame* trg, r360_frame* s
     // graphs for the plain pass (occlusion passes size their buffers on first use) without per-launch timing
     // events; R360_NO_GRAPH=1 launches one by one (A/B)
     static const bool no_graph = R360_KNOB("R360_NO_GRAPH", 0) != 0;
-    if (no_graph || R360_POLL || occlusion || ctx->timing) {
-        if (passes_of()) return -1;
-    } else {
-        if (align_graph_launch(ctx, trg, src, method, p, passes_of)) return -1;
+    int rc;
+    if (no_graph || R360_POLL || occlusion || ctx->timing) rc = passes_of();
+    else rc = align_graph_launch(ctx, trg, src, method, p, persist, passes_of);
+    if (rc) {
+        persist_release(ctx);
+        return -1;
     }
     ctx->async_nL = p->n_pyr;
+    ctx->async_persist = persist ? 1 : 0;
     ctx->async_pending = 1;
     return 0;
 }
@@ -891,12 +927,21 @@ extern "C" int r360_align360_result(r360_ctx* ctx, float pose_out[16], float H_o
     CHECK_ARG(ctx && ctx->async_pending, "no alignment pending");
     IcpState* h = ctx->h_state;
     R360_HIP(hipMemcpyAsync(h, ctx->d_state, sizeof(IcpState), hipMemcpyDeviceToHost, ctx->stream));
-    if (ctx_wait(ctx)) return -1;
+    const int wrc = ctx_wait(ctx);
+    persist_release(ctx);
+    if (wrc) return -1;
     ctx->async_pending = 0;
+    if (h->fault) {
+        r360_set_error("alignFrames360: a persistent level launch timed out waiting for a pass (GPU oversubscribed?)");
+        return -1;
+    }
     if (pose_out) memcpy(pose_out, h->pose, sizeof(float) * 16);
     if (H_out) memcpy(H_out, h->Hout, sizeof(float) * 36);
     if (g_out) memcpy(g_out, h->gout, sizeof(float) * 6);
-    if (st) fill_stats(h, st);
+    if (st) {
+        fill_stats(h, st);
+        st->persistent = ctx->async_persist;
+    }
     return h->illposed ? 1 : 0;
 }
 

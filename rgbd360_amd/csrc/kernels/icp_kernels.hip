@@ -14,6 +14,7 @@
 // bytes of SURVEY.md §8(d).  No Jacobian rows are materialised (the reference writes and
 // re-reads imgSize x 6 buffers, :2761-2767).
 #include <cstdio>
+#include <type_traits>
 #include "../r360_internal.h"
 #include "../libm_f32.h"
 
@@ -529,32 +530,58 @@ __device__ __forceinline__ void contribute_lean(Acc& A, WaveCnt& W, float& errf,
 
 
 // The last arrival of a pass's jobs (a job's last workgroup, or block 0 of a job that exits at entry) closes
-// the pass's in-kernel execution span, if any job ran.
-__device__ __forceinline__ void pass_arrive(unsigned long long* kt, bool ran, int level) {
-    const unsigned long long prev = __hip_atomic_fetch_add(kt + 17, 1ull + (ran ? (1ull << 32) : 0ull),
-                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if ((unsigned)prev != gridDim.y - 1) return;
-    __hip_atomic_store(kt + 17, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if ((prev >> 32) + (ran ? 1 : 0) == 0) return;
-    const unsigned long long t0 = __hip_atomic_load(kt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+// the pass's in-kernel execution span, if any job ran.  kp (optional): kt[0] and the level's three accumulators,
+// loaded before the step (nothing writes them during a launch but its last arrival).  A one-job launch needs no
+// arrival count: its job's last workgroup is the last arrival, and the span is stored without a dependent
+// memory round trip behind the step (three of them were ~2 us of every lone pass's tail).
+__device__ __forceinline__ void pass_arrive(unsigned long long* kt, bool ran, int level,
+                                            const unsigned long long* kp = nullptr, bool persist = false) {
+    unsigned long long runs = ran ? 1ull : 0ull;
+    if (gridDim.y > 1) {
+        const unsigned long long prev = __hip_atomic_fetch_add(kt + 17, 1ull + (ran ? (1ull << 32) : 0ull),
+                                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((unsigned)prev != gridDim.y - 1) return;
+        __hip_atomic_store(kt + 17, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        runs += prev >> 32;
+    }
+    if (runs == 0) return;
     const int lv = level & 7;
-    kt[1 + lv] += t1 > t0 ? t1 - t0 : 0;
-    kt[9 + lv] += 1;
-    kt[18 + lv] += (prev >> 32) + (ran ? 1 : 0);   // job passes (pairs) the launch ran
+    const unsigned long long t0 = kp ? kp[0] : __hip_atomic_load(kt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long a = kp ? kp[1] : kt[1 + lv], b = kp ? kp[2] : kt[9 + lv], c = kp ? kp[3] : kt[18 + lv];
+    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+    // sc1 stores: in a persistent launch the next pass's last workgroup (another CU) reads them
+    __hip_atomic_store(kt + 1 + lv, a + (t1 > t0 ? t1 - t0 : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(kt + 9 + lv, b + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(kt + 18 + lv, c + runs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // job passes (pairs) the launch ran
+    if (persist) __hip_atomic_store(kt, t1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // the next pass's start
 }
 
 // TOP = 1 only renames the level-0 instantiation, so traces (rocprofv3) separate level 0 from level 1,
 // which launch the same grid.  One launch runs gridDim.y independent alignments (jobs.j[blockIdx.y]), each
 // on gridDim.x workgroups with its own records, tickets and GN state: a job's sums and step are exactly
 // those of the same job launched alone.
-template <int METHOD, int PF, int TOP, int OCC>
-__global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs jobs, const float* __restrict__ sinphi,
-                                                 const float* __restrict__ cosphi, const float* __restrict__ sinth,
-                                                 const float* __restrict__ costh, int nRows, int nCols,
-                                                 IcpConst C, int first, int eval_only,
-                                                 unsigned long long* __restrict__ kt,
-                                                 const uint8_t* __restrict__ occf) {
+// One pass of one workgroup (the kernels below): PASS_SKIPPED if the job had stopped (nothing done),
+// PASS_STEPPED in the job's last workgroup (it ran the GN step and wrote the state back), PASS_ARRIVED otherwise.
+// PERSIST: the pass inside the persistent level launch (k_icp_level), where the state was written during the
+// launch by another workgroup: every load of it is an sc1 (L1-bypassing) vector load and the write-back is sc1
+// stores drained before the hand-off (MI355X_MICROARCH.md 'Valid forms', row 1).
+enum : int { PASS_SKIPPED = 0, PASS_ARRIVED = 1, PASS_STEPPED = 2 };
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int ld_sc1_i(const int* p) {
+    return (int)__hip_atomic_load(reinterpret_cast<const unsigned*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1_f(const float* p) {
+    return __uint_as_float(__hip_atomic_load(reinterpret_cast<const unsigned*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+template <int METHOD, int PF, int TOP, int OCC, bool PERSIST>
+__device__ __forceinline__ int icp_pass_body(const IcpJobs& jobs, const float* __restrict__ sinphi,
+                                             const float* __restrict__ cosphi, const float* __restrict__ sinth,
+                                             const float* __restrict__ costh, int nRows, int nCols,
+                                             const IcpConst& C, int first, int eval_only,
+                                             unsigned long long* __restrict__ kt,
+                                             const uint8_t* __restrict__ occf, const int tidx, const int bidx) {
     __shared__ float s_red[NW][32];
     __shared__ double s_err[NW], s_errd[NW];
     __shared__ double s_fin[RG][32];
@@ -579,7 +606,8 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
     // execution span: the start of the launch's first workgroup (dispatched first).  One store, not an
     // atomic-min per workgroup: same-address atomics serialise at the memory side (~25 ns each), and 512
     // of them outlasted a short pass.
-    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+    // (persistent launch: at its first pass; a later pass starts where the previous one's step published)
+    if (bidx == 0 && blockIdx.y == 0 && tidx == 0 && (!PERSIST || first))
         __hip_atomic_store(kt, (unsigned long long)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
 #ifdef R360_STAMPS
@@ -588,9 +616,11 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #endif
 #endif
-    if (S->stop || (!first && !S->active && !eval_only)) {
-        if (blockIdx.x == 0 && threadIdx.x == 0) pass_arrive(kt, false, C.level);
-        return;
+    const int st_stop = PERSIST ? ld_sc1_i(&S->stop) : S->stop;
+    const int st_active = PERSIST ? ld_sc1_i(&S->active) : S->active;
+    if (st_stop || (!first && !st_active && !eval_only)) {
+        if (!PERSIST && bidx == 0 && tidx == 0) pass_arrive(kt, false, C.level);
+        return PASS_SKIPPED;
     }
 #if defined(R360_STAMPS) && !defined(R360_STAMP_ENTRY)
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
@@ -601,8 +631,8 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
 #pragma unroll
-        for (int c = 0; c < 3; ++c) P.R[r * 3 + c] = pm[c * 4 + r];
-        P.t[r] = pm[12 + r];
+        for (int c = 0; c < 3; ++c) P.R[r * 3 + c] = PERSIST ? ld_sc1_f(pm + c * 4 + r) : pm[c * 4 + r];
+        P.t[r] = PERSIST ? ld_sc1_f(pm + 12 + r) : pm[12 + r];
     }
     const float angle_res = (float)(2 * R360_PI / nCols);
     const float angle_res_inv = 1 / angle_res;
@@ -645,7 +675,7 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
     const int stride = gridDim.x * TPB;
     if (PF == 1) {
         // large levels: 4-pixel units (vector loads), processed as two pixel pairs (ILP)
-        for (int u = blockIdx.x * TPB + threadIdx.x; u < units; u += stride) {
+        for (int u = bidx * TPB + tidx; u < units; u += stride) {
             const int r = u / cq;
             const int c4 = u - r * cq;
             const float4 a = src4[2 * u], b = src4[2 * u + 1];  // {g0,d0,g1,d1} {g2,d2,g3,d3}
@@ -659,7 +689,7 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
         // so row/column come from wave-uniform scalar arithmetic and the row LUT is wave-uniform): while
         // chunk k is accumulated, chunk k+1's target gathers and chunk k+2's source loads are in flight
         const int npx = nRows * nCols;
-        const int lane = threadIdx.x & 63;
+        const int lane = tidx & 63;
         struct Src { float d, g, sp, cp, st, ct; int f; };
         auto ld = [&](int base) {                          // base: wave-uniform first pixel
             const int r = __builtin_amdgcn_readfirstlane(base / nCols);
@@ -669,7 +699,7 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
         };
         const Gather gt{__builtin_amdgcn_make_buffer_rsrc(const_cast<float4*>(tg), 0, npx * 16, 0x00020000),
                         __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(trg), 0, npx * 8, 0x00020000)};
-        const int b0 = __builtin_amdgcn_readfirstlane((blockIdx.x * TPB + (threadIdx.x & ~63)));
+        const int b0 = __builtin_amdgcn_readfirstlane((bidx * TPB + (tidx & ~63)));
         if (b0 < npx) {
             // Unrolled by two with fixed register roles (A, B) and unconditional loads (the chunk index is
             // clamped to the wave's last chunk): no loop-carried copies of in-flight loads and the same
@@ -721,9 +751,9 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
         // compiler copy the accumulators), and the exact code runs at full lane occupancy instead of
         // once per chunk that has any flagged lane (about a quarter of them at level 0).
         const int npx = nRows * nCols;
-        const int lane = threadIdx.x & 63;
+        const int lane = tidx & 63;
         const int qcap = ((npx + stride - 1) / stride) * 64;
-        int* q = dq + ((long)blockIdx.x * NW + (threadIdx.x >> 6)) * qcap;
+        int* q = dq + ((long)bidx * NW + (tidx >> 6)) * qcap;
         int qn = 0;   // wave-uniform queue length
         auto acc = [&](const Proj& o, const float4 G, const float2 T, int fl) {
             contribute_fast<METHOD, OCC>(A, W, o, G, T, fl, angle_res_inv, C);
@@ -750,7 +780,7 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
                 qn += __popcll(m);
             }
         };
-        const int b0 = __builtin_amdgcn_readfirstlane((blockIdx.x * TPB + (threadIdx.x & ~63)));
+        const int b0 = __builtin_amdgcn_readfirstlane((bidx * TPB + (tidx & ~63)));
 #ifdef R360_EXP_NOLOOP   // experiment builds only: the pass without its pixel loop (fixed costs)
         if (false) {
 #else
@@ -812,9 +842,9 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
         // of its points, a few per pass: one drain chunk per workgroup instead of one mostly idle chunk per wave).
         constexpr bool LEAN = PF == 5;
         const int nv = __builtin_amdgcn_readfirstlane(*npts);
-        const int lane = threadIdx.x & 63;
+        const int lane = tidx & 63;
         const int qcap = ((nv + stride - 1) / stride) * 64;
-        int* q = dq + ((long)blockIdx.x * NW + (threadIdx.x >> 6)) * qcap;
+        int* q = dq + ((long)bidx * NW + (tidx >> 6)) * qcap;
         int qn = 0;
         auto acc = [&](const Proj& o, const float4 G, const float2 T) {
             if (LEAN) contribute_lean<METHOD>(A, W, errf, o, G, T, angle_res_inv, C);
@@ -845,8 +875,8 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
         // workgroup x runs on XCD x % 8; give each XCD one contiguous nb/8-workgroup slice of every stride
         // period, so a neighbourhood of the target's rows is gathered through one L2 instead of eight
         const int nbx = (int)gridDim.x;
-        const int bx = (nbx & 7) ? (int)blockIdx.x : ((int)blockIdx.x & 7) * (nbx >> 3) + ((int)blockIdx.x >> 3);
-        const int b0 = __builtin_amdgcn_readfirstlane((bx * TPB + (threadIdx.x & ~63)));
+        const int bx = (nbx & 7) ? (int)bidx : ((int)bidx & 7) * (nbx >> 3) + ((int)bidx >> 3);
+        const int b0 = __builtin_amdgcn_readfirstlane((bx * TPB + (tidx & ~63)));
         if (b0 < nv) {
             const int n_it = (nv - 1 - b0) / stride + 1;
             auto base = [&](int k) { return b0 + (k < n_it ? k : n_it - 1) * stride; };
@@ -889,15 +919,15 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
             // the workgroup's queues as one list (wave w's entries after those of waves < w), 64 entries per
             // drain chunk, chunk j on wave j % NW; the queue stores of other waves are ordered before the loads
             // by the workgroup-scope release / acquire of the barrier (one CU, one L1)
-            if (lane == 0) s_qn[threadIdx.x >> 6] = qn;
+            if (lane == 0) s_qn[tidx >> 6] = qn;
             __syncthreads();
             int pre[NW + 1];
             pre[0] = 0;
 #pragma unroll
             for (int w = 0; w < NW; ++w) pre[w + 1] = pre[w] + s_qn[w];
             const int tot = pre[NW];
-            const int* qb = dq + (long)blockIdx.x * NW * qcap;
-            for (int s0 = (threadIdx.x >> 6) * 64; s0 < tot; s0 += NW * 64) {
+            const int* qb = dq + (long)bidx * NW * qcap;
+            for (int s0 = (tidx >> 6) * 64; s0 < tot; s0 += NW * 64) {
                 const int g = s0 + lane;
                 const bool act = g < tot;
                 int w = 0;
@@ -921,9 +951,9 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
         // without a valid depth ride along as invisible lanes (~10 % at level 0).  Projection, lean terms and the
         // workgroup drain as PF 5.
         const int npx = nRows * nCols;
-        const int lane = threadIdx.x & 63;
+        const int lane = tidx & 63;
         const int qcap = ((npx + stride - 1) / stride) * 64;
-        int* q = dq + ((long)blockIdx.x * NW + (threadIdx.x >> 6)) * qcap;
+        int* q = dq + ((long)bidx * NW + (tidx >> 6)) * qcap;
         int qn = 0;
         const uint32_t* __restrict__ spk = J.spk;
         const auto rs_s = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(spk), 0, npx * 4, 0x00020000);
@@ -996,8 +1026,8 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
             }
         };
         const int nbx = (int)gridDim.x;   // XCD-aware stream order (as PF 4 / 5)
-        const int bx = (nbx & 7) ? (int)blockIdx.x : ((int)blockIdx.x & 7) * (nbx >> 3) + ((int)blockIdx.x >> 3);
-        const int b0 = __builtin_amdgcn_readfirstlane((bx * TPB + (threadIdx.x & ~63)));
+        const int bx = (nbx & 7) ? (int)bidx : ((int)bidx & 7) * (nbx >> 3) + ((int)bidx >> 3);
+        const int b0 = __builtin_amdgcn_readfirstlane((bx * TPB + (tidx & ~63)));
 #ifdef R360_EXP_NOLOOP   // experiment builds only: the pass without its pixel loop (fixed costs)
         if (false) {
 #else
@@ -1033,15 +1063,15 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
             }
         }
         // the workgroup's deferred lanes, drained together (as PF 5)
-        if (lane == 0) s_qn[threadIdx.x >> 6] = qn;
+        if (lane == 0) s_qn[tidx >> 6] = qn;
         __syncthreads();
         int pre[NW + 1];
         pre[0] = 0;
 #pragma unroll
         for (int w = 0; w < NW; ++w) pre[w + 1] = pre[w] + s_qn[w];
         const int tot = pre[NW];
-        const int* qb = dq + (long)blockIdx.x * NW * qcap;
-        for (int s0 = (threadIdx.x >> 6) * 64; s0 < tot; s0 += NW * 64) {
+        const int* qb = dq + (long)bidx * NW * qcap;
+        for (int s0 = (tidx >> 6) * 64; s0 < tot; s0 += NW * 64) {
             const int g = s0 + lane;
             const bool act = g < tot;
             int w = 0;
@@ -1068,9 +1098,9 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
         // without a valid depth ride along as invisible lanes (~10 % at level 0).  Projection, lean terms and the
         // workgroup drain as PF 5.
         const int npx = nRows * nCols;
-        const int lane = threadIdx.x & 63;
+        const int lane = tidx & 63;
         const int qcap = ((npx + stride - 1) / stride) * 64;
-        int* q = dq + ((long)blockIdx.x * NW + (threadIdx.x >> 6)) * qcap;
+        int* q = dq + ((long)bidx * NW + (tidx >> 6)) * qcap;
         int qn = 0;
         const uint32_t* __restrict__ spk = J.spk;
         const auto rs_s = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(spk), 0, npx * 4, 0x00020000);
@@ -1127,8 +1157,8 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
             }
         };
         const int nbx = (int)gridDim.x;   // XCD-aware stream order (as PF 4 / 5)
-        const int bx = (nbx & 7) ? (int)blockIdx.x : ((int)blockIdx.x & 7) * (nbx >> 3) + ((int)blockIdx.x >> 3);
-        const int b0 = __builtin_amdgcn_readfirstlane((bx * TPB + (threadIdx.x & ~63)));
+        const int bx = (nbx & 7) ? (int)bidx : ((int)bidx & 7) * (nbx >> 3) + ((int)bidx >> 3);
+        const int b0 = __builtin_amdgcn_readfirstlane((bx * TPB + (tidx & ~63)));
         if (b0 < npx) {
             // three-step pipeline over chunk slots 0..2 (chunk h in slot h % 3, source slot (h + 1) % 3 refilled
             // with chunk h + 4): each step loads the source of chunk h + 4, projects chunk h + 2 (its source
@@ -1179,15 +1209,15 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
             }
         }
         // the workgroup's deferred lanes, drained together (as PF 5)
-        if (lane == 0) s_qn[threadIdx.x >> 6] = qn;
+        if (lane == 0) s_qn[tidx >> 6] = qn;
         __syncthreads();
         int pre[NW + 1];
         pre[0] = 0;
 #pragma unroll
         for (int w = 0; w < NW; ++w) pre[w + 1] = pre[w] + s_qn[w];
         const int tot = pre[NW];
-        const int* qb = dq + (long)blockIdx.x * NW * qcap;
-        for (int s0 = (threadIdx.x >> 6) * 64; s0 < tot; s0 += NW * 64) {
+        const int* qb = dq + (long)bidx * NW * qcap;
+        for (int s0 = (tidx >> 6) * 64; s0 < tot; s0 += NW * 64) {
             const int g = s0 + lane;
             const bool act = g < tot;
             int w = 0;
@@ -1205,7 +1235,7 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
     } else {
         // small levels: one pixel per thread, so the latency chain per thread is a quarter as long
         const int npx = nRows * nCols;
-        for (int i = blockIdx.x * TPB + threadIdx.x; i < npx; i += stride) {
+        for (int i = bidx * TPB + tidx; i < npx; i += stride) {
             const int r = i / nCols;
             const int c = i - r * nCols;
             const float2 a = src[i];
@@ -1214,14 +1244,14 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
     }
 #ifdef R360_STAMPS
     const unsigned long long t_loop = __builtin_amdgcn_s_memrealtime();
-    if (threadIdx.x == 0) {   // earliest block start / latest loop end over the grid
-        if (blockIdx.x < 8192) {
-            g_blk_stamps[0][blockIdx.x] = t_start;
-            g_blk_stamps[1][blockIdx.x] = t_loop;
+    if (tidx == 0) {   // earliest block start / latest loop end over the grid
+        if (bidx < 8192) {
+            g_blk_stamps[0][bidx] = t_start;
+            g_blk_stamps[1][bidx] = t_loop;
             unsigned hw, xcc;
             asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
             asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-            g_blk_stamps[2][blockIdx.x] = ((unsigned long long)xcc << 32) | hw;
+            g_blk_stamps[2][bidx] = ((unsigned long long)xcc << 32) | hw;
         }
         // no grid-wide min / max here: 2 x 512 same-address atomics at the loop end serialised for ~10 us when
         // every workgroup finishes at once (coarse levels) and showed up as a ticket delay; the host takes
@@ -1230,12 +1260,12 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
 #endif
 
     // ---- stage 1: wave butterfly (f32) -> LDS -> per-workgroup fp64 record
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int lane = tidx & 63, wid = tidx >> 6;
     if (PF >= 3 && lane == 0) { A.h[27] += (float)W.c27; A.h[28] += (float)W.c28; A.h[29] += (float)W.c29; }
     if (PF >= 5) A.err2 = (double)errf;
 #ifdef R360_EXP_NOEPI   // experiment builds only
     if (A.h[0] == 1.2345f) S->dbg[7] = 1;
-    return;
+    return PASS_ARRIVED;
 #endif
 #ifdef R360_EXP_NOBFLY   // experiment builds only
     const float mine = A.h[lane & 31];
@@ -1250,24 +1280,25 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
     __syncthreads();
 #ifdef R360_EXP_NOREC   // experiment builds only: no record, no ticket
     if (s_red[0][0] == 1.2345f) S->dbg[7] = 1;
-    return;
+    return PASS_ARRIVED;
 #endif
-    if (threadIdx.x < 32) {
+    if (tidx < 32) {
         double v;
-        if (threadIdx.x == R360_SUM_ERR2) {
+        if (tidx == R360_SUM_ERR2) {
             v = 0; for (int w = 0; w < NW; ++w) v += s_err[w];
-        } else if (OCC && threadIdx.x == R360_SUM_ERR2D) {
+        } else if (OCC && tidx == R360_SUM_ERR2D) {
             v = 0; for (int w = 0; w < NW; ++w) v += s_errd[w];
         } else {
-            v = 0; for (int w = 0; w < NW; ++w) v += (double)s_red[w][threadIdx.x];
+            v = 0; for (int w = 0; w < NW; ++w) v += (double)s_red[w][tidx];
         }
         // write-through (sc1) store: visible at agent scope without an L2 write-back fence
-        __hip_atomic_store(reinterpret_cast<unsigned long long*>(partials) + (long)blockIdx.x * 32 + threadIdx.x,
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(partials) + (long)bidx * 32 + tidx,
                            (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
 #if R360_POLL
+#define R360_KPRE nullptr
     // ---- stage 2: record flags; the job's last workgroup polls them, reduces all records and runs the GN step
     // Every workgroup but the last stores this launch's sequence number (C.seq, unique per launch on the ctx)
     // into its own flag word once its record is drained (the sc1 record stores and the barrier as below); the
@@ -1277,12 +1308,12 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
     // workgroups all finish within a microsecond, and their ticket took ~12 us of the pass; profiles/r3_lone).
     {
         const int nb = (int)gridDim.x;
-        if ((int)blockIdx.x != nb - 1) {
-            if (threadIdx.x == 0)
-                __hip_atomic_store(gcnt + blockIdx.x, C.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return;
+        if ((int)bidx != nb - 1) {
+            if (tidx == 0)
+                __hip_atomic_store(gcnt + bidx, C.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return PASS_ARRIVED;
         }
-        for (int b = threadIdx.x; b < nb - 1; b += TPB)
+        for (int b = tidx; b < nb - 1; b += TPB)
             while (__hip_atomic_load(gcnt + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != C.seq)
                 __builtin_amdgcn_s_sleep(1);
         __syncthreads();
@@ -1305,18 +1336,39 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
     // batch; one load round on the last group's path instead of four (512 records, 8 in flight per lane).
     const int nb = (int)gridDim.x;
     const int ng = nb < R360_TICKET_GROUPS ? nb : R360_TICKET_GROUPS;
-    if (threadIdx.x == 0) {
-        const int g = (int)blockIdx.x % R360_TICKET_GROUPS;
+    if (tidx == 0) {
+        const int g = (int)bidx % R360_TICKET_GROUPS;
         const unsigned gsz = (unsigned)((nb - g + R360_TICKET_GROUPS - 1) / R360_TICKET_GROUPS);
         const unsigned prev = __hip_atomic_fetch_add(gcnt + g * R360_TICKET_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_last = prev == gsz - 1;
     }
     __syncthreads();
-    if (!s_last) return;
+    if (!s_last) return PASS_ARRIVED;
+    // The GN state, loaded by every group's last workgroup along with its group records: the step's workgroup then
+    // has it in registers when it wins the pass ticket (the load after the ticket was ~1.2 us of every pass,
+    // profiles/r4_gn).  Nothing writes the state during the pass but the ticket word, which the step resets.
+    constexpr int NQ = (int)(sizeof(IcpState) / 16);
+    static_assert(NQ <= TPB, "one 16-B word of the state per thread");
+    uint4 st_q = {0u, 0u, 0u, 0u};
+    if (!eval_only && (int)tidx < NQ) {   // sc1: a persistent launch's previous pass wrote it on another CU
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(__builtin_amdgcn_make_buffer_rsrc(S, 0, (int)sizeof(IcpState),
+                                                                                               0x00020000),
+                                                             (int)tidx * 16, 0, 16);
+        st_q = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+    unsigned long long kpre[4] = {0ull, 0ull, 0ull, 0ull};   // the span words pass_arrive updates
+    if (tidx == 0) {
+        const int lv = C.level & 7;
+        kpre[0] = __hip_atomic_load(kt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        kpre[1] = __hip_atomic_load(kt + 1 + lv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        kpre[2] = __hip_atomic_load(kt + 9 + lv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        kpre[3] = __hip_atomic_load(kt + 18 + lv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#define R360_KPRE kpre
     {
-        const int g = (int)blockIdx.x % R360_TICKET_GROUPS;
+        const int g = (int)bidx % R360_TICKET_GROUPS;
         const int gsz = (nb - g + R360_TICKET_GROUPS - 1) / R360_TICKET_GROUPS;
-        const int q = threadIdx.x & 15, sj = threadIdx.x >> 4;
+        const int q = tidx & 15, sj = tidx >> 4;
         const auto rs = __builtin_amdgcn_make_buffer_rsrc(partials, 0, (nb + R360_TICKET_GROUPS) * 256, 0x00020000);
         double a0 = 0.0, a1 = 0.0;
         for (int j = sj; j < gsz; j += 2 * RG) {
@@ -1333,28 +1385,29 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
         s_fin[sj][2 * q] = a0;
         s_fin[sj][2 * q + 1] = a1;
         __syncthreads();
-        if (threadIdx.x < 32) {
+        if (tidx < 32) {
             double t = 0.0;
-            for (int k = 0; k < RG; ++k) t += s_fin[k][threadIdx.x];
-            __hip_atomic_store(reinterpret_cast<unsigned long long*>(partials) + (long)(nb + g) * 32 + threadIdx.x,
+            for (int k = 0; k < RG; ++k) t += s_fin[k][tidx];
+            __hip_atomic_store(reinterpret_cast<unsigned long long*>(partials) + (long)(nb + g) * 32 + tidx,
                                (unsigned long long)__double_as_longlong(t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         __syncthreads();
     }
-    if (threadIdx.x == 0) {
+    if (tidx == 0) {
         const unsigned p2 = __hip_atomic_fetch_add(&S->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_last = p2 == (unsigned)ng - 1;
     }
     __syncthreads();
-    if (!s_last) return;
-    if (threadIdx.x < R360_TICKET_GROUPS)   // every group is complete: reset its counter for the next pass
-        __hip_atomic_store(gcnt + threadIdx.x * R360_TICKET_STRIDE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!s_last) return PASS_ARRIVED;
+    if (tidx < R360_TICKET_GROUPS)   // every group is complete: reset its counter for the next pass
+        __hip_atomic_store(gcnt + tidx * R360_TICKET_STRIDE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #else
-    if (threadIdx.x == 0) {
+#define R360_KPRE nullptr
+    if (tidx == 0) {
         const int nb = (int)gridDim.x;
         const int ng = nb < R360_TICKET_GROUPS ? nb : R360_TICKET_GROUPS;
-        const int g = (int)blockIdx.x % R360_TICKET_GROUPS;
+        const int g = (int)bidx % R360_TICKET_GROUPS;
         const unsigned gsz = (unsigned)((nb - g + R360_TICKET_GROUPS - 1) / R360_TICKET_GROUPS);
         const unsigned prev = __hip_atomic_fetch_add(gcnt + g * R360_TICKET_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         int last = 0;
@@ -1365,17 +1418,17 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
         s_last = last;
     }
     __syncthreads();
-    if (!s_last) return;
-    if (threadIdx.x < R360_TICKET_GROUPS)   // every group is complete: reset its counter for the next pass
-        __hip_atomic_store(gcnt + threadIdx.x * R360_TICKET_STRIDE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!s_last) return PASS_ARRIVED;
+    if (tidx < R360_TICKET_GROUPS)   // every group is complete: reset its counter for the next pass
+        __hip_atomic_store(gcnt + tidx * R360_TICKET_STRIDE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #endif
 #endif
 #ifdef R360_STAMPS
     const unsigned long long t_ticket = __builtin_amdgcn_s_memrealtime();
 #endif
 #if !R360_POLL && R360_GROUP_SUM
-    if (threadIdx.x < 16 * R360_TICKET_GROUPS) {   // the group records, 16 B per lane
-        const int q = threadIdx.x & 15, g = threadIdx.x >> 4;
+    if (tidx < 16 * R360_TICKET_GROUPS) {   // the group records, 16 B per lane
+        const int q = tidx & 15, g = tidx >> 4;
         double a0 = 0.0, a1 = 0.0;
         if (g < ng) {
             const auto rs = __builtin_amdgcn_make_buffer_rsrc(partials, 0, (nb + R360_TICKET_GROUPS) * 256, 0x00020000);
@@ -1391,7 +1444,7 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
         // fixed-order reduction of the per-workgroup records: lane q of a 16-lane group loads bytes
         // 16q..16q+15 of records g, g+RG, ... with L1-bypassing (sc1) 16-B buffer loads, 8 in flight;
         // then thread v sums slot v over the groups in order
-        const int q = threadIdx.x & 15, g = threadIdx.x >> 4;
+        const int q = tidx & 15, g = tidx >> 4;
         const int nb = (int)gridDim.x;
         const auto rs = __builtin_amdgcn_make_buffer_rsrc(partials, 0, nb * 256, 0x00020000);
         double a0 = 0.0, a1 = 0.0;
@@ -1413,19 +1466,19 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
     }
 #endif
     __syncthreads();
-    if (threadIdx.x < 32) {
+    if (tidx < 32) {
         double t = 0.0;
-        for (int g = 0; g < RG; ++g) t += s_fin[g][threadIdx.x];
-        s_fin[0][threadIdx.x] = t;
+        for (int g = 0; g < RG; ++g) t += s_fin[g][tidx];
+        s_fin[0][tidx] = t;
     }
     __syncthreads();
 #ifdef R360_STAMPS
     const unsigned long long t_recs = __builtin_amdgcn_s_memrealtime();
 #endif
     if (eval_only) {
-        if (threadIdx.x < 32) S->sums[threadIdx.x] = s_fin[0][threadIdx.x];
+        if (tidx < 32) S->sums[tidx] = s_fin[0][tidx];
 #ifdef R360_STAMPS
-        if (threadIdx.x == 0) {
+        if (tidx == 0) {
             const unsigned long long mn = __hip_atomic_load(&S->dbg[8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const unsigned long long mx = __hip_atomic_load(&S->dbg[9], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             S->dbg[5] = mn; S->dbg[6] = mx; S->dbg[8] = ~0ull; S->dbg[9] = 0;
@@ -1433,20 +1486,24 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
             S->dbg[4] = __builtin_amdgcn_s_memrealtime();
         }
 #endif
-        if (threadIdx.x == 0) {
+        if (tidx == 0) {
             S->ticket = 0;
-            pass_arrive(kt, true, C.level);   // the job's last workgroup
+            pass_arrive(kt, true, C.level, R360_KPRE);   // the job's last workgroup
         }
-        return;
+        return PASS_STEPPED;
     }
     // Stage the whole state in LDS with one coalesced 16-B access per thread, run the step on the LDS copy (one
     // lane walking global memory serialises ~150 dependent accesses, ~35 us), then write it back the same way.
-    constexpr int NQ = (int)(sizeof(IcpState) / 16);
     uint4* sq = reinterpret_cast<uint4*>(&s_state);
-    for (int q = threadIdx.x; q < NQ; q += TPB) sq[q] = reinterpret_cast<const uint4*>(S)[q];
+#if !R360_POLL && R360_GROUP_SUM
+    if ((int)tidx < NQ) sq[tidx] = st_q;   // loaded with the group records
+#else
+    constexpr int NQ = (int)(sizeof(IcpState) / 16);
+    for (int q = tidx; q < NQ; q += TPB) sq[q] = reinterpret_cast<const uint4*>(S)[q];
+#endif
     __syncthreads();
-    gn_step_block(&s_state, s_fin[0], C, first, &s_gn, threadIdx.x);
-    if (threadIdx.x == 0) {
+    gn_step_block(&s_state, s_fin[0], C, first, &s_gn, tidx);
+    if (tidx == 0) {
         s_state.ticket = 0;
 #ifdef R360_STAMPS
         s_state.dbg[5] = s_state.dbg[8]; s_state.dbg[6] = s_state.dbg[9];
@@ -1454,15 +1511,110 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
 #endif
     }
     __syncthreads();
-    for (int q = threadIdx.x; q < NQ; q += TPB) reinterpret_cast<uint4*>(S)[q] = sq[q];
-#ifdef R360_STAMPS
-    if (threadIdx.x == 0) {
+    if constexpr (PERSIST) {
+        // write-through (sc1) stores, drained by every wave before the barrier the hand-off follows; the last
+        // 16 B (the fault word that a timed-out waiter may set) are not written
+        const auto rsS = __builtin_amdgcn_make_buffer_rsrc(S, 0, (int)sizeof(IcpState), 0x00020000);
+        for (int q = tidx; q < NQ - 1; q += TPB) {
+            const uint4 v = sq[q];
+            const u32x4 w = {v.x, v.y, v.z, v.w};
+            __builtin_amdgcn_raw_buffer_store_b128(w, rsS, q * 16, 0, 16);
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
-        S->dbg[0] = t_start; S->dbg[1] = t_loop; S->dbg[2] = t_ticket; S->dbg[3] = t_recs; S->dbg[4] = t_end;
+    } else {
+        for (int q = tidx; q < NQ; q += TPB) reinterpret_cast<uint4*>(S)[q] = sq[q];
+    }
+#ifdef R360_STAMPS
+    if (tidx == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned long long st[5] = {t_start, t_loop, t_ticket, t_recs, __builtin_amdgcn_s_memrealtime()};
+        for (int k = 0; k < 5; ++k) __hip_atomic_store(&S->dbg[k], st[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 #endif
-    if (threadIdx.x == 0) pass_arrive(kt, true, C.level);   // the job's last workgroup
+    if constexpr (PERSIST) __syncthreads();   // every wave's state stores drained before the span and the hand-off
+    if (tidx == 0) pass_arrive(kt, true, C.level, R360_KPRE, PERSIST);   // the job's last workgroup
+#undef R360_KPRE
+    return PASS_STEPPED;
+}
+
+template <int METHOD, int PF, int TOP, int OCC>
+__global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs jobs, const float* __restrict__ sinphi,
+                                                 const float* __restrict__ cosphi, const float* __restrict__ sinth,
+                                                 const float* __restrict__ costh, int nRows, int nCols,
+                                                 IcpConst C, int first, int eval_only,
+                                                 unsigned long long* __restrict__ kt,
+                                                 const uint8_t* __restrict__ occf) {
+    (void)icp_pass_body<METHOD, PF, TOP, OCC, false>(jobs, sinphi, cosphi, sinth, costh, nRows, nCols, C, first,
+                                                     eval_only, kt, occf, (int)threadIdx.x, (int)blockIdx.x);
+}
+
+// ---- persistent level launch (lone alignments, plain pass: PF 6 at level 0, PF 5 above)
+// The level's 1 + maxIters passes in ONE launch on the pass grid of k_icp_pass (same workgroups, same pixel
+// order, same records: the sums and poses are bit for bit those of the per-pass launches).  Between passes the
+// step's workgroup publishes the pass generation (base + k + 1) after its state and span stores have drained;
+// every other workgroup's lane 0 polls it (sc1 loads, s_sleep) and the workgroup joins at a barrier, then
+// reads the new state with sc1 loads.  A level that converged ends the loop in every workgroup at once (they
+// all read the same published state), so no launch is dispatched for its remaining passes (a stopped pass was
+// a full-grid dispatch whose workgroups exit at entry, 29 of a lone pair's 65 launches), and the ~3 us kernel
+// boundary of every pass becomes a one-flag hand-off.  base: the generation word at the launch start (every
+// workgroup reads it before its first arrival, and nothing is published before all have arrived).  Every wait
+// is bounded (R360_PERSIST_SPIN_TICKS): a timed-out waiter sets S->fault and leaves, and so do the others at
+// their next wait, so the grid always drains.  The host launches it only when the grid fits one resident round
+// with a workgroup per CU to spare (icp_level_persist_grid) and no other persistent launch of the process is in
+// flight.
+#ifndef R360_PERSIST_SPIN_TICKS
+#define R360_PERSIST_SPIN_TICKS 50000000ull   // 0.5 s of the 100 MHz s_memrealtime clock
+#endif
+#if R360_POLL || defined(R360_EXP_NOEPI) || defined(R360_EXP_NOREC)
+#define R360_PERSIST_BUILT 0   // these experiment bodies have no step workgroup
+#else
+#define R360_PERSIST_BUILT 1
+#endif
+#ifndef R360_LEVEL_MINB
+#define R360_LEVEL_MINB 3   // waves per SIMD: a lone pass puts 2 workgroups on a CU, so registers are free up to 3
+#endif
+template <int METHOD, int PF, int TOP>
+__global__ __launch_bounds__(TPB, R360_LEVEL_MINB) void k_icp_level(const IcpJobs jobs, const float* __restrict__ sinphi,
+                                                  const float* __restrict__ cosphi, const float* __restrict__ sinth,
+                                                  const float* __restrict__ costh, int nRows, int nCols,
+                                                  IcpConst C, int passes, unsigned long long* __restrict__ kt) {
+    __shared__ int s_go;
+    IcpState* S = jobs.j[0].S;
+    unsigned* gen = jobs.j[0].gcnt + R360_PERSIST_FLAG_WORD;
+    unsigned base = 0;
+    if (threadIdx.x == 0) base = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int k = 0; k < passes; ++k) {
+        // the pass's operands laundered per iteration (empty asm): otherwise the compiler hoists the body's
+        // loop-invariant address and table arithmetic out of the pass loop, and the values it keeps live across
+        // the whole pass spilled to scratch (288 B per lane) and were reloaded inside the pixel loop
+        int tid = (int)threadIdx.x, bid = (int)blockIdx.x, nr = nRows, nc = nCols;
+        const float *sp = sinphi, *cp = cosphi, *st = sinth, *ct = costh;
+        unsigned long long* ktl = kt;
+        asm volatile("" : "+v"(tid));
+        asm volatile("" : "+s"(bid), "+s"(nr), "+s"(nc));
+        asm volatile("" : "+s"(sp), "+s"(cp), "+s"(st), "+s"(ct), "+s"(ktl));
+        const int r = icp_pass_body<METHOD, PF, TOP, 0, true>(jobs, sp, cp, st, ct, nr, nc, C, k == 0 ? 1 : 0, 0, ktl,
+                                                              nullptr, tid, bid);
+        if (r == PASS_SKIPPED || k + 1 == passes) break;   // stopped (uniform), or the level's last pass
+        if (threadIdx.x == 0) {
+            const unsigned tag = base + (unsigned)k + 1u;
+            int go = 1;
+            if (r == PASS_STEPPED) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(gen, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tag) {
+                    __builtin_amdgcn_s_sleep(2);
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > R360_PERSIST_SPIN_TICKS) { go = 0; break; }
+                }
+                if (!go) __hip_atomic_store(&S->fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            s_go = go;
+        }
+        __syncthreads();
+        if (!s_go) break;
+    }
 }
 
 // ---------------------------------------------------------------- occlusion variants (§8(f)1)
@@ -2018,6 +2170,76 @@ int launch_icp_jobs(r360_ctx* ctx, const IcpJobs& jobs, int n, const r360_frame*
         return -1;
     }
     return launch_jobs(ctx, jobs, n, Ls, geom->calib->trig[level], level, method, C, first, eval_only, G);
+}
+
+// ---- persistent level launch (k_icp_level): resident-round check and launch
+template <int M, int PF, int TOP>
+static int level_blocks_per_cu() {   // the occupancy query for the instantiation (one device model per process)
+    static const int n = [] {
+        int b = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_icp_level<M, PF, TOP>, TPB, 0) != hipSuccess) b = 0;
+        return b;
+    }();
+    return n;
+}
+
+static int level_blocks_per_cu(int method, int pf) {
+    auto by = [&](auto m) {
+        constexpr int M = decltype(m)::value;
+        return pf == 6 ? level_blocks_per_cu<M, 6, 1>() : level_blocks_per_cu<M, 5, 0>();
+    };
+    if (method == R360_PHOTO_CONSISTENCY) return by(std::integral_constant<int, R360_PHOTO_CONSISTENCY>{});
+    if (method == R360_DEPTH_CONSISTENCY) return by(std::integral_constant<int, R360_DEPTH_CONSISTENCY>{});
+    return by(std::integral_constant<int, R360_PHOTO_DEPTH>{});
+}
+
+bool icp_level_persist_ok(r360_ctx* ctx, const r360_frame* src, int level, int method) {
+    if (!R360_PERSIST_BUILT) return false;
+    const LevelBufs& Ls = src->lv[level];
+    const PassGrid G = pass_grid(ctx, Ls, 0);
+    if (G.pf != 5 && G.pf != 6) return false;   // the product forms of the plain pass
+    if (G.pf >= 3 && ctx->defer_cap < defer_need(Ls.rows * Ls.cols, G.nb)) return false;
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return false;
+    // the occupancy answer can be one workgroup per CU high (MI355X_MICROARCH.md, residency): keep one spare
+    const int per_cu = level_blocks_per_cu(method, G.pf);
+    return per_cu >= 2 && G.nb <= (per_cu - 1) * cus;
+}
+
+int launch_icp_level_persist(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src, int level, int method,
+                             const IcpConst& C0, int passes) {
+    const LevelBufs& Ls = src->lv[level];
+    const LevelBufs& Lt = trg->lv[level];
+    const LevelTrig& T = src->calib->trig[level];
+    const PassGrid G = pass_grid(ctx, Ls, 0);
+    if (C0.occ || (G.pf != 5 && G.pf != 6) || !R360_PERSIST_BUILT) {
+        r360_set_error("persistent level launch: plain pass forms only");
+        return -1;
+    }
+    IcpJobs jobs;
+    IcpJob& J = jobs.j[0];
+    J.src = Ls.p0; J.trg = Lt.p0; J.tg = Lt.tg; J.pts = Ls.pts; J.npts = src->d_npts + level;
+    J.spk = Ls.pk; J.tpk = Lt.pk;
+    J.S = ctx->d_state; J.partials = ctx->d_partials; J.gcnt = ctx->d_gticket; J.dq = ctx->d_defer;
+    IcpConst C = C0;
+    if (++ctx->icp_seq == 0) ++ctx->icp_seq;
+    C.seq = ctx->icp_seq;
+    const int slot = timing_begin(ctx, level == 0 ? "k_icp_level_L0" : "k_icp_level");
+    void (*kern)(const IcpJobs, const float*, const float*, const float*, const float*, int, int, IcpConst, int,
+                 unsigned long long*) = nullptr;
+    auto pick = [&](auto m) {
+        constexpr int M = decltype(m)::value;
+        kern = G.pf == 6 ? k_icp_level<M, 6, 1> : k_icp_level<M, 5, 0>;
+    };
+    if (method == R360_PHOTO_CONSISTENCY) pick(std::integral_constant<int, R360_PHOTO_CONSISTENCY>{});
+    else if (method == R360_DEPTH_CONSISTENCY) pick(std::integral_constant<int, R360_DEPTH_CONSISTENCY>{});
+    else pick(std::integral_constant<int, R360_PHOTO_DEPTH>{});
+    hipLaunchKernelGGL(kern, dim3(G.nb, 1), dim3(TPB), 0, ctx->stream, jobs, T.sinphi, T.cosphi, T.sinth, T.costh,
+                       Ls.rows, Ls.cols, C, passes, ctx->d_ktime);
+    timing_end(ctx, slot);
+    R360_HIP(hipGetLastError());
+    return 0;
 }
 
 int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src, int level, int method,

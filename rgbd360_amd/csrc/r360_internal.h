@@ -125,6 +125,10 @@ struct alignas(16) IcpState {
     int av_set;         // bit 0 photo/depth of the last pass assigned, bit 1 av_res assigned, bits 2/3 the copies
     double sums[32];    // last pass sums (eval mode)
     unsigned long long dbg[12];  // s_memrealtime stamps of the diagnostic build (-DR360_STAMPS)
+    // last 16 B, never written back by a persistent level launch's step: set by a workgroup whose wait for a
+    // pass's step timed out (the launch then ends and the alignment reports an error)
+    int fault;
+    int pad4[3];
 };
 
 // One alignment of a batched ICP launch (blockIdx.y = job): the pair's level buffers and its own GN state,
@@ -157,6 +161,9 @@ constexpr int R360_KT_SLOTS = 26;
 #endif
 constexpr int R360_TICKET_GROUPS = R360_TICKET_GROUPS_N;
 constexpr int R360_TICKET_STRIDE = 16384 / R360_TICKET_GROUPS_N;   // uints between group counters (4 KB at 16)
+// the persistent level launch's pass generation word: the last of the 16384 counter words, never a group counter
+constexpr int R360_PERSIST_FLAG_WORD = 16383;
+static_assert(R360_TICKET_STRIDE > 1, "the generation word must not be a group counter");
 
 // Pass sums.  Occlusion variants: NVALID counts photo terms (Occ1) or accepted points (Occ2), NDEPTH
 // the depth terms (Occ1), ERR2 the photometric and ERR2D the depth squared residuals.
@@ -304,6 +311,8 @@ struct r360_ctx {
     unsigned long long graph_clock = 0;
     IcpState* h_state = nullptr;  // pinned
     int timing = 0;
+    int persist_held = 0;
+    int async_persist = 0;  // the pending r360_align360 runs as persistent level launches   // this ctx holds the process's persistent-launch slot (runtime.cpp, persist_slot)
     std::vector<hipEvent_t> ev_pool;
     int ev_used = 0;
     struct TimedLaunch { std::string name; int a, b; };
@@ -459,6 +468,12 @@ int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src
 int launch_icp_jobs(r360_ctx* ctx, const IcpJobs& jobs, int n, const r360_frame* geom, int level, int method,
                     const IcpConst& C, int first, int eval_only);
 int icp_blocks_for(int n_pixels);
+// The persistent level launch (k_icp_level): all `passes` passes of a plain (C.occ == 0) lone alignment's level in
+// one launch.  icp_level_persist_ok: whether level's pass grid fits one resident round of that kernel with a
+// workgroup per CU to spare (and the build has it); launch_icp_level_persist enqueues it.
+bool icp_level_persist_ok(r360_ctx* ctx, const r360_frame* src, int level, int method);
+int launch_icp_level_persist(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src, int level, int method,
+                             const IcpConst& C, int passes);
 // sizes ctx->d_defer for passes over up to n_pixels pixels (synchronises the ctx stream when it grows,
 // so it never frees a queue an enqueued pass still uses); call before enqueuing a level sequence
 int ensure_defer(r360_ctx* ctx, long n_pixels);

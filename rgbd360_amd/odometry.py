@@ -233,22 +233,22 @@ class SequenceRunner:
             rec[R_ERR] = st.error
 
         nbuf = len(fr)
-        L = self.lookahead
-        depth = nbuf - L - 2
-        for j in range(a, min(a + L, b + 1)):   # frames a .. a+L-1 built, frame a+L uploaded
+        LA = self.lookahead
+        depth = nbuf - LA - 2
+        for j in range(a, min(a + LA, b + 1)):   # frames a .. a+LA-1 built, frame a+LA uploaded
             load(fr[(j - a) % nbuf], j)
             fr[(j - a) % nbuf].build(self.flags, sync=False)
-        if a + L <= b:
-            load(fr[L % nbuf], a + L)
+        if a + LA <= b:
+            load(fr[LA % nbuf], a + LA)
         pending = []
         sts = [IcpStats() for _ in range(depth + 1)]
         for i in range(a, b):
             t0 = time.perf_counter()
             cur, nxt = fr[(i - a) % nbuf], fr[(i + 1 - a) % nbuf]
-            if i + L <= b:
-                fr[(i + L - a) % nbuf].build(self.flags, sync=False)   # its upload was issued one iteration earlier
-            if i + L + 1 <= b:
-                load(fr[(i + L + 1 - a) % nbuf], i + L + 1)
+            if i + LA <= b:
+                fr[(i + LA - a) % nbuf].build(self.flags, sync=False)   # its upload was issued one iteration earlier
+            if i + LA + 1 <= b:
+                load(fr[(i + LA + 1 - a) % nbuf], i + LA + 1)
             t1 = time.perf_counter()
             ticket = C.c_long()
             if self.dense_only:

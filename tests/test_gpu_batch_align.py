@@ -151,3 +151,49 @@ def test_batched_alignment_is_deterministic(seq):
     for j in range(len(pairs)):
         assert np.array_equal(pa[j], pb[j]) and np.array_equal(Ha[j], Hb[j]) and np.array_equal(ga[j], gb[j]), j
         _same(sa[j], sb[j])
+
+
+def _same_outputs(a, b):
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
+    _same(a[3], b[3])
+    assert a[4] == b[4]
+
+
+@pytest.mark.parametrize("iters0", [20, 0])
+def test_persistent_equals_per_pass(seq, iters0):
+    """r360_align360 runs each level as ONE persistent launch (k_icp_level) when its pass grid fits a resident
+    round; with per-launch timing on it launches one kernel per pass.  Same grid, same records, same steps:
+    bit-identical outputs, under the fixed and the reference (converging) schedules."""
+    fr = seq["frames"]
+    a, b = R.Context(0), R.Context(0)
+    b.timing(True)
+    for t, s in [(fr[0], fr[1]), (fr[2], fr[5]), (fr[0], seq["other"])]:
+        ra = _single(a, t, s, None, _params(iters0))
+        rb = _single(b, t, s, None, _params(iters0))
+        assert ra[3].persistent == 1 and rb[3].persistent == 0
+        _same_outputs(ra, rb)
+    a.close()
+    b.close()
+
+
+def test_persistent_slot(seq):
+    """One persistent alignment in flight per process: a second context enqueuing meanwhile launches per pass
+    (and gets the same result); the slot is free again once the first result is read."""
+    fr = seq["frames"]
+    p = _params(20)
+    a, b = R.Context(0), R.Context(0)
+    init = np.eye(4, dtype=np.float32).T.copy().reshape(-1)
+    fp = lambda x: x.ctypes.data_as(R.C.POINTER(R.C.c_float))
+    assert R.lib().r360_align360_async(a.h, fr[3].h, fr[4].h, fp(init), R.PHOTO_DEPTH, 0, R.C.byref(p)) == 0
+    rb = _single(b, fr[3], fr[4], None, _params(20))
+    po, Ho, go = np.zeros(16, np.float32), np.zeros(36, np.float32), np.zeros(6, np.float32)
+    st = R.IcpStats()
+    rc = R.lib().r360_align360_result(a.h, fp(po), fp(Ho), fp(go), R.C.byref(st))
+    assert st.persistent == 1 and rb[3].persistent == 0
+    assert np.array_equal(po.reshape(4, 4).T, rb[0]) and rc == rb[4]
+    _same(st, rb[3])
+    rc2 = _single(b, fr[3], fr[4], None, _params(20))
+    assert rc2[3].persistent == 1
+    _same_outputs(rb, rc2)
+    a.close()
+    b.close()
