@@ -23,6 +23,23 @@ int align360_batch_enqueue(r360_ctx* ctx, int n, r360_frame* const* trg, r360_fr
 
 struct r360_dense_queue {
     r360_ctx* ctx = nullptr;           // the queue's own stream, GN states and batch buffers
+    // Batches in flight: up to n_ctx at once, batch k on cx[k % n_ctx]'s stream.  The dispatcher enqueues a batch
+    // as soon as jobs are pending and a stream is free; the collector thread reads results in batch order.  With
+    // one stream the next batch could only be enqueued after the previous one's result was read (a host round
+    // trip plus ~65 launches' enqueue per batch with the dense stream idle), and every pass's tail (ticket, GN step)
+    // left the GPU to the other streams alone.
+    r360_ctx* cx[2] = {nullptr, nullptr};
+    int n_ctx = 1;
+    bool busy[2] = {false, false};
+    struct Inflight {
+        int slot = 0, n = 0, rc = 0;
+        std::vector<long> take;
+        std::string err;
+    };
+    std::deque<Inflight> inflight;
+    bool dispatch_done = false;
+    std::thread collector;
+    std::condition_variable cv_flight;
     int max_batch = R360_MAX_BATCH;
     std::mutex m;
     std::condition_variable cv_work, cv_done;
@@ -60,14 +77,19 @@ static bool same_params(const r360_dense_queue::Job& a, const r360_dense_queue::
            a.src->n_levels == b.src->n_levels && a.trg->n_levels == b.trg->n_levels;
 }
 
+static int free_slot(const r360_dense_queue* q) {
+    for (int k = 0; k < q->n_ctx; ++k)
+        if (!q->busy[k]) return k;
+    return -1;
+}
+
 static void dispatcher(r360_dense_queue* q) {
     (void)hipSetDevice(q->ctx->device);
-    std::vector<long> take;
     std::vector<r360_frame*> trg, src;
     std::vector<float> init;
     for (;;) {
         std::unique_lock<std::mutex> lk(q->m);
-        q->cv_work.wait(lk, [&] { return q->quit || !q->pending.empty(); });
+        q->cv_work.wait(lk, [&] { return (!q->pending.empty() && free_slot(q) >= 0) || (q->quit && q->pending.empty()); });
         if (q->pending.empty()) break;   // quit with nothing pending
         // optional batch floor (R360_QUEUE_MIN jobs, waiting at most R360_QUEUE_WAIT_US): larger batches fill the
         // level-0 pass better at the cost of latency (experiment knob, off by default)
@@ -76,40 +98,74 @@ static void dispatcher(r360_dense_queue* q) {
         if (min_jobs > 1 && (int)q->pending.size() < min_jobs)
             q->cv_work.wait_for(lk, std::chrono::microseconds(wait_us),
                                 [&] { return q->quit || (int)q->pending.size() >= min_jobs; });
-        take.clear();
+        r360_dense_queue::Inflight b;
+        b.slot = free_slot(q);
+        q->busy[b.slot] = true;
         const r360_dense_queue::Job& first = q->jobs[q->pending.front()];
-        for (auto it = q->pending.begin(); it != q->pending.end() && (int)take.size() < q->max_batch;) {
-            if (same_params(q->jobs[*it], first)) { take.push_back(*it); it = q->pending.erase(it); }
+        for (auto it = q->pending.begin(); it != q->pending.end() && (int)b.take.size() < q->max_batch;) {
+            if (same_params(q->jobs[*it], first)) { b.take.push_back(*it); it = q->pending.erase(it); }
             else ++it;
         }
-        const int n = (int)take.size();
+        const int n = (int)b.take.size();
+        b.n = n;
         trg.resize(n); src.resize(n); init.resize(16 * (size_t)n);
         for (int j = 0; j < n; ++j) {
-            r360_dense_queue::Job& J = q->jobs[take[j]];
+            r360_dense_queue::Job& J = q->jobs[b.take[j]];
             trg[j] = J.trg; src[j] = J.src;
             memcpy(init.data() + 16 * j, J.init, sizeof J.init);
         }
         const int method = first.method;
         const r360_icp_params p = first.p;
         std::vector<hipEvent_t> evs;
-        for (long t : take) {
+        for (long t : b.take) {
             const r360_dense_queue::Job& J = q->jobs[t];
             for (int e = 0; e < J.nev; ++e) evs.push_back(J.ev[e]);
         }
         lk.unlock();
 
+        r360_ctx* c = q->cx[b.slot];
         int rc = 0;
         for (hipEvent_t e : evs)
-            if (hipStreamWaitEvent(q->ctx->stream, e, 0) != hipSuccess) { r360_set_error("hipStreamWaitEvent failed"); rc = -1; }
-        if (rc == 0) rc = align360_batch_enqueue(q->ctx, n, trg.data(), src.data(), init.data(), method, &p, false);
+            if (hipStreamWaitEvent(c->stream, e, 0) != hipSuccess) { r360_set_error("hipStreamWaitEvent failed"); rc = -1; }
+        if (rc == 0) rc = align360_batch_enqueue(c, n, trg.data(), src.data(), init.data(), method, &p, false);
+        b.rc = rc;
+        if (rc < 0) b.err = r360_last_error();
+
+        lk.lock();
+        q->inflight.push_back(std::move(b));
+        lk.unlock();
+        q->cv_flight.notify_one();
+    }
+    {
+        std::lock_guard<std::mutex> lk(q->m);
+        q->dispatch_done = true;
+    }
+    q->cv_flight.notify_one();
+}
+
+// Reads the batches' results in enqueue order and hands them to the waiting collectors.
+static void collector(r360_dense_queue* q) {
+    (void)hipSetDevice(q->ctx->device);
+    for (;;) {
+        std::unique_lock<std::mutex> lk(q->m);
+        q->cv_flight.wait(lk, [&] { return q->dispatch_done || !q->inflight.empty(); });
+        if (q->inflight.empty()) break;   // dispatcher gone, nothing left
+        r360_dense_queue::Inflight b = q->inflight.front();
+        lk.unlock();
+
+        const int n = b.n;
         std::vector<float> po(16 * (size_t)n), Ho(36 * (size_t)n), go(6 * (size_t)n);
         std::vector<r360_icp_stats> st(n);
-        if (rc == 0) rc = r360_align360_batch_result(q->ctx, po.data(), Ho.data(), go.data(), st.data());
-        const std::string err = rc < 0 ? r360_last_error() : "";
+        int rc = b.rc;
+        std::string err = b.err;
+        if (rc == 0) {
+            rc = r360_align360_batch_result(q->cx[b.slot], po.data(), Ho.data(), go.data(), st.data());
+            if (rc < 0) err = r360_last_error();
+        }
 
         lk.lock();
         for (int j = 0; j < n; ++j) {
-            r360_dense_queue::Job& J = q->jobs[take[j]];
+            r360_dense_queue::Job& J = q->jobs[b.take[j]];
             if (rc < 0) { J.rc = rc; J.err = err; }
             else {
                 memcpy(J.pose, po.data() + 16 * j, sizeof J.pose);
@@ -125,8 +181,11 @@ static void dispatcher(r360_dense_queue* q) {
         q->batches++;
         q->batched += n;
         if (n > q->max_seen) q->max_seen = n;
+        q->inflight.pop_front();
+        q->busy[b.slot] = false;
         lk.unlock();
         q->cv_done.notify_all();
+        q->cv_work.notify_one();
     }
 }
 
@@ -157,8 +216,24 @@ extern "C" int r360_dense_queue_create(int device, int max_batch, r360_dense_que
     }
     auto* q = new r360_dense_queue;
     q->ctx = ctx;
+    q->cx[0] = ctx;
+    // one batch stream; R360_QUEUE_STREAMS=2 (experiment builds) alternates batches over two: measured slower
+    // (1206-1227 vs 1263 pairs/s, profiles/r4_queue): the batches halve (4.1 vs 7.7 pairs per launch)
+    static const int streams = R360_KNOB("R360_QUEUE_STREAMS", 1);
+    if (streams >= 2) {
+        r360_ctx* c2 = nullptr;
+        if (int rc = r360_ctx_create(device, &c2)) {
+            r360_ctx_destroy(ctx);
+            delete q;
+            return rc;
+        }
+        q->cx[1] = c2;
+        q->n_ctx = 2;
+        ctx->stats_sibling = c2;   // kernel statistics of the queue ctx cover both streams
+    }
     q->max_batch = max_batch;
     q->worker = std::thread(dispatcher, q);
+    q->collector = std::thread(collector, q);
     *out = q;
     return 0;
 }
@@ -171,10 +246,13 @@ extern "C" void r360_dense_queue_destroy(r360_dense_queue* q) {
     }
     q->cv_work.notify_all();
     q->worker.join();
+    q->collector.join();
     (void)hipSetDevice(q->ctx->device);
     for (auto& kv : q->jobs)
         for (int e = 0; e < kv.second.nev; ++e) hipEventDestroy(kv.second.ev[e]);
     for (hipEvent_t e : q->ev_free) hipEventDestroy(e);
+    q->ctx->stats_sibling = nullptr;
+    if (q->cx[1]) r360_ctx_destroy(q->cx[1]);
     r360_ctx_destroy(q->ctx);
     delete q;
 }

@@ -223,12 +223,17 @@ extern "C" void r360_ctx_destroy(r360_ctx* c) {
 
 extern "C" int r360_ctx_kernel_stats(r360_ctx* ctx, int level, double* us_sum, long* launches, long* job_passes) {
     CHECK_ARG(ctx && level >= 0 && level < 8 && us_sum && launches, "invalid arguments");
-    unsigned long long k[R360_KT_SLOTS];
-    if (ctx_wait(ctx)) return -1;
-    R360_HIP(hipMemcpy(k, ctx->d_ktime, sizeof k, hipMemcpyDeviceToHost));
-    *us_sum = (double)k[1 + level] * 0.01;   // 100 MHz ticks
-    *launches = (long)k[9 + level];
-    if (job_passes) *job_passes = (long)k[18 + level];
+    *us_sum = 0.0;
+    *launches = 0;
+    if (job_passes) *job_passes = 0;
+    for (r360_ctx* c = ctx; c; c = (c == ctx) ? ctx->stats_sibling : nullptr) {
+        unsigned long long k[R360_KT_SLOTS];
+        if (ctx_wait(c)) return -1;
+        R360_HIP(hipMemcpy(k, c->d_ktime, sizeof k, hipMemcpyDeviceToHost));
+        *us_sum += (double)k[1 + level] * 0.01;   // 100 MHz ticks
+        *launches += (long)k[9 + level];
+        if (job_passes) *job_passes += (long)k[18 + level];
+    }
     return 0;
 }
 
@@ -250,9 +255,11 @@ extern "C" int r360_ctx_host_times(r360_ctx* ctx, double out[6], int reset) {
 
 extern "C" int r360_ctx_kernel_time_reset(r360_ctx* ctx) {
     CHECK_ARG(ctx, "null ctx");
-    if (ctx_wait(ctx)) return -1;
-    R360_HIP(hipMemset(ctx->d_ktime, 0, sizeof(unsigned long long) * R360_KT_SLOTS));
-    R360_HIP(hipMemset(ctx->d_ktime, 0xff, sizeof(unsigned long long)));
+    for (r360_ctx* c = ctx; c; c = (c == ctx) ? ctx->stats_sibling : nullptr) {
+        if (ctx_wait(c)) return -1;
+        R360_HIP(hipMemset(c->d_ktime, 0, sizeof(unsigned long long) * R360_KT_SLOTS));
+        R360_HIP(hipMemset(c->d_ktime, 0xff, sizeof(unsigned long long)));
+    }
     return 0;
 }
 

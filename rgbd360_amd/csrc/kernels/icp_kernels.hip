@@ -1562,6 +1562,9 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
 // their next wait, so the grid always drains.  The host launches it only when the grid fits one resident round
 // with a workgroup per CU to spare (icp_level_persist_grid) and no other persistent launch of the process is in
 // flight.
+#ifndef R360_PERSIST_SLEEP
+#define R360_PERSIST_SLEEP 2   // s_sleep between polls (units of 64 clocks)
+#endif
 #ifndef R360_PERSIST_SPIN_TICKS
 #define R360_PERSIST_SPIN_TICKS 50000000ull   // 0.5 s of the 100 MHz s_memrealtime clock
 #endif
@@ -1605,7 +1608,7 @@ __global__ __launch_bounds__(TPB, R360_LEVEL_MINB) void k_icp_level(const IcpJob
             } else {
                 const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
                 while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tag) {
-                    __builtin_amdgcn_s_sleep(2);
+                    __builtin_amdgcn_s_sleep(R360_PERSIST_SLEEP);
                     if (__builtin_amdgcn_s_memrealtime() - t0 > R360_PERSIST_SPIN_TICKS) { go = 0; break; }
                 }
                 if (!go) __hip_atomic_store(&S->fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

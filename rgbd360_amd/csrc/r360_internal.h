@@ -311,6 +311,7 @@ struct r360_ctx {
     unsigned long long graph_clock = 0;
     IcpState* h_state = nullptr;  // pinned
     int timing = 0;
+    r360_ctx* stats_sibling = nullptr;   // a dense queue's second stream: its kernel statistics are reported with these
     int persist_held = 0;
     int async_persist = 0;  // the pending r360_align360 runs as persistent level launches   // this ctx holds the process's persistent-launch slot (runtime.cpp, persist_slot)
     std::vector<hipEvent_t> ev_pool;
