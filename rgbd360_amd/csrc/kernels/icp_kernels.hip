@@ -616,8 +616,19 @@ __device__ __forceinline__ int icp_pass_body(const IcpJobs& jobs, const float* _
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #endif
 #endif
-    const int st_stop = PERSIST ? ld_sc1_i(&S->stop) : S->stop;
-    const int st_active = PERSIST ? ld_sc1_i(&S->active) : S->active;
+    // Persistent launch: 18 lanes of the workgroup read the state words once (sc1) and hand them over in LDS.  Every
+    // wave reading them itself put 2048 waves x 18 loads of the same two lines on one L2 channel per XCD at every
+    // pass start (~3 us; the per-pass kernel reads them through the scalar cache).
+    __shared__ unsigned s_pst[18];   // pose (16), stop, active
+    if constexpr (PERSIST) {
+        const float* pm0 = first ? S->pose : S->cand;
+        if (tidx < 16) s_pst[tidx] = __float_as_uint(ld_sc1_f(pm0 + tidx));
+        else if (tidx == 16) s_pst[16] = (unsigned)ld_sc1_i(&S->stop);
+        else if (tidx == 17) s_pst[17] = (unsigned)ld_sc1_i(&S->active);
+        __syncthreads();
+    }
+    const int st_stop = PERSIST ? (int)__builtin_amdgcn_readfirstlane(s_pst[16]) : S->stop;
+    const int st_active = PERSIST ? (int)__builtin_amdgcn_readfirstlane(s_pst[17]) : S->active;
     if (st_stop || (!first && !st_active && !eval_only)) {
         if (!PERSIST && bidx == 0 && tidx == 0) pass_arrive(kt, false, C.level);
         return PASS_SKIPPED;
@@ -631,8 +642,9 @@ __device__ __forceinline__ int icp_pass_body(const IcpJobs& jobs, const float* _
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
 #pragma unroll
-        for (int c = 0; c < 3; ++c) P.R[r * 3 + c] = PERSIST ? ld_sc1_f(pm + c * 4 + r) : pm[c * 4 + r];
-        P.t[r] = PERSIST ? ld_sc1_f(pm + 12 + r) : pm[12 + r];
+        for (int c = 0; c < 3; ++c)
+            P.R[r * 3 + c] = PERSIST ? __uint_as_float(__builtin_amdgcn_readfirstlane(s_pst[c * 4 + r])) : pm[c * 4 + r];
+        P.t[r] = PERSIST ? __uint_as_float(__builtin_amdgcn_readfirstlane(s_pst[12 + r])) : pm[12 + r];
     }
     const float angle_res = (float)(2 * R360_PI / nCols);
     const float angle_res_inv = 1 / angle_res;
@@ -1573,6 +1585,9 @@ __global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs j
 #else
 #define R360_PERSIST_BUILT 1
 #endif
+#ifndef R360_LEVEL_PF0
+#define R360_LEVEL_PF0 6   // the level-0 form of the persistent launch (experiment variant lpf7: PF 7's deeper pipeline)
+#endif
 #ifndef R360_LEVEL_MINB
 #define R360_LEVEL_MINB 3   // waves per SIMD: a lone pass puts 2 workgroups on a CU, so registers are free up to 3
 #endif
@@ -2189,7 +2204,7 @@ static int level_blocks_per_cu() {   // the occupancy query for the instantiatio
 static int level_blocks_per_cu(int method, int pf) {
     auto by = [&](auto m) {
         constexpr int M = decltype(m)::value;
-        return pf == 6 ? level_blocks_per_cu<M, 6, 1>() : level_blocks_per_cu<M, 5, 0>();
+        return pf == 6 ? level_blocks_per_cu<M, R360_LEVEL_PF0, 1>() : level_blocks_per_cu<M, 5, 0>();
     };
     if (method == R360_PHOTO_CONSISTENCY) return by(std::integral_constant<int, R360_PHOTO_CONSISTENCY>{});
     if (method == R360_DEPTH_CONSISTENCY) return by(std::integral_constant<int, R360_DEPTH_CONSISTENCY>{});
@@ -2233,7 +2248,7 @@ int launch_icp_level_persist(r360_ctx* ctx, const r360_frame* trg, const r360_fr
                  unsigned long long*) = nullptr;
     auto pick = [&](auto m) {
         constexpr int M = decltype(m)::value;
-        kern = G.pf == 6 ? k_icp_level<M, 6, 1> : k_icp_level<M, 5, 0>;
+        kern = G.pf == 6 ? k_icp_level<M, R360_LEVEL_PF0, 1> : k_icp_level<M, 5, 0>;
     };
     if (method == R360_PHOTO_CONSISTENCY) pick(std::integral_constant<int, R360_PHOTO_CONSISTENCY>{});
     else if (method == R360_DEPTH_CONSISTENCY) pick(std::integral_constant<int, R360_DEPTH_CONSISTENCY>{});

@@ -149,5 +149,8 @@ def test_product_library_holds_only_covered_pass_forms_and_no_knobs():
         covered |= {(m, 6, 1, 0), (m, 5, 0, 0), (m, 5, 1, 0)}
         covered |= {(m, pf, 0, occ) for pf in (0, 3) for occ in (1, 2)}
     assert forms == covered, sorted(forms ^ covered)
+    # the persistent level launch of lone alignments: the same two plain forms (PF 6 at level 0, PF 5 above)
+    levels = {tuple(int(x) for x in f) for f in re.findall(rb"k_icp_levelILi([0-2])ELi([0-9])ELi([01])EE", blob)}
+    assert levels == {(m, pf, top) for m in (0, 1, 2) for pf, top in ((6, 1), (5, 0))}, sorted(levels)
     env_names = set(re.findall(rb"\x00(R360_[A-Z0-9_]+)\x00", blob))
     assert env_names <= {b"R360_DATA_DIR"}, sorted(env_names)
