@@ -31,8 +31,10 @@ struct r360_dense_queue {
     r360_ctx* cx[2] = {nullptr, nullptr};
     int n_ctx = 1;
     bool busy[2] = {false, false};
+    bool split = false;   // each batch split over both streams (the halves' passes interleave on the GPU)
     struct Inflight {
         int slot = 0, n = 0, rc = 0;
+        int n0 = 0;       // split batch: jobs [0, n0) on cx[0], [n0, n) on cx[1]
         std::vector<long> take;
         std::string err;
     };
@@ -89,7 +91,8 @@ static void dispatcher(r360_dense_queue* q) {
     std::vector<float> init;
     for (;;) {
         std::unique_lock<std::mutex> lk(q->m);
-        q->cv_work.wait(lk, [&] { return (!q->pending.empty() && free_slot(q) >= 0) || (q->quit && q->pending.empty()); });
+        auto can_go = [&] { return q->split ? (!q->busy[0] && !q->busy[1]) : free_slot(q) >= 0; };
+        q->cv_work.wait(lk, [&] { return (!q->pending.empty() && can_go()) || (q->quit && q->pending.empty()); });
         if (q->pending.empty()) break;   // quit with nothing pending
         // optional batch floor (R360_QUEUE_MIN jobs, waiting at most R360_QUEUE_WAIT_US): larger batches fill the
         // level-0 pass better at the cost of latency (experiment knob, off by default)
@@ -108,6 +111,8 @@ static void dispatcher(r360_dense_queue* q) {
         }
         const int n = (int)b.take.size();
         b.n = n;
+        b.n0 = (q->split && n >= 2) ? (n + 1) / 2 : n;
+        if (b.n0 < n) { b.slot = 0; q->busy[0] = q->busy[1] = true; }
         trg.resize(n); src.resize(n); init.resize(16 * (size_t)n);
         for (int j = 0; j < n; ++j) {
             r360_dense_queue::Job& J = q->jobs[b.take[j]];
@@ -123,11 +128,15 @@ static void dispatcher(r360_dense_queue* q) {
         }
         lk.unlock();
 
-        r360_ctx* c = q->cx[b.slot];
         int rc = 0;
-        for (hipEvent_t e : evs)
-            if (hipStreamWaitEvent(c->stream, e, 0) != hipSuccess) { r360_set_error("hipStreamWaitEvent failed"); rc = -1; }
-        if (rc == 0) rc = align360_batch_enqueue(c, n, trg.data(), src.data(), init.data(), method, &p, false);
+        for (int part = 0; part < (b.n0 < n ? 2 : 1) && rc == 0; ++part) {
+            r360_ctx* c = q->cx[part ? 1 : b.slot];
+            const int j0 = part ? b.n0 : 0, nj = part ? n - b.n0 : b.n0;
+            for (hipEvent_t e : evs)
+                if (hipStreamWaitEvent(c->stream, e, 0) != hipSuccess) { r360_set_error("hipStreamWaitEvent failed"); rc = -1; }
+            if (rc == 0)
+                rc = align360_batch_enqueue(c, nj, trg.data() + j0, src.data() + j0, init.data() + 16 * j0, method, &p, false);
+        }
         b.rc = rc;
         if (rc < 0) b.err = r360_last_error();
 
@@ -160,6 +169,11 @@ static void collector(r360_dense_queue* q) {
         std::string err = b.err;
         if (rc == 0) {
             rc = r360_align360_batch_result(q->cx[b.slot], po.data(), Ho.data(), go.data(), st.data());
+            if (rc >= 0 && b.n0 < n) {
+                const int j0 = b.n0;
+                rc = r360_align360_batch_result(q->cx[1], po.data() + 16 * j0, Ho.data() + 36 * j0, go.data() + 6 * j0,
+                                                st.data() + j0);
+            }
             if (rc < 0) err = r360_last_error();
         }
 
@@ -183,6 +197,7 @@ static void collector(r360_dense_queue* q) {
         if (n > q->max_seen) q->max_seen = n;
         q->inflight.pop_front();
         q->busy[b.slot] = false;
+        if (b.n0 < n) q->busy[1] = false;
         lk.unlock();
         q->cv_done.notify_all();
         q->cv_work.notify_one();
@@ -220,7 +235,9 @@ extern "C" int r360_dense_queue_create(int device, int max_batch, r360_dense_que
     // one batch stream; R360_QUEUE_STREAMS=2 (experiment builds) alternates batches over two: measured slower
     // (1206-1227 vs 1263 pairs/s, profiles/r4_queue): the batches halve (4.1 vs 7.7 pairs per launch)
     static const int streams = R360_KNOB("R360_QUEUE_STREAMS", 1);
-    if (streams >= 2) {
+    // R360_QUEUE_SPLIT=1 (experiment builds): one batch at a time, its jobs split over the two streams
+    static const int split = R360_KNOB("R360_QUEUE_SPLIT", 0);
+    if (streams >= 2 || split) {
         r360_ctx* c2 = nullptr;
         if (int rc = r360_ctx_create(device, &c2)) {
             r360_ctx_destroy(ctx);
@@ -229,6 +246,7 @@ extern "C" int r360_dense_queue_create(int device, int max_batch, r360_dense_que
         }
         q->cx[1] = c2;
         q->n_ctx = 2;
+        q->split = split != 0;
         ctx->stats_sibling = c2;   // kernel statistics of the queue ctx cover both streams
     }
     q->max_batch = max_batch;
