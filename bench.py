@@ -306,6 +306,14 @@ def config5_leg(device, rt8, pairs=48, iters0=50, pipelines=8, depth=2, repeats=
     avg_ms = us / max(n, 1) * 1e-3
     ppl = nj / max(n, 1)
     ach = ppl * alg / (avg_ms * 1e-3) / 1e9 if n else None
+    # HBM bytes per level-0 launch from the HiRes rocprofv3 --pmc passes (tools/prof_r3.sh, tools/hires_summary.py,
+    # profiles/latest/hires_pmc.json), reported only when that profile measured the current ICP sources
+    traffic, traffic_src = None, None
+    hf = os.path.join(ROOT, "profiles", "latest", "hires_pmc.json")
+    if os.path.exists(hf):
+        prof = json.load(open(hf))
+        if prof.get("icp_source_hash") == icp_source_hash() and prof.get("hbm_bytes_per_pair_pass"):
+            traffic, traffic_src = prof["hbm_bytes_per_pair_pass"] * ppl, prof.get("tag", "latest/hires_pmc.json")
     # per-pair accuracy against the synthetic ground truth (the dense stage starts from identity)
     gt = [R.synth_path_pose(SEED, k).astype(np.float64) for k in range(nf)]
     rot_err = []
@@ -321,7 +329,8 @@ def config5_leg(device, rt8, pairs=48, iters0=50, pipelines=8, depth=2, repeats=
         "sphere": f"{H0}x{W0}", "value": pairs * repeats / elapsed, "unit": "pairs/s",
         "ms_per_pair": elapsed / (pairs * repeats) * 1e3,
         "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": (ach / HBM_PEAK_GBS) if ach else None, "traffic": None,
+                     "frac": (ach / HBM_PEAK_GBS) if ach else None, "traffic": traffic,
+                     "traffic_profile": traffic_src, "traffic_per_pair_pass": (traffic / ppl) if traffic else None,
                      "kernel": "k_icp_pass<PHOTO_DEPTH> (level 0)", "avg_launch_ms": avg_ms, "launches": n,
                      "pairs_per_launch": ppl, "bytes_per_pair_pass": alg, "visible_frac": sso,
                      "timing": "in-kernel execution span (s_memrealtime) of every level-0 launch of the timed repeats"},

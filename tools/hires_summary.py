@@ -56,4 +56,7 @@ try:
         out["traffic_over_algorithmic"] = out["hbm_bytes_per_pair_pass"] / out["algorithmic_bytes_per_pair_pass"]
 except Exception as e:   # noqa: BLE001
     out["bench_line_error"] = str(e)
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import bench  # noqa: E402  (the ICP source hash the bench line checks before it reports this profile's traffic)
+out["icp_source_hash"] = bench.icp_source_hash()
 print(json.dumps(out, indent=1))
