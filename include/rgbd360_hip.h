@@ -510,6 +510,13 @@ int r360_libm_eval(const float* x, const float* y, const float* z, int n, float*
 /* s_memrealtime stamps (100 MHz) of the last ICP pass; written only by a -DR360_STAMPS build. */
 int r360_ctx_debug_stamps(r360_ctx* ctx, unsigned long long* out12);
 
+/* Lone alignFrames360 (r360_align360*, occlusion 0) as ONE launch per pyramid level (k_icp_level: the level's passes
+ * in a persistent grid, the step's workgroup handing each pass over to the others) instead of one launch per pass.
+ * Same grid, records and steps: results are bit-identical either way (st->persistent says which ran).  Off by
+ * default: measured slower on MI355X.  Used only when every level's grid fits one resident
+ * round and no other persistent alignment of the process is in flight. */
+int r360_ctx_persistent_levels(r360_ctx* ctx, int enable);
+
 /* ---------------------------------------------------------------- timing hooks (bench) */
 /* enable: 0 off, 1 every launch on ctx's stream, 2 the level-0 ICP passes only (HIP events around each) */
 int r360_ctx_timing(r360_ctx* ctx, int enable);

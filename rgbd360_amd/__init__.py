@@ -270,6 +270,7 @@ _SIGS = [
     ("r360_ctx_kernel_stats", C.c_int, [_P, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_long),
                                         C.POINTER(C.c_long)]),
     ("r360_ctx_timing", C.c_int, [_P, C.c_int]),
+    ("r360_ctx_persistent_levels", C.c_int, [_P, C.c_int]),
     ("r360_ctx_timing_read", C.c_int, [_P, C.c_char_p, _DP, C.POINTER(C.c_long)]),
     ("r360_ctx_timing_reset", C.c_int, [_P]),
 ]
@@ -353,6 +354,10 @@ class Context:
 
     def sync(self):
         _check(lib().r360_ctx_sync(self.h), "r360_ctx_sync")
+
+    def persistent_levels(self, enable=True):
+        """Lone alignFrames360 as one persistent launch per pyramid level (bit-identical; off by default)."""
+        _check(lib().r360_ctx_persistent_levels(self.h, int(enable)), "persistent_levels")
 
     def timing(self, enable):
         """0/False off, 1/True HIP events around every launch, 2 around the level-0 ICP passes only."""

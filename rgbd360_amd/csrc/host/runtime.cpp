@@ -111,6 +111,12 @@ static void timing_flush(r360_ctx* ctx) {
     ctx->ev_used = 0;
 }
 
+extern "C" int r360_ctx_persistent_levels(r360_ctx* ctx, int enable) {
+    CHECK_ARG(ctx, "null ctx");
+    ctx->persist_levels = enable ? 1 : 0;
+    return 0;
+}
+
 extern "C" int r360_ctx_timing(r360_ctx* ctx, int enable) {
     CHECK_ARG(ctx, "null ctx");
     timing_flush(ctx);
@@ -879,11 +885,12 @@ extern "C" int r360_align360_async(r360_ctx* ctx, r360_frame* trg, r360_frame* s
     memcpy(h->cand, init, sizeof(float) * 16);
     h->dbg[8] = ~0ull;
     R360_HIP(hipMemcpyAsync(ctx->d_state, h, sizeof(IcpState), hipMemcpyHostToDevice, ctx->stream));
-    // the plain pass without per-launch timing events runs each level as one persistent launch (k_icp_level)
-    // when every level's grid fits; otherwise (occlusion variants, timing, another persistent launch in
-    // flight) one launch per pass.  R360_NO_PERSIST=1 (experiment builds) forces the per-pass launches.
-    static const bool no_persist = R360_KNOB("R360_NO_PERSIST", 0) != 0;
-    bool persist = !no_persist && !occlusion && !ctx->timing && !R360_POLL;
+    // with r360_ctx_persistent_levels(ctx, 1) the plain pass without per-launch timing events runs each level as
+    // one persistent launch (k_icp_level) when every level's grid fits; otherwise (the default, occlusion variants,
+    // timing, another persistent launch in flight) one launch per pass.  R360_PERSIST=1 (experiment builds) sets
+    // the option for every context.
+    static const bool persist_env = R360_KNOB("R360_PERSIST", 0) != 0;
+    bool persist = (ctx->persist_levels || persist_env) && !occlusion && !ctx->timing && !R360_POLL;
     for (int l = 0; persist && l < p->n_pyr; ++l) persist = icp_level_persist_ok(ctx, src, l, method);
     if (persist) persist = persist_take(ctx);
     auto passes_of = [&]() -> int {

@@ -312,6 +312,7 @@ struct r360_ctx {
     IcpState* h_state = nullptr;  // pinned
     int timing = 0;
     r360_ctx* stats_sibling = nullptr;   // a dense queue's second stream: its kernel statistics are reported with these
+    int persist_levels = 0; // r360_ctx_persistent_levels: lone alignments as one launch per level
     int persist_held = 0;
     int async_persist = 0;  // the pending r360_align360 runs as persistent level launches   // this ctx holds the process's persistent-launch slot (runtime.cpp, persist_slot)
     std::vector<hipEvent_t> ev_pool;

@@ -161,12 +161,12 @@ def _same_outputs(a, b):
 
 @pytest.mark.parametrize("iters0", [20, 0])
 def test_persistent_equals_per_pass(seq, iters0):
-    """r360_align360 runs each level as ONE persistent launch (k_icp_level) when its pass grid fits a resident
-    round; with per-launch timing on it launches one kernel per pass.  Same grid, same records, same steps:
-    bit-identical outputs, under the fixed and the reference (converging) schedules."""
+    """With r360_ctx_persistent_levels on, r360_align360 runs each level as ONE persistent launch (k_icp_level) when
+    its pass grid fits a resident round; by default it launches one kernel per pass.  Same grid, same records, same
+    steps: bit-identical outputs, under the fixed and the reference (converging) schedules."""
     fr = seq["frames"]
     a, b = R.Context(0), R.Context(0)
-    b.timing(True)
+    a.persistent_levels(True)
     for t, s in [(fr[0], fr[1]), (fr[2], fr[5]), (fr[0], seq["other"])]:
         ra = _single(a, t, s, None, _params(iters0))
         rb = _single(b, t, s, None, _params(iters0))
@@ -182,6 +182,8 @@ def test_persistent_slot(seq):
     fr = seq["frames"]
     p = _params(20)
     a, b = R.Context(0), R.Context(0)
+    a.persistent_levels(True)
+    b.persistent_levels(True)
     init = np.eye(4, dtype=np.float32).T.copy().reshape(-1)
     fp = lambda x: x.ctypes.data_as(R.C.POINTER(R.C.c_float))
     assert R.lib().r360_align360_async(a.h, fr[3].h, fr[4].h, fp(init), R.PHOTO_DEPTH, 0, R.C.byref(p)) == 0
