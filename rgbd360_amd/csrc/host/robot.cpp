@@ -34,7 +34,7 @@ int ensure_robot_buffers(r360_ctx* ctx) {
     R360_HIP(hipMalloc(&ctx->d_rob_sums, sizeof(double) * 32 * NJ));
     R360_HIP(hipHostMalloc(&ctx->h_rob_sums, sizeof(double) * 32 * NJ, hipHostMallocDefault));
     R360_HIP(hipMalloc(&ctx->d_rob_tickets, sizeof(unsigned) * NJ));
-    R360_HIP(hipMemset(ctx->d_rob_tickets, 0, sizeof(unsigned) * NJ));
+    R360_HIP(hipMemsetAsync(ctx->d_rob_tickets, 0, sizeof(unsigned) * NJ, ctx->stream));   // ordered before its kernels
     R360_HIP(hipMalloc(&ctx->d_rob_out, sizeof(RobotOut)));
     R360_HIP(hipHostMalloc(&ctx->h_rob_out, sizeof(RobotOut), hipHostMallocDefault));
     return 0;

@@ -182,15 +182,17 @@ extern "C" int r360_ctx_create(int device, r360_ctx** out) {
         R360_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     }
     R360_HIP(hipEventCreateWithFlags(&c->wait_ev, hipEventDisableTiming | hipEventBlockingSync));
+    // Initial contents on the ctx's own stream: hipMemset runs on the null stream, which does not order with a
+    // non-blocking stream (and returns before it completes), so a first kernel on c->stream could overtake it.
     R360_HIP(hipMalloc(&c->d_state, sizeof(IcpState)));
-    R360_HIP(hipMemset(c->d_state, 0, sizeof(IcpState)));
+    R360_HIP(hipMemsetAsync(c->d_state, 0, sizeof(IcpState), c->stream));
     c->partials_cap = 2048;
     R360_HIP(hipMalloc(&c->d_partials, sizeof(double) * 32 * c->partials_cap));
     R360_HIP(hipMalloc(&c->d_gticket, sizeof(unsigned) * R360_TICKET_STRIDE * R360_TICKET_GROUPS));
-    R360_HIP(hipMemset(c->d_gticket, 0, sizeof(unsigned) * R360_TICKET_STRIDE * R360_TICKET_GROUPS));
+    R360_HIP(hipMemsetAsync(c->d_gticket, 0, sizeof(unsigned) * R360_TICKET_STRIDE * R360_TICKET_GROUPS, c->stream));
     R360_HIP(hipMalloc(&c->d_ktime, sizeof(unsigned long long) * R360_KT_SLOTS));
-    R360_HIP(hipMemset(c->d_ktime, 0, sizeof(unsigned long long) * R360_KT_SLOTS));
-    R360_HIP(hipMemset(c->d_ktime, 0xff, sizeof(unsigned long long)));
+    R360_HIP(hipMemsetAsync(c->d_ktime, 0, sizeof(unsigned long long) * R360_KT_SLOTS, c->stream));
+    R360_HIP(hipMemsetAsync(c->d_ktime, 0xff, sizeof(unsigned long long), c->stream));
     R360_HIP(hipHostMalloc(&c->h_state, sizeof(IcpState), hipHostMallocDefault));
     r360_match_params_default(&c->match);
     *out = c;
@@ -263,8 +265,8 @@ extern "C" int r360_ctx_kernel_time_reset(r360_ctx* ctx) {
     CHECK_ARG(ctx, "null ctx");
     for (r360_ctx* c = ctx; c; c = (c == ctx) ? ctx->stats_sibling : nullptr) {
         if (ctx_wait(c)) return -1;
-        R360_HIP(hipMemset(c->d_ktime, 0, sizeof(unsigned long long) * R360_KT_SLOTS));
-        R360_HIP(hipMemset(c->d_ktime, 0xff, sizeof(unsigned long long)));
+        R360_HIP(hipMemsetAsync(c->d_ktime, 0, sizeof(unsigned long long) * R360_KT_SLOTS, c->stream));
+        R360_HIP(hipMemsetAsync(c->d_ktime, 0xff, sizeof(unsigned long long), c->stream));
     }
     return 0;
 }
@@ -529,7 +531,7 @@ extern "C" int r360_frame_create(r360_ctx* ctx, const r360_calib* calib, r360_fr
     }
     f->src_blocks = (int)((nsph + R360_SRC_BLOCK - 1) / R360_SRC_BLOCK);
     R360_HIP(hipMalloc(&f->d_npts, sizeof(int) * R360_MAX_PYR));
-    R360_HIP(hipMemset(f->d_npts, 0, sizeof(int) * R360_MAX_PYR));
+    R360_HIP(hipMemsetAsync(f->d_npts, 0, sizeof(int) * R360_MAX_PYR, f->ctx->stream));
     R360_HIP(hipMalloc(&f->d_src_cnt, sizeof(int) * R360_MAX_PYR * (size_t)f->src_blocks));
     SrcLevel sl[R360_MAX_PYR];
     for (int l = 0; l < f->n_levels; ++l) {

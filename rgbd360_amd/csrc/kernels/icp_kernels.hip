@@ -2082,7 +2082,10 @@ int ensure_batch(r360_ctx* ctx, int n, long n_pixels) {
     R360_HIP(hipMalloc(&ctx->d_bstate, sizeof(IcpState) * cap));
     R360_HIP(hipMalloc(&ctx->d_bpartials, sizeof(double) * 32 * (size_t)ctx->partials_cap * cap));
     R360_HIP(hipMalloc(&ctx->d_bgticket, sizeof(unsigned) * tk * cap));
-    R360_HIP(hipMemset(ctx->d_bgticket, 0, sizeof(unsigned) * tk * cap));
+    // zeroed on the ctx stream, ahead of the batch's passes: hipMemset (null stream) neither orders with the
+    // non-blocking ctx stream nor completes before returning, and recycled memory left the first batches' group
+    // counters non-zero now and then (a wrong last workgroup: one pair in a few hundred off the single-pair result)
+    R360_HIP(hipMemsetAsync(ctx->d_bgticket, 0, sizeof(unsigned) * tk * cap, ctx->stream));
     R360_HIP(hipMalloc(&ctx->d_bdefer, sizeof(int) * (size_t)dcap * cap));
     R360_HIP(hipHostMalloc(&ctx->h_bstate, sizeof(IcpState) * cap, hipHostMallocDefault));
     ctx->batch_cap = cap;

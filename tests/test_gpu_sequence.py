@@ -130,3 +130,28 @@ def test_queued_dense_stage_reproduces_the_records(seq):
         runner.close()
     assert st["jobs"] == 255 and st["batches"] < 255
     assert np.array_equal(rec[0], seq["rec"])
+
+
+@pytest.mark.parametrize("depth,lookahead", [(3, 1), (2, 2)])
+def test_queued_repeats_as_one_stream(seq, depth, lookahead):
+    """Queued pipelines run their repeats as one stream of frames (a repeat's first frame is built while the
+    previous repeat's last alignments are in flight; buffers are refilled only after every pair that used them is
+    collected): short runs (the 1/8-shard shape, 6-7 pairs per pipeline) repeated three times give every repeat's
+    records bit-identical to the single-GPU run's."""
+    bgr, dep = seq["bgr"], seq["dep"]
+    p0, p1 = OD.shard_pairs(7, 8)
+    runs = OD.split_range(p0, p1, 5)
+    runner = OD.SequenceRunner(0, 480, 640, 5, seq["params"], queue=16, depth=depth, lookahead=lookahead)
+    try:
+        rec = np.zeros((3, p1 - p0, OD.REC), np.float32)
+        runner.run(p0, p1, lambda i: (bgr[i], dep[i]), rec, repeats=3, runs=runs)
+    finally:
+        runner.close()
+    ref = seq["rec"][p0:p1]
+    for r in range(3):
+        bad = []
+        for i in range(p1 - p0):
+            d = np.nonzero(rec[r, i] != ref[i])[0]
+            if len(d):
+                bad.append((i, int((d < 16).sum()), int(((d >= 16) & (d < 52)).sum()), [int(k) for k in d[d >= 52]]))
+        assert not bad, (r, "pair, pose fields, info fields, other fields", bad[:8])
