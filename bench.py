@@ -240,7 +240,7 @@ def half_leg(kind, device, rows, cols, p0, p1, frames_of, params, pipelines, que
         out["pbmap_failed"] = int((st == 1).sum())
     else:
         us, n, nj = qctx.kernel_stats(0)
-        W0 = cols * 8
+        W0 = rows * 8                       # sphere width: 8 sensors of `rows` (the sensors are mounted sideways)
         N0 = int(W0 * 0.5 * 60.0 / 180) * W0
         sso = float(np.mean(rec[:, :, OD.R_SSO]))
         alg = 8.0 * N0 + 24.0 * sso * N0
