@@ -445,6 +445,10 @@ int planes_enqueue(r360_frame* f) {
 }
 
 void planes_join(r360_frame* f) {
+    // A frame's planes may be awaited from two host threads at once (the frame where one pipeline's run ends and
+    // the next one's starts, registered by both): the join is serialised per frame (striped by address).
+    static std::mutex stripes[64];
+    std::lock_guard<std::mutex> lk(stripes[(reinterpret_cast<uintptr_t>(f) >> 6) & 63]);
     PlaneBufs& P = f->pl;
     if (P.worker) {
         P.worker->join();

@@ -104,7 +104,8 @@ class SequenceRunner:
 
     def __init__(self, device: int, rows: int, cols: int, pipelines: int, params: IcpParams,
                  planes: bool = True, max_match_planes: int = 25, mode: int = PLANAR_3DoF, dense_only: bool = False,
-                 queue: int = 0, planes_only: bool = False, depth: int = 1, lookahead: int = 1):
+                 queue: int = 0, planes_only: bool = False, depth: int = 1, lookahead: int = 1,
+                 share_edges: bool = True):
         self.P = pipelines
         self.lookahead = max(1, lookahead)   # queued mode: frames whose build is enqueued ahead of the pair in hand
         self.dense_only = dense_only
@@ -125,6 +126,12 @@ class SequenceRunner:
             # queued: depth alignments in flight, the pair being registered, the frames built ahead and the next
             # frame's prefetched upload
             self.frames.append([Frame360(cal) for _ in range(self.depth + self.lookahead + 2 if self.queue else 2)])
+        # queued mode: the frame where pipeline p's run starts is also where pipeline p-1's run ends; pipeline p
+        # builds it (in a buffer of its own, outside its ring) and pipeline p-1 registers its last pair against
+        # it, so contiguous runs cost no halo frame builds (share_edges=False: each pipeline builds both)
+        self.share_edges = bool(self.queue) and share_edges
+        self.edge_frames = [Frame360(cal) for cal in self.cals] if self.share_edges else None
+        self.edges = None
         self.stats = [IcpStats() for _ in range(pipelines)]
         # host-side time per pipeline: [load + build enqueue, PbMap stage (register_async), dense wait, pairs]
         self.host_s = np.zeros((pipelines, 4))
@@ -213,16 +220,52 @@ class SequenceRunner:
         hs = self.host_s[p]
         nfr = b - a + 1                  # frames per repeat
         T = nfr * repeats                # frame positions
+        # shared run edges: position k = 0 of a repeat lives in this pipeline's edge buffer (left edge, built
+        # here for the left neighbour too); k = nfr - 1 is the right neighbour's edge buffer (not built here)
+        E = self.edges if self.share_edges else None
+        left = E is not None and p > 0 and E[p]["shared"]
+        right = E is not None and p + 1 < len(E) and E[p + 1]["shared"]
 
         def fidx(t):
             return a + t % nfr
 
+        def buf(t):
+            k = t % nfr
+            if left and k == 0:
+                return self.edge_frames[p]
+            if right and k == nfr - 1:
+                return self.edge_frames[p + 1]
+            return fr[t % nbuf]
+
+        def built_here(t):
+            return not (right and t % nfr == nfr - 1)
+
         def load(t):
-            f, i = fr[t % nbuf], fidx(t)
+            if not built_here(t):
+                return
+            k, r = t % nfr, t // nfr
+            if left and k == 0:
+                # the left neighbour must be done with the previous repeat's copy, and so must this pipeline
+                while pending and pending[0][1] <= t - nfr:
+                    finish(*pending.pop(0))
+                e = E[p]
+                with e["cv"]:
+                    e["cv"].wait_for(lambda: e["released"] >= r - 1)
+            f, i = buf(t), fidx(t)
             if device_inputs:
                 f.upload_device(*frames_of(i))
             else:
                 f.upload_async(*frames_of(i))
+
+        def build(t):
+            if not built_here(t):
+                return
+            buf(t).build(self.flags, sync=False)
+            if left and t % nfr == 0:
+                e = E[p]
+                with e["cv"]:
+                    e["built"] = t // nfr
+                    e["cv"].notify_all()
 
         def finish(ticket, t, st):
             rec = out[t // nfr][fidx(t) - p0]
@@ -243,17 +286,22 @@ class SequenceRunner:
             rec[R_STATUS] = 2 if st.illposed else rc
             rec[R_SSO] = st.sso
             rec[R_ERR] = st.error
+            if right and t % nfr == nfr - 2:   # the last pair of a repeat: the right neighbour's edge is free again
+                e = E[p + 1]
+                with e["cv"]:
+                    e["released"] = t // nfr
+                    e["cv"].notify_all()
 
         nbuf = len(fr)
+        pending = []
         LA = self.lookahead
         depth = nbuf - LA - 2
         last = T - 1
         for t in range(0, min(LA, last + 1)):   # positions 0 .. LA-1 built, position LA uploaded
             load(t)
-            fr[t % nbuf].build(self.flags, sync=False)
+            build(t)
         if LA <= last:
             load(LA)
-        pending = []
         sts = [IcpStats() for _ in range(depth + 1)]
         n_sub = 0
         for t in range(0, last):
@@ -262,15 +310,19 @@ class SequenceRunner:
             # and (u, u + 1) that used it (without repeat boundaries the in-flight limit below already has)
             while pending and pending[0][1] <= t + LA + 1 - nbuf:
                 finish(*pending.pop(0))
-            cur, nxt = fr[t % nbuf], fr[(t + 1) % nbuf]
+            cur, nxt = buf(t), buf(t + 1)
             if t + LA <= last:
-                fr[(t + LA) % nbuf].build(self.flags, sync=False)   # its upload was issued one iteration earlier
+                build(t + LA)   # its upload was issued one iteration earlier
             if t + LA + 1 <= last:
                 load(t + LA + 1)
             t1 = time.perf_counter()
             if t % nfr == nfr - 1:   # the last frame of a repeat: no pair
                 hs[0] += t1 - t0
                 continue
+            if not built_here(t + 1):   # the right neighbour's edge frame: built for this repeat?
+                e = E[p + 1]
+                with e["cv"]:
+                    e["cv"].wait_for(lambda: e["built"] >= (t + 1) // nfr)
             ticket = C.c_long()
             if self.dense_only:
                 rc = L.r360_dense_queue_submit(q.h, cur.h, nxt.h, _fptr(self.eye), PHOTO_DEPTH, C.byref(self.params),
@@ -300,6 +352,12 @@ class SequenceRunner:
         assert len(runs) <= self.P
 
         body = self._pipeline_queued if self.queue else self._pipeline
+        if self.share_edges:
+            import threading
+            # edge p (between runs p-1 and p, shared only where they meet): pipeline p has built its first frame
+            # for repeat `built`; pipeline p-1 is done with it through repeat `released`
+            self.edges = [None] + [{"cv": threading.Condition(), "built": -1, "released": -1,
+                                     "shared": runs[q - 1][1] == runs[q][0]} for q in range(1, len(runs))]
 
         def worker(p):
             import threading
@@ -321,6 +379,8 @@ class SequenceRunner:
         for fr in self.frames:
             for f in fr:
                 f.close()
+        for f in self.edge_frames or []:
+            f.close()
         for c in self.cals:
             c.close()
         for c in self.ctxs:
