@@ -93,6 +93,9 @@ def trajectory_error(T: np.ndarray, gt: np.ndarray) -> dict:
             "final_rot_err_deg": rot[-1], "final_trans_err_m": trans[-1], "path_length_m": path}
 
 
+EDGE_WAIT_S = 120.0   # a shared edge frame not built / released within this time: the neighbour pipeline is stuck
+
+
 class SequenceRunner:
     """P pipelines on one GPU, each an r360_ctx (HIP stream + device GN state) driven by its own host thread
     (ctypes drops the GIL inside the library), each with two Frame360 buffers used in turn.
@@ -250,7 +253,8 @@ class SequenceRunner:
                     finish(*pending.pop(0))
                 e = E[p]
                 with e["cv"]:
-                    e["cv"].wait_for(lambda: e["released"] >= r - 1)
+                    if not e["cv"].wait_for(lambda: e["released"] >= r - 1 or e["failed"], EDGE_WAIT_S) or e["failed"]:
+                        raise RuntimeError(f"pipeline {p}: left neighbour did not release edge frame {fidx(t)}")
             f, i = buf(t), fidx(t)
             if device_inputs:
                 f.upload_device(*frames_of(i))
@@ -322,7 +326,9 @@ class SequenceRunner:
             if not built_here(t + 1):   # the right neighbour's edge frame: built for this repeat?
                 e = E[p + 1]
                 with e["cv"]:
-                    e["cv"].wait_for(lambda: e["built"] >= (t + 1) // nfr)
+                    if not e["cv"].wait_for(lambda: e["built"] >= (t + 1) // nfr or e["failed"], EDGE_WAIT_S) \
+                            or e["built"] < (t + 1) // nfr:
+                        raise RuntimeError(f"pipeline {p}: right neighbour did not build edge frame {fidx(t + 1)}")
             ticket = C.c_long()
             if self.dense_only:
                 rc = L.r360_dense_queue_submit(q.h, cur.h, nxt.h, _fptr(self.eye), PHOTO_DEPTH, C.byref(self.params),
@@ -356,14 +362,23 @@ class SequenceRunner:
             import threading
             # edge p (between runs p-1 and p, shared only where they meet): pipeline p has built its first frame
             # for repeat `built`; pipeline p-1 is done with it through repeat `released`
-            self.edges = [None] + [{"cv": threading.Condition(), "built": -1, "released": -1,
+            self.edges = [None] + [{"cv": threading.Condition(), "built": -1, "released": -1, "failed": False,
                                      "shared": runs[q - 1][1] == runs[q][0]} for q in range(1, len(runs))]
 
         def worker(p):
             import threading
             self.native_ids.add(threading.get_native_id())
             if self.queue:   # the repeats as one stream of frames (no drain between them)
-                body(p, runs[p], frames_of, out, p0, device_inputs, repeats)
+                try:
+                    body(p, runs[p], frames_of, out, p0, device_inputs, repeats)
+                except BaseException:
+                    # a failed pipeline must not leave its neighbours waiting on its edges
+                    for e in (self.edges or [])[p:p + 2]:
+                        if e is not None:
+                            with e["cv"]:
+                                e["failed"] = True
+                                e["cv"].notify_all()
+                    raise
                 return
             for r in range(repeats):
                 body(p, runs[p], frames_of, out[r], p0, device_inputs)
