@@ -352,7 +352,9 @@ def main(argv=None, runner_factory=None):
     ap.add_argument("--iters0", type=int, default=20)
     ap.add_argument("--frames", type=int, default=256, help="sequence length (frames)")
     ap.add_argument("--workload", choices=["sequence", "dense", "planes"], default="sequence")
-    ap.add_argument("--streams", type=int, default=8, help="max pipelines per GPU (host thread + HIP stream each)")
+    ap.add_argument("--streams", type=int, default=10, help="max pipelines per GPU (host thread + HIP stream each; "
+                    "10 since the pipelines share their run edges: 1330-1342 vs 1299-1301 pairs/s at 8, "
+                    "profiles/r4_streams/)")
     ap.add_argument("--min-run", type=int, default=6,
                     help="min pairs per pipeline run (each run rebuilds a halo frame): 6 gives a 1/8 shard (31-32 pairs) "
                          "5 pipelines, 8-10 %% faster than 8 (3-4 pipelines) and 4 (8); N=1 and 1/4 shards keep 8 "
