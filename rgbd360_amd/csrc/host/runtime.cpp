@@ -4,6 +4,7 @@
 #include <atomic>
 #include <chrono>
 #include <dlfcn.h>
+#include <sys/prctl.h>
 #include <cmath>
 #include <thread>
 #include <cstdarg>
@@ -60,7 +61,15 @@ static std::string calib_dir_or_default(const char* dir, const char* sub) {
 // whole wait even on a blocking-sync event (measured: every per-frame assembly thread and pipeline thread
 // of the bench burned its wait, 15 of 16 host cores at 16 pipelines), and a sleeping poll gives the cores
 // back to the PbMap host stages; the added latency is at most one sleep (<= 100 us) on ms-scale waits.
+// Polls e with short sleeps.  The waiting thread's timer slack is set to 1 us first (its own setting, per thread):
+// with Linux's default 50 us slack a 20 us sleep overslept to ~70 us, so every short wait (a lone alignment's
+// result, RegisterPbMap's match tables) paid up to that much after the GPU had finished.
 int event_wait(hipEvent_t e) {
+    static thread_local bool slack_set = false;
+    if (!slack_set) {
+        (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0UL, 0UL, 0UL);
+        slack_set = true;
+    }
     for (int k = 0;; ++k) {
         const hipError_t r = hipEventQuery(e);
         if (r == hipSuccess) return 0;
@@ -68,7 +77,7 @@ int event_wait(hipEvent_t e) {
             r360_set_error("hipEventQuery -> %s", hipGetErrorString(r));
             return -1;
         }
-        std::this_thread::sleep_for(std::chrono::microseconds(k < 8 ? 20 : k < 32 ? 50 : 100));
+        std::this_thread::sleep_for(std::chrono::microseconds(k < 32 ? 5 : k < 96 ? 20 : 100));
     }
 }
 
