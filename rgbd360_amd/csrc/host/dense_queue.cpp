@@ -20,6 +20,7 @@ extern "C" int r360_align360_batch_async(r360_ctx* ctx, int n, r360_frame* const
                                          const float* init, int method, const r360_icp_params* p);
 int align360_batch_enqueue(r360_ctx* ctx, int n, r360_frame* const* trg, r360_frame* const* src, const float* init,
                            int method, const r360_icp_params* p, bool wait_frames);
+hipEvent_t frame_build_event(const r360_frame* f);   // runtime.cpp: recorded after the frame's last pyramid build
 
 struct r360_dense_queue {
     r360_ctx* ctx = nullptr;           // the queue's own stream, GN states and batch buffers
@@ -51,7 +52,8 @@ struct r360_dense_queue {
         float init[16];
         int method = 0;
         r360_icp_params p{};
-        hipEvent_t ev[2] = {nullptr, nullptr};   // the producers' streams up to the submit (frame builds)
+        hipEvent_t ev[2] = {nullptr, nullptr};   // the frames' builds (their build events, or the streams at submit)
+        bool own[2] = {false, false};            // ev[e] came from ev_free (the frames' build events are not ours)
         int nev = 0;
         int reg = 0, good = 0;                   // Register(): PbMap outcome and information
         float info[36];
@@ -188,7 +190,8 @@ static void collector(r360_dense_queue* q) {
                 J.st = st[j];
                 J.rc = st[j].illposed ? 1 : 0;
             }
-            for (int e = 0; e < J.nev; ++e) q->ev_free.push_back(J.ev[e]);
+            for (int e = 0; e < J.nev; ++e)
+                if (J.own[e]) q->ev_free.push_back(J.ev[e]);
             J.nev = 0;
             J.done = 1;
         }
@@ -267,7 +270,8 @@ extern "C" void r360_dense_queue_destroy(r360_dense_queue* q) {
     q->collector.join();
     (void)hipSetDevice(q->ctx->device);
     for (auto& kv : q->jobs)
-        for (int e = 0; e < kv.second.nev; ++e) hipEventDestroy(kv.second.ev[e]);
+        for (int e = 0; e < kv.second.nev; ++e)
+            if (kv.second.own[e]) hipEventDestroy(kv.second.ev[e]);
     for (hipEvent_t e : q->ev_free) hipEventDestroy(e);
     q->ctx->stats_sibling = nullptr;
     if (q->cx[1]) r360_ctx_destroy(q->cx[1]);
@@ -294,18 +298,21 @@ static int queue_submit(r360_dense_queue* q, r360_frame* trg, r360_frame* src, c
               "frames and queue on different devices");
     CHECK_ARG((trg->built & R360_BUILD_PYRAMID) && (src->built & R360_BUILD_PYRAMID),
               "frames need R360_BUILD_PYRAMID");
-    // events on the producers' streams: the batch waits for the frames' builds enqueued so far
-    hipStream_t streams[2] = {trg->ctx->stream, src->ctx->stream};
-    const int ns = streams[0] == streams[1] ? 1 : 2;
+    // what the batch waits for: each frame's build event (recorded right after its pyramid build), or, for a frame
+    // built without one, an event on its stream now (everything enqueued there so far)
+    const r360_frame* fs[2] = {trg, src};
+    const int ns = trg == src ? 1 : 2;
     hipEvent_t ev[2] = {nullptr, nullptr};
+    bool own[2] = {false, false};
+    for (int i = 0; i < ns; ++i) ev[i] = frame_build_event(fs[i]);
     {
         std::lock_guard<std::mutex> lk(q->m);
         for (int i = 0; i < ns; ++i)
-            if (!q->ev_free.empty()) { ev[i] = q->ev_free.back(); q->ev_free.pop_back(); }
+            if (!ev[i] && !q->ev_free.empty()) { ev[i] = q->ev_free.back(); q->ev_free.pop_back(); own[i] = true; }
     }
     for (int i = 0; i < ns; ++i) {
-        if (!ev[i]) R360_HIP(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
-        R360_HIP(hipEventRecord(ev[i], streams[i]));
+        if (!ev[i]) { R360_HIP(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming)); own[i] = true; }
+        if (own[i]) R360_HIP(hipEventRecord(ev[i], fs[i]->ctx->stream));
     }
     {
         std::lock_guard<std::mutex> lk(q->m);
@@ -315,7 +322,7 @@ static int queue_submit(r360_dense_queue* q, r360_frame* trg, r360_frame* src, c
         memcpy(J.init, init, sizeof J.init);
         J.method = method;
         J.p = *p;
-        J.ev[0] = ev[0]; J.ev[1] = ev[1]; J.nev = ns;
+        J.ev[0] = ev[0]; J.ev[1] = ev[1]; J.own[0] = own[0]; J.own[1] = own[1]; J.nev = ns;
         J.reg = reg; J.good = good;
         if (info) memcpy(J.info, info, sizeof J.info);
         q->pending.push_back(t);

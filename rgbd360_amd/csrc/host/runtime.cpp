@@ -4,6 +4,8 @@
 #include <atomic>
 #include <chrono>
 #include <dlfcn.h>
+#include <mutex>
+#include <unordered_map>
 #include <sys/prctl.h>
 #include <cmath>
 #include <thread>
@@ -553,8 +555,44 @@ extern "C" int r360_frame_create(r360_ctx* ctx, const r360_calib* calib, r360_fr
     return 0;
 }
 
+// The event recorded on a frame's stream right after its last pyramid build (r360_frame_build_async).  The dense
+// queue's batches wait on it instead of on the stream's tail at submit time, which by then also held the next
+// frame's upload (a pipeline prefetches it right after the build).  Kept beside the frame (keyed by its address).
+static std::mutex g_bev_m;
+static std::unordered_map<const r360_frame*, hipEvent_t> g_bev;
+
+hipEvent_t frame_build_event(const r360_frame* f) {
+    std::lock_guard<std::mutex> lk(g_bev_m);
+    auto it = g_bev.find(f);
+    return it == g_bev.end() ? nullptr : it->second;
+}
+
+static int frame_build_event_record(const r360_frame* f) {
+    hipEvent_t e = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_bev_m);
+        auto it = g_bev.find(f);
+        if (it != g_bev.end()) e = it->second;
+    }
+    if (!e) {
+        R360_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        std::lock_guard<std::mutex> lk(g_bev_m);
+        g_bev[f] = e;
+    }
+    R360_HIP(hipEventRecord(e, f->ctx->stream));
+    return 0;
+}
+
 extern "C" void r360_frame_destroy(r360_frame* f) {
     if (!f) return;
+    {
+        std::lock_guard<std::mutex> lk(g_bev_m);
+        auto it = g_bev.find(f);
+        if (it != g_bev.end()) {
+            (void)hipEventDestroy(it->second);
+            g_bev.erase(it);
+        }
+    }
     // hipFree synchronises the device; the frame never dereferences its ctx here so frames may
     // outlive their context at interpreter shutdown.
     hipFree(f->d_bgr); hipFree(f->d_depth); hipFree(f->d_depth_m); hipFree(f->d_sph_bgr); hipFree(f->d_sph_depth);
@@ -615,7 +653,7 @@ extern "C" int r360_frame_set_sphere(r360_frame* f, const uint8_t* bgr, const ui
     const size_t n = (size_t)sph_rows * sph_cols;
     R360_HIP(hipMemcpyAsync(f->d_sph_bgr, bgr, n * 3, hipMemcpyHostToDevice, f->ctx->stream));
     R360_HIP(hipMemcpyAsync(f->d_sph_depth, range_mm, n * 2, hipMemcpyHostToDevice, f->ctx->stream));
-    if (launch_sphere_level0(f) || launch_pyramid(f)) return -1;
+    if (launch_sphere_level0(f) || launch_pyramid(f) || frame_build_event_record(f)) return -1;
     R360_HIP(hipStreamSynchronize(f->ctx->stream));
     f->built = (f->built & ~(unsigned)(R360_BUILD_SPHERE | R360_BUILD_PYRAMID)) | R360_BUILD_SPHERE | R360_BUILD_PYRAMID;
     return 0;
@@ -657,6 +695,7 @@ extern "C" int r360_frame_build_async(r360_frame* f, unsigned flags) {
     if (flags & R360_BUILD_PYRAMID) {
         if (launch_pyramid(f)) return -1;
         f->built |= R360_BUILD_PYRAMID;
+        if (frame_build_event_record(f)) return -1;
     }
     if (flags & R360_BUILD_SENSOR_PYRAMID) {
         if (launch_sensor_pyramid(f)) return -1;
