@@ -239,7 +239,8 @@ def half_leg(kind, device, rows, cols, p0, p1, frames_of, params, pipelines, que
                            "RegisterPbMap(25 planes, PLANAR_3DoF), no alignFrames360")
         out["pbmap_failed"] = int((st == 1).sum())
     else:
-        us, n, nj = qctx.kernel_stats(0)
+        # unqueued runs (--queue 0: each pipeline aligns on its own context) have no shared in-kernel statistics
+        us, n, nj = qctx.kernel_stats(0) if qctx else (0.0, 0, 0)
         W0 = rows * 8                       # sphere width: 8 sensors of `rows` (the sensors are mounted sideways)
         N0 = int(W0 * 0.5 * 60.0 / 180) * W0
         sso = float(np.mean(rec[:, :, OD.R_SSO]))

@@ -1716,7 +1716,9 @@ __global__ void __launch_bounds__(TR_TPB) k_trace(const uint8_t* __restrict__ nb
             int chunk = atomicAdd(&s_nch, 1), pos = 0;
             s_head[m] = chunk;
             auto append = [&](int idx) {
-                if (chunk < TR_NCH) list[chunk * TR_CHUNK + pos] = idx;
+                // past the list's end the chunk index is clamped instead of branched on: s_nch > TR_NCH then, the
+                // whole list is discarded (s_over) and the overflow walk below writes the points
+                list[min(chunk, TR_NCH - 1) * TR_CHUNK + pos] = idx;
                 if (++pos == TR_CHUNK) {
                     const int nc = atomicAdd(&s_nch, 1);
                     if (chunk < TR_NCH) link[chunk] = nc;
@@ -1727,10 +1729,12 @@ __global__ void __launch_bounds__(TR_TPB) k_trace(const uint8_t* __restrict__ nb
             append(start);
             n = 1;
             int cidx = start, dir = dir0;
+            unsigned mc = nb[cidx];
             do {
-                const int nd = trace_next(nb[cidx], dir);
+                const int nd = trace_next(mc, dir);
                 dir = (nd + 4) & 7;
                 cidx += step_off(nd);
+                mc = nb[cidx];   // the next step's mask (cidx is a member pixel): in flight under the bookkeeping
                 append(cidx);
                 if (++n > max_len) { atomicOr(err, 8); break; }
             } while (cidx != start);
