@@ -15,8 +15,8 @@
 //
 // What it provides, all opt-in through this header only:
 //   * Calib360, Frame360, RegisterPhotoICP, RegisterRGBD360, Plane in the global namespace;
-//   * Eigen::Matrix4f as r360::Matrix4f when Eigen itself is not used (RGBD360_WITH_EIGEN makes the façade use the
-//     real Eigen types instead);
+//   * Eigen::Matrix4f and Eigen::Matrix<float,6,6> as r360::Matrix4f / Matrix6f when Eigen itself is not used
+//     (RGBD360_WITH_EIGEN makes the façade use the real Eigen types instead);
 //   * mrpt::format (printf-style std::string) unless MRPT's own header came first;
 //   * PROJECT_SOURCE_PATH = r360_data_dir() (data/) unless the build defines it, so the reference's
 //     "%s/config_files/..." paths resolve to data/config_files/...;
@@ -29,14 +29,25 @@
 
 using r360::Calib360;
 using r360::Frame360;
+using r360::PbMap;
 using r360::Plane;
 using r360::RegisterPhotoICP;
 using r360::RegisterRGBD360;
 
 #if !defined(RGBD360_WITH_EIGEN) && !defined(EIGEN_CORE_H) && !defined(EIGEN_CORE_MODULE_H)
+namespace r360 {
+template <typename Scalar, int Rows, int Cols>
+struct EigenStandIn;                    // only the two fixed-size float matrices of the registration surface
+template <> struct EigenStandIn<float, 4, 4> { typedef Matrix4f type; };
+template <> struct EigenStandIn<float, 6, 6> { typedef Matrix6f type; };
+}  // namespace r360
 namespace Eigen {
 typedef r360::Matrix4f Matrix4f;
-}
+// Eigen::Matrix<float,6,6> (getInfoMat / getHessian, SphereGraphSLAM.cpp:200-201, LoopClosure360.h:314) and
+// Eigen::Matrix<float,4,4>
+template <typename Scalar, int Rows, int Cols, int Options = 0, int MaxRows = Rows, int MaxCols = Cols>
+using Matrix = typename r360::EigenStandIn<Scalar, Rows, Cols>::type;
+}  // namespace Eigen
 #endif
 
 #if !defined(MRPT_FORMAT_H) && !defined(RGBD360_NO_MRPT_FORMAT)

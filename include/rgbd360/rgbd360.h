@@ -40,6 +40,8 @@
 #include <limits>
 #include <ostream>
 #include <map>
+#include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -124,6 +126,13 @@ inline std::ostream& operator<<(std::ostream& os, const MatrixNf<N>& m) {
     }
     return os;
 }
+// scalar * matrix (e.g. registerer.getAreaMatched() * registerer.getInfoMat(), KFsphere_SLAM.cpp:454)
+template <int N>
+inline MatrixNf<N> operator*(float s, const MatrixNf<N>& m) {
+    MatrixNf<N> o;
+    for (int i = 0; i < N * N; ++i) o.v[i] = s * m.v[i];
+    return o;
+}
 typedef MatrixNf<4> Matrix4f;
 typedef MatrixNf<6> Matrix6f;
 #endif
@@ -155,17 +164,23 @@ class Context {
     r360_ctx* h_ = nullptr;
 };
 
-// The context the reference-signature constructors bind to: one per host thread (its own HIP stream), on device
-// $R360_DEVICE (default 0), created on first use and destroyed at thread exit — objects built on a thread must not
-// outlive it.
+// The default contexts of the reference-signature constructors: one per host thread (its own HIP stream), on device
+// $R360_DEVICE (default 0), created on first use.  A thread's default context lives as long as its thread or the
+// last object built on it, whichever is longer: Calib360(Resolution) and the frames built on it hold a reference, so
+// frames built on one thread stay valid after it exits.  RegisterRGBD360(configFile) and RegisterPhotoICP() hold
+// no context of their own: each call runs on the CALLING thread's default context, so an object constructed on one
+// thread and used on another (LoopClosure360's registerer, constructed by the main thread and used by its loop
+// thread, LoopClosure360.h:83-94, 297) never shares a context between threads.  Frames are shared freely: a
+// registration on another thread's context waits for the frames' builds on their own streams.
 inline int default_device() {
     const char* e = std::getenv("R360_DEVICE");
     return e ? std::atoi(e) : 0;
 }
-inline Context& default_context() {
-    thread_local Context ctx(default_device());
+inline const std::shared_ptr<Context>& default_context_ptr() {
+    thread_local std::shared_ptr<Context> ctx = std::make_shared<Context>(default_device());
     return ctx;
 }
+inline Context& default_context() { return *default_context_ptr(); }
 
 // printf-style std::string (the callers' mrpt::format for file names)
 inline std::string format(const char* fmt, ...) {
@@ -184,7 +199,9 @@ class Calib360 {
     // Resolution mode of the device (Calib360.h:62-67): per-sensor images of 480/res x 640/res
     enum Resolution { VGA = 1, QVGA = 2, QQVGA = 4 };
     // Calib360(Resolution res = QVGA) (Calib360.h:70), on the thread's default context
-    explicit Calib360(Resolution res = QVGA) : Calib360(default_context(), 480 / int(res), 640 / int(res)) {}
+    explicit Calib360(Resolution res = QVGA) : Calib360(default_context(), 480 / int(res), 640 / int(res)) {
+        keep_ = default_context_ptr();
+    }
     // rows x cols per sensor (the reference's QVGA default, Calib360.h:73-77)
     explicit Calib360(Context& ctx, int rows = 240, int cols = 320) : ctx_(ctx) {
         check(r360_calib_create(ctx.get(), rows, cols, &h_), "r360_calib_create");
@@ -211,8 +228,11 @@ class Calib360 {
     }
     r360_calib* get() const { return h_; }
     Context& ctx() const { return ctx_; }
+    // the default context this calibration was built on (null for an explicit Context)
+    const std::shared_ptr<Context>& keepAlive() const { return keep_; }
   private:
     Context& ctx_;
+    std::shared_ptr<Context> keep_;
     r360_calib* h_ = nullptr;
 };
 
@@ -227,9 +247,23 @@ struct Plane {                          // mrpt::pbmap::Plane fields used on the
     std::string label;                  // Plane::label (labelization tools), kept by savePlanes
 };
 
+// mrpt::pbmap::PbMap as Frame360::planes holds it (Frame360.h:123): the planes in vPlanes (callers write
+// frame360->planes.vPlanes[i], OnlineOdometryRGBD360.cpp:172,330); size() / operator[] / iteration forward to it
+struct PbMap {
+    std::vector<Plane> vPlanes;
+    size_t size() const { return vPlanes.size(); }
+    bool empty() const { return vPlanes.empty(); }
+    Plane& operator[](size_t i) { return vPlanes[i]; }
+    const Plane& operator[](size_t i) const { return vPlanes[i]; }
+    std::vector<Plane>::iterator begin() { return vPlanes.begin(); }
+    std::vector<Plane>::iterator end() { return vPlanes.end(); }
+    std::vector<Plane>::const_iterator begin() const { return vPlanes.begin(); }
+    std::vector<Plane>::const_iterator end() const { return vPlanes.end(); }
+};
+
 class Frame360 {
   public:
-    explicit Frame360(Calib360* calib) : calib_(calib) {
+    explicit Frame360(Calib360* calib_) : calib(calib_), keep_(calib_->keepAlive()) {
         check(r360_frame_create(calib->ctx().get(), calib->get(), &h_), "r360_frame_create");
         int r, c, sr, sc;
         check(r360_frame_dims(h_, &r, &c, &sr, &sc), "r360_frame_dims");
@@ -246,7 +280,10 @@ class Frame360 {
     void loadFrame(const std::string& path) { check(r360_frame_load_bin(h_, path.c_str()), "loadFrame"); }
     void upload(const uint8_t* bgr8, const uint16_t* depth8) { check(r360_frame_upload(h_, bgr8, depth8), "upload"); }
     void undistort() { check(r360_frame_build(h_, R360_BUILD_UNDISTORT), "undistort"); }
-    void stitchSphericalImage() { check(r360_frame_build(h_, R360_BUILD_SPHERE | R360_BUILD_PYRAMID), "stitch"); }
+    void stitchSphericalImage() {
+        std::lock_guard<std::mutex> lk(build_m_);
+        check(r360_frame_build(h_, R360_BUILD_SPHERE | R360_BUILD_PYRAMID), "stitch");
+    }
     void buildSphereCloud() { check(r360_frame_build(h_, R360_BUILD_UNDISTORT | R360_BUILD_CLOUD), "buildSphereCloud"); }
     void getPlanes() {
         check(r360_frame_build(h_, R360_BUILD_UNDISTORT | R360_BUILD_PLANES), "getPlanes");
@@ -296,15 +333,27 @@ class Frame360 {
     Mat sphereRGB, sphereDepth;
     // copies the sphere's pixels into sphereRGB / sphereDepth (they stay views of this frame)
     void downloadSphere() {
+        ensureSpherePyramid();
         sphereRGB.bytes.resize(size_t(sphereRGB.rows) * sphereRGB.cols * 3);
         sphereDepth.bytes.resize(size_t(sphereDepth.rows) * sphereDepth.cols * 2);
         check(r360_frame_get_sphere(h_, sphereRGB.data(), reinterpret_cast<uint16_t*>(sphereDepth.data())),
               "downloadSphere");
     }
-    std::vector<Plane> planes;          // the frame's PbMap ("planes.vPlanes")
+    PbMap planes;                       // the frame's PbMap (planes.vPlanes)
     Matrix4f pose;
     unsigned id = 0;
+    unsigned node = 0;                  // topological node (submap) of the frame (Frame360.h:101)
+    Calib360* calib;                    // the sensor calibration (Frame360.h:97)
     r360_frame* get() const { return h_; }
+    // the stitched sphere and its pyramid, built once (stitchSphericalImage, or the first setSourceFrame /
+    // setTargetFrame of the frame's sphere views, possibly from another thread)
+    void ensureSpherePyramid() {
+        std::lock_guard<std::mutex> lk(build_m_);
+        unsigned built = 0;
+        check(r360_frame_built(h_, &built), "r360_frame_built");
+        const unsigned need = R360_BUILD_SPHERE | R360_BUILD_PYRAMID;   // the stitch reads the raw depth
+        if ((built & need) != need) check(r360_frame_build(h_, need), "pyramid");
+    }
 
   private:
     void push_labels() {
@@ -316,7 +365,7 @@ class Frame360 {
         check(r360_frame_get_planes(h_, nullptr, 0, &n), "getPlanes");
         std::vector<r360_plane> raw(n > 0 ? n : 1);
         check(r360_frame_get_planes(h_, raw.data(), n, &n), "getPlanes");
-        planes.clear();
+        planes.vPlanes.clear();
         for (int i = 0; i < n; ++i) {
             const r360_plane& r = raw[i];
             Plane p;
@@ -336,10 +385,11 @@ class Frame360 {
                 r360_frame_get_plane_label(h_, i, buf.data(), ll + 1);
                 p.label = buf.data();
             }
-            planes.push_back(p);
+            planes.vPlanes.push_back(p);
         }
     }
-    Calib360* calib_;
+    std::shared_ptr<Context> keep_;     // the default context the frame was built on (see default_context_ptr)
+    std::mutex build_m_;
     r360_frame* h_ = nullptr;
 };
 
@@ -347,9 +397,9 @@ class Frame360 {
 class RegisterPhotoICP {
   public:
     enum costFuncType { PHOTO_CONSISTENCY = 0, DEPTH_CONSISTENCY = 1, PHOTO_DEPTH = 2 };
-    explicit RegisterPhotoICP(Context& ctx) : ctx_(ctx) { r360_icp_default_params(&p_); }
-    // RegisterPhotoICP() (RegisterPhotoICP.h:201), on the thread's default context
-    RegisterPhotoICP() : RegisterPhotoICP(default_context()) {}
+    explicit RegisterPhotoICP(Context& ctx) : ctx_(&ctx) { r360_icp_default_params(&p_); }
+    // RegisterPhotoICP() (RegisterPhotoICP.h:201): every call on the calling thread's default context
+    RegisterPhotoICP() { r360_icp_default_params(&p_); }
     ~RegisterPhotoICP() {
         for (auto& o : own_) { r360_frame_destroy(o.frame); r360_calib_destroy(o.calib); }
     }
@@ -376,7 +426,7 @@ class RegisterPhotoICP {
     bool alignFrames360(const Matrix4f& pose_guess = Matrix4f::Identity(), costFuncType method = PHOTO_CONSISTENCY,
                         int occlusion = 0) {
         float g[6];
-        const int rc = check(r360_align360(ctx_.get(), trg_, src_, pose_guess.data(), method, occlusion,
+        const int rc = check(r360_align360(ctx().get(), trg_, src_, pose_guess.data(), method, occlusion,
                                            &p_, relPose_.data(), hessian_.data(), g, &st_),
                              "alignFrames360");
         std::memcpy(gradient_, g, sizeof g);
@@ -397,9 +447,8 @@ class RegisterPhotoICP {
     const r360_icp_stats& stats() const { return st_; }
     r360_icp_params& params() { return p_; }
   private:
-    static void ensure_pyramid(Frame360& f) {
-        check(r360_frame_build(f.get(), R360_BUILD_UNDISTORT | R360_BUILD_SPHERE | R360_BUILD_PYRAMID), "pyramid");
-    }
+    Context& ctx() const { return ctx_ ? *ctx_ : default_context(); }
+    static void ensure_pyramid(Frame360& f) { f.ensureSpherePyramid(); }
     r360_frame* sphere_frame(int role, Mat& rgb, Mat& depth) {
         if (rgb.frame && rgb.frame == depth.frame) {       // the frame's own sphere views
             Frame360& f = const_cast<Frame360&>(*rgb.frame);
@@ -414,18 +463,18 @@ class RegisterPhotoICP {
         for (auto& x : own_)
             if (x.role == role && x.rows == rgb.rows && x.cols == rgb.cols) o = &x;
         if (!o) {
-            own_.push_back(Own{role, rgb.rows, rgb.cols, nullptr, nullptr});
+            own_.push_back(Own{role, rgb.rows, rgb.cols, nullptr, nullptr, ctx_ ? nullptr : default_context_ptr()});
             o = &own_.back();
-            check(r360_calib_create_sphere(ctx_.get(), rgb.rows, rgb.cols, &o->calib), "sphere calibration");
-            check(r360_frame_create(ctx_.get(), o->calib, &o->frame), "sphere frame");
+            check(r360_calib_create_sphere(ctx().get(), rgb.rows, rgb.cols, &o->calib), "sphere calibration");
+            check(r360_frame_create(ctx().get(), o->calib, &o->frame), "sphere frame");
         }
         check(r360_frame_set_sphere(o->frame, rgb.data(), reinterpret_cast<const uint16_t*>(depth.data()), rgb.rows,
                                     rgb.cols), "setSourceFrame / setTargetFrame");
         return o->frame;
     }
-    struct Own { int role, rows, cols; r360_calib* calib; r360_frame* frame; };
+    struct Own { int role, rows, cols; r360_calib* calib; r360_frame* frame; std::shared_ptr<Context> keep; };
     std::vector<Own> own_;
-    Context& ctx_;
+    Context* ctx_ = nullptr;            // null: the calling thread's default context
     r360_icp_params p_;
     r360_icp_stats st_{};
     r360_frame* src_ = nullptr;
@@ -442,12 +491,9 @@ class RegisterRGBD360 {
     // matcher.configLocaliser.load_params(configFile) (:97-100): the [global]/[unary]/[binary] thresholds of
     // the mrpt-pbmap ini; without a file, configLocaliser_sphericalOdometry.ini's values
     // RegisterRGBD360(configFile) (RegisterRGBD360.h:97), on the thread's default context
-    explicit RegisterRGBD360(const std::string& configFile = "") : RegisterRGBD360(default_context(), configFile) {}
-    RegisterRGBD360(Context& ctx, const std::string& configFile = "") : ctx_(ctx), config_(configFile) {
-        std::memset(informationM_.data(), 0, sizeof(float) * 36);
-        r360_match_params_default(&match_);
-        if (!configFile.empty()) check(r360_match_params_load_ini(configFile.c_str(), &match_), "load_params");
-    }
+    // every call on the calling thread's default context
+    explicit RegisterRGBD360(const std::string& configFile = "") : config_(configFile) { init(); }
+    RegisterRGBD360(Context& ctx, const std::string& configFile = "") : ctx_(&ctx), config_(configFile) { init(); }
     r360_match_params& matchParams() { return match_; }
     void setReference(Frame360* ref, size_t max_match_planes = 0) { ref_ = ref; max_ = max_match_planes; done_ = false; }
     void setTarget(Frame360* trg, size_t max_match_planes = 0) { trg_ = trg; max_ = max_match_planes; done_ = false; }
@@ -459,8 +505,8 @@ class RegisterRGBD360 {
         done_ = true;
         std::vector<int> pairs(512);
         int n = 0;
-        check(r360_ctx_set_match_params(ctx_.get(), &match_), "matcher thresholds");
-        const int rc = check(r360_register_pbmap(ctx_.get(), ref_->get(), trg_->get(), max_, registMode,
+        check(r360_ctx_set_match_params(ctx().get(), &match_), "matcher thresholds");
+        const int rc = check(r360_register_pbmap(ctx().get(), ref_->get(), trg_->get(), max_, registMode,
                                                  rigidTransf_.data(), informationM_.data(), pairs.data(), 256, &n,
                                                  &areaMatched_, &areaSource, &areaTarget),
                              "RegisterPbMap");
@@ -497,8 +543,8 @@ class RegisterRGBD360 {
                   const Matrix4f& guess = Matrix4f::Identity(), size_t max_match_planes = 25,
                   registrationType registMode = PLANAR_3DoF) {
         r360_icp_stats st;
-        check(r360_ctx_set_match_params(ctx_.get(), &match_), "matcher thresholds");
-        const int rc = check(r360_register(ctx_.get(), frame1->get(), frame2->get(), guess.data(), &icp,
+        check(r360_ctx_set_match_params(ctx().get(), &match_), "matcher thresholds");
+        const int rc = check(r360_register(ctx().get(), frame1->get(), frame2->get(), guess.data(), &icp,
                                            max_match_planes, registMode, pose.data(), informationM_.data(), &st),
                              "Register");
         return rc == 0;
@@ -511,7 +557,7 @@ class RegisterRGBD360 {
                                registrationType registMode = DEFAULT_6DoF) {
         check(r360_frame_build(frame1->get(), R360_BUILD_SENSOR_PYRAMID), "setTargetFrame (sensor pyramids)");
         check(r360_frame_build(frame2->get(), R360_BUILD_SENSOR_PYRAMID), "setSourceFrame (sensor pyramids)");
-        const int rc = check(r360_register_dense(ctx_.get(), frame1->get(), frame2->get(), pose_estim.data(), method,
+        const int rc = check(r360_register_dense(ctx().get(), frame1->get(), frame2->get(), pose_estim.data(), method,
                                                  registMode, nullptr, rigidTransf_.data(), informationM_.data(),
                                                  &dense_st_),
                              "RegisterDensePhotoICP");
@@ -521,8 +567,14 @@ class RegisterRGBD360 {
     const r360_dense_stats& denseStats() const { return dense_st_; }
     float areaSource = 0.f, areaTarget = 0.f;
   private:
+    void init() {
+        std::memset(informationM_.data(), 0, sizeof(float) * 36);
+        r360_match_params_default(&match_);
+        if (!config_.empty()) check(r360_match_params_load_ini(config_.c_str(), &match_), "load_params");
+    }
+    Context& ctx() const { return ctx_ ? *ctx_ : default_context(); }
     r360_dense_stats dense_st_{};
-    Context& ctx_;
+    Context* ctx_ = nullptr;            // null: the calling thread's default context
     std::string config_;
     Frame360* ref_ = nullptr;
     Frame360* trg_ = nullptr;

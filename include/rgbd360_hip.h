@@ -102,6 +102,8 @@ int  r360_frame_get_timestamp(const r360_frame* f, uint64_t* ts);
 int  r360_frame_build(r360_frame* f, unsigned flags);
 int  r360_frame_build_async(r360_frame* f, unsigned flags);
 int  r360_frame_dims(const r360_frame* f, int* rows, int* cols, int* sph_rows, int* sph_cols);
+/* The R360_BUILD_* stages the frame's current images have been through (an upload or load clears them). */
+int  r360_frame_built(const r360_frame* f, unsigned* flags);
 /* sphereRGB (BGR u8) / sphereDepth (u16 range mm) (Frame360.h:104-107). */
 int  r360_frame_get_sphere(r360_frame* f, uint8_t* bgr, uint16_t* depth);
 /* Undistorted per-sensor depth in metres (CloudRGBD_Ext::m_depthEigUndistort). */
@@ -191,7 +193,9 @@ int r360_align360_batch_result(r360_ctx* ctx, float* pose_out, float* H_out, flo
  * r360_align360_batch call; the next batch accumulates while one runs.  submit records the frames' build
  * work (their contexts' streams) and returns a ticket at once; collect waits for that job and returns
  * what r360_align360_result would (0, 1 = ILL-POSED, < 0 error).  The frames must stay unmodified until
- * their job is collected.  Every ticket must be collected once.  Thread-safe. */
+ * their job is collected: a batch waits on each frame's build event, which a rebuild re-records, so a frame
+ * rebuilt between submit and dispatch fails the job with an error instead of aligning against the newer build.
+ * Every ticket must be collected once.  Thread-safe. */
 typedef struct r360_dense_queue r360_dense_queue;
 int  r360_dense_queue_create(int device, int max_batch, r360_dense_queue** out);
 void r360_dense_queue_destroy(r360_dense_queue* q);
@@ -331,7 +335,7 @@ typedef struct {
     float height_threshold;         /* [binary] relative height of parallel planes (m)                      */
     float cos_angle_parallel;       /* [binary]                                                             */
     float planar_normal_angle;      /* planar modes: vertical-normal tolerance (deg; not an ini key, 10)    */
-    long  max_nodes;                /* interpretation-tree node budget (deterministic cut-off)              */
+    long  max_nodes;                /* interpretation-tree node budget: a guard against pathological inputs  */
 } r360_match_params;
 /* The configLocaliser_sphericalOdometry.ini values (the odometry apps' file). */
 void r360_match_params_default(r360_match_params* m);
@@ -340,6 +344,15 @@ void r360_match_params_default(r360_match_params* m);
 int  r360_match_params_load_ini(const char* path, r360_match_params* m);
 int  r360_ctx_set_match_params(r360_ctx* ctx, const r360_match_params* m);
 int  r360_ctx_get_match_params(const r360_ctx* ctx, r360_match_params* m);
+/* The interpretation-tree searches run on ctx (every RegisterPbMap), how many of them stopped at max_nodes, and the
+ * most nodes one search visited.  MRPT's SubgraphMatcher (RegisterRGBD360.h:294) searches exhaustively; this one
+ * prunes with forward checking (exhaustive result), so a search that reaches the budget is the only way its result
+ * can differ from the exhaustive one — and it is counted here, never silent. */
+int  r360_ctx_match_stats(r360_ctx* ctx, long* calls, long* truncated, long* max_nodes);
+/* That search alone over given tables (host only; the layout r360_pbmap_match_tables returns, areas of the
+ * reference planes): best[i] = matched target of reference i or -1.  Returns 1 if max_nodes stopped it, 0 if not. */
+int  r360_match_tree_search(int ns, int nt, const uint8_t* unary, const uint64_t* binary, int words,
+                            const double* area, long max_nodes, int* best, long* nodes);
 
 /* RegisterPbMap(ref, trg, max_match_planes, mode) (:276-337): returns 1 (good alignment) or 0
  * (insufficient matching / ill-conditioned; pose and info are then left untouched, :306-310).

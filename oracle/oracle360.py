@@ -139,6 +139,8 @@ def lib() -> C.CDLL:
             "orc_pbmap_get": (C.c_int, [vp, C.c_int, C.POINTER(Plane), fp, C.c_int]),
             "orc_match_tables": (C.c_int, [vp, vp, C.c_size_t, C.c_int, ip, ip, ip, ip, vp, vp, C.c_int, vp]),
             "orc_register_pbmap": (C.c_int, [vp, vp, C.c_size_t, C.c_int, fp, fp, ip, C.c_int, ip, fp, fp, fp, vp]),
+            "orc_last_match_stats": (None, [C.POINTER(C.c_long), ip]),
+            "orc_tree_search": (C.c_int, [C.c_int, C.c_int, vp, vp, C.c_int, vp, C.c_long, ip, C.POINTER(C.c_long)]),
         }
         for k, (r, a) in sig.items():
             f = getattr(L, k)
@@ -623,6 +625,20 @@ def match_tables(ref: PbMap, trg: PbMap, max_match_planes=25, mode=PLANAR_3DoF, 
                 binary=bi[:n * m * w].reshape(n * m, w).copy(), words=w)
 
 
+def tree_search(unary: np.ndarray, binary: np.ndarray, area, max_nodes: int = 4000000):
+    """The oracle's interpretation tree alone: (best [ns], nodes, truncated)."""
+    unary = np.ascontiguousarray(unary, np.uint8)
+    ns, nt = unary.shape
+    words = (ns * nt + 63) // 64
+    binary = np.ascontiguousarray(binary, np.uint64).reshape(-1)
+    area = np.ascontiguousarray(area, np.float64)
+    best = np.zeros(max(ns, 1), np.int32)
+    nodes = C.c_long()
+    rc = lib().orc_tree_search(ns, nt, unary.ctypes.data, binary.ctypes.data, words, area.ctypes.data, max_nodes,
+                               best.ctypes.data_as(C.POINTER(C.c_int)), C.byref(nodes))
+    return best[:ns], nodes.value, bool(rc)
+
+
 def register_pbmap(ref: PbMap, trg: PbMap, max_match_planes=25, mode=PLANAR_3DoF, params=None):
     pose = np.zeros(16, np.float32)
     info = np.zeros(36, np.float32)
@@ -632,6 +648,9 @@ def register_pbmap(ref: PbMap, trg: PbMap, max_match_planes=25, mode=PLANAR_3DoF
     rc = lib().orc_register_pbmap(ref.h, trg.h, max_match_planes, mode, _f(pose), _f(info), pairs.ctypes.data_as(ip),
                                   256, C.byref(n), C.byref(am), C.byref(as_), C.byref(at),
                                   C.byref(params) if params is not None else None)
+    nodes, trunc = C.c_long(), C.c_int()
+    lib().orc_last_match_stats(C.byref(nodes), C.byref(trunc))
     return dict(good=rc, pose=from16(pose), info=info.reshape(6, 6).T.copy(),
                 matches={int(pairs[2 * k]): int(pairs[2 * k + 1]) for k in range(min(n.value, 256))},
-                area_matched=am.value, area_src=as_.value, area_trg=at.value)
+                area_matched=am.value, area_src=as_.value, area_trg=at.value, nodes=nodes.value,
+                truncated=bool(trunc.value))

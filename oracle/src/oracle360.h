@@ -219,6 +219,11 @@ int   orc_match_tables(const void* href, const void* htrg, size_t max_match_plan
 int   orc_register_pbmap(const void* href, const void* htrg, size_t max_match_planes, int mode, float pose[16],
                          float info[36], int* pairs, int pair_cap, int* n_match, float* area_matched,
                          float* area_src, float* area_trg, const orc_match_params* mp);
+/* Nodes the calling thread's last orc_register_pbmap search visited and whether the node budget stopped it. */
+void  orc_last_match_stats(long* nodes, int* truncated);
+/* The interpretation tree alone over given tables; returns 1 if max_nodes stopped it. */
+int   orc_tree_search(int ns, int nt, const uint8_t* unary, const uint64_t* binary, int words, const double* area,
+                      long max_nodes, int* best, long* nodes);
 
 #ifdef __cplusplus
 }

@@ -632,35 +632,62 @@ Tables build_tables(const std::vector<Plane>& S, const std::vector<int>& sid, co
     return tb;
 }
 
+// Interpretation tree (App. C.4): references in order, each tries its targets ascending and then "unmatched";
+// best = most matches, ties by matched reference area, first found among equals.  Forward checking keeps, per
+// reference below the current depth, the set of targets still allowed by the unary table and by the binary table
+// against every assignment made above it; the bound counts only references whose set is non-empty.  The cuts are
+// sound, so the search returns the exhaustive optimum unless the node budget stops it (then `truncated`).
 struct Search {
     const Tables* tb;
-    std::vector<double> area_s, rem_area;
+    std::vector<double> area_s;
+    std::vector<std::vector<std::vector<bool>>> doms;   // doms[depth][ref][target]
     std::vector<int> cur, best;         // cur[i] = target index or -1
     int n_cur = 0, n_best = 0;
     double a_cur = 0, a_best = 0;
     long nodes = 0, max_nodes = 0;
+    bool truncated = false;
+    void start() {
+        const int ns = tb->ns, nt = tb->nt;
+        doms.assign(ns + 1, std::vector<std::vector<bool>>(ns, std::vector<bool>(nt, false)));
+        for (int i = 0; i < ns; ++i)
+            for (int t = 0; t < nt; ++t) doms[0][i][t] = tb->unary[size_t(i) * nt + t] != 0;
+        cur.assign(ns, -1);
+        best.assign(ns, -1);
+        rec(0);
+    }
     void rec(int i) {
-        if (++nodes > max_nodes) return;
-        const int ns = tb->ns;
+        if (++nodes > max_nodes) { truncated = true; return; }
+        const int ns = tb->ns, nt = tb->nt;
         if (i == ns) {
             if (n_cur > n_best || (n_cur == n_best && a_cur > a_best)) {
                 best = cur; n_best = n_cur; a_best = a_cur;
             }
             return;
         }
-        const int remaining = ns - i;
-        if (n_cur + remaining < n_best) return;
-        if (n_cur + remaining == n_best && a_cur + rem_area[i] <= a_best) return;
-        for (int t = 0; t < tb->nt; ++t) {
-            if (!tb->unary[size_t(i) * tb->nt + t]) continue;
-            bool ok = true;
-            for (int k = 0; k < i && ok; ++k)
-                if (cur[k] >= 0) ok = (cur[k] != t) && tb->b(i, t, k, cur[k]);
-            if (!ok) continue;
+        const auto& D = doms[i];
+        int open = 0, free_targets = 0;
+        double open_area = 0;
+        for (int r = i; r < ns; ++r)
+            if (std::find(D[r].begin(), D[r].end(), true) != D[r].end()) { ++open; open_area += area_s[r]; }
+        for (int u = 0; u < nt; ++u) {
+            bool any = false;
+            for (int r = i; r < ns && !any; ++r) any = D[r][u];
+            free_targets += any ? 1 : 0;
+        }
+        open = std::min(open, free_targets);      // each target can still take one reference
+        if (n_cur + open < n_best) return;
+        if (n_cur + open == n_best && a_cur + open_area <= a_best) return;
+        auto& N = doms[i + 1];
+        for (int t = 0; t < nt; ++t) {
+            if (!D[i][t]) continue;
+            for (int r = i + 1; r < ns; ++r)
+                for (int u = 0; u < nt; ++u) N[r][u] = D[r][u] && u != t && tb->b(r, u, i, t);
             cur[i] = t; n_cur++; a_cur += area_s[i];
             rec(i + 1);
             cur[i] = -1; n_cur--; a_cur -= area_s[i];
+            if (truncated) return;
         }
+        for (int r = i + 1; r < ns; ++r) N[r] = D[r];
         rec(i + 1);
     }
 };
@@ -823,6 +850,31 @@ int orc_match_tables(const void* href, const void* htrg, size_t max_match_planes
     return tb.words;
 }
 
+// The search alone over given tables (unary [ns][nt], binary [(i*nt+j)][words], reference areas)
+int orc_tree_search(int ns, int nt, const uint8_t* unary, const uint64_t* binary, int words, const double* area,
+                    long max_nodes, int* best, long* nodes) {
+    Tables tb;
+    tb.ns = ns; tb.nt = nt; tb.words = words;
+    tb.unary.assign(unary, unary + size_t(ns) * nt);
+    tb.bin.assign(binary, binary + size_t(ns) * nt * words);
+    Search sr;
+    sr.tb = &tb;
+    sr.max_nodes = max_nodes;
+    sr.area_s.assign(area, area + ns);
+    sr.start();
+    for (int i = 0; i < ns; ++i) best[i] = sr.best[i];
+    *nodes = sr.nodes;
+    return sr.truncated ? 1 : 0;
+}
+
+// nodes visited by the last orc_register_pbmap search on this thread and whether the budget stopped it
+static thread_local long g_last_nodes = 0;
+static thread_local int g_last_truncated = 0;
+void orc_last_match_stats(long* nodes, int* truncated) {
+    if (nodes) *nodes = g_last_nodes;
+    if (truncated) *truncated = g_last_truncated;
+}
+
 int orc_register_pbmap(const void* href, const void* htrg, size_t max_match_planes, int mode, float pose[16],
                        float info[36], int* pairs, int pair_cap, int* n_match, float* area_matched, float* area_src,
                        float* area_trg, const orc_match_params* mp) {
@@ -835,12 +887,10 @@ int orc_register_pbmap(const void* href, const void* htrg, size_t max_match_plan
     sr.tb = &tb;
     sr.max_nodes = c.max_nodes;
     sr.area_s.resize(si.size());
-    sr.rem_area.assign(si.size() + 1, 0.0);
     for (size_t i = 0; i < si.size(); ++i) sr.area_s[i] = S[si[i]].area;
-    for (int i = int(si.size()) - 1; i >= 0; --i) sr.rem_area[i] = sr.rem_area[i + 1] + sr.area_s[i];
-    sr.cur.assign(si.size(), -1);
-    sr.best.assign(si.size(), -1);
-    sr.rec(0);
+    sr.start();
+    g_last_nodes = sr.nodes;
+    g_last_truncated = sr.truncated ? 1 : 0;
     std::map<unsigned, unsigned> best;
     for (size_t i = 0; i < si.size(); ++i)
         if (sr.best[i] >= 0) best[unsigned(si[i])] = unsigned(ti[sr.best[i]]);

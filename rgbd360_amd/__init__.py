@@ -182,6 +182,7 @@ _SIGS = [
     ("r360_frame_build", C.c_int, [_P, C.c_uint]),
     ("r360_frame_build_async", C.c_int, [_P, C.c_uint]),
     ("r360_frame_dims", C.c_int, [_P, _IP, _IP, _IP, _IP]),
+    ("r360_frame_built", C.c_int, [_P, C.POINTER(C.c_uint)]),
     ("r360_frame_get_sphere", C.c_int, [_P, _P, _P]),
     ("r360_frame_get_depth_m", C.c_int, [_P, _P]),
     ("r360_frame_get_level", C.c_int, [_P, C.c_int, _IP, _IP, _P, _P, _P, _P, _P, _P]),
@@ -226,6 +227,8 @@ _SIGS = [
     ("r360_match_params_load_ini", C.c_int, [C.c_char_p, C.POINTER(MatchParams)]),
     ("r360_ctx_set_match_params", C.c_int, [_P, C.POINTER(MatchParams)]),
     ("r360_ctx_get_match_params", C.c_int, [_P, C.POINTER(MatchParams)]),
+    ("r360_ctx_match_stats", C.c_int, [_P, C.POINTER(C.c_long), C.POINTER(C.c_long), C.POINTER(C.c_long)]),
+    ("r360_match_tree_search", C.c_int, [C.c_int, C.c_int, _P, _P, C.c_int, _P, C.c_long, _P, C.POINTER(C.c_long)]),
     ("r360_batch_set_match_params", C.c_int, [_P, C.POINTER(MatchParams)]),
     ("r360_register_pbmap", C.c_int, [_P, _P, _P, C.c_size_t, C.c_int, _FP, _FP, _IP, C.c_int, _IP, _FP, _FP, _FP]),
     ("r360_register", C.c_int, [_P, _P, _P, _FP, C.POINTER(IcpParams), C.c_size_t, C.c_int, _FP, _FP,
@@ -392,6 +395,12 @@ class Context:
 
     def kernel_time_reset(self):
         _check(lib().r360_ctx_kernel_time_reset(self.h), "kernel_time_reset")
+
+    def match_stats(self):
+        """(interpretation-tree searches, searches stopped by the node budget, most nodes of one search) on this ctx."""
+        a, b, c = C.c_long(), C.c_long(), C.c_long()
+        _check(lib().r360_ctx_match_stats(self.h, C.byref(a), C.byref(b), C.byref(c)), "match_stats")
+        return a.value, b.value, c.value
 
     def close(self):
         if self.h:
@@ -1082,6 +1091,22 @@ class RegisterPhotoICP:
                                        C.byref(self.params), H.ctypes.data_as(_DP), g.ctypes.data_as(_DP),
                                        C.byref(e), C.byref(nv), C.byref(nvis)), "icp_eval_occ")
         return H.reshape(6, 6), g, e.value, nv.value, nvis.value
+
+
+def match_tree_search(unary: np.ndarray, binary: np.ndarray, area, max_nodes: int = 4000000):
+    """The interpretation-tree search alone (host only): unary [ns, nt] bool, binary [ns * nt, words] uint64 (bit k * nt
+    + l of row i * nt + j: references i, k matched to targets j, l are consistent), area [ns].  Returns (best [ns]
+    target or -1, nodes, truncated)."""
+    unary = np.ascontiguousarray(unary, np.uint8)
+    ns, nt = unary.shape
+    words = (ns * nt + 63) // 64
+    binary = np.ascontiguousarray(binary, np.uint64).reshape(ns * nt, words) if ns * nt else np.zeros((0, 0), np.uint64)
+    area = np.ascontiguousarray(area, np.float64)
+    best = np.zeros(max(ns, 1), np.int32)
+    nodes = C.c_long()
+    rc = _check(lib().r360_match_tree_search(ns, nt, _vptr(unary), _vptr(binary), words, _vptr(area), max_nodes,
+                                             _vptr(best), C.byref(nodes)), "match_tree_search")
+    return best[:ns], nodes.value, bool(rc)
 
 
 def refine_eval(state: np.ndarray, mask: np.ndarray, rb: int = 0, return_fallbacks: bool = False):

@@ -54,6 +54,7 @@ struct r360_dense_queue {
         r360_icp_params p{};
         hipEvent_t ev[2] = {nullptr, nullptr};   // the frames' builds (their build events, or the streams at submit)
         bool own[2] = {false, false};            // ev[e] came from ev_free (the frames' build events are not ours)
+        unsigned gen[2] = {0, 0};                // the frames' build generations when ev[e] was their build event
         int nev = 0;
         int reg = 0, good = 0;                   // Register(): PbMap outcome and information
         float info[36];
@@ -124,13 +125,23 @@ static void dispatcher(r360_dense_queue* q) {
         const int method = first.method;
         const r360_icp_params p = first.p;
         std::vector<hipEvent_t> evs;
+        int rc = 0;
         for (long t : b.take) {
             const r360_dense_queue::Job& J = q->jobs[t];
-            for (int e = 0; e < J.nev; ++e) evs.push_back(J.ev[e]);
+            for (int e = 0; e < J.nev; ++e) {
+                evs.push_back(J.ev[e]);
+                // a frame's build event is re-recorded by every rebuild: the job's frames must not have been
+                // rebuilt between its submit and this dispatch (the callers collect a pair before refilling its
+                // buffers), or the batch would wait on the wrong build
+                const r360_frame* f = e == 0 ? J.trg : J.src;
+                if (!J.own[e] && f->build_gen.load(std::memory_order_acquire) != J.gen[e]) {
+                    r360_set_error("dense queue: a frame was rebuilt while its alignment was pending");
+                    rc = -1;
+                }
+            }
         }
         lk.unlock();
 
-        int rc = 0;
         for (int part = 0; part < (b.n0 < n ? 2 : 1) && rc == 0; ++part) {
             r360_ctx* c = q->cx[part ? 1 : b.slot];
             const int j0 = part ? b.n0 : 0, nj = part ? n - b.n0 : b.n0;
@@ -304,7 +315,11 @@ static int queue_submit(r360_dense_queue* q, r360_frame* trg, r360_frame* src, c
     const int ns = trg == src ? 1 : 2;
     hipEvent_t ev[2] = {nullptr, nullptr};
     bool own[2] = {false, false};
-    for (int i = 0; i < ns; ++i) ev[i] = frame_build_event(fs[i]);
+    unsigned gen[2] = {0, 0};
+    for (int i = 0; i < ns; ++i) {
+        gen[i] = fs[i]->build_gen.load(std::memory_order_acquire);
+        ev[i] = frame_build_event(fs[i]);
+    }
     {
         std::lock_guard<std::mutex> lk(q->m);
         for (int i = 0; i < ns; ++i)
@@ -323,6 +338,7 @@ static int queue_submit(r360_dense_queue* q, r360_frame* trg, r360_frame* src, c
         J.method = method;
         J.p = *p;
         J.ev[0] = ev[0]; J.ev[1] = ev[1]; J.own[0] = own[0]; J.own[1] = own[1]; J.nev = ns;
+        J.gen[0] = gen[0]; J.gen[1] = gen[1];
         J.reg = reg; J.good = good;
         if (info) memcpy(J.info, info, sizeof J.info);
         q->pending.push_back(t);

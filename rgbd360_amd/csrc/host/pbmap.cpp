@@ -690,34 +690,83 @@ int gpu_tables(r360_ctx* ctx, const std::vector<HPlane>& S, const std::vector<in
     return event_wait(ctx->mwait_ev);
 }
 
-// interpretation tree: depth-first over reference planes; largest consistent set, ties by matched
-// reference area; deterministic node budget
+// interpretation tree: depth-first over reference planes (targets ascending, then "no match"); the largest consistent
+// set wins, ties by matched reference area, the first one found in that order among equals.  Forward checking: each
+// reference plane below the current depth keeps its domain, the targets still consistent (unary, distinct, binary)
+// with every assignment above it, so a branch is cut as soon as the planes that can still match cannot beat the best
+// set.  Every cut is sound (an upper bound on what the branch can add), so the result is the exhaustive search's;
+// the node budget (r360_match_params::max_nodes) only guards against pathological inputs, and a search that
+// reaches it is counted (r360_ctx_match_stats) instead of passing silently.
 struct Tree {
     const Tables* tb = nullptr;
-    std::vector<double> area, rest;
+    std::vector<double> area;
+    int W = 1;                            // 64-bit words per target set
+    std::vector<uint64_t> fc;             // [(k * nt + l) * ns + i][W]: targets t of reference i consistent with k -> l
+    std::vector<uint8_t> fc_done;         // [(k * nt + l)]: fc rows computed (on first use)
+    std::vector<uint64_t> dom;            // [depth][ns][W] domains at each depth
     std::vector<int> cur, best;
-    int n_cur = 0, n_best = 0;
+    int ns = 0, nt = 0, n_cur = 0, n_best = 0;
     double a_cur = 0, a_best = 0;
     long nodes = 0, budget = 4000000;
+    bool truncated = false;
+    void init() {
+        ns = tb->ns; nt = tb->nt;
+        W = std::max(1, (nt + 63) / 64);
+        fc.assign((size_t)ns * nt * ns * W, 0);
+        fc_done.assign((size_t)ns * nt, 0);
+        dom.assign((size_t)(ns + 1) * ns * W, 0);
+        for (int i = 0; i < ns; ++i)
+            for (int t = 0; t < nt; ++t)
+                if (tb->unary[(size_t)i * nt + t]) dom[(size_t)i * W + t / 64] |= 1ull << (t % 64);
+        cur.assign(ns, -1);
+        best.assign(ns, -1);
+    }
+    const uint64_t* fc_row(int k, int l) {
+        uint64_t* r = &fc[(size_t)(k * nt + l) * ns * W];
+        if (!fc_done[(size_t)k * nt + l]) {
+            for (int i = k + 1; i < ns; ++i)
+                for (int t = 0; t < nt; ++t)
+                    if (t != l && tb->pair_ok(i, t, k, l)) r[(size_t)i * W + t / 64] |= 1ull << (t % 64);
+            fc_done[(size_t)k * nt + l] = 1;
+        }
+        return r;
+    }
     void go(int i) {
-        if (++nodes > budget) return;
-        if (i == tb->ns) {
+        if (++nodes > budget) { truncated = true; return; }
+        if (i == ns) {
             if (n_cur > n_best || (n_cur == n_best && a_cur > a_best)) { best = cur; n_best = n_cur; a_best = a_cur; }
             return;
         }
-        const int left = tb->ns - i;
-        if (n_cur + left < n_best) return;
-        if (n_cur + left == n_best && a_cur + rest[i] <= a_best) return;
-        for (int t = 0; t < tb->nt; ++t) {
-            if (!tb->unary[(size_t)i * tb->nt + t]) continue;
-            bool ok = true;
-            for (int k = 0; k < i && ok; ++k)
-                if (cur[k] >= 0) ok = cur[k] != t && tb->pair_ok(i, t, k, cur[k]);
-            if (!ok) continue;
-            cur[i] = t; ++n_cur; a_cur += area[i];
-            go(i + 1);
-            cur[i] = -1; --n_cur; a_cur -= area[i];
+        const uint64_t* D = &dom[(size_t)i * ns * W];   // domains of references i..ns-1 at this depth
+        // references with a non-empty domain, and the distinct targets those domains hold, both bound the matches
+        // still possible (a reference takes one target, a target one reference)
+        int left = 0, targets = 0;
+        double rest = 0;
+        for (int w = 0; w < W; ++w) {
+            uint64_t any = 0;
+            for (int r = i; r < ns; ++r) any |= D[(size_t)r * W + w];
+            targets += __builtin_popcountll(any);
         }
+        for (int r = i; r < ns; ++r) {
+            bool any = false;
+            for (int w = 0; w < W; ++w) any = any || D[(size_t)r * W + w] != 0;
+            if (any) { ++left; rest += area[r]; }
+        }
+        left = std::min(left, targets);
+        if (n_cur + left < n_best) return;
+        if (n_cur + left == n_best && a_cur + rest <= a_best) return;
+        uint64_t* Dn = &dom[(size_t)(i + 1) * ns * W];
+        for (int w = 0; w < W; ++w)
+            for (uint64_t m = D[(size_t)i * W + w]; m; m &= m - 1) {
+                const int t = w * 64 + __builtin_ctzll(m);
+                const uint64_t* F = fc_row(i, t);
+                for (size_t x = (size_t)(i + 1) * W; x < (size_t)ns * W; ++x) Dn[x] = D[x] & F[x];
+                cur[i] = t; ++n_cur; a_cur += area[i];
+                go(i + 1);
+                cur[i] = -1; --n_cur; a_cur -= area[i];
+                if (truncated) return;
+            }
+        for (size_t x = (size_t)(i + 1) * W; x < (size_t)ns * W; ++x) Dn[x] = D[x];
         go(i + 1);
     }
 };
@@ -808,6 +857,27 @@ int ready(r360_frame* f) {
 
 }  // namespace
 
+// The interpretation tree alone over given tables (host only, no device): best[i] = target of reference i or -1.
+// Returns 1 when the node budget stopped the search, 0 when it ran to the end.
+extern "C" int r360_match_tree_search(int ns, int nt, const uint8_t* unary, const uint64_t* binary, int words,
+                                      const double* area, long max_nodes, int* best, long* nodes) {
+    CHECK_ARG(ns >= 0 && nt >= 0 && (ns == 0 || (unary && area && best)) && max_nodes > 0, "bad arguments");
+    CHECK_ARG(words == (ns * nt + 63) / 64 && (ns * nt == 0 || binary), "binary table: words != ceil(ns * nt / 64)");
+    Tables tb;
+    tb.ns = ns; tb.nt = nt; tb.words = words;
+    tb.unary = unary;
+    tb.bin = reinterpret_cast<const unsigned long long*>(binary);
+    Tree tr;
+    tr.tb = &tb;
+    tr.budget = max_nodes;
+    tr.area.assign(area, area + ns);
+    tr.init();
+    tr.go(0);
+    for (int i = 0; i < ns; ++i) best[i] = tr.best[i];
+    if (nodes) *nodes = tr.nodes;
+    return tr.truncated ? 1 : 0;
+}
+
 extern "C" int r360_frame_get_planes(r360_frame* f, r360_plane* out, int cap, int* n) {
     if (int rc = ready(f)) return rc;
     const auto& P = f->pbmap->planes;
@@ -890,12 +960,13 @@ extern "C" int r360_register_pbmap(r360_ctx* ctx, r360_frame* ref, r360_frame* t
     tr.tb = &tb;
     tr.budget = ctx->match.max_nodes;
     tr.area.resize(si.size());
-    tr.rest.assign(si.size() + 1, 0.0);
     for (size_t i = 0; i < si.size(); ++i) tr.area[i] = S[si[i]].area;
-    for (int i = int(si.size()) - 1; i >= 0; --i) tr.rest[i] = tr.rest[i + 1] + tr.area[i];
-    tr.cur.assign(si.size(), -1);
-    tr.best.assign(si.size(), -1);
+    tr.init();
     tr.go(0);
+    ctx->match_calls.fetch_add(1, std::memory_order_relaxed);
+    if (tr.truncated) ctx->match_truncated.fetch_add(1, std::memory_order_relaxed);
+    for (long m = ctx->match_nodes_max.load(std::memory_order_relaxed); tr.nodes > m;)
+        if (ctx->match_nodes_max.compare_exchange_weak(m, tr.nodes)) break;
     std::map<unsigned, unsigned> best;
     for (size_t i = 0; i < si.size(); ++i)
         if (tr.best[i] >= 0) best[unsigned(si[i])] = unsigned(ti[tr.best[i]]);
@@ -981,6 +1052,14 @@ extern "C" int r360_ctx_set_match_params(r360_ctx* ctx, const r360_match_params*
     CHECK_ARG(ctx && m, "null arg");
     CHECK_ARG(m->max_nodes > 0, "max_nodes must be positive");
     ctx->match = *m;
+    return 0;
+}
+
+extern "C" int r360_ctx_match_stats(r360_ctx* ctx, long* calls, long* truncated, long* max_nodes) {
+    CHECK_ARG(ctx, "null ctx");
+    if (calls) *calls = ctx->match_calls.load();
+    if (truncated) *truncated = ctx->match_truncated.load();
+    if (max_nodes) *max_nodes = ctx->match_nodes_max.load();
     return 0;
 }
 

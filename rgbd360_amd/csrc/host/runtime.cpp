@@ -63,23 +63,34 @@ static std::string calib_dir_or_default(const char* dir, const char* sub) {
 // whole wait even on a blocking-sync event (measured: every per-frame assembly thread and pipeline thread
 // of the bench burned its wait, 15 of 16 host cores at 16 pipelines), and a sleeping poll gives the cores
 // back to the PbMap host stages; the added latency is at most one sleep (<= 100 us) on ms-scale waits.
-// Polls e with short sleeps.  The waiting thread's timer slack is set to 1 us first (its own setting, per thread):
-// with Linux's default 50 us slack a 20 us sleep overslept to ~70 us, so every short wait (a lone alignment's
-// result, RegisterPbMap's match tables) paid up to that much after the GPU had finished.
+// Polls e with short sleeps.  While it sleeps, the waiting thread's timer slack is 1 us (its own setting, per
+// thread): with Linux's default 50 us slack a 20 us sleep overslept to ~70 us, so every short wait (a lone
+// alignment's result, RegisterPbMap's match tables) paid up to that much after the GPU had finished.  The caller's
+// own slack is restored before returning (the thread may be the application's).
 int event_wait(hipEvent_t e) {
-    static thread_local bool slack_set = false;
-    if (!slack_set) {
-        (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0UL, 0UL, 0UL);
-        slack_set = true;
+    const hipError_t r0 = hipEventQuery(e);
+    if (r0 == hipSuccess) return 0;
+    if (r0 != hipErrorNotReady) {
+        r360_set_error("hipEventQuery -> %s", hipGetErrorString(r0));
+        return -1;
     }
+    struct Slack {
+        long old;
+        Slack() : old(prctl(PR_GET_TIMERSLACK, 0UL, 0UL, 0UL, 0UL)) {
+            if (old != 1000) (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0UL, 0UL, 0UL);
+        }
+        ~Slack() {
+            if (old > 0 && old != 1000) (void)prctl(PR_SET_TIMERSLACK, (unsigned long)old, 0UL, 0UL, 0UL);
+        }
+    } slack;
     for (int k = 0;; ++k) {
+        std::this_thread::sleep_for(std::chrono::microseconds(k < 32 ? 5 : k < 96 ? 20 : 100));
         const hipError_t r = hipEventQuery(e);
         if (r == hipSuccess) return 0;
         if (r != hipErrorNotReady) {
             r360_set_error("hipEventQuery -> %s", hipGetErrorString(r));
             return -1;
         }
-        std::this_thread::sleep_for(std::chrono::microseconds(k < 32 ? 5 : k < 96 ? 20 : 100));
     }
 }
 
@@ -580,6 +591,7 @@ static int frame_build_event_record(const r360_frame* f) {
         g_bev[f] = e;
     }
     R360_HIP(hipEventRecord(e, f->ctx->stream));
+    const_cast<r360_frame*>(f)->build_gen.fetch_add(1, std::memory_order_release);
     return 0;
 }
 
@@ -718,6 +730,12 @@ extern "C" int r360_frame_dims(const r360_frame* f, int* rows, int* cols, int* s
     if (cols) *cols = f->cols;
     if (sph_rows) *sph_rows = f->sph_rows;
     if (sph_cols) *sph_cols = f->sph_cols;
+    return 0;
+}
+
+extern "C" int r360_frame_built(const r360_frame* f, unsigned* flags) {
+    CHECK_ARG(f && flags, "null arg");
+    *flags = f->built.load();
     return 0;
 }
 
@@ -929,6 +947,10 @@ extern "C" int r360_align360_async(r360_ctx* ctx, r360_frame* trg, r360_frame* s
     CHECK_ARG(method >= 0 && method <= 2, "invalid method");
     CHECK_ARG(occlusion >= 0 && occlusion <= 2, "occlusion must be 0, 1 or 2");
     if (ensure_defer(ctx, src->lv[0].rows * src->lv[0].cols)) return -1;
+    // frames built on another context (another thread's): this stream waits for their pyramid builds
+    for (const r360_frame* f : {trg, src})
+        if (f->ctx != ctx)
+            if (hipEvent_t e = frame_build_event(f)) R360_HIP(hipStreamWaitEvent(ctx->stream, e, 0));
     IcpState* h = ctx->h_state;
     memset(h, 0, sizeof(IcpState));
     memcpy(h->pose, init, sizeof(float) * 16);
@@ -996,6 +1018,12 @@ extern "C" int r360_align360_result(r360_ctx* ctx, float pose_out[16], float H_o
     if (wrc) return -1;
     ctx->async_pending = 0;
     if (h->fault) {
+        // the drained grid left the group arrival counters part-way (only a pass's step workgroup resets them): zero
+        // them so the next alignment on this ctx picks the right last workgroup (the pass ticket lives in the state,
+        // which every alignment re-uploads)
+        R360_HIP(hipMemsetAsync(ctx->d_gticket, 0, sizeof(unsigned) * R360_TICKET_STRIDE * R360_TICKET_GROUPS,
+                                ctx->stream));
+        R360_HIP(hipStreamSynchronize(ctx->stream));
         r360_set_error("alignFrames360: a persistent level launch timed out waiting for a pass (GPU oversubscribed?)");
         return -1;
     }

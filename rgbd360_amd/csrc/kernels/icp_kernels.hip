@@ -34,6 +34,8 @@ constexpr int NW = TPB / 64;
 constexpr int RG = TPB / 16;  // record-reduction groups (16 lanes x 16 B per record)
 // the two-level record sum maps ticket group g to the final-stage row g (threadIdx.x >> 4) and sums rows k < RG
 static_assert(!R360_GROUP_SUM || R360_TICKET_GROUPS == RG, "R360_GROUP_SUM needs R360_TICKET_GROUPS == TPB / 16");
+// gn_step_block (icp_gn.inc) runs the rank test on wave 1 and the solve on wave 2 of the step's workgroup
+static_assert(NW >= 3, "the GN step needs at least 3 waves per workgroup (R360_ICP_TPB >= 192)");
 
 struct Pose12 { float R[9]; float t[3]; };
 

@@ -350,6 +350,8 @@ struct r360_ctx {
     // PbMap matcher scratch (k_match_tables)
     int match_cap = 0;                       // planes per subgraph
     r360_match_params match{};               // SubgraphMatcher thresholds (r360_ctx_set_match_params)
+    // interpretation-tree searches on this ctx, those cut by the node budget, and the most nodes one search visited
+    std::atomic<long> match_calls{0}, match_truncated{0}, match_nodes_max{0};
     float* d_match_desc = nullptr;
     uint8_t* d_unary = nullptr;
     unsigned long long* d_bin = nullptr;
@@ -418,12 +420,18 @@ struct r360_frame {
     // per-sensor pinhole pyramids (R360_BUILD_SENSOR_PYRAMID): level l = [8][rows>>l][cols>>l], no seam mask
     LevelBufs sp[R360_MAX_PYR];
     int n_slevels = 0;
-    unsigned built = 0;
+    // R360_BUILD_* stages done (atomic: a frame built on one thread may have its sphere built from another,
+    // while the first reads its plane flags)
+    std::atomic<unsigned> built{0};
     PlaneBufs pl;
     PbMapHost* pbmap = nullptr;
     uint64_t timestamp = 0;            // Frame360::timeStamp (Frame360.h:181-184)
     bool lv0_compacted = false;        // lv[0].pts / d_npts[0] hold level 0's compacted points
     SphereCloudHost* sphere_cloud = nullptr;  // sphereCloud set by loadCloud (Frame360.h:187-193)
+    // builds recorded on the frame's build event (runtime.cpp frame_build_event_record): a dense-queue job snapshots
+    // it at submit and its batch refuses to run if the frame was rebuilt meanwhile (the event would then stand for
+    // the newer build)
+    std::atomic<unsigned> build_gen{0};
 };
 
 // ------------------------------------------------------------------ kernel launchers

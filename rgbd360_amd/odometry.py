@@ -324,6 +324,10 @@ class SequenceRunner:
                 hs[0] += t1 - t0
                 continue
             if not built_here(t + 1):   # the right neighbour's edge frame: built for this repeat?
+                # collect the previous repeats' pairs first: the last of them releases the neighbour's edge for its
+                # rebuild, which the neighbour may be waiting on (runs of at most `depth` pairs keep it pending here)
+                while pending and pending[0][1] // nfr < (t + 1) // nfr:
+                    finish(*pending.pop(0))
                 e = E[p + 1]
                 with e["cv"]:
                     if not e["cv"].wait_for(lambda: e["built"] >= (t + 1) // nfr or e["failed"], EDGE_WAIT_S) \

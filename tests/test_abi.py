@@ -126,6 +126,19 @@ def test_reference_call_sequence_compiles_unchanged(root):
     assert p.returncode == 0, p.stderr[-3000:]
 
 
+def test_sphere_graph_call_sites_compile_unchanged(root):
+    """Source-level drop-in of the SphereGraphSLAM / LoopClosure360 call sites (SLAM/SphereGraphSLAM.cpp:78-231,
+    include/LoopClosure360.h:83-126, 297-321): frame360->id / node, planes.vPlanes, Eigen::Matrix<float,6,6> from
+    getInfoMat() / getHessian(), getAreaMatched() / areaSource, RegisterRGBD360::RegisterRGBD360::...::PLANAR_3DoF,
+    a RegisterRGBD360 member constructed on one thread and used on another (std::thread), with g++ alone.  The
+    reference's own size_t > int comparison (LoopClosure360.h:298) is kept, hence -Wno-sign-compare."""
+    import subprocess
+    p = subprocess.run(["g++", "-std=c++17", "-O0", "-fsyntax-only", "-Wall", "-Wextra", "-Werror", "-Wno-sign-compare",
+                        "-pthread", f"-I{root}/include", f"{root}/tests/dropin/sphere_graph_dropin.cpp"],
+                       capture_output=True, text=True)
+    assert p.returncode == 0, p.stderr[-3000:]
+
+
 def test_data_dir_is_the_shipped_tree(root):
     """r360_data_dir() (the reference's PROJECT_SOURCE_PATH for calib/ and config_files/) resolves to this tree's
     data/ from the library's own location, so default-argument loads find the shipped calibration."""

@@ -153,8 +153,12 @@ def test_match_tables_and_register_pbmap(ctx, request, which, mode, ini):
     for key in ("sid", "tid", "unary", "binary"):
         assert np.array_equal(gt[key], ot[key]), key
     D.setdefault("tables", {})[(mode, ini)] = ot
+    calls0, trunc0, _ = ctx.match_stats()
     ok = reg.RegisterPbMap(D["frames"][0], D["frames"][1], 25, mode)
     r = O.register_pbmap(maps[0], maps[1], 25, mode, params=op)
+    calls1, trunc1, max_nodes = ctx.match_stats()
+    # the interpretation tree searched to the end (no node-budget cut) on both sides
+    assert calls1 == calls0 + 1 and trunc1 == trunc0 and not r["truncated"] and max_nodes >= r["nodes"]
     assert ok == bool(r["good"])
     assert reg.getMatchedPlanes() == r["matches"]
     assert reg.getAreaMatched() == r["area_matched"]

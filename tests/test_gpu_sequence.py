@@ -155,3 +155,22 @@ def test_queued_repeats_as_one_stream(seq, depth, lookahead):
             if len(d):
                 bad.append((i, int((d < 16).sum()), int(((d >= 16) & (d < 52)).sum()), [int(k) for k in d[d >= 52]]))
         assert not bad, (r, "pair, pose fields, info fields, other fields", bad[:8])
+
+
+@pytest.mark.parametrize("run_len", [1, 2])
+def test_short_runs_sharing_edges_do_not_deadlock(seq, run_len):
+    """Runs of at most `depth` pairs sharing their edge frames, repeated: a pipeline collects its previous repeat's
+    pairs (whose last releases its right neighbour's edge frame) before it waits for that neighbour's rebuild of the
+    edge, so neither waits on the other; every repeat reproduces the single-GPU records."""
+    bgr, dep = seq["bgr"], seq["dep"]
+    p0 = 40
+    runs = [(p0 + k * run_len, p0 + (k + 1) * run_len) for k in range(4)]
+    p1 = runs[-1][1]
+    runner = OD.SequenceRunner(0, 480, 640, 4, seq["params"], queue=16, depth=3)
+    try:
+        rec = np.zeros((3, p1 - p0, OD.REC), np.float32)
+        runner.run(p0, p1, lambda i: (bgr[i], dep[i]), rec, repeats=3, runs=runs)
+    finally:
+        runner.close()
+    for r in range(3):
+        assert np.array_equal(rec[r], seq["rec"][p0:p1]), r
