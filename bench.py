@@ -209,6 +209,98 @@ def cpu_baseline(cal, frames_of, first, last, workload, iters0, budget_s=10.0):
                       "thread count; value = the faster run"}
 
 
+def config1_leg(device, reps=5):
+    """BASELINE configs[0]: RegisterPairRGBD360 on the reference's sample captures sphere_images_1.bin vs _10.bin
+    (Registration/RegisterPairRGBD360.cpp:72-95: two Frame360 loads, undistort, buildSphereCloud + getPlanes, then
+    RegisterPbMap(25 planes, PLANAR_3DoF)), per stage, median of `reps` runs after one warm-up.  The CPU leg is the
+    oracle (OpenMP at the reference's 8 threads, Frame360.h:620); the GPU leg is the same stages through the library
+    (Frame360 load + upload, plane build incl. the host PbMap assembly, RegisterPbMap)."""
+    import rgbd360_amd as R
+    from oracle import oracle360 as O
+    paths = [os.path.join(R.SAMPLES_DIR, f"sphere_images_{k}.bin") for k in (1, 10)]
+    rt8 = O.read_extrinsics(R.EXTRINSICS_DIR)
+    clams = [O.Clams(os.path.join(R.INTRINSICS_DIR, f"distortion_model{k + 1}.r360")) for k in range(8)]
+    gomp = None
+    try:
+        gomp = ctypes.CDLL("libgomp.so.1")
+        gomp.omp_set_num_threads(8)
+    except OSError:
+        pass
+    cpu = {k: [] for k in ("loadFrame", "undistort", "getPlanes", "RegisterPbMap", "total")}
+    r = None
+    for it in range(reps + 1):
+        t = [time.perf_counter()]
+        raw = [O.load_bin(pth) for pth in paths]
+        t.append(time.perf_counter())
+        dm = [np.stack([clams[k].undistort(O.depth_to_m(d[k])) for k in range(8)]) for _, d in raw]
+        t.append(time.perf_counter())
+        maps = [O.PbMap(m, b, rt8) for m, (b, _) in zip(dm, raw)]
+        t.append(time.perf_counter())
+        r = O.register_pbmap(maps[0], maps[1], 25, O.PLANAR_3DoF)
+        t.append(time.perf_counter())
+        if it:
+            for k, name in enumerate(("loadFrame", "undistort", "getPlanes", "RegisterPbMap")):
+                cpu[name].append((t[k + 1] - t[k]) * 1e3)
+            cpu["total"].append((t[-1] - t[0]) * 1e3)
+    ctx = R.Context(device)
+    cal = R.Calib360(ctx, 240, 320)
+    cal.loadExtrinsicCalibration(R.EXTRINSICS_DIR)
+    cal.loadIntrinsicCalibration(R.INTRINSICS_DIR)
+    frames = [R.Frame360(cal), R.Frame360(cal)]
+    reg = R.RegisterRGBD360(ctx)
+    gpu = {k: [] for k in ("loadFrame", "undistort+getPlanes", "RegisterPbMap", "total")}
+    good, matches = None, None
+    for it in range(reps + 1):
+        t = [time.perf_counter()]
+        for f, pth in zip(frames, paths):
+            f.loadFrame(pth)
+        ctx.sync()
+        t.append(time.perf_counter())
+        for f in frames:
+            f.build(R.BUILD_UNDISTORT | R.BUILD_PLANES, sync=False)
+        for f in frames:
+            f.planes()
+        t.append(time.perf_counter())
+        good = reg.RegisterPbMap(frames[0], frames[1], 25, R.PLANAR_3DoF)
+        matches = reg.getMatchedPlanes()
+        t.append(time.perf_counter())
+        if it:
+            for k, name in enumerate(("loadFrame", "undistort+getPlanes", "RegisterPbMap")):
+                gpu[name].append((t[k + 1] - t[k]) * 1e3)
+            gpu["total"].append((t[-1] - t[0]) * 1e3)
+    for f in frames:
+        f.close()
+    cal.close()
+    ctx.close()
+    med = lambda d: {k: round(float(np.median(v)), 3) for k, v in d.items()}
+    return {"workload": "config1: RegisterPairRGBD360 on samples/sphere_images_1.bin vs _10.bin (QVGA 8x240x320, CLAMS + "
+                        "Rt calibration): 2 x (loadFrame, undistort, buildSphereCloud + getPlanes) + RegisterPbMap(25, "
+                        "PLANAR_3DoF)",
+            "cpu_ms": med(cpu), "cpu_threads": 8, "cpu_kind": "port (oracle/liboracle360.so)",
+            "gpu_ms": med(gpu), "runs": reps,
+            "pbmap_good": bool(good), "matches": len(matches or {}), "oracle_matches": len(r["matches"]),
+            "same_matches": bool(matches == r["matches"])}
+
+
+def sequential_leg(device, rows, cols, p0, frames_of, params, pairs=32):
+    """The reference's sequential caller (Registration/OdometryRGBD360.cpp:141-257): one pair at a time through the
+    C++ sequence runner with one pipeline and no dense queue (upload + build of the new frame, Register() on the
+    pipeline's own stream, wait), over `pairs` consecutive pairs of the same sequence."""
+    from rgbd360_amd import odometry as OD
+    runner = OD.SequenceRunner(device, rows, cols, 1, params, queue=0)
+    try:
+        runner.run(p0, p0 + 4, frames_of, np.zeros((1, 4, OD.REC), np.float32))   # warm-up
+        rec = np.zeros((1, pairs, OD.REC), np.float32)
+        t0 = time.perf_counter()
+        runner.run(p0, p0 + pairs, frames_of, rec)
+        dt = time.perf_counter() - t0
+    finally:
+        runner.close()
+    return {"value": pairs / dt, "unit": "pairs/s", "ms_per_pair": dt / pairs * 1e3, "pairs": pairs,
+            "workload": "config4's pairs one at a time (C++ runner, 1 pipeline, no dense queue): upload, Frame360 build, "
+                        "Register() per pair, as OdometryRGBD360.cpp:141-257 calls it"}
+
+
 def half_leg(kind, device, rows, cols, p0, p1, frames_of, params, pipelines, queue, depth, min_run, repeats=3):
     """BASELINE configs[1] / configs[2] as secondary blocks of the default line: one half of the headline workload
     over the same synthetic sequence, same pipelines, batched like the headline run.
@@ -471,6 +563,11 @@ def main(argv=None, runner_factory=None):
                   "other_live_top": sorted((round((th1[t] - th0.get(t, 0.0)) / elapsed, 2) for t in th1
                                             if t not in runner.native_ids), reverse=True)[:6]}
     barrier()
+    # interpretation-tree searches of the pipelines' RegisterPbMap calls (warm-up + timed), and how many of them stopped
+    # at the node budget (r360_ctx_match_stats; none may: the search is then exhaustive, as MRPT's)
+    mstats = np.sum([c.match_stats() for c in runner.ctxs], axis=0) if runner.ctxs else np.zeros(3)
+    matcher = {"searches": int(mstats[0]), "budget_hits": int(mstats[1]),
+               "max_nodes": int(max([c.match_stats()[2] for c in runner.ctxs] or [0]))}
     l0_ms, l0_n, k0_us, k0_n, k0_jobs, stage = 0.0, 0, 0.0, 0, 0, {}
     qstats = None
     if runner.queue:   # batches of the timed run
@@ -646,6 +743,8 @@ def main(argv=None, runner_factory=None):
         **({"stage_ms_per_pair": {k: v / max(args.steps * steps_pairs, 1) for k, v in stage.items()}}
            if args.stage_timing else {}),
         "pipeline_host_ms_per_pair": host_ms,
+        "pbmap_matcher": matcher, "pbmap_budget_hits": matcher["budget_hits"],
+        "runner": "C++ (r360_sequence, rgbd360_amd/csrc/host/sequence.cpp)",
         "host_cores_busy": round(host_cores_busy, 2),
         "host_cores_split": host_split,
         **({"dense_queue": {**qstats, "mean_batch": qstats["jobs"] / max(qstats["batches"], 1)}} if qstats else {}),
@@ -662,6 +761,9 @@ def main(argv=None, runner_factory=None):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(runner.cals[0], frames_of, p0, p1, args.workload, args.iters0)
     runner.close()
+    if rank == 0 and world == 1 and not args.no_halves and args.workload == "sequence":
+        out["sequential_cpp"] = sequential_leg(local, args.rows, args.cols, p0, frames_of, params)
+        out["config1"] = config1_leg(local)
     # configs[1] and configs[2] (the two halves of each pair's work) over the same sequence, after the timed region
     if rank == 0 and world == 1 and not args.no_halves and args.workload == "sequence":
         out["config2"] = half_leg("planes", local, args.rows, args.cols, p0, p1, frames_of, params, args.streams,

@@ -206,6 +206,14 @@ _SIGS = [
     ("r360_register_submit", C.c_int, [_P, _P, _P, _P, _FP, C.POINTER(IcpParams), C.c_size_t, C.c_int,
                                        C.POINTER(C.c_long)]),
     ("r360_register_collect", C.c_int, [_P, C.c_long, _FP, _FP, C.POINTER(IcpStats)]),
+    ("r360_sequence_default_params", None, [_P]),
+    ("r360_sequence_create", C.c_int, [C.c_int, _P, C.c_char_p, C.POINTER(_P)]),
+    ("r360_sequence_destroy", None, [_P]),
+    ("r360_sequence_run", C.c_int, [_P, C.c_int, C.c_int, _P, _P, C.c_int, C.c_int, _P, C.c_int, _P]),
+    ("r360_sequence_info", C.c_int, [_P, _IP, C.POINTER(_P)]),
+    ("r360_sequence_pipeline", C.c_int, [_P, C.c_int, C.POINTER(_P), C.POINTER(_P), _P, C.c_int, _IP,
+                                         C.POINTER(C.c_long)]),
+    ("r360_sequence_host_times", C.c_int, [_P, _P, C.c_int]),
     ("r360_icp_eval", C.c_int, [_P, _P, _P, C.c_int, _FP, C.c_int, C.POINTER(IcpParams), _DP, _DP, _DP, _IP,
                                 _IP]),
     ("r360_icp_eval_occ", C.c_int, [_P, _P, _P, C.c_int, _FP, C.c_int, C.c_int, C.POINTER(IcpParams), _DP, _DP,
@@ -355,6 +363,14 @@ class Context:
         self.h = h
         self.device = device
 
+    @classmethod
+    def _view(cls, h, device: int) -> "Context":
+        """A non-owning view of a context the library owns (a sequence runner's pipeline, a dense queue)."""
+        c = cls.__new__(cls)
+        c.h, c.device = h, device
+        c.close = lambda: None
+        return c
+
     def sync(self):
         _check(lib().r360_ctx_sync(self.h), "r360_ctx_sync")
 
@@ -427,6 +443,14 @@ class Calib360:
         self.h, self.ctx, self.rows, self.cols = h, ctx, rows, cols
 
     @classmethod
+    def _view(cls, h, ctx: Context, rows: int, cols: int) -> "Calib360":
+        """A non-owning view of a calibration the library owns."""
+        c = cls.__new__(cls)
+        c.h, c.ctx, c.rows, c.cols = h, ctx, rows, cols
+        c.close = lambda: None
+        return c
+
+    @classmethod
     def for_sphere(cls, ctx: Context, sph_rows: int, sph_cols: int) -> "Calib360":
         """A calibration without sensors for spheres given as images (setSourceFrame / setTargetFrame(cv::Mat&,
         cv::Mat&), RegisterPhotoICP.h:480-516)."""
@@ -480,6 +504,17 @@ class Frame360:
         r, c, sr, sc = C.c_int(), C.c_int(), C.c_int(), C.c_int()
         lib().r360_frame_dims(h, C.byref(r), C.byref(c), C.byref(sr), C.byref(sc))
         self.rows, self.cols, self.sph_rows, self.sph_cols = r.value, c.value, sr.value, sc.value
+
+    @classmethod
+    def _view(cls, h, calib: Calib360) -> "Frame360":
+        """A non-owning view of a frame the library owns (a sequence runner's ring buffer)."""
+        f = cls.__new__(cls)
+        f.h, f.calib = h, calib
+        r, c, sr, sc = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+        lib().r360_frame_dims(h, C.byref(r), C.byref(c), C.byref(sr), C.byref(sc))
+        f.rows, f.cols, f.sph_rows, f.sph_cols = r.value, c.value, sr.value, sc.value
+        f.close = lambda: None
+        return f
 
     def loadFrame(self, path: str):
         _check(lib().r360_frame_load_bin(self.h, path.encode()), "loadFrame")
@@ -902,6 +937,15 @@ class DenseQueue:
         ctx.h, ctx.device = C.c_void_p(lib().r360_dense_queue_ctx(h)), device
         ctx.close = lambda: None
         self.ctx = ctx
+
+    @classmethod
+    def _view(cls, h, device: int) -> "DenseQueue":
+        """A non-owning view of a dense queue the library owns (a sequence runner's)."""
+        q = cls.__new__(cls)
+        q.h, q.device = h, device
+        q.ctx = Context._view(C.c_void_p(lib().r360_dense_queue_ctx(h)), device)
+        q.close = lambda: None
+        return q
 
     def submit(self, trg: "Frame360", src: "Frame360", init=None, method: int = PHOTO_DEPTH,
                params: "IcpParams" = None) -> int:

@@ -1,0 +1,544 @@
+// sequence.cpp — OdometryRGBD360 over a frame sequence, pipelined on one GPU (BASELINE configs[3]).
+//
+// The reference's loop (Registration/OdometryRGBD360.cpp:141-257) registers each new Frame360 against the previous
+// one: RegisterPbMap, the rotOffset-conjugated alignFrames360 (the Register() alias, OdometryKeyFrame360.cpp:
+// 205-254), and composes currentPose = currentPose * rigidTransf (:257).  Pair (i, i+1) needs only frames i and i+1,
+// so the caller's pairs [p0, p1) are split into contiguous runs, one per pipeline; a pipeline is a host thread of
+// this object with its own r360_ctx (HIP stream, GN state, matcher scratch) and a ring of Frame360 buffers.
+//
+// Queued mode (params.queue > 0): every pipeline's alignFrames360 goes to one dense queue (r360_dense_queue, up to
+// `queue` pairs per launch), and a pipeline keeps `depth` alignments in flight while it builds and PbMap-registers
+// the next frames.  Frames are built `lookahead` positions ahead of the pair in hand and the next frame's upload is
+// issued right after a build on the same stream.  The `repeats` passes over a run are one stream of frame positions
+// t = 0 .. repeats * nfr - 1 (frame a + t mod nfr, nfr = frames per run), so a repeat's first frames are built while
+// the previous repeat's last alignments are still in flight.  A buffer is refilled only after every pair that used
+// its previous frame was collected (the dense queue refuses a job whose frame was rebuilt meanwhile).
+//
+// Shared run edges: the frame where run p-1 ends and run p starts is built once, by pipeline p, in an edge buffer of
+// its own; pipeline p-1 registers its last pair against it.  A per-edge handshake orders the two: p-1 waits until p
+// has built the edge for the current repeat, p rebuilds it for the next repeat only after p-1 released it (collected
+// its last pair of the repeat).  Before waiting for its right edge, a pipeline collects its earlier repeats' pairs
+// (the last of them is the release the right neighbour may be waiting on).  Edges are shared only when every run has
+// at least lookahead + 1 pairs: a shorter run would refill its edge buffer before submitting the pair that reads it.
+//
+// Every record equals the single-pair Register() result (batched alignments are bit-identical to lone ones).
+#include <array>
+#include <chrono>
+#include <cmath>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <sys/syscall.h>
+#include <thread>
+#include <unistd.h>
+#include <vector>
+
+#include "../r360_internal.h"
+
+namespace {
+
+constexpr int REC = R360_SEQ_RECORD;          // pose 16, info 36, status, SSO, error, (spare)
+constexpr double kEdgeWaitS = 120.0;          // a neighbour that neither builds nor releases its edge is stuck
+
+struct EdgeSync {
+    std::mutex m;
+    std::condition_variable cv;
+    int built = -1, released = -1;            // repeat whose edge frame pipeline p built / p-1 is done with
+    bool failed = false;                      // one of the two pipelines failed: the other stops waiting
+    bool shared = false;                      // runs p-1 and p meet at this frame
+};
+
+double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// rotOffset of OdometryRGBD360.cpp:136-139 (angle in float, PI = 3.14159265359), entries rounded to float, and the
+// conjugation back to the rig frame of a dense pose, rotOffset^-1 * D * rotOffset, in double
+void rig_from_dense(const float dense[16], float out[16]) {
+    const double a = double(157.5f) * 3.14159265359 / 180;
+    const double c = double(float(std::cos(a))), s = double(float(std::sin(a)));
+    double Ro[16] = {1, 0, 0, 0, 0, c, -s, 0, 0, s, c, 0, 0, 0, 0, 1};   // column-major: (1,2) = s, (2,1) = -s
+    double Ri[16] = {1, 0, 0, 0, 0, c, s, 0, 0, -s, c, 0, 0, 0, 0, 1};
+    double D[16], T[16];
+    for (int i = 0; i < 16; ++i) D[i] = dense[i];
+    auto mul = [](const double* A, const double* B, double* Cm) {
+        for (int col = 0; col < 4; ++col)
+            for (int r = 0; r < 4; ++r) {
+                double acc = 0;
+                for (int k = 0; k < 4; ++k) acc += A[k * 4 + r] * B[col * 4 + k];
+                Cm[col * 4 + r] = acc;
+            }
+    };
+    double U[16];
+    mul(Ri, D, T);
+    mul(T, Ro, U);
+    for (int i = 0; i < 16; ++i) out[i] = float(U[i]);
+}
+
+}  // namespace
+
+struct r360_sequence {
+    int device = 0;
+    r360_sequence_params prm{};
+    int P = 0;
+    unsigned flags = 0;
+    std::vector<r360_ctx*> ctx;
+    std::vector<r360_calib*> cal;
+    std::vector<std::vector<r360_frame*>> ring;   // per pipeline
+    std::vector<r360_frame*> edge;                // per pipeline (queued, shared edges)
+    r360_dense_queue* q = nullptr;
+    // persistent pipeline threads
+    std::vector<std::thread> th;
+    std::vector<long> tid;
+    std::mutex m;
+    std::condition_variable cv_go, cv_done;
+    long gen = 0;
+    int done = 0;
+    bool quit = false;
+    // the run in progress
+    struct Job {
+        int p0 = 0, p1 = 0, repeats = 1, device_inputs = 0;
+        bool share = false;
+        std::vector<std::pair<int, int>> runs;
+        const void* const* bgr = nullptr;
+        const void* const* dep = nullptr;
+        float* out = nullptr;
+    } job;
+    std::vector<std::unique_ptr<EdgeSync>> edges;  // edges[p]: between runs p-1 and p (edges[0] unused)
+    std::vector<int> rc;
+    std::vector<std::string> err;
+    std::vector<std::array<double, 4>> host_s;     // per pipeline: load + build enqueue, PbMap stage, dense wait, pairs
+};
+
+namespace {
+
+struct Fail {};   // a pipeline step failed: r360_last_error() holds the reason
+
+void req_rc(int rc) { if (rc < 0) throw Fail{}; }
+
+float* record(r360_sequence* s, int rep, int pair) {
+    return s->job.out + ((size_t)rep * (s->job.p1 - s->job.p0) + (pair - s->job.p0)) * REC;
+}
+
+void load_frame(r360_sequence* s, r360_frame* f, int i) {
+    const int k = i - s->job.p0;
+    if (s->job.device_inputs) req_rc(r360_frame_upload_device(f, s->job.bgr[k], s->job.dep[k]));
+    else req_rc(r360_frame_upload_async(f, static_cast<const uint8_t*>(s->job.bgr[k]),
+                                        static_cast<const uint16_t*>(s->job.dep[k])));
+}
+
+void fill(float* rec, const float pose[16], const float info[36], int status, const r360_icp_stats& st) {
+    std::memcpy(rec, pose, sizeof(float) * 16);
+    std::memcpy(rec + 16, info, sizeof(float) * 36);
+    rec[52] = float(status);
+    rec[53] = st.sso;
+    rec[54] = float(st.error);
+}
+
+const float kEye[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+
+// One pair on the pipeline's own context (no dense queue): the reference's sequential Register() per pair.
+void pipeline_plain(r360_sequence* s, int p) {
+    r360_ctx* ctx = s->ctx[p];
+    auto& hs = s->host_s[p];
+    const int a = s->job.runs[p].first, b = s->job.runs[p].second;
+    const int wl = s->prm.workload;
+    for (int r = 0; r < s->job.repeats; ++r) {
+        r360_frame* fa = s->ring[p][0];
+        r360_frame* fb = s->ring[p][1];
+        load_frame(s, fa, a);
+        req_rc(r360_frame_build_async(fa, s->flags));
+        for (int i = a; i < b; ++i) {
+            const double t0 = now_s();
+            load_frame(s, fb, i + 1);
+            req_rc(r360_frame_build_async(fb, s->flags));
+            const double t1 = now_s();
+            float pose[16], info[36] = {0};
+            std::memcpy(pose, kEye, sizeof pose);
+            r360_icp_stats st{};
+            int status = 0;
+            if (wl == R360_SEQ_PLANES) {          // configs[1]: RegisterPbMap alone
+                const int rc = r360_register_pbmap(ctx, fa, fb, s->prm.max_match_planes, s->prm.mode, pose, info,
+                                                   nullptr, 0, nullptr, nullptr, nullptr, nullptr);
+                req_rc(rc);
+                status = rc == 1 ? 0 : 1;
+                hs[0] += t1 - t0; hs[1] += now_s() - t1; hs[3] += 1;
+            } else if (wl == R360_SEQ_DENSE) {    // configs[2] / [4]: alignFrames360 from identity
+                req_rc(r360_align360_async(ctx, fa, fb, kEye, R360_PHOTO_DEPTH, 0, &s->prm.icp));
+                float dense[16];
+                req_rc(r360_align360_result(ctx, dense, nullptr, nullptr, &st));
+                rig_from_dense(dense, pose);
+                hs[0] += t1 - t0; hs[2] += now_s() - t1; hs[3] += 1;
+            } else {                              // configs[3]: the Register() alias
+                req_rc(r360_register_async(ctx, fa, fb, kEye, &s->prm.icp, s->prm.max_match_planes, s->prm.mode));
+                const double t2 = now_s();
+                const int rc = r360_register_result(ctx, pose, info, &st);
+                req_rc(rc);
+                status = rc;
+                hs[0] += t1 - t0; hs[1] += t2 - t1; hs[2] += now_s() - t2; hs[3] += 1;
+            }
+            if (st.illposed) status = 2;
+            fill(record(s, r, i), pose, info, status, st);
+            std::swap(fa, fb);
+        }
+    }
+}
+
+void pipeline_queued(r360_sequence* s, int p) {
+    r360_ctx* ctx = s->ctx[p];
+    auto& hs = s->host_s[p];
+    const int a = s->job.runs[p].first, b = s->job.runs[p].second;
+    const int wl = s->prm.workload;
+    const int nfr = b - a + 1, T = nfr * s->job.repeats;
+    const int P = (int)s->job.runs.size();
+    const bool left = s->job.share && p > 0 && s->edges[p]->shared;
+    const bool right = s->job.share && p + 1 < P && s->edges[p + 1]->shared;
+    const std::vector<r360_frame*>& fr = s->ring[p];
+    const int nbuf = (int)fr.size();
+    const int LA = s->prm.lookahead;
+
+    auto fidx = [&](int t) { return a + t % nfr; };
+    auto buf = [&](int t) -> r360_frame* {
+        const int k = t % nfr;
+        if (left && k == 0) return s->edge[p];
+        if (right && k == nfr - 1) return s->edge[p + 1];
+        return fr[t % nbuf];
+    };
+    auto built_here = [&](int t) { return !(right && t % nfr == nfr - 1); };
+
+    struct Pending { long ticket; int t; r360_icp_stats st; };
+    std::deque<Pending> pending;
+
+    auto finish = [&](Pending& pd) {
+        float pose[16], info[36] = {0};
+        int status;
+        if (wl == R360_SEQ_DENSE) {
+            float dense[16];
+            req_rc(r360_dense_queue_collect(s->q, pd.ticket, dense, nullptr, nullptr, &pd.st));
+            rig_from_dense(dense, pose);
+            status = 0;
+        } else {
+            const int rc = r360_register_collect(s->q, pd.ticket, pose, info, &pd.st);
+            req_rc(rc);
+            status = rc;
+        }
+        if (pd.st.illposed) status = 2;
+        fill(record(s, pd.t / nfr, fidx(pd.t)), pose, info, status, pd.st);
+        if (right && pd.t % nfr == nfr - 2) {     // the last pair of a repeat: the right neighbour's edge is free
+            EdgeSync& e = *s->edges[p + 1];
+            std::lock_guard<std::mutex> lk(e.m);
+            e.released = pd.t / nfr;
+            e.cv.notify_all();
+        }
+    };
+    auto finish_front = [&]() {
+        Pending pd = pending.front();
+        pending.pop_front();
+        finish(pd);
+    };
+    auto wait_edge = [&](EdgeSync& e, auto pred, const char* what, int frame) {
+        std::unique_lock<std::mutex> lk(e.m);
+        const bool ok = e.cv.wait_for(lk, std::chrono::duration<double>(kEdgeWaitS), [&] { return pred() || e.failed; });
+        if (!ok || !pred()) {
+            r360_set_error("pipeline %d: %s edge frame %d", p, what, frame);
+            throw Fail{};
+        }
+    };
+    auto load = [&](int t) {
+        if (!built_here(t)) return;
+        const int k = t % nfr, r = t / nfr;
+        if (left && k == 0) {
+            // this pipeline and its left neighbour must both be done with the previous repeat's copy
+            while (!pending.empty() && pending.front().t <= t - nfr) finish_front();
+            EdgeSync& e = *s->edges[p];
+            wait_edge(e, [&] { return e.released >= r - 1; }, "left neighbour did not release", fidx(t));
+        }
+        load_frame(s, buf(t), fidx(t));
+    };
+    auto build = [&](int t) {
+        if (!built_here(t)) return;
+        req_rc(r360_frame_build_async(buf(t), s->flags));
+        if (left && t % nfr == 0) {
+            EdgeSync& e = *s->edges[p];
+            std::lock_guard<std::mutex> lk(e.m);
+            e.built = t / nfr;
+            e.cv.notify_all();
+        }
+    };
+
+    const int last = T - 1;
+    for (int t = 0; t < std::min(LA, last + 1); ++t) {   // positions 0 .. LA-1 built, position LA uploaded
+        load(t);
+        build(t);
+    }
+    if (LA <= last) load(LA);
+    const int depth = nbuf - LA - 2;
+    for (int t = 0; t < last; ++t) {
+        const double t0 = now_s();
+        // position t + LA + 1 refills the buffer of position u = t + LA + 1 - nbuf: collect the pairs that used it
+        while (!pending.empty() && pending.front().t <= t + LA + 1 - nbuf) finish_front();
+        r360_frame* cur = buf(t);
+        r360_frame* nxt = buf(t + 1);
+        if (t + LA <= last) build(t + LA);                  // its upload was issued one iteration earlier
+        if (t + LA + 1 <= last) load(t + LA + 1);
+        const double t1 = now_s();
+        if (t % nfr == nfr - 1) {                           // the last frame of a repeat: no pair
+            hs[0] += t1 - t0;
+            continue;
+        }
+        if (!built_here(t + 1)) {                           // the right neighbour's edge frame of this repeat
+            const int R = (t + 1) / nfr;
+            while (!pending.empty() && pending.front().t / nfr < R) finish_front();
+            EdgeSync& e = *s->edges[p + 1];
+            wait_edge(e, [&] { return e.built >= R; }, "right neighbour did not build", fidx(t + 1));
+        }
+        long ticket = 0;
+        if (wl == R360_SEQ_DENSE)
+            req_rc(r360_dense_queue_submit(s->q, cur, nxt, kEye, R360_PHOTO_DEPTH, &s->prm.icp, &ticket));
+        else
+            req_rc(r360_register_submit(ctx, s->q, cur, nxt, kEye, &s->prm.icp, s->prm.max_match_planes, s->prm.mode,
+                                        &ticket));
+        const double t2 = now_s();
+        pending.push_back(Pending{ticket, t, r360_icp_stats{}});
+        if ((int)pending.size() > depth) finish_front();
+        hs[0] += t1 - t0; hs[1] += t2 - t1; hs[2] += now_s() - t2; hs[3] += 1;
+    }
+    const double t2 = now_s();
+    while (!pending.empty()) finish_front();
+    hs[2] += now_s() - t2;
+}
+
+void worker(r360_sequence* s, int p) {
+    (void)hipSetDevice(s->device);
+    {
+        std::lock_guard<std::mutex> lk(s->m);
+        s->tid[p] = (long)syscall(SYS_gettid);
+    }
+    s->cv_done.notify_all();
+    long seen = 0;
+    for (;;) {
+        {
+            std::unique_lock<std::mutex> lk(s->m);
+            s->cv_go.wait(lk, [&] { return s->quit || s->gen != seen; });
+            if (s->quit) return;
+            seen = s->gen;
+        }
+        int rc = 0;
+        std::string err;
+        if (p < (int)s->job.runs.size()) {
+            try {
+                if (s->q) pipeline_queued(s, p);
+                else pipeline_plain(s, p);
+            } catch (const Fail&) {
+                rc = -1;
+                err = r360_last_error();
+            } catch (const std::exception& e) {
+                rc = -1;
+                err = std::string("pipeline: ") + e.what();
+            }
+            if (rc && s->job.share)               // the neighbours must not keep waiting on this pipeline's edges
+                for (int e : {p, p + 1})
+                    if (e > 0 && e < (int)s->edges.size()) {
+                        std::lock_guard<std::mutex> lk(s->edges[e]->m);
+                        s->edges[e]->failed = true;
+                        s->edges[e]->cv.notify_all();
+                    }
+        }
+        std::lock_guard<std::mutex> lk(s->m);
+        s->rc[p] = rc;
+        s->err[p] = err;
+        ++s->done;
+        s->cv_done.notify_all();
+    }
+}
+
+}  // namespace
+
+extern "C" void r360_sequence_default_params(r360_sequence_params* p) {
+    if (!p) return;
+    std::memset(p, 0, sizeof(*p));
+    p->rows = 480; p->cols = 640;
+    p->pipelines = 10;
+    p->queue = 16;
+    p->depth = 3;
+    p->lookahead = 1;
+    p->share_edges = 1;
+    p->workload = R360_SEQ_FULL;
+    p->max_match_planes = 25;
+    p->mode = R360_PLANAR_3DoF;
+    r360_icp_default_params(&p->icp);
+    p->icp.n_pyr = 5;                              // OdometryRGBD360.cpp:92-95
+    p->icp.std_dev_photo = 3.0f / 255;
+    p->icp.fixed_iters_level0 = 20;               // timing mode
+}
+
+extern "C" void r360_sequence_destroy(r360_sequence* s);
+
+extern "C" int r360_sequence_create(int device, const r360_sequence_params* prm, const char* extrinsics_dir,
+                                    r360_sequence** out) {
+    CHECK_ARG(prm && out, "null arg");
+    CHECK_ARG(prm->pipelines >= 1 && prm->pipelines <= 64, "pipelines must be 1..64");
+    CHECK_ARG(prm->rows > 0 && prm->cols > 0, "rows / cols");
+    CHECK_ARG(prm->workload >= R360_SEQ_FULL && prm->workload <= R360_SEQ_DENSE, "workload");
+    CHECK_ARG(prm->queue >= 0 && prm->queue <= R360_MAX_BATCH, "queue must be 0..R360_MAX_BATCH_ALIGN");
+    if (bind_device(device)) return -1;
+    std::unique_ptr<r360_sequence> s(new r360_sequence);
+    s->device = device;
+    s->prm = *prm;
+    if (s->prm.workload == R360_SEQ_PLANES) s->prm.queue = 0;   // no dense stage
+    s->prm.depth = std::max(1, s->prm.depth);
+    s->prm.lookahead = std::max(1, s->prm.lookahead);
+    s->P = prm->pipelines;
+    // configs[1] needs the planes only, configs[2] / [4] the sphere pyramid only
+    s->flags = s->prm.workload == R360_SEQ_PLANES ? (R360_BUILD_UNDISTORT | R360_BUILD_PLANES)
+             : s->prm.workload == R360_SEQ_DENSE ? (R360_BUILD_UNDISTORT | R360_BUILD_SPHERE | R360_BUILD_PYRAMID)
+             : (R360_BUILD_UNDISTORT | R360_BUILD_SPHERE | R360_BUILD_PYRAMID | R360_BUILD_PLANES);
+    auto fail = [&]() {
+        r360_sequence_destroy(s.release());
+        return -1;
+    };
+    if (s->prm.queue > 0 && r360_dense_queue_create(device, s->prm.queue, &s->q)) return fail();
+    const bool queued = s->q != nullptr;
+    const int nbuf = queued ? s->prm.depth + s->prm.lookahead + 2 : 2;
+    for (int p = 0; p < s->P; ++p) {
+        r360_ctx* c = nullptr;
+        if (r360_ctx_create(device, &c)) return fail();
+        s->ctx.push_back(c);
+        r360_calib* k = nullptr;
+        if (r360_calib_create(c, prm->rows, prm->cols, &k)) return fail();
+        s->cal.push_back(k);
+        if (r360_calib_load_extrinsics(k, extrinsics_dir)) return fail();
+        s->ring.emplace_back();
+        for (int j = 0; j < nbuf; ++j) {
+            r360_frame* f = nullptr;
+            if (r360_frame_create(c, k, &f)) return fail();
+            s->ring.back().push_back(f);
+        }
+        if (queued && s->prm.share_edges) {
+            r360_frame* f = nullptr;
+            if (r360_frame_create(c, k, &f)) return fail();
+            s->edge.push_back(f);
+        }
+    }
+    s->tid.assign(s->P, 0);
+    s->rc.assign(s->P, 0);
+    s->err.assign(s->P, std::string());
+    s->host_s.assign(s->P, std::array<double, 4>{0, 0, 0, 0});
+    for (int p = 0; p < s->P; ++p) s->th.emplace_back(worker, s.get(), p);
+    {   // the threads' ids (host CPU accounting of the callers)
+        std::unique_lock<std::mutex> lk(s->m);
+        s->cv_done.wait(lk, [&] {
+            for (long t : s->tid) if (!t) return false;
+            return true;
+        });
+    }
+    *out = s.release();
+    return 0;
+}
+
+extern "C" void r360_sequence_destroy(r360_sequence* s) {
+    if (!s) return;
+    {
+        std::lock_guard<std::mutex> lk(s->m);
+        s->quit = true;
+    }
+    s->cv_go.notify_all();
+    for (auto& t : s->th) t.join();
+    for (r360_frame* f : s->edge) r360_frame_destroy(f);
+    for (auto& r : s->ring)
+        for (r360_frame* f : r) r360_frame_destroy(f);
+    for (r360_calib* k : s->cal) r360_calib_destroy(k);
+    if (s->q) r360_dense_queue_destroy(s->q);
+    for (r360_ctx* c : s->ctx) r360_ctx_destroy(c);
+    delete s;
+}
+
+extern "C" int r360_sequence_run(r360_sequence* s, int p0, int p1, const void* const* bgr, const void* const* depth,
+                                 int device_inputs, int repeats, const int* runs, int n_runs, float* records) {
+    CHECK_ARG(s && bgr && depth && records, "null arg");
+    CHECK_ARG(p1 > p0 && repeats >= 1, "empty run");
+    if (bind_device(s->device)) return -1;
+    std::vector<std::pair<int, int>> rv;
+    if (runs && n_runs > 0) {
+        CHECK_ARG(n_runs <= s->P, "more runs than pipelines");
+        int at = p0;
+        for (int k = 0; k < n_runs; ++k) {
+            CHECK_ARG(runs[2 * k] == at && runs[2 * k + 1] > runs[2 * k], "runs must tile [p0, p1) in order");
+            rv.emplace_back(runs[2 * k], runs[2 * k + 1]);
+            at = runs[2 * k + 1];
+        }
+        CHECK_ARG(at == p1, "runs must tile [p0, p1)");
+    } else {   // [p0, p1) in P contiguous runs whose sizes differ by at most one
+        const int n = p1 - p0, parts = std::min(s->P, n);
+        int at = p0;
+        for (int k = 0; k < parts; ++k) {
+            const int e = at + n / parts + (k < n % parts ? 1 : 0);
+            rv.emplace_back(at, e);
+            at = e;
+        }
+    }
+    int shortest = p1 - p0;
+    for (auto& r : rv) shortest = std::min(shortest, r.second - r.first);
+    s->job.p0 = p0; s->job.p1 = p1; s->job.repeats = repeats; s->job.device_inputs = device_inputs;
+    s->job.runs = rv;
+    s->job.bgr = bgr; s->job.dep = depth; s->job.out = records;
+    s->job.share = s->q && !s->edge.empty() && shortest >= s->prm.lookahead + 1;
+    s->edges.clear();
+    for (size_t k = 0; k <= rv.size(); ++k) {
+        s->edges.emplace_back(new EdgeSync);
+        s->edges.back()->shared = k > 0 && k < rv.size() && rv[k - 1].second == rv[k].first;
+    }
+    {
+        std::lock_guard<std::mutex> lk(s->m);
+        s->done = 0;
+        ++s->gen;
+    }
+    s->cv_go.notify_all();
+    {
+        std::unique_lock<std::mutex> lk(s->m);
+        s->cv_done.wait(lk, [&] { return s->done == s->P; });
+    }
+    for (r360_ctx* c : s->ctx) if (r360_ctx_sync(c)) return -1;
+    for (int p = 0; p < s->P; ++p)
+        if (s->rc[p]) {
+            r360_set_error("%s", s->err[p].c_str());
+            return -1;
+        }
+    return 0;
+}
+
+extern "C" int r360_sequence_info(r360_sequence* s, int* pipelines, r360_dense_queue** queue) {
+    CHECK_ARG(s, "null sequence");
+    if (pipelines) *pipelines = s->P;
+    if (queue) *queue = s->q;
+    return 0;
+}
+
+extern "C" int r360_sequence_pipeline(r360_sequence* s, int p, r360_ctx** ctx, r360_calib** calib, r360_frame** frames,
+                                      int cap, int* n_frames, long* thread_id) {
+    CHECK_ARG(s && p >= 0 && p < s->P, "pipeline out of range");
+    if (ctx) *ctx = s->ctx[p];
+    if (calib) *calib = s->cal[p];
+    const int n = (int)s->ring[p].size();
+    if (n_frames) *n_frames = n;
+    for (int j = 0; j < n && j < cap && frames; ++j) frames[j] = s->ring[p][j];
+    if (thread_id) {
+        std::lock_guard<std::mutex> lk(s->m);
+        *thread_id = s->tid[p];
+    }
+    return 0;
+}
+
+extern "C" int r360_sequence_host_times(r360_sequence* s, double* out, int reset) {
+    CHECK_ARG(s, "null sequence");
+    std::lock_guard<std::mutex> lk(s->m);
+    for (int p = 0; p < s->P; ++p)
+        for (int k = 0; k < 4; ++k) {
+            if (out) out[4 * p + k] = s->host_s[p][k];
+            if (reset) s->host_s[p][k] = 0;
+        }
+    return 0;
+}

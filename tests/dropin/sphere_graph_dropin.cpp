@@ -221,8 +221,10 @@ class SphereGraphSLAM {
                     }
                     frameRegistered = true;
                     vSSO[std::make_pair(newLocalFrameID, compareLocalIdx)] = registerer.getAreaMatched() / registerer.areaSource;
-                    print_pose("track pose", Map.mmConnectionKFs[frameOrder][*compareSphereId].first);
-                    print_info("track info", Map.mmConnectionKFs[frameOrder][*compareSphereId].second);
+                    // (what mmConnectionKFs received; *compareSphereId, a reverse iterator, names the new frame since
+                    // the insert above)
+                    print_pose("track pose", registerer.getPose());
+                    print_info("track info", registerer.getInfoMat());
                     cout << "track SSO " << setprecision(9) << vSSO[std::make_pair(newLocalFrameID, compareLocalIdx)]
                          << " increment " << Map.vTrajectoryIncrements.back() << setprecision(6) << '\n';
                     print_pose("current", currentPose);

@@ -114,6 +114,7 @@ class _StubCtx:
     def timing_read(self, name): return 0.0, 0
     def kernel_stats(self, level): return 0.0, 0, 0
     def host_times(self, reset=False): return np.zeros(6)
+    def match_stats(self): return 0, 0, 0
 
 
 class _StubRunner:
