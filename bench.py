@@ -301,7 +301,7 @@ def sequential_leg(device, rows, cols, p0, frames_of, params, pairs=32):
                         "Register() per pair, as OdometryRGBD360.cpp:141-257 calls it"}
 
 
-def half_leg(kind, device, rows, cols, p0, p1, frames_of, params, pipelines, queue, depth, min_run, repeats=3):
+def half_leg(kind, device, rows, cols, p0, p1, frames_of, params, pipelines, queue, depth, repeats=3):
     """BASELINE configs[1] / configs[2] as secondary blocks of the default line: one half of the headline workload
     over the same synthetic sequence, same pipelines, batched like the headline run.
       kind "planes" (configs[1]): per pair the upload + Frame360 build with planes (PbMap) + RegisterPbMap(25,
@@ -311,20 +311,19 @@ def half_leg(kind, device, rows, cols, p0, p1, frames_of, params, pipelines, que
                                   iterations at level 0, the dense queue batching the pipelines' alignments.
     Returns pairs/s (whole sequence x repeats after one warm-up pass) and, for the dense half, its level-0 pass."""
     from rgbd360_amd import odometry as OD
-    P = OD.pipelines_for(p1 - p0, pipelines, min_run)
-    runs = OD.split_range(p0, p1, P)
-    runner = OD.SequenceRunner(device, rows, cols, len(runs), params, planes=kind == "planes",
+    P = min(pipelines, p1 - p0)
+    runner = OD.SequenceRunner(device, rows, cols, P, params, planes=kind == "planes",
                                dense_only=kind == "dense", queue=queue, planes_only=kind == "planes", depth=depth)
-    runner.run(p0, p1, frames_of, np.zeros((1, p1 - p0, OD.REC), np.float32), repeats=1, runs=runs)   # warm-up
+    runner.run(p0, p1, frames_of, np.zeros((1, p1 - p0, OD.REC), np.float32), repeats=1)   # warm-up
     qctx = runner.queue.ctx if runner.queue else None
     if qctx:
         qctx.kernel_time_reset()
     rec = np.zeros((repeats, p1 - p0, OD.REC), np.float32)
     t0 = time.perf_counter()
-    runner.run(p0, p1, frames_of, rec, repeats=repeats, runs=runs)
+    runner.run(p0, p1, frames_of, rec, repeats=repeats)
     elapsed = time.perf_counter() - t0
     out = {"value": (p1 - p0) * repeats / elapsed, "unit": "pairs/s", "pairs": p1 - p0, "repeats": repeats,
-           "ms_per_pair": elapsed / ((p1 - p0) * repeats) * 1e3, "pipelines": len(runs)}
+           "ms_per_pair": elapsed / ((p1 - p0) * repeats) * 1e3, "pipelines": P}
     if kind == "planes":
         st = rec[-1, :, OD.R_STATUS]
         out["workload"] = ("config2 over the config4 sequence: per pair upload + Frame360 build with planes (PbMap) + "
@@ -373,19 +372,18 @@ def config5_leg(device, rt8, pairs=48, iters0=50, pipelines=8, depth=2, repeats=
     params.n_pyr = 5
     params.std_dev_photo = np.float32(3.0 / 255)
     params.fixed_iters_level0 = iters0
-    runs = OD.split_range(0, pairs, pipelines)
-    runner = OD.SequenceRunner(device, rows, cols, len(runs), params, planes=False, dense_only=True, queue=16,
+    runner = OD.SequenceRunner(device, rows, cols, pipelines, params, planes=False, dense_only=True, queue=16,
                                depth=depth)
 
     def frames_of(i):
         return BGR[i], DEP[i]
-    runner.run(0, pairs, frames_of, np.zeros((1, pairs, OD.REC), np.float32), repeats=1, runs=runs)   # warmup
+    runner.run(0, pairs, frames_of, np.zeros((1, pairs, OD.REC), np.float32), repeats=1)   # warmup
     qctx = runner.queue.ctx
     q0 = runner.queue.stats()
     qctx.kernel_time_reset()
     rec = np.zeros((repeats, pairs, OD.REC), np.float32)
     t0 = time.perf_counter()
-    runner.run(0, pairs, frames_of, rec, repeats=repeats, runs=runs)
+    runner.run(0, pairs, frames_of, rec, repeats=repeats)
     elapsed = time.perf_counter() - t0
     us, n, nj = qctx.kernel_stats(0)
     q1 = runner.queue.stats()
@@ -417,7 +415,7 @@ def config5_leg(device, rt8, pairs=48, iters0=50, pipelines=8, depth=2, repeats=
     return {
         "workload": (f"config5: synthetic 8x{cols}x{rows} sequence, {pairs} consecutive pairs x {repeats} repeats; per "
                      f"pair: upload, stitch + 5-level pyramid, alignFrames360(PHOTO_DEPTH) levels 4..1 reference "
-                     f"schedule + {iters0} GN iterations at level 0 ({len(runs)} pipelines x {depth} in flight, dense "
+                     f"schedule + {iters0} GN iterations at level 0 ({pipelines} pipelines x {depth} in flight, dense "
                      "queue batches of up to 16 pairs)"),
         "sphere": f"{H0}x{W0}", "value": pairs * repeats / elapsed, "unit": "pairs/s",
         "ms_per_pair": elapsed / (pairs * repeats) * 1e3,
@@ -449,9 +447,10 @@ def main(argv=None, runner_factory=None):
                     "10 since the pipelines share their run edges: 1330-1342 vs 1299-1301 pairs/s at 8, "
                     "profiles/r4_streams/)")
     ap.add_argument("--min-run", type=int, default=6,
-                    help="min pairs per pipeline run (each run rebuilds a halo frame): 6 gives a 1/8 shard (31-32 pairs) "
-                         "5 pipelines, 8-10 %% faster than 8 (3-4 pipelines) and 4 (8); N=1 and 1/4 shards keep 8 "
-                         "pipelines either way (profiles/r3_shards)")
+                    help="with --per-step-runs: min pairs per pipeline run (each run rebuilds a halo frame)")
+    ap.add_argument("--per-step-runs", action="store_true",
+                    help="split each step's pairs into one run per pipeline (rounds 2-4) instead of cutting the steps x "
+                         "pairs stream into one contiguous piece per pipeline (default)")
     ap.add_argument("--stage-timing", action="store_true",
                     help="diagnostic: HIP events around EVERY launch of the timed run (per-stage times; slows the run)")
     ap.add_argument("--queue", type=int, default=16,
@@ -488,9 +487,14 @@ def main(argv=None, runner_factory=None):
     from rgbd360_amd import odometry as OD
 
     p0, p1 = OD.shard_pairs(shard_rank, shard_world, args.frames)
-    P = OD.pipelines_for(p1 - p0, args.streams, args.min_run)
-    runs = OD.split_range(p0, p1, P)
-    P = len(runs)
+    # the steps x shard pairs form one stream, cut into one contiguous piece per pipeline (each piece rebuilds the
+    # first frame of each of its segments: a few extra frame builds per step, no coupling between pipelines)
+    if args.per_step_runs:
+        runs = OD.split_range(p0, p1, OD.pipelines_for(p1 - p0, args.streams, args.min_run))
+        P = len(runs)
+    else:
+        runs = None
+        P = max(1, min(args.streams, (p1 - p0) * max(args.steps, 1)))
 
     # raw frames p0..p1 of this rank, rendered on the host, in page-locked memory (uploaded per pair
     # inside the timed region)
@@ -527,9 +531,14 @@ def main(argv=None, runner_factory=None):
     # warmup: every buffer (frames, queues, records) is allocated here, outside the timed region
     runner.run(p0, p1, frames_of, np.zeros((max(args.warmup, 1), p1 - p0, OD.REC), np.float32),
                repeats=max(args.warmup, 1), runs=runs)
+    # frame builds per step beyond one per pair: the first frame of every segment of every piece
+    halo_per_step = ((len(runs) * args.steps) if runs else
+                     sum(len(g) for g in OD.stream_pieces(p0, p1, args.steps, P))) / args.steps
 
     rec = np.zeros((args.steps, p1 - p0, OD.REC), np.float32)
     runner.host_s[:] = 0
+    if hasattr(runner, "host_detail"):
+        runner.host_detail[:] = 0
     for c in runner.ctxs:
         c.host_times(reset=True)
     barrier()
@@ -588,6 +597,10 @@ def main(argv=None, runner_factory=None):
             stage[name] = stage.get(name, 0.0) + ms
     hs = runner.host_s.sum(axis=0)
     host_ms = {k: 1e3 * v / max(hs[3], 1) for k, v in zip(("load_build_enqueue", "pbmap_stage", "dense_wait"), hs[:3])}
+    if hasattr(runner, "host_detail"):   # inside load_build_enqueue
+        hd = runner.host_detail.sum(axis=0)
+        host_ms["load_split"] = {k: 1e3 * v / max(hs[3], 1) for k, v in
+                                 zip(("build_enqueue", "upload_enqueue", "refill_collects", "edge_waits"), hd)}
     ht = np.sum([c.host_times() for c in runner.ctxs], axis=0)   # inside RegisterPbMap
     host_ms["pbmap_stage_split"] = {k: 1e3 * v / max(ht[3], 1) for k, v in
                                     zip(("wait_frame_pbmaps", "match_tables", "tree_and_pose"), ht[:3])}
@@ -596,11 +609,11 @@ def main(argv=None, runner_factory=None):
     if group is not None:
         # per-rank figures for diagnosing a scaling run from its own line: pairs, time to the end of its shard, the
         # record gather's share of the timed region, and the halo frames (one per pipeline run) it rebuilt
-        mine = np.array([rank, p1 - p0, elapsed, t_run, gather_s, len(runs), P], np.float64)
+        mine = np.array([rank, p1 - p0, elapsed, t_run, gather_s, halo_per_step, P], np.float64)
         allm = group.allgather(mine.astype(np.float32))
         per_rank = [{"rank": int(m[0]), "pairs_per_step": int(m[1]), "pairs_per_s": float(m[1] * args.steps / m[2]),
                      "shard_s": float(m[3]), "timed_s": float(m[2]), "gather_ms": float(m[4] * 1e3),
-                     "halo_frames_per_step": int(m[5]), "pipelines": int(m[6])} for m in allm]
+                     "halo_frames_per_step": float(m[5]), "pipelines": int(m[6])} for m in allm]
         elapsed = group.max(elapsed)
     pairs_job = args.steps * sum(sizes)
     value = pairs_job / elapsed
@@ -719,6 +732,9 @@ def main(argv=None, runner_factory=None):
             "workload": workload, "sensors": f"8x{args.cols}x{args.rows}", "sphere": f"{H0}x{W0}",
             "n_pyr": 5, "parallelism": f"pair-shard dp{world}", "pairs_per_step": pairs_job // args.steps,
             "pairs_per_step_this_rank": steps_pairs, "pipelines_per_gpu": P,
+            "pipeline_work": ("one run of each step per pipeline" if runs else
+                              "the steps x pairs stream cut into one contiguous piece per pipeline"),
+            "extra_frame_builds_per_step": halo_per_step,
             "dense_batch": args.queue, "dense_in_flight_per_pipeline": args.depth if args.queue else 1,
             "frames_built_ahead": args.lookahead if args.queue else 1,
             **({"emulated_shard": f"{shard_rank}/{shard_world}"} if args.emulate else {}),
@@ -767,9 +783,9 @@ def main(argv=None, runner_factory=None):
     # configs[1] and configs[2] (the two halves of each pair's work) over the same sequence, after the timed region
     if rank == 0 and world == 1 and not args.no_halves and args.workload == "sequence":
         out["config2"] = half_leg("planes", local, args.rows, args.cols, p0, p1, frames_of, params, args.streams,
-                                  args.queue, args.depth, args.min_run)
+                                  args.queue, args.depth)
         out["config3"] = half_leg("dense", local, args.rows, args.cols, p0, p1, frames_of, params, args.streams,
-                                  args.queue, args.depth, args.min_run)
+                                  args.queue, args.depth)
     pinned.close()
     if rank == 0 and world == 1 and not args.no_config5 and args.workload == "sequence" and args.rows == 480:
         del BGR, DEP

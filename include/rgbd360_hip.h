@@ -386,8 +386,8 @@ int r360_register_collect(r360_dense_queue* q, long ticket, float pose[16], floa
  * pipeline (a host thread of the object with its own r360_ctx and ring of Frame360 buffers); per pair the new frame
  * is uploaded and built on the GPU and registered with the Register() alias (RegisterPbMap -> rotOffset conjugation
  * -> alignFrames360, OdometryKeyFrame360.cpp:205-254).  With queue > 0 the alignments of all pipelines are batched on
- * one dense queue, `depth` in flight per pipeline, frames built `lookahead` ahead, neighbouring runs sharing the frame
- * where they meet.  Each pair's record equals the single-pair Register() result. */
+ * one dense queue, `depth` in flight per pipeline, frames built `lookahead` ahead.  Each pair's record equals the
+ * single-pair Register() result. */
 enum { R360_SEQ_FULL = 0,     /* configs[3]: Register() per pair                                        */
        R360_SEQ_PLANES = 1,   /* configs[1]: planes + RegisterPbMap only                                  */
        R360_SEQ_DENSE = 2 };  /* configs[2] / [4]: stitch + pyramid + alignFrames360 from identity       */
@@ -401,7 +401,6 @@ typedef struct {
     int queue;                      /* dense queue batch (pairs per launch); 0 = each pipeline aligns alone */
     int depth;                      /* queued: alignments in flight per pipeline                        */
     int lookahead;                  /* queued: frames built ahead of the pair in hand                   */
-    int share_edges;                /* queued: neighbouring runs build their common frame once          */
     int workload;                   /* R360_SEQ_*                                                       */
     size_t max_match_planes;        /* RegisterPbMap (25)                                               */
     int mode;                       /* registrationType (PLANAR_3DoF)                                   */
@@ -414,9 +413,10 @@ int  r360_sequence_create(int device, const r360_sequence_params* p, const char*
 void r360_sequence_destroy(r360_sequence* s);
 /* Registers pairs [p0, p1) `repeats` times.  Frame i's raw images (BGR u8 8 x rows x cols x 3, depth u16 mm
  * 8 x rows x cols) are bgr[i - p0] / depth[i - p0] for i in [p0, p1]: host memory (page-locked for asynchronous
- * uploads) or, with device_inputs, device memory.  runs: n_runs (first, last + 1) pairs tiling [p0, p1) in order,
- * one per pipeline (NULL: P near-equal runs).  records: repeats x (p1 - p0) x R360_SEQ_RECORD floats.  Returns 0, or
- * < 0 with the failing pipeline's error. */
+ * uploads) or, with device_inputs, device memory.  The repeats x (p1 - p0) registrations form one stream (repeat-
+ * major) cut into P contiguous pieces, one per pipeline; runs (optional): n_runs (first, last + 1) pairs tiling
+ * [p0, p1) in order, pipeline k taking run k of every repeat instead.  records: repeats x (p1 - p0) x
+ * R360_SEQ_RECORD floats.  Returns 0, or < 0 with the failing pipeline's error. */
 int  r360_sequence_run(r360_sequence* s, int p0, int p1, const void* const* bgr, const void* const* depth,
                        int device_inputs, int repeats, const int* runs, int n_runs, float* records);
 /* Pipelines and the dense queue (NULL when unqueued). */
@@ -424,8 +424,9 @@ int  r360_sequence_info(r360_sequence* s, int* pipelines, r360_dense_queue** que
 /* Pipeline p's context, calibration, frame ring (up to cap handles) and OS thread id. */
 int  r360_sequence_pipeline(r360_sequence* s, int p, r360_ctx** ctx, r360_calib** calib, r360_frame** frames, int cap,
                             int* n_frames, long* thread_id);
-/* Host seconds per pipeline since the last reset: out[4 p + k], k = load + build enqueue, PbMap stage (RegisterPbMap
- * and submit), dense wait, pairs registered. */
+/* Host seconds per pipeline since the last reset: out[8 p + k], k = 0 load + build enqueue (with the collects that
+ * free a buffer), 1 PbMap stage (RegisterPbMap and submit), 2 dense wait, 3 pairs registered; within 0 (queued):
+ * 4 build enqueue, 5 upload enqueue, 6 collects before a buffer refill; 7 unused. */
 int  r360_sequence_host_times(r360_sequence* s, double* out, int reset);
 /* Parity hook: the two raster sweeps of OrganizedMultiPlaneSegmentation::refine as k_refine* run them, on
  * 8 sensors' refinement states (-1 no label, -2 non-planar label, m >= 0 planar model m) and closeness

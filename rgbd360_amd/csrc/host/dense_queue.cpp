@@ -232,12 +232,28 @@ extern "C" int r360_dense_queue_create(int device, int max_batch, r360_dense_que
         int least = 0, greatest = 0;
         R360_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
         hipStream_t hs = nullptr;
-        R360_HIP(hipStreamCreateWithPriority(&hs, hipStreamNonBlocking, prio_env ? greatest : least));
+        // R360_QUEUE_PRIORITY=2: the queue's stream at the lowest priority (its own hardware queue), pipelines normal
+        R360_HIP(hipStreamCreateWithPriority(&hs, hipStreamNonBlocking, prio_env == 1 ? greatest : least));
         R360_HIP(hipStreamDestroy(ctx->stream));
         ctx->stream = hs;
     }
     uint32_t mask[R360_CU_MASK_WORDS];
-    if (r360_cu_mask(device, 1, mask)) {   // CU partition experiment: the queue's stream off the excluded CUs
+    // The queue's stream on a hardware queue of its own (a stream with a CU mask, here every CU, gets a dedicated HSA
+    // queue outside the pool of GPU_MAX_HW_QUEUES that plain streams share).  In the pooled queues, whose packets run
+    // in order, the batches waited behind the plane kernels of whichever pipelines shared their queue, and which ones
+    // did depended on stream creation and first use: 1240-1250 vs 1320-1335 pairs/s with its own queue, in one session
+    // (profiles/r5_queues).  R360_QUEUE_OWNQ=0 (experiment builds) leaves it in the pool.
+    static const int ownq = R360_KNOB("R360_QUEUE_OWNQ", 1);
+    if (ownq && prio_env == 0 && ctx_prio == 0) {
+        int cus = 0;
+        R360_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+        for (int w = 0; w < R360_CU_MASK_WORDS; ++w) mask[w] = 0;
+        for (int i = 0; i < cus && i < 32 * R360_CU_MASK_WORDS; ++i) mask[i / 32] |= 1u << (i % 32);
+        hipStream_t hs = nullptr;
+        R360_HIP(hipExtStreamCreateWithCUMask(&hs, R360_CU_MASK_WORDS * 32, mask));
+        R360_HIP(hipStreamDestroy(ctx->stream));
+        ctx->stream = hs;
+    } else if (r360_cu_mask(device, 1, mask)) {   // CU partition experiment: the queue's stream off the excluded CUs
         hipStream_t hs = nullptr;
         R360_HIP(hipExtStreamCreateWithCUMask(&hs, R360_CU_MASK_WORDS * 32, mask));
         R360_HIP(hipStreamDestroy(ctx->stream));

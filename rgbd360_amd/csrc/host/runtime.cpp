@@ -247,7 +247,7 @@ extern "C" void r360_ctx_destroy(r360_ctx* c) {
     hipFree(c->d_match_desc); hipFree(c->d_unary); hipFree(c->d_bin); hipFree(c->d_vhash);
     hipFree(c->d_vlist); hipFree(c->d_vcnt);
     hipHostFree(c->h_unary); hipHostFree(c->h_bin);
-    hipStreamDestroy(c->stream);
+    if (!c->stream_borrowed) hipStreamDestroy(c->stream);
     delete c;
 }
 

@@ -2,24 +2,21 @@
 //
 // The reference's loop (Registration/OdometryRGBD360.cpp:141-257) registers each new Frame360 against the previous
 // one: RegisterPbMap, the rotOffset-conjugated alignFrames360 (the Register() alias, OdometryKeyFrame360.cpp:
-// 205-254), and composes currentPose = currentPose * rigidTransf (:257).  Pair (i, i+1) needs only frames i and i+1,
-// so the caller's pairs [p0, p1) are split into contiguous runs, one per pipeline; a pipeline is a host thread of
-// this object with its own r360_ctx (HIP stream, GN state, matcher scratch) and a ring of Frame360 buffers.
+// 205-254), and composes currentPose = currentPose * rigidTransf (:257).  Pair (i, i+1) needs only frames i and i+1.
+// A call registers the pairs [p0, p1) `repeats` times; the repeats x (p1 - p0) pair registrations form one stream
+// (repeat-major) that is cut into contiguous pieces, one per pipeline: a host thread of this object with its own
+// r360_ctx (HIP stream, GN state, matcher scratch) and a ring of Frame360 buffers.  A piece is a list of segments
+// (repeat r, pairs [a, b)); its frame positions are the segments' frames a..b back to back, and positions t, t + 1
+// form a pair unless t ends a segment.  Pipelines share nothing but the dense queue: a piece builds its first frame
+// (and the first frame of each later segment) itself, which costs one extra frame build per pipeline and segment
+// boundary and no coupling between pipelines (runs that shared their edge frames waited on each other at every
+// repeat: 1.2-1.9 ms per pair, profiles/r5_seq).
 //
 // Queued mode (params.queue > 0): every pipeline's alignFrames360 goes to one dense queue (r360_dense_queue, up to
 // `queue` pairs per launch), and a pipeline keeps `depth` alignments in flight while it builds and PbMap-registers
 // the next frames.  Frames are built `lookahead` positions ahead of the pair in hand and the next frame's upload is
-// issued right after a build on the same stream.  The `repeats` passes over a run are one stream of frame positions
-// t = 0 .. repeats * nfr - 1 (frame a + t mod nfr, nfr = frames per run), so a repeat's first frames are built while
-// the previous repeat's last alignments are still in flight.  A buffer is refilled only after every pair that used
-// its previous frame was collected (the dense queue refuses a job whose frame was rebuilt meanwhile).
-//
-// Shared run edges: the frame where run p-1 ends and run p starts is built once, by pipeline p, in an edge buffer of
-// its own; pipeline p-1 registers its last pair against it.  A per-edge handshake orders the two: p-1 waits until p
-// has built the edge for the current repeat, p rebuilds it for the next repeat only after p-1 released it (collected
-// its last pair of the repeat).  Before waiting for its right edge, a pipeline collects its earlier repeats' pairs
-// (the last of them is the release the right neighbour may be waiting on).  Edges are shared only when every run has
-// at least lookahead + 1 pairs: a shorter run would refill its edge buffer before submitting the pair that reads it.
+// issued right after a build on the same stream.  A ring buffer is refilled only after every pair that used its
+// previous frame was collected (the dense queue refuses a job whose frame was rebuilt meanwhile).
 //
 // Every record equals the single-pair Register() result (batched alignments are bit-identical to lone ones).
 #include <array>
@@ -41,15 +38,7 @@
 namespace {
 
 constexpr int REC = R360_SEQ_RECORD;          // pose 16, info 36, status, SSO, error, (spare)
-constexpr double kEdgeWaitS = 120.0;          // a neighbour that neither builds nor releases its edge is stuck
 
-struct EdgeSync {
-    std::mutex m;
-    std::condition_variable cv;
-    int built = -1, released = -1;            // repeat whose edge frame pipeline p built / p-1 is done with
-    bool failed = false;                      // one of the two pipelines failed: the other stops waiting
-    bool shared = false;                      // runs p-1 and p meet at this frame
-};
 
 double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -88,7 +77,6 @@ struct r360_sequence {
     std::vector<r360_ctx*> ctx;
     std::vector<r360_calib*> cal;
     std::vector<std::vector<r360_frame*>> ring;   // per pipeline
-    std::vector<r360_frame*> edge;                // per pipeline (queued, shared edges)
     r360_dense_queue* q = nullptr;
     // persistent pipeline threads
     std::vector<std::thread> th;
@@ -99,18 +87,17 @@ struct r360_sequence {
     int done = 0;
     bool quit = false;
     // the run in progress
+    struct Seg { int rep, a, b; };               // pairs [a, b) of repeat rep
     struct Job {
         int p0 = 0, p1 = 0, repeats = 1, device_inputs = 0;
-        bool share = false;
-        std::vector<std::pair<int, int>> runs;
+        std::vector<std::vector<Seg>> piece;       // per pipeline
         const void* const* bgr = nullptr;
         const void* const* dep = nullptr;
         float* out = nullptr;
     } job;
-    std::vector<std::unique_ptr<EdgeSync>> edges;  // edges[p]: between runs p-1 and p (edges[0] unused)
     std::vector<int> rc;
     std::vector<std::string> err;
-    std::vector<std::array<double, 4>> host_s;     // per pipeline: load + build enqueue, PbMap stage, dense wait, pairs
+    std::vector<std::array<double, 8>> host_s;     // per pipeline: see r360_sequence_host_times
 };
 
 namespace {
@@ -140,22 +127,39 @@ void fill(float* rec, const float pose[16], const float info[36], int status, co
 
 const float kEye[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
 
-// One pair on the pipeline's own context (no dense queue): the reference's sequential Register() per pair.
+// The frame positions of pipeline p's piece: frame index, repeat, and whether positions t, t + 1 form a pair.
+struct Positions {
+    std::vector<int> frame, rep;
+    std::vector<char> pair;
+};
+Positions positions_of(const r360_sequence* s, int p) {
+    Positions P;
+    for (const auto& g : s->job.piece[p])
+        for (int i = g.a; i <= g.b; ++i) {
+            P.frame.push_back(i);
+            P.rep.push_back(g.rep);
+            P.pair.push_back(i < g.b);
+        }
+    return P;
+}
+
+// No dense queue: the pairs one by one on the pipeline's own context, the reference's sequential Register().
 void pipeline_plain(r360_sequence* s, int p) {
     r360_ctx* ctx = s->ctx[p];
     auto& hs = s->host_s[p];
-    const int a = s->job.runs[p].first, b = s->job.runs[p].second;
     const int wl = s->prm.workload;
-    for (int r = 0; r < s->job.repeats; ++r) {
-        r360_frame* fa = s->ring[p][0];
-        r360_frame* fb = s->ring[p][1];
-        load_frame(s, fa, a);
-        req_rc(r360_frame_build_async(fa, s->flags));
-        for (int i = a; i < b; ++i) {
-            const double t0 = now_s();
-            load_frame(s, fb, i + 1);
-            req_rc(r360_frame_build_async(fb, s->flags));
-            const double t1 = now_s();
+    const Positions X = positions_of(s, p);
+    const int T = (int)X.frame.size();
+    r360_frame* fa = s->ring[p][0];
+    r360_frame* fb = s->ring[p][1];
+    load_frame(s, fa, X.frame[0]);
+    req_rc(r360_frame_build_async(fa, s->flags));
+    for (int t = 0; t + 1 < T; ++t) {
+        const double t0 = now_s();
+        load_frame(s, fb, X.frame[t + 1]);
+        req_rc(r360_frame_build_async(fb, s->flags));
+        const double t1 = now_s();
+        if (X.pair[t]) {
             float pose[16], info[36] = {0};
             std::memcpy(pose, kEye, sizeof pose);
             r360_icp_stats st{};
@@ -181,38 +185,30 @@ void pipeline_plain(r360_sequence* s, int p) {
                 hs[0] += t1 - t0; hs[1] += t2 - t1; hs[2] += now_s() - t2; hs[3] += 1;
             }
             if (st.illposed) status = 2;
-            fill(record(s, r, i), pose, info, status, st);
-            std::swap(fa, fb);
+            fill(record(s, X.rep[t], X.frame[t]), pose, info, status, st);
+        } else {
+            hs[0] += t1 - t0;
         }
+        std::swap(fa, fb);
     }
 }
 
 void pipeline_queued(r360_sequence* s, int p) {
     r360_ctx* ctx = s->ctx[p];
     auto& hs = s->host_s[p];
-    const int a = s->job.runs[p].first, b = s->job.runs[p].second;
     const int wl = s->prm.workload;
-    const int nfr = b - a + 1, T = nfr * s->job.repeats;
-    const int P = (int)s->job.runs.size();
-    const bool left = s->job.share && p > 0 && s->edges[p]->shared;
-    const bool right = s->job.share && p + 1 < P && s->edges[p + 1]->shared;
+    const Positions X = positions_of(s, p);
+    const int T = (int)X.frame.size();
     const std::vector<r360_frame*>& fr = s->ring[p];
     const int nbuf = (int)fr.size();
     const int LA = s->prm.lookahead;
-
-    auto fidx = [&](int t) { return a + t % nfr; };
-    auto buf = [&](int t) -> r360_frame* {
-        const int k = t % nfr;
-        if (left && k == 0) return s->edge[p];
-        if (right && k == nfr - 1) return s->edge[p + 1];
-        return fr[t % nbuf];
-    };
-    auto built_here = [&](int t) { return !(right && t % nfr == nfr - 1); };
+    auto buf = [&](int t) { return fr[t % nbuf]; };
 
     struct Pending { long ticket; int t; r360_icp_stats st; };
     std::deque<Pending> pending;
-
-    auto finish = [&](Pending& pd) {
+    auto finish_front = [&]() {
+        Pending pd = pending.front();
+        pending.pop_front();
         float pose[16], info[36] = {0};
         int status;
         if (wl == R360_SEQ_DENSE) {
@@ -226,47 +222,17 @@ void pipeline_queued(r360_sequence* s, int p) {
             status = rc;
         }
         if (pd.st.illposed) status = 2;
-        fill(record(s, pd.t / nfr, fidx(pd.t)), pose, info, status, pd.st);
-        if (right && pd.t % nfr == nfr - 2) {     // the last pair of a repeat: the right neighbour's edge is free
-            EdgeSync& e = *s->edges[p + 1];
-            std::lock_guard<std::mutex> lk(e.m);
-            e.released = pd.t / nfr;
-            e.cv.notify_all();
-        }
-    };
-    auto finish_front = [&]() {
-        Pending pd = pending.front();
-        pending.pop_front();
-        finish(pd);
-    };
-    auto wait_edge = [&](EdgeSync& e, auto pred, const char* what, int frame) {
-        std::unique_lock<std::mutex> lk(e.m);
-        const bool ok = e.cv.wait_for(lk, std::chrono::duration<double>(kEdgeWaitS), [&] { return pred() || e.failed; });
-        if (!ok || !pred()) {
-            r360_set_error("pipeline %d: %s edge frame %d", p, what, frame);
-            throw Fail{};
-        }
+        fill(record(s, X.rep[pd.t], X.frame[pd.t]), pose, info, status, pd.st);
     };
     auto load = [&](int t) {
-        if (!built_here(t)) return;
-        const int k = t % nfr, r = t / nfr;
-        if (left && k == 0) {
-            // this pipeline and its left neighbour must both be done with the previous repeat's copy
-            while (!pending.empty() && pending.front().t <= t - nfr) finish_front();
-            EdgeSync& e = *s->edges[p];
-            wait_edge(e, [&] { return e.released >= r - 1; }, "left neighbour did not release", fidx(t));
-        }
-        load_frame(s, buf(t), fidx(t));
+        const double u0 = now_s();
+        load_frame(s, buf(t), X.frame[t]);
+        hs[5] += now_s() - u0;
     };
     auto build = [&](int t) {
-        if (!built_here(t)) return;
+        const double b0 = now_s();
         req_rc(r360_frame_build_async(buf(t), s->flags));
-        if (left && t % nfr == 0) {
-            EdgeSync& e = *s->edges[p];
-            std::lock_guard<std::mutex> lk(e.m);
-            e.built = t / nfr;
-            e.cv.notify_all();
-        }
+        hs[4] += now_s() - b0;
     };
 
     const int last = T - 1;
@@ -280,20 +246,15 @@ void pipeline_queued(r360_sequence* s, int p) {
         const double t0 = now_s();
         // position t + LA + 1 refills the buffer of position u = t + LA + 1 - nbuf: collect the pairs that used it
         while (!pending.empty() && pending.front().t <= t + LA + 1 - nbuf) finish_front();
+        hs[6] += now_s() - t0;
         r360_frame* cur = buf(t);
         r360_frame* nxt = buf(t + 1);
         if (t + LA <= last) build(t + LA);                  // its upload was issued one iteration earlier
         if (t + LA + 1 <= last) load(t + LA + 1);
         const double t1 = now_s();
-        if (t % nfr == nfr - 1) {                           // the last frame of a repeat: no pair
+        if (!X.pair[t]) {                                   // the last frame of a segment: no pair
             hs[0] += t1 - t0;
             continue;
-        }
-        if (!built_here(t + 1)) {                           // the right neighbour's edge frame of this repeat
-            const int R = (t + 1) / nfr;
-            while (!pending.empty() && pending.front().t / nfr < R) finish_front();
-            EdgeSync& e = *s->edges[p + 1];
-            wait_edge(e, [&] { return e.built >= R; }, "right neighbour did not build", fidx(t + 1));
         }
         long ticket = 0;
         if (wl == R360_SEQ_DENSE)
@@ -328,7 +289,10 @@ void worker(r360_sequence* s, int p) {
         }
         int rc = 0;
         std::string err;
-        if (p < (int)s->job.runs.size()) {
+        if (p < (int)s->job.piece.size() && !s->job.piece[p].empty()) {
+            // experiment builds: start pipeline p p x R360_SEQ_STAGGER_US later
+            static const int stagger_us = R360_KNOB("R360_SEQ_STAGGER_US", 0);
+            if (stagger_us) std::this_thread::sleep_for(std::chrono::microseconds((long)p * stagger_us));
             try {
                 if (s->q) pipeline_queued(s, p);
                 else pipeline_plain(s, p);
@@ -339,13 +303,6 @@ void worker(r360_sequence* s, int p) {
                 rc = -1;
                 err = std::string("pipeline: ") + e.what();
             }
-            if (rc && s->job.share)               // the neighbours must not keep waiting on this pipeline's edges
-                for (int e : {p, p + 1})
-                    if (e > 0 && e < (int)s->edges.size()) {
-                        std::lock_guard<std::mutex> lk(s->edges[e]->m);
-                        s->edges[e]->failed = true;
-                        s->edges[e]->cv.notify_all();
-                    }
         }
         std::lock_guard<std::mutex> lk(s->m);
         s->rc[p] = rc;
@@ -365,7 +322,6 @@ extern "C" void r360_sequence_default_params(r360_sequence_params* p) {
     p->queue = 16;
     p->depth = 3;
     p->lookahead = 1;
-    p->share_edges = 1;
     p->workload = R360_SEQ_FULL;
     p->max_match_planes = 25;
     p->mode = R360_PLANAR_3DoF;
@@ -407,6 +363,14 @@ extern "C" int r360_sequence_create(int device, const r360_sequence_params* prm,
         r360_ctx* c = nullptr;
         if (r360_ctx_create(device, &c)) return fail();
         s->ctx.push_back(c);
+        // experiment builds: R360_SEQ_SHARE=k puts the first k pipelines' work on the dense queue's stream
+        static const int share = R360_KNOB("R360_SEQ_SHARE", 0);
+        if (queued && p < share) {
+            R360_HIP(hipStreamSynchronize(c->stream));
+            R360_HIP(hipStreamDestroy(c->stream));
+            c->stream = r360_dense_queue_ctx(s->q)->stream;
+            c->stream_borrowed = true;
+        }
         r360_calib* k = nullptr;
         if (r360_calib_create(c, prm->rows, prm->cols, &k)) return fail();
         s->cal.push_back(k);
@@ -417,16 +381,11 @@ extern "C" int r360_sequence_create(int device, const r360_sequence_params* prm,
             if (r360_frame_create(c, k, &f)) return fail();
             s->ring.back().push_back(f);
         }
-        if (queued && s->prm.share_edges) {
-            r360_frame* f = nullptr;
-            if (r360_frame_create(c, k, &f)) return fail();
-            s->edge.push_back(f);
-        }
     }
     s->tid.assign(s->P, 0);
     s->rc.assign(s->P, 0);
     s->err.assign(s->P, std::string());
-    s->host_s.assign(s->P, std::array<double, 4>{0, 0, 0, 0});
+    s->host_s.assign(s->P, std::array<double, 8>{});
     for (int p = 0; p < s->P; ++p) s->th.emplace_back(worker, s.get(), p);
     {   // the threads' ids (host CPU accounting of the callers)
         std::unique_lock<std::mutex> lk(s->m);
@@ -447,7 +406,6 @@ extern "C" void r360_sequence_destroy(r360_sequence* s) {
     }
     s->cv_go.notify_all();
     for (auto& t : s->th) t.join();
-    for (r360_frame* f : s->edge) r360_frame_destroy(f);
     for (auto& r : s->ring)
         for (r360_frame* f : r) r360_frame_destroy(f);
     for (r360_calib* k : s->cal) r360_calib_destroy(k);
@@ -461,36 +419,35 @@ extern "C" int r360_sequence_run(r360_sequence* s, int p0, int p1, const void* c
     CHECK_ARG(s && bgr && depth && records, "null arg");
     CHECK_ARG(p1 > p0 && repeats >= 1, "empty run");
     if (bind_device(s->device)) return -1;
-    std::vector<std::pair<int, int>> rv;
-    if (runs && n_runs > 0) {
+    const int n = p1 - p0;
+    std::vector<std::vector<r360_sequence::Seg>> piece(s->P);
+    if (runs && n_runs > 0) {   // every repeat split the same way: pipeline k takes run k of each repeat
         CHECK_ARG(n_runs <= s->P, "more runs than pipelines");
         int at = p0;
         for (int k = 0; k < n_runs; ++k) {
             CHECK_ARG(runs[2 * k] == at && runs[2 * k + 1] > runs[2 * k], "runs must tile [p0, p1) in order");
-            rv.emplace_back(runs[2 * k], runs[2 * k + 1]);
+            for (int r = 0; r < repeats; ++r) piece[k].push_back({r, runs[2 * k], runs[2 * k + 1]});
             at = runs[2 * k + 1];
         }
         CHECK_ARG(at == p1, "runs must tile [p0, p1)");
-    } else {   // [p0, p1) in P contiguous runs whose sizes differ by at most one
-        const int n = p1 - p0, parts = std::min(s->P, n);
-        int at = p0;
+    } else {   // the repeats x n pair registrations as one stream, cut into P near-equal contiguous pieces
+        const long total = (long)repeats * n;
+        const int parts = (int)std::min<long>(s->P, total);
+        long at = 0;
         for (int k = 0; k < parts; ++k) {
-            const int e = at + n / parts + (k < n % parts ? 1 : 0);
-            rv.emplace_back(at, e);
+            const long e = at + total / parts + (k < total % parts ? 1 : 0);
+            for (long u = at; u < e;) {            // u = r * n + (i - p0)
+                const int r = (int)(u / n), i = (int)(u % n);
+                const int b = (int)std::min<long>(n, i + (e - u));
+                piece[k].push_back({r, p0 + i, p0 + b});
+                u += b - i;
+            }
             at = e;
         }
     }
-    int shortest = p1 - p0;
-    for (auto& r : rv) shortest = std::min(shortest, r.second - r.first);
     s->job.p0 = p0; s->job.p1 = p1; s->job.repeats = repeats; s->job.device_inputs = device_inputs;
-    s->job.runs = rv;
+    s->job.piece = std::move(piece);
     s->job.bgr = bgr; s->job.dep = depth; s->job.out = records;
-    s->job.share = s->q && !s->edge.empty() && shortest >= s->prm.lookahead + 1;
-    s->edges.clear();
-    for (size_t k = 0; k <= rv.size(); ++k) {
-        s->edges.emplace_back(new EdgeSync);
-        s->edges.back()->shared = k > 0 && k < rv.size() && rv[k - 1].second == rv[k].first;
-    }
     {
         std::lock_guard<std::mutex> lk(s->m);
         s->done = 0;
@@ -536,8 +493,8 @@ extern "C" int r360_sequence_host_times(r360_sequence* s, double* out, int reset
     CHECK_ARG(s, "null sequence");
     std::lock_guard<std::mutex> lk(s->m);
     for (int p = 0; p < s->P; ++p)
-        for (int k = 0; k < 4; ++k) {
-            if (out) out[4 * p + k] = s->host_s[p][k];
+        for (int k = 0; k < 8; ++k) {
+            if (out) out[8 * p + k] = s->host_s[p][k];
             if (reset) s->host_s[p][k] = 0;
         }
     return 0;

@@ -272,6 +272,7 @@ struct PbMapHost;                    // host PbMap (host/pbmap.cpp)
 struct r360_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    bool stream_borrowed = false;   // another object's stream (a pipeline sharing its dense queue's): not destroyed
     hipEvent_t wait_ev = nullptr;   // blocking-sync event: host waits sleep instead of spinning
     // RegisterPbMap's match tables run on the device's shared high-priority match stream (pbmap.cpp): on the
     // ctx's stream they would queue behind the new frame's stitch and pyramid, which the host does not need yet

@@ -58,6 +58,26 @@ def shard_pairs(rank: int, world: int, n_frames: int = SEQ_FRAMES) -> tuple[int,
     return p0, p0 + base + (1 if rank < extra else 0)
 
 
+def stream_pieces(p0: int, p1: int, repeats: int, P: int) -> list[list[tuple[int, int, int]]]:
+    """How r360_sequence_run cuts the repeats x (p1 - p0) pair registrations (repeat-major) into P contiguous pieces:
+    per piece its segments (repeat, first pair, last pair + 1).  Each segment costs one frame build beyond its pairs."""
+    n = p1 - p0
+    total = repeats * n
+    parts = min(P, total)
+    out, at = [], 0
+    for k in range(parts):
+        e = at + total // parts + (1 if k < total % parts else 0)
+        segs, u = [], at
+        while u < e:
+            r, i = divmod(u, n)
+            b = min(n, i + (e - u))
+            segs.append((r, p0 + i, p0 + b))
+            u += b - i
+        out.append(segs)
+        at = e
+    return out
+
+
 def pipelines_for(n_pairs: int, streams: int, min_run: int) -> int:
     """Pipelines for a shard: at most `streams`, each with a run of at least `min_run` pairs (every run
     rebuilds its halo frame, so short runs cost extra frame builds)."""
@@ -91,7 +111,7 @@ def trajectory_error(T: np.ndarray, gt: np.ndarray) -> dict:
 class SequenceParams(C.Structure):
     """r360_sequence_params (include/rgbd360_hip.h)."""
     _fields_ = [("rows", C.c_int), ("cols", C.c_int), ("pipelines", C.c_int), ("queue", C.c_int), ("depth", C.c_int),
-                ("lookahead", C.c_int), ("share_edges", C.c_int), ("workload", C.c_int),
+                ("lookahead", C.c_int), ("workload", C.c_int),
                 ("max_match_planes", C.c_size_t), ("mode", C.c_int), ("icp", IcpParams)]
 
 
@@ -105,8 +125,8 @@ class SequenceRunner:
 
     queue > 0: the pipelines' alignFrames360 calls go to one dense queue (r360_dense_queue, batches of up to
     `queue` pairs per launch); each pipeline keeps `depth` alignments in flight while it builds (`lookahead` frames
-    ahead) and PbMap-registers the next frames, and neighbouring runs share the frame where they meet.  Every record
-    is identical to the unqueued run's (a batched alignment equals the single-pair one bit for bit).
+    ahead) and PbMap-registers the next frames.  Every record is identical to the unqueued run's (a batched alignment
+    equals the single-pair one bit for bit).
 
     Attributes mirror the pipelines: ctxs / cals / frames (non-owning views of each pipeline's context, calibration
     and frame ring), queue (the dense queue's view, or None), host_s ([P, 4] host seconds: load + build enqueue,
@@ -114,14 +134,13 @@ class SequenceRunner:
 
     def __init__(self, device: int, rows: int, cols: int, pipelines: int, params: IcpParams,
                  planes: bool = True, max_match_planes: int = 25, mode: int = PLANAR_3DoF, dense_only: bool = False,
-                 queue: int = 0, planes_only: bool = False, depth: int = 1, lookahead: int = 1,
-                 share_edges: bool = True):
+                 queue: int = 0, planes_only: bool = False, depth: int = 1, lookahead: int = 1):
         L = lib()
         sp = SequenceParams()
         L.r360_sequence_default_params(C.byref(sp))
         sp.rows, sp.cols, sp.pipelines = rows, cols, pipelines
         sp.queue = 0 if planes_only else queue
-        sp.depth, sp.lookahead, sp.share_edges = max(1, depth), max(1, lookahead), int(share_edges)
+        sp.depth, sp.lookahead = max(1, depth), max(1, lookahead)
         sp.workload = SEQ_PLANES if planes_only else SEQ_DENSE if dense_only or not planes else SEQ_FULL
         sp.max_match_planes, sp.mode = max_match_planes, mode
         sp.icp = params
@@ -146,14 +165,15 @@ class SequenceRunner:
             self.frames.append([Frame360._view(C.c_void_p(fr[k]), cal) for k in range(min(n.value, 16))])
             self.native_ids.add(tid.value)
         self.host_s = np.zeros((pipelines, 4))
+        self.host_detail = np.zeros((pipelines, 4))   # build enqueue, upload enqueue, refill collects, edge waits
 
     def run(self, p0: int, p1: int, frames_of, out: np.ndarray, repeats: int = 1, runs=None,
             device_inputs: bool = False):
         """Registers pairs [p0, p1) `repeats` times (out: (repeats, p1 - p0, REC) float32); frames_of(i) returns
         frame i's (bgr, depth): host arrays, which must outlive the call, or with device_inputs device pointers of
-        images resident in HBM.  runs: the pipelines' pair runs (default: [p0, p1) split over the pipelines)."""
-        runs = runs or split_range(p0, p1, self.P)
-        assert len(runs) <= self.P and out.dtype == np.float32 and out.flags.c_contiguous
+        images resident in HBM.  The repeats x (p1 - p0) registrations form one stream cut into contiguous pieces, one
+        per pipeline; runs (optional): pair runs tiling [p0, p1), pipeline k taking run k of every repeat instead."""
+        assert (runs is None or len(runs) <= self.P) and out.dtype == np.float32 and out.flags.c_contiguous
         assert out.shape[0] >= repeats and out.shape[1] == p1 - p0 and out.shape[2] == REC
         n = p1 - p0 + 1
         bgr, dep = (C.c_void_p * n)(), (C.c_void_p * n)()
@@ -166,13 +186,14 @@ class SequenceRunner:
                 assert b.dtype == np.uint8 and d.dtype == np.uint16 and b.flags.c_contiguous and d.flags.c_contiguous
                 keep.append((b, d))
                 bgr[k], dep[k] = b.ctypes.data, d.ctypes.data
-        rv = np.asarray(runs, np.int32).reshape(-1)
+        rv = np.asarray(runs if runs else [(0, 0)], np.int32).reshape(-1)
         L = lib()
-        rc = L.r360_sequence_run(self.h, p0, p1, bgr, dep, int(device_inputs), repeats, rv.ctypes.data, len(runs),
-                                 out.ctypes.data)
-        hs = np.zeros(4 * self.P)
+        rc = L.r360_sequence_run(self.h, p0, p1, bgr, dep, int(device_inputs), repeats, rv.ctypes.data,
+                                 len(runs) if runs else 0, out.ctypes.data)
+        hs = np.zeros(8 * self.P)
         L.r360_sequence_host_times(self.h, hs.ctypes.data, 1)
-        self.host_s += hs.reshape(self.P, 4)
+        self.host_s += hs.reshape(self.P, 8)[:, :4]
+        self.host_detail += hs.reshape(self.P, 8)[:, 4:]
         if rc != 0:
             raise RuntimeError(f"r360_sequence_run: {L.r360_last_error().decode()}")
 

@@ -39,6 +39,23 @@ def test_pair_partition_covers_each_pair_once(world, streams, min_run):
     assert max(sizes) - min(sizes) <= 1
 
 
+@pytest.mark.parametrize("world", [1, 8])
+@pytest.mark.parametrize("steps,P", [(10, 10), (3, 10), (1, 16), (10, 7)])
+def test_stream_pieces_cover_every_step_pair_once(world, steps, P):
+    """The runner's default work split (r360_sequence_run, odometry.stream_pieces): the steps x shard pairs, repeat-
+    major, cut into at most P contiguous pieces of near-equal size; every (step, pair) exactly once, in order."""
+    for r in range(world):
+        p0, p1 = OD.shard_pairs(r, world)
+        pieces = OD.stream_pieces(p0, p1, steps, P)
+        assert 1 <= len(pieces) <= P
+        flat = [(rep, i) for segs in pieces for rep, a, b in segs for i in range(a, b)]
+        assert flat == [(rep, i) for rep in range(steps) for i in range(p0, p1)]
+        sizes = [sum(b - a for _, a, b in segs) for segs in pieces]
+        assert max(sizes) - min(sizes) <= 1
+        for segs in pieces:
+            assert all(p0 <= a < b <= p1 for _, a, b in segs)
+
+
 def test_compose_is_the_prefix_product():
     rng = np.random.default_rng(1)
     rec = np.zeros((5, OD.REC), np.float32)
@@ -131,7 +148,7 @@ class _StubRunner:
         self.rank = int(os.environ["RANK"])
 
     def run(self, p0, p1, frames_of, out, repeats=1, runs=None, device_inputs=False):
-        assert runs[0][0] == p0 and runs[-1][1] == p1
+        assert runs is None or (runs[0][0] == p0 and runs[-1][1] == p1)
         for i in range(p0, p1):
             for f in (i, i + 1):
                 b, d = frames_of(f)
