@@ -460,6 +460,9 @@ def main(argv=None, runner_factory=None):
                     help="dense queue: alignments in flight per pipeline (each needs one more Frame360 buffer)")
     ap.add_argument("--lookahead", type=int, default=1,
                     help="dense queue: frames whose build is enqueued ahead of the pair being registered")
+    ap.add_argument("--plane-batch", type=int, default=8,
+                    help="plane stages of up to N frames per launch on one stream (0: each pipeline builds its frames' "
+                         "planes on its own stream)")
     ap.add_argument("--emulate", type=str, default=None,
                     help="RANK/WORLD: run that rank's shard alone (single-GPU rehearsal of an N-GPU shard)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -520,7 +523,8 @@ def main(argv=None, runner_factory=None):
     runner = (runner_factory or OD.SequenceRunner)(local, args.rows, args.cols, P, params,
                                                    planes=args.workload != "dense", dense_only=args.workload == "dense",
                                                    queue=args.queue, planes_only=args.workload == "planes",
-                                                   depth=args.depth, lookahead=args.lookahead)
+                                                   depth=args.depth, lookahead=args.lookahead,
+                                                   **({"plane_batch": args.plane_batch} if runner_factory is None else {}))
     ctxs = runner.ctxs + ([runner.queue.ctx] if runner.queue else [])
     dense_ctx = runner.queue.ctx if runner.queue else ctxs[0]   # where pipeline 0's alignments run
 
@@ -549,6 +553,7 @@ def main(argv=None, runner_factory=None):
         c.timing_reset()
         c.kernel_time_reset()
     q0 = runner.queue.stats() if runner.queue else None
+    pq0 = runner.plane_stats() if hasattr(runner, "plane_stats") else None
     ru0 = os.times()
     th0 = thread_cpu_s()
     t0 = time.perf_counter()
@@ -582,6 +587,12 @@ def main(argv=None, runner_factory=None):
     if runner.queue:   # batches of the timed run
         q1 = runner.queue.stats()
         qstats = {"batches": q1["batches"] - q0["batches"], "jobs": q1["jobs"] - q0["jobs"], "max_batch": q1["max_batch"]}
+    pqstats = None
+    if pq0 is not None:   # the plane queue's batches of the timed run
+        pq1 = runner.plane_stats()
+        pqstats = {"batches": pq1["batches"] - pq0["batches"], "frames": pq1["frames"] - pq0["frames"],
+                   "max_batch": pq1["max_batch"]}
+        pqstats["mean_batch"] = pqstats["frames"] / max(pqstats["batches"], 1)
     for c in ctxs:
         c.timing(False)
         ms, n = c.timing_read("k_icp_pass_L0")
@@ -737,6 +748,7 @@ def main(argv=None, runner_factory=None):
             "extra_frame_builds_per_step": halo_per_step,
             "dense_batch": args.queue, "dense_in_flight_per_pipeline": args.depth if args.queue else 1,
             "frames_built_ahead": args.lookahead if args.queue else 1,
+            "plane_batch": args.plane_batch,
             **({"emulated_shard": f"{shard_rank}/{shard_world}"} if args.emulate else {}),
         },
         "value_hbm_resident_inputs": resident,
@@ -764,6 +776,7 @@ def main(argv=None, runner_factory=None):
         "host_cores_busy": round(host_cores_busy, 2),
         "host_cores_split": host_split,
         **({"dense_queue": {**qstats, "mean_batch": qstats["jobs"] / max(qstats["batches"], 1)}} if qstats else {}),
+        **({"plane_queue": pqstats} if pqstats and pqstats["batches"] else {}),
         **({"per_rank": per_rank} if per_rank else {"gather_ms": gather_s * 1e3}),
         "frame_generation_s": round(gen_s, 1),
     }

@@ -401,6 +401,8 @@ typedef struct {
     int queue;                      /* dense queue batch (pairs per launch); 0 = each pipeline aligns alone */
     int depth;                      /* queued: alignments in flight per pipeline                        */
     int lookahead;                  /* queued: frames built ahead of the pair in hand                   */
+    int plane_batch;                /* plane stages of up to this many frames per launch on one stream (0: each
+                                       pipeline builds its frames' planes on its own stream)            */
     int workload;                   /* R360_SEQ_*                                                       */
     size_t max_match_planes;        /* RegisterPbMap (25)                                               */
     int mode;                       /* registrationType (PLANAR_3DoF)                                   */
@@ -421,6 +423,8 @@ int  r360_sequence_run(r360_sequence* s, int p0, int p1, const void* const* bgr,
                        int device_inputs, int repeats, const int* runs, int n_runs, float* records);
 /* Pipelines and the dense queue (NULL when unqueued). */
 int  r360_sequence_info(r360_sequence* s, int* pipelines, r360_dense_queue** queue);
+/* The plane queue's batches, frames and largest batch so far, and its context (NULL without one). */
+int  r360_sequence_plane_stats(r360_sequence* s, long* batches, long* frames, int* max_batch_seen, r360_ctx** ctx);
 /* Pipeline p's context, calibration, frame ring (up to cap handles) and OS thread id. */
 int  r360_sequence_pipeline(r360_sequence* s, int p, r360_ctx** ctx, r360_calib** calib, r360_frame** frames, int cap,
                             int* n_frames, long* thread_id);

@@ -214,6 +214,7 @@ _SIGS = [
     ("r360_sequence_pipeline", C.c_int, [_P, C.c_int, C.POINTER(_P), C.POINTER(_P), _P, C.c_int, _IP,
                                          C.POINTER(C.c_long)]),
     ("r360_sequence_host_times", C.c_int, [_P, _P, C.c_int]),
+    ("r360_sequence_plane_stats", C.c_int, [_P, C.POINTER(C.c_long), C.POINTER(C.c_long), _IP, C.POINTER(_P)]),
     ("r360_icp_eval", C.c_int, [_P, _P, _P, C.c_int, _FP, C.c_int, C.POINTER(IcpParams), _DP, _DP, _DP, _IP,
                                 _IP]),
     ("r360_icp_eval_occ", C.c_int, [_P, _P, _P, C.c_int, _FP, C.c_int, C.c_int, C.POINTER(IcpParams), _DP, _DP,

@@ -147,6 +147,7 @@ extern "C" int r360_frame_save_bin(r360_frame* f, const char* path) {
 #pragma clang fp contract(off)
 static int sphere_cloud_from_device(r360_frame* f, SphereCloudHost& sc) {
     const PlaneBufs& P = f->pl;
+    planes_join(f);   // a plane queue builds the cloud on its own stream: its frame's assembly has waited for it
     const size_t per = (size_t)P.w * P.h, n = 8 * per;
     std::vector<float4> xyz(n);
     std::vector<uchar4> rgb(n);

@@ -366,6 +366,7 @@ int plane_bufs_alloc(r360_frame* f) {
     R360_HIP(hipHostMalloc(&P.contour, sizeof(float4) * P.contour_cap));
     R360_HIP(hipHostMalloc(&P.vox, sizeof(VoxOut) * P.vox_cap));
     R360_HIP(hipEventCreateWithFlags(&P.done, hipEventDisableTiming | hipEventBlockingSync));
+    R360_HIP(hipEventCreateWithFlags(&P.ready, hipEventDisableTiming));
     R360_HIP(hipMalloc(&P.totals, sizeof(long) * 4));
     R360_HIP(hipMalloc(&P.err, sizeof(int)));
     R360_HIP(hipHostMalloc(&P.h_out, sizeof(PlaneOut) * 8 * R360_MAX_MODELS));
@@ -384,6 +385,7 @@ void plane_bufs_free(r360_frame* f) {
     hipHostFree(P.h_out);
     hipHostFree(P.h_nmodels);
     if (P.done) hipEventDestroy(P.done);
+    if (P.ready) hipEventDestroy(P.ready);
     P = PlaneBufs();
     delete f->pbmap;
     f->pbmap = nullptr;
@@ -412,24 +414,77 @@ int ctx_vhash_reserve(r360_ctx* ctx, long min_cells, long list_entries, long lis
     return 0;
 }
 
-// GPU part of getPlanes (enqueued on the ctx stream): cloud, filter, normals, segmentation
+PlaneGeom plane_geom(const r360_frame* f) {
+    const PlaneBufs& P = f->pl;
+    return PlaneGeom{f->rows, f->cols, P.w, P.h, P.sd_max, P.grid_cells};
+}
+
+PlaneDev plane_dev(const r360_frame* f, const VoxScratch& vs) {
+    const PlaneBufs& P = f->pl;
+    PlaneDev D;
+    D.depth_m = f->d_depth_m; D.bgr = f->d_bgr;
+    D.cloud = P.cloud; D.rgb = P.rgb; D.nrm = P.nrm; D.dist0 = P.dist0; D.dist = P.dist; D.grids = P.grids; D.zmm = P.zmm;
+    D.parent = P.parent; D.root = P.root; D.lab = P.lab; D.labf = P.labf; D.cnt = P.cnt; D.aux = P.aux; D.chunk = P.chunk;
+    D.nlab = P.nlab; D.big = P.big; D.nbig = P.nbig; D.mom = P.mom; D.models = P.models; D.nmodels = P.nmodels;
+    D.state = P.state; D.state2 = P.state2; D.mask = P.mask; D.rbnd = P.rbnd; D.rflag = P.rflag;
+    D.rcode = P.rcode; D.rmsk = P.rmsk; D.rf1 = P.rf1; D.rf2 = P.rf2;
+    D.out = P.out; D.gpart = P.gpart; D.contour = P.contour; D.vox = P.vox; D.totals = P.totals; D.err = P.err;
+    D.h_out = P.h_out; D.h_nmodels = P.h_nmodels; D.rt = f->calib->d_rt;
+    D.vhash = vs.vhash; D.vlist = vs.vlist; D.vcnt = vs.vcnt;
+    D.contour_cap = P.contour_cap; D.vox_cap = P.vox_cap; D.vhash_cap = vs.cap;
+    return D;
+}
+
+// the chain of the plane stage (cloud, filter, normals, segmentation, refinement, descriptors' statistics, contours,
+// voxel fallback, publication into the frames' pinned host buffers) for F frames of the same size
+int planes_launch(const PlaneBatch& B, int F, const PlaneGeom& G, hipStream_t st, r360_ctx* tctx) {
+    // k_plane_begin (first kernel of launch_cloud_normals) zeroes the error word
+    if (launch_cloud_normals(B, F, G, st, tctx)) return -1;
+    if (launch_segmentation(B, F, G, st, tctx)) return -1;
+    return launch_plane_publish(B, F, st);
+}
+
+int plane_ticket_wait(const std::shared_ptr<PlaneTicket>& tk);   // plane_queue.cpp
+
+// GPU part of getPlanes: cloud, filter, normals, segmentation — enqueued on the frame's ctx stream, or submitted to
+// the ctx's plane queue (batched with other frames on the queue's stream)
 int planes_enqueue(r360_frame* f) {
     if (plane_bufs_alloc(f)) return -1;
     planes_join(f);
     PlaneBufs& P = f->pl;
-    // k_plane_begin (first kernel of launch_cloud_normals) zeroes the error word
-    if (launch_cloud_normals(f)) return -1;
-    if (launch_segmentation(f)) return -1;
-    if (launch_plane_publish(f)) return -1;
+    P.ticket.reset();
+    if (f->ctx->plane_q) {
+        if (plane_queue_submit(f->ctx->plane_q, f)) return -1;
+        return planes_spawn_assembly(f);
+    }
+    const PlaneGeom G = plane_geom(f);
+    long cells, entries, groups;
+    vox_scratch_need(G, &cells, &entries, &groups);
+    r360_ctx* ctx = f->ctx;
+    if (ctx_vhash_reserve(ctx, cells, entries, groups)) return -1;
+    PlaneBatch B;   // a batch of one (kernel arguments, copied at each launch)
+    std::memset(&B, 0, sizeof B);
+    B.f[0] = plane_dev(f, VoxScratch{ctx->d_vhash, (unsigned long long)ctx->vhash_cap, ctx->d_vlist, ctx->d_vcnt});
+    if (planes_launch(B, 1, G, ctx->stream, ctx)) return -1;
     R360_HIP(hipEventRecord(P.done, f->ctx->stream));
+    return planes_spawn_assembly(f);
+}
+
+// the per-plane host work of the frame runs on its own thread as soon as the GPU part is done, overlapping other
+// frames' kernels and the caller
+int planes_spawn_assembly(r360_frame* f) {
+    PlaneBufs& P = f->pl;
     delete f->pbmap;
     f->pbmap = nullptr;
-    // the per-plane host work of this frame runs on its own thread as soon as the GPU part is done,
-    // overlapping other frames' kernels and the caller
     P.worker_rc = 0;
     P.worker_err.clear();
     P.worker = new std::thread([f] {
         PlaneBufs& Q = f->pl;
+        if (Q.ticket && plane_ticket_wait(Q.ticket) != 0) {   // plane queue: wait until `done` is recorded
+            Q.worker_rc = -1;
+            Q.worker_err = std::string("plane build: ") + r360_last_error();
+            return;
+        }
         if (event_wait(Q.done) != 0) {
             Q.worker_rc = -1;
             Q.worker_err = "plane build: GPU work failed";

@@ -1,0 +1,226 @@
+// plane_queue.cpp — the plane stage of many frames, batched on one stream.
+//
+// Frame360::getPlanes (Frame360.h:615-640, 942-1081) per frame is a chain of ~35 kernels whose longest links
+// (the boundary trace, the refinement sweeps, the plane fit) are one workgroup per sensor.  With every pipeline
+// running its frames' chains on its own stream, those streams share the few pooled hardware queues (in-order
+// packets): a frame's chain waited behind the other pipelines' kernels, 5.4 ms per frame under load against 0.81 ms
+// alone (profiles/r5_queues).  Here the pipelines' frames go to one queue: a dispatcher thread takes every frame
+// waiting (up to max_batch of one size) and launches the chain ONCE for all of them (PlaneBatch: kernel grid z = the
+// frames), so a batch of F frames costs one chain of launches and its one-workgroup-per-sensor kernels run F x 8
+// workgroups side by side.  The queue's stream has a hardware queue of its own (CU-masked stream).  Each frame keeps
+// its own buffers and host assembly thread; its results equal its lone build's bit for bit (the kernels are the
+// same and every frame's arithmetic is independent of the others').
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include "../r360_internal.h"
+
+struct PlaneTicket {
+    std::mutex m;
+    std::condition_variable cv;
+    bool enqueued = false;   // the batch's kernels and the frame's `done` event are on the queue's stream
+    int rc = 0;
+    std::string err;
+};
+
+struct r360_plane_queue {
+    r360_ctx* ctx = nullptr;   // the queue's stream (and per-launch timing)
+    int max_batch = R360_PLANE_BATCH;
+    std::vector<VoxScratch> vox;   // voxel-fallback scratch per batch slot
+    std::vector<long> vox_cells, vox_entries, vox_groups;
+    struct Item { r360_frame* f; std::shared_ptr<PlaneTicket> tk; };
+    std::deque<Item> pending;
+    std::mutex m;
+    std::condition_variable cv;
+    bool quit = false;
+    std::thread worker;
+    int max_inflight = 1;                 // batches on the stream at once: the next one accumulates meanwhile
+    std::deque<hipEvent_t> inflight, free_ev;
+    long batches = 0, frames = 0;
+    int max_seen = 0;
+};
+
+int planes_launch(const PlaneBatch& B, int F, const PlaneGeom& G, hipStream_t st, r360_ctx* tctx);   // pbmap.cpp
+
+namespace {
+
+bool same_geom(const PlaneGeom& a, const PlaneGeom& b) {
+    return a.rows == b.rows && a.cols == b.cols && a.w == b.w && a.h == b.h && a.sd_max == b.sd_max &&
+           a.grid_cells == b.grid_cells;
+}
+
+// slot j's voxel scratch sized for G (zeroed hash table: k_vox_compact leaves the cells it used zero again)
+int vox_reserve(r360_plane_queue* q, int j, const PlaneGeom& G) {
+    long cells, entries, groups;
+    vox_scratch_need(G, &cells, &entries, &groups);
+    VoxScratch& v = q->vox[j];
+    if (q->vox_entries[j] < entries || q->vox_groups[j] < groups) {
+        hipFree(v.vlist);
+        hipFree(v.vcnt);
+        v.vlist = nullptr;
+        v.vcnt = nullptr;
+        R360_HIP(hipMalloc(&v.vlist, sizeof(int) * entries));
+        R360_HIP(hipMalloc(&v.vcnt, sizeof(int) * groups));
+        q->vox_entries[j] = entries;
+        q->vox_groups[j] = groups;
+    }
+    long cap = 1;
+    while (cap < cells) cap <<= 1;
+    if (q->vox_cells[j] < cap) {
+        hipFree(v.vhash);
+        v.vhash = nullptr;
+        R360_HIP(hipMalloc(&v.vhash, sizeof(VoxCell) * cap));
+        R360_HIP(hipMemsetAsync(v.vhash, 0, sizeof(VoxCell) * cap, q->ctx->stream));
+        q->vox_cells[j] = cap;
+        v.cap = (unsigned long long)cap;
+    }
+    return 0;
+}
+
+void dispatcher(r360_plane_queue* q) {
+    (void)hipSetDevice(q->ctx->device);
+    for (;;) {
+        // the next batch is taken only once fewer than max_inflight are on the stream, so frames that arrive while
+        // one runs go into the same launch
+        while ((int)q->inflight.size() >= q->max_inflight) {
+            (void)event_wait(q->inflight.front());
+            q->free_ev.push_back(q->inflight.front());
+            q->inflight.pop_front();
+        }
+        std::vector<r360_plane_queue::Item> take;
+        {
+            std::unique_lock<std::mutex> lk(q->m);
+            q->cv.wait(lk, [&] { return q->quit || !q->pending.empty(); });
+            if (q->pending.empty()) return;   // quit with nothing pending
+            const PlaneGeom G0 = plane_geom(q->pending.front().f);
+            for (auto it = q->pending.begin(); it != q->pending.end() && (int)take.size() < q->max_batch;) {
+                if (same_geom(plane_geom(it->f), G0)) { take.push_back(*it); it = q->pending.erase(it); }
+                else ++it;
+            }
+        }
+        const int F = (int)take.size();
+        const PlaneGeom G = plane_geom(take[0].f);
+        int rc = 0;
+        PlaneBatch B;
+        std::memset(&B, 0, sizeof B);
+        for (int j = 0; j < F && rc == 0; ++j) {
+            r360_frame* f = take[j].f;
+            rc = vox_reserve(q, j, G);
+            if (rc == 0 && hipStreamWaitEvent(q->ctx->stream, f->pl.ready, 0) != hipSuccess) {
+                r360_set_error("plane queue: hipStreamWaitEvent failed");
+                rc = -1;
+            }
+            B.f[j] = plane_dev(f, q->vox[j]);
+        }
+        if (rc == 0) rc = planes_launch(B, F, G, q->ctx->stream, q->ctx);
+        for (int j = 0; j < F && rc == 0; ++j)
+            if (hipEventRecord(take[j].f->pl.done, q->ctx->stream) != hipSuccess) {
+                r360_set_error("plane queue: hipEventRecord failed");
+                rc = -1;
+            }
+        if (rc == 0) {
+            hipEvent_t e = nullptr;
+            if (!q->free_ev.empty()) { e = q->free_ev.back(); q->free_ev.pop_back(); }
+            else if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
+            if (e && hipEventRecord(e, q->ctx->stream) == hipSuccess) q->inflight.push_back(e);
+        }
+        const std::string err = rc ? r360_last_error() : std::string();
+        for (auto& it : take) {
+            std::lock_guard<std::mutex> lk(it.tk->m);
+            it.tk->rc = rc;
+            it.tk->err = err;
+            it.tk->enqueued = true;
+            it.tk->cv.notify_all();
+        }
+        std::lock_guard<std::mutex> lk(q->m);
+        ++q->batches;
+        q->frames += F;
+        if (F > q->max_seen) q->max_seen = F;
+    }
+}
+
+}  // namespace
+
+int plane_queue_create(int device, int max_batch, r360_plane_queue** out) {
+    // experiment builds: R360_PLANE_INFLIGHT batches on the stream at once (default 1)
+    static const int inflight = R360_KNOB("R360_PLANE_INFLIGHT", 1);
+    CHECK_ARG(out && max_batch >= 1 && max_batch <= R360_PLANE_BATCH, "plane queue: max_batch must be 1..8");
+    r360_ctx* ctx = nullptr;
+    if (int rc = r360_ctx_create(device, &ctx)) return rc;
+    // a hardware queue of its own: a stream with a CU mask (all CUs) is not put in the pooled queues
+    int cus = 0;
+    R360_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    uint32_t mask[R360_CU_MASK_WORDS] = {0};
+    for (int i = 0; i < cus && i < 32 * R360_CU_MASK_WORDS; ++i) mask[i / 32] |= 1u << (i % 32);
+    hipStream_t hs = nullptr;
+    R360_HIP(hipExtStreamCreateWithCUMask(&hs, R360_CU_MASK_WORDS * 32, mask));
+    R360_HIP(hipStreamSynchronize(ctx->stream));
+    R360_HIP(hipStreamDestroy(ctx->stream));
+    ctx->stream = hs;
+    auto* q = new r360_plane_queue;
+    q->ctx = ctx;
+    q->max_batch = max_batch;
+    q->max_inflight = inflight > 0 ? inflight : 1;
+    q->vox.assign(max_batch, VoxScratch{nullptr, 0, nullptr, nullptr});
+    q->vox_cells.assign(max_batch, 0);
+    q->vox_entries.assign(max_batch, 0);
+    q->vox_groups.assign(max_batch, 0);
+    q->worker = std::thread(dispatcher, q);
+    *out = q;
+    return 0;
+}
+
+void plane_queue_destroy(r360_plane_queue* q) {
+    if (!q) return;
+    {
+        std::lock_guard<std::mutex> lk(q->m);
+        q->quit = true;
+    }
+    q->cv.notify_all();
+    q->worker.join();
+    (void)hipSetDevice(q->ctx->device);
+    (void)hipStreamSynchronize(q->ctx->stream);
+    for (auto& v : q->vox) { hipFree(v.vhash); hipFree(v.vlist); hipFree(v.vcnt); }
+    for (hipEvent_t e : q->inflight) hipEventDestroy(e);
+    for (hipEvent_t e : q->free_ev) hipEventDestroy(e);
+    r360_ctx_destroy(q->ctx);
+    delete q;
+}
+
+r360_ctx* plane_queue_ctx(r360_plane_queue* q) { return q ? q->ctx : nullptr; }
+
+int plane_queue_stats(const r360_plane_queue* q, long* batches, long* frames, int* max_batch_seen) {
+    CHECK_ARG(q, "null plane queue");
+    auto* mq = const_cast<r360_plane_queue*>(q);
+    std::lock_guard<std::mutex> lk(mq->m);
+    if (batches) *batches = q->batches;
+    if (frames) *frames = q->frames;
+    if (max_batch_seen) *max_batch_seen = q->max_seen;
+    return 0;
+}
+
+// The frame's inputs (upload, undistort) are enqueued on its own stream: its ready event marks their end, and the
+// queue's stream waits on it.  The frame's ticket tells its assembly thread when `done` has been recorded.
+int plane_queue_submit(r360_plane_queue* q, r360_frame* f) {
+    CHECK_ARG(q && f, "null arg");
+    PlaneBufs& P = f->pl;
+    R360_HIP(hipEventRecord(P.ready, f->ctx->stream));
+    auto tk = std::make_shared<PlaneTicket>();
+    P.ticket = tk;
+    {
+        std::lock_guard<std::mutex> lk(q->m);
+        q->pending.push_back(r360_plane_queue::Item{f, tk});
+    }
+    q->cv.notify_one();
+    return 0;
+}
+
+// Waits until the frame's batch is enqueued (its `done` event recorded); returns the dispatcher's rc.
+int plane_ticket_wait(const std::shared_ptr<PlaneTicket>& tk) {
+    std::unique_lock<std::mutex> lk(tk->m);
+    tk->cv.wait(lk, [&] { return tk->enqueued; });
+    if (tk->rc) r360_set_error("%s", tk->err.c_str());
+    return tk->rc;
+}

@@ -78,6 +78,7 @@ struct r360_sequence {
     std::vector<r360_calib*> cal;
     std::vector<std::vector<r360_frame*>> ring;   // per pipeline
     r360_dense_queue* q = nullptr;
+    r360_plane_queue* pq = nullptr;               // the pipelines' plane stages, batched (plane_batch > 0)
     // persistent pipeline threads
     std::vector<std::thread> th;
     std::vector<long> tid;
@@ -322,6 +323,7 @@ extern "C" void r360_sequence_default_params(r360_sequence_params* p) {
     p->queue = 16;
     p->depth = 3;
     p->lookahead = 1;
+    p->plane_batch = R360_PLANE_BATCH;
     p->workload = R360_SEQ_FULL;
     p->max_match_planes = 25;
     p->mode = R360_PLANAR_3DoF;
@@ -340,6 +342,7 @@ extern "C" int r360_sequence_create(int device, const r360_sequence_params* prm,
     CHECK_ARG(prm->rows > 0 && prm->cols > 0, "rows / cols");
     CHECK_ARG(prm->workload >= R360_SEQ_FULL && prm->workload <= R360_SEQ_DENSE, "workload");
     CHECK_ARG(prm->queue >= 0 && prm->queue <= R360_MAX_BATCH, "queue must be 0..R360_MAX_BATCH_ALIGN");
+    CHECK_ARG(prm->plane_batch >= 0 && prm->plane_batch <= R360_PLANE_BATCH, "plane_batch must be 0..8");
     if (bind_device(device)) return -1;
     std::unique_ptr<r360_sequence> s(new r360_sequence);
     s->device = device;
@@ -358,11 +361,15 @@ extern "C" int r360_sequence_create(int device, const r360_sequence_params* prm,
     };
     if (s->prm.queue > 0 && r360_dense_queue_create(device, s->prm.queue, &s->q)) return fail();
     const bool queued = s->q != nullptr;
+    if (s->prm.workload != R360_SEQ_DENSE && s->prm.plane_batch > 0 &&
+        plane_queue_create(device, s->prm.plane_batch, &s->pq))
+        return fail();
     const int nbuf = queued ? s->prm.depth + s->prm.lookahead + 2 : 2;
     for (int p = 0; p < s->P; ++p) {
         r360_ctx* c = nullptr;
         if (r360_ctx_create(device, &c)) return fail();
         s->ctx.push_back(c);
+        c->plane_q = s->pq;
         // experiment builds: R360_SEQ_SHARE=k puts the first k pipelines' work on the dense queue's stream
         static const int share = R360_KNOB("R360_SEQ_SHARE", 0);
         if (queued && p < share) {
@@ -409,6 +416,7 @@ extern "C" void r360_sequence_destroy(r360_sequence* s) {
     for (auto& r : s->ring)
         for (r360_frame* f : r) r360_frame_destroy(f);
     for (r360_calib* k : s->cal) r360_calib_destroy(k);
+    if (s->pq) plane_queue_destroy(s->pq);
     if (s->q) r360_dense_queue_destroy(s->q);
     for (r360_ctx* c : s->ctx) r360_ctx_destroy(c);
     delete s;
@@ -472,6 +480,19 @@ extern "C" int r360_sequence_info(r360_sequence* s, int* pipelines, r360_dense_q
     if (pipelines) *pipelines = s->P;
     if (queue) *queue = s->q;
     return 0;
+}
+
+extern "C" int r360_sequence_plane_stats(r360_sequence* s, long* batches, long* frames, int* max_batch_seen,
+                                         r360_ctx** ctx) {
+    CHECK_ARG(s, "null sequence");
+    if (ctx) *ctx = plane_queue_ctx(s->pq);
+    if (!s->pq) {
+        if (batches) *batches = 0;
+        if (frames) *frames = 0;
+        if (max_batch_seen) *max_batch_seen = 0;
+        return 0;
+    }
+    return plane_queue_stats(s->pq, batches, frames, max_batch_seen);
 }
 
 extern "C" int r360_sequence_pipeline(r360_sequence* s, int p, r360_ctx** ctx, r360_calib** calib, r360_frame** frames,

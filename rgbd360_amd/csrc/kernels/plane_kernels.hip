@@ -74,7 +74,7 @@ __device__ __forceinline__ float cloud_point_impl(const float* __restrict__ dept
     }
 }
 
-__global__ void k_cloud(const float* __restrict__ depth_m, const uint8_t* __restrict__ bgr, int rows, int cols,
+__device__ __forceinline__ void d_cloud(const float* __restrict__ depth_m, const uint8_t* __restrict__ bgr, int rows, int cols,
                         float inv_f, float ox, float oy, float4* __restrict__ cloud, uchar4* __restrict__ rgb,
                         int* __restrict__ zmm, int* __restrict__ wmm) {
     const int w = cols / 2, h = rows / 2;
@@ -107,18 +107,28 @@ __global__ void k_cloud(const float* __restrict__ depth_m, const uint8_t* __rest
         }
     }
 }
+__global__ void k_cloud(const PlaneBatch B, int rows, int cols, float inv_f, float ox, float oy) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    d_cloud(D.depth_m, D.bgr, rows, cols, inv_f, ox, oy, D.cloud, D.rgb, D.zmm, reinterpret_cast<int*>(D.dist0));
+}
+
 
 
 // the frame's plane stage starts: depth-range accumulators and the error word (one launch instead of memsets)
-__global__ void k_plane_begin(int* __restrict__ zmm, int* __restrict__ err) {
+__device__ __forceinline__ void d_plane_begin(int* __restrict__ zmm, int* __restrict__ err) {
     const int t = threadIdx.x;
     if (t < 8) zmm[t] = kOrdMinInit;
     else if (t < 16) zmm[t] = kOrdMaxInit;
     if (t == 0) *err = 0;
 }
+__global__ void k_plane_begin(const PlaneBatch B) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    d_plane_begin(D.zmm, D.err);
+}
+
 
 // per-sensor depth range from k_cloud's per-wave partials (waves inside one sensor)
-__global__ void __launch_bounds__(1024) k_zrange(const int* __restrict__ wmm, long N, int* __restrict__ zmm) {
+__device__ __forceinline__ void d_zrange(const int* __restrict__ wmm, long N, int* __restrict__ zmm) {
     __shared__ int smin[16], smax[16];
     const int s = blockIdx.x;
     const long w0 = (s * N + 63) / 64, w1 = ((s + 1) * N) / 64;   // waves starting inside the sensor
@@ -142,6 +152,11 @@ __global__ void __launch_bounds__(1024) k_zrange(const int* __restrict__ wmm, lo
         }
     }
 }
+__global__ void __launch_bounds__(1024) k_zrange(const PlaneBatch B, long N) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    d_zrange(reinterpret_cast<const int*>(D.dist0), N, D.zmm);
+}
+
 
 // ------------------------------------------------------------------ A4
 // pcl::FastBilateralFilter as four fully parallel kernels over the 8 sensors:
@@ -169,7 +184,7 @@ __device__ __forceinline__ bool bil_params(const int* __restrict__ zmm, int s, i
     return !over;
 }
 
-__global__ void __launch_bounds__(BIL_COLS) k_bil_splat(const float4* __restrict__ cloud_all, int w, int h, long sw,
+__device__ __forceinline__ void d_bil_splat(const float4* __restrict__ cloud_all, int w, int h, long sw,
                                                        long sh, const int* __restrict__ zmm, int sd_max,
                                                        float2* __restrict__ grids, long grid_cells,
                                                        int* __restrict__ err) {
@@ -212,9 +227,14 @@ __global__ void __launch_bounds__(BIL_COLS) k_bil_splat(const float4* __restrict
     float2* A = grids + (long)s * 2 * grid_cells;
     for (long z = 0; z < sd; ++z) A[z * ncol + col] = make_float2(cx[z][t], cy[z][t]);
 }
+__global__ void __launch_bounds__(BIL_COLS) k_bil_splat(const PlaneBatch B, int w, int h, long sw, long sh, int sd_max, long grid_cells) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    d_bil_splat(D.cloud, w, h, sw, sh, D.zmm, sd_max, D.grids, grid_cells, D.err);
+}
+
 
 template <int AX>
-__global__ void k_bil_blur(float2* __restrict__ grids, long grid_cells, int src_slot, long sw, long sh,
+__device__ __forceinline__ void d_bil_blur(float2* __restrict__ grids, long grid_cells, int src_slot, long sw, long sh,
                            const int* __restrict__ zmm, int sd_max) {
     const int s = blockIdx.y;
     float bmin, bmax;
@@ -246,8 +266,14 @@ __global__ void k_bil_blur(float2* __restrict__ grids, long grid_cells, int src_
     }
     dst[c] = make_float2((b1[0].x + b1[2].x + 2.0f * b1[1].x) / 4.0f, (b1[0].y + b1[2].y + 2.0f * b1[1].y) / 4.0f);
 }
+template <int AX>
+__global__ void k_bil_blur(const PlaneBatch B, long grid_cells, int src_slot, long sw, long sh, int sd_max) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    d_bil_blur<AX>(D.grids, grid_cells, src_slot, sw, sh, D.zmm, sd_max);
+}
 
-__global__ void k_bil_slice(float4* __restrict__ cloud_all, int w, int h, long sw, long sh,
+
+__device__ __forceinline__ void d_bil_slice(float4* __restrict__ cloud_all, int w, int h, long sw, long sh,
                             const int* __restrict__ zmm, int sd_max, const float2* __restrict__ grids, long grid_cells,
                             int slot) {
     const long N = (long)w * h, total = 8 * N;
@@ -288,6 +314,11 @@ __global__ void k_bil_slice(float4* __restrict__ cloud_all, int w, int h, long s
         cloud_all[i].z = D0 / D1;
     }
 }
+__global__ void k_bil_slice(const PlaneBatch B, int w, int h, long sw, long sh, int sd_max, long grid_cells, int slot) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    d_bil_slice(D.cloud, w, h, sw, sh, D.zmm, sd_max, D.grids, grid_cells, slot);
+}
+
 
 // ------------------------------------------------------------------ A6: depth-change map
 __device__ __forceinline__ bool dc_fail(float depth, float other) {
@@ -295,7 +326,7 @@ __device__ __forceinline__ bool dc_fail(float depth, float other) {
     return fabsf(depth - other) > ddc || !isfin(depth) || !isfin(other);
 }
 
-__global__ void k_dcm(const float4* __restrict__ cloud, int w, int h, float* __restrict__ dist) {
+__device__ __forceinline__ void d_dcm(const float4* __restrict__ cloud, int w, int h, float* __restrict__ dist) {
     const long N = (long)w * h, total = 8 * N;
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
         const int s = (int)(i / N);
@@ -310,6 +341,11 @@ __global__ void k_dcm(const float4* __restrict__ cloud, int w, int h, float* __r
         dist[i] = edge ? 0.0f : (float)(w + h);
     }
 }
+__global__ void k_dcm(const PlaneBatch B, int w, int h) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    d_dcm(D.cloud, w, h, D.dist0);
+}
+
 
 // ------------------------------------------------------------------ A6: distance map
 // The reference runs a forward and a backward chamfer pass over the whole image (1.0 / 1.4 steps).
@@ -324,7 +360,7 @@ constexpr int DM_BAND = 4, DM_HALO = 10, DM_TPB = 512;   // short bands: the hal
 
 __device__ __forceinline__ void dm_sync() { __syncthreads(); }
 
-__global__ void __launch_bounds__(DM_TPB) k_distmap(const float* __restrict__ init, int w, int h,
+__device__ __forceinline__ void d_distmap(const float* __restrict__ init, int w, int h,
                                                    float* __restrict__ out) {
     extern __shared__ float sm[];   // (DM_BAND + 2*DM_HALO + 2) rows x w, plus two temp rows
     const int s = blockIdx.y;
@@ -380,6 +416,11 @@ __global__ void __launch_bounds__(DM_TPB) k_distmap(const float* __restrict__ in
     const int rend = min(h, r0 + DM_BAND);
     for (int k = threadIdx.x; k < (rend - r0) * w; k += blockDim.x) out[s * N + (long)r0 * w + k] = L(r0)[k];
 }
+__global__ void __launch_bounds__(DM_TPB) k_distmap(const PlaneBatch B, int w, int h) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    d_distmap(D.dist0, w, h, D.dist);
+}
+
 
 // ------------------------------------------------------------------ A6: normals
 // Window sums of the central differences are sums of floats whose ulps are >= 2^-36 and whose
@@ -411,10 +452,10 @@ __device__ __forceinline__ void normal_out(const double (&gx)[3], const double (
     }
 }
 
-__global__ void __launch_bounds__(NT_TPB) k_normals(const float4* __restrict__ cloud, const float* __restrict__ dist,
+__device__ __forceinline__ void d_normals(const float4* __restrict__ cloud, const float* __restrict__ dist,
                                                    int w, int h, float4* __restrict__ nrm) {
     __shared__ float4 sdx[NT_SR * NT_SC], sdy[NT_SR * NT_SC];
-    const int s = blockIdx.z;
+    const int s = blockIdx.z & 7;   // sensor (blockIdx.z / 8: the frame of the batch)
     const int r0 = blockIdx.y * NT_R, c0 = blockIdx.x * NT_C;
     const long N = (long)w * h;
     const float4* P = cloud + (long)s * N;
@@ -485,6 +526,11 @@ __global__ void __launch_bounds__(NT_TPB) k_normals(const float4* __restrict__ c
         nrm[i] = o;
     }
 }
+__global__ void __launch_bounds__(NT_TPB) k_normals(const PlaneBatch B, int w, int h) {
+    const PlaneDev& D = B.f[blockIdx.z >> 3];
+    d_normals(D.cloud, D.dist, w, h, D.nrm);
+}
+
 
 
 // k_normals with the window sums read from summed-area tables of the staged tile instead of summed over the
@@ -496,10 +542,10 @@ __global__ void __launch_bounds__(NT_TPB) k_normals(const float4* __restrict__ c
 constexpr int NS_W = NT_SC + 1, NS_H = NT_SR + 1;   // table size with the leading zero row / column
 struct SatShared { double v[3][NS_H * NS_W]; int c[NS_H * NS_W]; };
 
-__global__ void __launch_bounds__(NT_TPB) k_normals_sat(const float4* __restrict__ cloud, const float* __restrict__ dist,
+__device__ __forceinline__ void d_normals_sat(const float4* __restrict__ cloud, const float* __restrict__ dist,
                                                        int w, int h, float4* __restrict__ nrm) {
     __shared__ SatShared T;
-    const int s = blockIdx.z;
+    const int s = blockIdx.z & 7;   // sensor (blockIdx.z / 8: the frame of the batch)
     const int r0 = blockIdx.y * NT_R, c0 = blockIdx.x * NT_C;
     const long N = (long)w * h;
     const float4* P = cloud + (long)s * N;
@@ -627,71 +673,71 @@ __global__ void __launch_bounds__(NT_TPB) k_normals_sat(const float4* __restrict
         nrm[(long)s * N + r * w + c] = o;
     }
 }
+__global__ void __launch_bounds__(NT_TPB) k_normals_sat(const PlaneBatch B, int w, int h) {
+    const PlaneDev& D = B.f[blockIdx.z >> 3];
+    d_normals_sat(D.cloud, D.dist, w, h, D.nrm);
+}
+
 
 }  // namespace
 
 // ------------------------------------------------------------------ launchers
-int launch_cloud_normals(r360_frame* f) {
-    PlaneBufs& P = f->pl;
-    hipStream_t st = f->ctx->stream;
-    const int w = P.w, h = P.h;
+int launch_cloud_normals(const PlaneBatch& B, int F, const PlaneGeom& G, hipStream_t st, r360_ctx* tctx) {
+    const int w = G.w, h = G.h;
     const long tot = 8L * w * h;
     const int blocks = (int)((tot + 255) / 256);
+    const unsigned nf = (unsigned)F;   // grid z: the batch's frames
     // CloudRGBD_Ext.h:97-102 constants, evaluated as the reference writes them
-    const float res_factor_VGA = f->cols / 640.0;
+    const float res_factor_VGA = G.cols / 640.0;
     const float focal_length = 525 * res_factor_VGA;
     const float inv_f = 1.f / focal_length;
-    const float ox = f->cols / 2 - 0.5, oy = f->rows / 2 - 0.5;
-    int slot = timing_begin(f->ctx, "k_cloud");
-    hipLaunchKernelGGL(k_plane_begin, dim3(1), dim3(64), 0, st, P.zmm, P.err);
-    hipLaunchKernelGGL(k_cloud, dim3(blocks), dim3(256), 0, st, f->d_depth_m, f->d_bgr, f->rows, f->cols, inv_f, ox, oy,
-                       P.cloud, P.rgb, P.zmm, reinterpret_cast<int*>(P.dist0));
-    hipLaunchKernelGGL(k_zrange, dim3(8), dim3(1024), 0, st, reinterpret_cast<const int*>(P.dist0), (long)w * h, P.zmm);
-    timing_end(f->ctx, slot);
+    const float ox = G.cols / 2 - 0.5, oy = G.rows / 2 - 0.5;
+    int slot = timing_begin(tctx, "k_cloud");
+    hipLaunchKernelGGL(k_plane_begin, dim3(1, 1, nf), dim3(64), 0, st, B);
+    hipLaunchKernelGGL(k_cloud, dim3(blocks, 1, nf), dim3(256), 0, st, B, G.rows, G.cols, inv_f, ox, oy);
+    hipLaunchKernelGGL(k_zrange, dim3(8, 1, nf), dim3(1024), 0, st, B, (long)w * h);
+    timing_end(tctx, slot);
     R360_HIP(hipGetLastError());
-    slot = timing_begin(f->ctx, "k_bilateral");
+    slot = timing_begin(tctx, "k_bilateral");
     {
         // grid extent (FastBilateralFilter): sw, sh from the image size; sd per sensor on the device
         const long sw = (long)(unsigned long)((float)(w - 1) / 10.0f) + 5;
         const long sh = (long)(unsigned long)((float)(h - 1) / 10.0f) + 5;
-        if (P.sd_max != BIL_SD_MAX || sw * sh * P.sd_max > P.grid_cells) {
+        if (G.sd_max != BIL_SD_MAX || sw * sh * G.sd_max > G.grid_cells) {
             r360_set_error("bilateral grid configuration mismatch");
             return -1;
         }
         const long ncol = sw * sh;
-        hipLaunchKernelGGL(k_bil_splat, dim3((ncol + BIL_COLS - 1) / BIL_COLS, 8), dim3(BIL_COLS), 0, st, P.cloud, w, h,
-                           sw, sh, P.zmm, P.sd_max, P.grids, P.grid_cells, P.err);
-        const dim3 gb((unsigned)((ncol * P.sd_max + 255) / 256), 8);
-        hipLaunchKernelGGL(k_bil_blur<0>, gb, dim3(256), 0, st, P.grids, P.grid_cells, 0, sw, sh, P.zmm, P.sd_max);
-        hipLaunchKernelGGL(k_bil_blur<1>, gb, dim3(256), 0, st, P.grids, P.grid_cells, 1, sw, sh, P.zmm, P.sd_max);
-        hipLaunchKernelGGL(k_bil_blur<2>, gb, dim3(256), 0, st, P.grids, P.grid_cells, 0, sw, sh, P.zmm, P.sd_max);
-        hipLaunchKernelGGL(k_bil_slice, dim3(blocks), dim3(256), 0, st, P.cloud, w, h, sw, sh, P.zmm, P.sd_max, P.grids,
-                           P.grid_cells, 1);
+        hipLaunchKernelGGL(k_bil_splat, dim3((ncol + BIL_COLS - 1) / BIL_COLS, 8, nf), dim3(BIL_COLS), 0, st, B, w, h,
+                           sw, sh, G.sd_max, G.grid_cells);
+        const dim3 gb((unsigned)((ncol * G.sd_max + 255) / 256), 8, nf);
+        hipLaunchKernelGGL(k_bil_blur<0>, gb, dim3(256), 0, st, B, G.grid_cells, 0, sw, sh, G.sd_max);
+        hipLaunchKernelGGL(k_bil_blur<1>, gb, dim3(256), 0, st, B, G.grid_cells, 1, sw, sh, G.sd_max);
+        hipLaunchKernelGGL(k_bil_blur<2>, gb, dim3(256), 0, st, B, G.grid_cells, 0, sw, sh, G.sd_max);
+        hipLaunchKernelGGL(k_bil_slice, dim3(blocks, 1, nf), dim3(256), 0, st, B, w, h, sw, sh, G.sd_max, G.grid_cells, 1);
     }
-    timing_end(f->ctx, slot);
+    timing_end(tctx, slot);
     R360_HIP(hipGetLastError());
-    slot = timing_begin(f->ctx, "k_dcm");
-    hipLaunchKernelGGL(k_dcm, dim3(blocks), dim3(256), 0, st, P.cloud, w, h, P.dist0);
-    timing_end(f->ctx, slot);
+    slot = timing_begin(tctx, "k_dcm");
+    hipLaunchKernelGGL(k_dcm, dim3(blocks, 1, nf), dim3(256), 0, st, B, w, h);
+    timing_end(tctx, slot);
     R360_HIP(hipGetLastError());
     const int nb = (h + DM_BAND - 1) / DM_BAND;
     const int max_rows = DM_BAND + 2 * DM_HALO + 2;
     const size_t lds = sizeof(float) * ((size_t)max_rows + 2) * w;
     if (lds > 160 * 1024) { r360_set_error("distance map: cloud width %d too large", w); return -1; }
-    slot = timing_begin(f->ctx, "k_distmap");
-    hipLaunchKernelGGL(k_distmap, dim3(nb, 8), dim3(DM_TPB), lds, st, P.dist0, w, h, P.dist);
-    timing_end(f->ctx, slot);
+    slot = timing_begin(tctx, "k_distmap");
+    hipLaunchKernelGGL(k_distmap, dim3(nb, 8, nf), dim3(DM_TPB), lds, st, B, w, h);
+    timing_end(tctx, slot);
     R360_HIP(hipGetLastError());
-    slot = timing_begin(f->ctx, "k_normals");
-    // summed-area-table windows (default; R360_NORMALS_SAT=0: the direct window sums of k_normals)
+    slot = timing_begin(tctx, "k_normals");
+    // summed-area-table windows (default; R360_NORMALS_SAT=0: the direct window sums of k_normals); grid z = 8 sensors
+    // x the batch's frames
     static const int nsat = R360_KNOB("R360_NORMALS_SAT", 1);
-    if (nsat)
-        hipLaunchKernelGGL(k_normals_sat, dim3((w + NT_C - 1) / NT_C, (h + NT_R - 1) / NT_R, 8), dim3(NT_TPB), 0, st, P.cloud,
-                       P.dist, w, h, P.nrm);
-    else
-        hipLaunchKernelGGL(k_normals, dim3((w + NT_C - 1) / NT_C, (h + NT_R - 1) / NT_R, 8), dim3(NT_TPB), 0, st, P.cloud,
-                       P.dist, w, h, P.nrm);
-    timing_end(f->ctx, slot);
+    const dim3 gn((w + NT_C - 1) / NT_C, (h + NT_R - 1) / NT_R, 8 * nf);
+    if (nsat) hipLaunchKernelGGL(k_normals_sat, gn, dim3(NT_TPB), 0, st, B, w, h);
+    else hipLaunchKernelGGL(k_normals, gn, dim3(NT_TPB), 0, st, B, w, h);
+    timing_end(tctx, slot);
     R360_HIP(hipGetLastError());
     return 0;
 }

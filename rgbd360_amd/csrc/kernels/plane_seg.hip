@@ -18,6 +18,7 @@
 // Arithmetic follows oracle/src/planes_oracle.cpp and pbmap_oracle.cpp; see rgbd360_amd/csrc/plane_math.h.
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 #include "../r360_internal.h"
 #include "../plane_math.h"
@@ -94,7 +95,7 @@ __device__ void lds_unite(int* lp, int a, int b) {
     }
 }
 
-__global__ void __launch_bounds__(CCL_TPB) k_ccl_local(const float4* __restrict__ cloud, const float4* __restrict__ nrm,
+__device__ __forceinline__ void d_ccl_local(const float4* __restrict__ cloud, const float4* __restrict__ nrm,
                                                       int w, int h, float ang_thr, int* __restrict__ parent) {
     extern __shared__ int lp[];
     const int s = blockIdx.y, r0 = blockIdx.x * CCL_ROWS;
@@ -116,8 +117,13 @@ __global__ void __launch_bounds__(CCL_TPB) k_ccl_local(const float4* __restrict_
         parent[base + k] = v < 0 ? -1 : (int)(base + lds_find(lp, k));
     }
 }
+__global__ void __launch_bounds__(CCL_TPB) k_ccl_local(const PlaneBatch B, int w, int h, float ang_thr) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    d_ccl_local(D.cloud, D.nrm, w, h, ang_thr, D.parent);
+}
 
-__global__ void k_ccl_border(const float4* __restrict__ cloud, const float4* __restrict__ nrm, int w, int h,
+
+__device__ __forceinline__ void d_ccl_border(const float4* __restrict__ cloud, const float4* __restrict__ nrm, int w, int h,
                              float ang_thr, int* __restrict__ parent) {
     const int nb = (h - 1) / CCL_ROWS;                          // band boundaries per sensor
     const long total = 8L * nb * w;
@@ -130,12 +136,17 @@ __global__ void k_ccl_border(const float4* __restrict__ cloud, const float4* __r
         if (plane_cmp(cloud[i], nrm[i], nrm[i - w], ang_thr)) unite(parent, (int)i, (int)(i - w));
     }
 }
+__global__ void k_ccl_border(const PlaneBatch B, int w, int h, float ang_thr) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    d_ccl_border(D.cloud, D.nrm, w, h, ang_thr, D.parent);
+}
+
 
 // Roots, and the root count of every chunk of NUMC pixels of a sensor (grid (chunks, 8)) for k_ccl_number; also
 // zeroes the label counts k_ccl_label accumulates (one launch instead of a memset).
 constexpr int NUMC = 256;   // elements per chunk = threads per workgroup of the chunked numbering kernels
 
-__global__ void __launch_bounds__(NUMC) k_ccl_flatten(int* __restrict__ parent, int N, int* __restrict__ root,
+__device__ __forceinline__ void d_ccl_flatten(int* __restrict__ parent, int N, int* __restrict__ root,
                                                      int* __restrict__ cnt, int* __restrict__ ccnt) {
     const int s = blockIdx.y, j = blockIdx.x * NUMC + threadIdx.x;
     const long i = (long)s * N + j;
@@ -149,6 +160,11 @@ __global__ void __launch_bounds__(NUMC) k_ccl_flatten(int* __restrict__ parent, 
     const int c = __syncthreads_count(is_root);
     if (threadIdx.x == 0) ccnt[s * gridDim.x + blockIdx.x] = c;
 }
+__global__ void __launch_bounds__(NUMC) k_ccl_flatten(const PlaneBatch B, int N) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    d_ccl_flatten(D.parent, N, D.root, D.cnt, D.chunk);
+}
+
 
 // Exclusive rank of this thread's flag within its chunk, the chunk's offset (the sum of the counts of the chunks
 // before it in the sensor) and the chunk's total; one workgroup of NUMC threads per chunk.
@@ -170,7 +186,7 @@ __device__ __forceinline__ int chunk_rank(bool flag, const int* __restrict__ ccn
 
 // roots -> label ids in raster order; rank stored at the root's slot.  Grid (chunks, 8): a chunk's offset is the
 // sum of k_ccl_flatten's root counts of the chunks before it, its roots are ranked with a ballot scan.
-__global__ void __launch_bounds__(NUMC) k_ccl_number(const int* __restrict__ root, int N, const int* __restrict__ ccnt,
+__device__ __forceinline__ void d_ccl_number(const int* __restrict__ root, int N, const int* __restrict__ ccnt,
                                                     int* __restrict__ rank, int* __restrict__ nlab) {
     const int s = blockIdx.y, j = blockIdx.x * NUMC + threadIdx.x;
     const long i = (long)s * N + j;
@@ -180,8 +196,13 @@ __global__ void __launch_bounds__(NUMC) k_ccl_number(const int* __restrict__ roo
     if (is_root) rank[i] = off + r;
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) nlab[s] = off + tot;
 }
+__global__ void __launch_bounds__(NUMC) k_ccl_number(const PlaneBatch B, int N) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    d_ccl_number(D.root, N, D.chunk, D.parent, D.nlab);
+}
 
-__global__ void k_ccl_label(const int* __restrict__ root, const int* __restrict__ rank, int N, int* __restrict__ lab,
+
+__device__ __forceinline__ void d_ccl_label(const int* __restrict__ root, const int* __restrict__ rank, int N, int* __restrict__ lab,
                             int* __restrict__ cnt) {
     const long total = 8L * N;
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
@@ -203,6 +224,11 @@ __global__ void k_ccl_label(const int* __restrict__ root, const int* __restrict_
         }
     }
 }
+__global__ void k_ccl_label(const PlaneBatch B, int N) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    d_ccl_label(D.root, D.parent, N, D.lab, D.cnt);
+}
+
 
 // ------------------------------------------------------------------ moments
 // float min / max through integer atomics (the accumulators start at +inf / -inf; -0 orders below +0)
@@ -225,7 +251,7 @@ __device__ __forceinline__ void add128(unsigned long long* p, r360p::i128 v) {
 // (-1 for the others).  Grid (chunks of label ids, 8): k_big_count counts each chunk's large labels, k_big_list
 // ranks them after the chunks before; the sensor's last chunk also zeroes the large labels' moment accumulators
 // k_gm<false> adds into.
-__global__ void __launch_bounds__(NUMC) k_big_count(const int* __restrict__ cnt, const int* __restrict__ nlab, int N,
+__device__ __forceinline__ void d_big_count(const int* __restrict__ cnt, const int* __restrict__ nlab, int N,
                                                    int min_inliers, int* __restrict__ bmap, int* __restrict__ ccnt) {
     const int s = blockIdx.y, j = blockIdx.x * NUMC + threadIdx.x;
     const long i = (long)s * N + j;
@@ -237,8 +263,13 @@ __global__ void __launch_bounds__(NUMC) k_big_count(const int* __restrict__ cnt,
     const int c = __syncthreads_count(big);
     if (threadIdx.x == 0) ccnt[s * gridDim.x + blockIdx.x] = c;
 }
+__global__ void __launch_bounds__(NUMC) k_big_count(const PlaneBatch B, int N, int min_inliers) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    d_big_count(D.cnt, D.nlab, N, min_inliers, D.parent, D.chunk);
+}
 
-__global__ void __launch_bounds__(NUMC) k_big_list(const int* __restrict__ cnt, const int* __restrict__ nlab, int N,
+
+__device__ __forceinline__ void d_big_list(const int* __restrict__ cnt, const int* __restrict__ nlab, int N,
                                                   int min_inliers, const int* __restrict__ ccnt, int* __restrict__ big,
                                                   int* __restrict__ nbig, int maxbig, int* __restrict__ err,
                                                   int* __restrict__ bmap, r360p::Moments* __restrict__ mom,
@@ -265,6 +296,11 @@ __global__ void __launch_bounds__(NUMC) k_big_list(const int* __restrict__ cnt, 
         }
     }
 }
+__global__ void __launch_bounds__(NUMC) k_big_list(const PlaneBatch B, int N, int min_inliers, int maxbig) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    d_big_list(D.cnt, D.nlab, N, min_inliers, D.chunk, D.big, D.nbig, maxbig, D.err, D.parent, D.mom, D.aux);
+}
+
 
 // ------------------------------------------------------------------ pixel-order grouped moments
 // The moments of every large label (k_gm<false>) and of every refined model region (k_gm<true>) straight from the
@@ -403,7 +439,7 @@ __device__ __forceinline__ void gm_seg_scan(GmAcc& v, int lane, int head) {
 //   the local-frame bounds, into copy blockIdx.x % GM_COPIES.  The accumulators were zeroed (bounds at -+3.4e38) by
 //   k_big_list / k_plane_fit.
 template <bool MODEL, int CPW>   // CPW: chunks of 64 pixels per wave (a workgroup takes 256 * CPW pixels)
-__global__ void __launch_bounds__(GM_TPB) k_gm(const float4* __restrict__ cloud, const uchar4* __restrict__ rgb,
+__device__ __forceinline__ void d_gm(const float4* __restrict__ cloud, const uchar4* __restrict__ rgb,
                                              const int* __restrict__ lab, int N, const int* __restrict__ kmap,
                                              int* __restrict__ mmap_clear, const float* __restrict__ rt8,
                                              r360p::Moments* __restrict__ gmom, int* __restrict__ gfirst,
@@ -525,6 +561,12 @@ __global__ void __launch_bounds__(GM_TPB) k_gm(const float4* __restrict__ cloud,
         }
     }
 }
+template <bool MODEL, int CPW>
+__global__ void __launch_bounds__(GM_TPB) k_gm(const PlaneBatch B, int N, int exp) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    d_gm<MODEL, CPW>(D.cloud, MODEL ? D.rgb : nullptr, MODEL ? D.labf : D.lab, N, MODEL ? D.root : D.parent, MODEL ? nullptr : D.root, MODEL ? D.rt : nullptr, MODEL ? nullptr : D.mom, MODEL ? nullptr : D.aux, MODEL ? D.gpart : nullptr, exp);
+}
+
 
 // OrganizedMultiPlaneSegmentation::segment plane fit, one thread per sensor over its large labels in
 // label order (the viewpoint vp accumulates across labels, as in PCL 1.7)
@@ -534,7 +576,7 @@ __global__ void __launch_bounds__(GM_TPB) k_gm(const float4* __restrict__ cloud,
 // planar labels are then numbered in label order.
 constexpr int PF_TPB = 256;
 
-__global__ void __launch_bounds__(PF_TPB) k_plane_fit(const r360p::Moments* __restrict__ mom, const int* __restrict__ big,
+__device__ __forceinline__ void d_plane_fit(const r360p::Moments* __restrict__ mom, const int* __restrict__ big,
                                                      const int* __restrict__ nbig, int maxbig, float max_curvature,
                                                      PlaneModel* __restrict__ models, int* __restrict__ nmodels,
                                                      int* __restrict__ err, int N, int* __restrict__ mmap,
@@ -613,10 +655,15 @@ __global__ void __launch_bounds__(PF_TPB) k_plane_fit(const r360p::Moments* __re
         O.vox_off = 0;
     }
 }
+__global__ void __launch_bounds__(PF_TPB) k_plane_fit(const PlaneBatch B, int maxbig, float max_curvature, int N) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    d_plane_fit(D.mom, D.big, D.nbig, maxbig, max_curvature, D.models, D.nmodels, D.err, N, D.root, D.aux, D.out, D.gpart);
+}
+
 
 // ------------------------------------------------------------------ refine
 // state: -1 no label, -2 non-planar label, m >= 0 planar model m.  mask bit m: |model_m . p| < 0.02
-__global__ void k_refine_init(const float4* __restrict__ cloud, const int* __restrict__ lab, int N,
+__device__ __forceinline__ void d_refine_init(const float4* __restrict__ cloud, const int* __restrict__ lab, int N,
                               const PlaneModel* __restrict__ models, const int* __restrict__ nmodels,
                               int8_t* __restrict__ state, unsigned long long* __restrict__ mask) {
     const long total = 8L * N;
@@ -637,6 +684,11 @@ __global__ void k_refine_init(const float4* __restrict__ cloud, const int* __res
         mask[i] = bits;
     }
 }
+__global__ void k_refine_init(const PlaneBatch B, int N) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    d_refine_init(D.cloud, D.lab, N, D.models, D.nmodels, D.state, D.mask);
+}
+
 
 // Chain resolution of one row.  The row is laid out in walking order across the wave: lane l holds
 // the K consecutive walking positions l*K .. l*K+K-1 (left-to-right in the first sweep, right-to-left
@@ -813,10 +865,16 @@ __device__ void refine_sweeps(int8_t* __restrict__ state_all, const unsigned lon
 }
 
 template <int K>
-__global__ void __launch_bounds__(64) k_refine(int8_t* __restrict__ state_all,
+__device__ __forceinline__ void d_refine(int8_t* __restrict__ state_all,
                                               const unsigned long long* __restrict__ mask_all, int w, int h) {
     refine_sweeps<K>(state_all, mask_all, w, h, blockIdx.x, 3);
 }
+template <int K>
+__global__ void __launch_bounds__(64) k_refine(const PlaneBatch B, int w, int h) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    d_refine<K>(D.state, D.mask, w, h);
+}
+
 
 // ------------------------------------------------------------------ banded refine
 // The sweeps are sequential along rows (row r's swept states change row r+1 in the first sweep, row r-1
@@ -961,7 +1019,7 @@ __device__ void refine_band(const int8_t* __restrict__ Sin, int8_t* __restrict__
 }
 
 template <int K, int DIR>
-__global__ void __launch_bounds__(64) k_refine_p1(const int8_t* __restrict__ Sin, int8_t* __restrict__ Sout,
+__device__ __forceinline__ void d_refine_p1(const int8_t* __restrict__ Sin, int8_t* __restrict__ Sout,
                                                  const unsigned long long* __restrict__ MK, int w, int h, int rb,
                                                  int8_t* __restrict__ bnd, int* __restrict__ flag) {
     const int b = blockIdx.x, s = blockIdx.y;
@@ -970,9 +1028,15 @@ __global__ void __launch_bounds__(64) k_refine_p1(const int8_t* __restrict__ Sin
     refine_band<K, DIR>(Sin + s * N, Sout + s * N, MK + s * N, w, h, r0, r1, nullptr,
                         bnd + ((long)s * R360_REFINE_BANDS + b) * w, flag + s * R360_REFINE_BANDS + b, false);
 }
+template <int K, int DIR>
+__global__ void __launch_bounds__(64) k_refine_p1(const PlaneBatch B, int w, int h, int rb) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    d_refine_p1<K, DIR>(DIR > 0 ? D.state : D.state2, DIR > 0 ? D.state2 : D.state, D.mask, w, h, rb, D.rbnd, D.rflag);
+}
+
 
 template <int K, int DIR>
-__global__ void __launch_bounds__(64) k_refine_p2(const int8_t* __restrict__ Sin, int8_t* __restrict__ Sout,
+__device__ __forceinline__ void d_refine_p2(const int8_t* __restrict__ Sin, int8_t* __restrict__ Sout,
                                                  const unsigned long long* __restrict__ MK, int w, int h, int rb,
                                                  int nb, int8_t* __restrict__ bnd, int* __restrict__ flag) {
     const int s = blockIdx.x;
@@ -992,6 +1056,12 @@ __global__ void __launch_bounds__(64) k_refine_p2(const int8_t* __restrict__ Sin
                             Fl + b, true);
     }
 }
+template <int K, int DIR>
+__global__ void __launch_bounds__(64) k_refine_p2(const PlaneBatch B, int w, int h, int rb, int nb) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    d_refine_p2<K, DIR>(DIR > 0 ? D.state : D.state2, DIR > 0 ? D.state2 : D.state, D.mask, w, h, rb, nb, D.rbnd, D.rflag);
+}
+
 
 // ------------------------------------------------------------------ wavefront refine
 // The sweeps as anti-diagonal wavefronts.  In the first sweep a pixel's state depends only on the pixel above
@@ -1019,7 +1089,7 @@ __global__ void __launch_bounds__(64) k_refine_p2(const int8_t* __restrict__ Sin
 // loads are coalesced; code = state | static push conditions << 8.
 constexpr int RW_PF = 8;   // diagonals prefetched ahead
 
-__global__ void k_refine_skew(const int8_t* __restrict__ S, const unsigned long long* __restrict__ MK, int w, int h,
+__device__ __forceinline__ void d_refine_skew(const int8_t* __restrict__ S, const unsigned long long* __restrict__ MK, int w, int h,
                               uint16_t* __restrict__ code, unsigned long long* __restrict__ msk, int* __restrict__ fb) {
     // one thread per skewed slot (coalesced stores; the raster reads walk down-left diagonals, which reuse
     // each cache line for the next diagonals); slots outside the image are never used
@@ -1040,6 +1110,11 @@ __global__ void k_refine_skew(const int8_t* __restrict__ S, const unsigned long 
         msk[d] = MK[i];
     }
 }
+__global__ void k_refine_skew(const PlaneBatch B, int w, int h) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    d_refine_skew(D.state, D.mask, w, h, D.rcode, D.rmsk, D.rflag);
+}
+
 
 __device__ __forceinline__ bool mbit(unsigned long long m, int v) { return (v >= 0) & (((m >> (v & 63)) & 1ull) != 0); }
 
@@ -1060,7 +1135,7 @@ __device__ __forceinline__ bool mbit(unsigned long long m, int v) { return (v >=
 constexpr int RW_MAX_REDO = 64;
 
 template <int DIR>
-__global__ void __launch_bounds__(1024) k_refine_wave(const uint16_t* __restrict__ code_all,
+__device__ __forceinline__ void d_refine_wave(const uint16_t* __restrict__ code_all,
                                                       const unsigned long long* __restrict__ msk_all,
                                                       int8_t* __restrict__ f1_all, int8_t* __restrict__ f2_all,
                                                       int* __restrict__ fb, int w, int h) {
@@ -1203,6 +1278,12 @@ __global__ void __launch_bounds__(1024) k_refine_wave(const uint16_t* __restrict
         __syncthreads();
     }
 }
+template <int DIR>
+__global__ void __launch_bounds__(1024) k_refine_wave(const PlaneBatch B, int w, int h) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    d_refine_wave<DIR>(D.rcode, D.rmsk, D.rf1, DIR > 0 ? D.state : D.rf2, D.rflag, w, h);
+}
+
 
 // ------------------------------------------------------------------ pipelined wavefront
 // The same wavefront with no workgroup barrier per diagonal: wave g owns the 64-row band r0 = 64 g .. r0 + 63
@@ -1518,7 +1599,7 @@ __device__ __forceinline__ void refine_pipe_body(const uint16_t* __restrict__ co
 
 // NW: the most waves (bands) it is launched with; 4 (h <= 256) leaves each wave up to 512 VGPRs
 template <int DIR, int NW>
-__global__ void __launch_bounds__(64 * NW) k_refine_pipe(const uint16_t* __restrict__ code_all,
+__device__ __forceinline__ void d_refine_pipe(const uint16_t* __restrict__ code_all,
                                                              const unsigned long long* __restrict__ msk_all,
                                                              int8_t* __restrict__ f1_all, int8_t* __restrict__ f2_all,
                                                              const int* __restrict__ nmodels, int* __restrict__ fb,
@@ -1527,9 +1608,15 @@ __global__ void __launch_bounds__(64 * NW) k_refine_pipe(const uint16_t* __restr
     if (nmodels[blockIdx.x] <= narrow_max) refine_pipe_body<DIR, true>(code_all, msk_all, f1_all, f2_all, fb, w, h, P);
     else refine_pipe_body<DIR, false>(code_all, msk_all, f1_all, f2_all, fb, w, h, P);
 }
+template <int DIR, int NW>
+__global__ void __launch_bounds__(64 * NW) k_refine_pipe(const PlaneBatch B, int w, int h, int narrow_max) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    d_refine_pipe<DIR, NW>(D.rcode, D.rmsk, D.rf1, D.rf2, D.nmodels, D.rflag, w, h, narrow_max);
+}
+
 
 // the second sweep's states back to raster order (sensors handed to k_refine_fb are written by it)
-__global__ void k_refine_unskew(const int8_t* __restrict__ f2_all, int8_t* __restrict__ S_all,
+__device__ __forceinline__ void d_refine_unskew(const int8_t* __restrict__ f2_all, int8_t* __restrict__ S_all,
                                 const int* __restrict__ fb, int w, int h) {
     const long N = (long)w * h, SK = (long)(h + w - 1) * h, total = 8 * N;
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
@@ -1539,12 +1626,17 @@ __global__ void k_refine_unskew(const int8_t* __restrict__ f2_all, int8_t* __res
         S_all[i] = f2_all[s * SK + (long)(r + c) * h + r];
     }
 }
+__global__ void k_refine_unskew(const PlaneBatch B, int w, int h) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    d_refine_unskew(D.rf2, D.state, D.rflag, w, h);
+}
+
 
 // The exact second sweep for a sensor whose wavefront saw the wrap push fire, first at target row r0 = fb - 1:
 // rows below r0 are exact (nothing they depend on fired), so rows 0..r0 get the first sweep's states back and
 // the single-wave sweep resumes at source row r0 + 1 (re-chaining a swept row leaves it unchanged).
 template <int K>
-__global__ void __launch_bounds__(64) k_refine_fb(const int8_t* __restrict__ f1_all, const int8_t* __restrict__ f2_all,
+__device__ __forceinline__ void d_refine_fb(const int8_t* __restrict__ f1_all, const int8_t* __restrict__ f2_all,
                                                  int8_t* __restrict__ S_all,
                                                  const unsigned long long* __restrict__ MK, const int* __restrict__ fb,
                                                  int w, int h) {
@@ -1566,8 +1658,14 @@ __global__ void __launch_bounds__(64) k_refine_fb(const int8_t* __restrict__ f1_
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     refine_sweeps<K>(S_all, MK, w, h, s, 2, r0 + 1);
 }
+template <int K>
+__global__ void __launch_bounds__(64) k_refine_fb(const PlaneBatch B, int w, int h) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    d_refine_fb<K>(D.rf1, D.rf2, D.state, D.mask, D.rflag, w, h);
+}
 
-__global__ void k_refine_final(const int8_t* __restrict__ state, const int* __restrict__ lab, int N,
+
+__device__ __forceinline__ void d_refine_final(const int8_t* __restrict__ state, const int* __restrict__ lab, int N,
                                const PlaneModel* __restrict__ models, int* __restrict__ labf) {
     const long total = 8L * N;
     for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
@@ -1576,6 +1674,11 @@ __global__ void k_refine_final(const int8_t* __restrict__ state, const int* __re
         labf[i] = st >= 0 ? models[s * R360_MAX_MODELS + st].label : (st == -2 ? lab[i] : -1);
     }
 }
+__global__ void k_refine_final(const PlaneBatch B, int N) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    d_refine_final(D.state, D.lab, N, D.models, D.labf);
+}
+
 
 // findLabeledRegionBoundary (Moore-neighbour trace), all regions of a sensor in one workgroup.
 // k_nbmask first stores, per pixel, the 8-bit mask of the neighbours carrying the same refined label
@@ -1587,7 +1690,7 @@ __global__ void k_refine_final(const int8_t* __restrict__ state, const int* __re
 // an LDS list; then the whole workgroup writes the contour points to the pool in trace order.
 // Threads 0 .. 20 * 8 * R360_MAX_MODELS - 1 also fold the region accumulators' copies of k_gm<true> into the region
 // records, one word each (exact integer sums, min / max), for k_alloc and the host.
-__global__ void k_nbmask(const int* __restrict__ labf, int w, int h, uint8_t* __restrict__ nb,
+__device__ __forceinline__ void d_nbmask(const int* __restrict__ labf, int w, int h, uint8_t* __restrict__ nb,
                          const RegionPart* __restrict__ gpart, const int* __restrict__ nmodels,
                          PlaneOut* __restrict__ out) {
     const int N = w * h;
@@ -1645,6 +1748,11 @@ __global__ void k_nbmask(const int* __restrict__ labf, int w, int h, uint8_t* __
         nb[i] = (uint8_t)m;
     }
 }
+__global__ void k_nbmask(const PlaneBatch B, int w, int h) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    d_nbmask(D.labf, w, h, reinterpret_cast<uint8_t*>(D.mask), D.gpart, D.nmodels, D.out);
+}
+
 
 constexpr int TR_TPB = 1024;
 constexpr int TR_CHUNK = 32;
@@ -1664,7 +1772,7 @@ __device__ __forceinline__ int trace_next(unsigned m8, int dir) {
 }
 
 template <bool LDS>
-__global__ void __launch_bounds__(TR_TPB) k_trace(const uint8_t* __restrict__ nbg, const float4* __restrict__ cloud,
+__device__ __forceinline__ void d_trace(const uint8_t* __restrict__ nbg, const float4* __restrict__ cloud,
                                                  int w, int h, const int* __restrict__ nmodels,
                                                  PlaneOut* __restrict__ out, float4* __restrict__ pool, long pool_cap,
                                                  int* __restrict__ err) {
@@ -1795,12 +1903,18 @@ __global__ void __launch_bounds__(TR_TPB) k_trace(const uint8_t* __restrict__ nb
         } while (++n <= max_len && cidx != start);
     }
 }
+template <bool LDS>
+__global__ void __launch_bounds__(TR_TPB) k_trace(const PlaneBatch B, int w, int h) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    d_trace<LDS>(reinterpret_cast<const uint8_t*>(D.mask), D.cloud, w, h, D.nmodels, D.out, D.contour, D.contour_cap, D.err);
+}
+
 
 // contour total of the frame (profiling / pool accounting), and the voxel hash table size for this
 // frame: a power of two >= 2x a bound on the distinct voxels of the regions without a contour (per region the
 // smaller of its inliers and its bounding box's voxels), capped by the allocation
 // one workgroup of 512 threads, thread = (sensor, model)
-__global__ void __launch_bounds__(512) k_alloc(const int* __restrict__ nmodels, const PlaneOut* __restrict__ out,
+__device__ __forceinline__ void d_alloc(const int* __restrict__ nmodels, const PlaneOut* __restrict__ out,
                                                unsigned long long cap,
                                                long* __restrict__ totals) {
     __shared__ long sco[8], sca[8];
@@ -1831,6 +1945,11 @@ __global__ void __launch_bounds__(512) k_alloc(const int* __restrict__ nmodels, 
     totals[2] = (long)(t - 1);   // hash mask
     totals[3] = cand;            // bound on the voxels of the regions without a contour (0: no voxel stage work)
 }
+__global__ void __launch_bounds__(512) k_alloc(const PlaneBatch B) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    d_alloc(D.nmodels, D.out, D.vhash_cap, D.totals);
+}
+
 
 
 // pcl::VoxelGrid (leaf 0.05) of the inliers of regions without a contour (Frame360.h:1017-1026):
@@ -1870,7 +1989,7 @@ __device__ __forceinline__ void vox_global_add(VoxCell* __restrict__ tab, unsign
     atomicAdd(&tab[hsh].cnt, n);
 }
 
-__global__ void __launch_bounds__(VOX_TPB) k_vox_hash(const float4* __restrict__ cloud, const int8_t* __restrict__ state,
+__device__ __forceinline__ void d_vox_hash(const float4* __restrict__ cloud, const int8_t* __restrict__ state,
                                                      int N, const int* __restrict__ nmodels, PlaneOut* __restrict__ out,
                                                      VoxCell* __restrict__ tab, const long* __restrict__ totals,
                                                      int* __restrict__ err, int px, int* __restrict__ vlist,
@@ -1960,9 +2079,14 @@ __global__ void __launch_bounds__(VOX_TPB) k_vox_hash(const float4* __restrict__
         if (nnew[sm]) atomicAdd(&out[sm].n_vox, nnew[sm]);
     }
 }
+__global__ void __launch_bounds__(VOX_TPB) k_vox_hash(const PlaneBatch B, int N, int px) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    d_vox_hash(D.cloud, D.state, N, D.nmodels, D.out, D.vhash, D.totals, D.err, px, D.vlist, D.vcnt);
+}
+
 
 // voxel list offsets per region in (sensor, model) order: one workgroup of 512 threads, exclusive scan
-__global__ void __launch_bounds__(512) k_vox_alloc(const int* __restrict__ nmodels, PlaneOut* __restrict__ out,
+__device__ __forceinline__ void d_vox_alloc(const int* __restrict__ nmodels, PlaneOut* __restrict__ out,
                                                    long* __restrict__ totals, long vox_cap, int* __restrict__ err) {
     __shared__ long sw[8];
     const int q = threadIdx.x, lane = q & 63, wid = q >> 6;
@@ -1983,6 +2107,11 @@ __global__ void __launch_bounds__(512) k_vox_alloc(const int* __restrict__ nmode
         if (pre + x > vox_cap) atomicOr(err, 16);
     }
 }
+__global__ void __launch_bounds__(512) k_vox_alloc(const PlaneBatch B) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    d_vox_alloc(D.nmodels, D.out, D.totals, D.vox_cap, D.err);
+}
+
 
 // one workgroup per k_vox_hash workgroup: the cells that workgroup claimed (its list) are counted per region in LDS
 // (one LDS atomic per (wave, region)), one global atomic per (workgroup, region) reserves the slots, then the cells
@@ -2004,7 +2133,7 @@ __device__ __forceinline__ void wave_by_key(int key, F&& f) {
     }
 }
 
-__global__ void __launch_bounds__(VOXC_TPB) k_vox_compact(VoxCell* __restrict__ tab,
+__device__ __forceinline__ void d_vox_compact(VoxCell* __restrict__ tab,
                                                          const long* __restrict__ totals, PlaneOut* __restrict__ out,
                                                          VoxOut* __restrict__ pool, long pool_cap,
                                                          const int* __restrict__ vlist, const int* __restrict__ vcnt,
@@ -2058,11 +2187,14 @@ __global__ void __launch_bounds__(VOXC_TPB) k_vox_compact(VoxCell* __restrict__ 
         tab[c].cnt = 0;
     }
 }
+__global__ void __launch_bounds__(VOXC_TPB) k_vox_compact(const PlaneBatch B, int px) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    d_vox_compact(D.vhash, D.totals, D.out, D.vox, D.vox_cap, D.vlist, D.vcnt, px);
+}
+
 
 }  // namespace
 
-// buffers of the wavefront refinement (skewed layout, [8][h + w - 1][h] each)
-struct RefineWaveBufs { uint16_t* code; unsigned long long* msk; int8_t* f1; int8_t* f2; };
 
 // refinement mode: -1 the wavefront sweeps (default; pipelined bands for h <= 512), -2 the wavefront sweeps with a
 // barrier per diagonal, 0 the single-wave sweeps, rb > 0 banded with rb rows per band (R360_REFINE_ROWS overrides)
@@ -2074,39 +2206,34 @@ int refine_band_rows(int h) {
     return rb;
 }
 
-// refine()'s two sweeps over 8 sensors' states S (in place), closeness masks MK.  rb > 0: banded (phases 1 and
-// 2 per sweep; S2 holds the first sweep's output); rb = 0: one wave per sensor walks every row (k_refine).
-int launch_refine_sweeps(hipStream_t st, int8_t* S, int8_t* S2, const unsigned long long* MK, int8_t* bnd, int* flag,
-                         int w, int h, int rb, const RefineWaveBufs* wb, const int* nmodels) {
+// refine()'s two sweeps over 8 sensors' states (PlaneDev::state, in place) and closeness masks (mask) of each frame of
+// the batch.  rb > 0: banded (phases 1 and 2 per sweep; state2 holds the first sweep's output); rb = 0: one wave per
+// sensor walks every row (k_refine); rb < 0: the wavefront sweeps (rcode / rmsk / rf1 / rf2, rflag).
+int launch_refine_sweeps(const PlaneBatch& B, int F, hipStream_t st, int w, int h, int rb, bool wave_bufs) {
     const int K = (w + 63) / 64;
-    if (rb < 0 && (w < 2 || h > 1024 || !wb)) rb = 0;
+    const unsigned nf = (unsigned)F;
+    if (rb < 0 && (w < 2 || h > 1024 || !wave_bufs)) rb = 0;
     if (rb < 0) {
         const long slots = 8L * (h + w - 1) * h;
-        hipLaunchKernelGGL(k_refine_skew, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, st, S, MK, w, h, wb->code,
-                           wb->msk, flag);
+        hipLaunchKernelGGL(k_refine_skew, dim3((unsigned)((slots + 255) / 256), 1, nf), dim3(256), 0, st, B, w, h);
         const int tpb = 64 * ((h + 63) / 64);
         // R360_REFINE_NARROW=0: the 64-bit mask path for every sensor (inspection)
         static const int narrow_max = R360_KNOB("R360_REFINE_NARROW", 1) == 0 ? -1 : 30;
-        if (rb == -1 && h <= 64 * RP_MAXB && w <= RP_MAXW && nmodels) {
+        if (rb == -1 && h <= 64 * RP_MAXB && w <= RP_MAXW) {
             if (h <= 256) {
-                hipLaunchKernelGGL((k_refine_pipe<1, 4>), dim3(8), dim3(tpb), 0, st, wb->code, wb->msk, wb->f1, wb->f2,
-                                   nmodels, flag, w, h, narrow_max);
-                hipLaunchKernelGGL((k_refine_pipe<-1, 4>), dim3(8), dim3(tpb), 0, st, wb->code, wb->msk, wb->f1, wb->f2,
-                                   nmodels, flag, w, h, narrow_max);
+                hipLaunchKernelGGL((k_refine_pipe<1, 4>), dim3(8, 1, nf), dim3(tpb), 0, st, B, w, h, narrow_max);
+                hipLaunchKernelGGL((k_refine_pipe<-1, 4>), dim3(8, 1, nf), dim3(tpb), 0, st, B, w, h, narrow_max);
             } else {
-                hipLaunchKernelGGL((k_refine_pipe<1, RP_MAXB>), dim3(8), dim3(tpb), 0, st, wb->code, wb->msk, wb->f1,
-                                   wb->f2, nmodels, flag, w, h, narrow_max);
-                hipLaunchKernelGGL((k_refine_pipe<-1, RP_MAXB>), dim3(8), dim3(tpb), 0, st, wb->code, wb->msk, wb->f1,
-                                   wb->f2, nmodels, flag, w, h, narrow_max);
+                hipLaunchKernelGGL((k_refine_pipe<1, RP_MAXB>), dim3(8, 1, nf), dim3(tpb), 0, st, B, w, h, narrow_max);
+                hipLaunchKernelGGL((k_refine_pipe<-1, RP_MAXB>), dim3(8, 1, nf), dim3(tpb), 0, st, B, w, h, narrow_max);
             }
         } else {
-            hipLaunchKernelGGL(k_refine_wave<1>, dim3(8), dim3(tpb), 0, st, wb->code, wb->msk, wb->f1, S, flag, w, h);
-            hipLaunchKernelGGL(k_refine_wave<-1>, dim3(8), dim3(tpb), 0, st, wb->code, wb->msk, wb->f1, wb->f2, flag, w, h);
+            hipLaunchKernelGGL(k_refine_wave<1>, dim3(8, 1, nf), dim3(tpb), 0, st, B, w, h);
+            hipLaunchKernelGGL(k_refine_wave<-1>, dim3(8, 1, nf), dim3(tpb), 0, st, B, w, h);
         }
-        hipLaunchKernelGGL(k_refine_unskew, dim3((unsigned)((8L * w * h + 255) / 256)), dim3(256), 0, st, wb->f2, S, flag,
-                           w, h);
+        hipLaunchKernelGGL(k_refine_unskew, dim3((unsigned)((8L * w * h + 255) / 256), 1, nf), dim3(256), 0, st, B, w, h);
         switch (K) {
-#define R360_FB_CASE(k) case k: hipLaunchKernelGGL(k_refine_fb<k>, dim3(8), dim3(64), 0, st, wb->f1, wb->f2, S, MK, flag, w, h); break;
+#define R360_FB_CASE(k) case k: hipLaunchKernelGGL(k_refine_fb<k>, dim3(8, 1, nf), dim3(64), 0, st, B, w, h); break;
             R360_FB_CASE(1) R360_FB_CASE(2) R360_FB_CASE(3) R360_FB_CASE(4) R360_FB_CASE(5)
             R360_FB_CASE(6) R360_FB_CASE(7) R360_FB_CASE(8) R360_FB_CASE(9) R360_FB_CASE(10)
 #undef R360_FB_CASE
@@ -2120,11 +2247,11 @@ int launch_refine_sweeps(hipStream_t st, int8_t* S, int8_t* S2, const unsigned l
     switch (K) {
 #define R360_REFINE_CASE(k)                                                                                     \
     case k:                                                                                                     \
-        if (rb == 0) { hipLaunchKernelGGL(k_refine<k>, dim3(8), dim3(64), 0, st, S, MK, w, h); break; }          \
-        hipLaunchKernelGGL((k_refine_p1<k, 1>), dim3(nb, 8), dim3(64), 0, st, S, S2, MK, w, h, rb, bnd, flag);   \
-        hipLaunchKernelGGL((k_refine_p2<k, 1>), dim3(8), dim3(64), 0, st, S, S2, MK, w, h, rb, nb, bnd, flag);   \
-        hipLaunchKernelGGL((k_refine_p1<k, -1>), dim3(nb, 8), dim3(64), 0, st, S2, S, MK, w, h, rb, bnd, flag);  \
-        hipLaunchKernelGGL((k_refine_p2<k, -1>), dim3(8), dim3(64), 0, st, S2, S, MK, w, h, rb, nb, bnd, flag);  \
+        if (rb == 0) { hipLaunchKernelGGL(k_refine<k>, dim3(8, 1, nf), dim3(64), 0, st, B, w, h); break; }      \
+        hipLaunchKernelGGL((k_refine_p1<k, 1>), dim3(nb, 8, nf), dim3(64), 0, st, B, w, h, rb);                 \
+        hipLaunchKernelGGL((k_refine_p2<k, 1>), dim3(8, 1, nf), dim3(64), 0, st, B, w, h, rb, nb);              \
+        hipLaunchKernelGGL((k_refine_p1<k, -1>), dim3(nb, 8, nf), dim3(64), 0, st, B, w, h, rb);                \
+        hipLaunchKernelGGL((k_refine_p2<k, -1>), dim3(8, 1, nf), dim3(64), 0, st, B, w, h, rb, nb);             \
         break;
         R360_REFINE_CASE(1) R360_REFINE_CASE(2) R360_REFINE_CASE(3) R360_REFINE_CASE(4) R360_REFINE_CASE(5)
         R360_REFINE_CASE(6) R360_REFINE_CASE(7) R360_REFINE_CASE(8) R360_REFINE_CASE(9) R360_REFINE_CASE(10)
@@ -2137,15 +2264,13 @@ int launch_refine_sweeps(hipStream_t st, int8_t* S, int8_t* S2, const unsigned l
 
 // ------------------------------------------------------------------ launcher
 template <bool MODEL>
-int launch_gm(int px, long total, hipStream_t st, const float4* cloud, const uchar4* rgb, const int* lab, int N,
-              const int* kmap, int* mmap_clear, const float* rt8, r360p::Moments* gmom, int* gfirst, RegionPart* gpart) {
+int launch_gm(int px, long total, const PlaneBatch& B, int F, hipStream_t st, int N) {
     const unsigned blocks = (unsigned)((total + px - 1) / px);
     static const int exp = R360_KNOB("R360_EXP_GM", 0);   // timing experiments only
     switch (px) {
 #define R360_GM_CASE(cpw)                                                                                         \
     case 256 * cpw:                                                                                               \
-        hipLaunchKernelGGL((k_gm<MODEL, cpw>), dim3(blocks), dim3(GM_TPB), 0, st, cloud, rgb, lab, N, kmap,        \
-                           mmap_clear, rt8, gmom, gfirst, gpart, exp);                                            \
+        hipLaunchKernelGGL((k_gm<MODEL, cpw>), dim3(blocks, 1, (unsigned)F), dim3(GM_TPB), 0, st, B, N, exp);    \
         return 0;
         R360_GM_CASE(1) R360_GM_CASE(2) R360_GM_CASE(4) R360_GM_CASE(8) R360_GM_CASE(16)
 #undef R360_GM_CASE
@@ -2154,95 +2279,83 @@ int launch_gm(int px, long total, hipStream_t st, const float4* cloud, const uch
     return -1;
 }
 
-int launch_segmentation(r360_frame* f) {
-    PlaneBufs& P = f->pl;
-    r360_ctx* ctx = f->ctx;
-    hipStream_t st = ctx->stream;
-    const int w = P.w, h = P.h, N = w * h;
+int launch_segmentation(const PlaneBatch& B, int F, const PlaneGeom& G, hipStream_t st, r360_ctx* tctx) {
+    const int w = G.w, h = G.h, N = w * h;
     const long total = 8L * N;
     const int blocks = (int)((total + 255) / 256);
+    const unsigned nf = (unsigned)F;
     // PlaneCoefficientComparator::setAngularThreshold stores cosf(angle) (angle 0.039812, Frame360.h:959)
     const float ang_thr = cosf((float)0.039812);
-    int slot = timing_begin(ctx, "k_ccl");
-    hipLaunchKernelGGL(k_ccl_local, dim3((h + CCL_ROWS - 1) / CCL_ROWS, 8), dim3(CCL_TPB), sizeof(int) * CCL_ROWS * w,
-                       st, P.cloud, P.nrm, w, h, ang_thr, P.parent);
+    int slot = timing_begin(tctx, "k_ccl");
+    hipLaunchKernelGGL(k_ccl_local, dim3((h + CCL_ROWS - 1) / CCL_ROWS, 8, nf), dim3(CCL_TPB), sizeof(int) * CCL_ROWS * w,
+                       st, B, w, h, ang_thr);
     {
         const long edges = 8L * ((h - 1) / CCL_ROWS) * w;
         if (edges > 0)
-            hipLaunchKernelGGL(k_ccl_border, dim3((unsigned)((edges + 255) / 256)), dim3(256), 0, st, P.cloud, P.nrm, w,
-                               h, ang_thr, P.parent);
+            hipLaunchKernelGGL(k_ccl_border, dim3((unsigned)((edges + 255) / 256), 1, nf), dim3(256), 0, st, B, w, h, ang_thr);
     }
-    const int nch = (N + NUMC - 1) / NUMC;   // numbering chunks per sensor; their counts in P.chunk [8][nch]
-    hipLaunchKernelGGL(k_ccl_flatten, dim3(nch, 8), dim3(NUMC), 0, st, P.parent, N, P.root, P.cnt, P.chunk);
-    hipLaunchKernelGGL(k_ccl_number, dim3(nch, 8), dim3(NUMC), 0, st, P.root, N, P.chunk, P.parent, P.nlab);
-    hipLaunchKernelGGL(k_ccl_label, dim3(blocks), dim3(256), 0, st, P.root, P.parent, N, P.lab, P.cnt);
-    timing_end(ctx, slot);
+    const int nch = (N + NUMC - 1) / NUMC;   // numbering chunks per sensor; their counts in chunk [8][nch]
+    hipLaunchKernelGGL(k_ccl_flatten, dim3(nch, 8, nf), dim3(NUMC), 0, st, B, N);
+    hipLaunchKernelGGL(k_ccl_number, dim3(nch, 8, nf), dim3(NUMC), 0, st, B, N);
+    hipLaunchKernelGGL(k_ccl_label, dim3(blocks, 1, nf), dim3(256), 0, st, B, N);
+    timing_end(tctx, slot);
     R360_HIP(hipGetLastError());
-    slot = timing_begin(ctx, "k_plane_fit");
+    slot = timing_begin(tctx, "k_plane_fit");
     // aux: the large labels' first pixels [8][MAX_BIG].  parent / root are free after the labelling and hold the
-    // label -> large-label and label -> model maps.
-    int* bfirst = P.aux;
-    int* bmap = P.parent;
-    int* mmap = P.root;
-    hipLaunchKernelGGL(k_big_count, dim3(nch, 8), dim3(NUMC), 0, st, P.cnt, P.nlab, N, 80, bmap, P.chunk);
-    hipLaunchKernelGGL(k_big_list, dim3(nch, 8), dim3(NUMC), 0, st, P.cnt, P.nlab, N, 80, P.chunk, P.big, P.nbig,
-                       R360_MAX_BIG, P.err, bmap, P.mom, bfirst);
+    // label -> large-label and label -> model maps (the kernels' PlaneDev mapping, k_big_* / k_gm / k_plane_fit).
+    hipLaunchKernelGGL(k_big_count, dim3(nch, 8, nf), dim3(NUMC), 0, st, B, N, 80);
+    hipLaunchKernelGGL(k_big_list, dim3(nch, 8, nf), dim3(NUMC), 0, st, B, N, 80, R360_MAX_BIG);
     // pixels per workgroup of the grouped-moment kernels (R360_GM_PX, experiments)
     static const int gm_px = R360_KNOB("R360_GM_PX", GM_PX);
-    if (launch_gm<false>(gm_px, total, st, P.cloud, nullptr, P.lab, N, bmap, mmap, nullptr, P.mom, bfirst, nullptr))
-        return -1;
-    hipLaunchKernelGGL(k_plane_fit, dim3(8), dim3(PF_TPB), 0, st, P.mom, P.big, P.nbig, R360_MAX_BIG, 0.001f, P.models,
-                       P.nmodels, P.err, N, mmap, bfirst, P.out, P.gpart);
-    timing_end(ctx, slot);
+    if (launch_gm<false>(gm_px, total, B, F, st, N)) return -1;
+    hipLaunchKernelGGL(k_plane_fit, dim3(8, 1, nf), dim3(PF_TPB), 0, st, B, R360_MAX_BIG, 0.001f, N);
+    timing_end(tctx, slot);
     R360_HIP(hipGetLastError());
-    slot = timing_begin(ctx, "k_refine");
-    hipLaunchKernelGGL(k_refine_init, dim3(blocks), dim3(256), 0, st, P.cloud, P.lab, N, P.models, P.nmodels, P.state,
-                       P.mask);
-    const RefineWaveBufs wb{P.rcode, P.rmsk, P.rf1, P.rf2};
-    if (launch_refine_sweeps(st, P.state, P.state2, P.mask, P.rbnd, P.rflag, w, h, refine_band_rows(h), &wb, P.nmodels))
-        return -1;
-    hipLaunchKernelGGL(k_refine_final, dim3(blocks), dim3(256), 0, st, P.state, P.lab, N, P.models, P.labf);
-    timing_end(ctx, slot);
+    slot = timing_begin(tctx, "k_refine");
+    hipLaunchKernelGGL(k_refine_init, dim3(blocks, 1, nf), dim3(256), 0, st, B, N);
+    if (launch_refine_sweeps(B, F, st, w, h, refine_band_rows(h), true)) return -1;
+    hipLaunchKernelGGL(k_refine_final, dim3(blocks, 1, nf), dim3(256), 0, st, B, N);
+    timing_end(tctx, slot);
     R360_HIP(hipGetLastError());
-    slot = timing_begin(ctx, "k_model_stats");
-    if (launch_gm<true>(gm_px, total, st, P.cloud, P.rgb, P.labf, N, mmap, nullptr, f->calib->d_rt, nullptr, nullptr,
-                        P.gpart))
-        return -1;
+    slot = timing_begin(tctx, "k_model_stats");
+    if (launch_gm<true>(gm_px, total, B, F, st, N)) return -1;
     // the refinement's closeness masks are dead here: their storage holds the neighbour masks
-    uint8_t* nbm = reinterpret_cast<uint8_t*>(P.mask);
-    hipLaunchKernelGGL(k_nbmask, dim3(std::max(blocks, 20 * 8 * R360_MAX_MODELS / 256)), dim3(256), 0, st, P.labf, w, h, nbm,
-                       P.gpart, P.nmodels, P.out);
-    if (N <= TR_NB_MAX)
-        hipLaunchKernelGGL(k_trace<true>, dim3(8), dim3(TR_TPB), 0, st, nbm, P.cloud, w, h, P.nmodels, P.out,
-                           P.contour, P.contour_cap, P.err);
-    else
-        hipLaunchKernelGGL(k_trace<false>, dim3(8), dim3(TR_TPB), 0, st, nbm, P.cloud, w, h, P.nmodels, P.out,
-                           P.contour, P.contour_cap, P.err);
-    static const int vox_px_env = R360_KNOB("R360_VOX_PX", VOX_PX);   // experiments
-    const int vox_px = std::min(vox_px_env, N);   // a block spans at most two sensors
-    const long vox_blocks = (total + vox_px - 1) / vox_px;
-    if (ctx_vhash_reserve(ctx, 12L * N, vox_blocks * vox_px, vox_blocks)) return -1;
-    hipLaunchKernelGGL(k_alloc, dim3(1), dim3(512), 0, st, P.nmodels, P.out,
-                       (unsigned long long)ctx->vhash_cap, P.totals);
-    timing_end(ctx, slot);
+    hipLaunchKernelGGL(k_nbmask, dim3(std::max(blocks, 20 * 8 * R360_MAX_MODELS / 256), 1, nf), dim3(256), 0, st, B, w, h);
+    if (N <= TR_NB_MAX) hipLaunchKernelGGL(k_trace<true>, dim3(8, 1, nf), dim3(TR_TPB), 0, st, B, w, h);
+    else hipLaunchKernelGGL(k_trace<false>, dim3(8, 1, nf), dim3(TR_TPB), 0, st, B, w, h);
+    long cells, entries, groups;
+    vox_scratch_need(G, &cells, &entries, &groups);
+    const int vox_px = (int)(entries / groups);
+    hipLaunchKernelGGL(k_alloc, dim3(1, 1, nf), dim3(512), 0, st, B);
+    timing_end(tctx, slot);
     R360_HIP(hipGetLastError());
-    slot = timing_begin(ctx, "k_voxel");
+    slot = timing_begin(tctx, "k_voxel");
     // the voxel kernels exit at entry when no region lacks a contour (totals[3] == 0, the usual case); the table is
     // zero on allocation and k_vox_compact clears every cell it reads
-    hipLaunchKernelGGL(k_vox_hash, dim3((unsigned)vox_blocks), dim3(VOX_TPB), 0, st, P.cloud, P.state, N, P.nmodels,
-                       P.out, ctx->d_vhash, P.totals, P.err, vox_px, ctx->d_vlist, ctx->d_vcnt);
-    hipLaunchKernelGGL(k_vox_alloc, dim3(1), dim3(512), 0, st, P.nmodels, P.out, P.totals, P.vox_cap, P.err);
-    hipLaunchKernelGGL(k_vox_compact, dim3((unsigned)vox_blocks), dim3(VOXC_TPB), 0, st, ctx->d_vhash, P.totals, P.out,
-                       P.vox, P.vox_cap, ctx->d_vlist, ctx->d_vcnt, vox_px);
-    timing_end(ctx, slot);
+    hipLaunchKernelGGL(k_vox_hash, dim3((unsigned)groups, 1, nf), dim3(VOX_TPB), 0, st, B, N, vox_px);
+    hipLaunchKernelGGL(k_vox_alloc, dim3(1, 1, nf), dim3(512), 0, st, B);
+    hipLaunchKernelGGL(k_vox_compact, dim3((unsigned)groups, 1, nf), dim3(VOXC_TPB), 0, st, B, vox_px);
+    timing_end(tctx, slot);
     R360_HIP(hipGetLastError());
     return 0;
+}
+
+// hash cells (a bound on a frame's distinct (region, voxel) cells, k_alloc), and the claimed-cell lists of
+// k_vox_hash: one per workgroup of vox_px pixels (R360_VOX_PX in experiment builds)
+void vox_scratch_need(const PlaneGeom& G, long* cells, long* entries, long* groups) {
+    const int N = G.w * G.h;
+    static const int vox_px_env = R360_KNOB("R360_VOX_PX", VOX_PX);   // experiments
+    const int vox_px = std::min(vox_px_env, N);   // a block spans at most two sensors
+    const long vox_blocks = (8L * N + vox_px - 1) / vox_px;
+    *cells = 12L * N;
+    *entries = vox_blocks * vox_px;
+    *groups = vox_blocks;
 }
 
 namespace {
 // the plane stage's outputs for the host assembly, written straight into pinned host memory (one launch
 // instead of four device-to-host copies): the region records, models per sensor, error word, totals
-__global__ void k_plane_publish(const PlaneOut* __restrict__ out, const int* __restrict__ nmodels,
+__device__ __forceinline__ void d_plane_publish(const PlaneOut* __restrict__ out, const int* __restrict__ nmodels,
                                 const int* __restrict__ err, const long* __restrict__ totals, PlaneOut* __restrict__ h_out,
                                 int* __restrict__ h_nm, int nwords) {
     const int* src = reinterpret_cast<const int*>(out);
@@ -2253,14 +2366,17 @@ __global__ void k_plane_publish(const PlaneOut* __restrict__ out, const int* __r
         h_nm[t] = t < 8 ? nmodels[t] : t == 8 ? *err : reinterpret_cast<const int*>(totals)[t - 10];
     }
 }
+__global__ void k_plane_publish(const PlaneBatch B, int nwords) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    d_plane_publish(D.out, D.nmodels, D.err, D.totals, D.h_out, D.h_nmodels, nwords);
+}
+
 }  // namespace
 
-int launch_plane_publish(r360_frame* f) {
-    PlaneBufs& P = f->pl;
+int launch_plane_publish(const PlaneBatch& B, int F, hipStream_t st) {
     static_assert(sizeof(PlaneOut) % 4 == 0, "PlaneOut is copied as 32-bit words");
     const int nwords = (int)(sizeof(PlaneOut) * 8 * R360_MAX_MODELS / 4);
-    hipLaunchKernelGGL(k_plane_publish, dim3((nwords + 255) / 256), dim3(256), 0, f->ctx->stream, P.out, P.nmodels, P.err,
-                       P.totals, P.h_out, P.h_nmodels, nwords);
+    hipLaunchKernelGGL(k_plane_publish, dim3((nwords + 255) / 256, 1, (unsigned)F), dim3(256), 0, st, B, nwords);
     R360_HIP(hipGetLastError());
     return 0;
 }
@@ -2282,12 +2398,12 @@ extern "C" int r360_refine_eval(const int8_t* state, const uint64_t* mask, int w
     R360_HIP(hipMalloc(&flag, sizeof(int) * 8 * R360_REFINE_BANDS));
     R360_HIP(hipMemcpy(S, state, T, hipMemcpyHostToDevice));
     R360_HIP(hipMemcpy(MK, mask, sizeof(unsigned long long) * T, hipMemcpyHostToDevice));
-    RefineWaveBufs wb{};
+    uint16_t* code; unsigned long long* msk; int8_t *f1, *f2;
     const size_t SK = 8 * (size_t)(h + w - 1) * h;
-    R360_HIP(hipMalloc(&wb.code, sizeof(uint16_t) * SK));
-    R360_HIP(hipMalloc(&wb.msk, sizeof(unsigned long long) * SK));
-    R360_HIP(hipMalloc(&wb.f1, SK));
-    R360_HIP(hipMalloc(&wb.f2, SK));
+    R360_HIP(hipMalloc(&code, sizeof(uint16_t) * SK));
+    R360_HIP(hipMalloc(&msk, sizeof(unsigned long long) * SK));
+    R360_HIP(hipMalloc(&f1, SK));
+    R360_HIP(hipMalloc(&f2, SK));
     // models per sensor as the pipeline's k_plane_fit counts them: above every label and closeness bit
     int nmh[8], *nm;
     for (int s = 0; s < 8; ++s) {
@@ -2300,7 +2416,12 @@ extern "C" int r360_refine_eval(const int8_t* state, const uint64_t* mask, int w
     }
     R360_HIP(hipMalloc(&nm, sizeof(nmh)));
     R360_HIP(hipMemcpy(nm, nmh, sizeof(nmh), hipMemcpyHostToDevice));
-    int rc = launch_refine_sweeps(0, S, S2, MK, bnd, flag, w, h, rb, &wb, nm);
+    PlaneBatch B;
+    std::memset(&B, 0, sizeof B);
+    PlaneDev& D = B.f[0];
+    D.state = S; D.state2 = S2; D.mask = MK; D.rbnd = bnd; D.rflag = flag;
+    D.rcode = code; D.rmsk = msk; D.rf1 = f1; D.rf2 = f2; D.nmodels = nm;
+    int rc = launch_refine_sweeps(B, 1, 0, w, h, rb, true);
     if (rc == 0) {
         R360_HIP(hipMemcpy(out, S, T, hipMemcpyDeviceToHost));
         if (rb < 0 && w >= 2 && h <= 1024) {
@@ -2312,6 +2433,6 @@ extern "C" int r360_refine_eval(const int8_t* state, const uint64_t* mask, int w
         }
     }
     (void)hipFree(S); (void)hipFree(S2); (void)hipFree(MK); (void)hipFree(bnd); (void)hipFree(flag); (void)hipFree(nm);
-    (void)hipFree(wb.code); (void)hipFree(wb.msk); (void)hipFree(wb.f1); (void)hipFree(wb.f2);
+    (void)hipFree(code); (void)hipFree(msk); (void)hipFree(f1); (void)hipFree(f2);
     return rc;
 }

@@ -4,6 +4,7 @@
 #include <atomic>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <memory>
 #include <string>
 #include <thread>
 #include <vector>
@@ -262,14 +263,39 @@ struct PlaneBufs {
     int* h_nmodels = nullptr;        // [8], then err at [8], totals at (long*)(h_nmodels + 10)
     // host assembly thread (planes_enqueue -> planes_finish)
     hipEvent_t done = nullptr;
+    hipEvent_t ready = nullptr;      // plane queue: recorded on the frame's stream once its inputs are built
+    std::shared_ptr<struct PlaneTicket> ticket;   // plane queue: set when the batch's kernels and `done` are enqueued
     std::thread* worker = nullptr;
     int worker_rc = 0;
     std::string worker_err;
 };
 struct PbMapHost;                    // host PbMap (host/pbmap.cpp)
 
+// One frame's plane-stage buffers as the plane kernels see them.  Every plane kernel takes a PlaneBatch (by value, in
+// the kernel-argument segment) and serves frame blockIdx.z of it (k_normals*: blockIdx.z / 8), so one launch runs
+// the same stage of up to R360_PLANE_BATCH frames of the same size (host/plane_queue.cpp), and a lone frame's build
+// is a batch of one.
+struct PlaneDev {
+    const float* depth_m; const uint8_t* bgr;
+    float4* cloud; uchar4* rgb; float4* nrm; float* dist0; float* dist; float2* grids; int* zmm;
+    int* parent; int* root; int* lab; int* labf; int* cnt; int* aux; int* chunk; int* nlab; int* big; int* nbig;
+    r360p::Moments* mom; PlaneModel* models; int* nmodels;
+    int8_t* state; int8_t* state2; unsigned long long* mask; int8_t* rbnd; int* rflag;
+    uint16_t* rcode; unsigned long long* rmsk; int8_t* rf1; int8_t* rf2;
+    PlaneOut* out; RegionPart* gpart; float4* contour; VoxOut* vox; long* totals; int* err;
+    PlaneOut* h_out; int* h_nmodels; const float* rt;
+    VoxCell* vhash; int* vlist; int* vcnt;
+    long contour_cap, vox_cap;
+    unsigned long long vhash_cap;
+};
+#define R360_PLANE_BATCH 8
+struct PlaneBatch { PlaneDev f[R360_PLANE_BATCH]; };
+static_assert(sizeof(PlaneBatch) + 256 <= 4096, "the plane batch travels as a kernel argument");
+
 // ------------------------------------------------------------------ host objects
+struct r360_plane_queue;
 struct r360_ctx {
+    r360_plane_queue* plane_q = nullptr;   // frames built on this ctx run their plane stage on this queue (batched)
     int device = 0;
     hipStream_t stream = nullptr;
     bool stream_borrowed = false;   // another object's stream (a pipeline sharing its dense queue's): not destroyed
@@ -492,12 +518,29 @@ int ensure_defer(r360_ctx* ctx, long n_pixels);
 int ensure_batch(r360_ctx* ctx, int n, long n_pixels);
 // ctx's stream waits for the work enqueued so far on the streams of the frames' contexts
 int ctx_wait_frames(r360_ctx* ctx, r360_frame* const* frames, int n);
-int launch_cloud_normals(r360_frame* f);
-int launch_segmentation(r360_frame* f);
-int launch_plane_publish(r360_frame* f);   // plane outputs -> pinned host buffers (h_out, h_nmodels)
+// The plane stage of a batch of F frames of the same size (PlaneBatch, r360_internal.h) on stream st; tctx: the
+// context whose per-launch timing (r360_ctx_timing) records the launches, if any
+struct PlaneGeom { int rows, cols, w, h, sd_max; long grid_cells; };
+PlaneGeom plane_geom(const r360_frame* f);
+int launch_cloud_normals(const PlaneBatch& B, int F, const PlaneGeom& G, hipStream_t st, r360_ctx* tctx);
+int launch_segmentation(const PlaneBatch& B, int F, const PlaneGeom& G, hipStream_t st, r360_ctx* tctx);
+int launch_plane_publish(const PlaneBatch& B, int F, hipStream_t st);   // plane outputs -> pinned host buffers
+// voxel-fallback scratch the plane stage of one frame uses (its context's, or a plane queue slot's)
+struct VoxScratch { VoxCell* vhash; unsigned long long cap; int* vlist; int* vcnt; };
+// the voxel scratch sizes a frame of G needs: hash cells, list entries, list groups (workgroups)
+void vox_scratch_need(const PlaneGeom& G, long* cells, long* entries, long* groups);
+PlaneDev plane_dev(const r360_frame* f, const VoxScratch& vs);
 int plane_bufs_alloc(r360_frame* f);
 void plane_bufs_free(r360_frame* f);
 int planes_enqueue(r360_frame* f);
+int planes_spawn_assembly(r360_frame* f);
+// Plane queue (host/plane_queue.cpp): the plane stage of frames built on any context attached to it (ctx->plane_q),
+// batched into launches over up to max_batch frames on the queue's own stream
+int plane_queue_create(int device, int max_batch, r360_plane_queue** out);
+void plane_queue_destroy(r360_plane_queue* q);
+int plane_queue_submit(r360_plane_queue* q, r360_frame* f);   // after plane_bufs_alloc; records f's ready event
+int plane_queue_stats(const r360_plane_queue* q, long* batches, long* frames, int* max_batch_seen);
+r360_ctx* plane_queue_ctx(r360_plane_queue* q);
 int ctx_vhash_reserve(r360_ctx* ctx, long min_cells, long list_entries, long list_groups);
 int planes_finish(r360_frame* f);
 // rotOffset (157.5 deg about x, OdometryRGBD360.cpp:138-139) and its inverse; column-major 4x4 product C = A*B

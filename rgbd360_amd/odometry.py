@@ -111,7 +111,7 @@ def trajectory_error(T: np.ndarray, gt: np.ndarray) -> dict:
 class SequenceParams(C.Structure):
     """r360_sequence_params (include/rgbd360_hip.h)."""
     _fields_ = [("rows", C.c_int), ("cols", C.c_int), ("pipelines", C.c_int), ("queue", C.c_int), ("depth", C.c_int),
-                ("lookahead", C.c_int), ("workload", C.c_int),
+                ("lookahead", C.c_int), ("plane_batch", C.c_int), ("workload", C.c_int),
                 ("max_match_planes", C.c_size_t), ("mode", C.c_int), ("icp", IcpParams)]
 
 
@@ -134,13 +134,16 @@ class SequenceRunner:
 
     def __init__(self, device: int, rows: int, cols: int, pipelines: int, params: IcpParams,
                  planes: bool = True, max_match_planes: int = 25, mode: int = PLANAR_3DoF, dense_only: bool = False,
-                 queue: int = 0, planes_only: bool = False, depth: int = 1, lookahead: int = 1):
+                 queue: int = 0, planes_only: bool = False, depth: int = 1, lookahead: int = 1,
+                 plane_batch: int | None = None):
         L = lib()
         sp = SequenceParams()
         L.r360_sequence_default_params(C.byref(sp))
         sp.rows, sp.cols, sp.pipelines = rows, cols, pipelines
         sp.queue = 0 if planes_only else queue
         sp.depth, sp.lookahead = max(1, depth), max(1, lookahead)
+        if plane_batch is not None:
+            sp.plane_batch = plane_batch
         sp.workload = SEQ_PLANES if planes_only else SEQ_DENSE if dense_only or not planes else SEQ_FULL
         sp.max_match_planes, sp.mode = max_match_planes, mode
         sp.icp = params
@@ -165,6 +168,9 @@ class SequenceRunner:
             self.frames.append([Frame360._view(C.c_void_p(fr[k]), cal) for k in range(min(n.value, 16))])
             self.native_ids.add(tid.value)
         self.host_s = np.zeros((pipelines, 4))
+        pc = C.c_void_p()
+        _check(L.r360_sequence_plane_stats(h, None, None, None, C.byref(pc)), "r360_sequence_plane_stats")
+        self.plane_ctx = Context._view(pc, device) if pc.value else None
         self.host_detail = np.zeros((pipelines, 4))   # build enqueue, upload enqueue, refill collects, edge waits
 
     def run(self, p0: int, p1: int, frames_of, out: np.ndarray, repeats: int = 1, runs=None,
@@ -196,6 +202,12 @@ class SequenceRunner:
         self.host_detail += hs.reshape(self.P, 8)[:, 4:]
         if rc != 0:
             raise RuntimeError(f"r360_sequence_run: {L.r360_last_error().decode()}")
+
+    def plane_stats(self):
+        """The plane queue's {batches, frames, max_batch} so far (zeros without one)."""
+        b, f, m = C.c_long(), C.c_long(), C.c_int()
+        _check(lib().r360_sequence_plane_stats(self.h, C.byref(b), C.byref(f), C.byref(m), None), "plane_stats")
+        return {"batches": b.value, "frames": f.value, "max_batch": m.value}
 
     def close(self):
         if self.h:
