@@ -101,6 +101,11 @@ int  r360_frame_set_timestamp(r360_frame* f, uint64_t ts);
 int  r360_frame_get_timestamp(const r360_frame* f, uint64_t* ts);
 int  r360_frame_build(r360_frame* f, unsigned flags);
 int  r360_frame_build_async(r360_frame* f, unsigned flags);
+/* r360_frame_build of n distinct frames of one device (Frame360::getPlanes of a keyframe batch, Frame360.h:615-640):
+ * the plane stages of frames of one size run batched, up to 8 frames per launch of the plane kernels, on the stream
+ * of frames[0]'s context; every other stage on each frame's own stream.  Synchronous; each frame's results equal
+ * its r360_frame_build's. */
+int  r360_frames_build(r360_frame* const* frames, int n, unsigned flags);
 int  r360_frame_dims(const r360_frame* f, int* rows, int* cols, int* sph_rows, int* sph_cols);
 /* The R360_BUILD_* stages the frame's current images have been through (an upload or load clears them). */
 int  r360_frame_built(const r360_frame* f, unsigned* flags);

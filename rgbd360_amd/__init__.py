@@ -181,6 +181,7 @@ _SIGS = [
     ("r360_frame_get_plane_label", C.c_int, [_P, C.c_int, C.c_char_p, C.c_int]),
     ("r360_frame_build", C.c_int, [_P, C.c_uint]),
     ("r360_frame_build_async", C.c_int, [_P, C.c_uint]),
+    ("r360_frames_build", C.c_int, [_P, C.c_int, C.c_uint]),
     ("r360_frame_dims", C.c_int, [_P, _IP, _IP, _IP, _IP]),
     ("r360_frame_built", C.c_int, [_P, C.POINTER(C.c_uint)]),
     ("r360_frame_get_sphere", C.c_int, [_P, _P, _P]),
@@ -822,6 +823,15 @@ class RegisterRGBD360:
         n, m = ns.value, nt.value
         return dict(sid=sid[:n].copy(), tid=tid[:m].copy(), unary=un[:n * m].reshape(n, m).copy(),
                     binary=bi[:n * m * w].reshape(n * m, w).copy(), words=w)
+
+
+def frames_build(frames, flags: int = None):
+    """r360_frames_build: Frame360::getPlanes (Frame360.h:615-640) of several frames with their plane stages batched
+    (up to 8 frames of one size per launch, on frames[0]'s context stream).  Same results as building each alone."""
+    if flags is None:
+        flags = BUILD_UNDISTORT | BUILD_CLOUD | BUILD_PLANES | BUILD_SPHERE | BUILD_PYRAMID
+    arr = (C.c_void_p * len(frames))(*[f.h for f in frames])
+    _check(lib().r360_frames_build(arr, len(frames), flags), "r360_frames_build")
 
 
 def register(ctx: "Context", ref: "Frame360", trg: "Frame360", guess=None, params: "IcpParams | None" = None,

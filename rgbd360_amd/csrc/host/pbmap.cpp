@@ -414,6 +414,44 @@ int ctx_vhash_reserve(r360_ctx* ctx, long min_cells, long list_entries, long lis
     return 0;
 }
 
+int vox_slot_reserve(VoxSlot& s, const PlaneGeom& G, hipStream_t st) {
+    long cells, entries, groups;
+    vox_scratch_need(G, &cells, &entries, &groups);
+    VoxScratch& v = s.v;
+    if (s.entries < entries || s.groups < groups) {
+        hipFree(v.vlist);
+        hipFree(v.vcnt);
+        v.vlist = nullptr;
+        v.vcnt = nullptr;
+        s.entries = s.groups = 0;
+        R360_HIP(hipMalloc(&v.vlist, sizeof(int) * entries));
+        R360_HIP(hipMalloc(&v.vcnt, sizeof(int) * groups));
+        s.entries = entries;
+        s.groups = groups;
+    }
+    long cap = 1;
+    while (cap < cells) cap <<= 1;
+    if (s.cells < cap) {
+        hipFree(v.vhash);
+        v.vhash = nullptr;
+        s.cells = 0;
+        v.cap = 0;
+        R360_HIP(hipMalloc(&v.vhash, sizeof(VoxCell) * cap));
+        // zeroed once: k_vox_compact leaves every cell it used zero again
+        R360_HIP(hipMemsetAsync(v.vhash, 0, sizeof(VoxCell) * cap, st));
+        s.cells = cap;
+        v.cap = (unsigned long long)cap;
+    }
+    return 0;
+}
+
+void vox_slot_free(VoxSlot& s) {
+    hipFree(s.v.vhash);
+    hipFree(s.v.vlist);
+    hipFree(s.v.vcnt);
+    s = VoxSlot();
+}
+
 PlaneGeom plane_geom(const r360_frame* f) {
     const PlaneBufs& P = f->pl;
     return PlaneGeom{f->rows, f->cols, P.w, P.h, P.sd_max, P.grid_cells};
@@ -468,6 +506,83 @@ int planes_enqueue(r360_frame* f) {
     if (planes_launch(B, 1, G, ctx->stream, ctx)) return -1;
     R360_HIP(hipEventRecord(P.done, f->ctx->stream));
     return planes_spawn_assembly(f);
+}
+
+// Frame360::getPlanes of n frames (Frame360.h:615-640) with their plane stages batched: frames of one size go up to
+// R360_PLANE_BATCH per launch of the chain, on the stream of frames[0]'s context, each after its own undistortion
+// (on its own stream).  The other stages (stitch, pyramids) run on each frame's own stream as r360_frame_build would.
+// Every frame's results equal its lone build's.
+extern "C" int r360_frames_build(r360_frame* const* frames, int n, unsigned flags) {
+    CHECK_ARG(frames && n >= 1, "frames_build: need at least one frame");
+    for (int i = 0; i < n; ++i) {
+        CHECK_ARG(frames[i], "frames_build: null frame");
+        CHECK_ARG(frames[i]->ctx->device == frames[0]->ctx->device, "frames_build: frames of different devices");
+        CHECK_ARG(frames[i]->rows > 0 || flags == 0, "a sphere-only frame has no sensor images to build from");
+        for (int j = 0; j < i; ++j) CHECK_ARG(frames[j] != frames[i], "frames_build: a frame is listed twice");
+    }
+    const unsigned plane_flags = R360_BUILD_CLOUD | R360_BUILD_PLANES;
+    if (!(flags & plane_flags)) {
+        for (int i = 0; i < n; ++i)
+            if (int rc = r360_frame_build(frames[i], flags)) return rc;
+        return 0;
+    }
+    r360_ctx* H = frames[0]->ctx;
+    if (bind_device(H->device)) return -1;
+    for (int i = 0; i < n; ++i)
+        if (int rc = r360_frame_build_async(frames[i], R360_BUILD_UNDISTORT)) return rc;
+    if ((int)H->bvox.size() < R360_PLANE_BATCH - 1) H->bvox.resize(R360_PLANE_BATCH - 1);
+    for (int i = 0; i < n; ++i)
+        if (plane_bufs_alloc(frames[i])) return -1;
+    std::vector<char> taken(n, 0);
+    for (int i0 = 0; i0 < n; ++i0) {
+        if (taken[i0]) continue;
+        // the next batch: frame i0 and the following frames of its size, up to R360_PLANE_BATCH
+        const PlaneGeom G = plane_geom(frames[i0]);
+        std::vector<r360_frame*> bf;
+        for (int i = i0; i < n && (int)bf.size() < R360_PLANE_BATCH; ++i) {
+            const PlaneGeom g = plane_geom(frames[i]);
+            if (taken[i] || g.rows != G.rows || g.cols != G.cols || g.w != G.w || g.h != G.h ||
+                g.sd_max != G.sd_max || g.grid_cells != G.grid_cells)
+                continue;
+            taken[i] = 1;
+            bf.push_back(frames[i]);
+        }
+        PlaneBatch B;
+        std::memset(&B, 0, sizeof B);
+        long cells, entries, groups;
+        vox_scratch_need(G, &cells, &entries, &groups);
+        if (ctx_vhash_reserve(H, cells, entries, groups)) return -1;
+        for (int j = 0; j < (int)bf.size(); ++j) {
+            r360_frame* f = bf[j];
+            planes_join(f);   // a previous build's assembly still reading the buffers
+            f->pl.ticket.reset();
+            R360_HIP(hipEventRecord(f->pl.ready, f->ctx->stream));
+            R360_HIP(hipStreamWaitEvent(H->stream, f->pl.ready, 0));
+            VoxScratch vs{H->d_vhash, (unsigned long long)H->vhash_cap, H->d_vlist, H->d_vcnt};
+            if (j > 0) {
+                if (vox_slot_reserve(H->bvox[j - 1], G, H->stream)) return -1;
+                vs = H->bvox[j - 1].v;
+            }
+            B.f[j] = plane_dev(f, vs);
+        }
+        if (planes_launch(B, (int)bf.size(), G, H->stream, H)) return -1;
+        for (r360_frame* f : bf) {
+            R360_HIP(hipEventRecord(f->pl.done, H->stream));
+            if (planes_spawn_assembly(f)) return -1;
+            f->built |= R360_BUILD_UNDISTORT | plane_flags;
+            delete f->sphere_cloud;   // a cloud set by loadCloud is replaced by the built one
+            f->sphere_cloud = nullptr;
+        }
+    }
+    const unsigned rest = flags & ~(R360_BUILD_UNDISTORT | plane_flags);
+    for (int i = 0; i < n; ++i)
+        if (rest)
+            if (int rc = r360_frame_build_async(frames[i], rest)) return rc;
+    for (int i = 0; i < n; ++i) {
+        if (int rc = planes_finish(frames[i])) return rc;
+        R360_HIP(hipStreamSynchronize(frames[i]->ctx->stream));
+    }
+    return 0;
 }
 
 // the per-plane host work of the frame runs on its own thread as soon as the GPU part is done, overlapping other

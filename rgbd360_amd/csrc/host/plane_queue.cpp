@@ -28,8 +28,7 @@ struct PlaneTicket {
 struct r360_plane_queue {
     r360_ctx* ctx = nullptr;   // the queue's stream (and per-launch timing)
     int max_batch = R360_PLANE_BATCH;
-    std::vector<VoxScratch> vox;   // voxel-fallback scratch per batch slot
-    std::vector<long> vox_cells, vox_entries, vox_groups;
+    std::vector<VoxSlot> vox;   // voxel-fallback scratch per batch slot
     struct Item { r360_frame* f; std::shared_ptr<PlaneTicket> tk; };
     std::deque<Item> pending;
     std::mutex m;
@@ -49,34 +48,6 @@ namespace {
 bool same_geom(const PlaneGeom& a, const PlaneGeom& b) {
     return a.rows == b.rows && a.cols == b.cols && a.w == b.w && a.h == b.h && a.sd_max == b.sd_max &&
            a.grid_cells == b.grid_cells;
-}
-
-// slot j's voxel scratch sized for G (zeroed hash table: k_vox_compact leaves the cells it used zero again)
-int vox_reserve(r360_plane_queue* q, int j, const PlaneGeom& G) {
-    long cells, entries, groups;
-    vox_scratch_need(G, &cells, &entries, &groups);
-    VoxScratch& v = q->vox[j];
-    if (q->vox_entries[j] < entries || q->vox_groups[j] < groups) {
-        hipFree(v.vlist);
-        hipFree(v.vcnt);
-        v.vlist = nullptr;
-        v.vcnt = nullptr;
-        R360_HIP(hipMalloc(&v.vlist, sizeof(int) * entries));
-        R360_HIP(hipMalloc(&v.vcnt, sizeof(int) * groups));
-        q->vox_entries[j] = entries;
-        q->vox_groups[j] = groups;
-    }
-    long cap = 1;
-    while (cap < cells) cap <<= 1;
-    if (q->vox_cells[j] < cap) {
-        hipFree(v.vhash);
-        v.vhash = nullptr;
-        R360_HIP(hipMalloc(&v.vhash, sizeof(VoxCell) * cap));
-        R360_HIP(hipMemsetAsync(v.vhash, 0, sizeof(VoxCell) * cap, q->ctx->stream));
-        q->vox_cells[j] = cap;
-        v.cap = (unsigned long long)cap;
-    }
-    return 0;
 }
 
 void dispatcher(r360_plane_queue* q) {
@@ -107,12 +78,12 @@ void dispatcher(r360_plane_queue* q) {
         std::memset(&B, 0, sizeof B);
         for (int j = 0; j < F && rc == 0; ++j) {
             r360_frame* f = take[j].f;
-            rc = vox_reserve(q, j, G);
+            rc = vox_slot_reserve(q->vox[j], G, q->ctx->stream);
             if (rc == 0 && hipStreamWaitEvent(q->ctx->stream, f->pl.ready, 0) != hipSuccess) {
                 r360_set_error("plane queue: hipStreamWaitEvent failed");
                 rc = -1;
             }
-            B.f[j] = plane_dev(f, q->vox[j]);
+            B.f[j] = plane_dev(f, q->vox[j].v);
         }
         if (rc == 0) rc = planes_launch(B, F, G, q->ctx->stream, q->ctx);
         for (int j = 0; j < F && rc == 0; ++j)
@@ -163,10 +134,7 @@ int plane_queue_create(int device, int max_batch, r360_plane_queue** out) {
     q->ctx = ctx;
     q->max_batch = max_batch;
     q->max_inflight = inflight > 0 ? inflight : 1;
-    q->vox.assign(max_batch, VoxScratch{nullptr, 0, nullptr, nullptr});
-    q->vox_cells.assign(max_batch, 0);
-    q->vox_entries.assign(max_batch, 0);
-    q->vox_groups.assign(max_batch, 0);
+    q->vox.resize(max_batch);
     q->worker = std::thread(dispatcher, q);
     *out = q;
     return 0;
@@ -182,7 +150,7 @@ void plane_queue_destroy(r360_plane_queue* q) {
     q->worker.join();
     (void)hipSetDevice(q->ctx->device);
     (void)hipStreamSynchronize(q->ctx->stream);
-    for (auto& v : q->vox) { hipFree(v.vhash); hipFree(v.vlist); hipFree(v.vcnt); }
+    for (auto& v : q->vox) vox_slot_free(v);
     for (hipEvent_t e : q->inflight) hipEventDestroy(e);
     for (hipEvent_t e : q->free_ev) hipEventDestroy(e);
     r360_ctx_destroy(q->ctx);

@@ -246,6 +246,7 @@ extern "C" void r360_ctx_destroy(r360_ctx* c) {
     hipFree(c->d_rob_out); hipHostFree(c->h_rob_jobs); hipHostFree(c->h_rob_sums); hipHostFree(c->h_rob_out);
     hipFree(c->d_match_desc); hipFree(c->d_unary); hipFree(c->d_bin); hipFree(c->d_vhash);
     hipFree(c->d_vlist); hipFree(c->d_vcnt);
+    for (auto& s : c->bvox) vox_slot_free(s);
     hipHostFree(c->h_unary); hipHostFree(c->h_bin);
     if (!c->stream_borrowed) hipStreamDestroy(c->stream);
     delete c;
@@ -620,6 +621,7 @@ extern "C" int r360_frame_upload(r360_frame* f, const uint8_t* bgr8, const uint1
     CHECK_ARG(f && bgr8 && depth8, "null arg");
     if (f && bind_device(f->ctx->device)) return -1;
     CHECK_ARG(f->rows > 0, "a sphere-only frame has no sensor images");
+    planes_join(f);   // a plane stage still reading the images (a plane queue's batch) ends first
     const size_t ns = (size_t)8 * f->rows * f->cols;
     R360_HIP(hipMemcpyAsync(f->d_bgr, bgr8, ns * 3, hipMemcpyHostToDevice, f->ctx->stream));
     R360_HIP(hipMemcpyAsync(f->d_depth, depth8, ns * 2, hipMemcpyHostToDevice, f->ctx->stream));
@@ -634,6 +636,7 @@ extern "C" int r360_frame_upload_async(r360_frame* f, const uint8_t* bgr8, const
     CHECK_ARG(f && bgr8 && depth8, "null arg");
     if (f && bind_device(f->ctx->device)) return -1;
     CHECK_ARG(f->rows > 0, "a sphere-only frame has no sensor images");
+    planes_join(f);   // a plane stage still reading the images (a plane queue's batch) ends first
     const size_t ns = (size_t)8 * f->rows * f->cols;
     R360_HIP(hipMemcpyAsync(f->d_bgr, bgr8, ns * 3, hipMemcpyHostToDevice, f->ctx->stream));
     R360_HIP(hipMemcpyAsync(f->d_depth, depth8, ns * 2, hipMemcpyHostToDevice, f->ctx->stream));
@@ -675,6 +678,7 @@ extern "C" int r360_frame_upload_device(r360_frame* f, const void* d_bgr8, const
     CHECK_ARG(f && d_bgr8 && d_depth8, "null arg");
     if (f && bind_device(f->ctx->device)) return -1;
     CHECK_ARG(f->rows > 0, "a sphere-only frame has no sensor images");
+    planes_join(f);   // a plane stage still reading the images (a plane queue's batch) ends first
     const size_t ns = (size_t)8 * f->rows * f->cols;
     R360_HIP(hipMemcpyAsync(f->d_bgr, d_bgr8, ns * 3, hipMemcpyDeviceToDevice, f->ctx->stream));
     R360_HIP(hipMemcpyAsync(f->d_depth, d_depth8, ns * 2, hipMemcpyDeviceToDevice, f->ctx->stream));
@@ -687,6 +691,9 @@ extern "C" int r360_frame_build_async(r360_frame* f, unsigned flags) {
     if (f && bind_device(f->ctx->device)) return -1;
     CHECK_ARG(f->rows > 0 || flags == 0, "a sphere-only frame has no sensor images to build from (r360_frame_set_sphere)");
     if (flags & (R360_BUILD_UNDISTORT | R360_BUILD_CLOUD | R360_BUILD_PLANES)) {
+        // the previous build's plane stage may run on another stream (plane queue, r360_frames_build) and read the
+        // undistorted depth: its assembly thread has waited for it
+        planes_join(f);
         if (launch_undistort(f)) return -1;
         f->built |= R360_BUILD_UNDISTORT;
     }

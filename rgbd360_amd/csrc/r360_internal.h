@@ -294,6 +294,7 @@ static_assert(sizeof(PlaneBatch) + 256 <= 4096, "the plane batch travels as a ke
 
 // ------------------------------------------------------------------ host objects
 struct r360_plane_queue;
+struct VoxSlot;
 struct r360_ctx {
     r360_plane_queue* plane_q = nullptr;   // frames built on this ctx run their plane stage on this queue (batched)
     int device = 0;
@@ -390,6 +391,8 @@ struct r360_ctx {
     int* d_vlist = nullptr;          // cells each k_vox_hash workgroup claimed [vlist_cap], its count per workgroup
     int* d_vcnt = nullptr;           //   [vcnt_cap] (k_vox_compact walks these instead of the whole table)
     long vlist_cap = 0, vcnt_cap = 0;
+    // r360_frames_build: voxel scratch of batch slots 1.. (slot 0 is the table above); VoxSlot is declared below
+    std::vector<VoxSlot> bvox;
     // Register() in flight (r360_register_async)
     int reg_pending = 0, reg_good = 0;
     float reg_info[36];
@@ -529,6 +532,10 @@ int launch_plane_publish(const PlaneBatch& B, int F, hipStream_t st);   // plane
 struct VoxScratch { VoxCell* vhash; unsigned long long cap; int* vlist; int* vcnt; };
 // the voxel scratch sizes a frame of G needs: hash cells, list entries, list groups (workgroups)
 void vox_scratch_need(const PlaneGeom& G, long* cells, long* entries, long* groups);
+// one batch slot's voxel scratch with its capacities (plane queue slots, r360_frames_build slots)
+struct VoxSlot { VoxScratch v{nullptr, 0, nullptr, nullptr}; long cells = 0, entries = 0, groups = 0; };
+int vox_slot_reserve(VoxSlot& s, const PlaneGeom& G, hipStream_t st);   // zeroed hash (memset on st when it grows)
+void vox_slot_free(VoxSlot& s);
 PlaneDev plane_dev(const r360_frame* f, const VoxScratch& vs);
 int plane_bufs_alloc(r360_frame* f);
 void plane_bufs_free(r360_frame* f);

@@ -243,3 +243,42 @@ def test_register_alias_parity_synth_vga(ctx, vga):
     rel = vga["rel"]
     assert np.rad2deg(O.rot_angle(pose[:3, :3], rel[:3, :3])) < 0.2
     assert np.linalg.norm(pose[:3, 3] - rel[:3, 3]) < 0.02
+
+
+def test_batched_plane_builds_equal_lone_builds(qvga, vga):
+    """r360_frames_build: nine synthetic VGA frames (a batch of 8 and a batch of 1) and the two QVGA captures (a
+    batch of 2) in one call, frames of two contexts, the batches on the first frame's context stream.  Every frame's
+    cloud, normals, labels, PbMap planes and sphere equal its lone build's, and a second batched build of the same
+    frames (reused voxel tables and plane buffers) gives them again."""
+    ctx2 = R.Context(0)
+    calv, calv2 = vga["cal"], R.Calib360(ctx2, 480, 640)
+    calv2.loadExtrinsicCalibration(R.EXTRINSICS_DIR)
+    seed = (360 << 16) + 7
+    imgs = [calv.synth_frame(seed, R.synth_path_pose(seed, i)) for i in range(9)]
+    flags = R.BUILD_UNDISTORT | R.BUILD_CLOUD | R.BUILD_PLANES | R.BUILD_SPHERE | R.BUILD_PYRAMID
+    lone, batch = [], []
+    for i, (b, d) in enumerate(imgs):
+        f = R.Frame360(calv)
+        f.upload(b, d)
+        f.build(flags)
+        lone.append(f)
+        g = R.Frame360(calv2 if i % 2 == 0 else calv)
+        g.upload(b, d)
+        batch.append(g)
+    qb = []
+    for name in ("sphere_images_1.bin", "sphere_images_10.bin"):
+        g = R.Frame360(qvga["cal"])
+        g.loadFrame(os.path.join(R.SAMPLES_DIR, name))
+        qb.append(g)
+    order = [batch[0], qb[0], *batch[1:5], qb[1], *batch[5:]]
+    for rep in range(2):
+        R.frames_build(order, flags)
+        for g, f in list(zip(batch, lone)) + list(zip(qb, qvga["frames"])):
+            for a, b in zip(g.cloud(), f.cloud()):
+                assert _same(a, b), rep
+            for a, b in zip(g.labels(), f.labels()):
+                assert np.array_equal(a, b), rep
+            _cmp_planes(g.planes(), f.planes())
+        for g, f in zip(batch, lone):
+            for a, b in zip(g.sphere(), f.sphere()):
+                assert np.array_equal(a, b), rep

@@ -29,7 +29,7 @@ def seq():
     p.n_pyr = 5
     p.std_dev_photo = np.float32(3.0 / 255)
     p.fixed_iters_level0 = 20
-    runner = OD.SequenceRunner(0, 480, 640, 16, p)
+    runner = OD.SequenceRunner(0, 480, 640, 16, p, plane_batch=0)   # plane stages on the pipelines' own streams
     rec = np.zeros((1, 255, OD.REC), np.float32)
     runner.run(0, 255, lambda i: (bgr[i], dep[i]), rec)
     yield dict(bgr=bgr, dep=dep, runner=runner, rec=rec[0], params=p, rt8=rt8)
@@ -119,7 +119,8 @@ def test_trajectory_follows_ground_truth(seq):
 
 def test_queued_dense_stage_reproduces_the_records(seq):
     """The same 255 pairs with the alignments batched on a dense queue (r360_dense_queue, up to 16 pairs per
-    launch, one alignment in flight per pipeline): every record is bit-identical to the unqueued run's."""
+    launch, one alignment in flight per pipeline) and the plane stages batched on a plane queue (up to 8 frames per
+    launch): every record is bit-identical to the unqueued run's (plane stages on the pipelines' own streams)."""
     bgr, dep = seq["bgr"], seq["dep"]
     runner = OD.SequenceRunner(0, 480, 640, 16, seq["params"], queue=16)
     try:
