@@ -23,6 +23,9 @@ namespace {
 #ifndef R360_ICP_TPB
 #define R360_ICP_TPB 256
 #endif
+#ifndef R360_PK_ACC
+#define R360_PK_ACC 0   // PF 6 sums J J^T with packed FMAs (contribute_pk)
+#endif
 #ifndef R360_ICP_MINB
 #define R360_ICP_MINB 5   // waves per SIMD (HIP launch_bounds 2nd arg): caps the pass at 102 VGPRs (94 used)
 #endif
@@ -527,6 +530,129 @@ __device__ __forceinline__ void contribute_lean(Acc& A, WaveCnt& W, float& errf,
     }
 }
 
+// Packed accumulation (PF 6): the 27 sums of J J^T and J r over a lane's pixels as 12 register pairs and 3 scalars,
+// updated by v_pk_fma_f32 (two FMAs per VALU instruction) instead of 27 v_fma per Jacobian row.  The row's
+// components are taken in the order q = (u1, u2 | u0, J3 | J4, J5 | r) and summed two rows of H at a time: pair
+// (q0, q1) times every q_j, j >= 1, and so on; the broadcast operand of each update comes from a half of an
+// existing pair (op_sel), so the update needs no register moves.  pk_fold maps the sums back to Acc's slots.
+typedef float f2v __attribute__((ext_vector_type(2)));
+struct AccPk {
+    f2v a0, a2, a3, a4, a5, a6;   // (q0 q0, q1 q1), (q0, q1) x q2 .. q6
+    f2v b0, b4, b5, b6;           // (q2 q2, q3 q3), (q2, q3) x q4 .. q6
+    f2v c0, c6;                   // (q4 q4, q5 q5), (q4, q5) x q6
+    float sa, sb, sc;             // q0 q1, q2 q3, q4 q5
+};
+__device__ __forceinline__ f2v pkfma(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2v bc2(float x) { return f2v{x, x}; }
+
+__device__ __forceinline__ void pk_zero(AccPk& K) {
+    K.a0 = K.a2 = K.a3 = K.a4 = K.a5 = K.a6 = K.b0 = K.b4 = K.b5 = K.b6 = K.c0 = K.c6 = f2v{0.f, 0.f};
+    K.sa = K.sb = K.sc = 0.f;
+}
+
+// one Jacobian row J = [u0, u1, u2, p' x u] (u12 = (u1, u2)) with residual r
+__device__ __forceinline__ void pk_row(AccPk& K, f2v u12, float u0, float X, float Y, float Z, float r) {
+#pragma clang fp contract(fast)
+    const float J3 = Y * u12.y - Z * u12.x, J4 = Z * u0 - X * u12.y, J5 = X * u12.x - Y * u0;
+    const f2v Pb = f2v{u0, J3}, Pc = f2v{J4, J5};
+    K.a0 = pkfma(u12, u12, K.a0);
+    K.sa = __builtin_fmaf(u12.x, u12.y, K.sa);
+    K.a2 = pkfma(u12, bc2(u0), K.a2);
+    K.a3 = pkfma(u12, bc2(J3), K.a3);
+    K.a4 = pkfma(u12, bc2(J4), K.a4);
+    K.a5 = pkfma(u12, bc2(J5), K.a5);
+    K.a6 = pkfma(u12, bc2(r), K.a6);
+    K.b0 = pkfma(Pb, Pb, K.b0);
+    K.sb = __builtin_fmaf(u0, J3, K.sb);
+    K.b4 = pkfma(Pb, bc2(J4), K.b4);
+    K.b5 = pkfma(Pb, bc2(J5), K.b5);
+    K.b6 = pkfma(Pb, bc2(r), K.b6);
+    K.c0 = pkfma(Pc, Pc, K.c0);
+    K.sc = __builtin_fmaf(J4, J5, K.sc);
+    K.c6 = pkfma(Pc, bc2(r), K.c6);
+}
+
+// the packed sums into Acc's slots (0..20 upper-triangle H row-major, 21..26 g)
+__device__ __forceinline__ void pk_fold(Acc& A, const AccPk& K) {
+    A.h[6] += K.a0.x;  A.h[11] += K.a0.y; A.h[7] += K.sa;
+    A.h[1] += K.a2.x;  A.h[2] += K.a2.y;
+    A.h[8] += K.a3.x;  A.h[12] += K.a3.y;
+    A.h[9] += K.a4.x;  A.h[13] += K.a4.y;
+    A.h[10] += K.a5.x; A.h[14] += K.a5.y;
+    A.h[22] += K.a6.x; A.h[23] += K.a6.y;
+    A.h[0] += K.b0.x;  A.h[15] += K.b0.y; A.h[3] += K.sb;
+    A.h[4] += K.b4.x;  A.h[16] += K.b4.y;
+    A.h[5] += K.b5.x;  A.h[17] += K.b5.y;
+    A.h[21] += K.b6.x; A.h[24] += K.b6.y;
+    A.h[18] += K.c0.x; A.h[20] += K.c0.y; A.h[19] += K.sc;
+    A.h[25] += K.c6.x; A.h[26] += K.c6.y;
+}
+
+// contribute_lean<METHOD, false> (PF 6: the target depth is finite) with the Jacobian rows built in pairs and summed
+// by pk_row: u = J_proj^T [gx gy]^T as (A, B) = w (gx, gy) * (s, t), u0 = -B r2, (u1, u2) = A (Z, -Y) + B X (Y, Z)
+template <int METHOD>
+__device__ __forceinline__ void contribute_pk(AccPk& K, WaveCnt& W, float& errf, const Proj& o, const float4 G,
+                                              const float2 T, float angle_res_inv, const IcpConst& C) {
+    constexpr bool photo = (METHOD == R360_PHOTO_CONSISTENCY || METHOD == R360_PHOTO_DEPTH);
+    constexpr bool depth = (METHOD == R360_DEPTH_CONSISTENCY || METHOD == R360_PHOTO_DEPTH);
+    const bool sal_p = !(fabsf(G.x) < C.thr_int && fabsf(G.y) < C.thr_int);
+    const bool sal_d = !(fabsf(G.z) < C.thr_depth && fabsf(G.w) < C.thr_depth);
+    const bool p_ok = photo && o.vis && sal_p;
+    const bool d_ok = depth && o.vis && (!photo || sal_p) && sal_d;   // (:3064-3073)
+    float wp = 0.f, rp = 0.f, wd = 0.f, rd = 0.f;
+    {
+#pragma clang fp contract(fast)
+        if (photo) {
+            const float e = T.x - o.gray_s;
+            const float a = fabsf(e), k = C.sd_photo;
+            const float t = 2.f * k * a - k * k;
+            const float h = a < k ? 1.f : t * __builtin_amdgcn_rsqf(t * a * a);   // weightHuber (:545-554)
+            wp = p_ok ? h * C.sd_photo_inv_f : 0.f;                                 // (:3047)
+            rp = wp * e;
+        }
+        if (depth) {
+            const float e = T.y - o.dist;
+            const float a = fabsf(e), k = C.sd_depth * T.y, k2 = k * k;
+            const float t = 2.f * k * a - k2;
+            const bool in = a < k;
+            const float w = (in ? 1.f : t) * __builtin_amdgcn_rsqf(in ? k2 : t * a * a * k2);   // (:3077-3078)
+            wd = d_ok ? w : 0.f;
+            rd = d_ok ? w * e : 0.f;
+        }
+        errf += rp * rp + rd * rd;
+    }
+    W.c28 += wave_count(o.vis);                                                            // numVisiblePixels
+    W.c27 += (photo ? wave_count(p_ok) : 0) + (depth ? wave_count(d_ok) : 0);
+    const float X = o.X, Y = o.Y, Z = o.Z;
+    const float dist_inv = o.vis ? o.dist_inv : 0.5f;
+    {
+#pragma clang fp contract(fast)
+        const float r2 = o.vis ? Y * Y + Z * Z : 1.f;
+        // 1 / angle_res enters through the row's weight (no loop-invariant register pair)
+        const f2v st = f2v{__builtin_amdgcn_rcpf(r2), __builtin_amdgcn_rsqf(r2) * (dist_inv * dist_inv)};
+        const f2v YZ = f2v{Y, Z}, ZnY = f2v{Z, -Y};
+        auto row = [&](f2v g, float w, f2v& u12, float& u0) {
+            const f2v AB = (g * st) * bc2(w * angle_res_inv);
+            const float BX = AB.y * X;
+            u0 = -AB.y * r2;
+            u12 = pkfma(bc2(BX), YZ, bc2(AB.x) * ZnY);
+        };
+        if (photo) {
+            f2v u12;
+            float u0;
+            row(f2v{G.x, G.y}, wp, u12, u0);
+            pk_row(K, u12, u0, X, Y, Z, rp);
+        }
+        if (depth) {
+            f2v u12;
+            float u0;
+            row(f2v{G.z, G.w}, wd, u12, u0);
+            const float wdi = wd * dist_inv;
+            pk_row(K, pkfma(bc2(-wdi), YZ, u12), u0 - wdi * X, X, Y, Z, rd);
+        }
+    }
+}
+
 // ---------------------------------------------------------------- GN step (thread 0 of last block)
 #include "icp_gn.inc"
 
@@ -985,13 +1111,21 @@ __device__ __forceinline__ int icp_pass_body(const IcpJobs& jobs, const float* _
         };
         auto gT = [&](int t) { return __builtin_amdgcn_raw_buffer_load_b32(rs_t, t * 4, 0, 0); };
 #endif
+#if R360_PK_ACC
+        AccPk K;
+        pk_zero(K);
+#endif
         auto acc = [&](const Proj& o, const float4 G, unsigned tv) {
 #ifdef R360_EXP_NOACC   // experiment builds only: keep the operands alive, skip the math
             A.h[0] += o.vis ? G.x + G.y + G.z + G.w + gray_of(tv) + depth_of(tv) + o.X + o.dist : 0.f;
             W.c28 += wave_count(o.vis);
             return;
 #endif
+#if R360_PK_ACC
+            contribute_pk<METHOD>(K, W, errf, o, G, make_float2(gray_of(tv), depth_of(tv)), angle_res_inv, C);
+#else
             contribute_lean<METHOD, false>(A, W, errf, o, G, make_float2(gray_of(tv), depth_of(tv)), angle_res_inv, C);
+#endif
         };
         // row of a wave-uniform pixel index: a float estimate corrected by one step either way (exact for
         // pixel indices below 2^24, every level-0 size here)
@@ -1100,6 +1234,9 @@ __device__ __forceinline__ int icp_pass_body(const IcpJobs& jobs, const float* _
             o.t = o.vis ? o.t : 0;
             acc(o, gG(o.t), gT(o.t));
         }
+#if R360_PK_ACC
+        pk_fold(A, K);
+#endif
     } else if (PF == 7) {
         // PF 6 with a deeper software pipeline (sources two steps ahead of their projection, gathers two steps
         // ahead of their accumulation): the level-0 pass is bound by memory latency, not by VALU or bytes
