@@ -26,17 +26,19 @@ struct PlaneTicket {
 };
 
 struct r360_plane_queue {
-    r360_ctx* ctx = nullptr;   // the queue's stream (and per-launch timing)
+    r360_ctx* ctx = nullptr;   // the queue's first stream (and per-launch timing)
     int max_batch = R360_PLANE_BATCH;
-    std::vector<VoxSlot> vox;   // voxel-fallback scratch per batch slot
+    // the queue's streams (each with a hardware queue of its own): batches go to the stream whose previous batch
+    // has finished, so the latency-bound chains of two batches can overlap; stream k's batches use vox[k]
+    std::vector<hipStream_t> streams;
+    std::vector<std::vector<VoxSlot>> vox;   // voxel-fallback scratch per stream and batch slot
+    std::vector<hipEvent_t> last;            // per stream: the end of its last batch (nullptr: none yet)
     struct Item { r360_frame* f; std::shared_ptr<PlaneTicket> tk; };
     std::deque<Item> pending;
     std::mutex m;
     std::condition_variable cv;
     bool quit = false;
     std::thread worker;
-    int max_inflight = 1;                 // batches on the stream at once: the next one accumulates meanwhile
-    std::deque<hipEvent_t> inflight, free_ev;
     long batches = 0, frames = 0;
     int max_seen = 0;
 };
@@ -52,14 +54,21 @@ bool same_geom(const PlaneGeom& a, const PlaneGeom& b) {
 
 void dispatcher(r360_plane_queue* q) {
     (void)hipSetDevice(q->ctx->device);
+    const int ns = (int)q->streams.size();
+    int next = 0;
     for (;;) {
-        // the next batch is taken only once fewer than max_inflight are on the stream, so frames that arrive while
-        // one runs go into the same launch
-        while ((int)q->inflight.size() >= q->max_inflight) {
-            (void)event_wait(q->inflight.front());
-            q->free_ev.push_back(q->inflight.front());
-            q->inflight.pop_front();
+        // a stream whose previous batch has finished (else wait for the one that started first): frames that
+        // arrive while every stream is busy go into the next launch
+        int k = -1;
+        for (int t = 0; t < ns && k < 0; ++t) {
+            const int c = (next + t) % ns;
+            if (!q->last[c] || hipEventQuery(q->last[c]) == hipSuccess) k = c;
         }
+        if (k < 0) {
+            k = next;
+            (void)event_wait(q->last[k]);
+        }
+        next = (k + 1) % ns;
         std::vector<r360_plane_queue::Item> take;
         {
             std::unique_lock<std::mutex> lk(q->m);
@@ -73,29 +82,32 @@ void dispatcher(r360_plane_queue* q) {
         }
         const int F = (int)take.size();
         const PlaneGeom G = plane_geom(take[0].f);
+        hipStream_t st = q->streams[k];
         int rc = 0;
         PlaneBatch B;
         std::memset(&B, 0, sizeof B);
         for (int j = 0; j < F && rc == 0; ++j) {
             r360_frame* f = take[j].f;
-            rc = vox_slot_reserve(q->vox[j], G, q->ctx->stream);
-            if (rc == 0 && hipStreamWaitEvent(q->ctx->stream, f->pl.ready, 0) != hipSuccess) {
+            rc = vox_slot_reserve(q->vox[k][j], G, st);
+            if (rc == 0 && hipStreamWaitEvent(st, f->pl.ready, 0) != hipSuccess) {
                 r360_set_error("plane queue: hipStreamWaitEvent failed");
                 rc = -1;
             }
-            B.f[j] = plane_dev(f, q->vox[j].v);
+            B.f[j] = plane_dev(f, q->vox[k][j].v);
         }
-        if (rc == 0) rc = planes_launch(B, F, G, q->ctx->stream, q->ctx);
+        // per-launch timing (r360_ctx_timing) records on the ctx's stream: the first stream's batches only
+        if (rc == 0) rc = planes_launch(B, F, G, st, k == 0 ? q->ctx : nullptr);
         for (int j = 0; j < F && rc == 0; ++j)
-            if (hipEventRecord(take[j].f->pl.done, q->ctx->stream) != hipSuccess) {
+            if (hipEventRecord(take[j].f->pl.done, st) != hipSuccess) {
                 r360_set_error("plane queue: hipEventRecord failed");
                 rc = -1;
             }
         if (rc == 0) {
-            hipEvent_t e = nullptr;
-            if (!q->free_ev.empty()) { e = q->free_ev.back(); q->free_ev.pop_back(); }
-            else if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
-            if (e && hipEventRecord(e, q->ctx->stream) == hipSuccess) q->inflight.push_back(e);
+            if (!q->last[k] && hipEventCreateWithFlags(&q->last[k], hipEventDisableTiming) != hipSuccess) q->last[k] = nullptr;
+            if (q->last[k] && hipEventRecord(q->last[k], st) != hipSuccess) {
+                hipEventDestroy(q->last[k]);
+                q->last[k] = nullptr;
+            }
         }
         const std::string err = rc ? r360_last_error() : std::string();
         for (auto& it : take) {
@@ -115,26 +127,36 @@ void dispatcher(r360_plane_queue* q) {
 }  // namespace
 
 int plane_queue_create(int device, int max_batch, r360_plane_queue** out) {
-    // experiment builds: R360_PLANE_INFLIGHT batches on the stream at once (default 1)
-    static const int inflight = R360_KNOB("R360_PLANE_INFLIGHT", 1);
+    // experiment builds: R360_PLANE_STREAMS streams (default 1)
+    static const int nstreams = R360_KNOB("R360_PLANE_STREAMS", 1);
     CHECK_ARG(out && max_batch >= 1 && max_batch <= R360_PLANE_BATCH, "plane queue: max_batch must be 1..8");
     r360_ctx* ctx = nullptr;
     if (int rc = r360_ctx_create(device, &ctx)) return rc;
-    // a hardware queue of its own: a stream with a CU mask (all CUs) is not put in the pooled queues
+    // hardware queues of their own: a stream with a CU mask (all CUs) is not put in the pooled queues
     int cus = 0;
     R360_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
     uint32_t mask[R360_CU_MASK_WORDS] = {0};
     for (int i = 0; i < cus && i < 32 * R360_CU_MASK_WORDS; ++i) mask[i / 32] |= 1u << (i % 32);
-    hipStream_t hs = nullptr;
-    R360_HIP(hipExtStreamCreateWithCUMask(&hs, R360_CU_MASK_WORDS * 32, mask));
-    R360_HIP(hipStreamSynchronize(ctx->stream));
-    R360_HIP(hipStreamDestroy(ctx->stream));
-    ctx->stream = hs;
     auto* q = new r360_plane_queue;
     q->ctx = ctx;
     q->max_batch = max_batch;
-    q->max_inflight = inflight > 0 ? inflight : 1;
-    q->vox.resize(max_batch);
+    const int ns = nstreams >= 1 && nstreams <= 4 ? nstreams : 1;
+    for (int k = 0; k < ns; ++k) {
+        hipStream_t hs = nullptr;
+        if (hipExtStreamCreateWithCUMask(&hs, R360_CU_MASK_WORDS * 32, mask) != hipSuccess) {
+            r360_set_error("plane queue: hipExtStreamCreateWithCUMask failed");
+            for (hipStream_t t : q->streams) hipStreamDestroy(t);
+            r360_ctx_destroy(ctx);
+            delete q;
+            return -1;
+        }
+        q->streams.push_back(hs);
+    }
+    R360_HIP(hipStreamSynchronize(ctx->stream));
+    R360_HIP(hipStreamDestroy(ctx->stream));
+    ctx->stream = q->streams[0];
+    q->vox.assign(ns, std::vector<VoxSlot>(max_batch));
+    q->last.assign(ns, nullptr);
     q->worker = std::thread(dispatcher, q);
     *out = q;
     return 0;
@@ -149,11 +171,13 @@ void plane_queue_destroy(r360_plane_queue* q) {
     q->cv.notify_all();
     q->worker.join();
     (void)hipSetDevice(q->ctx->device);
-    (void)hipStreamSynchronize(q->ctx->stream);
-    for (auto& v : q->vox) vox_slot_free(v);
-    for (hipEvent_t e : q->inflight) hipEventDestroy(e);
-    for (hipEvent_t e : q->free_ev) hipEventDestroy(e);
-    r360_ctx_destroy(q->ctx);
+    for (hipStream_t st : q->streams) (void)hipStreamSynchronize(st);
+    for (auto& vs : q->vox)
+        for (auto& v : vs) vox_slot_free(v);
+    for (hipEvent_t e : q->last)
+        if (e) hipEventDestroy(e);
+    for (size_t k = 1; k < q->streams.size(); ++k) hipStreamDestroy(q->streams[k]);
+    r360_ctx_destroy(q->ctx);   // destroys streams[0] (the ctx's stream)
     delete q;
 }
 

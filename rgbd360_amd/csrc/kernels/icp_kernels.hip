@@ -530,6 +530,7 @@ __device__ __forceinline__ void contribute_lean(Acc& A, WaveCnt& W, float& errf,
     }
 }
 
+#if R360_PK_ACC
 // Packed accumulation (PF 6): the 27 sums of J J^T and J r over a lane's pixels as 12 register pairs and 3 scalars,
 // updated by v_pk_fma_f32 (two FMAs per VALU instruction) instead of 27 v_fma per Jacobian row.  The row's
 // components are taken in the order q = (u1, u2 | u0, J3 | J4, J5 | r) and summed two rows of H at a time: pair
@@ -652,6 +653,7 @@ __device__ __forceinline__ void contribute_pk(AccPk& K, WaveCnt& W, float& errf,
         }
     }
 }
+#endif
 
 // ---------------------------------------------------------------- GN step (thread 0 of last block)
 #include "icp_gn.inc"
