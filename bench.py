@@ -443,9 +443,8 @@ def main(argv=None, runner_factory=None):
     ap.add_argument("--iters0", type=int, default=20)
     ap.add_argument("--frames", type=int, default=256, help="sequence length (frames)")
     ap.add_argument("--workload", choices=["sequence", "dense", "planes"], default="sequence")
-    ap.add_argument("--streams", type=int, default=10, help="max pipelines per GPU (host thread + HIP stream each; "
-                    "10 since the pipelines share their run edges: 1330-1342 vs 1299-1301 pairs/s at 8, "
-                    "profiles/r4_streams/)")
+    ap.add_argument("--streams", type=int, default=12, help="max pipelines per GPU (host thread + HIP stream each; "
+                    "12 with the batched plane stage: 1472-1477 vs 1437-1458 pairs/s at 10, profiles/r5_pq2/)")
     ap.add_argument("--min-run", type=int, default=6,
                     help="with --per-step-runs: min pairs per pipeline run (each run rebuilds a halo frame)")
     ap.add_argument("--per-step-runs", action="store_true",

@@ -127,8 +127,8 @@ void dispatcher(r360_plane_queue* q) {
 }  // namespace
 
 int plane_queue_create(int device, int max_batch, r360_plane_queue** out) {
-    // experiment builds: R360_PLANE_STREAMS streams (default 1)
-    static const int nstreams = R360_KNOB("R360_PLANE_STREAMS", 1);
+    // experiment builds: R360_PLANE_STREAMS streams (default 2)
+    static const int nstreams = R360_KNOB("R360_PLANE_STREAMS", 2);
     CHECK_ARG(out && max_batch >= 1 && max_batch <= R360_PLANE_BATCH, "plane queue: max_batch must be 1..8");
     r360_ctx* ctx = nullptr;
     if (int rc = r360_ctx_create(device, &ctx)) return rc;

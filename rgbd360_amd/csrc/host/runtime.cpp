@@ -969,15 +969,17 @@ extern "C" int r360_align360_async(r360_ctx* ctx, r360_frame* trg, r360_frame* s
     // timing, another persistent launch in flight) one launch per pass.  R360_PERSIST=1 (experiment builds) sets
     // the option for every context.
     static const bool persist_env = R360_KNOB("R360_PERSIST", 0) != 0;
+    // R360_PERSIST_MIN_LEVEL (experiment builds): only levels >= it run persistent, the finer ones pass by pass
+    static const int persist_min = R360_KNOB("R360_PERSIST_MIN_LEVEL", 0);
     bool persist = (ctx->persist_levels || persist_env) && !occlusion && !ctx->timing && !R360_POLL;
-    for (int l = 0; persist && l < p->n_pyr; ++l) persist = icp_level_persist_ok(ctx, src, l, method);
+    for (int l = persist_min; persist && l < p->n_pyr; ++l) persist = icp_level_persist_ok(ctx, src, l, method);
     if (persist) persist = persist_take(ctx);
     auto passes_of = [&]() -> int {
         for (int l = p->n_pyr - 1; l >= 0; --l) {
             const int np = src->lv[l].rows * src->lv[l].cols;
             const IcpConst C = make_const(p, l, np, occlusion);
             const int passes = 1 + ((l == 0 && p->fixed_iters_level0 > 0) ? p->fixed_iters_level0 : p->max_iters);
-            if (persist) {
+            if (persist && l >= persist_min) {
                 if (launch_icp_level_persist(ctx, trg, src, l, method, C, passes)) return -1;
                 continue;
             }
