@@ -1,6 +1,6 @@
 // frame_kernels.hip — Frame360 construction on gfx950:
 //   k_undistort : loadDepthEigen + CLAMS undistort           (Frame360.h:254-258, 293-310)
-//   k_stitch    : stitchSphericalImage + cvtColor + depth m   (Frame360.h:1099-1148,
+//   k_stitch(_t): stitchSphericalImage + cvtColor + depth m   (Frame360.h:1099-1148,
 //                 RegisterPhotoICP.h:485-486, 316-317)
 //   k_pyramid   : pyrDown (gray) + buildPyramidRange (depth)  (RegisterPhotoICP.h:292-354)
 //   k_gradient  : calcGradientXY for gray and depth + the alignFrames360 seam mask
@@ -161,6 +161,82 @@ __global__ void k_stitch4(const uint8_t* __restrict__ bgr8, const uint16_t* __re
     }
 }
 
+// k_stitch with the sphere walked in 64-row x 16-column tiles, one wave per sphere column: a sphere column maps onto
+// one sensor row (the sensors are mounted on their side: sphere rows run along sensor columns), so a wave's 64 gathers
+// of BGR bytes and ranges read a few consecutive cache lines of one sensor row, where k_stitch4's row-major waves read
+// 64 sensor rows (a line per byte).  The tile goes through LDS and is stored row-major as k_stitch4 stores it.  Per
+// pixel the expressions of k_stitch (the sensor pose loaded once per column, which is one sensor), bit for bit.
+constexpr int STT_R = 64, STT_C = 16;
+__global__ void __launch_bounds__(256) k_stitch_t(const uint8_t* __restrict__ bgr8, const uint16_t* __restrict__ depth8,
+                                                  int rows, int cols, int H, int W, const float* __restrict__ sinphi,
+                                                  const float* __restrict__ cosphi, const float* __restrict__ sinth,
+                                                  const float* __restrict__ costh, const float* __restrict__ rt_inv,
+                                                  float fx, float fy, float cx, float cy, uint8_t* __restrict__ sph_bgr,
+                                                  uint16_t* __restrict__ sph_depth, float2* __restrict__ p0,
+                                                  uint32_t* __restrict__ pk) {
+    __shared__ uint32_t s_pk[STT_C][STT_R + 1];    // range mm | luma << 16
+    __shared__ uint32_t s_bgr[STT_C][STT_R + 1];   // b | g << 8 | r << 16
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int tiles_x = W / STT_C;
+    const int tx = blockIdx.x % tiles_x, ty = blockIdx.x / tiles_x;
+    const int row = ty * STT_R + lane;
+    const bool in = row < H;
+    const float v0 = in ? sinphi[row] : 0.f, cos_phi = in ? cosphi[row] : 0.f;
+#pragma unroll
+    for (int j = 0; j < STT_C / 4; ++j) {
+        const int cl = w * (STT_C / 4) + j;
+        const int col = __builtin_amdgcn_readfirstlane(tx * STT_C + cl);
+        const int k = 7 - col / rows;
+        const float* T = rt_inv + 16 * k;
+        const float v1 = cos_phi * sinth[col];
+        const float v2 = cos_phi * costh[col];
+        float p0x = T[0] * v0 + T[4] * v1 + T[8] * v2;
+        float p1 = T[1] * v0 + T[5] * v1 + T[9] * v2;
+        float p2 = T[2] * v0 + T[6] * v1 + T[10] * v2;
+        p0x = p0x + T[12]; p1 = p1 + T[13]; p2 = p2 + T[14];
+        const float u = fx * p0x / p2 + cx;                          // :1133
+        const float v = fy * p1 / p2 + cy;                           // :1134
+        unsigned b = 0, g = 0, r = 0, dd = 0;
+        if (in && u >= 0 && u < cols && v >= 0 && v < rows) {
+            const int iu = (int)u, iv = (int)v;
+            const long si = (long)k * rows * cols + (long)iv * cols + iu;
+            b = bgr8[si * 3 + 0]; g = bgr8[si * 3 + 1]; r = bgr8[si * 3 + 2];
+            const double du = (double)((u - cx) / fx), dv = (double)((v - cy) / fy);
+            dd = (uint16_t)(depth8[si] * sqrt(1 + du * du + dv * dv));  // :1142 (range in mm)
+        }
+        const unsigned y = (b * 4899 + g * 9617 + r * 1868 + (1 << 13)) >> 14;
+        s_pk[cl][lane] = dd | (y << 16);
+        s_bgr[cl][lane] = b | (g << 8) | (r << 16);
+    }
+    __syncthreads();
+    // row-major stores: thread t writes 4 consecutive pixels of tile row t / 4
+    const int tr = threadIdx.x >> 2, c0 = (threadIdx.x & 3) * 4;
+    const int grow = ty * STT_R + tr;
+    if (grow >= H) return;
+    const long i0 = (long)grow * W + tx * STT_C + c0;
+    unsigned pk4[4], px[12];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        pk4[e] = s_pk[c0 + e][tr];
+        const unsigned q = s_bgr[c0 + e][tr];
+        px[3 * e] = q & 255; px[3 * e + 1] = (q >> 8) & 255; px[3 * e + 2] = q >> 16;
+    }
+    uint3 wb;
+    wb.x = px[0] | (px[1] << 8) | (px[2] << 16) | (px[3] << 24);
+    wb.y = px[4] | (px[5] << 8) | (px[6] << 16) | (px[7] << 24);
+    wb.z = px[8] | (px[9] << 8) | (px[10] << 16) | (px[11] << 24);
+    *reinterpret_cast<uint3*>(sph_bgr + 3 * i0) = wb;
+    *reinterpret_cast<uint2*>(sph_depth + i0) = make_uint2((pk4[0] & 0xffffu) | (pk4[1] << 16),
+                                                            (pk4[2] & 0xffffu) | (pk4[3] << 16));
+    float2 o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)   // setSourceFrame / setTargetFrame level 0: gray /255, depth * 0.001
+        o[e] = make_float2((float)(pk4[e] >> 16) * (float)(1. / 255), (float)(pk4[e] & 0xffffu) * 0.001f);
+    *reinterpret_cast<float4*>(p0 + i0) = make_float4(o[0].x, o[0].y, o[1].x, o[1].y);
+    *reinterpret_cast<float4*>(p0 + i0 + 2) = make_float4(o[2].x, o[2].y, o[3].x, o[3].y);
+    *reinterpret_cast<uint4*>(pk + i0) = make_uint4(pk4[0], pk4[1], pk4[2], pk4[3]);
+}
+
 __device__ __forceinline__ int refl101(int p, int n) {
     p = p < 0 ? -p : p;
     return p >= n ? 2 * n - p - 2 : p;
@@ -304,7 +380,14 @@ int launch_stitch(r360_frame* f) {
     const r360_calib* c = f->calib;
     const long n = (long)f->sph_rows * f->sph_cols;
     const int slot = timing_begin(f->ctx, "k_stitch");
-    if (f->sph_cols % 4 == 0)
+    // experiment builds: R360_STITCH=4 forces the row-major k_stitch4
+    static const int form = R360_KNOB("R360_STITCH", 0);
+    if (f->sph_cols % STT_C == 0 && form != 4)
+        hipLaunchKernelGGL(k_stitch_t, dim3((f->sph_cols / STT_C) * ((f->sph_rows + STT_R - 1) / STT_R)), dim3(256), 0,
+                           f->ctx->stream, f->d_bgr, f->d_depth, f->rows, f->cols, f->sph_rows, f->sph_cols,
+                           c->d_st_sinphi, c->d_st_cosphi, c->d_st_sinth, c->d_st_costh, c->d_rt_inv, c->K[0], c->K[4],
+                           c->K[6], c->K[7], f->d_sph_bgr, f->d_sph_depth, f->lv[0].p0, f->lv[0].pk);
+    else if (f->sph_cols % 4 == 0)
         hipLaunchKernelGGL(k_stitch4, dim3(grid_for(n / 4)), dim3(TPB), 0, f->ctx->stream, f->d_bgr, f->d_depth,
                            f->rows, f->cols, f->sph_rows, f->sph_cols, c->d_st_sinphi, c->d_st_cosphi, c->d_st_sinth,
                            c->d_st_costh, c->d_rt_inv, c->K[0], c->K[4], c->K[6], c->K[7], f->d_sph_bgr,
