@@ -243,15 +243,34 @@ __device__ __forceinline__ int refl101(int p, int n) {
 }
 
 // ------------------------------------------------------------------ pyramid (level l -> l+1)
+// Level l's {gray, depth} through a loader: the float2 image, or level 0's packed image (4 B per pixel instead of
+// 8: luma * (float)(1/255) and range * 0.001f are the stitch's own expressions, so the values are those of p0).
+struct LvF2 {
+    const float2* p;
+    __device__ __forceinline__ float g(long i) const { return p[i].x; }
+    __device__ __forceinline__ float d(long i) const { return p[i].y; }
+    __device__ __forceinline__ float2 gd(long i) const { return p[i]; }
+};
+struct LvPk {
+    const uint32_t* p;
+    __device__ __forceinline__ float g(long i) const { return (float)(p[i] >> 16) * (float)(1. / 255); }
+    __device__ __forceinline__ float d(long i) const { return (float)(p[i] & 0xffffu) * 0.001f; }
+    __device__ __forceinline__ float2 gd(long i) const {
+        const uint32_t v = p[i];
+        return make_float2((float)(v >> 16) * (float)(1. / 255), (float)(v & 0xffffu) * 0.001f);
+    }
+};
+
 // nimg images of R x C stored back to back (the sphere: 1; the per-sensor pyramids: 8)
-__global__ void k_pyramid(const float2* __restrict__ in_all, int R, int C, float2* __restrict__ out_all, float min_d,
-                          float max_d, int nimg) {
+template <class IN>
+__global__ void k_pyramid(const IN in_all, int R, int C, float2* __restrict__ out_all, float min_d, float max_d,
+                          int nimg) {
     const int dr = R / 2, dc = C / 2;
     const long per = (long)dr * dc, n = per * nimg;
     for (long j = blockIdx.x * (long)blockDim.x + threadIdx.x; j < n; j += (long)gridDim.x * blockDim.x) {
         const int img = (int)(j / per);
         const long i = j - (long)img * per;
-        const float2* in = in_all + (long)img * R * C;
+        const long in0 = (long)img * R * C;
         float2* out = out_all + (long)img * per;
         const int y = (int)(i / dc), x = (int)(i - (long)y * dc);
         // cv::pyrDown: horizontal [1 4 6 4 1] per source row, then the vertical SSE order.
@@ -261,8 +280,9 @@ __global__ void k_pyramid(const float2* __restrict__ in_all, int R, int C, float
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
             const int yy = refl101(2 * y - 2 + k, R);
-            const float2* s = in + (long)yy * C;
-            const float a = s[xa].x, b = s[xb].x, c = s[sx].x, d = s[xd].x, e = s[xe].x;
+            const long s = in0 + (long)yy * C;
+            const float a = in_all.g(s + xa), b = in_all.g(s + xb), c = in_all.g(s + sx), d = in_all.g(s + xd),
+                        e = in_all.g(s + xe);
             h[k] = c * 6 + (b + d) * 4 + a + e;
         }
         float t0 = h[0] + h[4];
@@ -272,9 +292,9 @@ __global__ void k_pyramid(const float2* __restrict__ in_all, int R, int C, float
         const float gray = t0 * (1.f / 256);
         // buildPyramidRange: mean of the 2x2 depths in (minDepth, maxDepth) (:330-348)
         float av = 0.f; unsigned nv = 0;
-        const float2* s0 = in + (long)(2 * y) * C + sx;
-        const float2* s1 = s0 + C;
-        const float z0 = s0[0].y, z1 = s0[1].y, z2 = s1[0].y, z3 = s1[1].y;
+        const long s0 = in0 + (long)(2 * y) * C + sx;
+        const long s1 = s0 + C;
+        const float z0 = in_all.d(s0), z1 = in_all.d(s0 + 1), z2 = in_all.d(s1), z3 = in_all.d(s1 + 1);
         if (z0 > min_d && z0 < max_d) { av += z0; ++nv; }
         if (z1 > min_d && z1 < max_d) { av += z1; ++nv; }
         if (z2 > min_d && z2 < max_d) { av += z2; ++nv; }
@@ -316,11 +336,29 @@ __global__ void k_gradient(const float2* __restrict__ p0, int R, int C, float4* 
 // belongs to the level l with blk0[l] <= b < blk0[l + 1], one pixel per thread
 struct GradLevels {
     const float2* p0[R360_MAX_PYR];
+    const uint32_t* pk0;   // level 0's packed image (read instead of p0[0] when set)
     float4* tg[R360_MAX_PYR];
     int rows[R360_MAX_PYR], cols[R360_MAX_PYR];
     int blk0[R360_MAX_PYR + 1];
     int nl;
 };
+
+template <class IN>
+__device__ __forceinline__ void gradient_px(const IN p0, long i, int R, int C, float4* __restrict__ tg) {
+    const int ws = C / 8;   // >= 1: calib_build_tables stops the pyramid before a level narrower than 8
+    const int r = (int)(i / C), c = (int)(i - (long)r * C);
+    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int m = ws > 0 ? c % ws : 1;   // seam columns as k_gradient (alignFrames360 :4538-4549)
+    const bool seam = ws > 0 && (c >= ws - 1) && (c < 7 * ws + 1) && (m == 0 || m == ws - 1);
+    if (!seam && r >= 1 && r < R - 1 && c >= 1 && c < C - 1) {
+        const float2 f = p0.gd(i), fl = p0.gd(i - 1), fr = p0.gd(i + 1), fu = p0.gd(i - C), fd = p0.gd(i + C);
+        o.x = harm(fl.x, f.x, fr.x);
+        o.y = harm(fu.x, f.x, fd.x);
+        o.z = harm(fl.y, f.y, fr.y);
+        o.w = harm(fu.y, f.y, fd.y);
+    }
+    tg[i] = o;
+}
 
 __global__ void k_gradient_levels(GradLevels G) {
     int l = 0;
@@ -328,20 +366,8 @@ __global__ void k_gradient_levels(GradLevels G) {
     const int R = G.rows[l], C = G.cols[l];
     const long i = (long)(blockIdx.x - G.blk0[l]) * blockDim.x + threadIdx.x;
     if (i >= (long)R * C) return;
-    const float2* p0 = G.p0[l];
-    const int ws = C / 8;   // >= 1: calib_build_tables stops the pyramid before a level narrower than 8
-    const int r = (int)(i / C), c = (int)(i - (long)r * C);
-    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
-    const int m = ws > 0 ? c % ws : 1;   // seam columns as k_gradient (alignFrames360 :4538-4549)
-    const bool seam = ws > 0 && (c >= ws - 1) && (c < 7 * ws + 1) && (m == 0 || m == ws - 1);
-    if (!seam && r >= 1 && r < R - 1 && c >= 1 && c < C - 1) {
-        const float2 f = p0[i], fl = p0[i - 1], fr = p0[i + 1], fu = p0[i - C], fd = p0[i + C];
-        o.x = harm(fl.x, f.x, fr.x);
-        o.y = harm(fu.x, f.x, fd.x);
-        o.z = harm(fl.y, f.y, fr.y);
-        o.w = harm(fu.y, f.y, fd.y);
-    }
-    G.tg[l][i] = o;
+    if (l == 0 && G.pk0) gradient_px(LvPk{G.pk0}, i, R, C, G.tg[0]);
+    else gradient_px(LvF2{G.p0[l]}, i, R, C, G.tg[l]);
 }
 
 // setSourceFrame / setTargetFrame level 0 of each sensor's raw images (:480-516): CV_RGB2GRAY on the
@@ -511,14 +537,21 @@ int launch_sphere_level0(r360_frame* f) {
 int launch_pyramid(r360_frame* f) {
     // RegisterPhotoICP constructor defaults minDepth 0.3 / maxDepth 6.0 (:202-203)
     const float min_d = 0.3f, max_d = 6.0f;
+    static const bool pyr_f2 = R360_KNOB("R360_PYR_F2", 0) != 0;   // experiment builds: level 0 read as float2
     for (int l = 1; l < f->n_levels; ++l) {
         const long n = (long)f->lv[l].rows * f->lv[l].cols;
-        hipLaunchKernelGGL(k_pyramid, dim3(grid_for(n)), dim3(TPB), 0, f->ctx->stream, f->lv[l - 1].p0,
-                           f->lv[l - 1].rows, f->lv[l - 1].cols, f->lv[l].p0, min_d, max_d, 1);
+        // level 1 from level 0's packed image (half the bytes of its float2 image, the same values)
+        if (l == 1 && f->lv[0].pk && !pyr_f2)
+            hipLaunchKernelGGL(k_pyramid<LvPk>, dim3(grid_for(n)), dim3(TPB), 0, f->ctx->stream, LvPk{f->lv[0].pk},
+                               f->lv[0].rows, f->lv[0].cols, f->lv[1].p0, min_d, max_d, 1);
+        else
+            hipLaunchKernelGGL(k_pyramid<LvF2>, dim3(grid_for(n)), dim3(TPB), 0, f->ctx->stream, LvF2{f->lv[l - 1].p0},
+                               f->lv[l - 1].rows, f->lv[l - 1].cols, f->lv[l].p0, min_d, max_d, 1);
     }
     {
         GradLevels GL{};
         GL.nl = f->n_levels;
+        GL.pk0 = pyr_f2 ? nullptr : f->lv[0].pk;
         for (int l = 0; l < f->n_levels; ++l) {
             GL.p0[l] = f->lv[l].p0;
             GL.tg[l] = f->lv[l].tg;
@@ -577,7 +610,7 @@ int launch_sensor_pyramid(r360_frame* f) {
                        (uint32_t*)nullptr);
     for (int l = 1; l < f->n_slevels; ++l) {
         const long n = 8L * f->sp[l].rows * f->sp[l].cols;
-        hipLaunchKernelGGL(k_pyramid, dim3(grid_for(n)), dim3(TPB), 0, st, f->sp[l - 1].p0, f->sp[l - 1].rows,
+        hipLaunchKernelGGL(k_pyramid<LvF2>, dim3(grid_for(n)), dim3(TPB), 0, st, LvF2{f->sp[l - 1].p0}, f->sp[l - 1].rows,
                            f->sp[l - 1].cols, f->sp[l].p0, min_d, max_d, 8);
     }
     for (int l = 0; l < f->n_slevels; ++l) {
