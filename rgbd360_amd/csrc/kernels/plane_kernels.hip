@@ -578,22 +578,41 @@ __device__ __forceinline__ void d_normals_sat(const float4* __restrict__ cloud, 
     }
 #pragma unroll
     for (int ph = 0; ph < 2; ++ph) {   // 0: x differences (right - left), 1: y differences (down - up)
-        // stage the differences at table position (y + 1, x + 1); row 0 and column 0 are zero
-        for (int k = threadIdx.x; k < NS_H * NS_W; k += NT_TPB) {
-            const int ty = k / NS_W, tx = k - ty * NS_W;
-            double d0 = 0.0, d1 = 0.0, d2 = 0.0;
-            int n = 0;
-            if (ty > 0 && tx > 0) {
-                const int yy = r0 - NT_H + ty - 1, xx = c0 - NT_H + tx - 1;
-                n = 1;   // outside [1, h-2] x [1, w-2]: zero and counted, as k_normals
-                if (yy >= 1 && yy <= h - 2 && xx >= 1 && xx <= w - 2) {
-                    const int q = yy * w + xx;
-                    const float4 a = ph ? P[q + w] : P[q + 1], b = ph ? P[q - w] : P[q - 1];
-                    const float e0 = a.x - b.x, e1 = a.y - b.y, e2 = a.z - b.z;
-                    if (isfin(e0 + e1 + e2)) { d0 = e0; d1 = e1; d2 = e2; } else n = 0;
+        // stage the differences at table position (y + 1, x + 1); row 0 and column 0 are zero.  NT_STG entries per
+        // thread at a time: their point loads are issued together before any of them is used
+        constexpr int NT_STG = 4;
+        for (int k0 = 0; k0 < NS_H * NS_W; k0 += NT_STG * NT_TPB) {
+            float4 a[NT_STG], b[NT_STG];
+            int st[NT_STG];   // 0: outside the table, 1: zero and counted, 2: a difference
+#pragma unroll
+            for (int u = 0; u < NT_STG; ++u) {
+                const int k = k0 + u * NT_TPB + threadIdx.x;
+                const int ty = k / NS_W, tx = k - ty * NS_W;
+                st[u] = 0;
+                a[u] = b[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (k < NS_H * NS_W && ty > 0 && tx > 0) {
+                    const int yy = r0 - NT_H + ty - 1, xx = c0 - NT_H + tx - 1;
+                    st[u] = 1;   // outside [1, h-2] x [1, w-2]: zero and counted, as k_normals
+                    if (yy >= 1 && yy <= h - 2 && xx >= 1 && xx <= w - 2) {
+                        const int q = yy * w + xx;
+                        a[u] = ph ? P[q + w] : P[q + 1];
+                        b[u] = ph ? P[q - w] : P[q - 1];
+                        st[u] = 2;
+                    }
                 }
             }
-            T.v[0][k] = d0; T.v[1][k] = d1; T.v[2][k] = d2; T.c[k] = n;
+#pragma unroll
+            for (int u = 0; u < NT_STG; ++u) {
+                const int k = k0 + u * NT_TPB + threadIdx.x;
+                if (k >= NS_H * NS_W) continue;
+                double d0 = 0.0, d1 = 0.0, d2 = 0.0;
+                int n = st[u] ? 1 : 0;
+                if (st[u] == 2) {
+                    const float e0 = a[u].x - b[u].x, e1 = a[u].y - b[u].y, e2 = a[u].z - b[u].z;
+                    if (isfin(e0 + e1 + e2)) { d0 = e0; d1 = e1; d2 = e2; } else n = 0;
+                }
+                T.v[0][k] = d0; T.v[1][k] = d1; T.v[2][k] = d2; T.c[k] = n;
+            }
         }
         __syncthreads();
         // row prefix sums (one thread per (row, channel)), then column prefix sums (one per (column, channel))
