@@ -286,6 +286,14 @@ extern "C" int r360_dense_queue_create(int device, int max_batch, r360_dense_que
     return 0;
 }
 
+// Sizes the queue's batch buffers for its largest batch of frames of n_pixels level-0 pixels now (before any job:
+// ensure_batch synchronises the device when it grows a buffer, which a first large batch would otherwise do mid-run)
+int dense_queue_reserve(r360_dense_queue* q, long n_pixels) {
+    for (int k = 0; k < q->n_ctx; ++k)
+        if (ensure_batch(q->cx[k], q->max_batch, n_pixels)) return -1;
+    return 0;
+}
+
 extern "C" void r360_dense_queue_destroy(r360_dense_queue* q) {
     if (!q) return;
     {

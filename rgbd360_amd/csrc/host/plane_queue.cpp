@@ -183,6 +183,15 @@ void plane_queue_destroy(r360_plane_queue* q) {
 
 r360_ctx* plane_queue_ctx(r360_plane_queue* q) { return q ? q->ctx : nullptr; }
 
+// every stream's batch slots' voxel scratch sized for frames of G now (before any frame is submitted)
+int plane_queue_reserve(r360_plane_queue* q, const PlaneGeom& G) {
+    for (size_t k = 0; k < q->streams.size(); ++k)
+        for (auto& v : q->vox[k])
+            if (vox_slot_reserve(v, G, q->streams[k])) return -1;
+    R360_HIP(hipDeviceSynchronize());
+    return 0;
+}
+
 int plane_queue_stats(const r360_plane_queue* q, long* batches, long* frames, int* max_batch_seen) {
     CHECK_ARG(q, "null plane queue");
     auto* mq = const_cast<r360_plane_queue*>(q);

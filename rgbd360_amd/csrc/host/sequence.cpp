@@ -334,6 +334,8 @@ extern "C" void r360_sequence_default_params(r360_sequence_params* p) {
 }
 
 extern "C" void r360_sequence_destroy(r360_sequence* s);
+int plane_queue_reserve(r360_plane_queue* q, const PlaneGeom& G);   // plane_queue.cpp
+int dense_queue_reserve(r360_dense_queue* q, long n_pixels);          // dense_queue.cpp
 
 extern "C" int r360_sequence_create(int device, const r360_sequence_params* prm, const char* extrinsics_dir,
                                     r360_sequence** out) {
@@ -388,6 +390,35 @@ extern "C" int r360_sequence_create(int device, const r360_sequence_params* prm,
             if (r360_frame_create(c, k, &f)) return fail();
             s->ring.back().push_back(f);
         }
+    }
+    // every buffer the runs size on first use, sized now: a short run (one rank's shard: a few pairs per pipeline
+    // and step) would otherwise allocate inside its timed steps, and hipMalloc synchronises the device
+    {
+        r360_frame* f0 = s->ring[0][0];
+        const long npx = (long)f0->lv[0].rows * f0->lv[0].cols;
+        if (s->flags & R360_BUILD_PLANES) {
+            for (auto& r : s->ring)
+                for (r360_frame* f : r)
+                    if (plane_bufs_alloc(f)) return fail();
+            const PlaneGeom G = plane_geom(f0);
+            if (s->pq) {
+                if (plane_queue_reserve(s->pq, G)) return fail();
+            } else {
+                long cells, entries, groups;
+                vox_scratch_need(G, &cells, &entries, &groups);
+                for (r360_ctx* c : s->ctx)
+                    if (ctx_vhash_reserve(c, cells, entries, groups)) return fail();
+            }
+        }
+        if (s->prm.workload != R360_SEQ_PLANES) {
+            if (s->q) {
+                if (dense_queue_reserve(s->q, npx)) return fail();
+            } else {
+                for (r360_ctx* c : s->ctx)
+                    if (ensure_defer(c, npx)) return fail();
+            }
+        }
+        R360_HIP(hipDeviceSynchronize());
     }
     s->tid.assign(s->P, 0);
     s->rc.assign(s->P, 0);
