@@ -28,62 +28,88 @@ static std::vector<uint8_t> timestamp_to_digits(uint64_t v) {
     return std::vector<uint8_t>(d.rbegin(), d.rend());
 }
 
-int parse_bin_file(const char* path, int rows, int cols, std::vector<uint8_t>& bgr, std::vector<uint16_t>& depth,
-                   uint64_t* timestamp) {
-    std::ifstream f(path, std::ios::binary);
-    if (!f) { r360_set_error("cannot open %s", path); return -1; }
-    std::vector<uint8_t> b((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
-    static const char kTag[] = "serialization::archive";
-    if (b.size() < 45 + 24 || memcmp(b.data() + 8, kTag, 22) != 0) {
-        r360_set_error("%s: not a boost binary archive", path);
-        return -1;
+// The calling thread's page-locked staging buffer for .bin files (grown as needed, freed with the thread): a file
+// is read into it in one call and its mats go to the device images by DMA.  Byte-wise stream reads and copies out of
+// pageable memory were 4.9 ms of the 5.6 ms a QVGA loadFrame took (BASELINE configs[0]'s loadFrame).
+namespace {
+struct PinnedFileBuf {
+    uint8_t* p = nullptr;
+    size_t cap = 0;
+    ~PinnedFileBuf() { if (p) hipHostFree(p); }
+    int reserve(size_t n) {
+        if (n <= cap) return 0;
+        if (p) hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        R360_HIP(hipHostMalloc(&p, n, hipHostMallocDefault));
+        cap = n;
+        return 0;
     }
-    size_t off = 45;
-    const size_t npx = (size_t)rows * cols;
-    bgr.resize(8 * npx * 3);
-    depth.resize(8 * npx);
-    for (int s = 0; s < 8; ++s)
-        for (int m = 0; m < 2; ++m) {
-            if (off + 24 > b.size()) { r360_set_error("%s: truncated", path); return -1; }
-            int32_t c, r; uint64_t esz, et;
-            memcpy(&c, &b[off], 4); memcpy(&r, &b[off + 4], 4); memcpy(&esz, &b[off + 8], 8); memcpy(&et, &b[off + 16], 8);
-            off += 24;
-            if (r != rows || c != cols) {
-                r360_set_error("%s: sensor %d is %dx%d, calib expects %dx%d", path, s, r, c, rows, cols);
-                return -1;
-            }
-            const size_t n = (size_t)r * c * esz;
-            if (off + n > b.size()) { r360_set_error("%s: truncated payload", path); return -1; }
-            if (m == 0) {
-                if (esz != 3 || et != 16) { r360_set_error("%s: RGB mat type %llu", path, (unsigned long long)et); return -1; }
-                memcpy(&bgr[s * npx * 3], &b[off], n);
-            } else {
-                if (esz != 2 || et != 2) { r360_set_error("%s: depth mat type %llu", path, (unsigned long long)et); return -1; }
-                memcpy(&depth[s * npx], &b[off], n);
-            }
-            off += n;
-        }
-    // the timestamp mat (Frame360.h:244-247); loadFrame swallows archive errors here, so a missing
-    // or malformed one leaves the timestamp at 0
-    *timestamp = 0;
-    if (off + 24 <= b.size()) {
-        int32_t c, r; uint64_t esz, et;
-        memcpy(&c, &b[off], 4); memcpy(&r, &b[off + 4], 4); memcpy(&esz, &b[off + 8], 8); memcpy(&et, &b[off + 16], 8);
-        off += 24;
-        const size_t n = (c > 0 && r > 0) ? (size_t)c * r * esz : 0;
-        if (n && esz == 1 && off + n <= b.size()) *timestamp = timestamp_from_digits(&b[off], (int)n);
-    }
-    return 0;
-}
+};
+thread_local PinnedFileBuf t_file;
+}  // namespace
 
+// Frame360::loadFrame (Frame360.h:231-266): the archive prologue is checked and skipped, the 8 x {RGB, depth} mats
+// checked against the calibration's sensor size and copied to the frame's images, the timestamp mat decoded.
 extern "C" int r360_frame_load_bin(r360_frame* f, const char* path) {
     if (f && bind_device(f->ctx->device)) return -1;
     if (!f || !path) { r360_set_error("null arg"); return -2; }
-    std::vector<uint8_t> bgr;
-    std::vector<uint16_t> depth;
+    CHECK_ARG(f->rows > 0, "a sphere-only frame has no sensor images");
+    FILE* fp = fopen(path, "rb");
+    if (!fp) { r360_set_error("cannot open %s", path); return -1; }
+    fseek(fp, 0, SEEK_END);
+    const long len = ftell(fp);
+    fseek(fp, 0, SEEK_SET);
+    if (len < 0 || t_file.reserve((size_t)len + 1)) { fclose(fp); if (len < 0) r360_set_error("cannot size %s", path); return -1; }
+    const size_t got = fread(t_file.p, 1, (size_t)len, fp);
+    fclose(fp);
+    if (got != (size_t)len) { r360_set_error("%s: short read", path); return -1; }
+    const uint8_t* b = t_file.p;
+    const size_t size = (size_t)len;
+    static const char kTag[] = "serialization::archive";
+    if (size < 45 + 24 || memcmp(b + 8, kTag, 22) != 0) {
+        r360_set_error("%s: not a boost binary archive", path);
+        return -1;
+    }
+    // every mat checked before any is copied (a malformed file leaves the frame as it was)
+    size_t off = 45;
+    size_t moff[8][2];
+    const size_t npx = (size_t)f->rows * f->cols;
+    for (int s = 0; s < 8; ++s)
+        for (int m = 0; m < 2; ++m) {
+            if (off + 24 > size) { r360_set_error("%s: truncated", path); return -1; }
+            int32_t c, r; uint64_t esz, et;
+            memcpy(&c, b + off, 4); memcpy(&r, b + off + 4, 4); memcpy(&esz, b + off + 8, 8); memcpy(&et, b + off + 16, 8);
+            off += 24;
+            if (r != f->rows || c != f->cols) {
+                r360_set_error("%s: sensor %d is %dx%d, calib expects %dx%d", path, s, r, c, f->rows, f->cols);
+                return -1;
+            }
+            const size_t n = (size_t)r * c * esz;
+            if (off + n > size) { r360_set_error("%s: truncated payload", path); return -1; }
+            if (m == 0 && (esz != 3 || et != 16)) { r360_set_error("%s: RGB mat type %llu", path, (unsigned long long)et); return -1; }
+            if (m == 1 && (esz != 2 || et != 2)) { r360_set_error("%s: depth mat type %llu", path, (unsigned long long)et); return -1; }
+            moff[s][m] = off;
+            off += n;
+        }
+    planes_join(f);   // a plane stage still reading the images (a plane queue's batch) ends first
+    hipStream_t st = f->ctx->stream;
+    for (int s = 0; s < 8; ++s) {
+        R360_HIP(hipMemcpyAsync(f->d_bgr + s * npx * 3, b + moff[s][0], npx * 3, hipMemcpyHostToDevice, st));
+        R360_HIP(hipMemcpyAsync(f->d_depth + s * npx, b + moff[s][1], npx * 2, hipMemcpyHostToDevice, st));
+    }
+    // the timestamp mat (Frame360.h:244-247); loadFrame swallows archive errors here, so a missing
+    // or malformed one leaves the timestamp at 0
     uint64_t ts = 0;
-    if (parse_bin_file(path, f->rows, f->cols, bgr, depth, &ts)) return -1;
-    if (int rc = r360_frame_upload(f, bgr.data(), depth.data())) return rc;
+    if (off + 24 <= size) {
+        int32_t c, r; uint64_t esz, et;
+        memcpy(&c, b + off, 4); memcpy(&r, b + off + 4, 4); memcpy(&esz, b + off + 8, 8); memcpy(&et, b + off + 16, 8);
+        off += 24;
+        const size_t n = (c > 0 && r > 0) ? (size_t)c * r * esz : 0;
+        if (n && esz == 1 && off + n <= size) ts = timestamp_from_digits(b + off, (int)n);
+    }
+    R360_HIP(hipStreamSynchronize(st));   // the staging buffer is the thread's next file's
+    f->built = 0;
     f->timestamp = ts;
     return 0;
 }
