@@ -44,6 +44,46 @@ __global__ void k_undistort(const uint16_t* __restrict__ depth, float* __restric
     }
 }
 
+// k_undistort with 4 consecutive pixels of one sensor row per thread (cols % 4 == 0): one 8-byte load and one 16-byte
+// store per thread instead of a 2-byte load and a 4-byte store per pixel, the same per-pixel expressions
+__device__ __forceinline__ float undistort_px(float z, long i, int rows, int cols, const float* __restrict__ mult,
+                                              const float* __restrict__ counts, int nx, int bin_w, int bin_h, int nb,
+                                              double bin_depth) {
+    const int s = (int)(i / ((long)rows * cols));
+    const int pix = (int)(i - (long)s * rows * cols);
+    const int v = pix / cols, u = pix - v * cols;
+    const long fr = ((long)s * (rows / bin_h) * nx + (long)(v / bin_h) * nx + (u / bin_w)) * nb;
+    int idx = (int)floor(z / bin_depth);
+    idx = idx < nb - 1 ? idx : nb - 1;
+    float start = (float)(bin_depth * idx);
+    int idx1 = (z - start < bin_depth / 2) ? idx : idx + 1;  // interpolatedUndistort :48-68
+    int idx0 = idx1 - 1;
+    if (idx0 < 0 || idx1 >= nb || counts[fr + idx0] < 50 || counts[fr + idx1] < 50) return z * mult[fr + idx];
+    double z0 = (idx0 + 1) * bin_depth - bin_depth * 0.5;
+    double c1 = (z - z0) / bin_depth;
+    double c0 = 1.0 - c1;
+    double m = c0 * mult[fr + idx0] + c1 * mult[fr + idx1];
+    return (float)(z * m);
+}
+
+__global__ void k_undistort4(const uint16_t* __restrict__ depth, float* __restrict__ depth_m, int rows, int cols,
+                             const float* __restrict__ mult, const float* __restrict__ counts, int nx, int bin_w,
+                             int bin_h, int nb, double bin_depth, int apply) {
+    const long nq = (long)R360_NUM_SENSORS * rows * cols / 4;
+    for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < nq; q += (long)gridDim.x * blockDim.x) {
+        const uint2 d4 = reinterpret_cast<const uint2*>(depth)[q];
+        const unsigned dv[4] = {d4.x & 0xffffu, d4.x >> 16, d4.y & 0xffffu, d4.y >> 16};
+        float z[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            z[e] = (float)dv[e] * 0.001f;                          // convertTo(CV_32FC1, 0.001)
+            if (apply && z[e] != 0)                                // discrete_depth_distortion_model.cpp:175-186
+                z[e] = undistort_px(z[e], 4 * q + e, rows, cols, mult, counts, nx, bin_w, bin_h, nb, bin_depth);
+        }
+        reinterpret_cast<float4*>(depth_m)[q] = make_float4(z[0], z[1], z[2], z[3]);
+    }
+}
+
 // ------------------------------------------------------------------ stitch
 // One thread per sphere pixel.  Sensor k owns columns [(7-k)*rows, (8-k)*rows)  (:1119-1120).
 __global__ void k_stitch(const uint8_t* __restrict__ bgr8, const uint16_t* __restrict__ depth8, int rows, int cols,
@@ -395,6 +435,13 @@ int launch_undistort(r360_frame* f) {
     const r360_calib* c = f->calib;
     const long n = (long)R360_NUM_SENSORS * f->rows * f->cols;
     const bool apply = c->has_intrinsics && c->clams.width == f->cols && c->clams.height == f->rows;
+    if (f->cols % 4 == 0) {
+        hipLaunchKernelGGL(k_undistort4, dim3(grid_for(n / 4)), dim3(TPB), 0, f->ctx->stream, f->d_depth, f->d_depth_m,
+                           f->rows, f->cols, c->clams.d_mult, c->clams.d_counts, c->clams.nx, c->clams.bin_w,
+                           c->clams.bin_h, c->clams.num_bins, c->clams.bin_depth, apply ? 1 : 0);
+        R360_HIP(hipGetLastError());
+        return 0;
+    }
     hipLaunchKernelGGL(k_undistort, dim3(grid_for(n)), dim3(TPB), 0, f->ctx->stream, f->d_depth, f->d_depth_m, f->rows,
                        f->cols, c->clams.d_mult, c->clams.d_counts, c->clams.nx, c->clams.bin_w, c->clams.bin_h,
                        c->clams.num_bins, c->clams.bin_depth, apply ? 1 : 0);
@@ -433,8 +480,9 @@ int launch_stitch(r360_frame* f) {
 // minDepth < depth < maxDepth, the LUT_xyz_sphere point (RegisterPhotoICP.h:4553-4587, the same float
 // expressions) and the gray value; both are fixed for a source frame.  They are compacted here once per
 // frame, in raster order (a deterministic two-kernel scan), so the pass streams only valid pixels.
-// blockIdx.y = pyramid level; a block covers R360_SRC_BLOCK consecutive pixels, 4 per thread.
-constexpr int SRC_TPB = R360_SRC_BLOCK / 4;
+// A block covers R360_SRC_BLOCK consecutive pixels, SRC_PPT consecutive ones per thread (256-thread workgroups: a
+// 1024-thread one had to find 16 free wave slots on one CU, which under load delayed the frame's build).
+constexpr int SRC_PPT = 16, SRC_TPB = R360_SRC_BLOCK / SRC_PPT;
 
 // flattened (level, block) grid: level l owns blocks [blk0[l], blk0[l + 1]) (the coarse levels need a quarter, a
 // sixteenth ... of level 0's blocks; a 2D grid sized for level 0 dispatched thousands of empty workgroups)
@@ -458,7 +506,7 @@ __global__ void __launch_bounds__(SRC_TPB) k_src_count(const SrcLevel* __restric
     if (b0 >= n) return;
     int c = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < SRC_PPT; ++k) {
         const long i = b0 + k * SRC_TPB + threadIdx.x;
         c += (i < n && src_valid(S.p0[i].y, min_d, max_d)) ? 1 : 0;
     }
@@ -492,35 +540,43 @@ __global__ void __launch_bounds__(SRC_TPB) k_src_compact(const SrcLevel* __restr
     base = 0;
     for (int w = 0; w < SRC_TPB / 64; ++w) base += sh[w];
     __syncthreads();
-    // raster order: pixel b0 + 4t + k is the k-th of thread t
-    const long i0 = b0 + 4L * threadIdx.x;
-    bool v[4];
-    int c = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        v[k] = i0 + k < n && src_valid(S.p0[i0 + k].y, min_d, max_d);
-        c += v[k] ? 1 : 0;
-    }
+    // raster order: the block's pixels as SRC_PPT rows of SRC_TPB, pixel b0 + k SRC_TPB + t (coalesced loads); a
+    // pixel's slot = the valid pixels of the rows before k, then of the waves before this one in row k, then of the
+    // lanes before it (ballot masks: one LDS round for the whole block)
+    __shared__ int s_cnt[SRC_PPT][SRC_TPB / 64];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    int x = c;                                           // inclusive wave scan
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) sh[wid] = x;
-    __syncthreads();
-    int wbase = 0;
-    for (int w = 0; w < wid; ++w) wbase += sh[w];
-    int pos = base + wbase + x - c;
+    const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    float2 a[SRC_PPT];
+    unsigned long long m[SRC_PPT];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        if (!v[k]) continue;
-        const long i = i0 + k;
-        const int r = (int)(i / S.cols), cc = (int)(i - (long)r * S.cols);
-        const float2 a = S.p0[i];
-        const float d = a.y;
-        // LUT_xyz_sphere (:4580-4582): x = d sin(phi), y = -d cos(phi) sin(theta), z = -d cos(phi) cos(theta)
-        S.pts[pos++] = make_float4(d * S.sinphi[r], -d * S.cosphi[r] * S.sinth[cc], -d * S.cosphi[r] * S.costh[cc], a.x);
+    for (int k = 0; k < SRC_PPT; ++k) {
+        const long i = b0 + (long)k * SRC_TPB + threadIdx.x;
+        a[k] = i < n ? S.p0[i] : make_float2(0.f, 0.f);
+        m[k] = __ballot(i < n && src_valid(a[k].y, min_d, max_d));
+    }
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < SRC_PPT; ++k) s_cnt[k][wid] = __popcll(m[k]);
+    __syncthreads();
+    int pos = base;
+#pragma unroll
+    for (int k = 0; k < SRC_PPT; ++k) {
+        int before = pos, row = 0;
+#pragma unroll
+        for (int w = 0; w < SRC_TPB / 64; ++w) {
+            const int cw = s_cnt[k][w];
+            before += w < wid ? cw : 0;
+            row += cw;
+        }
+        if ((m[k] >> lane) & 1ull) {
+            const long i = b0 + (long)k * SRC_TPB + threadIdx.x;
+            const int r = (int)(i / S.cols), cc = (int)(i - (long)r * S.cols);
+            const float d = a[k].y;
+            // LUT_xyz_sphere (:4580-4582): x = d sin(phi), y = -d cos(phi) sin(theta), z = -d cos(phi) cos(theta)
+            S.pts[before + __popcll(m[k] & lt)] =
+                make_float4(d * S.sinphi[r], -d * S.cosphi[r] * S.sinth[cc], -d * S.cosphi[r] * S.costh[cc], a[k].x);
+        }
+        pos += row;
     }
     if (bx == (int)((n - 1) / R360_SRC_BLOCK) && threadIdx.x == SRC_TPB - 1) npts[lvl] = pos;
 }
