@@ -2237,7 +2237,7 @@ int ensure_batch(r360_ctx* ctx, int n, long n_pixels) {
 // grid of one job's pass at level `level` of `geom` (the same for every job of a batch): the pass form and
 // the number of workgroups
 struct PassGrid { int pf, nb; };
-static PassGrid pass_grid(const r360_ctx* ctx, const LevelBufs& Ls, int occ, int njobs = 1) {
+static PassGrid pass_grid(const r360_ctx* ctx, const LevelBufs& Ls, int occ, int njobs = 1, bool batched = false) {
     // 4-pixel units on the large levels, one pixel per thread where that still fits one resident
     // round (latency-bound small levels); R360_ICP_PF=0/1 forces one form (experiments)
     static const int pf_env = R360_KNOB("R360_ICP_PF", -1);
@@ -2262,7 +2262,15 @@ static PassGrid pass_grid(const r360_ctx* ctx, const LevelBufs& Ls, int occ, int
     // pair's sums (pixels to waves, records in workgroup order) and thus its pose are the same in any batch
     // and on any number of ranks.  R360_ICP_WG_TOTAL (experiment only: breaks that) splits a per-launch total
     // over the launch's jobs.
+    // Batched launches (r360_align360_batch_*, the dense queue): one workgroup per CU and job, so a wave streams twice
+    // the chunks of a lone pass and the per-workgroup tail (the exact re-projection of the deferred lanes, the record
+    // reduction) is paid over twice the pixels: 1535 -> 1588-1595 pairs/s, dense alone 2205 -> 2274 (profiles/r5_cap).
+    // A lone alignment keeps two per CU: with the GPU to itself it is latency-bound, and one per CU made a lone pair
+    // 0.94 -> 1.16 ms.  Every batch of any size (and every rank) uses the batched grid, so a pair's batched result is
+    // the same in any batch; a lone alignment sums the same pixels over twice the records (within rounding of it).
+    static const int cap_batch_env = R360_KNOB("R360_ICP_CAP_BATCH", -1);
     int cap = cap_env > 0 ? cap_env : 2 * cus;
+    if (batched) cap = cap_batch_env > 0 ? cap_batch_env : cus;
     static const int tot_env = R360_KNOB("R360_ICP_WG_TOTAL", -1);
     if (tot_env > 0) cap = ((tot_env / (njobs > 0 ? njobs : 1) + 7) / 8) * 8;
     if (cap > ctx->partials_cap - R360_TICKET_GROUPS) cap = ctx->partials_cap - R360_TICKET_GROUPS;   // + group records
@@ -2326,7 +2334,7 @@ int launch_icp_jobs(r360_ctx* ctx, const IcpJobs& jobs, int n, const r360_frame*
     if (C.occ) { r360_set_error("batched passes: occlusion variants run one alignment per launch"); return -2; }
     if (n < 1 || n > R360_MAX_BATCH) { r360_set_error("batched passes: %d jobs (1..%d)", n, R360_MAX_BATCH); return -2; }
     const LevelBufs& Ls = geom->lv[level];
-    const PassGrid G = pass_grid(ctx, Ls, 0, n);
+    const PassGrid G = pass_grid(ctx, Ls, 0, n, true);
     if (G.pf >= 3 && ctx->bdefer_cap < defer_need(Ls.rows * Ls.cols, G.nb)) {
         r360_set_error("batched passes: deferred-pixel queues not sized for %d pixels", Ls.rows * Ls.cols);
         return -1;

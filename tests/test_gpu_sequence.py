@@ -29,7 +29,8 @@ def seq():
     p.n_pyr = 5
     p.std_dev_photo = np.float32(3.0 / 255)
     p.fixed_iters_level0 = 20
-    runner = OD.SequenceRunner(0, 480, 640, 16, p, plane_batch=0)   # plane stages on the pipelines' own streams
+    # dense stages batched on a dense queue, plane stages on the pipelines' own streams
+    runner = OD.SequenceRunner(0, 480, 640, 16, p, queue=16, plane_batch=0)
     rec = np.zeros((1, 255, OD.REC), np.float32)
     runner.run(0, 255, lambda i: (bgr[i], dep[i]), rec)
     yield dict(bgr=bgr, dep=dep, runner=runner, rec=rec[0], params=p, rt8=rt8)
@@ -117,20 +118,41 @@ def test_trajectory_follows_ground_truth(seq):
     assert e["max_rot_err_deg"] < 2.0 and e["max_trans_err_m"] < 0.02 * e["path_length_m"], e
 
 
-def test_queued_dense_stage_reproduces_the_records(seq):
-    """The same 255 pairs with the alignments batched on a dense queue (r360_dense_queue, up to 16 pairs per
-    launch, one alignment in flight per pipeline) and the plane stages batched on a plane queue (up to 8 frames per
-    launch): every record is bit-identical to the unqueued run's (plane stages on the pipelines' own streams)."""
+def test_plane_queue_reproduces_the_records(seq):
+    """The same 255 pairs with the plane stages batched on a plane queue (up to 8 frames per launch, two streams):
+    every record is bit-identical to the run with plane stages on the pipelines' own streams."""
     bgr, dep = seq["bgr"], seq["dep"]
     runner = OD.SequenceRunner(0, 480, 640, 16, seq["params"], queue=16)
     try:
         rec = np.zeros((1, 255, OD.REC), np.float32)
         runner.run(0, 255, lambda i: (bgr[i], dep[i]), rec)
         st = runner.queue.stats()
+        pst = runner.plane_stats()
     finally:
         runner.close()
     assert st["jobs"] == 255 and st["batches"] < 255
+    assert pst["frames"] >= 256 and pst["batches"] < pst["frames"]
     assert np.array_equal(rec[0], seq["rec"])
+
+
+def test_unqueued_lone_alignments_match_the_records(seq):
+    """Without the dense queue every pair is a lone alignFrames360 (r360_register_async, the sequential callers'
+    path: two workgroups per CU against the batched grid's one), so the records equal the queued run's to rounding:
+    the same PbMap stages, poses within 2e-5 rad / 2e-4 m."""
+    from oracle import oracle360 as O
+    bgr, dep = seq["bgr"], seq["dep"]
+    runner = OD.SequenceRunner(0, 480, 640, 16, seq["params"], plane_batch=0)
+    try:
+        rec = np.zeros((1, 255, OD.REC), np.float32)
+        runner.run(0, 255, lambda i: (bgr[i], dep[i]), rec)
+    finally:
+        runner.close()
+    ref = seq["rec"]
+    assert np.array_equal(rec[0][:, OD.R_STATUS], ref[:, OD.R_STATUS])
+    for i in range(255):
+        a, b = rec[0][i, :16].reshape(4, 4).T, ref[i, :16].reshape(4, 4).T
+        assert O.rot_angle(a[:3, :3], b[:3, :3]) <= 2e-5, i
+        assert np.linalg.norm(a[:3, 3] - b[:3, 3]) <= 2e-4, i
 
 
 @pytest.mark.parametrize("depth,lookahead", [(3, 1), (2, 2)])
