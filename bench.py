@@ -312,8 +312,11 @@ def half_leg(kind, device, rows, cols, p0, p1, frames_of, params, pipelines, que
     Returns pairs/s (whole sequence x repeats after one warm-up pass) and, for the dense half, its level-0 pass."""
     from rgbd360_amd import odometry as OD
     P = min(pipelines, p1 - p0)
+    # the plane half alone runs every pipeline's plane stage on its own stream: with no dense half competing for the
+    # GPU, twelve concurrent chains beat batches on the plane queue (2759 vs 2289 pairs/s, profiles/r5_planes)
     runner = OD.SequenceRunner(device, rows, cols, P, params, planes=kind == "planes",
-                               dense_only=kind == "dense", queue=queue, planes_only=kind == "planes", depth=depth)
+                               dense_only=kind == "dense", queue=queue, planes_only=kind == "planes", depth=depth,
+                               plane_batch=0 if kind == "planes" else None)
     runner.run(p0, p1, frames_of, np.zeros((1, p1 - p0, OD.REC), np.float32), repeats=1)   # warm-up
     qctx = runner.queue.ctx if runner.queue else None
     if qctx:
