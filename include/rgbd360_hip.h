@@ -107,6 +107,9 @@ int  r360_frame_build_async(r360_frame* f, unsigned flags);
  * its r360_frame_build's. */
 int  r360_frames_build(r360_frame* const* frames, int n, unsigned flags);
 int  r360_frame_dims(const r360_frame* f, int* rows, int* cols, int* sph_rows, int* sph_cols);
+/* RegisterPhotoICP::setNumPyr (RegisterPhotoICP.h:224-227) for the frame: its pyramid stops at n levels (default:
+ * the calibration's full depth).  Alignments of the frame then take nPyr <= n. */
+int  r360_frame_set_levels(r360_frame* f, int n);
 /* The R360_BUILD_* stages the frame's current images have been through (an upload or load clears them). */
 int  r360_frame_built(const r360_frame* f, unsigned* flags);
 /* sphereRGB (BGR u8) / sphereDepth (u16 range mm) (Frame360.h:104-107). */

@@ -183,6 +183,7 @@ _SIGS = [
     ("r360_frame_build_async", C.c_int, [_P, C.c_uint]),
     ("r360_frames_build", C.c_int, [_P, C.c_int, C.c_uint]),
     ("r360_frame_dims", C.c_int, [_P, _IP, _IP, _IP, _IP]),
+    ("r360_frame_set_levels", C.c_int, [_P, C.c_int]),
     ("r360_frame_built", C.c_int, [_P, C.POINTER(C.c_uint)]),
     ("r360_frame_get_sphere", C.c_int, [_P, _P, _P]),
     ("r360_frame_get_depth_m", C.c_int, [_P, _P]),
@@ -517,6 +518,10 @@ class Frame360:
         f.rows, f.cols, f.sph_rows, f.sph_cols = r.value, c.value, sr.value, sc.value
         f.close = lambda: None
         return f
+
+    def setNumPyr(self, n: int):
+        """r360_frame_set_levels: the frame's pyramid stops at n levels (RegisterPhotoICP::setNumPyr)."""
+        _check(lib().r360_frame_set_levels(self.h, int(n)), "r360_frame_set_levels")
 
     def loadFrame(self, path: str):
         _check(lib().r360_frame_load_bin(self.h, path.encode()), "loadFrame")

@@ -609,7 +609,7 @@ extern "C" void r360_frame_destroy(r360_frame* f) {
     // hipFree synchronises the device; the frame never dereferences its ctx here so frames may
     // outlive their context at interpreter shutdown.
     hipFree(f->d_bgr); hipFree(f->d_depth); hipFree(f->d_depth_m); hipFree(f->d_sph_bgr); hipFree(f->d_sph_depth);
-    for (int l = 0; l < f->n_levels; ++l) { hipFree(f->lv[l].p0); hipFree(f->lv[l].tg); hipFree(f->lv[l].pts); hipFree(f->lv[l].pk); }
+    for (int l = 0; l < R360_MAX_PYR; ++l) { hipFree(f->lv[l].p0); hipFree(f->lv[l].tg); hipFree(f->lv[l].pts); hipFree(f->lv[l].pk); }
     hipFree(f->d_npts); hipFree(f->d_src_cnt); hipFree(f->d_src_levels);
     for (int l = 0; l < f->n_slevels; ++l) { hipFree(f->sp[l].p0); hipFree(f->sp[l].tg); }
     plane_bufs_free(f);
@@ -728,6 +728,18 @@ extern "C" int r360_frame_build(r360_frame* f, unsigned flags) {
     if (rc) return rc;
     if (flags & R360_BUILD_PLANES) return planes_finish(f);
     R360_HIP(hipStreamSynchronize(f->ctx->stream));
+    return 0;
+}
+
+// RegisterPhotoICP::setNumPyr (RegisterPhotoICP.h:224-227) fixes how many pyramid levels setSourceFrame /
+// setTargetFrame build: a frame builds the calibration's full depth unless told to stop at n levels (its buffers for
+// the deeper levels stay allocated, unused).  Clears the frame's built stages.
+extern "C" int r360_frame_set_levels(r360_frame* f, int n) {
+    CHECK_ARG(f && f->calib, "null frame");
+    CHECK_ARG(n >= 1 && n <= f->calib->n_levels, "levels must be 1 .. the calibration's pyramid depth");
+    planes_join(f);
+    f->n_levels = n;
+    f->built = 0;
     return 0;
 }
 

@@ -389,6 +389,10 @@ extern "C" int r360_sequence_create(int device, const r360_sequence_params* prm,
             r360_frame* f = nullptr;
             if (r360_frame_create(c, k, &f)) return fail();
             s->ring.back().push_back(f);
+            // the pyramid the alignments use (setNumPyr): deeper levels would be built for nothing
+            if (s->prm.workload != R360_SEQ_PLANES && s->prm.icp.n_pyr < f->n_levels &&
+                r360_frame_set_levels(f, s->prm.icp.n_pyr))
+                return fail();
         }
     }
     // every buffer the runs size on first use, sized now: a short run (one rank's shard: a few pairs per pipeline

@@ -219,3 +219,38 @@ def test_persistent_slot(seq):
     _same_outputs(rb, rc2)
     a.close()
     b.close()
+
+
+def test_frames_with_the_alignment_pyramid_only(seq):
+    """setNumPyr on the frames (r360_frame_set_levels: the pyramid stops at the 5 levels the alignment uses, as the
+    sequence runner builds its frames): the same levels, so the same lone and batched results bit for bit; an
+    alignment asking for more levels than the frame has is refused."""
+    fr = seq["frames"]
+    cal = seq["cals"][0]
+    short = []
+    for i in (1, 2):
+        b, d = cal.synth_frame(SEED, R.synth_path_pose(SEED, 3 * i))
+        f = R.Frame360(cal)
+        f.setNumPyr(5)
+        f.upload(b, d)
+        f.build(R.BUILD_UNDISTORT | R.BUILD_SPHERE | R.BUILD_PYRAMID)
+        short.append(f)
+    for lv in range(5):
+        a, b_ = short[0].level(lv), fr[1].level(lv)
+        for x, y in zip(a, b_):
+            assert np.array_equal(x, y), lv
+    p = _params(20)
+    ref = _single(seq["ctxs"][0], fr[1], fr[2], None, _params(20))
+    got = _single(seq["ctxs"][0], short[0], short[1], None, _params(20))
+    assert np.array_equal(ref[0], got[0]) and np.array_equal(ref[1], got[1])
+    bctx = R.Context(0)
+    b1 = R.align360_batch(bctx, [(fr[1], fr[2])], None, R.PHOTO_DEPTH, p)
+    b2 = R.align360_batch(bctx, [(short[0], short[1])], None, R.PHOTO_DEPTH, p)
+    assert np.array_equal(b1[0][0], b2[0][0]) and np.array_equal(b1[1][0], b2[1][0])
+    deep = _params(20)
+    deep.n_pyr = 6
+    with pytest.raises(RuntimeError):
+        _single(seq["ctxs"][0], short[0], short[1], None, deep)
+    bctx.close()
+    for f in short:
+        f.close()
