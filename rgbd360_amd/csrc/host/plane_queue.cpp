@@ -7,9 +7,10 @@
 // alone (profiles/r5_queues).  Here the pipelines' frames go to one queue: a dispatcher thread takes every frame
 // waiting (up to max_batch of one size) and launches the chain ONCE for all of them (PlaneBatch: kernel grid z = the
 // frames), so a batch of F frames costs one chain of launches and its one-workgroup-per-sensor kernels run F x 8
-// workgroups side by side.  The queue's stream has a hardware queue of its own (CU-masked stream).  Each frame keeps
-// its own buffers and host assembly thread; its results equal its lone build's bit for bit (the kernels are the
-// same and every frame's arithmetic is independent of the others').
+// workgroups side by side.  The queue has two streams, each with a hardware queue of its own (CU-masked streams): a
+// batch goes to the stream whose previous batch has finished, so the latency-bound chains of two batches overlap.
+// Each frame keeps its own buffers and host assembly thread; its results equal its lone build's bit for bit (the
+// kernels are the same and every frame's arithmetic is independent of the others').
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
@@ -134,7 +135,11 @@ int plane_queue_create(int device, int max_batch, r360_plane_queue** out) {
     if (int rc = r360_ctx_create(device, &ctx)) return rc;
     // hardware queues of their own: a stream with a CU mask (all CUs) is not put in the pooled queues
     int cus = 0;
-    R360_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) {
+        r360_set_error("plane queue: hipDeviceGetAttribute failed");
+        r360_ctx_destroy(ctx);
+        return -1;
+    }
     uint32_t mask[R360_CU_MASK_WORDS] = {0};
     for (int i = 0; i < cus && i < 32 * R360_CU_MASK_WORDS; ++i) mask[i / 32] |= 1u << (i % 32);
     auto* q = new r360_plane_queue;
@@ -152,8 +157,15 @@ int plane_queue_create(int device, int max_batch, r360_plane_queue** out) {
         }
         q->streams.push_back(hs);
     }
-    R360_HIP(hipStreamSynchronize(ctx->stream));
-    R360_HIP(hipStreamDestroy(ctx->stream));
+    // the ctx's own stream is replaced by the first CU-masked one (nothing was enqueued on it yet)
+    if (hipStreamSynchronize(ctx->stream) != hipSuccess || hipStreamDestroy(ctx->stream) != hipSuccess) {
+        r360_set_error("plane queue: releasing the context's stream failed");
+        for (hipStream_t t : q->streams) hipStreamDestroy(t);
+        ctx->stream_borrowed = true;   // already released
+        r360_ctx_destroy(ctx);
+        delete q;
+        return -1;
+    }
     ctx->stream = q->streams[0];
     q->vox.assign(ns, std::vector<VoxSlot>(max_batch));
     q->last.assign(ns, nullptr);
