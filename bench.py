@@ -345,8 +345,17 @@ def half_leg(kind, device, rows, cols, p0, p1, frames_of, params, pipelines, que
         out["workload"] = ("config3 over the config4 sequence: per pair upload, stitch + 5-level pyramid, "
                            f"alignFrames360(PHOTO_DEPTH) levels 4..1 reference schedule + {params.fixed_iters_level0} GN "
                            "iterations at level 0 (dense queue batches of up to 16 pairs)")
+        # the same kernel on the same frame size as the headline: its PMC profile's HBM bytes per pair-pass apply,
+        # scaled to this leg's pairs per launch (when the profile measured the current ICP sources)
+        traffic, tsrc = None, None
+        tf = os.path.join(ROOT, "profiles", "latest", "l0_pass.json")
+        if n and (rows, cols) == (480, 640) and os.path.exists(tf):
+            prof = json.load(open(tf))
+            if prof.get("icp_source_hash") == icp_source_hash() and prof.get("hbm_bytes_per_pair_pass"):
+                traffic, tsrc = prof["hbm_bytes_per_pair_pass"] * ppl, prof.get("tag")
         out["roofline"] = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                           "frac": (ach / HBM_PEAK_GBS) if ach else None, "avg_launch_ms": avg_ms, "launches": n,
+                           "frac": (ach / HBM_PEAK_GBS) if ach else None, "traffic": traffic,
+                           "traffic_profile": tsrc, "avg_launch_ms": avg_ms, "launches": n,
                            "pairs_per_launch": ppl, "bytes_per_pair_pass": alg,
                            "kernel": "k_icp_pass<PHOTO_DEPTH> (level 0)", "timing": "in-kernel execution span"}
     runner.close()
