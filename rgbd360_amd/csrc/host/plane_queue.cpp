@@ -146,10 +146,21 @@ int plane_queue_create(int device, int max_batch, r360_plane_queue** out) {
     q->ctx = ctx;
     q->max_batch = max_batch;
     const int ns = nstreams >= 1 && nstreams <= 4 ? nstreams : 1;
+    // experiment builds: R360_PLANE_PRIO=1 / 2 gives the streams the device's highest / lowest priority instead of
+    // a CU mask (a priority stream also gets a hardware queue of its own)
+    static const int prio = R360_KNOB("R360_PLANE_PRIO", 0);
     for (int k = 0; k < ns; ++k) {
         hipStream_t hs = nullptr;
-        if (hipExtStreamCreateWithCUMask(&hs, R360_CU_MASK_WORDS * 32, mask) != hipSuccess) {
-            r360_set_error("plane queue: hipExtStreamCreateWithCUMask failed");
+        if (prio) {
+            int least = 0, greatest = 0;
+            if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess ||
+                hipStreamCreateWithPriority(&hs, hipStreamNonBlocking, prio == 1 ? greatest : least) != hipSuccess)
+                hs = nullptr;
+        } else if (hipExtStreamCreateWithCUMask(&hs, R360_CU_MASK_WORDS * 32, mask) != hipSuccess) {
+            hs = nullptr;
+        }
+        if (!hs) {
+            r360_set_error("plane queue: stream creation failed");
             for (hipStream_t t : q->streams) hipStreamDestroy(t);
             r360_ctx_destroy(ctx);
             delete q;
