@@ -681,8 +681,9 @@ def main(argv=None, runner_factory=None):
     # pipeline 0 has built, alignFrames360 with the same schedule, nothing else running
     iso_ms, n, iso_ach, lone_ms = 0.0, 0, None, None
     if not args.no_isolated:
-        fa, fb = runner.frames[0][:2]
-        # two consecutive frames of the sequence (the pipeline's ring buffers hold frames up to depth + 2 apart)
+        # two consecutive frames of the sequence, built as a caller of the façade builds them (Frame360 on pipeline 0's
+        # calibration; the runner's queued ring frames skip the compacted level-0 points a lone pass reads)
+        fa, fb = R.Frame360(runner.cals[0]), R.Frame360(runner.cals[0])
         for f, j in ((fa, p0), (fb, p0 + 1)):
             f.upload(*frames_of(j))
             f.build()

@@ -617,10 +617,11 @@ int launch_pyramid(r360_frame* f) {
         }
         hipLaunchKernelGGL(k_gradient_levels, dim3(GL.blk0[f->n_levels]), dim3(TPB), 0, f->ctx->stream, GL);
     }
-    // level 0 streams its packed image (PF 6) where rows split into whole waves: its compacted points are built
-    // only on request (r360_frame_get_points, or a pass form forced by R360_ICP_PF)
+    // level 0's compacted points feed a lone alignment's level-0 pass (PF 5); batched passes stream the packed image
+    // (PF 6) where rows split into whole waves, so frames that only enter batches (f->compact0 unset: the sequence
+    // runner's queued ring) skip them (built on request: r360_frame_get_points, or a form forced by R360_ICP_PF)
     static const int pf_env = R360_KNOB("R360_ICP_PF", -1);
-    const bool skip0 = f->lv[0].pk && f->lv[0].cols % 64 == 0 && !(pf_env == 4 || pf_env == 5);
+    const bool skip0 = f->lv[0].pk && f->lv[0].cols % 64 == 0 && !f->compact0 && !(pf_env == 4 || pf_env == 5);
     f->lv0_compacted = !skip0;
     return launch_src_compaction(f, skip0 ? 1 : 0, f->n_levels);
 }

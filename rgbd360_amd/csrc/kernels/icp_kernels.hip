@@ -2163,8 +2163,8 @@ extern "C" int r360_debug_block_stamps(unsigned long long* out, int n) {
 }
 #endif
 
-// The pass forms the product library holds (each covered by the parity suite): PF 6 at level 0 (TOP = 1), PF 5 on
-// the other levels (and at level 0 where the packed image is not streamable), PF 3 / PF 0 for the occlusion
+// The pass forms the product library holds (each covered by the parity suite): PF 6 at level 0 (TOP = 1) of batched
+// launches, PF 5 on the other levels and at level 0 of lone alignments (and where the packed image is not streamable), PF 3 / PF 0 for the occlusion
 // variants (PF 0 where rows do not split into whole waves).  PF 1 / 2 / 4 / 7 and the forced-form knobs exist only
 // in the experiment builds (R360_EXPERIMENTS, make exp).
 template <int M, int PF>
@@ -2237,7 +2237,8 @@ int ensure_batch(r360_ctx* ctx, int n, long n_pixels) {
 // grid of one job's pass at level `level` of `geom` (the same for every job of a batch): the pass form and
 // the number of workgroups
 struct PassGrid { int pf, nb; };
-static PassGrid pass_grid(const r360_ctx* ctx, const LevelBufs& Ls, int occ, int njobs = 1, bool batched = false) {
+static PassGrid pass_grid(const r360_ctx* ctx, const LevelBufs& Ls, int occ, int njobs = 1, bool batched = false,
+                          bool pts0 = false) {
     // 4-pixel units on the large levels, one pixel per thread where that still fits one resident
     // round (latency-bound small levels); R360_ICP_PF=0/1 forces one form (experiments)
     static const int pf_env = R360_KNOB("R360_ICP_PF", -1);
@@ -2252,9 +2253,14 @@ static PassGrid pass_grid(const r360_ctx* ctx, const LevelBufs& Ls, int occ, int
     const int npx = Ls.rows * Ls.cols;
     // PF 4 (compacted source points) for the plain pass; the occlusion variants index their flags by source
     // pixel and keep the image stream (PF 3 where rows split into whole waves)
-    // level 0 (the only level with a packed image) streams the packed images where rows split into whole waves
+    // level 0 (the only level with a packed image) streams the packed images where rows split into whole waves, in
+    // batched launches: PF 6 reads 0.64x PF 5's bytes with fewer instructions, which a full chip of waves turns into
+    // throughput.  A lone alignment's pass (two workgroups per CU, latency-bound) runs PF 5 over the source's
+    // compacted level-0 points (pts0: built with the frame, r360_frame::compact0): only valid pixels, no deferred
+    // lanes, the shorter dependent chain; level-0 pass 26.9 -> 24.2 us in-kernel, lone pair 0.92 -> 0.85 ms
+    // (profiles/r5_lone).  The two forms sum the same pixels in different orders (equal to rounding).
     const bool pk_ok = Ls.pk != nullptr && Ls.cols % 64 == 0;
-    const int pf_dflt = occ ? ((Ls.cols % 64 == 0) ? 3 : 0) : (pk_ok ? 6 : 5);
+    const int pf_dflt = occ ? ((Ls.cols % 64 == 0) ? 3 : 0) : (pk_ok && (batched || !pts0) ? 6 : 5);
     const int pf = R360_EXPERIMENTS && pf_env >= 0 && !(pf_env >= 4 && occ) && !(pf_env >= 6 && !pk_ok) ? pf_env : pf_dflt;
     // workgroups per job and pass: 2 per CU (one resident round holds occ_q.per[pf] per CU; a batched launch
     // fills the rest with other jobs, and fewer records per job shorten the reduction tail)
@@ -2366,7 +2372,7 @@ static int level_blocks_per_cu(int method, int pf) {
 bool icp_level_persist_ok(r360_ctx* ctx, const r360_frame* src, int level, int method) {
     if (!R360_PERSIST_BUILT) return false;
     const LevelBufs& Ls = src->lv[level];
-    const PassGrid G = pass_grid(ctx, Ls, 0);
+    const PassGrid G = pass_grid(ctx, Ls, 0, 1, false, src->lv0_compacted);
     if (G.pf != 5 && G.pf != 6) return false;   // the product forms of the plain pass
     if (G.pf >= 3 && ctx->defer_cap < defer_need(Ls.rows * Ls.cols, G.nb)) return false;
     int dev = 0, cus = 0;
@@ -2382,7 +2388,7 @@ int launch_icp_level_persist(r360_ctx* ctx, const r360_frame* trg, const r360_fr
     const LevelBufs& Ls = src->lv[level];
     const LevelBufs& Lt = trg->lv[level];
     const LevelTrig& T = src->calib->trig[level];
-    const PassGrid G = pass_grid(ctx, Ls, 0);
+    const PassGrid G = pass_grid(ctx, Ls, 0, 1, false, src->lv0_compacted);
     if (C0.occ || (G.pf != 5 && G.pf != 6) || !R360_PERSIST_BUILT) {
         r360_set_error("persistent level launch: plain pass forms only");
         return -1;
@@ -2417,7 +2423,7 @@ int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src
     const LevelBufs& Ls = src->lv[level];
     const LevelBufs& Lt = trg->lv[level];
     const LevelTrig& T = src->calib->trig[level];
-    const PassGrid G = pass_grid(ctx, Ls, C.occ);
+    const PassGrid G = pass_grid(ctx, Ls, C.occ, 1, false, src->lv0_compacted);
     const int npx = Ls.rows * Ls.cols;
     if (G.pf >= 3 && ctx->defer_cap < defer_need(npx, G.nb)) {   // one queue per wave, room for every pixel
         r360_set_error("deferred-pixel queue not sized for %d pixels (ensure_defer)", npx);

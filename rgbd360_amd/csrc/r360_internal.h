@@ -457,6 +457,9 @@ struct r360_frame {
     PbMapHost* pbmap = nullptr;
     uint64_t timestamp = 0;            // Frame360::timeStamp (Frame360.h:181-184)
     bool lv0_compacted = false;        // lv[0].pts / d_npts[0] hold level 0's compacted points
+    // the pyramid build compacts level 0 too: a lone alignment's level-0 pass (PF 5) reads the compacted points;
+    // the sequence runner's queued ring frames skip it (their batched passes stream the packed image, PF 6)
+    bool compact0 = true;
     SphereCloudHost* sphere_cloud = nullptr;  // sphereCloud set by loadCloud (Frame360.h:187-193)
     // builds recorded on the frame's build event (runtime.cpp frame_build_event_record): a dense-queue job snapshots
     // it at submit and its batch refuses to run if the frame was rebuilt meanwhile (the event would then stand for

@@ -150,8 +150,8 @@ def test_data_dir_is_the_shipped_tree(root):
 
 
 def test_product_library_holds_only_covered_pass_forms_and_no_knobs():
-    """The shipped library contains only the k_icp_pass forms the parity suite covers — PF 6 at level 0, PF 5 on the
-    other levels, PF 3 / PF 0 for the occlusion variants, for the three cost functions — and reads no experiment
+    """The shipped library contains only the k_icp_pass forms the parity suite covers — PF 6 at level 0 of batched launches, PF 5 on
+    the other levels and at level 0 of lone alignments, PF 3 / PF 0 for the occlusion variants, for the three cost functions — and reads no experiment
     knob from the environment (R360_ICP_PF / _CAP / _WG_TOTAL / _PXT, R360_DIAG_EXTRA_ITERS, ...: experiment builds
     only, make exp), so no environment variable can change a registration."""
     blob = open(R.LIB_PATH, "rb").read()
