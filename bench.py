@@ -679,7 +679,7 @@ def main(argv=None, runner_factory=None):
     achieved = pairs_per_launch * alg_bytes / (avg_ms * 1e-3) / 1e9 if k0_n else None
     # a lone pair on an idle GPU (OdometryRGBD360's sequential caller registers one pair at a time): two frames
     # pipeline 0 has built, alignFrames360 with the same schedule, nothing else running
-    iso_ms, n, iso_ach, lone_ms = 0.0, 0, None, None
+    iso_ms, n, iso_ach, lone_ms, lone_mean_ms = 0.0, 0, None, None, None
     if not args.no_isolated:
         # two consecutive frames of the sequence, built as a caller of the façade builds them (Frame360 on pipeline 0's
         # calibration; the runner's queued ring frames skip the compacted level-0 points a lone pass reads)
@@ -695,10 +695,13 @@ def main(argv=None, runner_factory=None):
             reg.alignFrames360(np.eye(4, dtype=np.float32), R.PHOTO_DEPTH)
         ctxs[0].sync()
         ctxs[0].kernel_time_reset()
-        t_l = time.perf_counter()
-        for _ in range(5):
+        tl = []
+        for _ in range(20):   # median of 20 (one late host wake-up would move a 5-call mean by ~2 %)
+            t_l = time.perf_counter()
             reg.alignFrames360(np.eye(4, dtype=np.float32), R.PHOTO_DEPTH)
-        lone_ms = (time.perf_counter() - t_l) / 5 * 1e3
+            tl.append(time.perf_counter() - t_l)
+        lone_ms = float(np.median(tl)) * 1e3
+        lone_mean_ms = float(np.mean(tl)) * 1e3
         us, n, nj = ctxs[0].kernel_stats(0)
         iso_ms = us / max(n, 1) * 1e-3
         iso_ach = (nj / max(n, 1)) * alg_bytes / (iso_ms * 1e-3) / 1e9 if n else None
@@ -775,7 +778,7 @@ def main(argv=None, runner_factory=None):
             "event_avg_launch_ms": event_ms, "bytes_per_launch": pairs_per_launch * alg_bytes,
             "bytes_per_pair_pass": alg_bytes, "visible_frac": sso,
             "isolated": {"avg_launch_ms": iso_ms, "launches": n, "achieved": iso_ach,
-                         "frac": (iso_ach / HBM_PEAK_GBS) if iso_ach else None, "align_ms_per_pair": lone_ms,
+                         "frac": (iso_ach / HBM_PEAK_GBS) if iso_ach else None, "align_ms_per_pair": lone_ms, "align_ms_per_pair_mean": lone_mean_ms,
                          "note": "a lone pair on an idle GPU: alignFrames360 (same schedule) of two built frames, "
                                  "one pair per launch, 5 calls after 2 warm-up calls"},
             **({"eval_probe": probe} if probe else {}),
