@@ -677,8 +677,8 @@ def main(argv=None, runner_factory=None):
     event_ms = l0_ms / max(l0_n, 1)
     pairs_per_launch = k0_jobs / max(k0_n, 1)      # a batched launch runs one level-0 pass per pair
     achieved = pairs_per_launch * alg_bytes / (avg_ms * 1e-3) / 1e9 if k0_n else None
-    # a lone pair on an idle GPU (OdometryRGBD360's sequential caller registers one pair at a time): two frames
-    # pipeline 0 has built, alignFrames360 with the same schedule, nothing else running
+    # a lone pair on an idle GPU (OdometryRGBD360's sequential caller registers one pair at a time): the sequence's
+    # first two frames built through the façade, alignFrames360 with the same schedule, nothing else running
     iso_ms, n, iso_ach, lone_ms, lone_mean_ms = 0.0, 0, None, None, None
     if not args.no_isolated:
         # two consecutive frames of the sequence, built as a caller of the façade builds them (Frame360 on pipeline 0's
