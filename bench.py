@@ -681,20 +681,23 @@ def main(argv=None, runner_factory=None):
     # first two frames built through the façade, alignFrames360 with the same schedule, nothing else running
     iso_ms, n, iso_ach, lone_ms, lone_mean_ms = 0.0, 0, None, None, None
     if not args.no_isolated:
-        # two consecutive frames of the sequence, built as a caller of the façade builds them (Frame360 on pipeline 0's
-        # calibration; the runner's queued ring frames skip the compacted level-0 points a lone pass reads)
-        fa, fb = R.Frame360(runner.cals[0]), R.Frame360(runner.cals[0])
+        # two consecutive frames of the sequence, built as a caller of the façade builds them, on a context of their
+        # own (the runner's queued ring frames skip the compacted level-0 points a lone pass reads)
+        ictx = R.Context(local)
+        ical = R.Calib360(ictx, args.rows, args.cols)
+        ical.loadExtrinsicCalibration(R.EXTRINSICS_DIR)
+        fa, fb = R.Frame360(ical), R.Frame360(ical)
         for f, j in ((fa, p0), (fb, p0 + 1)):
             f.upload(*frames_of(j))
             f.build()
-        reg = R.RegisterPhotoICP(ctxs[0])
+        reg = R.RegisterPhotoICP(ictx)
         reg.params = params
         reg.setTargetFrame(fa)
         reg.setSourceFrame(fb)
         for _ in range(2):
             reg.alignFrames360(np.eye(4, dtype=np.float32), R.PHOTO_DEPTH)
-        ctxs[0].sync()
-        ctxs[0].kernel_time_reset()
+        ictx.sync()
+        ictx.kernel_time_reset()
         tl = []
         for _ in range(20):   # median of 20 (one late host wake-up would move a 5-call mean by ~2 %)
             t_l = time.perf_counter()
@@ -702,9 +705,10 @@ def main(argv=None, runner_factory=None):
             tl.append(time.perf_counter() - t_l)
         lone_ms = float(np.median(tl)) * 1e3
         lone_mean_ms = float(np.mean(tl)) * 1e3
-        us, n, nj = ctxs[0].kernel_stats(0)
+        us, n, nj = ictx.kernel_stats(0)
         iso_ms = us / max(n, 1) * 1e-3
         iso_ach = (nj / max(n, 1)) * alg_bytes / (iso_ms * 1e-3) / 1e9 if n else None
+        del reg, fa, fb, ical, ictx   # the frames and calibration hold their context: it goes last
     probe = None
     if args.eval_probe:   # opt-in diagnostic: the level-0 pass in eval mode (no GN step) at identity, alone
         fa, fb = runner.frames[0][:2]
