@@ -67,6 +67,21 @@ static std::string calib_dir_or_default(const char* dir, const char* sub) {
 // thread): with Linux's default 50 us slack a 20 us sleep overslept to ~70 us, so every short wait (a lone
 // alignment's result, RegisterPbMap's match tables) paid up to that much after the GPU had finished.  The caller's
 // own slack is restored before returning (the thread may be the application's).
+namespace {
+// 1 us timer slack on the calling thread for the duration of a wait (restored after): the default 50 us made every
+// short sleep of a poll loop overshoot
+struct Slack {
+    long old;
+    Slack() : old(prctl(PR_GET_TIMERSLACK, 0UL, 0UL, 0UL, 0UL)) {
+        if (old != 1000) (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0UL, 0UL, 0UL);
+    }
+    ~Slack() {
+        if (old > 0 && old != 1000) (void)prctl(PR_SET_TIMERSLACK, (unsigned long)old, 0UL, 0UL, 0UL);
+    }
+};
+double now_s() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
+}  // namespace
+
 int event_wait(hipEvent_t e) {
     const hipError_t r0 = hipEventQuery(e);
     if (r0 == hipSuccess) return 0;
@@ -74,15 +89,7 @@ int event_wait(hipEvent_t e) {
         r360_set_error("hipEventQuery -> %s", hipGetErrorString(r0));
         return -1;
     }
-    struct Slack {
-        long old;
-        Slack() : old(prctl(PR_GET_TIMERSLACK, 0UL, 0UL, 0UL, 0UL)) {
-            if (old != 1000) (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0UL, 0UL, 0UL);
-        }
-        ~Slack() {
-            if (old > 0 && old != 1000) (void)prctl(PR_SET_TIMERSLACK, (unsigned long)old, 0UL, 0UL, 0UL);
-        }
-    } slack;
+    Slack slack;
     for (int k = 0;; ++k) {
         std::this_thread::sleep_for(std::chrono::microseconds(k < 32 ? 5 : k < 96 ? 20 : 100));
         const hipError_t r = hipEventQuery(e);
@@ -96,6 +103,31 @@ int event_wait(hipEvent_t e) {
 
 int ctx_wait(r360_ctx* ctx) {
     R360_HIP(hipEventRecord(ctx->wait_ev, ctx->stream));
+    return event_wait(ctx->wait_ev);
+}
+
+// A lone alignment's result wait.  The previous alignment on the ctx took align_est seconds from its enqueue: until
+// 90 % of that has passed the wait checks every 50 us, then every ~2 us until 3x, then as event_wait (whose 20 us
+// polls by then came ~10 us late on average).  A wrong estimate (another frame size) costs at most one coarse check.
+static int align_wait(r360_ctx* ctx) {
+    R360_HIP(hipEventRecord(ctx->wait_ev, ctx->stream));
+    const double est = ctx->align_est;
+    if (est > 0 && est < 0.05) {
+        Slack slack;
+        const double t_fine = ctx->align_t0 + 0.9 * est, t_end = ctx->align_t0 + 3 * est;
+        for (;;) {
+            const hipError_t r = hipEventQuery(ctx->wait_ev);
+            if (r == hipSuccess) return 0;
+            if (r != hipErrorNotReady) {
+                r360_set_error("hipEventQuery -> %s", hipGetErrorString(r));
+                return -1;
+            }
+            const double t = now_s();
+            if (t > t_end) break;
+            const double left = t_fine - t;
+            std::this_thread::sleep_for(std::chrono::microseconds(left > 50e-6 ? 50 : left > 2e-6 ? (long)(left * 1e6) : 2));
+        }
+    }
     return event_wait(ctx->wait_ev);
 }
 
@@ -971,6 +1003,7 @@ extern "C" int r360_align360_async(r360_ctx* ctx, r360_frame* trg, r360_frame* s
         if (f->ctx != ctx)
             if (hipEvent_t e = frame_build_event(f)) R360_HIP(hipStreamWaitEvent(ctx->stream, e, 0));
     IcpState* h = ctx->h_state;
+    ctx->align_t0 = now_s();
     memset(h, 0, sizeof(IcpState));
     memcpy(h->pose, init, sizeof(float) * 16);
     memcpy(h->cand, init, sizeof(float) * 16);
@@ -1034,7 +1067,8 @@ extern "C" int r360_align360_result(r360_ctx* ctx, float pose_out[16], float H_o
     CHECK_ARG(ctx && ctx->async_pending, "no alignment pending");
     IcpState* h = ctx->h_state;
     R360_HIP(hipMemcpyAsync(h, ctx->d_state, sizeof(IcpState), hipMemcpyDeviceToHost, ctx->stream));
-    const int wrc = ctx_wait(ctx);
+    const int wrc = align_wait(ctx);
+    if (wrc == 0) ctx->align_est = now_s() - ctx->align_t0;   // the next alignment's wait plan
     persist_release(ctx);
     if (wrc) return -1;
     ctx->async_pending = 0;

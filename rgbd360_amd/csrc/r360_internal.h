@@ -351,6 +351,7 @@ struct r360_ctx {
     std::vector<std::pair<std::string, Acc>> acc;
     // async-align bookkeeping
     int async_nL = 0, async_pending = 0;
+    double align_t0 = 0, align_est = 0;   // the pending lone alignment's enqueue time, the previous one's duration (s)
     // batched alignFrames360 (r360_align360_batch_*): per-job state / records / counters / queues
     int batch_cap = 0;               // jobs the batch buffers hold
     long bdefer_cap = 0;             // deferred-queue entries per job
