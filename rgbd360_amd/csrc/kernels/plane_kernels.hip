@@ -354,21 +354,24 @@ __global__ void k_dcm(const PlaneBatch B, int w, int h) {
 // and a 10-term window for the within-row chain reproduce every value below the cap bit for bit
 // (rounding is monotone: fl(min(a,b)+1) = min(fl(a+1), fl(b+1))).  Values at or above the cap are
 // upper bounds of the true ones and never win the min.
-constexpr int DM_BAND = 4, DM_HALO = 10, DM_TPB = 512;   // short bands: the halo rows run in parallel
+// DM_BAND output rows per workgroup, which also sweeps DM_HALO rows above and below: 4 rows kept the isolated
+// latency lowest (38 row steps per workgroup), 8 halves the redundant halo sweeps (1590-1596 -> 1614-1615 pairs/s
+// in the batched plane stage, profiles/r5_dm; 16 / 32 within noise of 8)
+constexpr int DM_BAND = 8, DM_HALO = 10, DM_TPB = 512;
 // (one wave per band measured 2.3x slower: the 10-term chain windows of 5 columns per lane serialise); a thread per
 // column at VGA (w = 320): 256 threads 64 us, 320 41 us, 512 39 us per frame; bands of 2 / 3 / 6 / 8 rows slower
 
 __device__ __forceinline__ void dm_sync() { __syncthreads(); }
 
-__device__ __forceinline__ void d_distmap(const float* __restrict__ init, int w, int h,
+__device__ __forceinline__ void d_distmap(const float* __restrict__ init, int w, int h, int band,
                                                    float* __restrict__ out) {
-    extern __shared__ float sm[];   // (DM_BAND + 2*DM_HALO + 2) rows x w, plus two temp rows
+    extern __shared__ float sm[];   // (band + 2*DM_HALO + 2) rows x w, plus two temp rows
     const int s = blockIdx.y;
-    const int r0 = blockIdx.x * DM_BAND;
+    const int r0 = blockIdx.x * band;
     if (r0 >= h) return;
     const long N = (long)w * h;
     const float* I = init + s * N;
-    const int R1 = max(1, r0 - DM_HALO), R2 = min(h - 1, r0 + DM_BAND + DM_HALO);
+    const int R1 = max(1, r0 - DM_HALO), R2 = min(h - 1, r0 + band + DM_HALO);
     const int base = R1 - 1;                       // LDS row 0 = image row R1-1
     const int nrows = R2 - base + 1;
     float* tmp = sm + (long)nrows * w;
@@ -395,7 +398,7 @@ __device__ __forceinline__ void d_distmap(const float* __restrict__ init, int w,
         dm_sync();
     }
     // backward pass rows Rb..r0
-    const int Rb = min(h - 2, r0 + DM_BAND + DM_HALO - 1);
+    const int Rb = min(h - 2, r0 + band + DM_HALO - 1);
     for (int r = Rb; r >= r0; --r) {
         const float* next = L(r + 1);
         float* cur = L(r);
@@ -413,12 +416,12 @@ __device__ __forceinline__ void d_distmap(const float* __restrict__ init, int w,
         }
         dm_sync();
     }
-    const int rend = min(h, r0 + DM_BAND);
+    const int rend = min(h, r0 + band);
     for (int k = threadIdx.x; k < (rend - r0) * w; k += blockDim.x) out[s * N + (long)r0 * w + k] = L(r0)[k];
 }
-__global__ void __launch_bounds__(DM_TPB) k_distmap(const PlaneBatch B, int w, int h) {
+__global__ void __launch_bounds__(DM_TPB) k_distmap(const PlaneBatch B, int w, int h, int band) {
     const PlaneDev& D = B.f[blockIdx.z];
-    d_distmap(D.dist0, w, h, D.dist);
+    d_distmap(D.dist0, w, h, band, D.dist);
 }
 
 
@@ -741,12 +744,15 @@ int launch_cloud_normals(const PlaneBatch& B, int F, const PlaneGeom& G, hipStre
     hipLaunchKernelGGL(k_dcm, dim3(blocks, 1, nf), dim3(256), 0, st, B, w, h);
     timing_end(tctx, slot);
     R360_HIP(hipGetLastError());
-    const int nb = (h + DM_BAND - 1) / DM_BAND;
-    const int max_rows = DM_BAND + 2 * DM_HALO + 2;
+    // experiment builds: R360_DM_BAND rows per workgroup (each workgroup also sweeps 2 x DM_HALO halo rows)
+    static const int dm_band = R360_KNOB("R360_DM_BAND", DM_BAND);
+    const int band = dm_band >= 1 && dm_band <= 64 ? dm_band : DM_BAND;
+    const int nb = (h + band - 1) / band;
+    const int max_rows = band + 2 * DM_HALO + 2;
     const size_t lds = sizeof(float) * ((size_t)max_rows + 2) * w;
     if (lds > 160 * 1024) { r360_set_error("distance map: cloud width %d too large", w); return -1; }
     slot = timing_begin(tctx, "k_distmap");
-    hipLaunchKernelGGL(k_distmap, dim3(nb, 8, nf), dim3(DM_TPB), lds, st, B, w, h);
+    hipLaunchKernelGGL(k_distmap, dim3(nb, 8, nf), dim3(DM_TPB), lds, st, B, w, h, band);
     timing_end(tctx, slot);
     R360_HIP(hipGetLastError());
     slot = timing_begin(tctx, "k_normals");
