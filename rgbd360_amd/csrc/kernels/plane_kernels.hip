@@ -273,6 +273,85 @@ __global__ void k_bil_blur(const PlaneBatch B, long grid_cells, int src_slot, lo
 }
 
 
+// The three axis passes in one launch: a workgroup stages a BT_X x BT_Y x BT_Z tile of the splat grid with a 2-cell
+// halo in LDS, blurs along x over the tile's y / z halo, then along y over its z halo, then along z, and writes the
+// tile once (the three launches read and wrote the whole grid three times).  Every cell is computed by d_bil_blur's
+// expressions from the same inputs, so the result is that of the three passes bit for bit; a halo cell outside the
+// grid is staged as zero and never enters an interior cell's value (a pass reads only in-grid neighbours of interior
+// cells, and every boundary cell of every pass is zero).
+constexpr int BT_X = 16, BT_Y = 8, BT_Z = 4, BT_TPB = 256;
+constexpr int BT_SX = BT_X + 4, BT_SY = BT_Y + 4, BT_SZ = BT_Z + 4;
+
+__device__ __forceinline__ float2 bil_121(float2 a, float2 b, float2 m) {
+    return make_float2((a.x + b.x + 2.0f * m.x) / 4.0f, (a.y + b.y + 2.0f * m.y) / 4.0f);
+}
+// one pass's output at axis coordinate a0 (extent an) from the five values v[0..4] at a0 - 2 .. a0 + 2; zero when the
+// cell is on a boundary of the grid (bnd: of the other two axes, or of this one)
+__device__ __forceinline__ float2 bil_pass(const float2 (&v)[5], long a0, long an, bool bnd) {
+    if (bnd || a0 <= 0 || a0 >= an - 1) return make_float2(0.f, 0.f);
+    float2 b1[3];
+#pragma unroll
+    for (int k = -1; k <= 1; ++k) {
+        const long ak = a0 + k;
+        b1[k + 1] = (ak <= 0 || ak >= an - 1) ? make_float2(0.f, 0.f) : bil_121(v[k + 1], v[k + 3], v[k + 2]);
+    }
+    return make_float2((b1[0].x + b1[2].x + 2.0f * b1[1].x) / 4.0f, (b1[0].y + b1[2].y + 2.0f * b1[1].y) / 4.0f);
+}
+
+__global__ void __launch_bounds__(BT_TPB) k_bil_blur3(const PlaneBatch B, long grid_cells, long sw, long sh, int sd_max) {
+    __shared__ float2 S[BT_SZ][BT_SY][BT_SX];   // source tile + halo
+    __shared__ float2 XB[BT_SZ][BT_SY][BT_X];   // after the x pass
+    __shared__ float2 YB[BT_SZ][BT_Y][BT_X];    // after the y pass
+    const PlaneDev& D = B.f[blockIdx.z / 8];
+    const int s = blockIdx.z & 7;
+    float bmin, bmax;
+    long sd;
+    bool over;
+    if (!bil_params(D.zmm, s, sd_max, bmin, bmax, sd, over)) return;
+    const long ntx = (sw + BT_X - 1) / BT_X;
+    const long x0 = (long)(blockIdx.x % ntx) * BT_X, y0 = (long)(blockIdx.x / ntx) * BT_Y, z0 = (long)blockIdx.y * BT_Z;
+    if (z0 >= sd) return;
+    const long ncol = sw * sh;
+    const float2* src = D.grids + (long)s * 2 * grid_cells;            // slot 0
+    float2* dst = D.grids + (long)s * 2 * grid_cells + grid_cells;     // slot 1
+    const int t = threadIdx.x;
+    for (int k = t; k < BT_SZ * BT_SY * BT_SX; k += BT_TPB) {
+        const int lx = k % BT_SX, ly = (k / BT_SX) % BT_SY, lz = k / (BT_SX * BT_SY);
+        const long x = x0 - 2 + lx, y = y0 - 2 + ly, z = z0 - 2 + lz;
+        S[lz][ly][lx] = (x >= 0 && x < sw && y >= 0 && y < sh && z >= 0 && z < sd) ? src[z * ncol + y * sw + x]
+                                                                                    : make_float2(0.f, 0.f);
+    }
+    __syncthreads();
+    for (int k = t; k < BT_SZ * BT_SY * BT_X; k += BT_TPB) {   // x pass
+        const int lx = k % BT_X, ly = (k / BT_X) % BT_SY, lz = k / (BT_X * BT_SY);
+        const long x = x0 + lx, y = y0 - 2 + ly, z = z0 - 2 + lz;
+        float2 v[5];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) v[j] = S[lz][ly][lx + j];
+        XB[lz][ly][lx] = bil_pass(v, x, sw, y <= 0 || y >= sh - 1 || z <= 0 || z >= sd - 1);
+    }
+    __syncthreads();
+    for (int k = t; k < BT_SZ * BT_Y * BT_X; k += BT_TPB) {    // y pass
+        const int lx = k % BT_X, ly = (k / BT_X) % BT_Y, lz = k / (BT_X * BT_Y);
+        const long x = x0 + lx, y = y0 + ly, z = z0 - 2 + lz;
+        float2 v[5];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) v[j] = XB[lz][ly + j][lx];
+        YB[lz][ly][lx] = bil_pass(v, y, sh, x <= 0 || x >= sw - 1 || z <= 0 || z >= sd - 1);
+    }
+    __syncthreads();
+    for (int k = t; k < BT_Z * BT_Y * BT_X; k += BT_TPB) {     // z pass and the tile's write
+        const int lx = k % BT_X, ly = (k / BT_X) % BT_Y, lz = k / (BT_X * BT_Y);
+        const long x = x0 + lx, y = y0 + ly, z = z0 + lz;
+        if (x >= sw || y >= sh || z >= sd) continue;
+        float2 v[5];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) v[j] = YB[lz + j][ly][lx];
+        dst[z * ncol + y * sw + x] = bil_pass(v, z, sd, x <= 0 || x >= sw - 1 || y <= 0 || y >= sh - 1);
+    }
+}
+
+
 __device__ __forceinline__ void d_bil_slice(float4* __restrict__ cloud_all, int w, int h, long sw, long sh,
                             const int* __restrict__ zmm, int sd_max, const float2* __restrict__ grids, long grid_cells,
                             int slot) {
@@ -732,10 +811,18 @@ int launch_cloud_normals(const PlaneBatch& B, int F, const PlaneGeom& G, hipStre
         const long ncol = sw * sh;
         hipLaunchKernelGGL(k_bil_splat, dim3((ncol + BIL_COLS - 1) / BIL_COLS, 8, nf), dim3(BIL_COLS), 0, st, B, w, h,
                            sw, sh, G.sd_max, G.grid_cells);
-        const dim3 gb((unsigned)((ncol * G.sd_max + 255) / 256), 8, nf);
-        hipLaunchKernelGGL(k_bil_blur<0>, gb, dim3(256), 0, st, B, G.grid_cells, 0, sw, sh, G.sd_max);
-        hipLaunchKernelGGL(k_bil_blur<1>, gb, dim3(256), 0, st, B, G.grid_cells, 1, sw, sh, G.sd_max);
-        hipLaunchKernelGGL(k_bil_blur<2>, gb, dim3(256), 0, st, B, G.grid_cells, 0, sw, sh, G.sd_max);
+        // the three axis passes fused (k_bil_blur3; R360_BIL_FUSED=0, experiment builds: one launch per axis)
+        static const int fused = R360_KNOB("R360_BIL_FUSED", 1);
+        if (fused) {
+            const long ntile = ((sw + BT_X - 1) / BT_X) * ((sh + BT_Y - 1) / BT_Y);
+            hipLaunchKernelGGL(k_bil_blur3, dim3((unsigned)ntile, (unsigned)((G.sd_max + BT_Z - 1) / BT_Z), 8 * nf),
+                               dim3(BT_TPB), 0, st, B, G.grid_cells, sw, sh, G.sd_max);
+        } else {
+            const dim3 gb((unsigned)((ncol * G.sd_max + 255) / 256), 8, nf);
+            hipLaunchKernelGGL(k_bil_blur<0>, gb, dim3(256), 0, st, B, G.grid_cells, 0, sw, sh, G.sd_max);
+            hipLaunchKernelGGL(k_bil_blur<1>, gb, dim3(256), 0, st, B, G.grid_cells, 1, sw, sh, G.sd_max);
+            hipLaunchKernelGGL(k_bil_blur<2>, gb, dim3(256), 0, st, B, G.grid_cells, 0, sw, sh, G.sd_max);
+        }
         hipLaunchKernelGGL(k_bil_slice, dim3(blocks, 1, nf), dim3(256), 0, st, B, w, h, sw, sh, G.sd_max, G.grid_cells, 1);
     }
     timing_end(tctx, slot);
