@@ -49,6 +49,13 @@ ICP_SOURCES = ["rgbd360_amd/csrc/kernels/icp_kernels.hip", "rgbd360_amd/csrc/ker
                "rgbd360_amd/csrc/libm_f32.h", "rgbd360_amd/csrc/r360_internal.h"]
 
 
+def _sha16(path):
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def icp_source_hash():
     """Hash of the ICP pass's sources: a profile's PMC traffic is reported only for the kernel it measured."""
     h = hashlib.sha256()
@@ -768,6 +775,10 @@ def main(argv=None, runner_factory=None):
             "dense_batch": args.queue, "dense_in_flight_per_pipeline": args.depth if args.queue else 1,
             "frames_built_ahead": args.lookahead if args.queue else 1,
             "plane_batch": args.plane_batch,
+            # the hardware-queue pool this run had (bench.py sets 16 only where the environment left it unset)
+            "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
+            # the library the binding loaded (R360_LIB can point the binding elsewhere: shown, never silent)
+            "library": os.path.relpath(R.LIB_PATH, ROOT), "library_sha16": _sha16(R.LIB_PATH),
             **({"emulated_shard": f"{shard_rank}/{shard_world}"} if args.emulate else {}),
         },
         "value_hbm_resident_inputs": resident,

@@ -46,12 +46,9 @@ __global__ void k_undistort(const uint16_t* __restrict__ depth, float* __restric
 
 // k_undistort with 4 consecutive pixels of one sensor row per thread (cols % 4 == 0): one 8-byte load and one 16-byte
 // store per thread instead of a 2-byte load and a 4-byte store per pixel, the same per-pixel expressions
-__device__ __forceinline__ float undistort_px(float z, long i, int rows, int cols, const float* __restrict__ mult,
-                                              const float* __restrict__ counts, int nx, int bin_w, int bin_h, int nb,
-                                              double bin_depth) {
-    const int s = (int)(i / ((long)rows * cols));
-    const int pix = (int)(i - (long)s * rows * cols);
-    const int v = pix / cols, u = pix - v * cols;
+__device__ __forceinline__ float undistort_px(float z, int s, int v, int u, int rows, int cols,
+                                              const float* __restrict__ mult, const float* __restrict__ counts, int nx,
+                                              int bin_w, int bin_h, int nb, double bin_depth) {
     const long fr = ((long)s * (rows / bin_h) * nx + (long)(v / bin_h) * nx + (u / bin_w)) * nb;
     int idx = (int)floor(z / bin_depth);
     idx = idx < nb - 1 ? idx : nb - 1;
@@ -74,11 +71,17 @@ __global__ void k_undistort4(const uint16_t* __restrict__ depth, float* __restri
         const uint2 d4 = reinterpret_cast<const uint2*>(depth)[q];
         const unsigned dv[4] = {d4.x & 0xffffu, d4.x >> 16, d4.y & 0xffffu, d4.y >> 16};
         float z[4];
+        // the quad's sensor, row and first column (one row: cols % 4 == 0; 32-bit: a sensor image < 2^31 pixels)
+        const int pq = rows * cols / 4;
+        const int qi = (int)q;
+        const int s = qi / pq;
+        const int pix = (qi - s * pq) * 4;
+        const int v = pix / cols, u0 = pix - v * cols;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             z[e] = (float)dv[e] * 0.001f;                          // convertTo(CV_32FC1, 0.001)
             if (apply && z[e] != 0)                                // discrete_depth_distortion_model.cpp:175-186
-                z[e] = undistort_px(z[e], 4 * q + e, rows, cols, mult, counts, nx, bin_w, bin_h, nb, bin_depth);
+                z[e] = undistort_px(z[e], s, v, u0 + e, rows, cols, mult, counts, nx, bin_w, bin_h, nb, bin_depth);
         }
         reinterpret_cast<float4*>(depth_m)[q] = make_float4(z[0], z[1], z[2], z[3]);
     }
@@ -302,17 +305,18 @@ struct LvPk {
 };
 
 // nimg images of R x C stored back to back (the sphere: 1; the per-sensor pyramids: 8)
+// (32-bit index arithmetic: nimg * R * C < 2^31, checked by the launchers)
 template <class IN>
 __global__ void k_pyramid(const IN in_all, int R, int C, float2* __restrict__ out_all, float min_d, float max_d,
                           int nimg) {
     const int dr = R / 2, dc = C / 2;
-    const long per = (long)dr * dc, n = per * nimg;
-    for (long j = blockIdx.x * (long)blockDim.x + threadIdx.x; j < n; j += (long)gridDim.x * blockDim.x) {
-        const int img = (int)(j / per);
-        const long i = j - (long)img * per;
+    const unsigned per = (unsigned)(dr * dc), n = per * (unsigned)nimg;
+    for (unsigned j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+        const unsigned img = nimg > 1 ? j / per : 0u;
+        const unsigned i = j - img * per;
         const long in0 = (long)img * R * C;
         float2* out = out_all + (long)img * per;
-        const int y = (int)(i / dc), x = (int)(i - (long)y * dc);
+        const int y = (int)(i / (unsigned)dc), x = (int)(i - (unsigned)y * dc);
         // cv::pyrDown: horizontal [1 4 6 4 1] per source row, then the vertical SSE order.
         const int sx = 2 * x;
         const int xa = refl101(sx - 2, C), xb = refl101(sx - 1, C), xd = refl101(sx + 1, C), xe = refl101(sx + 2, C);
@@ -593,6 +597,10 @@ int launch_sphere_level0(r360_frame* f) {
 int launch_pyramid(r360_frame* f) {
     // RegisterPhotoICP constructor defaults minDepth 0.3 / maxDepth 6.0 (:202-203)
     const float min_d = 0.3f, max_d = 6.0f;
+    if ((long)f->lv[0].rows * f->lv[0].cols > 0x7fffffffL) {   // 32-bit pixel indices
+        r360_set_error("sphere of %d x %d pixels is too large", f->lv[0].rows, f->lv[0].cols);
+        return -1;
+    }
     static const bool pyr_f2 = R360_KNOB("R360_PYR_F2", 0) != 0;   // experiment builds: level 0 read as float2
     for (int l = 1; l < f->n_levels; ++l) {
         const long n = (long)f->lv[l].rows * f->lv[l].cols;
@@ -663,6 +671,10 @@ int launch_sensor_pyramid(r360_frame* f) {
     }
     hipStream_t st = f->ctx->stream;
     const long n0 = 8L * f->rows * f->cols;
+    if (n0 > 0x7fffffffL) {   // k_pyramid's 32-bit pixel indices
+        r360_set_error("sensor images of %d x %d pixels are too large", f->rows, f->cols);
+        return -1;
+    }
     hipLaunchKernelGGL(k_sensor_level0, dim3(grid_for(n0)), dim3(TPB), 0, st, f->d_bgr, f->d_depth, n0, f->sp[0].p0,
                        (uint32_t*)nullptr);
     for (int l = 1; l < f->n_slevels; ++l) {
