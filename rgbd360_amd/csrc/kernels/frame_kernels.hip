@@ -387,31 +387,46 @@ struct GradLevels {
     int nl;
 };
 
+// GRAD_PPT pixels per thread: a wave covers GRAD_PPT x 64 consecutive pixels, pixel k of a lane at i0 + 64 k (every
+// load and store coalesced across the wave); the row and column of the first pixel come from one 32-bit division and
+// are stepped by 64 columns for the others (one level search and one division per 4 pixels instead of per pixel:
+// in the pipeline the launch had 12.8 k single-pixel-per-thread workgroups per frame)
+constexpr int GRAD_PPT = 4;
+
 template <class IN>
-__device__ __forceinline__ void gradient_px(const IN p0, long i, int R, int C, float4* __restrict__ tg) {
+__device__ __forceinline__ void gradient_run(const IN p0, int i0, int R, int C, float4* __restrict__ tg) {
     const int ws = C / 8;   // >= 1: calib_build_tables stops the pyramid before a level narrower than 8
-    const int r = (int)(i / C), c = (int)(i - (long)r * C);
-    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
-    const int m = ws > 0 ? c % ws : 1;   // seam columns as k_gradient (alignFrames360 :4538-4549)
-    const bool seam = ws > 0 && (c >= ws - 1) && (c < 7 * ws + 1) && (m == 0 || m == ws - 1);
-    if (!seam && r >= 1 && r < R - 1 && c >= 1 && c < C - 1) {
-        const float2 f = p0.gd(i), fl = p0.gd(i - 1), fr = p0.gd(i + 1), fu = p0.gd(i - C), fd = p0.gd(i + C);
-        o.x = harm(fl.x, f.x, fr.x);
-        o.y = harm(fu.x, f.x, fd.x);
-        o.z = harm(fl.y, f.y, fr.y);
-        o.w = harm(fu.y, f.y, fd.y);
+    const int n = R * C;
+    int r = i0 / C, c = i0 - r * C;
+#pragma unroll
+    for (int k = 0; k < GRAD_PPT; ++k) {
+        const int i = i0 + 64 * k;
+        if (i >= n) break;
+        float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+        const int m = ws > 0 ? c % ws : 1;   // seam columns as k_gradient (alignFrames360 :4538-4549)
+        const bool seam = ws > 0 && (c >= ws - 1) && (c < 7 * ws + 1) && (m == 0 || m == ws - 1);
+        if (!seam && r >= 1 && r < R - 1 && c >= 1 && c < C - 1) {
+            const float2 f = p0.gd(i), fl = p0.gd(i - 1), fr = p0.gd(i + 1), fu = p0.gd(i - C), fd = p0.gd(i + C);
+            o.x = harm(fl.x, f.x, fr.x);
+            o.y = harm(fu.x, f.x, fd.x);
+            o.z = harm(fl.y, f.y, fr.y);
+            o.w = harm(fu.y, f.y, fd.y);
+        }
+        tg[i] = o;
+        c += 64;   // the lane's next pixel (C may be below 64 on the small levels: several rows on)
+        while (c >= C) { c -= C; ++r; }
     }
-    tg[i] = o;
 }
 
 __global__ void k_gradient_levels(GradLevels G) {
     int l = 0;
     while (l + 1 < G.nl && (int)blockIdx.x >= G.blk0[l + 1]) ++l;
     const int R = G.rows[l], C = G.cols[l];
-    const long i = (long)(blockIdx.x - G.blk0[l]) * blockDim.x + threadIdx.x;
-    if (i >= (long)R * C) return;
-    if (l == 0 && G.pk0) gradient_px(LvPk{G.pk0}, i, R, C, G.tg[0]);
-    else gradient_px(LvF2{G.p0[l]}, i, R, C, G.tg[l]);
+    const int i0 = (int)((blockIdx.x - G.blk0[l]) * blockDim.x * GRAD_PPT + (threadIdx.x & ~63u) * GRAD_PPT +
+                         (threadIdx.x & 63u));
+    if (i0 >= R * C) return;
+    if (l == 0 && G.pk0) gradient_run(LvPk{G.pk0}, i0, R, C, G.tg[0]);
+    else gradient_run(LvF2{G.p0[l]}, i0, R, C, G.tg[l]);
 }
 
 // setSourceFrame / setTargetFrame level 0 of each sensor's raw images (:480-516): CV_RGB2GRAY on the
@@ -597,7 +612,7 @@ int launch_sphere_level0(r360_frame* f) {
 int launch_pyramid(r360_frame* f) {
     // RegisterPhotoICP constructor defaults minDepth 0.3 / maxDepth 6.0 (:202-203)
     const float min_d = 0.3f, max_d = 6.0f;
-    if ((long)f->lv[0].rows * f->lv[0].cols > 0x7fffffffL) {   // 32-bit pixel indices
+    if ((long)f->lv[0].rows * f->lv[0].cols > 0x7fffffffL - 4096) {   // 32-bit pixel indices
         r360_set_error("sphere of %d x %d pixels is too large", f->lv[0].rows, f->lv[0].cols);
         return -1;
     }
@@ -621,7 +636,7 @@ int launch_pyramid(r360_frame* f) {
             GL.tg[l] = f->lv[l].tg;
             GL.rows[l] = f->lv[l].rows;
             GL.cols[l] = f->lv[l].cols;
-            GL.blk0[l + 1] = GL.blk0[l] + (int)(((long)f->lv[l].rows * f->lv[l].cols + TPB - 1) / TPB);
+            GL.blk0[l + 1] = GL.blk0[l] + (int)(((long)f->lv[l].rows * f->lv[l].cols + TPB * GRAD_PPT - 1) / (TPB * GRAD_PPT));
         }
         hipLaunchKernelGGL(k_gradient_levels, dim3(GL.blk0[f->n_levels]), dim3(TPB), 0, f->ctx->stream, GL);
     }
