@@ -2284,7 +2284,11 @@ static PassGrid pass_grid(const r360_ctx* ctx, const LevelBufs& Ls, int occ, int
     // level 0) then run on a few hundred / dozen workgroups per pair instead of one thread per point, which
     // shortens their record / ticket / final-sum tail (level 0 at VGA has ~19 per thread on the capped grid)
     static const int pxt_env = R360_KNOB("R360_ICP_PXT", -1);
-    const int pxt = pxt_env > 0 ? pxt_env : 1;
+    // Batched launches take at least 8 points per thread (round 5): levels 2-4 then run on 75 / 19 / 5 workgroups per
+    // job instead of 256 / 150 / 38 (level 0 and 1 stay at the one-per-CU cap), so a batch's coarse passes need fewer
+    // CU slots (under the pipelines' load their first workgroups waited for slots, profiles/r5_trace) and sum fewer
+    // records: +0.9 % in an A/B (profiles/r5_envab/pxt/, r5_prep2/pxt8/).  The grid still depends only on the level size.
+    const int pxt = pxt_env > 0 ? pxt_env : (batched ? 8 : 1);
     int nb = pf == 1 ? icp_blocks_for(npx) : (npx + TPB * pxt - 1) / (TPB * pxt);
     if (nb > cap) nb = cap;
     if (nb < 1) nb = 1;
