@@ -36,9 +36,11 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-# Hardware queues per process (HIP's default is 4): the per-frame plane kernels are latency-bound
-# (one workgroup or wave per sensor), so throughput comes from many pipelines' kernels running at
-# once; 16 queues let 16 streams reach the hardware side by side.  Must precede HIP initialisation.
+# Hardware queues per process: 16 only where the environment leaves GPU_MAX_HW_QUEUES unset.  The GPU box
+# presets 4 (HIP's default), so the driver's bench lines run with a pool of 4 pooled queues (the line records the
+# value in config.gpu_max_hw_queues); the dense queue and the plane queue have CU-masked hardware queues of their
+# own outside the pool, and 4 vs 16 pooled queues measured within 1 % (profiles/r5_envab/).
+# Must precede HIP initialisation.
 os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 
 METRIC = "registered Frame360 pairs/sec @ 8×640×480; ICP-reduce HBM GB/s vs roofline"
@@ -551,8 +553,8 @@ def main(argv=None, runner_factory=None):
             group.barrier(ctxs)
 
     # warmup: every buffer (frames, queues, records) is allocated here, outside the timed region
-    runner.run(p0, p1, frames_of, np.zeros((max(args.warmup, 1), p1 - p0, OD.REC), np.float32),
-               repeats=max(args.warmup, 1), runs=runs)
+    wrec = np.zeros((max(args.warmup, 1), p1 - p0, OD.REC), np.float32)
+    runner.run(p0, p1, frames_of, wrec, repeats=max(args.warmup, 1), runs=runs)
     # frame builds per step beyond one per pair: the first frame of every segment of every piece
     halo_per_step = ((len(runs) * args.steps) if runs else
                      sum(len(g) for g in OD.stream_pieces(p0, p1, args.steps, P))) / args.steps
@@ -646,6 +648,10 @@ def main(argv=None, runner_factory=None):
         elapsed = group.max(elapsed)
     pairs_job = args.steps * sum(sizes)
     value = pairs_job / elapsed
+    # every timed step's pair records against the first warm-up step's, bit for bit (the same pairs, registered in
+    # other pipeline pieces and dense batches): a wrong frame buffer at a piece's repeat boundary would show here
+    records_same = {"timed_steps": bool((rec == wrec[0][None]).all()),
+                    "warmup_steps": bool((wrec == wrec[0][None]).all())}
 
     # secondary: the same steps with the raw images already resident in HBM (device-to-device copies
     # into the frames instead of PCIe uploads)
@@ -670,6 +676,7 @@ def main(argv=None, runner_factory=None):
         resident = pairs_job / e2
         dB.close()
         dD.close()
+        records_same["resident_steps"] = bool((rec2 == wrec[0][None]).all())
 
     W0 = args.rows * 8
     H0 = int(W0 * 0.5 * 60.0 / 180)               # Frame360.h:391-392 (640 x 3840 at VGA)
@@ -782,6 +789,9 @@ def main(argv=None, runner_factory=None):
             **({"emulated_shard": f"{shard_rank}/{shard_world}"} if args.emulate else {}),
         },
         "value_hbm_resident_inputs": resident,
+        "records_identical": all(records_same.values()),
+        "records_check": {**records_same, "reference": "first warm-up step, same runner mode",
+                          **({"ranks": "per rank, own shard"} if group is not None else {})},
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,

@@ -183,9 +183,13 @@ int r360_align360_result(r360_ctx* ctx, float pose_out[16], float H_out[36], flo
                          r360_icp_stats* st);
 
 /* Batched alignFrames360 (occlusion 0): n <= R360_MAX_BATCH independent alignments of pairs
- * (trg[j], src[j]) from init[16 j..], each exactly the computation r360_align360 performs on that pair
- * (same passes, same per-pair Gauss-Newton state and decisions; results bit-identical), run as one launch
- * per pass over all pairs.  This is how the reference's callers' many alignFrames360 calls (one per
+ * (trg[j], src[j]) from init[16 j..], each the alignFrames360 of r360_align360 on that pair (same schedule,
+ * same per-pair Gauss-Newton state and logic), run as one launch per pass over all pairs.  Batch-invariant:
+ * a pair's result is bit-identical in any batch of any size, on any context or rank (the batched grid depends
+ * on the level size only).  It equals r360_align360's result to rounding, not bit for bit: a lone alignment
+ * sums the same pixels over twice the workgroup records (two per CU) and, on frames with compacted level-0
+ * points, with PF 5 instead of PF 6, so a pair whose accept / stop test sits at a rounding edge can stop on
+ * another pass (tests/test_gpu_batch_align.py pins the drift).  This is how the reference's callers' many alignFrames360 calls (one per
  * consecutive pair in OdometryRGBD360.cpp:141-257, per keyframe candidate in SphereGraphSLAM /
  * LoopClosure360) fill the GPU.  Frames must share one sphere size and may belong to any ctx of the device:
  * ctx's stream waits for the work already enqueued on their contexts' streams.  _result fills n poses /
@@ -200,7 +204,8 @@ int r360_align360_batch_result(r360_ctx* ctx, float* pose_out, float* H_out, flo
  * stream.  A dispatcher thread runs every pending job (up to max_batch of one method / parameter set) as one
  * r360_align360_batch call; the next batch accumulates while one runs.  submit records the frames' build
  * work (their contexts' streams) and returns a ticket at once; collect waits for that job and returns
- * what r360_align360_result would (0, 1 = ILL-POSED, < 0 error).  The frames must stay unmodified until
+ * what r360_align360_batch_result returns for the job (0, 1 = ILL-POSED, < 0 error): the batched result,
+ * the same in any batch, equal to a lone r360_align360 to rounding (above).  The frames must stay unmodified until
  * their job is collected: a batch waits on each frame's build event, which a rebuild re-records, so a frame
  * rebuilt between submit and dispatch fails the job with an error instead of aligning against the newer build.
  * Every ticket must be collected once.  Thread-safe. */
@@ -460,9 +465,9 @@ int r360_pbmap_match_tables(r360_ctx* ctx, r360_frame* ref, r360_frame* trg, siz
  * keyframes) and LoopClosure360's candidate checks (include/LoopClosure360.h:280-366: RegisterPbMap
  * PLANAR_3DoF, gate on matches/area, alignFrames360 refinement) issue them.  A batch owns `lanes`
  * worker contexts (own HIP stream, ICP state and matcher scratch) and runs the jobs of one call
- * concurrently, one host thread per lane.  Every job computes exactly what the sequential reference
- * call computes: the result of a batched job is identical to r360_register_pbmap / r360_align360 on
- * the same frames.  Frames may belong to any ctx of the same device; each lane's stream waits for
+ * concurrently, one host thread per lane.  Every job is the sequential call itself on its lane's
+ * context: the result of a batched job is identical to r360_register_pbmap / r360_align360 on the
+ * same frames (lone alignments, not the batched grid of r360_align360_batch).  Frames may belong to any ctx of the same device; each lane's stream waits for
  * the frames' build work before reading them.  The caller must not modify or destroy a frame while a
  * batch call that names it runs.  Calls on one batch are serialised: a call made while another thread's
  * call runs waits for it. */

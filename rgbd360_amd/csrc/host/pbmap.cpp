@@ -13,6 +13,8 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <deque>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -482,7 +484,6 @@ int planes_launch(const PlaneBatch& B, int F, const PlaneGeom& G, hipStream_t st
     return launch_plane_publish(B, F, st);
 }
 
-int plane_ticket_wait(const std::shared_ptr<PlaneTicket>& tk);   // plane_queue.cpp
 
 // GPU part of getPlanes: cloud, filter, normals, segmentation — enqueued on the frame's ctx stream, or submitted to
 // the ctx's plane queue (batched with other frames on the queue's stream)
@@ -585,46 +586,148 @@ extern "C" int r360_frames_build(r360_frame* const* frames, int n, unsigned flag
     return 0;
 }
 
-// the per-plane host work of the frame runs on its own thread as soon as the GPU part is done, overlapping other
-// frames' kernels and the caller
+// Host PbMap assembly (A8 + A9: planes_assemble) of the frames whose plane stage is on the GPU, by a persistent pool
+// (round 6; a thread per frame before).  One watcher thread sweeps the pending frames in submission order every ~50 us:
+// a frame is ready once its plane-queue ticket says its batch is enqueued and its `done` event has completed.  Ready
+// frames go to R360_ASM_WORKERS worker threads that sleep on a condition variable.  The per-frame threads each polled
+// their event (5 / 20 / 100 us sleeps over the several milliseconds a batched plane stage takes: ~100 wake-ups and
+// event queries per frame) and were created and joined per frame; the bench counted 2.04 host cores in them at 1603
+// pairs/s.  The pool is created on first use and lives until the process exits.
+namespace {
+constexpr int R360_ASM_WORKERS = 4;
+
+struct AsmPool {
+    std::mutex m;
+    std::condition_variable cv_watch, cv_work, cv_done;
+    std::deque<r360_frame*> pending, ready;
+    std::vector<std::thread> th;   // never joined: the pool outlives every frame (the process's lifetime)
+    long assembled = 0;
+};
+
+void asm_finish(AsmPool& A, r360_frame* f, int rc, const std::string& err) {   // under A.m
+    f->pl.worker_rc = rc;
+    f->pl.worker_err = err;
+    f->pl.asm_busy = false;
+    ++A.assembled;
+}
+
+void asm_worker(AsmPool* A) {
+    for (;;) {
+        r360_frame* f;
+        {
+            std::unique_lock<std::mutex> lk(A->m);
+            A->cv_work.wait(lk, [&] { return !A->ready.empty(); });
+            f = A->ready.front();
+            A->ready.pop_front();
+        }
+        const auto a0 = std::chrono::steady_clock::now();
+        const int rc = planes_assemble(f);
+        const std::string err = rc ? std::string(r360_last_error()) : std::string();
+        const long ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - a0).count();
+        {
+            std::lock_guard<std::mutex> lk(A->m);
+            f->ctx->host_ns[4] += ns;
+            f->ctx->host_ns[5] += 1;
+            asm_finish(*A, f, rc, err);
+        }
+        A->cv_done.notify_all();
+    }
+}
+
+// 1: the frame's GPU part is complete, 0: not yet, -1: it failed (err)
+int asm_poll(r360_frame* f, std::string& err) {
+    PlaneBufs& P = f->pl;
+    if (P.ticket) {
+        const int t = plane_ticket_poll(P.ticket, &err);   // the plane queue has not recorded `done` before this
+        if (t <= 0) {
+            if (t < 0) err = "plane build: " + err;
+            return t;
+        }
+    }
+    const hipError_t r = hipEventQuery(P.done);
+    if (r == hipSuccess) return 1;
+    if (r == hipErrorNotReady) return 0;
+    err = "plane build: GPU work failed";
+    return -1;
+}
+
+void asm_watcher(AsmPool* A) {
+    std::vector<r360_frame*> snap;
+    std::vector<std::pair<r360_frame*, int>> fin;
+    std::vector<std::string> errs;
+    for (;;) {
+        {
+            std::unique_lock<std::mutex> lk(A->m);
+            A->cv_watch.wait(lk, [&] { return !A->pending.empty(); });
+            snap.assign(A->pending.begin(), A->pending.end());
+        }
+        fin.clear();
+        errs.clear();
+        for (r360_frame* f : snap) {
+            std::string err;
+            const int st = asm_poll(f, err);
+            if (st != 0) {
+                fin.push_back({f, st});
+                errs.push_back(err);
+            }
+        }
+        if (fin.empty()) {
+            std::this_thread::sleep_for(std::chrono::microseconds(50));
+            continue;
+        }
+        bool failed = false;
+        {
+            std::lock_guard<std::mutex> lk(A->m);
+            for (size_t k = 0; k < fin.size(); ++k) {
+                A->pending.erase(std::find(A->pending.begin(), A->pending.end(), fin[k].first));
+                if (fin[k].second > 0) {
+                    A->ready.push_back(fin[k].first);
+                } else {
+                    asm_finish(*A, fin[k].first, -1, errs[k]);
+                    failed = true;
+                }
+            }
+        }
+        A->cv_work.notify_all();
+        if (failed) A->cv_done.notify_all();
+    }
+}
+
+AsmPool& asm_pool() {
+    static AsmPool* A = [] {
+        auto* p = new AsmPool;
+        p->th.emplace_back(asm_watcher, p);
+        for (int k = 0; k < R360_ASM_WORKERS; ++k) p->th.emplace_back(asm_worker, p);
+        return p;
+    }();
+    return *A;
+}
+}  // namespace
+
+// the frame's host assembly, queued behind its GPU part (the caller has joined any earlier one: planes_enqueue)
 int planes_spawn_assembly(r360_frame* f) {
     PlaneBufs& P = f->pl;
     delete f->pbmap;
     f->pbmap = nullptr;
-    P.worker_rc = 0;
-    P.worker_err.clear();
-    P.worker = new std::thread([f] {
-        PlaneBufs& Q = f->pl;
-        if (Q.ticket && plane_ticket_wait(Q.ticket) != 0) {   // plane queue: wait until `done` is recorded
-            Q.worker_rc = -1;
-            Q.worker_err = std::string("plane build: ") + r360_last_error();
-            return;
-        }
-        if (event_wait(Q.done) != 0) {
-            Q.worker_rc = -1;
-            Q.worker_err = "plane build: GPU work failed";
-            return;
-        }
-        const auto a0 = std::chrono::steady_clock::now();
-        Q.worker_rc = planes_assemble(f);
-        if (Q.worker_rc) Q.worker_err = r360_last_error();
-        f->ctx->host_ns[4] += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - a0).count();
-        f->ctx->host_ns[5] += 1;
-    });
+    AsmPool& A = asm_pool();
+    {
+        std::lock_guard<std::mutex> lk(A.m);
+        P.worker_rc = 0;
+        P.worker_err.clear();
+        P.asm_busy = true;
+        A.pending.push_back(f);
+    }
+    A.cv_watch.notify_one();
     return 0;
 }
 
+// waits until the frame's queued assembly (if any) has finished; any number of threads may wait for one frame
 void planes_join(r360_frame* f) {
-    // A frame's planes may be awaited from two host threads at once (the frame where one pipeline's run ends and
-    // the next one's starts, registered by both): the join is serialised per frame (striped by address).
-    static std::mutex stripes[64];
-    std::lock_guard<std::mutex> lk(stripes[(reinterpret_cast<uintptr_t>(f) >> 6) & 63]);
     PlaneBufs& P = f->pl;
-    if (P.worker) {
-        P.worker->join();
-        delete P.worker;
-        P.worker = nullptr;
-    }
+    if (!P.cloud) return;   // never built planes: nothing was queued
+    AsmPool& A = asm_pool();
+    std::unique_lock<std::mutex> lk(A.m);
+    A.cv_done.wait(lk, [&] { return !P.asm_busy; });
 }
 
 // Host part of getPlanes: waits for the assembly thread
@@ -647,8 +750,6 @@ int planes_assemble(r360_frame* f) {
     auto us = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
         return std::chrono::duration<double, std::micro>(b - a).count();
     };
-    const auto t0 = now();
-    const auto t1 = now();
     const int err = P.h_nmodels[8];
     if (err) {
         r360_set_error("plane segmentation capacity exceeded (code %d: 1 bilateral depth range, 2 labels, 4 models, "
@@ -662,6 +763,15 @@ int planes_assemble(r360_frame* f) {
     const r360_calib* cal = f->calib;
     std::vector<std::vector<HPlane>> local(8);
     std::vector<char> keep;
+    // R360_PBMAP_PROFILE (experiment builds): per-phase times (us) and sizes of this frame's assembly
+    double tp_pre = 0, tp_hull = 0, tp_desc = 0, tp_local = 0;
+    long np_in = 0, np_kept = 0, np_hull = 0, n_models = 0, n_vox = 0;
+    auto tick = [&](double& acc, std::chrono::steady_clock::time_point& t) {
+        if (!prof) return;
+        const auto u = now();
+        acc += us(t, u);
+        t = u;
+    };
     for (int s = 0; s < 8; ++s) {
         const float* Rt = cal->rt[s];
         for (int m = 0; m < P.h_nmodels[s]; ++m) {
@@ -675,6 +785,8 @@ int planes_assemble(r360_frame* f) {
             pl.st = O.stats;
             std::vector<P3> pts;
             const int ax = axis_of(pl.normal), ha = (ax + 1) % 3, hb = (ax + 2) % 3;
+            auto tq = prof ? now() : t2;
+            if (prof) { ++n_models; np_in += O.n_contour > 0 ? O.n_contour : O.n_vox; n_vox += O.n_contour > 0 ? 0 : O.n_vox; }
             if (O.n_contour > 0) {
                 const float4* c = contour + O.contour_off;
                 auto get = [c](int k) { return P3{c[k].x, c[k].y, c[k].z}; };
@@ -692,11 +804,15 @@ int planes_assemble(r360_frame* f) {
                 std::sort(v.begin(), v.end(), [](const VoxOut& a, const VoxOut& b) { return a.key < b.key; });
                 for (const VoxOut& q : v) pts.push_back({q.x, q.y, q.z});
             }
+            tick(tp_pre, tq);
             convex_hull(pl, pts);
+            if (prof) { np_kept += (long)pts.size(); np_hull += (long)pl.hull.size(); }
+            tick(tp_hull, tq);
             area_and_center(pl);
             if (pl.area < kMinArea) continue;                           // :1034
             pl.d = -dot(pl.normal, pl.center);                          // :1037
             descriptors(pl);
+            tick(tp_desc, tq);
             if (pl.elongation > kMaxElongation) continue;               // :1041
             pl.normal = linear(Rt, pl.normal);                          // transform(Rt) :1051
             pl.center = affine(Rt, pl.center);
@@ -714,6 +830,7 @@ int planes_assemble(r360_frame* f) {
                 pl.id = int(local[s].size());
                 local[s].push_back(pl);
             }
+            tick(tp_local, tq);
         }
     }
     const auto t3 = now();
@@ -748,6 +865,7 @@ int planes_assemble(r360_frame* f) {
         prev = next;
         if (s == 6) prev.insert(first.begin(), first.end());
     }
+    const auto t4 = now();
     // mergePlanes (:657-739)
     for (size_t j = 0; j < G.size(); j++) {
         if (!(G[j].curvature < kMaxCurvature)) continue;
@@ -767,9 +885,11 @@ int planes_assemble(r360_frame* f) {
     }
     f->pbmap = pm;
     if (prof)
-        fprintf(stderr, "[pbmap] gpu wait %.0f us, pools %ld+%ld pts (voxel table %ld cells, bound %ld) D2H %.0f us, "
-                "descriptors %.0f us, group/merge %.0f us\n", us(t0, t1), totals[0], totals[1], totals[2] + 1, totals[3],
-                us(t1, t2), us(t2, t3), us(t3, now()));
+        fprintf(stderr, "[pbmap] pools %ld+%ld pts (voxel table %ld cells, bound %ld) | sensors %.0f us: prefilter %.0f, "
+                "hull %.0f, area+desc %.0f, local merges %.0f | groupPlanes %.0f us, mergePlanes %.0f us | models %ld, "
+                "points %ld (voxels %ld) -> %ld kept -> %ld hull vertices, planes %zu\n", totals[0], totals[1],
+                totals[2] + 1, totals[3], us(t2, t3), tp_pre, tp_hull, tp_desc, tp_local, us(t3, t4), us(t4, now()),
+                n_models, np_in, n_vox, np_kept, np_hull, G.size());
     return 0;
 }
 
@@ -871,8 +991,11 @@ struct Tree {
     const Tables* tb = nullptr;
     std::vector<double> area;
     int W = 1;                            // 64-bit words per target set
-    std::vector<uint64_t> fc;             // [(k * nt + l) * ns + i][W]: targets t of reference i consistent with k -> l
-    std::vector<uint8_t> fc_done;         // [(k * nt + l)]: fc rows computed (on first use)
+    // forward-check rows, built on first use: fc_at[k * nt + l] = offset in fc of the row of assignment k -> l, whose
+    // [i][W] words are the targets t of reference i consistent with it.  A search visits a small part of the ns x nt
+    // assignments, so rows are appended as they are needed (an eager ns * nt * ns * W table was 256 MB at 200 planes)
+    std::vector<uint64_t> fc;
+    std::vector<uint32_t> fc_at;
     std::vector<uint64_t> dom;            // [depth][ns][W] domains at each depth
     std::vector<int> cur, best;
     int ns = 0, nt = 0, n_cur = 0, n_best = 0;
@@ -882,8 +1005,8 @@ struct Tree {
     void init() {
         ns = tb->ns; nt = tb->nt;
         W = std::max(1, (nt + 63) / 64);
-        fc.assign((size_t)ns * nt * ns * W, 0);
-        fc_done.assign((size_t)ns * nt, 0);
+        fc.clear();
+        fc_at.assign((size_t)ns * nt, UINT32_MAX);
         dom.assign((size_t)(ns + 1) * ns * W, 0);
         for (int i = 0; i < ns; ++i)
             for (int t = 0; t < nt; ++t)
@@ -891,15 +1014,18 @@ struct Tree {
         cur.assign(ns, -1);
         best.assign(ns, -1);
     }
+    // (the pointer is valid until the next fc_row call: go() reads it before recursing)
     const uint64_t* fc_row(int k, int l) {
-        uint64_t* r = &fc[(size_t)(k * nt + l) * ns * W];
-        if (!fc_done[(size_t)k * nt + l]) {
+        uint32_t& at = fc_at[(size_t)k * nt + l];
+        if (at == UINT32_MAX) {
+            at = (uint32_t)fc.size();
+            fc.resize(fc.size() + (size_t)ns * W, 0);
+            uint64_t* r = &fc[at];
             for (int i = k + 1; i < ns; ++i)
                 for (int t = 0; t < nt; ++t)
                     if (t != l && tb->pair_ok(i, t, k, l)) r[(size_t)i * W + t / 64] |= 1ull << (t % 64);
-            fc_done[(size_t)k * nt + l] = 1;
         }
-        return r;
+        return &fc[at];
     }
     void go(int i) {
         if (++nodes > budget) { truncated = true; return; }
@@ -1032,6 +1158,8 @@ int ready(r360_frame* f) {
 extern "C" int r360_match_tree_search(int ns, int nt, const uint8_t* unary, const uint64_t* binary, int words,
                                       const double* area, long max_nodes, int* best, long* nodes) {
     CHECK_ARG(ns >= 0 && nt >= 0 && (ns == 0 || (unary && area && best)) && max_nodes > 0, "bad arguments");
+    // the tables' index arithmetic is 32-bit (ns * nt pairs, each a row of ns * nt bits)
+    CHECK_ARG(ns <= 1024 && nt <= 1024, "at most 1024 reference and 1024 target planes");
     CHECK_ARG(words == (ns * nt + 63) / 64 && (ns * nt == 0 || binary), "binary table: words != ceil(ns * nt / 64)");
     Tables tb;
     tb.ns = ns; tb.nt = nt; tb.words = words;

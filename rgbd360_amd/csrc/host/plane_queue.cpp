@@ -9,7 +9,7 @@
 // frames), so a batch of F frames costs one chain of launches and its one-workgroup-per-sensor kernels run F x 8
 // workgroups side by side.  The queue has two streams, each with a hardware queue of its own (CU-masked streams): a
 // batch goes to the stream whose previous batch has finished, so the latency-bound chains of two batches overlap.
-// Each frame keeps its own buffers and host assembly thread; its results equal its lone build's bit for bit (the
+// Each frame keeps its own buffers and host assembly; its results equal its lone build's bit for bit (the
 // kernels are the same and every frame's arithmetic is independent of the others').
 #include <chrono>
 #include <condition_variable>
@@ -226,7 +226,7 @@ int plane_queue_stats(const r360_plane_queue* q, long* batches, long* frames, in
 }
 
 // The frame's inputs (upload, undistort) are enqueued on its own stream: its ready event marks their end, and the
-// queue's stream waits on it.  The frame's ticket tells its assembly thread when `done` has been recorded.
+// queue's stream waits on it.  The frame's ticket tells the assembly pool when `done` has been recorded.
 int plane_queue_submit(r360_plane_queue* q, r360_frame* f) {
     CHECK_ARG(q && f, "null arg");
     PlaneBufs& P = f->pl;
@@ -241,10 +241,13 @@ int plane_queue_submit(r360_plane_queue* q, r360_frame* f) {
     return 0;
 }
 
-// Waits until the frame's batch is enqueued (its `done` event recorded); returns the dispatcher's rc.
-int plane_ticket_wait(const std::shared_ptr<PlaneTicket>& tk) {
-    std::unique_lock<std::mutex> lk(tk->m);
-    tk->cv.wait(lk, [&] { return tk->enqueued; });
-    if (tk->rc) r360_set_error("%s", tk->err.c_str());
-    return tk->rc;
+// the frame's batch state for the host assembly pool (host/pbmap.cpp): whether `done` has been recorded
+int plane_ticket_poll(const std::shared_ptr<PlaneTicket>& tk, std::string* err) {
+    std::lock_guard<std::mutex> lk(tk->m);
+    if (!tk->enqueued) return 0;
+    if (tk->rc) {
+        if (err) *err = tk->err;
+        return -1;
+    }
+    return 1;
 }

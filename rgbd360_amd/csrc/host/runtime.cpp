@@ -107,25 +107,36 @@ int ctx_wait(r360_ctx* ctx) {
 }
 
 // A lone alignment's result wait.  The previous alignment on the ctx took align_est seconds from its enqueue: until
-// 90 % of that has passed the wait checks every 50 us, then every ~2 us until 3x, then as event_wait (whose 20 us
-// polls by then came ~10 us late on average).  A wrong estimate (another frame size) costs at most one coarse check.
-static int align_wait(r360_ctx* ctx) {
+// 90 % of that has passed the wait checks every 50 us, then every ~2 us for at most 200 us, then as event_wait (whose
+// 20 us polls by then came ~10 us late on average).  A wrong estimate (another frame size) costs at most one coarse
+// check.  *waited: the alignment was still running at the first check, so the time to the end of this wait measures
+// the alignment; a result call that came after it had finished says nothing about its duration (a late
+// caller inflated the next estimate and with it the fine-poll window).
+static int align_wait(r360_ctx* ctx, bool* waited) {
     R360_HIP(hipEventRecord(ctx->wait_ev, ctx->stream));
+    *waited = false;
+    const hipError_t r0 = hipEventQuery(ctx->wait_ev);
+    if (r0 == hipSuccess) return 0;
+    if (r0 != hipErrorNotReady) {
+        r360_set_error("hipEventQuery -> %s", hipGetErrorString(r0));
+        return -1;
+    }
+    *waited = true;
     const double est = ctx->align_est;
     if (est > 0 && est < 0.05) {
         Slack slack;
-        const double t_fine = ctx->align_t0 + 0.9 * est, t_end = ctx->align_t0 + 3 * est;
+        const double t_fine = ctx->align_t0 + 0.9 * est, t_end = t_fine + std::min(2.1 * est, 200e-6);
         for (;;) {
+            const double t = now_s();
+            if (t > t_end) break;
+            const double left = t_fine - t;
+            std::this_thread::sleep_for(std::chrono::microseconds(left > 50e-6 ? 50 : left > 2e-6 ? (long)(left * 1e6) : 2));
             const hipError_t r = hipEventQuery(ctx->wait_ev);
             if (r == hipSuccess) return 0;
             if (r != hipErrorNotReady) {
                 r360_set_error("hipEventQuery -> %s", hipGetErrorString(r));
                 return -1;
             }
-            const double t = now_s();
-            if (t > t_end) break;
-            const double left = t_fine - t;
-            std::this_thread::sleep_for(std::chrono::microseconds(left > 50e-6 ? 50 : left > 2e-6 ? (long)(left * 1e6) : 2));
         }
     }
     return event_wait(ctx->wait_ev);
@@ -1067,8 +1078,9 @@ extern "C" int r360_align360_result(r360_ctx* ctx, float pose_out[16], float H_o
     CHECK_ARG(ctx && ctx->async_pending, "no alignment pending");
     IcpState* h = ctx->h_state;
     R360_HIP(hipMemcpyAsync(h, ctx->d_state, sizeof(IcpState), hipMemcpyDeviceToHost, ctx->stream));
-    const int wrc = align_wait(ctx);
-    if (wrc == 0) ctx->align_est = now_s() - ctx->align_t0;   // the next alignment's wait plan
+    bool waited = false;
+    const int wrc = align_wait(ctx, &waited);
+    if (wrc == 0 && waited) ctx->align_est = now_s() - ctx->align_t0;   // the next alignment's wait plan
     persist_release(ctx);
     if (wrc) return -1;
     ctx->async_pending = 0;

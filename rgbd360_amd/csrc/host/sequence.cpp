@@ -18,7 +18,10 @@
 // issued right after a build on the same stream.  A ring buffer is refilled only after every pair that used its
 // previous frame was collected (the dense queue refuses a job whose frame was rebuilt meanwhile).
 //
-// Every record equals the single-pair Register() result (batched alignments are bit-identical to lone ones).
+// Records are batch-invariant: a pair's record is bit-identical however the pairs are cut into pieces, pipelines,
+// dense batches and ranks (the batched ICP grid depends on the level size only).  Against an unqueued run (each
+// pair a lone Register() on its pipeline's context) the PbMap stage is identical and the dense pose equal to
+// rounding (lone passes use two workgroups per CU).
 #include <array>
 #include <chrono>
 #include <cmath>
@@ -237,40 +240,56 @@ void pipeline_queued(r360_sequence* s, int p) {
     };
 
     const int last = T - 1;
-    for (int t = 0; t < std::min(LA, last + 1); ++t) {   // positions 0 .. LA-1 built, position LA uploaded
-        load(t);
-        build(t);
-    }
-    if (LA <= last) load(LA);
-    const int depth = nbuf - LA - 2;
-    for (int t = 0; t < last; ++t) {
-        const double t0 = now_s();
-        // position t + LA + 1 refills the buffer of position u = t + LA + 1 - nbuf: collect the pairs that used it
-        while (!pending.empty() && pending.front().t <= t + LA + 1 - nbuf) finish_front();
-        hs[6] += now_s() - t0;
-        r360_frame* cur = buf(t);
-        r360_frame* nxt = buf(t + 1);
-        if (t + LA <= last) build(t + LA);                  // its upload was issued one iteration earlier
-        if (t + LA + 1 <= last) load(t + LA + 1);
-        const double t1 = now_s();
-        if (!X.pair[t]) {                                   // the last frame of a segment: no pair
-            hs[0] += t1 - t0;
-            continue;
+    // A failed step leaves no ticket behind: every pending job is collected (its result, or error, dropped) before
+    // the failure propagates, so the dense queue holds no job that reads this pipeline's frames once the run returns
+    // (a later run refills them, r360_sequence_destroy frees them) and none of its job entries leak.
+    try {
+        for (int t = 0; t < std::min(LA, last + 1); ++t) {   // positions 0 .. LA-1 built, position LA uploaded
+            load(t);
+            build(t);
         }
-        long ticket = 0;
-        if (wl == R360_SEQ_DENSE)
-            req_rc(r360_dense_queue_submit(s->q, cur, nxt, kEye, R360_PHOTO_DEPTH, &s->prm.icp, &ticket));
-        else
-            req_rc(r360_register_submit(ctx, s->q, cur, nxt, kEye, &s->prm.icp, s->prm.max_match_planes, s->prm.mode,
-                                        &ticket));
+        if (LA <= last) load(LA);
+        const int depth = nbuf - LA - 2;
+        for (int t = 0; t < last; ++t) {
+            const double t0 = now_s();
+            // position t + LA + 1 refills the buffer of position u = t + LA + 1 - nbuf: collect the pairs that used it
+            while (!pending.empty() && pending.front().t <= t + LA + 1 - nbuf) finish_front();
+            hs[6] += now_s() - t0;
+            r360_frame* cur = buf(t);
+            r360_frame* nxt = buf(t + 1);
+            if (t + LA <= last) build(t + LA);                  // its upload was issued one iteration earlier
+            if (t + LA + 1 <= last) load(t + LA + 1);
+            const double t1 = now_s();
+            if (!X.pair[t]) {                                   // the last frame of a segment: no pair
+                hs[0] += t1 - t0;
+                continue;
+            }
+            long ticket = 0;
+            if (wl == R360_SEQ_DENSE)
+                req_rc(r360_dense_queue_submit(s->q, cur, nxt, kEye, R360_PHOTO_DEPTH, &s->prm.icp, &ticket));
+            else
+                req_rc(r360_register_submit(ctx, s->q, cur, nxt, kEye, &s->prm.icp, s->prm.max_match_planes, s->prm.mode,
+                                            &ticket));
+            const double t2 = now_s();
+            pending.push_back(Pending{ticket, t, r360_icp_stats{}});
+            if ((int)pending.size() > depth) finish_front();
+            hs[0] += t1 - t0; hs[1] += t2 - t1; hs[2] += now_s() - t2; hs[3] += 1;
+        }
         const double t2 = now_s();
-        pending.push_back(Pending{ticket, t, r360_icp_stats{}});
-        if ((int)pending.size() > depth) finish_front();
-        hs[0] += t1 - t0; hs[1] += t2 - t1; hs[2] += now_s() - t2; hs[3] += 1;
+        while (!pending.empty()) finish_front();
+        hs[2] += now_s() - t2;
+    } catch (...) {
+        const std::string why = r360_last_error();
+        for (const Pending& pd : pending) {
+            float pose[16], info[36];
+            r360_icp_stats st{};
+            if (wl == R360_SEQ_DENSE) (void)r360_dense_queue_collect(s->q, pd.ticket, pose, nullptr, nullptr, &st);
+            else (void)r360_register_collect(s->q, pd.ticket, pose, info, &st);
+        }
+        pending.clear();
+        r360_set_error("%s", why.c_str());   // the first failure, not a drained job's
+        throw;
     }
-    const double t2 = now_s();
-    while (!pending.empty()) finish_front();
-    hs[2] += now_s() - t2;
 }
 
 void worker(r360_sequence* s, int p) {
@@ -450,11 +469,15 @@ extern "C" void r360_sequence_destroy(r360_sequence* s) {
     }
     s->cv_go.notify_all();
     for (auto& t : s->th) t.join();
-    for (auto& r : s->ring)
-        for (r360_frame* f : r) r360_frame_destroy(f);
-    for (r360_calib* k : s->cal) r360_calib_destroy(k);
-    if (s->pq) plane_queue_destroy(s->pq);
+    // the queues first: their dispatchers drain what is still queued, which reads the ring frames
     if (s->q) r360_dense_queue_destroy(s->q);
+    if (s->pq) plane_queue_destroy(s->pq);
+    for (auto& r : s->ring)
+        for (r360_frame* f : r) {
+            planes_join(f);
+            r360_frame_destroy(f);
+        }
+    for (r360_calib* k : s->cal) r360_calib_destroy(k);
     for (r360_ctx* c : s->ctx) r360_ctx_destroy(c);
     delete s;
 }

@@ -265,7 +265,7 @@ struct PlaneBufs {
     hipEvent_t done = nullptr;
     hipEvent_t ready = nullptr;      // plane queue: recorded on the frame's stream once its inputs are built
     std::shared_ptr<struct PlaneTicket> ticket;   // plane queue: set when the batch's kernels and `done` are enqueued
-    std::thread* worker = nullptr;
+    bool asm_busy = false;           // the host assembly is queued or running (host/pbmap.cpp AsmPool; under its lock)
     int worker_rc = 0;
     std::string worker_err;
 };
@@ -554,6 +554,8 @@ int plane_queue_stats(const r360_plane_queue* q, long* batches, long* frames, in
 r360_ctx* plane_queue_ctx(r360_plane_queue* q);
 int ctx_vhash_reserve(r360_ctx* ctx, long min_cells, long list_entries, long list_groups);
 int planes_finish(r360_frame* f);
+// plane queue ticket: 1 the frame's batch and `done` event are enqueued, 0 not yet, -1 the batch failed (*err)
+int plane_ticket_poll(const std::shared_ptr<struct PlaneTicket>& tk, std::string* err);
 // rotOffset (157.5 deg about x, OdometryRGBD360.cpp:138-139) and its inverse; column-major 4x4 product C = A*B
 void r360_rot_offset(float Ro[16], float Ri[16]);
 void r360_mul4(const float* A, const float* B, float* C);

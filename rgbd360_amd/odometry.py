@@ -125,8 +125,9 @@ class SequenceRunner:
 
     queue > 0: the pipelines' alignFrames360 calls go to one dense queue (r360_dense_queue, batches of up to
     `queue` pairs per launch); each pipeline keeps `depth` alignments in flight while it builds (`lookahead` frames
-    ahead) and PbMap-registers the next frames.  Every record is identical to the unqueued run's (a batched alignment
-    equals the single-pair one bit for bit).
+    ahead) and PbMap-registers the next frames.  Records are batch-invariant (bit-identical for any cut into pipelines,
+    batches and ranks); against the unqueued run (lone alignments, two workgroups per CU) the PbMap stage is identical
+    and the poses equal to rounding (tests/test_gpu_sequence.py).
 
     Attributes mirror the pipelines: ctxs / cals / frames (non-owning views of each pipeline's context, calibration
     and frame ring), queue (the dense queue's view, or None), host_s ([P, 4] host seconds: load + build enqueue,
@@ -186,7 +187,9 @@ class SequenceRunner:
         keep = []
         for k in range(n):
             b, d = frames_of(p0 + k)
-            if device_inputs:
+            if b is None or d is None:   # null image pointers: the library fails the run (failure-path tests)
+                bgr[k], dep[k] = None, None
+            elif device_inputs:
                 bgr[k], dep[k] = int(b), int(d)
             else:
                 assert b.dtype == np.uint8 and d.dtype == np.uint16 and b.flags.c_contiguous and d.flags.c_contiguous

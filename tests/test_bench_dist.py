@@ -177,29 +177,35 @@ def _main_worker(rank, world, port, out_dir):
         f.write(buf.getvalue())
 
 
-def test_bench_main_two_ranks(tmp_path):
-    """bench.main itself at world size 2 over gloo (R360_BENCH_REHEARSAL: records gathered by gloo instead of the
+@pytest.mark.parametrize("world", [2, 8])
+def test_bench_main_multi_rank(tmp_path, world):
+    """bench.main itself at world size 2 and 8 over gloo (R360_BENCH_REHEARSAL: records gathered by gloo instead of the
     library's RCCL communicator), with a CPU stand-in for the GPU pipelines: each rank registers only its shard,
     rank 0 gathers every rank's records, composes the whole trajectory and prints the one JSON line with the
-    whole-job pair count; the other rank prints nothing."""
+    whole-job pair count; the other ranks print nothing.  World size 8 is the driver's 8-GPU node (one process per
+    GPU, 8 shards of the 23 pairs of the 24-frame test sequence)."""
     import json
-    world = 2
     mp.spawn(_main_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
-    assert (tmp_path / "out1.txt").read_text() == ""
+    for r in range(1, world):
+        assert (tmp_path / f"out{r}.txt").read_text() == ""
     lines = (tmp_path / "out0.txt").read_text().strip().splitlines()
     assert len(lines) == 1
     out = json.loads(lines[0])
-    assert out["n_gpus"] == 2 and out["steps"] == 2 and out["scaling"] == "strong"
-    assert out["config"]["parallelism"] == "pair-shard dp2"
-    assert out["config"]["pairs_per_step"] == 23 and out["config"]["pairs_per_step_this_rank"] == 12
+    sizes = [OD.shard_pairs(r, world, 24)[1] - OD.shard_pairs(r, world, 24)[0] for r in range(world)]
+    assert sum(sizes) == 23 and max(sizes) - min(sizes) <= 1
+    assert out["n_gpus"] == world and out["steps"] == 2 and out["scaling"] == "strong"
+    assert out["config"]["parallelism"] == f"pair-shard dp{world}"
+    assert out["config"]["pairs_per_step"] == 23 and out["config"]["pairs_per_step_this_rank"] == sizes[0]
+    assert out["records_identical"] is True
     tr = out["trajectory"]
     assert tr["pairs"] == 23 and tr["frames"] == 24
     # every pair composed once, in order (the floor: f32 records, arccos of a trace within 1e-7 of 3)
     assert tr["max_rot_err_deg"] < 0.05 and tr["max_trans_err_m"] < 1e-5
-    assert tr["pbmap_failed"] == 11 and tr["illposed"] == 0                  # status = rank: rank 1's 11 pairs arrived
+    # status = rank: rank 1's pairs count as PbMap failures, rank 2's as ill-posed
+    assert tr["pbmap_failed"] == sizes[1] and tr["illposed"] == (sizes[2] if world > 2 else 0)
     assert out["value"] > 0 and abs(out["value"] - 46 / (out["ms_per_step"] * 2e-3)) < 1e-6 * out["value"]
     # per-rank diagnostics of the N > 1 line: shard sizes, rates, the gather's time, halo frames
     pr = out["per_rank"]
-    assert [r["rank"] for r in pr] == [0, 1] and [r["pairs_per_step"] for r in pr] == [12, 11]
+    assert [r["rank"] for r in pr] == list(range(world)) and [r["pairs_per_step"] for r in pr] == sizes
     assert all(r["pairs_per_s"] > 0 and r["gather_ms"] >= 0 and r["halo_frames_per_step"] >= 1 for r in pr)
     assert max(r["timed_s"] for r in pr) == pytest.approx(out["ms_per_step"] * 2e-3, rel=1e-5)

@@ -155,6 +155,45 @@ def test_unqueued_lone_alignments_match_the_records(seq):
         assert np.linalg.norm(a[:3, 3] - b[:3, 3]) <= 2e-4, i
 
 
+def test_bench_runner_mode_reproduces_the_records(seq):
+    """The mode the headline bench line runs in (bench.py defaults: 12 pipelines, dense queue batches of 16, 3
+    alignments in flight per pipeline, 1 frame built ahead, plane stages batched 8 frames per launch, runs=None: the
+    repeats x 255 registrations cut into 12 contiguous pieces that cross repeat boundaries): every repeat's records
+    equal the single-run records bit for bit, so no pair at a piece's repeat boundary takes a wrong frame buffer."""
+    bgr, dep = seq["bgr"], seq["dep"]
+    runner = OD.SequenceRunner(0, 480, 640, 12, seq["params"], queue=16, depth=3, lookahead=1, plane_batch=8)
+    try:
+        rec = np.zeros((3, 255, OD.REC), np.float32)
+        runner.run(0, 255, lambda i: (bgr[i], dep[i]), rec, repeats=3)
+        pieces = OD.stream_pieces(0, 255, 3, 12)
+    finally:
+        runner.close()
+    # the cut really crosses repeat boundaries (pieces with segments of two repeats)
+    assert sum(len(p) > 1 for p in pieces) >= 2
+    for r in range(3):
+        bad = np.nonzero((rec[r] != seq["rec"]).any(axis=1))[0]
+        assert len(bad) == 0, (r, bad[:16].tolist())
+
+
+def test_failed_pipeline_drains_its_tickets(seq):
+    """A pipeline step that fails (here: a frame with null image pointers) collects every alignment it still had in
+    flight before the run returns its error, so the dense queue holds no job over the pipeline's frames: the next run
+    on the same runner reproduces the records and destroying the runner afterwards is clean."""
+    bgr, dep = seq["bgr"], seq["dep"]
+    runner = OD.SequenceRunner(0, 480, 640, 4, seq["params"], queue=16, depth=3, lookahead=1)
+    try:
+        out = np.zeros((1, 40, OD.REC), np.float32)
+        with pytest.raises(RuntimeError, match="null arg"):
+            runner.run(0, 40, lambda i: (None, None) if i == 27 else (bgr[i], dep[i]), out)
+        q = runner.queue.stats()
+        rec = np.zeros((1, 40, OD.REC), np.float32)
+        runner.run(0, 40, lambda i: (bgr[i], dep[i]), rec)
+        assert runner.queue.stats()["jobs"] == q["jobs"] + 40
+        assert np.array_equal(rec[0], seq["rec"][:40])
+    finally:
+        runner.close()
+
+
 @pytest.mark.parametrize("depth,lookahead", [(3, 1), (2, 2)])
 def test_queued_repeats_as_one_stream(seq, depth, lookahead):
     """Queued pipelines run their repeats as one stream of frames (a repeat's first frame is built while the

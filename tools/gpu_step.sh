@@ -1,0 +1,40 @@
+#!/bin/bash
+# GPU box: one development step.  usage: tools/gpu_step.sh <tag> [stages...]
+#   tests  every -m gpu test            smoke   __graft_entry__.smoke()
+#   bench  the default bench line        quick   a short sequence-only bench line (no CPU / config-5 / halves legs)
+#   pbprof PbMap assembly phase profile (experiment build, R360_PBMAP_PROFILE) over a short sequence run
+#   c5     the config-5 leg alone (HiRes dense, 50 level-0 iterations)
+# results in gpurun_out/<tag>/; every GPU step under its own time limit, the first failure ends the script
+set -o pipefail
+TAG=${1:?tag}; shift
+R=${GRAFT_REPO_ROOT:-$(pwd)}; O=$R/gpurun_out/$TAG; mkdir -p $O
+cd $R
+Q="--no-cpu-baseline --no-resident --no-config5 --no-isolated --no-halves"
+for st in "$@"; do
+  case $st in
+    tests)
+      timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/gpu_tests.log 2>&1 \
+        || { tail -40 $O/gpu_tests.log; exit 1; }
+      tail -2 $O/gpu_tests.log ;;
+    smoke)
+      timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 2; }
+      tail -2 $O/smoke.log ;;
+    bench)
+      timeout -k 10 500 python -u bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 3; }
+      python3 tools/bench_line.py $O/bench.json ;;
+    quick)
+      timeout -k 10 200 python -u bench.py $Q > $O/quick.json 2> $O/quick.err || { tail -20 $O/quick.err; exit 4; }
+      python3 tools/bench_line.py $O/quick.json ;;
+    pbprof)
+      R360_LIB=$R/rgbd360_amd/lib/librgbd360_hip_exp.so R360_PBMAP_PROFILE=1 timeout -k 10 200 python -u bench.py $Q \
+        --steps 2 --warmup 1 > $O/pbprof.json 2> $O/pbprof.err || { tail -20 $O/pbprof.err; exit 5; }
+      grep -c '^\[pbmap\]' $O/pbprof.err; python3 tools/pbprof_summary.py $O/pbprof.err | tee $O/pbprof.txt ;;
+    c5)
+      timeout -k 10 300 python -u -c "
+import json, sys; sys.argv=['bench.py']; import numpy as np, bench, rgbd360_amd as R
+rt8 = np.stack([np.loadtxt(f'{R.EXTRINSICS_DIR}/Rt_0{k + 1}.txt', dtype=np.float32) for k in range(8)])
+print(json.dumps(bench.config5_leg(0, rt8)))" > $O/c5.json 2> $O/c5.err || { tail -20 $O/c5.err; exit 6; }
+      python3 -c "import json; d=json.load(open('$O/c5.json')); r=d['roofline']; print('config5', round(d['value'],1), 'pairs/s frac', round(r['frac'],3), 'L0', round(r['avg_launch_ms']*1e3,1), 'us/launch', round(r['pairs_per_launch'],2), 'pairs/launch')" ;;
+    *) echo "unknown stage $st"; exit 9 ;;
+  esac
+done
