@@ -602,7 +602,7 @@ def main(argv=None, runner_factory=None):
     mstats = np.sum([c.match_stats() for c in runner.ctxs], axis=0) if runner.ctxs else np.zeros(3)
     matcher = {"searches": int(mstats[0]), "budget_hits": int(mstats[1]),
                "max_nodes": int(max([c.match_stats()[2] for c in runner.ctxs] or [0]))}
-    l0_ms, l0_n, k0_us, k0_n, k0_jobs, stage = 0.0, 0, 0.0, 0, 0, {}
+    l0_ms, l0_n, k0_us, k0_n, k0_jobs, stage, coarse = 0.0, 0, 0.0, 0, 0, {}, {}
     qstats = None
     if runner.queue:   # batches of the timed run
         q1 = runner.queue.stats()
@@ -622,6 +622,12 @@ def main(argv=None, runner_factory=None):
         k0_us += us
         k0_n += n
         k0_jobs += nj
+        for lv in range(1, 5):   # the coarse levels (diagnostic): launches that ran a job, their in-kernel span
+            us, n, nj = c.kernel_stats(lv)
+            kc = coarse.setdefault(lv, [0.0, 0, 0])
+            kc[0] += us
+            kc[1] += n
+            kc[2] += nj
         for name in ("k_undistort", "k_stitch", "k_pyramid", "k_cloud", "k_bilateral", "k_distmap", "k_normals",
                      "k_ccl", "k_plane_fit", "k_refine", "k_model_stats", "k_icp_pass", "k_icp_pass_L0"):
             ms, n = c.timing_read(name)
@@ -810,6 +816,8 @@ def main(argv=None, runner_factory=None):
         },
         **({"stage_ms_per_pair": {k: v / max(args.steps * steps_pairs, 1) for k, v in stage.items()}}
            if args.stage_timing else {}),
+        "coarse_levels": {f"L{lv}": {"launches": v[1], "avg_launch_us": v[0] / max(v[1], 1), "pair_passes": v[2],
+                                     "ms_per_step": v[0] * 1e-3 / args.steps} for lv, v in sorted(coarse.items())},
         "pipeline_host_ms_per_pair": host_ms,
         "pbmap_matcher": matcher, "pbmap_budget_hits": matcher["budget_hits"],
         "runner": "C++ (r360_sequence, rgbd360_amd/csrc/host/sequence.cpp)",

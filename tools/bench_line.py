@@ -24,3 +24,6 @@ for k in ("config2", "config3", "sequential_cpp", "config1", "cpu_baseline"):
         print(k, {kk: (round(vv, 3) if isinstance(vv, float) else vv) for kk, vv in v.items()
                   if not isinstance(vv, (dict, list)) and kk not in ("workload", "sample", "note")})
 print("matcher", d.get("pbmap_matcher"), "dense_queue", d.get("dense_queue"), "plane_queue", d.get("plane_queue"))
+if d.get("coarse_levels"):
+    print("coarse", {k: (v["launches"], round(v["avg_launch_us"], 1), v["pair_passes"], round(v["ms_per_step"], 1))
+                     for k, v in d["coarse_levels"].items()}, "(launches, us, pair passes, ms/step)")

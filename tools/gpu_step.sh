@@ -35,6 +35,18 @@ import json, sys; sys.argv=['bench.py']; import numpy as np, bench, rgbd360_amd 
 rt8 = np.stack([np.loadtxt(f'{R.EXTRINSICS_DIR}/Rt_0{k + 1}.txt', dtype=np.float32) for k in range(8)])
 print(json.dumps(bench.config5_leg(0, rt8)))" > $O/c5.json 2> $O/c5.err || { tail -20 $O/c5.err; exit 6; }
       python3 -c "import json; d=json.load(open('$O/c5.json')); r=d['roofline']; print('config5', round(d['value'],1), 'pairs/s frac', round(r['frac'],3), 'L0', round(r['avg_launch_ms']*1e3,1), 'us/launch', round(r['pairs_per_launch'],2), 'pairs/launch')" ;;
+    pfab)   # level-0 pass forms / occupancy: dense-alone VGA and config 5, per experiment library:PF (PFAB="exp:6 minb4:7")
+      for spec in ${PFAB:-exp:6 minb4:7 minb4:6}; do
+        lib=${spec%%:*}; pf=${spec##*:}; n=${lib}_pf$pf
+        R360_LIB=$R/rgbd360_amd/lib/librgbd360_hip_$lib.so R360_ICP_PF=$pf timeout -k 10 200 python -u bench.py --workload dense \
+          $Q > $O/dense_$n.json 2> $O/dense_$n.err || { tail -20 $O/dense_$n.err; exit 7; }
+        echo "== $n dense"; python3 tools/bench_line.py $O/dense_$n.json | head -1
+        R360_LIB=$R/rgbd360_amd/lib/librgbd360_hip_$lib.so R360_ICP_PF=$pf timeout -k 10 300 python -u -c "
+import json, sys; sys.argv=['bench.py']; import numpy as np, bench, rgbd360_amd as R
+rt8 = np.stack([np.loadtxt(f'{R.EXTRINSICS_DIR}/Rt_0{k + 1}.txt', dtype=np.float32) for k in range(8)])
+print(json.dumps(bench.config5_leg(0, rt8)))" > $O/c5_$n.json 2> $O/c5_$n.err || { tail -20 $O/c5_$n.err; exit 8; }
+        python3 -c "import json; d=json.load(open('$O/c5_$n.json')); r=d['roofline']; print('config5', round(d['value'],1), 'pairs/s frac', round(r['frac'],3), 'L0', round(r['avg_launch_ms']*1e3,1), 'us/launch', round(r['pairs_per_launch'],2), 'pairs/launch')"
+      done ;;
     *) echo "unknown stage $st"; exit 9 ;;
   esac
 done
