@@ -110,6 +110,12 @@ int  r360_frame_dims(const r360_frame* f, int* rows, int* cols, int* sph_rows, i
 /* RegisterPhotoICP::setNumPyr (RegisterPhotoICP.h:224-227) for the frame: its pyramid stops at n levels (default:
  * the calibration's full depth).  Alignments of the frame then take nPyr <= n. */
 int  r360_frame_set_levels(r360_frame* f, int n);
+/* Source-point compaction of the frame's pyramid builds (no reference counterpart: a layout choice).  all = 1
+ * (default): every level's valid source pixels are compacted once per build, which a lone alignment's passes read
+ * (PF 5).  all = 0: only the levels a batched pass cannot stream as an image are compacted (two launches per build
+ * fewer, for frames that only enter batched alignments, e.g. a dense queue's); a lone alignment then streams the
+ * images too.  Poses are equal to rounding either way.  Takes effect at the next build. */
+int  r360_frame_set_compaction(r360_frame* f, int all);
 /* The R360_BUILD_* stages the frame's current images have been through (an upload or load clears them). */
 int  r360_frame_built(const r360_frame* f, unsigned* flags);
 /* sphereRGB (BGR u8) / sphereDepth (u16 range mm) (Frame360.h:104-107). */

@@ -184,6 +184,7 @@ _SIGS = [
     ("r360_frames_build", C.c_int, [_P, C.c_int, C.c_uint]),
     ("r360_frame_dims", C.c_int, [_P, _IP, _IP, _IP, _IP]),
     ("r360_frame_set_levels", C.c_int, [_P, C.c_int]),
+    ("r360_frame_set_compaction", C.c_int, [_P, C.c_int]),
     ("r360_frame_built", C.c_int, [_P, C.POINTER(C.c_uint)]),
     ("r360_frame_get_sphere", C.c_int, [_P, _P, _P]),
     ("r360_frame_get_depth_m", C.c_int, [_P, _P]),
@@ -522,6 +523,11 @@ class Frame360:
     def setNumPyr(self, n: int):
         """r360_frame_set_levels: the frame's pyramid stops at n levels (RegisterPhotoICP::setNumPyr)."""
         _check(lib().r360_frame_set_levels(self.h, int(n)), "r360_frame_set_levels")
+
+    def setCompaction(self, all_levels: bool):
+        """r360_frame_set_compaction: compact every level's source points at the next build (default), or only the
+        levels a batched pass cannot stream as an image."""
+        _check(lib().r360_frame_set_compaction(self.h, int(bool(all_levels))), "r360_frame_set_compaction")
 
     def loadFrame(self, path: str):
         _check(lib().r360_frame_load_bin(self.h, path.encode()), "loadFrame")

@@ -786,6 +786,12 @@ extern "C" int r360_frame_set_levels(r360_frame* f, int n) {
     return 0;
 }
 
+extern "C" int r360_frame_set_compaction(r360_frame* f, int all) {
+    CHECK_ARG(f, "null frame");
+    f->compact_all = all != 0;
+    return 0;
+}
+
 extern "C" int r360_frame_dims(const r360_frame* f, int* rows, int* cols, int* sph_rows, int* sph_cols) {
     CHECK_ARG(f, "null frame");
     if (rows) *rows = f->rows;
@@ -853,9 +859,9 @@ extern "C" int r360_frame_get_points(r360_frame* f, int level, float* xyzg, int 
     CHECK_ARG(f && n, "null arg");
     CHECK_ARG(level >= 0 && level < f->n_levels, "level out of range");
     CHECK_ARG(f->built & R360_BUILD_PYRAMID, "pyramid not built");
-    if (level == 0 && !f->lv0_compacted) {   // level 0 streams its packed image; compact it on request
-        if (int rc = launch_src_compaction(f, 0, 1)) return rc;
-        f->lv0_compacted = true;
+    if (!((f->compacted >> level) & 1u)) {   // a level batched passes stream as an image: compacted on request
+        if (int rc = launch_src_compaction(f, 1u << level)) return rc;
+        f->compacted |= 1u << level;
     }
     int np = 0;
     R360_HIP(hipMemcpyAsync(&np, f->d_npts + level, sizeof(int), hipMemcpyDeviceToHost, f->ctx->stream));

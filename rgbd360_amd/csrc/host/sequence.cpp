@@ -408,8 +408,8 @@ extern "C" int r360_sequence_create(int device, const r360_sequence_params* prm,
             r360_frame* f = nullptr;
             if (r360_frame_create(c, k, &f)) return fail();
             s->ring.back().push_back(f);
-            // queued alignments are batched (PF 6 streams the packed level 0): no compacted level-0 points
-            if (s->q) f->compact0 = false;
+            // queued alignments are batched (PF 6 / PF 8 stream the images): no compacted source points
+            if (s->q) f->compact_all = false;
             // the pyramid the alignments use (setNumPyr): deeper levels would be built for nothing
             if (s->prm.workload != R360_SEQ_PLANES && s->prm.icp.n_pyr < f->n_levels &&
                 r360_frame_set_levels(f, s->prm.icp.n_pyr))

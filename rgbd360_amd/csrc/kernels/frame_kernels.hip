@@ -640,24 +640,35 @@ int launch_pyramid(r360_frame* f) {
         }
         hipLaunchKernelGGL(k_gradient_levels, dim3(GL.blk0[f->n_levels]), dim3(TPB), 0, f->ctx->stream, GL);
     }
-    // level 0's compacted points feed a lone alignment's level-0 pass (PF 5); batched passes stream the packed image
-    // (PF 6) where rows split into whole waves, so frames that only enter batches (f->compact0 unset: the sequence
-    // runner's queued ring) skip them (built on request: r360_frame_get_points, or a form forced by R360_ICP_PF)
+    // the compacted points feed a lone alignment's passes (PF 5); batched passes stream the images (PF 6 at level 0
+    // where its rows split into whole waves, PF 8 on levels of >= 64 columns), so frames that only enter batches
+    // (f->compact_all unset: the sequence runner's queued ring) skip the levels a batched pass streams (built on
+    // request: r360_frame_get_points, or a form forced by R360_ICP_PF)
     static const int pf_env = R360_KNOB("R360_ICP_PF", -1);
-    const bool skip0 = f->lv[0].pk && f->lv[0].cols % 64 == 0 && !f->compact0 && !(pf_env == 4 || pf_env == 5);
-    f->lv0_compacted = !skip0;
-    return launch_src_compaction(f, skip0 ? 1 : 0, f->n_levels);
+    const bool skip_ok = !f->compact_all && !(pf_env == 4 || pf_env == 5);
+    unsigned need = 0;
+    for (int l = 0; l < f->n_levels; ++l) {
+        static const bool coarse_pf5 = R360_KNOB("R360_COARSE_PF5", 0) != 0;   // experiment builds (icp_kernels.hip)
+        const bool streamed = l == 0 && f->lv[0].pk ? f->lv[0].cols % 64 == 0 : f->lv[l].cols >= 64 && !coarse_pf5;
+        if (!skip_ok || !streamed) need |= 1u << l;
+    }
+    f->compacted = need;
+    return launch_src_compaction(f, need);
 }
 
-// The compaction of levels [l0, l1) (one count + one compact launch over a flattened (level, block) grid)
-int launch_src_compaction(r360_frame* f, int l0, int l1) {
+// The compaction of the levels in `levels` (bit l: level l), one count + one compact launch over a flattened
+// (level, block) grid
+int launch_src_compaction(r360_frame* f, unsigned levels) {
     const float min_d = 0.3f, max_d = 6.0f;
-    if (l0 >= l1) return 0;
+    int l1 = 0;
+    for (int l = 0; l < f->n_levels; ++l)
+        if ((levels >> l) & 1u) l1 = l + 1;
+    if (l1 == 0) return 0;
     SrcGrid G{};
     G.nl = l1;
     for (int l = 0; l < l1; ++l)
-        G.blk0[l + 1] = G.blk0[l] +
-                        (l < l0 ? 0 : (int)(((long)f->lv[l].rows * f->lv[l].cols + R360_SRC_BLOCK - 1) / R360_SRC_BLOCK));
+        G.blk0[l + 1] = G.blk0[l] + (((levels >> l) & 1u) ? (int)(((long)f->lv[l].rows * f->lv[l].cols + R360_SRC_BLOCK - 1) /
+                                                                      R360_SRC_BLOCK) : 0);
     const dim3 g(G.blk0[l1]);
     hipLaunchKernelGGL(k_src_count, g, dim3(SRC_TPB), 0, f->ctx->stream, f->d_src_levels, G, min_d, max_d, f->d_src_cnt,
                        f->src_blocks);

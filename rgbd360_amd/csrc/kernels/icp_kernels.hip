@@ -1239,6 +1239,144 @@ __device__ __forceinline__ int icp_pass_body(const IcpJobs& jobs, const float* _
 #if R360_PK_ACC
         pk_fold(A, K);
 #endif
+    } else if (PF == 8 || PF == 9) {
+        // Coarse levels of batched launches from the level's {gray, depth} IMAGE instead of the source's compacted
+        // points (round 6): frames that only enter batches then skip the per-frame source compaction (two launches per
+        // frame).  PF 6's wave stream: one wave = 64 consecutive pixels, a cursor in scalar registers; where the rows
+        // split into whole waves (cols % 64 == 0, PF 8) the row is wave-uniform (scalar sin / cos phi), otherwise (PF 9:
+        // levels of 240 / 480 columns) a wave spans two rows and each lane takes its own (vector table loads).  The LUT point comes
+        // from the tables by the compaction's float expressions (lut_point) and the target {gray, depth} is gathered as
+        // a float2: per pixel the values, validity and lean terms of PF 5, summed in another lane order.
+        const int npx = nRows * nCols;
+        const int lane = tidx & 63;
+        const int qcap = ((npx + stride - 1) / stride) * 64;
+        int* q = dq + ((long)bidx * NW + (tidx >> 6)) * qcap;
+        int qn = 0;
+        constexpr bool whole = PF == 8;
+        const auto rs_s = __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(src), 0, npx * 8, 0x00020000);
+        const auto rs_g = __builtin_amdgcn_make_buffer_rsrc(const_cast<float4*>(tg), 0, npx * 16, 0x00020000);
+        const auto rs_t = __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(trg), 0, npx * 8, 0x00020000);
+        const auto rs_sp = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(sinphi), 0, nRows * 4, 0x00020000);
+        const auto rs_cp = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(cosphi), 0, nRows * 4, 0x00020000);
+        const auto rs_st = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(sinth), 0, nCols * 4, 0x00020000);
+        const auto rs_ct = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(costh), 0, nCols * 4, 0x00020000);
+        auto f2 = [](decltype(__builtin_amdgcn_raw_buffer_load_b64(rs_s, 0, 0, 0)) v) {
+            return make_float2(__uint_as_float(v[0]), __uint_as_float(v[1]));
+        };
+        auto gG = [&](int t) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs_g, t * 16, 0, 0);
+            return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+        };
+        auto gT = [&](int t) { return f2(__builtin_amdgcn_raw_buffer_load_b64(rs_t, t * 8, 0, 0)); };
+        auto acc = [&](const Proj& o, const float4 G, const float2 T) {
+            contribute_lean<METHOD>(A, W, errf, o, G, T, angle_res_inv, C);
+        };
+        const float inv_cols = 1.f / (float)nCols;
+        auto row_of = [&](int i) {
+            int r = (int)((float)i * inv_cols);
+            r -= (r * nCols > i) ? 1 : 0;
+            r += ((r + 1) * nCols <= i) ? 1 : 0;
+            return r;
+        };
+        struct Src { float2 v; float sp, cp, st, ct; };
+        int n_it_ = 0;
+        int cur_k = 0, cur_i = 0, cur_r = 0, cur_c = 0;
+        const int st_r = stride / nCols, st_c = stride - (stride / nCols) * nCols;
+        auto ld = [&]() {
+            int c = cur_c + lane, r = cur_r;
+            float sp, cp;
+            if constexpr (whole) {
+                sp = sinphi[cur_r];
+                cp = cosphi[cur_r];
+            } else {   // the wave's pixels past the row end start the next row (nCols >= 64); past the image: depth 0
+                const bool nx = c >= nCols;
+                c -= nx ? nCols : 0;
+                r += nx ? 1 : 0;
+                sp = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_sp, r * 4, 0, 0));
+                cp = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_cp, r * 4, 0, 0));
+            }
+            const Src x{f2(__builtin_amdgcn_raw_buffer_load_b64(rs_s, (cur_i + lane) * 8, 0, 0)), sp, cp,
+                        __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_st, c * 4, 0, 0)),
+                        __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_ct, c * 4, 0, 0))};
+            if (cur_k + 1 < n_it_) {
+                ++cur_k;
+                cur_i += stride;
+                cur_r += st_r;
+                cur_c += st_c;
+                if (cur_c >= nCols) { cur_c -= nCols; ++cur_r; }
+            }
+            return x;
+        };
+        auto prj = [&](const Src& x) {
+            return project_fast<true>(P, lut_point(x.v.y, x.sp, x.cp, x.st, x.ct, C), x.v.x, nRows, nCols,
+                                      angle_res_inv, asin_out);
+        };
+        auto defer = [&](Proj& o, int base) {
+            const unsigned long long m = __ballot(o.fix);
+            if (m) {
+                const int pos = qn + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                                                   __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+                if (o.fix) { q[pos] = base + lane; o.vis = false; o.t = 0; }
+                qn += __popcll(m);
+            }
+        };
+        const int nbx = (int)gridDim.x;   // XCD-aware stream order (as PF 4 / 5 / 6)
+        const int bx = (nbx & 7) ? (int)bidx : ((int)bidx & 7) * (nbx >> 3) + ((int)bidx >> 3);
+        const int b0 = __builtin_amdgcn_readfirstlane((bx * TPB + (tidx & ~63)));
+        if (b0 < npx) {
+            const int n_it = (npx - 1 - b0) / stride + 1;
+            n_it_ = n_it;
+            cur_i = b0;
+            cur_r = __builtin_amdgcn_readfirstlane(row_of(b0));
+            cur_c = b0 - cur_r * nCols;
+            auto base = [&](int k) { return b0 + (k < n_it ? k : n_it - 1) * stride; };
+            Src sA = ld();
+            Src sB = ld();
+            Proj oA = prj(sA);
+            defer(oA, base(0));
+            float4 GA = gG(oA.t);
+            float2 TA = gT(oA.t);
+            for (int k = 0;; k += 2) {
+                sA = ld();
+                Proj oB = prj(sB);
+                if (k + 1 < n_it) defer(oB, base(k + 1));   // a clamped tail chunk is never accumulated
+                const float4 GB = gG(oB.t);
+                const float2 TB = gT(oB.t);
+                acc(oA, GA, TA);
+                if (k + 1 >= n_it) break;
+                sB = ld();
+                oA = prj(sA);
+                if (k + 2 < n_it) defer(oA, base(k + 2));
+                GA = gG(oA.t);
+                TA = gT(oA.t);
+                acc(oB, GB, TB);
+                if (k + 2 >= n_it) break;
+            }
+        }
+        // the workgroup's deferred lanes, drained together (as PF 5)
+        if (lane == 0) s_qn[tidx >> 6] = qn;
+        __syncthreads();
+        int pre[NW + 1];
+        pre[0] = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) pre[w + 1] = pre[w] + s_qn[w];
+        const int tot = pre[NW];
+        const int* qb = dq + (long)bidx * NW * qcap;
+        for (int s0 = (tidx >> 6) * 64; s0 < tot; s0 += NW * 64) {
+            const int g = s0 + lane;
+            const bool act = g < tot;
+            int w = 0;
+#pragma unroll
+            for (int v = 1; v < NW; ++v) w += g >= pre[v] ? 1 : 0;
+            const int i = act ? qb[w * qcap + (g - pre[w])] : 0;
+            const float2 v = src[i];
+            const int r = i / nCols, c = i - r * nCols;
+            Proj o = project_exact(P, lut_point(v.y, sinphi[r], cosphi[r], sinth[c], costh[c], C), v.x, nRows, nCols,
+                                   half_nRows, angle_res_inv);
+            o.vis = o.vis && act;
+            o.t = o.vis ? o.t : 0;
+            acc(o, gG(o.t), gT(o.t));
+        }
     } else if (PF == 7) {
         // PF 6 with a deeper software pipeline (sources two steps ahead of their projection, gathers two steps
         // ahead of their accumulation): the level-0 pass is bound by memory latency, not by VALU or bytes
@@ -1690,8 +1828,10 @@ __device__ __forceinline__ int icp_pass_body(const IcpJobs& jobs, const float* _
     return PASS_STEPPED;
 }
 
+// PF 9 (coarse levels whose rows do not split into whole waves: per-lane rows, one more table pair live) at 4 waves per
+// SIMD: at 5 its pipelined chunks spilled 20 B per lane; the levels it serves are the two smallest
 template <int METHOD, int PF, int TOP, int OCC>
-__global__ __launch_bounds__(TPB, R360_ICP_MINB) void k_icp_pass(const IcpJobs jobs, const float* __restrict__ sinphi,
+__global__ __launch_bounds__(TPB, PF == 9 ? 4 : R360_ICP_MINB) void k_icp_pass(const IcpJobs jobs, const float* __restrict__ sinphi,
                                                  const float* __restrict__ cosphi, const float* __restrict__ sinth,
                                                  const float* __restrict__ costh, int nRows, int nCols,
                                                  IcpConst C, int first, int eval_only,
@@ -2181,6 +2321,8 @@ static int launch_pass(r360_ctx* ctx, int nb, int njobs, const IcpJobs& jobs, co
         kern = top ? k_icp_pass<M, PF, 1, 0> : k_icp_pass<M, PF, 0, 0>;
     } else if constexpr (PF == 6) {
         kern = k_icp_pass<M, PF, 1, 0>;   // level 0 only
+    } else if constexpr (PF == 8 || PF == 9) {
+        kern = k_icp_pass<M, PF, 0, 0>;   // the coarse levels of batched launches
     }
     if (!kern) {
         r360_set_error("k_icp_pass: form PF %d (occlusion %d, top %d) is not in this build", PF, C.occ, (int)top);
@@ -2238,7 +2380,7 @@ int ensure_batch(r360_ctx* ctx, int n, long n_pixels) {
 // the number of workgroups
 struct PassGrid { int pf, nb; };
 static PassGrid pass_grid(const r360_ctx* ctx, const LevelBufs& Ls, int occ, int njobs = 1, bool batched = false,
-                          bool pts0 = false) {
+                          bool pts = false) {
     // 4-pixel units on the large levels, one pixel per thread where that still fits one resident
     // round (latency-bound small levels); R360_ICP_PF=0/1 forces one form (experiments)
     static const int pf_env = R360_KNOB("R360_ICP_PF", -1);
@@ -2256,12 +2398,21 @@ static PassGrid pass_grid(const r360_ctx* ctx, const LevelBufs& Ls, int occ, int
     // level 0 (the only level with a packed image) streams the packed images where rows split into whole waves, in
     // batched launches: PF 6 reads 0.64x PF 5's bytes with fewer instructions, which a full chip of waves turns into
     // throughput.  A lone alignment's pass (two workgroups per CU, latency-bound) runs PF 5 over the source's
-    // compacted level-0 points (pts0: built with the frame, r360_frame::compact0): only valid pixels, no deferred
+    // compacted level-0 points (pts: built with the frame, r360_frame::compact_all): only valid pixels, no deferred
     // lanes, the shorter dependent chain; level-0 pass 26.9 -> 24.2 us in-kernel, lone pair 0.92 -> 0.85 ms
     // (profiles/r5_lone).  The two forms sum the same pixels in different orders (equal to rounding).
+    // Round 6: the coarse levels of batched launches stream the level's image too (PF 8, levels of >= 64 columns), so
+    // the frames of batched alignments need no compacted source points at all (the sequence runner's ring frames skip
+    // the two compaction launches per frame).  A lone alignment keeps PF 5 where its source has the level's points
+    // (pts), and streams the image where it has not.
     const bool pk_ok = Ls.pk != nullptr && Ls.cols % 64 == 0;
-    const int pf_dflt = occ ? ((Ls.cols % 64 == 0) ? 3 : 0) : (pk_ok && (batched || !pts0) ? 6 : 5);
-    const int pf = R360_EXPERIMENTS && pf_env >= 0 && !(pf_env >= 4 && occ) && !(pf_env >= 6 && !pk_ok) ? pf_env : pf_dflt;
+    static const bool coarse_pf5 = R360_KNOB("R360_COARSE_PF5", 0) != 0;   // experiment builds: round 5's coarse form
+    const bool img_ok = !pk_ok && Ls.cols >= 64 && !coarse_pf5;
+    const int pf_img = pk_ok ? 6 : img_ok ? (Ls.cols % 64 == 0 ? 8 : 9) : 5;
+    const int pf_dflt = occ ? ((Ls.cols % 64 == 0) ? 3 : 0) : (batched || !pts ? pf_img : 5);
+    const bool env_ok = pf_env >= 0 && !(pf_env >= 4 && occ) && !((pf_env == 6 || pf_env == 7) && !pk_ok) &&
+                        !(pf_env == 8 && Ls.cols % 64 != 0) && !(pf_env == 9 && Ls.cols < 64);
+    const int pf = R360_EXPERIMENTS && env_ok ? pf_env : pf_dflt;
     // workgroups per job and pass: 2 per CU (one resident round holds occ_q.per[pf] per CU; a batched launch
     // fills the rest with other jobs, and fewer records per job shorten the reduction tail)
     // workgroups per job and pass: a fixed number per level size, never a function of the batch, so that a
@@ -2324,6 +2475,8 @@ static int launch_jobs(r360_ctx* ctx, const IcpJobs& jobs, int njobs, const Leve
         if (pf == 3) rc = launch_pass<M, 3>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top);      \
         else if (pf == 5) rc = launch_pass<M, 5>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top); \
         else if (pf == 6) rc = launch_pass<M, 6>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top); \
+        else if (pf == 8) rc = launch_pass<M, 8>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top); \
+        else if (pf == 9) rc = launch_pass<M, 9>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top); \
         R360_LAUNCH_EXP(M)                                                                               \
         else rc = launch_pass<M, 0>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top);              \
     } while (0)
@@ -2376,7 +2529,7 @@ static int level_blocks_per_cu(int method, int pf) {
 bool icp_level_persist_ok(r360_ctx* ctx, const r360_frame* src, int level, int method) {
     if (!R360_PERSIST_BUILT) return false;
     const LevelBufs& Ls = src->lv[level];
-    const PassGrid G = pass_grid(ctx, Ls, 0, 1, false, src->lv0_compacted);
+    const PassGrid G = pass_grid(ctx, Ls, 0, 1, false, (src->compacted >> level) & 1u);
     if (G.pf != 5 && G.pf != 6) return false;   // the product forms of the plain pass
     if (G.pf >= 3 && ctx->defer_cap < defer_need(Ls.rows * Ls.cols, G.nb)) return false;
     int dev = 0, cus = 0;
@@ -2392,7 +2545,7 @@ int launch_icp_level_persist(r360_ctx* ctx, const r360_frame* trg, const r360_fr
     const LevelBufs& Ls = src->lv[level];
     const LevelBufs& Lt = trg->lv[level];
     const LevelTrig& T = src->calib->trig[level];
-    const PassGrid G = pass_grid(ctx, Ls, 0, 1, false, src->lv0_compacted);
+    const PassGrid G = pass_grid(ctx, Ls, 0, 1, false, (src->compacted >> level) & 1u);
     if (C0.occ || (G.pf != 5 && G.pf != 6) || !R360_PERSIST_BUILT) {
         r360_set_error("persistent level launch: plain pass forms only");
         return -1;
@@ -2427,7 +2580,7 @@ int launch_icp_level(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src
     const LevelBufs& Ls = src->lv[level];
     const LevelBufs& Lt = trg->lv[level];
     const LevelTrig& T = src->calib->trig[level];
-    const PassGrid G = pass_grid(ctx, Ls, C.occ, 1, false, src->lv0_compacted);
+    const PassGrid G = pass_grid(ctx, Ls, C.occ, 1, false, (src->compacted >> level) & 1u);
     const int npx = Ls.rows * Ls.cols;
     if (G.pf >= 3 && ctx->defer_cap < defer_need(npx, G.nb)) {   // one queue per wave, room for every pixel
         r360_set_error("deferred-pixel queue not sized for %d pixels (ensure_defer)", npx);

@@ -457,10 +457,11 @@ struct r360_frame {
     PlaneBufs pl;
     PbMapHost* pbmap = nullptr;
     uint64_t timestamp = 0;            // Frame360::timeStamp (Frame360.h:181-184)
-    bool lv0_compacted = false;        // lv[0].pts / d_npts[0] hold level 0's compacted points
-    // the pyramid build compacts level 0 too: a lone alignment's level-0 pass (PF 5) reads the compacted points;
-    // the sequence runner's queued ring frames skip it (their batched passes stream the packed image, PF 6)
-    bool compact0 = true;
+    unsigned compacted = 0;            // bit l: lv[l].pts / d_npts[l] hold level l's compacted source points
+    // the pyramid build compacts every level: a lone alignment's passes (PF 5) read the compacted points.  Frames that
+    // only enter batched alignments (compact_all unset: the sequence runner's queued ring) skip it on every level a
+    // batched pass streams as an image (PF 6 at level 0, PF 8 above; round 6: two launches per frame fewer)
+    bool compact_all = true;
     SphereCloudHost* sphere_cloud = nullptr;  // sphereCloud set by loadCloud (Frame360.h:187-193)
     // builds recorded on the frame's build event (runtime.cpp frame_build_event_record): a dense-queue job snapshots
     // it at submit and its batch refuses to run if the frame was rebuilt meanwhile (the event would then stand for
@@ -472,7 +473,7 @@ struct r360_frame {
 int launch_undistort(r360_frame* f);
 int launch_stitch(r360_frame* f);
 int launch_pyramid(r360_frame* f);
-int launch_src_compaction(r360_frame* f, int l0, int l1);   // compacted source points of levels [l0, l1)
+int launch_src_compaction(r360_frame* f, unsigned levels);   // compacted source points of the levels (bit l)
 constexpr int R360_CU_MASK_WORDS = 8;
 bool r360_cu_mask(int device, int for_queue, uint32_t* mask);   // CU partition experiment (runtime.cpp)
 int launch_sphere_level0(r360_frame* f);   // level 0 {gray, depth m} from the frame's sphere images

@@ -150,8 +150,9 @@ def test_data_dir_is_the_shipped_tree(root):
 
 
 def test_product_library_holds_only_covered_pass_forms_and_no_knobs():
-    """The shipped library contains only the k_icp_pass forms the parity suite covers — PF 6 at level 0 of batched launches, PF 5 on
-    the other levels and at level 0 of lone alignments, PF 3 / PF 0 for the occlusion variants, for the three cost functions — and reads no experiment
+    """The shipped library contains only the k_icp_pass forms the parity suite covers — PF 6 at level 0 of batched launches, PF 8 /
+    PF 9 on their coarse levels, PF 5 on the coarse levels and at level 0 of lone alignments, PF 3 / PF 0 for the occlusion
+    variants, for the three cost functions — and reads no experiment
     knob from the environment (R360_ICP_PF / _CAP / _WG_TOTAL / _PXT, R360_DIAG_EXTRA_ITERS, ...: experiment builds
     only, make exp), so no environment variable can change a registration."""
     blob = open(R.LIB_PATH, "rb").read()
@@ -159,7 +160,7 @@ def test_product_library_holds_only_covered_pass_forms_and_no_knobs():
     forms = {tuple(int(x) for x in f) for f in forms}
     covered = set()
     for m in (0, 1, 2):
-        covered |= {(m, 6, 1, 0), (m, 5, 0, 0), (m, 5, 1, 0)}
+        covered |= {(m, 6, 1, 0), (m, 5, 0, 0), (m, 5, 1, 0), (m, 8, 0, 0), (m, 9, 0, 0)}
         covered |= {(m, pf, 0, occ) for pf in (0, 3) for occ in (1, 2)}
     assert forms == covered, sorted(forms ^ covered)
     # the persistent level launch of lone alignments: the same two plain forms (PF 6 at level 0, PF 5 above)

@@ -1,12 +1,20 @@
 """GPU tests of the batched alignFrames360 (r360_align360_batch_async / _result): n pairs' passes run as one
 launch per pass, each pair with its own device Gauss-Newton state.
 
-The bar is identity with the single-pair path: every output of a batched pair (pose, Hessian, gradient,
-iteration counts, passes, SSO, error) is bit-identical to r360_align360 on that pair alone, under both the
-bench's timing schedule (exactly 20 level-0 iterations) and the reference schedule (RegisterPhotoICP.h:4611,
-where pairs converge after different numbers of iterations, so jobs of one launch exit at entry at different
-passes).  The single path itself is checked against the CPU oracle in test_gpu_dense.py; one pair of the batch
-is checked against the oracle here too."""
+The bars:
+* batch invariance: every output of a batched pair (pose, Hessian, gradient, iteration counts, passes, SSO, error)
+  is bit-identical in any batch of any size (the batched grid depends on the level size only), under both the
+  bench's timing schedule (exactly 20 level-0 iterations) and the reference schedule (RegisterPhotoICP.h:4611, where
+  pairs converge after different numbers of iterations, so jobs of one launch exit at entry at different passes);
+* against a lone r360_align360 of the same pair (two workgroups per CU, PF 5 over compacted points where the batched
+  grid streams the images, PF 6 / 8 / 9): the same pixels and terms summed in another order, so equal to rounding
+  while every Gauss-Newton accept / stop decision is the same, and within the north-star bar when one sits at a
+  rounding edge and flips (at most one iteration per level);
+* one batched pair against the CPU oracle (north-star tolerance).  The single path itself is checked against the
+  oracle in test_gpu_dense.py."""
+import json
+import os
+
 import numpy as np
 import pytest
 
@@ -78,20 +86,31 @@ def _inits(frames, pairs):
     return out
 
 
-def _close_to(pose, ref, H, Href):
-    """a batched and a lone alignment of one pair: the same pixels summed over other workgroup records (the batched
-    grid has one workgroup per CU and job, a lone pass two), so equal to rounding, well inside the north-star bar"""
+def _close_to(pose, ref, H, Href, st=None, sst=None):
+    """A batched and a lone alignment of one pair: the same pixels summed over other workgroup records and lane orders.
+    With the same Gauss-Newton decisions (per-level iteration counts) they are equal to rounding; a decision at a
+    rounding edge may flip (one iteration more or less at a level), which moves the pose within the north-star bar.
+    Returns (rotation, translation, flipped) for the drift record."""
     from oracle import oracle360 as O
-    assert O.rot_angle(pose, ref) <= 2e-5
-    assert np.linalg.norm(pose[:3, 3] - ref[:3, 3]) <= 2e-4
-    scale = np.abs(Href).max()
-    assert np.abs(H - Href).max() <= 1e-3 * scale
+    dr, dt = O.rot_angle(pose, ref), float(np.linalg.norm(pose[:3, 3] - ref[:3, 3]))
+    flipped = st is not None and list(st.iters[:5]) != list(sst.iters[:5])
+    if flipped:
+        assert all(abs(a - b) <= 1 for a, b in zip(st.iters[:5], sst.iters[:5])), (list(st.iters), list(sst.iters))
+        assert dr <= 1e-4 and dt <= 1e-3, (dr, dt)
+    else:
+        assert dr <= 2e-5 and dt <= 2e-4, (dr, dt)
+        scale = np.abs(Href).max()
+        assert np.abs(H - Href).max() <= 1e-3 * scale
+    return dr, dt, flipped
 
 
 @pytest.mark.parametrize("iters0", [20, 0])
 def test_batch_equals_single(seq, iters0):
     """A pair's result in a batch of 8 equals its batch of one bit for bit (the batched grid depends on the level
-    size only), and a lone r360_align360 of it to rounding."""
+    size only), and a lone r360_align360 of it to rounding (_close_to).  The two unrelated-scene pairs (j = 6, 7:
+    alignments that do not converge to a true motion) pin how far lone and batched may drift apart there: the same
+    status, and poses within the north-star bar of each other (measured on MI355X: 0 and 7e-10 rad,
+    profiles/r6_s4/drift_iters*.json)."""
     fr = seq["frames"]
     pairs = [(fr[i], fr[i + 1]) for i in range(6)] + [(fr[0], seq["other"]), (fr[2], fr[5])]
     inits = _inits(fr, pairs)
@@ -99,6 +118,8 @@ def test_batch_equals_single(seq, iters0):
     bctx = R.Context(0)
     poses, H, g, st, ill = R.align360_batch(bctx, pairs, inits, R.PHOTO_DEPTH, p)
     n_ill = 0
+    drift = []
+    from oracle import oracle360 as O
     for j, (t, s) in enumerate(pairs):
         one = R.align360_batch(seq["ctxs"][j % 2], [(t, s)], [inits[j]], R.PHOTO_DEPTH, _params(iters0))
         assert np.array_equal(poses[j], one[0][0]), j
@@ -106,9 +127,19 @@ def test_batch_equals_single(seq, iters0):
         assert np.array_equal(g[j], one[2][0]), j
         _same(st[j], one[3][0])
         n_ill += one[4]
-        if j < 6:   # the unrelated-scene pairs stop on a different pass when summed otherwise: same-scene only
-            sp, sH, sg, sst, rc = _single(seq["ctxs"][j % 2], t, s, inits[j], _params(iters0))
-            _close_to(poses[j], sp, H[j], sH)
+        sp, sH, sg, sst, rc = _single(seq["ctxs"][j % 2], t, s, inits[j], _params(iters0))
+        if j < 6:
+            drift.append((j,) + _close_to(poses[j], sp, H[j], sH, st[j], sst))
+        else:
+            dr, dt = O.rot_angle(poses[j], sp), float(np.linalg.norm(poses[j][:3, 3] - sp[:3, 3]))
+            drift.append((j, dr, dt, list(st[j].iters[:5]) != list(sst.iters[:5])))
+            assert bool(st[j].illposed) == bool(sst.illposed), j
+            assert dr <= 1e-4 and dt <= 1e-3, (j, dr, dt)
+    out = os.environ.get("R360_TEST_DRIFT_OUT")
+    if out:   # the measured drift (gpu_step.sh tests): lone vs batched, per pair
+        with open(f"{out}_iters{iters0}.json", "w") as fo:
+            json.dump([{"pair": int(a), "rot_rad": float(b), "trans_m": float(c), "decision_flipped": bool(d)}
+                       for a, b, c, d in drift], fo)
     assert ill == n_ill
     if iters0 == 0:   # the reference schedule: the pairs do not all stop at the same pass
         assert len({tuple(s.iters[:5]) for s in st}) > 1
@@ -127,7 +158,7 @@ def test_batch_of_one_and_reuse(seq):
         assert np.array_equal(poses[0], first[0]) and np.array_equal(H[0], first[1])
         _same(st[0], first[2])
     sp, sH, sg, sst, rc = _single(seq["ctxs"][0], fr[1], fr[2], None, _params(20))
-    _close_to(first[0], sp, first[1], sH)
+    _close_to(first[0], sp, first[1], sH, first[2], sst)
     full = [(fr[i % 6], fr[i % 6 + 1]) for i in range(R.MAX_BATCH_ALIGN)]
     poses, H, g, st, ill = R.align360_batch(bctx, full, None, R.PHOTO_DEPTH, p)
     assert np.array_equal(poses[1], first[0])

@@ -134,6 +134,35 @@ def test_icp_pass_parity_samples(ctx, qvga, method):
             _icp_check(H, g, e2, nv, nvis, Hr, gr, e2r, nvr, nvisr, lt["gray"].size)
 
 
+@pytest.mark.parametrize("method", [0, 1, 2])
+def test_icp_image_stream_pass_parity_samples(ctx, qvga, method):
+    """The pass forms of batched launches over frames without compacted source points (r360_frame_set_compaction 0:
+    the sequence runner's ring frames): the level's image streamed as PF 6 at level 0 (packed), PF 8 where rows split
+    into whole waves (960 columns) and PF 9 where a wave spans two rows (480 / 240 / 120 columns); sums, counts and
+    errors against the oracle at every level with the bars of the compacted form."""
+    cal = qvga["cal"]
+    f1, f2 = R.Frame360(cal), R.Frame360(cal)
+    for f, k in ((f1, 0), (f2, 2)):
+        b, d = qvga["raw"][k], qvga["raw"][k + 1]
+        f.setCompaction(False)
+        f.upload(b, d)
+        f.build()
+    reg = R.RegisterPhotoICP(ctx)
+    reg.setTargetFrame(f1); reg.setSourceFrame(f2)
+    poses = [np.eye(4, dtype=np.float32), O.exp_se3([0.02, -0.03, 0.05, 0.01, -0.015, 0.02])]
+    for l in range(5):
+        lt, ls = f1.level(l), f2.level(l)
+        for P in poses:
+            H, g, e2, nv, nvis = reg.eval(l, P, method)
+            e, e2r, nvr = O.error_sphere(ls, lt, P, method)
+            Hr, gr, nvisr = O.hessgrad_sphere(ls, lt, P, method)
+            _icp_check(H, g, e2, nv, nvis, Hr, gr, e2r, nvr, nvisr, lt["gray"].size)
+    # compacted on request, as before
+    pts = f2.points(2)
+    d = f2.level(2)["depth"].reshape(-1)
+    assert pts.shape[0] == int(((d > np.float32(0.3)) & (d < np.float32(6.0))).sum())
+
+
 def test_align360_parity_samples(ctx, qvga):
     reg = R.RegisterPhotoICP(ctx)
     reg.setNumPyr(5); reg.setGrayVariance(3.0 / 255)           # Registration/OdometryRGBD360.cpp:92-95

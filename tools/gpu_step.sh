@@ -13,7 +13,7 @@ Q="--no-cpu-baseline --no-resident --no-config5 --no-isolated --no-halves"
 for st in "$@"; do
   case $st in
     tests)
-      timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/gpu_tests.log 2>&1 \
+      R360_TEST_DRIFT_OUT=$O/drift timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/gpu_tests.log 2>&1 \
         || { tail -40 $O/gpu_tests.log; exit 1; }
       tail -2 $O/gpu_tests.log ;;
     smoke)
@@ -35,6 +35,16 @@ import json, sys; sys.argv=['bench.py']; import numpy as np, bench, rgbd360_amd 
 rt8 = np.stack([np.loadtxt(f'{R.EXTRINSICS_DIR}/Rt_0{k + 1}.txt', dtype=np.float32) for k in range(8)])
 print(json.dumps(bench.config5_leg(0, rt8)))" > $O/c5.json 2> $O/c5.err || { tail -20 $O/c5.err; exit 6; }
       python3 -c "import json; d=json.load(open('$O/c5.json')); r=d['roofline']; print('config5', round(d['value'],1), 'pairs/s frac', round(r['frac'],3), 'L0', round(r['avg_launch_ms']*1e3,1), 'us/launch', round(r['pairs_per_launch'],2), 'pairs/launch')" ;;
+    envab)  # the default sequence line (quick legs) alternating two environments of the experiment library, ENVAB="A|B"
+      IFS='|' read -r EA EB <<< "${ENVAB:?ENVAB=envA|envB}"
+      for rep in 1 2; do
+        for arm in A B; do
+          e=$EA; [ $arm = B ] && e=$EB
+          env R360_LIB=$R/rgbd360_amd/lib/librgbd360_hip_exp.so $e timeout -k 10 200 python -u bench.py $Q \
+            > $O/ab_${arm}_$rep.json 2> $O/ab_${arm}_$rep.err || { tail -20 $O/ab_${arm}_$rep.err; exit 10; }
+          echo "== $arm ($e) rep $rep"; python3 tools/bench_line.py $O/ab_${arm}_$rep.json | head -2
+        done
+      done ;;
     pfab)   # level-0 pass forms / occupancy: dense-alone VGA and config 5, per experiment library:PF (PFAB="exp:6 minb4:7")
       for spec in ${PFAB:-exp:6 minb4:7 minb4:6}; do
         lib=${spec%%:*}; pf=${spec##*:}; n=${lib}_pf$pf
