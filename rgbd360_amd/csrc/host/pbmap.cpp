@@ -419,6 +419,7 @@ int plane_bufs_alloc(r360_frame* f) {
     // few hundred KB per frame), so the host assembly needs no second device->host copy
     R360_HIP(hipHostMalloc(&P.contour, sizeof(float4) * P.contour_cap));
     R360_HIP(hipHostMalloc(&P.vox, sizeof(VoxOut) * P.vox_cap));
+    R360_HIP(hipMalloc(&P.vox_dev, sizeof(VoxOut) * P.vox_cap));
     R360_HIP(hipEventCreateWithFlags(&P.done, hipEventDisableTiming | hipEventBlockingSync));
     R360_HIP(hipEventCreateWithFlags(&P.ready, hipEventDisableTiming));
     R360_HIP(hipMalloc(&P.totals, sizeof(long) * 4));
@@ -432,7 +433,7 @@ void plane_bufs_free(r360_frame* f) {
     PlaneBufs& P = f->pl;
     planes_join(f);
     void* dev[] = {P.cloud, P.rgb, P.nrm, P.dist0, P.dist, P.grids, P.zmm, P.parent, P.root, P.lab, P.labf, P.cnt, P.gpart, P.aux, P.chunk, P.nlab,
-                   P.big, P.nbig, P.mom, P.models, P.nmodels, P.state, P.state2, P.rbnd, P.rflag, P.mask, P.rcode, P.rmsk, P.rf1, P.rf2, P.out, P.totals, P.err};
+                   P.big, P.nbig, P.mom, P.models, P.nmodels, P.state, P.state2, P.rbnd, P.rflag, P.mask, P.rcode, P.rmsk, P.rf1, P.rf2, P.out, P.totals, P.err, P.vox_dev};
     for (void* p : dev) hipFree(p);
     hipHostFree(P.contour);
     hipHostFree(P.vox);
@@ -520,7 +521,7 @@ PlaneDev plane_dev(const r360_frame* f, const VoxScratch& vs) {
     D.nlab = P.nlab; D.big = P.big; D.nbig = P.nbig; D.mom = P.mom; D.models = P.models; D.nmodels = P.nmodels;
     D.state = P.state; D.state2 = P.state2; D.mask = P.mask; D.rbnd = P.rbnd; D.rflag = P.rflag;
     D.rcode = P.rcode; D.rmsk = P.rmsk; D.rf1 = P.rf1; D.rf2 = P.rf2;
-    D.out = P.out; D.gpart = P.gpart; D.contour = P.contour; D.vox = P.vox; D.totals = P.totals; D.err = P.err;
+    D.out = P.out; D.gpart = P.gpart; D.contour = P.contour; D.vox = P.vox; D.vox_dev = P.vox_dev; D.totals = P.totals; D.err = P.err;
     D.h_out = P.h_out; D.h_nmodels = P.h_nmodels; D.rt = f->calib->d_rt;
     D.vhash = vs.vhash; D.vlist = vs.vlist; D.vcnt = vs.vcnt;
     D.contour_cap = P.contour_cap; D.vox_cap = P.vox_cap; D.vhash_cap = vs.cap;
@@ -645,13 +646,32 @@ extern "C" int r360_frames_build(r360_frame* const* frames, int n, unsigned flag
 // their event (5 / 20 / 100 us sleeps over the several milliseconds a batched plane stage takes: ~100 wake-ups and
 // event queries per frame) and were created and joined per frame; the bench counted 2.04 host cores in them at 1603
 // pairs/s.  The pool is created on first use and lives until the process exits.
+// R360_PBMAP_PROFILE (experiment builds): per-phase times (us) and sizes of one sensor's assembly
+struct AsmProf;
+static void planes_assemble_sensor(r360_frame* f, int s, std::vector<HPlane>& local, AsmProf* pf);
+static int planes_assemble_group(r360_frame* f, std::vector<std::vector<HPlane>>& local, const AsmProf* pf,
+                                 double sensors_us);
+static int planes_capacity_ok(r360_frame* f);
+struct AsmProf { double pre = 0, hull = 0, desc = 0, local = 0; long in = 0, kept = 0, hullv = 0, models = 0, vox = 0; };
+
 namespace {
 constexpr int R360_ASM_WORKERS = 4;
+
+// one frame's assembly in flight: its 8 sensor tasks run on any workers; the one that finishes last groups them
+struct AsmWork {
+    r360_frame* f;
+    std::vector<std::vector<HPlane>> local = std::vector<std::vector<HPlane>>(8);
+    AsmProf prof[8];
+    std::atomic<int> left{8};
+    std::atomic<long> ns{0};
+    std::chrono::steady_clock::time_point t0;
+};
 
 struct AsmPool {
     std::mutex m;
     std::condition_variable cv_watch, cv_work, cv_done;
-    std::deque<r360_frame*> pending, ready;
+    std::deque<r360_frame*> pending;
+    std::deque<std::pair<AsmWork*, int>> ready;   // (frame, sensor) tasks
     std::vector<std::thread> th;   // never joined: the pool outlives every frame (the process's lifetime)
     long assembled = 0;
 };
@@ -663,25 +683,35 @@ void asm_finish(AsmPool& A, r360_frame* f, int rc, const std::string& err) {   /
     ++A.assembled;
 }
 
+// Per-sensor tasks (round 6): a frame's sensors are assembled by up to all workers at once and the last one groups
+// them, so one frame's assembly takes about a quarter of its CPU time in wall time (the sequential callers wait for
+// it; the pipelined runner only gets its PbMaps sooner).
 void asm_worker(AsmPool* A) {
     for (;;) {
-        r360_frame* f;
+        std::pair<AsmWork*, int> t;
         {
             std::unique_lock<std::mutex> lk(A->m);
             A->cv_work.wait(lk, [&] { return !A->ready.empty(); });
-            f = A->ready.front();
+            t = A->ready.front();
             A->ready.pop_front();
         }
+        AsmWork* W = t.first;
         const auto a0 = std::chrono::steady_clock::now();
-        const int rc = planes_assemble(f);
+        planes_assemble_sensor(W->f, t.second, W->local[t.second], &W->prof[t.second]);
+        W->ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - a0).count();
+        if (W->left.fetch_sub(1) != 1) continue;
+        const auto g0 = std::chrono::steady_clock::now();
+        const int rc = planes_assemble_group(W->f, W->local,  W->prof,
+                                             std::chrono::duration<double, std::micro>(g0 - W->t0).count());
         const std::string err = rc ? std::string(r360_last_error()) : std::string();
-        const long ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - a0).count();
+        W->ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - g0).count();
         {
             std::lock_guard<std::mutex> lk(A->m);
-            f->ctx->host_ns[4] += ns;
-            f->ctx->host_ns[5] += 1;
-            asm_finish(*A, f, rc, err);
+            W->f->ctx->host_ns[4] += W->ns.load();
+            W->f->ctx->host_ns[5] += 1;
+            asm_finish(*A, W->f, rc, err);
         }
+        delete W;
         A->cv_done.notify_all();
     }
 }
@@ -731,11 +761,15 @@ void asm_watcher(AsmPool* A) {
         {
             std::lock_guard<std::mutex> lk(A->m);
             for (size_t k = 0; k < fin.size(); ++k) {
-                A->pending.erase(std::find(A->pending.begin(), A->pending.end(), fin[k].first));
-                if (fin[k].second > 0) {
-                    A->ready.push_back(fin[k].first);
+                r360_frame* f = fin[k].first;
+                A->pending.erase(std::find(A->pending.begin(), A->pending.end(), f));
+                if (fin[k].second > 0 && planes_capacity_ok(f) == 0) {
+                    auto* W = new AsmWork;
+                    W->f = f;
+                    W->t0 = std::chrono::steady_clock::now();
+                    for (int s = 0; s < 8; ++s) A->ready.push_back({W, s});
                 } else {
-                    asm_finish(*A, fin[k].first, -1, errs[k]);
+                    asm_finish(*A, f, -1, fin[k].second > 0 ? std::string(r360_last_error()) : errs[k]);
                     failed = true;
                 }
             }
@@ -793,104 +827,113 @@ int planes_finish(r360_frame* f) {
     return 0;
 }
 
-// Per-plane host part of getPlanes (A8 + A9), run by the frame's assembly thread once the GPU part
-// (including the pinned contour/voxel outputs) is complete
-int planes_assemble(r360_frame* f) {
+// Per-plane host part of getPlanes (A8 + A9), run by the assembly pool once the GPU part (including the pinned
+// contour / voxel outputs) is complete: the per-sensor part (getPlanesSensor's hull, area, descriptors, transform and
+// same-plane merges, Frame360.h:940-1075) sensor by sensor as independent tasks, then groupPlanes / mergePlanes
+// (:657-832) over the sensors' planes.
+namespace {
+std::chrono::steady_clock::time_point asm_now() { return std::chrono::steady_clock::now(); }
+double asm_us(std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+    return std::chrono::duration<double, std::micro>(b - a).count();
+}
+}  // namespace
+
+// the frame's segmentation stayed within the kernels' capacities (else the error, with its code)
+static int planes_capacity_ok(r360_frame* f) {
+    const int err = f->pl.h_nmodels[8];
+    if (!err) return 0;
+    r360_set_error("plane segmentation capacity exceeded (code %d: 1 bilateral depth range, 2 labels, 4 models, "
+                   "8 contour length, 16 pools)", err);
+    return -1;
+}
+
+// sensor s's planes (A8) into `local`, independent of the other sensors
+static void planes_assemble_sensor(r360_frame* f, int s, std::vector<HPlane>& local, AsmProf* pf) {
     PlaneBufs& P = f->pl;
     static const bool prof = R360_KNOB_STR("R360_PBMAP_PROFILE") != nullptr;
-    auto now = [] { return std::chrono::steady_clock::now(); };
-    auto us = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
-        return std::chrono::duration<double, std::micro>(b - a).count();
-    };
-    const int err = P.h_nmodels[8];
-    if (err) {
-        r360_set_error("plane segmentation capacity exceeded (code %d: 1 bilateral depth range, 2 labels, 4 models, "
-                       "8 contour length, 16 pools)", err);
-        return -1;
-    }
-    const long* totals = reinterpret_cast<const long*>(P.h_nmodels + 10);
     const float4* contour = P.contour;
     const VoxOut* vox = P.vox;
-    const auto t2 = now();
-    const r360_calib* cal = f->calib;
-    std::vector<std::vector<HPlane>> local(8);
     static thread_local std::vector<char> keep;
     static thread_local std::vector<double> hx, hy;
     static thread_local std::vector<HullPt> hq;
-    // R360_PBMAP_PROFILE (experiment builds): per-phase times (us) and sizes of this frame's assembly
-    double tp_pre = 0, tp_hull = 0, tp_desc = 0, tp_local = 0;
-    long np_in = 0, np_kept = 0, np_hull = 0, n_models = 0, n_vox = 0;
     auto tick = [&](double& acc, std::chrono::steady_clock::time_point& t) {
         if (!prof) return;
-        const auto u = now();
-        acc += us(t, u);
+        const auto u = asm_now();
+        acc += asm_us(t, u);
         t = u;
     };
-    for (int s = 0; s < 8; ++s) {
-        const float* Rt = cal->rt[s];
-        for (int m = 0; m < P.h_nmodels[s]; ++m) {
-            const PlaneOut& O = P.h_out[s * R360_MAX_MODELS + m];
-            HPlane pl;
-            pl.sensor = s;
-            pl.center = {O.model.centroid[0], O.model.centroid[1], O.model.centroid[2]};
-            pl.normal = {O.model.v[0], O.model.v[1], O.model.v[2]};
-            if (dot(pl.normal, pl.center) > 0) pl.normal = {-pl.normal.x, -pl.normal.y, -pl.normal.z};  // :988-992
-            pl.curvature = O.model.curvature;
-            pl.st = O.stats;
-            const int ax = axis_of(pl.normal), ha = (ax + 1) % 3, hb = (ax + 2) % 3;
-            auto tq = prof ? now() : t2;
-            if (prof) { ++n_models; np_in += O.n_contour > 0 ? O.n_contour : O.n_vox; n_vox += O.n_contour > 0 ? 0 : O.n_vox; }
-            // the hull's input: the contour in trace order, or ("HULL 000", :1017-1026) the VoxelGrid centroids from
-            // k_vox_* ranked by voxel index (PCL's output order); only the prefilter's survivors, with that rank
-            const bool cont = O.n_contour > 0;
-            const int n = cont ? O.n_contour : O.n_vox;
-            const float4* c = contour + O.contour_off;
-            const VoxOut* v0 = vox + O.vox_off;
-            auto get = [&](int k) { return cont ? P3{c[k].x, c[k].y, c[k].z} : P3{v0[k].x, v0[k].y, v0[k].z}; };
-            hx.resize(n);
-            hy.resize(n);
-            keep.resize(n);
-            for (int k = 0; k < n; ++k) {
-                const P3 q = get(k);
-                hx[k] = q.at(ha);
-                hy[k] = q.at(hb);
-            }
-            hull_prefilter(n, hx.data(), hy.data(), keep.data());
-            hq.clear();
-            for (int k = 0; k < n; ++k)
-                if (keep[k]) hq.push_back({(float)hx[k], (float)hy[k], cont ? (long long)k : v0[k].key, get(k)});
-            tick(tp_pre, tq);
-            if (prof) np_kept += (long)hq.size();
-            convex_hull_of(pl, hq);
-            if (prof) np_hull += (long)pl.hull.size();
-            tick(tp_hull, tq);
-            area_and_center(pl);
-            if (pl.area < kMinArea) continue;                           // :1034
-            pl.d = -dot(pl.normal, pl.center);                          // :1037
-            descriptors(pl);
-            tick(tp_desc, tq);
-            if (pl.elongation > kMaxElongation) continue;               // :1041
-            pl.normal = linear(Rt, pl.normal);                          // transform(Rt) :1051
-            pl.center = affine(Rt, pl.center);
-            pl.d = -dot(pl.normal, pl.center);
-            for (P3& v : pl.hull) v = affine(Rt, v);
-            bool merged = false;
-            if (pl.curvature < kMaxCurvature)
-                for (HPlane& q : local[s])
-                    if (q.curvature < kMaxCurvature && same_plane(q, pl, 0.99f, 0.05f, 0.2f)) {
-                        merge_into(q, pl);
-                        merged = true;
-                        break;
-                    }
-            if (!merged) {
-                pl.id = int(local[s].size());
-                local[s].push_back(pl);
-            }
-            tick(tp_local, tq);
+    const float* Rt = f->calib->rt[s];
+    local.clear();
+    for (int m = 0; m < P.h_nmodels[s]; ++m) {
+        const PlaneOut& O = P.h_out[s * R360_MAX_MODELS + m];
+        HPlane pl;
+        pl.sensor = s;
+        pl.center = {O.model.centroid[0], O.model.centroid[1], O.model.centroid[2]};
+        pl.normal = {O.model.v[0], O.model.v[1], O.model.v[2]};
+        if (dot(pl.normal, pl.center) > 0) pl.normal = {-pl.normal.x, -pl.normal.y, -pl.normal.z};  // :988-992
+        pl.curvature = O.model.curvature;
+        pl.st = O.stats;
+        const int ax = axis_of(pl.normal), ha = (ax + 1) % 3, hb = (ax + 2) % 3;
+        auto tq = prof ? asm_now() : std::chrono::steady_clock::time_point{};
+        if (prof) { ++pf->models; pf->in += O.n_contour > 0 ? O.n_contour : O.n_vox; pf->vox += O.n_contour > 0 ? 0 : O.n_vox; }
+        // the hull's input: the contour in trace order, or ("HULL 000", :1017-1026) the VoxelGrid centroids from
+        // k_vox_* ranked by voxel index (PCL's output order); only the prefilter's survivors, with that rank
+        // (the voxel lists arrive prefiltered by k_vox_hullpre: vox_fill survivors of n_vox; the contour is filtered here)
+        const bool cont = O.n_contour > 0;
+        const int n = cont ? O.n_contour : O.vox_fill;
+        const float4* c = contour + O.contour_off;
+        const VoxOut* v0 = vox + O.vox_off;
+        auto get = [&](int k) { return cont ? P3{c[k].x, c[k].y, c[k].z} : P3{v0[k].x, v0[k].y, v0[k].z}; };
+        hx.resize(n);
+        hy.resize(n);
+        keep.resize(n);
+        for (int k = 0; k < n; ++k) {
+            const P3 q = get(k);
+            hx[k] = q.at(ha);
+            hy[k] = q.at(hb);
         }
+        if (cont) hull_prefilter(n, hx.data(), hy.data(), keep.data());
+        else std::fill(keep.begin(), keep.end(), 1);
+        hq.clear();
+        for (int k = 0; k < n; ++k)
+            if (keep[k]) hq.push_back({(float)hx[k], (float)hy[k], cont ? (long long)k : v0[k].key, get(k)});
+        tick(pf->pre, tq);
+        if (prof) pf->kept += (long)hq.size();
+        convex_hull_of(pl, hq);
+        if (prof) pf->hullv += (long)pl.hull.size();
+        tick(pf->hull, tq);
+        area_and_center(pl);
+        if (pl.area < kMinArea) continue;                           // :1034
+        pl.d = -dot(pl.normal, pl.center);                          // :1037
+        descriptors(pl);
+        tick(pf->desc, tq);
+        if (pl.elongation > kMaxElongation) continue;               // :1041
+        pl.normal = linear(Rt, pl.normal);                          // transform(Rt) :1051
+        pl.center = affine(Rt, pl.center);
+        pl.d = -dot(pl.normal, pl.center);
+        for (P3& v : pl.hull) v = affine(Rt, v);
+        bool merged = false;
+        if (pl.curvature < kMaxCurvature)
+            for (HPlane& q : local)
+                if (q.curvature < kMaxCurvature && same_plane(q, pl, 0.99f, 0.05f, 0.2f)) {
+                    merge_into(q, pl);
+                    merged = true;
+                    break;
+                }
+        if (!merged) {
+            pl.id = int(local.size());
+            local.push_back(pl);
+        }
+        tick(pf->local, tq);
     }
-    const auto t3 = now();
-    // groupPlanes (:742-832)
+}
+
+// groupPlanes (:742-832) and mergePlanes (:657-739) over the sensors' planes: the frame's PbMap.  pf (profile runs):
+// the sensors' phase times, sensors_us the wall time from the first sensor task's start
+static int planes_assemble_group(r360_frame* f, std::vector<std::vector<HPlane>>& local, const AsmProf* pf,
+                                 double sensors_us) {
+    static const bool prof = R360_KNOB_STR("R360_PBMAP_PROFILE") != nullptr;
+    const auto t3 = asm_now();
     auto* pm = new PbMapHost;
     std::vector<HPlane>& G = pm->planes;
     G = local[0];
@@ -921,7 +964,7 @@ int planes_assemble(r360_frame* f) {
         prev = next;
         if (s == 6) prev.insert(first.begin(), first.end());
     }
-    const auto t4 = now();
+    const auto t4 = asm_now();
     // mergePlanes (:657-739)
     for (size_t j = 0; j < G.size(); j++) {
         if (!(G[j].curvature < kMaxCurvature)) continue;
@@ -940,13 +983,30 @@ int planes_assemble(r360_frame* f) {
         }
     }
     f->pbmap = pm;
-    if (prof)
+    if (prof && pf) {
+        AsmProf t;
+        for (int s = 0; s < 8; ++s) {
+            t.pre += pf[s].pre; t.hull += pf[s].hull; t.desc += pf[s].desc; t.local += pf[s].local;
+            t.in += pf[s].in; t.kept += pf[s].kept; t.hullv += pf[s].hullv; t.models += pf[s].models; t.vox += pf[s].vox;
+        }
+        const long* totals = reinterpret_cast<const long*>(f->pl.h_nmodels + 10);
         fprintf(stderr, "[pbmap] pools %ld+%ld pts (voxel table %ld cells, bound %ld) | sensors %.0f us: prefilter %.0f, "
                 "hull %.0f, area+desc %.0f, local merges %.0f | groupPlanes %.0f us, mergePlanes %.0f us | models %ld, "
                 "points %ld (voxels %ld) -> %ld kept -> %ld hull vertices, planes %zu\n", totals[0], totals[1],
-                totals[2] + 1, totals[3], us(t2, t3), tp_pre, tp_hull, tp_desc, tp_local, us(t3, t4), us(t4, now()),
-                n_models, np_in, n_vox, np_kept, np_hull, G.size());
+                totals[2] + 1, totals[3], sensors_us, t.pre, t.hull, t.desc, t.local, asm_us(t3, t4),
+                asm_us(t4, asm_now()), t.models, t.in, t.vox, t.kept, t.hullv, G.size());
+    }
     return 0;
+}
+
+// the whole assembly on the calling thread
+int planes_assemble(r360_frame* f) {
+    if (planes_capacity_ok(f)) return -1;
+    std::vector<std::vector<HPlane>> local(8);
+    AsmProf pf[8];
+    const auto t0 = asm_now();
+    for (int s = 0; s < 8; ++s) planes_assemble_sensor(f, s, local[s], &pf[s]);
+    return planes_assemble_group(f, local, pf, asm_us(t0, asm_now()));
 }
 
 // ------------------------------------------------------------------ RegisterRGBD360

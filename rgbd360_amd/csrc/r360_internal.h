@@ -192,7 +192,8 @@ struct alignas(16) PlaneOut {
     r360p::Moments stats;   // final inliers: rig-frame moments + colour sums
     PlaneModel model;
     int start;              // inlier_indices[i][0]
-    int n_contour, n_vox, vox_fill;
+    int n_contour, n_vox, vox_fill; // vox_fill: k_vox_compact's fill counter, then (k_vox_hullpre) the count of the
+                                    // region's hull candidates at vox_off of the pinned pool
     float bmin[3], bmax[3]; // local-frame bounds of the inliers (VoxelGrid)
     long contour_off, vox_off;
 };
@@ -254,7 +255,8 @@ struct PlaneBufs {
     RegionPart* gpart = nullptr;     // [R360_GM_COPIES][8][R360_MAX_MODELS] region accumulators (k_gm<true>)
     float4* contour = nullptr;       // contour pool
     long contour_cap = 0;
-    VoxOut* vox = nullptr;           // voxel-fallback centroids
+    VoxOut* vox = nullptr;           // voxel-fallback centroids kept by the hull prefilter (pinned host)
+    VoxOut* vox_dev = nullptr;       // all voxel-fallback centroids (device; k_vox_compact -> k_vox_hullpre)
     long vox_cap = 0;
     long* totals = nullptr;          // [2] pool usage
     int* err = nullptr;              // error bits
@@ -282,7 +284,7 @@ struct PlaneDev {
     r360p::Moments* mom; PlaneModel* models; int* nmodels;
     int8_t* state; int8_t* state2; unsigned long long* mask; int8_t* rbnd; int* rflag;
     uint16_t* rcode; unsigned long long* rmsk; int8_t* rf1; int8_t* rf2;
-    PlaneOut* out; RegionPart* gpart; float4* contour; VoxOut* vox; long* totals; int* err;
+    PlaneOut* out; RegionPart* gpart; float4* contour; VoxOut* vox; VoxOut* vox_dev; long* totals; int* err;
     PlaneOut* h_out; int* h_nmodels; const float* rt;
     VoxCell* vhash; int* vlist; int* vcnt;
     long contour_cap, vox_cap;
