@@ -70,18 +70,34 @@ int axis_of(const P3& n) {
 // ordered by (a, b, tie), tie = the point's rank in the reference's input order (its position in the contour, its
 // voxel index in VoxelGrid's output), which only decides between points of equal (a, b).
 struct HullPt { float x, y; long long tie; P3 p; };
+// (x, y) as one unsigned key whose integer order is the floats' order (x major; -0 taken as +0, as the float
+// comparison does; no NaN reaches the hull)
+inline uint32_t ord_bits(float v) {
+    uint32_t u;
+    v = v + 0.0f;   // -0 -> +0
+    std::memcpy(&u, &v, 4);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
 void convex_hull_of(HPlane& pl, std::vector<HullPt>& q) {
     pl.hull.clear();
     const int n = int(q.size());
     if (!n) return;
-    std::sort(q.begin(), q.end(), [](const HullPt& u, const HullPt& v) {
-        return u.x < v.x || (u.x == v.x && (u.y < v.y || (u.y == v.y && u.tie < v.tie)));
-    });
+    // sorted by (x, y, tie) through integer keys (round 6: the comparator on the floats was 0.19 ms of a frame's
+    // assembly for ~4.8k points)
+    struct K { uint64_t k; long long tie; int i; };
+    static thread_local std::vector<K> ks;
+    static thread_local std::vector<int> ord;
+    ks.resize(n);
+    for (int i = 0; i < n; ++i) ks[i] = {(uint64_t)ord_bits(q[i].x) << 32 | ord_bits(q[i].y), q[i].tie, i};
+    std::sort(ks.begin(), ks.end(), [](const K& u, const K& v) { return u.k < v.k || (u.k == v.k && u.tie < v.tie); });
+    ord.resize(n);
+    for (int i = 0; i < n; ++i) ord[i] = ks[i].i;
     auto turn = [&](int o, int p, int r) {
-        const double ox = q[o].x, oy = q[o].y;
-        return ((double)q[p].x - ox) * ((double)q[r].y - oy) - ((double)q[p].y - oy) * ((double)q[r].x - ox);
+        const HullPt &O = q[ord[o]], &Pp = q[ord[p]], &Rr = q[ord[r]];
+        const double ox = O.x, oy = O.y;
+        return ((double)Pp.x - ox) * ((double)Rr.y - oy) - ((double)Pp.y - oy) * ((double)Rr.x - ox);
     };
-    static thread_local std::vector<int> chain;   // positions in q
+    static thread_local std::vector<int> chain;   // positions in the sorted order
     chain.clear();
     chain.reserve(2 * n + 1);
     for (int i = 0; i < n; ++i) {           // lower hull
@@ -93,7 +109,8 @@ void convex_hull_of(HPlane& pl, std::vector<HullPt>& q) {
         while (chain.size() >= lower && turn(chain[chain.size() - 2], chain.back(), i) <= 0) chain.pop_back();
         chain.push_back(i);
     }
-    for (int c : chain) pl.hull.push_back(q[c].p);
+    pl.hull.reserve(chain.size());
+    for (int c : chain) pl.hull.push_back(q[ord[c]].p);
 }
 
 void convex_hull(HPlane& pl, const std::vector<P3>& pts) {
