@@ -2466,9 +2466,15 @@ namespace {
 __device__ __forceinline__ void d_plane_publish(const PlaneOut* __restrict__ out, const int* __restrict__ nmodels,
                                 const int* __restrict__ err, const long* __restrict__ totals, PlaneOut* __restrict__ h_out,
                                 int* __restrict__ h_nm, int nwords) {
+    // only the sensors' live region records (slots [0, nmodels[s]) of each sensor; ~48 of the 512): the rest would
+    // be written over PCIe for nothing (round 6: the kernel's stores to pinned host memory hold its completion)
     const int* src = reinterpret_cast<const int*>(out);
     int* dst = reinterpret_cast<int*>(h_out);
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nwords; i += gridDim.x * blockDim.x) dst[i] = src[i];
+    constexpr int per = (int)(sizeof(PlaneOut) / 4);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nwords; i += gridDim.x * blockDim.x) {
+        const int slot = i / per;
+        if (slot % R360_MAX_MODELS < nmodels[slot / R360_MAX_MODELS]) dst[i] = src[i];
+    }
     if (blockIdx.x == 0 && threadIdx.x < 14 && threadIdx.x != 9) {
         const int t = threadIdx.x;
         h_nm[t] = t < 8 ? nmodels[t] : t == 8 ? *err : reinterpret_cast<const int*>(totals)[t - 10];
