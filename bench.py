@@ -291,21 +291,34 @@ def config1_leg(device, reps=5):
             "same_matches": bool(matches == r["matches"])}
 
 
-def sequential_leg(device, rows, cols, p0, frames_of, params, pairs=32):
+def sequential_leg(device, rows, cols, p0, frames_of, params, pairs=32, plane_batch=None):
     """The reference's sequential caller (Registration/OdometryRGBD360.cpp:141-257): one pair at a time through the
     C++ sequence runner with one pipeline and no dense queue (upload + build of the new frame, Register() on the
-    pipeline's own stream, wait), over `pairs` consecutive pairs of the same sequence."""
+    pipeline's own stream, wait), over `pairs` consecutive pairs of the same sequence.  plane_batch None: the runner's
+    default plane queue (its CU-masked streams; 2.28-2.29 ms per pair against 2.32-2.60 with the plane stage on the
+    pipeline's stream, profiles/r6_s11).  Returns the rate and the per-pair host split (load + build enqueue, the PbMap
+    stage with its waits, the dense wait)."""
     from rgbd360_amd import odometry as OD
-    runner = OD.SequenceRunner(device, rows, cols, 1, params, queue=0)
+    runner = OD.SequenceRunner(device, rows, cols, 1, params, queue=0, plane_batch=plane_batch)
     try:
         runner.run(p0, p0 + 4, frames_of, np.zeros((1, 4, OD.REC), np.float32))   # warm-up
         rec = np.zeros((1, pairs, OD.REC), np.float32)
+        runner.host_s[:] = 0
+        for c in runner.ctxs:
+            c.host_times(reset=True)
         t0 = time.perf_counter()
         runner.run(p0, p0 + pairs, frames_of, rec)
         dt = time.perf_counter() - t0
+        hs = runner.host_s.sum(axis=0)
+        ht = np.sum([c.host_times() for c in runner.ctxs], axis=0)
+        split = {k: round(1e3 * v / pairs, 3) for k, v in
+                 zip(("load_build_enqueue", "pbmap_stage", "dense_wait"), hs[:3])}
+        split.update({k: round(1e3 * v / max(ht[3], 1), 3) for k, v in
+                      zip(("pbmap_wait_frames", "pbmap_match_tables", "pbmap_tree_pose"), ht[:3])})
     finally:
         runner.close()
     return {"value": pairs / dt, "unit": "pairs/s", "ms_per_pair": dt / pairs * 1e3, "pairs": pairs,
+            "plane_batch": plane_batch, "host_ms_per_pair": split,
             "workload": "config4's pairs one at a time (C++ runner, 1 pipeline, no dense queue): upload, Frame360 build, "
                         "Register() per pair, as OdometryRGBD360.cpp:141-257 calls it"}
 

@@ -1189,6 +1189,10 @@ int align360_batch_enqueue(r360_ctx* ctx, int n, r360_frame* const* trg, r360_fr
         const int np = src[0]->lv[l].rows * src[0]->lv[l].cols;
         const IcpConst C = make_const(p, l, np, 0);
         const int passes = 1 + ((l == 0 && p->fixed_iters_level0 > 0) ? p->fixed_iters_level0 : p->max_iters);
+        // the coarse levels as one persistent launch each (k_icp_levels_batch); level 0 pass by pass
+        const int prc = launch_icp_levels_batch(ctx, jobs, n, src[0], l, method, C, passes);
+        if (prc < 0) return prc;
+        if (prc == 0) continue;
         for (int k = 0; k < passes; ++k)
             if (int rc = launch_icp_jobs(ctx, jobs, n, src[0], l, method, C, k == 0, 0)) return rc;
     }
@@ -1204,6 +1208,17 @@ extern "C" int r360_align360_batch_result(r360_ctx* ctx, float* pose_out, float*
     R360_HIP(hipMemcpyAsync(ctx->h_bstate, ctx->d_bstate, sizeof(IcpState) * n, hipMemcpyDeviceToHost, ctx->stream));
     if (ctx_wait(ctx)) return -1;
     ctx->batch_pending = 0;
+    bool fault = false;
+    for (int j = 0; j < n; ++j) fault = fault || ctx->h_bstate[j].fault;
+    if (fault) {
+        // a persistent coarse-level launch timed out on a job's hand-off: its drained grid left group arrival counters
+        // part-way (only a pass's step workgroup resets them); zero every job's for the next batch on this ctx
+        R360_HIP(hipMemsetAsync(ctx->d_bgticket, 0, sizeof(unsigned) * R360_TICKET_STRIDE * R360_TICKET_GROUPS * n,
+                                ctx->stream));
+        R360_HIP(hipStreamSynchronize(ctx->stream));
+        r360_set_error("alignFrames360 batch: a persistent level launch timed out waiting for a pass (GPU oversubscribed?)");
+        return -1;
+    }
     int ill = 0;
     for (int j = 0; j < n; ++j) {
         const IcpState* h = ctx->h_bstate + j;

@@ -1823,7 +1823,12 @@ __device__ __forceinline__ int icp_pass_body(const IcpJobs& jobs, const float* _
     }
 #endif
     if constexpr (PERSIST) __syncthreads();   // every wave's state stores drained before the span and the hand-off
-    if (tidx == 0) pass_arrive(kt, true, C.level, R360_KPRE, PERSIST);   // the job's last workgroup
+    if (tidx == 0) {   // the job's last workgroup
+        if (PERSIST && gridDim.y > 1)   // a batched persistent level launch: its span is closed by the last exit
+            __hip_atomic_fetch_add(kt + 18 + (C.level & 7), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+            pass_arrive(kt, true, C.level, R360_KPRE, PERSIST);
+    }
 #undef R360_KPRE
     return PASS_STEPPED;
 }
@@ -1872,14 +1877,15 @@ __global__ __launch_bounds__(TPB, PF == 9 ? 4 : R360_ICP_MINB) void k_icp_pass(c
 #ifndef R360_LEVEL_MINB
 #define R360_LEVEL_MINB 3   // waves per SIMD: a lone pass puts 2 workgroups on a CU, so registers are free up to 3
 #endif
+// The level loop of a persistent launch, for job blockIdx.y (its own state, records, tickets and generation word).
 template <int METHOD, int PF, int TOP>
-__global__ __launch_bounds__(TPB, R360_LEVEL_MINB) void k_icp_level(const IcpJobs jobs, const float* __restrict__ sinphi,
-                                                  const float* __restrict__ cosphi, const float* __restrict__ sinth,
-                                                  const float* __restrict__ costh, int nRows, int nCols,
-                                                  IcpConst C, int passes, unsigned long long* __restrict__ kt) {
+__device__ __forceinline__ void icp_level_loop(const IcpJobs& jobs, const float* __restrict__ sinphi,
+                                               const float* __restrict__ cosphi, const float* __restrict__ sinth,
+                                               const float* __restrict__ costh, int nRows, int nCols, const IcpConst& C,
+                                               int passes, unsigned long long* __restrict__ kt) {
     __shared__ int s_go;
-    IcpState* S = jobs.j[0].S;
-    unsigned* gen = jobs.j[0].gcnt + R360_PERSIST_FLAG_WORD;
+    IcpState* S = jobs.j[blockIdx.y].S;
+    unsigned* gen = jobs.j[blockIdx.y].gcnt + R360_PERSIST_FLAG_WORD;
     unsigned base = 0;
     if (threadIdx.x == 0) base = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (int k = 0; k < passes; ++k) {
@@ -1915,6 +1921,47 @@ __global__ __launch_bounds__(TPB, R360_LEVEL_MINB) void k_icp_level(const IcpJob
         if (!s_go) break;
     }
 }
+
+template <int METHOD, int PF, int TOP>
+__global__ __launch_bounds__(TPB, R360_LEVEL_MINB) void k_icp_level(const IcpJobs jobs, const float* __restrict__ sinphi,
+                                                  const float* __restrict__ cosphi, const float* __restrict__ sinth,
+                                                  const float* __restrict__ costh, int nRows, int nCols,
+                                                  IcpConst C, int passes, unsigned long long* __restrict__ kt) {
+    icp_level_loop<METHOD, PF, TOP>(jobs, sinphi, cosphi, sinth, costh, nRows, nCols, C, passes, kt);
+}
+
+// ---- batched persistent coarse levels (round 6, experiment builds: measured slower, see launch_icp_levels_batch): ONE
+// launch runs a coarse level of every job of a batch, each job on
+// its own R360_COARSE_WG workgroups looping over the level's 1 + maxIters passes with the hand-off above (per-job
+// generation word; a job that stops leaves the loop, so no launch is spent on converged passes).  Per batch that
+// replaces 4 x 11 per-pass launches (most exiting at entry once their jobs converged, each with its launch gap on the
+// dense stream, profiles/r6_s8) with 4.  A job's workgroups never wait on another job's, so the launch needs no
+// resident round: workgroups are dispatched in index order (x, then the job y), the earliest unfinished job's
+// workgroups are dispatched before any later job's, and each job's <= R360_COARSE_WG workgroups fit the GPU.  The
+// bounded waits of the hand-off stay as the guard (a timed-out job faults, its batch returns an error).  The last
+// workgroup to exit closes the launch's in-kernel span.  3 waves per SIMD: inside the level loop the pass keeps more
+// values live (158 VGPRs; at 4 / 5 waves it spilled 52 / 148 B per lane).
+#if R360_EXPERIMENTS
+template <int METHOD, int PF>
+__global__ __launch_bounds__(TPB, 3) void k_icp_levels_batch(
+        const IcpJobs jobs, const float* __restrict__ sinphi, const float* __restrict__ cosphi,
+        const float* __restrict__ sinth, const float* __restrict__ costh, int nRows, int nCols, IcpConst C, int passes,
+        unsigned long long* __restrict__ kt) {
+    icp_level_loop<METHOD, PF, 0>(jobs, sinphi, cosphi, sinth, costh, nRows, nCols, C, passes, kt);
+    if (threadIdx.x == 0) {
+        const unsigned long long total = (unsigned long long)gridDim.x * gridDim.y;
+        const unsigned long long prev = __hip_atomic_fetch_add(kt + 17, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == total - 1) {
+            __hip_atomic_store(kt + 17, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int lv = C.level & 7;
+            const unsigned long long t0 = __hip_atomic_load(kt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+            __hip_atomic_fetch_add(kt + 1 + lv, t1 > t0 ? t1 - t0 : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(kt + 9 + lv, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+#endif
 
 // ---------------------------------------------------------------- occlusion variants (§8(f)1)
 // Per pass, before the fused pass and at the same pose:
@@ -2503,6 +2550,51 @@ int launch_icp_jobs(r360_ctx* ctx, const IcpJobs& jobs, int n, const r360_frame*
         return -1;
     }
     return launch_jobs(ctx, jobs, n, Ls, geom->calib->trig[level], level, method, C, first, eval_only, G);
+}
+
+// ---- batched persistent coarse levels (k_icp_levels_batch, experiment builds only: R360_COARSE_PERSIST=1): at most
+// R360_COARSE_WG workgroups per job, PF 8 / 9.  Measured slower than the per-pass launches in the pipelined bench (1690.7 /
+// 1696.4 vs 1738.0 / 1739.0 pairs/s alternating, profiles/r6_s9): the levels' workgroups, resident at 3 waves per SIMD
+// and spinning between passes, hold CU slots the pipelines' frame and plane kernels wait for.  Returns 1 (launch the
+// level pass by pass) in the product library and whenever the level has no persistent batched form.
+int launch_icp_levels_batch(r360_ctx* ctx, const IcpJobs& jobs, int n, const r360_frame* geom, int level, int method,
+                            const IcpConst& C0, int passes) {
+#if !R360_EXPERIMENTS
+    (void)ctx; (void)jobs; (void)n; (void)geom; (void)level; (void)method; (void)C0; (void)passes;
+    return 1;
+#else
+    constexpr int R360_COARSE_WG = 64;
+    static const bool persist = R360_KNOB("R360_COARSE_PERSIST", 0) != 0;
+    if (level == 0 || C0.occ || !persist || !R360_PERSIST_BUILT) return 1;
+    if (n < 1 || n > R360_MAX_BATCH) { r360_set_error("batched passes: %d jobs (1..%d)", n, R360_MAX_BATCH); return -2; }
+    const LevelBufs& Ls = geom->lv[level];
+    PassGrid G = pass_grid(ctx, Ls, 0, n, true);
+    if (G.pf != 8 && G.pf != 9) return 1;
+    if (G.nb > R360_COARSE_WG) G.nb = R360_COARSE_WG;
+    if (ctx->bdefer_cap < defer_need(Ls.rows * Ls.cols, G.nb)) {
+        r360_set_error("batched passes: deferred-pixel queues not sized for %d pixels", Ls.rows * Ls.cols);
+        return -1;
+    }
+    const LevelTrig& T = geom->calib->trig[level];
+    IcpConst C = C0;
+    if (++ctx->icp_seq == 0) ++ctx->icp_seq;
+    C.seq = ctx->icp_seq;
+    void (*kern)(const IcpJobs, const float*, const float*, const float*, const float*, int, int, IcpConst, int,
+                 unsigned long long*) = nullptr;
+    auto pick = [&](auto m) {
+        constexpr int M = decltype(m)::value;
+        kern = G.pf == 8 ? k_icp_levels_batch<M, 8> : k_icp_levels_batch<M, 9>;
+    };
+    if (method == R360_PHOTO_CONSISTENCY) pick(std::integral_constant<int, R360_PHOTO_CONSISTENCY>{});
+    else if (method == R360_DEPTH_CONSISTENCY) pick(std::integral_constant<int, R360_DEPTH_CONSISTENCY>{});
+    else pick(std::integral_constant<int, R360_PHOTO_DEPTH>{});
+    const int slot = timing_begin(ctx, "k_icp_levels");
+    hipLaunchKernelGGL(kern, dim3(G.nb, n), dim3(TPB), 0, ctx->stream, jobs, T.sinphi, T.cosphi, T.sinth, T.costh,
+                       Ls.rows, Ls.cols, C, passes, ctx->d_ktime);
+    timing_end(ctx, slot);
+    R360_HIP(hipGetLastError());
+    return 0;
+#endif
 }
 
 // ---- persistent level launch (k_icp_level): resident-round check and launch

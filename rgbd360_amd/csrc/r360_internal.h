@@ -519,6 +519,9 @@ int icp_blocks_for(int n_pixels);
 // one launch.  icp_level_persist_ok: whether level's pass grid fits one resident round of that kernel with a
 // workgroup per CU to spare (and the build has it); launch_icp_level_persist enqueues it.
 bool icp_level_persist_ok(r360_ctx* ctx, const r360_frame* src, int level, int method);
+// a coarse level of a batch as one persistent launch (k_icp_levels_batch); 1 = no such form for it (launch per pass)
+int launch_icp_levels_batch(r360_ctx* ctx, const IcpJobs& jobs, int n, const r360_frame* geom, int level, int method,
+                            const IcpConst& C, int passes);
 int launch_icp_level_persist(r360_ctx* ctx, const r360_frame* trg, const r360_frame* src, int level, int method,
                              const IcpConst& C, int passes);
 // sizes ctx->d_defer for passes over up to n_pixels pixels (synchronises the ctx stream when it grows,

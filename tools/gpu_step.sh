@@ -45,6 +45,29 @@ print(json.dumps(bench.config5_leg(0, rt8)))" > $O/c5.json 2> $O/c5.err || { tai
           echo "== $arm ($e) rep $rep"; python3 tools/bench_line.py $O/ab_${arm}_$rep.json | head -2
         done
       done ;;
+    trace)  # kernel trace of the default sequence line (quick legs): dense-stream gaps, GPU busy, per-kernel stats
+      ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
+          -d $O/trace -o trace -- python3 $R/bench.py $Q > $O/trace_bench.json 2> $O/trace.err ) \
+        || { tail -20 $O/trace.err; exit 11; }
+      T=$(ls $O/trace/*kernel_trace.csv | head -1)
+      python3 tools/dense_gaps.py $T > $O/dense_gaps.txt && python3 tools/busy.py $T 1000 > $O/busy.txt \
+        && cp $(ls $O/trace/*kernel_stats.csv | head -1) $O/kernel_stats.csv
+      find $O/trace -name "*.csv" -delete
+      head -8 $O/dense_gaps.txt; head -3 $O/busy.txt; python3 tools/bench_line.py $O/trace_bench.json | head -1 ;;
+    seq)    # the sequential caller's leg alone, plane stage on the pipeline's stream (0) and on a plane queue (8)
+      timeout -k 10 300 python -u -c "
+import json, sys; sys.argv=['bench.py']; import numpy as np, bench, rgbd360_amd as R
+rt8 = np.stack([np.loadtxt(f'{R.EXTRINSICS_DIR}/Rt_0{k + 1}.txt', dtype=np.float32) for k in range(8)])
+BGR = np.zeros((40, 8, 480, 640, 3), np.uint8); DEP = np.zeros((40, 8, 480, 640), np.uint16)
+for j in range(40): BGR[j], DEP[j] = R.synth_frame_rt(480, 640, rt8, bench.SEED, R.synth_path_pose(bench.SEED, j))
+pin = R.HostPinned(BGR, DEP)
+p = R.IcpParams.default(); p.n_pyr = 5; p.std_dev_photo = np.float32(3.0 / 255); p.fixed_iters_level0 = 20
+out = {}
+for rep in range(2):
+    for pb in (0, 8):
+        out[f'pb{pb}_{rep}'] = bench.sequential_leg(0, 480, 640, 0, lambda i: (BGR[i], DEP[i]), p, pairs=32, plane_batch=pb)
+print(json.dumps(out))" > $O/seq.json 2> $O/seq.err || { tail -20 $O/seq.err; exit 12; }
+      cat $O/seq.json ;;
     pfab)   # level-0 pass forms / occupancy: dense-alone VGA and config 5, per experiment library:PF (PFAB="exp:6 minb4:7")
       for spec in ${PFAB:-exp:6 minb4:7 minb4:6}; do
         lib=${spec%%:*}; pf=${spec##*:}; n=${lib}_pf$pf
