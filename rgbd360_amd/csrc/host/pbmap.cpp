@@ -121,66 +121,8 @@ void convex_hull(HPlane& pl, const std::vector<P3>& pts) {
     convex_hull_of(pl, q);
 }
 
-// Akl-Toussaint prefilter for convex_hull: keep[i] = 0 for points strictly inside the octagon spanned by the extreme
-// points in 8 directions (a convex polygon inside the hull), by a relative margin far above the rounding of the
-// double turn test.  In exact arithmetic the monotone chain's output does not depend on interior points, so the hull
-// is unchanged while a 40k-point plane shrinks to its rim.  xs / ys: the points' two hull coordinates.
-// Round 6: the inside test is branch-free over a fixed 8 edges (the octagon's, edge 0 repeated when it has fewer), so
-// the compiler vectorises it; the margin 1e-7 (|e_x| + |e_y|) S uses S = the points' box width + height, which bounds
-// every |p_x| + |p_y| of round 5's per-point margin from above.  The test therefore drops a subset of the points the
-// round-5 filter dropped (it keeps a superset), and the hull is the same (R360_PBMAP_PROFILE: this filter was 0.67 of
-// 0.91 ms of a synthetic frame's assembly, 49k points per frame).
-__attribute__((target("avx2")))
-static int hull_prefilter(int n, const double* xs, const double* ys, char* keep) {
-    if (n < 64) {
-        std::fill(keep, keep + n, 1);
-        return n;
-    }
-    // extreme indices for directions at 180, 225, 270, 315, 0, 45, 90, 135 degrees (CCW order)
-    int ex[8];
-    double best[8];
-    for (int k = 0; k < 8; ++k) { ex[k] = 0; best[k] = -INFINITY; }
-    for (int i = 0; i < n; ++i) {
-        const double x = xs[i], y = ys[i];
-        const double v[8] = {-x, -x - y, -y, x - y, x, x + y, y, y - x};
-        for (int k = 0; k < 8; ++k)
-            if (v[k] > best[k]) { best[k] = v[k]; ex[k] = i; }
-    }
-    double vx[8], vy[8];
-    int m = 0;
-    for (int k = 0; k < 8; ++k) {
-        const double x = xs[ex[k]], y = ys[ex[k]];
-        if (m && x == vx[m - 1] && y == vy[m - 1]) continue;
-        vx[m] = x; vy[m] = y; ++m;
-    }
-    if (m > 1 && vx[m - 1] == vx[0] && vy[m - 1] == vy[0]) --m;
-    if (m < 3) {
-        std::fill(keep, keep + n, 1);
-        return n;
-    }
-    // the points' box: -best[0] = min x, best[4] = max x, -best[2] = min y, best[6] = max y
-    const double S = (best[4] + best[0]) + (best[6] + best[2]);
-    double exk[8], eyk[8], vxk[8], vyk[8], M[8];
-    for (int k = 0; k < 8; ++k) {
-        const int e = k < m ? k : 0, e1 = (e + 1) % m;
-        exk[k] = vx[e1] - vx[e];
-        eyk[k] = vy[e1] - vy[e];
-        vxk[k] = vx[e];
-        vyk[k] = vy[e];
-        M[k] = 1e-7 * (std::fabs(exk[k]) + std::fabs(eyk[k])) * S;
-    }
-    int kept = 0;
-#pragma clang loop vectorize(enable)
-    for (int i = 0; i < n; ++i) {
-        const double x = xs[i], y = ys[i];
-        bool inside = true;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) inside &= (exk[k] * (y - vyk[k]) - eyk[k] * (x - vxk[k])) > M[k];
-        keep[i] = !inside;
-        kept += !inside;
-    }
-    return kept;
-}
+// The hull's input is prefiltered on the device (plane_seg.hip k_hullpre, the Akl-Toussaint octagon test that ran here
+// until round 6): only the points not strictly inside the octagon of the extreme points in 8 directions reach the host.
 
 // computeMassCenterAndArea
 void area_and_center(HPlane& pl) {
@@ -435,6 +377,7 @@ int plane_bufs_alloc(r360_frame* f) {
     // the contour and voxel outputs are written by the kernels straight into pinned host memory (a
     // few hundred KB per frame), so the host assembly needs no second device->host copy
     R360_HIP(hipHostMalloc(&P.contour, sizeof(float4) * P.contour_cap));
+    R360_HIP(hipMalloc(&P.contour_dev, sizeof(float4) * P.contour_cap));
     R360_HIP(hipHostMalloc(&P.vox, sizeof(VoxOut) * P.vox_cap));
     R360_HIP(hipMalloc(&P.vox_dev, sizeof(VoxOut) * P.vox_cap));
     R360_HIP(hipEventCreateWithFlags(&P.done, hipEventDisableTiming | hipEventBlockingSync));
@@ -450,7 +393,7 @@ void plane_bufs_free(r360_frame* f) {
     PlaneBufs& P = f->pl;
     planes_join(f);
     void* dev[] = {P.cloud, P.rgb, P.nrm, P.dist0, P.dist, P.grids, P.zmm, P.parent, P.root, P.lab, P.labf, P.cnt, P.gpart, P.aux, P.chunk, P.nlab,
-                   P.big, P.nbig, P.mom, P.models, P.nmodels, P.state, P.state2, P.rbnd, P.rflag, P.mask, P.rcode, P.rmsk, P.rf1, P.rf2, P.out, P.totals, P.err, P.vox_dev};
+                   P.big, P.nbig, P.mom, P.models, P.nmodels, P.state, P.state2, P.rbnd, P.rflag, P.mask, P.rcode, P.rmsk, P.rf1, P.rf2, P.out, P.totals, P.err, P.vox_dev, P.contour_dev};
     for (void* p : dev) hipFree(p);
     hipHostFree(P.contour);
     hipHostFree(P.vox);
@@ -538,7 +481,7 @@ PlaneDev plane_dev(const r360_frame* f, const VoxScratch& vs) {
     D.nlab = P.nlab; D.big = P.big; D.nbig = P.nbig; D.mom = P.mom; D.models = P.models; D.nmodels = P.nmodels;
     D.state = P.state; D.state2 = P.state2; D.mask = P.mask; D.rbnd = P.rbnd; D.rflag = P.rflag;
     D.rcode = P.rcode; D.rmsk = P.rmsk; D.rf1 = P.rf1; D.rf2 = P.rf2;
-    D.out = P.out; D.gpart = P.gpart; D.contour = P.contour; D.vox = P.vox; D.vox_dev = P.vox_dev; D.totals = P.totals; D.err = P.err;
+    D.out = P.out; D.gpart = P.gpart; D.contour = P.contour; D.contour_dev = P.contour_dev; D.vox = P.vox; D.vox_dev = P.vox_dev; D.totals = P.totals; D.err = P.err;
     D.h_out = P.h_out; D.h_nmodels = P.h_nmodels; D.rt = f->calib->d_rt;
     D.vhash = vs.vhash; D.vlist = vs.vlist; D.vcnt = vs.vcnt;
     D.contour_cap = P.contour_cap; D.vox_cap = P.vox_cap; D.vhash_cap = vs.cap;
@@ -870,8 +813,6 @@ static void planes_assemble_sensor(r360_frame* f, int s, std::vector<HPlane>& lo
     static const bool prof = R360_KNOB_STR("R360_PBMAP_PROFILE") != nullptr;
     const float4* contour = P.contour;
     const VoxOut* vox = P.vox;
-    static thread_local std::vector<char> keep;
-    static thread_local std::vector<double> hx, hy;
     static thread_local std::vector<HullPt> hq;
     auto tick = [&](double& acc, std::chrono::steady_clock::time_point& t) {
         if (!prof) return;
@@ -895,25 +836,17 @@ static void planes_assemble_sensor(r360_frame* f, int s, std::vector<HPlane>& lo
         if (prof) { ++pf->models; pf->in += O.n_contour > 0 ? O.n_contour : O.n_vox; pf->vox += O.n_contour > 0 ? 0 : O.n_vox; }
         // the hull's input: the contour in trace order, or ("HULL 000", :1017-1026) the VoxelGrid centroids from
         // k_vox_* ranked by voxel index (PCL's output order); only the prefilter's survivors, with that rank
-        // (the voxel lists arrive prefiltered by k_vox_hullpre: vox_fill survivors of n_vox; the contour is filtered here)
+        // (both lists arrive prefiltered by k_hullpre: hull_n candidates of the n_contour / n_vox points)
         const bool cont = O.n_contour > 0;
-        const int n = cont ? O.n_contour : O.vox_fill;
+        const int n = O.hull_n;
         const float4* c = contour + O.contour_off;
         const VoxOut* v0 = vox + O.vox_off;
         auto get = [&](int k) { return cont ? P3{c[k].x, c[k].y, c[k].z} : P3{v0[k].x, v0[k].y, v0[k].z}; };
-        hx.resize(n);
-        hy.resize(n);
-        keep.resize(n);
+        hq.resize(n);
         for (int k = 0; k < n; ++k) {
             const P3 q = get(k);
-            hx[k] = q.at(ha);
-            hy[k] = q.at(hb);
+            hq[k] = {q.at(ha), q.at(hb), cont ? (long long)k : v0[k].key, q};
         }
-        if (cont) hull_prefilter(n, hx.data(), hy.data(), keep.data());
-        else std::fill(keep.begin(), keep.end(), 1);
-        hq.clear();
-        for (int k = 0; k < n; ++k)
-            if (keep[k]) hq.push_back({(float)hx[k], (float)hy[k], cont ? (long long)k : v0[k].key, get(k)});
         tick(pf->pre, tq);
         if (prof) pf->kept += (long)hq.size();
         convex_hull_of(pl, hq);

@@ -1906,7 +1906,7 @@ __device__ __forceinline__ void d_trace(const uint8_t* __restrict__ nbg, const f
 template <bool LDS>
 __global__ void __launch_bounds__(TR_TPB) k_trace(const PlaneBatch B, int w, int h) {
     const PlaneDev& D = B.f[blockIdx.z];
-    d_trace<LDS>(reinterpret_cast<const uint8_t*>(D.mask), D.cloud, w, h, D.nmodels, D.out, D.contour, D.contour_cap, D.err);
+    d_trace<LDS>(reinterpret_cast<const uint8_t*>(D.mask), D.cloud, w, h, D.nmodels, D.out, D.contour_dev, D.contour_cap, D.err);
 }
 
 
@@ -2192,32 +2192,28 @@ __global__ void __launch_bounds__(VOXC_TPB) k_vox_compact(const PlaneBatch B, in
     d_vox_compact(D.vhash, D.totals, D.out, D.vox_dev, D.vox_cap, D.vlist, D.vcnt, px);
 }
 
-// The host hull's Akl-Toussaint prefilter (host/pbmap.cpp hull_prefilter) for the VoxelGrid regions, on the device
-// (round 6: on the host it was 0.6 of the 0.9 ms a synthetic frame's assembly took, 42k centroids per frame).  One
-// workgroup per region: the extreme centroids in 8 directions of the hull plane's two coordinates (the octagon, a
-// convex polygon of input points, so inside the hull), then every centroid strictly inside the octagon by the host
-// filter's margin 1e-7 (|e_x| + |e_y|) S (S = the box width + height of the region's points) is dropped, the others
-// are compacted into the pinned pool at the region's vox_off and vox_fill becomes their count.  The host builds the
-// hull of the survivors: the same hull as of every centroid (the monotone chain's output does not depend on points
-// strictly inside it; regions of fewer than 64 centroids keep all, as on the host).  The survivors' order is the
-// device list's; the host ranks them by voxel index (PCL's order), as it did.
+// The convex hull's Akl-Toussaint prefilter, on the device (round 6: on the host it was 0.67 of the 0.91 ms a synthetic
+// frame's PbMap assembly took, 49k points per frame, and the full point lists crossed PCIe into pinned memory).  One
+// workgroup per region, over its traced contour (k_trace, in trace order) or, for a region without one, its VoxelGrid
+// centroids (k_vox_compact): the extreme points in 8 directions of the hull plane's two coordinates form an octagon (a
+// convex polygon of input points, so inside the hull); every point strictly inside it by the margin 1e-7 (|e_x| + |e_y|) S
+// (S = the box width + height of the region's points; far above the rounding of the host's double turn test) is dropped,
+// and the survivors are compacted, in list order, into the pinned pool at the region's contour_off / vox_off; hull_n
+// becomes their count.  The host's monotone chain over the survivors gives the hull of all points (its output does not
+// depend on points strictly inside the hull; regions of fewer than 64 points keep all).  Contour survivors keep their
+// relative order (the host ranks ties by it); voxel survivors are ranked by voxel index on the host, as before.
 constexpr int VOXH_TPB = 256;
-__global__ void __launch_bounds__(VOXH_TPB) k_vox_hullpre(const PlaneBatch B) {
-    const PlaneDev& D = B.f[blockIdx.z];
-    const int q = blockIdx.x, s = q / R360_MAX_MODELS, m = q % R360_MAX_MODELS;
-    if (D.totals[3] == 0 || m >= D.nmodels[s]) return;
-    PlaneOut& O = D.out[q];
-    const int n = O.n_vox;
-    if (O.n_contour > 0 || n == 0) return;
-    const VoxOut* __restrict__ src = D.vox_dev + O.vox_off;
-    VoxOut* __restrict__ dst = D.vox + O.vox_off;
+template <class PT>
+__device__ __forceinline__ float pt_coord(const PT& v, int c) { return c == 0 ? v.x : c == 1 ? v.y : v.z; }
+
+template <class PT>
+__device__ __forceinline__ int d_hullpre(const PT* __restrict__ src, PT* __restrict__ dst, int n, const PlaneModel& model) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     // the hull plane: the two coordinates other than the normal's dominant axis (pbmap.cpp axis_of)
-    const float n0 = fabsf(O.model.v[0]), n1 = fabsf(O.model.v[1]), n2 = fabsf(O.model.v[2]);
+    const float n0 = fabsf(model.v[0]), n1 = fabsf(model.v[1]), n2 = fabsf(model.v[2]);
     int k0 = n0 > n1 ? 0 : 1;
     k0 = (k0 == 0 ? n0 : n1) > n2 ? k0 : 2;
     const int ca = (k0 + 1) % 3, cb = (k0 + 2) % 3;
-    auto coord = [](const VoxOut& v, int c) { return c == 0 ? v.x : c == 1 ? v.y : v.z; };
     __shared__ double s_v[VOXH_TPB];
     __shared__ int s_i[VOXH_TPB];
     __shared__ double s_best[8], s_ex[8], s_ey[8], s_vx[8], s_vy[8], s_M[8];
@@ -2227,7 +2223,7 @@ __global__ void __launch_bounds__(VOXH_TPB) k_vox_hullpre(const PlaneBatch B) {
     int bi[8];
     for (int k = 0; k < 8; ++k) { best[k] = -INFINITY; bi[k] = 0x7fffffff; }
     for (int i = tid; i < n; i += VOXH_TPB) {
-        const double x = coord(src[i], ca), y = coord(src[i], cb);
+        const double x = pt_coord(src[i], ca), y = pt_coord(src[i], cb);
         const double v[8] = {-x, -x - y, -y, x - y, x, x + y, y, y - x};
         for (int k = 0; k < 8; ++k)
             if (v[k] > best[k]) { best[k] = v[k]; bi[k] = i; }
@@ -2247,12 +2243,12 @@ __global__ void __launch_bounds__(VOXH_TPB) k_vox_hullpre(const PlaneBatch B) {
         if (tid == 0) { s_best[k] = s_v[0]; s_idx[k] = s_i[0]; }
         __syncthreads();
     }
-    // the octagon (the host filter's construction) and its edges' constants
+    // the octagon (consecutive equal vertices merged) and its edges' constants
     if (tid == 0) {
         double vx[8], vy[8];
         int mm = 0;
         for (int k = 0; k < 8; ++k) {
-            const double x = coord(src[s_idx[k]], ca), y = coord(src[s_idx[k]], cb);
+            const double x = pt_coord(src[s_idx[k]], ca), y = pt_coord(src[s_idx[k]], cb);
             if (mm && x == vx[mm - 1] && y == vy[mm - 1]) continue;
             vx[mm] = x; vy[mm] = y; ++mm;
         }
@@ -2275,12 +2271,12 @@ __global__ void __launch_bounds__(VOXH_TPB) k_vox_hullpre(const PlaneBatch B) {
     for (int i0 = 0; i0 < n; i0 += VOXH_TPB) {
         const int i = i0 + tid;
         bool keep = false;
-        VoxOut v;
+        PT v;
         if (i < n) {
             v = src[i];
             keep = true;
             if (!all) {
-                const double x = coord(v, ca), y = coord(v, cb);
+                const double x = pt_coord(v, ca), y = pt_coord(v, cb);
                 bool inside = true;
                 for (int k = 0; k < 8; ++k) inside = inside && (s_ex[k] * (y - s_vy[k]) - s_ey[k] * (x - s_vx[k])) > s_M[k];
                 keep = !inside;
@@ -2296,10 +2292,21 @@ __global__ void __launch_bounds__(VOXH_TPB) k_vox_hullpre(const PlaneBatch B) {
         if (tid == 0) for (int w = 0; w < VOXH_TPB / 64; ++w) s_base += s_wc[w];
         __syncthreads();
     }
-    if (tid == 0) O.vox_fill = s_base;
+    return s_base;
 }
 
-
+__global__ void __launch_bounds__(VOXH_TPB) k_hullpre(const PlaneBatch B) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    const int q = blockIdx.x, s = q / R360_MAX_MODELS, m = q % R360_MAX_MODELS;
+    if (m >= D.nmodels[s]) return;
+    PlaneOut& O = D.out[q];
+    int kept = 0;
+    if (O.n_contour > 0)
+        kept = d_hullpre(D.contour_dev + O.contour_off, D.contour + O.contour_off, O.n_contour, O.model);
+    else if (O.n_vox > 0 && D.totals[3] != 0)
+        kept = d_hullpre(D.vox_dev + O.vox_off, D.vox + O.vox_off, O.n_vox, O.model);
+    if (threadIdx.x == 0) O.hull_n = kept;
+}
 }  // namespace
 
 
@@ -2442,7 +2449,7 @@ int launch_segmentation(const PlaneBatch& B, int F, const PlaneGeom& G, hipStrea
     hipLaunchKernelGGL(k_vox_hash, dim3((unsigned)groups, 1, nf), dim3(VOX_TPB), 0, st, B, N, vox_px);
     hipLaunchKernelGGL(k_vox_alloc, dim3(1, 1, nf), dim3(512), 0, st, B);
     hipLaunchKernelGGL(k_vox_compact, dim3((unsigned)groups, 1, nf), dim3(VOXC_TPB), 0, st, B, vox_px);
-    hipLaunchKernelGGL(k_vox_hullpre, dim3(8 * R360_MAX_MODELS, 1, nf), dim3(VOXH_TPB), 0, st, B);
+    hipLaunchKernelGGL(k_hullpre, dim3(8 * R360_MAX_MODELS, 1, nf), dim3(VOXH_TPB), 0, st, B);
     timing_end(tctx, slot);
     R360_HIP(hipGetLastError());
     return 0;

@@ -192,8 +192,9 @@ struct alignas(16) PlaneOut {
     r360p::Moments stats;   // final inliers: rig-frame moments + colour sums
     PlaneModel model;
     int start;              // inlier_indices[i][0]
-    int n_contour, n_vox, vox_fill; // vox_fill: k_vox_compact's fill counter, then (k_vox_hullpre) the count of the
-                                    // region's hull candidates at vox_off of the pinned pool
+    int n_contour, n_vox, vox_fill;
+    int hull_n;             // the region's hull candidates (k_hullpre: contour or voxel points not strictly inside
+                            // the Akl-Toussaint octagon), at contour_off / vox_off of the pinned pools
     float bmin[3], bmax[3]; // local-frame bounds of the inliers (VoxelGrid)
     long contour_off, vox_off;
 };
@@ -253,10 +254,11 @@ struct PlaneBufs {
     int8_t* rf2 = nullptr;               //   second sweep's states, skewed
     PlaneOut* out = nullptr;         // [8][R360_MAX_MODELS]
     RegionPart* gpart = nullptr;     // [R360_GM_COPIES][8][R360_MAX_MODELS] region accumulators (k_gm<true>)
-    float4* contour = nullptr;       // contour pool
+    float4* contour = nullptr;       // contour points kept by the hull prefilter (pinned host)
     long contour_cap = 0;
     VoxOut* vox = nullptr;           // voxel-fallback centroids kept by the hull prefilter (pinned host)
-    VoxOut* vox_dev = nullptr;       // all voxel-fallback centroids (device; k_vox_compact -> k_vox_hullpre)
+    float4* contour_dev = nullptr;   // the traced contours (device; k_trace -> k_hullpre)
+    VoxOut* vox_dev = nullptr;       // all voxel-fallback centroids (device; k_vox_compact -> k_hullpre)
     long vox_cap = 0;
     long* totals = nullptr;          // [2] pool usage
     int* err = nullptr;              // error bits
@@ -284,7 +286,7 @@ struct PlaneDev {
     r360p::Moments* mom; PlaneModel* models; int* nmodels;
     int8_t* state; int8_t* state2; unsigned long long* mask; int8_t* rbnd; int* rflag;
     uint16_t* rcode; unsigned long long* rmsk; int8_t* rf1; int8_t* rf2;
-    PlaneOut* out; RegionPart* gpart; float4* contour; VoxOut* vox; VoxOut* vox_dev; long* totals; int* err;
+    PlaneOut* out; RegionPart* gpart; float4* contour; float4* contour_dev; VoxOut* vox; VoxOut* vox_dev; long* totals; int* err;
     PlaneOut* h_out; int* h_nmodels; const float* rt;
     VoxCell* vhash; int* vlist; int* vcnt;
     long contour_cap, vox_cap;
