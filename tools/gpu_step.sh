@@ -68,6 +68,15 @@ for rep in range(2):
         out[f'pb{pb}_{rep}'] = bench.sequential_leg(0, 480, 640, 0, lambda i: (BGR[i], DEP[i]), p, pairs=32, plane_batch=pb)
 print(json.dumps(out))" > $O/seq.json 2> $O/seq.err || { tail -20 $O/seq.err; exit 12; }
       cat $O/seq.json ;;
+    argab)  # the default sequence line (quick legs) over bench argument sets, ARGAB="args1|args2|...", twice each
+      IFS='|' read -ra ARMS <<< "${ARGAB:?ARGAB=args1|args2}"
+      for rep in 1 2; do
+        for i in "${!ARMS[@]}"; do
+          timeout -k 10 200 python -u bench.py $Q ${ARMS[$i]} > $O/arg_${i}_$rep.json 2> $O/arg_${i}_$rep.err \
+            || { tail -20 $O/arg_${i}_$rep.err; exit 13; }
+          echo "== [${ARMS[$i]}] rep $rep"; python3 tools/bench_line.py $O/arg_${i}_$rep.json | head -1
+        done
+      done ;;
     pfab)   # level-0 pass forms / occupancy: dense-alone VGA and config 5, per experiment library:PF (PFAB="exp:6 minb4:7")
       for spec in ${PFAB:-exp:6 minb4:7 minb4:6}; do
         lib=${spec%%:*}; pf=${spec##*:}; n=${lib}_pf$pf
