@@ -291,13 +291,14 @@ def config1_leg(device, reps=5):
             "same_matches": bool(matches == r["matches"])}
 
 
-def sequential_leg(device, rows, cols, p0, frames_of, params, pairs=32, plane_batch=None):
+def sequential_leg(device, rows, cols, p0, frames_of, params, pairs=32, plane_batch=0):
     """The reference's sequential caller (Registration/OdometryRGBD360.cpp:141-257): one pair at a time through the
     C++ sequence runner with one pipeline and no dense queue (upload + build of the new frame, Register() on the
-    pipeline's own stream, wait), over `pairs` consecutive pairs of the same sequence.  plane_batch None: the runner's
-    default plane queue (its CU-masked streams; 2.28-2.29 ms per pair against 2.32-2.60 with the plane stage on the
-    pipeline's stream, profiles/r6_s11).  Returns the rate and the per-pair host split (load + build enqueue, the PbMap
-    stage with its waits, the dense wait)."""
+    pipeline's own stream, wait), over `pairs` consecutive pairs of the same sequence.  plane_batch 0: the plane stage
+    on the pipeline's own stream (a lone frame has nothing to batch with); since the waiting thread assembles the new
+    frame's PbMap itself (round 6, pbmap.cpp planes_join) that is 2.22 ms per pair against 2.32 through a plane queue
+    (None: the runner's default, profiles/r6_seq).  Returns the rate and the per-pair host split (load + build
+    enqueue, the PbMap stage with its waits, the dense wait)."""
     from rgbd360_amd import odometry as OD
     runner = OD.SequenceRunner(device, rows, cols, 1, params, queue=0, plane_batch=plane_batch)
     try:

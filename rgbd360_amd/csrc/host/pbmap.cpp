@@ -645,7 +645,29 @@ void asm_finish(AsmPool& A, r360_frame* f, int rc, const std::string& err) {   /
 
 // Per-sensor tasks (round 6): a frame's sensors are assembled by up to all workers at once and the last one groups
 // them, so one frame's assembly takes about a quarter of its CPU time in wall time (the sequential callers wait for
-// it; the pipelined runner only gets its PbMaps sooner).
+// it; the pipelined runner only gets its PbMaps sooner).  Runs one task taken off A->ready (by a worker or a joining
+// thread, planes_join); the thread that completes the frame's last sensor groups them and finishes the frame.
+void asm_run(AsmPool* A, const std::pair<AsmWork*, int>& t) {
+    AsmWork* W = t.first;
+    const auto a0 = std::chrono::steady_clock::now();
+    planes_assemble_sensor(W->f, t.second, W->local[t.second], &W->prof[t.second]);
+    W->ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - a0).count();
+    if (W->left.fetch_sub(1) != 1) return;
+    const auto g0 = std::chrono::steady_clock::now();
+    const int rc = planes_assemble_group(W->f, W->local,  W->prof,
+                                         std::chrono::duration<double, std::micro>(g0 - W->t0).count());
+    const std::string err = rc ? std::string(r360_last_error()) : std::string();
+    W->ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - g0).count();
+    {
+        std::lock_guard<std::mutex> lk(A->m);
+        W->f->ctx->host_ns[4] += W->ns.load();
+        W->f->ctx->host_ns[5] += 1;
+        asm_finish(*A, W->f, rc, err);
+    }
+    delete W;
+    A->cv_done.notify_all();
+}
+
 void asm_worker(AsmPool* A) {
     for (;;) {
         std::pair<AsmWork*, int> t;
@@ -655,24 +677,7 @@ void asm_worker(AsmPool* A) {
             t = A->ready.front();
             A->ready.pop_front();
         }
-        AsmWork* W = t.first;
-        const auto a0 = std::chrono::steady_clock::now();
-        planes_assemble_sensor(W->f, t.second, W->local[t.second], &W->prof[t.second]);
-        W->ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - a0).count();
-        if (W->left.fetch_sub(1) != 1) continue;
-        const auto g0 = std::chrono::steady_clock::now();
-        const int rc = planes_assemble_group(W->f, W->local,  W->prof,
-                                             std::chrono::duration<double, std::micro>(g0 - W->t0).count());
-        const std::string err = rc ? std::string(r360_last_error()) : std::string();
-        W->ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - g0).count();
-        {
-            std::lock_guard<std::mutex> lk(A->m);
-            W->f->ctx->host_ns[4] += W->ns.load();
-            W->f->ctx->host_ns[5] += 1;
-            asm_finish(*A, W->f, rc, err);
-        }
-        delete W;
-        A->cv_done.notify_all();
+        asm_run(A, t);
     }
 }
 
@@ -691,6 +696,20 @@ int asm_poll(r360_frame* f, std::string& err) {
     if (r == hipErrorNotReady) return 0;
     err = "plane build: GPU work failed";
     return -1;
+}
+
+// a frame taken off A->pending whose GPU part has ended (st > 0) or failed: its sensor tasks go to A->ready, or it
+// finishes with the error.  Under A->m; returns false if the frame failed (the caller notifies cv_done).
+bool asm_dispatch(AsmPool* A, r360_frame* f, int st, const std::string& err) {
+    if (st > 0 && planes_capacity_ok(f) == 0) {
+        auto* W = new AsmWork;
+        W->f = f;
+        W->t0 = std::chrono::steady_clock::now();
+        for (int s = 0; s < 8; ++s) A->ready.push_back({W, s});
+        return true;
+    }
+    asm_finish(*A, f, -1, st > 0 ? std::string(r360_last_error()) : err);
+    return false;
 }
 
 void asm_watcher(AsmPool* A) {
@@ -721,17 +740,10 @@ void asm_watcher(AsmPool* A) {
         {
             std::lock_guard<std::mutex> lk(A->m);
             for (size_t k = 0; k < fin.size(); ++k) {
-                r360_frame* f = fin[k].first;
-                A->pending.erase(std::find(A->pending.begin(), A->pending.end(), f));
-                if (fin[k].second > 0 && planes_capacity_ok(f) == 0) {
-                    auto* W = new AsmWork;
-                    W->f = f;
-                    W->t0 = std::chrono::steady_clock::now();
-                    for (int s = 0; s < 8; ++s) A->ready.push_back({W, s});
-                } else {
-                    asm_finish(*A, f, -1, fin[k].second > 0 ? std::string(r360_last_error()) : errs[k]);
-                    failed = true;
-                }
+                auto it = std::find(A->pending.begin(), A->pending.end(), fin[k].first);
+                if (it == A->pending.end()) continue;   // a joining thread took it meanwhile (planes_join)
+                A->pending.erase(it);
+                failed = !asm_dispatch(A, fin[k].first, fin[k].second, errs[k]) || failed;
             }
         }
         A->cv_work.notify_all();
@@ -767,12 +779,48 @@ int planes_spawn_assembly(r360_frame* f) {
     return 0;
 }
 
-// waits until the frame's queued assembly (if any) has finished; any number of threads may wait for one frame
+// Waits until the frame's queued assembly (if any) has finished; any number of threads may wait for one frame.  With
+// the frame's ctx->join_help (default) the waiting thread does not leave the frame to the pool's 50 us sweeps and
+// wake-ups: it polls the frame's GPU part itself (yielding between queries), dispatches its sensor tasks the moment
+// it has ended and runs them beside the workers, so a lone frame's PbMap is ready ~0.1 ms sooner (the sequential
+// caller's critical path).  Which thread runs a task does not change its result.
 void planes_join(r360_frame* f) {
     PlaneBufs& P = f->pl;
     if (!P.cloud) return;   // never built planes: nothing was queued
     AsmPool& A = asm_pool();
     std::unique_lock<std::mutex> lk(A.m);
+    if (f->ctx && f->ctx->join_help) {
+        while (P.asm_busy) {
+            if (std::find(A.pending.begin(), A.pending.end(), f) != A.pending.end()) {
+                lk.unlock();
+                std::string err;
+                int st;
+                while ((st = asm_poll(f, err)) == 0) std::this_thread::yield();
+                lk.lock();
+                auto it = std::find(A.pending.begin(), A.pending.end(), f);
+                if (it == A.pending.end()) continue;   // the watcher took it meanwhile
+                A.pending.erase(it);
+                const bool ok = asm_dispatch(&A, f, st, err);
+                lk.unlock();
+                A.cv_work.notify_all();
+                if (!ok) A.cv_done.notify_all();
+                lk.lock();
+                continue;
+            }
+            auto t = std::find_if(A.ready.begin(), A.ready.end(),
+                                  [&](const std::pair<AsmWork*, int>& x) { return x.first->f == f; });
+            if (t != A.ready.end()) {
+                const std::pair<AsmWork*, int> task = *t;
+                A.ready.erase(t);
+                lk.unlock();
+                asm_run(&A, task);
+                lk.lock();
+                continue;
+            }
+            A.cv_done.wait(lk, [&] { return !P.asm_busy; });   // its last tasks run on workers
+        }
+        return;
+    }
     A.cv_done.wait(lk, [&] { return !P.asm_busy; });
 }
 

@@ -345,8 +345,12 @@ struct r360_ctx {
     int timing = 0;
     r360_ctx* stats_sibling = nullptr;   // a dense queue's second stream: its kernel statistics are reported with these
     int persist_levels = 0; // r360_ctx_persistent_levels: lone alignments as one launch per level
-    int persist_held = 0;
-    int async_persist = 0;  // the pending r360_align360 runs as persistent level launches   // this ctx holds the process's persistent-launch slot (runtime.cpp, persist_slot)
+    int persist_held = 0;   // this ctx holds the process's persistent-launch slot (runtime.cpp, persist_slot)
+    int async_persist = 0;  // the pending r360_align360 runs as persistent level launches
+    // a thread that waits for the PbMap of a frame built on this ctx polls the frame's GPU part itself and runs its
+    // assembly tasks (pbmap.cpp planes_join): the latency of a lone frame.  The queued sequence runner turns it off
+    // for its pipelines (their waits would spin host cores the other pipelines' frames need)
+    bool join_help = true;
     std::vector<hipEvent_t> ev_pool;
     int ev_used = 0;
     struct TimedLaunch { std::string name; int a, b; };
