@@ -615,7 +615,7 @@ static int planes_capacity_ok(r360_frame* f);
 struct AsmProf { double pre = 0, hull = 0, desc = 0, local = 0; long in = 0, kept = 0, hullv = 0, models = 0, vox = 0; };
 
 namespace {
-constexpr int R360_ASM_WORKERS = 4;
+constexpr int R360_ASM_WORKERS = 7;   // with a joining thread, one per sensor of a lone frame
 
 // one frame's assembly in flight: its 8 sensor tasks run on any workers; the one that finishes last groups them
 struct AsmWork {
@@ -705,7 +705,18 @@ bool asm_dispatch(AsmPool* A, r360_frame* f, int st, const std::string& err) {
         auto* W = new AsmWork;
         W->f = f;
         W->t0 = std::chrono::steady_clock::now();
-        for (int s = 0; s < 8; ++s) A->ready.push_back({W, s});
+        // heaviest sensors first (hull candidates + a per-plane constant): the frame's wall time is its longest
+        // chain of tasks, and the sensors' loads differ several-fold
+        const PlaneBufs& P = f->pl;
+        int order[8];
+        long wt[8];
+        for (int s = 0; s < 8; ++s) {
+            order[s] = s;
+            wt[s] = 0;
+            for (int m = 0; m < P.h_nmodels[s]; ++m) wt[s] += P.h_out[s * R360_MAX_MODELS + m].hull_n + 32;
+        }
+        std::stable_sort(order, order + 8, [&](int a, int b) { return wt[a] > wt[b]; });
+        for (int s : order) A->ready.push_back({W, s});
         return true;
     }
     asm_finish(*A, f, -1, st > 0 ? std::string(r360_last_error()) : err);
