@@ -490,10 +490,11 @@ PlaneDev plane_dev(const r360_frame* f, const VoxScratch& vs) {
 
 // the chain of the plane stage (cloud, filter, normals, segmentation, refinement, descriptors' statistics, contours,
 // voxel fallback, publication into the frames' pinned host buffers) for F frames of the same size
-int planes_launch(const PlaneBatch& B, int F, const PlaneGeom& G, hipStream_t st, r360_ctx* tctx) {
+int planes_launch(const PlaneBatch& B, int F, const PlaneGeom& G, hipStream_t st, r360_ctx* tctx,
+                  const hipEvent_t* bgr_ev) {
     // k_plane_begin (first kernel of launch_cloud_normals) zeroes the error word
     if (launch_cloud_normals(B, F, G, st, tctx)) return -1;
-    if (launch_segmentation(B, F, G, st, tctx)) return -1;
+    if (launch_segmentation(B, F, G, st, tctx, bgr_ev)) return -1;
     return launch_plane_publish(B, F, st);
 }
 
@@ -517,7 +518,7 @@ int planes_enqueue(r360_frame* f) {
     PlaneBatch B;   // a batch of one (kernel arguments, copied at each launch)
     std::memset(&B, 0, sizeof B);
     B.f[0] = plane_dev(f, VoxScratch{ctx->d_vhash, (unsigned long long)ctx->vhash_cap, ctx->d_vlist, ctx->d_vcnt});
-    if (planes_launch(B, 1, G, ctx->stream, ctx)) return -1;
+    if (planes_launch(B, 1, G, ctx->stream, ctx, &f->bgr_ev)) return -1;
     R360_HIP(hipEventRecord(P.done, f->ctx->stream));
     return planes_spawn_assembly(f);
 }
@@ -579,7 +580,9 @@ extern "C" int r360_frames_build(r360_frame* const* frames, int n, unsigned flag
             }
             B.f[j] = plane_dev(f, vs);
         }
-        if (planes_launch(B, (int)bf.size(), G, H->stream, H)) return -1;
+        std::vector<hipEvent_t> bev;
+        for (r360_frame* f : bf) bev.push_back(f->bgr_ev);
+        if (planes_launch(B, (int)bf.size(), G, H->stream, H, bev.data())) return -1;
         for (r360_frame* f : bf) {
             R360_HIP(hipEventRecord(f->pl.done, H->stream));
             if (planes_spawn_assembly(f)) return -1;

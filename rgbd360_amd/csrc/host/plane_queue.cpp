@@ -44,7 +44,8 @@ struct r360_plane_queue {
     int max_seen = 0;
 };
 
-int planes_launch(const PlaneBatch& B, int F, const PlaneGeom& G, hipStream_t st, r360_ctx* tctx);   // pbmap.cpp
+int planes_launch(const PlaneBatch& B, int F, const PlaneGeom& G, hipStream_t st, r360_ctx* tctx,
+                  const hipEvent_t* bgr_ev);   // pbmap.cpp
 
 namespace {
 
@@ -97,7 +98,9 @@ void dispatcher(r360_plane_queue* q) {
             B.f[j] = plane_dev(f, q->vox[k][j].v);
         }
         // per-launch timing (r360_ctx_timing) records on the ctx's stream: the first stream's batches only
-        if (rc == 0) rc = planes_launch(B, F, G, st, k == 0 ? q->ctx : nullptr);
+        hipEvent_t bev[R360_PLANE_BATCH] = {};
+        for (int j = 0; j < F; ++j) bev[j] = take[j].f->bgr_ev;
+        if (rc == 0) rc = planes_launch(B, F, G, st, k == 0 ? q->ctx : nullptr, bev);
         for (int j = 0; j < F && rc == 0; ++j)
             if (hipEventRecord(take[j].f->pl.done, st) != hipSuccess) {
                 r360_set_error("plane queue: hipEventRecord failed");

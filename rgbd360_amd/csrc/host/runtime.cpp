@@ -291,6 +291,11 @@ extern "C" void r360_ctx_destroy(r360_ctx* c) {
     hipFree(c->d_vlist); hipFree(c->d_vcnt);
     for (auto& s : c->bvox) vox_slot_free(s);
     hipHostFree(c->h_unary); hipHostFree(c->h_bin);
+    if (c->up_stream) {
+        hipStreamSynchronize(c->up_stream);
+        hipStreamDestroy(c->up_stream);
+        hipEventDestroy(c->up_ev);
+    }
     if (!c->stream_borrowed) hipStreamDestroy(c->stream);
     delete c;
 }
@@ -606,6 +611,7 @@ extern "C" int r360_frame_create(r360_ctx* ctx, const r360_calib* calib, r360_fr
     }
     R360_HIP(hipMalloc(&f->d_src_levels, sizeof(SrcLevel) * R360_MAX_PYR));
     R360_HIP(hipMemcpy(f->d_src_levels, sl, sizeof(SrcLevel) * f->n_levels, hipMemcpyHostToDevice));
+    R360_HIP(hipEventCreateWithFlags(&f->bgr_ev, hipEventDisableTiming));
     *out = f;
     return 0;
 }
@@ -656,8 +662,34 @@ extern "C" void r360_frame_destroy(r360_frame* f) {
     hipFree(f->d_npts); hipFree(f->d_src_cnt); hipFree(f->d_src_levels);
     for (int l = 0; l < f->n_slevels; ++l) { hipFree(f->sp[l].p0); hipFree(f->sp[l].tg); }
     plane_bufs_free(f);
+    if (f->bgr_ev) hipEventDestroy(f->bgr_ev);
     delete f->sphere_cloud;
     delete f;
+}
+
+// The sensor images into the frame.  The depth goes first, on the ctx stream; with ctx->split_upload the BGR images
+// follow on the ctx's upload stream, after the depth copy and after everything the ctx stream had enqueued before (the
+// previous build's readers of d_bgr), so the undistortion and the plane stage's geometric part start one copy earlier
+// (the colours are first read by launch_rgb, behind f->bgr_ev).  Otherwise both on the ctx stream.
+static int frame_copy_images(r360_frame* f, const void* bgr8, const void* depth8, hipMemcpyKind kind) {
+    r360_ctx* ctx = f->ctx;
+    const size_t ns = (size_t)8 * f->rows * f->cols;
+    R360_HIP(hipMemcpyAsync(f->d_depth, depth8, ns * 2, kind, ctx->stream));
+    if (ctx->split_upload) {
+        if (!ctx->up_stream) {
+            R360_HIP(hipStreamCreateWithFlags(&ctx->up_stream, hipStreamNonBlocking));
+            R360_HIP(hipEventCreateWithFlags(&ctx->up_ev, hipEventDisableTiming));
+        }
+        R360_HIP(hipEventRecord(ctx->up_ev, ctx->stream));
+        R360_HIP(hipStreamWaitEvent(ctx->up_stream, ctx->up_ev, 0));
+        R360_HIP(hipMemcpyAsync(f->d_bgr, bgr8, ns * 3, kind, ctx->up_stream));
+        R360_HIP(hipEventRecord(f->bgr_ev, ctx->up_stream));
+    } else {
+        R360_HIP(hipStreamWaitEvent(ctx->stream, f->bgr_ev, 0));   // an earlier split copy into d_bgr
+        R360_HIP(hipMemcpyAsync(f->d_bgr, bgr8, ns * 3, kind, ctx->stream));
+        R360_HIP(hipEventRecord(f->bgr_ev, ctx->stream));
+    }
+    return 0;
 }
 
 extern "C" int r360_frame_upload(r360_frame* f, const uint8_t* bgr8, const uint16_t* depth8) {
@@ -665,24 +697,21 @@ extern "C" int r360_frame_upload(r360_frame* f, const uint8_t* bgr8, const uint1
     if (f && bind_device(f->ctx->device)) return -1;
     CHECK_ARG(f->rows > 0, "a sphere-only frame has no sensor images");
     planes_join(f);   // a plane stage still reading the images (a plane queue's batch) ends first
-    const size_t ns = (size_t)8 * f->rows * f->cols;
-    R360_HIP(hipMemcpyAsync(f->d_bgr, bgr8, ns * 3, hipMemcpyHostToDevice, f->ctx->stream));
-    R360_HIP(hipMemcpyAsync(f->d_depth, depth8, ns * 2, hipMemcpyHostToDevice, f->ctx->stream));
+    if (frame_copy_images(f, bgr8, depth8, hipMemcpyHostToDevice)) return -1;
     R360_HIP(hipStreamSynchronize(f->ctx->stream));
+    R360_HIP(hipEventSynchronize(f->bgr_ev));
     f->built = 0;
     return 0;
 }
 
-// Enqueued on the ctx stream; the host buffers must stay valid until the stream reaches the copies
-// (page-locked buffers, r360_host_register, make the copies truly asynchronous).
+// Enqueued on the ctx stream (and its upload stream); the host buffers must stay valid until the streams reach the
+// copies (page-locked buffers, r360_host_register, make the copies truly asynchronous).
 extern "C" int r360_frame_upload_async(r360_frame* f, const uint8_t* bgr8, const uint16_t* depth8) {
     CHECK_ARG(f && bgr8 && depth8, "null arg");
     if (f && bind_device(f->ctx->device)) return -1;
     CHECK_ARG(f->rows > 0, "a sphere-only frame has no sensor images");
     planes_join(f);   // a plane stage still reading the images (a plane queue's batch) ends first
-    const size_t ns = (size_t)8 * f->rows * f->cols;
-    R360_HIP(hipMemcpyAsync(f->d_bgr, bgr8, ns * 3, hipMemcpyHostToDevice, f->ctx->stream));
-    R360_HIP(hipMemcpyAsync(f->d_depth, depth8, ns * 2, hipMemcpyHostToDevice, f->ctx->stream));
+    if (frame_copy_images(f, bgr8, depth8, hipMemcpyHostToDevice)) return -1;
     f->built = 0;
     return 0;
 }
@@ -723,7 +752,9 @@ extern "C" int r360_frame_upload_device(r360_frame* f, const void* d_bgr8, const
     CHECK_ARG(f->rows > 0, "a sphere-only frame has no sensor images");
     planes_join(f);   // a plane stage still reading the images (a plane queue's batch) ends first
     const size_t ns = (size_t)8 * f->rows * f->cols;
+    R360_HIP(hipStreamWaitEvent(f->ctx->stream, f->bgr_ev, 0));   // an earlier split copy into d_bgr
     R360_HIP(hipMemcpyAsync(f->d_bgr, d_bgr8, ns * 3, hipMemcpyDeviceToDevice, f->ctx->stream));
+    R360_HIP(hipEventRecord(f->bgr_ev, f->ctx->stream));
     R360_HIP(hipMemcpyAsync(f->d_depth, d_depth8, ns * 2, hipMemcpyDeviceToDevice, f->ctx->stream));
     f->built = 0;
     return 0;

@@ -27,9 +27,9 @@ constexpr int kOrdMinInit = 0x7f7f7f7f;            // memset byte 0x7f: above ev
 constexpr int kOrdMaxInit = (int)0x80808080;       // memset byte 0x80: below every finite float
 
 // one output point of k_cloud; returns its z
-__device__ __forceinline__ float cloud_point_impl(const float* __restrict__ depth_m, const uint8_t* __restrict__ bgr, int rows,
-                                  int cols, float inv_f, float ox, float oy, float4* __restrict__ cloud,
-                                  uchar4* __restrict__ rgb, long i, int w, long N, float nan) {
+__device__ __forceinline__ float cloud_point_impl(const float* __restrict__ depth_m, int rows, int cols, float inv_f,
+                                                  float ox, float oy, float4* __restrict__ cloud, long i, int w, long N,
+                                                  float nan) {
     {
         const int s = (int)(i / N);
         const int j = (int)(i - (long)s * N);
@@ -67,16 +67,13 @@ __device__ __forceinline__ float cloud_point_impl(const float* __restrict__ dept
             else
                 o = make_float4(nan, nan, nan, 0.f);
         }
-        cloud[i] = o;
-        const uint8_t* b = bgr + ((long)s * rows * cols + (long)(r + 1) * cols + c + 1) * 3;
-        rgb[i] = make_uchar4(b[2], b[1], b[0], 0);
+        cloud[i] = o;   // its colour: k_rgb (the BGR images may still be on their way, r360_ctx::split_upload)
         return o.z;
     }
 }
 
-__device__ __forceinline__ void d_cloud(const float* __restrict__ depth_m, const uint8_t* __restrict__ bgr, int rows, int cols,
-                        float inv_f, float ox, float oy, float4* __restrict__ cloud, uchar4* __restrict__ rgb,
-                        int* __restrict__ zmm, int* __restrict__ wmm) {
+__device__ __forceinline__ void d_cloud(const float* __restrict__ depth_m, int rows, int cols, float inv_f, float ox,
+                                        float oy, float4* __restrict__ cloud, int* __restrict__ zmm, int* __restrict__ wmm) {
     const int w = cols / 2, h = rows / 2;
     const long N = (long)w * h, total = 8 * N;
     const float nan = __builtin_nanf("");
@@ -87,7 +84,7 @@ __device__ __forceinline__ void d_cloud(const float* __restrict__ depth_m, const
         int emin = kOrdMinInit, emax = kOrdMaxInit;
         const int s0 = (int)(i0 / N);
         if (i < total) {
-            const float z = cloud_point_impl(depth_m, bgr, rows, cols, inv_f, ox, oy, cloud, rgb, i, w, N, nan);
+            const float z = cloud_point_impl(depth_m, rows, cols, inv_f, ox, oy, cloud, i, w, N, nan);
             if (isfin(z)) { emin = f2ord(z); emax = emin; }
         }
         const bool one_sensor = (i0 + 63 < total) && ((i0 + 63) / N == s0);
@@ -109,7 +106,22 @@ __device__ __forceinline__ void d_cloud(const float* __restrict__ depth_m, const
 }
 __global__ void k_cloud(const PlaneBatch B, int rows, int cols, float inv_f, float ox, float oy) {
     const PlaneDev& D = B.f[blockIdx.z];
-    d_cloud(D.depth_m, D.bgr, rows, cols, inv_f, ox, oy, D.cloud, D.rgb, D.zmm, reinterpret_cast<int*>(D.dist0));
+    d_cloud(D.depth_m, rows, cols, inv_f, ox, oy, D.cloud, D.zmm, reinterpret_cast<int*>(D.dist0));
+}
+
+// the organized clouds' colours: point (r2, c2) of a sensor takes the BGR pixel (2 r2 + 1, 2 c2 + 1) as {r, g, b, 0}
+// (CloudRGBD_Ext.h:78-139, DownsampleRGBD.h:209-311: the centre pixel of the 2x2 block)
+__global__ void k_rgb(const PlaneBatch B, int rows, int cols) {
+    const PlaneDev& D = B.f[blockIdx.z];
+    const int w = cols / 2, h = rows / 2;
+    const long N = (long)w * h, total = 8 * N;
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+        const int s = (int)(i / N);
+        const int j = (int)(i - (long)s * N);
+        const int r2 = j / w, c2 = j - r2 * w;
+        const uint8_t* b = D.bgr + ((long)s * rows * cols + (long)(2 * r2 + 1) * cols + 2 * c2 + 1) * 3;
+        D.rgb[i] = make_uchar4(b[2], b[1], b[0], 0);
+    }
 }
 
 
@@ -783,6 +795,14 @@ __global__ void __launch_bounds__(NT_TPB) k_normals_sat(const PlaneBatch B, int 
 }  // namespace
 
 // ------------------------------------------------------------------ launchers
+int launch_rgb(const PlaneBatch& B, int F, const PlaneGeom& G, hipStream_t st) {
+    const long tot = 8L * G.w * G.h;
+    const int blocks = (int)std::min<long>((tot + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_rgb, dim3(blocks, 1, (unsigned)F), dim3(256), 0, st, B, G.rows, G.cols);
+    R360_HIP(hipGetLastError());
+    return 0;
+}
+
 int launch_cloud_normals(const PlaneBatch& B, int F, const PlaneGeom& G, hipStream_t st, r360_ctx* tctx) {
     const int w = G.w, h = G.h;
     const long tot = 8L * w * h;

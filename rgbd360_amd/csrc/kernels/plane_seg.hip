@@ -2393,7 +2393,8 @@ int launch_gm(int px, long total, const PlaneBatch& B, int F, hipStream_t st, in
     return -1;
 }
 
-int launch_segmentation(const PlaneBatch& B, int F, const PlaneGeom& G, hipStream_t st, r360_ctx* tctx) {
+int launch_segmentation(const PlaneBatch& B, int F, const PlaneGeom& G, hipStream_t st, r360_ctx* tctx,
+                        const hipEvent_t* bgr_ev) {
     const int w = G.w, h = G.h, N = w * h;
     const long total = 8L * N;
     const int blocks = (int)((total + 255) / 256);
@@ -2432,6 +2433,11 @@ int launch_segmentation(const PlaneBatch& B, int F, const PlaneGeom& G, hipStrea
     timing_end(tctx, slot);
     R360_HIP(hipGetLastError());
     slot = timing_begin(tctx, "k_model_stats");
+    // the colours: the first kernel of the stage that reads the BGR images (a split upload copies them beside the
+    // geometric part above)
+    for (int j = 0; bgr_ev && j < F; ++j)
+        if (bgr_ev[j]) R360_HIP(hipStreamWaitEvent(st, bgr_ev[j], 0));
+    if (launch_rgb(B, F, G, st)) return -1;
     if (launch_gm<true>(gm_px, total, B, F, st, N)) return -1;
     // the refinement's closeness masks are dead here: their storage holds the neighbour masks
     hipLaunchKernelGGL(k_nbmask, dim3(std::max(blocks, 20 * 8 * R360_MAX_MODELS / 256), 1, nf), dim3(256), 0, st, B, w, h);

@@ -351,6 +351,12 @@ struct r360_ctx {
     // assembly tasks (pbmap.cpp planes_join): the latency of a lone frame.  The queued sequence runner turns it off
     // for its pipelines (their waits would spin host cores the other pipelines' frames need)
     bool join_help = true;
+    // with split_upload (the same latency-bound callers) r360_frame_upload_async copies the depth images first on the
+    // ctx stream and the BGR images after them on up_stream, beside the plane stage's geometric part, which needs only
+    // the depth; the stage waits for the BGR images (f->bgr_ev) just before its colour moments
+    bool split_upload = true;
+    hipStream_t up_stream = nullptr;
+    hipEvent_t up_ev = nullptr;
     std::vector<hipEvent_t> ev_pool;
     int ev_used = 0;
     struct TimedLaunch { std::string name; int a, b; };
@@ -447,6 +453,9 @@ struct r360_frame {
     const r360_calib* calib = nullptr;
     int rows = 0, cols = 0, sph_rows = 0, sph_cols = 0, n_levels = 0;
     uint8_t* d_bgr = nullptr;      // [8][rows][cols][3]
+    // recorded on the stream that last wrote d_bgr (r360_frame_upload*, the loaders): its readers (the stitch, the
+    // sensor pyramid, the plane stage's colours) wait on it; a never-recorded event does not hold a wait
+    hipEvent_t bgr_ev = nullptr;
     uint16_t* d_depth = nullptr;   // [8][rows][cols] mm
     float* d_depth_m = nullptr;    // [8][rows][cols] undistorted metres
     int* d_npts = nullptr;         // [R360_MAX_PYR] valid source points per level (LevelBufs::pts)
@@ -542,7 +551,10 @@ int ctx_wait_frames(r360_ctx* ctx, r360_frame* const* frames, int n);
 struct PlaneGeom { int rows, cols, w, h, sd_max; long grid_cells; };
 PlaneGeom plane_geom(const r360_frame* f);
 int launch_cloud_normals(const PlaneBatch& B, int F, const PlaneGeom& G, hipStream_t st, r360_ctx* tctx);
-int launch_segmentation(const PlaneBatch& B, int F, const PlaneGeom& G, hipStream_t st, r360_ctx* tctx);
+// bgr_ev: the F frames' BGR events (nullptr: none), waited on before the colour moments (launch_rgb, k_gm<true>)
+int launch_segmentation(const PlaneBatch& B, int F, const PlaneGeom& G, hipStream_t st, r360_ctx* tctx,
+                        const hipEvent_t* bgr_ev);
+int launch_rgb(const PlaneBatch& B, int F, const PlaneGeom& G, hipStream_t st);   // the clouds' colours (P.rgb)
 int launch_plane_publish(const PlaneBatch& B, int F, hipStream_t st);   // plane outputs -> pinned host buffers
 // voxel-fallback scratch the plane stage of one frame uses (its context's, or a plane queue slot's)
 struct VoxScratch { VoxCell* vhash; unsigned long long cap; int* vlist; int* vcnt; };
