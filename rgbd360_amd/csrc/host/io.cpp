@@ -94,12 +94,12 @@ extern "C" int r360_frame_load_bin(r360_frame* f, const char* path) {
         }
     planes_join(f);   // a plane stage still reading the images (a plane queue's batch) ends first
     hipStream_t st = f->ctx->stream;
-    R360_HIP(hipStreamWaitEvent(st, f->bgr_ev, 0));   // a split upload's BGR copy still writing d_bgr
+    if (hipEvent_t e = f->bgr_wait()) R360_HIP(hipStreamWaitEvent(st, e, 0));   // a split upload's copy in flight
     for (int s = 0; s < 8; ++s) {
         R360_HIP(hipMemcpyAsync(f->d_bgr + s * npx * 3, b + moff[s][0], npx * 3, hipMemcpyHostToDevice, st));
         R360_HIP(hipMemcpyAsync(f->d_depth + s * npx, b + moff[s][1], npx * 2, hipMemcpyHostToDevice, st));
     }
-    R360_HIP(hipEventRecord(f->bgr_ev, st));
+    f->bgr_split = false;
     // the timestamp mat (Frame360.h:244-247); loadFrame swallows archive errors here, so a missing
     // or malformed one leaves the timestamp at 0
     uint64_t ts = 0;
@@ -137,7 +137,7 @@ extern "C" int r360_frame_save_bin(r360_frame* f, const char* path) {
     const size_t npx = (size_t)f->rows * f->cols;
     std::vector<uint8_t> bgr(8 * npx * 3);
     std::vector<uint16_t> depth(8 * npx);
-    R360_HIP(hipStreamWaitEvent(f->ctx->stream, f->bgr_ev, 0));
+    if (hipEvent_t e = f->bgr_wait()) R360_HIP(hipStreamWaitEvent(f->ctx->stream, e, 0));
     R360_HIP(hipMemcpyAsync(bgr.data(), f->d_bgr, bgr.size(), hipMemcpyDeviceToHost, f->ctx->stream));
     R360_HIP(hipMemcpyAsync(depth.data(), f->d_depth, depth.size() * 2, hipMemcpyDeviceToHost, f->ctx->stream));
     R360_HIP(hipStreamSynchronize(f->ctx->stream));

@@ -499,6 +499,47 @@ int planes_launch(const PlaneBatch& B, int F, const PlaneGeom& G, hipStream_t st
 }
 
 
+// One part of a lone frame's plane stage as a graph (0: cloud, filter, normals, segmentation, refinement; 1: colours,
+// statistics, contours, voxels, hull prefilter, publication), captured on first use for the frame's buffers and
+// geometry and replayed after: ~40 launches become two, so the stage no longer waits for the host to enqueue it
+// behind a split upload's depth copy.  The kernels and their arguments are those planes_launch enqueues.
+static int plane_graph_launch(r360_ctx* ctx, const PlaneBatch& B, const PlaneGeom& G, int part) {
+    std::string key(reinterpret_cast<const char*>(&B.f[0]), sizeof(PlaneDev));
+    const long gk[7] = {G.rows, G.cols, G.w, G.h, G.sd_max, G.grid_cells, part};
+    key.append(reinterpret_cast<const char*>(gk), sizeof gk);
+    ++ctx->graph_clock;
+    for (auto& g : ctx->plane_graphs)
+        if (g.key == key) {
+            g.used = ctx->graph_clock;
+            R360_HIP(hipGraphLaunch(g.exec, ctx->stream));
+            return 0;
+        }
+    hipGraph_t graph = nullptr;
+    R360_HIP(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeRelaxed));
+    int rc = 0;
+    if (part == 0) rc = launch_cloud_normals(B, 1, G, ctx->stream, nullptr) ? -1 : launch_segmentation_geom(B, 1, G, ctx->stream, nullptr);
+    else rc = launch_segmentation_model(B, 1, G, ctx->stream, nullptr) ? -1 : launch_plane_publish(B, 1, ctx->stream);
+    const hipError_t ec = hipStreamEndCapture(ctx->stream, &graph);
+    if (rc) { if (graph) (void)hipGraphDestroy(graph); return rc; }
+    R360_HIP(ec);
+    hipGraphExec_t exec = nullptr;
+    const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    R360_HIP(ei);
+    constexpr size_t kMaxGraphs = 8;   // two parts for each of a few rotating frame buffers
+    if (ctx->plane_graphs.size() >= kMaxGraphs) {
+        size_t lru = 0;
+        for (size_t i = 1; i < ctx->plane_graphs.size(); ++i)
+            if (ctx->plane_graphs[i].used < ctx->plane_graphs[lru].used) lru = i;
+        R360_HIP(hipStreamSynchronize(ctx->stream));   // the evicted graph may still be running
+        (void)hipGraphExecDestroy(ctx->plane_graphs[lru].exec);
+        ctx->plane_graphs.erase(ctx->plane_graphs.begin() + (long)lru);
+    }
+    ctx->plane_graphs.push_back({std::move(key), exec, ctx->graph_clock});
+    R360_HIP(hipGraphLaunch(exec, ctx->stream));
+    return 0;
+}
+
 // GPU part of getPlanes: cloud, filter, normals, segmentation — enqueued on the frame's ctx stream, or submitted to
 // the ctx's plane queue (batched with other frames on the queue's stream)
 int planes_enqueue(r360_frame* f) {
@@ -518,7 +559,16 @@ int planes_enqueue(r360_frame* f) {
     PlaneBatch B;   // a batch of one (kernel arguments, copied at each launch)
     std::memset(&B, 0, sizeof B);
     B.f[0] = plane_dev(f, VoxScratch{ctx->d_vhash, (unsigned long long)ctx->vhash_cap, ctx->d_vlist, ctx->d_vcnt});
-    if (planes_launch(B, 1, G, ctx->stream, ctx, &f->bgr_ev)) return -1;
+    // experiment builds: R360_NO_PLANE_GRAPH=1 launches a split-upload context's stage kernel by kernel (A/B)
+    static const bool no_graph = R360_KNOB("R360_NO_PLANE_GRAPH", 0) != 0;
+    if (ctx->split_upload && !ctx->timing && !no_graph) {
+        if (plane_graph_launch(ctx, B, G, 0)) return -1;
+        if (hipEvent_t e = f->bgr_wait()) R360_HIP(hipStreamWaitEvent(ctx->stream, e, 0));
+        if (plane_graph_launch(ctx, B, G, 1)) return -1;
+    } else {
+        const hipEvent_t bev = f->bgr_wait();
+        if (planes_launch(B, 1, G, ctx->stream, ctx, &bev)) return -1;
+    }
     R360_HIP(hipEventRecord(P.done, f->ctx->stream));
     return planes_spawn_assembly(f);
 }
@@ -581,7 +631,7 @@ extern "C" int r360_frames_build(r360_frame* const* frames, int n, unsigned flag
             B.f[j] = plane_dev(f, vs);
         }
         std::vector<hipEvent_t> bev;
-        for (r360_frame* f : bf) bev.push_back(f->bgr_ev);
+        for (r360_frame* f : bf) bev.push_back(f->bgr_wait());
         if (planes_launch(B, (int)bf.size(), G, H->stream, H, bev.data())) return -1;
         for (r360_frame* f : bf) {
             R360_HIP(hipEventRecord(f->pl.done, H->stream));

@@ -99,7 +99,7 @@ void dispatcher(r360_plane_queue* q) {
         }
         // per-launch timing (r360_ctx_timing) records on the ctx's stream: the first stream's batches only
         hipEvent_t bev[R360_PLANE_BATCH] = {};
-        for (int j = 0; j < F; ++j) bev[j] = take[j].f->bgr_ev;
+        for (int j = 0; j < F; ++j) bev[j] = take[j].f->bgr_wait();
         if (rc == 0) rc = planes_launch(B, F, G, st, k == 0 ? q->ctx : nullptr, bev);
         for (int j = 0; j < F && rc == 0; ++j)
             if (hipEventRecord(take[j].f->pl.done, st) != hipSuccess) {

@@ -275,6 +275,7 @@ extern "C" void r360_ctx_destroy(r360_ctx* c) {
     hipEventDestroy(c->wait_ev);
     if (c->mwait_ev) hipEventDestroy(c->mwait_ev);   // mstream is the device's shared match stream
     for (auto& g : c->graphs) hipGraphExecDestroy(g.exec);
+    for (auto& g : c->plane_graphs) hipGraphExecDestroy(g.exec);
     hipFree(c->d_state);
     hipFree(c->d_partials);
     hipFree(c->d_gticket);
@@ -667,15 +668,16 @@ extern "C" void r360_frame_destroy(r360_frame* f) {
     delete f;
 }
 
-// The sensor images into the frame.  The depth goes first, on the ctx stream; with ctx->split_upload the BGR images
+// The sensor images into the frame.  With ctx->split_upload the depth goes first, on the ctx stream, and the BGR images
 // follow on the ctx's upload stream, after the depth copy and after everything the ctx stream had enqueued before (the
 // previous build's readers of d_bgr), so the undistortion and the plane stage's geometric part start one copy earlier
-// (the colours are first read by launch_rgb, behind f->bgr_ev).  Otherwise both on the ctx stream.
+// (the colours are first read by launch_rgb, behind f->bgr_ev).  Otherwise both on the ctx stream, and nothing waits
+// on an event (throughput runs: the waits measured 6 % of the headline, profiles/r6_split).
 static int frame_copy_images(r360_frame* f, const void* bgr8, const void* depth8, hipMemcpyKind kind) {
     r360_ctx* ctx = f->ctx;
     const size_t ns = (size_t)8 * f->rows * f->cols;
-    R360_HIP(hipMemcpyAsync(f->d_depth, depth8, ns * 2, kind, ctx->stream));
     if (ctx->split_upload) {
+        R360_HIP(hipMemcpyAsync(f->d_depth, depth8, ns * 2, kind, ctx->stream));
         if (!ctx->up_stream) {
             R360_HIP(hipStreamCreateWithFlags(&ctx->up_stream, hipStreamNonBlocking));
             R360_HIP(hipEventCreateWithFlags(&ctx->up_ev, hipEventDisableTiming));
@@ -684,10 +686,12 @@ static int frame_copy_images(r360_frame* f, const void* bgr8, const void* depth8
         R360_HIP(hipStreamWaitEvent(ctx->up_stream, ctx->up_ev, 0));
         R360_HIP(hipMemcpyAsync(f->d_bgr, bgr8, ns * 3, kind, ctx->up_stream));
         R360_HIP(hipEventRecord(f->bgr_ev, ctx->up_stream));
+        f->bgr_split = true;
     } else {
-        R360_HIP(hipStreamWaitEvent(ctx->stream, f->bgr_ev, 0));   // an earlier split copy into d_bgr
+        if (hipEvent_t e = f->bgr_wait()) R360_HIP(hipStreamWaitEvent(ctx->stream, e, 0));   // an earlier split copy
         R360_HIP(hipMemcpyAsync(f->d_bgr, bgr8, ns * 3, kind, ctx->stream));
-        R360_HIP(hipEventRecord(f->bgr_ev, ctx->stream));
+        R360_HIP(hipMemcpyAsync(f->d_depth, depth8, ns * 2, kind, ctx->stream));
+        f->bgr_split = false;
     }
     return 0;
 }
@@ -699,7 +703,7 @@ extern "C" int r360_frame_upload(r360_frame* f, const uint8_t* bgr8, const uint1
     planes_join(f);   // a plane stage still reading the images (a plane queue's batch) ends first
     if (frame_copy_images(f, bgr8, depth8, hipMemcpyHostToDevice)) return -1;
     R360_HIP(hipStreamSynchronize(f->ctx->stream));
-    R360_HIP(hipEventSynchronize(f->bgr_ev));
+    if (hipEvent_t e = f->bgr_wait()) R360_HIP(hipEventSynchronize(e));
     f->built = 0;
     return 0;
 }
@@ -752,9 +756,9 @@ extern "C" int r360_frame_upload_device(r360_frame* f, const void* d_bgr8, const
     CHECK_ARG(f->rows > 0, "a sphere-only frame has no sensor images");
     planes_join(f);   // a plane stage still reading the images (a plane queue's batch) ends first
     const size_t ns = (size_t)8 * f->rows * f->cols;
-    R360_HIP(hipStreamWaitEvent(f->ctx->stream, f->bgr_ev, 0));   // an earlier split copy into d_bgr
+    if (hipEvent_t e = f->bgr_wait()) R360_HIP(hipStreamWaitEvent(f->ctx->stream, e, 0));   // an earlier split copy
     R360_HIP(hipMemcpyAsync(f->d_bgr, d_bgr8, ns * 3, hipMemcpyDeviceToDevice, f->ctx->stream));
-    R360_HIP(hipEventRecord(f->bgr_ev, f->ctx->stream));
+    f->bgr_split = false;
     R360_HIP(hipMemcpyAsync(f->d_depth, d_depth8, ns * 2, hipMemcpyDeviceToDevice, f->ctx->stream));
     f->built = 0;
     return 0;

@@ -471,7 +471,7 @@ int launch_undistort(r360_frame* f) {
 int launch_stitch(r360_frame* f) {
     const r360_calib* c = f->calib;
     const long n = (long)f->sph_rows * f->sph_cols;
-    R360_HIP(hipStreamWaitEvent(f->ctx->stream, f->bgr_ev, 0));   // the BGR images (a split upload's second copy)
+    if (hipEvent_t e = f->bgr_wait()) R360_HIP(hipStreamWaitEvent(f->ctx->stream, e, 0));   // a split upload's BGR copy
     const int slot = timing_begin(f->ctx, "k_stitch");
     // experiment builds: R360_STITCH=4 forces the row-major k_stitch4
     static const int form = R360_KNOB("R360_STITCH", 0);
@@ -702,7 +702,7 @@ int launch_sensor_pyramid(r360_frame* f) {
         r360_set_error("sensor images of %d x %d pixels are too large", f->rows, f->cols);
         return -1;
     }
-    R360_HIP(hipStreamWaitEvent(st, f->bgr_ev, 0));   // the BGR images (a split upload's second copy)
+    if (hipEvent_t e = f->bgr_wait()) R360_HIP(hipStreamWaitEvent(st, e, 0));   // a split upload's BGR copy
     hipLaunchKernelGGL(k_sensor_level0, dim3(grid_for(n0)), dim3(TPB), 0, st, f->d_bgr, f->d_depth, n0, f->sp[0].p0,
                        (uint32_t*)nullptr);
     for (int l = 1; l < f->n_slevels; ++l) {

@@ -2393,8 +2393,8 @@ int launch_gm(int px, long total, const PlaneBatch& B, int F, hipStream_t st, in
     return -1;
 }
 
-int launch_segmentation(const PlaneBatch& B, int F, const PlaneGeom& G, hipStream_t st, r360_ctx* tctx,
-                        const hipEvent_t* bgr_ev) {
+// the geometric part: connected components, plane fits, refinement (depth / normals only)
+int launch_segmentation_geom(const PlaneBatch& B, int F, const PlaneGeom& G, hipStream_t st, r360_ctx* tctx) {
     const int w = G.w, h = G.h, N = w * h;
     const long total = 8L * N;
     const int blocks = (int)((total + 255) / 256);
@@ -2432,11 +2432,18 @@ int launch_segmentation(const PlaneBatch& B, int F, const PlaneGeom& G, hipStrea
     hipLaunchKernelGGL(k_refine_final, dim3(blocks, 1, nf), dim3(256), 0, st, B, N);
     timing_end(tctx, slot);
     R360_HIP(hipGetLastError());
-    slot = timing_begin(tctx, "k_model_stats");
-    // the colours: the first kernel of the stage that reads the BGR images (a split upload copies them beside the
-    // geometric part above)
-    for (int j = 0; bgr_ev && j < F; ++j)
-        if (bgr_ev[j]) R360_HIP(hipStreamWaitEvent(st, bgr_ev[j], 0));
+    return 0;
+}
+
+// the model part: the clouds' colours (the first kernel of the stage that reads the BGR images), the regions'
+// statistics, contours, the voxel fallback and the hull prefilter
+int launch_segmentation_model(const PlaneBatch& B, int F, const PlaneGeom& G, hipStream_t st, r360_ctx* tctx) {
+    const int w = G.w, h = G.h, N = w * h;
+    const long total = 8L * N;
+    const int blocks = (int)((total + 255) / 256);
+    const unsigned nf = (unsigned)F;
+    static const int gm_px = R360_KNOB("R360_GM_PX", GM_PX);
+    int slot = timing_begin(tctx, "k_model_stats");
     if (launch_rgb(B, F, G, st)) return -1;
     if (launch_gm<true>(gm_px, total, B, F, st, N)) return -1;
     // the refinement's closeness masks are dead here: their storage holds the neighbour masks
@@ -2459,6 +2466,15 @@ int launch_segmentation(const PlaneBatch& B, int F, const PlaneGeom& G, hipStrea
     timing_end(tctx, slot);
     R360_HIP(hipGetLastError());
     return 0;
+}
+
+int launch_segmentation(const PlaneBatch& B, int F, const PlaneGeom& G, hipStream_t st, r360_ctx* tctx,
+                        const hipEvent_t* bgr_ev) {
+    if (launch_segmentation_geom(B, F, G, st, tctx)) return -1;
+    // a split upload copies the BGR images beside the geometric part
+    for (int j = 0; bgr_ev && j < F; ++j)
+        if (bgr_ev[j]) R360_HIP(hipStreamWaitEvent(st, bgr_ev[j], 0));
+    return launch_segmentation_model(B, F, G, st, tctx);
 }
 
 // hash cells (a bound on a frame's distinct (region, voxel) cells, k_alloc), and the claimed-cell lists of

@@ -341,6 +341,10 @@ struct r360_ctx {
     struct AlignGraph { std::vector<uintptr_t> key; hipGraphExec_t exec = nullptr; unsigned long long used = 0; };
     std::vector<AlignGraph> graphs;
     unsigned long long graph_clock = 0;
+    // a lone frame's plane stage (split_upload contexts) replayed as two graphs, the geometric part and the model part
+    // (the BGR wait between them), keyed by the frame's plane buffers and geometry (pbmap.cpp plane_graph_launch)
+    struct PlaneGraph { std::string key; hipGraphExec_t exec = nullptr; unsigned long long used = 0; };
+    std::vector<PlaneGraph> plane_graphs;
     IcpState* h_state = nullptr;  // pinned
     int timing = 0;
     r360_ctx* stats_sibling = nullptr;   // a dense queue's second stream: its kernel statistics are reported with these
@@ -453,9 +457,12 @@ struct r360_frame {
     const r360_calib* calib = nullptr;
     int rows = 0, cols = 0, sph_rows = 0, sph_cols = 0, n_levels = 0;
     uint8_t* d_bgr = nullptr;      // [8][rows][cols][3]
-    // recorded on the stream that last wrote d_bgr (r360_frame_upload*, the loaders): its readers (the stitch, the
-    // sensor pyramid, the plane stage's colours) wait on it; a never-recorded event does not hold a wait
+    // bgr_split: the last write of d_bgr was a split upload's copy on the ctx's upload stream (r360_ctx::split_upload),
+    // recorded on bgr_ev; its readers (the stitch, the sensor pyramid, the plane stage's colours) and the next writer
+    // wait on bgr_ev.  Otherwise d_bgr is written in the ctx stream's order and nothing waits (bgr_wait: nullptr)
     hipEvent_t bgr_ev = nullptr;
+    bool bgr_split = false;
+    hipEvent_t bgr_wait() const { return bgr_split ? bgr_ev : nullptr; }
     uint16_t* d_depth = nullptr;   // [8][rows][cols] mm
     float* d_depth_m = nullptr;    // [8][rows][cols] undistorted metres
     int* d_npts = nullptr;         // [R360_MAX_PYR] valid source points per level (LevelBufs::pts)
@@ -555,6 +562,8 @@ int launch_cloud_normals(const PlaneBatch& B, int F, const PlaneGeom& G, hipStre
 int launch_segmentation(const PlaneBatch& B, int F, const PlaneGeom& G, hipStream_t st, r360_ctx* tctx,
                         const hipEvent_t* bgr_ev);
 int launch_rgb(const PlaneBatch& B, int F, const PlaneGeom& G, hipStream_t st);   // the clouds' colours (P.rgb)
+int launch_segmentation_geom(const PlaneBatch& B, int F, const PlaneGeom& G, hipStream_t st, r360_ctx* tctx);
+int launch_segmentation_model(const PlaneBatch& B, int F, const PlaneGeom& G, hipStream_t st, r360_ctx* tctx);
 int launch_plane_publish(const PlaneBatch& B, int F, hipStream_t st);   // plane outputs -> pinned host buffers
 // voxel-fallback scratch the plane stage of one frame uses (its context's, or a plane queue slot's)
 struct VoxScratch { VoxCell* vhash; unsigned long long cap; int* vlist; int* vcnt; };

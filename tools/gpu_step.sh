@@ -77,6 +77,15 @@ print(json.dumps(out))" > $O/seq.json 2> $O/seq.err || { tail -20 $O/seq.err; ex
           echo "== [${ARMS[$i]}] rep $rep"; python3 tools/bench_line.py $O/arg_${i}_$rep.json | head -1
         done
       done ;;
+    libab)  # the default sequence line (quick legs) alternating libraries, LIBAB="name1|name2" (rgbd360_amd/lib/librgbd360_<name>.so)
+      IFS='|' read -ra LIBS <<< "${LIBAB:?LIBAB=name1|name2}"
+      for rep in 1 2; do
+        for l in "${LIBS[@]}"; do
+          R360_LIB=$R/rgbd360_amd/lib/librgbd360_$l.so timeout -k 10 200 python -u bench.py $Q > $O/lib_${l}_$rep.json \
+            2> $O/lib_${l}_$rep.err || { tail -20 $O/lib_${l}_$rep.err; exit 14; }
+          echo "== $l rep $rep"; python3 tools/bench_line.py $O/lib_${l}_$rep.json | head -2
+        done
+      done ;;
     pfab)   # level-0 pass forms / occupancy: dense-alone VGA and config 5, per experiment library:PF (PFAB="exp:6 minb4:7")
       for spec in ${PFAB:-exp:6 minb4:7 minb4:6}; do
         lib=${spec%%:*}; pf=${spec##*:}; n=${lib}_pf$pf
