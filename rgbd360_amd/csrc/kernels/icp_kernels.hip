@@ -2563,14 +2563,17 @@ int launch_icp_levels_batch(r360_ctx* ctx, const IcpJobs& jobs, int n, const r36
     (void)ctx; (void)jobs; (void)n; (void)geom; (void)level; (void)method; (void)C0; (void)passes;
     return 1;
 #else
-    constexpr int R360_COARSE_WG = 64;
+    // R360_COARSE_WG: workgroups per job (1: no hand-off waits at all); R360_COARSE_MIN_LEVEL: the finest level run
+    // this way (the finer ones pass by pass)
+    static const int coarse_wg = R360_KNOB("R360_COARSE_WG", 64);
+    static const int coarse_min = R360_KNOB("R360_COARSE_MIN_LEVEL", 1);
     static const bool persist = R360_KNOB("R360_COARSE_PERSIST", 0) != 0;
-    if (level == 0 || C0.occ || !persist || !R360_PERSIST_BUILT) return 1;
+    if (level == 0 || level < coarse_min || C0.occ || !persist || !R360_PERSIST_BUILT) return 1;
     if (n < 1 || n > R360_MAX_BATCH) { r360_set_error("batched passes: %d jobs (1..%d)", n, R360_MAX_BATCH); return -2; }
     const LevelBufs& Ls = geom->lv[level];
     PassGrid G = pass_grid(ctx, Ls, 0, n, true);
     if (G.pf != 8 && G.pf != 9) return 1;
-    if (G.nb > R360_COARSE_WG) G.nb = R360_COARSE_WG;
+    if (G.nb > coarse_wg) G.nb = coarse_wg;
     if (ctx->bdefer_cap < defer_need(Ls.rows * Ls.cols, G.nb)) {
         r360_set_error("batched passes: deferred-pixel queues not sized for %d pixels", Ls.rows * Ls.cols);
         return -1;

@@ -35,14 +35,13 @@ import json, sys; sys.argv=['bench.py']; import numpy as np, bench, rgbd360_amd 
 rt8 = np.stack([np.loadtxt(f'{R.EXTRINSICS_DIR}/Rt_0{k + 1}.txt', dtype=np.float32) for k in range(8)])
 print(json.dumps(bench.config5_leg(0, rt8)))" > $O/c5.json 2> $O/c5.err || { tail -20 $O/c5.err; exit 6; }
       python3 -c "import json; d=json.load(open('$O/c5.json')); r=d['roofline']; print('config5', round(d['value'],1), 'pairs/s frac', round(r['frac'],3), 'L0', round(r['avg_launch_ms']*1e3,1), 'us/launch', round(r['pairs_per_launch'],2), 'pairs/launch')" ;;
-    envab)  # the default sequence line (quick legs) alternating two environments of the experiment library, ENVAB="A|B"
-      IFS='|' read -r EA EB <<< "${ENVAB:?ENVAB=envA|envB}"
+    envab)  # the default sequence line (quick legs) over environments of the experiment library, ENVAB="env1|env2|...", twice each
+      IFS='|' read -ra ENVS <<< "${ENVAB:?ENVAB=env1|env2}"
       for rep in 1 2; do
-        for arm in A B; do
-          e=$EA; [ $arm = B ] && e=$EB
-          env R360_LIB=$R/rgbd360_amd/lib/librgbd360_hip_exp.so $e timeout -k 10 200 python -u bench.py $Q \
-            > $O/ab_${arm}_$rep.json 2> $O/ab_${arm}_$rep.err || { tail -20 $O/ab_${arm}_$rep.err; exit 10; }
-          echo "== $arm ($e) rep $rep"; python3 tools/bench_line.py $O/ab_${arm}_$rep.json | head -2
+        for i in "${!ENVS[@]}"; do
+          env R360_LIB=$R/rgbd360_amd/lib/librgbd360_hip_exp.so ${ENVS[$i]} timeout -k 10 200 python -u bench.py $Q \
+            > $O/ab_${i}_$rep.json 2> $O/ab_${i}_$rep.err || { tail -20 $O/ab_${i}_$rep.err; exit 10; }
+          echo "== [${ENVS[$i]}] rep $rep"; python3 tools/bench_line.py $O/ab_${i}_$rep.json | head -2
         done
       done ;;
     trace)  # kernel trace of the default sequence line (quick legs): dense-stream gaps, GPU busy, per-kernel stats
