@@ -263,6 +263,20 @@ bool boxes_apart(const HPlane& A, const HPlane& B, float thr) {
     return g2 > lim * lim;
 }
 
+// The same bound per segment pair: segments whose boxes are farther apart than lim (threshold + 1e-4 m) have no pair
+// of points within the threshold, so their seg_dist2 could not pass the test (round 6: most segment pairs of two
+// neighbouring planes that do not touch)
+bool segs_apart(const P3& a0, const P3& a1, const P3& b0, const P3& b1, double lim2) {
+    double g2 = 0;
+    for (int k = 0; k < 3; ++k) {
+        const float alo = std::min(a0.at(k), a1.at(k)), ahi = std::max(a0.at(k), a1.at(k));
+        const float blo = std::min(b0.at(k), b1.at(k)), bhi = std::max(b0.at(k), b1.at(k));
+        const double g = std::max({0.0, (double)blo - ahi, (double)alo - bhi});
+        g2 += g * g;
+    }
+    return g2 > lim2;
+}
+
 bool nearby(const HPlane& A, const HPlane& B, float thr) {
     if (boxes_apart(A, B, thr)) return false;
     const float t2 = thr * thr;
@@ -274,9 +288,12 @@ bool nearby(const HPlane& A, const HPlane& B, float thr) {
     for (size_t i = 1; i < A.hull.size(); i++)
         for (size_t j = 1; j < B.hull.size(); j++)
             if (norm2(minus(A.hull[i], B.hull[j])) < t2) return true;
+    const double lim = (double)thr + 1e-4, lim2 = lim * lim;
     for (size_t i = 1; i < A.hull.size(); i++)
         for (size_t j = 1; j < B.hull.size(); j++)
-            if (seg_dist2(A.hull[i], A.hull[i - 1], B.hull[j], B.hull[j - 1]) < t2) return true;
+            if (!segs_apart(A.hull[i], A.hull[i - 1], B.hull[j], B.hull[j - 1], lim2) &&
+                seg_dist2(A.hull[i], A.hull[i - 1], B.hull[j], B.hull[j - 1]) < t2)
+                return true;
     return false;
 }
 
@@ -313,8 +330,10 @@ bool hulls_touch(const HPlane& A, const HPlane& B, float max_dist, float max_nor
             const P3 diff = minus(A.hull[i], B.hull[ii]);
             if (std::sqrt(norm2(diff)) < max_dist && std::fabs(dot(A.normal, diff)) < max_normal_off) return true;
         }
+    const double lim = (double)max_dist + 1e-4, lim2 = lim * lim;
     for (size_t i = 1; i < A.hull.size(); i++)
         for (size_t ii = 1; ii < B.hull.size(); ii++) {
+            if (segs_apart(A.hull[i], A.hull[i - 1], B.hull[ii], B.hull[ii - 1], lim2)) continue;
             const float dist = std::sqrt(seg_dist2(A.hull[i], A.hull[i - 1], B.hull[ii], B.hull[ii - 1]));
             if (dist < max_dist) {
                 const P3 diff = minus(A.hull[i], B.hull[ii]);

@@ -1083,7 +1083,9 @@ __device__ __forceinline__ int icp_pass_body(const IcpJobs& jobs, const float* _
                 acc(o, gt.g(o.t), gt.T(o.t));
             }
         }
-    } else if (PF == 6) {
+    } else if (PF == 6 || PF == 10) {
+        // (PF 10, experiment builds: the same body without the two-chunk software pipeline, at R360_PF10_MINB waves per
+        // SIMD: latency hidden by more waves instead of a second chunk in flight)
         // Level 0 from the PACKED level-0 images (LevelBufs::pk, 4 B per pixel: range mm | luma << 16): the
         // source is streamed as the image itself, one wave = 64 consecutive pixels of one row (nCols % 64 == 0),
         // and the target {gray, depth} is gathered from the target's packed image (4 B instead of 8).  Per pass
@@ -1189,6 +1191,16 @@ __device__ __forceinline__ int icp_pass_body(const IcpJobs& jobs, const float* _
             cur_r = __builtin_amdgcn_readfirstlane(row_of(b0));
             cur_c = b0 - cur_r * nCols;
             auto base = [&](int k) { return b0 + (k < n_it ? k : n_it - 1) * stride; };
+            if constexpr (PF == 10) {
+                for (int k = 0; k < n_it; ++k) {
+                    const Src sx = ld();
+                    Proj ox = prj(sx);
+                    defer(ox, base(k));
+                    const float4 Gx = gG(ox.t);
+                    const unsigned Tx = gT(ox.t);
+                    acc(ox, Gx, Tx);
+                }
+            } else {
             Src sA = ld();
             Src sB = ld();
             Proj oA = prj(sA);
@@ -1210,6 +1222,7 @@ __device__ __forceinline__ int icp_pass_body(const IcpJobs& jobs, const float* _
                 TA = gT(oA.t);
                 acc(oB, GB, TB);
                 if (k + 2 >= n_it) break;
+            }
             }
         }
         // the workgroup's deferred lanes, drained together (as PF 5)
@@ -1836,7 +1849,10 @@ __device__ __forceinline__ int icp_pass_body(const IcpJobs& jobs, const float* _
 // PF 9 (coarse levels whose rows do not split into whole waves: per-lane rows, one more table pair live) at 4 waves per
 // SIMD: at 5 its pipelined chunks spilled 20 B per lane; the levels it serves are the two smallest
 template <int METHOD, int PF, int TOP, int OCC>
-__global__ __launch_bounds__(TPB, PF == 9 ? 4 : R360_ICP_MINB) void k_icp_pass(const IcpJobs jobs, const float* __restrict__ sinphi,
+#ifndef R360_PF10_MINB
+#define R360_PF10_MINB 6
+#endif
+__global__ __launch_bounds__(TPB, PF == 9 ? 4 : PF == 10 ? R360_PF10_MINB : R360_ICP_MINB) void k_icp_pass(const IcpJobs jobs, const float* __restrict__ sinphi,
                                                  const float* __restrict__ cosphi, const float* __restrict__ sinth,
                                                  const float* __restrict__ costh, int nRows, int nCols,
                                                  IcpConst C, int first, int eval_only,
@@ -2457,7 +2473,7 @@ static PassGrid pass_grid(const r360_ctx* ctx, const LevelBufs& Ls, int occ, int
     const bool img_ok = !pk_ok && Ls.cols >= 64 && !coarse_pf5;
     const int pf_img = pk_ok ? 6 : img_ok ? (Ls.cols % 64 == 0 ? 8 : 9) : 5;
     const int pf_dflt = occ ? ((Ls.cols % 64 == 0) ? 3 : 0) : (batched || !pts ? pf_img : 5);
-    const bool env_ok = pf_env >= 0 && !(pf_env >= 4 && occ) && !((pf_env == 6 || pf_env == 7) && !pk_ok) &&
+    const bool env_ok = pf_env >= 0 && !(pf_env >= 4 && occ) && !((pf_env == 6 || pf_env == 7 || pf_env == 10) && !pk_ok) &&
                         !(pf_env == 8 && Ls.cols % 64 != 0) && !(pf_env == 9 && Ls.cols < 64);
     const int pf = R360_EXPERIMENTS && env_ok ? pf_env : pf_dflt;
     // workgroups per job and pass: 2 per CU (one resident round holds occ_q.per[pf] per CU; a batched launch
@@ -2513,7 +2529,8 @@ static int launch_jobs(r360_ctx* ctx, const IcpJobs& jobs, int njobs, const Leve
         else if (pf == 1) rc = launch_pass<M, 1>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top); \
         else if (pf == 2) rc = launch_pass<M, 2>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top); \
         else if (pf == 4) rc = launch_pass<M, 4>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top); \
-        else if (pf == 7) rc = launch_pass<M, 7>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top);
+        else if (pf == 7) rc = launch_pass<M, 7>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top); \
+        else if (pf == 10) rc = launch_pass<M, 10>(ctx, nb, njobs, jobs, Ls, T, C, first, eval_only, top);
 #else
 #define R360_LAUNCH_EXP(M)
 #endif
