@@ -169,6 +169,25 @@ def test_unqueued_lone_alignments_match_the_records(seq):
     assert ((dr > 2e-5) | (dt > 2e-4)).sum() <= 13, np.flatnonzero((dr > 2e-5) | (dt > 2e-4))
 
 
+def test_single_pipeline_latency_path_equals_the_pipelined_lone_path(seq):
+    """One pipeline without a dense queue is the sequential caller's configuration (bench.sequential_leg): its context
+    waits for each new frame's PbMap by assembling it itself (join_help), uploads the depth images before the BGR
+    images on a second stream (split_upload) and replays the plane stage as two graphs around the BGR wait.  None of
+    that may change a record: the registrations equal those of 16 pipelines doing the same lone Register() calls with
+    the plane stage launched kernel by kernel, bit for bit."""
+    bgr, dep = seq["bgr"], seq["dep"]
+    recs = []
+    for P in (1, 16):
+        runner = OD.SequenceRunner(0, 480, 640, P, seq["params"], queue=0, plane_batch=0)
+        try:
+            rec = np.zeros((1, 48, OD.REC), np.float32)
+            runner.run(0, 48, lambda i: (bgr[i], dep[i]), rec)
+            recs.append(rec[0])
+        finally:
+            runner.close()
+    assert np.array_equal(recs[0], recs[1])
+
+
 def test_bench_runner_mode_reproduces_the_records(seq):
     """The mode the headline bench line runs in (bench.py defaults: 12 pipelines, dense queue batches of 16, 3
     alignments in flight per pipeline, 1 frame built ahead, plane stages batched 8 frames per launch, runs=None: the
