@@ -601,6 +601,14 @@ int r360_ctx_debug_stamps(r360_ctx* ctx, unsigned long long* out12);
  * round and no other persistent alignment of the process is in flight. */
 int r360_ctx_persistent_levels(r360_ctx* ctx, int enable);
 
+/* Latency mode (no reference counterpart: a scheduling choice; on by default).  On: a thread waiting for the PbMap of
+ * a frame built on ctx polls the frame's GPU part itself and runs its assembly tasks; r360_frame_upload_async copies
+ * the depth images first and the BGR images on a second stream beside the plane stage's geometric part; a lone
+ * frame's plane stage is replayed as two graphs.  Off: waits sleep on the assembly pool, both copies and every
+ * launch go in the ctx stream's order (what a context among many pipelines wants: the sequence runner turns it off
+ * for more than one pipeline).  Results are the same either way, bit for bit. */
+int r360_ctx_latency_mode(r360_ctx* ctx, int enable);
+
 /* ---------------------------------------------------------------- timing hooks (bench) */
 /* enable: 0 off, 1 every launch on ctx's stream, 2 the level-0 ICP passes only (HIP events around each) */
 int r360_ctx_timing(r360_ctx* ctx, int enable);

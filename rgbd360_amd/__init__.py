@@ -286,6 +286,7 @@ _SIGS = [
                                         C.POINTER(C.c_long)]),
     ("r360_ctx_timing", C.c_int, [_P, C.c_int]),
     ("r360_ctx_persistent_levels", C.c_int, [_P, C.c_int]),
+    ("r360_ctx_latency_mode", C.c_int, [_P, C.c_int]),
     ("r360_ctx_timing_read", C.c_int, [_P, C.c_char_p, _DP, C.POINTER(C.c_long)]),
     ("r360_ctx_timing_reset", C.c_int, [_P]),
 ]
@@ -381,6 +382,11 @@ class Context:
     def persistent_levels(self, enable=True):
         """Lone alignFrames360 as one persistent launch per pyramid level (bit-identical; off by default)."""
         _check(lib().r360_ctx_persistent_levels(self.h, int(enable)), "persistent_levels")
+
+    def latency_mode(self, enable=True):
+        """On (the default): PbMap waits assemble the frame themselves, split uploads, graph-replayed lone plane
+        stages; off for a context among many pipelines.  Results are identical either way."""
+        _check(lib().r360_ctx_latency_mode(self.h, int(enable)), "latency_mode")
 
     def timing(self, enable):
         """0/False off, 1/True HIP events around every launch, 2 around the level-0 ICP passes only."""

@@ -182,6 +182,13 @@ extern "C" int r360_ctx_persistent_levels(r360_ctx* ctx, int enable) {
     return 0;
 }
 
+extern "C" int r360_ctx_latency_mode(r360_ctx* ctx, int enable) {
+    CHECK_ARG(ctx, "null ctx");
+    ctx->join_help = enable != 0;
+    ctx->split_upload = enable != 0;
+    return 0;
+}
+
 extern "C" int r360_ctx_timing(r360_ctx* ctx, int enable) {
     CHECK_ARG(ctx, "null ctx");
     timing_flush(ctx);

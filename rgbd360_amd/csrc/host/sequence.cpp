@@ -393,8 +393,7 @@ extern "C" int r360_sequence_create(int device, const r360_sequence_params* prm,
         c->plane_q = s->pq;
         // a single pipeline waits for each new frame's PbMap (the sequential caller): its thread helps assemble it;
         // several pipelines leave it to the assembly pool (spinning waits would take the host cores it needs)
-        c->join_help = s->P == 1;
-        c->split_upload = s->P == 1;
+        if (r360_ctx_latency_mode(c, s->P == 1)) return fail();
         // experiment builds: R360_SEQ_SHARE=k puts the first k pipelines' work on the dense queue's stream
         static const int share = R360_KNOB("R360_SEQ_SHARE", 0);
         if (queued && p < share) {
