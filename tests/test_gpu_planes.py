@@ -73,6 +73,35 @@ def vga(ctx):
     return dict(cal=cal, frames=frames, inputs=inputs, rt=rt, rel=rel)
 
 
+def test_latency_mode_is_result_neutral(vga):
+    """The VGA pair on a context with latency mode off (both uploads in stream order, the plane stage launched kernel by
+    kernel, PbMap waits on the assembly pool) and rebuilt twice on the default context (the second build replays the
+    captured plane-stage graphs): clouds, colours, refined labels and PbMap planes equal the fixture's frames (built
+    with latency mode on: split upload, first capture) bit for bit."""
+    ctx2 = R.Context(0)
+    ctx2.latency_mode(False)
+    cal2 = R.Calib360(ctx2, 480, 640)
+    cal2.loadExtrinsicCalibration(R.EXTRINSICS_DIR)
+    seed = 360 << 16
+    A = R.synth_path_pose(seed, 0)
+    for k, P in enumerate((A, A @ vga["rel"])):
+        b, d = vga["cal"].synth_frame(seed, P)
+        ref = vga["frames"][k]
+        off = R.Frame360(cal2)
+        off.upload(b, d)
+        off.getPlanes()
+        again = R.Frame360(vga["cal"])
+        for _ in range(2):
+            again.upload(b, d)
+            again.getPlanes()
+        for f in (off, again):
+            for x, y in zip(f.cloud(), ref.cloud()):
+                assert _same(x, y)
+            for x, y in zip(f.labels(), ref.labels()):
+                assert np.array_equal(x, y)
+            _cmp_planes(f.planes(), ref.planes())
+
+
 def _per_sensor_oracle(b, dm):
     out = []
     for k in range(8):
