@@ -521,7 +521,9 @@ int planes_launch(const PlaneBatch& B, int F, const PlaneGeom& G, hipStream_t st
 // One part of a lone frame's plane stage as a graph (0: cloud, filter, normals, segmentation, refinement; 1: colours,
 // statistics, contours, voxels, hull prefilter, publication), captured on first use for the frame's buffers and
 // geometry and replayed after: ~40 launches become two, so the stage no longer waits for the host to enqueue it
-// behind a split upload's depth copy.  The kernels and their arguments are those planes_launch enqueues.
+// behind a split upload's depth copy.  The kernels and their arguments are those planes_launch enqueues.  Captured on
+// the ctx's capture stream, not on ctx->stream: an event recorded on a capturing stream cannot be queried, and the
+// assembly pool polls the previous frame's `done` event (recorded on ctx->stream) while this frame is captured.
 static int plane_graph_launch(r360_ctx* ctx, const PlaneBatch& B, const PlaneGeom& G, int part) {
     std::string key(reinterpret_cast<const char*>(&B.f[0]), sizeof(PlaneDev));
     const long gk[7] = {G.rows, G.cols, G.w, G.h, G.sd_max, G.grid_cells, part};
@@ -534,11 +536,12 @@ static int plane_graph_launch(r360_ctx* ctx, const PlaneBatch& B, const PlaneGeo
             return 0;
         }
     hipGraph_t graph = nullptr;
-    R360_HIP(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeRelaxed));
-    int rc = 0;
-    if (part == 0) rc = launch_cloud_normals(B, 1, G, ctx->stream, nullptr) ? -1 : launch_segmentation_geom(B, 1, G, ctx->stream, nullptr);
-    else rc = launch_segmentation_model(B, 1, G, ctx->stream, nullptr) ? -1 : launch_plane_publish(B, 1, ctx->stream);
-    const hipError_t ec = hipStreamEndCapture(ctx->stream, &graph);
+    hipStream_t cs = capture_stream(ctx);   // not ctx->stream: the pool polls events recorded there
+    if (!cs) return -1;
+    R360_HIP(hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed));
+    const int rc = part == 0 ? (launch_cloud_normals(B, 1, G, cs, nullptr) ? -1 : launch_segmentation_geom(B, 1, G, cs, nullptr))
+                             : (launch_segmentation_model(B, 1, G, cs, nullptr) ? -1 : launch_plane_publish(B, 1, cs));
+    const hipError_t ec = hipStreamEndCapture(cs, &graph);
     if (rc) { if (graph) (void)hipGraphDestroy(graph); return rc; }
     R360_HIP(ec);
     hipGraphExec_t exec = nullptr;

@@ -182,6 +182,14 @@ extern "C" int r360_ctx_persistent_levels(r360_ctx* ctx, int enable) {
     return 0;
 }
 
+hipStream_t capture_stream(r360_ctx* ctx) {
+    if (!ctx->cap_stream && hipStreamCreateWithFlags(&ctx->cap_stream, hipStreamNonBlocking) != hipSuccess) {
+        ctx->cap_stream = nullptr;
+        r360_set_error("hipStreamCreateWithFlags failed (graph capture stream)");
+    }
+    return ctx->cap_stream;
+}
+
 extern "C" int r360_ctx_latency_mode(r360_ctx* ctx, int enable) {
     CHECK_ARG(ctx, "null ctx");
     ctx->join_help = enable != 0;
@@ -283,6 +291,7 @@ extern "C" void r360_ctx_destroy(r360_ctx* c) {
     if (c->mwait_ev) hipEventDestroy(c->mwait_ev);   // mstream is the device's shared match stream
     for (auto& g : c->graphs) hipGraphExecDestroy(g.exec);
     for (auto& g : c->plane_graphs) hipGraphExecDestroy(g.exec);
+    if (c->cap_stream) hipStreamDestroy(c->cap_stream);
     hipFree(c->d_state);
     hipFree(c->d_partials);
     hipFree(c->d_gticket);
@@ -1008,9 +1017,15 @@ static int align_graph_launch(r360_ctx* ctx, const r360_frame* trg, const r360_f
             return 0;
         }
     hipGraph_t graph = nullptr;
-    R360_HIP(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeRelaxed));
+    // captured on the ctx's capture stream (the launchers enqueue on ctx->stream, pointed at it meanwhile)
+    hipStream_t cs = capture_stream(ctx);
+    if (!cs) return -1;
+    hipStream_t own = ctx->stream;
+    R360_HIP(hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed));
+    ctx->stream = cs;
     const int rc = enqueue();
-    const hipError_t ec = hipStreamEndCapture(ctx->stream, &graph);
+    ctx->stream = own;
+    const hipError_t ec = hipStreamEndCapture(cs, &graph);
     if (rc) { if (graph) (void)hipGraphDestroy(graph); return rc; }
     R360_HIP(ec);
     hipGraphExec_t exec = nullptr;

@@ -341,6 +341,9 @@ struct r360_ctx {
     struct AlignGraph { std::vector<uintptr_t> key; hipGraphExec_t exec = nullptr; unsigned long long used = 0; };
     std::vector<AlignGraph> graphs;
     unsigned long long graph_clock = 0;
+    // graphs are captured on a stream of their own (capture_stream) and launched on `stream`: an event recorded on a
+    // stream that is capturing cannot be queried meanwhile, and the assembly pool polls events recorded on `stream`
+    hipStream_t cap_stream = nullptr;
     // a lone frame's plane stage (split_upload contexts) replayed as two graphs, the geometric part and the model part
     // (the BGR wait between them), keyed by the frame's plane buffers and geometry (pbmap.cpp plane_graph_launch)
     struct PlaneGraph { std::string key; hipGraphExec_t exec = nullptr; unsigned long long used = 0; };
@@ -494,6 +497,7 @@ struct r360_frame {
 };
 
 // ------------------------------------------------------------------ kernel launchers
+hipStream_t capture_stream(r360_ctx* ctx);   // ctx->cap_stream, created on first use (nullptr on failure)
 int launch_undistort(r360_frame* f);
 int launch_stitch(r360_frame* f);
 int launch_pyramid(r360_frame* f);
