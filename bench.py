@@ -305,6 +305,7 @@ def sequential_leg(device, rows, cols, p0, frames_of, params, pairs=32, plane_ba
         runner.run(p0, p0 + 4, frames_of, np.zeros((1, 4, OD.REC), np.float32))   # warm-up
         rec = np.zeros((1, pairs, OD.REC), np.float32)
         runner.host_s[:] = 0
+        runner.host_detail[:] = 0
         for c in runner.ctxs:
             c.host_times(reset=True)
         t0 = time.perf_counter()
@@ -314,6 +315,8 @@ def sequential_leg(device, rows, cols, p0, frames_of, params, pairs=32, plane_ba
         ht = np.sum([c.host_times() for c in runner.ctxs], axis=0)
         split = {k: round(1e3 * v / pairs, 3) for k, v in
                  zip(("load_build_enqueue", "pbmap_stage", "dense_wait"), hs[:3])}
+        hd = runner.host_detail.sum(axis=0)   # inside load_build_enqueue
+        split.update({"upload_enqueue": round(1e3 * hd[1] / pairs, 3), "build_enqueue": round(1e3 * hd[0] / pairs, 3)})
         split.update({k: round(1e3 * v / max(ht[3], 1), 3) for k, v in
                       zip(("pbmap_wait_frames", "pbmap_match_tables", "pbmap_tree_pose"), ht[:3])})
     finally:

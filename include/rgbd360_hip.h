@@ -448,8 +448,8 @@ int  r360_sequence_plane_stats(r360_sequence* s, long* batches, long* frames, in
 int  r360_sequence_pipeline(r360_sequence* s, int p, r360_ctx** ctx, r360_calib** calib, r360_frame** frames, int cap,
                             int* n_frames, long* thread_id);
 /* Host seconds per pipeline since the last reset: out[8 p + k], k = 0 load + build enqueue (with the collects that
- * free a buffer), 1 PbMap stage (RegisterPbMap and submit), 2 dense wait, 3 pairs registered; within 0 (queued):
- * 4 build enqueue, 5 upload enqueue, 6 collects before a buffer refill; 7 unused. */
+ * free a buffer), 1 PbMap stage (RegisterPbMap and submit), 2 dense wait, 3 pairs registered; within 0: 4 build
+ * enqueue, 5 upload enqueue, 6 (queued) collects before a buffer refill; 7 unused. */
 int  r360_sequence_host_times(r360_sequence* s, double* out, int reset);
 /* Parity hook: the two raster sweeps of OrganizedMultiPlaneSegmentation::refine as k_refine* run them, on
  * 8 sensors' refinement states (-1 no label, -2 non-planar label, m >= 0 planar model m) and closeness

@@ -161,8 +161,11 @@ void pipeline_plain(r360_sequence* s, int p) {
     for (int t = 0; t + 1 < T; ++t) {
         const double t0 = now_s();
         load_frame(s, fb, X.frame[t + 1]);
+        const double tu = now_s();
         req_rc(r360_frame_build_async(fb, s->flags));
         const double t1 = now_s();
+        hs[5] += tu - t0;
+        hs[4] += t1 - tu;
         if (X.pair[t]) {
             float pose[16], info[36] = {0};
             std::memcpy(pose, kEye, sizeof pose);
