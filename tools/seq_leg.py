@@ -18,6 +18,7 @@ BGR = np.zeros((n, 8, 480, 640, 3), np.uint8)
 DEP = np.zeros((n, 8, 480, 640), np.uint16)
 for j in range(n):
     BGR[j], DEP[j] = R.synth_frame_rt(480, 640, rt8, bench.SEED, R.synth_path_pose(bench.SEED, j))
+pin = R.HostPinned(BGR, DEP)   # page-locked, as the bench's inputs (pageable copies are synchronous host staging)
 p = R.IcpParams.default()
 p.n_pyr = 5
 p.std_dev_photo = np.float32(3.0 / 255)
